@@ -1,0 +1,206 @@
+#!/usr/bin/env python3
+"""Benchmark of the MI355X forward-backward / objective-gradient path.
+
+Workload (BASELINE.json configs[2], SURVEY.md 8d "c3"): synthetic family-A
+automaton (1024 states, out-degree 8 + end, one symbol per state out of 64),
+1M distinct strings per GPU sampled from it (mean length ~32, capped at 128).
+One step = one QuasiNewtonLearner::OptimizationStep over the whole corpus:
+H2D of the weights, the forward-backward kernels, (RCCL all-reduce),
+D2H of [loglik, grad], the host O(n) update.  Inputs are resident in HBM.
+
+Multi-GPU (weak scaling): launched by torch.distributed.run, one process per
+GPU; every rank builds the same global corpus and keeps a contiguous shard;
+the gradient + log-likelihood are summed with one RCCL all-reduce per step.
+
+Prints ONE JSON line (rank 0).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "w-fsa_amd"))
+
+HBM_PEAK_GBS = 8000.0        # MI355X_MICROARCH.md: HBM3E 8 TB/s (spec)
+METRIC = "forward-backward strings/sec @1/2/4/8 GPU; log-lik rel-err vs MKL ref"
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--strings-per-gpu", type=int, default=1_000_000)
+    ap.add_argument("--states", type=int, default=1024)
+    ap.add_argument("--degree", type=int, default=8)
+    ap.add_argument("--vocab", type=int, default=64)
+    ap.add_argument("--emissions", type=int, default=1)
+    ap.add_argument("--max-len", type=int, default=128)
+    ap.add_argument("--seed", type=int, default=1)
+    ap.add_argument("--cpu-sample", type=int, default=200_000,
+                    help="strings timed through the CPU oracle (0 = skip)")
+    ap.add_argument("--profile-traffic", default=os.path.join(ROOT, "profiles", "traffic_latest.json"),
+                    help="committed PMC traffic measurement to quote (if present)")
+    return ap.parse_args()
+
+
+def cpu_baseline(syn_text, sym, off, wt, n_sample):
+    """Reference algorithm restated in C (oracle/): BFS path enumeration once,
+    then the SpMV chain per iteration, one core.  Also the log-likelihood of
+    the same sample through the device path, for the rel-err column."""
+    from oracle import ENUM, Oracle
+    import wfsa_amd as W
+    n = min(n_sample, len(wt))
+    s_off = off[: n + 1].copy()
+    s_sym = sym[: s_off[-1]].copy()
+    s_wt = wt[:n].copy()
+    t0 = time.perf_counter()
+    o = Oracle.from_arrays(syn_text, s_sym, s_off, s_wt, mode=ENUM, max_paths=1_000_000)
+    t_build = time.perf_counter() - t0
+    o.qn_init(7)
+    iters = 3
+    t0 = time.perf_counter()
+    for _ in range(iters):
+        kl_ref, ll_ref = o.objective_grad()
+    t_iter = (time.perf_counter() - t0) / iters
+    S = o.info["n_strings"]
+    # the same sample through the device
+    fsa = W.Fsa.read_text(syn_text)
+    lrn = W.QuasiNewtonLearner(0)
+    lrn.BuildFromPacked(fsa, s_sym, s_off, s_wt)
+    lrn.Finalize()
+    lrn.Init(7)
+    kl_dev, _, _ = lrn.objective_grad()
+    ll_dev = lrn.info()["loglik"]
+    rel = abs(ll_dev - ll_ref) / abs(ll_ref)
+    return {
+        "value": S / t_iter, "unit": "strings/s", "cores": 1, "kind": "port",
+        "sample": (f"first {n} strings of the same corpus; oracle/wfsa_oracle.c ENUM = the reference "
+                   f"algorithm (BFS path enumeration {t_build:.2f} s once = {S / t_build:.0f} strings/s, "
+                   f"then the P/M SpMV chain: {t_iter * 1e3:.1f} ms per objective+gradient)"),
+        "enumeration_s": t_build, "iteration_s": t_iter, "paths": o.info["n_paths"],
+    }, rel, ll_ref, ll_dev
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    n_gpus = max(args.gpus, world)
+    import torch
+    import torch.distributed as dist
+    distributed = world > 1
+    if distributed:
+        dist.init_process_group("gloo")   # rendezvous / timing barrier only; the data path is RCCL
+    torch.cuda.set_device(local_rank)
+
+    import wfsa_amd as W
+
+    total = args.strings_per_gpu * world
+    syn = W.Synthetic(n_states=args.states, degree=args.degree, vocab=args.vocab, emissions=args.emissions,
+                      n_strings=total, max_len=args.max_len, seed=args.seed)
+    sym, off, wt = syn.corpus()
+    fsa = W.Fsa.read_text(syn.wfsa_text)
+
+    lrn = W.QuasiNewtonLearner(device=local_rank)
+    if distributed:
+        uid = [W.Device.comm_unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(uid, src=0)
+        lrn.SetCommunicator(world, rank, uid[0])
+    t0 = time.perf_counter()
+    lrn.BuildFromPacked(fsa, sym, off, wt)
+    t_build = time.perf_counter() - t0
+    lrn.Finalize()
+    lrn.Init(7)
+    info = lrn.info()
+    local_sym = int(off[info["shard_end"]] - off[info["shard_begin"]])
+    local_strings = info["n_local_strings"]
+
+    def barrier():
+        if distributed:
+            dist.barrier()
+        torch.cuda.synchronize()
+
+    for _ in range(args.warmup):
+        lrn.OptimizationStep(1.0, 1e-6)
+    st0 = lrn.stats()
+    barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        lrn.OptimizationStep(1.0, 1e-6)
+    barrier()
+    dt = time.perf_counter() - t0
+    st1 = lrn.stats()
+    if distributed:
+        t = torch.tensor([dt], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+
+    strings_all = info["n_strings"]
+    value = strings_all * args.steps / dt
+    kern_ms = (st1["fb_kernel_ms"] - st0["fb_kernel_ms"]) / args.steps
+    alg_bytes = local_sym + 16 * local_strings          # bytes + off + p per string
+    achieved = alg_bytes / (kern_ms * 1e-3) / 1e9
+    traffic = None
+    if os.path.exists(args.profile_traffic):
+        try:
+            traffic = json.load(open(args.profile_traffic)).get("hbm_bytes_per_launch")
+        except Exception:
+            traffic = None
+
+    out = {
+        "metric": METRIC,
+        "value": value,
+        "unit": "strings/s",
+        "n_gpus": n_gpus,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": dt * 1e3 / args.steps,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f64",
+        "data": "synthetic",
+        "config": {
+            "workload": (f"c3 family A: {args.states}-state sparse WFSA, out-degree {args.degree}+end, "
+                         f"{args.emissions} of {args.vocab} symbols/state, {args.strings_per_gpu} distinct "
+                         f"strings per GPU (mean len {np.diff(off).mean():.1f}, max {args.max_len})"),
+            "global_strings": strings_all,
+            "strings_per_gpu": args.strings_per_gpu,
+            "parallelism": f"dp{n_gpus}",
+            "step": "QuasiNewtonLearner::OptimizationStep (H2D w, forward-backward, all-reduce, D2H grad, host update)",
+        },
+        "roofline": {
+            "bound": "hbm",
+            "achieved": achieved,
+            "peak": HBM_PEAK_GBS,
+            "unit": "GB/s",
+            "frac": achieved / HBM_PEAK_GBS,
+            "traffic": traffic,
+            "kernel": "fb_kernel<false> (forward-backward, weighted)",
+            "kernel_ms_per_launch": kern_ms,
+            "algorithmic_bytes_per_launch": alg_bytes,
+        },
+        "live_edges_per_step": st1["last_live_edges"],
+        "build_s": t_build,
+        "tier1_strings": st1["tier1_strings"],
+    }
+    if rank == 0 and world == 1 and args.cpu_sample > 0:
+        cb, rel, ll_ref, ll_dev = cpu_baseline(syn.wfsa_text, sym, off, wt, args.cpu_sample)
+        out["cpu_baseline"] = cb
+        out["ll_rel_err_vs_reference_algorithm"] = rel
+    else:
+        out["cpu_baseline"] = None
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if distributed:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

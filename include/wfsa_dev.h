@@ -1,0 +1,131 @@
+/*
+ * wfsa_dev.h -- the drop-in device boundary of the MI355X w-fsa path.
+ *
+ * The reference (gaebor/w-fsa) has no FFI: its hot path is the body of the
+ * Learner class hierarchy.  These C entry points replace, one for one, the
+ * hot functions a host-side Learner calls:
+ *
+ *   wfsa_dev_load_model     <- the Fsa graph walked by Recognizer
+ *                              (inc/Fsa.h:26-66, inc/Recognize.h:35-96)
+ *   wfsa_dev_load_corpus    <- Corpus strings + p (inc/Corpus.h:16-26,
+ *                              src/Learner.cpp:297-302)
+ *   wfsa_dev_recognize      <- Learner::BuildPaths (src/Learner.cpp:276-348):
+ *                              recognized flag, exact path count per string and
+ *                              the "used parameter" marks Trim consumes
+ *                              (src/Learner.cpp:310, :350-425)
+ *   wfsa_dev_objective_grad <- Learner::ComputeModeledProbs + ComputeObjective
+ *                              (src/Learner.cpp:515-553) and
+ *                              QuasiNewtonLearner::ComputeGrad
+ *                              (src/QuasiNewtonLearner.cpp:93-125) ==
+ *                              HessianLearner::ComputeGrad
+ *                              (src/HessianLearner.cpp:565-597)
+ *   wfsa_dev_comm_*         <- (new) one RCCL all-reduce per iteration when the
+ *                              corpus is sharded over GPUs
+ *
+ * Conventions: plain pointers and sizes, host buffers caller-owned and only
+ * touched during the call; all device memory belongs to the context.  Every
+ * entry point returns WFSA_OK (0) or a negative code and sets a thread-local
+ * message readable with wfsa_dev_last_error() -- the reference throws MyError
+ * subclasses with a message (inc/Utils.h:130-141); no exception crosses this
+ * ABI.  A context is bound to one device and is not re-entrant.
+ */
+#ifndef WFSA_DEV_H
+#define WFSA_DEV_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define WFSA_OK 0
+#define WFSA_ERR_ARG (-1)      /* invalid argument / call order            */
+#define WFSA_ERR_HIP (-2)      /* HIP runtime failure                       */
+#define WFSA_ERR_MODEL (-3)    /* automaton rejected (e.g. epsilon cycle)   */
+#define WFSA_ERR_CAPACITY (-4) /* a string's trellis exceeds device limits  */
+#define WFSA_ERR_RCCL (-5)     /* collective failure                        */
+#define WFSA_ERR_NODEV (-6)    /* no usable gfx950 device / kernels missing */
+
+typedef struct wfsa_dev wfsa_dev;
+
+/* The automaton after Fsa::AssignIndices (src/Fsa.cpp:207-238), flattened.
+ * States are 0..n_states-1; per state its emissions (byte strings, possibly
+ * empty or multi-byte) and its transitions.  *_param is the Fsa parameter
+ * index, or -1 for an unequivocal (single-member) group, whose weight is
+ * log 1.  `end` is the end state's id or -1 when nothing transitions to it. */
+typedef struct {
+    int32_t n_states;
+    int32_t start;
+    int32_t end;
+    int32_t n_params;          /* Fsa::GetNumberOfParameters() ("n_full")   */
+    const int32_t* em_ptr;     /* [n_states+1]                              */
+    const int64_t* em_off;     /* [n_em] offset of the emission in em_bytes */
+    const int32_t* em_len;     /* [n_em]                                    */
+    const int32_t* em_param;   /* [n_em]                                    */
+    const uint8_t* em_bytes;
+    const int32_t* tr_ptr;     /* [n_states+1]                              */
+    const int32_t* tr_dst;     /* [n_tr]                                    */
+    const int32_t* tr_param;   /* [n_tr]                                    */
+} wfsa_model_desc;
+
+typedef struct {
+    int64_t n_strings;         /* strings resident on this device           */
+    int64_t total_symbols;     /* sum of their lengths                      */
+    int32_t max_len;
+    int32_t n_nodes;           /* trellis nodes after epsilon removal       */
+    int64_t n_edges;           /* byte-consuming composite edges            */
+    int64_t n_end_edges;
+    int64_t fb_launches;       /* forward-backward launches timed so far    */
+    double fb_kernel_ms;       /* sum of their HIP-event durations          */
+    double last_fb_kernel_ms;  /* the last objective_grad call's FB kernels */
+    double last_call_ms;       /* the last objective_grad call, end to end  */
+    int64_t last_live_edges;   /* trellis edges touched by the last call    */
+    int32_t tier1_strings;     /* strings served by the large-slab tier     */
+    int32_t waves_per_block;
+} wfsa_dev_stats;
+
+/* context ---------------------------------------------------------------- */
+int wfsa_dev_create(int device, wfsa_dev** out);
+void wfsa_dev_destroy(wfsa_dev* ctx);
+const char* wfsa_dev_last_error(void);
+
+/* One-time uploads -------------------------------------------------------- */
+int wfsa_dev_load_model(wfsa_dev* ctx, const wfsa_model_desc* model);
+/* sym: packed bytes, off[n_strings+1] offsets into sym, p[n_strings] weights
+ * (the reference's p: corpus weight / sum over ALL strings). */
+int wfsa_dev_load_corpus(wfsa_dev* ctx, const uint8_t* sym, const int64_t* off,
+                         const double* p, int64_t n_strings);
+
+/* Structural pass (weights ignored) over the loaded strings.  Any output may
+ * be NULL.  recognized[s] = 1 iff the string has an accepting path;
+ * path_count[s] = number of accepting paths (exact below 2^53);
+ * used_param[j] = 1 iff Fsa parameter j lies on an accepting path of some
+ * string (OR over ranks when a communicator is attached). */
+int wfsa_dev_recognize(wfsa_dev* ctx, uint8_t* recognized, double* path_count,
+                       uint8_t* used_param);
+
+/* Per-iteration hot path.  w_full[n_params] = Learner::GetWeight(j)
+ * (src/Learner.cpp:427-436): x[trim[j]], 0 or -inf.  Outputs:
+ *   *loglik        = sum_s p_s log q_s
+ *   grad_full[j]   = -sum_s p_s E_{path|s}[count_j]   (NULL allowed)
+ *   logq[s]        = log q_s for the loaded strings     (NULL allowed)
+ * With a communicator attached, loglik and grad_full are summed over ranks
+ * (one RCCL all-reduce) and logq stays local. */
+int wfsa_dev_objective_grad(wfsa_dev* ctx, const double* w_full, double* loglik,
+                            double* grad_full, double* logq);
+
+/* Multi-GPU: one process per GPU.  Rank 0 creates the id, the launcher
+ * broadcasts the 128 bytes, every rank attaches.  wfsa_dev_allreduce sums
+ * `count` doubles of a host buffer in place over the ranks. */
+#define WFSA_COMM_ID_BYTES 128
+int wfsa_dev_comm_unique_id(uint8_t id[WFSA_COMM_ID_BYTES]);
+int wfsa_dev_comm_init(wfsa_dev* ctx, int nranks, int rank, const uint8_t id[WFSA_COMM_ID_BYTES]);
+int wfsa_dev_allreduce(wfsa_dev* ctx, double* host_buf, int64_t count);
+
+int wfsa_dev_get_stats(wfsa_dev* ctx, wfsa_dev_stats* out);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* WFSA_DEV_H */

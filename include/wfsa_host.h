@@ -1,0 +1,104 @@
+/*
+ * wfsa_host.h -- C ABI over the host-side mirror of the reference's Learner
+ * stack (Fsa / Corpus / Learner / QuasiNewtonLearner), for FFI callers
+ * (Python ctypes in this repo's tests and bench).  Each call maps to the
+ * reference method named beside it; errors are returned as negative codes
+ * with a thread-local message (the reference's MyError::what()).
+ */
+#ifndef WFSA_HOST_H
+#define WFSA_HOST_H
+
+#include <stdint.h>
+
+#include "wfsa_dev.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+const char* wfsa_host_last_error(void);
+
+/* ---- Fsa (inc/Fsa.h) ---------------------------------------------------- */
+typedef struct wfsa_fsa wfsa_fsa;
+int wfsa_fsa_read_text(const char* text, wfsa_fsa** out);     /* Fsa::Read */
+int wfsa_fsa_read_file(const char* path, wfsa_fsa** out);
+void wfsa_fsa_free(wfsa_fsa* fsa);
+/* the flattened graph handed to wfsa_dev_load_model (valid while fsa lives) */
+int wfsa_fsa_desc(wfsa_fsa* fsa, wfsa_model_desc* out);
+/* counts: states, transitions, emissions, parameters, constraints, free params */
+int wfsa_fsa_counts(wfsa_fsa* fsa, int64_t out[6]);
+/* Fsa parameter j -> owning state name, kind (0 emission / 1 transition), label */
+int wfsa_fsa_param_name(wfsa_fsa* fsa, int32_t j, const char** state, int32_t* kind, const char** label);
+
+/* ---- Corpus (inc/Corpus.h) ---------------------------------------------- */
+typedef struct wfsa_corpus wfsa_corpus;
+int wfsa_corpus_read_text(const char* text, wfsa_corpus** out);   /* Corpus::Read */
+int wfsa_corpus_read_file(const char* path, wfsa_corpus** out);
+void wfsa_corpus_free(wfsa_corpus* c);
+/* packed view: strings back to back, off[n+1]; weights as read (not normalized) */
+int wfsa_corpus_view(wfsa_corpus* c, const uint8_t** sym, const int64_t** off, const double** weights,
+                     int64_t* n_strings);
+
+/* ---- Learner (inc/Learner.h, inc/QuasiNewtonLearner.h) ------------------ */
+typedef struct wfsa_learner wfsa_learner;
+
+typedef struct {
+    int64_t n_strings;        /* recognized, all ranks (GetNumberOfStrings)   */
+    int64_t n_local_strings;  /* recognized on this rank                      */
+    int64_t n_paths;          /* sum of path counts (GetNumberOfPaths)        */
+    int32_t n_full;           /* Fsa parameters                               */
+    int32_t n_params;         /* after Trim (GetNumberOfParameters)           */
+    int32_t n_constraints;
+    int32_t unique_paths;
+    int64_t aux_params;
+    double common_support, plogp, model_volume, aux_hessian, kl, loglik;
+    int64_t shard_begin, shard_end;
+} wfsa_learner_info;
+
+/* optimizer: "QuasiNewton" (the reference's "Hessian" optimizer is not part
+ * of this build: SURVEY.md 8f item 1) */
+int wfsa_learner_create(const char* optimizer, int device, wfsa_learner** out);
+void wfsa_learner_destroy(wfsa_learner* l);
+int wfsa_learner_set_comm(wfsa_learner* l, int nranks, int rank, const uint8_t id[WFSA_COMM_ID_BYTES]);
+/* Learner::BuildFrom on (Fsa, Corpus); the corpus is renormalized first as
+ * main.cpp does.  With a communicator each rank keeps its shard. */
+int wfsa_learner_build(wfsa_learner* l, wfsa_fsa* fsa, wfsa_corpus* corpus);
+/* the same from packed strings + raw weights (renormalized here) */
+int wfsa_learner_build_packed(wfsa_learner* l, wfsa_fsa* fsa, const uint8_t* sym, const int64_t* off,
+                              const double* weights, int64_t n_strings);
+int wfsa_learner_finalize(wfsa_learner* l);                                 /* Learner::Finalize */
+int wfsa_learner_info_get(wfsa_learner* l, wfsa_learner_info* out);
+int wfsa_learner_init(wfsa_learner* l, int flags, const double* x0);       /* Learner::Init */
+/* OptimizationStep + GetOptimizationInfo (7 values) + HaltCondition(tol) */
+int wfsa_learner_step(wfsa_learner* l, double eta, double tol, double info[7], int32_t* halt);
+/* ComputeExpX, ComputeGrad, ComputeObjective at the current x:
+ * kl, grad[n_params] (trimmed order), logq[n_local_strings] (nullable) */
+int wfsa_learner_objective_grad(wfsa_learner* l, double* kl, double* grad, double* logq);
+int wfsa_learner_get_x(wfsa_learner* l, double* x);
+int wfsa_learner_set_x(wfsa_learner* l, const double* x);
+int wfsa_learner_get_p(wfsa_learner* l, double* p);                 /* [n_local_strings] */
+int wfsa_learner_trimmed_index(wfsa_learner* l, int32_t* out);      /* [n_full]          */
+int wfsa_learner_path_counts(wfsa_learner* l, double* out, uint8_t* recognized); /* [shard size] */
+int wfsa_learner_renormalize(wfsa_learner* l);                      /* Learner::Renormalize */
+/* RewriteWeights into the fsa, then Fsa::Dump to path */
+int wfsa_learner_dump(wfsa_learner* l, wfsa_fsa* fsa, const char* path);
+int wfsa_learner_stats(wfsa_learner* l, wfsa_dev_stats* out);
+
+/* ---- synthetic corpora (bench / tests) ---------------------------------- */
+/* family: N states, out-degree D (+ end), E distinct symbols per state out of
+ * V printable bytes, stop probability 1/32 per step, lengths capped at
+ * max_len; n_strings distinct strings sampled from the automaton; integer
+ * weights 1..10.  dense != 0: every state to every state (D ignored). */
+typedef struct wfsa_synth wfsa_synth;
+int wfsa_synth_make(int32_t n_states, int32_t degree, int32_t vocab, int32_t emissions, int32_t dense,
+                    int64_t n_strings, int32_t max_len, uint64_t seed, wfsa_synth** out);
+void wfsa_synth_free(wfsa_synth* s);
+const char* wfsa_synth_wfsa_text(wfsa_synth* s);
+int wfsa_synth_corpus(wfsa_synth* s, const uint8_t** sym, const int64_t** off, const double** weights,
+                      int64_t* n_strings);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* WFSA_HOST_H */

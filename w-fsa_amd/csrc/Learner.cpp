@@ -1,0 +1,286 @@
+#include "Learner.hpp"
+
+#include <algorithm>
+#include <cmath>
+#include <limits>
+#include <numeric>
+
+namespace wfsa {
+
+void ThrowOnDevError(int rc, const char* what) {
+    if (rc != WFSA_OK) throw LearnerError(what, " failed (", rc, "): ", wfsa_dev_last_error());
+}
+
+Learner::Learner() {}
+
+Learner::~Learner() {
+    if (dev) wfsa_dev_destroy(dev);
+}
+
+void Learner::SetDevice(int d) {
+    if (dev) throw LearnerError("SetDevice must come before BuildFrom");
+    device = d;
+}
+
+void Learner::SetCommunicator(int n, int r, const uint8_t* id) {
+    if (dev) throw LearnerError("SetCommunicator must come before BuildFrom");
+    if (n < 1 || r < 0 || r >= n) throw LearnerError("bad communicator: rank ", r, " of ", n);
+    nranks = n;
+    rank = r;
+    if (n > 1) {
+        if (!id) throw LearnerError("null communicator id");
+        comm_id.assign(id, id + WFSA_COMM_ID_BYTES);
+    }
+}
+
+void Learner::EnsureDevice() {
+    if (dev) return;
+    ThrowOnDevError(wfsa_dev_create(device, &dev), "wfsa_dev_create");
+    if (nranks > 1) ThrowOnDevError(wfsa_dev_comm_init(dev, nranks, rank, comm_id.data()), "wfsa_dev_comm_init");
+}
+
+double Learner::AllReduceSum(double v) const {
+    if (nranks > 1) ThrowOnDevError(wfsa_dev_allreduce(dev, &v, 1), "wfsa_dev_allreduce");
+    return v;
+}
+
+// Constraint matrix C (n x k, one 1 per row) and x from the file weights, in
+// map iteration order: equivocal emissions, then equivocal transitions, of
+// every state (src/Learner.cpp:221-265).
+void Learner::BuildConstraints(const Fsa& fsa) {
+    model_volume = 0;
+    Crow.clear();
+    Ccol.clear();
+    n_full = int32_t(fsa.GetNumberOfParameters());
+    _x.assign(size_t(n_full), 0.0);
+    int32_t k = 0;
+    auto collect = [&](const auto& group) {
+        if (group.size() <= 1) return;
+        for (const auto& member : group) {
+            if (member.index != int32_t(Ccol.size()))
+                throw LearnerError("Indexing error: ", member.index, " != ", Ccol.size());
+            Crow.push_back(int32_t(Ccol.size()));
+            Ccol.push_back(k);
+            _x[size_t(member.index)] = member.logprob;
+        }
+        ++k;
+        model_volume += log_simplex_volume(group.size());
+    };
+    for (const auto& t : fsa.GetTransitionMtx()) {
+        collect(t.second.emissions);
+        collect(t.second.transitions);
+    }
+    Crow.push_back(int32_t(Ccol.size()));
+}
+
+void Learner::BuildFrom(const Fsa& fsa, const Corpus& corpus, bool) {
+    PackedStrings ps;
+    std::vector<double> w;
+    w.reserve(corpus.size());
+    for (const auto& e : corpus) {
+        ps.add(e.first);
+        w.push_back(e.second);
+    }
+    BuildFromPacked(fsa, ps.sym.data(), ps.off.data(), w.data(), ps.size());
+}
+
+void Learner::BuildFromPacked(const Fsa& fsa, const uint8_t* sym, const int64_t* off, const double* weights,
+                              int64_t n_strings) {
+    BuildConstraints(fsa);
+    BuildPaths(fsa, sym, off, weights, n_strings);
+    Trim();
+}
+
+// Replacement of Learner::BuildPaths (src/Learner.cpp:276-348): the device
+// counting pass gives, per string, recognized / path count, and the used
+// parameters (OR over ranks); p keeps the recognized strings' weights in
+// corpus order.
+void Learner::BuildPaths(const Fsa& fsa, const uint8_t* sym, const int64_t* off, const double* weights, int64_t n) {
+    EnsureDevice();
+    // contiguous shard [b, e) of this rank, balanced on total length
+    const int64_t total = off[n];
+    auto bound = [&](int r) -> int64_t {
+        if (r <= 0) return 0;
+        if (r >= nranks) return n;
+        const long double thr = (long double)total * r / nranks;
+        return int64_t(std::lower_bound(off, off + n, int64_t(std::ceil(thr))) - off);
+    };
+    shard_begin = bound(rank);
+    shard_end = std::max(shard_begin, bound(rank + 1));
+    const int64_t ln = shard_end - shard_begin;
+    std::vector<int64_t> loff(size_t(ln) + 1);
+    for (int64_t s = 0; s <= ln; ++s) loff[size_t(s)] = off[shard_begin + s] - off[shard_begin];
+    const uint8_t* lsym = sym + off[shard_begin];
+    const double* lw = weights + shard_begin;
+
+    flat.reset(new FlatModel(fsa));
+    const wfsa_model_desc desc = flat->desc();
+    ThrowOnDevError(wfsa_dev_load_model(dev, &desc), "wfsa_dev_load_model");
+    ThrowOnDevError(wfsa_dev_load_corpus(dev, lsym, loff.data(), lw, ln), "wfsa_dev_load_corpus");
+    recognized_local.assign(size_t(ln), 0);
+    path_count_local.assign(size_t(ln), 0.0);
+    std::vector<uint8_t> used(size_t(std::max(n_full, 1)), 0);
+    ThrowOnDevError(wfsa_dev_recognize(dev, recognized_local.data(), path_count_local.data(), used.data()),
+                    "wfsa_dev_recognize");
+
+    // p over recognized strings; the rest become auxiliary parameters
+    p.clear();
+    PackedStrings rec;
+    double stats[5] = {0, 0, 0, 0, 0};   // support, #aux, aux_hessian, #strings, #paths
+    double non_unique = 0;
+    for (int64_t s = 0; s < ln; ++s) {
+        if (recognized_local[size_t(s)]) {
+            p.push_back(lw[s]);
+            stats[0] += lw[s];
+            stats[3] += 1;
+            stats[4] += path_count_local[size_t(s)];
+            if (path_count_local[size_t(s)] != 1.0) non_unique += 1;
+            rec.sym.insert(rec.sym.end(), lsym + loff[size_t(s)], lsym + loff[size_t(s) + 1]);
+            rec.off.push_back(int64_t(rec.sym.size()));
+        } else {
+            stats[1] += 1;
+            stats[2] -= std::log(lw[s]);
+        }
+    }
+    if (nranks > 1) {
+        double buf[6] = {stats[0], stats[1], stats[2], stats[3], stats[4], non_unique};
+        ThrowOnDevError(wfsa_dev_allreduce(dev, buf, 6), "wfsa_dev_allreduce");
+        std::copy(buf, buf + 5, stats);
+        non_unique = buf[5];
+    }
+    common_support = stats[0];
+    auxiliary_parameters = int64_t(stats[1]);
+    aux_hessian = stats[2];
+    n_strings_global = int64_t(stats[3]);
+    n_paths_global = int64_t(stats[4]);
+    unique_paths = non_unique == 0;
+
+    trimmed_weights.assign(size_t(n_full), -2);   // unused unless on an accepting path
+    for (int32_t j = 0; j < n_full; ++j)
+        if (used[size_t(j)]) trimmed_weights[size_t(j)] = 0;
+
+    // the per-iteration launches see only the recognized strings
+    ThrowOnDevError(wfsa_dev_load_corpus(dev, rec.sym.data(), rec.off.data(), p.data(), int64_t(p.size())),
+                    "wfsa_dev_load_corpus");
+    w_full.assign(size_t(n_full), 0.0);
+    grad_full.assign(size_t(n_full), 0.0);
+    logq_valid = false;
+}
+
+// Learner::Trim (src/Learner.cpp:350-425) without the P matrix: a used
+// parameter alone in its constraint is fixed to log 1 (-1); the used ones
+// are renumbered, x and C follow.
+void Learner::Trim() {
+    const int32_t n = int32_t(Ccol.size());
+    int32_t c = -1, nnz_in_c = -1;
+    for (int32_t i = 0; i < n; ++i) {
+        const int32_t this_c = Ccol[size_t(i)];
+        if (this_c != c) {
+            c = this_c;
+            if (nnz_in_c >= 0) trimmed_weights[size_t(nnz_in_c)] = -1;
+            nnz_in_c = -1;
+        }
+        if (trimmed_weights[size_t(i)] >= 0) nnz_in_c = (nnz_in_c == -1) ? i : -2;
+    }
+    if (nnz_in_c >= 0) trimmed_weights[size_t(nnz_in_c)] = -1;
+
+    std::vector<int32_t> ccol_new;
+    ccol_new.reserve(size_t(n));
+    int32_t good = 0, good_c = -1;
+    c = -1;
+    for (int32_t i = 0; i < n; ++i) {
+        if (trimmed_weights[size_t(i)] != 0) continue;
+        trimmed_weights[size_t(i)] = good++;
+        _x[size_t(trimmed_weights[size_t(i)])] = _x[size_t(i)];
+        if (c < Ccol[size_t(i)]) {
+            ++good_c;
+            c = Ccol[size_t(i)];
+        }
+        ccol_new.push_back(good_c);
+    }
+    Ccol.swap(ccol_new);
+    Crow.resize(size_t(good) + 1);
+    _x.resize(size_t(good));
+}
+
+double Learner::GetWeight(int32_t i) const {   // src/Learner.cpp:427-436
+    switch (trimmed_weights[size_t(i)]) {
+        case -2: return -std::numeric_limits<double>::infinity();
+        case -1: return 0.0;
+        default: return _x[size_t(trimmed_weights[size_t(i)])];
+    }
+}
+
+void Learner::SetWeights(const double* x) { std::copy(x, x + _x.size(), _x.begin()); }
+
+void Learner::Renormalize() {   // src/Learner.cpp:23-43: x -= C log(C^T exp(x))
+    const int32_t k = GetNumberOfConstraints();
+    std::vector<double> g(size_t(k), 0.0);
+    for (size_t i = 0; i < _x.size(); ++i) g[size_t(Ccol[i])] += std::exp(_x[i]);
+    for (auto& v : g) v = std::log(v);
+    for (size_t i = 0; i < _x.size(); ++i) _x[i] -= g[size_t(Ccol[i])];
+}
+
+void Learner::RewriteWeights(Fsa& fsa) const {   // src/Learner.cpp:45-58
+    for (auto& t : fsa.GetTransitionMtx()) {
+        for (auto& e : t.second.emissions) e.logprob = e.index >= 0 ? GetWeight(e.index) : 0.0;
+        for (auto& e : t.second.transitions) e.logprob = e.index >= 0 ? GetWeight(e.index) : 0.0;
+    }
+}
+
+std::vector<double> Learner::GetOptimizationInfo() { return {}; }
+std::string Learner::GetOptimizationHeader() const { return std::string(); }
+std::vector<double> Learner::GetOptimizationResult(bool) { return {}; }
+bool Learner::HaltCondition(double) { return false; }
+
+void Learner::LambdaUpdate(double* lstep, double* l, double eta, bool exponential) const {
+    const int32_t k = GetNumberOfConstraints();
+    if (!exponential) {
+        for (int32_t c = 0; c < k; ++c) l[c] -= eta * lstep[c];
+    } else {   // lambda *= exp(-eta * lstep / lambda)
+        for (int32_t c = 0; c < k; ++c) l[c] *= std::exp(-eta * (lstep[c] / l[c]));
+    }
+}
+
+void Learner::FinalizeCallback() {}
+void Learner::InitCallback(int) {}
+
+void Learner::Finalize() {   // src/Learner.cpp:466-488
+    double local = 0;
+    for (double v : p) local += v * std::log(v);
+    plogp = AllReduceSum(local);
+    logq.assign(p.size(), 0.0);
+    grad_cache.assign(_x.size(), 0.0);
+    FinalizeCallback();
+}
+
+void Learner::Init(int flags, const double* initialx) {
+    if (initialx) std::copy(initialx, initialx + _x.size(), _x.begin());
+    InitCallback(flags);
+}
+
+void Learner::EvaluateDevice(std::vector<double>& grad_out, bool want_logq) {
+    if (!dev) throw LearnerError("BuildFrom has not run");
+    for (int32_t j = 0; j < n_full; ++j) w_full[size_t(j)] = GetWeight(j);
+    if (want_logq) logq.assign(p.size(), 0.0);
+    ThrowOnDevError(wfsa_dev_objective_grad(dev, w_full.data(), &loglik, grad_full.data(),
+                                            want_logq ? logq.data() : nullptr),
+                    "wfsa_dev_objective_grad");
+    logq_valid = want_logq;
+    grad_out.assign(_x.size(), 0.0);
+    for (int32_t j = 0; j < n_full; ++j) {
+        const int32_t t = trimmed_weights[size_t(j)];
+        if (t >= 0) grad_out[size_t(t)] = grad_full[size_t(j)];
+    }
+}
+
+void Learner::ComputeModeledProbs() { EvaluateDevice(grad_cache, false); }
+
+void Learner::ComputeObjective() { kl = plogp - loglik; }
+
+const std::vector<double>& Learner::GetLogQ() {
+    if (!logq_valid) EvaluateDevice(grad_cache, true);
+    return logq;
+}
+
+}  // namespace wfsa

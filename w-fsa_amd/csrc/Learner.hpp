@@ -1,0 +1,152 @@
+// Learner: host-side mirror of the reference's Learner (inc/Learner.h:17-169)
+// with the hot path moved behind the device boundary (include/wfsa_dev.h).
+//
+// What stays the same: the public methods, BuildConstraints, Trim,
+// GetWeight, Renormalize, LambdaUpdate, Finalize's plogp, parameter
+// numbering.  What changes: BuildPaths no longer enumerates paths and no
+// P / M matrices exist -- the device's structural pass supplies the
+// recognized strings, path counts and used parameters, and
+// ComputeModeledProbs + ComputeObjective + the gradient come from one
+// forward-backward launch per iteration.
+//
+// Data parallelism: with a communicator attached the corpus is split into
+// contiguous shards (balanced on total length), each rank uploads only its
+// shard, and the device sums [loglik, grad] over ranks with one RCCL
+// all-reduce; host-side scalars (plogp, counts) are all-reduced once after
+// BuildFrom.  Every rank then runs the identical O(n) optimizer update.
+#pragma once
+
+#include <cstdint>
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "Corpus.hpp"
+#include "Fsa.hpp"
+#include "text.hpp"
+#include "wfsa_dev.h"
+
+namespace wfsa {
+
+struct LearnerError : public MyError {
+    using MyError::MyError;
+};
+
+class Learner {
+public:
+    Learner();
+    virtual ~Learner();
+    Learner(const Learner&) = delete;
+    Learner& operator=(const Learner&) = delete;
+
+    // Device / sharding setup (new; call before BuildFrom).
+    void SetDevice(int device);
+    void SetCommunicator(int nranks, int rank, const uint8_t* unique_id);
+
+    // `corpus` weights must already be normalized over the whole corpus
+    // (main.cpp renormalizes before BuildFrom).  With a communicator, every
+    // rank passes the full corpus and keeps its own shard.  `bfs` is
+    // accepted for interface parity; the trellis has no BFS/DFS choice.
+    void BuildFrom(const Fsa& fsa, const Corpus& corpus, bool bfs = true);
+    // Same from packed strings (sym/off) and normalized weights.
+    void BuildFromPacked(const Fsa& fsa, const uint8_t* sym, const int64_t* off, const double* weights,
+                         int64_t n_strings);
+
+    void Renormalize();
+    void RewriteWeights(Fsa& fsa) const;
+    const double* GetWeights() const { return _x.data(); }
+
+    virtual std::vector<double> GetOptimizationInfo();
+    virtual std::string GetOptimizationHeader() const;
+    virtual std::vector<double> GetOptimizationResult(bool verbose = false);
+    virtual bool HaltCondition(double tol);
+
+    double GetCommonSupport() const { return common_support; }
+
+    // log q for every (local) recognized string, then q (src/Learner.cpp:515-547)
+    void ComputeModeledProbs();
+    // kl = plogp - p.log q (src/Learner.cpp:549-553)
+    void ComputeObjective();
+
+    int32_t GetNumberOfStrings() const { return int32_t(n_strings_global); }
+    int64_t GetNumberOfPaths() const { return n_paths_global; }
+    int32_t GetNumberOfParameters() const { return int32_t(Ccol.size()); }
+    int32_t GetNumberOfConstraints() const { return Ccol.empty() ? 0 : Ccol.back() + 1; }
+    int32_t GetNumberOfLocalStrings() const { return int32_t(p.size()); }
+    int32_t GetNumberOfFullParameters() const { return n_full; }
+
+    bool HasUniquePaths() const { return unique_paths; }
+    double GetKLDistance() const { return kl; }
+    double gKLDistance() const { return kl + mxlogx(common_support); }
+
+    virtual void OptimizationStep(double eta = 1.0, bool verbose = false) = 0;
+    virtual void Init(int flags, const double* initialx = nullptr);
+
+    double LogModelVolume() const { return model_volume; }
+    double LogAuxiliaryVolume() const { return log_simplex_volume(auxiliary_parameters); }
+    double LogVolume() const { return LogModelVolume() + LogAuxiliaryVolume(); }
+    double LogDetAuxiliaryHessian() const { return aux_hessian; }
+    int32_t GetNumberOfAuxParameters() const { return int32_t(auxiliary_parameters); }
+
+    void Finalize();
+
+    // accessors used by the C-ABI / tests
+    const std::vector<double>& GetP() const { return p; }
+    const std::vector<double>& GetLogQ();           // fetches log q from the device
+    const std::vector<int32_t>& GetTrimmedIndex() const { return trimmed_weights; }
+    const std::vector<double>& GetPathCounts() const { return path_count_local; }   // per local corpus string
+    const std::vector<uint8_t>& GetRecognized() const { return recognized_local; }
+    double GetWeight(int32_t i) const;
+    void SetWeights(const double* x);
+    double GetLogLikelihood() const { return loglik; }
+    double GetPLogP() const { return plogp; }
+    wfsa_dev* Device() const { return dev; }
+    const FlatModel* Model() const { return flat.get(); }
+    int64_t ShardBegin() const { return shard_begin; }
+    int64_t ShardEnd() const { return shard_end; }
+
+protected:
+    virtual void FinalizeCallback();
+    virtual void InitCallback(int flags);
+    void LambdaUpdate(double* lstep, double* l, double eta = 1.0, bool exponential = false) const;
+
+    // One device evaluation at the current _x: loglik, gradient (trimmed,
+    // reference sign: -sum p E[count]) into `grad_out`.
+    void EvaluateDevice(std::vector<double>& grad_out, bool want_logq);
+    double AllReduceSum(double v) const;
+
+    std::vector<double> _x;
+    std::vector<double> grad_cache;   // gradient of the last ComputeModeledProbs
+    std::vector<double> p;
+    std::vector<double> logq;
+    std::vector<double> aux;
+    std::vector<int32_t> Crow, Ccol;
+
+private:
+    void BuildConstraints(const Fsa& fsa);
+    void BuildPaths(const Fsa& fsa, const uint8_t* sym, const int64_t* off, const double* weights, int64_t n);
+    void Trim();
+    void EnsureDevice();
+
+    double common_support = 0, plogp = 0, kl = 0, aux_hessian = 0, model_volume = 0, loglik = 0;
+    int64_t auxiliary_parameters = 0;
+    int64_t n_strings_global = 0, n_paths_global = 0;
+    bool unique_paths = true;
+    int32_t n_full = 0;
+    std::vector<int32_t> trimmed_weights;
+    std::vector<double> w_full, grad_full;
+    std::vector<double> path_count_local;
+    std::vector<uint8_t> recognized_local;
+    bool logq_valid = false;
+
+    int device = 0;
+    wfsa_dev* dev = nullptr;
+    int nranks = 1, rank = 0;
+    std::vector<uint8_t> comm_id;
+    std::unique_ptr<FlatModel> flat;
+    int64_t shard_begin = 0, shard_end = 0;
+};
+
+void ThrowOnDevError(int rc, const char* what);
+
+}  // namespace wfsa

@@ -1,0 +1,101 @@
+#include "QuasiNewtonLearner.hpp"
+
+#include <algorithm>
+#include <cmath>
+
+namespace wfsa {
+
+void QuasiNewtonLearner::FinalizeCallback() {   // src/QuasiNewtonLearner.cpp:17-27
+    const size_t n = size_t(GetNumberOfParameters()), k = size_t(GetNumberOfConstraints());
+    grad.assign(n, 0.0);
+    expx.assign(n, 0.0);
+    rhs.assign(n, 0.0);
+    lambda.assign(k, 1.0);
+    g.assign(k, 0.0);
+}
+
+void QuasiNewtonLearner::InitCallback(int flags) {   // :29-51
+    if (flags & 1) std::fill(_x.begin(), _x.end(), 0.0);
+    if (flags & 2) Renormalize();
+    if (flags & 4) {
+        ComputeExpX();
+        ComputeGrad();
+        std::fill(lambda.begin(), lambda.end(), 0.0);   // lambda <- -C^T grad
+        for (size_t i = 0; i < grad.size(); ++i) lambda[size_t(Ccol[i])] -= grad[i];
+    }
+    exponential_lambda = (flags & 32) != 0;
+}
+
+void QuasiNewtonLearner::ComputeExpX() {
+    for (size_t i = 0; i < _x.size(); ++i) expx[i] = std::exp(_x[i]);
+}
+
+std::string QuasiNewtonLearner::GetOptimizationHeader() const {
+    return "       KL   graderr     g_min     g_max lambdamin      rmin";
+}
+
+// [KL, graderr, g_min, g_max, lambda_min, rmin, rmin index].  The last two
+// (smallest relative path probability, src/QuasiNewtonLearner.cpp:80-84)
+// need an explicit path list and are reported as 0.
+std::vector<double> QuasiNewtonLearner::GetOptimizationInfo() {
+    return {GetKLDistance(), grad_error, g_min, g_max, lambda_min, 0.0, 0.0};
+}
+
+bool QuasiNewtonLearner::HaltCondition(double tol) {   // :88-91
+    return grad_error <= tol && std::abs(g_min) <= tol && std::abs(g_max) <= tol;
+}
+
+// grad = -sum_s p_s E[count | s] straight from the device; the reference's
+// grad_aux / relative_path_probs bookkeeping (:93-125) has no counterpart.
+void QuasiNewtonLearner::ComputeGrad() {
+    ComputeModeledProbs();
+    grad = grad_cache;
+}
+
+void QuasiNewtonLearner::ComputeLambdaNext(std::vector<double>& result) {   // :127-146
+    const size_t k = size_t(GetNumberOfConstraints());
+    result.resize(k);
+    for (size_t c = 0; c < k; ++c) result[c] = lambda[c] * g[c];
+    for (size_t i = 0; i < grad.size(); ++i) result[size_t(Ccol[i])] -= grad[i];
+    for (size_t c = 0; c < k; ++c) {
+        g[c] += 1.0;
+        result[c] /= g[c];
+    }
+}
+
+void QuasiNewtonLearner::ComputeG() {   // :148-160: g = C^T exp(x) - 1
+    std::fill(g.begin(), g.end(), -1.0);
+    for (size_t i = 0; i < expx.size(); ++i) g[size_t(Ccol[i])] += expx[i];
+    if (g.empty()) {
+        g_min = g_max = 0.0;
+        return;
+    }
+    g_min = *std::min_element(g.begin(), g.end());
+    g_max = *std::max_element(g.begin(), g.end());
+}
+
+void QuasiNewtonLearner::OptimizationStep(double eta, bool) {   // :162-201
+    ComputeExpX();
+    ComputeG();
+    ComputeGrad();
+    ComputeObjective();
+    const size_t n = _x.size(), k = lambda.size();
+    aux.resize(n);
+    grad_error = 0.0;
+    for (size_t i = 0; i < n; ++i) {
+        aux[i] = expx[i] * lambda[size_t(Ccol[i])];   // J_g . lambda
+        rhs[i] = grad[i] + aux[i];
+        grad_error = std::max(grad_error, std::abs(rhs[i]));
+    }
+    lambda_min = k ? *std::min_element(lambda.begin(), lambda.end()) : 0.0;
+    std::vector<double> laux;
+    ComputeLambdaNext(laux);
+    for (size_t i = 0; i < n; ++i) {
+        rhs[i] = (grad[i] + expx[i] * laux[size_t(Ccol[i])]) / aux[i];
+        _x[i] -= eta * rhs[i];
+    }
+    for (size_t c = 0; c < k; ++c) laux[c] = lambda[c] - laux[c];
+    LambdaUpdate(laux.data(), lambda.data(), eta, exponential_lambda);
+}
+
+}  // namespace wfsa

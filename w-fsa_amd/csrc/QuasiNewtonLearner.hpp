@@ -1,0 +1,36 @@
+// QuasiNewtonLearner: mirror of the reference's optimizer
+// (inc/QuasiNewtonLearner.h, src/QuasiNewtonLearner.cpp).  The KKT-diagonal
+// update is O(n + k) host work; ComputeGrad is one device forward-backward.
+#pragma once
+
+#include "Learner.hpp"
+
+namespace wfsa {
+
+class QuasiNewtonLearner : public Learner {
+public:
+    QuasiNewtonLearner() {}
+    void OptimizationStep(double eta = 1.0, bool verbose = false) override;
+    std::vector<double> GetOptimizationInfo() override;
+    std::string GetOptimizationHeader() const override;
+    bool HaltCondition(double tol) override;
+
+    const std::vector<double>& GetGradient() const { return grad; }
+    const std::vector<double>& GetLambda() const { return lambda; }
+
+    void ComputeExpX();
+    void ComputeG();
+    void ComputeGrad();
+
+protected:
+    void FinalizeCallback() override;
+    void InitCallback(int flags) override;
+    void ComputeLambdaNext(std::vector<double>& result);
+
+private:
+    std::vector<double> grad, expx, lambda, g, rhs;
+    double grad_error = 0, lambda_min = 0, g_min = 0, g_max = 0;
+    bool exponential_lambda = false;
+};
+
+}  // namespace wfsa

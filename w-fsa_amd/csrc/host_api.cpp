@@ -1,0 +1,373 @@
+// C ABI over the host mirror (include/wfsa_host.h).  Exceptions stop here.
+#include "wfsa_host.h"
+
+#include <cstdio>
+#include <cstring>
+#include <memory>
+#include <new>
+#include <string>
+#include <vector>
+
+#include "Corpus.hpp"
+#include "Fsa.hpp"
+#include "Learner.hpp"
+#include "QuasiNewtonLearner.hpp"
+#include "synth.hpp"
+
+using namespace wfsa;
+
+struct wfsa_fsa {
+    Fsa fsa;
+    std::unique_ptr<FlatModel> flat;
+};
+
+struct wfsa_corpus {
+    Corpus corpus;
+    PackedStrings packed;
+    std::vector<double> weights;
+};
+
+struct wfsa_learner {
+    std::unique_ptr<QuasiNewtonLearner> qn;
+};
+
+struct wfsa_synth {
+    SynthOutput out;
+};
+
+namespace {
+
+thread_local std::string g_host_error;
+
+template <class F>
+int guarded(F&& f) {
+    try {
+        f();
+        return WFSA_OK;
+    } catch (const std::bad_alloc&) {
+        g_host_error = "out of memory";
+    } catch (const std::exception& e) {
+        g_host_error = e.what();
+    }
+    return WFSA_ERR_ARG;
+}
+
+int null_arg(const char* what) {
+    g_host_error = std::string("null argument: ") + what;
+    return WFSA_ERR_ARG;
+}
+
+}  // namespace
+
+extern "C" {
+
+const char* wfsa_host_last_error(void) { return g_host_error.c_str(); }
+
+int wfsa_fsa_read_text(const char* text, wfsa_fsa** out) {
+    if (!text || !out) return null_arg("text/out");
+    *out = nullptr;
+    return guarded([&] {
+        std::unique_ptr<wfsa_fsa> f(new wfsa_fsa());
+        f->fsa.ReadText(text);
+        *out = f.release();
+    });
+}
+
+int wfsa_fsa_read_file(const char* path, wfsa_fsa** out) {
+    if (!path || !out) return null_arg("path/out");
+    *out = nullptr;
+    return guarded([&] {
+        FILE* fp = std::fopen(path, "rb");
+        if (!fp) throw FsaError("Unable to open \"", path, "\"!");
+        std::unique_ptr<wfsa_fsa> f(new wfsa_fsa());
+        try {
+            f->fsa.Read(fp);
+        } catch (...) {
+            std::fclose(fp);
+            throw;
+        }
+        std::fclose(fp);
+        *out = f.release();
+    });
+}
+
+void wfsa_fsa_free(wfsa_fsa* f) { delete f; }
+
+int wfsa_fsa_desc(wfsa_fsa* f, wfsa_model_desc* out) {
+    if (!f || !out) return null_arg("fsa/out");
+    return guarded([&] {
+        if (!f->flat) f->flat.reset(new FlatModel(f->fsa));
+        *out = f->flat->desc();
+    });
+}
+
+int wfsa_fsa_counts(wfsa_fsa* f, int64_t out[6]) {
+    if (!f || !out) return null_arg("fsa/out");
+    out[0] = int64_t(f->fsa.GetNumberOfStates());
+    out[1] = int64_t(f->fsa.GetNumberOfTransitions());
+    out[2] = int64_t(f->fsa.GetNumberOfEmissions());
+    out[3] = int64_t(f->fsa.GetNumberOfParameters());
+    out[4] = int64_t(f->fsa.GetNumberOfConstraints());
+    out[5] = int64_t(f->fsa.GetNumberOfFreeParameters());
+    return WFSA_OK;
+}
+
+int wfsa_fsa_param_name(wfsa_fsa* f, int32_t j, const char** state, int32_t* kind, const char** label) {
+    if (!f || !state || !kind || !label) return null_arg("fsa/outputs");
+    return guarded([&] {
+        if (!f->flat) f->flat.reset(new FlatModel(f->fsa));
+        if (j < 0 || j >= f->flat->n_params) throw FsaError("parameter index ", j, " out of range");
+        *state = f->flat->state_names[size_t(f->flat->param_state[size_t(j)])];
+        *kind = f->flat->param_kind[size_t(j)];
+        *label = f->flat->param_label[size_t(j)];
+    });
+}
+
+static void pack_corpus(wfsa_corpus* c) {
+    c->packed = PackedStrings();
+    c->weights.clear();
+    for (const auto& e : c->corpus) {
+        c->packed.add(e.first);
+        c->weights.push_back(e.second);
+    }
+}
+
+int wfsa_corpus_read_text(const char* text, wfsa_corpus** out) {
+    if (!text || !out) return null_arg("text/out");
+    *out = nullptr;
+    return guarded([&] {
+        std::unique_ptr<wfsa_corpus> c(new wfsa_corpus());
+        c->corpus.ReadText(text);
+        pack_corpus(c.get());
+        *out = c.release();
+    });
+}
+
+int wfsa_corpus_read_file(const char* path, wfsa_corpus** out) {
+    if (!path || !out) return null_arg("path/out");
+    *out = nullptr;
+    return guarded([&] {
+        FILE* fp = std::fopen(path, "rb");
+        if (!fp) throw CorpusError("Unable to open \"", path, "\"!");
+        std::unique_ptr<wfsa_corpus> c(new wfsa_corpus());
+        try {
+            c->corpus.Read(fp);
+        } catch (...) {
+            std::fclose(fp);
+            throw;
+        }
+        std::fclose(fp);
+        pack_corpus(c.get());
+        *out = c.release();
+    });
+}
+
+void wfsa_corpus_free(wfsa_corpus* c) { delete c; }
+
+int wfsa_corpus_view(wfsa_corpus* c, const uint8_t** sym, const int64_t** off, const double** weights,
+                     int64_t* n) {
+    if (!c || !sym || !off || !weights || !n) return null_arg("corpus/outputs");
+    *sym = c->packed.sym.data();
+    *off = c->packed.off.data();
+    *weights = c->weights.data();
+    *n = c->packed.size();
+    return WFSA_OK;
+}
+
+int wfsa_learner_create(const char* optimizer, int device, wfsa_learner** out) {
+    if (!optimizer || !out) return null_arg("optimizer/out");
+    *out = nullptr;
+    return guarded([&] {
+        if (std::strcmp(optimizer, "QuasiNewton") != 0)
+            throw LearnerError("optimizer \"", optimizer, "\" is not available in this build (QuasiNewton only)");
+        std::unique_ptr<wfsa_learner> l(new wfsa_learner());
+        l->qn.reset(new QuasiNewtonLearner());
+        l->qn->SetDevice(device);
+        *out = l.release();
+    });
+}
+
+void wfsa_learner_destroy(wfsa_learner* l) { delete l; }
+
+int wfsa_learner_set_comm(wfsa_learner* l, int nranks, int rank, const uint8_t id[WFSA_COMM_ID_BYTES]) {
+    if (!l) return null_arg("learner");
+    return guarded([&] { l->qn->SetCommunicator(nranks, rank, id); });
+}
+
+int wfsa_learner_build_packed(wfsa_learner* l, wfsa_fsa* f, const uint8_t* sym, const int64_t* off,
+                              const double* weights, int64_t n) {
+    if (!l || !f || !off || (n > 0 && (!weights || !sym))) return null_arg("learner/fsa/corpus");
+    return guarded([&] {
+        double sum = 0.0;
+        for (int64_t s = 0; s < n; ++s) sum += weights[s];
+        std::vector<double> w(weights, weights + n);
+        for (auto& v : w) v /= sum;   // Corpus::Renormalize (main.cpp:154)
+        l->qn->BuildFromPacked(f->fsa, sym, off, w.data(), n);
+    });
+}
+
+int wfsa_learner_build(wfsa_learner* l, wfsa_fsa* f, wfsa_corpus* c) {
+    if (!l || !f || !c) return null_arg("learner/fsa/corpus");
+    return wfsa_learner_build_packed(l, f, c->packed.sym.data(), c->packed.off.data(), c->weights.data(),
+                                     c->packed.size());
+}
+
+int wfsa_learner_finalize(wfsa_learner* l) {
+    if (!l) return null_arg("learner");
+    return guarded([&] {
+        if (l->qn->GetNumberOfParameters() == 0) throw LearnerError("Empty automaton!");
+        if (l->qn->GetNumberOfStrings() == 0) throw LearnerError("Automaton cannot generate any of the strings!");
+        l->qn->Finalize();
+    });
+}
+
+int wfsa_learner_info_get(wfsa_learner* l, wfsa_learner_info* o) {
+    if (!l || !o) return null_arg("learner/out");
+    QuasiNewtonLearner& q = *l->qn;
+    o->n_strings = q.GetNumberOfStrings();
+    o->n_local_strings = q.GetNumberOfLocalStrings();
+    o->n_paths = q.GetNumberOfPaths();
+    o->n_full = q.GetNumberOfFullParameters();
+    o->n_params = q.GetNumberOfParameters();
+    o->n_constraints = q.GetNumberOfConstraints();
+    o->unique_paths = q.HasUniquePaths() ? 1 : 0;
+    o->aux_params = q.GetNumberOfAuxParameters();
+    o->common_support = q.GetCommonSupport();
+    o->plogp = q.GetPLogP();
+    o->model_volume = q.LogModelVolume();
+    o->aux_hessian = q.LogDetAuxiliaryHessian();
+    o->kl = q.GetKLDistance();
+    o->loglik = q.GetLogLikelihood();
+    o->shard_begin = q.ShardBegin();
+    o->shard_end = q.ShardEnd();
+    return WFSA_OK;
+}
+
+int wfsa_learner_init(wfsa_learner* l, int flags, const double* x0) {
+    if (!l) return null_arg("learner");
+    return guarded([&] { l->qn->Init(flags, x0); });
+}
+
+int wfsa_learner_step(wfsa_learner* l, double eta, double tol, double info[7], int32_t* halt) {
+    if (!l) return null_arg("learner");
+    return guarded([&] {
+        l->qn->OptimizationStep(eta, false);
+        const auto v = l->qn->GetOptimizationInfo();
+        if (info)
+            for (size_t i = 0; i < 7; ++i) info[i] = i < v.size() ? v[i] : 0.0;
+        if (halt) *halt = l->qn->HaltCondition(tol) ? 1 : 0;
+    });
+}
+
+int wfsa_learner_objective_grad(wfsa_learner* l, double* kl, double* grad, double* logq) {
+    if (!l) return null_arg("learner");
+    return guarded([&] {
+        QuasiNewtonLearner& q = *l->qn;
+        q.ComputeExpX();
+        q.ComputeGrad();
+        q.ComputeObjective();
+        if (kl) *kl = q.GetKLDistance();
+        if (grad) std::memcpy(grad, q.GetGradient().data(), q.GetGradient().size() * sizeof(double));
+        if (logq) {
+            const auto& lq = q.GetLogQ();
+            std::memcpy(logq, lq.data(), lq.size() * sizeof(double));
+        }
+    });
+}
+
+int wfsa_learner_get_x(wfsa_learner* l, double* x) {
+    if (!l || !x) return null_arg("learner/x");
+    std::memcpy(x, l->qn->GetWeights(), size_t(l->qn->GetNumberOfParameters()) * sizeof(double));
+    return WFSA_OK;
+}
+
+int wfsa_learner_set_x(wfsa_learner* l, const double* x) {
+    if (!l || !x) return null_arg("learner/x");
+    l->qn->SetWeights(x);
+    return WFSA_OK;
+}
+
+int wfsa_learner_get_p(wfsa_learner* l, double* p) {
+    if (!l || !p) return null_arg("learner/p");
+    const auto& v = l->qn->GetP();
+    std::memcpy(p, v.data(), v.size() * sizeof(double));
+    return WFSA_OK;
+}
+
+int wfsa_learner_trimmed_index(wfsa_learner* l, int32_t* out) {
+    if (!l || !out) return null_arg("learner/out");
+    const auto& v = l->qn->GetTrimmedIndex();
+    std::memcpy(out, v.data(), v.size() * sizeof(int32_t));
+    return WFSA_OK;
+}
+
+int wfsa_learner_path_counts(wfsa_learner* l, double* out, uint8_t* recognized) {
+    if (!l) return null_arg("learner");
+    const auto& pc = l->qn->GetPathCounts();
+    const auto& rc = l->qn->GetRecognized();
+    if (out) std::memcpy(out, pc.data(), pc.size() * sizeof(double));
+    if (recognized) std::memcpy(recognized, rc.data(), rc.size());
+    return WFSA_OK;
+}
+
+int wfsa_learner_renormalize(wfsa_learner* l) {
+    if (!l) return null_arg("learner");
+    return guarded([&] { l->qn->Renormalize(); });
+}
+
+int wfsa_learner_dump(wfsa_learner* l, wfsa_fsa* f, const char* path) {
+    if (!l || !f || !path) return null_arg("learner/fsa/path");
+    return guarded([&] {
+        l->qn->RewriteWeights(f->fsa);
+        FILE* fp = std::fopen(path, "wb");
+        if (!fp) throw LearnerError("Unable to open output file \"", path, "\" for writing!");
+        f->fsa.Dump(fp);
+        std::fclose(fp);
+    });
+}
+
+int wfsa_learner_stats(wfsa_learner* l, wfsa_dev_stats* out) {
+    if (!l || !out) return null_arg("learner/out");
+    if (!l->qn->Device()) {
+        g_host_error = "learner has no device context yet";
+        return WFSA_ERR_ARG;
+    }
+    return wfsa_dev_get_stats(l->qn->Device(), out);
+}
+
+int wfsa_synth_make(int32_t n_states, int32_t degree, int32_t vocab, int32_t emissions, int32_t dense,
+                    int64_t n_strings, int32_t max_len, uint64_t seed, wfsa_synth** out) {
+    if (!out) return null_arg("out");
+    *out = nullptr;
+    return guarded([&] {
+        SynthSpec spec;
+        spec.n_states = n_states;
+        spec.degree = degree;
+        spec.vocab = vocab;
+        spec.emissions = emissions;
+        spec.dense = dense;
+        spec.n_strings = n_strings;
+        spec.max_len = max_len;
+        spec.seed = seed;
+        std::unique_ptr<wfsa_synth> s(new wfsa_synth());
+        const std::string err = make_synthetic(spec, s->out);
+        if (!err.empty()) throw MyError(err);
+        *out = s.release();
+    });
+}
+
+void wfsa_synth_free(wfsa_synth* s) { delete s; }
+
+const char* wfsa_synth_wfsa_text(wfsa_synth* s) { return s ? s->out.wfsa_text.c_str() : ""; }
+
+int wfsa_synth_corpus(wfsa_synth* s, const uint8_t** sym, const int64_t** off, const double** weights,
+                      int64_t* n) {
+    if (!s || !sym || !off || !weights || !n) return null_arg("synth/outputs");
+    *sym = s->out.sym.data();
+    *off = s->out.off.data();
+    *weights = s->out.weights.data();
+    *n = int64_t(s->out.weights.size());
+    return WFSA_OK;
+}
+
+}  // extern "C"

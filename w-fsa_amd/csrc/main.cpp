@@ -1,0 +1,182 @@
+// wfsa: command-line driver with the reference's flags (src/main.cpp:66-108)
+// for the QuasiNewton optimizer, running the objective/gradient on the GPU.
+//
+//   wfsa -a A.wfsa -c C.corpus [-opt QuasiNewton] [-e epochs] [-l eta]
+//        [-tol t] [-i flags] [-n] [-eval] [-s] [-o out.wfsa] [-x] [-d device]
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <iostream>
+#include <string>
+#include <vector>
+
+#include "Corpus.hpp"
+#include "Fsa.hpp"
+#include "QuasiNewtonLearner.hpp"
+
+using namespace wfsa;
+
+namespace {
+
+// PrintFixedWidth (src/Utils.cpp:82-97): the epoch table's number format
+void print_fixed_width(FILE* out, double x, int width) {
+    const int mag = (x == 0) ? 0 : int(std::floor(std::log10(std::abs(x))));
+    if (mag <= width - 2 && mag >= 0) {
+        if (std::floor(x) == x) std::fprintf(out, "%*.0f", width, x);
+        else std::fprintf(out, "%*.*f", width, std::max(0, width - 3 - mag), x);
+    } else if (-4 < mag && mag < 0) {
+        std::fprintf(out, "%*.*f", width, width - 3, x);
+    } else {
+        std::fprintf(out, "%*.*e", width, width - 7, x);
+    }
+}
+
+void usage() {
+    std::cerr << "usage: wfsa -a automaton.wfsa -c strings.corpus [options]\n"
+                 "  -a, --automaton FILE   FSA to load\n"
+                 "  -c, --corpus FILE      corpus to load\n"
+                 "  -o, --output FILE      write the learned WFSA here (default stdout)\n"
+                 "  -e, --epochs N         maximum optimization epochs (20)\n"
+                 "  -l, --eta X            learning rate (1.0)\n"
+                 "  -tol X                 halting tolerance (1e-6)\n"
+                 "  -i, --init FLAGS       1 uniform, 2 normalize, 4 Lagrange init, 32 exponential lambda\n"
+                 "  -n, --normalize        normalize the automaton after optimization\n"
+                 "  -eval                  evaluate the model after optimization\n"
+                 "  -s, --suppress         do not print the learned FSA\n"
+                 "  -x, --initx            read the initial x vector from stdin\n"
+                 "  -opt NAME              QuasiNewton (Hessian is not part of this build)\n"
+                 "  -d, --device N         GPU to use (0)\n";
+}
+
+}  // namespace
+
+int main(int argc, const char* argv[]) {
+    std::string automaton, corpus_file, output, optimizer = "QuasiNewton";
+    int epochs = 20, initflags = 0, device = 0;
+    double eta = 1.0, tol = 1e-6;
+    bool normalize = false, suppress = false, evaluate = false, initx = false;
+    for (int i = 1; i < argc; ++i) {
+        const std::string a = argv[i];
+        auto next = [&]() -> const char* {
+            if (i + 1 >= argc) {
+                std::cerr << "missing value for " << a << std::endl;
+                std::exit(1);
+            }
+            return argv[++i];
+        };
+        if (a == "-h" || a == "--help") { usage(); return 0; }
+        else if (a == "-a" || a == "--automaton" || a == "--load") automaton = next();
+        else if (a == "-c" || a == "--corpus") corpus_file = next();
+        else if (a == "-o" || a == "--output") output = next();
+        else if (a == "-e" || a == "--epoch" || a == "--epochs") epochs = std::atoi(next());
+        else if (a == "-l" || a == "--learning" || a == "--eta") eta = std::atof(next());
+        else if (a == "-tol" || a == "--tol" || a == "--tolerance") tol = std::atof(next());
+        else if (a == "-i" || a == "--init") initflags = std::atoi(next());
+        else if (a == "-opt" || a == "--optimizer") optimizer = next();
+        else if (a == "-d" || a == "--device") device = std::atoi(next());
+        else if (a == "-n" || a == "--normalize") normalize = true;
+        else if (a == "-eval" || a == "--eval" || a == "--evaluate") evaluate = true;
+        else if (a == "-s" || a == "--suppress") suppress = true;
+        else if (a == "-x" || a == "--initx" || a == "--initial") initx = true;
+        else if (a == "-p" || a == "--print" || a == "-pr" || a == "--print-recognize") { /* no path listing */ }
+        else { std::cerr << "unknown argument " << a << std::endl; usage(); return 1; }
+    }
+    if (optimizer != "QuasiNewton") {
+        std::cerr << "optimizer \"" << optimizer << "\" is not available in this build (QuasiNewton only)" << std::endl;
+        return 1;
+    }
+    try {
+        Corpus corpus;
+        if (FILE* f = std::fopen(corpus_file.c_str(), "rb")) {
+            corpus.Read(f);
+            std::fclose(f);
+        } else {
+            std::cerr << "\nUnable to open \"" << corpus_file << "\"!" << std::endl;
+            return 1;
+        }
+        std::cerr << "Corpus:\n\tsize: " << corpus.size() << "\n\tsum: " << corpus.Sum();
+        corpus.Renormalize();
+        std::cerr << ", renormalized to " << corpus.Sum() << std::endl;
+        Fsa fsa;
+        if (FILE* f = std::fopen(automaton.c_str(), "rb")) {
+            fsa.Read(f);
+            std::fclose(f);
+        } else {
+            std::cerr << "\nUnable to open \"" << automaton << "\"!" << std::endl;
+            return 1;
+        }
+        std::cerr << "Automaton:\n\tstates: " << fsa.GetNumberOfStates()
+                  << "\n\ttransitions: " << fsa.GetNumberOfTransitions()
+                  << "\n\temissions: " << fsa.GetNumberOfEmissions()
+                  << "\n\tparameters: " << fsa.GetNumberOfParameters()
+                  << "\n\tconstraints: " << fsa.GetNumberOfConstraints()
+                  << "\n\tfree parameters: " << fsa.GetNumberOfFreeParameters() << std::endl;
+        QuasiNewtonLearner learner;
+        learner.SetDevice(device);
+        learner.BuildFrom(fsa, corpus);
+        std::cerr << "Recognize:\n\tstrings: " << learner.GetNumberOfStrings()
+                  << "\n\tpaths: " << learner.GetNumberOfPaths()
+                  << "\n\tcommon support: " << learner.GetCommonSupport()
+                  << "\n\tunique paths: " << (learner.HasUniquePaths() ? "true" : "false")
+                  << "\nAfter trimming:\n\tparameters: " << learner.GetNumberOfParameters()
+                  << "\n\tconstraints: " << learner.GetNumberOfConstraints() << std::endl;
+        if (learner.GetNumberOfParameters() == 0) {
+            std::cerr << "Empty automaton!" << std::endl;
+            return 1;
+        }
+        if (learner.GetNumberOfStrings() == 0) {
+            std::cerr << "Automaton cannot generate any of the strings!" << std::endl;
+            return 1;
+        }
+        learner.Finalize();
+        std::cerr << "Initialize ... ";
+        if (initx) {
+            std::vector<double> x;
+            while (std::cin && int32_t(x.size()) < learner.GetNumberOfParameters()) {
+                x.emplace_back();
+                std::cin >> x.back();
+            }
+            if (!std::cin) throw MyError("Cannot read initial x value!");
+            learner.Init(initflags, x.data());
+        } else {
+            learner.Init(initflags);
+        }
+        std::cerr << "done" << std::endl;
+        const int width = int(std::ceil(std::log10(epochs + 1)));
+        if (epochs > 0) std::cerr << "Optimization:" << std::endl;
+        for (int e = 1; e <= epochs; ++e) {
+            if (e % 20 == 1) std::cerr << "epoch\t" << learner.GetOptimizationHeader() << std::endl;
+            learner.OptimizationStep(eta, false);
+            std::fprintf(stderr, "%0*d\t", width, e);
+            const auto info = learner.GetOptimizationInfo();
+            for (double x : info) {
+                print_fixed_width(stderr, x, 9);
+                std::fputs(" ", stderr);
+            }
+            std::cerr << std::endl;
+            for (double x : info)
+                if (!std::isfinite(x)) throw LearnerError(x, " detected at epoch ", e);
+            if (learner.HaltCondition(tol)) break;
+        }
+        if (normalize) learner.Renormalize();
+        if (evaluate) {
+            const auto results = learner.GetOptimizationResult(false);
+            std::cerr.precision(15);
+            std::cerr << "Result:";
+            for (double x : results) std::cerr << ' ' << x;
+            std::cerr << std::endl;
+        }
+        if (!suppress) {
+            FILE* outf = output.empty() ? stdout : std::fopen(output.c_str(), "w");
+            if (!outf) throw MyError("Unable to open output file \"", output, "\" for writing!");
+            learner.RewriteWeights(fsa);
+            fsa.Dump(outf);
+            if (outf != stdout) std::fclose(outf);
+        }
+    } catch (const std::exception& e) {
+        std::fprintf(stderr, "%s\n", e.what());
+        return 1;
+    }
+    return 0;
+}

@@ -1,0 +1,322 @@
+"""MI355X-native objective/gradient path of w-fsa (weighted FSA weight learning).
+
+Python mirror of the reference's host interface (Fsa, Corpus, Learner,
+QuasiNewtonLearner; inc/*.h of gaebor/w-fsa) over the C ABI in
+include/wfsa_host.h, plus direct access to the device boundary
+(include/wfsa_dev.h) through `Device`.  All compute runs in the HIP library
+libwfsa_amd.so on a gfx950 GPU; there is no CPU fallback.
+"""
+import ctypes as C
+
+import numpy as np
+
+from . import _lib
+from ._lib import WfsaError, check_dev, check_host, load
+
+__all__ = ["Fsa", "Corpus", "QuasiNewtonLearner", "Device", "Synthetic", "WfsaError", "load"]
+
+
+def _ptr(a):
+    return None if a is None else a.ctypes.data_as(C.c_void_p)
+
+
+def _b(s):
+    return s if isinstance(s, bytes) else s.encode("latin-1")
+
+
+class Fsa:
+    """The automaton (inc/Fsa.h): .wfsa reader, parameter numbering, Dump."""
+
+    def __init__(self, handle):
+        self._h = handle
+
+    @classmethod
+    def read_text(cls, text):
+        h = C.c_void_p()
+        check_host(load().wfsa_fsa_read_text(_b(text), C.byref(h)))
+        return cls(h)
+
+    @classmethod
+    def read_file(cls, path):
+        h = C.c_void_p()
+        check_host(load().wfsa_fsa_read_file(_b(path), C.byref(h)))
+        return cls(h)
+
+    def __del__(self):
+        if getattr(self, "_h", None):
+            load().wfsa_fsa_free(self._h)
+            self._h = None
+
+    def counts(self):
+        a = np.zeros(6, dtype=np.int64)
+        check_host(load().wfsa_fsa_counts(self._h, _ptr(a)))
+        keys = ("states", "transitions", "emissions", "parameters", "constraints", "free_parameters")
+        return dict(zip(keys, (int(v) for v in a)))
+
+    def desc(self):
+        d = _lib.ModelDesc()
+        check_host(load().wfsa_fsa_desc(self._h, C.byref(d)))
+        return d
+
+    def param_name(self, j):
+        s, k, l = C.c_char_p(), C.c_int32(), C.c_char_p()
+        check_host(load().wfsa_fsa_param_name(self._h, j, C.byref(s), C.byref(k), C.byref(l)))
+        return s.value.decode("latin-1"), "ET"[k.value], l.value.decode("latin-1")
+
+    def param_names(self):
+        return [self.param_name(j) for j in range(self.counts()["parameters"])]
+
+
+class Corpus:
+    """The string store (inc/Corpus.h): .corpus reader; weights as read."""
+
+    def __init__(self, handle):
+        self._h = handle
+
+    @classmethod
+    def read_text(cls, text):
+        h = C.c_void_p()
+        check_host(load().wfsa_corpus_read_text(_b(text), C.byref(h)))
+        return cls(h)
+
+    @classmethod
+    def read_file(cls, path):
+        h = C.c_void_p()
+        check_host(load().wfsa_corpus_read_file(_b(path), C.byref(h)))
+        return cls(h)
+
+    def __del__(self):
+        if getattr(self, "_h", None):
+            load().wfsa_corpus_free(self._h)
+            self._h = None
+
+    def packed(self):
+        """(sym uint8[], off int64[n+1], weights float64[n]) copies"""
+        sym, off, w, n = C.c_void_p(), C.c_void_p(), C.c_void_p(), C.c_int64()
+        check_host(load().wfsa_corpus_view(self._h, C.byref(sym), C.byref(off), C.byref(w), C.byref(n)))
+        n = n.value
+        off_a = np.ctypeslib.as_array(C.cast(off, C.POINTER(C.c_int64)), shape=(n + 1,)).copy()
+        w_a = np.ctypeslib.as_array(C.cast(w, C.POINTER(C.c_double)), shape=(max(n, 1),))[:n].copy()
+        total = int(off_a[-1])
+        sym_a = (np.ctypeslib.as_array(C.cast(sym, C.POINTER(C.c_uint8)), shape=(total,)).copy()
+                 if total else np.zeros(0, dtype=np.uint8))
+        return sym_a, off_a, w_a
+
+    def strings(self):
+        sym, off, w = self.packed()
+        return [bytes(sym[off[i]:off[i + 1]]).decode("latin-1") for i in range(len(w))], w
+
+
+class Synthetic:
+    """Synthetic automaton + corpus (SURVEY.md 8d families)."""
+
+    def __init__(self, n_states=1024, degree=8, vocab=64, emissions=1, dense=False, n_strings=1000,
+                 max_len=128, seed=1):
+        h = C.c_void_p()
+        check_host(load().wfsa_synth_make(n_states, degree, vocab, emissions, int(dense), n_strings, max_len,
+                                          seed, C.byref(h)))
+        self._h = h
+        self.wfsa_text = load().wfsa_synth_wfsa_text(h).decode("latin-1")
+
+    def __del__(self):
+        if getattr(self, "_h", None):
+            load().wfsa_synth_free(self._h)
+            self._h = None
+
+    def corpus(self):
+        sym, off, w, n = C.c_void_p(), C.c_void_p(), C.c_void_p(), C.c_int64()
+        check_host(load().wfsa_synth_corpus(self._h, C.byref(sym), C.byref(off), C.byref(w), C.byref(n)))
+        n = n.value
+        off_a = np.ctypeslib.as_array(C.cast(off, C.POINTER(C.c_int64)), shape=(n + 1,)).copy()
+        w_a = np.ctypeslib.as_array(C.cast(w, C.POINTER(C.c_double)), shape=(n,)).copy()
+        sym_a = np.ctypeslib.as_array(C.cast(sym, C.POINTER(C.c_uint8)), shape=(int(off_a[-1]),)).copy()
+        return sym_a, off_a, w_a
+
+
+class QuasiNewtonLearner:
+    """inc/QuasiNewtonLearner.h: BuildFrom -> Finalize -> Init -> OptimizationStep*."""
+
+    def __init__(self, device=0, optimizer="QuasiNewton"):
+        h = C.c_void_p()
+        check_host(load().wfsa_learner_create(_b(optimizer), device, C.byref(h)))
+        self._h = h
+        self._fsa = None
+
+    def __del__(self):
+        if getattr(self, "_h", None):
+            load().wfsa_learner_destroy(self._h)
+            self._h = None
+
+    def SetCommunicator(self, nranks, rank, unique_id):
+        buf = (C.c_uint8 * _lib.COMM_ID_BYTES).from_buffer_copy(bytes(unique_id))
+        check_host(load().wfsa_learner_set_comm(self._h, nranks, rank, buf))
+
+    def BuildFrom(self, fsa, corpus):
+        self._fsa = fsa
+        check_host(load().wfsa_learner_build(self._h, fsa._h, corpus._h))
+
+    def BuildFromPacked(self, fsa, sym, off, weights):
+        self._fsa = fsa
+        sym = np.ascontiguousarray(sym, dtype=np.uint8)
+        off = np.ascontiguousarray(off, dtype=np.int64)
+        weights = np.ascontiguousarray(weights, dtype=np.float64)
+        check_host(load().wfsa_learner_build_packed(self._h, fsa._h, _ptr(sym), _ptr(off), _ptr(weights),
+                                                    len(off) - 1))
+
+    def Finalize(self):
+        check_host(load().wfsa_learner_finalize(self._h))
+
+    def info(self):
+        i = _lib.LearnerInfo()
+        check_host(load().wfsa_learner_info_get(self._h, C.byref(i)))
+        return {f: getattr(i, f) for f, _ in _lib.LearnerInfo._fields_}
+
+    @property
+    def n(self):
+        return self.info()["n_params"]
+
+    def Init(self, flags, x0=None):
+        x0 = None if x0 is None else np.ascontiguousarray(x0, dtype=np.float64)
+        check_host(load().wfsa_learner_init(self._h, flags, _ptr(x0)))
+
+    def OptimizationStep(self, eta=1.0, tol=1e-6):
+        info = np.zeros(7, dtype=np.float64)
+        halt = C.c_int32()
+        check_host(load().wfsa_learner_step(self._h, eta, tol, _ptr(info), C.byref(halt)))
+        return info, bool(halt.value)
+
+    def objective_grad(self, want_logq=False):
+        """(KL, grad[n_params], logq or None) at the current x"""
+        inf = self.info()
+        grad = np.zeros(inf["n_params"], dtype=np.float64)
+        logq = np.zeros(inf["n_local_strings"], dtype=np.float64) if want_logq else None
+        kl = C.c_double()
+        check_host(load().wfsa_learner_objective_grad(self._h, C.byref(kl), _ptr(grad), _ptr(logq)))
+        return kl.value, grad, logq
+
+    def x(self):
+        a = np.zeros(self.n, dtype=np.float64)
+        check_host(load().wfsa_learner_get_x(self._h, _ptr(a)))
+        return a
+
+    def set_x(self, x):
+        x = np.ascontiguousarray(x, dtype=np.float64)
+        assert x.shape == (self.n,)
+        check_host(load().wfsa_learner_set_x(self._h, _ptr(x)))
+
+    def p(self):
+        a = np.zeros(self.info()["n_local_strings"], dtype=np.float64)
+        check_host(load().wfsa_learner_get_p(self._h, _ptr(a)))
+        return a
+
+    def trimmed_index(self):
+        a = np.zeros(self.info()["n_full"], dtype=np.int32)
+        check_host(load().wfsa_learner_trimmed_index(self._h, _ptr(a)))
+        return a
+
+    def path_counts(self):
+        inf = self.info()
+        m = inf["shard_end"] - inf["shard_begin"]
+        pc = np.zeros(m, dtype=np.float64)
+        rec = np.zeros(m, dtype=np.uint8)
+        check_host(load().wfsa_learner_path_counts(self._h, _ptr(pc), _ptr(rec)))
+        return pc, rec
+
+    def Renormalize(self):
+        check_host(load().wfsa_learner_renormalize(self._h))
+
+    def Dump(self, path, fsa=None):
+        check_host(load().wfsa_learner_dump(self._h, (fsa or self._fsa)._h, _b(path)))
+
+    def stats(self):
+        s = _lib.DevStats()
+        check_host(load().wfsa_learner_stats(self._h, C.byref(s)))
+        return {f: getattr(s, f) for f, _ in _lib.DevStats._fields_}
+
+    def param_names(self):
+        """trimmed index -> (state, kind, label)"""
+        fsa = self._fsa
+        tw = self.trimmed_index()
+        names = [None] * self.n
+        for j, t in enumerate(tw):
+            if t >= 0:
+                names[t] = fsa.param_name(j)
+        return names
+
+    def run(self, flags=7, epochs=20, eta=1.0, tol=1e-6):
+        """main.cpp's epoch loop (src/main.cpp:276-303): list of info rows"""
+        self.Init(flags)
+        rows = []
+        for _ in range(epochs):
+            info, halt = self.OptimizationStep(eta, tol)
+            rows.append(info)
+            if not np.all(np.isfinite(info)):
+                raise WfsaError(-1, "non-finite epoch info")
+            if halt:
+                break
+        return rows
+
+
+class Device:
+    """Direct handle on the device boundary (include/wfsa_dev.h)."""
+
+    def __init__(self, device=0):
+        h = C.c_void_p()
+        check_dev(load().wfsa_dev_create(device, C.byref(h)))
+        self._h = h
+        self.n_params = 0
+        self.n_strings = 0
+
+    def __del__(self):
+        if getattr(self, "_h", None):
+            load().wfsa_dev_destroy(self._h)
+            self._h = None
+
+    def load_model(self, fsa):
+        d = fsa.desc()
+        self._fsa = fsa   # keeps the desc arrays alive
+        check_dev(load().wfsa_dev_load_model(self._h, C.byref(d)))
+        self.n_params = d.n_params
+
+    def load_corpus(self, sym, off, p):
+        self._sym = np.ascontiguousarray(sym, dtype=np.uint8)
+        self._off = np.ascontiguousarray(off, dtype=np.int64)
+        self._p = np.ascontiguousarray(p, dtype=np.float64)
+        check_dev(load().wfsa_dev_load_corpus(self._h, _ptr(self._sym), _ptr(self._off), _ptr(self._p),
+                                              len(self._off) - 1))
+        self.n_strings = len(self._off) - 1
+
+    def recognize(self):
+        rec = np.zeros(self.n_strings, dtype=np.uint8)
+        pc = np.zeros(self.n_strings, dtype=np.float64)
+        used = np.zeros(max(self.n_params, 1), dtype=np.uint8)
+        check_dev(load().wfsa_dev_recognize(self._h, _ptr(rec), _ptr(pc), _ptr(used)))
+        return rec, pc, used[:self.n_params]
+
+    def objective_grad(self, w_full, want_logq=True):
+        w = np.ascontiguousarray(w_full, dtype=np.float64)
+        grad = np.zeros(max(self.n_params, 1), dtype=np.float64)
+        logq = np.zeros(self.n_strings, dtype=np.float64) if want_logq else None
+        ll = C.c_double()
+        check_dev(load().wfsa_dev_objective_grad(self._h, _ptr(w), C.byref(ll), _ptr(grad), _ptr(logq)))
+        return ll.value, grad[:self.n_params], logq
+
+    def comm_init(self, nranks, rank, unique_id):
+        buf = (C.c_uint8 * _lib.COMM_ID_BYTES).from_buffer_copy(bytes(unique_id))
+        check_dev(load().wfsa_dev_comm_init(self._h, nranks, rank, buf))
+
+    @staticmethod
+    def comm_unique_id():
+        buf = (C.c_uint8 * _lib.COMM_ID_BYTES)()
+        check_dev(load().wfsa_dev_comm_unique_id(buf))
+        return bytes(buf)
+
+    def allreduce(self, values):
+        a = np.ascontiguousarray(values, dtype=np.float64).copy()
+        check_dev(load().wfsa_dev_allreduce(self._h, _ptr(a), len(a)))
+        return a
+
+    def stats(self):
+        s = _lib.DevStats()
+        check_dev(load().wfsa_dev_get_stats(self._h, C.byref(s)))
+        return {f: getattr(s, f) for f, _ in _lib.DevStats._fields_}
