@@ -143,8 +143,12 @@ def main():
 
     strings_all = info["n_strings"]
     value = strings_all * args.steps / dt
-    kern_ms = (st1["fb_kernel_ms"] - st0["fb_kernel_ms"]) / args.steps
-    alg_bytes = local_sym + 16 * local_strings          # bytes + off + p per string
+    kern_ms = (st1["compiled_kernel_ms"] - st0["compiled_kernel_ms"]) / args.steps
+    fb_ms = (st1["fb_kernel_ms"] - st0["fb_kernel_ms"]) / args.steps
+    # algorithmic bytes: string bytes + offset + p per string,
+    # for the strings the compiled kernel serves
+    comp = st1["compiled_strings"]
+    alg_bytes = int(local_sym * comp / max(local_strings, 1)) + 16 * comp
     achieved = alg_bytes / (kern_ms * 1e-3) / 1e9
     traffic = None
     if os.path.exists(args.profile_traffic):
@@ -182,13 +186,19 @@ def main():
             "unit": "GB/s",
             "frac": achieved / HBM_PEAK_GBS,
             "traffic": traffic,
-            "kernel": "fb_kernel<false> (forward-backward, weighted)",
+            "kernel": "fbc_kernel (compiled-stream forward-backward)",
             "kernel_ms_per_launch": kern_ms,
+            "all_fb_kernels_ms_per_step": fb_ms,
             "algorithmic_bytes_per_launch": alg_bytes,
         },
         "live_edges_per_step": st1["last_live_edges"],
         "build_s": t_build,
         "tier1_strings": st1["tier1_strings"],
+        "compiled_strings": st1["compiled_strings"],
+        "fallback_strings": st1["fallback_strings"],
+        "stream_words": st1["stream_words"],
+        "bubble_words": st1["bubble_words"],
+        "prepare_ms": st1["prepare_ms"],
     }
     if rank == 0 and world == 1 and args.cpu_sample > 0:
         cb, rel, ll_ref, ll_dev = cpu_baseline(syn.wfsa_text, sym, off, wt, args.cpu_sample)

@@ -75,13 +75,20 @@ typedef struct {
     int32_t n_nodes;           /* trellis nodes after epsilon removal       */
     int64_t n_edges;           /* byte-consuming composite edges            */
     int64_t n_end_edges;
-    int64_t fb_launches;       /* forward-backward launches timed so far    */
-    double fb_kernel_ms;       /* sum of their HIP-event durations          */
-    double last_fb_kernel_ms;  /* the last objective_grad call's FB kernels */
-    double last_call_ms;       /* the last objective_grad call, end to end  */
-    int64_t last_live_edges;   /* trellis edges touched by the last call    */
-    int32_t tier1_strings;     /* strings served by the large-slab tier     */
+    int64_t compiled_strings;  /* served by the compiled-stream kernel      */
+    int64_t fallback_strings;  /* served by the traversal kernel            */
+    int64_t stream_words;      /* compiled main-stream words (with padding) */
+    int64_t bubble_words;
+    int64_t fb_launches;       /* objective_grad calls timed so far         */
+    double fb_kernel_ms;       /* sum of their forward-backward kernel time */
+    double last_fb_kernel_ms;  /* last call: compiled + traversal kernels   */
+    double last_compiled_ms;   /* last call: compiled-stream kernel alone   */
+    double last_call_ms;       /* last call, device side, end to end        */
+    int64_t last_live_edges;   /* traversal-path trellis edges, last call   */
+    int32_t tier1_strings;     /* strings needing the large-slab tier       */
     int32_t waves_per_block;
+    double prepare_ms;         /* structural pass + stream compilation      */
+    double compiled_kernel_ms; /* sum over calls of the compiled kernel     */
 } wfsa_dev_stats;
 
 /* context ---------------------------------------------------------------- */

@@ -111,9 +111,12 @@ def test_device_matches_oracle_trellis_random_weights(family):
     syn = W.Synthetic(seed=11, **family)
     sym, off, wt = syn.corpus()
     p = wt / wt.sum()
-    w_by_name, ll, grad, logq, rec, pc, _ = _device_eval(syn.wfsa_text, sym, off, p, rng)
+    w_by_name, ll, grad, logq, rec, pc, dev = _device_eval(syn.wfsa_text, sym, off, p, rng)
     oll, ologq, ograd, _ = _oracle_eval(syn.wfsa_text, sym, off, wt, w_by_name)
     assert rec.all()
+    st = dev.stats()
+    assert st["compiled_strings"] + st["fallback_strings"] == len(wt)
+    print(f"compiled {st['compiled_strings']} fallback {st['fallback_strings']} tier1 {st['tier1_strings']}")
     np.testing.assert_allclose(logq, ologq, rtol=1e-11, atol=1e-12)
     assert _close(ll, oll, rel=1e-11)
     keys = sorted(ograd)
@@ -216,6 +219,9 @@ def test_full_size_family_a_properties():
     end = [j for j, n in enumerate(names) if n[1] == "T" and n[2] == "$"]
     assert _close(grad[start].sum(), -1.0, rel=1e-9)
     assert _close(grad[end].sum(), -1.0, rel=1e-9)
+    st = dev.stats()
+    assert st["compiled_strings"] + st["fallback_strings"] == len(wt)
+    assert st["compiled_strings"] > 0.95 * len(wt)   # the compiled-stream kernel carries family A
     # a random subset against the oracle
     idx = np.sort(rng.choice(len(wt), size=1500, replace=False))
     sub_off = np.concatenate([[0], np.cumsum(np.diff(off)[idx])])

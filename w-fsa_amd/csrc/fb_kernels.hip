@@ -1,6 +1,4 @@
-// Forward-backward over the (position, node) trellis of each corpus string,
-// one wavefront per string, the whole trellis of the string kept in a
-// per-wave LDS slab.
+// Forward-backward over the (position, node) trellis of each corpus string.
 //
 // Replaces, per iteration, the reference's SpMV chain over the path matrices
 // (Learner::ComputeModeledProbs / ComputeObjective, src/Learner.cpp:515-553;
@@ -10,20 +8,27 @@
 //
 // Per string s of length L (bytes c_0..c_{L-1}):
 //   forward   alpha_0 = {start: 1};  alpha_{i+1}(T) = sum over edges S->T with
-//             byte c_i of alpha_i(S) * w_edge;  every position is rescaled by
-//             an exact power of two (its max -> [0.5, 1)), so no underflow and
-//             no rounding is added by the scaling;
-//   end       q_hat = sum_S alpha_L(S) * w_end(S);  log q = log q_hat + ln2 * E
-//   backward  beta_L(S) = w_end(S) / q_hat;  beta_i(S) = sum_edges w * beta_{i+1}(T)
-//             * 2^-d_{i+1};  an edge's posterior is alpha_i(S) * w * beta_{i+1}(T)
-//             * 2^-d_{i+1}, added (times -p_s) to every parameter of the edge.
-// Counting mode runs the same passes with every weight 1: q is the number of
-// accepting paths, and an edge is "used" when its posterior is positive.
+//             byte c_i of alpha_i(S) * w_edge;
+//   end       q = sum_S alpha_L(S) * w_end(S)
+//   backward  beta_L(S) = w_end(S);  beta_i(S) = sum_edges w * beta_{i+1}(T);
+//             an edge's posterior alpha_i(S) w beta_{i+1}(T) / q is added
+//             (times -p_s) to every parameter of the edge.
 //
-// Frontier nodes of a position are created on first touch through a node ->
-// slot map in LDS (CAS claim, ballot compaction) and summed with LDS fp64
-// atomics; live edges are logged for the backward pass, so the backward pass
-// never searches the automaton again.
+// trav_kernel (one wavefront per string) walks the automaton: frontier nodes
+// are created on first touch through a node->slot map in LDS (CAS claim,
+// ballot compaction), summed with LDS fp64 atomics, every position rescaled
+// by an exact power of two.  Its counting mode (all weights 1) gives the path
+// count, the used parameters and the compiled stream of the string:
+//
+// Compiled stream.  A position with exactly one live node (one on an
+// accepting path) is a cut: every path passes through it.  Between two
+// consecutive cuts the trellis is either ONE edge (a "trivial" word: the edge
+// id; its posterior is exactly 1) or a "bubble" (a small DAG stored once in a
+// bubble buffer).  With the posterior of a bubble edge taken relative to the
+// bubble's own start and end, alpha_seg(src) w beta_seg(dst) / Z_seg, the
+// whole string decomposes into independent segments, and
+//   log q = sum_trivial lw_e + sum_bubbles log Z_seg.
+// fbc_kernel evaluates these streams every iteration, one lane per string.
 #include "fb_kernels.hpp"
 
 #include <hip/hip_runtime.h>
@@ -58,9 +63,11 @@ __device__ __forceinline__ int ld_rlx(const int* p) {
 __device__ __forceinline__ void st_rlx(int* p, int v) {
     __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
 }
-
 __device__ __forceinline__ void lds_add(double* p, double v) {
     __hip_atomic_fetch_add(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+}
+__device__ __forceinline__ void block_add(double* p, double v) {
+    __hip_atomic_fetch_add(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
 __device__ __forceinline__ void global_add(double* p, double v) {
     __hip_atomic_fetch_add(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -104,8 +111,108 @@ __device__ __forceinline__ void edge_range(const ModelView& m, int S, int c, int
     cnt = l2 - l;
 }
 
-template <bool COUNTING>
-__global__ __launch_bounds__(256) void fb_kernel(FBArgs a) {
+struct Slab {
+    double* alpha;
+    double* beta;
+    int* state;
+    int* e_g;
+    int* e_src;
+    int* e_dst;
+    int* fpos;
+    int* epos;
+    int* dsc;
+    int* slot;
+};
+
+// Compiled stream of one string from its counted trellis (lane 0 only;
+// beta > 0 marks live entries).  Returns false when a bubble exceeds the
+// kernel limits; the string then stays on the traversal path.
+template <bool WRITE>
+__device__ bool compile_walk(const Slab& sl, const ModelView& m, int L, int& n_main, int& n_bub,
+                             int32_t* stream, int64_t s_base, int32_t* bub, int64_t b_base) {
+    long long* lid = reinterpret_cast<long long*>(sl.alpha);   // alpha is dead in counting mode
+    n_main = 0;
+    n_bub = 0;
+    int a = 0, fa = 0;
+    while (a <= L) {
+        int b = a + 1, fbn = -1;
+        for (; b <= L; ++b) {
+            int cnt = 0, last = -1;
+            for (int f = sl.fpos[b]; f < sl.fpos[b + 1]; ++f)
+                if (sl.beta[f] > 0.0) { ++cnt; last = f; }
+            if (cnt == 1) { fbn = last; break; }
+        }
+        const bool to_end = b > L;
+        // trivial segments
+        if (!to_end && b == a + 1) {
+            int cnt = 0, ge = -1;
+            for (int e = sl.epos[a]; e < sl.epos[a + 1]; ++e)
+                if (sl.beta[sl.e_dst[e]] > 0.0) { ++cnt; ge = e; }
+            if (cnt == 1) {
+                if (WRITE) stream[s_base + int64_t(kWave) * n_main] = sl.e_g[ge];
+                ++n_main;
+                a = b;
+                fa = fbn;
+                continue;
+            }
+        }
+        if (to_end && a == L) {
+            const int S = sl.state[fa];
+            if (m.x_ptr[S + 1] - m.x_ptr[S] == 1) {
+                if (WRITE) stream[s_base + int64_t(kWave) * n_main] = m.n_edges + m.x_ptr[S];
+                ++n_main;
+                break;
+            }
+        }
+        // bubble: local ids in position order
+        int nodes = 0;
+        lid[fa] = nodes++;
+        const int last_pos = to_end ? L : b - 1;
+        for (int pos = a + 1; pos <= last_pos; ++pos)
+            for (int f = sl.fpos[pos]; f < sl.fpos[pos + 1]; ++f)
+                if (sl.beta[f] > 0.0) lid[f] = nodes++;
+        const int end_id = nodes++;   // the cut node b, or the virtual end node
+        if (!to_end) lid[fbn] = end_id;
+        int edges = 0;
+        for (int e = sl.epos[a]; e < sl.epos[b <= L ? b : L]; ++e)
+            if (sl.beta[sl.e_dst[e]] > 0.0) ++edges;
+        if (to_end)
+            for (int f = sl.fpos[L]; f < sl.fpos[L + 1]; ++f)
+                if (sl.beta[f] > 0.0) edges += m.x_ptr[sl.state[f] + 1] - m.x_ptr[sl.state[f]];
+        if (nodes > kMaxBubbleNodes || edges > kMaxBubbleEdges) return false;
+        if (WRITE) {
+            int64_t w = b_base + n_bub;
+            bub[w++] = nodes | (edges << 16);
+            for (int e = sl.epos[a]; e < sl.epos[b <= L ? b : L]; ++e) {
+                const int h = sl.e_dst[e];
+                if (!(sl.beta[h] > 0.0)) continue;
+                bub[w++] = sl.e_g[e];
+                bub[w++] = int(lid[sl.e_src[e]]) | (int(lid[h]) << 16);
+            }
+            if (to_end) {
+                for (int f = sl.fpos[L]; f < sl.fpos[L + 1]; ++f) {
+                    if (!(sl.beta[f] > 0.0)) continue;
+                    const int S = sl.state[f];
+                    for (int x = m.x_ptr[S]; x < m.x_ptr[S + 1]; ++x) {
+                        bub[w++] = m.n_edges + x;
+                        bub[w++] = int(lid[f]) | (end_id << 16);
+                    }
+                }
+            }
+            stream[s_base + int64_t(kWave) * n_main] = -int(1 + b_base + n_bub);
+        }
+        n_bub += 1 + 2 * edges;
+        ++n_main;
+        if (to_end) break;
+        a = b;
+        fa = fbn;
+    }
+    return true;
+}
+
+template <int MODE>
+__global__ __launch_bounds__(256) void trav_kernel(TravArgs a) {
+    constexpr bool COUNTING = MODE != MODE_WEIGHTED;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int lane = lane_id();
     const int wib = int(threadIdx.x) / kWave;
@@ -114,19 +221,25 @@ __global__ __launch_bounds__(256) void fb_kernel(FBArgs a) {
     const int nw = int(gridDim.x) * wpb;
 
     unsigned char* base = smem + size_t(wib) * size_t(a.slab.bytes);
-    double* falpha = reinterpret_cast<double*>(base + a.lay.alpha);
-    double* fbeta = reinterpret_cast<double*>(base + a.lay.beta);
-    int* fstate = reinterpret_cast<int*>(base + a.lay.state);
-    int* e_g = reinterpret_cast<int*>(base + a.lay.eg);
-    int* e_src = reinterpret_cast<int*>(base + a.lay.esrc);
-    int* e_dst = reinterpret_cast<int*>(base + a.lay.edst);
-    int* fpos = reinterpret_cast<int*>(base + a.lay.fpos);
-    int* epos = reinterpret_cast<int*>(base + a.lay.epos);
-    int* dsc = reinterpret_cast<int*>(base + a.lay.dsc);
-    int* slot = reinterpret_cast<int*>(base + a.lay.slot);
+    Slab sl;
+    sl.alpha = reinterpret_cast<double*>(base + a.lay.alpha);
+    sl.beta = reinterpret_cast<double*>(base + a.lay.beta);
+    sl.state = reinterpret_cast<int*>(base + a.lay.state);
+    sl.e_g = reinterpret_cast<int*>(base + a.lay.eg);
+    sl.e_src = reinterpret_cast<int*>(base + a.lay.esrc);
+    sl.e_dst = reinterpret_cast<int*>(base + a.lay.edst);
+    sl.fpos = reinterpret_cast<int*>(base + a.lay.fpos);
+    sl.epos = reinterpret_cast<int*>(base + a.lay.epos);
+    sl.dsc = reinterpret_cast<int*>(base + a.lay.dsc);
+    sl.slot = reinterpret_cast<int*>(base + a.lay.slot);
+    double* falpha = sl.alpha;
+    double* fbeta = sl.beta;
+    int* fstate = sl.state;
+    int* slot = sl.slot;
 
     const ModelView& m = a.m;
     const int cap_f = a.slab.cap_f, cap_e = a.slab.cap_e;
+    const bool want_back = !COUNTING || a.used || a.c_main || MODE == MODE_EMIT;
 
     for (int j = lane; j < m.n_nodes; j += kWave) st_rlx(&slot[j], -1);
     wave_sync();
@@ -144,10 +257,10 @@ __global__ __launch_bounds__(256) void fb_kernel(FBArgs a) {
             fstate[0] = m.start;
             falpha[0] = 1.0;
             fbeta[0] = 0.0;
-            fpos[0] = 0;
-            fpos[1] = 1;
-            epos[0] = 0;
-            dsc[0] = 0;
+            sl.fpos[0] = 0;
+            sl.fpos[1] = 1;
+            sl.epos[0] = 0;
+            sl.dsc[0] = 0;
         }
         int nF = 1, nE = 0;
         bool ovf = false;
@@ -162,7 +275,7 @@ __global__ __launch_bounds__(256) void fb_kernel(FBArgs a) {
                 chunk = k < L ? uint32_t(str[k]) : 0u;
             }
             const int c = __builtin_amdgcn_readlane(int(chunk), i & (kWave - 1));
-            const int fb = fpos[i];
+            const int fb = sl.fpos[i];
             const int fe = nF;
             for (int fbase = fb; fbase < fe && !ovf; fbase += kWave) {
                 const int f = fbase + lane;
@@ -181,10 +294,10 @@ __global__ __launch_bounds__(256) void fb_kernel(FBArgs a) {
                     double v = 0.0;
                     if (has) {
                         d = m.o_dst[g];
-                        v = COUNTING ? af : af * m.o_w[g];
+                        v = COUNTING ? af : af * m.ew[g];
                     }
-                    int sl = has ? ld_rlx(&slot[d]) : 0;
-                    const bool need = has && sl < 0;
+                    int slv = has ? ld_rlx(&slot[d]) : 0;
+                    const bool need = has && slv < 0;
                     bool won = false;
                     if (need) won = atomicCAS(&slot[d], -1, -2) == -1;
                     const unsigned long long wm = __ballot(won);
@@ -204,13 +317,13 @@ __global__ __launch_bounds__(256) void fb_kernel(FBArgs a) {
                     }
                     nF += nwon;
                     wave_sync();
-                    if (need) sl = ld_rlx(&slot[d]);
+                    if (need) slv = ld_rlx(&slot[d]);
                     if (has) {
-                        lds_add(&falpha[sl], v);
+                        lds_add(&falpha[slv], v);
                         const int k = nE + rank_below(hm);
-                        e_g[k] = g;
-                        e_src[k] = f;
-                        e_dst[k] = sl;
+                        sl.e_g[k] = g;
+                        sl.e_src[k] = f;
+                        sl.e_dst[k] = slv;
                     }
                     nE += nhas;
                     wave_sync();
@@ -230,9 +343,9 @@ __global__ __launch_bounds__(256) void fb_kernel(FBArgs a) {
             if (ex != 0)
                 for (int j = fe + lane; j < nF; j += kWave) falpha[j] = ldexp(falpha[j], -ex);
             if (lane == 0) {
-                fpos[i + 2] = nF;
-                epos[i + 1] = nE;
-                dsc[i + 1] = ex;
+                sl.fpos[i + 2] = nF;
+                sl.epos[i + 1] = nE;
+                sl.dsc[i + 1] = ex;
             }
             wave_sync();
             if (nF == fe) {   // empty frontier: no accepting path
@@ -252,7 +365,7 @@ __global__ __launch_bounds__(256) void fb_kernel(FBArgs a) {
         // ---------------- end + log q ----------------
         double qh = 0.0;
         int esum = 0;
-        const int fl0 = alive ? fpos[L] : 0;
+        const int fl0 = alive ? sl.fpos[L] : 0;
         const int fl1 = alive ? nF : 0;
         for (int j = fl0 + lane; j < fl1; j += kWave) {
             const int S = fstate[j];
@@ -261,23 +374,23 @@ __global__ __launch_bounds__(256) void fb_kernel(FBArgs a) {
         qh = wave_sum(qh);
         if (alive) {
             int es = 0;
-            for (int j = 1 + lane; j <= L; j += kWave) es += dsc[j];
+            for (int j = 1 + lane; j <= L; j += kWave) es += sl.dsc[j];
             esum = wave_sum_i(es);
         }
         const double lq = qh > 0.0 ? log(qh) + kLn2 * double(esum) : -INFINITY;
         const double ps = COUNTING ? 0.0 : a.p[sidx];
         if (lane == 0) {
-            if (COUNTING) {
+            if (MODE == MODE_COUNT) {
                 if (a.path_count) a.path_count[sidx] = qh > 0.0 ? ldexp(qh, esum) : 0.0;
                 if (a.recognized) a.recognized[sidx] = qh > 0.0 ? 1 : 0;
-            } else if (a.logq) {
+                if (a.c_bub && !(qh > 0.0)) a.c_bub[sidx] = -1;
+            } else if (MODE == MODE_WEIGHTED && a.logq) {
                 a.logq[sidx] = lq;
             }
         }
         if (!COUNTING) ll_acc += ps * lq;
         edges_acc += (unsigned long long)nE;
-        if (!(qh > 0.0)) continue;
-        if (COUNTING && !a.used) continue;
+        if (!(qh > 0.0) || !want_back) continue;
 
         // ---------------- backward ----------------
         const double inv_q = 1.0 / qh;
@@ -286,30 +399,48 @@ __global__ __launch_bounds__(256) void fb_kernel(FBArgs a) {
             const double af = falpha[j];
             fbeta[j] = (COUNTING ? m.node_end_count[S] : m.node_end[S]) * inv_q;
             for (int x = m.x_ptr[S]; x < m.x_ptr[S + 1]; ++x) {
-                const double xi = af * (COUNTING ? 1.0 : m.x_w[x]) * inv_q;
+                const int gx = m.n_edges + x;
+                const double xi = af * (COUNTING ? 1.0 : m.ew[gx]) * inv_q;
                 if (!(xi > 0.0)) continue;
-                for (int k = m.x_pptr[x]; k < m.x_pptr[x + 1]; ++k) {
-                    if (COUNTING) a.used[m.x_pidx[k]] = 1;
-                    else global_add(&a.grad[m.x_pidx[k]], -ps * xi);
+                for (int k = m.pptr[gx]; k < m.pptr[gx + 1]; ++k) {
+                    if (COUNTING) { if (a.used) a.used[m.pidx[k]] = 1; }
+                    else global_add(&a.grad[m.pidx[k]], -ps * xi);
                 }
             }
         }
         wave_sync();
         for (int i = L - 1; i >= 0; --i) {
-            const double sc = ldexp(1.0, -dsc[i + 1]);
-            const int eb = epos[i], ee = epos[i + 1];
+            const double sc = ldexp(1.0, -sl.dsc[i + 1]);
+            const int eb = sl.epos[i], ee = sl.epos[i + 1];
             for (int k = eb + lane; k < ee; k += kWave) {
-                const int g = e_g[k];
-                const int f = e_src[k];
-                const int h = e_dst[k];
-                const double b = (COUNTING ? 1.0 : m.o_w[g]) * fbeta[h] * sc;
+                const int g = sl.e_g[k];
+                const int f = sl.e_src[k];
+                const int h = sl.e_dst[k];
+                const double b = (COUNTING ? 1.0 : m.ew[g]) * fbeta[h] * sc;
                 if (b != 0.0) lds_add(&fbeta[f], b);
                 const double xi = falpha[f] * b;
                 if (xi > 0.0) {
-                    for (int q = m.o_pptr[g]; q < m.o_pptr[g + 1]; ++q) {
-                        if (COUNTING) a.used[m.o_pidx[q]] = 1;
-                        else global_add(&a.grad[m.o_pidx[q]], -ps * xi);
+                    for (int q = m.pptr[g]; q < m.pptr[g + 1]; ++q) {
+                        if (COUNTING) { if (a.used) a.used[m.pidx[q]] = 1; }
+                        else global_add(&a.grad[m.pidx[q]], -ps * xi);
                     }
+                }
+            }
+            wave_sync();
+        }
+
+        // ---------------- compiled stream ----------------
+        if (COUNTING && (a.c_main || MODE == MODE_EMIT)) {
+            if (lane == 0) {
+                int n_main = 0, n_bub = 0;
+                bool ok;
+                if (MODE == MODE_EMIT)
+                    ok = compile_walk<true>(sl, m, L, n_main, n_bub, a.stream, a.s_base[sidx], a.bub, a.b_base[sidx]);
+                else
+                    ok = compile_walk<false>(sl, m, L, n_main, n_bub, nullptr, 0, nullptr, 0);
+                if (MODE == MODE_COUNT) {
+                    a.c_main[sidx] = ok ? n_main : 0;
+                    a.c_bub[sidx] = ok ? n_bub : -1;
                 }
             }
             wave_sync();
@@ -322,13 +453,100 @@ __global__ __launch_bounds__(256) void fb_kernel(FBArgs a) {
     }
 }
 
+// One bubble of a compiled stream: local forward, local backward, posteriors
+// relative to the bubble; returns log Z_seg.
+template <bool LDS_GRAD>
+__device__ double eval_bubble(const CompiledArgs& a, int64_t off, double p, double* A, double* B, double* gacc) {
+    const int hdr = a.bub[off];
+    const int nodes = hdr & 0xffff, edges = hdr >> 16;
+    const int32_t* ed = a.bub + off + 1;
+    for (int i = 0; i < nodes; ++i) {
+        A[i] = 0.0;
+        B[i] = 0.0;
+    }
+    A[0] = 1.0;
+    for (int e = 0; e < edges; ++e) {
+        const int g = ed[2 * e], sd = ed[2 * e + 1];
+        A[sd >> 16] += A[sd & 0xffff] * a.m.ew[g];
+    }
+    const double Z = A[nodes - 1];
+    const double inv = 1.0 / Z;
+    B[nodes - 1] = 1.0;
+    for (int e = edges - 1; e >= 0; --e) {
+        const int g = ed[2 * e], sd = ed[2 * e + 1];
+        const int src = sd & 0xffff;
+        const double b = a.m.ew[g] * B[sd >> 16];
+        B[src] += b;
+        const double xi = A[src] * b * inv;
+        for (int q = a.m.pptr[g]; q < a.m.pptr[g + 1]; ++q) {
+            if (LDS_GRAD) block_add(&gacc[a.m.pidx[q]], -p * xi);
+            else global_add(&a.grad[a.m.pidx[q]], -p * xi);
+        }
+    }
+    return log(Z);
+}
+
+template <bool LDS_GRAD>
+__global__ __launch_bounds__(512) void fbc_kernel(CompiledArgs a) {
+    extern __shared__ __attribute__((aligned(16))) double gacc[];
+    const int lane = lane_id();
+    const int wpb = int(blockDim.x) / kWave;
+    const int gw = int(blockIdx.x) * wpb + int(threadIdx.x) / kWave;
+    const int nw = int(gridDim.x) * wpb;
+    if (LDS_GRAD) {
+        for (int j = int(threadIdx.x); j < a.n_params; j += int(blockDim.x)) gacc[j] = 0.0;
+        __syncthreads();
+    }
+    double* A = a.scratch + (size_t(gw) * kWave + lane) * (2 * kMaxBubbleNodes);
+    double* B = A + kMaxBubbleNodes;
+    const double* lw = a.m.lw;
+    double ll_acc = 0.0;
+
+    for (int grp = gw; grp < a.n_groups; grp += nw) {
+        const int s = a.l_str[grp * kWave + lane];
+        const int len = a.l_len[grp * kWave + lane];
+        const int glen = a.g_len[grp];
+        const int32_t* st = a.stream + a.g_base[grp] + lane;
+        const double p = s >= 0 ? a.p[s] : 0.0;
+        double acc = 0.0;
+        for (int k = 0; k < glen; ++k) {
+            if (k >= len) break;
+            const int w = st[int64_t(kWave) * k];
+            if (w >= 0) {
+                acc += lw[w];
+                for (int q = a.m.pptr[w]; q < a.m.pptr[w + 1]; ++q) {
+                    if (LDS_GRAD) block_add(&gacc[a.m.pidx[q]], -p);
+                    else global_add(&a.grad[a.m.pidx[q]], -p);
+                }
+            } else {
+                acc += eval_bubble<LDS_GRAD>(a, int64_t(-(w + 1)), p, A, B, gacc);
+            }
+        }
+        if (s >= 0) {
+            ll_acc += p * acc;
+            if (a.logq) a.logq[s] = acc;
+        }
+    }
+    ll_acc = wave_sum(ll_acc);
+    if (lane == 0) a.ll_part[gw] = ll_acc;
+    if (LDS_GRAD) {
+        __syncthreads();
+        for (int j = int(threadIdx.x); j < a.n_params; j += int(blockDim.x)) {
+            const double v = gacc[j];
+            if (v != 0.0) global_add(&a.grad[j], v);
+        }
+    }
+}
+
 __global__ void edge_weights_kernel(const double* __restrict__ w_full, const int32_t* __restrict__ pptr,
-                                    const int32_t* __restrict__ pidx, double* __restrict__ out, int64_t n) {
+                                    const int32_t* __restrict__ pidx, double* __restrict__ lw,
+                                    double* __restrict__ ew, int64_t n) {
     const int64_t g = int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
     if (g >= n) return;
     double s = 0.0;
     for (int32_t k = pptr[g]; k < pptr[g + 1]; ++k) s += w_full[pidx[k]];
-    out[g] = exp(s);
+    lw[g] = s;
+    ew[g] = exp(s);
 }
 
 __global__ void node_end_kernel(const int32_t* __restrict__ x_ptr, const double* __restrict__ x_w,
@@ -357,29 +575,49 @@ __global__ __launch_bounds__(256) void finalize_kernel(const double* __restrict_
 
 }  // namespace
 
-hipError_t configure_fb_kernels(int max_dynamic_lds) {
-    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&fb_kernel<true>),
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, max_dynamic_lds);
-    if (e != hipSuccess) return e;
-    return hipFuncSetAttribute(reinterpret_cast<const void*>(&fb_kernel<false>),
-                               hipFuncAttributeMaxDynamicSharedMemorySize, max_dynamic_lds);
+hipError_t configure_kernels(int max_dynamic_lds) {
+    const void* fns[] = {reinterpret_cast<const void*>(&trav_kernel<MODE_WEIGHTED>),
+                         reinterpret_cast<const void*>(&trav_kernel<MODE_COUNT>),
+                         reinterpret_cast<const void*>(&trav_kernel<MODE_EMIT>),
+                         reinterpret_cast<const void*>(&fbc_kernel<true>),
+                         reinterpret_cast<const void*>(&fbc_kernel<false>)};
+    for (const void* f : fns) {
+        hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, max_dynamic_lds);
+        if (e != hipSuccess) return e;
+    }
+    return hipSuccess;
 }
 
-hipError_t launch_fb(bool counting, const FBArgs& a, int grid, hipStream_t stream) {
+hipError_t launch_trav(TravMode mode, const TravArgs& a, int grid, hipStream_t stream) {
     const dim3 block(unsigned(a.slab.waves_per_block * kWave));
     const size_t lds = size_t(a.slab.bytes) * size_t(a.slab.waves_per_block);
-    if (counting)
-        hipLaunchKernelGGL(fb_kernel<true>, dim3(unsigned(grid)), block, lds, stream, a);
-    else
-        hipLaunchKernelGGL(fb_kernel<false>, dim3(unsigned(grid)), block, lds, stream, a);
+    switch (mode) {
+        case MODE_WEIGHTED:
+            hipLaunchKernelGGL(trav_kernel<MODE_WEIGHTED>, dim3(unsigned(grid)), block, lds, stream, a);
+            break;
+        case MODE_COUNT:
+            hipLaunchKernelGGL(trav_kernel<MODE_COUNT>, dim3(unsigned(grid)), block, lds, stream, a);
+            break;
+        case MODE_EMIT:
+            hipLaunchKernelGGL(trav_kernel<MODE_EMIT>, dim3(unsigned(grid)), block, lds, stream, a);
+            break;
+    }
     return hipGetLastError();
 }
 
-hipError_t launch_edge_weights(const double* w_full, const int32_t* pptr, const int32_t* pidx, double* out,
-                               int64_t n_edges, hipStream_t stream) {
+hipError_t launch_compiled(const CompiledArgs& a, int grid, int block, size_t lds, hipStream_t stream) {
+    if (a.grad_in_lds)
+        hipLaunchKernelGGL(fbc_kernel<true>, dim3(unsigned(grid)), dim3(unsigned(block)), lds, stream, a);
+    else
+        hipLaunchKernelGGL(fbc_kernel<false>, dim3(unsigned(grid)), dim3(unsigned(block)), 0, stream, a);
+    return hipGetLastError();
+}
+
+hipError_t launch_edge_weights(const double* w_full, const int32_t* pptr, const int32_t* pidx, double* lw,
+                               double* ew, int64_t n_edges, hipStream_t stream) {
     if (n_edges <= 0) return hipSuccess;
     const unsigned blocks = unsigned((n_edges + 255) / 256);
-    hipLaunchKernelGGL(edge_weights_kernel, dim3(blocks), dim3(256), 0, stream, w_full, pptr, pidx, out, n_edges);
+    hipLaunchKernelGGL(edge_weights_kernel, dim3(blocks), dim3(256), 0, stream, w_full, pptr, pidx, lw, ew, n_edges);
     return hipGetLastError();
 }
 

@@ -1,4 +1,15 @@
-// Device-side views and launchers of the forward-backward kernels.
+// Device-side views and launchers of the trellis kernels.
+//
+// Two kernels carry the hot path:
+//   * trav_kernel<MODE> -- one wavefront per string, re-derives the string's
+//     trellis from the automaton (LDS slab).  MODE_COUNT is the one-time
+//     structural pass (recognition, path counts, used parameters, compiled
+//     stream sizes), MODE_EMIT writes the compiled streams, MODE_WEIGHTED is
+//     the per-iteration fallback for strings whose trellis does not compile.
+//   * fbc_kernel -- the per-iteration forward-backward over compiled
+//     streams, one lane per string, 64 strings of similar stream length per
+//     wavefront, stream words interleaved so every load is coalesced, and the
+//     gradient accumulated in LDS.
 #pragma once
 
 #include <hip/hip_runtime.h>
@@ -8,22 +19,25 @@
 
 namespace wfsa {
 
+constexpr int kMaxBubbleNodes = 32;    // nodes of one compiled bubble
+constexpr int kMaxBubbleEdges = 255;   // edges of one compiled bubble
+
 // Compiled trellis automaton resident in HBM (see trellis_model.hpp).
+// Edge ids: [0, E) byte-consuming edges, [E, E+X) end edges ("combined").
 struct ModelView {
     const int32_t* o_ptr;    // [n_nodes+1] out-edges by source node, sorted by byte
     const uint8_t* o_byte;
     const int32_t* o_dst;
-    const int32_t* o_pptr;   // [E+1] parameter list of each edge
-    const int32_t* o_pidx;
-    const double* o_w;       // [E] exp(sum of the edge's log-weights), per iteration
-    const int32_t* x_ptr;    // [n_nodes+1] end edges by source node
-    const int32_t* x_pptr;
-    const int32_t* x_pidx;
-    const double* x_w;       // [X] per iteration
+    const int32_t* x_ptr;    // [n_nodes+1] end edges by source node (ids relative to E)
+    const int32_t* pptr;     // [E+X+1] parameter list of each combined edge
+    const int32_t* pidx;
+    const double* ew;        // [E+X] exp(log-weight), per iteration
+    const double* lw;        // [E+X] log-weight, per iteration
     const double* node_end;  // [n_nodes] sum of the node's end-edge weights
     const double* node_end_count;  // [n_nodes] number of end edges (counting mode)
     int32_t n_nodes;
     int32_t start;
+    int32_t n_edges;         // E
 };
 
 // Per-wave LDS slab holding one string's trellis: frontier nodes (alpha,
@@ -59,7 +73,9 @@ inline SlabLayout slab_layout(int32_t cap_f, int32_t cap_e, int32_t max_len, int
     return l;
 }
 
-struct FBArgs {
+enum TravMode { MODE_WEIGHTED = 0, MODE_COUNT = 1, MODE_EMIT = 2 };
+
+struct TravArgs {
     ModelView m;
     const uint8_t* sym;      // packed corpus bytes
     const int64_t* off;      // [S+1]
@@ -68,22 +84,49 @@ struct FBArgs {
     int32_t n_list;
     SlabConfig slab;
     SlabLayout lay;
-    // weighted mode outputs
+    // weighted mode
     double* grad;            // [n_params]  accumulates -p_s * E[count]
-    double* ll_part;         // [waves in grid]  sum of p_s log q_s per wave
+    double* ll_part;         // [waves in grid]
     double* logq;            // [S] or null
-    // counting mode outputs
+    // counting mode
     double* path_count;      // [S] or null
     uint8_t* recognized;     // [S] or null
     uint8_t* used;           // [n_params] or null
+    int32_t* c_main;         // [S] compiled main-stream words, or null
+    int32_t* c_bub;          // [S] compiled bubble words (-1: does not compile)
+    // emit mode
+    int32_t* stream;         // interleaved main streams
+    const int64_t* s_base;   // [S] word index of the string's first main word
+    int32_t* bub;            // bubble buffer
+    const int64_t* b_base;   // [S] word index of the string's first bubble word
     uint8_t* overflow;       // [S] string did not fit the slab
-    unsigned long long* live_edges;  // total live edges touched
+    unsigned long long* live_edges;
 };
 
-hipError_t configure_fb_kernels(int max_dynamic_lds);
-hipError_t launch_fb(bool counting, const FBArgs& a, int grid, hipStream_t stream);
-hipError_t launch_edge_weights(const double* w_full, const int32_t* pptr, const int32_t* pidx, double* out,
-                               int64_t n_edges, hipStream_t stream);
+// Compiled streams of the per-iteration kernel.
+struct CompiledArgs {
+    ModelView m;
+    const double* p;         // [S]
+    const int32_t* stream;   // interleaved: word k of lane l of group g at g_base[g] + 64 k + l
+    const int32_t* bub;
+    const int64_t* g_base;   // [G]
+    const int32_t* g_len;    // [G] longest stream of the group (its first lane)
+    const int32_t* l_str;    // [64 G] string of each lane, -1 = padding
+    const int32_t* l_len;    // [64 G]
+    int32_t n_groups;
+    int32_t n_params;
+    int32_t grad_in_lds;     // 1: per-block LDS accumulator of n_params doubles
+    double* grad;            // [n_params]
+    double* ll_part;         // [waves in grid]
+    double* logq;            // [S] or null
+    double* scratch;         // per lane 2 * kMaxBubbleNodes doubles
+};
+
+hipError_t configure_kernels(int max_dynamic_lds);
+hipError_t launch_trav(TravMode mode, const TravArgs& a, int grid, hipStream_t stream);
+hipError_t launch_compiled(const CompiledArgs& a, int grid, int block, size_t lds, hipStream_t stream);
+hipError_t launch_edge_weights(const double* w_full, const int32_t* pptr, const int32_t* pidx, double* lw,
+                               double* ew, int64_t n_edges, hipStream_t stream);
 hipError_t launch_node_end(const int32_t* x_ptr, const double* x_w, double* node_end, int32_t n_nodes,
                            hipStream_t stream);
 hipError_t launch_finalize(const double* ll_part, int32_t n_part, double* out, hipStream_t stream);

@@ -1,16 +1,27 @@
 // Implementation of the C-ABI device boundary declared in include/wfsa_dev.h.
 //
 // A context owns one HIP stream on one gfx950 device, the compiled trellis
-// automaton, the packed corpus, per-wave scratch and (optionally) an RCCL
-// communicator.  Per iteration the host sends w_full (n_params doubles) and
-// receives [loglik, grad_full] (n_params+1 doubles); everything else stays in
-// HBM.
+// automaton, the packed corpus, the compiled per-string streams, scratch and
+// (optionally) an RCCL communicator.  Per iteration the host sends w_full
+// (n_params doubles) and receives [loglik, grad_full] (n_params+1 doubles);
+// everything else stays in HBM.
+//
+// Preparing a corpus (once per wfsa_dev_load_corpus):
+//   1. trav_kernel<MODE_COUNT> over every string (small-slab tier, then the
+//      single-wave tier for strings that overflow): recognition, path counts,
+//      used parameters, and the size of each string's compiled stream;
+//   2. host: strings sorted by stream length into groups of 64 (one
+//      wavefront each), interleaved stream offsets, bubble offsets;
+//   3. trav_kernel<MODE_EMIT> writes the streams.
+// Strings whose trellis does not compile (a bubble over the limits) stay on
+// the traversal kernel in weighted mode.
 #include "wfsa_dev.h"
 
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cstdarg>
 #include <cstdio>
 #include <cstring>
@@ -64,9 +75,9 @@ struct DevBuf {
     hipError_t alloc(size_t count) {
         if (count <= n && ptr) return hipSuccess;
         release();
-        const size_t bytes = std::max<size_t>(count, 1) * sizeof(T);
-        hipError_t e = hipMalloc(reinterpret_cast<void**>(&ptr), bytes);
-        if (e == hipSuccess) n = std::max<size_t>(count, 1);
+        const size_t c = std::max<size_t>(count, 1);
+        hipError_t e = hipMalloc(reinterpret_cast<void**>(&ptr), c * sizeof(T));
+        if (e == hipSuccess) n = c;
         return e;
     }
     hipError_t upload(const T* src, size_t count, hipStream_t s) {
@@ -74,10 +85,16 @@ struct DevBuf {
         if (e != hipSuccess || count == 0) return e;
         return hipMemcpyAsync(ptr, src, count * sizeof(T), hipMemcpyHostToDevice, s);
     }
+    hipError_t download(T* dst, size_t count, hipStream_t s) const {
+        if (count == 0) return hipSuccess;
+        return hipMemcpyAsync(dst, ptr, count * sizeof(T), hipMemcpyDeviceToHost, s);
+    }
 };
 
 constexpr int kLdsPerCu = 163840;
 constexpr int kNumCu = 256;
+constexpr int kWave = 64;
+constexpr int kCompiledBlock = 512;
 
 }  // namespace
 
@@ -85,15 +102,15 @@ struct wfsa_dev {
     int device = 0;
     int n_cu = kNumCu;
     hipStream_t stream = nullptr;
-    hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    hipEvent_t ev0 = nullptr, ev1 = nullptr, k0 = nullptr, k1 = nullptr, k2 = nullptr;
 
     // model
     bool has_model = false;
     int32_t n_params = 0, n_nodes = 0, start = 0;
     int64_t n_edges = 0, n_end = 0;
-    DevBuf<int32_t> o_ptr, o_dst, o_pptr, o_pidx, x_ptr, x_pptr, x_pidx;
+    DevBuf<int32_t> o_ptr, o_dst, x_ptr, pptr, pidx;
     DevBuf<uint8_t> o_byte;
-    DevBuf<double> o_w, x_w, node_end, node_end_count;
+    DevBuf<double> lw, ew, node_end, node_end_count;
 
     // corpus
     bool has_corpus = false;
@@ -104,18 +121,33 @@ struct wfsa_dev {
     DevBuf<double> p;
     DevBuf<int32_t> list_all;
 
-    // tiers: strings whose trellis fits the small slab / the large slab
-    bool tiers_ready = false;
+    // traversal tiers: small LDS slab (several waves per block) / whole LDS
     wfsa::SlabConfig cfg[2];
     wfsa::SlabLayout lay[2];
-    int grid[2] = {0, 0};
-    int32_t n_list[2] = {0, 0};
-    DevBuf<int32_t> list[2];
     DevBuf<uint8_t> overflow;
 
+    // preparation state (valid until the next load): 0 none, 1 counted,
+    // 2 counted + streams compiled
+    int prep_level = 0;
+    DevBuf<double> pcount;
+    DevBuf<uint8_t> recog, used;
+
+    // compiled streams
+    int32_t n_groups = 0;
+    int64_t n_compiled = 0;
+    DevBuf<int32_t> stream_w, bub, g_len, l_str, l_len;
+    DevBuf<int64_t> g_base;
+    DevBuf<double> scratch;
+    int c_grid = 0, c_lds_grad = 0;
+    size_t c_lds = 0;
+
+    // traversal fallback: per tier string lists
+    int32_t n_fall[2] = {0, 0};
+    int fall_grid[2] = {0, 0};
+    DevBuf<int32_t> fall[2];
+
     // work buffers
-    DevBuf<double> w_full, out, ll_part, logq, pcount;
-    DevBuf<uint8_t> used, recog;
+    DevBuf<double> w_full, out, ll_part, logq;
     DevBuf<unsigned long long> live;
     double* pinned = nullptr;   // n_params + 1 doubles
     size_t pinned_n = 0;
@@ -144,7 +176,7 @@ bool make_slab(int32_t budget, int32_t max_len, int32_t n_nodes, int32_t waves_p
     const int64_t fixed = 12 * int64_t(max_len + 2) + 4 * int64_t(n_nodes) + 16;
     const int64_t rem = int64_t(budget) - fixed;
     if (rem < 38 * 64) return false;
-    int32_t cap_f = int32_t(rem / 38) & ~1;
+    const int32_t cap_f = int32_t(rem / 38) & ~1;
     int32_t cap_e = int32_t((rem - 20 * int64_t(cap_f)) / 12);
     lay = wfsa::slab_layout(cap_f, cap_e, max_len, n_nodes);
     while (lay.total > budget && cap_e > 64) {
@@ -161,30 +193,35 @@ bool make_slab(int32_t budget, int32_t max_len, int32_t n_nodes, int32_t waves_p
     return true;
 }
 
-int grid_for(const wfsa::SlabConfig& c, int n_cu, int32_t n_list) {
+int trav_grid(const wfsa::SlabConfig& c, int n_cu, int64_t n_list) {
     const int block_lds = c.bytes * c.waves_per_block;
     int per_cu = std::max(1, std::min(kLdsPerCu / std::max(block_lds, 1), 32 / c.waves_per_block));
     per_cu = std::min(per_cu, 8);
-    const int64_t want = (int64_t(n_list) + c.waves_per_block - 1) / c.waves_per_block;
+    const int64_t want = (n_list + c.waves_per_block - 1) / c.waves_per_block;
     return int(std::max<int64_t>(1, std::min<int64_t>(want, int64_t(n_cu) * per_cu)));
 }
 
-wfsa::FBArgs base_args(wfsa_dev* ctx, int tier) {
-    wfsa::FBArgs a{};
-    a.m.o_ptr = ctx->o_ptr.ptr;
-    a.m.o_byte = ctx->o_byte.ptr;
-    a.m.o_dst = ctx->o_dst.ptr;
-    a.m.o_pptr = ctx->o_pptr.ptr;
-    a.m.o_pidx = ctx->o_pidx.ptr;
-    a.m.o_w = ctx->o_w.ptr;
-    a.m.x_ptr = ctx->x_ptr.ptr;
-    a.m.x_pptr = ctx->x_pptr.ptr;
-    a.m.x_pidx = ctx->x_pidx.ptr;
-    a.m.x_w = ctx->x_w.ptr;
-    a.m.node_end = ctx->node_end.ptr;
-    a.m.node_end_count = ctx->node_end_count.ptr;
-    a.m.n_nodes = ctx->n_nodes;
-    a.m.start = ctx->start;
+wfsa::ModelView model_view(wfsa_dev* ctx) {
+    wfsa::ModelView m{};
+    m.o_ptr = ctx->o_ptr.ptr;
+    m.o_byte = ctx->o_byte.ptr;
+    m.o_dst = ctx->o_dst.ptr;
+    m.x_ptr = ctx->x_ptr.ptr;
+    m.pptr = ctx->pptr.ptr;
+    m.pidx = ctx->pidx.ptr;
+    m.ew = ctx->ew.ptr;
+    m.lw = ctx->lw.ptr;
+    m.node_end = ctx->node_end.ptr;
+    m.node_end_count = ctx->node_end_count.ptr;
+    m.n_nodes = ctx->n_nodes;
+    m.start = ctx->start;
+    m.n_edges = int32_t(ctx->n_edges);
+    return m;
+}
+
+wfsa::TravArgs trav_args(wfsa_dev* ctx, int tier) {
+    wfsa::TravArgs a{};
+    a.m = model_view(ctx);
     a.sym = ctx->sym.ptr;
     a.off = ctx->off.ptr;
     a.p = ctx->p.ptr;
@@ -195,78 +232,17 @@ wfsa::FBArgs base_args(wfsa_dev* ctx, int tier) {
     return a;
 }
 
-// Counting pass over `list`; optional structural outputs.  Tier lists are
-// (re)built from the overflow flags when build_tiers is set.
-int counting_pass(wfsa_dev* ctx, bool want_outputs) {
-    const int64_t S = ctx->n_strings;
-    HIP_TRY(ctx->overflow.alloc(size_t(S)));
-    HIP_TRY(hipMemsetAsync(ctx->overflow.ptr, 0, size_t(S), ctx->stream));
-    if (want_outputs) {
-        HIP_TRY(ctx->pcount.alloc(size_t(S)));
-        HIP_TRY(ctx->recog.alloc(size_t(S)));
-        HIP_TRY(ctx->used.alloc(size_t(ctx->n_params)));
-        HIP_TRY(hipMemsetAsync(ctx->used.ptr, 0, size_t(std::max(ctx->n_params, 1)), ctx->stream));
-    }
-    HIP_TRY(hipMemsetAsync(ctx->live.ptr, 0, sizeof(unsigned long long), ctx->stream));
-    // tier 0 over all strings
-    wfsa::FBArgs a = base_args(ctx, 0);
-    a.list = ctx->list_all.ptr;
-    a.n_list = int32_t(S);
-    if (want_outputs) {
-        a.path_count = ctx->pcount.ptr;
-        a.recognized = ctx->recog.ptr;
-        a.used = ctx->used.ptr;
-    }
-    if (S > 0) HIP_TRY(wfsa::launch_fb(true, a, grid_for(ctx->cfg[0], ctx->n_cu, int32_t(S)), ctx->stream));
-    std::vector<uint8_t> ovf(static_cast<size_t>(S));
-    if (S > 0) HIP_TRY(hipMemcpyAsync(ovf.data(), ctx->overflow.ptr, size_t(S), hipMemcpyDeviceToHost, ctx->stream));
-    HIP_TRY(hipStreamSynchronize(ctx->stream));
-    std::vector<int32_t> l0, l1;
-    l0.reserve(size_t(S));
-    for (int64_t s = 0; s < S; ++s) (ovf[size_t(s)] ? l1 : l0).push_back(int32_t(s));
-    if (!l1.empty()) {
-        if (ctx->cfg[1].bytes == 0)
-            return fail(WFSA_ERR_CAPACITY, "%zu strings exceed the per-wave trellis slab and the model is too "
-                        "large for the single-wave tier", l1.size());
-        HIP_TRY(ctx->list[1].upload(l1.data(), l1.size(), ctx->stream));
-        wfsa::FBArgs b = base_args(ctx, 1);
-        b.list = ctx->list[1].ptr;
-        b.n_list = int32_t(l1.size());
-        if (want_outputs) {
-            b.path_count = ctx->pcount.ptr;
-            b.recognized = ctx->recog.ptr;
-            b.used = ctx->used.ptr;
-        }
-        HIP_TRY(hipMemsetAsync(ctx->overflow.ptr, 0, size_t(S), ctx->stream));
-        HIP_TRY(wfsa::launch_fb(true, b, grid_for(ctx->cfg[1], ctx->n_cu, b.n_list), ctx->stream));
-        HIP_TRY(hipMemcpyAsync(ovf.data(), ctx->overflow.ptr, size_t(S), hipMemcpyDeviceToHost, ctx->stream));
-        HIP_TRY(hipStreamSynchronize(ctx->stream));
-        for (int32_t s : l1)
-            if (ovf[size_t(s)])
-                return fail(WFSA_ERR_CAPACITY, "string %d: trellis exceeds %d frontier nodes / %d live edges "
-                            "(single-wave LDS tier)", s, ctx->cfg[1].cap_f, ctx->cfg[1].cap_e);
-    }
-    HIP_TRY(ctx->list[0].upload(l0.data(), l0.size(), ctx->stream));
-    ctx->n_list[0] = int32_t(l0.size());
-    ctx->n_list[1] = int32_t(l1.size());
-    for (int t = 0; t < 2; ++t) ctx->grid[t] = ctx->n_list[t] ? grid_for(ctx->cfg[t], ctx->n_cu, ctx->n_list[t]) : 0;
-    const size_t waves = size_t(ctx->grid[0]) * size_t(ctx->cfg[0].waves_per_block) +
-                         size_t(ctx->grid[1]) * size_t(ctx->cfg[1].waves_per_block);
-    HIP_TRY(ctx->ll_part.alloc(waves));
-    ctx->stats.tier1_strings = ctx->n_list[1];
-    ctx->stats.waves_per_block = ctx->cfg[0].waves_per_block;
-    ctx->tiers_ready = true;
-    return WFSA_OK;
-}
-
 int configure_tiers(wfsa_dev* ctx) {
-    // tier 0: 4 waves per block, ~20 KB per wave (8 waves per CU); grows
-    // to fit large automata.  tier 1: one wave per block, the whole LDS.
+    // tier 0: 4 waves per block, ~20 KB per wave (8 waves per CU), grown to
+    // fit large automata; tier 1: one wave per block with the whole LDS.
     ctx->cfg[0] = wfsa::SlabConfig{};
     ctx->cfg[1] = wfsa::SlabConfig{};
     bool ok0 = false;
     for (int budget : {20480, 40960}) {
-        if (make_slab(budget, ctx->max_len, ctx->n_nodes, 4, ctx->cfg[0], ctx->lay[0])) { ok0 = true; break; }
+        if (make_slab(budget, ctx->max_len, ctx->n_nodes, 4, ctx->cfg[0], ctx->lay[0])) {
+            ok0 = true;
+            break;
+        }
     }
     const bool ok1 = make_slab(kLdsPerCu - 1024, ctx->max_len, ctx->n_nodes, 1, ctx->cfg[1], ctx->lay[1]);
     if (!ok1) ctx->cfg[1] = wfsa::SlabConfig{};
@@ -277,7 +253,199 @@ int configure_tiers(wfsa_dev* ctx) {
         ctx->cfg[0] = ctx->cfg[1];
         ctx->lay[0] = ctx->lay[1];
     }
-    ctx->tiers_ready = false;
+    ctx->prep_level = 0;
+    return WFSA_OK;
+}
+
+// Structural pass (level 1) + stream compilation (level 2) for the loaded
+// corpus.
+int prepare(wfsa_dev* ctx, int level) {
+    const auto t_start = std::chrono::steady_clock::now();
+    hipStream_t s = ctx->stream;
+    const int64_t S = ctx->n_strings;
+    const size_t SZ = size_t(std::max<int64_t>(S, 1));
+    HIP_TRY(ctx->overflow.alloc(SZ));
+    HIP_TRY(ctx->pcount.alloc(SZ));
+    HIP_TRY(ctx->recog.alloc(SZ));
+    HIP_TRY(ctx->used.alloc(size_t(std::max(ctx->n_params, 1))));
+    DevBuf<int32_t> c_main, c_bub;
+    HIP_TRY(c_main.alloc(SZ));
+    HIP_TRY(c_bub.alloc(SZ));
+    HIP_TRY(hipMemsetAsync(ctx->overflow.ptr, 0, SZ, s));
+    HIP_TRY(hipMemsetAsync(ctx->used.ptr, 0, size_t(std::max(ctx->n_params, 1)), s));
+    HIP_TRY(hipMemsetAsync(c_main.ptr, 0, SZ * sizeof(int32_t), s));
+    HIP_TRY(hipMemsetAsync(c_bub.ptr, 0xff, SZ * sizeof(int32_t), s));   // -1: not compiled
+
+    // 1. counting pass, tier 0 then tier 1 for strings that overflow
+    std::vector<uint8_t> ovf(SZ, 0);
+    std::vector<uint8_t> tier(SZ, 0);
+    auto count_pass = [&](int t, const int32_t* list, int64_t n) -> int {
+        wfsa::TravArgs a = trav_args(ctx, t);
+        a.list = list;
+        a.n_list = int32_t(n);
+        a.path_count = ctx->pcount.ptr;
+        a.recognized = ctx->recog.ptr;
+        a.used = ctx->used.ptr;
+        a.c_main = level >= 2 ? c_main.ptr : nullptr;
+        a.c_bub = level >= 2 ? c_bub.ptr : nullptr;
+        HIP_TRY(wfsa::launch_trav(wfsa::MODE_COUNT, a, trav_grid(ctx->cfg[t], ctx->n_cu, n), s));
+        return WFSA_OK;
+    };
+    if (S > 0) {
+        if (int rc = count_pass(0, ctx->list_all.ptr, S)) return rc;
+        HIP_TRY(ctx->overflow.download(ovf.data(), size_t(S), s));
+        HIP_TRY(hipStreamSynchronize(s));
+    }
+    std::vector<int32_t> l1;
+    for (int64_t i = 0; i < S; ++i)
+        if (ovf[size_t(i)]) l1.push_back(int32_t(i));
+    DevBuf<int32_t> d_l1;
+    if (!l1.empty()) {
+        if (ctx->cfg[1].bytes == 0)
+            return fail(WFSA_ERR_CAPACITY, "%zu strings exceed the per-wave trellis slab and the automaton is too "
+                        "large for the single-wave tier", l1.size());
+        HIP_TRY(d_l1.upload(l1.data(), l1.size(), s));
+        HIP_TRY(hipMemsetAsync(ctx->overflow.ptr, 0, SZ, s));
+        if (int rc = count_pass(1, d_l1.ptr, int64_t(l1.size()))) return rc;
+        HIP_TRY(ctx->overflow.download(ovf.data(), size_t(S), s));
+        HIP_TRY(hipStreamSynchronize(s));
+        for (int32_t i : l1) {
+            if (ovf[size_t(i)])
+                return fail(WFSA_ERR_CAPACITY, "string %d: trellis exceeds %d frontier nodes / %d live edges "
+                            "(single-wave LDS tier)", i, ctx->cfg[1].cap_f, ctx->cfg[1].cap_e);
+            tier[size_t(i)] = 1;
+        }
+    }
+
+    if (level < 2) {
+        ctx->stats.tier1_strings = int32_t(l1.size());
+        ctx->prep_level = 1;
+        return WFSA_OK;
+    }
+
+    // 2. groups of 64 strings with similar stream length
+    std::vector<int32_t> h_main(SZ, 0), h_bub(SZ, -1);
+    if (S > 0) {
+        HIP_TRY(c_main.download(h_main.data(), size_t(S), s));
+        HIP_TRY(c_bub.download(h_bub.data(), size_t(S), s));
+        HIP_TRY(hipStreamSynchronize(s));
+    }
+    std::vector<int32_t> comp, fb[2];
+    int32_t max_main = 0;
+    for (int64_t i = 0; i < S; ++i) {
+        if (h_bub[size_t(i)] >= 0 && h_main[size_t(i)] > 0) {
+            comp.push_back(int32_t(i));
+            max_main = std::max(max_main, h_main[size_t(i)]);
+        } else {
+            fb[tier[size_t(i)]].push_back(int32_t(i));
+        }
+    }
+    {   // counting sort, longest first
+        std::vector<int64_t> cnt(size_t(max_main) + 2, 0);
+        for (int32_t i : comp) cnt[size_t(max_main - h_main[size_t(i)])]++;
+        int64_t acc = 0;
+        for (auto& c : cnt) { const int64_t t = c; c = acc; acc += t; }
+        std::vector<int32_t> sorted(comp.size());
+        for (int32_t i : comp) sorted[size_t(cnt[size_t(max_main - h_main[size_t(i)])]++)] = i;
+        comp.swap(sorted);
+    }
+    const int64_t nc = int64_t(comp.size());
+    const int32_t G = int32_t((nc + kWave - 1) / kWave);
+    std::vector<int64_t> g_base(size_t(G) + 1, 0), s_base(SZ, 0), b_base(SZ, 0);
+    std::vector<int32_t> g_len(size_t(std::max(G, 1)), 0), l_str(size_t(G) * kWave, -1), l_len(size_t(G) * kWave, 0);
+    int64_t words = 0;
+    for (int32_t g = 0; g < G; ++g) {
+        g_base[size_t(g)] = words;
+        g_len[size_t(g)] = h_main[size_t(comp[size_t(g) * kWave])];
+        for (int l = 0; l < kWave; ++l) {
+            const int64_t k = int64_t(g) * kWave + l;
+            if (k >= nc) break;
+            const int32_t str = comp[size_t(k)];
+            l_str[size_t(k)] = str;
+            l_len[size_t(k)] = h_main[size_t(str)];
+            s_base[size_t(str)] = words + l;
+        }
+        words += int64_t(kWave) * g_len[size_t(g)];
+    }
+    g_base[size_t(G)] = words;
+    int64_t bwords = 0;
+    for (int32_t str : comp) {
+        b_base[size_t(str)] = bwords;
+        bwords += h_bub[size_t(str)];
+    }
+    if (bwords >= (int64_t(1) << 31) - 2) return fail(WFSA_ERR_CAPACITY, "bubble buffer exceeds 2^31 words");
+
+    // 3. emit the streams (same tier as counted)
+    HIP_TRY(ctx->stream_w.alloc(size_t(std::max<int64_t>(words, 1))));
+    HIP_TRY(ctx->bub.alloc(size_t(std::max<int64_t>(bwords, 1))));
+    if (nc > 0) {
+        DevBuf<int64_t> d_sb, d_bb;
+        HIP_TRY(d_sb.upload(s_base.data(), size_t(S), s));
+        HIP_TRY(d_bb.upload(b_base.data(), size_t(S), s));
+        std::vector<int32_t> el[2];
+        for (int32_t str : comp) el[tier[size_t(str)]].push_back(str);
+        DevBuf<int32_t> d_el[2];
+        for (int t = 0; t < 2; ++t) {
+            if (el[t].empty()) continue;
+            HIP_TRY(d_el[t].upload(el[t].data(), el[t].size(), s));
+            wfsa::TravArgs a = trav_args(ctx, t);
+            a.list = d_el[t].ptr;
+            a.n_list = int32_t(el[t].size());
+            a.stream = ctx->stream_w.ptr;
+            a.s_base = d_sb.ptr;
+            a.bub = ctx->bub.ptr;
+            a.b_base = d_bb.ptr;
+            HIP_TRY(wfsa::launch_trav(wfsa::MODE_EMIT, a, trav_grid(ctx->cfg[t], ctx->n_cu, int64_t(el[t].size())), s));
+        }
+        HIP_TRY(hipStreamSynchronize(s));
+    }
+    HIP_TRY(ctx->g_base.upload(g_base.data(), size_t(G) + 1, s));
+    HIP_TRY(ctx->g_len.upload(g_len.data(), g_len.size(), s));
+    HIP_TRY(ctx->l_str.upload(l_str.data(), l_str.size(), s));
+    HIP_TRY(ctx->l_len.upload(l_len.data(), l_len.size(), s));
+    ctx->n_groups = G;
+    ctx->n_compiled = nc;
+
+    // compiled kernel geometry: 8 waves per block, gradient in LDS when it fits
+    const size_t grad_bytes = size_t(ctx->n_params) * sizeof(double);
+    int per_cu;
+    if (grad_bytes <= size_t(kLdsPerCu / 2 - 1024)) {
+        per_cu = 2;
+        ctx->c_lds_grad = 1;
+    } else if (grad_bytes <= size_t(kLdsPerCu - 1024)) {
+        per_cu = 1;
+        ctx->c_lds_grad = 1;
+    } else {
+        per_cu = 4;
+        ctx->c_lds_grad = 0;
+    }
+    ctx->c_lds = ctx->c_lds_grad ? grad_bytes : 0;
+    const int waves_per_block = kCompiledBlock / kWave;
+    ctx->c_grid = int(std::max<int64_t>(1, std::min<int64_t>(int64_t(ctx->n_cu) * per_cu,
+                                                             (int64_t(G) + waves_per_block - 1) / waves_per_block)));
+    HIP_TRY(ctx->scratch.alloc(size_t(ctx->c_grid) * kCompiledBlock * 2 * wfsa::kMaxBubbleNodes));
+
+    // traversal fallback lists
+    for (int t = 0; t < 2; ++t) {
+        ctx->n_fall[t] = int32_t(fb[t].size());
+        ctx->fall_grid[t] = fb[t].empty() ? 0 : trav_grid(ctx->cfg[t], ctx->n_cu, int64_t(fb[t].size()));
+        if (!fb[t].empty()) HIP_TRY(ctx->fall[t].upload(fb[t].data(), fb[t].size(), s));
+    }
+    const size_t waves = size_t(ctx->c_grid) * waves_per_block +
+                         size_t(ctx->fall_grid[0]) * size_t(ctx->cfg[0].waves_per_block) +
+                         size_t(ctx->fall_grid[1]) * size_t(ctx->cfg[1].waves_per_block);
+    HIP_TRY(ctx->ll_part.alloc(waves));
+    HIP_TRY(hipStreamSynchronize(s));
+
+    ctx->stats.compiled_strings = nc;
+    ctx->stats.fallback_strings = int64_t(fb[0].size() + fb[1].size());
+    ctx->stats.stream_words = words;
+    ctx->stats.bubble_words = bwords;
+    ctx->stats.tier1_strings = int32_t(l1.size());
+    ctx->stats.waves_per_block = ctx->cfg[0].waves_per_block;
+    ctx->stats.prepare_ms =
+        std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_start).count();
+    ctx->prep_level = 2;
     return WFSA_OK;
 }
 
@@ -300,13 +468,12 @@ int wfsa_dev_create(int device, wfsa_dev** out) {
     if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0)
         return fail(WFSA_ERR_NODEV, "device %d is %s; this build targets gfx950 (MI355X) only", device, prop.gcnArchName);
     HIP_TRY(hipSetDevice(device));
-    HIP_TRY(wfsa::configure_fb_kernels(kLdsPerCu));
+    HIP_TRY(wfsa::configure_kernels(kLdsPerCu));
     std::unique_ptr<wfsa_dev> ctx(new wfsa_dev());
     ctx->device = device;
     ctx->n_cu = prop.multiProcessorCount > 0 ? prop.multiProcessorCount : kNumCu;
     HIP_TRY(hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking));
-    HIP_TRY(hipEventCreate(&ctx->ev0));
-    HIP_TRY(hipEventCreate(&ctx->ev1));
+    for (hipEvent_t* ev : {&ctx->ev0, &ctx->ev1, &ctx->k0, &ctx->k1, &ctx->k2}) HIP_TRY(hipEventCreate(ev));
     HIP_TRY(ctx->live.alloc(1));
     *out = ctx.release();
     return WFSA_OK;
@@ -318,8 +485,8 @@ void wfsa_dev_destroy(wfsa_dev* ctx) {
     if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
     if (ctx->comm) (void)ncclCommDestroy(ctx->comm);
     if (ctx->pinned) (void)hipHostFree(ctx->pinned);
-    if (ctx->ev0) (void)hipEventDestroy(ctx->ev0);
-    if (ctx->ev1) (void)hipEventDestroy(ctx->ev1);
+    for (hipEvent_t ev : {ctx->ev0, ctx->ev1, ctx->k0, ctx->k1, ctx->k2})
+        if (ev) (void)hipEventDestroy(ev);
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
     delete ctx;
 }
@@ -330,27 +497,31 @@ int wfsa_dev_load_model(wfsa_dev* ctx, const wfsa_model_desc* model) {
     wfsa::TrellisModel tm;
     const std::string err = wfsa::compile_trellis_model(*model, tm);
     if (!err.empty()) return fail(WFSA_ERR_MODEL, "automaton rejected: %s", err.c_str());
+    // combined edge space: [0, E) byte edges, [E, E+X) end edges
+    const int64_t E = int64_t(tm.o_byte.size()), X = int64_t(tm.x_pptr.size()) - 1;
+    std::vector<int32_t> pptr(tm.o_pptr);
+    std::vector<int32_t> pidx(tm.o_pidx);
+    const int32_t shift = int32_t(tm.o_pidx.size());
+    for (int64_t x = 1; x <= X; ++x) pptr.push_back(tm.x_pptr[size_t(x)] + shift);
+    pidx.insert(pidx.end(), tm.x_pidx.begin(), tm.x_pidx.end());
     hipStream_t s = ctx->stream;
     HIP_TRY(ctx->o_ptr.upload(tm.o_ptr.data(), tm.o_ptr.size(), s));
     HIP_TRY(ctx->o_byte.upload(tm.o_byte.data(), tm.o_byte.size(), s));
     HIP_TRY(ctx->o_dst.upload(tm.o_dst.data(), tm.o_dst.size(), s));
-    HIP_TRY(ctx->o_pptr.upload(tm.o_pptr.data(), tm.o_pptr.size(), s));
-    HIP_TRY(ctx->o_pidx.upload(tm.o_pidx.data(), tm.o_pidx.size(), s));
     HIP_TRY(ctx->x_ptr.upload(tm.x_ptr.data(), tm.x_ptr.size(), s));
-    HIP_TRY(ctx->x_pptr.upload(tm.x_pptr.data(), tm.x_pptr.size(), s));
-    HIP_TRY(ctx->x_pidx.upload(tm.x_pidx.data(), tm.x_pidx.size(), s));
+    HIP_TRY(ctx->pptr.upload(pptr.data(), pptr.size(), s));
+    HIP_TRY(ctx->pidx.upload(pidx.data(), pidx.size(), s));
     HIP_TRY(ctx->node_end_count.upload(tm.node_end_count.data(), tm.node_end_count.size(), s));
-    ctx->n_edges = int64_t(tm.o_byte.size());
-    ctx->n_end = int64_t(tm.x_pptr.size()) - 1;
-    HIP_TRY(ctx->o_w.alloc(size_t(ctx->n_edges)));
-    HIP_TRY(ctx->x_w.alloc(size_t(ctx->n_end)));
+    HIP_TRY(ctx->lw.alloc(size_t(E + X)));
+    HIP_TRY(ctx->ew.alloc(size_t(E + X)));
     HIP_TRY(ctx->node_end.alloc(size_t(tm.n_nodes)));
+    ctx->n_edges = E;
+    ctx->n_end = X;
     ctx->n_params = tm.n_params;
     ctx->n_nodes = tm.n_nodes;
     ctx->start = tm.start;
     HIP_TRY(ctx->w_full.alloc(size_t(ctx->n_params)));
     HIP_TRY(ctx->out.alloc(size_t(ctx->n_params) + 1));
-    HIP_TRY(ctx->used.alloc(size_t(ctx->n_params)));
     if (ctx->pinned_n < size_t(ctx->n_params) + 1) {
         if (ctx->pinned) (void)hipHostFree(ctx->pinned);
         ctx->pinned = nullptr;
@@ -362,6 +533,7 @@ int wfsa_dev_load_model(wfsa_dev* ctx, const wfsa_model_desc* model) {
     ctx->stats.n_nodes = ctx->n_nodes;
     ctx->stats.n_edges = ctx->n_edges;
     ctx->stats.n_end_edges = ctx->n_end;
+    ctx->prep_level = 0;
     if (ctx->has_corpus) return configure_tiers(ctx);
     return WFSA_OK;
 }
@@ -387,11 +559,13 @@ int wfsa_dev_load_corpus(wfsa_dev* ctx, const uint8_t* sym, const int64_t* off, 
     std::vector<int32_t> ids(static_cast<size_t>(n_strings));
     for (int64_t i = 0; i < n_strings; ++i) ids[size_t(i)] = int32_t(i);
     HIP_TRY(ctx->list_all.upload(ids.data(), ids.size(), s));
+    HIP_TRY(ctx->logq.alloc(size_t(std::max<int64_t>(n_strings, 1))));
     HIP_TRY(hipStreamSynchronize(s));
     ctx->n_strings = n_strings;
     ctx->total_sym = total;
     ctx->max_len = int32_t(max_len);
     ctx->has_corpus = true;
+    ctx->prep_level = 0;
     ctx->stats.n_strings = n_strings;
     ctx->stats.total_symbols = total;
     ctx->stats.max_len = int32_t(max_len);
@@ -402,15 +576,15 @@ int wfsa_dev_load_corpus(wfsa_dev* ctx, const uint8_t* sym, const int64_t* off, 
 int wfsa_dev_recognize(wfsa_dev* ctx, uint8_t* recognized, double* path_count, uint8_t* used_param) {
     if (int rc = check_ctx(ctx)) return rc;
     if (!ctx->has_model || !ctx->has_corpus) return fail(WFSA_ERR_ARG, "load a model and a corpus first");
-    if (int rc = counting_pass(ctx, true)) return rc;
+    if (ctx->prep_level < 1)
+        if (int rc = prepare(ctx, 1)) return rc;
     hipStream_t s = ctx->stream;
     const size_t S = size_t(ctx->n_strings);
     if (ctx->comm && ctx->n_params > 0)
         RCCL_TRY(ncclAllReduce(ctx->used.ptr, ctx->used.ptr, size_t(ctx->n_params), ncclUint8, ncclMax, ctx->comm, s));
-    if (recognized && S) HIP_TRY(hipMemcpyAsync(recognized, ctx->recog.ptr, S, hipMemcpyDeviceToHost, s));
-    if (path_count && S) HIP_TRY(hipMemcpyAsync(path_count, ctx->pcount.ptr, S * sizeof(double), hipMemcpyDeviceToHost, s));
-    if (used_param && ctx->n_params)
-        HIP_TRY(hipMemcpyAsync(used_param, ctx->used.ptr, size_t(ctx->n_params), hipMemcpyDeviceToHost, s));
+    if (recognized) HIP_TRY(ctx->recog.download(recognized, S, s));
+    if (path_count) HIP_TRY(ctx->pcount.download(path_count, S, s));
+    if (used_param) HIP_TRY(ctx->used.download(used_param, size_t(ctx->n_params), s));
     HIP_TRY(hipStreamSynchronize(s));
     return WFSA_OK;
 }
@@ -419,58 +593,76 @@ int wfsa_dev_objective_grad(wfsa_dev* ctx, const double* w_full, double* loglik,
     if (int rc = check_ctx(ctx)) return rc;
     if (!ctx->has_model || !ctx->has_corpus) return fail(WFSA_ERR_ARG, "load a model and a corpus first");
     if (!w_full && ctx->n_params > 0) return fail(WFSA_ERR_ARG, "null weights");
-    if (!ctx->tiers_ready)
-        if (int rc = counting_pass(ctx, false)) return rc;
+    if (ctx->prep_level < 2)
+        if (int rc = prepare(ctx, 2)) return rc;
     hipStream_t s = ctx->stream;
     const int32_t np = ctx->n_params;
-    HIP_TRY(hipEventRecord(ctx->ev0, s));   // whole call, device side
+    HIP_TRY(hipEventRecord(ctx->ev0, s));
     if (np > 0) {
         std::memcpy(ctx->pinned, w_full, size_t(np) * sizeof(double));
         HIP_TRY(hipMemcpyAsync(ctx->w_full.ptr, ctx->pinned, size_t(np) * sizeof(double), hipMemcpyHostToDevice, s));
     }
-    HIP_TRY(wfsa::launch_edge_weights(ctx->w_full.ptr, ctx->o_pptr.ptr, ctx->o_pidx.ptr, ctx->o_w.ptr, ctx->n_edges, s));
-    HIP_TRY(wfsa::launch_edge_weights(ctx->w_full.ptr, ctx->x_pptr.ptr, ctx->x_pidx.ptr, ctx->x_w.ptr, ctx->n_end, s));
-    HIP_TRY(wfsa::launch_node_end(ctx->x_ptr.ptr, ctx->x_w.ptr, ctx->node_end.ptr, ctx->n_nodes, s));
+    HIP_TRY(wfsa::launch_edge_weights(ctx->w_full.ptr, ctx->pptr.ptr, ctx->pidx.ptr, ctx->lw.ptr, ctx->ew.ptr,
+                                      ctx->n_edges + ctx->n_end, s));
+    const bool any_fall = ctx->n_fall[0] + ctx->n_fall[1] > 0;
+    if (any_fall) HIP_TRY(wfsa::launch_node_end(ctx->x_ptr.ptr, ctx->ew.ptr + ctx->n_edges, ctx->node_end.ptr, ctx->n_nodes, s));
     HIP_TRY(hipMemsetAsync(ctx->out.ptr, 0, (size_t(np) + 1) * sizeof(double), s));
     HIP_TRY(hipMemsetAsync(ctx->live.ptr, 0, sizeof(unsigned long long), s));
-    if (logq) HIP_TRY(ctx->logq.alloc(size_t(ctx->n_strings)));
-    hipEvent_t k0, k1;
-    HIP_TRY(hipEventCreate(&k0));
-    HIP_TRY(hipEventCreate(&k1));
-    HIP_TRY(hipEventRecord(k0, s));
     int32_t wave_off = 0;
+    HIP_TRY(hipEventRecord(ctx->k0, s));
+    if (ctx->n_groups > 0) {
+        wfsa::CompiledArgs c{};
+        c.m = model_view(ctx);
+        c.p = ctx->p.ptr;
+        c.stream = ctx->stream_w.ptr;
+        c.bub = ctx->bub.ptr;
+        c.g_base = ctx->g_base.ptr;
+        c.g_len = ctx->g_len.ptr;
+        c.l_str = ctx->l_str.ptr;
+        c.l_len = ctx->l_len.ptr;
+        c.n_groups = ctx->n_groups;
+        c.n_params = np;
+        c.grad_in_lds = ctx->c_lds_grad;
+        c.grad = ctx->out.ptr + 1;
+        c.ll_part = ctx->ll_part.ptr;
+        c.logq = logq ? ctx->logq.ptr : nullptr;
+        c.scratch = ctx->scratch.ptr;
+        HIP_TRY(wfsa::launch_compiled(c, ctx->c_grid, kCompiledBlock, ctx->c_lds, s));
+        wave_off += ctx->c_grid * (kCompiledBlock / kWave);
+    }
+    HIP_TRY(hipEventRecord(ctx->k1, s));
     for (int t = 0; t < 2; ++t) {
-        if (!ctx->n_list[t]) continue;
-        wfsa::FBArgs a = base_args(ctx, t);
-        a.list = ctx->list[t].ptr;
-        a.n_list = ctx->n_list[t];
+        if (!ctx->n_fall[t]) continue;
+        wfsa::TravArgs a = trav_args(ctx, t);
+        a.list = ctx->fall[t].ptr;
+        a.n_list = ctx->n_fall[t];
         a.grad = ctx->out.ptr + 1;
         a.ll_part = ctx->ll_part.ptr + wave_off;
         a.logq = logq ? ctx->logq.ptr : nullptr;
-        HIP_TRY(wfsa::launch_fb(false, a, ctx->grid[t], s));
-        wave_off += ctx->grid[t] * ctx->cfg[t].waves_per_block;
+        HIP_TRY(wfsa::launch_trav(wfsa::MODE_WEIGHTED, a, ctx->fall_grid[t], s));
+        wave_off += ctx->fall_grid[t] * ctx->cfg[t].waves_per_block;
     }
-    HIP_TRY(hipEventRecord(k1, s));
+    HIP_TRY(hipEventRecord(ctx->k2, s));
     HIP_TRY(wfsa::launch_finalize(ctx->ll_part.ptr, wave_off, ctx->out.ptr, s));
     if (ctx->comm) RCCL_TRY(ncclAllReduce(ctx->out.ptr, ctx->out.ptr, size_t(np) + 1, ncclDouble, ncclSum, ctx->comm, s));
     HIP_TRY(hipMemcpyAsync(ctx->pinned, ctx->out.ptr, (size_t(np) + 1) * sizeof(double), hipMemcpyDeviceToHost, s));
-    if (logq && ctx->n_strings)
-        HIP_TRY(hipMemcpyAsync(logq, ctx->logq.ptr, size_t(ctx->n_strings) * sizeof(double), hipMemcpyDeviceToHost, s));
+    if (logq) HIP_TRY(ctx->logq.download(logq, size_t(ctx->n_strings), s));
     unsigned long long live = 0;
     HIP_TRY(hipMemcpyAsync(&live, ctx->live.ptr, sizeof live, hipMemcpyDeviceToHost, s));
     HIP_TRY(hipEventRecord(ctx->ev1, s));
     HIP_TRY(hipStreamSynchronize(s));
-    float kms = 0.f, cms = 0.f;
-    HIP_TRY(hipEventElapsedTime(&kms, k0, k1));
-    HIP_TRY(hipEventElapsedTime(&cms, ctx->ev0, ctx->ev1));
-    (void)hipEventDestroy(k0);
-    (void)hipEventDestroy(k1);
+    float c_ms = 0.f, f_ms = 0.f, all_ms = 0.f;
+    HIP_TRY(hipEventElapsedTime(&c_ms, ctx->k0, ctx->k1));
+    HIP_TRY(hipEventElapsedTime(&f_ms, ctx->k1, ctx->k2));
+    HIP_TRY(hipEventElapsedTime(&all_ms, ctx->ev0, ctx->ev1));
     if (loglik) *loglik = ctx->pinned[0];
     if (grad_full && np > 0) std::memcpy(grad_full, ctx->pinned + 1, size_t(np) * sizeof(double));
     ctx->stats.fb_launches += 1;
-    ctx->stats.fb_kernel_ms += double(kms);
-    ctx->stats.last_fb_kernel_ms = double(kms);
-    ctx->stats.last_call_ms = double(cms);
+    ctx->stats.fb_kernel_ms += double(c_ms) + double(f_ms);
+    ctx->stats.last_fb_kernel_ms = double(c_ms) + double(f_ms);
+    ctx->stats.last_compiled_ms = double(c_ms);
+    ctx->stats.compiled_kernel_ms += double(c_ms);
+    ctx->stats.last_call_ms = double(all_ms);
     ctx->stats.last_live_edges = int64_t(live);
     return WFSA_OK;
 }
@@ -507,7 +699,7 @@ int wfsa_dev_allreduce(wfsa_dev* ctx, double* host_buf, int64_t count) {
     DevBuf<double> tmp;
     HIP_TRY(tmp.upload(host_buf, size_t(count), ctx->stream));
     RCCL_TRY(ncclAllReduce(tmp.ptr, tmp.ptr, size_t(count), ncclDouble, ncclSum, ctx->comm, ctx->stream));
-    HIP_TRY(hipMemcpyAsync(host_buf, tmp.ptr, size_t(count) * sizeof(double), hipMemcpyDeviceToHost, ctx->stream));
+    HIP_TRY(tmp.download(host_buf, size_t(count), ctx->stream));
     HIP_TRY(hipStreamSynchronize(ctx->stream));
     return WFSA_OK;
 }
