@@ -79,6 +79,7 @@ typedef struct {
     int64_t fallback_strings;  /* served by the traversal kernel            */
     int64_t stream_words;      /* compiled main-stream words (with padding) */
     int64_t bubble_words;
+    int64_t n_bubbles;         /* compiled bubbles (bubble kernel lanes)    */
     int64_t fb_launches;       /* objective_grad calls timed so far         */
     double fb_kernel_ms;       /* sum of their forward-backward kernel time */
     double last_fb_kernel_ms;  /* last call: compiled + traversal kernels   */

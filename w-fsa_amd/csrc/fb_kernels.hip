@@ -125,14 +125,17 @@ struct Slab {
 };
 
 // Compiled stream of one string from its counted trellis (lane 0 only;
-// beta > 0 marks live entries).  Returns false when a bubble exceeds the
+// beta > 0 marks live entries).  Trivial segments go to the main stream,
+// bubbles to the bubble buffer.  Returns false when a bubble exceeds the
 // kernel limits; the string then stays on the traversal path.
 template <bool WRITE>
-__device__ bool compile_walk(const Slab& sl, const ModelView& m, int L, int& n_main, int& n_bub,
-                             int32_t* stream, int64_t s_base, int32_t* bub, int64_t b_base) {
+__device__ bool compile_walk(const Slab& sl, const ModelView& m, int L, int sidx, int& n_main, int& n_bub,
+                             int& n_nb, int32_t* stream, int64_t s_base, int32_t* bub, int64_t b_base,
+                             int32_t* bub_off, int32_t b_first) {
     long long* lid = reinterpret_cast<long long*>(sl.alpha);   // alpha is dead in counting mode
     n_main = 0;
     n_bub = 0;
+    n_nb = 0;
     int a = 0, fa = 0;
     while (a <= L) {
         int b = a + 1, fbn = -1;
@@ -173,8 +176,9 @@ __device__ bool compile_walk(const Slab& sl, const ModelView& m, int L, int& n_m
                 if (sl.beta[f] > 0.0) lid[f] = nodes++;
         const int end_id = nodes++;   // the cut node b, or the virtual end node
         if (!to_end) lid[fbn] = end_id;
+        const int e_hi = sl.epos[to_end ? L : b];
         int edges = 0;
-        for (int e = sl.epos[a]; e < sl.epos[b <= L ? b : L]; ++e)
+        for (int e = sl.epos[a]; e < e_hi; ++e)
             if (sl.beta[sl.e_dst[e]] > 0.0) ++edges;
         if (to_end)
             for (int f = sl.fpos[L]; f < sl.fpos[L + 1]; ++f)
@@ -182,8 +186,10 @@ __device__ bool compile_walk(const Slab& sl, const ModelView& m, int L, int& n_m
         if (nodes > kMaxBubbleNodes || edges > kMaxBubbleEdges) return false;
         if (WRITE) {
             int64_t w = b_base + n_bub;
+            bub_off[b_first + n_nb] = int32_t(w);
             bub[w++] = nodes | (edges << 16);
-            for (int e = sl.epos[a]; e < sl.epos[b <= L ? b : L]; ++e) {
+            bub[w++] = sidx;
+            for (int e = sl.epos[a]; e < e_hi; ++e) {
                 const int h = sl.e_dst[e];
                 if (!(sl.beta[h] > 0.0)) continue;
                 bub[w++] = sl.e_g[e];
@@ -199,10 +205,9 @@ __device__ bool compile_walk(const Slab& sl, const ModelView& m, int L, int& n_m
                     }
                 }
             }
-            stream[s_base + int64_t(kWave) * n_main] = -int(1 + b_base + n_bub);
         }
-        n_bub += 1 + 2 * edges;
-        ++n_main;
+        n_bub += 2 + 2 * edges;
+        ++n_nb;
         if (to_end) break;
         a = b;
         fa = fbn;
@@ -432,15 +437,17 @@ __global__ __launch_bounds__(256) void trav_kernel(TravArgs a) {
         // ---------------- compiled stream ----------------
         if (COUNTING && (a.c_main || MODE == MODE_EMIT)) {
             if (lane == 0) {
-                int n_main = 0, n_bub = 0;
+                int n_main = 0, n_bub = 0, n_nb = 0;
                 bool ok;
                 if (MODE == MODE_EMIT)
-                    ok = compile_walk<true>(sl, m, L, n_main, n_bub, a.stream, a.s_base[sidx], a.bub, a.b_base[sidx]);
+                    ok = compile_walk<true>(sl, m, L, sidx, n_main, n_bub, n_nb, a.stream, a.s_base[sidx], a.bub,
+                                            a.b_base[sidx], a.bub_off, a.b_first[sidx]);
                 else
-                    ok = compile_walk<false>(sl, m, L, n_main, n_bub, nullptr, 0, nullptr, 0);
+                    ok = compile_walk<false>(sl, m, L, sidx, n_main, n_bub, n_nb, nullptr, 0, nullptr, 0, nullptr, 0);
                 if (MODE == MODE_COUNT) {
                     a.c_main[sidx] = ok ? n_main : 0;
                     a.c_bub[sidx] = ok ? n_bub : -1;
+                    a.c_nbub[sidx] = ok ? n_nb : 0;
                 }
             }
             wave_sync();
@@ -453,39 +460,10 @@ __global__ __launch_bounds__(256) void trav_kernel(TravArgs a) {
     }
 }
 
-// One bubble of a compiled stream: local forward, local backward, posteriors
-// relative to the bubble; returns log Z_seg.
-template <bool LDS_GRAD>
-__device__ double eval_bubble(const CompiledArgs& a, int64_t off, double p, double* A, double* B, double* gacc) {
-    const int hdr = a.bub[off];
-    const int nodes = hdr & 0xffff, edges = hdr >> 16;
-    const int32_t* ed = a.bub + off + 1;
-    for (int i = 0; i < nodes; ++i) {
-        A[i] = 0.0;
-        B[i] = 0.0;
-    }
-    A[0] = 1.0;
-    for (int e = 0; e < edges; ++e) {
-        const int g = ed[2 * e], sd = ed[2 * e + 1];
-        A[sd >> 16] += A[sd & 0xffff] * a.m.ew[g];
-    }
-    const double Z = A[nodes - 1];
-    const double inv = 1.0 / Z;
-    B[nodes - 1] = 1.0;
-    for (int e = edges - 1; e >= 0; --e) {
-        const int g = ed[2 * e], sd = ed[2 * e + 1];
-        const int src = sd & 0xffff;
-        const double b = a.m.ew[g] * B[sd >> 16];
-        B[src] += b;
-        const double xi = A[src] * b * inv;
-        for (int q = a.m.pptr[g]; q < a.m.pptr[g + 1]; ++q) {
-            if (LDS_GRAD) block_add(&gacc[a.m.pidx[q]], -p * xi);
-            else global_add(&a.grad[a.m.pidx[q]], -p * xi);
-        }
-    }
-    return log(Z);
-}
-
+// Main streams: one lane per string, 64 strings of similar stream length per
+// wavefront, trivial words only.  Every word is an edge on all of the
+// string's paths: log q accumulates its log-weight, its parameters get -p_s.
+// Groups are dealt to waves in snake order (longest first) to balance them.
 template <bool LDS_GRAD>
 __global__ __launch_bounds__(512) void fbc_kernel(CompiledArgs a) {
     extern __shared__ __attribute__((aligned(16))) double gacc[];
@@ -497,30 +475,48 @@ __global__ __launch_bounds__(512) void fbc_kernel(CompiledArgs a) {
         for (int j = int(threadIdx.x); j < a.n_params; j += int(blockDim.x)) gacc[j] = 0.0;
         __syncthreads();
     }
-    double* A = a.scratch + (size_t(gw) * kWave + lane) * (2 * kMaxBubbleNodes);
-    double* B = A + kMaxBubbleNodes;
-    const double* lw = a.m.lw;
+    const EdgeRec* erec = a.m.erec;
     double ll_acc = 0.0;
+    constexpr int U = 8;   // stream words in flight per lane
 
-    for (int grp = gw; grp < a.n_groups; grp += nw) {
+    for (int round = 0;; ++round) {
+        const int grp = round * nw + ((round & 1) ? (nw - 1 - gw) : gw);
+        if (grp >= a.n_groups) break;
         const int s = a.l_str[grp * kWave + lane];
         const int len = a.l_len[grp * kWave + lane];
         const int glen = a.g_len[grp];
         const int32_t* st = a.stream + a.g_base[grp] + lane;
         const double p = s >= 0 ? a.p[s] : 0.0;
         double acc = 0.0;
-        for (int k = 0; k < glen; ++k) {
-            if (k >= len) break;
-            const int w = st[int64_t(kWave) * k];
-            if (w >= 0) {
-                acc += lw[w];
-                for (int q = a.m.pptr[w]; q < a.m.pptr[w + 1]; ++q) {
-                    if (LDS_GRAD) block_add(&gacc[a.m.pidx[q]], -p);
-                    else global_add(&a.grad[a.m.pidx[q]], -p);
-                }
-            } else {
-                acc += eval_bubble<LDS_GRAD>(a, int64_t(-(w + 1)), p, A, B, gacc);
+        int w[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) w[u] = (u < len) ? st[int64_t(kWave) * u] : -1;
+        for (int k0 = 0; k0 < glen; k0 += U) {
+            EdgeRec r[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) r[u] = w[u] >= 0 ? erec[w[u]] : EdgeRec{0.0, 0, 0};
+            // next chunk's words are in flight while this chunk is applied
+            int wn[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const int k = k0 + U + u;
+                wn[u] = (k < len) ? st[int64_t(kWave) * k] : -1;
             }
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                acc += r[u].lw;
+                if (r[u].np == 1) {
+                    if (LDS_GRAD) block_add(&gacc[r[u].p0], -p);
+                    else global_add(&a.grad[r[u].p0], -p);
+                } else if (r[u].np > 1) {
+                    for (int q = a.m.pptr[w[u]]; q < a.m.pptr[w[u] + 1]; ++q) {
+                        if (LDS_GRAD) block_add(&gacc[a.m.pidx[q]], -p);
+                        else global_add(&a.grad[a.m.pidx[q]], -p);
+                    }
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < U; ++u) w[u] = wn[u];
         }
         if (s >= 0) {
             ll_acc += p * acc;
@@ -538,15 +534,75 @@ __global__ __launch_bounds__(512) void fbc_kernel(CompiledArgs a) {
     }
 }
 
+// Bubbles: one lane per bubble (largest first).  Local forward from the
+// bubble's first cut, local backward from its last cut; an edge's posterior
+// is alpha(src) w beta(dst) / Z and -p_s times it goes to the edge's
+// contribution slot; log Z joins the string's log q.
+__global__ __launch_bounds__(kBubbleBlock) void bubble_kernel(BubbleArgs a) {
+    __shared__ double scr[kBubbleBlock][2 * kMaxBubbleNodes + 1];
+    const int lane = lane_id();
+    const int gw = int(blockIdx.x) * (kBubbleBlock / kWave) + int(threadIdx.x) / kWave;
+    double* A = scr[threadIdx.x];
+    double* B = A + kMaxBubbleNodes;
+    double ll_acc = 0.0;
+    for (int bi = int(blockIdx.x * blockDim.x + threadIdx.x); bi < a.n_bubbles; bi += int(gridDim.x * blockDim.x)) {
+        const int off = a.bub_off[bi];
+        const int hdr = a.bub[off];
+        const int s = a.bub[off + 1];
+        const int nodes = hdr & 0xffff, edges = hdr >> 16;
+        const int32_t* ed = a.bub + off + 2;
+        const double p = a.p[s];
+        for (int i = 0; i < nodes; ++i) {
+            A[i] = 0.0;
+            B[i] = 0.0;
+        }
+        A[0] = 1.0;
+        for (int e = 0; e < edges; ++e) {
+            const int g = ed[2 * e], sd = ed[2 * e + 1];
+            A[sd >> 16] += A[sd & 0xffff] * a.m.ew[g];
+        }
+        const double Z = A[nodes - 1];
+        const double scale = -p / Z;
+        B[nodes - 1] = 1.0;
+        double* c = a.contrib + (off >> 1) + 1;
+        for (int e = edges - 1; e >= 0; --e) {
+            const int g = ed[2 * e], sd = ed[2 * e + 1];
+            const int src = sd & 0xffff;
+            const double b = a.m.ew[g] * B[sd >> 16];
+            B[src] += b;
+            c[e] = A[src] * b * scale;
+        }
+        const double lz = log(Z);
+        ll_acc += p * lz;
+        if (a.logq) global_add(&a.logq[s], lz);
+    }
+    ll_acc = wave_sum(ll_acc);
+    if (lane == 0) a.ll_part[gw] = ll_acc;
+}
+
+__global__ __launch_bounds__(256) void bubble_grad_kernel(BubbleGradArgs a) {
+    const int c = int(blockIdx.x) * 4 + int(threadIdx.x) / kWave;
+    if (c >= a.n_chunks) return;
+    const int lane = lane_id();
+    double s = 0.0;
+    for (int k = a.chunk_ptr[c] + lane; k < a.chunk_ptr[c + 1]; k += kWave) s += a.contrib[a.slot[k]];
+    s = wave_sum(s);
+    if (lane == 0) global_add(&a.grad[a.chunk_param[c]], s);
+}
+
+// Per iteration: log-weight, weight and parameter record of every combined
+// edge from the GetWeight-expanded parameter vector.
 __global__ void edge_weights_kernel(const double* __restrict__ w_full, const int32_t* __restrict__ pptr,
                                     const int32_t* __restrict__ pidx, double* __restrict__ lw,
-                                    double* __restrict__ ew, int64_t n) {
+                                    double* __restrict__ ew, EdgeRec* __restrict__ erec, int64_t n) {
     const int64_t g = int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
     if (g >= n) return;
+    const int32_t b = pptr[g], e = pptr[g + 1];
     double s = 0.0;
-    for (int32_t k = pptr[g]; k < pptr[g + 1]; ++k) s += w_full[pidx[k]];
+    for (int32_t k = b; k < e; ++k) s += w_full[pidx[k]];
     lw[g] = s;
     ew[g] = exp(s);
+    erec[g] = EdgeRec{s, e > b ? pidx[b] : 0, e - b};
 }
 
 __global__ void node_end_kernel(const int32_t* __restrict__ x_ptr, const double* __restrict__ x_w,
@@ -613,11 +669,24 @@ hipError_t launch_compiled(const CompiledArgs& a, int grid, int block, size_t ld
     return hipGetLastError();
 }
 
+hipError_t launch_bubbles(const BubbleArgs& a, int grid, hipStream_t stream) {
+    if (a.n_bubbles <= 0) return hipSuccess;
+    hipLaunchKernelGGL(bubble_kernel, dim3(unsigned(grid)), dim3(kBubbleBlock), 0, stream, a);
+    return hipGetLastError();
+}
+
+hipError_t launch_bubble_grad(const BubbleGradArgs& a, hipStream_t stream) {
+    if (a.n_chunks <= 0) return hipSuccess;
+    hipLaunchKernelGGL(bubble_grad_kernel, dim3(unsigned((a.n_chunks + 3) / 4)), dim3(256), 0, stream, a);
+    return hipGetLastError();
+}
+
 hipError_t launch_edge_weights(const double* w_full, const int32_t* pptr, const int32_t* pidx, double* lw,
-                               double* ew, int64_t n_edges, hipStream_t stream) {
+                               double* ew, EdgeRec* erec, int64_t n_edges, hipStream_t stream) {
     if (n_edges <= 0) return hipSuccess;
     const unsigned blocks = unsigned((n_edges + 255) / 256);
-    hipLaunchKernelGGL(edge_weights_kernel, dim3(blocks), dim3(256), 0, stream, w_full, pptr, pidx, lw, ew, n_edges);
+    hipLaunchKernelGGL(edge_weights_kernel, dim3(blocks), dim3(256), 0, stream, w_full, pptr, pidx, lw, ew, erec,
+                       n_edges);
     return hipGetLastError();
 }
 

@@ -19,8 +19,16 @@
 
 namespace wfsa {
 
-constexpr int kMaxBubbleNodes = 32;    // nodes of one compiled bubble
+constexpr int kMaxBubbleNodes = 16;    // nodes of one compiled bubble
 constexpr int kMaxBubbleEdges = 255;   // edges of one compiled bubble
+
+// Per-iteration record of a combined edge, one 16-byte gather in the
+// compiled kernel: its log-weight and its parameter list (p0 when np == 1).
+struct alignas(16) EdgeRec {
+    double lw;
+    int32_t p0;   // first parameter (np >= 1)
+    int32_t np;   // number of parameters
+};
 
 // Compiled trellis automaton resident in HBM (see trellis_model.hpp).
 // Edge ids: [0, E) byte-consuming edges, [E, E+X) end edges ("combined").
@@ -33,6 +41,7 @@ struct ModelView {
     const int32_t* pidx;
     const double* ew;        // [E+X] exp(log-weight), per iteration
     const double* lw;        // [E+X] log-weight, per iteration
+    const EdgeRec* erec;     // [E+X] log-weight + parameters, per iteration
     const double* node_end;  // [n_nodes] sum of the node's end-edge weights
     const double* node_end_count;  // [n_nodes] number of end edges (counting mode)
     int32_t n_nodes;
@@ -94,21 +103,28 @@ struct TravArgs {
     uint8_t* used;           // [n_params] or null
     int32_t* c_main;         // [S] compiled main-stream words, or null
     int32_t* c_bub;          // [S] compiled bubble words (-1: does not compile)
+    int32_t* c_nbub;         // [S] number of bubbles
     // emit mode
     int32_t* stream;         // interleaved main streams
     const int64_t* s_base;   // [S] word index of the string's first main word
     int32_t* bub;            // bubble buffer
     const int64_t* b_base;   // [S] word index of the string's first bubble word
+    const int32_t* b_first;  // [S] ordinal of the string's first bubble
+    int32_t* bub_off;        // [n_bubbles] word offset of each bubble
     uint8_t* overflow;       // [S] string did not fit the slab
     unsigned long long* live_edges;
 };
 
-// Compiled streams of the per-iteration kernel.
+// Compiled streams of the per-iteration kernels.
+//   main stream: only "trivial" words (edge ids whose posterior is 1),
+//     interleaved: word k of lane l of group g at g_base[g] + 64 k + l;
+//   bubble buffer: per bubble [nodes | edges << 16, string, (edge id,
+//     src | dst << 16) x edges], always at an even word offset, so edge e of
+//     the bubble at offset o owns contribution slot o / 2 + 1 + e.
 struct CompiledArgs {
     ModelView m;
     const double* p;         // [S]
-    const int32_t* stream;   // interleaved: word k of lane l of group g at g_base[g] + 64 k + l
-    const int32_t* bub;
+    const int32_t* stream;
     const int64_t* g_base;   // [G]
     const int32_t* g_len;    // [G] longest stream of the group (its first lane)
     const int32_t* l_str;    // [64 G] string of each lane, -1 = padding
@@ -119,14 +135,40 @@ struct CompiledArgs {
     double* grad;            // [n_params]
     double* ll_part;         // [waves in grid]
     double* logq;            // [S] or null
-    double* scratch;         // per lane 2 * kMaxBubbleNodes doubles
+};
+
+struct BubbleArgs {
+    ModelView m;
+    const double* p;
+    const int32_t* bub;
+    const int32_t* bub_off;  // [n_bubbles], largest bubbles first
+    int32_t n_bubbles;
+    double* contrib;         // [bubble words / 2] -p_s * posterior per bubble edge
+    double* ll_part;         // [waves in grid]
+    double* logq;            // [S] or null: log Z added to the string's entry
+};
+
+// grad[j] += sum of contrib over the bubble edges carrying parameter j, in
+// chunks of at most kBubbleGradChunk slots (one wavefront per chunk, so a hot
+// parameter's long slot list is summed by many waves).
+constexpr int kBubbleGradChunk = 512;
+struct BubbleGradArgs {
+    const int32_t* chunk_param;  // [n_chunks]
+    const int32_t* chunk_ptr;    // [n_chunks+1] into slot
+    const int32_t* slot;
+    const double* contrib;
+    int32_t n_chunks;
+    double* grad;
 };
 
 hipError_t configure_kernels(int max_dynamic_lds);
 hipError_t launch_trav(TravMode mode, const TravArgs& a, int grid, hipStream_t stream);
 hipError_t launch_compiled(const CompiledArgs& a, int grid, int block, size_t lds, hipStream_t stream);
+constexpr int kBubbleBlock = 128;
+hipError_t launch_bubbles(const BubbleArgs& a, int grid, hipStream_t stream);
+hipError_t launch_bubble_grad(const BubbleGradArgs& a, hipStream_t stream);
 hipError_t launch_edge_weights(const double* w_full, const int32_t* pptr, const int32_t* pidx, double* lw,
-                               double* ew, int64_t n_edges, hipStream_t stream);
+                               double* ew, EdgeRec* erec, int64_t n_edges, hipStream_t stream);
 hipError_t launch_node_end(const int32_t* x_ptr, const double* x_w, double* node_end, int32_t n_nodes,
                            hipStream_t stream);
 hipError_t launch_finalize(const double* ll_part, int32_t n_part, double* out, hipStream_t stream);

@@ -111,6 +111,7 @@ struct wfsa_dev {
     DevBuf<int32_t> o_ptr, o_dst, x_ptr, pptr, pidx;
     DevBuf<uint8_t> o_byte;
     DevBuf<double> lw, ew, node_end, node_end_count;
+    DevBuf<wfsa::EdgeRec> erec;
 
     // corpus
     bool has_corpus = false;
@@ -137,8 +138,14 @@ struct wfsa_dev {
     int64_t n_compiled = 0;
     DevBuf<int32_t> stream_w, bub, g_len, l_str, l_len;
     DevBuf<int64_t> g_base;
-    DevBuf<double> scratch;
     int c_grid = 0, c_lds_grad = 0;
+    // bubbles
+    int32_t n_bubbles = 0;
+    int b_grid = 0;
+    int32_t n_bg_chunks = 0;
+    DevBuf<int32_t> bub_off, bg_chunk_param, bg_chunk_ptr, bg_slot;
+    DevBuf<double> contrib;
+    std::vector<int32_t> h_pptr, h_pidx;   // host copy of the combined parameter lists
     size_t c_lds = 0;
 
     // traversal fallback: per tier string lists
@@ -211,6 +218,7 @@ wfsa::ModelView model_view(wfsa_dev* ctx) {
     m.pidx = ctx->pidx.ptr;
     m.ew = ctx->ew.ptr;
     m.lw = ctx->lw.ptr;
+    m.erec = ctx->erec.ptr;
     m.node_end = ctx->node_end.ptr;
     m.node_end_count = ctx->node_end_count.ptr;
     m.n_nodes = ctx->n_nodes;
@@ -268,13 +276,15 @@ int prepare(wfsa_dev* ctx, int level) {
     HIP_TRY(ctx->pcount.alloc(SZ));
     HIP_TRY(ctx->recog.alloc(SZ));
     HIP_TRY(ctx->used.alloc(size_t(std::max(ctx->n_params, 1))));
-    DevBuf<int32_t> c_main, c_bub;
+    DevBuf<int32_t> c_main, c_bub, c_nbub;
     HIP_TRY(c_main.alloc(SZ));
     HIP_TRY(c_bub.alloc(SZ));
+    HIP_TRY(c_nbub.alloc(SZ));
     HIP_TRY(hipMemsetAsync(ctx->overflow.ptr, 0, SZ, s));
     HIP_TRY(hipMemsetAsync(ctx->used.ptr, 0, size_t(std::max(ctx->n_params, 1)), s));
     HIP_TRY(hipMemsetAsync(c_main.ptr, 0, SZ * sizeof(int32_t), s));
     HIP_TRY(hipMemsetAsync(c_bub.ptr, 0xff, SZ * sizeof(int32_t), s));   // -1: not compiled
+    HIP_TRY(hipMemsetAsync(c_nbub.ptr, 0, SZ * sizeof(int32_t), s));
 
     // 1. counting pass, tier 0 then tier 1 for strings that overflow
     std::vector<uint8_t> ovf(SZ, 0);
@@ -288,6 +298,7 @@ int prepare(wfsa_dev* ctx, int level) {
         a.used = ctx->used.ptr;
         a.c_main = level >= 2 ? c_main.ptr : nullptr;
         a.c_bub = level >= 2 ? c_bub.ptr : nullptr;
+        a.c_nbub = level >= 2 ? c_nbub.ptr : nullptr;
         HIP_TRY(wfsa::launch_trav(wfsa::MODE_COUNT, a, trav_grid(ctx->cfg[t], ctx->n_cu, n), s));
         return WFSA_OK;
     };
@@ -324,16 +335,17 @@ int prepare(wfsa_dev* ctx, int level) {
     }
 
     // 2. groups of 64 strings with similar stream length
-    std::vector<int32_t> h_main(SZ, 0), h_bub(SZ, -1);
+    std::vector<int32_t> h_main(SZ, 0), h_bub(SZ, -1), h_nb(SZ, 0);
     if (S > 0) {
         HIP_TRY(c_main.download(h_main.data(), size_t(S), s));
         HIP_TRY(c_bub.download(h_bub.data(), size_t(S), s));
+        HIP_TRY(c_nbub.download(h_nb.data(), size_t(S), s));
         HIP_TRY(hipStreamSynchronize(s));
     }
     std::vector<int32_t> comp, fb[2];
     int32_t max_main = 0;
     for (int64_t i = 0; i < S; ++i) {
-        if (h_bub[size_t(i)] >= 0 && h_main[size_t(i)] > 0) {
+        if (h_bub[size_t(i)] >= 0) {
             comp.push_back(int32_t(i));
             max_main = std::max(max_main, h_main[size_t(i)]);
         } else {
@@ -353,6 +365,7 @@ int prepare(wfsa_dev* ctx, int level) {
     const int32_t G = int32_t((nc + kWave - 1) / kWave);
     std::vector<int64_t> g_base(size_t(G) + 1, 0), s_base(SZ, 0), b_base(SZ, 0);
     std::vector<int32_t> g_len(size_t(std::max(G, 1)), 0), l_str(size_t(G) * kWave, -1), l_len(size_t(G) * kWave, 0);
+    std::vector<int32_t> b_first(SZ, 0);
     int64_t words = 0;
     for (int32_t g = 0; g < G; ++g) {
         g_base[size_t(g)] = words;
@@ -368,20 +381,25 @@ int prepare(wfsa_dev* ctx, int level) {
         words += int64_t(kWave) * g_len[size_t(g)];
     }
     g_base[size_t(G)] = words;
-    int64_t bwords = 0;
+    int64_t bwords = 0, nbub = 0;
     for (int32_t str : comp) {
         b_base[size_t(str)] = bwords;
+        b_first[size_t(str)] = int32_t(nbub);
         bwords += h_bub[size_t(str)];
+        nbub += h_nb[size_t(str)];
     }
     if (bwords >= (int64_t(1) << 31) - 2) return fail(WFSA_ERR_CAPACITY, "bubble buffer exceeds 2^31 words");
 
     // 3. emit the streams (same tier as counted)
     HIP_TRY(ctx->stream_w.alloc(size_t(std::max<int64_t>(words, 1))));
-    HIP_TRY(ctx->bub.alloc(size_t(std::max<int64_t>(bwords, 1))));
+    HIP_TRY(ctx->bub.alloc(size_t(std::max<int64_t>(bwords, 2))));
+    HIP_TRY(ctx->bub_off.alloc(size_t(std::max<int64_t>(nbub, 1))));
     if (nc > 0) {
         DevBuf<int64_t> d_sb, d_bb;
+        DevBuf<int32_t> d_bf;
         HIP_TRY(d_sb.upload(s_base.data(), size_t(S), s));
         HIP_TRY(d_bb.upload(b_base.data(), size_t(S), s));
+        HIP_TRY(d_bf.upload(b_first.data(), size_t(S), s));
         std::vector<int32_t> el[2];
         for (int32_t str : comp) el[tier[size_t(str)]].push_back(str);
         DevBuf<int32_t> d_el[2];
@@ -395,6 +413,8 @@ int prepare(wfsa_dev* ctx, int level) {
             a.s_base = d_sb.ptr;
             a.bub = ctx->bub.ptr;
             a.b_base = d_bb.ptr;
+            a.b_first = d_bf.ptr;
+            a.bub_off = ctx->bub_off.ptr;
             HIP_TRY(wfsa::launch_trav(wfsa::MODE_EMIT, a, trav_grid(ctx->cfg[t], ctx->n_cu, int64_t(el[t].size())), s));
         }
         HIP_TRY(hipStreamSynchronize(s));
@@ -405,6 +425,59 @@ int prepare(wfsa_dev* ctx, int level) {
     HIP_TRY(ctx->l_len.upload(l_len.data(), l_len.size(), s));
     ctx->n_groups = G;
     ctx->n_compiled = nc;
+
+    // bubbles: largest first (similar lanes per wave), and the parameter ->
+    // contribution-slot index of their edges
+    ctx->n_bubbles = int32_t(nbub);
+    if (nbub > 0) {
+        std::vector<int32_t> h_bubbuf(static_cast<size_t>(bwords)), h_off(static_cast<size_t>(nbub));
+        HIP_TRY(ctx->bub.download(h_bubbuf.data(), size_t(bwords), s));
+        HIP_TRY(ctx->bub_off.download(h_off.data(), size_t(nbub), s));
+        HIP_TRY(hipStreamSynchronize(s));
+        std::vector<int64_t> cnt(size_t(wfsa::kMaxBubbleEdges) + 2, 0);
+        for (int32_t o : h_off) cnt[size_t(wfsa::kMaxBubbleEdges - (h_bubbuf[size_t(o)] >> 16))]++;
+        int64_t acc = 0;
+        for (auto& c : cnt) { const int64_t t = c; c = acc; acc += t; }
+        std::vector<int32_t> order(static_cast<size_t>(nbub));
+        for (int32_t o : h_off) order[size_t(cnt[size_t(wfsa::kMaxBubbleEdges - (h_bubbuf[size_t(o)] >> 16))]++)] = o;
+        HIP_TRY(ctx->bub_off.upload(order.data(), order.size(), s));
+        std::vector<int32_t> pc(size_t(ctx->n_params) + 1, 0);
+        for (int32_t o : h_off) {
+            const int edges = h_bubbuf[size_t(o)] >> 16;
+            for (int e = 0; e < edges; ++e) {
+                const int32_t g = h_bubbuf[size_t(o) + 2 + 2 * size_t(e)];
+                for (int32_t q = ctx->h_pptr[size_t(g)]; q < ctx->h_pptr[size_t(g) + 1]; ++q)
+                    pc[size_t(ctx->h_pidx[size_t(q)]) + 1]++;
+            }
+        }
+        for (size_t j = 1; j < pc.size(); ++j) pc[j] += pc[j - 1];
+        std::vector<int32_t> slot(size_t(pc.back())), fill(pc.begin(), pc.end() - 1);
+        for (int32_t o : h_off) {
+            const int edges = h_bubbuf[size_t(o)] >> 16;
+            for (int e = 0; e < edges; ++e) {
+                const int32_t g = h_bubbuf[size_t(o) + 2 + 2 * size_t(e)];
+                for (int32_t q = ctx->h_pptr[size_t(g)]; q < ctx->h_pptr[size_t(g) + 1]; ++q)
+                    slot[size_t(fill[size_t(ctx->h_pidx[size_t(q)])]++)] = (o >> 1) + 1 + e;
+            }
+        }
+        std::vector<int32_t> cparam, cptr;
+        for (int32_t j = 0; j < ctx->n_params; ++j)
+            for (int32_t b = pc[size_t(j)]; b < pc[size_t(j) + 1]; b += wfsa::kBubbleGradChunk) {
+                cparam.push_back(j);
+                cptr.push_back(b);
+            }
+        cptr.push_back(pc.back());
+        ctx->n_bg_chunks = int32_t(cparam.size());
+        HIP_TRY(ctx->bg_chunk_param.upload(cparam.data(), cparam.size(), s));
+        HIP_TRY(ctx->bg_chunk_ptr.upload(cptr.data(), cptr.size(), s));
+        HIP_TRY(ctx->bg_slot.upload(slot.data(), slot.size(), s));
+        HIP_TRY(ctx->contrib.alloc(size_t(bwords / 2) + 1));
+        HIP_TRY(hipMemsetAsync(ctx->contrib.ptr, 0, (size_t(bwords / 2) + 1) * sizeof(double), s));
+        ctx->b_grid = int(std::max<int64_t>(1, std::min<int64_t>((nbub + wfsa::kBubbleBlock - 1) / wfsa::kBubbleBlock,
+                                                                  int64_t(ctx->n_cu) * 8)));
+    } else {
+        ctx->b_grid = 0;
+    }
 
     // compiled kernel geometry: 8 waves per block, gradient in LDS when it fits
     const size_t grad_bytes = size_t(ctx->n_params) * sizeof(double);
@@ -423,7 +496,6 @@ int prepare(wfsa_dev* ctx, int level) {
     const int waves_per_block = kCompiledBlock / kWave;
     ctx->c_grid = int(std::max<int64_t>(1, std::min<int64_t>(int64_t(ctx->n_cu) * per_cu,
                                                              (int64_t(G) + waves_per_block - 1) / waves_per_block)));
-    HIP_TRY(ctx->scratch.alloc(size_t(ctx->c_grid) * kCompiledBlock * 2 * wfsa::kMaxBubbleNodes));
 
     // traversal fallback lists
     for (int t = 0; t < 2; ++t) {
@@ -431,7 +503,7 @@ int prepare(wfsa_dev* ctx, int level) {
         ctx->fall_grid[t] = fb[t].empty() ? 0 : trav_grid(ctx->cfg[t], ctx->n_cu, int64_t(fb[t].size()));
         if (!fb[t].empty()) HIP_TRY(ctx->fall[t].upload(fb[t].data(), fb[t].size(), s));
     }
-    const size_t waves = size_t(ctx->c_grid) * waves_per_block +
+    const size_t waves = size_t(ctx->c_grid) * waves_per_block + size_t(ctx->b_grid) * (wfsa::kBubbleBlock / kWave) +
                          size_t(ctx->fall_grid[0]) * size_t(ctx->cfg[0].waves_per_block) +
                          size_t(ctx->fall_grid[1]) * size_t(ctx->cfg[1].waves_per_block);
     HIP_TRY(ctx->ll_part.alloc(waves));
@@ -440,6 +512,7 @@ int prepare(wfsa_dev* ctx, int level) {
     ctx->stats.compiled_strings = nc;
     ctx->stats.fallback_strings = int64_t(fb[0].size() + fb[1].size());
     ctx->stats.stream_words = words;
+    ctx->stats.n_bubbles = nbub;
     ctx->stats.bubble_words = bwords;
     ctx->stats.tier1_strings = int32_t(l1.size());
     ctx->stats.waves_per_block = ctx->cfg[0].waves_per_block;
@@ -511,9 +584,12 @@ int wfsa_dev_load_model(wfsa_dev* ctx, const wfsa_model_desc* model) {
     HIP_TRY(ctx->x_ptr.upload(tm.x_ptr.data(), tm.x_ptr.size(), s));
     HIP_TRY(ctx->pptr.upload(pptr.data(), pptr.size(), s));
     HIP_TRY(ctx->pidx.upload(pidx.data(), pidx.size(), s));
+    ctx->h_pptr = pptr;
+    ctx->h_pidx = pidx;
     HIP_TRY(ctx->node_end_count.upload(tm.node_end_count.data(), tm.node_end_count.size(), s));
     HIP_TRY(ctx->lw.alloc(size_t(E + X)));
     HIP_TRY(ctx->ew.alloc(size_t(E + X)));
+    HIP_TRY(ctx->erec.alloc(size_t(E + X)));
     HIP_TRY(ctx->node_end.alloc(size_t(tm.n_nodes)));
     ctx->n_edges = E;
     ctx->n_end = X;
@@ -602,7 +678,7 @@ int wfsa_dev_objective_grad(wfsa_dev* ctx, const double* w_full, double* loglik,
         std::memcpy(ctx->pinned, w_full, size_t(np) * sizeof(double));
         HIP_TRY(hipMemcpyAsync(ctx->w_full.ptr, ctx->pinned, size_t(np) * sizeof(double), hipMemcpyHostToDevice, s));
     }
-    HIP_TRY(wfsa::launch_edge_weights(ctx->w_full.ptr, ctx->pptr.ptr, ctx->pidx.ptr, ctx->lw.ptr, ctx->ew.ptr,
+    HIP_TRY(wfsa::launch_edge_weights(ctx->w_full.ptr, ctx->pptr.ptr, ctx->pidx.ptr, ctx->lw.ptr, ctx->ew.ptr, ctx->erec.ptr,
                                       ctx->n_edges + ctx->n_end, s));
     const bool any_fall = ctx->n_fall[0] + ctx->n_fall[1] > 0;
     if (any_fall) HIP_TRY(wfsa::launch_node_end(ctx->x_ptr.ptr, ctx->ew.ptr + ctx->n_edges, ctx->node_end.ptr, ctx->n_nodes, s));
@@ -615,7 +691,6 @@ int wfsa_dev_objective_grad(wfsa_dev* ctx, const double* w_full, double* loglik,
         c.m = model_view(ctx);
         c.p = ctx->p.ptr;
         c.stream = ctx->stream_w.ptr;
-        c.bub = ctx->bub.ptr;
         c.g_base = ctx->g_base.ptr;
         c.g_len = ctx->g_len.ptr;
         c.l_str = ctx->l_str.ptr;
@@ -626,9 +701,24 @@ int wfsa_dev_objective_grad(wfsa_dev* ctx, const double* w_full, double* loglik,
         c.grad = ctx->out.ptr + 1;
         c.ll_part = ctx->ll_part.ptr;
         c.logq = logq ? ctx->logq.ptr : nullptr;
-        c.scratch = ctx->scratch.ptr;
         HIP_TRY(wfsa::launch_compiled(c, ctx->c_grid, kCompiledBlock, ctx->c_lds, s));
         wave_off += ctx->c_grid * (kCompiledBlock / kWave);
+    }
+    if (ctx->n_bubbles > 0) {
+        wfsa::BubbleArgs b{};
+        b.m = model_view(ctx);
+        b.p = ctx->p.ptr;
+        b.bub = ctx->bub.ptr;
+        b.bub_off = ctx->bub_off.ptr;
+        b.n_bubbles = ctx->n_bubbles;
+        b.contrib = ctx->contrib.ptr;
+        b.ll_part = ctx->ll_part.ptr + wave_off;
+        b.logq = logq ? ctx->logq.ptr : nullptr;
+        HIP_TRY(wfsa::launch_bubbles(b, ctx->b_grid, s));
+        wave_off += ctx->b_grid * (wfsa::kBubbleBlock / kWave);
+        wfsa::BubbleGradArgs bg{ctx->bg_chunk_param.ptr, ctx->bg_chunk_ptr.ptr, ctx->bg_slot.ptr, ctx->contrib.ptr,
+                                ctx->n_bg_chunks, ctx->out.ptr + 1};
+        HIP_TRY(wfsa::launch_bubble_grad(bg, s));
     }
     HIP_TRY(hipEventRecord(ctx->k1, s));
     for (int t = 0; t < 2; ++t) {

@@ -36,7 +36,7 @@ class DevStats(C.Structure):
     _fields_ = [
         ("n_strings", i64), ("total_symbols", i64), ("max_len", i32), ("n_nodes", i32),
         ("n_edges", i64), ("n_end_edges", i64), ("compiled_strings", i64), ("fallback_strings", i64),
-        ("stream_words", i64), ("bubble_words", i64), ("fb_launches", i64), ("fb_kernel_ms", dbl),
+        ("stream_words", i64), ("bubble_words", i64), ("n_bubbles", i64), ("fb_launches", i64), ("fb_kernel_ms", dbl),
         ("last_fb_kernel_ms", dbl), ("last_compiled_ms", dbl), ("last_call_ms", dbl),
         ("last_live_edges", i64), ("tier1_strings", i32), ("waves_per_block", i32), ("prepare_ms", dbl),
         ("compiled_kernel_ms", dbl),
