@@ -77,7 +77,8 @@ typedef struct {
     int64_t n_end_edges;
     int64_t compiled_strings;  /* served by the compiled-stream kernel      */
     int64_t fallback_strings;  /* served by the traversal kernel            */
-    int64_t stream_words;      /* compiled main-stream words (with padding) */
+    int64_t stream_words;      /* compiled main-stream words                */
+    int64_t stream_bytes;      /* main-stream bytes incl. chunk padding     */
     int64_t bubble_words;
     int64_t n_bubbles;         /* compiled bubbles (bubble kernel lanes)    */
     int64_t fb_launches;       /* objective_grad calls timed so far         */

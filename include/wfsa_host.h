@@ -84,6 +84,16 @@ int wfsa_learner_renormalize(wfsa_learner* l);                      /* Learner::
 int wfsa_learner_dump(wfsa_learner* l, wfsa_fsa* fsa, const char* path);
 int wfsa_learner_stats(wfsa_learner* l, wfsa_dev_stats* out);
 
+/* ---- host-only helpers (no device needed) -------------------------------- */
+/* Contiguous shard [begin, end) of rank `rank` out of `nranks` over strings
+ * with offsets off[0..n], balanced on total length (what Learner::BuildFrom
+ * keeps on each rank). */
+int wfsa_shard_range(const int64_t* off, int64_t n, int nranks, int rank, int64_t* begin, int64_t* end);
+/* Compile the automaton to the byte-step trellis the device walks, without a
+ * device: out = {nodes, byte edges, end edges, parameter-list entries}.
+ * Fails (WFSA_ERR_MODEL) e.g. on epsilon cycles. */
+int wfsa_trellis_compile_stats(const wfsa_model_desc* model, int64_t out[4]);
+
 /* ---- synthetic corpora (bench / tests) ---------------------------------- */
 /* family: N states, out-degree D (+ end), E distinct symbols per state out of
  * V printable bytes, stop probability 1/32 per step, lengths capped at

@@ -1,0 +1,97 @@
+"""The CPU oracle (oracle/wfsa_oracle.c) pinned against the reference's own
+recorded outputs (SURVEY.md Appendix A -> tests/golden/appendix_a.json) and
+its CTest outcomes; its two engines (path enumeration = the reference
+algorithm, dense trellis) checked against each other."""
+import json
+import os
+
+import numpy as np
+import pytest
+
+from conftest import DATA, ROOT
+
+GOLD = json.load(open(os.path.join(ROOT, "tests", "golden", "appendix_a.json")))
+CASES = [c for c in GOLD["cases"] if not c.get("empty")]
+EMPTY = [c for c in GOLD["cases"] if c.get("empty")]
+
+
+def _oracle(case, mode):
+    from oracle import Oracle
+    return Oracle.from_files(os.path.join(DATA, case["wfsa"] + ".wfsa"),
+                             os.path.join(DATA, case["corpus"] + ".corpus"), mode=mode)
+
+
+def _close(a, b, rel=1e-12, atol=1e-14):
+    return abs(a - b) <= max(atol, rel * max(abs(a), abs(b)))
+
+
+@pytest.mark.parametrize("mode", [0, 1], ids=["enum", "trellis"])
+@pytest.mark.parametrize("case", CASES, ids=lambda c: f"{c['wfsa']}+{c['corpus']}")
+def test_oracle_matches_appendix_a(case, mode):
+    o = _oracle(case, mode)
+    i = o.info
+    assert (i["n_strings"], i["n_paths"], i["n_params"], i["n_constraints"], bool(i["unique"])) == \
+        (case["strings"], case["paths"], case["n"], case["k"], case["unique"])
+    assert _close(i["plogp"], case["plogp"])
+    o.qn_init(7)
+    kl0, ll0 = o.objective_grad()
+    assert _close(kl0, case["kl0"], rel=1e-12)
+    assert _close(ll0, case["ll0"])
+    assert _close(float(np.linalg.norm(o.grad())), case["grad0_norm"])
+    rows = _oracle(case, mode).qn_run(flags=7, epochs=20)
+    assert len(rows) == case["epochs"]
+    assert _close(rows[-1][0], case["kl_final"], rel=1e-11, atol=1e-13)
+
+
+@pytest.mark.parametrize("case", EMPTY, ids=lambda c: f"{c['wfsa']}+{c['corpus']}")
+def test_oracle_empty_cases(case):
+    o = _oracle(case, 0)
+    assert o.info["n_strings"] == case["strings"]
+    assert o.info["n_params"] == 0
+
+
+def test_oracle_talk_per_string():
+    case = next(c for c in CASES if c["wfsa"] == "talk")
+    o = _oracle(case, 0)
+    o.qn_init(7)
+    o.objective_grad()
+    np.testing.assert_allclose(o.p(), case["p"], rtol=1e-15)
+    np.testing.assert_allclose(o.logq(), case["logq"], rtol=1e-14)
+    # q(talk) = 1/2 * 1/3 + 1/2 * 1/2 = 5/12 (by hand)
+    assert _close(o.logq()[0], np.log(5 / 12))
+
+
+@pytest.mark.parametrize("seed", [1, 2, 3])
+def test_enum_and_trellis_engines_agree(seed):
+    """the reference algorithm (path enumeration) and the trellis agree on
+    small ambiguous automata at random weights"""
+    import wfsa_amd as W
+    from oracle import ENUM, TRELLIS, Oracle
+    syn = W.Synthetic(n_states=24, degree=4, vocab=5, emissions=2, n_strings=300, max_len=9, seed=seed)
+    sym, off, wt = syn.corpus()
+    oe = Oracle.from_arrays(syn.wfsa_text, sym, off, wt, mode=ENUM, max_paths=10_000_000)
+    ot = Oracle.from_arrays(syn.wfsa_text, sym, off, wt, mode=TRELLIS)
+    assert oe.info["n_paths"] == ot.info["n_paths"]
+    assert oe.info["n_params"] == ot.info["n_params"]
+    x = np.random.default_rng(seed).normal(-1.0, 0.5, size=oe.n)
+    oe.set_x(x)
+    ot.set_x(x)
+    kle, _ = oe.objective_grad()
+    klt, _ = ot.objective_grad()
+    assert _close(kle, klt, rel=1e-11)
+    np.testing.assert_allclose(oe.logq(), ot.logq(), rtol=1e-12)
+    np.testing.assert_allclose(oe.grad(), ot.grad(), rtol=1e-10, atol=1e-15)
+
+
+def test_reference_ctest_outcomes_hold_for_oracle():
+    """CMakeLists.txt:34-57: test1 and test_talk2 fail (empty automaton), the
+    other pairs run; the oracle agrees on which inputs are empty."""
+    exit_codes = GOLD["ctest_exit_codes"]
+    pairs = {"test1": ("test", "test"), "testlist": ("test.list", "test"), "test2": ("test2", "test"),
+             "test3": ("test3", "test"), "test4": ("test4", "test"), "test_loop": ("test.loop", "test"),
+             "test_talk": ("talk", "talk"), "test_talk2": ("talk", "test")}
+    from oracle import Oracle
+    for name, (a, c) in pairs.items():
+        o = Oracle.from_files(os.path.join(DATA, a + ".wfsa"), os.path.join(DATA, c + ".corpus"))
+        empty = o.info["n_params"] == 0 or o.info["n_strings"] == 0
+        assert empty == (exit_codes[name] == 1), name

@@ -11,6 +11,18 @@ void ThrowOnDevError(int rc, const char* what) {
     if (rc != WFSA_OK) throw LearnerError(what, " failed (", rc, "): ", wfsa_dev_last_error());
 }
 
+ShardRange shard_range(const int64_t* off, int64_t n, int nranks, int rank) {
+    const int64_t total = off[n];
+    auto bound = [&](int r) -> int64_t {
+        if (r <= 0) return 0;
+        if (r >= nranks) return n;
+        const long double thr = (long double)total * r / nranks;
+        return int64_t(std::lower_bound(off, off + n, int64_t(std::ceil(thr))) - off);
+    };
+    const int64_t b = bound(rank);
+    return ShardRange{b, std::max(b, bound(rank + 1))};
+}
+
 Learner::Learner() {}
 
 Learner::~Learner() {
@@ -97,16 +109,9 @@ void Learner::BuildFromPacked(const Fsa& fsa, const uint8_t* sym, const int64_t*
 // corpus order.
 void Learner::BuildPaths(const Fsa& fsa, const uint8_t* sym, const int64_t* off, const double* weights, int64_t n) {
     EnsureDevice();
-    // contiguous shard [b, e) of this rank, balanced on total length
-    const int64_t total = off[n];
-    auto bound = [&](int r) -> int64_t {
-        if (r <= 0) return 0;
-        if (r >= nranks) return n;
-        const long double thr = (long double)total * r / nranks;
-        return int64_t(std::lower_bound(off, off + n, int64_t(std::ceil(thr))) - off);
-    };
-    shard_begin = bound(rank);
-    shard_end = std::max(shard_begin, bound(rank + 1));
+    const ShardRange sr = shard_range(off, n, nranks, rank);
+    shard_begin = sr.begin;
+    shard_end = sr.end;
     const int64_t ln = shard_end - shard_begin;
     std::vector<int64_t> loff(size_t(ln) + 1);
     for (int64_t s = 0; s <= ln; ++s) loff[size_t(s)] = off[shard_begin + s] - off[shard_begin];

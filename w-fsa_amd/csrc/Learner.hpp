@@ -149,4 +149,11 @@ private:
 
 void ThrowOnDevError(int rc, const char* what);
 
+// Contiguous shard of `rank` over strings with offsets off[0..n], balanced on
+// total length: [begin, end).
+struct ShardRange {
+    int64_t begin, end;
+};
+ShardRange shard_range(const int64_t* off, int64_t n, int nranks, int rank);
+
 }  // namespace wfsa

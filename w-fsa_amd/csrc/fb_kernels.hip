@@ -124,13 +124,35 @@ struct Slab {
     int* slot;
 };
 
+// Main-stream word of a trivial edge g (posterior 1): an edge with one
+// parameter is stored as that parameter's index (log-weight w[j], gradient
+// slot j); an edge without parameters (weight log 1) is not stored; an edge
+// with several parameters (epsilon composites) by its multi-edge index.
+__device__ __forceinline__ bool put_trivial(const ModelView& m, int g, bool write, void* stream, int wide,
+                                            int64_t s_base, int& n_main) {
+    const int np = m.pptr[g + 1] - m.pptr[g];
+    if (np == 0) return false;
+    if (write) {
+        const int k = n_main;
+        if (wide) {
+            const int v = np == 1 ? m.pidx[m.pptr[g]] : -(g + 2);
+            static_cast<int32_t*>(stream)[s_base + int64_t(k >> 2) * 256 + (k & 3)] = v;
+        } else {
+            const int v = np == 1 ? m.pidx[m.pptr[g]] : 0x8000 + m.multi_of[g];
+            static_cast<uint16_t*>(stream)[s_base + int64_t(k >> 3) * 512 + (k & 7)] = uint16_t(v);
+        }
+    }
+    ++n_main;
+    return true;
+}
+
 // Compiled stream of one string from its counted trellis (lane 0 only;
 // beta > 0 marks live entries).  Trivial segments go to the main stream,
 // bubbles to the bubble buffer.  Returns false when a bubble exceeds the
 // kernel limits; the string then stays on the traversal path.
 template <bool WRITE>
 __device__ bool compile_walk(const Slab& sl, const ModelView& m, int L, int sidx, int& n_main, int& n_bub,
-                             int& n_nb, int32_t* stream, int64_t s_base, int32_t* bub, int64_t b_base,
+                             int& n_nb, void* stream, int wide, int64_t s_base, int32_t* bub, int64_t b_base,
                              int32_t* bub_off, int32_t b_first) {
     long long* lid = reinterpret_cast<long long*>(sl.alpha);   // alpha is dead in counting mode
     n_main = 0;
@@ -152,8 +174,7 @@ __device__ bool compile_walk(const Slab& sl, const ModelView& m, int L, int sidx
             for (int e = sl.epos[a]; e < sl.epos[a + 1]; ++e)
                 if (sl.beta[sl.e_dst[e]] > 0.0) { ++cnt; ge = e; }
             if (cnt == 1) {
-                if (WRITE) stream[s_base + int64_t(kWave) * n_main] = sl.e_g[ge];
-                ++n_main;
+                put_trivial(m, sl.e_g[ge], WRITE, stream, wide, s_base, n_main);
                 a = b;
                 fa = fbn;
                 continue;
@@ -162,8 +183,7 @@ __device__ bool compile_walk(const Slab& sl, const ModelView& m, int L, int sidx
         if (to_end && a == L) {
             const int S = sl.state[fa];
             if (m.x_ptr[S + 1] - m.x_ptr[S] == 1) {
-                if (WRITE) stream[s_base + int64_t(kWave) * n_main] = m.n_edges + m.x_ptr[S];
-                ++n_main;
+                put_trivial(m, m.n_edges + m.x_ptr[S], WRITE, stream, wide, s_base, n_main);
                 break;
             }
         }
@@ -440,10 +460,10 @@ __global__ __launch_bounds__(256) void trav_kernel(TravArgs a) {
                 int n_main = 0, n_bub = 0, n_nb = 0;
                 bool ok;
                 if (MODE == MODE_EMIT)
-                    ok = compile_walk<true>(sl, m, L, sidx, n_main, n_bub, n_nb, a.stream, a.s_base[sidx], a.bub,
-                                            a.b_base[sidx], a.bub_off, a.b_first[sidx]);
+                    ok = compile_walk<true>(sl, m, L, sidx, n_main, n_bub, n_nb, a.stream, a.wide, a.s_base[sidx],
+                                            a.bub, a.b_base[sidx], a.bub_off, a.b_first[sidx]);
                 else
-                    ok = compile_walk<false>(sl, m, L, sidx, n_main, n_bub, n_nb, nullptr, 0, nullptr, 0, nullptr, 0);
+                    ok = compile_walk<false>(sl, m, L, sidx, n_main, n_bub, n_nb, nullptr, 0, 0, nullptr, 0, nullptr, 0);
                 if (MODE == MODE_COUNT) {
                     a.c_main[sidx] = ok ? n_main : 0;
                     a.c_bub[sidx] = ok ? n_bub : -1;
@@ -461,62 +481,77 @@ __global__ __launch_bounds__(256) void trav_kernel(TravArgs a) {
 }
 
 // Main streams: one lane per string, 64 strings of similar stream length per
-// wavefront, trivial words only.  Every word is an edge on all of the
-// string's paths: log q accumulates its log-weight, its parameters get -p_s.
+// wavefront.  Every word is an edge on all of the string's paths (posterior
+// 1): log q accumulates its log-weight and its parameters get -p_s.  A
+// single-parameter word j reads w[j] and adds to gradient slot j; with
+// TABLES == 2 both live in LDS (w staged per block), so the only global
+// traffic is the stream itself, one 16-byte chunk per lane per load (the next
+// chunk in flight while the current one is applied).  Multi-parameter words
+// (rare) read the edge's log-weight and parameter list from global memory.
 // Groups are dealt to waves in snake order (longest first) to balance them.
-template <bool LDS_GRAD>
-__global__ __launch_bounds__(512) void fbc_kernel(CompiledArgs a) {
-    extern __shared__ __attribute__((aligned(16))) double gacc[];
+template <int TABLES, bool WIDE>   // TABLES 2: w + grad in LDS, 1: grad in LDS, 0: none
+__global__ __launch_bounds__(1024) void fbc_kernel(CompiledArgs a) {
+    extern __shared__ __attribute__((aligned(16))) double lds[];
+    double* gacc = lds;                 // [n_params] when TABLES >= 1
+    double* wl = lds + a.n_params;      // [n_params] when TABLES == 2
     const int lane = lane_id();
     const int wpb = int(blockDim.x) / kWave;
     const int gw = int(blockIdx.x) * wpb + int(threadIdx.x) / kWave;
     const int nw = int(gridDim.x) * wpb;
-    if (LDS_GRAD) {
-        for (int j = int(threadIdx.x); j < a.n_params; j += int(blockDim.x)) gacc[j] = 0.0;
+    if (TABLES >= 1) {
+        for (int j = int(threadIdx.x); j < a.n_params; j += int(blockDim.x)) {
+            gacc[j] = 0.0;
+            if (TABLES == 2) wl[j] = a.w[j];
+        }
         __syncthreads();
     }
-    const EdgeRec* erec = a.m.erec;
+    const double* wsrc = TABLES == 2 ? wl : a.w;
+    constexpr int PER = WIDE ? 4 : 8;   // words per 16-byte chunk
+    const uint4 pad = make_uint4(0xffffffffu, 0xffffffffu, 0xffffffffu, 0xffffffffu);
     double ll_acc = 0.0;
-    constexpr int U = 8;   // stream words in flight per lane
+
+    auto apply = [&](int j_single, int g_multi, double p, double& acc) {
+        if (j_single >= 0) {
+            acc += wsrc[j_single];
+            if (TABLES >= 1) block_add(&gacc[j_single], -p);
+            else global_add(&a.grad[j_single], -p);
+        } else if (g_multi >= 0) {
+            acc += a.m.lw[g_multi];
+            for (int q = a.m.pptr[g_multi]; q < a.m.pptr[g_multi + 1]; ++q) {
+                if (TABLES >= 1) block_add(&gacc[a.m.pidx[q]], -p);
+                else global_add(&a.grad[a.m.pidx[q]], -p);
+            }
+        }
+    };
 
     for (int round = 0;; ++round) {
         const int grp = round * nw + ((round & 1) ? (nw - 1 - gw) : gw);
         if (grp >= a.n_groups) break;
         const int s = a.l_str[grp * kWave + lane];
-        const int len = a.l_len[grp * kWave + lane];
-        const int glen = a.g_len[grp];
-        const int32_t* st = a.stream + a.g_base[grp] + lane;
+        const int nch = (a.l_len[grp * kWave + lane] + PER - 1) / PER;
+        const int gch = a.g_len[grp];
+        const uint4* st = a.stream + a.g_base[grp] + lane;
         const double p = s >= 0 ? a.p[s] : 0.0;
         double acc = 0.0;
-        int w[U];
+        uint4 cur = nch > 0 ? st[0] : pad;
+        for (int c = 0; c < gch; ++c) {
+            const uint4 nxt = (c + 1 < nch) ? st[int64_t(kWave) * (c + 1)] : pad;
+            const uint32_t v[4] = {cur.x, cur.y, cur.z, cur.w};
 #pragma unroll
-        for (int u = 0; u < U; ++u) w[u] = (u < len) ? st[int64_t(kWave) * u] : -1;
-        for (int k0 = 0; k0 < glen; k0 += U) {
-            EdgeRec r[U];
+            for (int i = 0; i < 4; ++i) {
+                if (WIDE) {
+                    const int x = int(v[i]);
+                    apply(x, x < -1 ? -(x + 2) : -1, p, acc);
+                } else {
 #pragma unroll
-            for (int u = 0; u < U; ++u) r[u] = w[u] >= 0 ? erec[w[u]] : EdgeRec{0.0, 0, 0};
-            // next chunk's words are in flight while this chunk is applied
-            int wn[U];
-#pragma unroll
-            for (int u = 0; u < U; ++u) {
-                const int k = k0 + U + u;
-                wn[u] = (k < len) ? st[int64_t(kWave) * k] : -1;
-            }
-#pragma unroll
-            for (int u = 0; u < U; ++u) {
-                acc += r[u].lw;
-                if (r[u].np == 1) {
-                    if (LDS_GRAD) block_add(&gacc[r[u].p0], -p);
-                    else global_add(&a.grad[r[u].p0], -p);
-                } else if (r[u].np > 1) {
-                    for (int q = a.m.pptr[w[u]]; q < a.m.pptr[w[u] + 1]; ++q) {
-                        if (LDS_GRAD) block_add(&gacc[a.m.pidx[q]], -p);
-                        else global_add(&a.grad[a.m.pidx[q]], -p);
+                    for (int h = 0; h < 2; ++h) {
+                        const int x = int((v[i] >> (16 * h)) & 0xffffu);
+                        if (x < 0x8000) apply(x, -1, p, acc);
+                        else if (x != 0xffff) apply(-1, a.m.multi_edge[x - 0x8000], p, acc);
                     }
                 }
             }
-#pragma unroll
-            for (int u = 0; u < U; ++u) w[u] = wn[u];
+            cur = nxt;
         }
         if (s >= 0) {
             ll_acc += p * acc;
@@ -525,7 +560,7 @@ __global__ __launch_bounds__(512) void fbc_kernel(CompiledArgs a) {
     }
     ll_acc = wave_sum(ll_acc);
     if (lane == 0) a.ll_part[gw] = ll_acc;
-    if (LDS_GRAD) {
+    if (TABLES >= 1) {
         __syncthreads();
         for (int j = int(threadIdx.x); j < a.n_params; j += int(blockDim.x)) {
             const double v = gacc[j];
@@ -635,8 +670,12 @@ hipError_t configure_kernels(int max_dynamic_lds) {
     const void* fns[] = {reinterpret_cast<const void*>(&trav_kernel<MODE_WEIGHTED>),
                          reinterpret_cast<const void*>(&trav_kernel<MODE_COUNT>),
                          reinterpret_cast<const void*>(&trav_kernel<MODE_EMIT>),
-                         reinterpret_cast<const void*>(&fbc_kernel<true>),
-                         reinterpret_cast<const void*>(&fbc_kernel<false>)};
+                         reinterpret_cast<const void*>(&fbc_kernel<0, false>),
+                         reinterpret_cast<const void*>(&fbc_kernel<1, false>),
+                         reinterpret_cast<const void*>(&fbc_kernel<2, false>),
+                         reinterpret_cast<const void*>(&fbc_kernel<0, true>),
+                         reinterpret_cast<const void*>(&fbc_kernel<1, true>),
+                         reinterpret_cast<const void*>(&fbc_kernel<2, true>)};
     for (const void* f : fns) {
         hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, max_dynamic_lds);
         if (e != hipSuccess) return e;
@@ -662,10 +701,16 @@ hipError_t launch_trav(TravMode mode, const TravArgs& a, int grid, hipStream_t s
 }
 
 hipError_t launch_compiled(const CompiledArgs& a, int grid, int block, size_t lds, hipStream_t stream) {
-    if (a.grad_in_lds)
-        hipLaunchKernelGGL(fbc_kernel<true>, dim3(unsigned(grid)), dim3(unsigned(block)), lds, stream, a);
-    else
-        hipLaunchKernelGGL(fbc_kernel<false>, dim3(unsigned(grid)), dim3(unsigned(block)), 0, stream, a);
+    const dim3 g{unsigned(grid), 1, 1}, b{unsigned(block), 1, 1};
+    const int key = a.tables * 2 + (a.wide ? 1 : 0);
+    switch (key) {
+        case 4: hipLaunchKernelGGL((fbc_kernel<2, false>), g, b, lds, stream, a); break;
+        case 5: hipLaunchKernelGGL((fbc_kernel<2, true>), g, b, lds, stream, a); break;
+        case 2: hipLaunchKernelGGL((fbc_kernel<1, false>), g, b, lds, stream, a); break;
+        case 3: hipLaunchKernelGGL((fbc_kernel<1, true>), g, b, lds, stream, a); break;
+        case 1: hipLaunchKernelGGL((fbc_kernel<0, true>), g, b, 0, stream, a); break;
+        default: hipLaunchKernelGGL((fbc_kernel<0, false>), g, b, 0, stream, a); break;
+    }
     return hipGetLastError();
 }
 

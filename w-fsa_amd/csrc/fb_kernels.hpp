@@ -44,6 +44,8 @@ struct ModelView {
     const EdgeRec* erec;     // [E+X] log-weight + parameters, per iteration
     const double* node_end;  // [n_nodes] sum of the node's end-edge weights
     const double* node_end_count;  // [n_nodes] number of end edges (counting mode)
+    const int32_t* multi_of;       // [E+X] index among multi-parameter edges, or -1
+    const int32_t* multi_edge;     // [n_multi] combined edge of each multi-parameter edge
     int32_t n_nodes;
     int32_t start;
     int32_t n_edges;         // E
@@ -105,8 +107,9 @@ struct TravArgs {
     int32_t* c_bub;          // [S] compiled bubble words (-1: does not compile)
     int32_t* c_nbub;         // [S] number of bubbles
     // emit mode
-    int32_t* stream;         // interleaved main streams
-    const int64_t* s_base;   // [S] word index of the string's first main word
+    void* stream;            // interleaved main streams (see CompiledArgs)
+    int32_t wide;            // 32-bit words (else 16-bit)
+    const int64_t* s_base;   // [S] element index of the string's first main word
     int32_t* bub;            // bubble buffer
     const int64_t* b_base;   // [S] word index of the string's first bubble word
     const int32_t* b_first;  // [S] ordinal of the string's first bubble
@@ -116,22 +119,29 @@ struct TravArgs {
 };
 
 // Compiled streams of the per-iteration kernels.
-//   main stream: only "trivial" words (edge ids whose posterior is 1),
-//     interleaved: word k of lane l of group g at g_base[g] + 64 k + l;
+//   main stream: only "trivial" words (edges whose posterior is 1).  Narrow
+//     (16-bit) words: j < 0x8000 a single-parameter edge with parameter j,
+//     0x8000 + m the m-th multi-parameter edge, 0xFFFF padding.  Wide (32-bit)
+//     words: j >= 0 a parameter, -(g+2) multi-parameter combined edge g, -1
+//     padding.  Each lane's words are cut into 16-byte chunks (8 narrow / 4
+//     wide words); chunk c of lane l of group g sits at chunk index
+//     g_base[g] + 64 c + l, so one wavefront reads 1 KiB per load.
 //   bubble buffer: per bubble [nodes | edges << 16, string, (edge id,
 //     src | dst << 16) x edges], always at an even word offset, so edge e of
 //     the bubble at offset o owns contribution slot o / 2 + 1 + e.
 struct CompiledArgs {
     ModelView m;
     const double* p;         // [S]
-    const int32_t* stream;
-    const int64_t* g_base;   // [G]
-    const int32_t* g_len;    // [G] longest stream of the group (its first lane)
+    const uint4* stream;     // 16-byte chunks
+    const int64_t* g_base;   // [G] first chunk of the group
+    const int32_t* g_len;    // [G] chunks of the group's longest lane (its first)
     const int32_t* l_str;    // [64 G] string of each lane, -1 = padding
-    const int32_t* l_len;    // [64 G]
+    const int32_t* l_len;    // [64 G] words of each lane
     int32_t n_groups;
     int32_t n_params;
-    int32_t grad_in_lds;     // 1: per-block LDS accumulator of n_params doubles
+    int32_t tables;          // 2: w and grad staged in LDS, 1: grad in LDS, 0: global
+    int32_t wide;
+    const double* w;         // [n_params] w_full (GetWeight form)
     double* grad;            // [n_params]
     double* ll_part;         // [waves in grid]
     double* logq;            // [S] or null

@@ -13,6 +13,7 @@
 #include "Learner.hpp"
 #include "QuasiNewtonLearner.hpp"
 #include "synth.hpp"
+#include "trellis_model.hpp"
 
 using namespace wfsa;
 
@@ -333,6 +334,29 @@ int wfsa_learner_stats(wfsa_learner* l, wfsa_dev_stats* out) {
         return WFSA_ERR_ARG;
     }
     return wfsa_dev_get_stats(l->qn->Device(), out);
+}
+
+int wfsa_shard_range(const int64_t* off, int64_t n, int nranks, int rank, int64_t* begin, int64_t* end) {
+    if (!off || !begin || !end || n < 0 || nranks < 1 || rank < 0 || rank >= nranks) return null_arg("shard arguments");
+    const ShardRange r = shard_range(off, n, nranks, rank);
+    *begin = r.begin;
+    *end = r.end;
+    return WFSA_OK;
+}
+
+int wfsa_trellis_compile_stats(const wfsa_model_desc* model, int64_t out[4]) {
+    if (!model || !out) return null_arg("model/out");
+    TrellisModel tm;
+    const std::string err = compile_trellis_model(*model, tm);
+    if (!err.empty()) {
+        g_host_error = "automaton rejected: " + err;
+        return WFSA_ERR_MODEL;
+    }
+    out[0] = tm.n_nodes;
+    out[1] = int64_t(tm.o_byte.size());
+    out[2] = int64_t(tm.x_pptr.size()) - 1;
+    out[3] = int64_t(tm.o_pidx.size() + tm.x_pidx.size());
+    return WFSA_OK;
 }
 
 int wfsa_synth_make(int32_t n_states, int32_t degree, int32_t vocab, int32_t emissions, int32_t dense,

@@ -111,6 +111,8 @@ struct wfsa_dev {
     DevBuf<int32_t> o_ptr, o_dst, x_ptr, pptr, pidx;
     DevBuf<uint8_t> o_byte;
     DevBuf<double> lw, ew, node_end, node_end_count;
+    DevBuf<int32_t> multi_of, multi_edge;   // multi-parameter combined edges
+    int32_t n_multi = 0;
     DevBuf<wfsa::EdgeRec> erec;
 
     // corpus
@@ -136,9 +138,11 @@ struct wfsa_dev {
     // compiled streams
     int32_t n_groups = 0;
     int64_t n_compiled = 0;
-    DevBuf<int32_t> stream_w, bub, g_len, l_str, l_len;
+    DevBuf<uint4> stream_w;   // 16-byte chunks
+    int wide = 0;             // 32-bit stream words
+    DevBuf<int32_t> bub, g_len, l_str, l_len;
     DevBuf<int64_t> g_base;
-    int c_grid = 0, c_lds_grad = 0;
+    int c_grid = 0, c_tables = 0;
     // bubbles
     int32_t n_bubbles = 0;
     int b_grid = 0;
@@ -221,6 +225,8 @@ wfsa::ModelView model_view(wfsa_dev* ctx) {
     m.erec = ctx->erec.ptr;
     m.node_end = ctx->node_end.ptr;
     m.node_end_count = ctx->node_end_count.ptr;
+    m.multi_of = ctx->multi_of.ptr;
+    m.multi_edge = ctx->multi_edge.ptr;
     m.n_nodes = ctx->n_nodes;
     m.start = ctx->start;
     m.n_edges = int32_t(ctx->n_edges);
@@ -366,21 +372,25 @@ int prepare(wfsa_dev* ctx, int level) {
     std::vector<int64_t> g_base(size_t(G) + 1, 0), s_base(SZ, 0), b_base(SZ, 0);
     std::vector<int32_t> g_len(size_t(std::max(G, 1)), 0), l_str(size_t(G) * kWave, -1), l_len(size_t(G) * kWave, 0);
     std::vector<int32_t> b_first(SZ, 0);
-    int64_t words = 0;
+    // 16-byte chunks of 8 narrow / 4 wide words; chunk c of lane l at
+    // g_base + 64 c + l (chunk units); s_base in word (element) units
+    const int per = ctx->wide ? 4 : 8;
+    int64_t chunks = 0, words = 0;
     for (int32_t g = 0; g < G; ++g) {
-        g_base[size_t(g)] = words;
-        g_len[size_t(g)] = h_main[size_t(comp[size_t(g) * kWave])];
+        g_base[size_t(g)] = chunks;
+        g_len[size_t(g)] = (h_main[size_t(comp[size_t(g) * kWave])] + per - 1) / per;
         for (int l = 0; l < kWave; ++l) {
             const int64_t k = int64_t(g) * kWave + l;
             if (k >= nc) break;
             const int32_t str = comp[size_t(k)];
             l_str[size_t(k)] = str;
             l_len[size_t(k)] = h_main[size_t(str)];
-            s_base[size_t(str)] = words + l;
+            s_base[size_t(str)] = (chunks + l) * per;
+            words += h_main[size_t(str)];
         }
-        words += int64_t(kWave) * g_len[size_t(g)];
+        chunks += int64_t(kWave) * g_len[size_t(g)];
     }
-    g_base[size_t(G)] = words;
+    g_base[size_t(G)] = chunks;
     int64_t bwords = 0, nbub = 0;
     for (int32_t str : comp) {
         b_base[size_t(str)] = bwords;
@@ -391,7 +401,8 @@ int prepare(wfsa_dev* ctx, int level) {
     if (bwords >= (int64_t(1) << 31) - 2) return fail(WFSA_ERR_CAPACITY, "bubble buffer exceeds 2^31 words");
 
     // 3. emit the streams (same tier as counted)
-    HIP_TRY(ctx->stream_w.alloc(size_t(std::max<int64_t>(words, 1))));
+    HIP_TRY(ctx->stream_w.alloc(size_t(std::max<int64_t>(chunks, 1))));
+    HIP_TRY(hipMemsetAsync(ctx->stream_w.ptr, 0xff, size_t(std::max<int64_t>(chunks, 1)) * sizeof(uint4), s));
     HIP_TRY(ctx->bub.alloc(size_t(std::max<int64_t>(bwords, 2))));
     HIP_TRY(ctx->bub_off.alloc(size_t(std::max<int64_t>(nbub, 1))));
     if (nc > 0) {
@@ -410,6 +421,7 @@ int prepare(wfsa_dev* ctx, int level) {
             a.list = d_el[t].ptr;
             a.n_list = int32_t(el[t].size());
             a.stream = ctx->stream_w.ptr;
+            a.wide = ctx->wide;
             a.s_base = d_sb.ptr;
             a.bub = ctx->bub.ptr;
             a.b_base = d_bb.ptr;
@@ -479,21 +491,21 @@ int prepare(wfsa_dev* ctx, int level) {
         ctx->b_grid = 0;
     }
 
-    // compiled kernel geometry: 8 waves per block, gradient in LDS when it fits
-    const size_t grad_bytes = size_t(ctx->n_params) * sizeof(double);
-    int per_cu;
-    if (grad_bytes <= size_t(kLdsPerCu / 2 - 1024)) {
-        per_cu = 2;
-        ctx->c_lds_grad = 1;
-    } else if (grad_bytes <= size_t(kLdsPerCu - 1024)) {
-        per_cu = 1;
-        ctx->c_lds_grad = 1;
+    // compiled kernel geometry: 16 waves per block, one block per CU; w and
+    // the gradient staged in LDS when both fit, else the gradient alone
+    const size_t table_bytes = size_t(ctx->n_params) * sizeof(double);
+    if (2 * table_bytes <= size_t(kLdsPerCu - 1024)) {
+        ctx->c_tables = 2;
+        ctx->c_lds = 2 * table_bytes;
+    } else if (table_bytes <= size_t(kLdsPerCu - 1024)) {
+        ctx->c_tables = 1;
+        ctx->c_lds = table_bytes;
     } else {
-        per_cu = 4;
-        ctx->c_lds_grad = 0;
+        ctx->c_tables = 0;
+        ctx->c_lds = 0;
     }
-    ctx->c_lds = ctx->c_lds_grad ? grad_bytes : 0;
     const int waves_per_block = kCompiledBlock / kWave;
+    const int per_cu = ctx->c_tables ? 1 : 2;
     ctx->c_grid = int(std::max<int64_t>(1, std::min<int64_t>(int64_t(ctx->n_cu) * per_cu,
                                                              (int64_t(G) + waves_per_block - 1) / waves_per_block)));
 
@@ -512,6 +524,7 @@ int prepare(wfsa_dev* ctx, int level) {
     ctx->stats.compiled_strings = nc;
     ctx->stats.fallback_strings = int64_t(fb[0].size() + fb[1].size());
     ctx->stats.stream_words = words;
+    ctx->stats.stream_bytes = chunks * 16;
     ctx->stats.n_bubbles = nbub;
     ctx->stats.bubble_words = bwords;
     ctx->stats.tier1_strings = int32_t(l1.size());
@@ -586,6 +599,19 @@ int wfsa_dev_load_model(wfsa_dev* ctx, const wfsa_model_desc* model) {
     HIP_TRY(ctx->pidx.upload(pidx.data(), pidx.size(), s));
     ctx->h_pptr = pptr;
     ctx->h_pidx = pidx;
+    {
+        std::vector<int32_t> mof(size_t(E + X), -1), medge;
+        for (int64_t g = 0; g < E + X; ++g)
+            if (pptr[size_t(g) + 1] - pptr[size_t(g)] >= 2) {
+                mof[size_t(g)] = int32_t(medge.size());
+                medge.push_back(int32_t(g));
+            }
+        ctx->n_multi = int32_t(medge.size());
+        HIP_TRY(ctx->multi_of.upload(mof.data(), mof.size(), s));
+        HIP_TRY(ctx->multi_edge.upload(medge.data(), medge.size(), s));
+    }
+    // narrow (16-bit) stream words unless parameters or multi edges overflow them
+    ctx->wide = (tm.n_params >= 0x8000 || ctx->n_multi >= 0x7fff) ? 1 : 0;
     HIP_TRY(ctx->node_end_count.upload(tm.node_end_count.data(), tm.node_end_count.size(), s));
     HIP_TRY(ctx->lw.alloc(size_t(E + X)));
     HIP_TRY(ctx->ew.alloc(size_t(E + X)));
@@ -691,13 +717,15 @@ int wfsa_dev_objective_grad(wfsa_dev* ctx, const double* w_full, double* loglik,
         c.m = model_view(ctx);
         c.p = ctx->p.ptr;
         c.stream = ctx->stream_w.ptr;
+        c.wide = ctx->wide;
         c.g_base = ctx->g_base.ptr;
         c.g_len = ctx->g_len.ptr;
         c.l_str = ctx->l_str.ptr;
         c.l_len = ctx->l_len.ptr;
         c.n_groups = ctx->n_groups;
         c.n_params = np;
-        c.grad_in_lds = ctx->c_lds_grad;
+        c.tables = ctx->c_tables;
+        c.w = ctx->w_full.ptr;
         c.grad = ctx->out.ptr + 1;
         c.ll_part = ctx->ll_part.ptr;
         c.logq = logq ? ctx->logq.ptr : nullptr;

@@ -13,11 +13,29 @@ import numpy as np
 from . import _lib
 from ._lib import WfsaError, check_dev, check_host, load
 
-__all__ = ["Fsa", "Corpus", "QuasiNewtonLearner", "Device", "Synthetic", "WfsaError", "load"]
-
 
 def _ptr(a):
     return None if a is None else a.ctypes.data_as(C.c_void_p)
+
+
+__all__ = ["Fsa", "Corpus", "QuasiNewtonLearner", "Device", "Synthetic", "WfsaError", "load", "shard_range",
+           "trellis_stats"]
+
+
+def shard_range(off, nranks, rank):
+    """[begin, end) of the strings rank `rank` keeps (balanced on total length)"""
+    off = np.ascontiguousarray(off, dtype=np.int64)
+    b, e = C.c_int64(), C.c_int64()
+    check_host(load().wfsa_shard_range(_ptr(off), len(off) - 1, nranks, rank, C.byref(b), C.byref(e)))
+    return b.value, e.value
+
+
+def trellis_stats(fsa):
+    """(nodes, byte edges, end edges, parameter-list entries) of the compiled trellis"""
+    d = fsa.desc()
+    out = np.zeros(4, dtype=np.int64)
+    check_host(load().wfsa_trellis_compile_stats(C.byref(d), _ptr(out)))
+    return tuple(int(v) for v in out)
 
 
 def _b(s):

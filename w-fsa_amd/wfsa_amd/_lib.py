@@ -36,7 +36,7 @@ class DevStats(C.Structure):
     _fields_ = [
         ("n_strings", i64), ("total_symbols", i64), ("max_len", i32), ("n_nodes", i32),
         ("n_edges", i64), ("n_end_edges", i64), ("compiled_strings", i64), ("fallback_strings", i64),
-        ("stream_words", i64), ("bubble_words", i64), ("n_bubbles", i64), ("fb_launches", i64), ("fb_kernel_ms", dbl),
+        ("stream_words", i64), ("stream_bytes", i64), ("bubble_words", i64), ("n_bubbles", i64), ("fb_launches", i64), ("fb_kernel_ms", dbl),
         ("last_fb_kernel_ms", dbl), ("last_compiled_ms", dbl), ("last_call_ms", dbl),
         ("last_live_edges", i64), ("tier1_strings", i32), ("waves_per_block", i32), ("prepare_ms", dbl),
         ("compiled_kernel_ms", dbl),
@@ -97,6 +97,8 @@ _SIGS = {
     "wfsa_learner_renormalize": (C.c_int, [vp]),
     "wfsa_learner_dump": (C.c_int, [vp, vp, C.c_char_p]),
     "wfsa_learner_stats": (C.c_int, [vp, P(DevStats)]),
+    "wfsa_shard_range": (C.c_int, [vp, i64, C.c_int, C.c_int, P(i64), P(i64)]),
+    "wfsa_trellis_compile_stats": (C.c_int, [P(ModelDesc), vp]),
     "wfsa_synth_make": (C.c_int, [i32, i32, i32, i32, i32, i64, i32, C.c_uint64, P(vp)]),
     "wfsa_synth_free": (None, [vp]),
     "wfsa_synth_wfsa_text": (C.c_char_p, [vp]),
