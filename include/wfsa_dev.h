@@ -91,6 +91,8 @@ typedef struct {
     int32_t waves_per_block;
     double prepare_ms;         /* structural pass + stream compilation      */
     double compiled_kernel_ms; /* sum over calls of the compiled kernel     */
+    int32_t graph;             /* last call replayed a captured hipGraph    */
+    int32_t reserved;
 } wfsa_dev_stats;
 
 /* context ---------------------------------------------------------------- */

@@ -33,6 +33,7 @@
 
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cmath>
 
 namespace wfsa {
@@ -109,6 +110,13 @@ __device__ __forceinline__ void edge_range(const ModelView& m, int S, int c, int
     }
     lo = l;
     cnt = l2 - l;
+}
+
+// sum of the weights of node S's end edges (this iteration)
+__device__ __forceinline__ double end_weight(const ModelView& m, int S) {
+    double s = 0.0;
+    for (int x = m.x_ptr[S]; x < m.x_ptr[S + 1]; ++x) s += m.ew[m.n_edges + x];
+    return s;
 }
 
 struct Slab {
@@ -394,7 +402,7 @@ __global__ __launch_bounds__(256) void trav_kernel(TravArgs a) {
         const int fl1 = alive ? nF : 0;
         for (int j = fl0 + lane; j < fl1; j += kWave) {
             const int S = fstate[j];
-            qh += falpha[j] * (COUNTING ? m.node_end_count[S] : m.node_end[S]);
+            qh += falpha[j] * (COUNTING ? m.node_end_count[S] : end_weight(m, S));
         }
         qh = wave_sum(qh);
         if (alive) {
@@ -422,7 +430,7 @@ __global__ __launch_bounds__(256) void trav_kernel(TravArgs a) {
         for (int j = fl0 + lane; j < fl1; j += kWave) {
             const int S = fstate[j];
             const double af = falpha[j];
-            fbeta[j] = (COUNTING ? m.node_end_count[S] : m.node_end[S]) * inv_q;
+            fbeta[j] = (COUNTING ? m.node_end_count[S] : end_weight(m, S)) * inv_q;
             for (int x = m.x_ptr[S]; x < m.x_ptr[S + 1]; ++x) {
                 const int gx = m.n_edges + x;
                 const double xi = af * (COUNTING ? 1.0 : m.ew[gx]) * inv_q;
@@ -503,6 +511,21 @@ __global__ __launch_bounds__(1024) void fbc_kernel(CompiledArgs a) {
             gacc[j] = 0.0;
             if (TABLES == 2) wl[j] = a.w[j];
         }
+        // this block's slice of the per-edge weights (bubbles and the
+        // traversal fallback read them after this launch), and the zeroed
+        // result vector
+        const int64_t per = (a.n_comb + gridDim.x - 1) / gridDim.x;
+        const int64_t e_end = min(a.n_comb, per * int64_t(blockIdx.x + 1));
+        for (int64_t g = per * int64_t(blockIdx.x) + threadIdx.x; g < e_end; g += blockDim.x) {
+            const int32_t b = a.m.pptr[g], e = a.m.pptr[g + 1];
+            double sum = 0.0;
+            for (int32_t k = b; k < e; ++k) sum += a.w[a.m.pidx[k]];
+            a.lw_out[g] = sum;
+            a.ew_out[g] = exp(sum);
+            a.erec_out[g] = EdgeRec{sum, e > b ? a.m.pidx[b] : 0, e - b};
+        }
+        if (blockIdx.x == 0)
+            for (int j = int(threadIdx.x); j <= a.n_params; j += int(blockDim.x)) a.out[j] = 0.0;
         __syncthreads();
     }
     const double* wsrc = TABLES == 2 ? wl : a.w;
@@ -516,10 +539,11 @@ __global__ __launch_bounds__(1024) void fbc_kernel(CompiledArgs a) {
             if (TABLES >= 1) block_add(&gacc[j_single], -p);
             else global_add(&a.grad[j_single], -p);
         } else if (g_multi >= 0) {
-            acc += a.m.lw[g_multi];
             for (int q = a.m.pptr[g_multi]; q < a.m.pptr[g_multi + 1]; ++q) {
-                if (TABLES >= 1) block_add(&gacc[a.m.pidx[q]], -p);
-                else global_add(&a.grad[a.m.pidx[q]], -p);
+                const int j = a.m.pidx[q];
+                acc += wsrc[j];
+                if (TABLES >= 1) block_add(&gacc[j], -p);
+                else global_add(&a.grad[j], -p);
             }
         }
     };
@@ -560,12 +584,10 @@ __global__ __launch_bounds__(1024) void fbc_kernel(CompiledArgs a) {
     }
     ll_acc = wave_sum(ll_acc);
     if (lane == 0) a.ll_part[gw] = ll_acc;
-    if (TABLES >= 1) {
+    if (TABLES >= 1) {   // this block's partial gradient, summed by the tail kernel
         __syncthreads();
-        for (int j = int(threadIdx.x); j < a.n_params; j += int(blockDim.x)) {
-            const double v = gacc[j];
-            if (v != 0.0) global_add(&a.grad[j], v);
-        }
+        double* slab = a.gpart + size_t(blockIdx.x) * size_t(a.n_params);
+        for (int j = int(threadIdx.x); j < a.n_params; j += int(blockDim.x)) slab[j] = gacc[j];
     }
 }
 
@@ -615,22 +637,50 @@ __global__ __launch_bounds__(kBubbleBlock) void bubble_kernel(BubbleArgs a) {
     if (lane == 0) a.ll_part[gw] = ll_acc;
 }
 
-__global__ __launch_bounds__(256) void bubble_grad_kernel(BubbleGradArgs a) {
-    const int c = int(blockIdx.x) * 4 + int(threadIdx.x) / kWave;
-    if (c >= a.n_chunks) return;
-    const int lane = lane_id();
-    double s = 0.0;
-    for (int k = a.chunk_ptr[c] + lane; k < a.chunk_ptr[c + 1]; k += kWave) s += a.contrib[a.slot[k]];
-    s = wave_sum(s);
-    if (lane == 0) global_add(&a.grad[a.chunk_param[c]], s);
+__global__ __launch_bounds__(256) void tail_kernel(TailArgs a) {
+    const int n_tiles = (a.n_params + 255) / 256;
+    const int n_slab_groups = (a.n_gpart + kTailSlabs - 1) / kTailSlabs;
+    const int n_param_blocks = n_tiles * n_slab_groups;
+    const int n_chunk_blocks = (a.n_chunks + 3) / 4;
+    const int b = int(blockIdx.x);
+    if (b < n_param_blocks) {             // column sums of kTailSlabs partial slabs
+        const int j = (b % n_tiles) * 256 + int(threadIdx.x);
+        const int k0 = (b / n_tiles) * kTailSlabs;
+        if (j >= a.n_params) return;
+        const int k1 = min(a.n_gpart, k0 + kTailSlabs);
+        double s = 0.0;
+        for (int k = k0; k < k1; ++k) s += a.gpart[size_t(k) * size_t(a.n_params) + size_t(j)];
+        if (s != 0.0) global_add(&a.out[1 + j], s);
+    } else if (b < n_param_blocks + n_chunk_blocks) {   // bubble contributions
+        const int c = (b - n_param_blocks) * 4 + int(threadIdx.x) / kWave;
+        if (c >= a.n_chunks) return;
+        const int lane = lane_id();
+        double s = 0.0;
+        for (int k = a.chunk_ptr[c] + lane; k < a.chunk_ptr[c + 1]; k += kWave) s += a.contrib[a.slot[k]];
+        s = wave_sum(s);
+        if (lane == 0) global_add(&a.out[1 + a.chunk_param[c]], s);
+    } else {                              // log-likelihood, fixed order
+        __shared__ double red[256];
+        double s = 0.0;
+        for (int32_t i = int32_t(threadIdx.x); i < a.n_ll; i += 256) s += a.ll_part[i];
+        red[threadIdx.x] = s;
+        __syncthreads();
+        for (int w = 128; w > 0; w >>= 1) {
+            if (int(threadIdx.x) < w) red[threadIdx.x] += red[threadIdx.x + w];
+            __syncthreads();
+        }
+        if (threadIdx.x == 0) a.out[0] = red[0];
+    }
 }
 
 // Per iteration: log-weight, weight and parameter record of every combined
 // edge from the GetWeight-expanded parameter vector.
 __global__ void edge_weights_kernel(const double* __restrict__ w_full, const int32_t* __restrict__ pptr,
                                     const int32_t* __restrict__ pidx, double* __restrict__ lw,
-                                    double* __restrict__ ew, EdgeRec* __restrict__ erec, int64_t n) {
+                                    double* __restrict__ ew, EdgeRec* __restrict__ erec, int64_t n,
+                                    double* __restrict__ out, int64_t n_out) {
     const int64_t g = int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+    if (g < n_out) out[g] = 0.0;
     if (g >= n) return;
     const int32_t b = pptr[g], e = pptr[g + 1];
     double s = 0.0;
@@ -647,21 +697,6 @@ __global__ void node_end_kernel(const int32_t* __restrict__ x_ptr, const double*
     double s = 0.0;
     for (int32_t x = x_ptr[u]; x < x_ptr[u + 1]; ++x) s += x_w[x];
     node_end[u] = s;
-}
-
-// out[0] = sum of the per-wave log-likelihood partials, in a fixed order
-__global__ __launch_bounds__(256) void finalize_kernel(const double* __restrict__ part, int32_t n,
-                                                       double* __restrict__ out) {
-    __shared__ double red[256];
-    double s = 0.0;
-    for (int32_t i = int32_t(threadIdx.x); i < n; i += 256) s += part[i];
-    red[threadIdx.x] = s;
-    __syncthreads();
-    for (int w = 128; w > 0; w >>= 1) {
-        if (int(threadIdx.x) < w) red[threadIdx.x] += red[threadIdx.x + w];
-        __syncthreads();
-    }
-    if (threadIdx.x == 0) out[0] = red[0];
 }
 
 }  // namespace
@@ -720,18 +755,21 @@ hipError_t launch_bubbles(const BubbleArgs& a, int grid, hipStream_t stream) {
     return hipGetLastError();
 }
 
-hipError_t launch_bubble_grad(const BubbleGradArgs& a, hipStream_t stream) {
-    if (a.n_chunks <= 0) return hipSuccess;
-    hipLaunchKernelGGL(bubble_grad_kernel, dim3(unsigned((a.n_chunks + 3) / 4)), dim3(256), 0, stream, a);
+hipError_t launch_tail(const TailArgs& a, hipStream_t stream) {
+    const int blocks = (a.n_params + 255) / 256 * ((a.n_gpart + kTailSlabs - 1) / kTailSlabs) +
+                       (a.n_chunks + 3) / 4 + 1;
+    hipLaunchKernelGGL(tail_kernel, dim3(unsigned(blocks)), dim3(256), 0, stream, a);
     return hipGetLastError();
 }
 
 hipError_t launch_edge_weights(const double* w_full, const int32_t* pptr, const int32_t* pidx, double* lw,
-                               double* ew, EdgeRec* erec, int64_t n_edges, hipStream_t stream) {
-    if (n_edges <= 0) return hipSuccess;
-    const unsigned blocks = unsigned((n_edges + 255) / 256);
+                               double* ew, EdgeRec* erec, int64_t n_edges, double* out, int64_t n_out,
+                               hipStream_t stream) {
+    const int64_t n = std::max(n_edges, n_out);
+    if (n <= 0) return hipSuccess;
+    const unsigned blocks = unsigned((n + 255) / 256);
     hipLaunchKernelGGL(edge_weights_kernel, dim3(blocks), dim3(256), 0, stream, w_full, pptr, pidx, lw, ew, erec,
-                       n_edges);
+                       n_edges, out, n_out);
     return hipGetLastError();
 }
 
@@ -740,11 +778,6 @@ hipError_t launch_node_end(const int32_t* x_ptr, const double* x_w, double* node
     if (n_nodes <= 0) return hipSuccess;
     const unsigned blocks = unsigned((n_nodes + 255) / 256);
     hipLaunchKernelGGL(node_end_kernel, dim3(blocks), dim3(256), 0, stream, x_ptr, x_w, node_end, n_nodes);
-    return hipGetLastError();
-}
-
-hipError_t launch_finalize(const double* ll_part, int32_t n_part, double* out, hipStream_t stream) {
-    hipLaunchKernelGGL(finalize_kernel, dim3(1), dim3(256), 0, stream, ll_part, n_part, out);
     return hipGetLastError();
 }
 

@@ -142,7 +142,16 @@ struct CompiledArgs {
     int32_t tables;          // 2: w and grad staged in LDS, 1: grad in LDS, 0: global
     int32_t wide;
     const double* w;         // [n_params] w_full (GetWeight form)
-    double* grad;            // [n_params]
+    double* grad;            // [n_params] (TABLES == 0: atomics straight into it)
+    double* gpart;           // [grid][n_params] per-block partial gradients (TABLES >= 1)
+    // prologue work folded into this launch when TABLES >= 1 (no other kernel
+    // then runs before it): per-edge weights of all combined edges and the
+    // zeroing of the result vector
+    int64_t n_comb;          // E + X
+    double* lw_out;
+    double* ew_out;
+    EdgeRec* erec_out;
+    double* out;             // [1 + n_params], zeroed by block 0
     double* ll_part;         // [waves in grid]
     double* logq;            // [S] or null
 };
@@ -158,17 +167,25 @@ struct BubbleArgs {
     double* logq;            // [S] or null: log Z added to the string's entry
 };
 
-// grad[j] += sum of contrib over the bubble edges carrying parameter j, in
-// chunks of at most kBubbleGradChunk slots (one wavefront per chunk, so a hot
-// parameter's long slot list is summed by many waves).
+// The per-iteration tail, one launch: out[1+j] += sum over blocks of the
+// compiled kernel's partial gradients, += the bubble contributions of
+// parameter j (chunks of at most kBubbleGradChunk slots, one wavefront per
+// chunk, so a hot parameter's long list is summed by many waves), and
+// out[0] = sum of the per-wave log-likelihood partials in a fixed order.
 constexpr int kBubbleGradChunk = 512;
-struct BubbleGradArgs {
+constexpr int kTailSlabs = 8;    // partial slabs summed per thread
+struct TailArgs {
+    const double* gpart;         // [n_gpart][n_params]
+    int32_t n_gpart;
     const int32_t* chunk_param;  // [n_chunks]
     const int32_t* chunk_ptr;    // [n_chunks+1] into slot
     const int32_t* slot;
     const double* contrib;
     int32_t n_chunks;
-    double* grad;
+    const double* ll_part;
+    int32_t n_ll;
+    int32_t n_params;
+    double* out;                 // [1 + n_params]
 };
 
 hipError_t configure_kernels(int max_dynamic_lds);
@@ -176,11 +193,12 @@ hipError_t launch_trav(TravMode mode, const TravArgs& a, int grid, hipStream_t s
 hipError_t launch_compiled(const CompiledArgs& a, int grid, int block, size_t lds, hipStream_t stream);
 constexpr int kBubbleBlock = 128;
 hipError_t launch_bubbles(const BubbleArgs& a, int grid, hipStream_t stream);
-hipError_t launch_bubble_grad(const BubbleGradArgs& a, hipStream_t stream);
+hipError_t launch_tail(const TailArgs& a, hipStream_t stream);
+// also zeroes out[0..n_out) (the accumulators of this iteration)
 hipError_t launch_edge_weights(const double* w_full, const int32_t* pptr, const int32_t* pidx, double* lw,
-                               double* ew, EdgeRec* erec, int64_t n_edges, hipStream_t stream);
+                               double* ew, EdgeRec* erec, int64_t n_edges, double* out, int64_t n_out,
+                               hipStream_t stream);
 hipError_t launch_node_end(const int32_t* x_ptr, const double* x_w, double* node_end, int32_t n_nodes,
                            hipStream_t stream);
-hipError_t launch_finalize(const double* ll_part, int32_t n_part, double* out, hipStream_t stream);
 
 }  // namespace wfsa

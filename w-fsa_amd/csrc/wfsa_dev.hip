@@ -23,6 +23,7 @@
 #include <algorithm>
 #include <chrono>
 #include <cstdarg>
+#include <cstdlib>
 #include <cstdio>
 #include <cstring>
 #include <memory>
@@ -160,8 +161,15 @@ struct wfsa_dev {
     // work buffers
     DevBuf<double> w_full, out, ll_part, logq;
     DevBuf<unsigned long long> live;
-    double* pinned = nullptr;   // n_params + 1 doubles
+    double* pinned = nullptr;   // [0, n_params+1): results; [n_params+1, 2 n_params+1): weights
     size_t pinned_n = 0;
+    DevBuf<double> gpart;        // per-block partial gradients of the compiled kernel
+
+    // the per-iteration device sequence, captured once per prepared corpus
+    hipGraph_t graph = nullptr;
+    hipGraphExec_t graph_exec = nullptr;
+    bool graph_failed = false;
+    bool use_graph = false;   // WFSA_GRAPH=1: replay a captured graph (no per-kernel timing)
 
     // communicator
     ncclComm_t comm = nullptr;
@@ -273,8 +281,11 @@ int configure_tiers(wfsa_dev* ctx) {
 
 // Structural pass (level 1) + stream compilation (level 2) for the loaded
 // corpus.
+void drop_graph(wfsa_dev* ctx);
+
 int prepare(wfsa_dev* ctx, int level) {
     const auto t_start = std::chrono::steady_clock::now();
+    drop_graph(ctx);
     hipStream_t s = ctx->stream;
     const int64_t S = ctx->n_strings;
     const size_t SZ = size_t(std::max<int64_t>(S, 1));
@@ -508,6 +519,7 @@ int prepare(wfsa_dev* ctx, int level) {
     const int per_cu = ctx->c_tables ? 1 : 2;
     ctx->c_grid = int(std::max<int64_t>(1, std::min<int64_t>(int64_t(ctx->n_cu) * per_cu,
                                                              (int64_t(G) + waves_per_block - 1) / waves_per_block)));
+    if (ctx->c_tables >= 1) HIP_TRY(ctx->gpart.alloc(size_t(ctx->c_grid) * size_t(std::max(ctx->n_params, 1))));
 
     // traversal fallback lists
     for (int t = 0; t < 2; ++t) {
@@ -535,6 +547,103 @@ int prepare(wfsa_dev* ctx, int level) {
     return WFSA_OK;
 }
 
+// The device work of one objective/gradient evaluation, enqueued on the
+// context's stream (captured into a graph on first use): weights in,
+// per-edge weights, compiled streams + bubbles (timed by k0..k1), traversal
+// fallback (k1..k2), the tail reduction, and -- without a communicator --
+// the results out.
+int enqueue_iteration(wfsa_dev* ctx) {
+    hipStream_t s = ctx->stream;
+    const int32_t np = ctx->n_params;
+    if (np > 0)
+        HIP_TRY(hipMemcpyAsync(ctx->w_full.ptr, ctx->pinned + np + 1, size_t(np) * sizeof(double),
+                               hipMemcpyHostToDevice, s));
+    // the compiled kernel folds the edge weights and the zeroing of `out`
+    // into its prologue when it keeps its gradient in LDS
+    const bool fused = ctx->n_groups > 0 && ctx->c_tables >= 1;
+    if (!fused)
+        HIP_TRY(wfsa::launch_edge_weights(ctx->w_full.ptr, ctx->pptr.ptr, ctx->pidx.ptr, ctx->lw.ptr, ctx->ew.ptr,
+                                          ctx->erec.ptr, ctx->n_edges + ctx->n_end, ctx->out.ptr, int64_t(np) + 1, s));
+    int32_t wave_off = 0;
+    HIP_TRY(hipEventRecord(ctx->k0, s));
+    if (ctx->n_groups > 0) {
+        wfsa::CompiledArgs c{};
+        c.m = model_view(ctx);
+        c.p = ctx->p.ptr;
+        c.stream = ctx->stream_w.ptr;
+        c.wide = ctx->wide;
+        c.g_base = ctx->g_base.ptr;
+        c.g_len = ctx->g_len.ptr;
+        c.l_str = ctx->l_str.ptr;
+        c.l_len = ctx->l_len.ptr;
+        c.n_groups = ctx->n_groups;
+        c.n_params = np;
+        c.tables = ctx->c_tables;
+        c.w = ctx->w_full.ptr;
+        c.grad = ctx->out.ptr + 1;
+        c.gpart = ctx->gpart.ptr;
+        c.n_comb = ctx->n_edges + ctx->n_end;
+        c.lw_out = ctx->lw.ptr;
+        c.ew_out = ctx->ew.ptr;
+        c.erec_out = ctx->erec.ptr;
+        c.out = ctx->out.ptr;
+        c.ll_part = ctx->ll_part.ptr;
+        c.logq = ctx->logq.ptr;
+        HIP_TRY(wfsa::launch_compiled(c, ctx->c_grid, kCompiledBlock, ctx->c_lds, s));
+        wave_off += ctx->c_grid * (kCompiledBlock / kWave);
+    }
+    if (ctx->n_bubbles > 0) {
+        wfsa::BubbleArgs b{};
+        b.m = model_view(ctx);
+        b.p = ctx->p.ptr;
+        b.bub = ctx->bub.ptr;
+        b.bub_off = ctx->bub_off.ptr;
+        b.n_bubbles = ctx->n_bubbles;
+        b.contrib = ctx->contrib.ptr;
+        b.ll_part = ctx->ll_part.ptr + wave_off;
+        b.logq = ctx->logq.ptr;
+        HIP_TRY(wfsa::launch_bubbles(b, ctx->b_grid, s));
+        wave_off += ctx->b_grid * (wfsa::kBubbleBlock / kWave);
+    }
+    HIP_TRY(hipEventRecord(ctx->k1, s));
+    for (int t = 0; t < 2; ++t) {
+        if (!ctx->n_fall[t]) continue;
+        wfsa::TravArgs a = trav_args(ctx, t);
+        a.list = ctx->fall[t].ptr;
+        a.n_list = ctx->n_fall[t];
+        a.grad = ctx->out.ptr + 1;
+        a.ll_part = ctx->ll_part.ptr + wave_off;
+        a.logq = ctx->logq.ptr;
+        HIP_TRY(wfsa::launch_trav(wfsa::MODE_WEIGHTED, a, ctx->fall_grid[t], s));
+        wave_off += ctx->fall_grid[t] * ctx->cfg[t].waves_per_block;
+    }
+    HIP_TRY(hipEventRecord(ctx->k2, s));
+    wfsa::TailArgs t{};
+    t.gpart = ctx->gpart.ptr;
+    t.n_gpart = (ctx->n_groups > 0 && ctx->c_tables >= 1) ? ctx->c_grid : 0;
+    t.chunk_param = ctx->bg_chunk_param.ptr;
+    t.chunk_ptr = ctx->bg_chunk_ptr.ptr;
+    t.slot = ctx->bg_slot.ptr;
+    t.contrib = ctx->contrib.ptr;
+    t.n_chunks = ctx->n_bubbles > 0 ? ctx->n_bg_chunks : 0;
+    t.ll_part = ctx->ll_part.ptr;
+    t.n_ll = wave_off;
+    t.n_params = np;
+    t.out = ctx->out.ptr;
+    HIP_TRY(wfsa::launch_tail(t, s));
+    if (!ctx->comm)
+        HIP_TRY(hipMemcpyAsync(ctx->pinned, ctx->out.ptr, (size_t(np) + 1) * sizeof(double), hipMemcpyDeviceToHost, s));
+    return WFSA_OK;
+}
+
+void drop_graph(wfsa_dev* ctx) {
+    if (ctx->graph_exec) (void)hipGraphExecDestroy(ctx->graph_exec);
+    if (ctx->graph) (void)hipGraphDestroy(ctx->graph);
+    ctx->graph_exec = nullptr;
+    ctx->graph = nullptr;
+    ctx->graph_failed = false;
+}
+
 }  // namespace
 
 extern "C" {
@@ -558,6 +667,7 @@ int wfsa_dev_create(int device, wfsa_dev** out) {
     std::unique_ptr<wfsa_dev> ctx(new wfsa_dev());
     ctx->device = device;
     ctx->n_cu = prop.multiProcessorCount > 0 ? prop.multiProcessorCount : kNumCu;
+    if (const char* e = std::getenv("WFSA_GRAPH")) ctx->use_graph = e[0] == '1';
     HIP_TRY(hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking));
     for (hipEvent_t* ev : {&ctx->ev0, &ctx->ev1, &ctx->k0, &ctx->k1, &ctx->k2}) HIP_TRY(hipEventCreate(ev));
     HIP_TRY(ctx->live.alloc(1));
@@ -569,6 +679,7 @@ void wfsa_dev_destroy(wfsa_dev* ctx) {
     if (!ctx) return;
     (void)hipSetDevice(ctx->device);
     if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
+    drop_graph(ctx);
     if (ctx->comm) (void)ncclCommDestroy(ctx->comm);
     if (ctx->pinned) (void)hipHostFree(ctx->pinned);
     for (hipEvent_t ev : {ctx->ev0, ctx->ev1, ctx->k0, ctx->k1, ctx->k2})
@@ -624,11 +735,11 @@ int wfsa_dev_load_model(wfsa_dev* ctx, const wfsa_model_desc* model) {
     ctx->start = tm.start;
     HIP_TRY(ctx->w_full.alloc(size_t(ctx->n_params)));
     HIP_TRY(ctx->out.alloc(size_t(ctx->n_params) + 1));
-    if (ctx->pinned_n < size_t(ctx->n_params) + 1) {
+    if (ctx->pinned_n < 2 * size_t(ctx->n_params) + 1) {
         if (ctx->pinned) (void)hipHostFree(ctx->pinned);
         ctx->pinned = nullptr;
-        HIP_TRY(hipHostMalloc(reinterpret_cast<void**>(&ctx->pinned), (size_t(ctx->n_params) + 1) * sizeof(double)));
-        ctx->pinned_n = size_t(ctx->n_params) + 1;
+        HIP_TRY(hipHostMalloc(reinterpret_cast<void**>(&ctx->pinned), (2 * size_t(ctx->n_params) + 1) * sizeof(double)));
+        ctx->pinned_n = 2 * size_t(ctx->n_params) + 1;
     }
     HIP_TRY(hipStreamSynchronize(s));
     ctx->has_model = true;
@@ -699,89 +810,54 @@ int wfsa_dev_objective_grad(wfsa_dev* ctx, const double* w_full, double* loglik,
         if (int rc = prepare(ctx, 2)) return rc;
     hipStream_t s = ctx->stream;
     const int32_t np = ctx->n_params;
+    double* res = ctx->pinned;            // [LL, grad]
+    double* win = ctx->pinned + np + 1;   // weights in
+    if (np > 0) std::memcpy(win, w_full, size_t(np) * sizeof(double));
     HIP_TRY(hipEventRecord(ctx->ev0, s));
-    if (np > 0) {
-        std::memcpy(ctx->pinned, w_full, size_t(np) * sizeof(double));
-        HIP_TRY(hipMemcpyAsync(ctx->w_full.ptr, ctx->pinned, size_t(np) * sizeof(double), hipMemcpyHostToDevice, s));
+    if (ctx->use_graph && !ctx->graph_exec && !ctx->graph_failed) {
+        // capture once; a capture the runtime rejects falls back to eager launches
+        if (hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal) == hipSuccess) {
+            const int rc = enqueue_iteration(ctx);
+            hipGraph_t g = nullptr;
+            const hipError_t e = hipStreamEndCapture(s, &g);
+            if (rc == WFSA_OK && e == hipSuccess && g &&
+                hipGraphInstantiate(&ctx->graph_exec, g, nullptr, nullptr, 0) == hipSuccess) {
+                ctx->graph = g;
+            } else {
+                if (g) (void)hipGraphDestroy(g);
+                ctx->graph_exec = nullptr;
+                ctx->graph_failed = true;
+                (void)hipGetLastError();
+            }
+        } else {
+            ctx->graph_failed = true;
+            (void)hipGetLastError();
+        }
     }
-    HIP_TRY(wfsa::launch_edge_weights(ctx->w_full.ptr, ctx->pptr.ptr, ctx->pidx.ptr, ctx->lw.ptr, ctx->ew.ptr, ctx->erec.ptr,
-                                      ctx->n_edges + ctx->n_end, s));
-    const bool any_fall = ctx->n_fall[0] + ctx->n_fall[1] > 0;
-    if (any_fall) HIP_TRY(wfsa::launch_node_end(ctx->x_ptr.ptr, ctx->ew.ptr + ctx->n_edges, ctx->node_end.ptr, ctx->n_nodes, s));
-    HIP_TRY(hipMemsetAsync(ctx->out.ptr, 0, (size_t(np) + 1) * sizeof(double), s));
-    HIP_TRY(hipMemsetAsync(ctx->live.ptr, 0, sizeof(unsigned long long), s));
-    int32_t wave_off = 0;
-    HIP_TRY(hipEventRecord(ctx->k0, s));
-    if (ctx->n_groups > 0) {
-        wfsa::CompiledArgs c{};
-        c.m = model_view(ctx);
-        c.p = ctx->p.ptr;
-        c.stream = ctx->stream_w.ptr;
-        c.wide = ctx->wide;
-        c.g_base = ctx->g_base.ptr;
-        c.g_len = ctx->g_len.ptr;
-        c.l_str = ctx->l_str.ptr;
-        c.l_len = ctx->l_len.ptr;
-        c.n_groups = ctx->n_groups;
-        c.n_params = np;
-        c.tables = ctx->c_tables;
-        c.w = ctx->w_full.ptr;
-        c.grad = ctx->out.ptr + 1;
-        c.ll_part = ctx->ll_part.ptr;
-        c.logq = logq ? ctx->logq.ptr : nullptr;
-        HIP_TRY(wfsa::launch_compiled(c, ctx->c_grid, kCompiledBlock, ctx->c_lds, s));
-        wave_off += ctx->c_grid * (kCompiledBlock / kWave);
+    if (ctx->graph_exec) HIP_TRY(hipGraphLaunch(ctx->graph_exec, s));
+    else if (int rc = enqueue_iteration(ctx)) return rc;
+    if (ctx->comm) {
+        RCCL_TRY(ncclAllReduce(ctx->out.ptr, ctx->out.ptr, size_t(np) + 1, ncclDouble, ncclSum, ctx->comm, s));
+        HIP_TRY(hipMemcpyAsync(res, ctx->out.ptr, (size_t(np) + 1) * sizeof(double), hipMemcpyDeviceToHost, s));
     }
-    if (ctx->n_bubbles > 0) {
-        wfsa::BubbleArgs b{};
-        b.m = model_view(ctx);
-        b.p = ctx->p.ptr;
-        b.bub = ctx->bub.ptr;
-        b.bub_off = ctx->bub_off.ptr;
-        b.n_bubbles = ctx->n_bubbles;
-        b.contrib = ctx->contrib.ptr;
-        b.ll_part = ctx->ll_part.ptr + wave_off;
-        b.logq = logq ? ctx->logq.ptr : nullptr;
-        HIP_TRY(wfsa::launch_bubbles(b, ctx->b_grid, s));
-        wave_off += ctx->b_grid * (wfsa::kBubbleBlock / kWave);
-        wfsa::BubbleGradArgs bg{ctx->bg_chunk_param.ptr, ctx->bg_chunk_ptr.ptr, ctx->bg_slot.ptr, ctx->contrib.ptr,
-                                ctx->n_bg_chunks, ctx->out.ptr + 1};
-        HIP_TRY(wfsa::launch_bubble_grad(bg, s));
-    }
-    HIP_TRY(hipEventRecord(ctx->k1, s));
-    for (int t = 0; t < 2; ++t) {
-        if (!ctx->n_fall[t]) continue;
-        wfsa::TravArgs a = trav_args(ctx, t);
-        a.list = ctx->fall[t].ptr;
-        a.n_list = ctx->n_fall[t];
-        a.grad = ctx->out.ptr + 1;
-        a.ll_part = ctx->ll_part.ptr + wave_off;
-        a.logq = logq ? ctx->logq.ptr : nullptr;
-        HIP_TRY(wfsa::launch_trav(wfsa::MODE_WEIGHTED, a, ctx->fall_grid[t], s));
-        wave_off += ctx->fall_grid[t] * ctx->cfg[t].waves_per_block;
-    }
-    HIP_TRY(hipEventRecord(ctx->k2, s));
-    HIP_TRY(wfsa::launch_finalize(ctx->ll_part.ptr, wave_off, ctx->out.ptr, s));
-    if (ctx->comm) RCCL_TRY(ncclAllReduce(ctx->out.ptr, ctx->out.ptr, size_t(np) + 1, ncclDouble, ncclSum, ctx->comm, s));
-    HIP_TRY(hipMemcpyAsync(ctx->pinned, ctx->out.ptr, (size_t(np) + 1) * sizeof(double), hipMemcpyDeviceToHost, s));
     if (logq) HIP_TRY(ctx->logq.download(logq, size_t(ctx->n_strings), s));
-    unsigned long long live = 0;
-    HIP_TRY(hipMemcpyAsync(&live, ctx->live.ptr, sizeof live, hipMemcpyDeviceToHost, s));
     HIP_TRY(hipEventRecord(ctx->ev1, s));
     HIP_TRY(hipStreamSynchronize(s));
     float c_ms = 0.f, f_ms = 0.f, all_ms = 0.f;
-    HIP_TRY(hipEventElapsedTime(&c_ms, ctx->k0, ctx->k1));
-    HIP_TRY(hipEventElapsedTime(&f_ms, ctx->k1, ctx->k2));
+    if (!ctx->graph_exec) {   // events recorded inside a captured graph are not timeable
+        HIP_TRY(hipEventElapsedTime(&c_ms, ctx->k0, ctx->k1));
+        HIP_TRY(hipEventElapsedTime(&f_ms, ctx->k1, ctx->k2));
+    }
     HIP_TRY(hipEventElapsedTime(&all_ms, ctx->ev0, ctx->ev1));
-    if (loglik) *loglik = ctx->pinned[0];
-    if (grad_full && np > 0) std::memcpy(grad_full, ctx->pinned + 1, size_t(np) * sizeof(double));
+    if (loglik) *loglik = res[0];
+    if (grad_full && np > 0) std::memcpy(grad_full, res + 1, size_t(np) * sizeof(double));
     ctx->stats.fb_launches += 1;
     ctx->stats.fb_kernel_ms += double(c_ms) + double(f_ms);
     ctx->stats.last_fb_kernel_ms = double(c_ms) + double(f_ms);
     ctx->stats.last_compiled_ms = double(c_ms);
     ctx->stats.compiled_kernel_ms += double(c_ms);
     ctx->stats.last_call_ms = double(all_ms);
-    ctx->stats.last_live_edges = int64_t(live);
+    ctx->stats.graph = ctx->graph_exec ? 1 : 0;
     return WFSA_OK;
 }
 
