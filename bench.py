@@ -126,14 +126,16 @@ def main():
             dist.barrier()
         torch.cuda.synchronize()
 
-    for _ in range(args.warmup):
-        lrn.OptimizationStep(1.0, 1e-6)
+    # main.cpp's epoch loop runs natively (wfsa_learner_run); tol < 0 never
+    # halts, so exactly `steps` OptimizationSteps run
+    if args.warmup:
+        lrn.Run(args.warmup, 1.0, -1.0)
     st0 = lrn.stats()
     barrier()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
-        lrn.OptimizationStep(1.0, 1e-6)
+    rows = lrn.Run(args.steps, 1.0, -1.0)
     barrier()
+    assert len(rows) == args.steps
     dt = time.perf_counter() - t0
     st1 = lrn.stats()
     if distributed:
@@ -177,7 +179,7 @@ def main():
             "global_strings": strings_all,
             "strings_per_gpu": args.strings_per_gpu,
             "parallelism": f"dp{n_gpus}",
-            "step": "QuasiNewtonLearner::OptimizationStep (H2D w, forward-backward, all-reduce, D2H grad, host update)",
+            "step": "QuasiNewtonLearner::OptimizationStep (H2D w, forward-backward, all-reduce, D2H grad, host update; epoch loop in wfsa_learner_run)",
         },
         "roofline": {
             "bound": "hbm",

@@ -124,6 +124,11 @@ int wfsa_dev_recognize(wfsa_dev* ctx, uint8_t* recognized, double* path_count,
  * (one RCCL all-reduce) and logq stays local. */
 int wfsa_dev_objective_grad(wfsa_dev* ctx, const double* w_full, double* loglik,
                             double* grad_full, double* logq);
+/* The same split in two so host work can overlap the device: _begin copies
+ * w_full and enqueues the evaluation (plus the all-reduce) and returns;
+ * _end waits and writes the outputs.  Exactly one _end per _begin. */
+int wfsa_dev_objective_grad_begin(wfsa_dev* ctx, const double* w_full, int want_logq);
+int wfsa_dev_objective_grad_end(wfsa_dev* ctx, double* loglik, double* grad_full, double* logq);
 
 /* Multi-GPU: one process per GPU.  Rank 0 creates the id, the launcher
  * broadcasts the 128 bytes, every rank attaches.  wfsa_dev_allreduce sums

@@ -71,6 +71,13 @@ int wfsa_learner_info_get(wfsa_learner* l, wfsa_learner_info* out);
 int wfsa_learner_init(wfsa_learner* l, int flags, const double* x0);       /* Learner::Init */
 /* OptimizationStep + GetOptimizationInfo (7 values) + HaltCondition(tol) */
 int wfsa_learner_step(wfsa_learner* l, double eta, double tol, double info[7], int32_t* halt);
+/* main.cpp's epoch loop (src/main.cpp:276-303) without the per-epoch FFI
+ * round trip: up to max_epochs steps, info_rows[7*e..] (nullable) gets each
+ * epoch's info, stops after the epoch whose HaltCondition(tol) holds; a
+ * non-finite info value fails with "<x> detected at epoch <e>" (the
+ * reference's LearnerError) after recording that row. */
+int wfsa_learner_run(wfsa_learner* l, double eta, double tol, int32_t max_epochs, double* info_rows,
+                     int32_t* epochs_done);
 /* ComputeExpX, ComputeGrad, ComputeObjective at the current x:
  * kl, grad[n_params] (trimmed order), logq[n_local_strings] (nullable) */
 int wfsa_learner_objective_grad(wfsa_learner* l, double* kl, double* grad, double* logq);

@@ -228,3 +228,38 @@ def test_full_size_family_a_properties():
     sub_sym = np.concatenate([sym[off[i]:off[i + 1]] for i in idx])
     oll, ologq, _, _ = _oracle_eval(syn.wfsa_text, sub_sym, sub_off, wt[idx], dict(zip(names, w)))
     np.testing.assert_allclose(logq[idx], ologq, rtol=1e-11)
+
+
+def test_async_begin_end_and_native_epoch_loop():
+    """wfsa_dev_objective_grad_begin/_end == wfsa_dev_objective_grad; call
+    order is checked; wfsa_learner_run == OptimizationStep one by one"""
+    import wfsa_amd as W
+    syn = W.Synthetic(n_states=64, degree=8, vocab=16, emissions=1, n_strings=3000, max_len=64, seed=5)
+    sym, off, wt = syn.corpus()
+    fsa = W.Fsa.read_text(syn.wfsa_text)
+    w = np.random.default_rng(1).normal(-1.5, 0.5, size=len(fsa.param_names()))
+    dev = W.Device(0)
+    dev.load_model(fsa)
+    dev.load_corpus(sym, off, wt / wt.sum())
+    dev.recognize()
+    ll, grad, logq = dev.objective_grad(w)
+    with pytest.raises(W.WfsaError):
+        dev.objective_grad_end()                 # nothing in flight
+    dev.objective_grad_begin(w, want_logq=True)
+    with pytest.raises(W.WfsaError):
+        dev.objective_grad_begin(w)              # one in flight already
+    ll2, grad2, logq2 = dev.objective_grad_end()
+    assert _close(ll, ll2, rel=1e-13)
+    np.testing.assert_allclose(grad2, grad, rtol=1e-12, atol=1e-16)
+    np.testing.assert_allclose(logq2, logq, rtol=1e-13)
+    a, b = W.QuasiNewtonLearner(0), W.QuasiNewtonLearner(0)
+    for lrn in (a, b):
+        lrn.BuildFromPacked(fsa, sym, off, wt)
+        lrn.Finalize()
+        lrn.Init(7)
+    rows_a = a.Run(6, 1.0, -1.0)
+    rows_b = [b.OptimizationStep(1.0, -1.0)[0] for _ in range(6)]
+    assert len(rows_a) == 6
+    for r, q in zip(rows_a, rows_b):
+        for u, v in zip(r[:5], q[:5]):
+            assert _close(u, v, rel=1e-11, atol=1e-14)

@@ -264,19 +264,43 @@ void Learner::Init(int flags, const double* initialx) {
     InitCallback(flags);
 }
 
-void Learner::EvaluateDevice(std::vector<double>& grad_out, bool want_logq) {
+void Learner::BeginModeledProbs(bool want_logq) {
     if (!dev) throw LearnerError("BuildFrom has not run");
-    for (int32_t j = 0; j < n_full; ++j) w_full[size_t(j)] = GetWeight(j);
-    if (want_logq) logq.assign(p.size(), 0.0);
-    ThrowOnDevError(wfsa_dev_objective_grad(dev, w_full.data(), &loglik, grad_full.data(),
-                                            want_logq ? logq.data() : nullptr),
-                    "wfsa_dev_objective_grad");
-    logq_valid = want_logq;
-    grad_out.assign(_x.size(), 0.0);
-    for (int32_t j = 0; j < n_full; ++j) {
-        const int32_t t = trimmed_weights[size_t(j)];
-        if (t >= 0) grad_out[size_t(t)] = grad_full[size_t(j)];
+    if (eval_in_flight) throw LearnerError("an evaluation is already in flight");
+    const int32_t* tw = trimmed_weights.data();
+    const double* x = _x.data();
+    double* w = w_full.data();
+    for (int32_t j = 0; j < n_full; ++j) {   // GetWeight(j), src/Learner.cpp:427-436
+        const int32_t t = tw[j];
+        w[j] = t >= 0 ? x[t] : (t == -1 ? 0.0 : -std::numeric_limits<double>::infinity());
     }
+    ThrowOnDevError(wfsa_dev_objective_grad_begin(dev, w, want_logq ? 1 : 0),
+                    "wfsa_dev_objective_grad_begin");
+    eval_in_flight = true;
+    eval_logq = want_logq;
+}
+
+void Learner::EndModeledProbs(std::vector<double>& grad_out) {
+    if (!eval_in_flight) throw LearnerError("no evaluation in flight");
+    eval_in_flight = false;
+    if (eval_logq) logq.resize(p.size());
+    ThrowOnDevError(wfsa_dev_objective_grad_end(dev, &loglik, grad_full.data(),
+                                                eval_logq ? logq.data() : nullptr),
+                    "wfsa_dev_objective_grad_end");
+    logq_valid = eval_logq;
+    grad_out.resize(_x.size());
+    const int32_t* tw = trimmed_weights.data();
+    const double* gf = grad_full.data();
+    double* go = grad_out.data();
+    for (int32_t j = 0; j < n_full; ++j) {   // every kept parameter has exactly one full index
+        const int32_t t = tw[j];
+        if (t >= 0) go[t] = gf[j];
+    }
+}
+
+void Learner::EvaluateDevice(std::vector<double>& grad_out, bool want_logq) {
+    BeginModeledProbs(want_logq);
+    EndModeledProbs(grad_out);
 }
 
 void Learner::ComputeModeledProbs() { EvaluateDevice(grad_cache, false); }

@@ -113,6 +113,12 @@ protected:
     // One device evaluation at the current _x: loglik, gradient (trimmed,
     // reference sign: -sum p E[count]) into `grad_out`.
     void EvaluateDevice(std::vector<double>& grad_out, bool want_logq);
+    // The same, split: Begin enqueues the device work at the current _x and
+    // returns, so the caller can do host work that does not need the
+    // gradient; End waits and fills grad_out.  (ComputeModeledProbs ==
+    // BeginModeledProbs + EndModeledProbs.)
+    void BeginModeledProbs(bool want_logq = false);
+    void EndModeledProbs(std::vector<double>& grad_out);
     double AllReduceSum(double v) const;
 
     std::vector<double> _x;
@@ -138,6 +144,7 @@ private:
     std::vector<double> path_count_local;
     std::vector<uint8_t> recognized_local;
     bool logq_valid = false;
+    bool eval_in_flight = false, eval_logq = false;
 
     int device = 0;
     wfsa_dev* dev = nullptr;

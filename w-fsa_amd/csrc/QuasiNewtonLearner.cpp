@@ -75,9 +75,14 @@ void QuasiNewtonLearner::ComputeG() {   // :148-160: g = C^T exp(x) - 1
 }
 
 void QuasiNewtonLearner::OptimizationStep(double eta, bool) {   // :162-201
+    // ComputeExpX and ComputeG do not depend on the gradient: run them on
+    // the host while the device evaluates (same results as the reference's
+    // ExpX, G, Grad order).
+    BeginModeledProbs();
     ComputeExpX();
     ComputeG();
-    ComputeGrad();
+    EndModeledProbs(grad_cache);
+    grad = grad_cache;
     ComputeObjective();
     const size_t n = _x.size(), k = lambda.size();
     aux.resize(n);

@@ -557,25 +557,34 @@ __global__ __launch_bounds__(1024) void fbc_kernel(CompiledArgs a) {
         const uint4* st = a.stream + a.g_base[grp] + lane;
         const double p = s >= 0 ? a.p[s] : 0.0;
         double acc = 0.0;
-        uint4 cur = nch > 0 ? st[0] : pad;
-        for (int c = 0; c < gch; ++c) {
-            const uint4 nxt = (c + 1 < nch) ? st[int64_t(kWave) * (c + 1)] : pad;
-            const uint32_t v[4] = {cur.x, cur.y, cur.z, cur.w};
+        // ring of D chunks in flight per lane (~64 KB per CU with 16 waves)
+        constexpr int D = 4;
+        uint4 buf[D];
 #pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                if (WIDE) {
-                    const int x = int(v[i]);
-                    apply(x, x < -1 ? -(x + 2) : -1, p, acc);
-                } else {
+        for (int d = 0; d < D; ++d) buf[d] = d < nch ? st[int64_t(kWave) * d] : pad;
+        for (int c0 = 0; c0 < gch; c0 += D) {
 #pragma unroll
-                    for (int h = 0; h < 2; ++h) {
-                        const int x = int((v[i] >> (16 * h)) & 0xffffu);
-                        if (x < 0x8000) apply(x, -1, p, acc);
-                        else if (x != 0xffff) apply(-1, a.m.multi_edge[x - 0x8000], p, acc);
+            for (int d = 0; d < D; ++d) {
+                const int c = c0 + d;
+                if (c >= gch) break;
+                const uint4 cur = buf[d];
+                buf[d] = (c + D < nch) ? st[int64_t(kWave) * (c + D)] : pad;
+                const uint32_t v[4] = {cur.x, cur.y, cur.z, cur.w};
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    if (WIDE) {
+                        const int x = int(v[i]);
+                        apply(x, x < -1 ? -(x + 2) : -1, p, acc);
+                    } else {
+#pragma unroll
+                        for (int h = 0; h < 2; ++h) {
+                            const int x = int((v[i] >> (16 * h)) & 0xffffu);
+                            if (x < 0x8000) apply(x, -1, p, acc);
+                            else if (x != 0xffff) apply(-1, a.m.multi_edge[x - 0x8000], p, acc);
+                        }
                     }
                 }
             }
-            cur = nxt;
         }
         if (s >= 0) {
             ll_acc += p * acc;

@@ -169,7 +169,9 @@ struct wfsa_dev {
     hipGraph_t graph = nullptr;
     hipGraphExec_t graph_exec = nullptr;
     bool graph_failed = false;
-    bool use_graph = false;   // WFSA_GRAPH=1: replay a captured graph (no per-kernel timing)
+    bool use_graph = false;    // WFSA_GRAPH=1: replay a captured graph (no per-kernel timing)
+    bool in_flight = false;    // between objective_grad_begin and _end
+    bool logq_ready = false;   // the call in flight computes log q
 
     // communicator
     ncclComm_t comm = nullptr;
@@ -552,7 +554,7 @@ int prepare(wfsa_dev* ctx, int level) {
 // per-edge weights, compiled streams + bubbles (timed by k0..k1), traversal
 // fallback (k1..k2), the tail reduction, and -- without a communicator --
 // the results out.
-int enqueue_iteration(wfsa_dev* ctx) {
+int enqueue_iteration(wfsa_dev* ctx, bool want_logq) {
     hipStream_t s = ctx->stream;
     const int32_t np = ctx->n_params;
     if (np > 0)
@@ -588,7 +590,7 @@ int enqueue_iteration(wfsa_dev* ctx) {
         c.erec_out = ctx->erec.ptr;
         c.out = ctx->out.ptr;
         c.ll_part = ctx->ll_part.ptr;
-        c.logq = ctx->logq.ptr;
+        c.logq = want_logq ? ctx->logq.ptr : nullptr;
         HIP_TRY(wfsa::launch_compiled(c, ctx->c_grid, kCompiledBlock, ctx->c_lds, s));
         wave_off += ctx->c_grid * (kCompiledBlock / kWave);
     }
@@ -601,7 +603,7 @@ int enqueue_iteration(wfsa_dev* ctx) {
         b.n_bubbles = ctx->n_bubbles;
         b.contrib = ctx->contrib.ptr;
         b.ll_part = ctx->ll_part.ptr + wave_off;
-        b.logq = ctx->logq.ptr;
+        b.logq = want_logq ? ctx->logq.ptr : nullptr;
         HIP_TRY(wfsa::launch_bubbles(b, ctx->b_grid, s));
         wave_off += ctx->b_grid * (wfsa::kBubbleBlock / kWave);
     }
@@ -613,7 +615,7 @@ int enqueue_iteration(wfsa_dev* ctx) {
         a.n_list = ctx->n_fall[t];
         a.grad = ctx->out.ptr + 1;
         a.ll_part = ctx->ll_part.ptr + wave_off;
-        a.logq = ctx->logq.ptr;
+        a.logq = want_logq ? ctx->logq.ptr : nullptr;
         HIP_TRY(wfsa::launch_trav(wfsa::MODE_WEIGHTED, a, ctx->fall_grid[t], s));
         wave_off += ctx->fall_grid[t] * ctx->cfg[t].waves_per_block;
     }
@@ -802,10 +804,11 @@ int wfsa_dev_recognize(wfsa_dev* ctx, uint8_t* recognized, double* path_count, u
     return WFSA_OK;
 }
 
-int wfsa_dev_objective_grad(wfsa_dev* ctx, const double* w_full, double* loglik, double* grad_full, double* logq) {
+int wfsa_dev_objective_grad_begin(wfsa_dev* ctx, const double* w_full, int want_logq) {
     if (int rc = check_ctx(ctx)) return rc;
     if (!ctx->has_model || !ctx->has_corpus) return fail(WFSA_ERR_ARG, "load a model and a corpus first");
     if (!w_full && ctx->n_params > 0) return fail(WFSA_ERR_ARG, "null weights");
+    if (ctx->in_flight) return fail(WFSA_ERR_ARG, "objective_grad_begin called twice without _end");
     if (ctx->prep_level < 2)
         if (int rc = prepare(ctx, 2)) return rc;
     hipStream_t s = ctx->stream;
@@ -817,7 +820,7 @@ int wfsa_dev_objective_grad(wfsa_dev* ctx, const double* w_full, double* loglik,
     if (ctx->use_graph && !ctx->graph_exec && !ctx->graph_failed) {
         // capture once; a capture the runtime rejects falls back to eager launches
         if (hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal) == hipSuccess) {
-            const int rc = enqueue_iteration(ctx);
+            const int rc = enqueue_iteration(ctx, true);
             hipGraph_t g = nullptr;
             const hipError_t e = hipStreamEndCapture(s, &g);
             if (rc == WFSA_OK && e == hipSuccess && g &&
@@ -835,22 +838,37 @@ int wfsa_dev_objective_grad(wfsa_dev* ctx, const double* w_full, double* loglik,
         }
     }
     if (ctx->graph_exec) HIP_TRY(hipGraphLaunch(ctx->graph_exec, s));
-    else if (int rc = enqueue_iteration(ctx)) return rc;
+    else if (int rc = enqueue_iteration(ctx, want_logq != 0)) return rc;
     if (ctx->comm) {
         RCCL_TRY(ncclAllReduce(ctx->out.ptr, ctx->out.ptr, size_t(np) + 1, ncclDouble, ncclSum, ctx->comm, s));
         HIP_TRY(hipMemcpyAsync(res, ctx->out.ptr, (size_t(np) + 1) * sizeof(double), hipMemcpyDeviceToHost, s));
     }
-    if (logq) HIP_TRY(ctx->logq.download(logq, size_t(ctx->n_strings), s));
     HIP_TRY(hipEventRecord(ctx->ev1, s));
+    ctx->in_flight = true;
+    ctx->logq_ready = want_logq != 0 || ctx->graph_exec != nullptr;
+    return WFSA_OK;
+}
+
+int wfsa_dev_objective_grad_end(wfsa_dev* ctx, double* loglik, double* grad_full, double* logq) {
+    if (int rc = check_ctx(ctx)) return rc;
+    if (!ctx->in_flight) return fail(WFSA_ERR_ARG, "objective_grad_end without _begin");
+    ctx->in_flight = false;
+    hipStream_t s = ctx->stream;
+    const int32_t np = ctx->n_params;
     HIP_TRY(hipStreamSynchronize(s));
+    if (logq) {
+        if (!ctx->logq_ready) return fail(WFSA_ERR_ARG, "log q was not requested at _begin");
+        HIP_TRY(ctx->logq.download(logq, size_t(ctx->n_strings), s));
+        HIP_TRY(hipStreamSynchronize(s));
+    }
     float c_ms = 0.f, f_ms = 0.f, all_ms = 0.f;
     if (!ctx->graph_exec) {   // events recorded inside a captured graph are not timeable
         HIP_TRY(hipEventElapsedTime(&c_ms, ctx->k0, ctx->k1));
         HIP_TRY(hipEventElapsedTime(&f_ms, ctx->k1, ctx->k2));
     }
     HIP_TRY(hipEventElapsedTime(&all_ms, ctx->ev0, ctx->ev1));
-    if (loglik) *loglik = res[0];
-    if (grad_full && np > 0) std::memcpy(grad_full, res + 1, size_t(np) * sizeof(double));
+    if (loglik) *loglik = ctx->pinned[0];
+    if (grad_full && np > 0) std::memcpy(grad_full, ctx->pinned + 1, size_t(np) * sizeof(double));
     ctx->stats.fb_launches += 1;
     ctx->stats.fb_kernel_ms += double(c_ms) + double(f_ms);
     ctx->stats.last_fb_kernel_ms = double(c_ms) + double(f_ms);
@@ -859,6 +877,11 @@ int wfsa_dev_objective_grad(wfsa_dev* ctx, const double* w_full, double* loglik,
     ctx->stats.last_call_ms = double(all_ms);
     ctx->stats.graph = ctx->graph_exec ? 1 : 0;
     return WFSA_OK;
+}
+
+int wfsa_dev_objective_grad(wfsa_dev* ctx, const double* w_full, double* loglik, double* grad_full, double* logq) {
+    if (int rc = wfsa_dev_objective_grad_begin(ctx, w_full, logq != nullptr)) return rc;
+    return wfsa_dev_objective_grad_end(ctx, loglik, grad_full, logq);
 }
 
 int wfsa_dev_comm_unique_id(uint8_t id[WFSA_COMM_ID_BYTES]) {

@@ -262,17 +262,18 @@ class QuasiNewtonLearner:
         return names
 
     def run(self, flags=7, epochs=20, eta=1.0, tol=1e-6):
-        """main.cpp's epoch loop (src/main.cpp:276-303): list of info rows"""
+        """main.cpp's epoch loop (src/main.cpp:276-303), run natively by
+        wfsa_learner_run: list of info rows (the epochs actually run)"""
         self.Init(flags)
-        rows = []
-        for _ in range(epochs):
-            info, halt = self.OptimizationStep(eta, tol)
-            rows.append(info)
-            if not np.all(np.isfinite(info)):
-                raise WfsaError(-1, "non-finite epoch info")
-            if halt:
-                break
-        return rows
+        return self.Run(epochs, eta, tol)
+
+    def Run(self, epochs, eta=1.0, tol=1e-6):
+        """up to `epochs` OptimizationSteps in one native call (no Init)"""
+        rows = np.zeros((max(epochs, 0), 7))
+        done = C.c_int32(0)
+        rc = load().wfsa_learner_run(self._h, eta, tol, int(epochs), _ptr(rows), C.byref(done))
+        check_host(rc)
+        return [list(r) for r in rows[:done.value]]
 
 
 class Device:
@@ -317,6 +318,19 @@ class Device:
         logq = np.zeros(self.n_strings, dtype=np.float64) if want_logq else None
         ll = C.c_double()
         check_dev(load().wfsa_dev_objective_grad(self._h, _ptr(w), C.byref(ll), _ptr(grad), _ptr(logq)))
+        return ll.value, grad[:self.n_params], logq
+
+    def objective_grad_begin(self, w_full, want_logq=True):
+        """enqueue the evaluation and return (wfsa_dev_objective_grad_begin)"""
+        self._w_keep = np.ascontiguousarray(w_full, dtype=np.float64)
+        self._want_logq = want_logq
+        check_dev(load().wfsa_dev_objective_grad_begin(self._h, _ptr(self._w_keep), int(want_logq)))
+
+    def objective_grad_end(self):
+        grad = np.zeros(max(self.n_params, 1), dtype=np.float64)
+        logq = np.zeros(self.n_strings, dtype=np.float64) if getattr(self, "_want_logq", False) else None
+        ll = C.c_double()
+        check_dev(load().wfsa_dev_objective_grad_end(self._h, C.byref(ll), _ptr(grad), _ptr(logq)))
         return ll.value, grad[:self.n_params], logq
 
     def comm_init(self, nranks, rank, unique_id):
