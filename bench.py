@@ -151,7 +151,7 @@ def main():
     # for the strings the compiled kernel serves
     comp = st1["compiled_strings"]
     alg_bytes = int(local_sym * comp / max(local_strings, 1)) + 16 * comp
-    achieved = alg_bytes / (kern_ms * 1e-3) / 1e9
+    achieved = alg_bytes / (kern_ms * 1e-3) / 1e9 if kern_ms > 0 else None   # None: WFSA_TIMING=0
     traffic = None
     if os.path.exists(args.profile_traffic):
         try:
@@ -186,13 +186,17 @@ def main():
             "achieved": achieved,
             "peak": HBM_PEAK_GBS,
             "unit": "GB/s",
-            "frac": achieved / HBM_PEAK_GBS,
+            "frac": achieved / HBM_PEAK_GBS if achieved else None,
             "traffic": traffic,
             "kernel": "fbc_kernel (compiled-stream forward-backward)",
             "kernel_ms_per_launch": kern_ms,
             "all_fb_kernels_ms_per_step": fb_ms,
             "algorithmic_bytes_per_launch": alg_bytes,
         },
+        "host_ms_per_step": {k: (st1["host_" + k + "_ms"] - st0["host_" + k + "_ms"]) /
+                             max(st1["host_steps"] - st0["host_steps"], 1)
+                             for k in ("begin", "overlap", "wait", "post")},
+        "device_call_ms_last": st1["last_call_ms"],
         "live_edges_per_step": st1["last_live_edges"],
         "build_s": t_build,
         "tier1_strings": st1["tier1_strings"],

@@ -93,6 +93,12 @@ typedef struct {
     double compiled_kernel_ms; /* sum over calls of the compiled kernel     */
     int32_t graph;             /* last call replayed a captured hipGraph    */
     int32_t reserved;
+    /* filled by wfsa_learner_stats (zero from wfsa_dev_get_stats): host time
+     * of the learner's optimization steps, summed over host_steps steps --
+     * before the device call is enqueued, overlapped with it, waiting for
+     * it, after it (gradient mapping + update) */
+    int64_t host_steps;
+    double host_begin_ms, host_overlap_ms, host_wait_ms, host_post_ms;
 } wfsa_dev_stats;
 
 /* context ---------------------------------------------------------------- */

@@ -1,6 +1,7 @@
 #include "QuasiNewtonLearner.hpp"
 
 #include <algorithm>
+#include <chrono>
 #include <cmath>
 
 namespace wfsa {
@@ -78,10 +79,15 @@ void QuasiNewtonLearner::OptimizationStep(double eta, bool) {   // :162-201
     // ComputeExpX and ComputeG do not depend on the gradient: run them on
     // the host while the device evaluates (same results as the reference's
     // ExpX, G, Grad order).
+    using clk = std::chrono::steady_clock;
+    const auto t0 = clk::now();
     BeginModeledProbs();
+    const auto t1 = clk::now();
     ComputeExpX();
     ComputeG();
+    const auto t2 = clk::now();
     EndModeledProbs(grad_cache);
+    const auto t3 = clk::now();
     grad = grad_cache;
     ComputeObjective();
     const size_t n = _x.size(), k = lambda.size();
@@ -101,6 +107,13 @@ void QuasiNewtonLearner::OptimizationStep(double eta, bool) {   // :162-201
     }
     for (size_t c = 0; c < k; ++c) laux[c] = lambda[c] - laux[c];
     LambdaUpdate(laux.data(), lambda.data(), eta, exponential_lambda);
+    const auto t4 = clk::now();
+    auto ms = [](clk::time_point a, clk::time_point b) { return std::chrono::duration<double, std::milli>(b - a).count(); };
+    timing.steps += 1;
+    timing.begin_ms += ms(t0, t1);
+    timing.overlap_ms += ms(t1, t2);
+    timing.wait_ms += ms(t2, t3);
+    timing.post_ms += ms(t3, t4);
 }
 
 }  // namespace wfsa

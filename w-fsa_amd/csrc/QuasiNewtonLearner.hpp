@@ -22,6 +22,12 @@ public:
     void ComputeG();
     void ComputeGrad();
 
+    struct Timing {
+        int64_t steps = 0;
+        double begin_ms = 0, overlap_ms = 0, wait_ms = 0, post_ms = 0;
+    };
+    const Timing& StepTiming() const { return timing; }
+
 protected:
     void FinalizeCallback() override;
     void InitCallback(int flags) override;
@@ -31,6 +37,7 @@ private:
     std::vector<double> grad, expx, lambda, g, rhs;
     double grad_error = 0, lambda_min = 0, g_min = 0, g_max = 0;
     bool exponential_lambda = false;
+    Timing timing;
 };
 
 }  // namespace wfsa

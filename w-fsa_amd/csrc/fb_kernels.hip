@@ -497,19 +497,29 @@ __global__ __launch_bounds__(256) void trav_kernel(TravArgs a) {
 // chunk in flight while the current one is applied).  Multi-parameter words
 // (rare) read the edge's log-weight and parameter list from global memory.
 // Groups are dealt to waves in snake order (longest first) to balance them.
-template <int TABLES, bool WIDE>   // TABLES 2: w + grad in LDS, 1: grad in LDS, 0: none
+//
+// GRAD == false is the per-iteration form: a trivial word's posterior is 1
+// whatever the weights, so its gradient contribution -p_s is a constant of
+// the corpus (the reference keeps the same constant for unique-path corpora,
+// grad_aux = -P^T p, src/QuasiNewtonLearner.cpp:95-101).  It is accumulated
+// once (GRAD == true, at preparation) and added by the tail kernel; every
+// iteration then only sums the words' log-weights per string (log q) -- no
+// atomics.  TABLES then means: 2 or 1 = w staged in LDS, 0 = w from global.
+template <int TABLES, bool WIDE, bool GRAD>   // GRAD: TABLES 2 w + grad in LDS, 1 grad in LDS, 0 none
 __global__ __launch_bounds__(1024) void fbc_kernel(CompiledArgs a) {
     extern __shared__ __attribute__((aligned(16))) double lds[];
-    double* gacc = lds;                 // [n_params] when TABLES >= 1
-    double* wl = lds + a.n_params;      // [n_params] when TABLES == 2
+    double* gacc = lds;                              // [n_params] when GRAD && TABLES >= 1
+    double* wl = GRAD ? lds + a.n_params : lds;      // [n_params] when w is staged
+    constexpr bool W_LDS = GRAD ? TABLES == 2 : TABLES >= 1;
+    constexpr bool G_LDS = GRAD && TABLES >= 1;
     const int lane = lane_id();
     const int wpb = int(blockDim.x) / kWave;
     const int gw = int(blockIdx.x) * wpb + int(threadIdx.x) / kWave;
     const int nw = int(gridDim.x) * wpb;
     if (TABLES >= 1) {
         for (int j = int(threadIdx.x); j < a.n_params; j += int(blockDim.x)) {
-            gacc[j] = 0.0;
-            if (TABLES == 2) wl[j] = a.w[j];
+            if (G_LDS) gacc[j] = 0.0;
+            if (W_LDS) wl[j] = a.w[j];
         }
         // this block's slice of the per-edge weights (bubbles and the
         // traversal fallback read them after this launch), and the zeroed
@@ -528,7 +538,7 @@ __global__ __launch_bounds__(1024) void fbc_kernel(CompiledArgs a) {
             for (int j = int(threadIdx.x); j <= a.n_params; j += int(blockDim.x)) a.out[j] = 0.0;
         __syncthreads();
     }
-    const double* wsrc = TABLES == 2 ? wl : a.w;
+    const double* wsrc = W_LDS ? wl : a.w;
     constexpr int PER = WIDE ? 4 : 8;   // words per 16-byte chunk
     const uint4 pad = make_uint4(0xffffffffu, 0xffffffffu, 0xffffffffu, 0xffffffffu);
     double ll_acc = 0.0;
@@ -536,14 +546,14 @@ __global__ __launch_bounds__(1024) void fbc_kernel(CompiledArgs a) {
     auto apply = [&](int j_single, int g_multi, double p, double& acc) {
         if (j_single >= 0) {
             acc += wsrc[j_single];
-            if (TABLES >= 1) block_add(&gacc[j_single], -p);
-            else global_add(&a.grad[j_single], -p);
+            if (G_LDS) block_add(&gacc[j_single], -p);
+            else if (GRAD) global_add(&a.grad[j_single], -p);
         } else if (g_multi >= 0) {
             for (int q = a.m.pptr[g_multi]; q < a.m.pptr[g_multi + 1]; ++q) {
                 const int j = a.m.pidx[q];
                 acc += wsrc[j];
-                if (TABLES >= 1) block_add(&gacc[j], -p);
-                else global_add(&a.grad[j], -p);
+                if (G_LDS) block_add(&gacc[j], -p);
+                else if (GRAD) global_add(&a.grad[j], -p);
             }
         }
     };
@@ -593,7 +603,7 @@ __global__ __launch_bounds__(1024) void fbc_kernel(CompiledArgs a) {
     }
     ll_acc = wave_sum(ll_acc);
     if (lane == 0) a.ll_part[gw] = ll_acc;
-    if (TABLES >= 1) {   // this block's partial gradient, summed by the tail kernel
+    if (G_LDS) {   // this block's partial gradient, summed by the tail kernel
         __syncthreads();
         double* slab = a.gpart + size_t(blockIdx.x) * size_t(a.n_params);
         for (int j = int(threadIdx.x); j < a.n_params; j += int(blockDim.x)) slab[j] = gacc[j];
@@ -646,6 +656,25 @@ __global__ __launch_bounds__(kBubbleBlock) void bubble_kernel(BubbleArgs a) {
     if (lane == 0) a.ll_part[gw] = ll_acc;
 }
 
+// One block copies out[0, n) to host-mapped memory in 16-byte stores (n
+// rounded up to even; both buffers are padded), fences at system scope and
+// stores the next sequence number into the host-mapped flag.  A separate
+// launch after the reductions: the kernel boundary makes their results
+// visible, where a last-block ticket would need an L2 write-back per block.
+__global__ __launch_bounds__(256) void publish_kernel(const double* out, Publish pub) {
+    const int n2 = (pub.n + 1) / 2;
+    const double2* src = reinterpret_cast<const double2*>(out);
+    double2* dst = reinterpret_cast<double2*>(pub.host_out);
+    for (int i = int(threadIdx.x); i < n2; i += int(blockDim.x)) dst[i] = src[i];
+    __threadfence_system();
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const unsigned v = *pub.seq + 1u;
+        *pub.seq = v;
+        __hip_atomic_store(pub.host_flag, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+}
+
 __global__ __launch_bounds__(256) void tail_kernel(TailArgs a) {
     const int n_tiles = (a.n_params + 255) / 256;
     const int n_slab_groups = (a.n_gpart + kTailSlabs - 1) / kTailSlabs;
@@ -655,19 +684,21 @@ __global__ __launch_bounds__(256) void tail_kernel(TailArgs a) {
     if (b < n_param_blocks) {             // column sums of kTailSlabs partial slabs
         const int j = (b % n_tiles) * 256 + int(threadIdx.x);
         const int k0 = (b / n_tiles) * kTailSlabs;
-        if (j >= a.n_params) return;
-        const int k1 = min(a.n_gpart, k0 + kTailSlabs);
-        double s = 0.0;
-        for (int k = k0; k < k1; ++k) s += a.gpart[size_t(k) * size_t(a.n_params) + size_t(j)];
-        if (s != 0.0) global_add(&a.out[1 + j], s);
+        if (j < a.n_params) {
+            const int k1 = min(a.n_gpart, k0 + kTailSlabs);
+            double s = 0.0;
+            for (int k = k0; k < k1; ++k) s += a.gpart[size_t(k) * size_t(a.n_params) + size_t(j)];
+            if (s != 0.0) global_add(&a.out[1 + j], s);
+        }
     } else if (b < n_param_blocks + n_chunk_blocks) {   // bubble contributions
         const int c = (b - n_param_blocks) * 4 + int(threadIdx.x) / kWave;
-        if (c >= a.n_chunks) return;
-        const int lane = lane_id();
-        double s = 0.0;
-        for (int k = a.chunk_ptr[c] + lane; k < a.chunk_ptr[c + 1]; k += kWave) s += a.contrib[a.slot[k]];
-        s = wave_sum(s);
-        if (lane == 0) global_add(&a.out[1 + a.chunk_param[c]], s);
+        if (c < a.n_chunks) {
+            const int lane = lane_id();
+            double s = 0.0;
+            for (int k = a.chunk_ptr[c] + lane; k < a.chunk_ptr[c + 1]; k += kWave) s += a.contrib[a.slot[k]];
+            s = wave_sum(s);
+            if (lane == 0) global_add(&a.out[1 + a.chunk_param[c]], s);
+        }
     } else {                              // log-likelihood, fixed order
         __shared__ double red[256];
         double s = 0.0;
@@ -678,8 +709,15 @@ __global__ __launch_bounds__(256) void tail_kernel(TailArgs a) {
             if (int(threadIdx.x) < w) red[threadIdx.x] += red[threadIdx.x + w];
             __syncthreads();
         }
-        if (threadIdx.x == 0) a.out[0] = red[0];
+        if (threadIdx.x == 0) global_add(&a.out[0], red[0]);
     }
+}
+
+// host-mapped weights -> device, 16-byte loads (both buffers padded to even)
+__global__ __launch_bounds__(256) void stage_kernel(const double2* __restrict__ host_w, double2* __restrict__ w,
+                                                    int32_t n2) {
+    for (int32_t i = int32_t(blockIdx.x * blockDim.x + threadIdx.x); i < n2; i += int32_t(gridDim.x * blockDim.x))
+        w[i] = host_w[i];
 }
 
 // Per iteration: log-weight, weight and parameter record of every combined
@@ -714,12 +752,16 @@ hipError_t configure_kernels(int max_dynamic_lds) {
     const void* fns[] = {reinterpret_cast<const void*>(&trav_kernel<MODE_WEIGHTED>),
                          reinterpret_cast<const void*>(&trav_kernel<MODE_COUNT>),
                          reinterpret_cast<const void*>(&trav_kernel<MODE_EMIT>),
-                         reinterpret_cast<const void*>(&fbc_kernel<0, false>),
-                         reinterpret_cast<const void*>(&fbc_kernel<1, false>),
-                         reinterpret_cast<const void*>(&fbc_kernel<2, false>),
-                         reinterpret_cast<const void*>(&fbc_kernel<0, true>),
-                         reinterpret_cast<const void*>(&fbc_kernel<1, true>),
-                         reinterpret_cast<const void*>(&fbc_kernel<2, true>)};
+                         reinterpret_cast<const void*>(&fbc_kernel<0, false, true>),
+                         reinterpret_cast<const void*>(&fbc_kernel<1, false, true>),
+                         reinterpret_cast<const void*>(&fbc_kernel<2, false, true>),
+                         reinterpret_cast<const void*>(&fbc_kernel<0, true, true>),
+                         reinterpret_cast<const void*>(&fbc_kernel<1, true, true>),
+                         reinterpret_cast<const void*>(&fbc_kernel<2, true, true>),
+                         reinterpret_cast<const void*>(&fbc_kernel<0, false, false>),
+                         reinterpret_cast<const void*>(&fbc_kernel<1, false, false>),
+                         reinterpret_cast<const void*>(&fbc_kernel<0, true, false>),
+                         reinterpret_cast<const void*>(&fbc_kernel<1, true, false>)};
     for (const void* f : fns) {
         hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, max_dynamic_lds);
         if (e != hipSuccess) return e;
@@ -746,14 +788,22 @@ hipError_t launch_trav(TravMode mode, const TravArgs& a, int grid, hipStream_t s
 
 hipError_t launch_compiled(const CompiledArgs& a, int grid, int block, size_t lds, hipStream_t stream) {
     const dim3 g{unsigned(grid), 1, 1}, b{unsigned(block), 1, 1};
+    if (!a.with_grad) {   // per-iteration form: w staged in LDS or read from global
+        const bool t = a.tables >= 1;
+        if (t && a.wide) hipLaunchKernelGGL((fbc_kernel<1, true, false>), g, b, lds, stream, a);
+        else if (t) hipLaunchKernelGGL((fbc_kernel<1, false, false>), g, b, lds, stream, a);
+        else if (a.wide) hipLaunchKernelGGL((fbc_kernel<0, true, false>), g, b, 0, stream, a);
+        else hipLaunchKernelGGL((fbc_kernel<0, false, false>), g, b, 0, stream, a);
+        return hipGetLastError();
+    }
     const int key = a.tables * 2 + (a.wide ? 1 : 0);
     switch (key) {
-        case 4: hipLaunchKernelGGL((fbc_kernel<2, false>), g, b, lds, stream, a); break;
-        case 5: hipLaunchKernelGGL((fbc_kernel<2, true>), g, b, lds, stream, a); break;
-        case 2: hipLaunchKernelGGL((fbc_kernel<1, false>), g, b, lds, stream, a); break;
-        case 3: hipLaunchKernelGGL((fbc_kernel<1, true>), g, b, lds, stream, a); break;
-        case 1: hipLaunchKernelGGL((fbc_kernel<0, true>), g, b, 0, stream, a); break;
-        default: hipLaunchKernelGGL((fbc_kernel<0, false>), g, b, 0, stream, a); break;
+        case 4: hipLaunchKernelGGL((fbc_kernel<2, false, true>), g, b, lds, stream, a); break;
+        case 5: hipLaunchKernelGGL((fbc_kernel<2, true, true>), g, b, lds, stream, a); break;
+        case 2: hipLaunchKernelGGL((fbc_kernel<1, false, true>), g, b, lds, stream, a); break;
+        case 3: hipLaunchKernelGGL((fbc_kernel<1, true, true>), g, b, lds, stream, a); break;
+        case 1: hipLaunchKernelGGL((fbc_kernel<0, true, true>), g, b, 0, stream, a); break;
+        default: hipLaunchKernelGGL((fbc_kernel<0, false, true>), g, b, 0, stream, a); break;
     }
     return hipGetLastError();
 }
@@ -768,6 +818,20 @@ hipError_t launch_tail(const TailArgs& a, hipStream_t stream) {
     const int blocks = (a.n_params + 255) / 256 * ((a.n_gpart + kTailSlabs - 1) / kTailSlabs) +
                        (a.n_chunks + 3) / 4 + 1;
     hipLaunchKernelGGL(tail_kernel, dim3(unsigned(blocks)), dim3(256), 0, stream, a);
+    return hipGetLastError();
+}
+
+hipError_t launch_publish(const double* out, const Publish& pub, hipStream_t stream) {
+    hipLaunchKernelGGL(publish_kernel, dim3(1), dim3(256), 0, stream, out, pub);
+    return hipGetLastError();
+}
+
+hipError_t launch_stage(const double* host_w, double* w, int32_t n, hipStream_t stream) {
+    if (n <= 0) return hipSuccess;
+    const int32_t n2 = (n + 1) / 2;
+    const unsigned blocks = unsigned(std::min<int32_t>(8, (n2 + 255) / 256));
+    hipLaunchKernelGGL(stage_kernel, dim3(blocks), dim3(256), 0, stream, reinterpret_cast<const double2*>(host_w),
+                       reinterpret_cast<double2*>(w), n2);
     return hipGetLastError();
 }
 

@@ -139,8 +139,10 @@ struct CompiledArgs {
     const int32_t* l_len;    // [64 G] words of each lane
     int32_t n_groups;
     int32_t n_params;
-    int32_t tables;          // 2: w and grad staged in LDS, 1: grad in LDS, 0: global
+    int32_t tables;          // with_grad: 2 w and grad staged in LDS, 1 grad in LDS, 0 global;
+                             // else: >= 1 w staged in LDS, 0 global
     int32_t wide;
+    int32_t with_grad;       // accumulate the (weight-independent) trivial-word gradient
     const double* w;         // [n_params] w_full (GetWeight form)
     double* grad;            // [n_params] (TABLES == 0: atomics straight into it)
     double* gpart;           // [grid][n_params] per-block partial gradients (TABLES >= 1)
@@ -173,6 +175,15 @@ struct BubbleArgs {
 // chunk, so a hot parameter's long list is summed by many waves), and
 // out[0] = sum of the per-wave log-likelihood partials in a fixed order.
 constexpr int kBubbleGradChunk = 512;
+// Completion without a DMA copy or a stream synchronisation: a one-block
+// kernel copies out[0, n) into host-mapped memory, fences at system scope and
+// then stores the next sequence number into a host-mapped flag the host polls.
+struct Publish {
+    double* host_out;            // host-mapped [n rounded up to even]
+    int32_t n;
+    unsigned* seq;               // device sequence counter
+    unsigned* host_flag;         // host-mapped: last published sequence number
+};
 constexpr int kTailSlabs = 8;    // partial slabs summed per thread
 struct TailArgs {
     const double* gpart;         // [n_gpart][n_params]
@@ -194,6 +205,10 @@ hipError_t launch_compiled(const CompiledArgs& a, int grid, int block, size_t ld
 constexpr int kBubbleBlock = 128;
 hipError_t launch_bubbles(const BubbleArgs& a, int grid, hipStream_t stream);
 hipError_t launch_tail(const TailArgs& a, hipStream_t stream);
+// out[0, n) -> host-mapped memory, then the flag (one block)
+hipError_t launch_publish(const double* out, const Publish& pub, hipStream_t stream);
+// host-mapped weights -> device (buffers padded to an even count)
+hipError_t launch_stage(const double* host_w, double* w, int32_t n, hipStream_t stream);
 // also zeroes out[0..n_out) (the accumulators of this iteration)
 hipError_t launch_edge_weights(const double* w_full, const int32_t* pptr, const int32_t* pidx, double* lw,
                                double* ew, EdgeRec* erec, int64_t n_edges, double* out, int64_t n_out,

@@ -353,7 +353,16 @@ int wfsa_learner_stats(wfsa_learner* l, wfsa_dev_stats* out) {
         g_host_error = "learner has no device context yet";
         return WFSA_ERR_ARG;
     }
-    return wfsa_dev_get_stats(l->qn->Device(), out);
+    const int rc = wfsa_dev_get_stats(l->qn->Device(), out);
+    if (rc == WFSA_OK) {
+        const auto& t = l->qn->StepTiming();
+        out->host_steps = t.steps;
+        out->host_begin_ms = t.begin_ms;
+        out->host_overlap_ms = t.overlap_ms;
+        out->host_wait_ms = t.wait_ms;
+        out->host_post_ms = t.post_ms;
+    }
+    return rc;
 }
 
 int wfsa_shard_range(const int64_t* off, int64_t n, int nranks, int rank, int64_t* begin, int64_t* end) {

@@ -96,6 +96,10 @@ constexpr int kLdsPerCu = 163840;
 constexpr int kNumCu = 256;
 constexpr int kWave = 64;
 constexpr int kCompiledBlock = 512;
+constexpr int kMaxWavesPerCu = 32;
+
+// weights after the results in the host-mapped buffer, 16-byte aligned
+inline size_t weights_off(int32_t np) { return (size_t(np) + 3) & ~size_t(1); }
 
 }  // namespace
 
@@ -103,7 +107,7 @@ struct wfsa_dev {
     int device = 0;
     int n_cu = kNumCu;
     hipStream_t stream = nullptr;
-    hipEvent_t ev0 = nullptr, ev1 = nullptr, k0 = nullptr, k1 = nullptr, k2 = nullptr;
+    hipEvent_t ev0 = nullptr, ev1 = nullptr, k0 = nullptr, kc = nullptr, k1 = nullptr, k2 = nullptr;
 
     // model
     bool has_model = false;
@@ -143,7 +147,11 @@ struct wfsa_dev {
     int wide = 0;             // 32-bit stream words
     DevBuf<int32_t> bub, g_len, l_str, l_len;
     DevBuf<int64_t> g_base;
-    int c_grid = 0, c_tables = 0;
+    int c_grid = 0, c_tables = 0;    // gradient pass (once, at preparation)
+    int i_grid = 0, i_tables = 0;    // per-iteration pass (log-weights only)
+    int i_block = 1024;
+    size_t i_lds = 0;
+    DevBuf<double> fixed_grad;       // [n_params] gradient of the trivial words (constant)
     // bubbles
     int32_t n_bubbles = 0;
     int b_grid = 0;
@@ -161,8 +169,16 @@ struct wfsa_dev {
     // work buffers
     DevBuf<double> w_full, out, ll_part, logq;
     DevBuf<unsigned long long> live;
-    double* pinned = nullptr;   // [0, n_params+1): results; [n_params+1, 2 n_params+1): weights
+    double* pinned = nullptr;   // [0, n_params+1): results; from weights_off(n_params): weights
+    double* pinned_dev = nullptr;   // the same memory as the device addresses it
     size_t pinned_n = 0;
+    // completion flag (host-mapped) and the device sequence counter
+    unsigned* flag = nullptr;
+    unsigned* flag_dev = nullptr;
+    DevBuf<unsigned> counters;   // [0] sequence
+    unsigned seq = 0;            // last sequence number the host expects
+    bool timing_pending = false; // events of the last call not yet read
+    bool kernel_timing = true;
     DevBuf<double> gpart;        // per-block partial gradients of the compiled kernel
 
     // the per-iteration device sequence, captured once per prepared corpus
@@ -284,6 +300,63 @@ int configure_tiers(wfsa_dev* ctx) {
 // Structural pass (level 1) + stream compilation (level 2) for the loaded
 // corpus.
 void drop_graph(wfsa_dev* ctx);
+
+int enqueue_compiled(wfsa_dev* ctx, bool with_grad, bool want_logq);
+
+// per-kernel timing events (WFSA_TIMING=0 leaves them out)
+hipError_t record(wfsa_dev* ctx, hipEvent_t ev, hipStream_t s) {
+    return ctx->kernel_timing ? hipEventRecord(ev, s) : hipSuccess;
+}
+
+wfsa::Publish publish_args(wfsa_dev* ctx) {
+    wfsa::Publish p{};
+    p.host_out = ctx->pinned_dev;
+    p.n = ctx->n_params + 1;
+    p.seq = ctx->counters.ptr;
+    p.host_flag = ctx->flag_dev;
+    return p;
+}
+
+// Event timings of the previous call, read once its events have completed.
+int collect_timing(wfsa_dev* ctx) {
+    if (!ctx->timing_pending) return WFSA_OK;
+    ctx->timing_pending = false;
+    HIP_TRY(hipEventSynchronize(ctx->ev1));
+    float c_ms = 0.f, b_ms = 0.f, f_ms = 0.f, all_ms = 0.f;
+    if (!ctx->graph_exec && ctx->kernel_timing) {   // events inside a captured graph are not timeable
+        HIP_TRY(hipEventElapsedTime(&c_ms, ctx->k0, ctx->kc));
+        HIP_TRY(hipEventElapsedTime(&b_ms, ctx->kc, ctx->k1));
+        HIP_TRY(hipEventElapsedTime(&f_ms, ctx->k1, ctx->k2));
+    }
+    HIP_TRY(hipEventElapsedTime(&all_ms, ctx->ev0, ctx->ev1));
+    const double fb = double(c_ms) + double(b_ms) + double(f_ms);
+    ctx->stats.fb_launches += 1;
+    ctx->stats.fb_kernel_ms += fb;
+    ctx->stats.last_fb_kernel_ms = fb;
+    ctx->stats.last_compiled_ms = double(c_ms);
+    ctx->stats.compiled_kernel_ms += double(c_ms);
+    ctx->stats.last_call_ms = double(all_ms);
+    ctx->stats.graph = ctx->graph_exec ? 1 : 0;
+    return WFSA_OK;
+}
+
+// Wait for the published sequence number: poll the host-mapped flag, and
+// the stream now and then so a failed launch surfaces as an error.
+int wait_published(wfsa_dev* ctx) {
+    const unsigned want = ctx->seq;
+    for (uint64_t spin = 1;; ++spin) {
+        if (__atomic_load_n(ctx->flag, __ATOMIC_ACQUIRE) == want) return WFSA_OK;
+        if ((spin & 0x3fff) == 0) {
+            const hipError_t e = hipStreamQuery(ctx->stream);
+            if (e == hipSuccess) {
+                if (__atomic_load_n(ctx->flag, __ATOMIC_ACQUIRE) == want) return WFSA_OK;
+                return fail(WFSA_ERR_HIP, "device finished without publishing the result (sequence %u)", want);
+            }
+            if (e != hipErrorNotReady) return fail(WFSA_ERR_HIP, "device failure: %s", hipGetErrorString(e));
+        }
+        __builtin_ia32_pause();
+    }
+}
 
 int prepare(wfsa_dev* ctx, int level) {
     const auto t_start = std::chrono::steady_clock::now();
@@ -518,10 +591,21 @@ int prepare(wfsa_dev* ctx, int level) {
         ctx->c_lds = 0;
     }
     const int waves_per_block = kCompiledBlock / kWave;
+    const int64_t want_blocks = (int64_t(G) + waves_per_block - 1) / waves_per_block;
     const int per_cu = ctx->c_tables ? 1 : 2;
-    ctx->c_grid = int(std::max<int64_t>(1, std::min<int64_t>(int64_t(ctx->n_cu) * per_cu,
-                                                             (int64_t(G) + waves_per_block - 1) / waves_per_block)));
+    ctx->c_grid = int(std::max<int64_t>(1, std::min<int64_t>(int64_t(ctx->n_cu) * per_cu, want_blocks)));
     if (ctx->c_tables >= 1) HIP_TRY(ctx->gpart.alloc(size_t(ctx->c_grid) * size_t(std::max(ctx->n_params, 1))));
+    // the per-iteration pass keeps only w in LDS: as many blocks per CU as fit
+    ctx->i_tables = table_bytes <= size_t(kLdsPerCu - 1024) ? 1 : 0;
+    ctx->i_lds = ctx->i_tables ? table_bytes : 0;
+    if (const char* e = std::getenv("WFSA_IBLOCK")) ctx->i_block = std::max(64, std::min(1024, std::atoi(e))) & ~63;
+    const int i_wpb = ctx->i_block / kWave;
+    int i_per_cu = kMaxWavesPerCu / i_wpb;
+    if (ctx->i_tables) i_per_cu = std::min<int>(i_per_cu, int(size_t(kLdsPerCu) / std::max<size_t>(table_bytes, 1)));
+    i_per_cu = std::max(1, i_per_cu);
+    ctx->i_grid = int(std::max<int64_t>(1, std::min<int64_t>(int64_t(ctx->n_cu) * i_per_cu,
+                                                             (int64_t(G) + i_wpb - 1) / i_wpb)));
+    HIP_TRY(ctx->fixed_grad.alloc(size_t(std::max(ctx->n_params, 1))));
 
     // traversal fallback lists
     for (int t = 0; t < 2; ++t) {
@@ -529,10 +613,21 @@ int prepare(wfsa_dev* ctx, int level) {
         ctx->fall_grid[t] = fb[t].empty() ? 0 : trav_grid(ctx->cfg[t], ctx->n_cu, int64_t(fb[t].size()));
         if (!fb[t].empty()) HIP_TRY(ctx->fall[t].upload(fb[t].data(), fb[t].size(), s));
     }
-    const size_t waves = size_t(ctx->c_grid) * waves_per_block + size_t(ctx->b_grid) * (wfsa::kBubbleBlock / kWave) +
+    const size_t waves = std::max(size_t(ctx->c_grid) * waves_per_block, size_t(ctx->i_grid) * size_t(i_wpb)) +
+                         size_t(ctx->b_grid) * (wfsa::kBubbleBlock / kWave) +
                          size_t(ctx->fall_grid[0]) * size_t(ctx->cfg[0].waves_per_block) +
                          size_t(ctx->fall_grid[1]) * size_t(ctx->cfg[1].waves_per_block);
     HIP_TRY(ctx->ll_part.alloc(waves));
+    HIP_TRY(hipStreamSynchronize(s));
+
+    // the trivial words' gradient, once: compiled pass with gradient at
+    // w = 0 (its log-weights are discarded), then the slab sum
+    if (nc > 0) {
+        HIP_TRY(hipMemsetAsync(ctx->w_full.ptr, 0, size_t(std::max(ctx->n_params, 1)) * sizeof(double), s));
+        if (int rc = enqueue_compiled(ctx, true, false)) return rc;
+        HIP_TRY(hipMemcpyAsync(ctx->fixed_grad.ptr, ctx->out.ptr + 1, size_t(ctx->n_params) * sizeof(double),
+                               hipMemcpyDeviceToDevice, s));
+    }
     HIP_TRY(hipStreamSynchronize(s));
 
     ctx->stats.compiled_strings = nc;
@@ -549,25 +644,19 @@ int prepare(wfsa_dev* ctx, int level) {
     return WFSA_OK;
 }
 
-// The device work of one objective/gradient evaluation, enqueued on the
-// context's stream (captured into a graph on first use): weights in,
-// per-edge weights, compiled streams + bubbles (timed by k0..k1), traversal
-// fallback (k1..k2), the tail reduction, and -- without a communicator --
-// the results out.
-int enqueue_iteration(wfsa_dev* ctx, bool want_logq) {
+// The compiled-stream kernel over the weights in w_full, preceded by the
+// edge-weight kernel unless the kernel folds that into its prologue (it does
+// when it stages w in LDS).  with_grad: the preparation-time gradient pass
+// (followed by its slab reduction into out); else the per-iteration pass.
+int enqueue_compiled(wfsa_dev* ctx, bool with_grad, bool want_logq) {
     hipStream_t s = ctx->stream;
     const int32_t np = ctx->n_params;
-    if (np > 0)
-        HIP_TRY(hipMemcpyAsync(ctx->w_full.ptr, ctx->pinned + np + 1, size_t(np) * sizeof(double),
-                               hipMemcpyHostToDevice, s));
-    // the compiled kernel folds the edge weights and the zeroing of `out`
-    // into its prologue when it keeps its gradient in LDS
-    const bool fused = ctx->n_groups > 0 && ctx->c_tables >= 1;
+    const int tables = with_grad ? ctx->c_tables : ctx->i_tables;
+    const bool fused = ctx->n_groups > 0 && tables >= 1;
     if (!fused)
         HIP_TRY(wfsa::launch_edge_weights(ctx->w_full.ptr, ctx->pptr.ptr, ctx->pidx.ptr, ctx->lw.ptr, ctx->ew.ptr,
                                           ctx->erec.ptr, ctx->n_edges + ctx->n_end, ctx->out.ptr, int64_t(np) + 1, s));
-    int32_t wave_off = 0;
-    HIP_TRY(hipEventRecord(ctx->k0, s));
+    if (!with_grad) HIP_TRY(record(ctx, ctx->k0, s));
     if (ctx->n_groups > 0) {
         wfsa::CompiledArgs c{};
         c.m = model_view(ctx);
@@ -580,7 +669,8 @@ int enqueue_iteration(wfsa_dev* ctx, bool want_logq) {
         c.l_len = ctx->l_len.ptr;
         c.n_groups = ctx->n_groups;
         c.n_params = np;
-        c.tables = ctx->c_tables;
+        c.tables = tables;
+        c.with_grad = with_grad ? 1 : 0;
         c.w = ctx->w_full.ptr;
         c.grad = ctx->out.ptr + 1;
         c.gpart = ctx->gpart.ptr;
@@ -591,9 +681,34 @@ int enqueue_iteration(wfsa_dev* ctx, bool want_logq) {
         c.out = ctx->out.ptr;
         c.ll_part = ctx->ll_part.ptr;
         c.logq = want_logq ? ctx->logq.ptr : nullptr;
-        HIP_TRY(wfsa::launch_compiled(c, ctx->c_grid, kCompiledBlock, ctx->c_lds, s));
-        wave_off += ctx->c_grid * (kCompiledBlock / kWave);
+        if (with_grad) HIP_TRY(wfsa::launch_compiled(c, ctx->c_grid, kCompiledBlock, ctx->c_lds, s));
+        else HIP_TRY(wfsa::launch_compiled(c, ctx->i_grid, ctx->i_block, ctx->i_lds, s));
     }
+    if (!with_grad) HIP_TRY(record(ctx, ctx->kc, s));
+    if (with_grad) {
+        wfsa::TailArgs t{};
+        t.gpart = ctx->gpart.ptr;
+        t.n_gpart = (ctx->n_groups > 0 && ctx->c_tables >= 1) ? ctx->c_grid : 0;
+        t.n_params = np;
+        t.ll_part = ctx->ll_part.ptr;
+        t.n_ll = 0;
+        t.out = ctx->out.ptr;
+        HIP_TRY(wfsa::launch_tail(t, s));
+    }
+    return WFSA_OK;
+}
+
+// The device work of one objective/gradient evaluation, enqueued on the
+// context's stream (captured into a graph on first use): weights in, the
+// compiled streams (with the per-edge weights) + bubbles (timed by k0..k1),
+// traversal fallback (k1..k2), the tail reduction (which adds the trivial
+// words' constant gradient), and -- without a communicator -- the results out.
+int enqueue_iteration(wfsa_dev* ctx, bool want_logq) {
+    hipStream_t s = ctx->stream;
+    const int32_t np = ctx->n_params;
+    HIP_TRY(wfsa::launch_stage(ctx->pinned_dev + weights_off(np), ctx->w_full.ptr, np, s));
+    if (int rc = enqueue_compiled(ctx, false, want_logq)) return rc;
+    int32_t wave_off = ctx->n_groups > 0 ? ctx->i_grid * (ctx->i_block / kWave) : 0;
     if (ctx->n_bubbles > 0) {
         wfsa::BubbleArgs b{};
         b.m = model_view(ctx);
@@ -607,7 +722,7 @@ int enqueue_iteration(wfsa_dev* ctx, bool want_logq) {
         HIP_TRY(wfsa::launch_bubbles(b, ctx->b_grid, s));
         wave_off += ctx->b_grid * (wfsa::kBubbleBlock / kWave);
     }
-    HIP_TRY(hipEventRecord(ctx->k1, s));
+    HIP_TRY(record(ctx, ctx->k1, s));
     for (int t = 0; t < 2; ++t) {
         if (!ctx->n_fall[t]) continue;
         wfsa::TravArgs a = trav_args(ctx, t);
@@ -619,10 +734,10 @@ int enqueue_iteration(wfsa_dev* ctx, bool want_logq) {
         HIP_TRY(wfsa::launch_trav(wfsa::MODE_WEIGHTED, a, ctx->fall_grid[t], s));
         wave_off += ctx->fall_grid[t] * ctx->cfg[t].waves_per_block;
     }
-    HIP_TRY(hipEventRecord(ctx->k2, s));
+    HIP_TRY(record(ctx, ctx->k2, s));
     wfsa::TailArgs t{};
-    t.gpart = ctx->gpart.ptr;
-    t.n_gpart = (ctx->n_groups > 0 && ctx->c_tables >= 1) ? ctx->c_grid : 0;
+    t.gpart = ctx->fixed_grad.ptr;
+    t.n_gpart = ctx->n_groups > 0 ? 1 : 0;
     t.chunk_param = ctx->bg_chunk_param.ptr;
     t.chunk_ptr = ctx->bg_chunk_ptr.ptr;
     t.slot = ctx->bg_slot.ptr;
@@ -633,8 +748,7 @@ int enqueue_iteration(wfsa_dev* ctx, bool want_logq) {
     t.n_params = np;
     t.out = ctx->out.ptr;
     HIP_TRY(wfsa::launch_tail(t, s));
-    if (!ctx->comm)
-        HIP_TRY(hipMemcpyAsync(ctx->pinned, ctx->out.ptr, (size_t(np) + 1) * sizeof(double), hipMemcpyDeviceToHost, s));
+    if (!ctx->comm) HIP_TRY(wfsa::launch_publish(ctx->out.ptr, publish_args(ctx), s));
     return WFSA_OK;
 }
 
@@ -670,9 +784,16 @@ int wfsa_dev_create(int device, wfsa_dev** out) {
     ctx->device = device;
     ctx->n_cu = prop.multiProcessorCount > 0 ? prop.multiProcessorCount : kNumCu;
     if (const char* e = std::getenv("WFSA_GRAPH")) ctx->use_graph = e[0] == '1';
+    if (const char* e = std::getenv("WFSA_TIMING")) ctx->kernel_timing = e[0] != '0';
     HIP_TRY(hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking));
-    for (hipEvent_t* ev : {&ctx->ev0, &ctx->ev1, &ctx->k0, &ctx->k1, &ctx->k2}) HIP_TRY(hipEventCreate(ev));
+    for (hipEvent_t* ev : {&ctx->ev0, &ctx->ev1, &ctx->k0, &ctx->kc, &ctx->k1, &ctx->k2}) HIP_TRY(hipEventCreate(ev));
     HIP_TRY(ctx->live.alloc(1));
+    HIP_TRY(hipHostMalloc(reinterpret_cast<void**>(&ctx->flag), 64, hipHostMallocMapped | hipHostMallocCoherent));
+    HIP_TRY(hipHostGetDevicePointer(reinterpret_cast<void**>(&ctx->flag_dev), ctx->flag, 0));
+    *ctx->flag = 0;
+    HIP_TRY(ctx->counters.alloc(1));
+    HIP_TRY(hipMemsetAsync(ctx->counters.ptr, 0, sizeof(unsigned), ctx->stream));
+    HIP_TRY(hipStreamSynchronize(ctx->stream));
     *out = ctx.release();
     return WFSA_OK;
 }
@@ -684,7 +805,8 @@ void wfsa_dev_destroy(wfsa_dev* ctx) {
     drop_graph(ctx);
     if (ctx->comm) (void)ncclCommDestroy(ctx->comm);
     if (ctx->pinned) (void)hipHostFree(ctx->pinned);
-    for (hipEvent_t ev : {ctx->ev0, ctx->ev1, ctx->k0, ctx->k1, ctx->k2})
+    if (ctx->flag) (void)hipHostFree(ctx->flag);
+    for (hipEvent_t ev : {ctx->ev0, ctx->ev1, ctx->k0, ctx->kc, ctx->k1, ctx->k2})
         if (ev) (void)hipEventDestroy(ev);
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
     delete ctx;
@@ -735,13 +857,16 @@ int wfsa_dev_load_model(wfsa_dev* ctx, const wfsa_model_desc* model) {
     ctx->n_params = tm.n_params;
     ctx->n_nodes = tm.n_nodes;
     ctx->start = tm.start;
-    HIP_TRY(ctx->w_full.alloc(size_t(ctx->n_params)));
-    HIP_TRY(ctx->out.alloc(size_t(ctx->n_params) + 1));
-    if (ctx->pinned_n < 2 * size_t(ctx->n_params) + 1) {
+    HIP_TRY(ctx->w_full.alloc(size_t(ctx->n_params) + 2));
+    HIP_TRY(ctx->out.alloc(size_t(ctx->n_params) + 2));
+    const size_t pinned_need = weights_off(ctx->n_params) + size_t(ctx->n_params) + 2;
+    if (ctx->pinned_n < pinned_need) {
         if (ctx->pinned) (void)hipHostFree(ctx->pinned);
         ctx->pinned = nullptr;
-        HIP_TRY(hipHostMalloc(reinterpret_cast<void**>(&ctx->pinned), (2 * size_t(ctx->n_params) + 1) * sizeof(double)));
-        ctx->pinned_n = 2 * size_t(ctx->n_params) + 1;
+        HIP_TRY(hipHostMalloc(reinterpret_cast<void**>(&ctx->pinned), pinned_need * sizeof(double),
+                              hipHostMallocMapped | hipHostMallocCoherent));
+        HIP_TRY(hipHostGetDevicePointer(reinterpret_cast<void**>(&ctx->pinned_dev), ctx->pinned, 0));
+        ctx->pinned_n = pinned_need;
     }
     HIP_TRY(hipStreamSynchronize(s));
     ctx->has_model = true;
@@ -811,10 +936,10 @@ int wfsa_dev_objective_grad_begin(wfsa_dev* ctx, const double* w_full, int want_
     if (ctx->in_flight) return fail(WFSA_ERR_ARG, "objective_grad_begin called twice without _end");
     if (ctx->prep_level < 2)
         if (int rc = prepare(ctx, 2)) return rc;
+    if (int rc = collect_timing(ctx)) return rc;
     hipStream_t s = ctx->stream;
     const int32_t np = ctx->n_params;
-    double* res = ctx->pinned;            // [LL, grad]
-    double* win = ctx->pinned + np + 1;   // weights in
+    double* win = ctx->pinned + weights_off(np);   // weights in
     if (np > 0) std::memcpy(win, w_full, size_t(np) * sizeof(double));
     HIP_TRY(hipEventRecord(ctx->ev0, s));
     if (ctx->use_graph && !ctx->graph_exec && !ctx->graph_failed) {
@@ -841,9 +966,10 @@ int wfsa_dev_objective_grad_begin(wfsa_dev* ctx, const double* w_full, int want_
     else if (int rc = enqueue_iteration(ctx, want_logq != 0)) return rc;
     if (ctx->comm) {
         RCCL_TRY(ncclAllReduce(ctx->out.ptr, ctx->out.ptr, size_t(np) + 1, ncclDouble, ncclSum, ctx->comm, s));
-        HIP_TRY(hipMemcpyAsync(res, ctx->out.ptr, (size_t(np) + 1) * sizeof(double), hipMemcpyDeviceToHost, s));
+        HIP_TRY(wfsa::launch_publish(ctx->out.ptr, publish_args(ctx), s));
     }
     HIP_TRY(hipEventRecord(ctx->ev1, s));
+    ++ctx->seq;
     ctx->in_flight = true;
     ctx->logq_ready = want_logq != 0 || ctx->graph_exec != nullptr;
     return WFSA_OK;
@@ -855,27 +981,16 @@ int wfsa_dev_objective_grad_end(wfsa_dev* ctx, double* loglik, double* grad_full
     ctx->in_flight = false;
     hipStream_t s = ctx->stream;
     const int32_t np = ctx->n_params;
-    HIP_TRY(hipStreamSynchronize(s));
+    if (int rc = wait_published(ctx)) return rc;
+    ctx->timing_pending = true;
+    if (loglik) *loglik = ctx->pinned[0];
+    if (grad_full && np > 0) std::memcpy(grad_full, ctx->pinned + 1, size_t(np) * sizeof(double));
     if (logq) {
         if (!ctx->logq_ready) return fail(WFSA_ERR_ARG, "log q was not requested at _begin");
+        HIP_TRY(hipStreamSynchronize(s));
         HIP_TRY(ctx->logq.download(logq, size_t(ctx->n_strings), s));
         HIP_TRY(hipStreamSynchronize(s));
     }
-    float c_ms = 0.f, f_ms = 0.f, all_ms = 0.f;
-    if (!ctx->graph_exec) {   // events recorded inside a captured graph are not timeable
-        HIP_TRY(hipEventElapsedTime(&c_ms, ctx->k0, ctx->k1));
-        HIP_TRY(hipEventElapsedTime(&f_ms, ctx->k1, ctx->k2));
-    }
-    HIP_TRY(hipEventElapsedTime(&all_ms, ctx->ev0, ctx->ev1));
-    if (loglik) *loglik = ctx->pinned[0];
-    if (grad_full && np > 0) std::memcpy(grad_full, ctx->pinned + 1, size_t(np) * sizeof(double));
-    ctx->stats.fb_launches += 1;
-    ctx->stats.fb_kernel_ms += double(c_ms) + double(f_ms);
-    ctx->stats.last_fb_kernel_ms = double(c_ms) + double(f_ms);
-    ctx->stats.last_compiled_ms = double(c_ms);
-    ctx->stats.compiled_kernel_ms += double(c_ms);
-    ctx->stats.last_call_ms = double(all_ms);
-    ctx->stats.graph = ctx->graph_exec ? 1 : 0;
     return WFSA_OK;
 }
 
@@ -923,6 +1038,8 @@ int wfsa_dev_allreduce(wfsa_dev* ctx, double* host_buf, int64_t count) {
 
 int wfsa_dev_get_stats(wfsa_dev* ctx, wfsa_dev_stats* out) {
     if (!ctx || !out) return fail(WFSA_ERR_ARG, "null argument");
+    if (!ctx->in_flight)
+        if (int rc = collect_timing(ctx)) return rc;
     *out = ctx->stats;
     return WFSA_OK;
 }
