@@ -610,6 +610,125 @@ __global__ __launch_bounds__(1024) void fbc_kernel(CompiledArgs a) {
     }
 }
 
+// Prologue of the per-iteration stream kernel (no other kernel runs before
+// it): this block's slice of the per-edge weights (bubbles and the traversal
+// fallback read them after this launch) and, by block 0, the zeroed result.
+__device__ __forceinline__ void edge_weight_slice(const CompiledArgs& a) {
+    const int64_t per = (a.n_comb + gridDim.x - 1) / gridDim.x;
+    const int64_t e_end = min(a.n_comb, per * int64_t(blockIdx.x + 1));
+    for (int64_t g = per * int64_t(blockIdx.x) + threadIdx.x; g < e_end; g += blockDim.x) {
+        const int32_t b = a.m.pptr[g], e = a.m.pptr[g + 1];
+        double sum = 0.0;
+        for (int32_t k = b; k < e; ++k) sum += a.w[a.m.pidx[k]];
+        a.lw_out[g] = sum;
+        a.ew_out[g] = exp(sum);
+        a.erec_out[g] = EdgeRec{sum, e > b ? a.m.pidx[b] : 0, e - b};
+    }
+    if (blockIdx.x == 0)
+        for (int j = int(threadIdx.x); j <= a.n_params; j += int(blockDim.x)) a.out[j] = 0.0;
+}
+
+// Per-iteration stream kernel: log q of every compiled string's trivial
+// words, sum_words w[j], one lane per string, no atomics (their gradient is
+// the constant added by the tail kernel).  w[n_params] is a zero slot, so a
+// padding word (0xFFFF / -1) and -- in the fast path -- a multi-parameter
+// word read 0.0 without a branch: index = min(word, n_params).  Chunks that
+// hold multi-parameter words (MULTI, automata with epsilon composites) take
+// a second, per-word pass.  Loads are unconditional up to the group's
+// longest lane (shorter lanes read their padding chunks), D chunks in flight.
+template <bool WIDE, bool W_LDS, bool MULTI>
+__global__ __launch_bounds__(1024) void fbs_kernel(CompiledArgs a) {
+    extern __shared__ __attribute__((aligned(16))) double lds[];
+    const int lane = lane_id();
+    const int wpb = int(blockDim.x) / kWave;
+    const int gw = __builtin_amdgcn_readfirstlane(int(blockIdx.x) * wpb + int(threadIdx.x) / kWave);
+    const int nw = int(gridDim.x) * wpb;
+    const uint32_t zslot = uint32_t(a.n_params);
+    if (W_LDS) {
+        for (int j = int(threadIdx.x); j <= a.n_params; j += int(blockDim.x)) lds[j] = a.w[j];
+        edge_weight_slice(a);
+        __syncthreads();
+    }
+    const double* wsrc = W_LDS ? lds : a.w;
+    double ll_acc = 0.0;
+    for (int round = 0;; ++round) {
+        const int grp = round * nw + ((round & 1) ? (nw - 1 - gw) : gw);
+        if (grp >= a.n_groups) break;
+        const int s = a.l_str[grp * kWave + lane];
+        const int gch = a.g_len[grp];
+        const uint4* st = a.stream + a.g_base[grp] + lane;
+        const double p = s >= 0 ? a.p[s] : 0.0;
+        double acc0 = 0.0, acc1 = 0.0;
+        // Two register sets of D chunks: one is applied while the other's
+        // loads are in flight, and the sets swap roles -- no register copy of
+        // an in-flight load, so the wait before a set is "all but the other
+        // set's D loads".  Loads are unconditional (the stream carries
+        // kStreamTailChunks chunks of slack after the last group); the only
+        // branches are the uniform end-of-group tests.
+        constexpr int D = kStreamPrefetch;
+        uint4 A[D], B[D];
+        auto load = [&](uint4 (&r)[D], int c0) {
+#pragma unroll
+            for (int d = 0; d < D; ++d) r[d] = st[int64_t(kWave) * (c0 + d)];
+        };
+        auto apply = [&](const uint4 (&r)[D], int c0) {
+#pragma unroll
+            for (int d = 0; d < D; ++d) {
+                if (c0 + d >= gch) break;
+                const uint32_t v[4] = {r[d].x, r[d].y, r[d].z, r[d].w};
+                bool multi = false;
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    if (WIDE) {
+                        const uint32_t x = v[i];
+                        const double t = wsrc[min(x, zslot)];
+                        if (i & 1) acc1 += t; else acc0 += t;
+                        if (MULTI) multi |= int(x) < -1;
+                    } else {
+                        const uint32_t lo = v[i] & 0xffffu, hi = v[i] >> 16;
+                        acc0 += wsrc[min(lo, zslot)];
+                        acc1 += wsrc[min(hi, zslot)];
+                        if (MULTI) multi |= (lo >= 0x8000u && lo != 0xffffu) || (hi >= 0x8000u && hi != 0xffffu);
+                    }
+                }
+                if (MULTI && multi) {   // rare: epsilon-composite edges
+                    for (int i = 0; i < 4; ++i) {
+                        for (int h = 0; h < (WIDE ? 1 : 2); ++h) {
+                            int g = -1;
+                            if (WIDE) {
+                                if (int(v[i]) < -1) g = -(int(v[i]) + 2);
+                            } else {
+                                const uint32_t x = (v[i] >> (16 * h)) & 0xffffu;
+                                if (x >= 0x8000u && x != 0xffffu) g = a.m.multi_edge[x - 0x8000u];
+                            }
+                            if (g >= 0)
+                                for (int q = a.m.pptr[g]; q < a.m.pptr[g + 1]; ++q) acc0 += wsrc[a.m.pidx[q]];
+                        }
+                    }
+                }
+            }
+        };
+        load(A, 0);
+        for (int c0 = 0;;) {
+            load(B, c0 + D);
+            apply(A, c0);
+            c0 += D;
+            if (c0 >= gch) break;
+            load(A, c0 + D);
+            apply(B, c0);
+            c0 += D;
+            if (c0 >= gch) break;
+        }
+        const double acc = acc0 + acc1;
+        if (s >= 0) {
+            ll_acc += p * acc;
+            if (a.logq) a.logq[s] = acc;
+        }
+    }
+    ll_acc = wave_sum(ll_acc);
+    if (lane == 0) a.ll_part[gw] = ll_acc;
+}
+
 // Bubbles: one lane per bubble (largest first).  Local forward from the
 // bubble's first cut, local backward from its last cut; an edge's posterior
 // is alpha(src) w beta(dst) / Z and -p_s times it goes to the edge's
@@ -758,10 +877,10 @@ hipError_t configure_kernels(int max_dynamic_lds) {
                          reinterpret_cast<const void*>(&fbc_kernel<0, true, true>),
                          reinterpret_cast<const void*>(&fbc_kernel<1, true, true>),
                          reinterpret_cast<const void*>(&fbc_kernel<2, true, true>),
-                         reinterpret_cast<const void*>(&fbc_kernel<0, false, false>),
-                         reinterpret_cast<const void*>(&fbc_kernel<1, false, false>),
-                         reinterpret_cast<const void*>(&fbc_kernel<0, true, false>),
-                         reinterpret_cast<const void*>(&fbc_kernel<1, true, false>)};
+                         reinterpret_cast<const void*>(&fbs_kernel<false, true, false>),
+                         reinterpret_cast<const void*>(&fbs_kernel<false, true, true>),
+                         reinterpret_cast<const void*>(&fbs_kernel<true, true, false>),
+                         reinterpret_cast<const void*>(&fbs_kernel<true, true, true>)};
     for (const void* f : fns) {
         hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, max_dynamic_lds);
         if (e != hipSuccess) return e;
@@ -789,11 +908,17 @@ hipError_t launch_trav(TravMode mode, const TravArgs& a, int grid, hipStream_t s
 hipError_t launch_compiled(const CompiledArgs& a, int grid, int block, size_t lds, hipStream_t stream) {
     const dim3 g{unsigned(grid), 1, 1}, b{unsigned(block), 1, 1};
     if (!a.with_grad) {   // per-iteration form: w staged in LDS or read from global
-        const bool t = a.tables >= 1;
-        if (t && a.wide) hipLaunchKernelGGL((fbc_kernel<1, true, false>), g, b, lds, stream, a);
-        else if (t) hipLaunchKernelGGL((fbc_kernel<1, false, false>), g, b, lds, stream, a);
-        else if (a.wide) hipLaunchKernelGGL((fbc_kernel<0, true, false>), g, b, 0, stream, a);
-        else hipLaunchKernelGGL((fbc_kernel<0, false, false>), g, b, 0, stream, a);
+        const int key = (a.tables >= 1 ? 4 : 0) + (a.wide ? 2 : 0) + (a.multi ? 1 : 0);
+        switch (key) {
+            case 0: hipLaunchKernelGGL((fbs_kernel<false, false, false>), g, b, 0, stream, a); break;
+            case 1: hipLaunchKernelGGL((fbs_kernel<false, false, true>), g, b, 0, stream, a); break;
+            case 2: hipLaunchKernelGGL((fbs_kernel<true, false, false>), g, b, 0, stream, a); break;
+            case 3: hipLaunchKernelGGL((fbs_kernel<true, false, true>), g, b, 0, stream, a); break;
+            case 4: hipLaunchKernelGGL((fbs_kernel<false, true, false>), g, b, lds, stream, a); break;
+            case 5: hipLaunchKernelGGL((fbs_kernel<false, true, true>), g, b, lds, stream, a); break;
+            case 6: hipLaunchKernelGGL((fbs_kernel<true, true, false>), g, b, lds, stream, a); break;
+            default: hipLaunchKernelGGL((fbs_kernel<true, true, true>), g, b, lds, stream, a); break;
+        }
         return hipGetLastError();
     }
     const int key = a.tables * 2 + (a.wide ? 1 : 0);
@@ -827,8 +952,7 @@ hipError_t launch_publish(const double* out, const Publish& pub, hipStream_t str
 }
 
 hipError_t launch_stage(const double* host_w, double* w, int32_t n, hipStream_t stream) {
-    if (n <= 0) return hipSuccess;
-    const int32_t n2 = (n + 1) / 2;
+    const int32_t n2 = (n + 2) / 2;   // n weights and the zero slot w[n]
     const unsigned blocks = unsigned(std::min<int32_t>(8, (n2 + 255) / 256));
     hipLaunchKernelGGL(stage_kernel, dim3(blocks), dim3(256), 0, stream, reinterpret_cast<const double2*>(host_w),
                        reinterpret_cast<double2*>(w), n2);

@@ -21,6 +21,9 @@ namespace wfsa {
 
 constexpr int kMaxBubbleNodes = 16;    // nodes of one compiled bubble
 constexpr int kMaxBubbleEdges = 255;   // edges of one compiled bubble
+constexpr int kStreamPrefetch = 4;     // 16-byte chunks in flight per lane
+// slack after the last group's chunks: the prefetch runs ahead unguarded
+constexpr int kStreamTailChunks = 64 * 8;
 
 // Per-iteration record of a combined edge, one 16-byte gather in the
 // compiled kernel: its log-weight and its parameter list (p0 when np == 1).
@@ -143,6 +146,7 @@ struct CompiledArgs {
                              // else: >= 1 w staged in LDS, 0 global
     int32_t wide;
     int32_t with_grad;       // accumulate the (weight-independent) trivial-word gradient
+    int32_t multi;           // the automaton has multi-parameter (epsilon-composite) edges
     const double* w;         // [n_params] w_full (GetWeight form)
     double* grad;            // [n_params] (TABLES == 0: atomics straight into it)
     double* gpart;           // [grid][n_params] per-block partial gradients (TABLES >= 1)
@@ -207,7 +211,8 @@ hipError_t launch_bubbles(const BubbleArgs& a, int grid, hipStream_t stream);
 hipError_t launch_tail(const TailArgs& a, hipStream_t stream);
 // out[0, n) -> host-mapped memory, then the flag (one block)
 hipError_t launch_publish(const double* out, const Publish& pub, hipStream_t stream);
-// host-mapped weights -> device (buffers padded to an even count)
+// host-mapped weights w[0, n) and the zero slot w[n] -> device (both
+// buffers padded to an even count)
 hipError_t launch_stage(const double* host_w, double* w, int32_t n, hipStream_t stream);
 // also zeroes out[0..n_out) (the accumulators of this iteration)
 hipError_t launch_edge_weights(const double* w_full, const int32_t* pptr, const int32_t* pidx, double* lw,

@@ -487,8 +487,9 @@ int prepare(wfsa_dev* ctx, int level) {
     if (bwords >= (int64_t(1) << 31) - 2) return fail(WFSA_ERR_CAPACITY, "bubble buffer exceeds 2^31 words");
 
     // 3. emit the streams (same tier as counted)
-    HIP_TRY(ctx->stream_w.alloc(size_t(std::max<int64_t>(chunks, 1))));
-    HIP_TRY(hipMemsetAsync(ctx->stream_w.ptr, 0xff, size_t(std::max<int64_t>(chunks, 1)) * sizeof(uint4), s));
+    const size_t chunk_alloc = size_t(chunks) + size_t(wfsa::kStreamTailChunks);
+    HIP_TRY(ctx->stream_w.alloc(chunk_alloc));
+    HIP_TRY(hipMemsetAsync(ctx->stream_w.ptr, 0xff, chunk_alloc * sizeof(uint4), s));
     HIP_TRY(ctx->bub.alloc(size_t(std::max<int64_t>(bwords, 2))));
     HIP_TRY(ctx->bub_off.alloc(size_t(std::max<int64_t>(nbub, 1))));
     if (nc > 0) {
@@ -596,8 +597,8 @@ int prepare(wfsa_dev* ctx, int level) {
     ctx->c_grid = int(std::max<int64_t>(1, std::min<int64_t>(int64_t(ctx->n_cu) * per_cu, want_blocks)));
     if (ctx->c_tables >= 1) HIP_TRY(ctx->gpart.alloc(size_t(ctx->c_grid) * size_t(std::max(ctx->n_params, 1))));
     // the per-iteration pass keeps only w in LDS: as many blocks per CU as fit
-    ctx->i_tables = table_bytes <= size_t(kLdsPerCu - 1024) ? 1 : 0;
-    ctx->i_lds = ctx->i_tables ? table_bytes : 0;
+    ctx->i_tables = table_bytes + 8 <= size_t(kLdsPerCu - 1024) ? 1 : 0;
+    ctx->i_lds = ctx->i_tables ? table_bytes + 8 : 0;   // + the zero slot
     if (const char* e = std::getenv("WFSA_IBLOCK")) ctx->i_block = std::max(64, std::min(1024, std::atoi(e))) & ~63;
     const int i_wpb = ctx->i_block / kWave;
     int i_per_cu = kMaxWavesPerCu / i_wpb;
@@ -623,7 +624,7 @@ int prepare(wfsa_dev* ctx, int level) {
     // the trivial words' gradient, once: compiled pass with gradient at
     // w = 0 (its log-weights are discarded), then the slab sum
     if (nc > 0) {
-        HIP_TRY(hipMemsetAsync(ctx->w_full.ptr, 0, size_t(std::max(ctx->n_params, 1)) * sizeof(double), s));
+        HIP_TRY(hipMemsetAsync(ctx->w_full.ptr, 0, (size_t(ctx->n_params) + 2) * sizeof(double), s));
         if (int rc = enqueue_compiled(ctx, true, false)) return rc;
         HIP_TRY(hipMemcpyAsync(ctx->fixed_grad.ptr, ctx->out.ptr + 1, size_t(ctx->n_params) * sizeof(double),
                                hipMemcpyDeviceToDevice, s));
@@ -671,6 +672,7 @@ int enqueue_compiled(wfsa_dev* ctx, bool with_grad, bool want_logq) {
         c.n_params = np;
         c.tables = tables;
         c.with_grad = with_grad ? 1 : 0;
+        c.multi = ctx->n_multi > 0 ? 1 : 0;
         c.w = ctx->w_full.ptr;
         c.grad = ctx->out.ptr + 1;
         c.gpart = ctx->gpart.ptr;
@@ -867,6 +869,7 @@ int wfsa_dev_load_model(wfsa_dev* ctx, const wfsa_model_desc* model) {
                               hipHostMallocMapped | hipHostMallocCoherent));
         HIP_TRY(hipHostGetDevicePointer(reinterpret_cast<void**>(&ctx->pinned_dev), ctx->pinned, 0));
         ctx->pinned_n = pinned_need;
+        std::memset(ctx->pinned, 0, pinned_need * sizeof(double));   // incl. the weights' zero slot
     }
     HIP_TRY(hipStreamSynchronize(s));
     ctx->has_model = true;
