@@ -136,6 +136,35 @@ int wfsa_dev_objective_grad(wfsa_dev* ctx, const double* w_full, double* loglik,
 int wfsa_dev_objective_grad_begin(wfsa_dev* ctx, const double* w_full, int want_logq);
 int wfsa_dev_objective_grad_end(wfsa_dev* ctx, double* loglik, double* grad_full, double* logq);
 
+/* Device-resident QuasiNewton: QuasiNewtonLearner::OptimizationStep
+ * (src/QuasiNewtonLearner.cpp:162-201) and the epoch loop (src/main.cpp:276-303)
+ * with x, lambda and w_full kept in HBM -- one step = the objective/gradient
+ * kernels at x, the (all-reduce), and a one-workgroup KKT-diagonal update that
+ * writes the next step's weights; steps are enqueued ahead and the host only
+ * reads each step's info row.
+ *   qn_setup:     once after Trim: trim[n_full] = Learner::trimmed_weights,
+ *                 ccol[n_params] = the constraint of each kept parameter (C),
+ *                 plogp = sum p log p (over all ranks), InitCallback flag 32.
+ *   qn_set_state: x[n_params], lambda[n_constraints] (after Init).
+ *   qn_get_state: x, lambda and the last step's gradient (any may be NULL).
+ *   qn_run:       up to max_steps steps; info_rows[7*s ..] gets step s's
+ *                 GetOptimizationInfo row (KL, graderr, g_min, g_max, lambda_min,
+ *                 0, 0); stops after the step whose HaltCondition(tol) holds
+ *                 (*status = 1) or whose info is not finite (*status = 2). */
+typedef struct {
+    int32_t n_params;
+    int32_t n_constraints;
+    const int32_t* trim;       /* [n_full]                                   */
+    const int32_t* ccol;       /* [n_params]                                 */
+    double plogp;
+    int32_t exponential_lambda;
+} wfsa_qn_desc;
+int wfsa_dev_qn_setup(wfsa_dev* ctx, const wfsa_qn_desc* desc);
+int wfsa_dev_qn_set_state(wfsa_dev* ctx, const double* x, const double* lambda);
+int wfsa_dev_qn_get_state(wfsa_dev* ctx, double* x, double* lambda, double* grad);
+int wfsa_dev_qn_run(wfsa_dev* ctx, double eta, double tol, int32_t max_steps, double* info_rows,
+                    int32_t* steps_done, int32_t* status);
+
 /* Multi-GPU: one process per GPU.  Rank 0 creates the id, the launcher
  * broadcasts the 128 bytes, every rank attaches.  wfsa_dev_allreduce sums
  * `count` doubles of a host buffer in place over the ranks. */

@@ -257,9 +257,20 @@ def test_async_begin_end_and_native_epoch_loop():
         lrn.BuildFromPacked(fsa, sym, off, wt)
         lrn.Finalize()
         lrn.Init(7)
-    rows_a = a.Run(6, 1.0, -1.0)
-    rows_b = [b.OptimizationStep(1.0, -1.0)[0] for _ in range(6)]
+    rows_a = a.Run(6, 1.0, -1.0)                              # device-resident QN
+    rows_b = [b.OptimizationStep(1.0, -1.0)[0] for _ in range(6)]   # host QN update
     assert len(rows_a) == 6
     for r, q in zip(rows_a, rows_b):
         for u, v in zip(r[:5], q[:5]):
             assert _close(u, v, rel=1e-11, atol=1e-14)
+    np.testing.assert_allclose(a.x(), b.x(), rtol=1e-11, atol=1e-13)
+    assert _close(a.info()["kl"], b.info()["kl"], rel=1e-12)
+    # a halting run stops at the same epoch on both sides
+    rows_a = a.Run(50, 1.0, 1e-3)
+    rows_b = []
+    for _ in range(50):
+        info, halt = b.OptimizationStep(1.0, 1e-3)
+        rows_b.append(info)
+        if halt:
+            break
+    assert len(rows_a) == len(rows_b)

@@ -305,6 +305,12 @@ void Learner::EvaluateDevice(std::vector<double>& grad_out, bool want_logq) {
 
 void Learner::ComputeModeledProbs() { EvaluateDevice(grad_cache, false); }
 
+void Learner::SetEvaluated(double loglik_value) {
+    loglik = loglik_value;
+    kl = plogp - loglik;
+    logq_valid = false;
+}
+
 void Learner::ComputeObjective() { kl = plogp - loglik; }
 
 const std::vector<double>& Learner::GetLogQ() {

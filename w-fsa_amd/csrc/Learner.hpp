@@ -119,6 +119,8 @@ protected:
     // BeginModeledProbs + EndModeledProbs.)
     void BeginModeledProbs(bool want_logq = false);
     void EndModeledProbs(std::vector<double>& grad_out);
+    // results of an evaluation that ran elsewhere (the device-resident QN run)
+    void SetEvaluated(double loglik_value);
     double AllReduceSum(double v) const;
 
     std::vector<double> _x;

@@ -116,4 +116,42 @@ void QuasiNewtonLearner::OptimizationStep(double eta, bool) {   // :162-201
     timing.post_ms += ms(t3, t4);
 }
 
+void QuasiNewtonLearner::RunDevice(double eta, double tol, int32_t max_epochs, double* info_rows,
+                                   int32_t* epochs_done) {
+    if (epochs_done) *epochs_done = 0;
+    wfsa_dev* d = Device();
+    if (!d) throw LearnerError("BuildFrom has not run");
+    wfsa_qn_desc desc{};
+    desc.n_params = GetNumberOfParameters();
+    desc.n_constraints = GetNumberOfConstraints();
+    desc.trim = GetTrimmedIndex().data();
+    desc.ccol = Ccol.data();
+    desc.plogp = GetPLogP();
+    desc.exponential_lambda = exponential_lambda ? 1 : 0;
+    auto check = [](int rc, const char* what) {
+        if (rc != WFSA_OK) throw LearnerError(what, ": ", wfsa_dev_last_error());
+    };
+    check(wfsa_dev_qn_setup(d, &desc), "wfsa_dev_qn_setup");
+    check(wfsa_dev_qn_set_state(d, _x.data(), lambda.data()), "wfsa_dev_qn_set_state");
+    std::vector<double> rows(size_t(std::max(max_epochs, 0)) * 7);
+    int32_t done = 0, status = 0;
+    check(wfsa_dev_qn_run(d, eta, tol, max_epochs, rows.data(), &done, &status), "wfsa_dev_qn_run");
+    check(wfsa_dev_qn_get_state(d, _x.data(), lambda.data(), grad.data()), "wfsa_dev_qn_get_state");
+    if (info_rows) std::copy(rows.begin(), rows.begin() + std::ptrdiff_t(done) * 7, info_rows);
+    if (epochs_done) *epochs_done = done;
+    if (done > 0) {
+        const double* r = rows.data() + size_t(done - 1) * 7;
+        grad_error = r[1];
+        g_min = r[2];
+        g_max = r[3];
+        lambda_min = r[4];
+        SetEvaluated(GetPLogP() - r[0]);
+        grad_cache = grad;
+        timing.steps += done;
+        if (status == 2)
+            for (int i = 0; i < 7; ++i)
+                if (!std::isfinite(r[i])) throw LearnerError(r[i], " detected at epoch ", done);
+    }
+}
+
 }  // namespace wfsa

@@ -22,6 +22,14 @@ public:
     void ComputeG();
     void ComputeGrad();
 
+    // The epoch loop of src/main.cpp:276-303 run device-resident
+    // (wfsa_dev_qn_run): up to max_epochs OptimizationSteps, info_rows[7*e..]
+    // (nullable) per epoch, stops after the epoch whose HaltCondition(tol)
+    // holds; a non-finite info value throws LearnerError like the reference
+    // after the row is recorded.  *epochs_done = the epochs run (set before
+    // any throw).
+    void RunDevice(double eta, double tol, int32_t max_epochs, double* info_rows, int32_t* epochs_done);
+
     struct Timing {
         int64_t steps = 0;
         double begin_ms = 0, overlap_ms = 0, wait_ms = 0, post_ms = 0;

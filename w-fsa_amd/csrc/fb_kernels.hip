@@ -246,6 +246,7 @@ __device__ bool compile_walk(const Slab& sl, const ModelView& m, int L, int sidx
 template <int MODE>
 __global__ __launch_bounds__(256) void trav_kernel(TravArgs a) {
     constexpr bool COUNTING = MODE != MODE_WEIGHTED;
+    if (a.halted && *a.halted) return;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int lane = lane_id();
     const int wib = int(threadIdx.x) / kWave;
@@ -638,6 +639,7 @@ __device__ __forceinline__ void edge_weight_slice(const CompiledArgs& a) {
 // longest lane (shorter lanes read their padding chunks), D chunks in flight.
 template <bool WIDE, bool W_LDS, bool MULTI>
 __global__ __launch_bounds__(1024) void fbs_kernel(CompiledArgs a) {
+    if (a.halted && *a.halted) return;
     extern __shared__ __attribute__((aligned(16))) double lds[];
     const int lane = lane_id();
     const int wpb = int(blockDim.x) / kWave;
@@ -734,6 +736,7 @@ __global__ __launch_bounds__(1024) void fbs_kernel(CompiledArgs a) {
 // is alpha(src) w beta(dst) / Z and -p_s times it goes to the edge's
 // contribution slot; log Z joins the string's log q.
 __global__ __launch_bounds__(kBubbleBlock) void bubble_kernel(BubbleArgs a) {
+    if (a.halted && *a.halted) return;
     __shared__ double scr[kBubbleBlock][2 * kMaxBubbleNodes + 1];
     const int lane = lane_id();
     const int gw = int(blockIdx.x) * (kBubbleBlock / kWave) + int(threadIdx.x) / kWave;
@@ -765,7 +768,12 @@ __global__ __launch_bounds__(kBubbleBlock) void bubble_kernel(BubbleArgs a) {
             const int src = sd & 0xffff;
             const double b = a.m.ew[g] * B[sd >> 16];
             B[src] += b;
-            c[e] = A[src] * b * scale;
+            const double v = A[src] * b * scale;
+            if (a.grad) {
+                for (int q = a.m.pptr[g]; q < a.m.pptr[g + 1]; ++q) global_add(&a.grad[a.m.pidx[q]], v);
+            } else {
+                c[e] = v;
+            }
         }
         const double lz = log(Z);
         ll_acc += p * lz;
@@ -795,6 +803,7 @@ __global__ __launch_bounds__(256) void publish_kernel(const double* out, Publish
 }
 
 __global__ __launch_bounds__(256) void tail_kernel(TailArgs a) {
+    if (a.halted && *a.halted) return;
     const int n_tiles = (a.n_params + 255) / 256;
     const int n_slab_groups = (a.n_gpart + kTailSlabs - 1) / kTailSlabs;
     const int n_param_blocks = n_tiles * n_slab_groups;

@@ -119,6 +119,7 @@ struct TravArgs {
     int32_t* bub_off;        // [n_bubbles] word offset of each bubble
     uint8_t* overflow;       // [S] string did not fit the slab
     unsigned long long* live_edges;
+    const unsigned* halted;  // device-resident QN run: nonzero = skip (or null)
 };
 
 // Compiled streams of the per-iteration kernels.
@@ -160,6 +161,7 @@ struct CompiledArgs {
     double* out;             // [1 + n_params], zeroed by block 0
     double* ll_part;         // [waves in grid]
     double* logq;            // [S] or null
+    const unsigned* halted;  // device-resident QN run: nonzero = skip (or null)
 };
 
 struct BubbleArgs {
@@ -168,9 +170,11 @@ struct BubbleArgs {
     const int32_t* bub;
     const int32_t* bub_off;  // [n_bubbles], largest bubbles first
     int32_t n_bubbles;
-    double* contrib;         // [bubble words / 2] -p_s * posterior per bubble edge
+    double* contrib;         // [bubble words / 2] -p_s * posterior per bubble edge (grad == null)
+    double* grad;            // or: [n_params] atomically accumulated (out + 1)
     double* ll_part;         // [waves in grid]
     double* logq;            // [S] or null: log Z added to the string's entry
+    const unsigned* halted;
 };
 
 // The per-iteration tail, one launch: out[1+j] += sum over blocks of the
@@ -201,6 +205,7 @@ struct TailArgs {
     int32_t n_ll;
     int32_t n_params;
     double* out;                 // [1 + n_params]
+    const unsigned* halted;
 };
 
 hipError_t configure_kernels(int max_dynamic_lds);
@@ -215,6 +220,45 @@ hipError_t launch_publish(const double* out, const Publish& pub, hipStream_t str
 // buffers padded to an even count)
 hipError_t launch_stage(const double* host_w, double* w, int32_t n, hipStream_t stream);
 // also zeroes out[0..n_out) (the accumulators of this iteration)
+// Device-resident QuasiNewton step (qn_kernel.hip): one workgroup updates x
+// and lambda from out = [LL, grad_full] and writes the next w_full; its info
+// row [KL, graderr, g_min, g_max, lambda_min, 0, 0, status] goes to a
+// host-mapped ring slot, then the completion flag is bumped.
+constexpr int kQnRow = 8;
+constexpr unsigned kQnRan = 0, kQnHalted = 1, kQnNonFinite = 2, kQnSkipped = 3;
+struct QnArgs {
+    const double* out;           // [1 + n_full]
+    // without a communicator the tail kernel is skipped: the gradient is
+    // out[1+j] + fixed[j] (bubble/fallback atomics + the constant trivial
+    // part) and the log-likelihood the sum of ll_part[0, n_ll); else (null)
+    // out is final
+    const double* fixed;
+    const double* ll_part;
+    int32_t n_ll;
+    int32_t n_full, n, k;
+    const int32_t* full_of;      // [n] full index of each kept parameter
+    const int32_t* trim;         // [n_full] trimmed index / -1 / -2
+    const int32_t* ccol;         // [n] constraint of each parameter
+    const int32_t* cptr;         // [k+1] constraint c owns parameters [cptr[c], cptr[c+1])
+    double* x;
+    double* lambda;
+    double* expx;
+    double* grad;
+    double* w_full;              // [n_full + 1] (zero slot)
+    double* partial;             // [qn_update_blocks(k)][4]
+    int32_t n_partial;
+    double plogp, eta, tol;
+    int32_t exp_lambda;
+    int32_t slot;                // ring slot of this step
+    unsigned* halted;            // device: nonzero after a halting step
+    unsigned* seq;               // device sequence counter
+    unsigned* host_flag;         // host-mapped completion flag
+    double* host_ring;           // host-mapped [slots][kQnRow]
+};
+int qn_update_blocks(int32_t k);
+hipError_t launch_qn(const QnArgs& a, hipStream_t stream);
+hipError_t launch_qn_weights(const double* x, const int32_t* trim, int32_t n_full, double* w_full,
+                             hipStream_t stream);
 hipError_t launch_edge_weights(const double* w_full, const int32_t* pptr, const int32_t* pidx, double* lw,
                                double* ew, EdgeRec* erec, int64_t n_edges, double* out, int64_t n_out,
                                hipStream_t stream);

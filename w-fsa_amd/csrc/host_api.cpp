@@ -1,6 +1,7 @@
 // C ABI over the host mirror (include/wfsa_host.h).  Exceptions stop here.
 #include "wfsa_host.h"
 
+#include <algorithm>
 #include <cmath>
 #include <cstdio>
 #include <cstring>
@@ -265,18 +266,8 @@ int wfsa_learner_run(wfsa_learner* l, double eta, double tol, int32_t max_epochs
                      int32_t* epochs_done) {
     if (!l) return null_arg("learner");
     if (epochs_done) *epochs_done = 0;
-    return guarded([&] {   // src/main.cpp:276-303
-        QuasiNewtonLearner& q = *l->qn;
-        for (int32_t e = 1; e <= max_epochs; ++e) {
-            q.OptimizationStep(eta, false);
-            const auto v = q.GetOptimizationInfo();
-            if (info_rows)
-                for (size_t i = 0; i < 7; ++i) info_rows[size_t(e - 1) * 7 + i] = i < v.size() ? v[i] : 0.0;
-            if (epochs_done) *epochs_done = e;
-            for (double x : v)
-                if (!std::isfinite(x)) throw LearnerError(x, " detected at epoch ", e);
-            if (q.HaltCondition(tol)) break;
-        }
+    return guarded([&] {   // src/main.cpp:276-303, device-resident
+        l->qn->RunDevice(eta, tol, max_epochs, info_rows, epochs_done);
     });
 }
 

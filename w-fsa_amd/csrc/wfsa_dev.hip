@@ -97,6 +97,8 @@ constexpr int kNumCu = 256;
 constexpr int kWave = 64;
 constexpr int kCompiledBlock = 512;
 constexpr int kMaxWavesPerCu = 32;
+constexpr int kQnDepth = 8;   // device-resident QN steps in flight
+constexpr int kTimingStride = 4;   // QN runs time every 4th step's kernels
 
 // weights after the results in the host-mapped buffer, 16-byte aligned
 inline size_t weights_off(int32_t np) { return (size_t(np) + 3) & ~size_t(1); }
@@ -107,7 +109,9 @@ struct wfsa_dev {
     int device = 0;
     int n_cu = kNumCu;
     hipStream_t stream = nullptr;
-    hipEvent_t ev0 = nullptr, ev1 = nullptr, k0 = nullptr, kc = nullptr, k1 = nullptr, k2 = nullptr;
+    hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    // per in-flight step: before the stream kernel, after it, after the tail
+    hipEvent_t k0[kQnDepth] = {}, kc[kQnDepth] = {}, k2[kQnDepth] = {};
 
     // model
     bool has_model = false;
@@ -179,6 +183,7 @@ struct wfsa_dev {
     unsigned seq = 0;            // last sequence number the host expects
     bool timing_pending = false; // events of the last call not yet read
     bool kernel_timing = true;
+    bool bubble_atomic = false;  // bubble gradients by global atomics (WFSA_BUBBLE_ATOMIC=1; measured slower)
     DevBuf<double> gpart;        // per-block partial gradients of the compiled kernel
 
     // the per-iteration device sequence, captured once per prepared corpus
@@ -188,6 +193,16 @@ struct wfsa_dev {
     bool use_graph = false;    // WFSA_GRAPH=1: replay a captured graph (no per-kernel timing)
     bool in_flight = false;    // between objective_grad_begin and _end
     bool logq_ready = false;   // the call in flight computes log q
+
+    // device-resident QuasiNewton (wfsa_dev_qn_*)
+    bool qn_ready = false;
+    int32_t qn_n = 0, qn_k = 0, qn_exp_lambda = 0;
+    double qn_plogp = 0.0;
+    DevBuf<int32_t> qn_trim, qn_full_of, qn_ccol, qn_cptr;
+    DevBuf<double> qn_x, qn_lambda, qn_expx, qn_grad, qn_partial;
+    DevBuf<unsigned> qn_halted;
+    double* qn_ring = nullptr;       // host-mapped [kQnDepth][kQnRow]
+    double* qn_ring_dev = nullptr;
 
     // communicator
     ncclComm_t comm = nullptr;
@@ -301,11 +316,14 @@ int configure_tiers(wfsa_dev* ctx) {
 // corpus.
 void drop_graph(wfsa_dev* ctx);
 
-int enqueue_compiled(wfsa_dev* ctx, bool with_grad, bool want_logq);
+int enqueue_compiled(wfsa_dev* ctx, bool with_grad, bool want_logq, const unsigned* halted = nullptr,
+                     int slot = -1);
 
-// per-kernel timing events (WFSA_TIMING=0 leaves them out)
-hipError_t record(wfsa_dev* ctx, hipEvent_t ev, hipStream_t s) {
-    return ctx->kernel_timing ? hipEventRecord(ev, s) : hipSuccess;
+// per-kernel timing events of slot `slot` (< 0: this launch is not timed;
+// WFSA_TIMING=0 leaves them all out).  An event between two kernels costs a
+// few microseconds of idle device, so QN runs time a sample of their steps.
+hipError_t record(wfsa_dev* ctx, hipEvent_t* evs, int slot, hipStream_t s) {
+    return ctx->kernel_timing && slot >= 0 ? hipEventRecord(evs[slot], s) : hipSuccess;
 }
 
 wfsa::Publish publish_args(wfsa_dev* ctx) {
@@ -322,14 +340,13 @@ int collect_timing(wfsa_dev* ctx) {
     if (!ctx->timing_pending) return WFSA_OK;
     ctx->timing_pending = false;
     HIP_TRY(hipEventSynchronize(ctx->ev1));
-    float c_ms = 0.f, b_ms = 0.f, f_ms = 0.f, all_ms = 0.f;
+    float c_ms = 0.f, fb_ms = 0.f, all_ms = 0.f;
     if (!ctx->graph_exec && ctx->kernel_timing) {   // events inside a captured graph are not timeable
-        HIP_TRY(hipEventElapsedTime(&c_ms, ctx->k0, ctx->kc));
-        HIP_TRY(hipEventElapsedTime(&b_ms, ctx->kc, ctx->k1));
-        HIP_TRY(hipEventElapsedTime(&f_ms, ctx->k1, ctx->k2));
+        HIP_TRY(hipEventElapsedTime(&c_ms, ctx->k0[0], ctx->kc[0]));
+        HIP_TRY(hipEventElapsedTime(&fb_ms, ctx->k0[0], ctx->k2[0]));
     }
     HIP_TRY(hipEventElapsedTime(&all_ms, ctx->ev0, ctx->ev1));
-    const double fb = double(c_ms) + double(b_ms) + double(f_ms);
+    const double fb = double(fb_ms);
     ctx->stats.fb_launches += 1;
     ctx->stats.fb_kernel_ms += fb;
     ctx->stats.last_fb_kernel_ms = fb;
@@ -340,17 +357,18 @@ int collect_timing(wfsa_dev* ctx) {
     return WFSA_OK;
 }
 
-// Wait for the published sequence number: poll the host-mapped flag, and
-// the stream now and then so a failed launch surfaces as an error.
-int wait_published(wfsa_dev* ctx) {
-    const unsigned want = ctx->seq;
+// Wait until the published sequence number reaches `want` (wrapping
+// compare): poll the host-mapped flag, and the stream now and then so a
+// failed launch surfaces as an error.
+int wait_published(wfsa_dev* ctx, unsigned want) {
+    auto reached = [&] { return int(__atomic_load_n(ctx->flag, __ATOMIC_ACQUIRE) - want) >= 0; };
     for (uint64_t spin = 1;; ++spin) {
-        if (__atomic_load_n(ctx->flag, __ATOMIC_ACQUIRE) == want) return WFSA_OK;
+        if (reached()) return WFSA_OK;
         if ((spin & 0x3fff) == 0) {
             const hipError_t e = hipStreamQuery(ctx->stream);
             if (e == hipSuccess) {
-                if (__atomic_load_n(ctx->flag, __ATOMIC_ACQUIRE) == want) return WFSA_OK;
-                return fail(WFSA_ERR_HIP, "device finished without publishing the result (sequence %u)", want);
+                if (reached()) return WFSA_OK;
+                return fail(WFSA_ERR_HIP, "device finished without publishing (sequence %u)", want);
             }
             if (e != hipErrorNotReady) return fail(WFSA_ERR_HIP, "device failure: %s", hipGetErrorString(e));
         }
@@ -649,7 +667,7 @@ int prepare(wfsa_dev* ctx, int level) {
 // edge-weight kernel unless the kernel folds that into its prologue (it does
 // when it stages w in LDS).  with_grad: the preparation-time gradient pass
 // (followed by its slab reduction into out); else the per-iteration pass.
-int enqueue_compiled(wfsa_dev* ctx, bool with_grad, bool want_logq) {
+int enqueue_compiled(wfsa_dev* ctx, bool with_grad, bool want_logq, const unsigned* halted, int slot) {
     hipStream_t s = ctx->stream;
     const int32_t np = ctx->n_params;
     const int tables = with_grad ? ctx->c_tables : ctx->i_tables;
@@ -657,7 +675,7 @@ int enqueue_compiled(wfsa_dev* ctx, bool with_grad, bool want_logq) {
     if (!fused)
         HIP_TRY(wfsa::launch_edge_weights(ctx->w_full.ptr, ctx->pptr.ptr, ctx->pidx.ptr, ctx->lw.ptr, ctx->ew.ptr,
                                           ctx->erec.ptr, ctx->n_edges + ctx->n_end, ctx->out.ptr, int64_t(np) + 1, s));
-    if (!with_grad) HIP_TRY(record(ctx, ctx->k0, s));
+    if (!with_grad) HIP_TRY(record(ctx, ctx->k0, slot, s));
     if (ctx->n_groups > 0) {
         wfsa::CompiledArgs c{};
         c.m = model_view(ctx);
@@ -683,10 +701,11 @@ int enqueue_compiled(wfsa_dev* ctx, bool with_grad, bool want_logq) {
         c.out = ctx->out.ptr;
         c.ll_part = ctx->ll_part.ptr;
         c.logq = want_logq ? ctx->logq.ptr : nullptr;
+        c.halted = halted;
         if (with_grad) HIP_TRY(wfsa::launch_compiled(c, ctx->c_grid, kCompiledBlock, ctx->c_lds, s));
         else HIP_TRY(wfsa::launch_compiled(c, ctx->i_grid, ctx->i_block, ctx->i_lds, s));
     }
-    if (!with_grad) HIP_TRY(record(ctx, ctx->kc, s));
+    if (!with_grad) HIP_TRY(record(ctx, ctx->kc, slot, s));
     if (with_grad) {
         wfsa::TailArgs t{};
         t.gpart = ctx->gpart.ptr;
@@ -705,11 +724,13 @@ int enqueue_compiled(wfsa_dev* ctx, bool with_grad, bool want_logq) {
 // compiled streams (with the per-edge weights) + bubbles (timed by k0..k1),
 // traversal fallback (k1..k2), the tail reduction (which adds the trivial
 // words' constant gradient), and -- without a communicator -- the results out.
-int enqueue_iteration(wfsa_dev* ctx, bool want_logq) {
+// The evaluation kernels; with_tail: finish out = [LL, grad_full] with the
+// tail kernel (else the consumer adds fixed_grad and sums ll_part[0, *n_ll)).
+int enqueue_evaluation(wfsa_dev* ctx, bool want_logq, const unsigned* halted, int slot, bool with_tail = true,
+                       int32_t* n_ll = nullptr) {
     hipStream_t s = ctx->stream;
     const int32_t np = ctx->n_params;
-    HIP_TRY(wfsa::launch_stage(ctx->pinned_dev + weights_off(np), ctx->w_full.ptr, np, s));
-    if (int rc = enqueue_compiled(ctx, false, want_logq)) return rc;
+    if (int rc = enqueue_compiled(ctx, false, want_logq, halted, slot)) return rc;
     int32_t wave_off = ctx->n_groups > 0 ? ctx->i_grid * (ctx->i_block / kWave) : 0;
     if (ctx->n_bubbles > 0) {
         wfsa::BubbleArgs b{};
@@ -719,12 +740,13 @@ int enqueue_iteration(wfsa_dev* ctx, bool want_logq) {
         b.bub_off = ctx->bub_off.ptr;
         b.n_bubbles = ctx->n_bubbles;
         b.contrib = ctx->contrib.ptr;
+        b.grad = ctx->bubble_atomic ? ctx->out.ptr + 1 : nullptr;
         b.ll_part = ctx->ll_part.ptr + wave_off;
         b.logq = want_logq ? ctx->logq.ptr : nullptr;
+        b.halted = halted;
         HIP_TRY(wfsa::launch_bubbles(b, ctx->b_grid, s));
         wave_off += ctx->b_grid * (wfsa::kBubbleBlock / kWave);
     }
-    HIP_TRY(record(ctx, ctx->k1, s));
     for (int t = 0; t < 2; ++t) {
         if (!ctx->n_fall[t]) continue;
         wfsa::TravArgs a = trav_args(ctx, t);
@@ -733,10 +755,15 @@ int enqueue_iteration(wfsa_dev* ctx, bool want_logq) {
         a.grad = ctx->out.ptr + 1;
         a.ll_part = ctx->ll_part.ptr + wave_off;
         a.logq = want_logq ? ctx->logq.ptr : nullptr;
+        a.halted = halted;
         HIP_TRY(wfsa::launch_trav(wfsa::MODE_WEIGHTED, a, ctx->fall_grid[t], s));
         wave_off += ctx->fall_grid[t] * ctx->cfg[t].waves_per_block;
     }
-    HIP_TRY(record(ctx, ctx->k2, s));
+    if (n_ll) *n_ll = wave_off;
+    if (!with_tail) {
+        HIP_TRY(record(ctx, ctx->k2, slot, s));
+        return WFSA_OK;
+    }
     wfsa::TailArgs t{};
     t.gpart = ctx->fixed_grad.ptr;
     t.n_gpart = ctx->n_groups > 0 ? 1 : 0;
@@ -744,13 +771,72 @@ int enqueue_iteration(wfsa_dev* ctx, bool want_logq) {
     t.chunk_ptr = ctx->bg_chunk_ptr.ptr;
     t.slot = ctx->bg_slot.ptr;
     t.contrib = ctx->contrib.ptr;
-    t.n_chunks = ctx->n_bubbles > 0 ? ctx->n_bg_chunks : 0;
+    t.n_chunks = (ctx->n_bubbles > 0 && !ctx->bubble_atomic) ? ctx->n_bg_chunks : 0;
     t.ll_part = ctx->ll_part.ptr;
     t.n_ll = wave_off;
     t.n_params = np;
     t.out = ctx->out.ptr;
+    t.halted = halted;
     HIP_TRY(wfsa::launch_tail(t, s));
+    HIP_TRY(record(ctx, ctx->k2, slot, s));
+    return WFSA_OK;
+}
+
+// One objective/gradient evaluation for the host: weights staged from the
+// host-mapped buffer, the evaluation, and -- without a communicator -- the
+// results published (with one, _begin all-reduces first).
+int enqueue_iteration(wfsa_dev* ctx, bool want_logq) {
+    hipStream_t s = ctx->stream;
+    const int32_t np = ctx->n_params;
+    HIP_TRY(wfsa::launch_stage(ctx->pinned_dev + weights_off(np), ctx->w_full.ptr, np, s));
+    if (int rc = enqueue_evaluation(ctx, want_logq, nullptr, 0)) return rc;
     if (!ctx->comm) HIP_TRY(wfsa::launch_publish(ctx->out.ptr, publish_args(ctx), s));
+    return WFSA_OK;
+}
+
+// One device-resident QuasiNewton step: the evaluation at the device's
+// w_full, the all-reduce, the update (which writes the next w_full and
+// publishes the info row of ring slot `slot`).
+int enqueue_qn_step(wfsa_dev* ctx, double eta, double tol, int slot, bool timed) {
+    hipStream_t s = ctx->stream;
+    const int32_t np = ctx->n_params;
+    // without a communicator the QN kernel finishes the reduction itself
+    const bool tail = ctx->comm != nullptr || !ctx->bubble_atomic;
+    int32_t n_ll = 0;
+    if (int rc = enqueue_evaluation(ctx, false, ctx->qn_halted.ptr, timed ? slot : -1, tail, &n_ll)) return rc;
+    if (ctx->comm)
+        RCCL_TRY(ncclAllReduce(ctx->out.ptr, ctx->out.ptr, size_t(np) + 1, ncclDouble, ncclSum, ctx->comm, s));
+    wfsa::QnArgs q{};
+    q.out = ctx->out.ptr;
+    if (!tail) {
+        q.fixed = ctx->n_groups > 0 ? ctx->fixed_grad.ptr : nullptr;
+        q.ll_part = ctx->ll_part.ptr;
+        q.n_ll = n_ll;
+    }
+    q.n_full = np;
+    q.n = ctx->qn_n;
+    q.k = ctx->qn_k;
+    q.full_of = ctx->qn_full_of.ptr;
+    q.trim = ctx->qn_trim.ptr;
+    q.ccol = ctx->qn_ccol.ptr;
+    q.cptr = ctx->qn_cptr.ptr;
+    q.x = ctx->qn_x.ptr;
+    q.lambda = ctx->qn_lambda.ptr;
+    q.expx = ctx->qn_expx.ptr;
+    q.grad = ctx->qn_grad.ptr;
+    q.w_full = ctx->w_full.ptr;
+    q.partial = ctx->qn_partial.ptr;
+    q.n_partial = wfsa::qn_update_blocks(ctx->qn_k);
+    q.plogp = ctx->qn_plogp;
+    q.eta = eta;
+    q.tol = tol;
+    q.exp_lambda = ctx->qn_exp_lambda;
+    q.slot = slot;
+    q.halted = ctx->qn_halted.ptr;
+    q.seq = ctx->counters.ptr;
+    q.host_flag = ctx->flag_dev;
+    q.host_ring = ctx->qn_ring_dev;
+    HIP_TRY(wfsa::launch_qn(q, s));
     return WFSA_OK;
 }
 
@@ -787,8 +873,12 @@ int wfsa_dev_create(int device, wfsa_dev** out) {
     ctx->n_cu = prop.multiProcessorCount > 0 ? prop.multiProcessorCount : kNumCu;
     if (const char* e = std::getenv("WFSA_GRAPH")) ctx->use_graph = e[0] == '1';
     if (const char* e = std::getenv("WFSA_TIMING")) ctx->kernel_timing = e[0] != '0';
+    if (const char* e = std::getenv("WFSA_BUBBLE_ATOMIC")) ctx->bubble_atomic = e[0] == '1';
     HIP_TRY(hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking));
-    for (hipEvent_t* ev : {&ctx->ev0, &ctx->ev1, &ctx->k0, &ctx->kc, &ctx->k1, &ctx->k2}) HIP_TRY(hipEventCreate(ev));
+    HIP_TRY(hipEventCreate(&ctx->ev0));
+    HIP_TRY(hipEventCreate(&ctx->ev1));
+    for (int i = 0; i < kQnDepth; ++i)
+        for (hipEvent_t* ev : {&ctx->k0[i], &ctx->kc[i], &ctx->k2[i]}) HIP_TRY(hipEventCreate(ev));
     HIP_TRY(ctx->live.alloc(1));
     HIP_TRY(hipHostMalloc(reinterpret_cast<void**>(&ctx->flag), 64, hipHostMallocMapped | hipHostMallocCoherent));
     HIP_TRY(hipHostGetDevicePointer(reinterpret_cast<void**>(&ctx->flag_dev), ctx->flag, 0));
@@ -808,8 +898,12 @@ void wfsa_dev_destroy(wfsa_dev* ctx) {
     if (ctx->comm) (void)ncclCommDestroy(ctx->comm);
     if (ctx->pinned) (void)hipHostFree(ctx->pinned);
     if (ctx->flag) (void)hipHostFree(ctx->flag);
-    for (hipEvent_t ev : {ctx->ev0, ctx->ev1, ctx->k0, ctx->kc, ctx->k1, ctx->k2})
+    for (hipEvent_t ev : {ctx->ev0, ctx->ev1})
         if (ev) (void)hipEventDestroy(ev);
+    for (int i = 0; i < kQnDepth; ++i)
+        for (hipEvent_t ev : {ctx->k0[i], ctx->kc[i], ctx->k2[i]})
+            if (ev) (void)hipEventDestroy(ev);
+    if (ctx->qn_ring) (void)hipHostFree(ctx->qn_ring);
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
     delete ctx;
 }
@@ -984,7 +1078,7 @@ int wfsa_dev_objective_grad_end(wfsa_dev* ctx, double* loglik, double* grad_full
     ctx->in_flight = false;
     hipStream_t s = ctx->stream;
     const int32_t np = ctx->n_params;
-    if (int rc = wait_published(ctx)) return rc;
+    if (int rc = wait_published(ctx, ctx->seq)) return rc;
     ctx->timing_pending = true;
     if (loglik) *loglik = ctx->pinned[0];
     if (grad_full && np > 0) std::memcpy(grad_full, ctx->pinned + 1, size_t(np) * sizeof(double));
@@ -1000,6 +1094,141 @@ int wfsa_dev_objective_grad_end(wfsa_dev* ctx, double* loglik, double* grad_full
 int wfsa_dev_objective_grad(wfsa_dev* ctx, const double* w_full, double* loglik, double* grad_full, double* logq) {
     if (int rc = wfsa_dev_objective_grad_begin(ctx, w_full, logq != nullptr)) return rc;
     return wfsa_dev_objective_grad_end(ctx, loglik, grad_full, logq);
+}
+
+int wfsa_dev_qn_setup(wfsa_dev* ctx, const wfsa_qn_desc* d) {
+    if (int rc = check_ctx(ctx)) return rc;
+    if (!d || d->n_params < 0 || d->n_constraints < 0) return fail(WFSA_ERR_ARG, "bad QN description");
+    if (!ctx->has_model) return fail(WFSA_ERR_ARG, "load a model first");
+    const int32_t nf = ctx->n_params, n = d->n_params, k = d->n_constraints;
+    if ((nf > 0 && !d->trim) || (n > 0 && !d->ccol)) return fail(WFSA_ERR_ARG, "null trim/ccol");
+    std::vector<int32_t> full_of(size_t(std::max(n, 1)), -1), cptr(size_t(k) + 1, 0);
+    for (int32_t j = 0; j < nf; ++j) {
+        const int32_t t = d->trim[j];
+        if (t >= n || t < -2) return fail(WFSA_ERR_ARG, "trimmed index %d of parameter %d out of range", t, j);
+        if (t >= 0) {
+            if (full_of[size_t(t)] >= 0) return fail(WFSA_ERR_ARG, "trimmed index %d used twice", t);
+            full_of[size_t(t)] = j;
+        }
+    }
+    for (int32_t i = 0; i < n; ++i) {
+        if (full_of[size_t(i)] < 0) return fail(WFSA_ERR_ARG, "kept parameter %d has no full index", i);
+        const int32_t c = d->ccol[i];
+        if (c < 0 || c >= k) return fail(WFSA_ERR_ARG, "constraint %d of parameter %d out of range", c, i);
+        // Learner::BuildConstraints numbers the members of a group consecutively
+        if (i > 0 && c < d->ccol[i - 1]) return fail(WFSA_ERR_ARG, "constraint columns must be non-decreasing");
+        cptr[size_t(c) + 1]++;
+    }
+    for (int32_t c = 0; c < k; ++c) cptr[size_t(c) + 1] += cptr[size_t(c)];
+    hipStream_t s = ctx->stream;
+    if (nf > 0) HIP_TRY(ctx->qn_trim.upload(d->trim, size_t(nf), s));
+    HIP_TRY(ctx->qn_full_of.upload(full_of.data(), full_of.size(), s));
+    if (n > 0) HIP_TRY(ctx->qn_ccol.upload(d->ccol, size_t(n), s));
+    HIP_TRY(ctx->qn_cptr.upload(cptr.data(), cptr.size(), s));
+    for (DevBuf<double>* b : {&ctx->qn_x, &ctx->qn_expx, &ctx->qn_grad}) HIP_TRY(b->alloc(size_t(std::max(n, 1))));
+    HIP_TRY(ctx->qn_lambda.alloc(size_t(std::max(k, 1))));
+    HIP_TRY(ctx->qn_partial.alloc(size_t(wfsa::qn_update_blocks(k)) * 4));
+    HIP_TRY(ctx->qn_halted.alloc(1));
+    if (!ctx->qn_ring) {
+        HIP_TRY(hipHostMalloc(reinterpret_cast<void**>(&ctx->qn_ring), sizeof(double) * kQnDepth * wfsa::kQnRow,
+                              hipHostMallocMapped | hipHostMallocCoherent));
+        HIP_TRY(hipHostGetDevicePointer(reinterpret_cast<void**>(&ctx->qn_ring_dev), ctx->qn_ring, 0));
+    }
+    HIP_TRY(hipStreamSynchronize(s));
+    ctx->qn_n = n;
+    ctx->qn_k = k;
+    ctx->qn_plogp = d->plogp;
+    ctx->qn_exp_lambda = d->exponential_lambda ? 1 : 0;
+    ctx->qn_ready = true;
+    return WFSA_OK;
+}
+
+int wfsa_dev_qn_set_state(wfsa_dev* ctx, const double* x, const double* lambda) {
+    if (int rc = check_ctx(ctx)) return rc;
+    if (!ctx->qn_ready) return fail(WFSA_ERR_ARG, "wfsa_dev_qn_setup has not run");
+    if ((ctx->qn_n > 0 && !x) || (ctx->qn_k > 0 && !lambda)) return fail(WFSA_ERR_ARG, "null state");
+    if (ctx->in_flight) return fail(WFSA_ERR_ARG, "an evaluation is in flight");
+    hipStream_t s = ctx->stream;
+    if (ctx->qn_n > 0) HIP_TRY(ctx->qn_x.upload(x, size_t(ctx->qn_n), s));
+    if (ctx->qn_k > 0) HIP_TRY(ctx->qn_lambda.upload(lambda, size_t(ctx->qn_k), s));
+    HIP_TRY(wfsa::launch_qn_weights(ctx->qn_x.ptr, ctx->qn_trim.ptr, ctx->n_params, ctx->w_full.ptr, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    return WFSA_OK;
+}
+
+int wfsa_dev_qn_get_state(wfsa_dev* ctx, double* x, double* lambda, double* grad) {
+    if (int rc = check_ctx(ctx)) return rc;
+    if (!ctx->qn_ready) return fail(WFSA_ERR_ARG, "wfsa_dev_qn_setup has not run");
+    hipStream_t s = ctx->stream;
+    if (x && ctx->qn_n > 0) HIP_TRY(ctx->qn_x.download(x, size_t(ctx->qn_n), s));
+    if (lambda && ctx->qn_k > 0) HIP_TRY(ctx->qn_lambda.download(lambda, size_t(ctx->qn_k), s));
+    if (grad && ctx->qn_n > 0) HIP_TRY(ctx->qn_grad.download(grad, size_t(ctx->qn_n), s));
+    HIP_TRY(hipStreamSynchronize(s));
+    return WFSA_OK;
+}
+
+int wfsa_dev_qn_run(wfsa_dev* ctx, double eta, double tol, int32_t max_steps, double* info_rows,
+                    int32_t* steps_done, int32_t* status) {
+    if (int rc = check_ctx(ctx)) return rc;
+    if (steps_done) *steps_done = 0;
+    if (status) *status = 0;
+    if (!ctx->qn_ready) return fail(WFSA_ERR_ARG, "wfsa_dev_qn_setup has not run");
+    if (!ctx->has_corpus) return fail(WFSA_ERR_ARG, "load a corpus first");
+    if (ctx->in_flight) return fail(WFSA_ERR_ARG, "an evaluation is in flight");
+    if (max_steps <= 0) return WFSA_OK;
+    if (ctx->prep_level < 2)
+        if (int rc = prepare(ctx, 2)) return rc;
+    if (int rc = collect_timing(ctx)) return rc;
+    hipStream_t s = ctx->stream;
+    HIP_TRY(hipMemsetAsync(ctx->qn_halted.ptr, 0, sizeof(unsigned), s));
+    const unsigned base = ctx->seq;
+    int32_t enq = 0, done = 0, st = 0;
+    bool stop = false;
+    double c_ms_sum = 0.0, fb_ms_sum = 0.0;
+    int64_t timed = 0;
+    while (done < max_steps) {
+        while (!stop && enq < max_steps && enq - done < kQnDepth) {
+            if (int rc = enqueue_qn_step(ctx, eta, tol, enq % kQnDepth, enq % kTimingStride == 0)) return rc;
+            ++enq;
+            ++ctx->seq;
+        }
+        if (done >= enq) break;
+        if (int rc = wait_published(ctx, base + unsigned(done) + 1u)) return rc;
+        const int slot = done % kQnDepth;
+        const double* row = ctx->qn_ring + size_t(slot) * wfsa::kQnRow;
+        const unsigned rs = unsigned(row[7]);
+        if (ctx->kernel_timing && done % kTimingStride == 0) {
+            float c = 0.f, f = 0.f;
+            if (hipEventSynchronize(ctx->k2[slot]) == hipSuccess &&
+                hipEventElapsedTime(&c, ctx->k0[slot], ctx->kc[slot]) == hipSuccess &&
+                hipEventElapsedTime(&f, ctx->k0[slot], ctx->k2[slot]) == hipSuccess) {
+                c_ms_sum += c;
+                fb_ms_sum += f;
+                ++timed;
+                ctx->stats.last_compiled_ms = c;
+                ctx->stats.last_fb_kernel_ms = f;
+            }
+        }
+        if (rs == wfsa::kQnSkipped) return fail(WFSA_ERR_HIP, "QN step %d skipped before a halt", done);
+        if (info_rows)
+            for (int i = 0; i < 7; ++i) info_rows[size_t(done) * 7 + size_t(i)] = row[i];
+        ++done;
+        if (rs == wfsa::kQnHalted || rs == wfsa::kQnNonFinite) {
+            st = int(rs);
+            stop = true;
+            break;
+        }
+    }
+    // drain the steps enqueued after a halt (they are no-ops)
+    if (enq > done)
+        if (int rc = wait_published(ctx, base + unsigned(enq))) return rc;
+    HIP_TRY(hipStreamSynchronize(s));
+    ctx->stats.fb_launches += timed;
+    ctx->stats.fb_kernel_ms += fb_ms_sum;
+    ctx->stats.compiled_kernel_ms += c_ms_sum;
+    if (steps_done) *steps_done = done;
+    if (status) *status = st;
+    return WFSA_OK;
 }
 
 int wfsa_dev_comm_unique_id(uint8_t id[WFSA_COMM_ID_BYTES]) {

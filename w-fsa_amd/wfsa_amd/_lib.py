@@ -67,6 +67,10 @@ _SIGS = {
     "wfsa_dev_objective_grad": (C.c_int, [vp, vp, P(dbl), vp, vp]),
     "wfsa_dev_objective_grad_begin": (C.c_int, [vp, vp, C.c_int]),
     "wfsa_dev_objective_grad_end": (C.c_int, [vp, P(dbl), vp, vp]),
+    "wfsa_dev_qn_setup": (C.c_int, [vp, vp]),
+    "wfsa_dev_qn_set_state": (C.c_int, [vp, vp, vp]),
+    "wfsa_dev_qn_get_state": (C.c_int, [vp, vp, vp, vp]),
+    "wfsa_dev_qn_run": (C.c_int, [vp, dbl, dbl, i32, vp, P(i32), P(i32)]),
     "wfsa_dev_comm_unique_id": (C.c_int, [vp]),
     "wfsa_dev_comm_init": (C.c_int, [vp, C.c_int, C.c_int, vp]),
     "wfsa_dev_allreduce": (C.c_int, [vp, vp, i64]),
