@@ -35,6 +35,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
 
 namespace wfsa {
 
@@ -637,18 +638,34 @@ __device__ __forceinline__ void edge_weight_slice(const CompiledArgs& a) {
 // hold multi-parameter words (MULTI, automata with epsilon composites) take
 // a second, per-word pass.  Loads are unconditional up to the group's
 // longest lane (shorter lanes read their padding chunks), D chunks in flight.
-template <bool WIDE, bool W_LDS, bool MULTI>
+// DBG (timing experiments only, WFSA_FBS_DBG): 1 no table gathers, 3 no
+// stream pass at all, 4 neither stream pass nor table staging, 5 return at once
+template <bool WIDE, bool W_LDS, bool MULTI, int DBG = 0>
 __global__ __launch_bounds__(1024) void fbs_kernel(CompiledArgs a) {
     if (a.halted && *a.halted) return;
+    if (DBG == 5) return;
     extern __shared__ __attribute__((aligned(16))) double lds[];
     const int lane = lane_id();
     const int wpb = int(blockDim.x) / kWave;
     const int gw = __builtin_amdgcn_readfirstlane(int(blockIdx.x) * wpb + int(threadIdx.x) / kWave);
     const int nw = int(gridDim.x) * wpb;
     const uint32_t zslot = uint32_t(a.n_params);
-    if (W_LDS) {
-        for (int j = int(threadIdx.x); j <= a.n_params; j += int(blockDim.x)) lds[j] = a.w[j];
-        edge_weight_slice(a);
+    if (W_LDS && DBG != 4) {
+        // stage w[0, n_params] in 16-byte pieces, all of a thread's loads
+        // issued before its first store (loads and stores unconditional --
+        // an index past the end is clamped to the last piece, which is then
+        // written twice with the same value -- so nothing is branched around)
+        const int n2 = (a.n_params + 2) / 2;
+        const double2* src = reinterpret_cast<const double2*>(a.w);
+        double2* dst = reinterpret_cast<double2*>(lds);
+        constexpr int kB = 8;
+        for (int j0 = int(threadIdx.x); j0 < n2; j0 += kB * int(blockDim.x)) {
+            double2 t[kB];
+#pragma unroll
+            for (int b = 0; b < kB; ++b) t[b] = src[min(j0 + b * int(blockDim.x), n2 - 1)];
+#pragma unroll
+            for (int b = 0; b < kB; ++b) dst[min(j0 + b * int(blockDim.x), n2 - 1)] = t[b];
+        }
         __syncthreads();
     }
     const double* wsrc = W_LDS ? lds : a.w;
@@ -656,10 +673,9 @@ __global__ __launch_bounds__(1024) void fbs_kernel(CompiledArgs a) {
     for (int round = 0;; ++round) {
         const int grp = round * nw + ((round & 1) ? (nw - 1 - gw) : gw);
         if (grp >= a.n_groups) break;
-        const int s = a.l_str[grp * kWave + lane];
         const int gch = a.g_len[grp];
         const uint4* st = a.stream + a.g_base[grp] + lane;
-        const double p = s >= 0 ? a.p[s] : 0.0;
+        const double p = a.p_lane[grp * kWave + lane];   // 0 on padding lanes
         double acc0 = 0.0, acc1 = 0.0;
         // Two register sets of D chunks: one is applied while the other's
         // loads are in flight, and the sets swap roles -- no register copy of
@@ -688,8 +704,13 @@ __global__ __launch_bounds__(1024) void fbs_kernel(CompiledArgs a) {
                         if (MULTI) multi |= int(x) < -1;
                     } else {
                         const uint32_t lo = v[i] & 0xffffu, hi = v[i] >> 16;
-                        acc0 += wsrc[min(lo, zslot)];
-                        acc1 += wsrc[min(hi, zslot)];
+                        if (DBG == 1) {
+                            acc0 += double(lo);
+                            acc1 += double(hi);
+                        } else {
+                            acc0 += wsrc[min(lo, zslot)];
+                            acc1 += wsrc[min(hi, zslot)];
+                        }
                         if (MULTI) multi |= (lo >= 0x8000u && lo != 0xffffu) || (hi >= 0x8000u && hi != 0xffffu);
                     }
                 }
@@ -710,8 +731,8 @@ __global__ __launch_bounds__(1024) void fbs_kernel(CompiledArgs a) {
                 }
             }
         };
-        load(A, 0);
-        for (int c0 = 0;;) {
+        if (DBG < 3) load(A, 0);
+        for (int c0 = 0; DBG < 3;) {
             load(B, c0 + D);
             apply(A, c0);
             c0 += D;
@@ -722,13 +743,17 @@ __global__ __launch_bounds__(1024) void fbs_kernel(CompiledArgs a) {
             if (c0 >= gch) break;
         }
         const double acc = acc0 + acc1;
-        if (s >= 0) {
-            ll_acc += p * acc;
-            if (a.logq) a.logq[s] = acc;
+        ll_acc += p * acc;
+        if (a.logq) {
+            const int s = a.l_str[grp * kWave + lane];
+            if (s >= 0) a.logq[s] = acc;
         }
     }
     ll_acc = wave_sum(ll_acc);
     if (lane == 0) a.ll_part[gw] = ll_acc;
+    // this block's slice of the per-edge weights and the zeroed result, for
+    // the kernels after this one (nothing in this launch reads them)
+    if (W_LDS) edge_weight_slice(a);
 }
 
 // Bubbles: one lane per bubble (largest first).  Local forward from the
@@ -889,7 +914,11 @@ hipError_t configure_kernels(int max_dynamic_lds) {
                          reinterpret_cast<const void*>(&fbs_kernel<false, true, false>),
                          reinterpret_cast<const void*>(&fbs_kernel<false, true, true>),
                          reinterpret_cast<const void*>(&fbs_kernel<true, true, false>),
-                         reinterpret_cast<const void*>(&fbs_kernel<true, true, true>)};
+                         reinterpret_cast<const void*>(&fbs_kernel<true, true, true>),
+                         reinterpret_cast<const void*>(&fbs_kernel<false, true, false, 1>),
+                         reinterpret_cast<const void*>(&fbs_kernel<false, true, false, 3>),
+                         reinterpret_cast<const void*>(&fbs_kernel<false, true, false, 4>),
+                         reinterpret_cast<const void*>(&fbs_kernel<false, true, false, 5>)};
     for (const void* f : fns) {
         hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, max_dynamic_lds);
         if (e != hipSuccess) return e;
@@ -917,6 +946,30 @@ hipError_t launch_trav(TravMode mode, const TravArgs& a, int grid, hipStream_t s
 hipError_t launch_compiled(const CompiledArgs& a, int grid, int block, size_t lds, hipStream_t stream) {
     const dim3 g{unsigned(grid), 1, 1}, b{unsigned(block), 1, 1};
     if (!a.with_grad) {   // per-iteration form: w staged in LDS or read from global
+        static const int dbg = [] {
+            const char* e = std::getenv("WFSA_FBS_DBG");
+            return e ? std::atoi(e) : 0;
+        }();
+        if (dbg == 1) {
+            hipLaunchKernelGGL((fbs_kernel<false, true, false, 1>), g, b, lds, stream, a);
+            return hipGetLastError();
+        }
+        if (dbg == 2) {
+            hipLaunchKernelGGL((fbs_kernel<false, false, false, 0>), g, b, 0, stream, a);
+            return hipGetLastError();
+        }
+        if (dbg == 3) {
+            hipLaunchKernelGGL((fbs_kernel<false, true, false, 3>), g, b, lds, stream, a);
+            return hipGetLastError();
+        }
+        if (dbg == 4) {
+            hipLaunchKernelGGL((fbs_kernel<false, true, false, 4>), g, b, lds, stream, a);
+            return hipGetLastError();
+        }
+        if (dbg == 5) {
+            hipLaunchKernelGGL((fbs_kernel<false, true, false, 5>), g, b, lds, stream, a);
+            return hipGetLastError();
+        }
         const int key = (a.tables >= 1 ? 4 : 0) + (a.wide ? 2 : 0) + (a.multi ? 1 : 0);
         switch (key) {
             case 0: hipLaunchKernelGGL((fbs_kernel<false, false, false>), g, b, 0, stream, a); break;

@@ -141,6 +141,7 @@ struct CompiledArgs {
     const int32_t* g_len;    // [G] chunks of the group's longest lane (its first)
     const int32_t* l_str;    // [64 G] string of each lane, -1 = padding
     const int32_t* l_len;    // [64 G] words of each lane
+    const double* p_lane;    // [64 G] p of each lane's string (0 on padding lanes)
     int32_t n_groups;
     int32_t n_params;
     int32_t tables;          // with_grad: 2 w and grad staged in LDS, 1 grad in LDS, 0 global;

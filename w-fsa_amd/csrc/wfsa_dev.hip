@@ -97,6 +97,7 @@ constexpr int kNumCu = 256;
 constexpr int kWave = 64;
 constexpr int kCompiledBlock = 512;
 constexpr int kMaxWavesPerCu = 32;
+constexpr int kIterWavesPerCu = 16;   // per-iteration stream kernel
 constexpr int kQnDepth = 8;   // device-resident QN steps in flight
 constexpr int kTimingStride = 4;   // QN runs time every 4th step's kernels
 
@@ -150,6 +151,7 @@ struct wfsa_dev {
     DevBuf<uint4> stream_w;   // 16-byte chunks
     int wide = 0;             // 32-bit stream words
     DevBuf<int32_t> bub, g_len, l_str, l_len;
+    DevBuf<double> p_lane;
     DevBuf<int64_t> g_base;
     int c_grid = 0, c_tables = 0;    // gradient pass (once, at preparation)
     int i_grid = 0, i_tables = 0;    // per-iteration pass (log-weights only)
@@ -540,6 +542,14 @@ int prepare(wfsa_dev* ctx, int level) {
     HIP_TRY(ctx->g_len.upload(g_len.data(), g_len.size(), s));
     HIP_TRY(ctx->l_str.upload(l_str.data(), l_str.size(), s));
     HIP_TRY(ctx->l_len.upload(l_len.data(), l_len.size(), s));
+    {   // p in lane order (coalesced in the per-iteration kernel)
+        std::vector<double> h_p(S > 0 ? size_t(S) : 1, 0.0), pl(l_str.size(), 0.0);
+        if (S > 0) HIP_TRY(ctx->p.download(h_p.data(), size_t(S), s));
+        HIP_TRY(hipStreamSynchronize(s));
+        for (size_t k = 0; k < l_str.size(); ++k)
+            if (l_str[k] >= 0) pl[k] = h_p[size_t(l_str[k])];
+        HIP_TRY(ctx->p_lane.upload(pl.data(), pl.size(), s));
+    }
     ctx->n_groups = G;
     ctx->n_compiled = nc;
 
@@ -615,12 +625,15 @@ int prepare(wfsa_dev* ctx, int level) {
     ctx->c_grid = int(std::max<int64_t>(1, std::min<int64_t>(int64_t(ctx->n_cu) * per_cu, want_blocks)));
     if (ctx->c_tables >= 1) HIP_TRY(ctx->gpart.alloc(size_t(ctx->c_grid) * size_t(std::max(ctx->n_params, 1))));
     // the per-iteration pass keeps only w in LDS: as many blocks per CU as fit
-    ctx->i_tables = table_bytes + 8 <= size_t(kLdsPerCu - 1024) ? 1 : 0;
-    ctx->i_lds = ctx->i_tables ? table_bytes + 8 : 0;   // + the zero slot
+    ctx->i_tables = table_bytes + 16 <= size_t(kLdsPerCu - 1024) ? 1 : 0;
+    ctx->i_lds = ctx->i_tables ? table_bytes + 16 : 0;   // + the zero slot, even count
     if (const char* e = std::getenv("WFSA_IBLOCK")) ctx->i_block = std::max(64, std::min(1024, std::atoi(e))) & ~63;
     const int i_wpb = ctx->i_block / kWave;
-    int i_per_cu = kMaxWavesPerCu / i_wpb;
+    // one block per CU: every block stages the whole table, so fewer blocks
+    // stage less (measured: 1/CU beats 2/CU at c3 even at half the waves)
+    int i_per_cu = std::max(1, kIterWavesPerCu / i_wpb);
     if (ctx->i_tables) i_per_cu = std::min<int>(i_per_cu, int(size_t(kLdsPerCu) / std::max<size_t>(table_bytes, 1)));
+    if (const char* e = std::getenv("WFSA_IPERCU")) i_per_cu = std::min(i_per_cu, std::atoi(e));
     i_per_cu = std::max(1, i_per_cu);
     ctx->i_grid = int(std::max<int64_t>(1, std::min<int64_t>(int64_t(ctx->n_cu) * i_per_cu,
                                                              (int64_t(G) + i_wpb - 1) / i_wpb)));
@@ -686,6 +699,7 @@ int enqueue_compiled(wfsa_dev* ctx, bool with_grad, bool want_logq, const unsign
         c.g_len = ctx->g_len.ptr;
         c.l_str = ctx->l_str.ptr;
         c.l_len = ctx->l_len.ptr;
+        c.p_lane = ctx->p_lane.ptr;
         c.n_groups = ctx->n_groups;
         c.n_params = np;
         c.tables = tables;
