@@ -160,9 +160,9 @@ __device__ __forceinline__ bool put_trivial(const ModelView& m, int g, bool writ
 // bubbles to the bubble buffer.  Returns false when a bubble exceeds the
 // kernel limits; the string then stays on the traversal path.
 template <bool WRITE>
-__device__ bool compile_walk(const Slab& sl, const ModelView& m, int L, int sidx, int& n_main, int& n_bub,
-                             int& n_nb, void* stream, int wide, int64_t s_base, int32_t* bub, int64_t b_base,
-                             int32_t* bub_off, int32_t b_first) {
+__device__ bool compile_walk(const Slab& sl, const ModelView& m, int L, int sidx, double p, int& n_main,
+                             int& n_bub, int& n_nb, void* stream, int wide, int64_t s_base, int32_t* bub,
+                             int64_t b_base, int32_t* bub_off, int32_t b_first) {
     long long* lid = reinterpret_cast<long long*>(sl.alpha);   // alpha is dead in counting mode
     n_main = 0;
     n_bub = 0;
@@ -218,6 +218,9 @@ __device__ bool compile_walk(const Slab& sl, const ModelView& m, int L, int sidx
             bub_off[b_first + n_nb] = int32_t(w);
             bub[w++] = nodes | (edges << 16);
             bub[w++] = sidx;
+            const unsigned long long pb = __double_as_longlong(p);
+            bub[w++] = int32_t(uint32_t(pb));
+            bub[w++] = int32_t(uint32_t(pb >> 32));
             for (int e = sl.epos[a]; e < e_hi; ++e) {
                 const int h = sl.e_dst[e];
                 if (!(sl.beta[h] > 0.0)) continue;
@@ -235,7 +238,7 @@ __device__ bool compile_walk(const Slab& sl, const ModelView& m, int L, int sidx
                 }
             }
         }
-        n_bub += 2 + 2 * edges;
+        n_bub += bubble_record_words(edges);
         ++n_nb;
         if (to_end) break;
         a = b;
@@ -470,10 +473,11 @@ __global__ __launch_bounds__(256) void trav_kernel(TravArgs a) {
                 int n_main = 0, n_bub = 0, n_nb = 0;
                 bool ok;
                 if (MODE == MODE_EMIT)
-                    ok = compile_walk<true>(sl, m, L, sidx, n_main, n_bub, n_nb, a.stream, a.wide, a.s_base[sidx],
-                                            a.bub, a.b_base[sidx], a.bub_off, a.b_first[sidx]);
+                    ok = compile_walk<true>(sl, m, L, sidx, a.p[sidx], n_main, n_bub, n_nb, a.stream, a.wide,
+                                            a.s_base[sidx], a.bub, a.b_base[sidx], a.bub_off, a.b_first[sidx]);
                 else
-                    ok = compile_walk<false>(sl, m, L, sidx, n_main, n_bub, n_nb, nullptr, 0, 0, nullptr, 0, nullptr, 0);
+                    ok = compile_walk<false>(sl, m, L, sidx, 0.0, n_main, n_bub, n_nb, nullptr, 0, 0, nullptr, 0,
+                                             nullptr, 0);
                 if (MODE == MODE_COUNT) {
                     a.c_main[sidx] = ok ? n_main : 0;
                     a.c_bub[sidx] = ok ? n_bub : -1;
@@ -759,7 +763,10 @@ __global__ __launch_bounds__(1024) void fbs_kernel(CompiledArgs a) {
 // Bubbles: one lane per bubble (largest first).  Local forward from the
 // bubble's first cut, local backward from its last cut; an edge's posterior
 // is alpha(src) w beta(dst) / Z and -p_s times it goes to the edge's
-// contribution slot; log Z joins the string's log q.
+// contribution slot; log Z joins the string's log q.  A record is 16-byte
+// aligned -- [nodes | edges << 16, string, p (2 words), (edge, src | dst << 16)
+// x edges] -- so a bubble of up to kBubbleRegEdges edges is two dependent
+// rounds of loads (its record, then its edges' weights), all issued at once.
 __global__ __launch_bounds__(kBubbleBlock) void bubble_kernel(BubbleArgs a) {
     if (a.halted && *a.halted) return;
     __shared__ double scr[kBubbleBlock][2 * kMaxBubbleNodes + 1];
@@ -768,36 +775,75 @@ __global__ __launch_bounds__(kBubbleBlock) void bubble_kernel(BubbleArgs a) {
     double* A = scr[threadIdx.x];
     double* B = A + kMaxBubbleNodes;
     double ll_acc = 0.0;
+    constexpr int RE = kBubbleRegEdges;
     for (int bi = int(blockIdx.x * blockDim.x + threadIdx.x); bi < a.n_bubbles; bi += int(gridDim.x * blockDim.x)) {
         const int off = a.bub_off[bi];
-        const int hdr = a.bub[off];
-        const int s = a.bub[off + 1];
-        const int nodes = hdr & 0xffff, edges = hdr >> 16;
-        const int32_t* ed = a.bub + off + 2;
-        const double p = a.p[s];
+        const int4* rec = reinterpret_cast<const int4*>(a.bub + off);
+        const int4 h = rec[0];
+        int4 ev[RE / 2];   // edges 2q, 2q+1 (the buffer has slack after the last record)
+#pragma unroll
+        for (int q = 0; q < RE / 2; ++q) ev[q] = rec[1 + q];
+        const int nodes = h.x & 0xffff, edges = h.x >> 16;
+        const int s = h.y;
+        const double p = __longlong_as_double((long long)(uint32_t(h.z)) | ((long long)(uint32_t(h.w)) << 32));
         for (int i = 0; i < nodes; ++i) {
             A[i] = 0.0;
             B[i] = 0.0;
         }
         A[0] = 1.0;
-        for (int e = 0; e < edges; ++e) {
-            const int g = ed[2 * e], sd = ed[2 * e + 1];
-            A[sd >> 16] += A[sd & 0xffff] * a.m.ew[g];
-        }
-        const double Z = A[nodes - 1];
-        const double scale = -p / Z;
-        B[nodes - 1] = 1.0;
-        double* c = a.contrib + (off >> 1) + 1;
-        for (int e = edges - 1; e >= 0; --e) {
-            const int g = ed[2 * e], sd = ed[2 * e + 1];
-            const int src = sd & 0xffff;
-            const double b = a.m.ew[g] * B[sd >> 16];
-            B[src] += b;
-            const double v = A[src] * b * scale;
-            if (a.grad) {
-                for (int q = a.m.pptr[g]; q < a.m.pptr[g + 1]; ++q) global_add(&a.grad[a.m.pidx[q]], v);
-            } else {
-                c[e] = v;
+        double Z;
+        double* c = a.contrib + (off >> 1) + 2;
+        if (edges <= RE) {
+            int eg[RE], esd[RE];
+            double ew[RE];
+#pragma unroll
+            for (int q = 0; q < RE / 2; ++q) {
+                eg[2 * q] = ev[q].x;
+                esd[2 * q] = ev[q].y;
+                eg[2 * q + 1] = ev[q].z;
+                esd[2 * q + 1] = ev[q].w;
+            }
+#pragma unroll
+            for (int e = 0; e < RE; ++e) ew[e] = a.m.ew[e < edges ? eg[e] : 0];
+#pragma unroll
+            for (int e = 0; e < RE; ++e)
+                if (e < edges) A[esd[e] >> 16] += A[esd[e] & 0xffff] * ew[e];
+            Z = A[nodes - 1];
+            const double scale = -p / Z;
+            B[nodes - 1] = 1.0;
+#pragma unroll
+            for (int e = RE - 1; e >= 0; --e)
+                if (e < edges) {
+                    const int src = esd[e] & 0xffff;
+                    const double b = ew[e] * B[esd[e] >> 16];
+                    B[src] += b;
+                    const double v = A[src] * b * scale;
+                    if (a.grad) {
+                        for (int q = a.m.pptr[eg[e]]; q < a.m.pptr[eg[e] + 1]; ++q) global_add(&a.grad[a.m.pidx[q]], v);
+                    } else {
+                        c[e] = v;
+                    }
+                }
+        } else {
+            const int32_t* ed = a.bub + off + 4;
+            for (int e = 0; e < edges; ++e) {
+                const int g = ed[2 * e], sd = ed[2 * e + 1];
+                A[sd >> 16] += A[sd & 0xffff] * a.m.ew[g];
+            }
+            Z = A[nodes - 1];
+            const double scale = -p / Z;
+            B[nodes - 1] = 1.0;
+            for (int e = edges - 1; e >= 0; --e) {
+                const int g = ed[2 * e], sd = ed[2 * e + 1];
+                const int src = sd & 0xffff;
+                const double b = a.m.ew[g] * B[sd >> 16];
+                B[src] += b;
+                const double v = A[src] * b * scale;
+                if (a.grad) {
+                    for (int q = a.m.pptr[g]; q < a.m.pptr[g + 1]; ++q) global_add(&a.grad[a.m.pidx[q]], v);
+                } else {
+                    c[e] = v;
+                }
             }
         }
         const double lz = log(Z);
@@ -848,14 +894,26 @@ __global__ __launch_bounds__(256) void tail_kernel(TailArgs a) {
         if (c < a.n_chunks) {
             const int lane = lane_id();
             double s = 0.0;
-            for (int k = a.chunk_ptr[c] + lane; k < a.chunk_ptr[c + 1]; k += kWave) s += a.contrib[a.slot[k]];
+            const int k0 = a.chunk_ptr[c], k1 = a.chunk_ptr[c + 1];
+            // a chunk is at most kBubbleGradChunk = 8 x 64 slots: one round
+            // of slot loads, one of contribution gathers
+            static_assert(kBubbleGradChunk <= 8 * kWave, "chunk larger than one gather round");
+            int sl[8];
+#pragma unroll
+            for (int b = 0; b < 8; ++b) sl[b] = a.slot[min(k0 + lane + b * kWave, k1 - 1)];
+            double v[8];
+#pragma unroll
+            for (int b = 0; b < 8; ++b) v[b] = a.contrib[sl[b]];
+#pragma unroll
+            for (int b = 0; b < 8; ++b)
+                if (k0 + lane + b * kWave < k1) s += v[b];
             s = wave_sum(s);
             if (lane == 0) global_add(&a.out[1 + a.chunk_param[c]], s);
         }
     } else {                              // log-likelihood, fixed order
         __shared__ double red[256];
         double s = 0.0;
-        for (int32_t i = int32_t(threadIdx.x); i < a.n_ll; i += 256) s += a.ll_part[i];
+        s = strided_sum(a.ll_part, a.n_ll, int(threadIdx.x), 256);
         red[threadIdx.x] = s;
         __syncthreads();
         for (int w = 128; w > 0; w >>= 1) {

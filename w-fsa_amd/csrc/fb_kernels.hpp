@@ -21,6 +21,10 @@ namespace wfsa {
 
 constexpr int kMaxBubbleNodes = 16;    // nodes of one compiled bubble
 constexpr int kMaxBubbleEdges = 255;   // edges of one compiled bubble
+constexpr int kBubbleRegEdges = 8;     // bubbles up to this many edges run from registers
+// bubble record: 4 header words + 2 per edge, rounded up to 16 bytes
+__host__ __device__ inline int bubble_record_words(int edges) { return (4 + 2 * edges + 3) & ~3; }
+constexpr int kBubbleSlackWords = 4 * (1 + kBubbleRegEdges / 2);   // over-read of the last record
 constexpr int kStreamPrefetch = 4;     // 16-byte chunks in flight per lane
 // slack after the last group's chunks: the prefetch runs ahead unguarded
 constexpr int kStreamTailChunks = 64 * 8;
@@ -130,9 +134,9 @@ struct TravArgs {
 //     padding.  Each lane's words are cut into 16-byte chunks (8 narrow / 4
 //     wide words); chunk c of lane l of group g sits at chunk index
 //     g_base[g] + 64 c + l, so one wavefront reads 1 KiB per load.
-//   bubble buffer: per bubble [nodes | edges << 16, string, (edge id,
-//     src | dst << 16) x edges], always at an even word offset, so edge e of
-//     the bubble at offset o owns contribution slot o / 2 + 1 + e.
+//   bubble buffer: per bubble [nodes | edges << 16, string, p (2 words),
+//     (edge id, src | dst << 16) x edges], 16-byte aligned (padded), so edge
+//     e of the bubble at word offset o owns contribution slot o / 2 + 2 + e.
 struct CompiledArgs {
     ModelView m;
     const double* p;         // [S]
@@ -208,6 +212,21 @@ struct TailArgs {
     double* out;                 // [1 + n_params]
     const unsigned* halted;
 };
+
+// sum of p[t], p[t + nt], p[t + 2 nt], ... below n, in that order, with the
+// loads issued eight at a time (a plain strided loop waits on every load)
+__device__ __forceinline__ double strided_sum(const double* __restrict__ p, int n, int t, int nt) {
+    double s = 0.0;
+    for (int i0 = t; i0 < n; i0 += 8 * nt) {
+        double v[8];
+#pragma unroll
+        for (int b = 0; b < 8; ++b) v[b] = p[min(i0 + b * nt, n - 1)];
+#pragma unroll
+        for (int b = 0; b < 8; ++b)
+            if (i0 + b * nt < n) s += v[b];
+    }
+    return s;
+}
 
 hipError_t configure_kernels(int max_dynamic_lds);
 hipError_t launch_trav(TravMode mode, const TravArgs& a, int grid, hipStream_t stream);

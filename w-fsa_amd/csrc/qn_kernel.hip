@@ -174,7 +174,7 @@ __global__ __launch_bounds__(kQnFinishBlock) void qn_finish_kernel(QnArgs a) {
             gerr = fmax(gerr, p[3]);
         }
         if (a.ll_part)
-            for (int i = t; i < a.n_ll; i += nt) ll += a.ll_part[i];
+            ll = strided_sum(a.ll_part, a.n_ll, t, nt);
     }
     gmin = block_reduce(gmin, 0, red);
     gmax = block_reduce(gmax, 1, red);
@@ -200,9 +200,9 @@ __global__ __launch_bounds__(kQnFinishBlock) void qn_finish_kernel(QnArgs a) {
         for (int i = 0; i < 7; ++i) row[i] = info[i];
         row[7] = double(status);
         if (status == kQnHalted || status == kQnNonFinite) *a.halted = status;
-        __threadfence_system();
         const unsigned v = *a.seq + 1u;
         *a.seq = v;
+        // the system-scope release orders the row before the flag
         __hip_atomic_store(a.host_flag, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
     }
 }

@@ -96,7 +96,6 @@ constexpr int kLdsPerCu = 163840;
 constexpr int kNumCu = 256;
 constexpr int kWave = 64;
 constexpr int kCompiledBlock = 512;
-constexpr int kMaxWavesPerCu = 32;
 constexpr int kIterWavesPerCu = 16;   // per-iteration stream kernel
 constexpr int kQnDepth = 8;   // device-resident QN steps in flight
 constexpr int kTimingStride = 4;   // QN runs time every 4th step's kernels
@@ -510,7 +509,8 @@ int prepare(wfsa_dev* ctx, int level) {
     const size_t chunk_alloc = size_t(chunks) + size_t(wfsa::kStreamTailChunks);
     HIP_TRY(ctx->stream_w.alloc(chunk_alloc));
     HIP_TRY(hipMemsetAsync(ctx->stream_w.ptr, 0xff, chunk_alloc * sizeof(uint4), s));
-    HIP_TRY(ctx->bub.alloc(size_t(std::max<int64_t>(bwords, 2))));
+    HIP_TRY(ctx->bub.alloc(size_t(bwords) + size_t(wfsa::kBubbleSlackWords)));
+    HIP_TRY(hipMemsetAsync(ctx->bub.ptr, 0, (size_t(bwords) + size_t(wfsa::kBubbleSlackWords)) * sizeof(int32_t), s));
     HIP_TRY(ctx->bub_off.alloc(size_t(std::max<int64_t>(nbub, 1))));
     if (nc > 0) {
         DevBuf<int64_t> d_sb, d_bb;
@@ -572,7 +572,7 @@ int prepare(wfsa_dev* ctx, int level) {
         for (int32_t o : h_off) {
             const int edges = h_bubbuf[size_t(o)] >> 16;
             for (int e = 0; e < edges; ++e) {
-                const int32_t g = h_bubbuf[size_t(o) + 2 + 2 * size_t(e)];
+                const int32_t g = h_bubbuf[size_t(o) + 4 + 2 * size_t(e)];
                 for (int32_t q = ctx->h_pptr[size_t(g)]; q < ctx->h_pptr[size_t(g) + 1]; ++q)
                     pc[size_t(ctx->h_pidx[size_t(q)]) + 1]++;
             }
@@ -582,9 +582,9 @@ int prepare(wfsa_dev* ctx, int level) {
         for (int32_t o : h_off) {
             const int edges = h_bubbuf[size_t(o)] >> 16;
             for (int e = 0; e < edges; ++e) {
-                const int32_t g = h_bubbuf[size_t(o) + 2 + 2 * size_t(e)];
+                const int32_t g = h_bubbuf[size_t(o) + 4 + 2 * size_t(e)];
                 for (int32_t q = ctx->h_pptr[size_t(g)]; q < ctx->h_pptr[size_t(g) + 1]; ++q)
-                    slot[size_t(fill[size_t(ctx->h_pidx[size_t(q)])]++)] = (o >> 1) + 1 + e;
+                    slot[size_t(fill[size_t(ctx->h_pidx[size_t(q)])]++)] = (o >> 1) + 2 + e;
             }
         }
         std::vector<int32_t> cparam, cptr;
