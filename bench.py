@@ -32,8 +32,8 @@ METRIC = "forward-backward strings/sec @1/2/4/8 GPU; log-lik rel-err vs MKL ref"
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--strings-per-gpu", type=int, default=1_000_000)
     ap.add_argument("--states", type=int, default=1024)
     ap.add_argument("--degree", type=int, default=8)
@@ -207,6 +207,7 @@ def main():
         "compiled_strings": st1["compiled_strings"],
         "fallback_strings": st1["fallback_strings"],
         "stream_words": st1["stream_words"],
+        "n_bubbles": st1["n_bubbles"],
         "bubble_words": st1["bubble_words"],
         "prepare_ms": st1["prepare_ms"],
     }

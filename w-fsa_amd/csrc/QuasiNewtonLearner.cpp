@@ -13,6 +13,7 @@ void QuasiNewtonLearner::FinalizeCallback() {   // src/QuasiNewtonLearner.cpp:17
     rhs.assign(n, 0.0);
     lambda.assign(k, 1.0);
     g.assign(k, 0.0);
+    dev_qn_ready = false;
 }
 
 void QuasiNewtonLearner::InitCallback(int flags) {   // :29-51
@@ -131,7 +132,11 @@ void QuasiNewtonLearner::RunDevice(double eta, double tol, int32_t max_epochs, d
     auto check = [](int rc, const char* what) {
         if (rc != WFSA_OK) throw LearnerError(what, ": ", wfsa_dev_last_error());
     };
-    check(wfsa_dev_qn_setup(d, &desc), "wfsa_dev_qn_setup");
+    if (!dev_qn_ready || dev_qn_exp != exponential_lambda) {   // once per Finalize (and lambda mode)
+        check(wfsa_dev_qn_setup(d, &desc), "wfsa_dev_qn_setup");
+        dev_qn_ready = true;
+        dev_qn_exp = exponential_lambda;
+    }
     check(wfsa_dev_qn_set_state(d, _x.data(), lambda.data()), "wfsa_dev_qn_set_state");
     std::vector<double> rows(size_t(std::max(max_epochs, 0)) * 7);
     int32_t done = 0, status = 0;

@@ -255,6 +255,11 @@ struct QnArgs {
     const double* fixed;
     const double* ll_part;
     int32_t n_ll;
+    // and the bubble contributions of kept parameter i: contrib[slot[q]] for
+    // q in [slot_ptr[i], slot_ptr[i+1]) (null: none / already in out)
+    const int32_t* slot_ptr;
+    const int32_t* slot;
+    const double* contrib;
     int32_t n_full, n, k;
     const int32_t* full_of;      // [n] full index of each kept parameter
     const int32_t* trim;         // [n_full] trimmed index / -1 / -2
@@ -269,7 +274,7 @@ struct QnArgs {
     int32_t n_partial;
     double plogp, eta, tol;
     int32_t exp_lambda;
-    int32_t slot;                // ring slot of this step
+    int32_t ring_slot;           // ring slot of this step
     unsigned* halted;            // device: nonzero after a halting step
     unsigned* seq;               // device sequence counter
     unsigned* host_flag;         // host-mapped completion flag

@@ -16,6 +16,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstdint>
 
 #pragma clang fp contract(off)
 
@@ -23,9 +24,8 @@ namespace wfsa {
 
 namespace {
 
-constexpr int kQnUpdateBlock = 64;    // one wavefront: registers for whole groups
+constexpr int kQnUpdateBlock = 256;   // four constraints (one wavefront each) per block
 constexpr int kQnFinishBlock = 1024;
-constexpr int kQnRegMembers = 16;     // constraint groups up to this size stay in registers
 
 __device__ double block_reduce(double v, int op, double* red) {   // op 0 min, 1 max
     for (int o = 32; o > 0; o >>= 1) {
@@ -60,100 +60,157 @@ __device__ double block_sum(double v, double* red) {   // fixed order for a fixe
     return red[32];
 }
 
-// qn_update: one thread per constraint, one wavefront per block (so a
-// thread may keep a whole group in registers).  Every quantity of the update
-// is local to a constraint -- its members are a contiguous, ascending range
-// of parameters -- so the blocks are independent; each writes its partial
-// (g_min, g_max, lambda_min, graderr) and qn_finish reduces them.
+__device__ __forceinline__ void wave_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+}
+
+// The gradient of kept parameter i as the QN step sees it: the device's
+// out[1 + j] (j = its full index) plus, without the tail kernel, the constant
+// trivial-word part and its bubble contributions.
+__device__ __forceinline__ double grad_of(const QnArgs& a, int i, int fo) {
+    double gi = a.out[1 + fo] + (a.fixed ? a.fixed[fo] : 0.0);
+    if (a.slot_ptr)
+        for (int q = a.slot_ptr[i]; q < a.slot_ptr[i + 1]; ++q) gi += a.contrib[a.slot[q]];
+    return gi;
+}
+
+// qn_update: one wavefront per constraint.  Every quantity of the update is
+// local to a constraint (its members are a contiguous, ascending range of
+// parameters), so waves are independent; each block writes its partial
+// (g_min, g_max, lambda_min, graderr) and qn_finish reduces them.  Lane m
+// owns member m: the bubble contributions of the constraint's members (a
+// contiguous run of slots) are gathered by all lanes and reduced by member
+// with a segmented wave scan (fixed order); exp and the x update are
+// per-lane; g and the lambda_next numerator are summed by lane 0 in member
+// order, as the host does.
 __global__ __launch_bounds__(kQnUpdateBlock) void qn_update_kernel(QnArgs a) {
     if (*a.halted) return;
-    const int c = int(blockIdx.x) * kQnUpdateBlock + int(threadIdx.x);
+    constexpr int W = kQnUpdateBlock / 64;
+    __shared__ double sh_ev[W][64], sh_gv[W][64], sh_acc[W][64];
+    __shared__ int sh_end[W][64];
+    __shared__ double sh_bc[W][2];
+    __shared__ double red[W][4];
+    const int lane = int(threadIdx.x) & 63, w = int(threadIdx.x) >> 6;
+    const int c = int(blockIdx.x) * W + w;
     double gmin = INFINITY, gmax = -INFINITY, lmin = INFINITY, gerr = 0.0;
     if (c < a.k) {
-        const double* __restrict__ out = a.out;
-        const int32_t* __restrict__ full_of = a.full_of;
-        double* __restrict__ x = a.x;
-        double* __restrict__ expx = a.expx;
-        double* __restrict__ grad = a.grad;
-        double* __restrict__ w_full = a.w_full;
-        const int b = a.cptr[c], e = a.cptr[c + 1];
+        const int b = a.cptr[c], e = a.cptr[c + 1], nm = e - b;
         const double lam = a.lambda[c];
-        double g = -1.0, laux;
-        if (e - b <= kQnRegMembers) {
-            // members in registers: every load issued before the first use
-            double xv[kQnRegMembers], gv[kQnRegMembers], ev[kQnRegMembers];
-#pragma unroll
-            for (int m = 0; m < kQnRegMembers; ++m)
-                if (b + m < e) {
-                    xv[m] = x[b + m];
-                    const int fo = full_of[b + m];
-                    gv[m] = out[1 + fo] + (a.fixed ? a.fixed[fo] : 0.0);
-                }
-            // ComputeExpX, ComputeG: g = -1 + sum exp(x) in member order
-#pragma unroll
-            for (int m = 0; m < kQnRegMembers; ++m)
-                if (b + m < e) {
-                    ev[m] = exp(xv[m]);
-                    g += ev[m];
-                }
-            // ComputeLambdaNext: (lambda g - sum grad) / (g + 1)
-            double r = lam * g;
-#pragma unroll
-            for (int m = 0; m < kQnRegMembers; ++m)
-                if (b + m < e) r -= gv[m];
-            laux = r / (g + 1.0);
-            // graderr (old lambda), x update (lambda_next), next weights
-#pragma unroll
-            for (int m = 0; m < kQnRegMembers; ++m)
-                if (b + m < e) {
-                    const double aux = ev[m] * lam;
-                    gerr = fmax(gerr, fabs(gv[m] + aux));
-                    const double xi = xv[m] - a.eta * ((gv[m] + ev[m] * laux) / aux);
-                    x[b + m] = xi;
-                    grad[b + m] = gv[m];
-                    w_full[full_of[b + m]] = xi;   // GetWeight for the next step
-                }
-        } else {   // large groups (dense automata): the same through memory
-            for (int i = b; i < e; ++i) {
-                const double ex = exp(x[i]);
-                expx[i] = ex;
-                g += ex;
+        double g, laux;
+        if (nm <= 64) {
+            double xi = 0.0, gi = 0.0;
+            int fo = 0;
+            if (lane < nm) {
+                xi = a.x[b + lane];
+                fo = a.full_of[b + lane];
+                gi = a.out[1 + fo] + (a.fixed ? a.fixed[fo] : 0.0);
             }
-            double r = lam * g;
-            for (int i = b; i < e; ++i) {
-                const double gi = out[1 + full_of[i]] + (a.fixed ? a.fixed[full_of[i]] : 0.0);
-                grad[i] = gi;
-                r -= gi;
+            if (a.slot_ptr) {
+                double* acc = sh_acc[w];
+                int* mend = sh_end[w];
+                acc[lane] = 0.0;
+                mend[lane] = lane < nm ? a.slot_ptr[b + lane + 1] : INT32_MAX;
+                const int q0 = a.slot_ptr[b], q1 = a.slot_ptr[e];
+                wave_sync();
+                for (int q = q0; q < q1; q += 64) {
+                    const int k = q + lane;
+                    const bool valid = k < q1;
+                    const double v0 = valid ? a.contrib[a.slot[k]] : 0.0;
+                    int m = 0;
+                    while (m < nm && mend[m] <= k) ++m;
+                    if (!valid) m = 1 << 20;
+                    double v = v0;
+#pragma unroll
+                    for (int d = 1; d < 64; d <<= 1) {
+                        const double ov = __shfl_up(v, d, 64);
+                        const int om = __shfl_up(m, d, 64);
+                        if (lane >= d && om == m) v += ov;
+                    }
+                    const int next_m = __shfl_down(m, 1, 64);
+                    if (valid && (lane == 63 || next_m != m)) acc[m] += v;
+                    wave_sync();
+                }
+                if (lane < nm) gi += acc[lane];
             }
-            laux = r / (g + 1.0);
-            for (int i = b; i < e; ++i) {
-                const double ex = expx[i], gi = grad[i];
-                const double aux = ex * lam;
-                gerr = fmax(gerr, fabs(gi + aux));
-                const double xi = x[i] - a.eta * ((gi + ex * laux) / aux);
-                x[i] = xi;
-                w_full[full_of[i]] = xi;
+            const double ei = lane < nm ? exp(xi) : 0.0;
+            sh_ev[w][lane] = ei;
+            sh_gv[w][lane] = gi;
+            wave_sync();
+            if (lane == 0) {   // ComputeG, ComputeLambdaNext in member order
+                double gg = -1.0;
+                for (int m = 0; m < nm; ++m) gg += sh_ev[w][m];
+                double r = lam * gg;
+                for (int m = 0; m < nm; ++m) r -= sh_gv[w][m];
+                sh_bc[w][0] = gg;
+                sh_bc[w][1] = r / (gg + 1.0);
             }
+            wave_sync();
+            g = sh_bc[w][0];
+            laux = sh_bc[w][1];
+            if (lane < nm) {   // graderr (old lambda), x update (lambda_next), next weights
+                const double aux = ei * lam;
+                gerr = fabs(gi + aux);
+                const double xn = xi - a.eta * ((gi + ei * laux) / aux);
+                a.x[b + lane] = xn;
+                a.grad[b + lane] = gi;
+                a.w_full[fo] = xn;   // GetWeight for the next step
+            }
+        } else {   // large groups (dense automata): lane 0 through memory
+            g = -1.0;
+            laux = 0.0;
+            if (lane == 0) {
+                for (int i = b; i < e; ++i) {
+                    const double ex = exp(a.x[i]);
+                    a.expx[i] = ex;
+                    a.grad[i] = grad_of(a, i, a.full_of[i]);
+                    g += ex;
+                }
+                double r = lam * g;
+                for (int i = b; i < e; ++i) r -= a.grad[i];
+                laux = r / (g + 1.0);
+                for (int i = b; i < e; ++i) {
+                    const double ex = a.expx[i], gi = a.grad[i];
+                    const double aux = ex * lam;
+                    gerr = fmax(gerr, fabs(gi + aux));
+                    const double xn = a.x[i] - a.eta * ((gi + ex * laux) / aux);
+                    a.x[i] = xn;
+                    a.w_full[a.full_of[i]] = xn;
+                }
+            }
+            g = __shfl(g, 0, 64);
+            laux = __shfl(laux, 0, 64);
         }
-        // LambdaUpdate (src/Learner.cpp:438-462)
-        const double d = lam - laux;
-        a.lambda[c] = a.exp_lambda ? lam * exp(-a.eta * (d / lam)) : lam - a.eta * d;
+        if (lane == 0) {   // LambdaUpdate (src/Learner.cpp:438-462)
+            const double d = lam - laux;
+            a.lambda[c] = a.exp_lambda ? lam * exp(-a.eta * (d / lam)) : lam - a.eta * d;
+        }
         gmin = g;
         gmax = g;
         lmin = lam;
     }
-    for (int o = 32; o > 0; o >>= 1) {
-        gmin = fmin(gmin, __shfl_xor(gmin, o, 64));
-        gmax = fmax(gmax, __shfl_xor(gmax, o, 64));
-        lmin = fmin(lmin, __shfl_xor(lmin, o, 64));
-        gerr = fmax(gerr, __shfl_xor(gerr, o, 64));
+    for (int o = 32; o > 0; o >>= 1) gerr = fmax(gerr, __shfl_xor(gerr, o, 64));
+    if (lane == 0) {
+        red[w][0] = gmin;
+        red[w][1] = gmax;
+        red[w][2] = lmin;
+        red[w][3] = gerr;
     }
+    __syncthreads();
     if (threadIdx.x == 0) {
+        double r0 = red[0][0], r1 = red[0][1], r2 = red[0][2], r3 = red[0][3];
+        for (int v = 1; v < W; ++v) {
+            r0 = fmin(r0, red[v][0]);
+            r1 = fmax(r1, red[v][1]);
+            r2 = fmin(r2, red[v][2]);
+            r3 = fmax(r3, red[v][3]);
+        }
         double* p = a.partial + size_t(blockIdx.x) * 4;
-        p[0] = gmin;
-        p[1] = gmax;
-        p[2] = lmin;
-        p[3] = gerr;
+        p[0] = r0;
+        p[1] = r1;
+        p[2] = r2;
+        p[3] = r3;
     }
 }
 
@@ -196,7 +253,7 @@ __global__ __launch_bounds__(kQnFinishBlock) void qn_finish_kernel(QnArgs a) {
             const bool halt = gerr <= a.tol && fabs(gmin) <= a.tol && fabs(gmax) <= a.tol;
             status = !finite ? kQnNonFinite : (halt ? kQnHalted : kQnRan);
         }
-        double* row = a.host_ring + size_t(a.slot) * kQnRow;
+        double* row = a.host_ring + size_t(a.ring_slot) * kQnRow;
         for (int i = 0; i < 7; ++i) row[i] = info[i];
         row[7] = double(status);
         if (status == kQnHalted || status == kQnNonFinite) *a.halted = status;
@@ -219,7 +276,10 @@ __global__ void qn_weights_kernel(const double* x, const int32_t* trim, int32_t 
 
 }  // namespace
 
-int qn_update_blocks(int32_t k) { return std::max(1, (k + kQnUpdateBlock - 1) / kQnUpdateBlock); }
+int qn_update_blocks(int32_t k) {
+    constexpr int W = kQnUpdateBlock / 64;
+    return std::max(1, (k + W - 1) / W);
+}
 
 hipError_t launch_qn(const QnArgs& a, hipStream_t stream) {
     hipLaunchKernelGGL(qn_update_kernel, dim3(unsigned(qn_update_blocks(a.k))), dim3(kQnUpdateBlock), 0, stream, a);

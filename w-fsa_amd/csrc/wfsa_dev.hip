@@ -164,6 +164,7 @@ struct wfsa_dev {
     DevBuf<int32_t> bub_off, bg_chunk_param, bg_chunk_ptr, bg_slot;
     DevBuf<double> contrib;
     std::vector<int32_t> h_pptr, h_pidx;   // host copy of the combined parameter lists
+    std::vector<int32_t> h_bslot_ptr, h_bslot;   // host copy of the bubble slot CSR by parameter
     size_t c_lds = 0;
 
     // traversal fallback: per tier string lists
@@ -200,6 +201,10 @@ struct wfsa_dev {
     int32_t qn_n = 0, qn_k = 0, qn_exp_lambda = 0;
     double qn_plogp = 0.0;
     DevBuf<int32_t> qn_trim, qn_full_of, qn_ccol, qn_cptr;
+    std::vector<int32_t> qn_h_full_of;
+    DevBuf<int32_t> qn_slot_ptr, qn_slot;   // bubble slots of each kept parameter (QN order)
+    int qn_slots_for = -1;                   // prep generation the slot CSR was built for
+    int prep_gen = 0;
     DevBuf<double> qn_x, qn_lambda, qn_expx, qn_grad, qn_partial;
     DevBuf<unsigned> qn_halted;
     double* qn_ring = nullptr;       // host-mapped [kQnDepth][kQnRow]
@@ -598,12 +603,16 @@ int prepare(wfsa_dev* ctx, int level) {
         HIP_TRY(ctx->bg_chunk_param.upload(cparam.data(), cparam.size(), s));
         HIP_TRY(ctx->bg_chunk_ptr.upload(cptr.data(), cptr.size(), s));
         HIP_TRY(ctx->bg_slot.upload(slot.data(), slot.size(), s));
+        ctx->h_bslot_ptr = pc;
+        ctx->h_bslot = slot;
         HIP_TRY(ctx->contrib.alloc(size_t(bwords / 2) + 1));
         HIP_TRY(hipMemsetAsync(ctx->contrib.ptr, 0, (size_t(bwords / 2) + 1) * sizeof(double), s));
         ctx->b_grid = int(std::max<int64_t>(1, std::min<int64_t>((nbub + wfsa::kBubbleBlock - 1) / wfsa::kBubbleBlock,
                                                                   int64_t(ctx->n_cu) * 8)));
     } else {
         ctx->b_grid = 0;
+        ctx->h_bslot_ptr.assign(size_t(ctx->n_params) + 1, 0);
+        ctx->h_bslot.clear();
     }
 
     // compiled kernel geometry: 16 waves per block, one block per CU; w and
@@ -673,6 +682,7 @@ int prepare(wfsa_dev* ctx, int level) {
     ctx->stats.prepare_ms =
         std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_start).count();
     ctx->prep_level = 2;
+    ++ctx->prep_gen;
     return WFSA_OK;
 }
 
@@ -815,6 +825,8 @@ int enqueue_qn_step(wfsa_dev* ctx, double eta, double tol, int slot, bool timed)
     hipStream_t s = ctx->stream;
     const int32_t np = ctx->n_params;
     // without a communicator the QN kernel finishes the reduction itself
+    // (the bubble contributions need the tail's param-chunk reduction: one
+    // wave per constraint cannot absorb a hot parameter's slot list)
     const bool tail = ctx->comm != nullptr || !ctx->bubble_atomic;
     int32_t n_ll = 0;
     if (int rc = enqueue_evaluation(ctx, false, ctx->qn_halted.ptr, timed ? slot : -1, tail, &n_ll)) return rc;
@@ -826,6 +838,11 @@ int enqueue_qn_step(wfsa_dev* ctx, double eta, double tol, int slot, bool timed)
         q.fixed = ctx->n_groups > 0 ? ctx->fixed_grad.ptr : nullptr;
         q.ll_part = ctx->ll_part.ptr;
         q.n_ll = n_ll;
+        if (ctx->n_bubbles > 0 && !ctx->bubble_atomic) {
+            q.slot_ptr = ctx->qn_slot_ptr.ptr;
+            q.slot = ctx->qn_slot.ptr;
+            q.contrib = ctx->contrib.ptr;
+        }
     }
     q.n_full = np;
     q.n = ctx->qn_n;
@@ -845,7 +862,7 @@ int enqueue_qn_step(wfsa_dev* ctx, double eta, double tol, int slot, bool timed)
     q.eta = eta;
     q.tol = tol;
     q.exp_lambda = ctx->qn_exp_lambda;
-    q.slot = slot;
+    q.ring_slot = slot;
     q.halted = ctx->qn_halted.ptr;
     q.seq = ctx->counters.ptr;
     q.host_flag = ctx->flag_dev;
@@ -1137,6 +1154,8 @@ int wfsa_dev_qn_setup(wfsa_dev* ctx, const wfsa_qn_desc* d) {
     hipStream_t s = ctx->stream;
     if (nf > 0) HIP_TRY(ctx->qn_trim.upload(d->trim, size_t(nf), s));
     HIP_TRY(ctx->qn_full_of.upload(full_of.data(), full_of.size(), s));
+    ctx->qn_h_full_of = full_of;
+    ctx->qn_slots_for = -1;
     if (n > 0) HIP_TRY(ctx->qn_ccol.upload(d->ccol, size_t(n), s));
     HIP_TRY(ctx->qn_cptr.upload(cptr.data(), cptr.size(), s));
     for (DevBuf<double>* b : {&ctx->qn_x, &ctx->qn_expx, &ctx->qn_grad}) HIP_TRY(b->alloc(size_t(std::max(n, 1))));
@@ -1194,6 +1213,21 @@ int wfsa_dev_qn_run(wfsa_dev* ctx, double eta, double tol, int32_t max_steps, do
         if (int rc = prepare(ctx, 2)) return rc;
     if (int rc = collect_timing(ctx)) return rc;
     hipStream_t s = ctx->stream;
+    if (ctx->qn_slots_for != ctx->prep_gen) {   // bubble slots re-indexed by kept parameter
+        std::vector<int32_t> sp(size_t(ctx->qn_n) + 1, 0), sl;
+        for (int32_t i = 0; i < ctx->qn_n; ++i) {
+            const int32_t j = ctx->qn_h_full_of[size_t(i)];
+            if (!ctx->h_bslot_ptr.empty())
+                sl.insert(sl.end(), ctx->h_bslot.begin() + ctx->h_bslot_ptr[size_t(j)],
+                          ctx->h_bslot.begin() + ctx->h_bslot_ptr[size_t(j) + 1]);
+            sp[size_t(i) + 1] = int32_t(sl.size());
+        }
+        if (sl.empty()) sl.push_back(0);
+        HIP_TRY(ctx->qn_slot_ptr.upload(sp.data(), sp.size(), s));
+        HIP_TRY(ctx->qn_slot.upload(sl.data(), sl.size(), s));
+        HIP_TRY(hipStreamSynchronize(s));
+        ctx->qn_slots_for = ctx->prep_gen;
+    }
     HIP_TRY(hipMemsetAsync(ctx->qn_halted.ptr, 0, sizeof(unsigned), s));
     const unsigned base = ctx->seq;
     int32_t enq = 0, done = 0, st = 0;
