@@ -224,7 +224,7 @@ __device__ bool compile_walk(const Slab& sl, const ModelView& m, int L, int sidx
             for (int e = sl.epos[a]; e < e_hi; ++e) {
                 const int h = sl.e_dst[e];
                 if (!(sl.beta[h] > 0.0)) continue;
-                bub[w++] = sl.e_g[e];
+                bub[w++] = edge_code(m.pptr, m.pidx, sl.e_g[e], m.n_params);
                 bub[w++] = int(lid[sl.e_src[e]]) | (int(lid[h]) << 16);
             }
             if (to_end) {
@@ -232,7 +232,7 @@ __device__ bool compile_walk(const Slab& sl, const ModelView& m, int L, int sidx
                     if (!(sl.beta[f] > 0.0)) continue;
                     const int S = sl.state[f];
                     for (int x = m.x_ptr[S]; x < m.x_ptr[S + 1]; ++x) {
-                        bub[w++] = m.n_edges + x;
+                        bub[w++] = edge_code(m.pptr, m.pidx, m.n_edges + x, m.n_params);
                         bub[w++] = int(lid[f]) | (end_id << 16);
                     }
                 }
@@ -763,93 +763,152 @@ __global__ __launch_bounds__(1024) void fbs_kernel(CompiledArgs a) {
 // Bubbles: one lane per bubble (largest first).  Local forward from the
 // bubble's first cut, local backward from its last cut; an edge's posterior
 // is alpha(src) w beta(dst) / Z and -p_s times it goes to the edge's
-// contribution slot; log Z joins the string's log q.  A record is 16-byte
-// aligned -- [nodes | edges << 16, string, p (2 words), (edge, src | dst << 16)
-// x edges] -- so a bubble of up to kBubbleRegEdges edges is two dependent
-// rounds of loads (its record, then its edges' weights), all issued at once.
+// contribution slot; log Z joins the string's log q.  alpha and beta of the
+// (at most kMaxBubbleNodes) nodes live in registers, addressed by compare-
+// and-select, so the kernel needs no LDS and runs at full occupancy.  A
+// record is 16-byte aligned -- [nodes | edges << 16, string, p (2 words),
+// (edge, src | dst << 16) x edges] -- and is read eight edges at a time with
+// the eight edge weights gathered together.
+// r[i] for i < 8 as a tree of selects on the bits of i (a compare chain is
+// re-formed into an indexed scratch load by the compiler)
+template <int N>
+__device__ __forceinline__ double reg_get(const double (&r)[N], int i) {
+    static_assert(N == 8, "register bubbles have 8 nodes");
+    const bool b0 = i & 1, b1 = i & 2, b2 = i & 4;
+    const double s0 = b0 ? r[1] : r[0], s1 = b0 ? r[3] : r[2], s2 = b0 ? r[5] : r[4], s3 = b0 ? r[7] : r[6];
+    const double t0 = b1 ? s1 : s0, t1 = b1 ? s3 : s2;
+    return b2 ? t1 : t0;
+}
+template <int N>
+__device__ __forceinline__ void reg_add(double (&r)[N], int i, double v) {
+#pragma unroll
+    for (int k = 0; k < N; ++k) r[k] = i == k ? r[k] + v : r[k];
+}
+
+// weight of a bubble edge from its code (edge_code): exp(w[j]) of its one
+// parameter j from the per-iteration table ewp (exp(w), with ewp[n_params]
+// = 1), or exp of the sum for a multi-parameter edge
+__device__ __noinline__ double multi_weight(const ModelView& m, const double* w, int g) {
+    double lw = 0.0;
+    for (int q = m.pptr[g]; q < m.pptr[g + 1]; ++q) lw += w[m.pidx[q]];
+    return exp(lw);
+}
+__device__ __forceinline__ double code_weight(const ModelView& m, const double* w, const double* ewp, int code) {
+    return code >= 0 ? ewp[code] : multi_weight(m, w, -code - 2);
+}
+
+// -p_s times the posterior of a bubble edge: into its contribution slot, or
+// (BubbleArgs::grad) atomically into its parameters' gradient
+__device__ __forceinline__ void bubble_contrib(const BubbleArgs& a, double* c, int e, int code, double v) {
+    if (!a.grad) {
+        c[e] = v;
+    } else if (code >= 0) {
+        if (code < a.m.n_params) global_add(&a.grad[code], v);
+    } else {
+        const int g = -code - 2;
+        for (int q = a.m.pptr[g]; q < a.m.pptr[g + 1]; ++q) global_add(&a.grad[a.m.pidx[q]], v);
+    }
+}
+
+template <int RE>
+__device__ __forceinline__ void bubble_round(const int4* rec, const ModelView& m, const double* wsrc, const double* ewp,
+                                             int e0, int edges, int (&eg)[RE], int (&esd)[RE], double (&ew)[RE]) {
+#pragma unroll
+    for (int q = 0; q < RE / 2; ++q) {
+        const int4 v = rec[1 + e0 / 2 + q];
+        eg[2 * q] = v.x;
+        esd[2 * q] = v.y;
+        eg[2 * q + 1] = v.z;
+        esd[2 * q + 1] = v.w;
+    }
+#pragma unroll
+    for (int e = 0; e < RE; ++e) ew[e] = e0 + e < edges ? code_weight(m, wsrc, ewp, eg[e]) : 0.0;
+}
+
+// One bubble of at most N nodes and RE edges (most bubbles: a diamond of 4
+// edges), alpha/beta and the edges in registers.
+template <int N>
+__device__ __forceinline__ void bubble_eval(const BubbleArgs& a, const double* wsrc, const double* ewp, int off,
+                                            int nodes, int edges, double p, double& lz) {
+    constexpr int RE = kBubbleRegEdges;
+    const int4* rec = reinterpret_cast<const int4*>(a.bub + off);
+    double A[N], B[N];
+#pragma unroll
+    for (int k = 0; k < N; ++k) {
+        A[k] = k == 0 ? 1.0 : 0.0;
+        B[k] = 0.0;
+    }
+    int g0[RE], sd0[RE];
+    double w0[RE];
+    bubble_round(rec, a.m, wsrc, ewp, 0, edges, g0, sd0, w0);
+#pragma unroll
+    for (int e = 0; e < RE; ++e)
+        if (e < edges) reg_add(A, sd0[e] >> 16, reg_get(A, sd0[e] & 0xffff) * w0[e]);
+    const double Z = reg_get(A, nodes - 1);
+    const double scale = -p / Z;
+    reg_add(B, nodes - 1, 1.0);
+    double* c = a.contrib + (off >> 1) + 2;
+#pragma unroll
+    for (int e = RE - 1; e >= 0; --e)
+        if (e < edges) {
+            const int src = sd0[e] & 0xffff;
+            const double b = w0[e] * reg_get(B, sd0[e] >> 16);
+            reg_add(B, src, b);
+            bubble_contrib(a, c, e, g0[e], reg_get(A, src) * b * scale);
+        }
+    lz = log(Z);
+}
+
+// Larger bubbles (more than kBubbleRegEdges edges; rare): the same through
+// a per-lane LDS scratch of 2 x kMaxBubbleNodes doubles.
+__device__ void bubble_eval_mem(const BubbleArgs& a, const double* wsrc, const double* ewp, int off, int nodes,
+                                int edges, double p, double* A, double& lz) {
+    double* B = A + kMaxBubbleNodes;
+    for (int i = 0; i < nodes; ++i) {
+        A[i] = i == 0 ? 1.0 : 0.0;
+        B[i] = 0.0;
+    }
+    const int32_t* ed = a.bub + off + 4;
+    for (int e = 0; e < edges; ++e) {
+        const int code = ed[2 * e], sd = ed[2 * e + 1];
+        A[sd >> 16] += A[sd & 0xffff] * code_weight(a.m, wsrc, ewp, code);
+    }
+    const double Z = A[nodes - 1];
+    const double scale = -p / Z;
+    B[nodes - 1] = 1.0;
+    double* c = a.contrib + (off >> 1) + 2;
+    for (int e = edges - 1; e >= 0; --e) {
+        const int code = ed[2 * e], sd = ed[2 * e + 1];
+        const int src = sd & 0xffff;
+        const double b = code_weight(a.m, wsrc, ewp, code) * B[sd >> 16];
+        B[src] += b;
+        bubble_contrib(a, c, e, code, A[src] * b * scale);
+    }
+    lz = log(Z);
+}
+
+// Bubble bi: log Z and its contributions; returns p log Z.
+__device__ __forceinline__ double bubble_one(const BubbleArgs& a, const double* wsrc, int bi, double* scr) {
+    const double* ewp = a.ewp;
+    const int off = a.bub_off[bi];
+    const int4 h = reinterpret_cast<const int4*>(a.bub + off)[0];
+    const int nodes = h.x & 0xffff, edges = h.x >> 16;
+    const double p = __longlong_as_double((long long)(uint32_t(h.z)) | ((long long)(uint32_t(h.w)) << 32));
+    double lz;
+    if (edges <= kBubbleRegEdges) bubble_eval<kBubbleRegNodes>(a, wsrc, ewp, off, nodes, edges, p, lz);
+    else bubble_eval_mem(a, wsrc, ewp, off, nodes, edges, p, scr, lz);
+    if (a.logq) global_add(&a.logq[h.y], lz);
+    return p * lz;
+}
+
 __global__ __launch_bounds__(kBubbleBlock) void bubble_kernel(BubbleArgs a) {
     if (a.halted && *a.halted) return;
-    __shared__ double scr[kBubbleBlock][2 * kMaxBubbleNodes + 1];
     const int lane = lane_id();
     const int gw = int(blockIdx.x) * (kBubbleBlock / kWave) + int(threadIdx.x) / kWave;
-    double* A = scr[threadIdx.x];
-    double* B = A + kMaxBubbleNodes;
+    __shared__ double scr[kBubbleBlock][2 * kMaxBubbleNodes];
     double ll_acc = 0.0;
-    constexpr int RE = kBubbleRegEdges;
-    for (int bi = int(blockIdx.x * blockDim.x + threadIdx.x); bi < a.n_bubbles; bi += int(gridDim.x * blockDim.x)) {
-        const int off = a.bub_off[bi];
-        const int4* rec = reinterpret_cast<const int4*>(a.bub + off);
-        const int4 h = rec[0];
-        int4 ev[RE / 2];   // edges 2q, 2q+1 (the buffer has slack after the last record)
-#pragma unroll
-        for (int q = 0; q < RE / 2; ++q) ev[q] = rec[1 + q];
-        const int nodes = h.x & 0xffff, edges = h.x >> 16;
-        const int s = h.y;
-        const double p = __longlong_as_double((long long)(uint32_t(h.z)) | ((long long)(uint32_t(h.w)) << 32));
-        for (int i = 0; i < nodes; ++i) {
-            A[i] = 0.0;
-            B[i] = 0.0;
-        }
-        A[0] = 1.0;
-        double Z;
-        double* c = a.contrib + (off >> 1) + 2;
-        if (edges <= RE) {
-            int eg[RE], esd[RE];
-            double ew[RE];
-#pragma unroll
-            for (int q = 0; q < RE / 2; ++q) {
-                eg[2 * q] = ev[q].x;
-                esd[2 * q] = ev[q].y;
-                eg[2 * q + 1] = ev[q].z;
-                esd[2 * q + 1] = ev[q].w;
-            }
-#pragma unroll
-            for (int e = 0; e < RE; ++e) ew[e] = a.m.ew[e < edges ? eg[e] : 0];
-#pragma unroll
-            for (int e = 0; e < RE; ++e)
-                if (e < edges) A[esd[e] >> 16] += A[esd[e] & 0xffff] * ew[e];
-            Z = A[nodes - 1];
-            const double scale = -p / Z;
-            B[nodes - 1] = 1.0;
-#pragma unroll
-            for (int e = RE - 1; e >= 0; --e)
-                if (e < edges) {
-                    const int src = esd[e] & 0xffff;
-                    const double b = ew[e] * B[esd[e] >> 16];
-                    B[src] += b;
-                    const double v = A[src] * b * scale;
-                    if (a.grad) {
-                        for (int q = a.m.pptr[eg[e]]; q < a.m.pptr[eg[e] + 1]; ++q) global_add(&a.grad[a.m.pidx[q]], v);
-                    } else {
-                        c[e] = v;
-                    }
-                }
-        } else {
-            const int32_t* ed = a.bub + off + 4;
-            for (int e = 0; e < edges; ++e) {
-                const int g = ed[2 * e], sd = ed[2 * e + 1];
-                A[sd >> 16] += A[sd & 0xffff] * a.m.ew[g];
-            }
-            Z = A[nodes - 1];
-            const double scale = -p / Z;
-            B[nodes - 1] = 1.0;
-            for (int e = edges - 1; e >= 0; --e) {
-                const int g = ed[2 * e], sd = ed[2 * e + 1];
-                const int src = sd & 0xffff;
-                const double b = a.m.ew[g] * B[sd >> 16];
-                B[src] += b;
-                const double v = A[src] * b * scale;
-                if (a.grad) {
-                    for (int q = a.m.pptr[g]; q < a.m.pptr[g + 1]; ++q) global_add(&a.grad[a.m.pidx[q]], v);
-                } else {
-                    c[e] = v;
-                }
-            }
-        }
-        const double lz = log(Z);
-        ll_acc += p * lz;
-        if (a.logq) global_add(&a.logq[s], lz);
-    }
+    for (int bi = int(blockIdx.x * blockDim.x + threadIdx.x); bi < a.n_bubbles; bi += int(gridDim.x * blockDim.x))
+        ll_acc += bubble_one(a, a.w, bi, scr[threadIdx.x]);
     ll_acc = wave_sum(ll_acc);
     if (lane == 0) a.ll_part[gw] = ll_acc;
 }
@@ -926,9 +985,12 @@ __global__ __launch_bounds__(256) void tail_kernel(TailArgs a) {
 
 // host-mapped weights -> device, 16-byte loads (both buffers padded to even)
 __global__ __launch_bounds__(256) void stage_kernel(const double2* __restrict__ host_w, double2* __restrict__ w,
-                                                    int32_t n2) {
-    for (int32_t i = int32_t(blockIdx.x * blockDim.x + threadIdx.x); i < n2; i += int32_t(gridDim.x * blockDim.x))
-        w[i] = host_w[i];
+                                                    double2* __restrict__ ewp, int32_t n2) {
+    for (int32_t i = int32_t(blockIdx.x * blockDim.x + threadIdx.x); i < n2; i += int32_t(gridDim.x * blockDim.x)) {
+        const double2 v = host_w[i];
+        w[i] = v;
+        ewp[i] = make_double2(exp(v.x), exp(v.y));
+    }
 }
 
 // Per iteration: log-weight, weight and parameter record of every combined
@@ -1071,11 +1133,11 @@ hipError_t launch_publish(const double* out, const Publish& pub, hipStream_t str
     return hipGetLastError();
 }
 
-hipError_t launch_stage(const double* host_w, double* w, int32_t n, hipStream_t stream) {
+hipError_t launch_stage(const double* host_w, double* w, double* ewp, int32_t n, hipStream_t stream) {
     const int32_t n2 = (n + 2) / 2;   // n weights and the zero slot w[n]
     const unsigned blocks = unsigned(std::min<int32_t>(8, (n2 + 255) / 256));
     hipLaunchKernelGGL(stage_kernel, dim3(blocks), dim3(256), 0, stream, reinterpret_cast<const double2*>(host_w),
-                       reinterpret_cast<double2*>(w), n2);
+                       reinterpret_cast<double2*>(w), reinterpret_cast<double2*>(ewp), n2);
     return hipGetLastError();
 }
 

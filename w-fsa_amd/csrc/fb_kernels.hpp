@@ -22,6 +22,7 @@ namespace wfsa {
 constexpr int kMaxBubbleNodes = 16;    // nodes of one compiled bubble
 constexpr int kMaxBubbleEdges = 255;   // edges of one compiled bubble
 constexpr int kBubbleRegEdges = 8;     // bubbles up to this many edges run from registers
+constexpr int kBubbleRegNodes = 8;     // (and so at most this many nodes)
 // bubble record: 4 header words + 2 per edge, rounded up to 16 bytes
 __host__ __device__ inline int bubble_record_words(int edges) { return (4 + 2 * edges + 3) & ~3; }
 constexpr int kBubbleSlackWords = 4 * (1 + kBubbleRegEdges / 2);   // over-read of the last record
@@ -56,7 +57,17 @@ struct ModelView {
     int32_t n_nodes;
     int32_t start;
     int32_t n_edges;         // E
+    int32_t n_params;        // Fsa parameters (w has a zero slot at n_params)
 };
+
+// Parameter code of combined edge g in a bubble record: its parameter when
+// it has exactly one, n_params (the zero slot: weight log 1) when it has
+// none, -(g + 2) when it has several.  The edge weight is then exp(w[code])
+// straight from the weight table in the common case.
+__host__ __device__ inline int32_t edge_code(const int32_t* pptr, const int32_t* pidx, int32_t g, int32_t n_params) {
+    const int32_t np = pptr[g + 1] - pptr[g];
+    return np == 1 ? pidx[pptr[g]] : (np == 0 ? n_params : -(g + 2));
+}
 
 // Per-wave LDS slab holding one string's trellis: frontier nodes (alpha,
 // beta, node id) for every position, the live edges between consecutive
@@ -135,8 +146,9 @@ struct TravArgs {
 //     wide words); chunk c of lane l of group g sits at chunk index
 //     g_base[g] + 64 c + l, so one wavefront reads 1 KiB per load.
 //   bubble buffer: per bubble [nodes | edges << 16, string, p (2 words),
-//     (edge id, src | dst << 16) x edges], 16-byte aligned (padded), so edge
-//     e of the bubble at word offset o owns contribution slot o / 2 + 2 + e.
+//     (edge code, src | dst << 16) x edges] (edge_code above), 16-byte aligned
+//     (padded), so edge e of the bubble at word offset o owns contribution
+//     slot o / 2 + 2 + e.
 struct CompiledArgs {
     ModelView m;
     const double* p;         // [S]
@@ -179,6 +191,8 @@ struct BubbleArgs {
     double* grad;            // or: [n_params] atomically accumulated (out + 1)
     double* ll_part;         // [waves in grid]
     double* logq;            // [S] or null: log Z added to the string's entry
+    const double* w;         // [n_params + 1] weights (GetWeight form) with the zero slot
+    const double* ewp;       // [n_params + 1] exp(w), ewp[n_params] = 1 (per iteration)
     const unsigned* halted;
 };
 
@@ -236,9 +250,9 @@ hipError_t launch_bubbles(const BubbleArgs& a, int grid, hipStream_t stream);
 hipError_t launch_tail(const TailArgs& a, hipStream_t stream);
 // out[0, n) -> host-mapped memory, then the flag (one block)
 hipError_t launch_publish(const double* out, const Publish& pub, hipStream_t stream);
-// host-mapped weights w[0, n) and the zero slot w[n] -> device (both
-// buffers padded to an even count)
-hipError_t launch_stage(const double* host_w, double* w, int32_t n, hipStream_t stream);
+// host-mapped weights w[0, n) and the zero slot w[n] -> device, with
+// ewp = exp(w) (all buffers padded to an even count)
+hipError_t launch_stage(const double* host_w, double* w, double* ewp, int32_t n, hipStream_t stream);
 // also zeroes out[0..n_out) (the accumulators of this iteration)
 // Device-resident QuasiNewton step (qn_kernel.hip): one workgroup updates x
 // and lambda from out = [LL, grad_full] and writes the next w_full; its info
@@ -270,6 +284,7 @@ struct QnArgs {
     double* expx;
     double* grad;
     double* w_full;              // [n_full + 1] (zero slot)
+    double* ewp;                 // [n_full + 1] exp(w_full), for the bubble kernel
     double* partial;             // [qn_update_blocks(k)][4]
     int32_t n_partial;
     double plogp, eta, tol;
@@ -282,7 +297,7 @@ struct QnArgs {
 };
 int qn_update_blocks(int32_t k);
 hipError_t launch_qn(const QnArgs& a, hipStream_t stream);
-hipError_t launch_qn_weights(const double* x, const int32_t* trim, int32_t n_full, double* w_full,
+hipError_t launch_qn_weights(const double* x, const int32_t* trim, int32_t n_full, double* w_full, double* ewp,
                              hipStream_t stream);
 hipError_t launch_edge_weights(const double* w_full, const int32_t* pptr, const int32_t* pidx, double* lw,
                                double* ew, EdgeRec* erec, int64_t n_edges, double* out, int64_t n_out,

@@ -156,6 +156,7 @@ __global__ __launch_bounds__(kQnUpdateBlock) void qn_update_kernel(QnArgs a) {
                 a.x[b + lane] = xn;
                 a.grad[b + lane] = gi;
                 a.w_full[fo] = xn;   // GetWeight for the next step
+                a.ewp[fo] = exp(xn);
             }
         } else {   // large groups (dense automata): lane 0 through memory
             g = -1.0;
@@ -177,6 +178,7 @@ __global__ __launch_bounds__(kQnUpdateBlock) void qn_update_kernel(QnArgs a) {
                     const double xn = a.x[i] - a.eta * ((gi + ex * laux) / aux);
                     a.x[i] = xn;
                     a.w_full[a.full_of[i]] = xn;
+                    a.ewp[a.full_of[i]] = exp(xn);
                 }
             }
             g = __shfl(g, 0, 64);
@@ -265,13 +267,17 @@ __global__ __launch_bounds__(kQnFinishBlock) void qn_finish_kernel(QnArgs a) {
 }
 
 // initial w_full from x (qn_set_state)
-__global__ void qn_weights_kernel(const double* x, const int32_t* trim, int32_t n_full, double* w_full) {
+__global__ void qn_weights_kernel(const double* x, const int32_t* trim, int32_t n_full, double* w_full, double* ewp) {
     const int j = int(blockIdx.x * blockDim.x + threadIdx.x);
     if (j < n_full) {
         const int tj = trim[j];
         w_full[j] = tj >= 0 ? x[tj] : (tj == -1 ? 0.0 : -INFINITY);
+        ewp[j] = exp(w_full[j]);
     }
-    if (j == n_full) w_full[j] = 0.0;   // the zero slot of the stream kernel
+    if (j == n_full) {   // the zero slot of the stream kernel
+        w_full[j] = 0.0;
+        ewp[j] = 1.0;
+    }
 }
 
 }  // namespace
@@ -287,10 +293,10 @@ hipError_t launch_qn(const QnArgs& a, hipStream_t stream) {
     return hipGetLastError();
 }
 
-hipError_t launch_qn_weights(const double* x, const int32_t* trim, int32_t n_full, double* w_full,
+hipError_t launch_qn_weights(const double* x, const int32_t* trim, int32_t n_full, double* w_full, double* ewp,
                              hipStream_t stream) {
     const unsigned blocks = unsigned((n_full + 1 + 255) / 256);
-    hipLaunchKernelGGL(qn_weights_kernel, dim3(blocks), dim3(256), 0, stream, x, trim, n_full, w_full);
+    hipLaunchKernelGGL(qn_weights_kernel, dim3(blocks), dim3(256), 0, stream, x, trim, n_full, w_full, ewp);
     return hipGetLastError();
 }
 

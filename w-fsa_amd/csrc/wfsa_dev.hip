@@ -109,6 +109,8 @@ struct wfsa_dev {
     int device = 0;
     int n_cu = kNumCu;
     hipStream_t stream = nullptr;
+    hipStream_t side_stream = nullptr;        // the bubble kernel beside the stream kernel
+    hipEvent_t fork = nullptr, join = nullptr;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     // per in-flight step: before the stream kernel, after it, after the tail
     hipEvent_t k0[kQnDepth] = {}, kc[kQnDepth] = {}, k2[kQnDepth] = {};
@@ -173,7 +175,7 @@ struct wfsa_dev {
     DevBuf<int32_t> fall[2];
 
     // work buffers
-    DevBuf<double> w_full, out, ll_part, logq;
+    DevBuf<double> w_full, ewp, out, ll_part, logq;
     DevBuf<unsigned long long> live;
     double* pinned = nullptr;   // [0, n_params+1): results; from weights_off(n_params): weights
     double* pinned_dev = nullptr;   // the same memory as the device addresses it
@@ -277,6 +279,7 @@ wfsa::ModelView model_view(wfsa_dev* ctx) {
     m.n_nodes = ctx->n_nodes;
     m.start = ctx->start;
     m.n_edges = int32_t(ctx->n_edges);
+    m.n_params = ctx->n_params;
     return m;
 }
 
@@ -573,13 +576,35 @@ int prepare(wfsa_dev* ctx, int level) {
         std::vector<int32_t> order(static_cast<size_t>(nbub));
         for (int32_t o : h_off) order[size_t(cnt[size_t(wfsa::kMaxBubbleEdges - (h_bubbuf[size_t(o)] >> 16))]++)] = o;
         HIP_TRY(ctx->bub_off.upload(order.data(), order.size(), s));
+
+        if (std::getenv("WFSA_DEBUG_BUBBLES")) {   // size histogram (diagnostics)
+            std::vector<int64_t> he(size_t(wfsa::kMaxBubbleEdges) + 1, 0), hn(size_t(wfsa::kMaxBubbleNodes) + 1, 0);
+            for (int32_t o : h_off) {
+                he[size_t(h_bubbuf[size_t(o)] >> 16)]++;
+                hn[size_t(h_bubbuf[size_t(o)] & 0xffff)]++;
+            }
+            std::fprintf(stderr, "bubbles %lld; by edges:", (long long)nbub);
+            for (size_t e = 0; e < he.size(); ++e)
+                if (he[e]) std::fprintf(stderr, " %zu:%lld", e, (long long)he[e]);
+            std::fprintf(stderr, "\nby nodes:");
+            for (size_t v = 0; v < hn.size(); ++v)
+                if (hn[v]) std::fprintf(stderr, " %zu:%lld", v, (long long)hn[v]);
+            std::fprintf(stderr, "\n");
+        }
+        // the parameters of a bubble edge from its code (edge_code)
+        auto for_edge_params = [&](int32_t code, auto&& f) {
+            if (code >= 0) {
+                if (code < ctx->n_params) f(code);
+            } else {
+                const int32_t g = -code - 2;
+                for (int32_t q = ctx->h_pptr[size_t(g)]; q < ctx->h_pptr[size_t(g) + 1]; ++q) f(ctx->h_pidx[size_t(q)]);
+            }
+        };
         std::vector<int32_t> pc(size_t(ctx->n_params) + 1, 0);
         for (int32_t o : h_off) {
             const int edges = h_bubbuf[size_t(o)] >> 16;
             for (int e = 0; e < edges; ++e) {
-                const int32_t g = h_bubbuf[size_t(o) + 4 + 2 * size_t(e)];
-                for (int32_t q = ctx->h_pptr[size_t(g)]; q < ctx->h_pptr[size_t(g) + 1]; ++q)
-                    pc[size_t(ctx->h_pidx[size_t(q)]) + 1]++;
+                for_edge_params(h_bubbuf[size_t(o) + 4 + 2 * size_t(e)], [&](int32_t j) { pc[size_t(j) + 1]++; });
             }
         }
         for (size_t j = 1; j < pc.size(); ++j) pc[j] += pc[j - 1];
@@ -587,9 +612,8 @@ int prepare(wfsa_dev* ctx, int level) {
         for (int32_t o : h_off) {
             const int edges = h_bubbuf[size_t(o)] >> 16;
             for (int e = 0; e < edges; ++e) {
-                const int32_t g = h_bubbuf[size_t(o) + 4 + 2 * size_t(e)];
-                for (int32_t q = ctx->h_pptr[size_t(g)]; q < ctx->h_pptr[size_t(g) + 1]; ++q)
-                    slot[size_t(fill[size_t(ctx->h_pidx[size_t(q)])]++)] = (o >> 1) + 2 + e;
+                for_edge_params(h_bubbuf[size_t(o) + 4 + 2 * size_t(e)],
+                                [&](int32_t j) { slot[size_t(fill[size_t(j)]++)] = (o >> 1) + 2 + e; });
             }
         }
         std::vector<int32_t> cparam, cptr;
@@ -748,29 +772,51 @@ int enqueue_compiled(wfsa_dev* ctx, bool with_grad, bool want_logq, const unsign
 // compiled streams (with the per-edge weights) + bubbles (timed by k0..k1),
 // traversal fallback (k1..k2), the tail reduction (which adds the trivial
 // words' constant gradient), and -- without a communicator -- the results out.
+int enqueue_bubbles(wfsa_dev* ctx, bool want_logq, const unsigned* halted, int32_t wave_off, hipStream_t s) {
+    wfsa::BubbleArgs b{};
+    b.m = model_view(ctx);
+    b.p = ctx->p.ptr;
+    b.bub = ctx->bub.ptr;
+    b.bub_off = ctx->bub_off.ptr;
+    b.n_bubbles = ctx->n_bubbles;
+    b.contrib = ctx->contrib.ptr;
+    b.grad = ctx->bubble_atomic ? ctx->out.ptr + 1 : nullptr;
+    b.w = ctx->w_full.ptr;
+    b.ewp = ctx->ewp.ptr;
+    b.ll_part = ctx->ll_part.ptr + wave_off;
+    b.logq = want_logq ? ctx->logq.ptr : nullptr;
+    b.halted = halted;
+    HIP_TRY(wfsa::launch_bubbles(b, ctx->b_grid, s));
+    return WFSA_OK;
+}
+
 // The evaluation kernels; with_tail: finish out = [LL, grad_full] with the
 // tail kernel (else the consumer adds fixed_grad and sums ll_part[0, *n_ll)).
 int enqueue_evaluation(wfsa_dev* ctx, bool want_logq, const unsigned* halted, int slot, bool with_tail = true,
                        int32_t* n_ll = nullptr) {
     hipStream_t s = ctx->stream;
     const int32_t np = ctx->n_params;
-    if (int rc = enqueue_compiled(ctx, false, want_logq, halted, slot)) return rc;
-    int32_t wave_off = ctx->n_groups > 0 ? ctx->i_grid * (ctx->i_block / kWave) : 0;
-    if (ctx->n_bubbles > 0) {
-        wfsa::BubbleArgs b{};
-        b.m = model_view(ctx);
-        b.p = ctx->p.ptr;
-        b.bub = ctx->bub.ptr;
-        b.bub_off = ctx->bub_off.ptr;
-        b.n_bubbles = ctx->n_bubbles;
-        b.contrib = ctx->contrib.ptr;
-        b.grad = ctx->bubble_atomic ? ctx->out.ptr + 1 : nullptr;
-        b.ll_part = ctx->ll_part.ptr + wave_off;
-        b.logq = want_logq ? ctx->logq.ptr : nullptr;
-        b.halted = halted;
-        HIP_TRY(wfsa::launch_bubbles(b, ctx->b_grid, s));
-        wave_off += ctx->b_grid * (wfsa::kBubbleBlock / kWave);
+    // The bubble kernel reads only the weights (ewp, staged before this
+    // point) and writes its own slots and ll partials, so it runs on a second
+    // stream beside the stream kernel (not with log q, where both write the
+    // strings' entries, nor with bubble atomics into out, which the stream
+    // kernel zeroes).
+    const bool side = ctx->n_bubbles > 0 && ctx->side_stream && !want_logq && !ctx->bubble_atomic;
+    if (side) {
+        HIP_TRY(hipEventRecord(ctx->fork, s));
+        HIP_TRY(hipStreamWaitEvent(ctx->side_stream, ctx->fork, 0));
     }
+    int32_t wave_off = ctx->n_groups > 0 ? ctx->i_grid * (ctx->i_block / kWave) : 0;
+    if (ctx->n_bubbles > 0 && side) {
+        if (int rc = enqueue_bubbles(ctx, want_logq, halted, wave_off, ctx->side_stream)) return rc;
+        HIP_TRY(hipEventRecord(ctx->join, ctx->side_stream));
+    }
+    if (int rc = enqueue_compiled(ctx, false, want_logq, halted, slot)) return rc;
+    if (side) HIP_TRY(hipStreamWaitEvent(s, ctx->join, 0));
+    if (ctx->n_bubbles > 0 && !side) {
+        if (int rc = enqueue_bubbles(ctx, want_logq, halted, wave_off, s)) return rc;
+    }
+    if (ctx->n_bubbles > 0) wave_off += ctx->b_grid * (wfsa::kBubbleBlock / kWave);
     for (int t = 0; t < 2; ++t) {
         if (!ctx->n_fall[t]) continue;
         wfsa::TravArgs a = trav_args(ctx, t);
@@ -812,7 +858,7 @@ int enqueue_evaluation(wfsa_dev* ctx, bool want_logq, const unsigned* halted, in
 int enqueue_iteration(wfsa_dev* ctx, bool want_logq) {
     hipStream_t s = ctx->stream;
     const int32_t np = ctx->n_params;
-    HIP_TRY(wfsa::launch_stage(ctx->pinned_dev + weights_off(np), ctx->w_full.ptr, np, s));
+    HIP_TRY(wfsa::launch_stage(ctx->pinned_dev + weights_off(np), ctx->w_full.ptr, ctx->ewp.ptr, np, s));
     if (int rc = enqueue_evaluation(ctx, want_logq, nullptr, 0)) return rc;
     if (!ctx->comm) HIP_TRY(wfsa::launch_publish(ctx->out.ptr, publish_args(ctx), s));
     return WFSA_OK;
@@ -856,6 +902,7 @@ int enqueue_qn_step(wfsa_dev* ctx, double eta, double tol, int slot, bool timed)
     q.expx = ctx->qn_expx.ptr;
     q.grad = ctx->qn_grad.ptr;
     q.w_full = ctx->w_full.ptr;
+    q.ewp = ctx->ewp.ptr;
     q.partial = ctx->qn_partial.ptr;
     q.n_partial = wfsa::qn_update_blocks(ctx->qn_k);
     q.plogp = ctx->qn_plogp;
@@ -906,6 +953,13 @@ int wfsa_dev_create(int device, wfsa_dev** out) {
     if (const char* e = std::getenv("WFSA_TIMING")) ctx->kernel_timing = e[0] != '0';
     if (const char* e = std::getenv("WFSA_BUBBLE_ATOMIC")) ctx->bubble_atomic = e[0] == '1';
     HIP_TRY(hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking));
+    // measured: the cross-stream fork/join costs more idle time (5-20 us)
+    // than the overlap saves, so the side stream is opt-in
+    if (const char* e = std::getenv("WFSA_SIDE_STREAM"); e && e[0] == '1') {
+        HIP_TRY(hipStreamCreateWithFlags(&ctx->side_stream, hipStreamNonBlocking));
+        HIP_TRY(hipEventCreateWithFlags(&ctx->fork, hipEventDisableTiming));
+        HIP_TRY(hipEventCreateWithFlags(&ctx->join, hipEventDisableTiming));
+    }
     HIP_TRY(hipEventCreate(&ctx->ev0));
     HIP_TRY(hipEventCreate(&ctx->ev1));
     for (int i = 0; i < kQnDepth; ++i)
@@ -935,6 +989,10 @@ void wfsa_dev_destroy(wfsa_dev* ctx) {
         for (hipEvent_t ev : {ctx->k0[i], ctx->kc[i], ctx->k2[i]})
             if (ev) (void)hipEventDestroy(ev);
     if (ctx->qn_ring) (void)hipHostFree(ctx->qn_ring);
+    if (ctx->side_stream) (void)hipStreamSynchronize(ctx->side_stream);
+    for (hipEvent_t ev : {ctx->fork, ctx->join})
+        if (ev) (void)hipEventDestroy(ev);
+    if (ctx->side_stream) (void)hipStreamDestroy(ctx->side_stream);
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
     delete ctx;
 }
@@ -985,6 +1043,7 @@ int wfsa_dev_load_model(wfsa_dev* ctx, const wfsa_model_desc* model) {
     ctx->n_nodes = tm.n_nodes;
     ctx->start = tm.start;
     HIP_TRY(ctx->w_full.alloc(size_t(ctx->n_params) + 2));
+    HIP_TRY(ctx->ewp.alloc(size_t(ctx->n_params) + 2));
     HIP_TRY(ctx->out.alloc(size_t(ctx->n_params) + 2));
     const size_t pinned_need = weights_off(ctx->n_params) + size_t(ctx->n_params) + 2;
     if (ctx->pinned_n < pinned_need) {
@@ -1184,7 +1243,7 @@ int wfsa_dev_qn_set_state(wfsa_dev* ctx, const double* x, const double* lambda) 
     hipStream_t s = ctx->stream;
     if (ctx->qn_n > 0) HIP_TRY(ctx->qn_x.upload(x, size_t(ctx->qn_n), s));
     if (ctx->qn_k > 0) HIP_TRY(ctx->qn_lambda.upload(lambda, size_t(ctx->qn_k), s));
-    HIP_TRY(wfsa::launch_qn_weights(ctx->qn_x.ptr, ctx->qn_trim.ptr, ctx->n_params, ctx->w_full.ptr, s));
+    HIP_TRY(wfsa::launch_qn_weights(ctx->qn_x.ptr, ctx->qn_trim.ptr, ctx->n_params, ctx->w_full.ptr, ctx->ewp.ptr, s));
     HIP_TRY(hipStreamSynchronize(s));
     return WFSA_OK;
 }
