@@ -1,2 +1,5 @@
-timeout -k 10 500 python -m pytest tests -m gpu -x -q > gpurun_out/gpu_tests.log 2>&1; tail -2 gpurun_out/gpu_tests.log
-for pc in 2 1; do WFSA_IPERCU=$pc timeout -k 10 300 python bench.py --cpu-sample 0 --steps 50 > gpurun_out/bench_pc$pc.json 2>gpurun_out/bench_pc$pc.err || exit 1; python3 -c "import json; d=json.load(open('gpurun_out/bench_pc$pc.json')); print($pc, d['value'], d['ms_per_step'], d['roofline']['kernel_ms_per_launch'])"; done
+export TMPDIR=/tmp
+for cfg in "0 0" "0 1" "1 1"; do set -- $cfg
+  WFSA_BUBBLE_REG=$1 WFSA_BUBBLE_SKIPBIG=$2 timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d $GRAFT_REPO_ROOT/gpurun_out/bx/r$1s$2 -o run -- python3 $GRAFT_REPO_ROOT/bench.py --cpu-sample 0 --steps 50 > $GRAFT_REPO_ROOT/gpurun_out/bx/r$1s$2.log 2>&1 || exit 1
+  echo "reg=$1 skipbig=$2"; grep bubble_kernel $GRAFT_REPO_ROOT/gpurun_out/bx/r$1s$2/run_kernel_stats.csv | cut -d, -f3-5
+done

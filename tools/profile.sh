@@ -21,4 +21,7 @@ run sq1 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_AN
 run sq2 --pmc SQ_LDS_BANK_CONFLICT SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_SALU SQ_WAIT_INST_LDS SQ_INSTS_SMEM GRBM_GUI_ACTIVE &&
 run fetch --pmc FETCH_SIZE &&
 run write --pmc WRITE_SIZE &&
-run tcc --pmc TCC_HIT_sum TCC_MISS_sum TCC_EA0_ATOMIC_sum
+run tcc --pmc TCC_HIT_sum TCC_MISS_sum TCC_EA0_ATOMIC_sum &&
+# calibration of FETCH_SIZE / WRITE_SIZE on a known byte count (same access width)
+timeout -k 10 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/calfetch" -o run -- "$R/tools/micro/fetch_calib" > "$OUT/calfetch.log" 2>&1 &&
+timeout -k 10 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/calwrite" -o run -- "$R/tools/micro/fetch_calib" > "$OUT/calwrite.log" 2>&1

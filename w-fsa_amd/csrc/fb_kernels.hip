@@ -760,15 +760,16 @@ __global__ __launch_bounds__(1024) void fbs_kernel(CompiledArgs a) {
     if (W_LDS) edge_weight_slice(a);
 }
 
-// Bubbles: one lane per bubble (largest first).  Local forward from the
-// bubble's first cut, local backward from its last cut; an edge's posterior
-// is alpha(src) w beta(dst) / Z and -p_s times it goes to the edge's
-// contribution slot; log Z joins the string's log q.  alpha and beta of the
-// (at most kMaxBubbleNodes) nodes live in registers, addressed by compare-
-// and-select, so the kernel needs no LDS and runs at full occupancy.  A
-// record is 16-byte aligned -- [nodes | edges << 16, string, p (2 words),
-// (edge, src | dst << 16) x edges] -- and is read eight edges at a time with
-// the eight edge weights gathered together.
+// Bubbles.  Local forward from the bubble's first cut, local backward from
+// its last cut; an edge's posterior is alpha(src) w beta(dst) / Z, -p_s times
+// it goes to the edge's slot(s) in the parameter-major contribution array;
+// log Z joins the string's log q.  The weight of an edge is exp(w[code]) from
+// the per-iteration table ewp (edge_code).
+//
+// Small bubbles, one lane each: the bubble's quads are loaded in one round
+// (structure-of-arrays, coalesced), the weights gathered in a second, and
+// alpha/beta of its at most 8 nodes live in registers, addressed through a
+// tree of selects on the node id.
 // r[i] for i < 8 as a tree of selects on the bits of i (a compare chain is
 // re-formed into an indexed scratch load by the compiler)
 template <int N>
@@ -785,130 +786,127 @@ __device__ __forceinline__ void reg_add(double (&r)[N], int i, double v) {
     for (int k = 0; k < N; ++k) r[k] = i == k ? r[k] + v : r[k];
 }
 
-// weight of a bubble edge from its code (edge_code): exp(w[j]) of its one
-// parameter j from the per-iteration table ewp (exp(w), with ewp[n_params]
-// = 1), or exp of the sum for a multi-parameter edge
-__device__ __noinline__ double multi_weight(const ModelView& m, const double* w, int g) {
-    double lw = 0.0;
-    for (int q = m.pptr[g]; q < m.pptr[g + 1]; ++q) lw += w[m.pidx[q]];
-    return exp(lw);
-}
-__device__ __forceinline__ double code_weight(const ModelView& m, const double* w, const double* ewp, int code) {
-    return code >= 0 ? ewp[code] : multi_weight(m, w, -code - 2);
-}
-
-// -p_s times the posterior of a bubble edge: into its contribution slot, or
-// (BubbleArgs::grad) atomically into its parameters' gradient
-__device__ __forceinline__ void bubble_contrib(const BubbleArgs& a, double* c, int e, int code, double v) {
-    if (!a.grad) {
-        c[e] = v;
-    } else if (code >= 0) {
-        if (code < a.m.n_params) global_add(&a.grad[code], v);
-    } else {
-        const int g = -code - 2;
-        for (int q = a.m.pptr[g]; q < a.m.pptr[g + 1]; ++q) global_add(&a.grad[a.m.pidx[q]], v);
-    }
-}
-
-template <int RE>
-__device__ __forceinline__ void bubble_round(const int4* rec, const ModelView& m, const double* wsrc, const double* ewp,
-                                             int e0, int edges, int (&eg)[RE], int (&esd)[RE], double (&ew)[RE]) {
+__device__ __forceinline__ double small_bubble(const BubbleArgs& a, int b) {
+    constexpr int RE = kBubbleRegEdges, N = kBubbleRegNodes;
+    int4 q[kSmallBubbleQuads];
 #pragma unroll
-    for (int q = 0; q < RE / 2; ++q) {
-        const int4 v = rec[1 + e0 / 2 + q];
-        eg[2 * q] = v.x;
-        esd[2 * q] = v.y;
-        eg[2 * q + 1] = v.z;
-        esd[2 * q + 1] = v.w;
+    for (int k = 0; k < kSmallBubbleQuads; ++k) q[k] = a.sm_tbl[size_t(k) * size_t(a.n_small) + size_t(b)];
+    const int nodes = q[0].x & 0xffff, edges = q[0].x >> 16;
+    const double p = __longlong_as_double((long long)(uint32_t(q[0].z)) | ((long long)(uint32_t(q[0].w)) << 32));
+    int code[RE], sd[RE], slot[RE];
+#pragma unroll
+    for (int k = 0; k < RE / 2; ++k) {
+        code[2 * k] = q[1 + k].x;
+        sd[2 * k] = q[1 + k].y;
+        code[2 * k + 1] = q[1 + k].z;
+        sd[2 * k + 1] = q[1 + k].w;
     }
 #pragma unroll
-    for (int e = 0; e < RE; ++e) ew[e] = e0 + e < edges ? code_weight(m, wsrc, ewp, eg[e]) : 0.0;
-}
-
-// One bubble of at most N nodes and RE edges (most bubbles: a diamond of 4
-// edges), alpha/beta and the edges in registers.
-template <int N>
-__device__ __forceinline__ void bubble_eval(const BubbleArgs& a, const double* wsrc, const double* ewp, int off,
-                                            int nodes, int edges, double p, double& lz) {
-    constexpr int RE = kBubbleRegEdges;
-    const int4* rec = reinterpret_cast<const int4*>(a.bub + off);
+    for (int k = 0; k < RE / 4; ++k) {
+        slot[4 * k] = q[5 + k].x;
+        slot[4 * k + 1] = q[5 + k].y;
+        slot[4 * k + 2] = q[5 + k].z;
+        slot[4 * k + 3] = q[5 + k].w;
+    }
+    double ew[RE];
+#pragma unroll
+    for (int e = 0; e < RE; ++e) ew[e] = a.ewp[code[e]];   // padding edges carry the zero-slot code
     double A[N], B[N];
 #pragma unroll
     for (int k = 0; k < N; ++k) {
         A[k] = k == 0 ? 1.0 : 0.0;
         B[k] = 0.0;
     }
-    int g0[RE], sd0[RE];
-    double w0[RE];
-    bubble_round(rec, a.m, wsrc, ewp, 0, edges, g0, sd0, w0);
 #pragma unroll
     for (int e = 0; e < RE; ++e)
-        if (e < edges) reg_add(A, sd0[e] >> 16, reg_get(A, sd0[e] & 0xffff) * w0[e]);
+        if (e < edges) reg_add(A, sd[e] >> 16, reg_get(A, sd[e] & 0xffff) * ew[e]);
     const double Z = reg_get(A, nodes - 1);
     const double scale = -p / Z;
     reg_add(B, nodes - 1, 1.0);
-    double* c = a.contrib + (off >> 1) + 2;
 #pragma unroll
     for (int e = RE - 1; e >= 0; --e)
         if (e < edges) {
-            const int src = sd0[e] & 0xffff;
-            const double b = w0[e] * reg_get(B, sd0[e] >> 16);
-            reg_add(B, src, b);
-            bubble_contrib(a, c, e, g0[e], reg_get(A, src) * b * scale);
+            const int src = sd[e] & 0xffff;
+            const double bb = ew[e] * reg_get(B, sd[e] >> 16);
+            reg_add(B, src, bb);
+            if (slot[e] >= 0) a.contrib[slot[e]] = reg_get(A, src) * bb * scale;
         }
-    lz = log(Z);
-}
-
-// Larger bubbles (more than kBubbleRegEdges edges; rare): the same through
-// a per-lane LDS scratch of 2 x kMaxBubbleNodes doubles.
-__device__ void bubble_eval_mem(const BubbleArgs& a, const double* wsrc, const double* ewp, int off, int nodes,
-                                int edges, double p, double* A, double& lz) {
-    double* B = A + kMaxBubbleNodes;
-    for (int i = 0; i < nodes; ++i) {
-        A[i] = i == 0 ? 1.0 : 0.0;
-        B[i] = 0.0;
-    }
-    const int32_t* ed = a.bub + off + 4;
-    for (int e = 0; e < edges; ++e) {
-        const int code = ed[2 * e], sd = ed[2 * e + 1];
-        A[sd >> 16] += A[sd & 0xffff] * code_weight(a.m, wsrc, ewp, code);
-    }
-    const double Z = A[nodes - 1];
-    const double scale = -p / Z;
-    B[nodes - 1] = 1.0;
-    double* c = a.contrib + (off >> 1) + 2;
-    for (int e = edges - 1; e >= 0; --e) {
-        const int code = ed[2 * e], sd = ed[2 * e + 1];
-        const int src = sd & 0xffff;
-        const double b = code_weight(a.m, wsrc, ewp, code) * B[sd >> 16];
-        B[src] += b;
-        bubble_contrib(a, c, e, code, A[src] * b * scale);
-    }
-    lz = log(Z);
-}
-
-// Bubble bi: log Z and its contributions; returns p log Z.
-__device__ __forceinline__ double bubble_one(const BubbleArgs& a, const double* wsrc, int bi, double* scr) {
-    const double* ewp = a.ewp;
-    const int off = a.bub_off[bi];
-    const int4 h = reinterpret_cast<const int4*>(a.bub + off)[0];
-    const int nodes = h.x & 0xffff, edges = h.x >> 16;
-    const double p = __longlong_as_double((long long)(uint32_t(h.z)) | ((long long)(uint32_t(h.w)) << 32));
-    double lz;
-    if (edges <= kBubbleRegEdges) bubble_eval<kBubbleRegNodes>(a, wsrc, ewp, off, nodes, edges, p, lz);
-    else bubble_eval_mem(a, wsrc, ewp, off, nodes, edges, p, scr, lz);
-    if (a.logq) global_add(&a.logq[h.y], lz);
+    const double lz = log(Z);
+    if (a.logq) global_add(&a.logq[q[0].y], lz);
     return p * lz;
+}
+
+// Big bubbles, one wavefront each: the lanes stage the edges (code, nodes,
+// weight) in LDS in parallel, lane 0 runs the two sweeps over the staged
+// edges, and the lanes write the contributions (an edge may have several
+// parameters, hence several slots).
+constexpr int kBigEdgeLds = 256;   // > kMaxBubbleEdges
+__device__ double big_bubble(const BubbleArgs& a, int i, int* lsd, double* lw, double* lv, double* AB) {
+    const int lane = lane_id();
+    const int off = a.big_off[i];
+    const int32_t* rec = a.bub + off;
+    const int hdr = rec[0];
+    const int nodes = hdr & 0xffff, edges = hdr >> 16;
+    const double p = __longlong_as_double((long long)(uint32_t(rec[2])) | ((long long)(uint32_t(rec[3])) << 32));
+    for (int e = lane; e < edges; e += kWave) {
+        const int code = rec[4 + 2 * e];
+        lsd[e] = rec[5 + 2 * e];
+        double wgt;
+        if (code >= 0) {
+            wgt = a.ewp[code];
+        } else {
+            const int g = -code - 2;
+            double s = 0.0;
+            for (int q = a.m.pptr[g]; q < a.m.pptr[g + 1]; ++q) s += a.w[a.m.pidx[q]];
+            wgt = exp(s);
+        }
+        lw[e] = wgt;
+    }
+    wave_sync();
+    double res = 0.0;
+    if (lane == 0) {
+        double* A = AB;
+        double* B = AB + kMaxBubbleNodes;
+        for (int v = 0; v < nodes; ++v) {
+            A[v] = v == 0 ? 1.0 : 0.0;
+            B[v] = 0.0;
+        }
+        for (int e = 0; e < edges; ++e) A[lsd[e] >> 16] += A[lsd[e] & 0xffff] * lw[e];
+        const double Z = A[nodes - 1];
+        const double scale = -p / Z;
+        B[nodes - 1] = 1.0;
+        for (int e = edges - 1; e >= 0; --e) {
+            const int src = lsd[e] & 0xffff;
+            const double bb = lw[e] * B[lsd[e] >> 16];
+            B[src] += bb;
+            lv[e] = A[src] * bb * scale;
+        }
+        const double lz = log(Z);
+        if (a.logq) global_add(&a.logq[rec[1]], lz);
+        res = p * lz;
+    }
+    wave_sync();
+    const int base = a.big_edge_base[i];
+    for (int e = lane; e < edges; e += kWave)
+        for (int q = a.big_eslot_ptr[base + e]; q < a.big_eslot_ptr[base + e + 1]; ++q) a.contrib[a.big_eslot[q]] = lv[e];
+    return res;
 }
 
 __global__ __launch_bounds__(kBubbleBlock) void bubble_kernel(BubbleArgs a) {
     if (a.halted && *a.halted) return;
+    constexpr int WPB = kBubbleBlock / kWave;
+    __shared__ int lsd[WPB][kBigEdgeLds];
+    __shared__ double lw[WPB][kBigEdgeLds], lv[WPB][kBigEdgeLds], lab[WPB][2 * kMaxBubbleNodes];
     const int lane = lane_id();
-    const int gw = int(blockIdx.x) * (kBubbleBlock / kWave) + int(threadIdx.x) / kWave;
-    __shared__ double scr[kBubbleBlock][2 * kMaxBubbleNodes];
+    const int wib = int(threadIdx.x) / kWave;
+    const int gw = int(blockIdx.x) * WPB + wib;
     double ll_acc = 0.0;
-    for (int bi = int(blockIdx.x * blockDim.x + threadIdx.x); bi < a.n_bubbles; bi += int(gridDim.x * blockDim.x))
-        ll_acc += bubble_one(a, a.w, bi, scr[threadIdx.x]);
+    if (gw < a.n_big) {
+        ll_acc = big_bubble(a, gw, lsd[wib], lw[wib], lv[wib], lab[wib]);
+    } else {
+        const int b = (gw - a.n_big) * kWave + lane;
+        if (b < a.n_small) ll_acc = small_bubble(a, b);
+    }
     ll_acc = wave_sum(ll_acc);
     if (lane == 0) a.ll_part[gw] = ll_acc;
 }
@@ -948,24 +946,19 @@ __global__ __launch_bounds__(256) void tail_kernel(TailArgs a) {
             for (int k = k0; k < k1; ++k) s += a.gpart[size_t(k) * size_t(a.n_params) + size_t(j)];
             if (s != 0.0) global_add(&a.out[1 + j], s);
         }
-    } else if (b < n_param_blocks + n_chunk_blocks) {   // bubble contributions
+    } else if (b < n_param_blocks + n_chunk_blocks) {   // bubble contributions, contiguous runs
         const int c = (b - n_param_blocks) * 4 + int(threadIdx.x) / kWave;
         if (c < a.n_chunks) {
             const int lane = lane_id();
-            double s = 0.0;
             const int k0 = a.chunk_ptr[c], k1 = a.chunk_ptr[c + 1];
-            // a chunk is at most kBubbleGradChunk = 8 x 64 slots: one round
-            // of slot loads, one of contribution gathers
-            static_assert(kBubbleGradChunk <= 8 * kWave, "chunk larger than one gather round");
-            int sl[8];
-#pragma unroll
-            for (int b = 0; b < 8; ++b) sl[b] = a.slot[min(k0 + lane + b * kWave, k1 - 1)];
+            static_assert(kBubbleGradChunk <= 8 * kWave, "run longer than one load round");
             double v[8];
 #pragma unroll
-            for (int b = 0; b < 8; ++b) v[b] = a.contrib[sl[b]];
+            for (int r = 0; r < 8; ++r) v[r] = a.contrib[min(k0 + lane + r * kWave, k1 - 1)];
+            double s = 0.0;
 #pragma unroll
-            for (int b = 0; b < 8; ++b)
-                if (k0 + lane + b * kWave < k1) s += v[b];
+            for (int r = 0; r < 8; ++r)
+                if (k0 + lane + r * kWave < k1) s += v[r];
             s = wave_sum(s);
             if (lane == 0) global_add(&a.out[1 + a.chunk_param[c]], s);
         }
@@ -1115,9 +1108,13 @@ hipError_t launch_compiled(const CompiledArgs& a, int grid, int block, size_t ld
     return hipGetLastError();
 }
 
-hipError_t launch_bubbles(const BubbleArgs& a, int grid, hipStream_t stream) {
-    if (a.n_bubbles <= 0) return hipSuccess;
-    hipLaunchKernelGGL(bubble_kernel, dim3(unsigned(grid)), dim3(kBubbleBlock), 0, stream, a);
+int bubble_waves(int32_t n_small, int32_t n_big) { return n_big + (n_small + kWave - 1) / kWave; }
+
+hipError_t launch_bubbles(const BubbleArgs& a, hipStream_t stream) {
+    const int waves = bubble_waves(a.n_small, a.n_big);
+    if (waves <= 0) return hipSuccess;
+    constexpr int WPB = kBubbleBlock / kWave;
+    hipLaunchKernelGGL(bubble_kernel, dim3(unsigned((waves + WPB - 1) / WPB)), dim3(kBubbleBlock), 0, stream, a);
     return hipGetLastError();
 }
 

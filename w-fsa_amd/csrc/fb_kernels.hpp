@@ -181,14 +181,31 @@ struct CompiledArgs {
     const unsigned* halted;  // device-resident QN run: nonzero = skip (or null)
 };
 
+// Bubble evaluation.  Contributions (-p_s x edge posterior) go straight to
+// their slots in `contrib`, which is parameter-major: parameter j owns the
+// contiguous range [slot_ptr[j], slot_ptr[j+1]) -- the tail kernel then sums
+// contiguous runs, no gather.
+//   small bubbles (<= kBubbleRegEdges edges, <= kBubbleRegNodes nodes, every
+//     edge with at most one parameter): a structure-of-arrays table of
+//     kSmallBubbleQuads 16-byte quads per bubble -- quad k of bubble b at
+//     sm_tbl[k * n_small + b]: [header: nodes | edges << 16, string, p (2
+//     words)], 4 x [(code, src | dst << 16) x 2], 2 x [slot x 4] (-1: the
+//     edge has no parameter) -- one lane per bubble, coalesced loads.
+//   big bubbles (the rest, rare): variable records in `bub` at big_off[i]
+//     (bubble record layout above), one wavefront per bubble; the slots of
+//     edge e of big bubble i are big_eslot[big_eslot_ptr[big_edge_base[i] + e] ..].
+constexpr int kSmallBubbleQuads = 7;
 struct BubbleArgs {
     ModelView m;
-    const double* p;
+    const int4* sm_tbl;
+    int32_t n_small;
     const int32_t* bub;
-    const int32_t* bub_off;  // [n_bubbles], largest bubbles first
-    int32_t n_bubbles;
-    double* contrib;         // [bubble words / 2] -p_s * posterior per bubble edge (grad == null)
-    double* grad;            // or: [n_params] atomically accumulated (out + 1)
+    const int32_t* big_off;
+    int32_t n_big;
+    const int32_t* big_edge_base;
+    const int32_t* big_eslot_ptr;
+    const int32_t* big_eslot;
+    double* contrib;
     double* ll_part;         // [waves in grid]
     double* logq;            // [S] or null: log Z added to the string's entry
     const double* w;         // [n_params + 1] weights (GetWeight form) with the zero slot
@@ -198,9 +215,10 @@ struct BubbleArgs {
 
 // The per-iteration tail, one launch: out[1+j] += sum over blocks of the
 // compiled kernel's partial gradients, += the bubble contributions of
-// parameter j (chunks of at most kBubbleGradChunk slots, one wavefront per
-// chunk, so a hot parameter's long list is summed by many waves), and
-// out[0] = sum of the per-wave log-likelihood partials in a fixed order.
+// parameter j (runs of at most kBubbleGradChunk contiguous slots, one
+// wavefront per run, so a hot parameter's long range is summed by many
+// waves), and out[0] = sum of the per-wave log-likelihood partials in a
+// fixed order.
 constexpr int kBubbleGradChunk = 512;
 // Completion without a DMA copy or a stream synchronisation: a one-block
 // kernel copies out[0, n) into host-mapped memory, fences at system scope and
@@ -216,8 +234,7 @@ struct TailArgs {
     const double* gpart;         // [n_gpart][n_params]
     int32_t n_gpart;
     const int32_t* chunk_param;  // [n_chunks]
-    const int32_t* chunk_ptr;    // [n_chunks+1] into slot
-    const int32_t* slot;
+    const int32_t* chunk_ptr;    // [n_chunks+1] contiguous runs of contrib
     const double* contrib;
     int32_t n_chunks;
     const double* ll_part;
@@ -246,7 +263,9 @@ hipError_t configure_kernels(int max_dynamic_lds);
 hipError_t launch_trav(TravMode mode, const TravArgs& a, int grid, hipStream_t stream);
 hipError_t launch_compiled(const CompiledArgs& a, int grid, int block, size_t lds, hipStream_t stream);
 constexpr int kBubbleBlock = 128;
-hipError_t launch_bubbles(const BubbleArgs& a, int grid, hipStream_t stream);
+// waves: n_big (one per big bubble) + ceil(n_small / 64)
+int bubble_waves(int32_t n_small, int32_t n_big);
+hipError_t launch_bubbles(const BubbleArgs& a, hipStream_t stream);
 hipError_t launch_tail(const TailArgs& a, hipStream_t stream);
 // out[0, n) -> host-mapped memory, then the flag (one block)
 hipError_t launch_publish(const double* out, const Publish& pub, hipStream_t stream);
@@ -269,11 +288,6 @@ struct QnArgs {
     const double* fixed;
     const double* ll_part;
     int32_t n_ll;
-    // and the bubble contributions of kept parameter i: contrib[slot[q]] for
-    // q in [slot_ptr[i], slot_ptr[i+1]) (null: none / already in out)
-    const int32_t* slot_ptr;
-    const int32_t* slot;
-    const double* contrib;
     int32_t n_full, n, k;
     const int32_t* full_of;      // [n] full index of each kept parameter
     const int32_t* trim;         // [n_full] trimmed index / -1 / -2

@@ -66,30 +66,16 @@ __device__ __forceinline__ void wave_sync() {
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
 }
 
-// The gradient of kept parameter i as the QN step sees it: the device's
-// out[1 + j] (j = its full index) plus, without the tail kernel, the constant
-// trivial-word part and its bubble contributions.
-__device__ __forceinline__ double grad_of(const QnArgs& a, int i, int fo) {
-    double gi = a.out[1 + fo] + (a.fixed ? a.fixed[fo] : 0.0);
-    if (a.slot_ptr)
-        for (int q = a.slot_ptr[i]; q < a.slot_ptr[i + 1]; ++q) gi += a.contrib[a.slot[q]];
-    return gi;
-}
-
 // qn_update: one wavefront per constraint.  Every quantity of the update is
 // local to a constraint (its members are a contiguous, ascending range of
 // parameters), so waves are independent; each block writes its partial
 // (g_min, g_max, lambda_min, graderr) and qn_finish reduces them.  Lane m
-// owns member m: the bubble contributions of the constraint's members (a
-// contiguous run of slots) are gathered by all lanes and reduced by member
-// with a segmented wave scan (fixed order); exp and the x update are
-// per-lane; g and the lambda_next numerator are summed by lane 0 in member
-// order, as the host does.
+// owns member m (exp and the x update); g and the lambda_next numerator are
+// summed by lane 0 in member order, as the host does.
 __global__ __launch_bounds__(kQnUpdateBlock) void qn_update_kernel(QnArgs a) {
     if (*a.halted) return;
     constexpr int W = kQnUpdateBlock / 64;
-    __shared__ double sh_ev[W][64], sh_gv[W][64], sh_acc[W][64];
-    __shared__ int sh_end[W][64];
+    __shared__ double sh_ev[W][64], sh_gv[W][64];
     __shared__ double sh_bc[W][2];
     __shared__ double red[W][4];
     const int lane = int(threadIdx.x) & 63, w = int(threadIdx.x) >> 6;
@@ -106,33 +92,6 @@ __global__ __launch_bounds__(kQnUpdateBlock) void qn_update_kernel(QnArgs a) {
                 xi = a.x[b + lane];
                 fo = a.full_of[b + lane];
                 gi = a.out[1 + fo] + (a.fixed ? a.fixed[fo] : 0.0);
-            }
-            if (a.slot_ptr) {
-                double* acc = sh_acc[w];
-                int* mend = sh_end[w];
-                acc[lane] = 0.0;
-                mend[lane] = lane < nm ? a.slot_ptr[b + lane + 1] : INT32_MAX;
-                const int q0 = a.slot_ptr[b], q1 = a.slot_ptr[e];
-                wave_sync();
-                for (int q = q0; q < q1; q += 64) {
-                    const int k = q + lane;
-                    const bool valid = k < q1;
-                    const double v0 = valid ? a.contrib[a.slot[k]] : 0.0;
-                    int m = 0;
-                    while (m < nm && mend[m] <= k) ++m;
-                    if (!valid) m = 1 << 20;
-                    double v = v0;
-#pragma unroll
-                    for (int d = 1; d < 64; d <<= 1) {
-                        const double ov = __shfl_up(v, d, 64);
-                        const int om = __shfl_up(m, d, 64);
-                        if (lane >= d && om == m) v += ov;
-                    }
-                    const int next_m = __shfl_down(m, 1, 64);
-                    if (valid && (lane == 63 || next_m != m)) acc[m] += v;
-                    wave_sync();
-                }
-                if (lane < nm) gi += acc[lane];
             }
             const double ei = lane < nm ? exp(xi) : 0.0;
             sh_ev[w][lane] = ei;
@@ -165,7 +124,7 @@ __global__ __launch_bounds__(kQnUpdateBlock) void qn_update_kernel(QnArgs a) {
                 for (int i = b; i < e; ++i) {
                     const double ex = exp(a.x[i]);
                     a.expx[i] = ex;
-                    a.grad[i] = grad_of(a, i, a.full_of[i]);
+                    a.grad[i] = a.out[1 + a.full_of[i]] + (a.fixed ? a.fixed[a.full_of[i]] : 0.0);
                     g += ex;
                 }
                 double r = lam * g;

@@ -160,13 +160,15 @@ struct wfsa_dev {
     size_t i_lds = 0;
     DevBuf<double> fixed_grad;       // [n_params] gradient of the trivial words (constant)
     // bubbles
-    int32_t n_bubbles = 0;
-    int b_grid = 0;
+    int32_t n_bubbles = 0, n_small = 0, n_big = 0;
+    int b_waves = 0;
+    DevBuf<int4> sm_tbl;
+    DevBuf<int32_t> big_off, big_edge_base, big_eslot_ptr, big_eslot;
     int32_t n_bg_chunks = 0;
-    DevBuf<int32_t> bub_off, bg_chunk_param, bg_chunk_ptr, bg_slot;
+    DevBuf<int32_t> bub_off, bg_chunk_param, bg_chunk_ptr;
     DevBuf<double> contrib;
     std::vector<int32_t> h_pptr, h_pidx;   // host copy of the combined parameter lists
-    std::vector<int32_t> h_bslot_ptr, h_bslot;   // host copy of the bubble slot CSR by parameter
+
     size_t c_lds = 0;
 
     // traversal fallback: per tier string lists
@@ -187,7 +189,7 @@ struct wfsa_dev {
     unsigned seq = 0;            // last sequence number the host expects
     bool timing_pending = false; // events of the last call not yet read
     bool kernel_timing = true;
-    bool bubble_atomic = false;  // bubble gradients by global atomics (WFSA_BUBBLE_ATOMIC=1; measured slower)
+
     DevBuf<double> gpart;        // per-block partial gradients of the compiled kernel
 
     // the per-iteration device sequence, captured once per prepared corpus
@@ -203,9 +205,6 @@ struct wfsa_dev {
     int32_t qn_n = 0, qn_k = 0, qn_exp_lambda = 0;
     double qn_plogp = 0.0;
     DevBuf<int32_t> qn_trim, qn_full_of, qn_ccol, qn_cptr;
-    std::vector<int32_t> qn_h_full_of;
-    DevBuf<int32_t> qn_slot_ptr, qn_slot;   // bubble slots of each kept parameter (QN order)
-    int qn_slots_for = -1;                   // prep generation the slot CSR was built for
     int prep_gen = 0;
     DevBuf<double> qn_x, qn_lambda, qn_expx, qn_grad, qn_partial;
     DevBuf<unsigned> qn_halted;
@@ -561,29 +560,43 @@ int prepare(wfsa_dev* ctx, int level) {
     ctx->n_groups = G;
     ctx->n_compiled = nc;
 
-    // bubbles: largest first (similar lanes per wave), and the parameter ->
-    // contribution-slot index of their edges
+    // bubbles: small ones into the structure-of-arrays table, big ones kept
+    // as records; every (bubble edge, parameter) pair gets a slot in the
+    // parameter-major contribution array, and runs of at most
+    // kBubbleGradChunk slots of one parameter form the tail's chunks
     ctx->n_bubbles = int32_t(nbub);
+    ctx->n_small = ctx->n_big = 0;
     if (nbub > 0) {
         std::vector<int32_t> h_bubbuf(static_cast<size_t>(bwords)), h_off(static_cast<size_t>(nbub));
         HIP_TRY(ctx->bub.download(h_bubbuf.data(), size_t(bwords), s));
         HIP_TRY(ctx->bub_off.download(h_off.data(), size_t(nbub), s));
         HIP_TRY(hipStreamSynchronize(s));
-        std::vector<int64_t> cnt(size_t(wfsa::kMaxBubbleEdges) + 2, 0);
-        for (int32_t o : h_off) cnt[size_t(wfsa::kMaxBubbleEdges - (h_bubbuf[size_t(o)] >> 16))]++;
-        int64_t acc = 0;
-        for (auto& c : cnt) { const int64_t t = c; c = acc; acc += t; }
-        std::vector<int32_t> order(static_cast<size_t>(nbub));
-        for (int32_t o : h_off) order[size_t(cnt[size_t(wfsa::kMaxBubbleEdges - (h_bubbuf[size_t(o)] >> 16))]++)] = o;
-        HIP_TRY(ctx->bub_off.upload(order.data(), order.size(), s));
-
+        const int32_t np = ctx->n_params;
+        auto edge_code_at = [&](int32_t o, int e) { return h_bubbuf[size_t(o) + 4 + 2 * size_t(e)]; };
+        // the parameters of a bubble edge from its code (edge_code)
+        auto for_edge_params = [&](int32_t code, auto&& f) {
+            if (code >= 0) {
+                if (code < np) f(code);
+            } else {
+                const int32_t g = -code - 2;
+                for (int32_t q = ctx->h_pptr[size_t(g)]; q < ctx->h_pptr[size_t(g) + 1]; ++q) f(ctx->h_pidx[size_t(q)]);
+            }
+        };
+        std::vector<int32_t> small, big;
+        for (int32_t o : h_off) {
+            const int hdr = h_bubbuf[size_t(o)];
+            const int nodes = hdr & 0xffff, edges = hdr >> 16;
+            bool sm = edges <= wfsa::kBubbleRegEdges && nodes <= wfsa::kBubbleRegNodes;
+            for (int e = 0; sm && e < edges; ++e) sm = edge_code_at(o, e) >= 0;
+            (sm ? small : big).push_back(o);
+        }
         if (std::getenv("WFSA_DEBUG_BUBBLES")) {   // size histogram (diagnostics)
             std::vector<int64_t> he(size_t(wfsa::kMaxBubbleEdges) + 1, 0), hn(size_t(wfsa::kMaxBubbleNodes) + 1, 0);
             for (int32_t o : h_off) {
                 he[size_t(h_bubbuf[size_t(o)] >> 16)]++;
                 hn[size_t(h_bubbuf[size_t(o)] & 0xffff)]++;
             }
-            std::fprintf(stderr, "bubbles %lld; by edges:", (long long)nbub);
+            std::fprintf(stderr, "bubbles %lld (small %zu, big %zu); by edges:", (long long)nbub, small.size(), big.size());
             for (size_t e = 0; e < he.size(); ++e)
                 if (he[e]) std::fprintf(stderr, " %zu:%lld", e, (long long)he[e]);
             std::fprintf(stderr, "\nby nodes:");
@@ -591,52 +604,67 @@ int prepare(wfsa_dev* ctx, int level) {
                 if (hn[v]) std::fprintf(stderr, " %zu:%lld", v, (long long)hn[v]);
             std::fprintf(stderr, "\n");
         }
-        // the parameters of a bubble edge from its code (edge_code)
-        auto for_edge_params = [&](int32_t code, auto&& f) {
-            if (code >= 0) {
-                if (code < ctx->n_params) f(code);
-            } else {
-                const int32_t g = -code - 2;
-                for (int32_t q = ctx->h_pptr[size_t(g)]; q < ctx->h_pptr[size_t(g) + 1]; ++q) f(ctx->h_pidx[size_t(q)]);
-            }
-        };
-        std::vector<int32_t> pc(size_t(ctx->n_params) + 1, 0);
-        for (int32_t o : h_off) {
+        // slots, parameter-major; within a parameter: small bubbles, then big
+        std::vector<int32_t> pc(size_t(np) + 1, 0);
+        for (const auto* list : {&small, &big})
+            for (int32_t o : *list)
+                for (int e = 0; e < (h_bubbuf[size_t(o)] >> 16); ++e)
+                    for_edge_params(edge_code_at(o, e), [&](int32_t jj) { pc[size_t(jj) + 1]++; });
+        for (size_t jj = 1; jj < pc.size(); ++jj) pc[jj] += pc[jj - 1];
+        std::vector<int32_t> fill(pc.begin(), pc.end() - 1);
+        const int64_t ns = int64_t(small.size()), nb = int64_t(big.size());
+        constexpr int Q = wfsa::kSmallBubbleQuads;
+        std::vector<int32_t> tbl(size_t(Q) * 4 * size_t(std::max<int64_t>(ns, 1)), 0);
+        auto quad = [&](int k, int64_t b) { return &tbl[(size_t(k) * size_t(ns) + size_t(b)) * 4]; };
+        for (int64_t b = 0; b < ns; ++b) {
+            const int32_t o = small[size_t(b)];
             const int edges = h_bubbuf[size_t(o)] >> 16;
-            for (int e = 0; e < edges; ++e) {
-                for_edge_params(h_bubbuf[size_t(o) + 4 + 2 * size_t(e)], [&](int32_t j) { pc[size_t(j) + 1]++; });
+            for (int w = 0; w < 4; ++w) quad(0, b)[w] = h_bubbuf[size_t(o) + size_t(w)];
+            for (int e = 0; e < wfsa::kBubbleRegEdges; ++e) {
+                int32_t code = np, sd = 0, sl = -1;   // padding edges: the zero-slot code
+                if (e < edges) {
+                    code = edge_code_at(o, e);
+                    sd = h_bubbuf[size_t(o) + 5 + 2 * size_t(e)];
+                    if (code < np) sl = fill[size_t(code)]++;
+                }
+                quad(1 + e / 2, b)[2 * (e & 1)] = code;
+                quad(1 + e / 2, b)[2 * (e & 1) + 1] = sd;
+                quad(5 + e / 4, b)[e & 3] = sl;
             }
         }
-        for (size_t j = 1; j < pc.size(); ++j) pc[j] += pc[j - 1];
-        std::vector<int32_t> slot(size_t(pc.back())), fill(pc.begin(), pc.end() - 1);
-        for (int32_t o : h_off) {
-            const int edges = h_bubbuf[size_t(o)] >> 16;
-            for (int e = 0; e < edges; ++e) {
-                for_edge_params(h_bubbuf[size_t(o) + 4 + 2 * size_t(e)],
-                                [&](int32_t j) { slot[size_t(fill[size_t(j)]++)] = (o >> 1) + 2 + e; });
+        std::vector<int32_t> big_edge_base(size_t(std::max<int64_t>(nb, 1)), 0), eslot_ptr(1, 0), eslot;
+        for (int64_t i = 0; i < nb; ++i) {
+            const int32_t o = big[size_t(i)];
+            big_edge_base[size_t(i)] = int32_t(eslot_ptr.size()) - 1;
+            for (int e = 0; e < (h_bubbuf[size_t(o)] >> 16); ++e) {
+                for_edge_params(edge_code_at(o, e), [&](int32_t jj) { eslot.push_back(fill[size_t(jj)]++); });
+                eslot_ptr.push_back(int32_t(eslot.size()));
             }
         }
+        if (eslot.empty()) eslot.push_back(0);
+        HIP_TRY(ctx->sm_tbl.upload(reinterpret_cast<const int4*>(tbl.data()), tbl.size() / 4, s));
+        HIP_TRY(ctx->big_off.upload(big.empty() ? h_off.data() : big.data(), std::max<size_t>(big.size(), 1), s));
+        HIP_TRY(ctx->big_edge_base.upload(big_edge_base.data(), big_edge_base.size(), s));
+        HIP_TRY(ctx->big_eslot_ptr.upload(eslot_ptr.data(), eslot_ptr.size(), s));
+        HIP_TRY(ctx->big_eslot.upload(eslot.data(), eslot.size(), s));
+        ctx->n_small = int32_t(ns);
+        ctx->n_big = int32_t(nb);
         std::vector<int32_t> cparam, cptr;
-        for (int32_t j = 0; j < ctx->n_params; ++j)
-            for (int32_t b = pc[size_t(j)]; b < pc[size_t(j) + 1]; b += wfsa::kBubbleGradChunk) {
-                cparam.push_back(j);
+        for (int32_t jj = 0; jj < np; ++jj)
+            for (int32_t b = pc[size_t(jj)]; b < pc[size_t(jj) + 1]; b += wfsa::kBubbleGradChunk) {
+                cparam.push_back(jj);
                 cptr.push_back(b);
             }
         cptr.push_back(pc.back());
         ctx->n_bg_chunks = int32_t(cparam.size());
-        HIP_TRY(ctx->bg_chunk_param.upload(cparam.data(), cparam.size(), s));
+        if (!cparam.empty()) HIP_TRY(ctx->bg_chunk_param.upload(cparam.data(), cparam.size(), s));
         HIP_TRY(ctx->bg_chunk_ptr.upload(cptr.data(), cptr.size(), s));
-        HIP_TRY(ctx->bg_slot.upload(slot.data(), slot.size(), s));
-        ctx->h_bslot_ptr = pc;
-        ctx->h_bslot = slot;
-        HIP_TRY(ctx->contrib.alloc(size_t(bwords / 2) + 1));
-        HIP_TRY(hipMemsetAsync(ctx->contrib.ptr, 0, (size_t(bwords / 2) + 1) * sizeof(double), s));
-        ctx->b_grid = int(std::max<int64_t>(1, std::min<int64_t>((nbub + wfsa::kBubbleBlock - 1) / wfsa::kBubbleBlock,
-                                                                  int64_t(ctx->n_cu) * 8)));
+        HIP_TRY(ctx->contrib.alloc(size_t(std::max(pc.back(), 1))));
+        HIP_TRY(hipMemsetAsync(ctx->contrib.ptr, 0, size_t(std::max(pc.back(), 1)) * sizeof(double), s));
+        ctx->b_waves = wfsa::bubble_waves(ctx->n_small, ctx->n_big);
+        HIP_TRY(hipStreamSynchronize(s));
     } else {
-        ctx->b_grid = 0;
-        ctx->h_bslot_ptr.assign(size_t(ctx->n_params) + 1, 0);
-        ctx->h_bslot.clear();
+        ctx->b_waves = 0;
     }
 
     // compiled kernel geometry: 16 waves per block, one block per CU; w and
@@ -679,7 +707,7 @@ int prepare(wfsa_dev* ctx, int level) {
         if (!fb[t].empty()) HIP_TRY(ctx->fall[t].upload(fb[t].data(), fb[t].size(), s));
     }
     const size_t waves = std::max(size_t(ctx->c_grid) * waves_per_block, size_t(ctx->i_grid) * size_t(i_wpb)) +
-                         size_t(ctx->b_grid) * (wfsa::kBubbleBlock / kWave) +
+                         size_t(ctx->b_waves) +
                          size_t(ctx->fall_grid[0]) * size_t(ctx->cfg[0].waves_per_block) +
                          size_t(ctx->fall_grid[1]) * size_t(ctx->cfg[1].waves_per_block);
     HIP_TRY(ctx->ll_part.alloc(waves));
@@ -775,18 +803,21 @@ int enqueue_compiled(wfsa_dev* ctx, bool with_grad, bool want_logq, const unsign
 int enqueue_bubbles(wfsa_dev* ctx, bool want_logq, const unsigned* halted, int32_t wave_off, hipStream_t s) {
     wfsa::BubbleArgs b{};
     b.m = model_view(ctx);
-    b.p = ctx->p.ptr;
+    b.sm_tbl = ctx->sm_tbl.ptr;
+    b.n_small = ctx->n_small;
     b.bub = ctx->bub.ptr;
-    b.bub_off = ctx->bub_off.ptr;
-    b.n_bubbles = ctx->n_bubbles;
+    b.big_off = ctx->big_off.ptr;
+    b.n_big = ctx->n_big;
+    b.big_edge_base = ctx->big_edge_base.ptr;
+    b.big_eslot_ptr = ctx->big_eslot_ptr.ptr;
+    b.big_eslot = ctx->big_eslot.ptr;
     b.contrib = ctx->contrib.ptr;
-    b.grad = ctx->bubble_atomic ? ctx->out.ptr + 1 : nullptr;
     b.w = ctx->w_full.ptr;
     b.ewp = ctx->ewp.ptr;
     b.ll_part = ctx->ll_part.ptr + wave_off;
     b.logq = want_logq ? ctx->logq.ptr : nullptr;
     b.halted = halted;
-    HIP_TRY(wfsa::launch_bubbles(b, ctx->b_grid, s));
+    HIP_TRY(wfsa::launch_bubbles(b, s));
     return WFSA_OK;
 }
 
@@ -801,7 +832,7 @@ int enqueue_evaluation(wfsa_dev* ctx, bool want_logq, const unsigned* halted, in
     // stream beside the stream kernel (not with log q, where both write the
     // strings' entries, nor with bubble atomics into out, which the stream
     // kernel zeroes).
-    const bool side = ctx->n_bubbles > 0 && ctx->side_stream && !want_logq && !ctx->bubble_atomic;
+    const bool side = ctx->n_bubbles > 0 && ctx->side_stream && !want_logq;
     if (side) {
         HIP_TRY(hipEventRecord(ctx->fork, s));
         HIP_TRY(hipStreamWaitEvent(ctx->side_stream, ctx->fork, 0));
@@ -816,7 +847,7 @@ int enqueue_evaluation(wfsa_dev* ctx, bool want_logq, const unsigned* halted, in
     if (ctx->n_bubbles > 0 && !side) {
         if (int rc = enqueue_bubbles(ctx, want_logq, halted, wave_off, s)) return rc;
     }
-    if (ctx->n_bubbles > 0) wave_off += ctx->b_grid * (wfsa::kBubbleBlock / kWave);
+    if (ctx->n_bubbles > 0) wave_off += ctx->b_waves;
     for (int t = 0; t < 2; ++t) {
         if (!ctx->n_fall[t]) continue;
         wfsa::TravArgs a = trav_args(ctx, t);
@@ -839,9 +870,8 @@ int enqueue_evaluation(wfsa_dev* ctx, bool want_logq, const unsigned* halted, in
     t.n_gpart = ctx->n_groups > 0 ? 1 : 0;
     t.chunk_param = ctx->bg_chunk_param.ptr;
     t.chunk_ptr = ctx->bg_chunk_ptr.ptr;
-    t.slot = ctx->bg_slot.ptr;
     t.contrib = ctx->contrib.ptr;
-    t.n_chunks = (ctx->n_bubbles > 0 && !ctx->bubble_atomic) ? ctx->n_bg_chunks : 0;
+    t.n_chunks = ctx->n_bubbles > 0 ? ctx->n_bg_chunks : 0;
     t.ll_part = ctx->ll_part.ptr;
     t.n_ll = wave_off;
     t.n_params = np;
@@ -871,9 +901,9 @@ int enqueue_qn_step(wfsa_dev* ctx, double eta, double tol, int slot, bool timed)
     hipStream_t s = ctx->stream;
     const int32_t np = ctx->n_params;
     // without a communicator the QN kernel finishes the reduction itself
-    // (the bubble contributions need the tail's param-chunk reduction: one
-    // wave per constraint cannot absorb a hot parameter's slot list)
-    const bool tail = ctx->comm != nullptr || !ctx->bubble_atomic;
+    // (the bubble contributions need the tail's run reduction: one wave per
+    // constraint cannot absorb a hot parameter's slot range)
+    const bool tail = ctx->comm != nullptr || ctx->n_bubbles > 0;
     int32_t n_ll = 0;
     if (int rc = enqueue_evaluation(ctx, false, ctx->qn_halted.ptr, timed ? slot : -1, tail, &n_ll)) return rc;
     if (ctx->comm)
@@ -884,11 +914,6 @@ int enqueue_qn_step(wfsa_dev* ctx, double eta, double tol, int slot, bool timed)
         q.fixed = ctx->n_groups > 0 ? ctx->fixed_grad.ptr : nullptr;
         q.ll_part = ctx->ll_part.ptr;
         q.n_ll = n_ll;
-        if (ctx->n_bubbles > 0 && !ctx->bubble_atomic) {
-            q.slot_ptr = ctx->qn_slot_ptr.ptr;
-            q.slot = ctx->qn_slot.ptr;
-            q.contrib = ctx->contrib.ptr;
-        }
     }
     q.n_full = np;
     q.n = ctx->qn_n;
@@ -951,7 +976,7 @@ int wfsa_dev_create(int device, wfsa_dev** out) {
     ctx->n_cu = prop.multiProcessorCount > 0 ? prop.multiProcessorCount : kNumCu;
     if (const char* e = std::getenv("WFSA_GRAPH")) ctx->use_graph = e[0] == '1';
     if (const char* e = std::getenv("WFSA_TIMING")) ctx->kernel_timing = e[0] != '0';
-    if (const char* e = std::getenv("WFSA_BUBBLE_ATOMIC")) ctx->bubble_atomic = e[0] == '1';
+
     HIP_TRY(hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking));
     // measured: the cross-stream fork/join costs more idle time (5-20 us)
     // than the overlap saves, so the side stream is opt-in
@@ -1213,8 +1238,7 @@ int wfsa_dev_qn_setup(wfsa_dev* ctx, const wfsa_qn_desc* d) {
     hipStream_t s = ctx->stream;
     if (nf > 0) HIP_TRY(ctx->qn_trim.upload(d->trim, size_t(nf), s));
     HIP_TRY(ctx->qn_full_of.upload(full_of.data(), full_of.size(), s));
-    ctx->qn_h_full_of = full_of;
-    ctx->qn_slots_for = -1;
+
     if (n > 0) HIP_TRY(ctx->qn_ccol.upload(d->ccol, size_t(n), s));
     HIP_TRY(ctx->qn_cptr.upload(cptr.data(), cptr.size(), s));
     for (DevBuf<double>* b : {&ctx->qn_x, &ctx->qn_expx, &ctx->qn_grad}) HIP_TRY(b->alloc(size_t(std::max(n, 1))));
@@ -1272,21 +1296,6 @@ int wfsa_dev_qn_run(wfsa_dev* ctx, double eta, double tol, int32_t max_steps, do
         if (int rc = prepare(ctx, 2)) return rc;
     if (int rc = collect_timing(ctx)) return rc;
     hipStream_t s = ctx->stream;
-    if (ctx->qn_slots_for != ctx->prep_gen) {   // bubble slots re-indexed by kept parameter
-        std::vector<int32_t> sp(size_t(ctx->qn_n) + 1, 0), sl;
-        for (int32_t i = 0; i < ctx->qn_n; ++i) {
-            const int32_t j = ctx->qn_h_full_of[size_t(i)];
-            if (!ctx->h_bslot_ptr.empty())
-                sl.insert(sl.end(), ctx->h_bslot.begin() + ctx->h_bslot_ptr[size_t(j)],
-                          ctx->h_bslot.begin() + ctx->h_bslot_ptr[size_t(j) + 1]);
-            sp[size_t(i) + 1] = int32_t(sl.size());
-        }
-        if (sl.empty()) sl.push_back(0);
-        HIP_TRY(ctx->qn_slot_ptr.upload(sp.data(), sp.size(), s));
-        HIP_TRY(ctx->qn_slot.upload(sl.data(), sl.size(), s));
-        HIP_TRY(hipStreamSynchronize(s));
-        ctx->qn_slots_for = ctx->prep_gen;
-    }
     HIP_TRY(hipMemsetAsync(ctx->qn_halted.ptr, 0, sizeof(unsigned), s));
     const unsigned base = ctx->seq;
     int32_t enq = 0, done = 0, st = 0;
