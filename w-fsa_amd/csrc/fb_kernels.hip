@@ -774,11 +774,17 @@ __global__ __launch_bounds__(1024) void fbs_kernel(CompiledArgs a) {
 // re-formed into an indexed scratch load by the compiler)
 template <int N>
 __device__ __forceinline__ double reg_get(const double (&r)[N], int i) {
-    static_assert(N == 8, "register bubbles have 8 nodes");
-    const bool b0 = i & 1, b1 = i & 2, b2 = i & 4;
-    const double s0 = b0 ? r[1] : r[0], s1 = b0 ? r[3] : r[2], s2 = b0 ? r[5] : r[4], s3 = b0 ? r[7] : r[6];
-    const double t0 = b1 ? s1 : s0, t1 = b1 ? s3 : s2;
-    return b2 ? t1 : t0;
+    static_assert(N == 4 || N == 8, "register bubbles have 4 or 8 nodes");
+    const bool b0 = i & 1, b1 = i & 2;
+    const double s0 = b0 ? r[1] : r[0], s1 = b0 ? r[3] : r[2];
+    const double t0 = b1 ? s1 : s0;
+    if constexpr (N == 4) {
+        return t0;
+    } else {
+        const double s2 = b0 ? r[5] : r[4], s3 = b0 ? r[7] : r[6];
+        const double t1 = b1 ? s3 : s2;
+        return (i & 4) ? t1 : t0;
+    }
 }
 template <int N>
 __device__ __forceinline__ void reg_add(double (&r)[N], int i, double v) {
@@ -786,11 +792,14 @@ __device__ __forceinline__ void reg_add(double (&r)[N], int i, double v) {
     for (int k = 0; k < N; ++k) r[k] = i == k ? r[k] + v : r[k];
 }
 
-__device__ __forceinline__ double small_bubble(const BubbleArgs& a, int b) {
-    constexpr int RE = kBubbleRegEdges, N = kBubbleRegNodes;
-    int4 q[kSmallBubbleQuads];
+// A small bubble of class (N nodes, RE edges): quads of bubble b at
+// tbl[k * n + b] -- [header], RE/2 x [(code, sd) x 2], RE/4 x [slot x 4].
+template <int N, int RE>
+__device__ __forceinline__ double small_bubble(const BubbleArgs& a, const int4* __restrict__ tbl, int n, int b) {
+    constexpr int NQ = 1 + RE / 2 + RE / 4;
+    int4 q[NQ];
 #pragma unroll
-    for (int k = 0; k < kSmallBubbleQuads; ++k) q[k] = a.sm_tbl[size_t(k) * size_t(a.n_small) + size_t(b)];
+    for (int k = 0; k < NQ; ++k) q[k] = tbl[size_t(k) * size_t(n) + size_t(b)];
     const int nodes = q[0].x & 0xffff, edges = q[0].x >> 16;
     const double p = __longlong_as_double((long long)(uint32_t(q[0].z)) | ((long long)(uint32_t(q[0].w)) << 32));
     int code[RE], sd[RE], slot[RE];
@@ -803,10 +812,10 @@ __device__ __forceinline__ double small_bubble(const BubbleArgs& a, int b) {
     }
 #pragma unroll
     for (int k = 0; k < RE / 4; ++k) {
-        slot[4 * k] = q[5 + k].x;
-        slot[4 * k + 1] = q[5 + k].y;
-        slot[4 * k + 2] = q[5 + k].z;
-        slot[4 * k + 3] = q[5 + k].w;
+        slot[4 * k] = q[1 + RE / 2 + k].x;
+        slot[4 * k + 1] = q[1 + RE / 2 + k].y;
+        slot[4 * k + 2] = q[1 + RE / 2 + k].z;
+        slot[4 * k + 3] = q[1 + RE / 2 + k].w;
     }
     double ew[RE];
 #pragma unroll
@@ -904,8 +913,10 @@ __global__ __launch_bounds__(kBubbleBlock) void bubble_kernel(BubbleArgs a) {
     if (gw < a.n_big) {
         ll_acc = big_bubble(a, gw, lsd[wib], lw[wib], lv[wib], lab[wib]);
     } else {
+        // class A (4 nodes / 4 edges: most bubbles) first, then class B
         const int b = (gw - a.n_big) * kWave + lane;
-        if (b < a.n_small) ll_acc = small_bubble(a, b);
+        if (b < a.n_small4) ll_acc = small_bubble<4, 4>(a, a.sm4_tbl, a.n_small4, b);
+        else if (b < a.n_small4 + a.n_small) ll_acc = small_bubble<8, 8>(a, a.sm_tbl, a.n_small, b - a.n_small4);
     }
     ll_acc = wave_sum(ll_acc);
     if (lane == 0) a.ll_part[gw] = ll_acc;
@@ -1111,7 +1122,7 @@ hipError_t launch_compiled(const CompiledArgs& a, int grid, int block, size_t ld
 int bubble_waves(int32_t n_small, int32_t n_big) { return n_big + (n_small + kWave - 1) / kWave; }
 
 hipError_t launch_bubbles(const BubbleArgs& a, hipStream_t stream) {
-    const int waves = bubble_waves(a.n_small, a.n_big);
+    const int waves = bubble_waves(a.n_small4 + a.n_small, a.n_big);
     if (waves <= 0) return hipSuccess;
     constexpr int WPB = kBubbleBlock / kWave;
     hipLaunchKernelGGL(bubble_kernel, dim3(unsigned((waves + WPB - 1) / WPB)), dim3(kBubbleBlock), 0, stream, a);

@@ -185,19 +185,22 @@ struct CompiledArgs {
 // their slots in `contrib`, which is parameter-major: parameter j owns the
 // contiguous range [slot_ptr[j], slot_ptr[j+1]) -- the tail kernel then sums
 // contiguous runs, no gather.
-//   small bubbles (<= kBubbleRegEdges edges, <= kBubbleRegNodes nodes, every
-//     edge with at most one parameter): a structure-of-arrays table of
-//     kSmallBubbleQuads 16-byte quads per bubble -- quad k of bubble b at
-//     sm_tbl[k * n_small + b]: [header: nodes | edges << 16, string, p (2
-//     words)], 4 x [(code, src | dst << 16) x 2], 2 x [slot x 4] (-1: the
-//     edge has no parameter) -- one lane per bubble, coalesced loads.
+//   small bubbles (every edge with at most one parameter) in two classes,
+//     A: <= 4 nodes and edges, B: <= kBubbleRegNodes nodes, <= kBubbleRegEdges
+//     edges; each a structure-of-arrays table of 16-byte quads -- quad k of
+//     bubble b at tbl[k * n + b]: [header: nodes | edges << 16, string, p (2
+//     words)], RE/2 x [(code, src | dst << 16) x 2], RE/4 x [slot x 4] (-1:
+//     the edge has no parameter) -- one lane per bubble, coalesced loads.
 //   big bubbles (the rest, rare): variable records in `bub` at big_off[i]
 //     (bubble record layout above), one wavefront per bubble; the slots of
 //     edge e of big bubble i are big_eslot[big_eslot_ptr[big_edge_base[i] + e] ..].
 constexpr int kSmallBubbleQuads = 7;
+constexpr int kSmallBubbleQuads4 = 4;   // class A: <= 4 nodes, <= 4 edges (1 + 2 + 1 quads)
 struct BubbleArgs {
     ModelView m;
-    const int4* sm_tbl;
+    const int4* sm4_tbl;     // class A table (most bubbles: diamonds)
+    int32_t n_small4;
+    const int4* sm_tbl;      // class B table (<= 8 nodes, <= 8 edges)
     int32_t n_small;
     const int32_t* bub;
     const int32_t* big_off;

@@ -160,9 +160,9 @@ struct wfsa_dev {
     size_t i_lds = 0;
     DevBuf<double> fixed_grad;       // [n_params] gradient of the trivial words (constant)
     // bubbles
-    int32_t n_bubbles = 0, n_small = 0, n_big = 0;
+    int32_t n_bubbles = 0, n_small4 = 0, n_small = 0, n_big = 0;
     int b_waves = 0;
-    DevBuf<int4> sm_tbl;
+    DevBuf<int4> sm4_tbl, sm_tbl;
     DevBuf<int32_t> big_off, big_edge_base, big_eslot_ptr, big_eslot;
     int32_t n_bg_chunks = 0;
     DevBuf<int32_t> bub_off, bg_chunk_param, bg_chunk_ptr;
@@ -565,7 +565,7 @@ int prepare(wfsa_dev* ctx, int level) {
     // parameter-major contribution array, and runs of at most
     // kBubbleGradChunk slots of one parameter form the tail's chunks
     ctx->n_bubbles = int32_t(nbub);
-    ctx->n_small = ctx->n_big = 0;
+    ctx->n_small4 = ctx->n_small = ctx->n_big = 0;
     if (nbub > 0) {
         std::vector<int32_t> h_bubbuf(static_cast<size_t>(bwords)), h_off(static_cast<size_t>(nbub));
         HIP_TRY(ctx->bub.download(h_bubbuf.data(), size_t(bwords), s));
@@ -582,13 +582,13 @@ int prepare(wfsa_dev* ctx, int level) {
                 for (int32_t q = ctx->h_pptr[size_t(g)]; q < ctx->h_pptr[size_t(g) + 1]; ++q) f(ctx->h_pidx[size_t(q)]);
             }
         };
-        std::vector<int32_t> small, big;
+        std::vector<int32_t> small4, small, big;
         for (int32_t o : h_off) {
             const int hdr = h_bubbuf[size_t(o)];
             const int nodes = hdr & 0xffff, edges = hdr >> 16;
             bool sm = edges <= wfsa::kBubbleRegEdges && nodes <= wfsa::kBubbleRegNodes;
             for (int e = 0; sm && e < edges; ++e) sm = edge_code_at(o, e) >= 0;
-            (sm ? small : big).push_back(o);
+            (!sm ? big : (edges <= 4 && nodes <= 4 ? small4 : small)).push_back(o);
         }
         if (std::getenv("WFSA_DEBUG_BUBBLES")) {   // size histogram (diagnostics)
             std::vector<int64_t> he(size_t(wfsa::kMaxBubbleEdges) + 1, 0), hn(size_t(wfsa::kMaxBubbleNodes) + 1, 0);
@@ -596,7 +596,8 @@ int prepare(wfsa_dev* ctx, int level) {
                 he[size_t(h_bubbuf[size_t(o)] >> 16)]++;
                 hn[size_t(h_bubbuf[size_t(o)] & 0xffff)]++;
             }
-            std::fprintf(stderr, "bubbles %lld (small %zu, big %zu); by edges:", (long long)nbub, small.size(), big.size());
+            std::fprintf(stderr, "bubbles %lld (small %zu + %zu, big %zu); by edges:", (long long)nbub, small4.size(),
+                         small.size(), big.size());
             for (size_t e = 0; e < he.size(); ++e)
                 if (he[e]) std::fprintf(stderr, " %zu:%lld", e, (long long)he[e]);
             std::fprintf(stderr, "\nby nodes:");
@@ -606,32 +607,39 @@ int prepare(wfsa_dev* ctx, int level) {
         }
         // slots, parameter-major; within a parameter: small bubbles, then big
         std::vector<int32_t> pc(size_t(np) + 1, 0);
-        for (const auto* list : {&small, &big})
+        for (const auto* list : {&small4, &small, &big})
             for (int32_t o : *list)
                 for (int e = 0; e < (h_bubbuf[size_t(o)] >> 16); ++e)
                     for_edge_params(edge_code_at(o, e), [&](int32_t jj) { pc[size_t(jj) + 1]++; });
         for (size_t jj = 1; jj < pc.size(); ++jj) pc[jj] += pc[jj - 1];
         std::vector<int32_t> fill(pc.begin(), pc.end() - 1);
-        const int64_t ns = int64_t(small.size()), nb = int64_t(big.size());
-        constexpr int Q = wfsa::kSmallBubbleQuads;
-        std::vector<int32_t> tbl(size_t(Q) * 4 * size_t(std::max<int64_t>(ns, 1)), 0);
-        auto quad = [&](int k, int64_t b) { return &tbl[(size_t(k) * size_t(ns) + size_t(b)) * 4]; };
-        for (int64_t b = 0; b < ns; ++b) {
-            const int32_t o = small[size_t(b)];
-            const int edges = h_bubbuf[size_t(o)] >> 16;
-            for (int w = 0; w < 4; ++w) quad(0, b)[w] = h_bubbuf[size_t(o) + size_t(w)];
-            for (int e = 0; e < wfsa::kBubbleRegEdges; ++e) {
-                int32_t code = np, sd = 0, sl = -1;   // padding edges: the zero-slot code
-                if (e < edges) {
-                    code = edge_code_at(o, e);
-                    sd = h_bubbuf[size_t(o) + 5 + 2 * size_t(e)];
-                    if (code < np) sl = fill[size_t(code)]++;
+        const int64_t nb = int64_t(big.size());
+        // class tables: RE edges, quads = 1 + RE/2 + RE/4
+        auto build_table = [&](const std::vector<int32_t>& list, int RE, std::vector<int32_t>& tbl) {
+            const int Q = 1 + RE / 2 + RE / 4;
+            const size_t n = list.size();
+            tbl.assign(size_t(Q) * 4 * std::max<size_t>(n, 1), 0);
+            auto quad = [&](int k, size_t b) { return &tbl[(size_t(k) * n + b) * 4]; };
+            for (size_t b = 0; b < n; ++b) {
+                const int32_t o = list[b];
+                const int edges = h_bubbuf[size_t(o)] >> 16;
+                for (int w = 0; w < 4; ++w) quad(0, b)[w] = h_bubbuf[size_t(o) + size_t(w)];
+                for (int e = 0; e < RE; ++e) {
+                    int32_t code = np, sd = 0, sl = -1;   // padding edges: the zero-slot code
+                    if (e < edges) {
+                        code = edge_code_at(o, e);
+                        sd = h_bubbuf[size_t(o) + 5 + 2 * size_t(e)];
+                        if (code < np) sl = fill[size_t(code)]++;
+                    }
+                    quad(1 + e / 2, b)[2 * (e & 1)] = code;
+                    quad(1 + e / 2, b)[2 * (e & 1) + 1] = sd;
+                    quad(1 + RE / 2 + e / 4, b)[e & 3] = sl;
                 }
-                quad(1 + e / 2, b)[2 * (e & 1)] = code;
-                quad(1 + e / 2, b)[2 * (e & 1) + 1] = sd;
-                quad(5 + e / 4, b)[e & 3] = sl;
             }
-        }
+        };
+        std::vector<int32_t> tbl4, tbl;
+        build_table(small4, 4, tbl4);
+        build_table(small, wfsa::kBubbleRegEdges, tbl);
         std::vector<int32_t> big_edge_base(size_t(std::max<int64_t>(nb, 1)), 0), eslot_ptr(1, 0), eslot;
         for (int64_t i = 0; i < nb; ++i) {
             const int32_t o = big[size_t(i)];
@@ -642,12 +650,14 @@ int prepare(wfsa_dev* ctx, int level) {
             }
         }
         if (eslot.empty()) eslot.push_back(0);
+        HIP_TRY(ctx->sm4_tbl.upload(reinterpret_cast<const int4*>(tbl4.data()), tbl4.size() / 4, s));
         HIP_TRY(ctx->sm_tbl.upload(reinterpret_cast<const int4*>(tbl.data()), tbl.size() / 4, s));
         HIP_TRY(ctx->big_off.upload(big.empty() ? h_off.data() : big.data(), std::max<size_t>(big.size(), 1), s));
         HIP_TRY(ctx->big_edge_base.upload(big_edge_base.data(), big_edge_base.size(), s));
         HIP_TRY(ctx->big_eslot_ptr.upload(eslot_ptr.data(), eslot_ptr.size(), s));
         HIP_TRY(ctx->big_eslot.upload(eslot.data(), eslot.size(), s));
-        ctx->n_small = int32_t(ns);
+        ctx->n_small4 = int32_t(small4.size());
+        ctx->n_small = int32_t(small.size());
         ctx->n_big = int32_t(nb);
         std::vector<int32_t> cparam, cptr;
         for (int32_t jj = 0; jj < np; ++jj)
@@ -661,7 +671,7 @@ int prepare(wfsa_dev* ctx, int level) {
         HIP_TRY(ctx->bg_chunk_ptr.upload(cptr.data(), cptr.size(), s));
         HIP_TRY(ctx->contrib.alloc(size_t(std::max(pc.back(), 1))));
         HIP_TRY(hipMemsetAsync(ctx->contrib.ptr, 0, size_t(std::max(pc.back(), 1)) * sizeof(double), s));
-        ctx->b_waves = wfsa::bubble_waves(ctx->n_small, ctx->n_big);
+        ctx->b_waves = wfsa::bubble_waves(ctx->n_small4 + ctx->n_small, ctx->n_big);
         HIP_TRY(hipStreamSynchronize(s));
     } else {
         ctx->b_waves = 0;
@@ -803,6 +813,8 @@ int enqueue_compiled(wfsa_dev* ctx, bool with_grad, bool want_logq, const unsign
 int enqueue_bubbles(wfsa_dev* ctx, bool want_logq, const unsigned* halted, int32_t wave_off, hipStream_t s) {
     wfsa::BubbleArgs b{};
     b.m = model_view(ctx);
+    b.sm4_tbl = ctx->sm4_tbl.ptr;
+    b.n_small4 = ctx->n_small4;
     b.sm_tbl = ctx->sm_tbl.ptr;
     b.n_small = ctx->n_small;
     b.bub = ctx->bub.ptr;
