@@ -30,6 +30,7 @@
 //   log q = sum_trivial lw_e + sum_bubbles log Z_seg.
 // fbc_kernel evaluates these streams every iteration, one lane per string.
 #include "fb_kernels.hpp"
+#include "qn_device.hpp"
 
 #include <hip/hip_runtime.h>
 
@@ -619,10 +620,10 @@ __global__ __launch_bounds__(1024) void fbc_kernel(CompiledArgs a) {
 // Prologue of the per-iteration stream kernel (no other kernel runs before
 // it): this block's slice of the per-edge weights (bubbles and the traversal
 // fallback read them after this launch) and, by block 0, the zeroed result.
-__device__ __forceinline__ void edge_weight_slice(const CompiledArgs& a) {
-    const int64_t per = (a.n_comb + gridDim.x - 1) / gridDim.x;
-    const int64_t e_end = min(a.n_comb, per * int64_t(blockIdx.x + 1));
-    for (int64_t g = per * int64_t(blockIdx.x) + threadIdx.x; g < e_end; g += blockDim.x) {
+__device__ __forceinline__ void edge_weight_slice(const CompiledArgs& a, int bid, int nblk) {
+    const int64_t per = (a.n_comb + nblk - 1) / nblk;
+    const int64_t e_end = min(a.n_comb, per * int64_t(bid + 1));
+    for (int64_t g = per * int64_t(bid) + threadIdx.x; g < e_end; g += blockDim.x) {
         const int32_t b = a.m.pptr[g], e = a.m.pptr[g + 1];
         double sum = 0.0;
         for (int32_t k = b; k < e; ++k) sum += a.w[a.m.pidx[k]];
@@ -630,7 +631,7 @@ __device__ __forceinline__ void edge_weight_slice(const CompiledArgs& a) {
         a.ew_out[g] = exp(sum);
         a.erec_out[g] = EdgeRec{sum, e > b ? a.m.pidx[b] : 0, e - b};
     }
-    if (blockIdx.x == 0)
+    if (bid == 0)
         for (int j = int(threadIdx.x); j <= a.n_params; j += int(blockDim.x)) a.out[j] = 0.0;
 }
 
@@ -646,13 +647,19 @@ __device__ __forceinline__ void edge_weight_slice(const CompiledArgs& a) {
 // stream pass at all, 4 neither stream pass nor table staging, 5 return at once
 template <bool WIDE, bool W_LDS, bool MULTI, int DBG = 0>
 __global__ __launch_bounds__(1024) void fbs_kernel(CompiledArgs a) {
+    if (a.fin_on && blockIdx.x == 0) {   // the previous QN step's finish (dispatched first)
+        qn_finish_block(a.fin);
+        return;
+    }
+    const int bid = int(blockIdx.x) - (a.fin_on ? 1 : 0);   // this block among the stream blocks
     if (a.halted && *a.halted) return;
     if (DBG == 5) return;
     extern __shared__ __attribute__((aligned(16))) double lds[];
     const int lane = lane_id();
     const int wpb = int(blockDim.x) / kWave;
-    const int gw = __builtin_amdgcn_readfirstlane(int(blockIdx.x) * wpb + int(threadIdx.x) / kWave);
-    const int nw = int(gridDim.x) * wpb;
+    const int gw = __builtin_amdgcn_readfirstlane(bid * wpb + int(threadIdx.x) / kWave);
+    const int nblk = int(gridDim.x) - (a.fin_on ? 1 : 0);   // (the finish block takes no share)
+    const int nw = nblk * wpb;
     const uint32_t zslot = uint32_t(a.n_params);
     if (W_LDS && DBG != 4) {
         // stage w[0, n_params] in 16-byte pieces, all of a thread's loads
@@ -757,7 +764,7 @@ __global__ __launch_bounds__(1024) void fbs_kernel(CompiledArgs a) {
     if (lane == 0) a.ll_part[gw] = ll_acc;
     // this block's slice of the per-edge weights and the zeroed result, for
     // the kernels after this one (nothing in this launch reads them)
-    if (W_LDS) edge_weight_slice(a);
+    if (W_LDS) edge_weight_slice(a, bid, nblk);
 }
 
 // Bubbles.  Local forward from the bubble's first cut, local backward from
@@ -1043,8 +1050,12 @@ hipError_t configure_kernels(int max_dynamic_lds) {
                          reinterpret_cast<const void*>(&fbs_kernel<false, true, false, 3>),
                          reinterpret_cast<const void*>(&fbs_kernel<false, true, false, 4>),
                          reinterpret_cast<const void*>(&fbs_kernel<false, true, false, 5>)};
-    for (const void* f : fns) {
-        hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, max_dynamic_lds);
+    for (const void* f : fns) {   // (static LDS counts against the same 160 KiB)
+        hipFuncAttributes attr{};
+        hipError_t e = hipFuncGetAttributes(&attr, f);
+        if (e != hipSuccess) return e;
+        e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                max_dynamic_lds - int(attr.sharedSizeBytes));
         if (e != hipSuccess) return e;
     }
     return hipSuccess;
@@ -1068,7 +1079,7 @@ hipError_t launch_trav(TravMode mode, const TravArgs& a, int grid, hipStream_t s
 }
 
 hipError_t launch_compiled(const CompiledArgs& a, int grid, int block, size_t lds, hipStream_t stream) {
-    const dim3 g{unsigned(grid), 1, 1}, b{unsigned(block), 1, 1};
+    const dim3 g{unsigned(grid + (a.fin_on && !a.with_grad ? 1 : 0)), 1, 1}, b{unsigned(block), 1, 1};
     if (!a.with_grad) {   // per-iteration form: w staged in LDS or read from global
         static const int dbg = [] {
             const char* e = std::getenv("WFSA_FBS_DBG");

@@ -137,6 +137,46 @@ struct TravArgs {
     const unsigned* halted;  // device-resident QN run: nonzero = skip (or null)
 };
 
+// Device-resident QuasiNewton step (qn_kernel.hip): qn_update (wavefront per
+// constraint) updates x and lambda from out = [LL, grad_full] and writes the
+// next w_full; the finish (qn_finish_block, qn_device.hpp) reduces the info
+// row [KL, graderr, g_min, g_max, lambda_min, 0, 0, status] into a
+// host-mapped ring slot and bumps the completion flag.  The finish of step k
+// runs in an extra block of step k+1's stream kernel (or a trailing kernel).
+constexpr int kQnRow = 8;
+constexpr unsigned kQnRan = 0, kQnHalted = 1, kQnNonFinite = 2, kQnSkipped = 3;
+struct QnArgs {
+    const double* out;           // [1 + n_full]
+    // without a communicator the tail kernel is skipped: the gradient is
+    // out[1+j] + fixed[j] (bubble/fallback atomics + the constant trivial
+    // part) and the log-likelihood the sum of ll_part[0, n_ll); else (null)
+    // out is final
+    const double* fixed;
+    const double* ll_part;
+    int32_t n_ll;
+    int32_t n_full, n, k;
+    const int32_t* full_of;      // [n] full index of each kept parameter
+    const int32_t* trim;         // [n_full] trimmed index / -1 / -2
+    const int32_t* ccol;         // [n] constraint of each parameter
+    const int32_t* cptr;         // [k+1] constraint c owns parameters [cptr[c], cptr[c+1])
+    double* x;
+    double* lambda;
+    double* expx;
+    double* grad;
+    double* w_full;              // [n_full + 1] (zero slot)
+    double* ewp;                 // [n_full + 1] exp(w_full), for the bubble kernel
+    double* partial;             // [qn_update_blocks(k)][4]
+    int32_t n_partial;
+    double* ll_val;              // with the tail: out[0] (LL) copied by qn_update for the finish
+    double plogp, eta, tol;
+    int32_t exp_lambda;
+    int32_t ring_slot;           // ring slot of this step
+    unsigned* halted;            // device: nonzero after a halting step
+    unsigned* seq;               // device sequence counter
+    unsigned* host_flag;         // host-mapped completion flag
+    double* host_ring;           // host-mapped [slots][kQnRow]
+};
+
 // Compiled streams of the per-iteration kernels.
 //   main stream: only "trivial" words (edges whose posterior is 1).  Narrow
 //     (16-bit) words: j < 0x8000 a single-parameter edge with parameter j,
@@ -164,6 +204,9 @@ struct CompiledArgs {
                              // else: >= 1 w staged in LDS, 0 global
     int32_t wide;
     int32_t with_grad;       // accumulate the (weight-independent) trivial-word gradient
+    // device-resident QN: the extra last block finishes the previous step
+    QnArgs fin;
+    int32_t fin_on;
     int32_t multi;           // the automaton has multi-parameter (epsilon-composite) edges
     const double* w;         // [n_params] w_full (GetWeight form)
     double* grad;            // [n_params] (TABLES == 0: atomics straight into it)
@@ -276,44 +319,9 @@ hipError_t launch_publish(const double* out, const Publish& pub, hipStream_t str
 // ewp = exp(w) (all buffers padded to an even count)
 hipError_t launch_stage(const double* host_w, double* w, double* ewp, int32_t n, hipStream_t stream);
 // also zeroes out[0..n_out) (the accumulators of this iteration)
-// Device-resident QuasiNewton step (qn_kernel.hip): one workgroup updates x
-// and lambda from out = [LL, grad_full] and writes the next w_full; its info
-// row [KL, graderr, g_min, g_max, lambda_min, 0, 0, status] goes to a
-// host-mapped ring slot, then the completion flag is bumped.
-constexpr int kQnRow = 8;
-constexpr unsigned kQnRan = 0, kQnHalted = 1, kQnNonFinite = 2, kQnSkipped = 3;
-struct QnArgs {
-    const double* out;           // [1 + n_full]
-    // without a communicator the tail kernel is skipped: the gradient is
-    // out[1+j] + fixed[j] (bubble/fallback atomics + the constant trivial
-    // part) and the log-likelihood the sum of ll_part[0, n_ll); else (null)
-    // out is final
-    const double* fixed;
-    const double* ll_part;
-    int32_t n_ll;
-    int32_t n_full, n, k;
-    const int32_t* full_of;      // [n] full index of each kept parameter
-    const int32_t* trim;         // [n_full] trimmed index / -1 / -2
-    const int32_t* ccol;         // [n] constraint of each parameter
-    const int32_t* cptr;         // [k+1] constraint c owns parameters [cptr[c], cptr[c+1])
-    double* x;
-    double* lambda;
-    double* expx;
-    double* grad;
-    double* w_full;              // [n_full + 1] (zero slot)
-    double* ewp;                 // [n_full + 1] exp(w_full), for the bubble kernel
-    double* partial;             // [qn_update_blocks(k)][4]
-    int32_t n_partial;
-    double plogp, eta, tol;
-    int32_t exp_lambda;
-    int32_t ring_slot;           // ring slot of this step
-    unsigned* halted;            // device: nonzero after a halting step
-    unsigned* seq;               // device sequence counter
-    unsigned* host_flag;         // host-mapped completion flag
-    double* host_ring;           // host-mapped [slots][kQnRow]
-};
 int qn_update_blocks(int32_t k);
-hipError_t launch_qn(const QnArgs& a, hipStream_t stream);
+hipError_t launch_qn_update(const QnArgs& a, hipStream_t stream);
+hipError_t launch_qn_finish(const QnArgs& a, hipStream_t stream);
 hipError_t launch_qn_weights(const double* x, const int32_t* trim, int32_t n_full, double* w_full, double* ewp,
                              hipStream_t stream);
 hipError_t launch_edge_weights(const double* w_full, const int32_t* pptr, const int32_t* pidx, double* lw,

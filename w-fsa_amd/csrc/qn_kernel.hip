@@ -11,6 +11,7 @@
 // summation orders, no FMA contraction) so the device and host trajectories
 // agree to the last bits up to exp()'s rounding.
 #include "fb_kernels.hpp"
+#include "qn_device.hpp"
 
 #include <hip/hip_runtime.h>
 
@@ -26,39 +27,6 @@ namespace {
 
 constexpr int kQnUpdateBlock = 256;   // four constraints (one wavefront each) per block
 constexpr int kQnFinishBlock = 1024;
-
-__device__ double block_reduce(double v, int op, double* red) {   // op 0 min, 1 max
-    for (int o = 32; o > 0; o >>= 1) {
-        const double t = __shfl_xor(v, o, 64);
-        v = op == 0 ? fmin(v, t) : fmax(v, t);
-    }
-    const int w = int(threadIdx.x) / 64, lane = int(threadIdx.x) & 63;
-    __syncthreads();
-    if (lane == 0) red[w] = v;
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        double r = red[0];
-        for (int i = 1; i < int(blockDim.x) / 64; ++i) r = op == 0 ? fmin(r, red[i]) : fmax(r, red[i]);
-        red[32] = r;
-    }
-    __syncthreads();
-    return red[32];
-}
-
-__device__ double block_sum(double v, double* red) {   // fixed order for a fixed block size
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-    const int w = int(threadIdx.x) / 64, lane = int(threadIdx.x) & 63;
-    __syncthreads();
-    if (lane == 0) red[w] = v;
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        double r = red[0];
-        for (int i = 1; i < int(blockDim.x) / 64; ++i) r += red[i];
-        red[32] = r;
-    }
-    __syncthreads();
-    return red[32];
-}
 
 __device__ __forceinline__ void wave_sync() {
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
@@ -160,6 +128,7 @@ __global__ __launch_bounds__(kQnUpdateBlock) void qn_update_kernel(QnArgs a) {
     }
     __syncthreads();
     if (threadIdx.x == 0) {
+        if (blockIdx.x == 0 && !a.ll_part) *a.ll_val = a.out[0];   // the finish may run after out is reused
         double r0 = red[0][0], r1 = red[0][1], r2 = red[0][2], r3 = red[0][3];
         for (int v = 1; v < W; ++v) {
             r0 = fmin(r0, red[v][0]);
@@ -178,52 +147,7 @@ __global__ __launch_bounds__(kQnUpdateBlock) void qn_update_kernel(QnArgs a) {
 // qn_finish: the info row of the step (the reductions of qn_update's
 // partials and, without the tail kernel, of the per-wave log-likelihood
 // partials in a fixed order), the halt decision, then the publication.
-__global__ __launch_bounds__(kQnFinishBlock) void qn_finish_kernel(QnArgs a) {
-    __shared__ double red[33];
-    const unsigned state = *a.halted;
-    const int t = int(threadIdx.x), nt = int(blockDim.x);
-    double gmin = INFINITY, gmax = -INFINITY, lmin = INFINITY, gerr = 0.0, ll = 0.0;
-    if (state == 0) {
-        for (int b = t; b < a.n_partial; b += nt) {
-            const double* p = a.partial + size_t(b) * 4;
-            gmin = fmin(gmin, p[0]);
-            gmax = fmax(gmax, p[1]);
-            lmin = fmin(lmin, p[2]);
-            gerr = fmax(gerr, p[3]);
-        }
-        if (a.ll_part)
-            ll = strided_sum(a.ll_part, a.n_ll, t, nt);
-    }
-    gmin = block_reduce(gmin, 0, red);
-    gmax = block_reduce(gmax, 1, red);
-    lmin = block_reduce(lmin, 0, red);
-    gerr = block_reduce(gerr, 1, red);
-    ll = block_sum(ll, red);
-    if (t == 0) {
-        unsigned status = kQnSkipped;
-        double info[7] = {0, 0, 0, 0, 0, 0, 0};
-        if (state == 0) {
-            if (a.k == 0) gmin = gmax = lmin = 0.0;
-            info[0] = a.plogp - (a.ll_part ? ll : a.out[0]);
-            info[1] = gerr;
-            info[2] = gmin;
-            info[3] = gmax;
-            info[4] = lmin;
-            bool finite = true;
-            for (int i = 0; i < 7; ++i) finite = finite && isfinite(info[i]);
-            const bool halt = gerr <= a.tol && fabs(gmin) <= a.tol && fabs(gmax) <= a.tol;
-            status = !finite ? kQnNonFinite : (halt ? kQnHalted : kQnRan);
-        }
-        double* row = a.host_ring + size_t(a.ring_slot) * kQnRow;
-        for (int i = 0; i < 7; ++i) row[i] = info[i];
-        row[7] = double(status);
-        if (status == kQnHalted || status == kQnNonFinite) *a.halted = status;
-        const unsigned v = *a.seq + 1u;
-        *a.seq = v;
-        // the system-scope release orders the row before the flag
-        __hip_atomic_store(a.host_flag, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-    }
-}
+__global__ __launch_bounds__(kQnFinishBlock) void qn_finish_kernel(QnArgs a) { qn_finish_block(a); }
 
 // initial w_full from x (qn_set_state)
 __global__ void qn_weights_kernel(const double* x, const int32_t* trim, int32_t n_full, double* w_full, double* ewp) {
@@ -246,8 +170,12 @@ int qn_update_blocks(int32_t k) {
     return std::max(1, (k + W - 1) / W);
 }
 
-hipError_t launch_qn(const QnArgs& a, hipStream_t stream) {
+hipError_t launch_qn_update(const QnArgs& a, hipStream_t stream) {
     hipLaunchKernelGGL(qn_update_kernel, dim3(unsigned(qn_update_blocks(a.k))), dim3(kQnUpdateBlock), 0, stream, a);
+    return hipGetLastError();
+}
+
+hipError_t launch_qn_finish(const QnArgs& a, hipStream_t stream) {
     hipLaunchKernelGGL(qn_finish_kernel, dim3(1), dim3(kQnFinishBlock), 0, stream, a);
     return hipGetLastError();
 }

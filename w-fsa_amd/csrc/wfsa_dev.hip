@@ -178,6 +178,8 @@ struct wfsa_dev {
 
     // work buffers
     DevBuf<double> w_full, ewp, out, ll_part, logq;
+    double* ll_cur = nullptr;      // this launch sequence's half of ll_part (QN steps alternate)
+    size_t ll_stride = 0;
     DevBuf<unsigned long long> live;
     double* pinned = nullptr;   // [0, n_params+1): results; from weights_off(n_params): weights
     double* pinned_dev = nullptr;   // the same memory as the device addresses it
@@ -325,7 +327,7 @@ int configure_tiers(wfsa_dev* ctx) {
 void drop_graph(wfsa_dev* ctx);
 
 int enqueue_compiled(wfsa_dev* ctx, bool with_grad, bool want_logq, const unsigned* halted = nullptr,
-                     int slot = -1);
+                     int slot = -1, const wfsa::QnArgs* fin = nullptr);
 
 // per-kernel timing events of slot `slot` (< 0: this launch is not timed;
 // WFSA_TIMING=0 leaves them all out).  An event between two kernels costs a
@@ -720,7 +722,11 @@ int prepare(wfsa_dev* ctx, int level) {
                          size_t(ctx->b_waves) +
                          size_t(ctx->fall_grid[0]) * size_t(ctx->cfg[0].waves_per_block) +
                          size_t(ctx->fall_grid[1]) * size_t(ctx->cfg[1].waves_per_block);
-    HIP_TRY(ctx->ll_part.alloc(waves));
+    // two halves: a device-resident QN step's finish reads its partials
+    // while the next step writes the other half
+    HIP_TRY(ctx->ll_part.alloc(2 * waves));
+    ctx->ll_stride = waves;
+    ctx->ll_cur = ctx->ll_part.ptr;
     HIP_TRY(hipStreamSynchronize(s));
 
     // the trivial words' gradient, once: compiled pass with gradient at
@@ -752,7 +758,8 @@ int prepare(wfsa_dev* ctx, int level) {
 // edge-weight kernel unless the kernel folds that into its prologue (it does
 // when it stages w in LDS).  with_grad: the preparation-time gradient pass
 // (followed by its slab reduction into out); else the per-iteration pass.
-int enqueue_compiled(wfsa_dev* ctx, bool with_grad, bool want_logq, const unsigned* halted, int slot) {
+int enqueue_compiled(wfsa_dev* ctx, bool with_grad, bool want_logq, const unsigned* halted, int slot,
+                     const wfsa::QnArgs* fin) {
     hipStream_t s = ctx->stream;
     const int32_t np = ctx->n_params;
     const int tables = with_grad ? ctx->c_tables : ctx->i_tables;
@@ -785,9 +792,13 @@ int enqueue_compiled(wfsa_dev* ctx, bool with_grad, bool want_logq, const unsign
         c.ew_out = ctx->ew.ptr;
         c.erec_out = ctx->erec.ptr;
         c.out = ctx->out.ptr;
-        c.ll_part = ctx->ll_part.ptr;
+        c.ll_part = ctx->ll_cur;
         c.logq = want_logq ? ctx->logq.ptr : nullptr;
         c.halted = halted;
+        if (fin && !with_grad && tables >= 1) {
+            c.fin = *fin;
+            c.fin_on = 1;
+        }
         if (with_grad) HIP_TRY(wfsa::launch_compiled(c, ctx->c_grid, kCompiledBlock, ctx->c_lds, s));
         else HIP_TRY(wfsa::launch_compiled(c, ctx->i_grid, ctx->i_block, ctx->i_lds, s));
     }
@@ -797,7 +808,7 @@ int enqueue_compiled(wfsa_dev* ctx, bool with_grad, bool want_logq, const unsign
         t.gpart = ctx->gpart.ptr;
         t.n_gpart = (ctx->n_groups > 0 && ctx->c_tables >= 1) ? ctx->c_grid : 0;
         t.n_params = np;
-        t.ll_part = ctx->ll_part.ptr;
+        t.ll_part = ctx->ll_cur;
         t.n_ll = 0;
         t.out = ctx->out.ptr;
         HIP_TRY(wfsa::launch_tail(t, s));
@@ -826,7 +837,7 @@ int enqueue_bubbles(wfsa_dev* ctx, bool want_logq, const unsigned* halted, int32
     b.contrib = ctx->contrib.ptr;
     b.w = ctx->w_full.ptr;
     b.ewp = ctx->ewp.ptr;
-    b.ll_part = ctx->ll_part.ptr + wave_off;
+    b.ll_part = ctx->ll_cur + wave_off;
     b.logq = want_logq ? ctx->logq.ptr : nullptr;
     b.halted = halted;
     HIP_TRY(wfsa::launch_bubbles(b, s));
@@ -836,7 +847,7 @@ int enqueue_bubbles(wfsa_dev* ctx, bool want_logq, const unsigned* halted, int32
 // The evaluation kernels; with_tail: finish out = [LL, grad_full] with the
 // tail kernel (else the consumer adds fixed_grad and sums ll_part[0, *n_ll)).
 int enqueue_evaluation(wfsa_dev* ctx, bool want_logq, const unsigned* halted, int slot, bool with_tail = true,
-                       int32_t* n_ll = nullptr) {
+                       int32_t* n_ll = nullptr, const wfsa::QnArgs* fin = nullptr, bool* fin_done = nullptr) {
     hipStream_t s = ctx->stream;
     const int32_t np = ctx->n_params;
     // The bubble kernel reads only the weights (ewp, staged before this
@@ -854,7 +865,8 @@ int enqueue_evaluation(wfsa_dev* ctx, bool want_logq, const unsigned* halted, in
         if (int rc = enqueue_bubbles(ctx, want_logq, halted, wave_off, ctx->side_stream)) return rc;
         HIP_TRY(hipEventRecord(ctx->join, ctx->side_stream));
     }
-    if (int rc = enqueue_compiled(ctx, false, want_logq, halted, slot)) return rc;
+    if (int rc = enqueue_compiled(ctx, false, want_logq, halted, slot, fin)) return rc;
+    if (fin_done) *fin_done = fin && ctx->n_groups > 0 && ctx->i_tables >= 1;
     if (side) HIP_TRY(hipStreamWaitEvent(s, ctx->join, 0));
     if (ctx->n_bubbles > 0 && !side) {
         if (int rc = enqueue_bubbles(ctx, want_logq, halted, wave_off, s)) return rc;
@@ -866,7 +878,7 @@ int enqueue_evaluation(wfsa_dev* ctx, bool want_logq, const unsigned* halted, in
         a.list = ctx->fall[t].ptr;
         a.n_list = ctx->n_fall[t];
         a.grad = ctx->out.ptr + 1;
-        a.ll_part = ctx->ll_part.ptr + wave_off;
+        a.ll_part = ctx->ll_cur + wave_off;
         a.logq = want_logq ? ctx->logq.ptr : nullptr;
         a.halted = halted;
         HIP_TRY(wfsa::launch_trav(wfsa::MODE_WEIGHTED, a, ctx->fall_grid[t], s));
@@ -884,7 +896,7 @@ int enqueue_evaluation(wfsa_dev* ctx, bool want_logq, const unsigned* halted, in
     t.chunk_ptr = ctx->bg_chunk_ptr.ptr;
     t.contrib = ctx->contrib.ptr;
     t.n_chunks = ctx->n_bubbles > 0 ? ctx->n_bg_chunks : 0;
-    t.ll_part = ctx->ll_part.ptr;
+    t.ll_part = ctx->ll_cur;
     t.n_ll = wave_off;
     t.n_params = np;
     t.out = ctx->out.ptr;
@@ -909,22 +921,33 @@ int enqueue_iteration(wfsa_dev* ctx, bool want_logq) {
 // One device-resident QuasiNewton step: the evaluation at the device's
 // w_full, the all-reduce, the update (which writes the next w_full and
 // publishes the info row of ring slot `slot`).
-int enqueue_qn_step(wfsa_dev* ctx, double eta, double tol, int slot, bool timed) {
+// One device-resident QuasiNewton step e: the evaluation at the device's
+// w_full (its stream kernel also runs `fin`, the previous step's finish,
+// in an extra block, when given), the all-reduce, the update.  *q receives
+// this step's finish arguments: the caller folds them into the next step or
+// launches them as a trailing kernel.
+int enqueue_qn_step(wfsa_dev* ctx, double eta, double tol, int64_t e, bool timed, const wfsa::QnArgs* fin,
+                    wfsa::QnArgs* q_out) {
     hipStream_t s = ctx->stream;
     const int32_t np = ctx->n_params;
-    // without a communicator the QN kernel finishes the reduction itself
-    // (the bubble contributions need the tail's run reduction: one wave per
-    // constraint cannot absorb a hot parameter's slot range)
+    const int par = int(e & 1);
+    const int slot = int(e % kQnDepth);
+    ctx->ll_cur = ctx->ll_part.ptr + size_t(par) * ctx->ll_stride;
+    // without the tail (no bubbles, no communicator) the QN kernels add the
+    // constant gradient and sum the log-likelihood partials themselves
     const bool tail = ctx->comm != nullptr || ctx->n_bubbles > 0;
     int32_t n_ll = 0;
-    if (int rc = enqueue_evaluation(ctx, false, ctx->qn_halted.ptr, timed ? slot : -1, tail, &n_ll)) return rc;
+    bool fin_done = false;
+    if (int rc = enqueue_evaluation(ctx, false, ctx->qn_halted.ptr, timed ? slot : -1, tail, &n_ll, fin, &fin_done))
+        return rc;
+    if (fin && !fin_done) HIP_TRY(wfsa::launch_qn_finish(*fin, s));   // (no stream kernel to carry it)
     if (ctx->comm)
         RCCL_TRY(ncclAllReduce(ctx->out.ptr, ctx->out.ptr, size_t(np) + 1, ncclDouble, ncclSum, ctx->comm, s));
     wfsa::QnArgs q{};
     q.out = ctx->out.ptr;
     if (!tail) {
         q.fixed = ctx->n_groups > 0 ? ctx->fixed_grad.ptr : nullptr;
-        q.ll_part = ctx->ll_part.ptr;
+        q.ll_part = ctx->ll_cur;
         q.n_ll = n_ll;
     }
     q.n_full = np;
@@ -940,8 +963,10 @@ int enqueue_qn_step(wfsa_dev* ctx, double eta, double tol, int slot, bool timed)
     q.grad = ctx->qn_grad.ptr;
     q.w_full = ctx->w_full.ptr;
     q.ewp = ctx->ewp.ptr;
-    q.partial = ctx->qn_partial.ptr;
-    q.n_partial = wfsa::qn_update_blocks(ctx->qn_k);
+    const int nbk = wfsa::qn_update_blocks(ctx->qn_k);
+    q.partial = ctx->qn_partial.ptr + size_t(par) * size_t(nbk) * 4;
+    q.n_partial = nbk;
+    q.ll_val = ctx->qn_partial.ptr + 2 * size_t(nbk) * 4 + size_t(par);
     q.plogp = ctx->qn_plogp;
     q.eta = eta;
     q.tol = tol;
@@ -951,7 +976,8 @@ int enqueue_qn_step(wfsa_dev* ctx, double eta, double tol, int slot, bool timed)
     q.seq = ctx->counters.ptr;
     q.host_flag = ctx->flag_dev;
     q.host_ring = ctx->qn_ring_dev;
-    HIP_TRY(wfsa::launch_qn(q, s));
+    HIP_TRY(wfsa::launch_qn_update(q, s));
+    *q_out = q;
     return WFSA_OK;
 }
 
@@ -1255,7 +1281,7 @@ int wfsa_dev_qn_setup(wfsa_dev* ctx, const wfsa_qn_desc* d) {
     HIP_TRY(ctx->qn_cptr.upload(cptr.data(), cptr.size(), s));
     for (DevBuf<double>* b : {&ctx->qn_x, &ctx->qn_expx, &ctx->qn_grad}) HIP_TRY(b->alloc(size_t(std::max(n, 1))));
     HIP_TRY(ctx->qn_lambda.alloc(size_t(std::max(k, 1))));
-    HIP_TRY(ctx->qn_partial.alloc(size_t(wfsa::qn_update_blocks(k)) * 4));
+    HIP_TRY(ctx->qn_partial.alloc(2 * size_t(wfsa::qn_update_blocks(k)) * 4 + 2));   // two halves + two LL slots
     HIP_TRY(ctx->qn_halted.alloc(1));
     if (!ctx->qn_ring) {
         HIP_TRY(hipHostMalloc(reinterpret_cast<void**>(&ctx->qn_ring), sizeof(double) * kQnDepth * wfsa::kQnRow,
@@ -1314,13 +1340,31 @@ int wfsa_dev_qn_run(wfsa_dev* ctx, double eta, double tol, int32_t max_steps, do
     bool stop = false;
     double c_ms_sum = 0.0, fb_ms_sum = 0.0;
     int64_t timed = 0;
+    // step e's finish (its info row and flag) runs inside step e+1's stream
+    // kernel; the last enqueued step's finish is a trailing kernel
+    wfsa::QnArgs pending{};
+    bool has_pending = false;
+    auto flush_pending = [&]() -> int {
+        if (has_pending) {
+            HIP_TRY(wfsa::launch_qn_finish(pending, s));
+            has_pending = false;
+        }
+        return WFSA_OK;
+    };
     while (done < max_steps) {
         while (!stop && enq < max_steps && enq - done < kQnDepth) {
-            if (int rc = enqueue_qn_step(ctx, eta, tol, enq % kQnDepth, enq % kTimingStride == 0)) return rc;
+            wfsa::QnArgs q{};
+            if (int rc = enqueue_qn_step(ctx, eta, tol, enq, enq % kTimingStride == 0,
+                                         has_pending ? &pending : nullptr, &q))
+                return rc;
+            pending = q;
+            has_pending = true;
             ++enq;
             ++ctx->seq;
         }
         if (done >= enq) break;
+        if (enq == done + 1)   // nothing after step `done` carries its finish
+            if (int rc = flush_pending()) return rc;
         if (int rc = wait_published(ctx, base + unsigned(done) + 1u)) return rc;
         const int slot = done % kQnDepth;
         const double* row = ctx->qn_ring + size_t(slot) * wfsa::kQnRow;
@@ -1348,6 +1392,7 @@ int wfsa_dev_qn_run(wfsa_dev* ctx, double eta, double tol, int32_t max_steps, do
         }
     }
     // drain the steps enqueued after a halt (they are no-ops)
+    if (int rc = flush_pending()) return rc;
     if (enq > done)
         if (int rc = wait_published(ctx, base + unsigned(enq))) return rc;
     HIP_TRY(hipStreamSynchronize(s));
