@@ -635,137 +635,6 @@ __device__ __forceinline__ void edge_weight_slice(const CompiledArgs& a, int bid
         for (int j = int(threadIdx.x); j <= a.n_params; j += int(blockDim.x)) a.out[j] = 0.0;
 }
 
-// Per-iteration stream kernel: log q of every compiled string's trivial
-// words, sum_words w[j], one lane per string, no atomics (their gradient is
-// the constant added by the tail kernel).  w[n_params] is a zero slot, so a
-// padding word (0xFFFF / -1) and -- in the fast path -- a multi-parameter
-// word read 0.0 without a branch: index = min(word, n_params).  Chunks that
-// hold multi-parameter words (MULTI, automata with epsilon composites) take
-// a second, per-word pass.  Loads are unconditional up to the group's
-// longest lane (shorter lanes read their padding chunks), D chunks in flight.
-// DBG (timing experiments only, WFSA_FBS_DBG): 1 no table gathers, 3 no
-// stream pass at all, 4 neither stream pass nor table staging, 5 return at once
-template <bool WIDE, bool W_LDS, bool MULTI, int DBG = 0>
-__global__ __launch_bounds__(1024) void fbs_kernel(CompiledArgs a) {
-    if (a.fin_on && blockIdx.x == 0) {   // the previous QN step's finish (dispatched first)
-        qn_finish_block(a.fin);
-        return;
-    }
-    const int bid = int(blockIdx.x) - (a.fin_on ? 1 : 0);   // this block among the stream blocks
-    if (a.halted && *a.halted) return;
-    if (DBG == 5) return;
-    extern __shared__ __attribute__((aligned(16))) double lds[];
-    const int lane = lane_id();
-    const int wpb = int(blockDim.x) / kWave;
-    const int gw = __builtin_amdgcn_readfirstlane(bid * wpb + int(threadIdx.x) / kWave);
-    const int nblk = int(gridDim.x) - (a.fin_on ? 1 : 0);   // (the finish block takes no share)
-    const int nw = nblk * wpb;
-    const uint32_t zslot = uint32_t(a.n_params);
-    if (W_LDS && DBG != 4) {
-        // stage w[0, n_params] in 16-byte pieces, all of a thread's loads
-        // issued before its first store (loads and stores unconditional --
-        // an index past the end is clamped to the last piece, which is then
-        // written twice with the same value -- so nothing is branched around)
-        const int n2 = (a.n_params + 2) / 2;
-        const double2* src = reinterpret_cast<const double2*>(a.w);
-        double2* dst = reinterpret_cast<double2*>(lds);
-        constexpr int kB = 8;
-        for (int j0 = int(threadIdx.x); j0 < n2; j0 += kB * int(blockDim.x)) {
-            double2 t[kB];
-#pragma unroll
-            for (int b = 0; b < kB; ++b) t[b] = src[min(j0 + b * int(blockDim.x), n2 - 1)];
-#pragma unroll
-            for (int b = 0; b < kB; ++b) dst[min(j0 + b * int(blockDim.x), n2 - 1)] = t[b];
-        }
-        __syncthreads();
-    }
-    const double* wsrc = W_LDS ? lds : a.w;
-    double ll_acc = 0.0;
-    for (int round = 0;; ++round) {
-        const int grp = round * nw + ((round & 1) ? (nw - 1 - gw) : gw);
-        if (grp >= a.n_groups) break;
-        const int gch = a.g_len[grp];
-        const uint4* st = a.stream + a.g_base[grp] + lane;
-        const double p = a.p_lane[grp * kWave + lane];   // 0 on padding lanes
-        double acc0 = 0.0, acc1 = 0.0;
-        // Two register sets of D chunks: one is applied while the other's
-        // loads are in flight, and the sets swap roles -- no register copy of
-        // an in-flight load, so the wait before a set is "all but the other
-        // set's D loads".  Loads are unconditional (the stream carries
-        // kStreamTailChunks chunks of slack after the last group); the only
-        // branches are the uniform end-of-group tests.
-        constexpr int D = kStreamPrefetch;
-        uint4 A[D], B[D];
-        auto load = [&](uint4 (&r)[D], int c0) {
-#pragma unroll
-            for (int d = 0; d < D; ++d) r[d] = st[int64_t(kWave) * (c0 + d)];
-        };
-        auto apply = [&](const uint4 (&r)[D], int c0) {
-#pragma unroll
-            for (int d = 0; d < D; ++d) {
-                if (c0 + d >= gch) break;
-                const uint32_t v[4] = {r[d].x, r[d].y, r[d].z, r[d].w};
-                bool multi = false;
-#pragma unroll
-                for (int i = 0; i < 4; ++i) {
-                    if (WIDE) {
-                        const uint32_t x = v[i];
-                        const double t = wsrc[min(x, zslot)];
-                        if (i & 1) acc1 += t; else acc0 += t;
-                        if (MULTI) multi |= int(x) < -1;
-                    } else {
-                        const uint32_t lo = v[i] & 0xffffu, hi = v[i] >> 16;
-                        if (DBG == 1) {
-                            acc0 += double(lo);
-                            acc1 += double(hi);
-                        } else {
-                            acc0 += wsrc[min(lo, zslot)];
-                            acc1 += wsrc[min(hi, zslot)];
-                        }
-                        if (MULTI) multi |= (lo >= 0x8000u && lo != 0xffffu) || (hi >= 0x8000u && hi != 0xffffu);
-                    }
-                }
-                if (MULTI && multi) {   // rare: epsilon-composite edges
-                    for (int i = 0; i < 4; ++i) {
-                        for (int h = 0; h < (WIDE ? 1 : 2); ++h) {
-                            int g = -1;
-                            if (WIDE) {
-                                if (int(v[i]) < -1) g = -(int(v[i]) + 2);
-                            } else {
-                                const uint32_t x = (v[i] >> (16 * h)) & 0xffffu;
-                                if (x >= 0x8000u && x != 0xffffu) g = a.m.multi_edge[x - 0x8000u];
-                            }
-                            if (g >= 0)
-                                for (int q = a.m.pptr[g]; q < a.m.pptr[g + 1]; ++q) acc0 += wsrc[a.m.pidx[q]];
-                        }
-                    }
-                }
-            }
-        };
-        if (DBG < 3) load(A, 0);
-        for (int c0 = 0; DBG < 3;) {
-            load(B, c0 + D);
-            apply(A, c0);
-            c0 += D;
-            if (c0 >= gch) break;
-            load(A, c0 + D);
-            apply(B, c0);
-            c0 += D;
-            if (c0 >= gch) break;
-        }
-        const double acc = acc0 + acc1;
-        ll_acc += p * acc;
-        if (a.logq) {
-            const int s = a.l_str[grp * kWave + lane];
-            if (s >= 0) a.logq[s] = acc;
-        }
-    }
-    ll_acc = wave_sum(ll_acc);
-    if (lane == 0) a.ll_part[gw] = ll_acc;
-    // this block's slice of the per-edge weights and the zeroed result, for
-    // the kernels after this one (nothing in this launch reads them)
-    if (W_LDS) edge_weight_slice(a, bid, nblk);
-}
 
 // Bubbles.  Local forward from the bubble's first cut, local backward from
 // its last cut; an edge's posterior is alpha(src) w beta(dst) / Z, -p_s times
@@ -856,7 +725,6 @@ __device__ __forceinline__ double small_bubble(const BubbleArgs& a, const int4* 
 // weight) in LDS in parallel, lane 0 runs the two sweeps over the staged
 // edges, and the lanes write the contributions (an edge may have several
 // parameters, hence several slots).
-constexpr int kBigEdgeLds = 256;   // > kMaxBubbleEdges
 __device__ double big_bubble(const BubbleArgs& a, int i, int* lsd, double* lw, double* lv, double* AB) {
     const int lane = lane_id();
     const int off = a.big_off[i];
@@ -927,6 +795,155 @@ __global__ __launch_bounds__(kBubbleBlock) void bubble_kernel(BubbleArgs a) {
     }
     ll_acc = wave_sum(ll_acc);
     if (lane == 0) a.ll_part[gw] = ll_acc;
+}
+
+// Per-iteration stream kernel: log q of every compiled string's trivial
+// words, sum_words w[j], one lane per string, no atomics (their gradient is
+// the constant added by the tail kernel).  w[n_params] is a zero slot, so a
+// padding word (0xFFFF / -1) and -- in the fast path -- a multi-parameter
+// word read 0.0 without a branch: index = min(word, n_params).  Chunks that
+// hold multi-parameter words (MULTI, automata with epsilon composites) take
+// a second, per-word pass.  Loads are unconditional up to the group's
+// longest lane (shorter lanes read their padding chunks), D chunks in flight.
+// DBG (timing experiments only, WFSA_FBS_DBG): 1 no table gathers, 3 no
+// stream pass at all, 4 neither stream pass nor table staging, 5 return at once
+template <bool WIDE, bool W_LDS, bool MULTI, int DBG = 0>
+__global__ __launch_bounds__(1024) void fbs_kernel(CompiledArgs a) {
+    extern __shared__ __attribute__((aligned(16))) double lds[];
+    const int lane = lane_id();
+    const int wpb = int(blockDim.x) / kWave;
+    const int nblk = int(gridDim.x) - (a.service ? 1 : 0);   // stream blocks (the service block takes no share)
+    const int nw = nblk * wpb;
+    if (a.service && blockIdx.x == 0) {   // dispatched first: the previous QN step's finish
+        qn_finish_block(a.fin);
+        return;
+    }
+    const int bid = int(blockIdx.x) - (a.service ? 1 : 0);   // this block among the stream blocks
+    if (a.halted && *a.halted) return;
+    if (DBG == 5) return;
+    const int gw = __builtin_amdgcn_readfirstlane(bid * wpb + int(threadIdx.x) / kWave);
+    const uint32_t zslot = uint32_t(a.n_params);
+    if (W_LDS && DBG != 4) {
+        // stage w[0, n_params] in 16-byte pieces, all of a thread's loads
+        // issued before its first store (loads and stores unconditional --
+        // an index past the end is clamped to the last piece, which is then
+        // written twice with the same value -- so nothing is branched around)
+        const int n2 = (a.n_params + 2) / 2;
+        const double2* src = reinterpret_cast<const double2*>(a.w);
+        double2* dst = reinterpret_cast<double2*>(lds);
+        constexpr int kB = 8;
+        for (int j0 = int(threadIdx.x); j0 < n2; j0 += kB * int(blockDim.x)) {
+            double2 t[kB];
+#pragma unroll
+            for (int b = 0; b < kB; ++b) t[b] = src[min(j0 + b * int(blockDim.x), n2 - 1)];
+#pragma unroll
+            for (int b = 0; b < kB; ++b) dst[min(j0 + b * int(blockDim.x), n2 - 1)] = t[b];
+        }
+        __syncthreads();
+    }
+    const double* wsrc = W_LDS ? lds : a.w;
+    double ll_acc = 0.0;
+    if (a.bub_on) {   // this wave's small bubbles (one per lane), before its streams
+        const int b = gw * kWave + lane;
+        if (b < a.bub.n_small4) ll_acc += small_bubble<4, 4>(a.bub, a.bub.sm4_tbl, a.bub.n_small4, b);
+        else if (b < a.bub.n_small4 + a.bub.n_small)
+            ll_acc += small_bubble<8, 8>(a.bub, a.bub.sm_tbl, a.bub.n_small, b - a.bub.n_small4);
+        // big bubbles, one wavefront each, from the last blocks' last waves
+        // down (the small ones fill the first waves), staged in LDS after w
+        const int w = int(threadIdx.x) / kWave;
+        const int r = (nblk - 1 - bid) + nblk * (wpb - 1 - w);
+        if (r < a.bub.n_big) {
+            const int E = a.bub.big_lds_edges;
+            char* st = reinterpret_cast<char*>(lds) + a.bub.big_lds_off + w * big_stage_bytes(E);
+            double* lw = reinterpret_cast<double*>(st);
+            int* lsd = reinterpret_cast<int*>(lw + E + 2 * kMaxBubbleNodes);
+            for (int i = r; i < a.bub.n_big; i += nw) ll_acc += big_bubble(a.bub, i, lsd, lw, lw, lw + E);
+        }
+    }
+    for (int round = 0;; ++round) {
+        const int grp = round * nw + ((round & 1) ? (nw - 1 - gw) : gw);
+        if (grp >= a.n_groups) break;
+        const int gch = a.g_len[grp];
+        const uint4* st = a.stream + a.g_base[grp] + lane;
+        const double p = a.p_lane[grp * kWave + lane];   // 0 on padding lanes
+        double acc0 = 0.0, acc1 = 0.0;
+        // Two register sets of D chunks: one is applied while the other's
+        // loads are in flight, and the sets swap roles -- no register copy of
+        // an in-flight load, so the wait before a set is "all but the other
+        // set's D loads".  Loads are unconditional (the stream carries
+        // kStreamTailChunks chunks of slack after the last group); the only
+        // branches are the uniform end-of-group tests.
+        constexpr int D = kStreamPrefetch;
+        uint4 A[D], B[D];
+        auto load = [&](uint4 (&r)[D], int c0) {
+#pragma unroll
+            for (int d = 0; d < D; ++d) r[d] = st[int64_t(kWave) * (c0 + d)];
+        };
+        auto apply = [&](const uint4 (&r)[D], int c0) {
+#pragma unroll
+            for (int d = 0; d < D; ++d) {
+                if (c0 + d >= gch) break;
+                const uint32_t v[4] = {r[d].x, r[d].y, r[d].z, r[d].w};
+                bool multi = false;
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    if (WIDE) {
+                        const uint32_t x = v[i];
+                        const double t = wsrc[min(x, zslot)];
+                        if (i & 1) acc1 += t; else acc0 += t;
+                        if (MULTI) multi |= int(x) < -1;
+                    } else {
+                        const uint32_t lo = v[i] & 0xffffu, hi = v[i] >> 16;
+                        if (DBG == 1) {
+                            acc0 += double(lo);
+                            acc1 += double(hi);
+                        } else {
+                            acc0 += wsrc[min(lo, zslot)];
+                            acc1 += wsrc[min(hi, zslot)];
+                        }
+                        if (MULTI) multi |= (lo >= 0x8000u && lo != 0xffffu) || (hi >= 0x8000u && hi != 0xffffu);
+                    }
+                }
+                if (MULTI && multi) {   // rare: epsilon-composite edges
+                    for (int i = 0; i < 4; ++i) {
+                        for (int h = 0; h < (WIDE ? 1 : 2); ++h) {
+                            int g = -1;
+                            if (WIDE) {
+                                if (int(v[i]) < -1) g = -(int(v[i]) + 2);
+                            } else {
+                                const uint32_t x = (v[i] >> (16 * h)) & 0xffffu;
+                                if (x >= 0x8000u && x != 0xffffu) g = a.m.multi_edge[x - 0x8000u];
+                            }
+                            if (g >= 0)
+                                for (int q = a.m.pptr[g]; q < a.m.pptr[g + 1]; ++q) acc0 += wsrc[a.m.pidx[q]];
+                        }
+                    }
+                }
+            }
+        };
+        if (DBG < 3) load(A, 0);
+        for (int c0 = 0; DBG < 3;) {
+            load(B, c0 + D);
+            apply(A, c0);
+            c0 += D;
+            if (c0 >= gch) break;
+            load(A, c0 + D);
+            apply(B, c0);
+            c0 += D;
+            if (c0 >= gch) break;
+        }
+        const double acc = acc0 + acc1;
+        ll_acc += p * acc;
+        if (a.logq) {
+            const int s = a.l_str[grp * kWave + lane];
+            if (s >= 0) a.logq[s] = acc;
+        }
+    }
+    ll_acc = wave_sum(ll_acc);
+    if (lane == 0) a.ll_part[gw] = ll_acc;
+    // this block's slice of the per-edge weights and the zeroed result, for
+    // the kernels after this one (nothing in this launch reads them)
+    if (W_LDS) edge_weight_slice(a, bid, nblk);
 }
 
 // One block copies out[0, n) to host-mapped memory in 16-byte stores (n
@@ -1079,7 +1096,7 @@ hipError_t launch_trav(TravMode mode, const TravArgs& a, int grid, hipStream_t s
 }
 
 hipError_t launch_compiled(const CompiledArgs& a, int grid, int block, size_t lds, hipStream_t stream) {
-    const dim3 g{unsigned(grid + (a.fin_on && !a.with_grad ? 1 : 0)), 1, 1}, b{unsigned(block), 1, 1};
+    const dim3 g{unsigned(grid + (a.service && !a.with_grad ? 1 : 0)), 1, 1}, b{unsigned(block), 1, 1};
     if (!a.with_grad) {   // per-iteration form: w staged in LDS or read from global
         static const int dbg = [] {
             const char* e = std::getenv("WFSA_FBS_DBG");

@@ -177,6 +177,48 @@ struct QnArgs {
     double* host_ring;           // host-mapped [slots][kQnRow]
 };
 
+// Bubble evaluation.  Contributions (-p_s x edge posterior) go straight to
+// their slots in `contrib`, which is parameter-major: parameter j owns the
+// contiguous range [slot_ptr[j], slot_ptr[j+1]) -- the tail kernel then sums
+// contiguous runs, no gather.
+//   small bubbles (every edge with at most one parameter) in two classes,
+//     A: <= 4 nodes and edges, B: <= kBubbleRegNodes nodes, <= kBubbleRegEdges
+//     edges; each a structure-of-arrays table of 16-byte quads -- quad k of
+//     bubble b at tbl[k * n + b]: [header: nodes | edges << 16, string, p (2
+//     words)], RE/2 x [(code, src | dst << 16) x 2], RE/4 x [slot x 4] (-1:
+//     the edge has no parameter) -- one lane per bubble, coalesced loads.
+//   big bubbles (the rest, rare): variable records in `bub` at big_off[i]
+//     (bubble record layout above), one wavefront per bubble; the slots of
+//     edge e of big bubble i are big_eslot[big_eslot_ptr[big_edge_base[i] + e] ..].
+constexpr int kSmallBubbleQuads = 7;
+constexpr int kBigEdgeLds = 256;   // > kMaxBubbleEdges: per-wave staging of a big bubble
+// per-wave LDS staging of a big bubble of at most E edges in the stream
+// kernel (E even): weights / contributions and alpha, beta (doubles), then
+// the edges' nodes (ints); 16-byte multiple
+__host__ __device__ inline int big_stage_bytes(int E) { return ((E + 2 * kMaxBubbleNodes) * 8 + E * 4 + 15) & ~15; }
+constexpr int kSmallBubbleQuads4 = 4;   // class A: <= 4 nodes, <= 4 edges (1 + 2 + 1 quads)
+struct BubbleArgs {
+    ModelView m;
+    const int4* sm4_tbl;     // class A table (most bubbles: diamonds)
+    int32_t n_small4;
+    const int4* sm_tbl;      // class B table (<= 8 nodes, <= 8 edges)
+    int32_t n_small;
+    const int32_t* bub;
+    const int32_t* big_off;
+    int32_t n_big;
+    int32_t big_lds_edges;   // fused: max edges of a big bubble (even) ...
+    int32_t big_lds_off;     // ... and the byte offset of the waves' staging in the stream kernel's LDS
+    const int32_t* big_edge_base;
+    const int32_t* big_eslot_ptr;
+    const int32_t* big_eslot;
+    double* contrib;
+    double* ll_part;         // [waves in grid]
+    double* logq;            // [S] or null: log Z added to the string's entry
+    const double* w;         // [n_params + 1] weights (GetWeight form) with the zero slot
+    const double* ewp;       // [n_params + 1] exp(w), ewp[n_params] = 1 (per iteration)
+    const unsigned* halted;
+};
+
 // Compiled streams of the per-iteration kernels.
 //   main stream: only "trivial" words (edges whose posterior is 1).  Narrow
 //     (16-bit) words: j < 0x8000 a single-parameter edge with parameter j,
@@ -204,9 +246,15 @@ struct CompiledArgs {
                              // else: >= 1 w staged in LDS, 0 global
     int32_t wide;
     int32_t with_grad;       // accumulate the (weight-independent) trivial-word gradient
-    // device-resident QN: the extra last block finishes the previous step
+    // service block (an extra first block, `service`): the previous
+    // device-resident QN step's finish.  bub_on: the stream waves also
+    // evaluate the bubbles before their streams (no separate bubble kernel)
+    // -- the small ones one per lane from the first waves, the big ones one
+    // per wavefront from the last
     QnArgs fin;
-    int32_t fin_on;
+    BubbleArgs bub;
+    int32_t bub_on;
+    int32_t service;
     int32_t multi;           // the automaton has multi-parameter (epsilon-composite) edges
     const double* w;         // [n_params] w_full (GetWeight form)
     double* grad;            // [n_params] (TABLES == 0: atomics straight into it)
@@ -224,40 +272,6 @@ struct CompiledArgs {
     const unsigned* halted;  // device-resident QN run: nonzero = skip (or null)
 };
 
-// Bubble evaluation.  Contributions (-p_s x edge posterior) go straight to
-// their slots in `contrib`, which is parameter-major: parameter j owns the
-// contiguous range [slot_ptr[j], slot_ptr[j+1]) -- the tail kernel then sums
-// contiguous runs, no gather.
-//   small bubbles (every edge with at most one parameter) in two classes,
-//     A: <= 4 nodes and edges, B: <= kBubbleRegNodes nodes, <= kBubbleRegEdges
-//     edges; each a structure-of-arrays table of 16-byte quads -- quad k of
-//     bubble b at tbl[k * n + b]: [header: nodes | edges << 16, string, p (2
-//     words)], RE/2 x [(code, src | dst << 16) x 2], RE/4 x [slot x 4] (-1:
-//     the edge has no parameter) -- one lane per bubble, coalesced loads.
-//   big bubbles (the rest, rare): variable records in `bub` at big_off[i]
-//     (bubble record layout above), one wavefront per bubble; the slots of
-//     edge e of big bubble i are big_eslot[big_eslot_ptr[big_edge_base[i] + e] ..].
-constexpr int kSmallBubbleQuads = 7;
-constexpr int kSmallBubbleQuads4 = 4;   // class A: <= 4 nodes, <= 4 edges (1 + 2 + 1 quads)
-struct BubbleArgs {
-    ModelView m;
-    const int4* sm4_tbl;     // class A table (most bubbles: diamonds)
-    int32_t n_small4;
-    const int4* sm_tbl;      // class B table (<= 8 nodes, <= 8 edges)
-    int32_t n_small;
-    const int32_t* bub;
-    const int32_t* big_off;
-    int32_t n_big;
-    const int32_t* big_edge_base;
-    const int32_t* big_eslot_ptr;
-    const int32_t* big_eslot;
-    double* contrib;
-    double* ll_part;         // [waves in grid]
-    double* logq;            // [S] or null: log Z added to the string's entry
-    const double* w;         // [n_params + 1] weights (GetWeight form) with the zero slot
-    const double* ewp;       // [n_params + 1] exp(w), ewp[n_params] = 1 (per iteration)
-    const unsigned* halted;
-};
 
 // The per-iteration tail, one launch: out[1+j] += sum over blocks of the
 // compiled kernel's partial gradients, += the bubble contributions of

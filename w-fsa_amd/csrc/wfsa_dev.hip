@@ -160,7 +160,7 @@ struct wfsa_dev {
     size_t i_lds = 0;
     DevBuf<double> fixed_grad;       // [n_params] gradient of the trivial words (constant)
     // bubbles
-    int32_t n_bubbles = 0, n_small4 = 0, n_small = 0, n_big = 0;
+    int32_t n_bubbles = 0, n_small4 = 0, n_small = 0, n_big = 0, big_lds_edges = 2;
     int b_waves = 0;
     DevBuf<int4> sm4_tbl, sm_tbl;
     DevBuf<int32_t> big_off, big_edge_base, big_eslot_ptr, big_eslot;
@@ -191,6 +191,7 @@ struct wfsa_dev {
     unsigned seq = 0;            // last sequence number the host expects
     bool timing_pending = false; // events of the last call not yet read
     bool kernel_timing = true;
+    bool fuse_bubbles = true;    // WFSA_FUSE_BUBBLES=0: separate bubble kernel
 
     DevBuf<double> gpart;        // per-block partial gradients of the compiled kernel
 
@@ -328,6 +329,10 @@ void drop_graph(wfsa_dev* ctx);
 
 int enqueue_compiled(wfsa_dev* ctx, bool with_grad, bool want_logq, const unsigned* halted = nullptr,
                      int slot = -1, const wfsa::QnArgs* fin = nullptr);
+wfsa::BubbleArgs bubble_args(wfsa_dev* ctx, bool want_logq, const unsigned* halted, double* ll_part);
+bool bubbles_fused(wfsa_dev* ctx, bool want_logq);
+// byte offset of the big bubbles' staging in the stream kernel's LDS (after w)
+size_t big_stage_off(const wfsa_dev* ctx) { return (ctx->i_lds + 15) & ~size_t(15); }
 
 // per-kernel timing events of slot `slot` (< 0: this launch is not timed;
 // WFSA_TIMING=0 leaves them all out).  An event between two kernels costs a
@@ -661,6 +666,9 @@ int prepare(wfsa_dev* ctx, int level) {
         ctx->n_small4 = int32_t(small4.size());
         ctx->n_small = int32_t(small.size());
         ctx->n_big = int32_t(nb);
+        ctx->big_lds_edges = 2;
+        for (int32_t o : big) ctx->big_lds_edges = std::max(ctx->big_lds_edges, (h_bubbuf[size_t(o)] >> 16) + 1);
+        ctx->big_lds_edges &= ~1;   // even
         std::vector<int32_t> cparam, cptr;
         for (int32_t jj = 0; jj < np; ++jj)
             for (int32_t b = pc[size_t(jj)]; b < pc[size_t(jj) + 1]; b += wfsa::kBubbleGradChunk) {
@@ -718,7 +726,7 @@ int prepare(wfsa_dev* ctx, int level) {
         ctx->fall_grid[t] = fb[t].empty() ? 0 : trav_grid(ctx->cfg[t], ctx->n_cu, int64_t(fb[t].size()));
         if (!fb[t].empty()) HIP_TRY(ctx->fall[t].upload(fb[t].data(), fb[t].size(), s));
     }
-    const size_t waves = std::max(size_t(ctx->c_grid) * waves_per_block, size_t(ctx->i_grid) * size_t(i_wpb)) +
+    const size_t waves = std::max(size_t(ctx->c_grid) * waves_per_block, size_t(ctx->i_grid + 1) * size_t(i_wpb)) +
                          size_t(ctx->b_waves) +
                          size_t(ctx->fall_grid[0]) * size_t(ctx->cfg[0].waves_per_block) +
                          size_t(ctx->fall_grid[1]) * size_t(ctx->cfg[1].waves_per_block);
@@ -795,12 +803,22 @@ int enqueue_compiled(wfsa_dev* ctx, bool with_grad, bool want_logq, const unsign
         c.ll_part = ctx->ll_cur;
         c.logq = want_logq ? ctx->logq.ptr : nullptr;
         c.halted = halted;
+        size_t lds = with_grad ? ctx->c_lds : ctx->i_lds;
         if (fin && !with_grad && tables >= 1) {
             c.fin = *fin;
-            c.fin_on = 1;
+            c.service = 1;
         }
-        if (with_grad) HIP_TRY(wfsa::launch_compiled(c, ctx->c_grid, kCompiledBlock, ctx->c_lds, s));
-        else HIP_TRY(wfsa::launch_compiled(c, ctx->i_grid, ctx->i_block, ctx->i_lds, s));
+        if (!with_grad && bubbles_fused(ctx, want_logq)) {
+            c.bub = bubble_args(ctx, false, halted, nullptr);
+            c.bub_on = 1;
+            if (ctx->n_big > 0) {
+                c.bub.big_lds_edges = ctx->big_lds_edges;
+                c.bub.big_lds_off = int32_t(big_stage_off(ctx));
+                lds = big_stage_off(ctx) + size_t(ctx->i_block / kWave) * size_t(wfsa::big_stage_bytes(ctx->big_lds_edges));
+            }
+        }
+        if (with_grad) HIP_TRY(wfsa::launch_compiled(c, ctx->c_grid, kCompiledBlock, lds, s));
+        else HIP_TRY(wfsa::launch_compiled(c, ctx->i_grid, ctx->i_block, lds, s));
     }
     if (!with_grad) HIP_TRY(record(ctx, ctx->kc, slot, s));
     if (with_grad) {
@@ -821,7 +839,7 @@ int enqueue_compiled(wfsa_dev* ctx, bool with_grad, bool want_logq, const unsign
 // compiled streams (with the per-edge weights) + bubbles (timed by k0..k1),
 // traversal fallback (k1..k2), the tail reduction (which adds the trivial
 // words' constant gradient), and -- without a communicator -- the results out.
-int enqueue_bubbles(wfsa_dev* ctx, bool want_logq, const unsigned* halted, int32_t wave_off, hipStream_t s) {
+wfsa::BubbleArgs bubble_args(wfsa_dev* ctx, bool want_logq, const unsigned* halted, double* ll_part) {
     wfsa::BubbleArgs b{};
     b.m = model_view(ctx);
     b.sm4_tbl = ctx->sm4_tbl.ptr;
@@ -837,11 +855,28 @@ int enqueue_bubbles(wfsa_dev* ctx, bool want_logq, const unsigned* halted, int32
     b.contrib = ctx->contrib.ptr;
     b.w = ctx->w_full.ptr;
     b.ewp = ctx->ewp.ptr;
-    b.ll_part = ctx->ll_cur + wave_off;
+    b.ll_part = ll_part;
     b.logq = want_logq ? ctx->logq.ptr : nullptr;
     b.halted = halted;
-    HIP_TRY(wfsa::launch_bubbles(b, s));
+    return b;
+}
+
+int enqueue_bubbles(wfsa_dev* ctx, bool want_logq, const unsigned* halted, int32_t wave_off, hipStream_t s) {
+    HIP_TRY(wfsa::launch_bubbles(bubble_args(ctx, want_logq, halted, ctx->ll_cur + wave_off), s));
     return WFSA_OK;
+}
+
+// The small bubbles ride in the stream kernel's waves and the big ones in
+// its service block when the kernel stages the weights (and log q is not
+// wanted: both would write the strings' entries).
+bool bubbles_fused(wfsa_dev* ctx, bool want_logq) {
+    if (!(ctx->n_bubbles > 0 && !want_logq && ctx->n_groups > 0 && ctx->i_tables >= 1 && !ctx->side_stream &&
+          ctx->fuse_bubbles))
+        return false;
+    // the big bubbles' staging must fit beside w
+    return ctx->n_big == 0 || big_stage_off(ctx) + size_t(ctx->i_block / kWave) *
+                                                       size_t(wfsa::big_stage_bytes(ctx->big_lds_edges)) <=
+                                  size_t(kLdsPerCu - 1024);
 }
 
 // The evaluation kernels; with_tail: finish out = [LL, grad_full] with the
@@ -860,6 +895,8 @@ int enqueue_evaluation(wfsa_dev* ctx, bool want_logq, const unsigned* halted, in
         HIP_TRY(hipEventRecord(ctx->fork, s));
         HIP_TRY(hipStreamWaitEvent(ctx->side_stream, ctx->fork, 0));
     }
+    const bool fusedb = bubbles_fused(ctx, want_logq);
+    // the stream kernel's ll partials: one per stream wave (its service block writes none)
     int32_t wave_off = ctx->n_groups > 0 ? ctx->i_grid * (ctx->i_block / kWave) : 0;
     if (ctx->n_bubbles > 0 && side) {
         if (int rc = enqueue_bubbles(ctx, want_logq, halted, wave_off, ctx->side_stream)) return rc;
@@ -868,10 +905,10 @@ int enqueue_evaluation(wfsa_dev* ctx, bool want_logq, const unsigned* halted, in
     if (int rc = enqueue_compiled(ctx, false, want_logq, halted, slot, fin)) return rc;
     if (fin_done) *fin_done = fin && ctx->n_groups > 0 && ctx->i_tables >= 1;
     if (side) HIP_TRY(hipStreamWaitEvent(s, ctx->join, 0));
-    if (ctx->n_bubbles > 0 && !side) {
+    if (ctx->n_bubbles > 0 && !side && !fusedb) {
         if (int rc = enqueue_bubbles(ctx, want_logq, halted, wave_off, s)) return rc;
     }
-    if (ctx->n_bubbles > 0) wave_off += ctx->b_waves;
+    if (ctx->n_bubbles > 0 && !fusedb) wave_off += ctx->b_waves;
     for (int t = 0; t < 2; ++t) {
         if (!ctx->n_fall[t]) continue;
         wfsa::TravArgs a = trav_args(ctx, t);
@@ -1014,6 +1051,7 @@ int wfsa_dev_create(int device, wfsa_dev** out) {
     ctx->n_cu = prop.multiProcessorCount > 0 ? prop.multiProcessorCount : kNumCu;
     if (const char* e = std::getenv("WFSA_GRAPH")) ctx->use_graph = e[0] == '1';
     if (const char* e = std::getenv("WFSA_TIMING")) ctx->kernel_timing = e[0] != '0';
+    if (const char* e = std::getenv("WFSA_FUSE_BUBBLES")) ctx->fuse_bubbles = e[0] != '0';
 
     HIP_TRY(hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking));
     // measured: the cross-stream fork/join costs more idle time (5-20 us)
