@@ -1,5 +1,17 @@
+# timing experiments: avg kernel durations per configuration
 export TMPDIR=/tmp
-for cfg in "0 0" "0 1" "1 1"; do set -- $cfg
-  WFSA_BUBBLE_REG=$1 WFSA_BUBBLE_SKIPBIG=$2 timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d $GRAFT_REPO_ROOT/gpurun_out/bx/r$1s$2 -o run -- python3 $GRAFT_REPO_ROOT/bench.py --cpu-sample 0 --steps 50 > $GRAFT_REPO_ROOT/gpurun_out/bx/r$1s$2.log 2>&1 || exit 1
-  echo "reg=$1 skipbig=$2"; grep bubble_kernel $GRAFT_REPO_ROOT/gpurun_out/bx/r$1s$2/run_kernel_stats.csv | cut -d, -f3-5
-done
+R=$GRAFT_REPO_ROOT/gpurun_out/ex
+mkdir -p $R
+run() {
+  name=$1; shift
+  env "$@" timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d $R/$name -o run -- python3 $GRAFT_REPO_ROOT/bench.py --cpu-sample 0 --steps 40 > $R/$name.log 2>&1 || return 1
+  python3 - $R/$name/run_kernel_stats.csv $name <<'PY'
+import csv,sys
+for r in csv.DictReader(open(sys.argv[1])):
+    n=r['Name']
+    if 'fbs_kernel' in n or 'bubble_kernel' in n:
+        print(f"{sys.argv[2]:24s} {n[:60]:60s} calls {r['Calls']:>5s} avg {float(r['AverageNs'])/1000:7.1f} us")
+PY
+  grep -o '"value": [0-9.]*' $R/$name.log
+}
+run base A=1 && run d3 WFSA_FBS_DBG=3 && run sc0 WFSA_SMALL_COST=0 WFSA_BIG_COST=0 && run sc16 WFSA_SMALL_COST=16 WFSA_BIG_COST=16 && run sc24 WFSA_SMALL_COST=24 WFSA_BIG_COST=24

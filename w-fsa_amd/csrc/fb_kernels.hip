@@ -143,7 +143,7 @@ __device__ __forceinline__ bool put_trivial(const ModelView& m, int g, bool writ
     const int np = m.pptr[g + 1] - m.pptr[g];
     if (np == 0) return false;
     if (write) {
-        const int k = n_main;
+        const int k = n_main + stream_hdr_words(wide);   // after the lane's group header
         if (wide) {
             const int v = np == 1 ? m.pidx[m.pptr[g]] : -(g + 2);
             static_cast<int32_t*>(stream)[s_base + int64_t(k >> 2) * 256 + (k & 3)] = v;
@@ -569,7 +569,7 @@ __global__ __launch_bounds__(1024) void fbc_kernel(CompiledArgs a) {
         const int grp = round * nw + ((round & 1) ? (nw - 1 - gw) : gw);
         if (grp >= a.n_groups) break;
         const int s = a.l_str[grp * kWave + lane];
-        const int nch = (a.l_len[grp * kWave + lane] + PER - 1) / PER;
+        const int nch = (a.l_len[grp * kWave + lane] + stream_hdr_words(WIDE) + PER - 1) / PER;
         const int gch = a.g_len[grp];
         const uint4* st = a.stream + a.g_base[grp] + lane;
         const double p = s >= 0 ? a.p[s] : 0.0;
@@ -584,8 +584,13 @@ __global__ __launch_bounds__(1024) void fbc_kernel(CompiledArgs a) {
             for (int d = 0; d < D; ++d) {
                 const int c = c0 + d;
                 if (c >= gch) break;
-                const uint4 cur = buf[d];
+                uint4 cur = buf[d];
                 buf[d] = (c + D < nch) ? st[int64_t(kWave) * (c + D)] : pad;
+                if (c == 0) {   // the group header reads as padding
+                    cur.x = 0xffffffffu;
+                    cur.y = 0xffffffffu;
+                    cur.z = WIDE ? 0xffffffffu : (cur.z | 0xffffu);
+                }
                 const uint32_t v[4] = {cur.x, cur.y, cur.z, cur.w};
 #pragma unroll
                 for (int i = 0; i < 4; ++i) {
@@ -695,7 +700,7 @@ __device__ __forceinline__ double small_bubble(const BubbleArgs& a, const int4* 
     }
     double ew[RE];
 #pragma unroll
-    for (int e = 0; e < RE; ++e) ew[e] = a.ewp[code[e]];   // padding edges carry the zero-slot code
+    for (int e = 0; e < RE; ++e) ew[e] = (a.dbg & 2) ? 1.0 + 1e-3 * code[e] : a.ewp[code[e]];   // padding edges carry the zero-slot code
     double A[N], B[N];
 #pragma unroll
     for (int k = 0; k < N; ++k) {
@@ -714,7 +719,7 @@ __device__ __forceinline__ double small_bubble(const BubbleArgs& a, const int4* 
             const int src = sd[e] & 0xffff;
             const double bb = ew[e] * reg_get(B, sd[e] >> 16);
             reg_add(B, src, bb);
-            if (slot[e] >= 0) a.contrib[slot[e]] = reg_get(A, src) * bb * scale;
+            if (slot[e] >= 0 && !(a.dbg & 1)) a.contrib[slot[e]] = reg_get(A, src) * bb * scale;
         }
     const double lz = log(Z);
     if (a.logq) global_add(&a.logq[q[0].y], lz);
@@ -800,11 +805,20 @@ __global__ __launch_bounds__(kBubbleBlock) void bubble_kernel(BubbleArgs a) {
 // Per-iteration stream kernel: log q of every compiled string's trivial
 // words, sum_words w[j], one lane per string, no atomics (their gradient is
 // the constant added by the tail kernel).  w[n_params] is a zero slot, so a
-// padding word (0xFFFF / -1) and -- in the fast path -- a multi-parameter
-// word read 0.0 without a branch: index = min(word, n_params).  Chunks that
-// hold multi-parameter words (MULTI, automata with epsilon composites) take
-// a second, per-word pass.  Loads are unconditional up to the group's
-// longest lane (shorter lanes read their padding chunks), D chunks in flight.
+// padding word (0xFFFF / -1), a header word and -- in the fast path -- a
+// multi-parameter word read 0.0 without a branch: index = min(word,
+// n_params).  Chunks that hold multi-parameter words (MULTI, automata with
+// epsilon composites) take a second, per-word pass.
+//
+// Each wave owns a contiguous run of groups (wave_first, balanced at
+// preparation on chunk rows and bubble work) and streams it as one run of
+// 1 KiB rows: two register sets of D rows, one applied while the other's
+// loads are in flight, across group boundaries (a group starts with its
+// header row: p of each lane's string and the group's row count), so the
+// prefetch never drains between strings.  Load rows are clamped to the run
+// (a clamped load re-reads the last row from cache, no over-read of HBM).
+// The first set is issued before the weights are staged and the bubbles
+// evaluated, so its latency hides behind that work (both sets would spill).
 // DBG (timing experiments only, WFSA_FBS_DBG): 1 no table gathers, 3 no
 // stream pass at all, 4 neither stream pass nor table staging, 5 return at once
 template <bool WIDE, bool W_LDS, bool MULTI, int DBG = 0>
@@ -812,17 +826,28 @@ __global__ __launch_bounds__(1024) void fbs_kernel(CompiledArgs a) {
     extern __shared__ __attribute__((aligned(16))) double lds[];
     const int lane = lane_id();
     const int wpb = int(blockDim.x) / kWave;
-    const int nblk = int(gridDim.x) - (a.service ? 1 : 0);   // stream blocks (the service block takes no share)
+    const int nblk = int(gridDim.x);
     const int nw = nblk * wpb;
-    if (a.service && blockIdx.x == 0) {   // dispatched first: the previous QN step's finish
-        qn_finish_block(a.fin);
-        return;
-    }
-    const int bid = int(blockIdx.x) - (a.service ? 1 : 0);   // this block among the stream blocks
+    const int bid = int(blockIdx.x);
+    const int w = int(threadIdx.x) / kWave;
+    const int gw = __builtin_amdgcn_readfirstlane(bid * wpb + w);
+    if (a.fin_on && gw == a.fin_wave) qn_finish_wave(a.fin);   // the previous QN step's finish
     if (a.halted && *a.halted) return;
     if (DBG == 5) return;
-    const int gw = __builtin_amdgcn_readfirstlane(bid * wpb + int(threadIdx.x) / kWave);
     const uint32_t zslot = uint32_t(a.n_params);
+    // this wave's run of chunk rows
+    const int g0 = a.wave_first[gw], g1 = a.wave_first[gw + 1];
+    const int64_t cb = a.g_base[g0];
+    const int rows = int((a.g_base[g1] - cb) / kWave);
+    const int last = max(rows - 1, 0);   // no groups: row 0 of the slack after the last group
+    const uint4* st = a.stream + cb + lane;
+    constexpr int D = kStreamPrefetch;
+    uint4 A[D], B[D];
+    auto load = [&](uint4 (&r)[D], int c0) {
+#pragma unroll
+        for (int d = 0; d < D; ++d) r[d] = st[int64_t(kWave) * min(c0 + d, last)];
+    };
+    if (DBG < 3) load(A, 0);
     if (W_LDS && DBG != 4) {
         // stage w[0, n_params] in 16-byte pieces, all of a thread's loads
         // issued before its first store (loads and stores unconditional --
@@ -843,107 +868,125 @@ __global__ __launch_bounds__(1024) void fbs_kernel(CompiledArgs a) {
     }
     const double* wsrc = W_LDS ? lds : a.w;
     double ll_acc = 0.0;
-    if (a.bub_on) {   // this wave's small bubbles (one per lane), before its streams
-        const int b = gw * kWave + lane;
-        if (b < a.bub.n_small4) ll_acc += small_bubble<4, 4>(a.bub, a.bub.sm4_tbl, a.bub.n_small4, b);
-        else if (b < a.bub.n_small4 + a.bub.n_small)
-            ll_acc += small_bubble<8, 8>(a.bub, a.bub.sm_tbl, a.bub.n_small, b - a.bub.n_small4);
+    if (a.bub_on) {   // this wave's bubbles, before its streams
+        // small ones, one per lane, from the first small_wpb waves of every
+        // block (spread over all CUs)
+        if (w < a.bub.small_wpb) {   // small_wpb <= waves per block (bubbles_fused)
+            const int b = (bid * a.bub.small_wpb + w) * kWave + lane;
+            if (b < a.bub.n_small4) ll_acc += small_bubble<4, 4>(a.bub, a.bub.sm4_tbl, a.bub.n_small4, b);
+            else if (b < a.bub.n_small4 + a.bub.n_small)
+                ll_acc += small_bubble<8, 8>(a.bub, a.bub.sm_tbl, a.bub.n_small, b - a.bub.n_small4);
+        }
         // big bubbles, one wavefront each, from the last blocks' last waves
-        // down (the small ones fill the first waves), staged in LDS after w
-        const int w = int(threadIdx.x) / kWave;
+        // down, staged in LDS after w
         const int r = (nblk - 1 - bid) + nblk * (wpb - 1 - w);
         if (r < a.bub.n_big) {
             const int E = a.bub.big_lds_edges;
-            char* st = reinterpret_cast<char*>(lds) + a.bub.big_lds_off + w * big_stage_bytes(E);
-            double* lw = reinterpret_cast<double*>(st);
+            char* stg = reinterpret_cast<char*>(lds) + a.bub.big_lds_off + w * big_stage_bytes(E);
+            double* lw = reinterpret_cast<double*>(stg);
             int* lsd = reinterpret_cast<int*>(lw + E + 2 * kMaxBubbleNodes);
             for (int i = r; i < a.bub.n_big; i += nw) ll_acc += big_bubble(a.bub, i, lsd, lw, lw, lw + E);
         }
     }
-    for (int round = 0;; ++round) {
-        const int grp = round * nw + ((round & 1) ? (nw - 1 - gw) : gw);
-        if (grp >= a.n_groups) break;
-        const int gch = a.g_len[grp];
-        const uint4* st = a.stream + a.g_base[grp] + lane;
-        const double p = a.p_lane[grp * kWave + lane];   // 0 on padding lanes
-        double acc0 = 0.0, acc1 = 0.0;
-        // Two register sets of D chunks: one is applied while the other's
-        // loads are in flight, and the sets swap roles -- no register copy of
-        // an in-flight load, so the wait before a set is "all but the other
-        // set's D loads".  Loads are unconditional (the stream carries
-        // kStreamTailChunks chunks of slack after the last group); the only
-        // branches are the uniform end-of-group tests.
-        constexpr int D = kStreamPrefetch;
-        uint4 A[D], B[D];
-        auto load = [&](uint4 (&r)[D], int c0) {
-#pragma unroll
-            for (int d = 0; d < D; ++d) r[d] = st[int64_t(kWave) * (c0 + d)];
-        };
-        auto apply = [&](const uint4 (&r)[D], int c0) {
-#pragma unroll
-            for (int d = 0; d < D; ++d) {
-                if (c0 + d >= gch) break;
-                const uint32_t v[4] = {r[d].x, r[d].y, r[d].z, r[d].w};
-                bool multi = false;
-#pragma unroll
-                for (int i = 0; i < 4; ++i) {
-                    if (WIDE) {
-                        const uint32_t x = v[i];
-                        const double t = wsrc[min(x, zslot)];
-                        if (i & 1) acc1 += t; else acc0 += t;
-                        if (MULTI) multi |= int(x) < -1;
-                    } else {
-                        const uint32_t lo = v[i] & 0xffffu, hi = v[i] >> 16;
-                        if (DBG == 1) {
-                            acc0 += double(lo);
-                            acc1 += double(hi);
-                        } else {
-                            acc0 += wsrc[min(lo, zslot)];
-                            acc1 += wsrc[min(hi, zslot)];
-                        }
-                        if (MULTI) multi |= (lo >= 0x8000u && lo != 0xffffu) || (hi >= 0x8000u && hi != 0xffffu);
-                    }
-                }
-                if (MULTI && multi) {   // rare: epsilon-composite edges
-                    for (int i = 0; i < 4; ++i) {
-                        for (int h = 0; h < (WIDE ? 1 : 2); ++h) {
-                            int g = -1;
-                            if (WIDE) {
-                                if (int(v[i]) < -1) g = -(int(v[i]) + 2);
-                            } else {
-                                const uint32_t x = (v[i] >> (16 * h)) & 0xffffu;
-                                if (x >= 0x8000u && x != 0xffffu) g = a.m.multi_edge[x - 0x8000u];
-                            }
-                            if (g >= 0)
-                                for (int q = a.m.pptr[g]; q < a.m.pptr[g + 1]; ++q) acc0 += wsrc[a.m.pidx[q]];
-                        }
-                    }
-                }
-            }
-        };
-        if (DBG < 3) load(A, 0);
-        for (int c0 = 0; DBG < 3;) {
-            load(B, c0 + D);
-            apply(A, c0);
-            c0 += D;
-            if (c0 >= gch) break;
-            load(A, c0 + D);
-            apply(B, c0);
-            c0 += D;
-            if (c0 >= gch) break;
-        }
+    if (DBG < 3) load(B, D);
+    double p = 0.0, acc0 = 0.0, acc1 = 0.0;
+    int hdr = 0, grp = g0 - 1;   // the next header row, the current group
+    auto flush = [&]() {   // the lane's string of the current group is complete
         const double acc = acc0 + acc1;
         ll_acc += p * acc;
-        if (a.logq) {
+        if (a.logq && grp >= g0) {
             const int s = a.l_str[grp * kWave + lane];
             if (s >= 0) a.logq[s] = acc;
         }
+    };
+    auto apply = [&](const uint4 (&r)[D], int c0) {
+#pragma unroll
+        for (int d = 0; d < D; ++d) {
+            const int c = c0 + d;
+            if (c >= rows) break;
+            uint4 v = r[d];
+            if (c == hdr) {   // uniform: the first row of the next group
+                flush();
+                acc0 = 0.0;
+                acc1 = 0.0;
+                p = __longlong_as_double((long long)(v.x) | ((long long)(v.y) << 32));
+                hdr += __builtin_amdgcn_readfirstlane(int(WIDE ? v.z : (v.z & 0xffffu)));
+                ++grp;
+                v.x = 0xffffffffu;
+                v.y = 0xffffffffu;
+                v.z = WIDE ? 0xffffffffu : (v.z | 0xffffu);
+            }
+            const uint32_t vw[4] = {v.x, v.y, v.z, v.w};
+            bool multi = false;
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                if (WIDE) {
+                    const uint32_t x = vw[i];
+                    const double t = wsrc[min(x, zslot)];
+                    if (i & 1) acc1 += t; else acc0 += t;
+                    if (MULTI) multi |= int(x) < -1;
+                } else {
+                    const uint32_t lo = vw[i] & 0xffffu, hi = vw[i] >> 16;
+                    if (DBG == 1) {
+                        acc0 += double(lo);
+                        acc1 += double(hi);
+                    } else {
+                        acc0 += wsrc[min(lo, zslot)];
+                        acc1 += wsrc[min(hi, zslot)];
+                    }
+                    if (MULTI) multi |= (lo >= 0x8000u && lo != 0xffffu) || (hi >= 0x8000u && hi != 0xffffu);
+                }
+            }
+            if (MULTI && multi) {   // rare: epsilon-composite edges
+                for (int i = 0; i < 4; ++i) {
+                    for (int h = 0; h < (WIDE ? 1 : 2); ++h) {
+                        int g = -1;
+                        if (WIDE) {
+                            if (int(vw[i]) < -1) g = -(int(vw[i]) + 2);
+                        } else {
+                            const uint32_t x = (vw[i] >> (16 * h)) & 0xffffu;
+                            if (x >= 0x8000u && x != 0xffffu) g = a.m.multi_edge[x - 0x8000u];
+                        }
+                        if (g >= 0)
+                            for (int q = a.m.pptr[g]; q < a.m.pptr[g + 1]; ++q) acc0 += wsrc[a.m.pidx[q]];
+                    }
+                }
+            }
+        }
+    };
+    if (DBG < 3 && rows > 0) {
+        for (int c0 = 0;;) {   // A holds rows [c0, c0 + D), B [c0 + D, c0 + 2D)
+            apply(A, c0);
+            if (c0 + D >= rows) break;
+            load(A, c0 + 2 * D);
+            apply(B, c0 + D);
+            c0 += 2 * D;
+            if (c0 >= rows) break;
+            load(B, c0 + D);
+        }
     }
+    flush();
     ll_acc = wave_sum(ll_acc);
     if (lane == 0) a.ll_part[gw] = ll_acc;
     // this block's slice of the per-edge weights and the zeroed result, for
     // the kernels after this one (nothing in this launch reads them)
     if (W_LDS) edge_weight_slice(a, bid, nblk);
+}
+
+// Group headers (stream_hdr_words), written after the streams are emitted:
+// lane l's first chunk of group g gets p of its string and the group's row
+// count; the string's words follow in the same chunk.
+__global__ void stream_headers_kernel(uint4* stream, const int64_t* g_base, const int32_t* g_len,
+                                      const double* p_lane, int32_t n_groups, int32_t wide) {
+    const int64_t k = int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+    if (k >= int64_t(n_groups) * kWave) return;
+    const int g = int(k / kWave), l = int(k % kWave);
+    uint4 v = stream[g_base[g] + l];
+    const unsigned long long pb = (unsigned long long)(__double_as_longlong(p_lane[k]));
+    v.x = uint32_t(pb);
+    v.y = uint32_t(pb >> 32);
+    v.z = wide ? uint32_t(g_len[g]) : ((v.z & 0xffff0000u) | uint32_t(g_len[g]));
+    stream[g_base[g] + l] = v;
 }
 
 // One block copies out[0, n) to host-mapped memory in 16-byte stores (n
@@ -1095,8 +1138,17 @@ hipError_t launch_trav(TravMode mode, const TravArgs& a, int grid, hipStream_t s
     return hipGetLastError();
 }
 
+hipError_t launch_stream_headers(uint4* stream, const int64_t* g_base, const int32_t* g_len, const double* p_lane,
+                                int32_t n_groups, int32_t wide, hipStream_t s) {
+    const int64_t n = int64_t(n_groups) * kWave;
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(stream_headers_kernel, dim3(unsigned((n + 255) / 256)), dim3(256), 0, s, stream, g_base, g_len,
+                       p_lane, n_groups, wide);
+    return hipGetLastError();
+}
+
 hipError_t launch_compiled(const CompiledArgs& a, int grid, int block, size_t lds, hipStream_t stream) {
-    const dim3 g{unsigned(grid + (a.service && !a.with_grad ? 1 : 0)), 1, 1}, b{unsigned(block), 1, 1};
+    const dim3 g{unsigned(grid), 1, 1}, b{unsigned(block), 1, 1};
     if (!a.with_grad) {   // per-iteration form: w staged in LDS or read from global
         static const int dbg = [] {
             const char* e = std::getenv("WFSA_FBS_DBG");

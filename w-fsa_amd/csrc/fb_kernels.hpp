@@ -26,9 +26,15 @@ constexpr int kBubbleRegNodes = 8;     // (and so at most this many nodes)
 // bubble record: 4 header words + 2 per edge, rounded up to 16 bytes
 __host__ __device__ inline int bubble_record_words(int edges) { return (4 + 2 * edges + 3) & ~3; }
 constexpr int kBubbleSlackWords = 4 * (1 + kBubbleRegEdges / 2);   // over-read of the last record
-constexpr int kStreamPrefetch = 4;     // 16-byte chunks in flight per lane
-// slack after the last group's chunks: the prefetch runs ahead unguarded
+constexpr int kStreamPrefetch = 4;     // 16-byte chunks in flight per lane (per register set)
+// slack after the last group's chunks (the prepare-time pass over-reads)
 constexpr int kStreamTailChunks = 64 * 8;
+// Each lane's first chunk of a group starts with a header: p of the lane's
+// string (64 bits) and the group's chunk rows (low 16 bits of the next word),
+// so the per-iteration kernel streams a wave's groups as one run.  Narrow
+// (16-bit) words: the header takes words 0..4, wide (32-bit): words 0..2;
+// the string's words follow.
+__host__ __device__ inline int stream_hdr_words(int wide) { return wide ? 3 : 5; }
 
 // Per-iteration record of a combined edge, one 16-byte gather in the
 // compiled kernel: its log-weight and its parameter list (p0 when np == 1).
@@ -139,10 +145,10 @@ struct TravArgs {
 
 // Device-resident QuasiNewton step (qn_kernel.hip): qn_update (wavefront per
 // constraint) updates x and lambda from out = [LL, grad_full] and writes the
-// next w_full; the finish (qn_finish_block, qn_device.hpp) reduces the info
+// next w_full; the finish (qn_finish_wave, qn_device.hpp) reduces the info
 // row [KL, graderr, g_min, g_max, lambda_min, 0, 0, status] into a
 // host-mapped ring slot and bumps the completion flag.  The finish of step k
-// runs in an extra block of step k+1's stream kernel (or a trailing kernel).
+// runs in one wave of step k+1's stream kernel (or a trailing one-wave kernel).
 constexpr int kQnRow = 8;
 constexpr unsigned kQnRan = 0, kQnHalted = 1, kQnNonFinite = 2, kQnSkipped = 3;
 struct QnArgs {
@@ -206,6 +212,7 @@ struct BubbleArgs {
     const int32_t* bub;
     const int32_t* big_off;
     int32_t n_big;
+    int32_t small_wpb;       // fused: waves [0, small_wpb) of every block take 64 small bubbles each
     int32_t big_lds_edges;   // fused: max edges of a big bubble (even) ...
     int32_t big_lds_off;     // ... and the byte offset of the waves' staging in the stream kernel's LDS
     const int32_t* big_edge_base;
@@ -217,6 +224,7 @@ struct BubbleArgs {
     const double* w;         // [n_params + 1] weights (GetWeight form) with the zero slot
     const double* ewp;       // [n_params + 1] exp(w), ewp[n_params] = 1 (per iteration)
     const unsigned* halted;
+    int32_t dbg;             // timing experiments only (WFSA_BUB_DBG): 1 no slot stores, 2 no weight gathers
 };
 
 // Compiled streams of the per-iteration kernels.
@@ -236,25 +244,27 @@ struct CompiledArgs {
     const double* p;         // [S]
     const uint4* stream;     // 16-byte chunks
     const int64_t* g_base;   // [G] first chunk of the group
-    const int32_t* g_len;    // [G] chunks of the group's longest lane (its first)
+    const int32_t* g_len;    // [G] chunk rows of the group (its longest lane, header included)
     const int32_t* l_str;    // [64 G] string of each lane, -1 = padding
-    const int32_t* l_len;    // [64 G] words of each lane
-    const double* p_lane;    // [64 G] p of each lane's string (0 on padding lanes)
+    const int32_t* l_len;    // [64 G] words of each lane (header excluded)
+    const int32_t* wave_first;   // [stream waves + 1] the per-iteration kernel's groups of
+                                 // wave w: [wave_first[w], wave_first[w + 1]), contiguous
     int32_t n_groups;
     int32_t n_params;
     int32_t tables;          // with_grad: 2 w and grad staged in LDS, 1 grad in LDS, 0 global;
                              // else: >= 1 w staged in LDS, 0 global
     int32_t wide;
     int32_t with_grad;       // accumulate the (weight-independent) trivial-word gradient
-    // service block (an extra first block, `service`): the previous
-    // device-resident QN step's finish.  bub_on: the stream waves also
-    // evaluate the bubbles before their streams (no separate bubble kernel)
-    // -- the small ones one per lane from the first waves, the big ones one
-    // per wavefront from the last
+    // fin_on: wave fin_wave first runs the previous device-resident QN
+    // step's finish (given extra weight in the wave balance).  bub_on: the
+    // stream waves also evaluate the bubbles before their streams (no
+    // separate bubble kernel) -- the small ones one per lane from the first
+    // waves, the big ones one per wavefront from the last
     QnArgs fin;
+    int32_t fin_on;
+    int32_t fin_wave;
     BubbleArgs bub;
     int32_t bub_on;
-    int32_t service;
     int32_t multi;           // the automaton has multi-parameter (epsilon-composite) edges
     const double* w;         // [n_params] w_full (GetWeight form)
     double* grad;            // [n_params] (TABLES == 0: atomics straight into it)
@@ -321,6 +331,8 @@ __device__ __forceinline__ double strided_sum(const double* __restrict__ p, int 
 
 hipError_t configure_kernels(int max_dynamic_lds);
 hipError_t launch_trav(TravMode mode, const TravArgs& a, int grid, hipStream_t stream);
+hipError_t launch_stream_headers(uint4* stream, const int64_t* g_base, const int32_t* g_len, const double* p_lane,
+                                int32_t n_groups, int32_t wide, hipStream_t s);
 hipError_t launch_compiled(const CompiledArgs& a, int grid, int block, size_t lds, hipStream_t stream);
 constexpr int kBubbleBlock = 128;
 // waves: n_big (one per big bubble) + ceil(n_small / 64)

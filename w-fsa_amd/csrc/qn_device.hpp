@@ -1,4 +1,4 @@
-// Device helpers shared by the QN kernels and the stream kernel: block
+// Device helpers shared by the QN kernels and the stream kernel: wave
 // reductions and the finish of a device-resident QuasiNewton step (the info
 // row from qn_update's per-block partials, the halt decision, publication).
 #pragma once
@@ -11,62 +11,36 @@
 
 namespace wfsa {
 
-__device__ inline double block_reduce(double v, int op, double* red) {   // op 0 min, 1 max
+__device__ inline double wave_reduce(double v, int op) {   // op 0 min, 1 max, 2 sum (fixed order)
     for (int o = 32; o > 0; o >>= 1) {
         const double t = __shfl_xor(v, o, 64);
-        v = op == 0 ? fmin(v, t) : fmax(v, t);
+        v = op == 0 ? fmin(v, t) : (op == 1 ? fmax(v, t) : v + t);
     }
-    const int w = int(threadIdx.x) / 64, lane = int(threadIdx.x) & 63;
-    __syncthreads();
-    if (lane == 0) red[w] = v;
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        double r = red[0];
-        for (int i = 1; i < int(blockDim.x) / 64; ++i) r = op == 0 ? fmin(r, red[i]) : fmax(r, red[i]);
-        red[32] = r;
-    }
-    __syncthreads();
-    return red[32];
+    return v;
 }
 
-__device__ inline double block_sum(double v, double* red) {   // fixed order for a fixed block size
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-    const int w = int(threadIdx.x) / 64, lane = int(threadIdx.x) & 63;
-    __syncthreads();
-    if (lane == 0) red[w] = v;
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        double r = red[0];
-        for (int i = 1; i < int(blockDim.x) / 64; ++i) r += red[i];
-        red[32] = r;
-    }
-    __syncthreads();
-    return red[32];
-}
-
-// The finish of one step by one block (any size, a multiple of 64).
-__device__ inline void qn_finish_block(const QnArgs& a) {
-    __shared__ double red[33];
+// The finish of one step by one wavefront (it runs inside the next step's
+// stream kernel, beside the streams, or as its own one-wave launch).
+__device__ inline void qn_finish_wave(const QnArgs& a) {
+    const int lane = int(threadIdx.x) & 63;
     const unsigned state = *a.halted;
-    const int t = int(threadIdx.x), nt = int(blockDim.x);
     double gmin = INFINITY, gmax = -INFINITY, lmin = INFINITY, gerr = 0.0, ll = 0.0;
     if (state == 0) {
-        for (int b = t; b < a.n_partial; b += nt) {
+        for (int b = lane; b < a.n_partial; b += 64) {
             const double* p = a.partial + size_t(b) * 4;
             gmin = fmin(gmin, p[0]);
             gmax = fmax(gmax, p[1]);
             lmin = fmin(lmin, p[2]);
             gerr = fmax(gerr, p[3]);
         }
-        if (a.ll_part)
-            ll = strided_sum(a.ll_part, a.n_ll, t, nt);
+        if (a.ll_part) ll = strided_sum(a.ll_part, a.n_ll, lane, 64);
     }
-    gmin = block_reduce(gmin, 0, red);
-    gmax = block_reduce(gmax, 1, red);
-    lmin = block_reduce(lmin, 0, red);
-    gerr = block_reduce(gerr, 1, red);
-    ll = block_sum(ll, red);
-    if (t == 0) {
+    gmin = wave_reduce(gmin, 0);
+    gmax = wave_reduce(gmax, 1);
+    lmin = wave_reduce(lmin, 0);
+    gerr = wave_reduce(gerr, 1);
+    ll = wave_reduce(ll, 2);
+    if (lane == 0) {
         unsigned status = kQnSkipped;
         double info[7] = {0, 0, 0, 0, 0, 0, 0};
         if (state == 0) {

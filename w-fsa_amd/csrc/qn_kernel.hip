@@ -3,7 +3,7 @@
 // with ComputeExpX :53-56, ComputeG :148-160, ComputeLambdaNext :127-146,
 // Learner::LambdaUpdate src/Learner.cpp:438-462, HaltCondition :88-91 and
 // GetOptimizationInfo :68-86) after the objective/gradient kernels of the
-// same step: qn_update (thread per constraint) + qn_finish (one workgroup).  It keeps x, lambda and the next step's w_full in
+// same step: qn_update (wave per constraint) + qn_finish (one wave).  It keeps x, lambda and the next step's w_full in
 // HBM, so consecutive steps need nothing from the host; each step publishes
 // its info row to host-mapped memory and bumps the completion flag.
 //
@@ -26,7 +26,6 @@ namespace wfsa {
 namespace {
 
 constexpr int kQnUpdateBlock = 256;   // four constraints (one wavefront each) per block
-constexpr int kQnFinishBlock = 1024;
 
 __device__ __forceinline__ void wave_sync() {
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
@@ -147,7 +146,7 @@ __global__ __launch_bounds__(kQnUpdateBlock) void qn_update_kernel(QnArgs a) {
 // qn_finish: the info row of the step (the reductions of qn_update's
 // partials and, without the tail kernel, of the per-wave log-likelihood
 // partials in a fixed order), the halt decision, then the publication.
-__global__ __launch_bounds__(kQnFinishBlock) void qn_finish_kernel(QnArgs a) { qn_finish_block(a); }
+__global__ __launch_bounds__(64) void qn_finish_kernel(QnArgs a) { qn_finish_wave(a); }
 
 // initial w_full from x (qn_set_state)
 __global__ void qn_weights_kernel(const double* x, const int32_t* trim, int32_t n_full, double* w_full, double* ewp) {
@@ -176,7 +175,7 @@ hipError_t launch_qn_update(const QnArgs& a, hipStream_t stream) {
 }
 
 hipError_t launch_qn_finish(const QnArgs& a, hipStream_t stream) {
-    hipLaunchKernelGGL(qn_finish_kernel, dim3(1), dim3(kQnFinishBlock), 0, stream, a);
+    hipLaunchKernelGGL(qn_finish_kernel, dim3(1), dim3(64), 0, stream, a);
     return hipGetLastError();
 }
 

@@ -24,6 +24,7 @@
 #include <chrono>
 #include <cstdarg>
 #include <cstdlib>
+#include <queue>
 #include <cstdio>
 #include <cstring>
 #include <memory>
@@ -152,7 +153,7 @@ struct wfsa_dev {
     DevBuf<uint4> stream_w;   // 16-byte chunks
     int wide = 0;             // 32-bit stream words
     DevBuf<int32_t> bub, g_len, l_str, l_len;
-    DevBuf<double> p_lane;
+    DevBuf<int32_t> wave_first;   // [stream waves + 1] the per-iteration kernel's groups of each wave
     DevBuf<int64_t> g_base;
     int c_grid = 0, c_tables = 0;    // gradient pass (once, at preparation)
     int i_grid = 0, i_tables = 0;    // per-iteration pass (log-weights only)
@@ -161,6 +162,7 @@ struct wfsa_dev {
     DevBuf<double> fixed_grad;       // [n_params] gradient of the trivial words (constant)
     // bubbles
     int32_t n_bubbles = 0, n_small4 = 0, n_small = 0, n_big = 0, big_lds_edges = 2;
+    int32_t fin_wave = 0;   // the stream kernel's wave that runs the previous QN step's finish
     int b_waves = 0;
     DevBuf<int4> sm4_tbl, sm_tbl;
     DevBuf<int32_t> big_off, big_edge_base, big_eslot_ptr, big_eslot;
@@ -331,6 +333,11 @@ int enqueue_compiled(wfsa_dev* ctx, bool with_grad, bool want_logq, const unsign
                      int slot = -1, const wfsa::QnArgs* fin = nullptr);
 wfsa::BubbleArgs bubble_args(wfsa_dev* ctx, bool want_logq, const unsigned* halted, double* ll_part);
 bool bubbles_fused(wfsa_dev* ctx, bool want_logq);
+// waves per block of the stream kernel that take the small bubbles (64 each)
+int small_waves_per_block(int64_t n_small, int nblk) {
+    const int64_t waves = (n_small + kWave - 1) / kWave;
+    return int((waves + nblk - 1) / std::max(nblk, 1));
+}
 // byte offset of the big bubbles' staging in the stream kernel's LDS (after w)
 size_t big_stage_off(const wfsa_dev* ctx) { return (ctx->i_lds + 15) & ~size_t(15); }
 
@@ -488,20 +495,101 @@ int prepare(wfsa_dev* ctx, int level) {
     }
     const int64_t nc = int64_t(comp.size());
     const int32_t G = int32_t((nc + kWave - 1) / kWave);
+    // 16-byte chunks of 8 narrow / 4 wide words; chunk c of lane l at
+    // g_base + 64 c + l (chunk units); s_base in word (element) units; each
+    // lane's first chunk starts with the group header
+    const int per = ctx->wide ? 4 : 8, hdr = wfsa::stream_hdr_words(ctx->wide);
+    std::vector<int32_t> rows0(size_t(std::max(G, 1)), 0);   // rows of each group (sorted order)
+    for (int32_t g = 0; g < G; ++g) {
+        rows0[size_t(g)] = (h_main[size_t(comp[size_t(g) * kWave])] + hdr + per - 1) / per;
+        if (!ctx->wide && rows0[size_t(g)] > 0xffff)
+            return fail(WFSA_ERR_CAPACITY, "string %d: %d stream words exceed the narrow group header",
+                        comp[size_t(g) * kWave], h_main[size_t(comp[size_t(g) * kWave])]);
+    }
+    // the per-iteration kernel's geometry: w staged in LDS when it fits, 16
+    // waves per block, one block per CU (every block stages the whole table,
+    // so fewer blocks stage less: measured 1/CU beats 2/CU at c3)
+    {
+        const size_t table_bytes = size_t(ctx->n_params) * sizeof(double);
+        ctx->i_tables = table_bytes + 16 <= size_t(kLdsPerCu - 1024) ? 1 : 0;
+        ctx->i_lds = ctx->i_tables ? table_bytes + 16 : 0;   // + the zero slot, even count
+        if (const char* e = std::getenv("WFSA_IBLOCK")) ctx->i_block = std::max(64, std::min(1024, std::atoi(e))) & ~63;
+        const int i_wpb = ctx->i_block / kWave;
+        int i_per_cu = std::max(1, kIterWavesPerCu / i_wpb);
+        if (ctx->i_tables)
+            i_per_cu = std::min<int>(i_per_cu, int(size_t(kLdsPerCu) / std::max<size_t>(table_bytes, 1)));
+        if (const char* e = std::getenv("WFSA_IPERCU")) i_per_cu = std::min(i_per_cu, std::atoi(e));
+        i_per_cu = std::max(1, i_per_cu);
+        ctx->i_grid = int(std::max<int64_t>(1, std::min<int64_t>(int64_t(ctx->n_cu) * i_per_cu,
+                                                                 (int64_t(G) + i_wpb - 1) / i_wpb)));
+    }
+    // Groups dealt to the per-iteration kernel's waves, longest first, each
+    // to the least loaded wave (rows, plus the bubble work the kernel gives
+    // the first waves -- small bubbles, one per lane -- and the last -- big
+    // ones, one per wave; the big ones are estimated here from the counted
+    // record sizes: a string whose bubbles average more than 8 edges has at
+    // least one).  Each wave's groups are then laid out contiguously.
+    const int i_wpb = ctx->i_block / kWave, i_nw = ctx->i_grid * i_wpb;
+    std::vector<int32_t> order;
+    std::vector<int32_t> wave_first(size_t(i_nw) + 1, 0);
+    {
+        double small_cost = 8.0, big_cost = 8.0;
+        if (const char* e = std::getenv("WFSA_SMALL_COST")) small_cost = std::atof(e);
+        if (const char* e = std::getenv("WFSA_BIG_COST")) big_cost = std::atof(e);
+        double fin_cost = 8.0;
+        if (const char* e = std::getenv("WFSA_FIN_COST")) fin_cost = std::atof(e);
+        int64_t n_b = 0, n_big_est = 0;
+        for (int32_t i : comp) {
+            n_b += h_nb[size_t(i)];
+            if (h_nb[size_t(i)] > 0 && h_bub[size_t(i)] > wfsa::bubble_record_words(wfsa::kBubbleRegEdges) * h_nb[size_t(i)])
+                ++n_big_est;
+        }
+        const int nblk = ctx->i_grid;
+        const int small_wpb = small_waves_per_block(n_b - n_big_est, nblk);
+        const int64_t small_waves = (n_b - n_big_est + kWave - 1) / kWave;
+        std::vector<double> load(size_t(i_nw), 0.0);
+        for (int w = 0; w < i_nw; ++w) {
+            const int bid = w / i_wpb, wib = w % i_wpb;
+            if (wib < small_wpb && int64_t(bid) * small_wpb + wib < small_waves) load[size_t(w)] += small_cost;
+            if ((nblk - 1 - bid) + int64_t(nblk) * (i_wpb - 1 - wib) < n_big_est) load[size_t(w)] += big_cost;
+        }
+        // the QN finish: the wave after the big bubbles' (in their order)
+        {
+            const int64_t r = std::min<int64_t>(n_big_est, i_nw - 1);
+            const int bid = nblk - 1 - int(r % nblk), wib = i_wpb - 1 - int(r / nblk);
+            ctx->fin_wave = bid * i_wpb + wib;
+            load[size_t(ctx->fin_wave)] += fin_cost;
+        }
+        using Item = std::pair<double, int32_t>;
+        std::priority_queue<Item, std::vector<Item>, std::greater<Item>> heap;
+        for (int w = 0; w < i_nw; ++w) heap.push({load[size_t(w)], w});
+        std::vector<std::vector<int32_t>> lists(static_cast<size_t>(i_nw));
+        for (int32_t g = 0; g < G; ++g) {
+            Item it = heap.top();
+            heap.pop();
+            lists[size_t(it.second)].push_back(g);
+            it.first += rows0[size_t(g)];
+            heap.push(it);
+        }
+        order.reserve(size_t(G));
+        for (int w = 0; w < i_nw; ++w) {
+            wave_first[size_t(w)] = int32_t(order.size());
+            order.insert(order.end(), lists[size_t(w)].begin(), lists[size_t(w)].end());
+        }
+        wave_first[size_t(i_nw)] = G;
+    }
     std::vector<int64_t> g_base(size_t(G) + 1, 0), s_base(SZ, 0), b_base(SZ, 0);
     std::vector<int32_t> g_len(size_t(std::max(G, 1)), 0), l_str(size_t(G) * kWave, -1), l_len(size_t(G) * kWave, 0);
     std::vector<int32_t> b_first(SZ, 0);
-    // 16-byte chunks of 8 narrow / 4 wide words; chunk c of lane l at
-    // g_base + 64 c + l (chunk units); s_base in word (element) units
-    const int per = ctx->wide ? 4 : 8;
     int64_t chunks = 0, words = 0;
     for (int32_t g = 0; g < G; ++g) {
+        const int32_t src = order[size_t(g)];   // the group in sorted order
         g_base[size_t(g)] = chunks;
-        g_len[size_t(g)] = (h_main[size_t(comp[size_t(g) * kWave])] + per - 1) / per;
+        g_len[size_t(g)] = rows0[size_t(src)];
         for (int l = 0; l < kWave; ++l) {
-            const int64_t k = int64_t(g) * kWave + l;
-            if (k >= nc) break;
-            const int32_t str = comp[size_t(k)];
+            const int64_t k = int64_t(g) * kWave + l, ks = int64_t(src) * kWave + l;
+            if (ks >= nc) break;
+            const int32_t str = comp[size_t(ks)];
             l_str[size_t(k)] = str;
             l_len[size_t(k)] = h_main[size_t(str)];
             s_base[size_t(str)] = (chunks + l) * per;
@@ -556,13 +644,18 @@ int prepare(wfsa_dev* ctx, int level) {
     HIP_TRY(ctx->g_len.upload(g_len.data(), g_len.size(), s));
     HIP_TRY(ctx->l_str.upload(l_str.data(), l_str.size(), s));
     HIP_TRY(ctx->l_len.upload(l_len.data(), l_len.size(), s));
-    {   // p in lane order (coalesced in the per-iteration kernel)
-        std::vector<double> h_p(S > 0 ? size_t(S) : 1, 0.0), pl(l_str.size(), 0.0);
+    HIP_TRY(ctx->wave_first.upload(wave_first.data(), wave_first.size(), s));
+    {   // the group headers: p of each lane's string and the group's rows
+        std::vector<double> h_p(S > 0 ? size_t(S) : 1, 0.0), pl(std::max<size_t>(l_str.size(), 1), 0.0);
         if (S > 0) HIP_TRY(ctx->p.download(h_p.data(), size_t(S), s));
         HIP_TRY(hipStreamSynchronize(s));
         for (size_t k = 0; k < l_str.size(); ++k)
             if (l_str[k] >= 0) pl[k] = h_p[size_t(l_str[k])];
-        HIP_TRY(ctx->p_lane.upload(pl.data(), pl.size(), s));
+        DevBuf<double> d_pl;
+        HIP_TRY(d_pl.upload(pl.data(), pl.size(), s));
+        HIP_TRY(wfsa::launch_stream_headers(ctx->stream_w.ptr, ctx->g_base.ptr, ctx->g_len.ptr, d_pl.ptr, G,
+                                            ctx->wide, s));
+        HIP_TRY(hipStreamSynchronize(s));
     }
     ctx->n_groups = G;
     ctx->n_compiled = nc;
@@ -705,19 +798,6 @@ int prepare(wfsa_dev* ctx, int level) {
     const int per_cu = ctx->c_tables ? 1 : 2;
     ctx->c_grid = int(std::max<int64_t>(1, std::min<int64_t>(int64_t(ctx->n_cu) * per_cu, want_blocks)));
     if (ctx->c_tables >= 1) HIP_TRY(ctx->gpart.alloc(size_t(ctx->c_grid) * size_t(std::max(ctx->n_params, 1))));
-    // the per-iteration pass keeps only w in LDS: as many blocks per CU as fit
-    ctx->i_tables = table_bytes + 16 <= size_t(kLdsPerCu - 1024) ? 1 : 0;
-    ctx->i_lds = ctx->i_tables ? table_bytes + 16 : 0;   // + the zero slot, even count
-    if (const char* e = std::getenv("WFSA_IBLOCK")) ctx->i_block = std::max(64, std::min(1024, std::atoi(e))) & ~63;
-    const int i_wpb = ctx->i_block / kWave;
-    // one block per CU: every block stages the whole table, so fewer blocks
-    // stage less (measured: 1/CU beats 2/CU at c3 even at half the waves)
-    int i_per_cu = std::max(1, kIterWavesPerCu / i_wpb);
-    if (ctx->i_tables) i_per_cu = std::min<int>(i_per_cu, int(size_t(kLdsPerCu) / std::max<size_t>(table_bytes, 1)));
-    if (const char* e = std::getenv("WFSA_IPERCU")) i_per_cu = std::min(i_per_cu, std::atoi(e));
-    i_per_cu = std::max(1, i_per_cu);
-    ctx->i_grid = int(std::max<int64_t>(1, std::min<int64_t>(int64_t(ctx->n_cu) * i_per_cu,
-                                                             (int64_t(G) + i_wpb - 1) / i_wpb)));
     HIP_TRY(ctx->fixed_grad.alloc(size_t(std::max(ctx->n_params, 1))));
 
     // traversal fallback lists
@@ -726,7 +806,7 @@ int prepare(wfsa_dev* ctx, int level) {
         ctx->fall_grid[t] = fb[t].empty() ? 0 : trav_grid(ctx->cfg[t], ctx->n_cu, int64_t(fb[t].size()));
         if (!fb[t].empty()) HIP_TRY(ctx->fall[t].upload(fb[t].data(), fb[t].size(), s));
     }
-    const size_t waves = std::max(size_t(ctx->c_grid) * waves_per_block, size_t(ctx->i_grid + 1) * size_t(i_wpb)) +
+    const size_t waves = std::max(size_t(ctx->c_grid) * waves_per_block, size_t(ctx->i_grid) * size_t(ctx->i_block / kWave)) +
                          size_t(ctx->b_waves) +
                          size_t(ctx->fall_grid[0]) * size_t(ctx->cfg[0].waves_per_block) +
                          size_t(ctx->fall_grid[1]) * size_t(ctx->cfg[1].waves_per_block);
@@ -786,7 +866,7 @@ int enqueue_compiled(wfsa_dev* ctx, bool with_grad, bool want_logq, const unsign
         c.g_len = ctx->g_len.ptr;
         c.l_str = ctx->l_str.ptr;
         c.l_len = ctx->l_len.ptr;
-        c.p_lane = ctx->p_lane.ptr;
+        c.wave_first = ctx->wave_first.ptr;
         c.n_groups = ctx->n_groups;
         c.n_params = np;
         c.tables = tables;
@@ -806,11 +886,13 @@ int enqueue_compiled(wfsa_dev* ctx, bool with_grad, bool want_logq, const unsign
         size_t lds = with_grad ? ctx->c_lds : ctx->i_lds;
         if (fin && !with_grad && tables >= 1) {
             c.fin = *fin;
-            c.service = 1;
+            c.fin_on = 1;
+            c.fin_wave = ctx->fin_wave;
         }
         if (!with_grad && bubbles_fused(ctx, want_logq)) {
             c.bub = bubble_args(ctx, false, halted, nullptr);
             c.bub_on = 1;
+            c.bub.small_wpb = small_waves_per_block(ctx->n_small4 + ctx->n_small, ctx->i_grid);
             if (ctx->n_big > 0) {
                 c.bub.big_lds_edges = ctx->big_lds_edges;
                 c.bub.big_lds_off = int32_t(big_stage_off(ctx));
@@ -858,6 +940,11 @@ wfsa::BubbleArgs bubble_args(wfsa_dev* ctx, bool want_logq, const unsigned* halt
     b.ll_part = ll_part;
     b.logq = want_logq ? ctx->logq.ptr : nullptr;
     b.halted = halted;
+    static const int dbg = [] {
+        const char* e = std::getenv("WFSA_BUB_DBG");
+        return e ? std::atoi(e) : 0;
+    }();
+    b.dbg = dbg;
     return b;
 }
 
@@ -866,14 +953,14 @@ int enqueue_bubbles(wfsa_dev* ctx, bool want_logq, const unsigned* halted, int32
     return WFSA_OK;
 }
 
-// The small bubbles ride in the stream kernel's waves and the big ones in
-// its service block when the kernel stages the weights (and log q is not
-// wanted: both would write the strings' entries).
+// The bubbles ride in the stream kernel's waves when the kernel stages the
+// weights (and log q is not wanted: both would write the strings' entries).
 bool bubbles_fused(wfsa_dev* ctx, bool want_logq) {
     if (!(ctx->n_bubbles > 0 && !want_logq && ctx->n_groups > 0 && ctx->i_tables >= 1 && !ctx->side_stream &&
           ctx->fuse_bubbles))
         return false;
-    // the big bubbles' staging must fit beside w
+    // at most one chunk of 64 small bubbles per wave; the big bubbles' staging must fit beside w
+    if (small_waves_per_block(ctx->n_small4 + ctx->n_small, ctx->i_grid) > ctx->i_block / kWave) return false;
     return ctx->n_big == 0 || big_stage_off(ctx) + size_t(ctx->i_block / kWave) *
                                                        size_t(wfsa::big_stage_bytes(ctx->big_lds_edges)) <=
                                   size_t(kLdsPerCu - 1024);
@@ -896,7 +983,7 @@ int enqueue_evaluation(wfsa_dev* ctx, bool want_logq, const unsigned* halted, in
         HIP_TRY(hipStreamWaitEvent(ctx->side_stream, ctx->fork, 0));
     }
     const bool fusedb = bubbles_fused(ctx, want_logq);
-    // the stream kernel's ll partials: one per stream wave (its service block writes none)
+    // the stream kernel's ll partials: one per stream wave
     int32_t wave_off = ctx->n_groups > 0 ? ctx->i_grid * (ctx->i_block / kWave) : 0;
     if (ctx->n_bubbles > 0 && side) {
         if (int rc = enqueue_bubbles(ctx, want_logq, halted, wave_off, ctx->side_stream)) return rc;
