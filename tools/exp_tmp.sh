@@ -14,4 +14,4 @@ for r in csv.DictReader(open(sys.argv[1])):
 PY
   grep -o '"value": [0-9.]*' $R/$name.log
 }
-run base A=1 && run d3 WFSA_FBS_DBG=3 && run sc0 WFSA_SMALL_COST=0 WFSA_BIG_COST=0 && run sc16 WFSA_SMALL_COST=16 WFSA_BIG_COST=16 && run sc24 WFSA_SMALL_COST=24 WFSA_BIG_COST=24
+run f0 A=1 && run d5 WFSA_FBS_DBG=5 && run nf0 WFSA_FUSE_BUBBLES=0 WFSA_SMALL_COST=0 WFSA_BIG_COST=0 && run nf3 WFSA_FBS_DBG=3 WFSA_FUSE_BUBBLES=0

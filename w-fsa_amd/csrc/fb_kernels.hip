@@ -820,7 +820,8 @@ __global__ __launch_bounds__(kBubbleBlock) void bubble_kernel(BubbleArgs a) {
 // The first set is issued before the weights are staged and the bubbles
 // evaluated, so its latency hides behind that work (both sets would spill).
 // DBG (timing experiments only, WFSA_FBS_DBG): 1 no table gathers, 3 no
-// stream pass at all, 4 neither stream pass nor table staging, 5 return at once
+// stream pass at all, 4 neither stream pass nor table staging, 5 return at once, 6 / 7
+// prefetch sets of 2 / 6 rows, 8 no bubble code, 9 stream loads only
 template <bool WIDE, bool W_LDS, bool MULTI, int DBG = 0>
 __global__ __launch_bounds__(1024) void fbs_kernel(CompiledArgs a) {
     extern __shared__ __attribute__((aligned(16))) double lds[];
@@ -831,8 +832,9 @@ __global__ __launch_bounds__(1024) void fbs_kernel(CompiledArgs a) {
     const int bid = int(blockIdx.x);
     const int w = int(threadIdx.x) / kWave;
     const int gw = __builtin_amdgcn_readfirstlane(bid * wpb + w);
+    const unsigned halted = a.halted ? *a.halted : 0u;   // (before the finish below may set it)
     if (a.fin_on && gw == a.fin_wave) qn_finish_wave(a.fin);   // the previous QN step's finish
-    if (a.halted && *a.halted) return;
+    if (halted) return;
     if (DBG == 5) return;
     const uint32_t zslot = uint32_t(a.n_params);
     // this wave's run of chunk rows
@@ -841,13 +843,14 @@ __global__ __launch_bounds__(1024) void fbs_kernel(CompiledArgs a) {
     const int rows = int((a.g_base[g1] - cb) / kWave);
     const int last = max(rows - 1, 0);   // no groups: row 0 of the slack after the last group
     const uint4* st = a.stream + cb + lane;
-    constexpr int D = kStreamPrefetch;
+    constexpr int D = DBG == 6 ? 2 : (DBG == 7 ? 6 : kStreamPrefetch);
     uint4 A[D], B[D];
     auto load = [&](uint4 (&r)[D], int c0) {
 #pragma unroll
         for (int d = 0; d < D; ++d) r[d] = st[int64_t(kWave) * min(c0 + d, last)];
     };
-    if (DBG < 3) load(A, 0);
+    constexpr bool kStreams = DBG != 3 && DBG != 4;   // (timing experiments)
+    if (kStreams) load(A, 0);
     if (W_LDS && DBG != 4) {
         // stage w[0, n_params] in 16-byte pieces, all of a thread's loads
         // issued before its first store (loads and stores unconditional --
@@ -868,7 +871,7 @@ __global__ __launch_bounds__(1024) void fbs_kernel(CompiledArgs a) {
     }
     const double* wsrc = W_LDS ? lds : a.w;
     double ll_acc = 0.0;
-    if (a.bub_on) {   // this wave's bubbles, before its streams
+    if (a.bub_on && DBG != 8) {   // this wave's bubbles, before its streams
         // small ones, one per lane, from the first small_wpb waves of every
         // block (spread over all CUs)
         if (w < a.bub.small_wpb) {   // small_wpb <= waves per block (bubbles_fused)
@@ -888,7 +891,7 @@ __global__ __launch_bounds__(1024) void fbs_kernel(CompiledArgs a) {
             for (int i = r; i < a.bub.n_big; i += nw) ll_acc += big_bubble(a.bub, i, lsd, lw, lw, lw + E);
         }
     }
-    if (DBG < 3) load(B, D);
+    if (kStreams) load(B, D);
     double p = 0.0, acc0 = 0.0, acc1 = 0.0;
     int hdr = 0, grp = g0 - 1;   // the next header row, the current group
     auto flush = [&]() {   // the lane's string of the current group is complete
@@ -917,6 +920,10 @@ __global__ __launch_bounds__(1024) void fbs_kernel(CompiledArgs a) {
                 v.z = WIDE ? 0xffffffffu : (v.z | 0xffffu);
             }
             const uint32_t vw[4] = {v.x, v.y, v.z, v.w};
+            if (DBG == 9) {   // loads only
+                acc0 += double(vw[0] ^ vw[1] ^ vw[2] ^ vw[3]);
+                continue;
+            }
             bool multi = false;
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
@@ -954,7 +961,7 @@ __global__ __launch_bounds__(1024) void fbs_kernel(CompiledArgs a) {
             }
         }
     };
-    if (DBG < 3 && rows > 0) {
+    if (kStreams && rows > 0) {
         for (int c0 = 0;;) {   // A holds rows [c0, c0 + D), B [c0 + D, c0 + 2D)
             apply(A, c0);
             if (c0 + D >= rows) break;
@@ -966,8 +973,16 @@ __global__ __launch_bounds__(1024) void fbs_kernel(CompiledArgs a) {
         }
     }
     flush();
+    // one log-likelihood partial per block (the QN finish sums them)
+    __shared__ double wsum[1024 / kWave];
     ll_acc = wave_sum(ll_acc);
-    if (lane == 0) a.ll_part[gw] = ll_acc;
+    if (lane == 0) wsum[w] = ll_acc;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        double t = 0.0;
+        for (int i = 0; i < wpb; ++i) t += wsum[i];
+        a.ll_part[bid] = t;
+    }
     // this block's slice of the per-edge weights and the zeroed result, for
     // the kernels after this one (nothing in this launch reads them)
     if (W_LDS) edge_weight_slice(a, bid, nblk);
@@ -1109,7 +1124,11 @@ hipError_t configure_kernels(int max_dynamic_lds) {
                          reinterpret_cast<const void*>(&fbs_kernel<false, true, false, 1>),
                          reinterpret_cast<const void*>(&fbs_kernel<false, true, false, 3>),
                          reinterpret_cast<const void*>(&fbs_kernel<false, true, false, 4>),
-                         reinterpret_cast<const void*>(&fbs_kernel<false, true, false, 5>)};
+                         reinterpret_cast<const void*>(&fbs_kernel<false, true, false, 5>),
+                         reinterpret_cast<const void*>(&fbs_kernel<false, true, false, 6>),
+                         reinterpret_cast<const void*>(&fbs_kernel<false, true, false, 7>),
+                         reinterpret_cast<const void*>(&fbs_kernel<false, true, false, 8>),
+                         reinterpret_cast<const void*>(&fbs_kernel<false, true, false, 9>)};
     for (const void* f : fns) {   // (static LDS counts against the same 160 KiB)
         hipFuncAttributes attr{};
         hipError_t e = hipFuncGetAttributes(&attr, f);
@@ -1172,6 +1191,22 @@ hipError_t launch_compiled(const CompiledArgs& a, int grid, int block, size_t ld
         }
         if (dbg == 5) {
             hipLaunchKernelGGL((fbs_kernel<false, true, false, 5>), g, b, lds, stream, a);
+            return hipGetLastError();
+        }
+        if (dbg == 6) {
+            hipLaunchKernelGGL((fbs_kernel<false, true, false, 6>), g, b, lds, stream, a);
+            return hipGetLastError();
+        }
+        if (dbg == 7) {
+            hipLaunchKernelGGL((fbs_kernel<false, true, false, 7>), g, b, lds, stream, a);
+            return hipGetLastError();
+        }
+        if (dbg == 8) {
+            hipLaunchKernelGGL((fbs_kernel<false, true, false, 8>), g, b, lds, stream, a);
+            return hipGetLastError();
+        }
+        if (dbg == 9) {
+            hipLaunchKernelGGL((fbs_kernel<false, true, false, 9>), g, b, lds, stream, a);
             return hipGetLastError();
         }
         const int key = (a.tables >= 1 ? 4 : 0) + (a.wide ? 2 : 0) + (a.multi ? 1 : 0);

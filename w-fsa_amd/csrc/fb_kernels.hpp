@@ -277,7 +277,7 @@ struct CompiledArgs {
     double* ew_out;
     EdgeRec* erec_out;
     double* out;             // [1 + n_params], zeroed by block 0
-    double* ll_part;         // [waves in grid]
+    double* ll_part;         // [waves in grid] (per-iteration stream kernel: [blocks])
     double* logq;            // [S] or null
     const unsigned* halted;  // device-resident QN run: nonzero = skip (or null)
 };

@@ -983,8 +983,8 @@ int enqueue_evaluation(wfsa_dev* ctx, bool want_logq, const unsigned* halted, in
         HIP_TRY(hipStreamWaitEvent(ctx->side_stream, ctx->fork, 0));
     }
     const bool fusedb = bubbles_fused(ctx, want_logq);
-    // the stream kernel's ll partials: one per stream wave
-    int32_t wave_off = ctx->n_groups > 0 ? ctx->i_grid * (ctx->i_block / kWave) : 0;
+    // the ll partials: the stream kernel's blocks, then the other kernels' waves
+    int32_t wave_off = ctx->n_groups > 0 ? ctx->i_grid : 0;   // one per stream-kernel block
     if (ctx->n_bubbles > 0 && side) {
         if (int rc = enqueue_bubbles(ctx, want_logq, halted, wave_off, ctx->side_stream)) return rc;
         HIP_TRY(hipEventRecord(ctx->join, ctx->side_stream));
