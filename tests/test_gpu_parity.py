@@ -274,3 +274,29 @@ def test_async_begin_end_and_native_epoch_loop():
         if halt:
             break
     assert len(rows_a) == len(rows_b)
+
+
+def test_single_rank_communicator_path():
+    """The data-parallel path (SetCommunicator: RCCL all-reduce of [LL, grad]
+    each step, src/main.cpp's loop run natively) at one rank equals the
+    communicator-free path: the host QN step and the device-resident loop."""
+    import wfsa_amd as W
+    syn = W.Synthetic(n_states=64, degree=8, vocab=16, emissions=1, n_strings=3000, max_len=64, seed=9)
+    sym, off, wt = syn.corpus()
+    fsa = W.Fsa.read_text(syn.wfsa_text)
+    plain, comm = W.QuasiNewtonLearner(0), W.QuasiNewtonLearner(0)
+    comm.SetCommunicator(1, 0, W.Device.comm_unique_id())
+    for lrn in (plain, comm):
+        lrn.BuildFromPacked(fsa, sym, off, wt)
+        lrn.Finalize()
+        lrn.Init(7)
+    assert comm.info()["n_strings"] == plain.info()["n_strings"]
+    ra = [plain.OptimizationStep(1.0, -1.0)[0] for _ in range(3)]
+    rb = [comm.OptimizationStep(1.0, -1.0)[0] for _ in range(3)]
+    ra += plain.Run(5, 1.0, -1.0)
+    rb += comm.Run(5, 1.0, -1.0)
+    assert len(ra) == len(rb) == 8
+    for r, q in zip(ra, rb):
+        for u, v in zip(r[:5], q[:5]):
+            assert _close(u, v, rel=1e-11, atol=1e-14)
+    np.testing.assert_allclose(comm.x(), plain.x(), rtol=1e-11, atol=1e-13)
