@@ -92,7 +92,7 @@ typedef struct {
     double prepare_ms;         /* structural pass + stream compilation      */
     double compiled_kernel_ms; /* sum over calls of the compiled kernel     */
     int32_t graph;             /* last call replayed a captured hipGraph    */
-    int32_t reserved;
+    int32_t dense;             /* the dense fp64 MFMA path serves the model */
     /* filled by wfsa_learner_stats (zero from wfsa_dev_get_stats): host time
      * of the learner's optimization steps, summed over host_steps steps --
      * before the device call is enqueued, overlapped with it, waiting for

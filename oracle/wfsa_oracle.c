@@ -492,6 +492,9 @@ typedef struct {
     double* alpha;      /* [(L+1) * N] */
     double* beta;
     int cap_L;
+    int* eb;            /* [N * 256] single-byte emission of state s with byte b, or -1 */
+    int* oth_ptr;       /* [N + 1] the other (epsilon / multi-byte) emissions of s ... */
+    int* oth;           /* ... as indices into s's emission list */
 } trellis_ws_t;
 
 static int eps_topo(const fsa_t* f, int* order, char* err, int errlen) {
@@ -523,6 +526,36 @@ static int eps_topo(const fsa_t* f, int* order, char* err, int errlen) {
     return OR_OK;
 }
 
+/* emission lookup: every emission of state s is either the single byte b
+ * (eb[s*256+b]) or in s's "other" list; the matching rule is unchanged
+ * (inc/Recognize.h:52: the emission must be a prefix of the rest of the word) */
+static void trellis_tables(const fsa_t* f, trellis_ws_t* ws) {
+    if (ws->eb) return;
+    int N = ws->N;
+    ws->eb = xrealloc(NULL, sizeof(int) * (size_t)N * 256);
+    ws->oth_ptr = xrealloc(NULL, sizeof(int) * (size_t)(N + 1));
+    for (size_t k = 0; k < (size_t)N * 256; ++k) ws->eb[k] = -1;
+    int n_oth = 0;
+    for (int s = 0; s < N; ++s)
+        for (int64_t e = 0; e < f->st.a[s].em.n; ++e) if (f->st.a[s].em.a[e].len != 1) ++n_oth;
+    ws->oth = xrealloc(NULL, sizeof(int) * (size_t)(n_oth + 1));
+    n_oth = 0;
+    for (int s = 0; s < N; ++s) {
+        ws->oth_ptr[s] = n_oth;
+        const state_t* st = &f->st.a[s];
+        for (int64_t e = 0; e < st->em.n; ++e) {
+            const emis_t* em = &st->em.a[e];
+            if (em->len == 1) ws->eb[(size_t)s * 256 + (unsigned char)em->str[0]] = (int)e;
+            else ws->oth[n_oth++] = (int)e;
+        }
+    }
+    ws->oth_ptr[N] = n_oth;
+}
+
+static void trellis_free(trellis_ws_t* ws) {
+    free(ws->topo); free(ws->alpha); free(ws->beta); free(ws->eb); free(ws->oth_ptr); free(ws->oth);
+}
+
 static void trellis_alloc(trellis_ws_t* ws, int L) {
     if (L + 1 > ws->cap_L) {
         ws->cap_L = L + 1;
@@ -532,21 +565,37 @@ static void trellis_alloc(trellis_ws_t* ws, int L) {
     }
 }
 
-/* weight function: w(j) for param j (index -1 -> 0) */
-typedef double (*wfun_t)(const void* ctx, int j);
+/* Calls BODY for every emission em (index EI in state D's list) of state D
+ * that matches the word at position i. */
+#define FOR_MATCHING_EMISSIONS(D, EI, BODY)                                          \
+    do {                                                                             \
+        const state_t* ds_ = &f->st.a[(D)];                                          \
+        if (i < L) {                                                                 \
+            int EI = ws->eb[(size_t)(D) * 256 + (unsigned char)word[i]];              \
+            if (EI >= 0) { BODY }                                                    \
+        }                                                                            \
+        for (int k_ = ws->oth_ptr[(D)]; k_ < ws->oth_ptr[(D) + 1]; ++k_) {           \
+            int EI = ws->oth[k_];                                                    \
+            const emis_t* e_ = &ds_->em.a[EI];                                       \
+            if (i + e_->len > L) continue;                                           \
+            if (memcmp(word + i, e_->str, (size_t)e_->len) != 0) continue;           \
+            { BODY }                                                                 \
+        }                                                                            \
+    } while (0)
 
-/* Forward-backward on one string.  Returns q (not log).  If counts != NULL,
- * adds scale * E[count_j] into counts[j] for every Fsa param j.  With
- * wf == NULL all weights are log 1 (counting semiring; q = path count). */
+/* Forward-backward on one string.  Returns q (not log).  ew[j] = exp(w_j)
+ * for Fsa parameter j; NULL = all weights 1 (counting semiring: q = path
+ * count).  If counts != NULL, adds scale * E[count_j] into counts[j]. */
 static double trellis_string(const fsa_t* f, trellis_ws_t* ws, const char* word, int L,
-                             wfun_t wf, const void* wctx, double* counts, double scale,
+                             const double* ew, double* counts, double scale,
                              unsigned char* used) {
     int N = ws->N;
+    trellis_tables(f, ws);
     trellis_alloc(ws, L);
     double* A = ws->alpha; double* B = ws->beta;
     memset(A, 0, sizeof(double) * (size_t)(L + 1) * (size_t)N);
     memset(B, 0, sizeof(double) * (size_t)(L + 1) * (size_t)N);
-#define W(j) ((j) < 0 ? 0.0 : (wf ? wf(wctx, (j)) : 0.0))
+#define EW(j) ((j) < 0 || !ew ? 1.0 : ew[(j)])
     A[f->start] = 1.0;
     for (int i = 0; i <= L; ++i) {
         double* Ai = A + (size_t)i * N;
@@ -558,13 +607,11 @@ static double trellis_string(const fsa_t* f, trellis_ws_t* ws, const char* word,
             for (int64_t t = 0; t < st->tr.n; ++t) {
                 const trans_t* tr = &st->tr.a[t];
                 if (tr->dst == f->end) continue;
-                const state_t* ds = &f->st.a[tr->dst];
-                for (int64_t e = 0; e < ds->em.n; ++e) {
-                    const emis_t* em = &ds->em.a[e];
-                    if (i + em->len > L) continue;
-                    if (memcmp(word + i, em->str, (size_t)em->len) != 0) continue;
-                    A[(size_t)(i + em->len) * N + tr->dst] += a * exp(W(tr->index) + W(em->index));
-                }
+                const double wt = EW(tr->index);
+                FOR_MATCHING_EMISSIONS(tr->dst, ei, {
+                    const emis_t* em = &ds_->em.a[ei];
+                    A[(size_t)(i + em->len) * N + tr->dst] += a * (wt * EW(em->index));
+                });
             }
         }
     }
@@ -574,7 +621,7 @@ static double trellis_string(const fsa_t* f, trellis_ws_t* ws, const char* word,
     for (int s = 0; s < N; ++s) {
         const state_t* st = &f->st.a[s];
         for (int64_t t = 0; t < st->tr.n; ++t) if (st->tr.a[t].dst == f->end) {
-            double we = exp(W(st->tr.a[t].index));
+            double we = EW(st->tr.a[t].index);
             BL[s] += we;
             q += AL[s] * we;
         }
@@ -588,13 +635,11 @@ static double trellis_string(const fsa_t* f, trellis_ws_t* ws, const char* word,
             for (int64_t t = 0; t < st->tr.n; ++t) {
                 const trans_t* tr = &st->tr.a[t];
                 if (tr->dst == f->end) continue;
-                const state_t* ds = &f->st.a[tr->dst];
-                for (int64_t e = 0; e < ds->em.n; ++e) {
-                    const emis_t* em = &ds->em.a[e];
-                    if (i + em->len > L) continue;
-                    if (memcmp(word + i, em->str, (size_t)em->len) != 0) continue;
-                    acc += exp(W(tr->index) + W(em->index)) * B[(size_t)(i + em->len) * N + tr->dst];
-                }
+                const double wt = EW(tr->index);
+                FOR_MATCHING_EMISSIONS(tr->dst, ei, {
+                    const emis_t* em = &ds_->em.a[ei];
+                    acc += (wt * EW(em->index)) * B[(size_t)(i + em->len) * N + tr->dst];
+                });
             }
             Bi[s] += acc;
         }
@@ -610,33 +655,38 @@ static double trellis_string(const fsa_t* f, trellis_ws_t* ws, const char* word,
                     const trans_t* tr = &st->tr.a[t];
                     if (tr->dst == f->end) {
                         if (i != L) continue;
-                        double xi = a * exp(W(tr->index)) / q;
+                        double xi = a * EW(tr->index) / q;
                         if (xi > 0 && tr->index >= 0) {
                             if (counts) counts[tr->index] += scale * xi;
                             if (used) used[tr->index] = 1;
                         }
                         continue;
                     }
-                    const state_t* ds = &f->st.a[tr->dst];
-                    for (int64_t e = 0; e < ds->em.n; ++e) {
-                        const emis_t* em = &ds->em.a[e];
-                        if (i + em->len > L) continue;
-                        if (memcmp(word + i, em->str, (size_t)em->len) != 0) continue;
+                    const double wt = EW(tr->index);
+                    FOR_MATCHING_EMISSIONS(tr->dst, ei, {
+                        const emis_t* em = &ds_->em.a[ei];
                         double b = B[(size_t)(i + em->len) * N + tr->dst];
-                        double xi = a * exp(W(tr->index) + W(em->index)) * b / q;
-                        if (!(xi > 0)) continue;
-                        if (tr->index >= 0) { if (counts) counts[tr->index] += scale * xi; if (used) used[tr->index] = 1; }
-                        if (em->index >= 0) { if (counts) counts[em->index] += scale * xi; if (used) used[em->index] = 1; }
-                    }
+                        double xi = a * (wt * EW(em->index)) * b / q;
+                        if (xi > 0) {
+                            if (tr->index >= 0) { if (counts) counts[tr->index] += scale * xi; if (used) used[tr->index] = 1; }
+                            if (em->index >= 0) { if (counts) counts[em->index] += scale * xi; if (used) used[em->index] = 1; }
+                        }
+                    });
                 }
             }
         }
     }
-#undef W
+#undef EW
     return q;
 }
 
-static double learner_wfun(const void* ctx, int j) { return get_weight((const learner_t*)ctx, j); }
+/* exp of the weights in GetWeight form, by Fsa parameter */
+static double* exp_weights(const learner_t* L, const double* w_full) {
+    double* ew = xrealloc(NULL, sizeof(double) * (size_t)(L->n_full + 1));
+    for (int j = 0; j < L->n_full; ++j) ew[j] = exp(w_full ? w_full[j] : get_weight(L, j));
+    return ew;
+}
+
 
 /* ------------------------------------------------------------------------ */
 /* public API                                                                 */
@@ -721,7 +771,7 @@ static learner_t* build_common(learner_t* L, int mode, int64_t max_paths, char* 
         unsigned char* used = calloc((size_t)(nf + 1), 1);
         L->n_paths = 0;
         for (int64_t i = 0; i < NC; ++i) {
-            double q = trellis_string(f, &ws, cp->words.a[i], cp->lens.a[i], NULL, NULL, NULL, 0, used);
+            double q = trellis_string(f, &ws, cp->words.a[i], cp->lens.a[i], NULL, NULL, 0, used);
             L->path_count[i] = (int64_t)q;
             if (q > 0) {
                 L->common_support += cp->w.a[i];
@@ -730,7 +780,7 @@ static learner_t* build_common(learner_t* L, int mode, int64_t max_paths, char* 
             } else { L->aux_params++; L->aux_hessian -= log(cp->w.a[i]); }
         }
         for (int j = 0; j < nf; ++j) if (used[j]) L->trimmed[j] = 0;
-        free(used); free(ws.topo); free(ws.alpha); free(ws.beta);
+        free(used); trellis_free(&ws);
     }
     L->S = S;
     trim(L, x_full, Ccol_full);
@@ -851,14 +901,15 @@ static void modeled_probs(learner_t* L) {
         char err[64];
         eps_topo(&L->fsa, ws.topo, err, 64);
         double* counts = calloc((size_t)L->n_full + 1, sizeof(double));
+        double* ew = exp_weights(L, NULL);
         for (int64_t s = 0; s < S; ++s) {
             int64_t i = L->str_of[s];
             double q = trellis_string(&L->fsa, &ws, L->corpus.words.a[i], L->corpus.lens.a[i],
-                                      learner_wfun, L, counts, -L->p[s], NULL);
+                                      ew, counts, -L->p[s], NULL);
             L->logq[s] = log(q);
         }
         for (int j = 0; j < L->n_full; ++j) if (L->trimmed[j] >= 0) L->grad[L->trimmed[j]] = counts[j];
-        free(counts); free(ws.topo); free(ws.alpha); free(ws.beta);
+        free(ew); free(counts); trellis_free(&ws);
     }
 }
 
@@ -981,8 +1032,6 @@ int oracle_qn_halt(const learner_t* L, double tol) {            /* :88-91 */
     return L->grad_error <= tol && fabs(L->g_min) <= tol && fabs(L->g_max) <= tol;
 }
 
-static double wfull_fun(const void* ctx, int j) { return ((const double*)ctx)[j]; }
-
 /* per-string trellis evaluation at Fsa-indexed log-weights w_full (index -1
  * -> 0): writes logq per corpus string and grad_full[j] = -sum p E[count_j]
  * over strings with q > 0 using the renormalized corpus weights.  Used to
@@ -993,17 +1042,18 @@ int oracle_trellis_eval(learner_t* L, const double* w_full, double* logq_corpus,
     ws.N = (int)L->fsa.st.n;
     ws.topo = xrealloc(NULL, sizeof(int) * (size_t)(ws.N + 1));
     if (eps_topo(&L->fsa, ws.topo, err, errlen) != OR_OK) { free(ws.topo); return OR_ERR; }
+    double* ew = exp_weights(L, w_full);
     double ll = 0;
     for (int j = 0; j < L->n_full; ++j) grad_full[j] = 0;
     for (int64_t i = 0; i < L->corpus.words.n; ++i) {
         double pw = L->corpus.w.a[i];
         double q = trellis_string(&L->fsa, &ws, L->corpus.words.a[i], L->corpus.lens.a[i],
-                                  wfull_fun, w_full, grad_full, -pw, NULL);
+                                  ew, grad_full, -pw, NULL);
         logq_corpus[i] = q > 0 ? log(q) : -INFINITY;
         if (q > 0) ll += pw * log(q);
     }
     *loglik = ll;
-    free(ws.topo); free(ws.alpha); free(ws.beta);
+    free(ew); trellis_free(&ws);
     return OR_OK;
 }
 

@@ -1,0 +1,165 @@
+"""GPU parity of the dense-automaton path (fp64 MFMA GEMMs, dense_path.hip;
+BASELINE.json configs[4], SURVEY.md 8d "c5") against the CPU oracle's
+trellis restatement and against the sparse trellis kernels on the same
+inputs.  All tests need a gfx950 device."""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def _close(a, b, rel, atol=1e-13):
+    return abs(a - b) <= max(atol, rel * max(abs(a), abs(b)))
+
+
+def _device(fsa, sym, off, p, monkeypatch, dense):
+    import wfsa_amd as W
+    monkeypatch.setenv("WFSA_DENSE", "1" if dense else "0")
+    dev = W.Device(0)
+    dev.load_model(fsa)
+    dev.load_corpus(sym, off, p)
+    assert dev.stats()["dense"] == (1 if dense else 0)
+    return dev
+
+
+def _oracle(text, sym, off, wt, w_by_name):
+    from oracle import Oracle, TRELLIS
+    o = Oracle.from_arrays(text, sym, off, wt, mode=TRELLIS)
+    names = o.full_param_names()
+    ll, logq, grad = o.trellis_eval(np.array([w_by_name[n] for n in names]))
+    return ll, logq, dict(zip(names, grad))
+
+
+@pytest.mark.parametrize("spec", [
+    dict(n_states=64, vocab=8, emissions=3, n_strings=400, max_len=24),     # partial emission sets
+    dict(n_states=100, vocab=16, emissions=16, n_strings=300, max_len=40),  # every state emits every symbol; np padded
+    dict(n_states=200, vocab=5, emissions=2, n_strings=700, max_len=70),    # two row tiles, ragged slots
+])
+def test_dense_matches_oracle_random_weights(spec, monkeypatch):
+    import wfsa_amd as W
+    syn = W.Synthetic(degree=1, dense=True, seed=13, **spec)
+    sym, off, wt = syn.corpus()
+    fsa = W.Fsa.read_text(syn.wfsa_text)
+    names = fsa.param_names()
+    p = wt / wt.sum()
+    w = np.random.default_rng(5).normal(-1.0, 0.8, size=len(names))
+    dev = _device(fsa, sym, off, p, monkeypatch, dense=True)
+    rec, pc, used = dev.recognize()
+    assert rec.all() and used.all()
+    ll, grad, logq = dev.objective_grad(w)
+    oll, ologq, ograd = _oracle(syn.wfsa_text, sym, off, wt, dict(zip(names, w)))
+    np.testing.assert_allclose(logq, ologq, rtol=1e-12)
+    assert _close(ll, oll, rel=1e-12)
+    np.testing.assert_allclose(grad, [ograd[n] for n in names], rtol=1e-10, atol=1e-17)
+
+
+def test_dense_equals_sparse_kernels(monkeypatch):
+    """same model, same inputs: the MFMA path and the trellis kernels agree on
+    recognition, path counts, used parameters, log q and the gradient"""
+    import wfsa_amd as W
+    # small enough for the trellis kernels' LDS slab (a dense 64-state model
+    # is not: it fails there with WFSA_ERR_CAPACITY)
+    syn = W.Synthetic(n_states=16, degree=1, vocab=6, emissions=2, dense=True, n_strings=500, max_len=9, seed=3)
+    sym, off, wt = syn.corpus()
+    # a few strings the automaton cannot emit (a byte nobody emits) and an empty one
+    extra = [b"\x01", b"", syn_bad := b"zz\x02"]
+    lens = np.diff(off)
+    strings = [bytes(sym[off[i]:off[i + 1]]) for i in range(len(lens))] + extra
+    sym2 = np.frombuffer(b"".join(strings), dtype=np.uint8).copy()
+    off2 = np.concatenate([[0], np.cumsum([len(s) for s in strings])]).astype(np.int64)
+    wt2 = np.concatenate([wt, [3.0, 2.0, 1.0]])
+    p2 = wt2 / wt2.sum()
+    fsa = W.Fsa.read_text(syn.wfsa_text)
+    names = fsa.param_names()
+    w = np.random.default_rng(2).normal(-0.7, 0.5, size=len(names))
+    sp = _device(fsa, sym2, off2, p2, monkeypatch, dense=False)
+    dn = _device(fsa, sym2, off2, p2, monkeypatch, dense=True)
+    r_s, pc_s, u_s = sp.recognize()
+    r_d, pc_d, u_d = dn.recognize()
+    np.testing.assert_array_equal(r_d, r_s)
+    assert list(r_d[-3:]) == [0, 0, 0] and syn_bad
+    np.testing.assert_allclose(pc_d, pc_s, rtol=1e-12)
+    np.testing.assert_array_equal(u_d, u_s)
+    # weighted pass over the recognized strings only (as the Learner does)
+    keep = np.flatnonzero(r_s)
+    ks = [strings[i] for i in keep]
+    sym3 = np.frombuffer(b"".join(ks), dtype=np.uint8).copy()
+    off3 = np.concatenate([[0], np.cumsum([len(s) for s in ks])]).astype(np.int64)
+    for d in (sp, dn):
+        d.load_corpus(sym3, off3, p2[keep])
+    ll_s, g_s, lq_s = sp.objective_grad(w)
+    ll_d, g_d, lq_d = dn.objective_grad(w)
+    np.testing.assert_allclose(lq_d, lq_s, rtol=1e-12)
+    assert _close(ll_d, ll_s, rel=1e-12)
+    np.testing.assert_allclose(g_d, g_s, rtol=1e-10, atol=1e-17)
+
+
+def test_dense_learner_qn_equals_sparse(monkeypatch):
+    """QuasiNewtonLearner end to end (BuildFrom, Trim, device-resident QN loop)"""
+    import wfsa_amd as W
+    syn = W.Synthetic(n_states=16, degree=1, vocab=8, emissions=2, dense=True, n_strings=300, max_len=9, seed=21)
+    sym, off, wt = syn.corpus()
+    fsa = W.Fsa.read_text(syn.wfsa_text)
+    rows = {}
+    xs = {}
+    for dense in (False, True):
+        monkeypatch.setenv("WFSA_DENSE", "1" if dense else "0")
+        lrn = W.QuasiNewtonLearner(0)
+        lrn.BuildFromPacked(fsa, sym, off, wt)
+        lrn.Finalize()
+        lrn.Init(7)
+        assert lrn.stats()["dense"] == (1 if dense else 0)
+        rows[dense] = [lrn.OptimizationStep(1.0, -1.0)[0] for _ in range(2)] + lrn.Run(4, 1.0, -1.0)
+        xs[dense] = lrn.x()
+    assert len(rows[True]) == len(rows[False]) == 6
+    for r, q in zip(rows[True], rows[False]):
+        for a, b in zip(r[:5], q[:5]):
+            assert _close(a, b, rel=1e-9, atol=1e-12)
+    np.testing.assert_allclose(xs[True], xs[False], rtol=1e-9, atol=1e-11)
+
+
+def test_dense_chosen_automatically(monkeypatch):
+    import wfsa_amd as W
+    monkeypatch.delenv("WFSA_DENSE", raising=False)
+    syn = W.Synthetic(n_states=128, degree=1, vocab=4, emissions=4, dense=True, n_strings=50, max_len=8, seed=1)
+    sym, off, wt = syn.corpus()
+    dev = W.Device(0)
+    dev.load_model(W.Fsa.read_text(syn.wfsa_text))
+    dev.load_corpus(sym, off, wt / wt.sum())
+    assert dev.stats()["dense"] == 1
+    sparse = W.Synthetic(n_states=128, degree=8, vocab=4, emissions=1, n_strings=50, max_len=8, seed=1)
+    dev2 = W.Device(0)
+    dev2.load_model(W.Fsa.read_text(sparse.wfsa_text))
+    assert dev2.stats()["dense"] == 0
+
+
+def test_dense_1024_properties(monkeypatch):
+    """c5 shape at 1024 states (every state emits every symbol of 16):
+    posterior counts add up (one start and one end edge per path, L emissions
+    and L-1 transitions), LL = p . log q, a string subset against the oracle"""
+    import wfsa_amd as W
+    syn = W.Synthetic(n_states=1024, degree=1, vocab=16, emissions=16, dense=True, n_strings=1500, max_len=64,
+                      seed=4)
+    sym, off, wt = syn.corpus()
+    fsa = W.Fsa.read_text(syn.wfsa_text)
+    names = fsa.param_names()
+    p = wt / wt.sum()
+    dev = _device(fsa, sym, off, p, monkeypatch, dense=True)
+    rec, pc, used = dev.recognize()
+    assert rec.all()
+    rng = np.random.default_rng(9)
+    w = rng.normal(-7.0, 1.0, size=len(names))
+    ll, grad, logq = dev.objective_grad(w)
+    assert np.isfinite(logq).all()
+    assert _close(ll, float(np.dot(p, logq)), rel=1e-12)
+    L = np.diff(off).astype(np.float64)
+    kind = np.array([0 if n[1] == "E" else (1 if n[0] == "^" else (2 if n[2] == "$" else 3)) for n in names])
+    assert _close(grad[kind == 1].sum(), -1.0, rel=1e-11)                       # ^ -> T
+    assert _close(grad[kind == 2].sum(), -1.0, rel=1e-11)                       # S -> $
+    assert _close(grad[kind == 0].sum(), -float(np.dot(p, L)), rel=1e-11)       # emissions
+    assert _close(grad[kind == 3].sum(), -float(np.dot(p, L - 1)), rel=1e-11)   # S -> T
+    idx = np.sort(rng.choice(len(wt), size=8, replace=False))
+    sub_off = np.concatenate([[0], np.cumsum(np.diff(off)[idx])])
+    sub_sym = np.concatenate([sym[off[i]:off[i + 1]] for i in idx])
+    _, ologq, _ = _oracle(syn.wfsa_text, sub_sym, sub_off, wt[idx], dict(zip(names, w)))
+    np.testing.assert_allclose(logq[idx], ologq, rtol=1e-12)

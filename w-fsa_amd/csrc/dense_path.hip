@@ -1,0 +1,814 @@
+// Dense-automaton forward-backward on fp64 MFMA (see dense_path.hpp).
+//
+// Per evaluation, on one stream:
+//   dense_weights   exp(w) tables: A (np x np), E^T ((V+1) x np), start and
+//                   end vectors; zeroes the result vector
+//   gemm<FWD>  x T  alpha[t+1] = (alpha[t] / rowsum) A (.) E[sym]  (row slots
+//                   that start a string take a (.) E[sym] instead)
+//   dense_final     log q per string, p . log q partials
+//   gemm<BWD>  x T  beta[t] = (Y[t+1] / rowsum) A^T, or e where a string ends;
+//                   writes Y[t] = E[sym] (.) beta[t], z[t] (Y scaled for the
+//                   gradient GEMM) and gamma[t] = alpha beta / q (scaled)
+//   gemm<GRAD>      G = alpha[0..T-2]^T z[1..T-1]; grad(S->T) = -A (.) G
+//   dense_reduce    gamma summed per (emitted symbol, state), per start and
+//                   end state, in fixed row chunks
+//   dense_scatter   chunk sums -> the emission / start / end gradients, LL
+// Every sum runs in a fixed order: results are deterministic.
+//
+// GEMM: 256 threads, 128 x 128 block tile, 64 x 64 per wavefront (4 x 4
+// tiles of v_mfma_f64_16x16x4f64), K staged through LDS in slices of 16,
+// double-buffered; operands are stored in LDS as [row][k] with a 2-double pad
+// (a fragment read of 64 lanes is bank-conflict free).  Blocks are dealt so
+// that each XCD owns a contiguous range of tiles (column panels shared in its
+// L2).
+#include "dense_path.hpp"
+
+#include <algorithm>
+#include <cmath>
+#include <cstdlib>
+#include <cstring>
+#include <limits>
+#include <numeric>
+#include <queue>
+
+namespace wfsa {
+
+namespace {
+
+typedef double d4 __attribute__((ext_vector_type(4)));
+
+constexpr int kT = kDenseTile;        // 128
+constexpr int kBK = 16;               // K slice per LDS stage
+constexpr int kLdk = kBK + 2;         // padded LDS row (doubles)
+constexpr int kGemmThreads = 256;
+constexpr int kStage = 2 * kT * kLdk; // doubles per stage (A and B operands)
+constexpr int kRedThreads = 128;      // dense_reduce: one column per thread
+constexpr int kRedWindow = 64;        // symbols per LDS pass of dense_reduce
+
+enum GemmMode { FWD = 0, BWD = 1, GRAD = 2 };
+
+struct GemmArgs {
+    int32_t R, np, nct;
+    int64_t kg;                // GRAD: K = (T - 1) R
+    const double* x;           // FWD alpha[t] / BWD Y[t+1] / GRAD alpha (steps 0..T-2)
+    const double* bm;          // FWD, BWD: A / GRAD: z from step 1
+    int32_t no_mma;            // every row of the step starts (FWD) / ends (BWD) a string
+    const int32_t* meta;       // [R] meta of the output step
+    const int32_t* sid;        // [R] (BWD)
+    const double* part_in;     // [nct][R] row-sum partials of the input rows
+    double* part_out;          // [nct][R] of the output rows
+    const double* et;          // [(V+1)][np]
+    const double* a0;
+    const double* aend;
+    double* out;               // FWD alpha[t+1] / BWD Y[t]
+    const double* la_in;       // FWD la[t]
+    double* la_out;            // FWD la[t+1]
+    const double* lb_in;       // BWD lb[t+1]
+    double* lb_out;            // BWD lb[t]
+    const double* la_t;        // BWD la[t]
+    const double* la_prev;     // BWD la[t-1] or null
+    const double* alpha_t;     // BWD alpha[t]
+    double* gam;               // BWD gamma[t]
+    double* z;                 // BWD z[t]
+    const double* p;
+    const double* logq;
+    const int32_t* code_a;     // GRAD
+    const double* amat;
+    double* grad;              // GRAD: out + 1
+    int32_t n_params;
+    const unsigned* halted;
+};
+
+// Global -> registers -> LDS staging of one 128 x 16 operand slice.  KC: the
+// operand's row r is contiguous along k (element (r, k) at base[r ld + k]);
+// RC: rows of memory run along the operand's rows (element (r, k) at
+// base[k ld + r]).  Either way LDS holds [r][k] (kLdk stride).
+template <bool KC>
+__device__ __forceinline__ void load_slice(const double* __restrict__ base, int64_t ld, int r0, int64_t k0, int tid,
+                                           double2 (&v)[4]) {
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+        const int idx = c * kGemmThreads + tid;
+        if (KC) {
+            const int row = idx >> 3, kp = idx & 7;
+            v[c] = *reinterpret_cast<const double2*>(base + int64_t(r0 + row) * ld + k0 + 2 * kp);
+        } else {
+            const int kk = idx >> 6, rp = idx & 63;
+            v[c] = *reinterpret_cast<const double2*>(base + (k0 + kk) * ld + r0 + 2 * rp);
+        }
+    }
+}
+
+template <bool KC>
+__device__ __forceinline__ void store_slice(double* __restrict__ s, int tid, const double2 (&v)[4]) {
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+        const int idx = c * kGemmThreads + tid;
+        if (KC) {
+            const int row = idx >> 3, kp = idx & 7;
+            *reinterpret_cast<double2*>(s + row * kLdk + 2 * kp) = v[c];
+        } else {
+            const int kk = idx >> 6, rp = idx & 63;
+            s[(2 * rp) * kLdk + kk] = v[c].x;
+            s[(2 * rp + 1) * kLdk + kk] = v[c].y;
+        }
+    }
+}
+
+template <int MODE>
+__global__ __launch_bounds__(kGemmThreads, 2) void dense_gemm_kernel(GemmArgs a) {
+    if (a.halted && *a.halted) return;
+    __shared__ __attribute__((aligned(16))) double lds[2 * kStage];
+    __shared__ double red[2][kT];
+    __shared__ double rs0[kT], rs1[kT], rs2[kT];
+    __shared__ int32_t rmeta[kT];
+
+    constexpr bool A_KC = MODE != GRAD;   // FWD / BWD: x rows are contiguous along k
+    constexpr bool B_KC = MODE == BWD;    // BWD: A^T (rows of A); FWD: A; GRAD: z
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int wm = wave >> 1, wn = wave & 1;
+    const int np = a.np;
+    const int mtiles = (MODE == GRAD ? np : a.R) / kT, ntiles = np / kT;
+    const int nb = mtiles * ntiles;
+    int bid = int(blockIdx.x);
+    if ((nb & 7) == 0) bid = (bid & 7) * (nb >> 3) + (bid >> 3);   // XCD x: tiles [x nb/8, (x+1) nb/8)
+    const int mt_ = bid % mtiles, nt_ = bid / mtiles;
+    const int r0 = mt_ * kT, c0 = nt_ * kT;
+
+    // per-row scalars of the block's output rows
+    if (MODE != GRAD && tid < kT) {
+        const int r = r0 + tid;
+        const int m = a.meta[r];
+        const bool start = (m >> 9) & 1, end = (m >> 10) & 1;
+        if (MODE == FWD) {
+            double inv = 0.0, la = 0.0;
+            if (!a.no_mma) {
+                double s = 0.0;
+                for (int ct = 0; ct < a.nct; ++ct) s += a.part_in[int64_t(ct) * a.R + r];
+                inv = s > 0.0 ? 1.0 / s : 0.0;
+                la = start ? 0.0 : a.la_in[r] + log(s);
+            }
+            rs0[tid] = inv;
+            if (nt_ == 0) a.la_out[r] = la;
+        } else {
+            double inv = 0.0, lb = 0.0;
+            if (!end && !a.no_mma) {
+                double u = 0.0;
+                for (int ct = 0; ct < a.nct; ++ct) u += a.part_in[int64_t(ct) * a.R + r];
+                inv = u > 0.0 ? 1.0 / u : 0.0;
+                lb = a.lb_in[r] + log(u);
+            }
+            if (nt_ == 0) a.lb_out[r] = lb;
+            double f1 = 0.0, f2 = 0.0;
+            const int s = a.sid[r];
+            if (s >= 0) {
+                const double lq = a.logq[s];
+                if (lq > -INFINITY) {
+                    f1 = a.p[s] * exp(a.la_t[r] + lb - lq);
+                    if (!start && a.la_prev) f2 = a.p[s] * exp(a.la_prev[r] + lb - lq);
+                }
+            }
+            rs0[tid] = inv;
+            rs1[tid] = f1;
+            rs2[tid] = f2;
+        }
+        rmeta[tid] = m;
+    }
+
+    d4 acc[4][4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = d4{0.0, 0.0, 0.0, 0.0};
+
+    if (!a.no_mma) {
+        const int64_t nk = (MODE == GRAD ? a.kg : int64_t(np)) / kBK;
+        const double* xa = a.x;
+        const double* xb = a.bm;
+        double2 va[4], vb[4];
+        load_slice<A_KC>(xa, np, r0, 0, tid, va);
+        load_slice<B_KC>(xb, np, c0, 0, tid, vb);
+        store_slice<A_KC>(lds, tid, va);
+        store_slice<B_KC>(lds + kT * kLdk, tid, vb);
+        __syncthreads();
+        for (int64_t kt = 0; kt < nk; ++kt) {
+            const bool more = kt + 1 < nk;
+            if (more) {
+                load_slice<A_KC>(xa, np, r0, (kt + 1) * kBK, tid, va);
+                load_slice<B_KC>(xb, np, c0, (kt + 1) * kBK, tid, vb);
+            }
+            const double* As = lds + (kt & 1) * kStage;
+            const double* Bs = As + kT * kLdk;
+#pragma unroll
+            for (int kk = 0; kk < kBK / 4; ++kk) {
+                double av[4], bv[4];
+#pragma unroll
+                for (int i = 0; i < 4; ++i) av[i] = As[(wm * 64 + i * 16 + (lane & 15)) * kLdk + kk * 4 + (lane >> 4)];
+#pragma unroll
+                for (int j = 0; j < 4; ++j) bv[j] = Bs[(wn * 64 + j * 16 + (lane & 15)) * kLdk + kk * 4 + (lane >> 4)];
+#pragma unroll
+                for (int i = 0; i < 4; ++i)
+#pragma unroll
+                    for (int j = 0; j < 4; ++j)
+                        acc[i][j] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[i], bv[j], acc[i][j], 0, 0, 0);
+            }
+            if (more) {
+                double* s = lds + ((kt + 1) & 1) * kStage;
+                store_slice<A_KC>(s, tid, va);
+                store_slice<B_KC>(s + kT * kLdk, tid, vb);
+            }
+            __syncthreads();
+        }
+    } else {
+        __syncthreads();
+    }
+
+    // epilogue: element (i, j, e) of this lane is row wm*64 + 16 i + (lane>>4)
+    // + 4 e, column wn*64 + 16 j + (lane & 15) of the block tile
+    if (MODE == GRAD) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    const int row = r0 + wm * 64 + 16 * i + (lane >> 4) + 4 * e;
+                    const int col = c0 + wn * 64 + 16 * j + (lane & 15);
+                    const int64_t o = int64_t(row) * np + col;
+                    const int32_t code = a.code_a[o];
+                    if (code >= 0 && code < a.n_params) a.grad[code] = -a.amat[o] * acc[i][j][e];
+                }
+        return;
+    }
+    double rsum[4][4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) rsum[i][e] = 0.0;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            const int rl = wm * 64 + 16 * i + (lane >> 4) + 4 * e;
+            const int row = r0 + rl;
+            const int m = rmeta[rl];
+            const int sym = m & 511;
+            const double* erow = a.et + int64_t(sym) * np;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const int col = c0 + wn * 64 + 16 * j + (lane & 15);
+                const int64_t o = int64_t(row) * np + col;
+                double v;
+                if (MODE == FWD) {
+                    v = ((m >> 9) & 1) ? a.a0[col] : acc[i][j][e] * rs0[rl];
+                    v *= erow[col];
+                    a.out[o] = v;
+                } else {
+                    const double beta = ((m >> 10) & 1) ? a.aend[col] : acc[i][j][e] * rs0[rl];
+                    a.gam[o] = a.alpha_t[o] * beta * rs1[rl];
+                    v = erow[col] * beta;
+                    a.out[o] = v;
+                    a.z[o] = v * rs2[rl];
+                }
+                rsum[i][e] += v;
+            }
+        }
+    // row sums over the tile's 128 columns: 16 lanes per row, then the two
+    // column halves (wn) through LDS
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            double v = rsum[i][e];
+            v += __shfl_xor(v, 1);
+            v += __shfl_xor(v, 2);
+            v += __shfl_xor(v, 4);
+            v += __shfl_xor(v, 8);
+            if ((lane & 15) == 0) red[wn][wm * 64 + 16 * i + (lane >> 4) + 4 * e] = v;
+        }
+    __syncthreads();
+    if (tid < kT) a.part_out[int64_t(nt_) * a.R + r0 + tid] = red[0][tid] + red[1][tid];
+}
+
+struct WeightsArgs {
+    const double* ewp;          // exp(w_full) (or all ones)
+    const int32_t* code_a;
+    const int32_t* code_em;
+    const int32_t* code_s;
+    const int32_t* code_e;
+    double* amat;
+    double* et;
+    double* a0;
+    double* aend;
+    int64_t n_a, n_em;
+    int32_t np;
+    double* out;                // [1 + n_params] zeroed
+    int32_t n_out;
+    const unsigned* halted;
+};
+
+__device__ __forceinline__ double code_weight(const double* ewp, int32_t c) {
+    return c >= 0 ? ewp[c] : (c == kCodeOne ? 1.0 : 0.0);
+}
+
+__global__ __launch_bounds__(256) void dense_weights_kernel(WeightsArgs a) {
+    if (a.halted && *a.halted) return;
+    const int64_t stride = int64_t(gridDim.x) * blockDim.x;
+    const int64_t t0 = int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+    for (int64_t i = t0; i < a.n_a; i += stride) a.amat[i] = code_weight(a.ewp, a.code_a[i]);
+    for (int64_t i = t0; i < a.n_em; i += stride) a.et[i] = code_weight(a.ewp, a.code_em[i]);
+    for (int64_t i = t0; i < a.np; i += stride) {
+        a.a0[i] = code_weight(a.ewp, a.code_s[i]);
+        a.aend[i] = code_weight(a.ewp, a.code_e[i]);
+    }
+    for (int64_t i = t0; i < a.n_out; i += stride) a.out[i] = 0.0;
+}
+
+struct FinalArgs {
+    const double* alpha;        // [T][R][np]
+    const double* la;           // [T][R]
+    const double* aend;
+    const int32_t* end_at;      // [S]
+    const double* p;
+    const double* ewp;
+    int32_t code_se;
+    int64_t n_strings;
+    int32_t np;
+    double* logq;               // [S]
+    double* logq_user;          // [S] or null
+    double* ll_part;            // [blocks]
+    const unsigned* halted;
+};
+
+// one wavefront per string: log q = la + log(alpha_L . e)
+__global__ __launch_bounds__(256) void dense_final_kernel(FinalArgs a) {
+    if (a.halted && *a.halted) return;
+    __shared__ double wsum[4];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int64_t s = int64_t(blockIdx.x) * 4 + w;
+    double contrib = 0.0;
+    if (s < a.n_strings) {
+        const int32_t at = a.end_at[s];
+        double lq;
+        if (at >= 0) {
+            const double* row = a.alpha + int64_t(at) * a.np;
+            double d = 0.0;
+            for (int c = lane; c < a.np; c += 64) d += row[c] * a.aend[c];
+#pragma unroll
+            for (int o = 32; o >= 1; o >>= 1) d += __shfl_xor(d, o);
+            lq = a.la[at] + log(d);
+        } else {
+            lq = log(code_weight(a.ewp, a.code_se));
+        }
+        if (lane == 0) {
+            a.logq[s] = lq;
+            if (a.logq_user) a.logq_user[s] = lq;
+        }
+        contrib = a.p[s] > 0.0 ? a.p[s] * lq : 0.0;
+    }
+    if (lane == 0) wsum[w] = contrib;
+    __syncthreads();
+    if (threadIdx.x == 0) a.ll_part[blockIdx.x] = ((wsum[0] + wsum[1]) + wsum[2]) + wsum[3];
+}
+
+struct ReduceArgs {
+    const double* gam;          // [T R][np]
+    const int32_t* meta;        // [T R]
+    int64_t rows;               // T R
+    int64_t rows_per_chunk;
+    int32_t np, vocab;
+    double* red;                // [chunks][vocab + 2][np]
+    const unsigned* halted;
+};
+
+// gamma rows of chunk blockIdx.y, columns [128 blockIdx.x, +128): sums per
+// emitted symbol, per start row (-> ^->T) and per end row (-> S->$)
+__global__ __launch_bounds__(kRedThreads) void dense_reduce_kernel(ReduceArgs a) {
+    if (a.halted && *a.halted) return;
+    __shared__ double acc[(kRedWindow + 2) * kRedThreads];
+    const int t = threadIdx.x;
+    const int col = int(blockIdx.x) * kRedThreads + t;
+    const int64_t rbeg = int64_t(blockIdx.y) * a.rows_per_chunk;
+    const int64_t rend = min(a.rows, rbeg + a.rows_per_chunk);
+    const int V = a.vocab;
+    double* outp = a.red + int64_t(blockIdx.y) * (V + 2) * a.np;
+    for (int vb = 0; vb < V || vb == 0; vb += kRedWindow) {
+        const int wv = min(kRedWindow, V - vb);
+        for (int k = 0; k < kRedWindow + 2; ++k) acc[k * kRedThreads + t] = 0.0;
+        double st = 0.0, en = 0.0;
+        for (int64_t r = rbeg; r < rend; ++r) {
+            const int m = a.meta[r];
+            const int sym = m & 511;
+            if (sym >= V) continue;   // idle slot
+            const double g = a.gam[r * a.np + col];
+            const int k = sym - vb;
+            if (k >= 0 && k < wv) acc[k * kRedThreads + t] += g;
+            if (vb == 0) {
+                if ((m >> 9) & 1) st += g;
+                if ((m >> 10) & 1) en += g;
+            }
+        }
+        for (int k = 0; k < wv; ++k) outp[int64_t(vb + k) * a.np + col] = acc[k * kRedThreads + t];
+        if (vb == 0) {
+            outp[int64_t(V) * a.np + col] = st;
+            outp[int64_t(V + 1) * a.np + col] = en;
+        }
+        if (V == 0) break;
+    }
+}
+
+struct ScatterArgs {
+    const double* red;          // [chunks][vocab + 2][np]
+    int32_t chunks;
+    int32_t np, vocab;
+    const int32_t* code_em;     // [vocab + 1][np]
+    const int32_t* code_s;
+    const int32_t* code_e;
+    int32_t code_se;
+    int32_t n_params;
+    double empty_p;             // sum of p over empty strings (posterior 1 on ^->$)
+    const double* ll_part;
+    int32_t n_ll;
+    double* out;                // [1 + n_params]
+    const unsigned* halted;
+};
+
+__global__ __launch_bounds__(256) void dense_scatter_kernel(ScatterArgs a) {
+    if (a.halted && *a.halted) return;
+    const int64_t n = int64_t(a.vocab + 2) * a.np;
+    const int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+    if (i < n) {
+        const int slot = int(i / a.np), col = int(i % a.np);
+        double s = 0.0;
+        for (int c = 0; c < a.chunks; ++c) s += a.red[(int64_t(c) * (a.vocab + 2) + slot) * a.np + col];
+        const int32_t code =
+            slot < a.vocab ? a.code_em[int64_t(slot) * a.np + col] : (slot == a.vocab ? a.code_s[col] : a.code_e[col]);
+        if (code >= 0 && code < a.n_params) a.out[1 + code] = -s;
+    }
+    if (i == 0) {
+        double ll = 0.0;
+        for (int b = 0; b < a.n_ll; ++b) ll += a.ll_part[b];
+        a.out[0] = ll;
+        if (a.code_se >= 0 && a.code_se < a.n_params) a.out[1 + a.code_se] = -a.empty_p;
+    }
+}
+
+template <typename T>
+hipError_t dalloc(T*& p, size_t n) {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    return hipMalloc(reinterpret_cast<void**>(&p), std::max<size_t>(n, 1) * sizeof(T));
+}
+
+template <typename T>
+void dfree(T*& p) {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+}
+
+#define DTRY(x)                                     \
+    do {                                            \
+        const hipError_t e_ = (x);                  \
+        if (e_ != hipSuccess) return e_;            \
+    } while (0)
+
+}  // namespace
+
+std::string dense_model_build(const wfsa_model_desc& d, bool force, DenseModel& out) {
+    const int32_t N = d.n_states;
+    if (N <= 0 || d.start < 0 || d.start >= N) return "no start state";
+    std::vector<int32_t> idx(size_t(N), -1);
+    int32_t n_int = 0;
+    for (int32_t s = 0; s < N; ++s)
+        if (s != d.start && s != d.end) idx[size_t(s)] = n_int++;
+    if (n_int == 0) return "no interior states";
+    // single-byte emissions only
+    bool used[256] = {};
+    for (int32_t s = 0; s < N; ++s) {
+        if (idx[size_t(s)] < 0) continue;
+        for (int32_t e = d.em_ptr[s]; e < d.em_ptr[s + 1]; ++e) {
+            if (d.em_len[e] != 1) return "an emission is not a single byte";
+            used[d.em_bytes[d.em_off[e]]] = true;
+        }
+    }
+    int64_t n_tr = 0;
+    for (int32_t s = 0; s < N; ++s)
+        if (idx[size_t(s)] >= 0)
+            for (int32_t t = d.tr_ptr[s]; t < d.tr_ptr[s + 1]; ++t)
+                if (d.tr_dst[t] != d.end && d.tr_dst[t] != d.start) ++n_tr;
+    if (!force) {
+        if (n_int < 64) return "fewer than 64 interior states";
+        if (double(n_tr) * 4.0 < double(n_int) * double(n_int)) return "transition matrix sparser than 1/4";
+    }
+    DenseModel m;
+    m.n_states = n_int;
+    m.np = (n_int + kDenseTile - 1) / kDenseTile * kDenseTile;
+    m.n_params = d.n_params;
+    m.n_transitions = n_tr;
+    int32_t V = 0;
+    for (int b = 0; b < 256; ++b) m.sym_of_byte[b] = -1;
+    for (int b = 0; b < 256; ++b)
+        if (used[b]) m.sym_of_byte[b] = int16_t(V++);
+    for (int b = 0; b < 256; ++b)
+        if (m.sym_of_byte[b] < 0) m.sym_of_byte[b] = int16_t(V);
+    m.vocab = V;
+    const size_t np = size_t(m.np);
+    auto code_of = [](int32_t param) { return param >= 0 ? param : kCodeOne; };
+    m.code_a.assign(np * np, kCodeNone);
+    m.code_s.assign(np, kCodeNone);
+    m.code_e.assign(np, kCodeNone);
+    m.code_em.assign(size_t(V + 1) * np, kCodeNone);
+    for (int32_t s = 0; s < N; ++s) {
+        const int32_t is = idx[size_t(s)];
+        if (s == d.end) continue;   // $ has no way out on an accepting path
+        for (int32_t t = d.tr_ptr[s]; t < d.tr_ptr[s + 1]; ++t) {
+            const int32_t dst = d.tr_dst[t];
+            if (dst == d.start) return "a transition into the start state";
+            int32_t* slot;
+            if (s == d.start) {
+                slot = dst == d.end ? &m.code_se : &m.code_s[size_t(idx[size_t(dst)])];
+            } else {
+                slot = dst == d.end ? &m.code_e[size_t(is)] : &m.code_a[size_t(is) * np + size_t(idx[size_t(dst)])];
+            }
+            if (*slot != kCodeNone) return "duplicate transition";
+            *slot = code_of(d.tr_param[t]);
+        }
+        if (is < 0) continue;
+        for (int32_t e = d.em_ptr[s]; e < d.em_ptr[s + 1]; ++e) {
+            const int32_t v = m.sym_of_byte[d.em_bytes[d.em_off[e]]];
+            int32_t& slot = m.code_em[size_t(v) * np + size_t(is)];
+            if (slot != kCodeNone) return "duplicate emission";
+            slot = code_of(d.em_param[e]);
+        }
+    }
+    out = std::move(m);
+    return std::string();
+}
+
+DensePath::~DensePath() {
+    free_corpus();
+    free_model();
+}
+
+void DensePath::free_model() {
+    dfree(code_a_); dfree(code_s_); dfree(code_e_); dfree(code_em_);
+    dfree(amat_); dfree(et_); dfree(a0_); dfree(aend_); dfree(ones_);
+}
+
+void DensePath::free_corpus() {
+    dfree(meta_); dfree(sid_); dfree(end_at_); dfree(p_); dfree(pones_); dfree(logq_);
+    dfree(la_); dfree(lb_); dfree(alpha_); dfree(gam_); dfree(z_); dfree(y_); dfree(part_);
+    dfree(ll_part_); dfree(red_);
+    n_strings_ = 0;
+    R_ = T_ = 0;
+}
+
+hipError_t DensePath::load_model(const DenseModel& m, hipStream_t s) {
+    free_corpus();
+    free_model();
+    n_params_ = m.n_params;
+    np_ = m.np;
+    vocab_ = m.vocab;
+    nct_ = m.np / kT;
+    code_se_ = m.code_se;
+    std::memcpy(sym_of_byte_, m.sym_of_byte, sizeof sym_of_byte_);
+    const size_t np = size_t(np_);
+    DTRY(dalloc(code_a_, np * np));
+    DTRY(dalloc(code_s_, np));
+    DTRY(dalloc(code_e_, np));
+    DTRY(dalloc(code_em_, size_t(vocab_ + 1) * np));
+    DTRY(hipMemcpyAsync(code_a_, m.code_a.data(), np * np * 4, hipMemcpyHostToDevice, s));
+    DTRY(hipMemcpyAsync(code_s_, m.code_s.data(), np * 4, hipMemcpyHostToDevice, s));
+    DTRY(hipMemcpyAsync(code_e_, m.code_e.data(), np * 4, hipMemcpyHostToDevice, s));
+    DTRY(hipMemcpyAsync(code_em_, m.code_em.data(), size_t(vocab_ + 1) * np * 4, hipMemcpyHostToDevice, s));
+    DTRY(dalloc(amat_, np * np));
+    DTRY(dalloc(et_, size_t(vocab_ + 1) * np));
+    DTRY(dalloc(a0_, np));
+    DTRY(dalloc(aend_, np));
+    std::vector<double> ones(size_t(n_params_) + 2, 1.0);
+    DTRY(dalloc(ones_, ones.size()));
+    DTRY(hipMemcpyAsync(ones_, ones.data(), ones.size() * 8, hipMemcpyHostToDevice, s));
+    return hipStreamSynchronize(s);
+}
+
+hipError_t DensePath::load_corpus(const uint8_t* sym, const int64_t* off, const double* p, int64_t n_strings,
+                                  hipStream_t s) {
+    free_corpus();
+    n_strings_ = n_strings;
+    const size_t S = size_t(n_strings);
+    int64_t total = 0, lmax = 0;
+    p0_sum_ = 0.0;
+    n0_ = 0.0;
+    std::vector<int32_t> order;
+    order.reserve(S);
+    for (size_t i = 0; i < S; ++i) {
+        const int64_t L = off[i + 1] - off[i];
+        total += L;
+        lmax = std::max(lmax, L);
+        if (L > 0) order.push_back(int32_t(i));
+        else { p0_sum_ += p[i]; n0_ += 1.0; }
+    }
+    total_sym_ = total;
+    // slots: enough that the longest string sets the step count
+    int64_t R = lmax > 0 ? (total + lmax - 1) / lmax : 1;
+    R = std::min<int64_t>(R, int64_t(order.size()));
+    R = std::max<int64_t>(1, (R + kT - 1) / kT) * kT;
+    std::stable_sort(order.begin(), order.end(), [&](int32_t a, int32_t b) {
+        return off[a + 1] - off[a] > off[b + 1] - off[b];
+    });
+    // longest first, each to the least loaded slot
+    std::vector<std::vector<int32_t>> slot(static_cast<size_t>(R));
+    std::vector<int64_t> load(static_cast<size_t>(R), 0);
+    {
+        using E = std::pair<int64_t, int32_t>;
+        std::priority_queue<E, std::vector<E>, std::greater<E>> pq;
+        for (int32_t r = 0; r < int32_t(R); ++r) pq.push({0, r});
+        for (int32_t str : order) {
+            E e = pq.top();
+            pq.pop();
+            slot[size_t(e.second)].push_back(str);
+            e.first += off[str + 1] - off[str];
+            load[size_t(e.second)] = e.first;
+            pq.push(e);
+        }
+    }
+    int64_t T = 0;
+    for (int64_t l : load) T = std::max(T, l);
+    T = std::max<int64_t>(T, 1);
+    if (T * R >= (int64_t(1) << 31)) return hipErrorInvalidValue;
+    R_ = int32_t(R);
+    T_ = int32_t(T);
+    const size_t TR = size_t(T) * size_t(R);
+    std::vector<int32_t> meta(TR, vocab_), sid(TR, -1), end_at(S, -1);
+    for (int32_t r = 0; r < int32_t(R); ++r) {
+        int64_t t = 0;
+        for (int32_t str : slot[size_t(r)]) {
+            const int64_t L = off[str + 1] - off[str];
+            for (int64_t j = 0; j < L; ++j, ++t) {
+                const size_t o = size_t(t) * size_t(R) + size_t(r);
+                meta[o] = int32_t(sym_of_byte_[sym[off[str] + j]]) | (j == 0 ? 1 << 9 : 0) | (j == L - 1 ? 1 << 10 : 0);
+                sid[o] = str;
+                if (j == L - 1) end_at[size_t(str)] = int32_t(o);
+            }
+        }
+    }
+    const size_t np = size_t(np_);
+    DTRY(dalloc(meta_, TR));
+    DTRY(dalloc(sid_, TR));
+    DTRY(dalloc(end_at_, S));
+    DTRY(dalloc(p_, S));
+    DTRY(dalloc(pones_, S));
+    DTRY(dalloc(logq_, S));
+    DTRY(hipMemcpyAsync(meta_, meta.data(), TR * 4, hipMemcpyHostToDevice, s));
+    DTRY(hipMemcpyAsync(sid_, sid.data(), TR * 4, hipMemcpyHostToDevice, s));
+    DTRY(hipMemcpyAsync(end_at_, end_at.data(), S * 4, hipMemcpyHostToDevice, s));
+    if (S) DTRY(hipMemcpyAsync(p_, p, S * 8, hipMemcpyHostToDevice, s));
+    std::vector<double> ones(std::max<size_t>(S, 1), 1.0);
+    DTRY(hipMemcpyAsync(pones_, ones.data(), S * 8, hipMemcpyHostToDevice, s));
+    DTRY(dalloc(la_, TR));
+    DTRY(dalloc(lb_, TR));
+    DTRY(dalloc(alpha_, TR * np));
+    DTRY(dalloc(gam_, TR * np));
+    DTRY(dalloc(z_, TR * np));
+    DTRY(dalloc(y_, 2 * size_t(R) * np));
+    DTRY(dalloc(part_, 2 * size_t(nct_) * size_t(R)));
+    n_ll_ = int32_t((S + 3) / 4);
+    DTRY(dalloc(ll_part_, size_t(std::max(n_ll_, 1))));
+    // gamma reduction: enough row chunks to fill the chip with column blocks
+    const int64_t cols = np / kRedThreads;
+    int64_t chunks = std::max<int64_t>(1, (1024 + cols - 1) / cols);
+    chunks = std::min<int64_t>(chunks, int64_t(TR));
+    reduce_chunks_ = int32_t(chunks);
+    DTRY(dalloc(red_, size_t(chunks) * size_t(vocab_ + 2) * np));
+    return hipStreamSynchronize(s);
+}
+
+double DensePath::issued_flops() const {
+    const double np = double(np_), R = double(R_), T = double(T_);
+    return 2.0 * np * np * R * (T - 1) * 3.0;
+}
+
+hipError_t DensePath::enqueue(const double* ewp, bool structural, double* out, double* logq, const unsigned* halted,
+                              hipStream_t s) {
+    const size_t np = size_t(np_), R = size_t(R_);
+    const double* w = structural ? ones_ : ewp;
+    const double* p = structural ? pones_ : p_;
+    {
+        WeightsArgs a{};
+        a.ewp = w;
+        a.code_a = code_a_; a.code_em = code_em_; a.code_s = code_s_; a.code_e = code_e_;
+        a.amat = amat_; a.et = et_; a.a0 = a0_; a.aend = aend_;
+        a.n_a = int64_t(np * np);
+        a.n_em = int64_t(size_t(vocab_ + 1) * np);
+        a.np = np_;
+        a.out = out;
+        a.n_out = n_params_ + 1;
+        a.halted = halted;
+        dense_weights_kernel<<<1024, 256, 0, s>>>(a);
+        DTRY(hipGetLastError());
+    }
+    if (n_strings_ == 0 || total_sym_ == 0) {
+        FinalArgs f{};
+        if (n_strings_ > 0) {
+            f.alpha = alpha_; f.la = la_; f.aend = aend_; f.end_at = end_at_; f.p = p; f.ewp = w;
+            f.code_se = code_se_; f.n_strings = n_strings_; f.np = np_; f.logq = logq_; f.logq_user = logq;
+            f.ll_part = ll_part_; f.halted = halted;
+            dense_final_kernel<<<n_ll_, 256, 0, s>>>(f);
+            DTRY(hipGetLastError());
+        }
+        ScatterArgs c{};
+        c.red = red_; c.chunks = 0; c.np = np_; c.vocab = vocab_;
+        c.code_em = code_em_; c.code_s = code_s_; c.code_e = code_e_; c.code_se = code_se_;
+        c.n_params = n_params_; c.empty_p = structural ? n0_ : p0_sum_;
+        c.ll_part = ll_part_; c.n_ll = n_strings_ > 0 ? n_ll_ : 0; c.out = out; c.halted = halted;
+        dense_scatter_kernel<<<1, 256, 0, s>>>(c);
+        return hipGetLastError();
+    }
+    const size_t step = R * np;
+    GemmArgs g{};
+    g.R = R_; g.np = np_; g.nct = nct_;
+    g.et = et_; g.a0 = a0_; g.aend = aend_;
+    g.p = p; g.logq = logq_;
+    g.n_params = n_params_;
+    g.halted = halted;
+    const int fb_blocks = int((R / kT) * (np / kT));
+    // forward: step 0 (every row starts a string), then t -> t+1
+    for (int64_t t = -1; t + 1 < T_; ++t) {
+        GemmArgs f = g;
+        f.no_mma = t < 0;
+        f.x = t < 0 ? alpha_ : alpha_ + size_t(t) * step;
+        f.bm = amat_;
+        f.meta = meta_ + size_t(t + 1) * R;
+        f.part_in = part_ + size_t(t & 1) * nct_ * R;
+        f.part_out = part_ + size_t((t + 1) & 1) * nct_ * R;
+        f.out = alpha_ + size_t(t + 1) * step;
+        f.la_in = t < 0 ? la_ : la_ + size_t(t) * R;
+        f.la_out = la_ + size_t(t + 1) * R;
+        dense_gemm_kernel<FWD><<<fb_blocks, kGemmThreads, 0, s>>>(f);
+        DTRY(hipGetLastError());
+    }
+    {
+        FinalArgs f{};
+        f.alpha = alpha_; f.la = la_; f.aend = aend_; f.end_at = end_at_; f.p = p; f.ewp = w;
+        f.code_se = code_se_; f.n_strings = n_strings_; f.np = np_; f.logq = logq_; f.logq_user = logq;
+        f.ll_part = ll_part_; f.halted = halted;
+        dense_final_kernel<<<n_ll_, 256, 0, s>>>(f);
+        DTRY(hipGetLastError());
+    }
+    // backward: step T-1 (every row ends), then t+1 -> t
+    for (int64_t t = T_ - 1; t >= 0; --t) {
+        GemmArgs b = g;
+        b.no_mma = t == T_ - 1;
+        b.x = y_ + size_t((t + 1) & 1) * step;
+        b.bm = amat_;
+        b.meta = meta_ + size_t(t) * R;
+        b.sid = sid_ + size_t(t) * R;
+        b.part_in = part_ + size_t((t + 1) & 1) * nct_ * R;
+        b.part_out = part_ + size_t(t & 1) * nct_ * R;
+        b.out = y_ + size_t(t & 1) * step;
+        b.lb_in = lb_ + size_t(std::min<int64_t>(t + 1, T_ - 1)) * R;
+        b.lb_out = lb_ + size_t(t) * R;
+        b.la_t = la_ + size_t(t) * R;
+        b.la_prev = t > 0 ? la_ + size_t(t - 1) * R : nullptr;
+        b.alpha_t = alpha_ + size_t(t) * step;
+        b.gam = gam_ + size_t(t) * step;
+        b.z = z_ + size_t(t) * step;
+        dense_gemm_kernel<BWD><<<fb_blocks, kGemmThreads, 0, s>>>(b);
+        DTRY(hipGetLastError());
+    }
+    if (T_ >= 2) {
+        GemmArgs q = g;
+        q.no_mma = 0;
+        q.kg = int64_t(T_ - 1) * int64_t(R);
+        q.x = alpha_;
+        q.bm = z_ + step;
+        q.code_a = code_a_;
+        q.amat = amat_;
+        q.grad = out + 1;
+        dense_gemm_kernel<GRAD><<<int((np / kT) * (np / kT)), kGemmThreads, 0, s>>>(q);
+        DTRY(hipGetLastError());
+    }
+    {
+        ReduceArgs r{};
+        r.gam = gam_; r.meta = meta_;
+        r.rows = int64_t(T_) * int64_t(R);
+        r.rows_per_chunk = (r.rows + reduce_chunks_ - 1) / reduce_chunks_;
+        r.np = np_; r.vocab = vocab_; r.red = red_; r.halted = halted;
+        dim3 grid(unsigned(np / kRedThreads), unsigned(reduce_chunks_));
+        dense_reduce_kernel<<<grid, kRedThreads, 0, s>>>(r);
+        DTRY(hipGetLastError());
+    }
+    {
+        ScatterArgs c{};
+        c.red = red_; c.chunks = reduce_chunks_; c.np = np_; c.vocab = vocab_;
+        c.code_em = code_em_; c.code_s = code_s_; c.code_e = code_e_; c.code_se = code_se_;
+        c.n_params = n_params_; c.empty_p = structural ? n0_ : p0_sum_;
+        c.ll_part = ll_part_; c.n_ll = n_ll_; c.out = out; c.halted = halted;
+        const int64_t n = int64_t(vocab_ + 2) * int64_t(np);
+        dense_scatter_kernel<<<unsigned((n + 255) / 256), 256, 0, s>>>(c);
+        DTRY(hipGetLastError());
+    }
+    return hipSuccess;
+}
+
+}  // namespace wfsa

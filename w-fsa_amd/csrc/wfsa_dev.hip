@@ -31,6 +31,7 @@
 #include <string>
 #include <vector>
 
+#include "dense_path.hpp"
 #include "fb_kernels.hpp"
 #include "trellis_model.hpp"
 
@@ -216,6 +217,13 @@ struct wfsa_dev {
     double* qn_ring = nullptr;       // host-mapped [kQnDepth][kQnRow]
     double* qn_ring_dev = nullptr;
 
+    // dense automata: the fp64 MFMA path (dense_path.hpp) replaces the
+    // trellis kernels; WFSA_DENSE=0 never, =1 whenever the model qualifies
+    // (any size), unset: when the transition matrix is at least 1/4 full
+    std::unique_ptr<wfsa::DensePath> dense;
+    int dense_mode = -1;
+    bool dense_struct = false;   // the structural pass ran on the loaded corpus
+
     // communicator
     ncclComm_t comm = nullptr;
     int nranks = 1, rank = 0;
@@ -398,7 +406,47 @@ int wait_published(wfsa_dev* ctx, unsigned want) {
     }
 }
 
+// Dense automata: no compilation; level 1 is the structural pass, one
+// evaluation at all-ones weights and p: log q = log(path count), and a
+// parameter is used iff its expected count is positive.
+int prepare_dense(wfsa_dev* ctx, int level) {
+    const auto t_start = std::chrono::steady_clock::now();
+    hipStream_t s = ctx->stream;
+    const int64_t S = ctx->n_strings;
+    const size_t SZ = size_t(std::max<int64_t>(S, 1));
+    const int32_t np = ctx->n_params;
+    if (level >= 1 && !ctx->dense_struct) {
+        HIP_TRY(ctx->pcount.alloc(SZ));
+        HIP_TRY(ctx->recog.alloc(SZ));
+        HIP_TRY(ctx->used.alloc(size_t(std::max(np, 1))));
+        HIP_TRY(ctx->dense->enqueue(nullptr, true, ctx->out.ptr, ctx->logq.ptr, nullptr, s));
+        std::vector<double> out(size_t(np) + 1), lq(SZ), pc(SZ);
+        HIP_TRY(ctx->out.download(out.data(), out.size(), s));
+        HIP_TRY(ctx->logq.download(lq.data(), size_t(S), s));
+        HIP_TRY(hipStreamSynchronize(s));
+        std::vector<uint8_t> rec(SZ, 0), used(size_t(std::max(np, 1)), 0);
+        for (int64_t i = 0; i < S; ++i) {
+            rec[size_t(i)] = lq[size_t(i)] > -INFINITY ? 1 : 0;
+            const double c = std::exp(lq[size_t(i)]);
+            pc[size_t(i)] = c < 9007199254740992.0 ? std::nearbyint(c) : c;   // exact below 2^53
+        }
+        for (int32_t j = 0; j < np; ++j) used[size_t(j)] = out[size_t(j) + 1] < 0.0 ? 1 : 0;
+        HIP_TRY(ctx->recog.upload(rec.data(), SZ, s));
+        HIP_TRY(ctx->pcount.upload(pc.data(), SZ, s));
+        HIP_TRY(ctx->used.upload(used.data(), used.size(), s));
+        HIP_TRY(hipStreamSynchronize(s));
+        ctx->dense_struct = true;
+    }
+    ctx->prep_level = std::max(ctx->prep_level, 2);
+    ctx->stats.compiled_strings = 0;
+    ctx->stats.fallback_strings = 0;
+    ctx->stats.prepare_ms +=
+        std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_start).count();
+    return WFSA_OK;
+}
+
 int prepare(wfsa_dev* ctx, int level) {
+    if (ctx->dense) return prepare_dense(ctx, level);
     const auto t_start = std::chrono::steady_clock::now();
     drop_graph(ctx);
     hipStream_t s = ctx->stream;
@@ -972,6 +1020,15 @@ int enqueue_evaluation(wfsa_dev* ctx, bool want_logq, const unsigned* halted, in
                        int32_t* n_ll = nullptr, const wfsa::QnArgs* fin = nullptr, bool* fin_done = nullptr) {
     hipStream_t s = ctx->stream;
     const int32_t np = ctx->n_params;
+    if (ctx->dense) {   // fp64 MFMA path: out is complete when it returns
+        HIP_TRY(record(ctx, ctx->k0, slot, s));
+        HIP_TRY(ctx->dense->enqueue(ctx->ewp.ptr, false, ctx->out.ptr, want_logq ? ctx->logq.ptr : nullptr, halted, s));
+        HIP_TRY(record(ctx, ctx->kc, slot, s));
+        HIP_TRY(record(ctx, ctx->k2, slot, s));
+        if (n_ll) *n_ll = 0;
+        if (fin_done) *fin_done = false;
+        return WFSA_OK;
+    }
     // The bubble kernel reads only the weights (ewp, staged before this
     // point) and writes its own slots and ll partials, so it runs on a second
     // stream beside the stream kernel (not with log q, where both write the
@@ -1059,7 +1116,7 @@ int enqueue_qn_step(wfsa_dev* ctx, double eta, double tol, int64_t e, bool timed
     ctx->ll_cur = ctx->ll_part.ptr + size_t(par) * ctx->ll_stride;
     // without the tail (no bubbles, no communicator) the QN kernels add the
     // constant gradient and sum the log-likelihood partials themselves
-    const bool tail = ctx->comm != nullptr || ctx->n_bubbles > 0;
+    const bool tail = ctx->comm != nullptr || ctx->n_bubbles > 0 || ctx->dense != nullptr;
     int32_t n_ll = 0;
     bool fin_done = false;
     if (int rc = enqueue_evaluation(ctx, false, ctx->qn_halted.ptr, timed ? slot : -1, tail, &n_ll, fin, &fin_done))
@@ -1113,6 +1170,71 @@ void drop_graph(wfsa_dev* ctx) {
     ctx->graph_failed = false;
 }
 
+// weights in / results out, sized by n_params
+int alloc_param_buffers(wfsa_dev* ctx) {
+    HIP_TRY(ctx->w_full.alloc(size_t(ctx->n_params) + 2));
+    HIP_TRY(ctx->ewp.alloc(size_t(ctx->n_params) + 2));
+    HIP_TRY(ctx->out.alloc(size_t(ctx->n_params) + 2));
+    const size_t pinned_need = weights_off(ctx->n_params) + size_t(ctx->n_params) + 2;
+    if (ctx->pinned_n < pinned_need) {
+        if (ctx->pinned) (void)hipHostFree(ctx->pinned);
+        ctx->pinned = nullptr;
+        HIP_TRY(hipHostMalloc(reinterpret_cast<void**>(&ctx->pinned), pinned_need * sizeof(double),
+                              hipHostMallocMapped | hipHostMallocCoherent));
+        HIP_TRY(hipHostGetDevicePointer(reinterpret_cast<void**>(&ctx->pinned_dev), ctx->pinned, 0));
+        ctx->pinned_n = pinned_need;
+        std::memset(ctx->pinned, 0, pinned_need * sizeof(double));   // incl. the weights' zero slot
+    }
+    return WFSA_OK;
+}
+
+// the loaded corpus handed to the dense path (host copies from the device)
+int dense_load_corpus(wfsa_dev* ctx, const uint8_t* sym, const int64_t* off, const double* p) {
+    hipStream_t s = ctx->stream;
+    const hipError_t e = ctx->dense->load_corpus(sym, off, p, ctx->n_strings, s);
+    if (e != hipSuccess)
+        return fail(WFSA_ERR_HIP, "dense path: corpus of %lld strings does not fit (%s)", (long long)ctx->n_strings,
+                    hipGetErrorString(e));
+    ctx->dense_struct = false;
+    ctx->prep_level = 0;
+    return WFSA_OK;
+}
+
+int load_dense_model(wfsa_dev* ctx, const wfsa::DenseModel& dm) {
+    hipStream_t s = ctx->stream;
+    auto d = std::make_unique<wfsa::DensePath>();
+    if (hipError_t e = d->load_model(dm, s); e != hipSuccess)
+        return fail(WFSA_ERR_HIP, "dense path: model upload failed (%s)", hipGetErrorString(e));
+    ctx->dense = std::move(d);
+    ctx->n_params = dm.n_params;
+    ctx->n_nodes = dm.n_states;
+    ctx->n_edges = dm.n_transitions;
+    ctx->n_end = 0;
+    ctx->start = 0;
+    ctx->n_groups = 0;
+    ctx->n_bubbles = 0;
+    ctx->n_fall[0] = ctx->n_fall[1] = 0;
+    if (int rc = alloc_param_buffers(ctx)) return rc;
+    HIP_TRY(hipStreamSynchronize(s));
+    ctx->has_model = true;
+    ctx->stats.n_nodes = ctx->n_nodes;
+    ctx->stats.n_edges = ctx->n_edges;
+    ctx->stats.n_end_edges = 0;
+    ctx->stats.dense = 1;
+    ctx->prep_level = 0;
+    if (!ctx->has_corpus) return WFSA_OK;
+    const size_t S = size_t(ctx->n_strings);
+    std::vector<int64_t> off(S + 1);
+    std::vector<double> p(std::max<size_t>(S, 1));
+    HIP_TRY(ctx->off.download(off.data(), S + 1, s));
+    HIP_TRY(ctx->p.download(p.data(), S, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    std::vector<uint8_t> sym(std::max<size_t>(size_t(off[S]), 1));
+    HIP_TRY(ctx->sym.download(sym.data(), size_t(off[S]), s));
+    HIP_TRY(hipStreamSynchronize(s));
+    return dense_load_corpus(ctx, sym.data(), off.data(), p.data());
+}
+
 }  // namespace
 
 extern "C" {
@@ -1139,6 +1261,7 @@ int wfsa_dev_create(int device, wfsa_dev** out) {
     if (const char* e = std::getenv("WFSA_GRAPH")) ctx->use_graph = e[0] == '1';
     if (const char* e = std::getenv("WFSA_TIMING")) ctx->kernel_timing = e[0] != '0';
     if (const char* e = std::getenv("WFSA_FUSE_BUBBLES")) ctx->fuse_bubbles = e[0] != '0';
+    if (const char* e = std::getenv("WFSA_DENSE"); e && e[0]) ctx->dense_mode = e[0] == '0' ? 0 : 1;
 
     HIP_TRY(hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking));
     // measured: the cross-stream fork/join costs more idle time (5-20 us)
@@ -1188,6 +1311,13 @@ void wfsa_dev_destroy(wfsa_dev* ctx) {
 int wfsa_dev_load_model(wfsa_dev* ctx, const wfsa_model_desc* model) {
     if (int rc = check_ctx(ctx)) return rc;
     if (!model) return fail(WFSA_ERR_ARG, "null model");
+    drop_graph(ctx);
+    ctx->dense.reset();
+    ctx->dense_struct = false;
+    if (ctx->dense_mode != 0) {
+        wfsa::DenseModel dm;
+        if (wfsa::dense_model_build(*model, ctx->dense_mode == 1, dm).empty()) return load_dense_model(ctx, dm);
+    }
     wfsa::TrellisModel tm;
     const std::string err = wfsa::compile_trellis_model(*model, tm);
     if (!err.empty()) return fail(WFSA_ERR_MODEL, "automaton rejected: %s", err.c_str());
@@ -1230,19 +1360,7 @@ int wfsa_dev_load_model(wfsa_dev* ctx, const wfsa_model_desc* model) {
     ctx->n_params = tm.n_params;
     ctx->n_nodes = tm.n_nodes;
     ctx->start = tm.start;
-    HIP_TRY(ctx->w_full.alloc(size_t(ctx->n_params) + 2));
-    HIP_TRY(ctx->ewp.alloc(size_t(ctx->n_params) + 2));
-    HIP_TRY(ctx->out.alloc(size_t(ctx->n_params) + 2));
-    const size_t pinned_need = weights_off(ctx->n_params) + size_t(ctx->n_params) + 2;
-    if (ctx->pinned_n < pinned_need) {
-        if (ctx->pinned) (void)hipHostFree(ctx->pinned);
-        ctx->pinned = nullptr;
-        HIP_TRY(hipHostMalloc(reinterpret_cast<void**>(&ctx->pinned), pinned_need * sizeof(double),
-                              hipHostMallocMapped | hipHostMallocCoherent));
-        HIP_TRY(hipHostGetDevicePointer(reinterpret_cast<void**>(&ctx->pinned_dev), ctx->pinned, 0));
-        ctx->pinned_n = pinned_need;
-        std::memset(ctx->pinned, 0, pinned_need * sizeof(double));   // incl. the weights' zero slot
-    }
+    if (int rc = alloc_param_buffers(ctx)) return rc;
     HIP_TRY(hipStreamSynchronize(s));
     ctx->has_model = true;
     ctx->stats.n_nodes = ctx->n_nodes;
@@ -1284,6 +1402,8 @@ int wfsa_dev_load_corpus(wfsa_dev* ctx, const uint8_t* sym, const int64_t* off, 
     ctx->stats.n_strings = n_strings;
     ctx->stats.total_symbols = total;
     ctx->stats.max_len = int32_t(max_len);
+    drop_graph(ctx);
+    if (ctx->dense) return dense_load_corpus(ctx, sym, off, p);
     if (ctx->has_model) return configure_tiers(ctx);
     return WFSA_OK;
 }
@@ -1291,7 +1411,7 @@ int wfsa_dev_load_corpus(wfsa_dev* ctx, const uint8_t* sym, const int64_t* off, 
 int wfsa_dev_recognize(wfsa_dev* ctx, uint8_t* recognized, double* path_count, uint8_t* used_param) {
     if (int rc = check_ctx(ctx)) return rc;
     if (!ctx->has_model || !ctx->has_corpus) return fail(WFSA_ERR_ARG, "load a model and a corpus first");
-    if (ctx->prep_level < 1)
+    if (ctx->dense ? !ctx->dense_struct : ctx->prep_level < 1)
         if (int rc = prepare(ctx, 1)) return rc;
     hipStream_t s = ctx->stream;
     const size_t S = size_t(ctx->n_strings);

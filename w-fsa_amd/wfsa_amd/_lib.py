@@ -39,7 +39,7 @@ class DevStats(C.Structure):
         ("stream_words", i64), ("stream_bytes", i64), ("bubble_words", i64), ("n_bubbles", i64), ("fb_launches", i64), ("fb_kernel_ms", dbl),
         ("last_fb_kernel_ms", dbl), ("last_compiled_ms", dbl), ("last_call_ms", dbl),
         ("last_live_edges", i64), ("tier1_strings", i32), ("waves_per_block", i32), ("prepare_ms", dbl),
-        ("compiled_kernel_ms", dbl), ("graph", i32), ("reserved", i32),
+        ("compiled_kernel_ms", dbl), ("graph", i32), ("dense", i32),
         ("host_steps", i64), ("host_begin_ms", dbl), ("host_overlap_ms", dbl), ("host_wait_ms", dbl),
         ("host_post_ms", dbl),
     ]
