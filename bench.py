@@ -26,26 +26,39 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "w-fsa_amd"))
 
 HBM_PEAK_GBS = 8000.0        # MI355X_MICROARCH.md: HBM3E 8 TB/s (spec)
+F64_MFMA_PEAK_TFS = 78.6     # MI355X spec: FP64 matrix (dense) 78.6 TF (= the FP64 vector rate)
 METRIC = "forward-backward strings/sec @1/2/4/8 GPU; log-lik rel-err vs MKL ref"
 
 
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=200)
-    ap.add_argument("--warmup", type=int, default=10)
-    ap.add_argument("--strings-per-gpu", type=int, default=1_000_000)
-    ap.add_argument("--states", type=int, default=1024)
+    ap.add_argument("--workload", choices=("c3", "c5"), default="c3",
+                    help="c3: 1024-state sparse family A, 1M strings/GPU (the headline); "
+                         "c5: dense 4096-state automaton on the fp64 MFMA path")
+    ap.add_argument("--steps", type=int, default=None)
+    ap.add_argument("--warmup", type=int, default=None)
+    ap.add_argument("--strings-per-gpu", type=int, default=None)
+    ap.add_argument("--states", type=int, default=None)
     ap.add_argument("--degree", type=int, default=8)
-    ap.add_argument("--vocab", type=int, default=64)
-    ap.add_argument("--emissions", type=int, default=1)
+    ap.add_argument("--vocab", type=int, default=None)
+    ap.add_argument("--emissions", type=int, default=None)
     ap.add_argument("--max-len", type=int, default=128)
     ap.add_argument("--seed", type=int, default=1)
-    ap.add_argument("--cpu-sample", type=int, default=200_000,
+    ap.add_argument("--cpu-sample", type=int, default=None,
                     help="strings timed through the CPU oracle (0 = skip)")
     ap.add_argument("--profile-traffic", default=os.path.join(ROOT, "profiles", "traffic_latest.json"),
                     help="committed PMC traffic measurement to quote (if present)")
-    return ap.parse_args()
+    a = ap.parse_args()
+    dense = a.workload == "c5"
+    defaults = dict(steps=(10 if dense else 200), warmup=(2 if dense else 10),
+                    strings_per_gpu=(4096 if dense else 1_000_000), states=(4096 if dense else 1024),
+                    vocab=(16 if dense else 64), emissions=(16 if dense else 1),
+                    cpu_sample=(1 if dense else 200_000))
+    for k, v in defaults.items():
+        if getattr(a, k) is None:
+            setattr(a, k, v)
+    return a
 
 
 def cpu_baseline(syn_text, sym, off, wt, n_sample):
@@ -86,6 +99,32 @@ def cpu_baseline(syn_text, sym, off, wt, n_sample):
     }, rel, ll_ref, ll_dev
 
 
+def cpu_baseline_dense(syn_text, sym, off, wt, n_sample):
+    """The oracle's trellis restatement (oracle/wfsa_oracle.c TRELLIS: dense
+    float64 forward-backward, one core) on the first strings of the corpus.
+    The reference algorithm (BFS path enumeration) cannot run this model:
+    a length-32 string has ~4096^32 paths."""
+    from oracle import Oracle, TRELLIS
+    n = min(n_sample, len(wt))
+    s_off = off[: n + 1].copy()
+    s_sym = sym[: s_off[-1]].copy()
+    t0 = time.perf_counter()
+    o = Oracle.from_arrays(syn_text, s_sym, s_off, wt[:n].copy(), mode=TRELLIS)
+    t_build = time.perf_counter() - t0
+    w = np.array(o.w_full())
+    t0 = time.perf_counter()
+    o.trellis_eval(w)
+    t_eval = time.perf_counter() - t0
+    return {
+        "value": n / t_eval, "unit": "strings/s", "cores": 1, "kind": "port",
+        "sample": (f"first {n} string(s) ({int(s_off[-1])} symbols) of the same corpus through oracle/wfsa_oracle.c "
+                   f"TRELLIS (dense fp64 forward-backward, one core): {t_eval:.1f} s per evaluation; "
+                   f"build incl. its structural pass {t_build:.1f} s; path enumeration (the reference "
+                   f"algorithm) is infeasible here"),
+        "iteration_s": t_eval,
+    }
+
+
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -102,8 +141,9 @@ def main():
     import wfsa_amd as W
 
     total = args.strings_per_gpu * world
+    dense = args.workload == "c5"
     syn = W.Synthetic(n_states=args.states, degree=args.degree, vocab=args.vocab, emissions=args.emissions,
-                      n_strings=total, max_len=args.max_len, seed=args.seed)
+                      dense=dense, n_strings=total, max_len=args.max_len, seed=args.seed)
     sym, off, wt = syn.corpus()
     fsa = W.Fsa.read_text(syn.wfsa_text)
 
@@ -156,11 +196,56 @@ def main():
     alg_bytes = int(local_sym * comp / max(local_strings, 1)) + 16 * comp
     achieved = alg_bytes / (kern_ms * 1e-3) / 1e9 if kern_ms > 0 else None   # None: WFSA_TIMING=0
     traffic = None
-    if os.path.exists(args.profile_traffic):
+    if not dense and os.path.exists(args.profile_traffic):
         try:
             traffic = json.load(open(args.profile_traffic)).get("hbm_bytes_per_launch")
         except Exception:
             traffic = None
+
+    if dense:
+        # 3 GEMM-equivalents of 2 N^2 flops per string
+        # position (forward, backward, gradient); every evaluation kernel is
+        # inside the timed span (weights, GEMMs, log q, reductions)
+        N = args.states
+        alg_flops = 6.0 * N * N * local_sym
+        npd, R, T = st1["dense_np"], st1["dense_rows"], st1["dense_steps"]
+        issued = 6.0 * npd * npd * R * max(T - 1, 0)
+        tf = alg_flops / (fb_ms * 1e-3) / 1e12 if fb_ms > 0 else None
+        workload = (f"c5 dense: {N}-state WFSA, full transition matrix (every S->T and S->$), every state "
+                    f"emits every one of {args.vocab} symbols, {args.strings_per_gpu} distinct strings per GPU "
+                    f"sampled from it (mean len {np.diff(off).mean():.1f}, max {args.max_len})")
+        roofline = {
+            "bound": "mfma",
+            "achieved": tf,
+            "peak": F64_MFMA_PEAK_TFS,
+            "unit": "TFLOP/s",
+            "frac": tf / F64_MFMA_PEAK_TFS if tf else None,
+            "traffic": None,
+            "kernel": "dense_gemm_kernel<FWD/BWD/GRAD> (v_mfma_f64_16x16x4f64) + its epilogue kernels, one evaluation",
+            "timed_launches": timed,
+            "evaluation_ms": fb_ms,
+            "algorithmic_flops_per_evaluation": alg_flops,
+            "issued_flops_per_evaluation": issued,
+            "row_slots": R,
+            "trellis_steps": T,
+        }
+    else:
+        workload = (f"c3 family A: {args.states}-state sparse WFSA, out-degree {args.degree}+end, "
+                    f"{args.emissions} of {args.vocab} symbols/state, {args.strings_per_gpu} distinct "
+                    f"strings per GPU (mean len {np.diff(off).mean():.1f}, max {args.max_len})")
+        roofline = {
+            "bound": "hbm",
+            "achieved": achieved,
+            "peak": HBM_PEAK_GBS,
+            "unit": "GB/s",
+            "frac": achieved / HBM_PEAK_GBS if achieved else None,
+            "traffic": traffic,
+            "kernel": "fbs_kernel (compiled-stream forward pass, per-iteration)",
+            "timed_launches": timed,
+            "kernel_ms_per_launch": kern_ms,
+            "all_fb_kernels_ms_per_step": fb_ms,
+            "algorithmic_bytes_per_launch": alg_bytes,
+        }
 
     out = {
         "metric": METRIC,
@@ -176,27 +261,13 @@ def main():
         "dtype": "f64",
         "data": "synthetic",
         "config": {
-            "workload": (f"c3 family A: {args.states}-state sparse WFSA, out-degree {args.degree}+end, "
-                         f"{args.emissions} of {args.vocab} symbols/state, {args.strings_per_gpu} distinct "
-                         f"strings per GPU (mean len {np.diff(off).mean():.1f}, max {args.max_len})"),
+            "workload": workload,
             "global_strings": strings_all,
             "strings_per_gpu": args.strings_per_gpu,
             "parallelism": f"dp{n_gpus}",
             "step": "QuasiNewtonLearner::OptimizationStep (H2D w, forward-backward, all-reduce, D2H grad, host update; epoch loop in wfsa_learner_run)",
         },
-        "roofline": {
-            "bound": "hbm",
-            "achieved": achieved,
-            "peak": HBM_PEAK_GBS,
-            "unit": "GB/s",
-            "frac": achieved / HBM_PEAK_GBS if achieved else None,
-            "traffic": traffic,
-            "kernel": "fbs_kernel (compiled-stream forward pass, per-iteration)",
-            "timed_launches": timed,
-            "kernel_ms_per_launch": kern_ms,
-            "all_fb_kernels_ms_per_step": fb_ms,
-            "algorithmic_bytes_per_launch": alg_bytes,
-        },
+        "roofline": roofline,
         "host_ms_per_step": {k: (st1["host_" + k + "_ms"] - st0["host_" + k + "_ms"]) /
                              max(st1["host_steps"] - st0["host_steps"], 1)
                              for k in ("begin", "overlap", "wait", "post")},
@@ -211,7 +282,9 @@ def main():
         "bubble_words": st1["bubble_words"],
         "prepare_ms": st1["prepare_ms"],
     }
-    if rank == 0 and world == 1 and args.cpu_sample > 0:
+    if rank == 0 and world == 1 and args.cpu_sample > 0 and dense:
+        out["cpu_baseline"] = cpu_baseline_dense(syn.wfsa_text, sym, off, wt, args.cpu_sample)
+    elif rank == 0 and world == 1 and args.cpu_sample > 0:
         cb, rel, ll_ref, ll_dev = cpu_baseline(syn.wfsa_text, sym, off, wt, args.cpu_sample)
         out["cpu_baseline"] = cb
         out["ll_rel_err_vs_reference_algorithm"] = rel

@@ -99,6 +99,9 @@ typedef struct {
      * it, after it (gradient mapping + update) */
     int64_t host_steps;
     double host_begin_ms, host_overlap_ms, host_wait_ms, host_post_ms;
+    /* dense path (dense == 1): row slots R and trellis steps T of the packed
+     * corpus; each evaluation runs 3 GEMMs of 2 np^2 R flops per step */
+    int32_t dense_rows, dense_steps, dense_np, dense_pad;
 } wfsa_dev_stats;
 
 /* context ---------------------------------------------------------------- */

@@ -38,17 +38,30 @@ namespace {
 typedef double d4 __attribute__((ext_vector_type(4)));
 
 constexpr int kT = kDenseTile;        // 128
-constexpr int kBK = 16;               // K slice per LDS stage
-constexpr int kLdk = kBK + 2;         // padded LDS row (doubles)
-constexpr int kGemmThreads = 256;
-constexpr int kStage = 2 * kT * kLdk; // doubles per stage (A and B operands)
+// K slice per LDS stage: 32 for the per-step GEMMs (one block per CU, the
+// longer slice hides the slice-boundary barrier), 16 for the gradient GEMM
+// (two blocks per CU)
+constexpr int kBkStep = 32, kBkGrad = 16;
+// waves per block: 8 for the per-step GEMMs (one block per CU: two waves per
+// SIMD hide each other's LDS and barrier time), 4 for the gradient GEMM (two
+// blocks per CU do that)
+constexpr int kNwStep = 8, kNwGrad = 4;
+// padded LDS row (doubles): BK + 2 == 2 (mod 32) keeps a 64-lane fragment
+// read conflict free
+template <int BK> constexpr int ldk() { return BK + 2; }
+template <int BK> constexpr int stage() { return 2 * kT * ldk<BK>(); }   // doubles per stage (A and B)
 constexpr int kRedThreads = 128;      // dense_reduce: one column per thread
+// row pitch of the row-slot buffers = np + 16 doubles: a 128-row tile read
+// along k then spreads over memory channels and L2 sets (a power-of-two pitch
+// puts every row of the tile on the same ones)
+constexpr int kRowPad = 16;
 constexpr int kRedWindow = 64;        // symbols per LDS pass of dense_reduce
 
 enum GemmMode { FWD = 0, BWD = 1, GRAD = 2 };
 
 struct GemmArgs {
     int32_t R, np, nct;
+    int32_t ldx;               // row pitch of the row-slot buffers (alpha, Y, z, gamma)
     int64_t kg;                // GRAD: K = (T - 1) R
     const double* x;           // FWD alpha[t] / BWD Y[t+1] / GRAD alpha (steps 0..T-2)
     const double* bm;          // FWD, BWD: A / GRAD: z from step 1
@@ -83,14 +96,18 @@ struct GemmArgs {
 // operand's row r is contiguous along k (element (r, k) at base[r ld + k]);
 // RC: rows of memory run along the operand's rows (element (r, k) at
 // base[k ld + r]).  Either way LDS holds [r][k] (kLdk stride).
-template <bool KC>
+// chunks of 16 bytes per thread for one 128 x BK slice
+template <int BK, int NT> constexpr int slice_chunks() { return kT * BK / 2 / NT; }
+
+template <bool KC, int BK, int NT>
 __device__ __forceinline__ void load_slice(const double* __restrict__ base, int64_t ld, int r0, int64_t k0, int tid,
-                                           double2 (&v)[4]) {
+                                           double2 (&v)[slice_chunks<BK, NT>()]) {
+    constexpr int kPairs = BK / 2;   // 16-byte chunks per row of the slice
 #pragma unroll
-    for (int c = 0; c < 4; ++c) {
-        const int idx = c * kGemmThreads + tid;
+    for (int c = 0; c < slice_chunks<BK, NT>(); ++c) {
+        const int idx = c * NT + tid;
         if (KC) {
-            const int row = idx >> 3, kp = idx & 7;
+            const int row = idx / kPairs, kp = idx % kPairs;
             v[c] = *reinterpret_cast<const double2*>(base + int64_t(r0 + row) * ld + k0 + 2 * kp);
         } else {
             const int kk = idx >> 6, rp = idx & 63;
@@ -99,35 +116,41 @@ __device__ __forceinline__ void load_slice(const double* __restrict__ base, int6
     }
 }
 
-template <bool KC>
-__device__ __forceinline__ void store_slice(double* __restrict__ s, int tid, const double2 (&v)[4]) {
+template <bool KC, int BK, int NT>
+__device__ __forceinline__ void store_slice(double* __restrict__ s, int tid, const double2 (&v)[slice_chunks<BK, NT>()]) {
+    constexpr int kPairs = BK / 2, L = ldk<BK>();
 #pragma unroll
-    for (int c = 0; c < 4; ++c) {
-        const int idx = c * kGemmThreads + tid;
+    for (int c = 0; c < slice_chunks<BK, NT>(); ++c) {
+        const int idx = c * NT + tid;
         if (KC) {
-            const int row = idx >> 3, kp = idx & 7;
-            *reinterpret_cast<double2*>(s + row * kLdk + 2 * kp) = v[c];
+            const int row = idx / kPairs, kp = idx % kPairs;
+            *reinterpret_cast<double2*>(s + row * L + 2 * kp) = v[c];
         } else {
             const int kk = idx >> 6, rp = idx & 63;
-            s[(2 * rp) * kLdk + kk] = v[c].x;
-            s[(2 * rp + 1) * kLdk + kk] = v[c].y;
+            s[(2 * rp) * L + kk] = v[c].x;
+            s[(2 * rp + 1) * L + kk] = v[c].y;
         }
     }
 }
 
-template <int MODE>
-__global__ __launch_bounds__(kGemmThreads, 2) void dense_gemm_kernel(GemmArgs a) {
+// NW waves per 128 x 128 block: 2 x (NW / 2), each a 64 x (256 / NW) tile
+// of 16 x 16 MFMA tiles (NJ of them per row of tiles)
+template <int MODE, int BK, int NW>
+__global__ __launch_bounds__(NW * 64, 2) void dense_gemm_kernel(GemmArgs a) {
     if (a.halted && *a.halted) return;
+    constexpr int NT = NW * 64, NWN = NW / 2, NJ = 16 / NW, WCOLS = 16 * NJ;
+    constexpr int kLdk = ldk<BK>(), kStage = stage<BK>();
+    constexpr int CH = slice_chunks<BK, NT>();
     __shared__ __attribute__((aligned(16))) double lds[2 * kStage];
-    __shared__ double red[2][kT];
+    __shared__ double red[NWN][kT];
     __shared__ double rs0[kT], rs1[kT], rs2[kT];
     __shared__ int32_t rmeta[kT];
 
     constexpr bool A_KC = MODE != GRAD;   // FWD / BWD: x rows are contiguous along k
-    constexpr bool B_KC = MODE == BWD;    // BWD: A^T (rows of A); FWD: A; GRAD: z
+    constexpr bool B_KC = false;          // FWD: A, BWD: A^T (stored), GRAD: z -- all along memory rows
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int wm = wave >> 1, wn = wave & 1;
-    const int np = a.np;
+    const int wm = wave / NWN, wn = wave % NWN;
+    const int np = a.np, ldx = a.ldx;
     const int mtiles = (MODE == GRAD ? np : a.R) / kT, ntiles = np / kT;
     const int nb = mtiles * ntiles;
     int bid = int(blockIdx.x);
@@ -135,7 +158,8 @@ __global__ __launch_bounds__(kGemmThreads, 2) void dense_gemm_kernel(GemmArgs a)
     const int mt_ = bid % mtiles, nt_ = bid / mtiles;
     const int r0 = mt_ * kT, c0 = nt_ * kT;
 
-    // per-row scalars of the block's output rows
+    // per-row scalars of the block's output rows (read by the epilogue)
+    auto row_scalars = [&]() {
     if (MODE != GRAD && tid < kT) {
         const int r = r0 + tid;
         const int m = a.meta[r];
@@ -174,66 +198,70 @@ __global__ __launch_bounds__(kGemmThreads, 2) void dense_gemm_kernel(GemmArgs a)
         }
         rmeta[tid] = m;
     }
+    };
 
-    d4 acc[4][4];
+    d4 acc[4][NJ];
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
-        for (int j = 0; j < 4; ++j) acc[i][j] = d4{0.0, 0.0, 0.0, 0.0};
+        for (int j = 0; j < NJ; ++j) acc[i][j] = d4{0.0, 0.0, 0.0, 0.0};
 
     if (!a.no_mma) {
-        const int64_t nk = (MODE == GRAD ? a.kg : int64_t(np)) / kBK;
+        const int64_t nk = (MODE == GRAD ? a.kg : int64_t(np)) / BK;
         const double* xa = a.x;
         const double* xb = a.bm;
-        double2 va[4], vb[4];
-        load_slice<A_KC>(xa, np, r0, 0, tid, va);
-        load_slice<B_KC>(xb, np, c0, 0, tid, vb);
-        store_slice<A_KC>(lds, tid, va);
-        store_slice<B_KC>(lds + kT * kLdk, tid, vb);
+        double2 va[CH], vb[CH];
+        const int ldb = MODE == GRAD ? ldx : np;   // z / A, A^T
+        load_slice<A_KC, BK, NT>(xa, ldx, r0, 0, tid, va);
+        load_slice<B_KC, BK, NT>(xb, ldb, c0, 0, tid, vb);
+        row_scalars();   // its loads overlap the first slice's
+        store_slice<A_KC, BK, NT>(lds, tid, va);
+        store_slice<B_KC, BK, NT>(lds + kT * kLdk, tid, vb);
         __syncthreads();
         for (int64_t kt = 0; kt < nk; ++kt) {
             const bool more = kt + 1 < nk;
             if (more) {
-                load_slice<A_KC>(xa, np, r0, (kt + 1) * kBK, tid, va);
-                load_slice<B_KC>(xb, np, c0, (kt + 1) * kBK, tid, vb);
+                load_slice<A_KC, BK, NT>(xa, ldx, r0, (kt + 1) * BK, tid, va);
+                load_slice<B_KC, BK, NT>(xb, ldb, c0, (kt + 1) * BK, tid, vb);
             }
             const double* As = lds + (kt & 1) * kStage;
             const double* Bs = As + kT * kLdk;
 #pragma unroll
-            for (int kk = 0; kk < kBK / 4; ++kk) {
-                double av[4], bv[4];
+            for (int kk = 0; kk < BK / 4; ++kk) {
+                double av[4], bv[NJ];
 #pragma unroll
                 for (int i = 0; i < 4; ++i) av[i] = As[(wm * 64 + i * 16 + (lane & 15)) * kLdk + kk * 4 + (lane >> 4)];
 #pragma unroll
-                for (int j = 0; j < 4; ++j) bv[j] = Bs[(wn * 64 + j * 16 + (lane & 15)) * kLdk + kk * 4 + (lane >> 4)];
+                for (int j = 0; j < NJ; ++j) bv[j] = Bs[(wn * WCOLS + j * 16 + (lane & 15)) * kLdk + kk * 4 + (lane >> 4)];
 #pragma unroll
                 for (int i = 0; i < 4; ++i)
 #pragma unroll
-                    for (int j = 0; j < 4; ++j)
+                    for (int j = 0; j < NJ; ++j)
                         acc[i][j] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[i], bv[j], acc[i][j], 0, 0, 0);
             }
             if (more) {
                 double* s = lds + ((kt + 1) & 1) * kStage;
-                store_slice<A_KC>(s, tid, va);
-                store_slice<B_KC>(s + kT * kLdk, tid, vb);
+                store_slice<A_KC, BK, NT>(s, tid, va);
+                store_slice<B_KC, BK, NT>(s + kT * kLdk, tid, vb);
             }
             __syncthreads();
         }
     } else {
+        row_scalars();
         __syncthreads();
     }
 
     // epilogue: element (i, j, e) of this lane is row wm*64 + 16 i + (lane>>4)
-    // + 4 e, column wn*64 + 16 j + (lane & 15) of the block tile
+    // + 4 e, column wn*WCOLS + 16 j + (lane & 15) of the block tile
     if (MODE == GRAD) {
 #pragma unroll
         for (int i = 0; i < 4; ++i)
 #pragma unroll
-            for (int j = 0; j < 4; ++j)
+            for (int j = 0; j < NJ; ++j)
 #pragma unroll
                 for (int e = 0; e < 4; ++e) {
                     const int row = r0 + wm * 64 + 16 * i + (lane >> 4) + 4 * e;
-                    const int col = c0 + wn * 64 + 16 * j + (lane & 15);
+                    const int col = c0 + wn * WCOLS + 16 * j + (lane & 15);
                     const int64_t o = int64_t(row) * np + col;
                     const int32_t code = a.code_a[o];
                     if (code >= 0 && code < a.n_params) a.grad[code] = -a.amat[o] * acc[i][j][e];
@@ -255,9 +283,9 @@ __global__ __launch_bounds__(kGemmThreads, 2) void dense_gemm_kernel(GemmArgs a)
             const int sym = m & 511;
             const double* erow = a.et + int64_t(sym) * np;
 #pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                const int col = c0 + wn * 64 + 16 * j + (lane & 15);
-                const int64_t o = int64_t(row) * np + col;
+            for (int j = 0; j < NJ; ++j) {
+                const int col = c0 + wn * WCOLS + 16 * j + (lane & 15);
+                const int64_t o = int64_t(row) * ldx + col;
                 double v;
                 if (MODE == FWD) {
                     v = ((m >> 9) & 1) ? a.a0[col] : acc[i][j][e] * rs0[rl];
@@ -273,8 +301,8 @@ __global__ __launch_bounds__(kGemmThreads, 2) void dense_gemm_kernel(GemmArgs a)
                 rsum[i][e] += v;
             }
         }
-    // row sums over the tile's 128 columns: 16 lanes per row, then the two
-    // column halves (wn) through LDS
+    // row sums over the tile's 128 columns: 16 lanes per row, then the
+    // NWN column groups (wn) through LDS
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
@@ -287,7 +315,12 @@ __global__ __launch_bounds__(kGemmThreads, 2) void dense_gemm_kernel(GemmArgs a)
             if ((lane & 15) == 0) red[wn][wm * 64 + 16 * i + (lane >> 4) + 4 * e] = v;
         }
     __syncthreads();
-    if (tid < kT) a.part_out[int64_t(nt_) * a.R + r0 + tid] = red[0][tid] + red[1][tid];
+    if (tid < kT) {
+        double v = red[0][tid];
+#pragma unroll
+        for (int g = 1; g < NWN; ++g) v += red[g][tid];
+        a.part_out[int64_t(nt_) * a.R + r0 + tid] = v;
+    }
 }
 
 struct WeightsArgs {
@@ -324,6 +357,21 @@ __global__ __launch_bounds__(256) void dense_weights_kernel(WeightsArgs a) {
     for (int64_t i = t0; i < a.n_out; i += stride) a.out[i] = 0.0;
 }
 
+// A^T for the backward GEMM (its B operand then streams along rows of
+// memory like the forward GEMM's): 32 x 32 tiles through LDS
+__global__ __launch_bounds__(256) void dense_transpose_kernel(const double* __restrict__ a, double* __restrict__ at,
+                                                              int32_t np, const unsigned* halted) {
+    if (halted && *halted) return;
+    __shared__ double tile[32][33];
+    const int bx = blockIdx.x * 32, by = blockIdx.y * 32;
+    const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;
+#pragma unroll
+    for (int k = 0; k < 32; k += 8) tile[ty + k][tx] = a[int64_t(by + ty + k) * np + bx + tx];
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < 32; k += 8) at[int64_t(bx + ty + k) * np + by + tx] = tile[tx][ty + k];
+}
+
 struct FinalArgs {
     const double* alpha;        // [T][R][np]
     const double* la;           // [T][R]
@@ -333,7 +381,7 @@ struct FinalArgs {
     const double* ewp;
     int32_t code_se;
     int64_t n_strings;
-    int32_t np;
+    int32_t np, ldx;
     double* logq;               // [S]
     double* logq_user;          // [S] or null
     double* ll_part;            // [blocks]
@@ -351,7 +399,7 @@ __global__ __launch_bounds__(256) void dense_final_kernel(FinalArgs a) {
         const int32_t at = a.end_at[s];
         double lq;
         if (at >= 0) {
-            const double* row = a.alpha + int64_t(at) * a.np;
+            const double* row = a.alpha + int64_t(at) * a.ldx;
             double d = 0.0;
             for (int c = lane; c < a.np; c += 64) d += row[c] * a.aend[c];
 #pragma unroll
@@ -376,7 +424,7 @@ struct ReduceArgs {
     const int32_t* meta;        // [T R]
     int64_t rows;               // T R
     int64_t rows_per_chunk;
-    int32_t np, vocab;
+    int32_t np, vocab, ldx;
     double* red;                // [chunks][vocab + 2][np]
     const unsigned* halted;
 };
@@ -400,7 +448,7 @@ __global__ __launch_bounds__(kRedThreads) void dense_reduce_kernel(ReduceArgs a)
             const int m = a.meta[r];
             const int sym = m & 511;
             if (sym >= V) continue;   // idle slot
-            const double g = a.gam[r * a.np + col];
+            const double g = a.gam[r * a.ldx + col];
             const int k = sym - vb;
             if (k >= 0 && k < wv) acc[k * kRedThreads + t] += g;
             if (vb == 0) {
@@ -552,7 +600,7 @@ DensePath::~DensePath() {
 
 void DensePath::free_model() {
     dfree(code_a_); dfree(code_s_); dfree(code_e_); dfree(code_em_);
-    dfree(amat_); dfree(et_); dfree(a0_); dfree(aend_); dfree(ones_);
+    dfree(amat_); dfree(amat_t_); dfree(et_); dfree(a0_); dfree(aend_); dfree(ones_);
 }
 
 void DensePath::free_corpus() {
@@ -564,6 +612,7 @@ void DensePath::free_corpus() {
 }
 
 hipError_t DensePath::load_model(const DenseModel& m, hipStream_t s) {
+    if (const char* e = std::getenv("WFSA_DENSE_GRAD_CFG")) grad_cfg_ = std::atoi(e);   // timing experiments
     free_corpus();
     free_model();
     n_params_ = m.n_params;
@@ -582,6 +631,7 @@ hipError_t DensePath::load_model(const DenseModel& m, hipStream_t s) {
     DTRY(hipMemcpyAsync(code_e_, m.code_e.data(), np * 4, hipMemcpyHostToDevice, s));
     DTRY(hipMemcpyAsync(code_em_, m.code_em.data(), size_t(vocab_ + 1) * np * 4, hipMemcpyHostToDevice, s));
     DTRY(dalloc(amat_, np * np));
+    DTRY(dalloc(amat_t_, np * np));
     DTRY(dalloc(et_, size_t(vocab_ + 1) * np));
     DTRY(dalloc(a0_, np));
     DTRY(dalloc(aend_, np));
@@ -609,10 +659,24 @@ hipError_t DensePath::load_corpus(const uint8_t* sym, const int64_t* off, const 
         else { p0_sum_ += p[i]; n0_ += 1.0; }
     }
     total_sym_ = total;
-    // slots: enough that the longest string sets the step count
-    int64_t R = lmax > 0 ? (total + lmax - 1) / lmax : 1;
-    R = std::min<int64_t>(R, int64_t(order.size()));
-    R = std::max<int64_t>(1, (R + kT - 1) / kT) * kT;
+    // slots: R rows (a multiple of the tile) and T >= max(lmax, total / R)
+    // steps; a step's GEMM is (R / 128) x (np / 128) blocks, which run in
+    // ceil(blocks / CUs) rounds -- pick the R with the fewest step-rounds
+    int64_t R = kT;
+    {
+        const int64_t cap = std::max<int64_t>(1, (int64_t(order.size()) + kT - 1) / kT);
+        double best = -1.0;
+        for (int64_t k = 1; k <= cap; ++k) {
+            const int64_t r = k * kT;
+            const int64_t t = std::max<int64_t>(lmax, (total + r - 1) / r);
+            const int64_t blocks = k * int64_t(nct_);
+            const double cost = double(std::max<int64_t>(t - 1, 1)) * double((blocks + n_cu_ - 1) / n_cu_);
+            if (best < 0.0 || cost < best - 1e-9) {
+                best = cost;
+                R = r;
+            }
+        }
+    }
     std::stable_sort(order.begin(), order.end(), [&](int32_t a, int32_t b) {
         return off[a + 1] - off[a] > off[b + 1] - off[b];
     });
@@ -667,10 +731,12 @@ hipError_t DensePath::load_corpus(const uint8_t* sym, const int64_t* off, const 
     DTRY(hipMemcpyAsync(pones_, ones.data(), S * 8, hipMemcpyHostToDevice, s));
     DTRY(dalloc(la_, TR));
     DTRY(dalloc(lb_, TR));
-    DTRY(dalloc(alpha_, TR * np));
-    DTRY(dalloc(gam_, TR * np));
-    DTRY(dalloc(z_, TR * np));
-    DTRY(dalloc(y_, 2 * size_t(R) * np));
+    ldx_ = np_ + kRowPad;
+    const size_t ld = size_t(ldx_);
+    DTRY(dalloc(alpha_, TR * ld));
+    DTRY(dalloc(gam_, TR * ld));
+    DTRY(dalloc(z_, TR * ld));
+    DTRY(dalloc(y_, 2 * size_t(R) * ld));
     DTRY(dalloc(part_, 2 * size_t(nct_) * size_t(R)));
     n_ll_ = int32_t((S + 3) / 4);
     DTRY(dalloc(ll_part_, size_t(std::max(n_ll_, 1))));
@@ -706,12 +772,14 @@ hipError_t DensePath::enqueue(const double* ewp, bool structural, double* out, d
         a.halted = halted;
         dense_weights_kernel<<<1024, 256, 0, s>>>(a);
         DTRY(hipGetLastError());
+        dense_transpose_kernel<<<dim3(unsigned(np / 32), unsigned(np / 32)), 256, 0, s>>>(amat_, amat_t_, np_, halted);
+        DTRY(hipGetLastError());
     }
     if (n_strings_ == 0 || total_sym_ == 0) {
         FinalArgs f{};
         if (n_strings_ > 0) {
             f.alpha = alpha_; f.la = la_; f.aend = aend_; f.end_at = end_at_; f.p = p; f.ewp = w;
-            f.code_se = code_se_; f.n_strings = n_strings_; f.np = np_; f.logq = logq_; f.logq_user = logq;
+            f.code_se = code_se_; f.n_strings = n_strings_; f.np = np_; f.ldx = ldx_; f.logq = logq_; f.logq_user = logq;
             f.ll_part = ll_part_; f.halted = halted;
             dense_final_kernel<<<n_ll_, 256, 0, s>>>(f);
             DTRY(hipGetLastError());
@@ -724,9 +792,9 @@ hipError_t DensePath::enqueue(const double* ewp, bool structural, double* out, d
         dense_scatter_kernel<<<1, 256, 0, s>>>(c);
         return hipGetLastError();
     }
-    const size_t step = R * np;
+    const size_t step = R * size_t(ldx_);
     GemmArgs g{};
-    g.R = R_; g.np = np_; g.nct = nct_;
+    g.R = R_; g.np = np_; g.nct = nct_; g.ldx = ldx_;
     g.et = et_; g.a0 = a0_; g.aend = aend_;
     g.p = p; g.logq = logq_;
     g.n_params = n_params_;
@@ -744,13 +812,13 @@ hipError_t DensePath::enqueue(const double* ewp, bool structural, double* out, d
         f.out = alpha_ + size_t(t + 1) * step;
         f.la_in = t < 0 ? la_ : la_ + size_t(t) * R;
         f.la_out = la_ + size_t(t + 1) * R;
-        dense_gemm_kernel<FWD><<<fb_blocks, kGemmThreads, 0, s>>>(f);
+        dense_gemm_kernel<FWD, kBkStep, kNwStep><<<fb_blocks, kNwStep * 64, 0, s>>>(f);
         DTRY(hipGetLastError());
     }
     {
         FinalArgs f{};
         f.alpha = alpha_; f.la = la_; f.aend = aend_; f.end_at = end_at_; f.p = p; f.ewp = w;
-        f.code_se = code_se_; f.n_strings = n_strings_; f.np = np_; f.logq = logq_; f.logq_user = logq;
+        f.code_se = code_se_; f.n_strings = n_strings_; f.np = np_; f.ldx = ldx_; f.logq = logq_; f.logq_user = logq;
         f.ll_part = ll_part_; f.halted = halted;
         dense_final_kernel<<<n_ll_, 256, 0, s>>>(f);
         DTRY(hipGetLastError());
@@ -760,7 +828,7 @@ hipError_t DensePath::enqueue(const double* ewp, bool structural, double* out, d
         GemmArgs b = g;
         b.no_mma = t == T_ - 1;
         b.x = y_ + size_t((t + 1) & 1) * step;
-        b.bm = amat_;
+        b.bm = amat_t_;
         b.meta = meta_ + size_t(t) * R;
         b.sid = sid_ + size_t(t) * R;
         b.part_in = part_ + size_t((t + 1) & 1) * nct_ * R;
@@ -773,7 +841,7 @@ hipError_t DensePath::enqueue(const double* ewp, bool structural, double* out, d
         b.alpha_t = alpha_ + size_t(t) * step;
         b.gam = gam_ + size_t(t) * step;
         b.z = z_ + size_t(t) * step;
-        dense_gemm_kernel<BWD><<<fb_blocks, kGemmThreads, 0, s>>>(b);
+        dense_gemm_kernel<BWD, kBkStep, kNwStep><<<fb_blocks, kNwStep * 64, 0, s>>>(b);
         DTRY(hipGetLastError());
     }
     if (T_ >= 2) {
@@ -785,7 +853,10 @@ hipError_t DensePath::enqueue(const double* ewp, bool structural, double* out, d
         q.code_a = code_a_;
         q.amat = amat_;
         q.grad = out + 1;
-        dense_gemm_kernel<GRAD><<<int((np / kT) * (np / kT)), kGemmThreads, 0, s>>>(q);
+        if (grad_cfg_ == 1)
+            dense_gemm_kernel<GRAD, kBkStep, kNwStep><<<int((np / kT) * (np / kT)), kNwStep * 64, 0, s>>>(q);
+        else
+            dense_gemm_kernel<GRAD, kBkGrad, kNwGrad><<<int((np / kT) * (np / kT)), kNwGrad * 64, 0, s>>>(q);
         DTRY(hipGetLastError());
     }
     {
@@ -793,7 +864,7 @@ hipError_t DensePath::enqueue(const double* ewp, bool structural, double* out, d
         r.gam = gam_; r.meta = meta_;
         r.rows = int64_t(T_) * int64_t(R);
         r.rows_per_chunk = (r.rows + reduce_chunks_ - 1) / reduce_chunks_;
-        r.np = np_; r.vocab = vocab_; r.red = red_; r.halted = halted;
+        r.np = np_; r.vocab = vocab_; r.ldx = ldx_; r.red = red_; r.halted = halted;
         dim3 grid(unsigned(np / kRedThreads), unsigned(reduce_chunks_));
         dense_reduce_kernel<<<grid, kRedThreads, 0, s>>>(r);
         DTRY(hipGetLastError());

@@ -59,7 +59,7 @@ std::string dense_model_build(const wfsa_model_desc& d, bool force, DenseModel& 
 
 class DensePath {
 public:
-    DensePath() = default;
+    explicit DensePath(int n_cu) : n_cu_(n_cu > 0 ? n_cu : 256) {}
     ~DensePath();
     DensePath(const DensePath&) = delete;
     DensePath& operator=(const DensePath&) = delete;
@@ -88,11 +88,14 @@ public:
     double issued_flops() const;
 
 private:
+    int n_cu_ = 256;
+    int grad_cfg_ = 1;   // WFSA_DENSE_GRAD_CFG=0: gradient GEMM with 4-wave blocks, K slices of 16
     int32_t n_params_ = 0, np_ = 0, vocab_ = 0, nct_ = 0;
     int32_t code_se_ = kCodeNone;
     int16_t sym_of_byte_[256] = {};
     int64_t n_strings_ = 0, total_sym_ = 0;
     int32_t R_ = 0, T_ = 0;
+    int32_t ldx_ = 0;                  // row pitch of alpha / gamma / z / Y
     double p0_sum_ = 0.0, n0_ = 0.0;   // sum of p / count of empty strings
     int32_t reduce_chunks_ = 0;
     // model tables
@@ -102,6 +105,7 @@ private:
     int32_t* code_em_ = nullptr;
     // per-iteration weights
     double* amat_ = nullptr;   // [np][np]
+    double* amat_t_ = nullptr; // [np][np] transposed
     double* et_ = nullptr;     // [vocab+1][np]
     double* a0_ = nullptr;     // [np]
     double* aend_ = nullptr;   // [np]

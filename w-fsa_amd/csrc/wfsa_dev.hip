@@ -1197,12 +1197,15 @@ int dense_load_corpus(wfsa_dev* ctx, const uint8_t* sym, const int64_t* off, con
                     hipGetErrorString(e));
     ctx->dense_struct = false;
     ctx->prep_level = 0;
+    ctx->stats.dense_rows = ctx->dense->rows();
+    ctx->stats.dense_steps = ctx->dense->steps();
+    ctx->stats.dense_np = ctx->dense->np();
     return WFSA_OK;
 }
 
 int load_dense_model(wfsa_dev* ctx, const wfsa::DenseModel& dm) {
     hipStream_t s = ctx->stream;
-    auto d = std::make_unique<wfsa::DensePath>();
+    auto d = std::make_unique<wfsa::DensePath>(ctx->n_cu);
     if (hipError_t e = d->load_model(dm, s); e != hipSuccess)
         return fail(WFSA_ERR_HIP, "dense path: model upload failed (%s)", hipGetErrorString(e));
     ctx->dense = std::move(d);
@@ -1314,6 +1317,8 @@ int wfsa_dev_load_model(wfsa_dev* ctx, const wfsa_model_desc* model) {
     drop_graph(ctx);
     ctx->dense.reset();
     ctx->dense_struct = false;
+    ctx->stats.dense = 0;
+    ctx->stats.dense_rows = ctx->stats.dense_steps = ctx->stats.dense_np = 0;
     if (ctx->dense_mode != 0) {
         wfsa::DenseModel dm;
         if (wfsa::dense_model_build(*model, ctx->dense_mode == 1, dm).empty()) return load_dense_model(ctx, dm);
