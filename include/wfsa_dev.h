@@ -101,7 +101,8 @@ typedef struct {
     double host_begin_ms, host_overlap_ms, host_wait_ms, host_post_ms;
     /* dense path (dense == 1): row slots R and trellis steps T of the packed
      * corpus; each evaluation runs 3 GEMMs of 2 np^2 R flops per step */
-    int32_t dense_rows, dense_steps, dense_np, dense_pad;
+    int32_t dense_rows, dense_steps, dense_np;
+    int32_t tier2_strings;     /* strings on the global-scratch traversal tier */
 } wfsa_dev_stats;
 
 /* context ---------------------------------------------------------------- */

@@ -495,6 +495,175 @@ __global__ __launch_bounds__(256) void trav_kernel(TravArgs a) {
     }
 }
 
+// block-wide reductions (every thread gets the result)
+__device__ __forceinline__ double block_sum(double v, double* red) {
+    v = wave_sum(v);
+    const int w = int(threadIdx.x) >> 6;
+    __syncthreads();
+    if ((threadIdx.x & 63) == 0) red[w] = v;
+    __syncthreads();
+    double s = 0.0;
+    for (int i = 0; i < int(blockDim.x) / kWave; ++i) s += red[i];
+    return s;
+}
+__device__ __forceinline__ double block_max(double v, double* red) {
+    v = wave_max(v);
+    const int w = int(threadIdx.x) >> 6;
+    __syncthreads();
+    if ((threadIdx.x & 63) == 0) red[w] = v;
+    __syncthreads();
+    double s = red[0];
+    for (int i = 1; i < int(blockDim.x) / kWave; ++i) s = fmax(s, red[i]);
+    return s;
+}
+
+// Tier 2 (fb_kernels.hpp WideArgs): one block per string, alpha per position
+// as a dense node vector in global scratch.  Position i+1 is nonzero only on
+// the destinations of byte c_i (the list D_c), so the forward writes exactly
+// D_c and the backward visits exactly those nodes; the rows are zeroed per
+// string because an in-edge gather reads arbitrary sources.
+template <bool COUNTING>
+__global__ __launch_bounds__(kWideBlock) void wide_kernel(WideArgs a) {
+    if (a.halted && *a.halted) return;
+    extern __shared__ __attribute__((aligned(16))) double gl[];   // [n_params] (weighted, grad_lds)
+    __shared__ double red[kWideBlock / kWave];
+    const int tid = int(threadIdx.x);
+    const ModelView& m = a.m;
+    const WideModel& W = a.w;
+    const int N = m.n_nodes;
+    double* A = a.scratch + int64_t(blockIdx.x) * a.scratch_stride;
+    double* B = A + (int64_t(a.max_len) + 1) * N;             // [2][N]
+    int* dsc = reinterpret_cast<int*>(B + 2 * int64_t(N));    // [max_len + 2]
+    const bool lgrad = !COUNTING && a.grad_lds;
+    if (lgrad)
+        for (int j = tid; j < m.n_params; j += kWideBlock) gl[j] = 0.0;
+    double ll = 0.0;
+    // parameters of edge g get -p xi (weighted) / are marked used (counting)
+    auto credit = [&](int g, double xi, double ps) {
+        for (int q = m.pptr[g]; q < m.pptr[g + 1]; ++q) {
+            if (COUNTING) { if (a.used) a.used[m.pidx[q]] = 1; }
+            else if (lgrad) block_add(&gl[m.pidx[q]], -ps * xi);
+            else global_add(&a.grad[m.pidx[q]], -ps * xi);
+        }
+    };
+    __syncthreads();
+    for (int li = int(blockIdx.x); li < a.n_list; li += int(gridDim.x)) {
+        const int sidx = a.list[li];
+        const int64_t o0 = a.off[sidx];
+        const int L = int(a.off[sidx + 1] - o0);
+        const uint8_t* str = a.sym + o0;
+        for (int64_t k = tid; k < (int64_t(L) + 1) * N; k += kWideBlock) A[k] = 0.0;
+        __syncthreads();
+        if (tid == 0) {
+            A[m.start] = 1.0;
+            dsc[0] = 0;
+        }
+        __syncthreads();
+        bool alive = true;
+        for (int i = 0; i < L; ++i) {
+            const int c = str[i];
+            const double* Ai = A + int64_t(i) * N;
+            double* An = A + int64_t(i + 1) * N;
+            const int cb = W.c_ptr[c], ce = W.c_ptr[c + 1];
+            double mx = 0.0;
+            for (int k = cb + tid; k < ce; k += kWideBlock) {
+                double v = 0.0;
+                for (int e = W.e_ptr[k]; e < W.e_ptr[k + 1]; ++e)
+                    v += COUNTING ? Ai[W.e_src[e]] : Ai[W.e_src[e]] * m.ew[W.e_g[e]];
+                An[W.dst[k]] = v;
+                mx = fmax(mx, v);
+            }
+            mx = block_max(mx, red);
+            if (!(mx > 0.0)) {
+                alive = false;
+                break;
+            }
+            const int ex = __builtin_amdgcn_frexp_exp(mx);
+            if (ex != 0)
+                for (int k = cb + tid; k < ce; k += kWideBlock) An[W.dst[k]] = ldexp(An[W.dst[k]], -ex);
+            if (tid == 0) dsc[i + 1] = ex;
+            __syncthreads();
+        }
+        // nodes live at position j: the destinations of byte c_{j-1}; at 0 the start
+        auto fr_begin = [&](int j) { return j == 0 ? 0 : W.c_ptr[str[j - 1]]; };
+        auto fr_end = [&](int j) { return j == 0 ? 1 : W.c_ptr[str[j - 1] + 1]; };
+        auto fr_node = [&](int j, int k) { return j == 0 ? m.start : W.dst[k]; };
+        double qh = 0.0;
+        int esum = 0;
+        if (alive) {
+            for (int k = fr_begin(L) + tid; k < fr_end(L); k += kWideBlock) {
+                const int S = fr_node(L, k);
+                qh += A[int64_t(L) * N + S] * (COUNTING ? m.node_end_count[S] : end_weight(m, S));
+            }
+            qh = block_sum(qh, red);
+            double es = 0.0;
+            for (int j = 1 + tid; j <= L; j += kWideBlock) es += double(dsc[j]);
+            esum = int(block_sum(es, red));
+        }
+        const double lq = qh > 0.0 ? log(qh) + kLn2 * double(esum) : -INFINITY;
+        const double ps = COUNTING ? 1.0 : a.p[sidx];
+        if (tid == 0) {
+            if (COUNTING) {
+                if (a.path_count) a.path_count[sidx] = qh > 0.0 ? ldexp(qh, esum) : 0.0;
+                if (a.recognized) a.recognized[sidx] = qh > 0.0 ? 1 : 0;
+            } else {
+                if (a.logq) a.logq[sidx] = lq;
+                ll += ps * lq;
+            }
+        }
+        if (!(qh > 0.0) || (COUNTING && !a.used)) {
+            __syncthreads();
+            continue;
+        }
+        // backward, scaled so that alpha_i beta_i is the posterior of the node
+        const double inv_q = 1.0 / qh;
+        {
+            double* BL = B + int64_t(L & 1) * N;
+            for (int k = fr_begin(L) + tid; k < fr_end(L); k += kWideBlock) {
+                const int S = fr_node(L, k);
+                const double af = A[int64_t(L) * N + S];
+                BL[S] = (COUNTING ? m.node_end_count[S] : end_weight(m, S)) * inv_q;
+                if (!(af > 0.0)) continue;
+                for (int x = m.x_ptr[S]; x < m.x_ptr[S + 1]; ++x) {
+                    const int gx = m.n_edges + x;
+                    const double xi = af * (COUNTING ? 1.0 : m.ew[gx]) * inv_q;
+                    if (xi > 0.0) credit(gx, xi, ps);
+                }
+            }
+        }
+        __syncthreads();
+        for (int i = L - 1; i >= 0; --i) {
+            const int c = str[i];
+            const double sc = ldexp(1.0, -dsc[i + 1]);
+            const double* Bn = B + int64_t((i + 1) & 1) * N;
+            double* Bi = B + int64_t(i & 1) * N;
+            for (int k = fr_begin(i) + tid; k < fr_end(i); k += kWideBlock) {
+                const int S = fr_node(i, k);
+                const double af = A[int64_t(i) * N + S];
+                double bs = 0.0;
+                if (af > 0.0) {
+                    int lo, cnt;
+                    edge_range(m, S, c, lo, cnt);
+                    for (int g = lo; g < lo + cnt; ++g) {
+                        const double b = (COUNTING ? 1.0 : m.ew[g]) * Bn[m.o_dst[g]] * sc;
+                        bs += b;
+                        const double xi = af * b;
+                        if (xi > 0.0) credit(g, xi, ps);
+                    }
+                }
+                Bi[S] = bs;
+            }
+            __syncthreads();
+        }
+    }
+    if (!COUNTING && tid == 0) a.ll_part[blockIdx.x] = ll;
+    if (lgrad) {
+        __syncthreads();
+        for (int j = tid; j < m.n_params; j += kWideBlock)
+            if (gl[j] != 0.0) global_add(&a.grad[j], gl[j]);
+    }
+}
+
 // Main streams: one lane per string, 64 strings of similar stream length per
 // wavefront.  Every word is an edge on all of the string's paths (posterior
 // 1): log q accumulates its log-weight and its parameters get -p_s.  A
@@ -1128,7 +1297,8 @@ hipError_t configure_kernels(int max_dynamic_lds) {
                          reinterpret_cast<const void*>(&fbs_kernel<false, true, false, 6>),
                          reinterpret_cast<const void*>(&fbs_kernel<false, true, false, 7>),
                          reinterpret_cast<const void*>(&fbs_kernel<false, true, false, 8>),
-                         reinterpret_cast<const void*>(&fbs_kernel<false, true, false, 9>)};
+                         reinterpret_cast<const void*>(&fbs_kernel<false, true, false, 9>),
+                         reinterpret_cast<const void*>(&wide_kernel<false>)};
     for (const void* f : fns) {   // (static LDS counts against the same 160 KiB)
         hipFuncAttributes attr{};
         hipError_t e = hipFuncGetAttributes(&attr, f);
@@ -1154,6 +1324,15 @@ hipError_t launch_trav(TravMode mode, const TravArgs& a, int grid, hipStream_t s
             hipLaunchKernelGGL(trav_kernel<MODE_EMIT>, dim3(unsigned(grid)), block, lds, stream, a);
             break;
     }
+    return hipGetLastError();
+}
+
+hipError_t launch_wide(bool counting, const WideArgs& a, int grid, hipStream_t stream) {
+    const size_t lds = (!counting && a.grad_lds) ? size_t(a.m.n_params) * sizeof(double) : 0;
+    if (counting)
+        hipLaunchKernelGGL(wide_kernel<true>, dim3(unsigned(grid)), dim3(kWideBlock), 0, stream, a);
+    else
+        hipLaunchKernelGGL(wide_kernel<false>, dim3(unsigned(grid)), dim3(kWideBlock), lds, stream, a);
     return hipGetLastError();
 }
 

@@ -143,6 +143,47 @@ struct TravArgs {
     const unsigned* halted;  // device-resident QN run: nonzero = skip (or null)
 };
 
+// Tier 2 of the traversal: strings whose trellis overflows every LDS slab
+// (ambiguous automata: hundreds of live nodes per position).  One block per
+// string; alpha of every position is a dense vector over the trellis nodes in
+// global scratch, built by gathering through the byte-indexed in-edge lists
+// (each destination node summed by one thread: no atomics); beta rolls over
+// two vectors, gathered through the out-edges; the gradient accumulates in
+// LDS when n_params fits (else global atomics).
+struct WideModel {
+    const int32_t* c_ptr;    // [257] destination entries of byte c: [c_ptr[c], c_ptr[c+1])
+    const int32_t* dst;      // [n_dst] the node (every destination of a byte-c edge, once)
+    const int32_t* e_ptr;    // [n_dst + 1] its in-edges with that byte
+    const int32_t* e_src;    // [E] source node
+    const int32_t* e_g;      // [E] edge id (ModelView numbering)
+};
+constexpr int kWideBlock = 256;
+struct WideArgs {
+    ModelView m;
+    WideModel w;
+    const uint8_t* sym;
+    const int64_t* off;
+    const double* p;
+    const int32_t* list;
+    int32_t n_list;
+    int32_t max_len;
+    double* scratch;         // per block: alpha [(max_len+1) n_nodes], beta [2 n_nodes], exponents
+    int64_t scratch_stride;  // doubles per block
+    int32_t grad_lds;        // weighted: the gradient accumulates in LDS (n_params doubles)
+    double* grad;            // [n_params]  -p_s E[count]
+    double* ll_part;         // [grid]
+    double* logq;            // [S] or null
+    double* path_count;      // counting: [S] or null
+    uint8_t* recognized;
+    uint8_t* used;
+    const unsigned* halted;
+};
+// doubles of scratch per block
+inline int64_t wide_scratch_stride(int32_t max_len, int32_t n_nodes) {
+    return (int64_t(max_len) + 3) * int64_t(n_nodes) + (int64_t(max_len) + 3) / 2 + 2;
+}
+hipError_t launch_wide(bool counting, const WideArgs& a, int grid, hipStream_t stream);
+
 // Device-resident QuasiNewton step (qn_kernel.hip): qn_update (wavefront per
 // constraint) updates x and lambda from out = [LL, grad_full] and writes the
 // next w_full; the finish (qn_finish_wave, qn_device.hpp) reduces the info

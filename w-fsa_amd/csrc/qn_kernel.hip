@@ -36,9 +36,10 @@ __device__ __forceinline__ void wave_sync() {
 // qn_update: one wavefront per constraint.  Every quantity of the update is
 // local to a constraint (its members are a contiguous, ascending range of
 // parameters), so waves are independent; each block writes its partial
-// (g_min, g_max, lambda_min, graderr) and qn_finish reduces them.  Lane m
-// owns member m (exp and the x update); g and the lambda_next numerator are
-// summed by lane 0 in member order, as the host does.
+// (g_min, g_max, lambda_min, graderr) and qn_finish reduces them.  Up to 64
+// members: lane m owns member m (exp and the x update); g and the
+// lambda_next numerator are summed by lane 0 in member order, as the host
+// does.  Larger groups stride their members over the lanes.
 __global__ __launch_bounds__(kQnUpdateBlock) void qn_update_kernel(QnArgs a) {
     if (*a.halted) return;
     constexpr int W = kQnUpdateBlock / 64;
@@ -84,31 +85,34 @@ __global__ __launch_bounds__(kQnUpdateBlock) void qn_update_kernel(QnArgs a) {
                 a.w_full[fo] = xn;   // GetWeight for the next step
                 a.ewp[fo] = exp(xn);
             }
-        } else {   // large groups (dense automata): lane 0 through memory
-            g = -1.0;
-            laux = 0.0;
-            if (lane == 0) {
-                for (int i = b; i < e; ++i) {
-                    const double ex = exp(a.x[i]);
-                    a.expx[i] = ex;
-                    a.grad[i] = a.out[1 + a.full_of[i]] + (a.fixed ? a.fixed[a.full_of[i]] : 0.0);
-                    g += ex;
-                }
-                double r = lam * g;
-                for (int i = b; i < e; ++i) r -= a.grad[i];
-                laux = r / (g + 1.0);
-                for (int i = b; i < e; ++i) {
-                    const double ex = a.expx[i], gi = a.grad[i];
-                    const double aux = ex * lam;
-                    gerr = fmax(gerr, fabs(gi + aux));
-                    const double xn = a.x[i] - a.eta * ((gi + ex * laux) / aux);
-                    a.x[i] = xn;
-                    a.w_full[a.full_of[i]] = xn;
-                    a.ewp[a.full_of[i]] = exp(xn);
-                }
+        } else {   // large groups (dense automata): members strided over the lanes,
+                   // lane sums combined by a fixed xor tree (deterministic; the
+                   // host's member-order sums differ from it by rounding only)
+            double gs = 0.0, gv = 0.0;
+            for (int i = b + lane; i < e; i += 64) {
+                const double ex = exp(a.x[i]);
+                const int fo = a.full_of[i];
+                const double gi = a.out[1 + fo] + (a.fixed ? a.fixed[fo] : 0.0);
+                a.expx[i] = ex;
+                a.grad[i] = gi;
+                gs += ex;
+                gv += gi;
             }
-            g = __shfl(g, 0, 64);
-            laux = __shfl(laux, 0, 64);
+            for (int o = 32; o > 0; o >>= 1) {
+                gs += __shfl_xor(gs, o, 64);
+                gv += __shfl_xor(gv, o, 64);
+            }
+            g = -1.0 + gs;
+            laux = (lam * g - gv) / (g + 1.0);
+            for (int i = b + lane; i < e; i += 64) {
+                const double ex = a.expx[i], gi = a.grad[i];
+                const double aux = ex * lam;
+                gerr = fmax(gerr, fabs(gi + aux));
+                const double xn = a.x[i] - a.eta * ((gi + ex * laux) / aux);
+                a.x[i] = xn;
+                a.w_full[a.full_of[i]] = xn;
+                a.ewp[a.full_of[i]] = exp(xn);
+            }
         }
         if (lane == 0) {   // LambdaUpdate (src/Learner.cpp:438-462)
             const double d = lam - laux;

@@ -174,10 +174,16 @@ struct wfsa_dev {
 
     size_t c_lds = 0;
 
-    // traversal fallback: per tier string lists
-    int32_t n_fall[2] = {0, 0};
-    int fall_grid[2] = {0, 0};
-    DevBuf<int32_t> fall[2];
+    // traversal fallback: per tier string lists (tier 2: wide_kernel)
+    int32_t n_fall[3] = {0, 0, 0};
+    int fall_grid[3] = {0, 0, 0};
+    DevBuf<int32_t> fall[3];
+    // tier 2: byte-indexed in-edge lists and per-block scratch
+    DevBuf<int32_t> w_cptr, w_dst, w_eptr, w_esrc, w_eg;
+    DevBuf<double> w_scratch;
+    int64_t w_stride = 0;
+    int32_t tier2_strings = 0;
+    bool force_tier2 = false;   // WFSA_TIER2=1: every string on tier 2 (tests)
 
     // work buffers
     DevBuf<double> w_full, ewp, out, ll_part, logq;
@@ -308,6 +314,32 @@ wfsa::TravArgs trav_args(wfsa_dev* ctx, int tier) {
     return a;
 }
 
+// tier 2: blocks in flight, bounded by a scratch budget of 4 GiB
+int wide_grid(wfsa_dev* ctx, int64_t n_list) {
+    ctx->w_stride = wfsa::wide_scratch_stride(ctx->max_len, ctx->n_nodes);
+    const int64_t budget = (int64_t(4) << 30) / 8;
+    int64_t g = std::max<int64_t>(1, std::min<int64_t>(4 * int64_t(ctx->n_cu), budget / std::max<int64_t>(ctx->w_stride, 1)));
+    return int(std::max<int64_t>(1, std::min<int64_t>(g, n_list)));
+}
+
+wfsa::WideArgs wide_args(wfsa_dev* ctx) {
+    wfsa::WideArgs a{};
+    a.m = model_view(ctx);
+    a.w.c_ptr = ctx->w_cptr.ptr;
+    a.w.dst = ctx->w_dst.ptr;
+    a.w.e_ptr = ctx->w_eptr.ptr;
+    a.w.e_src = ctx->w_esrc.ptr;
+    a.w.e_g = ctx->w_eg.ptr;
+    a.sym = ctx->sym.ptr;
+    a.off = ctx->off.ptr;
+    a.p = ctx->p.ptr;
+    a.max_len = ctx->max_len;
+    a.scratch = ctx->w_scratch.ptr;
+    a.scratch_stride = ctx->w_stride;
+    a.grad_lds = size_t(ctx->n_params) * sizeof(double) <= size_t(96 * 1024) ? 1 : 0;
+    return a;
+}
+
 int configure_tiers(wfsa_dev* ctx) {
     // tier 0: 4 waves per block, ~20 KB per wave (8 waves per CU), grown to
     // fit large automata; tier 1: one wave per block with the whole LDS.
@@ -322,13 +354,12 @@ int configure_tiers(wfsa_dev* ctx) {
     }
     const bool ok1 = make_slab(kLdsPerCu - 1024, ctx->max_len, ctx->n_nodes, 1, ctx->cfg[1], ctx->lay[1]);
     if (!ok1) ctx->cfg[1] = wfsa::SlabConfig{};
-    if (!ok0) {
-        if (!ok1)
-            return fail(WFSA_ERR_CAPACITY, "automaton too large for the LDS trellis slab (%d nodes, max length %d)",
-                        ctx->n_nodes, ctx->max_len);
+    if (!ok0 && ok1) {
         ctx->cfg[0] = ctx->cfg[1];
         ctx->lay[0] = ctx->lay[1];
     }
+    // neither fits (the node->slot map alone is too large): every string
+    // takes tier 2 (wide_kernel, global scratch)
     ctx->prep_level = 0;
     return WFSA_OK;
 }
@@ -482,34 +513,50 @@ int prepare(wfsa_dev* ctx, int level) {
         HIP_TRY(wfsa::launch_trav(wfsa::MODE_COUNT, a, trav_grid(ctx->cfg[t], ctx->n_cu, n), s));
         return WFSA_OK;
     };
-    if (S > 0) {
+    if (S > 0 && ctx->cfg[0].bytes > 0 && !ctx->force_tier2) {
         if (int rc = count_pass(0, ctx->list_all.ptr, S)) return rc;
         HIP_TRY(ctx->overflow.download(ovf.data(), size_t(S), s));
         HIP_TRY(hipStreamSynchronize(s));
+    } else {
+        std::fill(ovf.begin(), ovf.end(), uint8_t(S > 0 ? 1 : 0));
     }
-    std::vector<int32_t> l1;
+    std::vector<int32_t> l1, l2;
     for (int64_t i = 0; i < S; ++i)
         if (ovf[size_t(i)]) l1.push_back(int32_t(i));
-    DevBuf<int32_t> d_l1;
-    if (!l1.empty()) {
-        if (ctx->cfg[1].bytes == 0)
-            return fail(WFSA_ERR_CAPACITY, "%zu strings exceed the per-wave trellis slab and the automaton is too "
-                        "large for the single-wave tier", l1.size());
+    DevBuf<int32_t> d_l1, d_l2;
+    if (!l1.empty() && ctx->cfg[1].bytes > 0 && !ctx->force_tier2) {
         HIP_TRY(d_l1.upload(l1.data(), l1.size(), s));
         HIP_TRY(hipMemsetAsync(ctx->overflow.ptr, 0, SZ, s));
         if (int rc = count_pass(1, d_l1.ptr, int64_t(l1.size()))) return rc;
         HIP_TRY(ctx->overflow.download(ovf.data(), size_t(S), s));
         HIP_TRY(hipStreamSynchronize(s));
         for (int32_t i : l1) {
-            if (ovf[size_t(i)])
-                return fail(WFSA_ERR_CAPACITY, "string %d: trellis exceeds %d frontier nodes / %d live edges "
-                            "(single-wave LDS tier)", i, ctx->cfg[1].cap_f, ctx->cfg[1].cap_e);
-            tier[size_t(i)] = 1;
+            if (ovf[size_t(i)]) l2.push_back(i);
+            else tier[size_t(i)] = 1;
         }
+    } else {
+        l2 = l1;
     }
+    // tier 2: the strings no LDS slab holds
+    if (!l2.empty()) {
+        for (int32_t i : l2) tier[size_t(i)] = 2;
+        const int g2 = wide_grid(ctx, int64_t(l2.size()));
+        HIP_TRY(ctx->w_scratch.alloc(size_t(g2) * size_t(ctx->w_stride)));
+        HIP_TRY(d_l2.upload(l2.data(), l2.size(), s));
+        wfsa::WideArgs a = wide_args(ctx);
+        a.list = d_l2.ptr;
+        a.n_list = int32_t(l2.size());
+        a.path_count = ctx->pcount.ptr;
+        a.recognized = ctx->recog.ptr;
+        a.used = ctx->used.ptr;
+        HIP_TRY(wfsa::launch_wide(true, a, g2, s));
+        HIP_TRY(hipStreamSynchronize(s));
+    }
+    ctx->tier2_strings = int32_t(l2.size());
+    const int32_t n_tier1 = int32_t(l1.size() - l2.size());
 
     if (level < 2) {
-        ctx->stats.tier1_strings = int32_t(l1.size());
+        ctx->stats.tier1_strings = n_tier1;
         ctx->prep_level = 1;
         return WFSA_OK;
     }
@@ -522,7 +569,7 @@ int prepare(wfsa_dev* ctx, int level) {
         HIP_TRY(c_nbub.download(h_nb.data(), size_t(S), s));
         HIP_TRY(hipStreamSynchronize(s));
     }
-    std::vector<int32_t> comp, fb[2];
+    std::vector<int32_t> comp, fb[3];
     int32_t max_main = 0;
     for (int64_t i = 0; i < S; ++i) {
         if (h_bub[size_t(i)] >= 0) {
@@ -669,7 +716,7 @@ int prepare(wfsa_dev* ctx, int level) {
         HIP_TRY(d_bb.upload(b_base.data(), size_t(S), s));
         HIP_TRY(d_bf.upload(b_first.data(), size_t(S), s));
         std::vector<int32_t> el[2];
-        for (int32_t str : comp) el[tier[size_t(str)]].push_back(str);
+        for (int32_t str : comp) el[std::min<int>(tier[size_t(str)], 1)].push_back(str);
         DevBuf<int32_t> d_el[2];
         for (int t = 0; t < 2; ++t) {
             if (el[t].empty()) continue;
@@ -849,15 +896,17 @@ int prepare(wfsa_dev* ctx, int level) {
     HIP_TRY(ctx->fixed_grad.alloc(size_t(std::max(ctx->n_params, 1))));
 
     // traversal fallback lists
-    for (int t = 0; t < 2; ++t) {
+    for (int t = 0; t < 3; ++t) {
         ctx->n_fall[t] = int32_t(fb[t].size());
-        ctx->fall_grid[t] = fb[t].empty() ? 0 : trav_grid(ctx->cfg[t], ctx->n_cu, int64_t(fb[t].size()));
+        ctx->fall_grid[t] = fb[t].empty() ? 0
+                            : (t == 2 ? wide_grid(ctx, int64_t(fb[t].size()))
+                                      : trav_grid(ctx->cfg[t], ctx->n_cu, int64_t(fb[t].size())));
         if (!fb[t].empty()) HIP_TRY(ctx->fall[t].upload(fb[t].data(), fb[t].size(), s));
     }
     const size_t waves = std::max(size_t(ctx->c_grid) * waves_per_block, size_t(ctx->i_grid) * size_t(ctx->i_block / kWave)) +
                          size_t(ctx->b_waves) +
                          size_t(ctx->fall_grid[0]) * size_t(ctx->cfg[0].waves_per_block) +
-                         size_t(ctx->fall_grid[1]) * size_t(ctx->cfg[1].waves_per_block);
+                         size_t(ctx->fall_grid[1]) * size_t(ctx->cfg[1].waves_per_block) + size_t(ctx->fall_grid[2]);
     // two halves: a device-resident QN step's finish reads its partials
     // while the next step writes the other half
     HIP_TRY(ctx->ll_part.alloc(2 * waves));
@@ -876,12 +925,13 @@ int prepare(wfsa_dev* ctx, int level) {
     HIP_TRY(hipStreamSynchronize(s));
 
     ctx->stats.compiled_strings = nc;
-    ctx->stats.fallback_strings = int64_t(fb[0].size() + fb[1].size());
+    ctx->stats.fallback_strings = int64_t(fb[0].size() + fb[1].size() + fb[2].size());
+    ctx->stats.tier2_strings = ctx->tier2_strings;
     ctx->stats.stream_words = words;
     ctx->stats.stream_bytes = chunks * 16;
     ctx->stats.n_bubbles = nbub;
     ctx->stats.bubble_words = bwords;
-    ctx->stats.tier1_strings = int32_t(l1.size());
+    ctx->stats.tier1_strings = n_tier1;
     ctx->stats.waves_per_block = ctx->cfg[0].waves_per_block;
     ctx->stats.prepare_ms =
         std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_start).count();
@@ -1065,6 +1115,17 @@ int enqueue_evaluation(wfsa_dev* ctx, bool want_logq, const unsigned* halted, in
         HIP_TRY(wfsa::launch_trav(wfsa::MODE_WEIGHTED, a, ctx->fall_grid[t], s));
         wave_off += ctx->fall_grid[t] * ctx->cfg[t].waves_per_block;
     }
+    if (ctx->n_fall[2]) {
+        wfsa::WideArgs a = wide_args(ctx);
+        a.list = ctx->fall[2].ptr;
+        a.n_list = ctx->n_fall[2];
+        a.grad = ctx->out.ptr + 1;
+        a.ll_part = ctx->ll_cur + wave_off;
+        a.logq = want_logq ? ctx->logq.ptr : nullptr;
+        a.halted = halted;
+        HIP_TRY(wfsa::launch_wide(false, a, ctx->fall_grid[2], s));
+        wave_off += ctx->fall_grid[2];
+    }
     if (n_ll) *n_ll = wave_off;
     if (!with_tail) {
         HIP_TRY(record(ctx, ctx->k2, slot, s));
@@ -1216,7 +1277,7 @@ int load_dense_model(wfsa_dev* ctx, const wfsa::DenseModel& dm) {
     ctx->start = 0;
     ctx->n_groups = 0;
     ctx->n_bubbles = 0;
-    ctx->n_fall[0] = ctx->n_fall[1] = 0;
+    ctx->n_fall[0] = ctx->n_fall[1] = ctx->n_fall[2] = 0;
     if (int rc = alloc_param_buffers(ctx)) return rc;
     HIP_TRY(hipStreamSynchronize(s));
     ctx->has_model = true;
@@ -1265,6 +1326,7 @@ int wfsa_dev_create(int device, wfsa_dev** out) {
     if (const char* e = std::getenv("WFSA_TIMING")) ctx->kernel_timing = e[0] != '0';
     if (const char* e = std::getenv("WFSA_FUSE_BUBBLES")) ctx->fuse_bubbles = e[0] != '0';
     if (const char* e = std::getenv("WFSA_DENSE"); e && e[0]) ctx->dense_mode = e[0] == '0' ? 0 : 1;
+    if (const char* e = std::getenv("WFSA_TIER2")) ctx->force_tier2 = e[0] == '1';
 
     HIP_TRY(hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking));
     // measured: the cross-stream fork/join costs more idle time (5-20 us)
@@ -1356,6 +1418,40 @@ int wfsa_dev_load_model(wfsa_dev* ctx, const wfsa_model_desc* model) {
     // narrow (16-bit) stream words unless parameters or multi edges overflow them
     ctx->wide = (tm.n_params >= 0x8000 || ctx->n_multi >= 0x7fff) ? 1 : 0;
     HIP_TRY(ctx->node_end_count.upload(tm.node_end_count.data(), tm.node_end_count.size(), s));
+    {   // tier 2: for each byte c, every destination of a byte-c edge once, with its in-edges
+        std::vector<std::vector<std::pair<int32_t, int32_t>>> by(256);   // (dst, edge)
+        for (int32_t u = 0; u < tm.n_nodes; ++u)
+            for (int32_t g = tm.o_ptr[size_t(u)]; g < tm.o_ptr[size_t(u) + 1]; ++g)
+                by[tm.o_byte[size_t(g)]].push_back({tm.o_dst[size_t(g)], g});
+        std::vector<int32_t> edge_src(static_cast<size_t>(E));
+        for (int32_t u = 0; u < tm.n_nodes; ++u)
+            for (int32_t g = tm.o_ptr[size_t(u)]; g < tm.o_ptr[size_t(u) + 1]; ++g) edge_src[size_t(g)] = u;
+        std::vector<int32_t> cptr(257, 0), dst, eptr, esrc, eg;
+        for (int c = 0; c < 256; ++c) {
+            auto& v = by[size_t(c)];
+            std::stable_sort(v.begin(), v.end(), [](const auto& x, const auto& y) { return x.first < y.first; });
+            for (size_t i = 0; i < v.size(); ++i) {
+                if (i == 0 || v[i].first != v[i - 1].first) {
+                    dst.push_back(v[i].first);
+                    eptr.push_back(int32_t(esrc.size()));
+                }
+                esrc.push_back(edge_src[size_t(v[i].second)]);
+                eg.push_back(v[i].second);
+            }
+            cptr[size_t(c) + 1] = int32_t(dst.size());
+            v.clear();
+            v.shrink_to_fit();
+        }
+        eptr.push_back(int32_t(esrc.size()));
+        if (dst.empty()) dst.push_back(0);
+        if (esrc.empty()) { esrc.push_back(0); eg.push_back(0); }
+        HIP_TRY(ctx->w_cptr.upload(cptr.data(), cptr.size(), s));
+        HIP_TRY(ctx->w_dst.upload(dst.data(), std::max<size_t>(dst.size(), 1), s));
+        HIP_TRY(ctx->w_eptr.upload(eptr.data(), eptr.size(), s));
+        HIP_TRY(ctx->w_esrc.upload(esrc.data(), std::max<size_t>(esrc.size(), 1), s));
+        HIP_TRY(ctx->w_eg.upload(eg.data(), std::max<size_t>(eg.size(), 1), s));
+        HIP_TRY(hipStreamSynchronize(s));
+    }
     HIP_TRY(ctx->lw.alloc(size_t(E + X)));
     HIP_TRY(ctx->ew.alloc(size_t(E + X)));
     HIP_TRY(ctx->erec.alloc(size_t(E + X)));

@@ -42,7 +42,7 @@ class DevStats(C.Structure):
         ("compiled_kernel_ms", dbl), ("graph", i32), ("dense", i32),
         ("host_steps", i64), ("host_begin_ms", dbl), ("host_overlap_ms", dbl), ("host_wait_ms", dbl),
         ("host_post_ms", dbl),
-        ("dense_rows", i32), ("dense_steps", i32), ("dense_np", i32), ("dense_pad", i32),
+        ("dense_rows", i32), ("dense_steps", i32), ("dense_np", i32), ("tier2_strings", i32),
     ]
 
 
