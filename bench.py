@@ -61,6 +61,28 @@ def parse():
     return a
 
 
+def host_cpu():
+    """CPU model, logical CPUs of the machine, CPUs this process may use, and
+    the OpenMP threads the multi-core baselines use (OMP_NUM_THREADS, capped
+    by the CPUs available; the GPU box grants 16 per GPU)"""
+    model = "unknown"
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    try:
+        avail = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        avail = os.cpu_count() or 1
+    want = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or avail
+    return {"cpu_model": model, "nproc": os.cpu_count(), "cpus_available": avail,
+            "omp_threads": max(1, min(want, avail, 16))}
+
+
 def cpu_baseline(syn_text, sym, off, wt, n_sample):
     """Reference algorithm restated in C (oracle/): BFS path enumeration once,
     then the SpMV chain per iteration, one core.  Also the log-likelihood of
@@ -81,6 +103,29 @@ def cpu_baseline(syn_text, sym, off, wt, n_sample):
         kl_ref, ll_ref = o.objective_grad()
     t_iter = (time.perf_counter() - t0) / iters
     S = o.info["n_strings"]
+    host = host_cpu()
+    nt = host["omp_threads"]
+    # the same SpMV chain on every granted core (OpenMP over paths / strings)
+    o.set_threads(nt)
+    o.objective_grad()
+    t0 = time.perf_counter()
+    for _ in range(iters):
+        o.objective_grad()
+    t_iter_mt = (time.perf_counter() - t0) / iters
+    o.set_threads(1)
+    # the trellis restatement (oracle TRELLIS: forward-backward per string,
+    # OpenMP over strings) on a hundredth of the sample (it visits every state
+    # at every position: ~1 ms per family-A string on one core)
+    from oracle import TRELLIS
+    nt_s = max(1, n // 100)
+    t_off = off[: nt_s + 1].copy()
+    ot = Oracle.from_arrays(syn_text, sym[: t_off[-1]].copy(), t_off, wt[:nt_s].copy(), mode=TRELLIS)
+    ot.set_threads(nt)
+    wt_full = np.array(ot.w_full())
+    ot.trellis_eval(wt_full)
+    t0 = time.perf_counter()
+    ot.trellis_eval(wt_full)
+    t_trel = time.perf_counter() - t0
     # the same sample through the device
     fsa = W.Fsa.read_text(syn_text)
     lrn = W.QuasiNewtonLearner(0)
@@ -96,6 +141,13 @@ def cpu_baseline(syn_text, sym, off, wt, n_sample):
                    f"algorithm (BFS path enumeration {t_build:.2f} s once = {S / t_build:.0f} strings/s, "
                    f"then the P/M SpMV chain: {t_iter * 1e3:.1f} ms per objective+gradient)"),
         "enumeration_s": t_build, "iteration_s": t_iter, "paths": o.info["n_paths"],
+        "multi_core": {"value": S / t_iter_mt, "unit": "strings/s", "cores": nt, "kind": "port",
+                       "iteration_s": t_iter_mt,
+                       "sample": f"the same {n} strings, ENUM SpMV chain with {nt} OpenMP threads"},
+        "trellis_omp": {"value": nt_s / t_trel, "unit": "strings/s", "cores": nt, "kind": "port",
+                        "iteration_s": t_trel,
+                        "sample": f"first {nt_s} strings, oracle TRELLIS forward-backward, {nt} OpenMP threads"},
+        "host": host,
     }, rel, ll_ref, ll_dev
 
 
@@ -115,6 +167,7 @@ def cpu_baseline_dense(syn_text, sym, off, wt, n_sample):
     t0 = time.perf_counter()
     o.trellis_eval(w)
     t_eval = time.perf_counter() - t0
+    host = host_cpu()
     return {
         "value": n / t_eval, "unit": "strings/s", "cores": 1, "kind": "port",
         "sample": (f"first {n} string(s) ({int(s_off[-1])} symbols) of the same corpus through oracle/wfsa_oracle.c "
@@ -122,6 +175,7 @@ def cpu_baseline_dense(syn_text, sym, off, wt, n_sample):
                    f"build incl. its structural pass {t_build:.1f} s; path enumeration (the reference "
                    f"algorithm) is infeasible here"),
         "iteration_s": t_eval,
+        "host": host,
     }
 
 

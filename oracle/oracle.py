@@ -64,6 +64,7 @@ def lib():
         L.oracle_qn_halt.argtypes = [vp, dbl]
         L.oracle_qn_halt.restype = C.c_int
         L.oracle_trellis_eval.argtypes = [vp, vp, vp, vp, pd, C.c_char_p, C.c_int]
+        L.oracle_set_threads.argtypes = [vp, C.c_int]
         _lib = L
     return _lib
 
@@ -186,6 +187,10 @@ class Oracle:
         kl, ll = C.c_double(), C.c_double()
         lib().oracle_objective_grad(self._h, C.byref(kl), C.byref(ll))
         return kl.value, ll.value
+
+    def set_threads(self, n):
+        """OpenMP threads of objective_grad / trellis_eval (1 = serial, the default)"""
+        lib().oracle_set_threads(self._h, int(n))
 
     def renormalize(self):
         lib().oracle_renormalize(self._h)

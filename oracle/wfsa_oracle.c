@@ -30,6 +30,9 @@
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#ifdef _OPENMP
+#include <omp.h>
+#endif
 
 #define OR_OK 0
 #define OR_ERR -1
@@ -364,6 +367,7 @@ typedef struct {
     double grad_error, lambda_min, g_min, g_max;
     int exp_lambda;
     int64_t max_paths;
+    int threads;              /* OpenMP threads of the per-iteration passes (cpu_baseline); 1 = serial */
 } learner_t;
 
 static double get_weight(const learner_t* L, int j) {             /* src/Learner.cpp:427-436 */
@@ -875,18 +879,23 @@ double oracle_kl(const learner_t* L) { return L->kl; }
 static void modeled_probs(learner_t* L) {
     int64_t S = L->S;
     if (L->mode == 0) {
+        const int nt = L->threads > 1 ? L->threads : 1;
+        (void)nt;
         if (L->unique) {
+#pragma omp parallel for num_threads(nt) if (nt > 1) schedule(static)
             for (int64_t s = 0; s < S; ++s) {          /* logq = P.x (row s = path s) */
                 double a = 0;
                 for (int64_t k = L->Prow[s]; k < L->Prow[s + 1]; ++k) a += L->Pdata[k] * L->x[L->Pcol[k]];
                 L->logq[s] = a;
             }
         } else {
+#pragma omp parallel for num_threads(nt) if (nt > 1) schedule(static)
             for (int64_t r = 0; r < L->n_paths; ++r) {
                 double a = 0;
                 for (int64_t k = L->Prow[r]; k < L->Prow[r + 1]; ++k) a += L->Pdata[k] * L->x[L->Pcol[k]];
                 L->rpp[r] = exp(a);
             }
+#pragma omp parallel for num_threads(nt) if (nt > 1) schedule(static)
             for (int64_t s = 0; s < S; ++s) {
                 double q = 0;
                 for (int64_t r = L->Mrow[s]; r < L->Mrow[s + 1]; ++r) q += L->rpp[r];
@@ -938,12 +947,35 @@ static void compute_grad(learner_t* L) {
     modeled_probs(L);
     if (L->unique) {
         memcpy(L->grad, L->grad_aux, sizeof(double) * (size_t)n);
-    } else {
+    } else if (L->threads <= 1) {
         for (int j = 0; j < n; ++j) L->grad[j] = 0;
         for (int64_t r = 0; r < L->n_paths; ++r) {
             double a = L->rpp[r] * L->grad_aux[r];
             for (int64_t k = L->Prow[r]; k < L->Prow[r + 1]; ++k) L->grad[L->Pcol[k]] += L->Pdata[k] * a;
         }
+    } else {   /* P^T. with per-thread partial vectors, summed in thread order */
+        const int nt = L->threads;
+        double* part = calloc((size_t)nt * (size_t)(n + 1), sizeof(double));
+#pragma omp parallel num_threads(nt)
+        {
+#ifdef _OPENMP
+            const int t = omp_get_thread_num();
+#else
+            const int t = 0;
+#endif
+            double* g = part + (size_t)t * (size_t)(n + 1);
+#pragma omp for schedule(static)
+            for (int64_t r = 0; r < L->n_paths; ++r) {
+                double a = L->rpp[r] * L->grad_aux[r];
+                for (int64_t k = L->Prow[r]; k < L->Prow[r + 1]; ++k) g[L->Pcol[k]] += L->Pdata[k] * a;
+            }
+        }
+        for (int j = 0; j < n; ++j) {
+            double a = 0;
+            for (int t = 0; t < nt; ++t) a += part[(size_t)t * (size_t)(n + 1) + (size_t)j];
+            L->grad[j] = a;
+        }
+        free(part);
     }
 }
 
@@ -1038,22 +1070,45 @@ int oracle_qn_halt(const learner_t* L, double tol) {            /* :88-91 */
  * check the device path directly at arbitrary weights. */
 int oracle_trellis_eval(learner_t* L, const double* w_full, double* logq_corpus, double* grad_full,
                         double* loglik, char* err, int errlen) {
-    trellis_ws_t ws = {0};
-    ws.N = (int)L->fsa.st.n;
-    ws.topo = xrealloc(NULL, sizeof(int) * (size_t)(ws.N + 1));
-    if (eps_topo(&L->fsa, ws.topo, err, errlen) != OR_OK) { free(ws.topo); return OR_ERR; }
+    int* topo = xrealloc(NULL, sizeof(int) * (size_t)(L->fsa.st.n + 1));
+    if (eps_topo(&L->fsa, topo, err, errlen) != OR_OK) { free(topo); return OR_ERR; }
     double* ew = exp_weights(L, w_full);
-    double ll = 0;
-    for (int j = 0; j < L->n_full; ++j) grad_full[j] = 0;
-    for (int64_t i = 0; i < L->corpus.words.n; ++i) {
-        double pw = L->corpus.w.a[i];
-        double q = trellis_string(&L->fsa, &ws, L->corpus.words.a[i], L->corpus.lens.a[i],
-                                  ew, grad_full, -pw, NULL);
-        logq_corpus[i] = q > 0 ? log(q) : -INFINITY;
-        if (q > 0) ll += pw * log(q);
+    const int nt = L->threads > 1 ? L->threads : 1;
+    const int64_t NC = L->corpus.words.n;
+    const size_t nf = (size_t)L->n_full + 1;
+    /* per-thread workspaces and gradient partials, summed in thread order
+     * (one thread: the serial sum) */
+    double* part = calloc((size_t)nt * nf, sizeof(double));
+#pragma omp parallel num_threads(nt) if (nt > 1)
+    {
+#ifdef _OPENMP
+        const int t = omp_get_thread_num();
+#else
+        const int t = 0;
+#endif
+        trellis_ws_t ws = {0};
+        ws.N = (int)L->fsa.st.n;
+        ws.topo = xrealloc(NULL, sizeof(int) * (size_t)(ws.N + 1));
+        memcpy(ws.topo, topo, sizeof(int) * (size_t)ws.N);
+        double* g = part + (size_t)t * nf;
+#pragma omp for schedule(dynamic, 64)
+        for (int64_t i = 0; i < NC; ++i) {
+            double q = trellis_string(&L->fsa, &ws, L->corpus.words.a[i], L->corpus.lens.a[i],
+                                      ew, g, -L->corpus.w.a[i], NULL);
+            logq_corpus[i] = q > 0 ? log(q) : -INFINITY;
+        }
+        trellis_free(&ws);
     }
+    for (int j = 0; j < L->n_full; ++j) {
+        double a = 0;
+        for (int t = 0; t < nt; ++t) a += part[(size_t)t * nf + (size_t)j];
+        grad_full[j] = a;
+    }
+    double ll = 0;
+    for (int64_t i = 0; i < NC; ++i)
+        if (logq_corpus[i] > -INFINITY) ll += L->corpus.w.a[i] * logq_corpus[i];
     *loglik = ll;
-    free(ew); trellis_free(&ws);
+    free(part); free(ew); free(topo);
     return OR_OK;
 }
 
@@ -1069,3 +1124,7 @@ int oracle_full_param_name(const learner_t* L, int j, const char** state, int* k
     return OR_OK;
 }
 int oracle_trimmed_index(const learner_t* L, int j) { return L->trimmed[j]; }
+
+/* OpenMP threads of the per-iteration passes (ENUM SpMV chain, trellis
+ * evaluation); 1 (the default) = serial, like the reference (mkl_sequential) */
+void oracle_set_threads(learner_t* L, int threads) { L->threads = threads > 1 ? threads : 1; }
