@@ -125,6 +125,11 @@ int wfsa_dev_load_corpus(wfsa_dev* ctx, const uint8_t* sym, const int64_t* off,
 int wfsa_dev_recognize(wfsa_dev* ctx, uint8_t* recognized, double* path_count,
                        uint8_t* used_param);
 
+/* Where each loaded string runs (after compilation): tier[s] = -1 compiled
+ * stream (trivial words + bubbles), 0 / 1 LDS-slab traversal, 2 wide
+ * traversal (global scratch), 3 dense MFMA path. */
+int wfsa_dev_string_tiers(wfsa_dev* ctx, int8_t* tier);
+
 /* Per-iteration hot path.  w_full[n_params] = Learner::GetWeight(j)
  * (src/Learner.cpp:427-436): x[trim[j]], 0 or -inf.  Outputs:
  *   *loglik        = sum_s p_s log q_s
@@ -168,6 +173,19 @@ int wfsa_dev_qn_set_state(wfsa_dev* ctx, const double* x, const double* lambda);
 int wfsa_dev_qn_get_state(wfsa_dev* ctx, double* x, double* lambda, double* grad);
 int wfsa_dev_qn_run(wfsa_dev* ctx, double eta, double tol, int32_t max_steps, double* info_rows,
                     int32_t* steps_done, int32_t* status);
+
+/* Second-order term of the objective's Hessian for HessianLearner
+ * (ComputeHf, src/HessianLearner.cpp:498-547; pattern as AssembleH :381-446):
+ *   hf_setup: builds the pattern -- the pairs (j, k), j <= k, of Fsa
+ *             parameters whose counts vary together on some string -- after the
+ *             corpus is compiled; fails (WFSA_ERR_CAPACITY) when a string is
+ *             not compiled into bubbles, on the dense path, with a communicator.
+ *   hf_pairs: the pattern, pairs[2 t], pairs[2 t + 1] (ascending).
+ *   hf_eval:  values[t] = sum_s p_s Cov_s(count_j, count_k) at w_full
+ *             (HessianLearner adds -values to H). */
+int wfsa_dev_hf_setup(wfsa_dev* ctx, int64_t* n_pairs);
+int wfsa_dev_hf_pairs(wfsa_dev* ctx, int32_t* pairs);
+int wfsa_dev_hf_eval(wfsa_dev* ctx, const double* w_full, double* values);
 
 /* Multi-GPU: one process per GPU.  Rank 0 creates the id, the launcher
  * broadcasts the 128 bytes, every rank attaches.  wfsa_dev_allreduce sums

@@ -55,9 +55,11 @@ typedef struct {
     int64_t shard_begin, shard_end;
 } wfsa_learner_info;
 
-/* optimizer: "QuasiNewton" (the reference's "Hessian" optimizer is not part
- * of this build: SURVEY.md 8f item 1) */
+/* optimizer: "Hessian" (inc/HessianLearner.h, the reference's default) or
+ * "QuasiNewton" (inc/QuasiNewtonLearner.h) */
 int wfsa_learner_create(const char* optimizer, int device, wfsa_learner** out);
+/* values per GetOptimizationInfo row: 9 (Hessian), 7 (QuasiNewton) */
+int wfsa_learner_info_width(wfsa_learner* l);
 void wfsa_learner_destroy(wfsa_learner* l);
 int wfsa_learner_set_comm(wfsa_learner* l, int nranks, int rank, const uint8_t id[WFSA_COMM_ID_BYTES]);
 /* Learner::BuildFrom on (Fsa, Corpus); the corpus is renormalized first as
@@ -69,10 +71,11 @@ int wfsa_learner_build_packed(wfsa_learner* l, wfsa_fsa* fsa, const uint8_t* sym
 int wfsa_learner_finalize(wfsa_learner* l);                                 /* Learner::Finalize */
 int wfsa_learner_info_get(wfsa_learner* l, wfsa_learner_info* out);
 int wfsa_learner_init(wfsa_learner* l, int flags, const double* x0);       /* Learner::Init */
-/* OptimizationStep + GetOptimizationInfo (7 values) + HaltCondition(tol) */
-int wfsa_learner_step(wfsa_learner* l, double eta, double tol, double info[7], int32_t* halt);
+/* OptimizationStep + GetOptimizationInfo (info_width values) + HaltCondition(tol) */
+int wfsa_learner_step(wfsa_learner* l, double eta, double tol, double* info, int32_t* halt);
 /* main.cpp's epoch loop (src/main.cpp:276-303) without the per-epoch FFI
- * round trip: up to max_epochs steps, info_rows[7*e..] (nullable) gets each
+ * round trip (QuasiNewton: device-resident): up to max_epochs steps,
+ * info_rows[info_width*e..] (nullable) gets each
  * epoch's info, stops after the epoch whose HaltCondition(tol) holds; a
  * non-finite info value fails with "<x> detected at epoch <e>" (the
  * reference's LearnerError) after recording that row. */
@@ -90,6 +93,10 @@ int wfsa_learner_renormalize(wfsa_learner* l);                      /* Learner::
 /* RewriteWeights into the fsa, then Fsa::Dump to path */
 int wfsa_learner_dump(wfsa_learner* l, wfsa_fsa* fsa, const char* path);
 int wfsa_learner_stats(wfsa_learner* l, wfsa_dev_stats* out);
+/* GetOptimizationResult (src/HessianLearner.cpp:349-372; the -eval output):
+ * KL, mxlogx(support), LogModelVolume, LogAuxVolume, logdetHessian,
+ * LogDetAuxHessian, n - k, aux - 1 (Hessian only) */
+int wfsa_learner_result(wfsa_learner* l, double out[8]);
 
 /* ---- host-only helpers (no device needed) -------------------------------- */
 /* Contiguous shard [begin, end) of rank `rank` out of `nranks` over strings

@@ -65,6 +65,11 @@ def lib():
         L.oracle_qn_halt.restype = C.c_int
         L.oracle_trellis_eval.argtypes = [vp, vp, vp, vp, pd, C.c_char_p, C.c_int]
         L.oracle_set_threads.argtypes = [vp, C.c_int]
+        L.oracle_path_nnz.argtypes = [vp]
+        L.oracle_path_nnz.restype = i64
+        L.oracle_get_paths.argtypes = [vp, vp, vp, vp, vp]
+        L.oracle_get_paths.restype = C.c_int
+        L.oracle_get_ccol.argtypes = [vp, vp]
         _lib = L
     return _lib
 
@@ -150,6 +155,25 @@ class Oracle:
         a = np.zeros(self.info["n_corpus"], dtype=np.int64)
         lib().oracle_path_counts(self._h, _ptr(a))
         return a
+
+    def paths(self):
+        """ENUM path matrices: (Prow, Pcol, Pdata, Mrow) -- path l's parameter
+        counts are Pcol/Pdata[Prow[l]:Prow[l+1]], string s's paths Mrow[s]:Mrow[s+1]"""
+        nnz = lib().oracle_path_nnz(self._h)
+        if nnz < 0:
+            raise OracleError("path matrices exist in ENUM mode only")
+        prow = np.zeros(self.info["n_paths"] + 1, dtype=np.int64)
+        pcol = np.zeros(max(nnz, 1), dtype=np.int32)
+        pdata = np.zeros(max(nnz, 1), dtype=np.float64)
+        mrow = np.zeros(self.info["n_strings"] + 1, dtype=np.int64)
+        lib().oracle_get_paths(self._h, _ptr(prow), _ptr(pcol), _ptr(pdata), _ptr(mrow))
+        return prow, pcol[:nnz], pdata[:nnz], mrow
+
+    def ccol(self):
+        """constraint (normalisation group) of each trimmed parameter"""
+        a = np.zeros(max(self.n, 1), dtype=np.int32)
+        lib().oracle_get_ccol(self._h, _ptr(a))
+        return a[:self.n].astype(np.int64)
 
     def x(self):
         a = np.zeros(self.n, dtype=np.float64)

@@ -1128,3 +1128,18 @@ int oracle_trimmed_index(const learner_t* L, int j) { return L->trimmed[j]; }
 /* OpenMP threads of the per-iteration passes (ENUM SpMV chain, trellis
  * evaluation); 1 (the default) = serial, like the reference (mkl_sequential) */
 void oracle_set_threads(learner_t* L, int threads) { L->threads = threads > 1 ? threads : 1; }
+
+/* ENUM path matrices (src/Learner.cpp BuildFrom: P rows = paths, M rows =
+ * strings) and the trimmed constraint of each parameter (Ccol), for the
+ * second-order restatement in oracle/hessian.py.  nnz = Prow[n_paths]. */
+int64_t oracle_path_nnz(const learner_t* L) { return L->mode == 0 && L->Prow ? L->Prow[L->n_paths] : -1; }
+int oracle_get_paths(const learner_t* L, int64_t* prow, int* pcol, double* pdata, int64_t* mrow) {
+    if (L->mode != 0 || !L->Prow) return OR_ERR;
+    int64_t nnz = L->Prow[L->n_paths];
+    memcpy(prow, L->Prow, sizeof(int64_t) * (size_t)(L->n_paths + 1));
+    memcpy(pcol, L->Pcol, sizeof(int) * (size_t)nnz);
+    memcpy(pdata, L->Pdata, sizeof(double) * (size_t)nnz);
+    memcpy(mrow, L->Mrow, sizeof(int64_t) * (size_t)(L->S + 1));
+    return OR_OK;
+}
+void oracle_get_ccol(const learner_t* L, int* out) { memcpy(out, L->Ccol, sizeof(int) * (size_t)L->n); }

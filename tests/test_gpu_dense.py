@@ -163,3 +163,25 @@ def test_dense_1024_properties(monkeypatch):
     sub_sym = np.concatenate([sym[off[i]:off[i + 1]] for i in idx])
     _, ologq, _ = _oracle(syn.wfsa_text, sub_sym, sub_off, wt[idx], dict(zip(names, w)))
     np.testing.assert_allclose(logq[idx], ologq, rtol=1e-12)
+
+
+def test_dense_device_qn_large_groups_equals_host_update(monkeypatch):
+    """device-resident QN (constraint groups of 101 members: the strided
+    qn_update path) == the host QN update (QuasiNewtonLearner.cpp) step by step"""
+    import wfsa_amd as W
+    monkeypatch.setenv("WFSA_DENSE", "1")
+    syn = W.Synthetic(n_states=100, degree=1, vocab=4, emissions=2, dense=True, n_strings=200, max_len=12, seed=8)
+    sym, off, wt = syn.corpus()
+    fsa = W.Fsa.read_text(syn.wfsa_text)
+    a, b = W.QuasiNewtonLearner(0), W.QuasiNewtonLearner(0)
+    for lrn in (a, b):
+        lrn.BuildFromPacked(fsa, sym, off, wt)
+        lrn.Finalize()
+        lrn.Init(7)
+        assert lrn.stats()["dense"] == 1
+    rows_a = a.Run(5, 1.0, -1.0)
+    rows_b = [b.OptimizationStep(1.0, -1.0)[0] for _ in range(5)]
+    for r, q in zip(rows_a, rows_b):
+        for u, v in zip(r[:5], q[:5]):
+            assert _close(u, v, rel=1e-10, atol=1e-13)
+    np.testing.assert_allclose(a.x(), b.x(), rtol=1e-10, atol=1e-12)

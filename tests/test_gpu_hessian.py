@@ -1,0 +1,187 @@
+"""GPU tests of the HessianLearner path (the reference's default optimizer):
+the count-covariance kernel against finite differences of the device
+gradient, the CLI on every CTest case (CMakeLists.txt:34-57: default Hessian
+optimizer, -n -eval -e 20 -i 31) with the reference's exit codes, and the
+talk -eval Result vector of SURVEY.md Appendix A.  Needs a gfx950 device."""
+import json
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+from conftest import DATA, ROOT
+
+pytestmark = pytest.mark.gpu
+
+GOLD = json.load(open(os.path.join(ROOT, "tests", "golden", "appendix_a.json")))
+CLI = os.path.join(ROOT, "w-fsa_amd", "wfsa_amd", "wfsa")
+
+
+@pytest.mark.parametrize("family", [
+    dict(n_states=8, degree=2, vocab=4, emissions=1, n_strings=200, max_len=8),
+    dict(n_states=20, degree=4, vocab=6, emissions=2, n_strings=300, max_len=12),
+    dict(n_states=64, degree=4, vocab=16, emissions=1, n_strings=400, max_len=10),
+])
+def test_count_covariance_equals_gradient_derivative(family):
+    """sum_s p_s Cov_s(c_j, c_k) = -d grad_j / d w_k (grad_j = -sum p E[c_j]):
+    central differences of the device gradient, every pattern pair; and the
+    pairs outside the pattern have no derivative.  Second-order terms exist
+    for strings compiled into bubbles only, so the corpus is cut to those."""
+    import wfsa_amd as W
+    syn = W.Synthetic(seed=3, **family)
+    sym, off, wt = syn.corpus()
+    fsa = W.Fsa.read_text(syn.wfsa_text)
+    nf = len(fsa.param_names())
+    dev = W.Device(0)
+    dev.load_model(fsa)
+    dev.load_corpus(sym, off, wt / wt.sum())
+    rec, pc, used = dev.recognize()
+    tiers = dev.string_tiers()
+    keep = np.flatnonzero((tiers == -1) & (rec == 1))
+    assert len(keep) >= 10, (len(keep), np.bincount(tiers + 1))
+    strings = [bytes(sym[off[i]:off[i + 1]]) for i in keep]
+    sym2 = np.frombuffer(b"".join(strings), dtype=np.uint8).copy()
+    off2 = np.concatenate([[0], np.cumsum([len(x) for x in strings])]).astype(np.int64)
+    dev.load_corpus(sym2, off2, wt[keep] / wt.sum())
+    rec, pc, used = dev.recognize()
+    assert rec.all() and (pc > 1).any()
+    pairs = dev.hf_setup()
+    w = np.random.default_rng(1).normal(-1.0, 0.3, size=nf)
+    cov = dev.hf_eval(w)
+    assert len(pairs) > 0
+    h = 1e-5
+    jac = np.zeros((nf, nf))
+    for k in range(nf):
+        if not used[k]:
+            continue
+        wp, wm = w.copy(), w.copy()
+        wp[k] += h
+        wm[k] -= h
+        jac[:, k] = -(dev.objective_grad(wp, want_logq=False)[1] - dev.objective_grad(wm, want_logq=False)[1]) / (2 * h)
+    dense = np.zeros((nf, nf))
+    for (j, k), v in zip(pairs, cov):
+        dense[j, k] = v
+        dense[k, j] = v
+    scale = np.abs(jac).max()
+    np.testing.assert_allclose(dense, jac, rtol=0, atol=1e-7 * scale)
+    assert np.abs(jac - (jac + jac.T) / 2).max() <= 1e-7 * scale
+
+
+def _run_cli(wfsa, corpus, *extra):
+    r = subprocess.run([CLI, "-a", os.path.join(DATA, wfsa + ".wfsa"), "-c", os.path.join(DATA, corpus + ".corpus"),
+                        *extra], capture_output=True, text=True, timeout=120)
+    return r
+
+
+CTESTS = [("test", "test"), ("test.list", "test"), ("test2", "test"), ("test3", "test"), ("test4", "test"),
+          ("test.loop", "test"), ("talk", "talk"), ("talk", "test")]
+CTEST_NAMES = ["test1", "testlist", "test2", "test3", "test4", "test_loop", "test_talk", "test_talk2"]
+
+
+@pytest.mark.parametrize("case,name", list(zip(CTESTS, CTEST_NAMES)), ids=CTEST_NAMES)
+@pytest.mark.parametrize("verbose", [False, True], ids=["", "v"])
+def test_ctest_exit_codes(case, name, verbose):
+    extra = (["-p"] if verbose else []) + ["-n", "-eval", "-e", "20", "-i", "31"]
+    r = _run_cli(case[0], case[1], *extra)
+    assert r.returncode == GOLD["ctest_exit_codes"][name], r.stderr[-2000:]
+    if r.returncode == 0:
+        assert "Result:" in r.stderr
+
+
+def _check_talk_result(got, want):
+    """every entry but logdetH (index 4) to 5e-13; talk's weight-space
+    Hessian is exactly singular (tests/test_oracle.py), so logdetH is the log
+    of a rounding residue: only 'numerically singular' is pinned"""
+    keep = [0, 1, 2, 3, 5, 6, 7]
+    np.testing.assert_allclose(got[keep], want[keep], rtol=5e-13, atol=1e-14)
+    assert got[4] == np.inf or got[4] < -15.0
+
+
+def test_talk_eval_result_matches_reference():
+    """`wfsa -a talk.wfsa -c talk.corpus -n -eval -e 20 -i 31` Result line
+    (KL, mxlogx(support), LogModelVolume, LogAuxVolume, logdetH, LogDetAuxH,
+    n-k, aux-1) == the reference's printout (15 significant digits)"""
+    r = _run_cli("talk", "talk", "-n", "-eval", "-e", "20", "-i", "31", "-s")
+    assert r.returncode == 0, r.stderr[-2000:]
+    line = [l for l in r.stderr.splitlines() if l.startswith("Result:")][-1]
+    got = [float(v) for v in line.split()[1:]]
+    want = np.array(GOLD["talk_hessian_result"]["result"])
+    assert len(got) == len(want)
+    _check_talk_result(np.array(got), want)
+
+
+def test_hessian_learner_api_talk():
+    """the same through the C ABI (wfsa_learner_create("Hessian"))"""
+    import wfsa_amd as W
+    fsa = W.Fsa.read_file(os.path.join(DATA, "talk.wfsa"))
+    corpus = W.Corpus.read_file(os.path.join(DATA, "talk.corpus"))
+    lrn = W.HessianLearner(0)
+    assert lrn.width == 9
+    lrn.BuildFrom(fsa, corpus)
+    lrn.Finalize()
+    rows = lrn.run(flags=31, epochs=20, tol=1e-6)
+    assert 1 <= len(rows) <= 20
+    lrn.Renormalize()
+    _check_talk_result(np.array(lrn.result()), np.array(GOLD["talk_hessian_result"]["result"]))
+
+
+HCASES = [("talk", "talk"), ("test3", "test"), ("test4", "test"), ("test.list", "test"), ("test2", "test"),
+          ("test.loop", "test")]
+
+
+@pytest.mark.parametrize("wfsa", ["test5", "test5_2"])
+def test_hessian_learner_fails_loudly_beyond_bubbles(wfsa):
+    """test5's one string is a single 20-node ambiguity region, wider than a
+    compiled bubble: the second-order term is not available for it and the
+    learner says so (WFSA_ERR_CAPACITY) instead of dropping H_f"""
+    import wfsa_amd as W
+    lrn = W.HessianLearner(0)
+    lrn.BuildFrom(W.Fsa.read_file(os.path.join(DATA, wfsa + ".wfsa")),
+                  W.Corpus.read_file(os.path.join(DATA, "test5.corpus")))
+    lrn.Finalize()
+    with pytest.raises(W.WfsaError, match="traversal tiers"):
+        lrn.run(flags=31, epochs=20, tol=1e-6)
+
+
+@pytest.mark.parametrize("case", HCASES, ids=lambda c: f"{c[0]}+{c[1]}")
+def test_hessian_learner_epochs_match_restatement(case):
+    """HessianLearner through the C ABI, epoch by epoch (KL, graderr, g_min,
+    g_max, inertia +/-, lambda_min) and its Result vector, against the dense
+    restatement oracle/hessian.py on the oracle's enumerated paths.  logdetH is
+    compared where the Hessian is well conditioned (talk's is singular)."""
+    import wfsa_amd as W
+    from oracle import Oracle
+    from oracle.hessian import HessianOracle
+    wpath, cpath = os.path.join(DATA, case[0] + ".wfsa"), os.path.join(DATA, case[1] + ".corpus")
+    h = HessianOracle(Oracle.from_files(wpath, cpath))
+    want = np.array(h.run(flags=31, epochs=20, tol=1e-6))
+    h.renormalize()
+    want_res = h.result()
+    lrn = W.HessianLearner(0)
+    lrn.BuildFrom(W.Fsa.read_file(wpath), W.Corpus.read_file(cpath))
+    lrn.Finalize()
+    got = np.array(lrn.run(flags=31, epochs=20, tol=1e-6))
+    assert got.shape[0] == want.shape[0]
+    # KL and residuals; the residuals shrink to ~1e-12, so an absolute floor
+    np.testing.assert_allclose(got[:, 0], want[:, 0], rtol=1e-10, atol=1e-13)
+    np.testing.assert_allclose(got[:, 1:4], want[:, 1:4], rtol=1e-6, atol=1e-10)
+    np.testing.assert_array_equal(got[:, 4:6], want[:, 4:6])
+    np.testing.assert_allclose(got[:, 6], want[:, 6], rtol=1e-9, atol=1e-12)
+    lrn.Renormalize()
+    # same parameters, possibly another order: match them by name.  On a
+    # singular Hessian (talk: a one-dimensional set of optima) the last Newton
+    # steps move along the flat direction by rounding-sized amounts
+    ev = np.abs(np.linalg.eigvalsh(h.weight_hessian()))
+    well = ev.min() > 1e-8 * ev.max()
+    names = {n: i for i, n in enumerate(h.o.param_names())}
+    order = [names[n] for n in lrn.param_names()]
+    np.testing.assert_allclose(lrn.x(), h.x[order], rtol=0, atol=1e-8 if well else 1e-4)
+    res = np.array(lrn.result())
+    keep = [0, 1, 2, 3, 5, 6, 7]
+    np.testing.assert_allclose(res[keep], want_res[keep], rtol=1e-10, atol=1e-13)
+    if well:
+        if np.isinf(want_res[4]):
+            assert np.isinf(res[4])
+        else:
+            np.testing.assert_allclose(res[4], want_res[4], rtol=1e-8, atol=1e-10)

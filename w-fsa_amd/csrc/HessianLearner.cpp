@@ -1,0 +1,369 @@
+#include "HessianLearner.hpp"
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <limits>
+#include <numeric>
+
+namespace wfsa {
+
+// ---------------------------------------------------------------- LDL^T ----
+
+void DenseLdlt::Factor(std::vector<double>& A, int64_t n) {
+    n_ = n;
+    perm_.resize(size_t(n));
+    std::iota(perm_.begin(), perm_.end(), int64_t(0));
+    block_.assign(size_t(n), 1);
+    positive = negative = zero = 0;
+    log_abs_det = 0.0;
+    det_sign = 1;
+    const double alpha = (1.0 + std::sqrt(17.0)) / 8.0;   // Bunch-Kaufman
+    auto at = [&](int64_t i, int64_t j) -> double& { return A[size_t(i * n + j)]; };
+    auto swap_sym = [&](int64_t p, int64_t q) {   // rows and columns p <-> q, L columns included
+        if (p == q) return;
+        for (int64_t j = 0; j < n; ++j) std::swap(at(p, j), at(q, j));
+        for (int64_t i = 0; i < n; ++i) std::swap(at(i, p), at(i, q));
+        std::swap(perm_[size_t(p)], perm_[size_t(q)]);
+    };
+    std::vector<double> c1(static_cast<size_t>(n)), c2(static_cast<size_t>(n));
+    auto account = [&](double d) {
+        if (d > 0) ++positive;
+        else if (d < 0) ++negative;
+        else ++zero;
+        if (d == 0) {
+            log_abs_det = -std::numeric_limits<double>::infinity();
+            det_sign = 0;
+        } else {
+            log_abs_det += std::log(std::abs(d));
+            if (d < 0) det_sign = -det_sign;
+        }
+    };
+    int64_t k = 0;
+    while (k < n) {
+        int64_t kstep = 1, kp = k;
+        const double absakk = std::abs(at(k, k));
+        int64_t imax = k;
+        double colmax = 0.0;
+        for (int64_t i = k + 1; i < n; ++i)
+            if (std::abs(at(i, k)) > colmax) {
+                colmax = std::abs(at(i, k));
+                imax = i;
+            }
+        if (std::max(absakk, colmax) == 0.0 || absakk >= alpha * colmax) {
+            kp = k;
+        } else {
+            double rowmax = 0.0;
+            for (int64_t j = k; j < n; ++j)
+                if (j != imax) rowmax = std::max(rowmax, std::abs(at(imax, j)));
+            if (absakk >= alpha * colmax * (colmax / rowmax)) {
+                kp = k;
+            } else if (std::abs(at(imax, imax)) >= alpha * rowmax) {
+                kp = imax;
+            } else {
+                kp = imax;
+                kstep = 2;
+            }
+        }
+        const int64_t kk = k + kstep - 1;
+        if (kp != kk) swap_sym(kk, kp);
+        if (kstep == 1) {
+            const double d = at(k, k);
+            account(d);
+            for (int64_t i = k + 1; i < n; ++i) c1[size_t(i)] = at(i, k);
+            for (int64_t i = k + 1; i < n; ++i) {
+                const double li = d != 0.0 ? c1[size_t(i)] / d : 0.0;
+                if (li != 0.0)
+                    for (int64_t j = k + 1; j < n; ++j) at(i, j) -= li * c1[size_t(j)];
+                at(i, k) = li;
+            }
+        } else {
+            block_[size_t(k)] = 2;
+            block_[size_t(k) + 1] = 0;
+            const double d11 = at(k, k), d21 = at(k + 1, k), d22 = at(k + 1, k + 1);
+            const double det = d11 * d22 - d21 * d21;
+            if (det < 0) {
+                ++positive;
+                ++negative;
+            } else if (det > 0) {
+                if (d11 + d22 > 0) positive += 2;
+                else negative += 2;
+            } else {
+                ++zero;
+                if (d11 + d22 > 0) ++positive;
+                else if (d11 + d22 < 0) ++negative;
+                else ++zero;
+            }
+            if (det == 0) {
+                log_abs_det = -std::numeric_limits<double>::infinity();
+                det_sign = 0;
+            } else {
+                log_abs_det += std::log(std::abs(det));
+                if (det < 0) det_sign = -det_sign;
+            }
+            for (int64_t i = k + 2; i < n; ++i) {
+                c1[size_t(i)] = at(i, k);
+                c2[size_t(i)] = at(i, k + 1);
+            }
+            for (int64_t i = k + 2; i < n; ++i) {
+                const double l1 = (c1[size_t(i)] * d22 - c2[size_t(i)] * d21) / det;
+                const double l2 = (c2[size_t(i)] * d11 - c1[size_t(i)] * d21) / det;
+                for (int64_t j = k + 2; j < n; ++j) at(i, j) -= l1 * c1[size_t(j)] + l2 * c2[size_t(j)];
+                at(i, k) = l1;
+                at(i, k + 1) = l2;
+            }
+        }
+        k += kstep;
+    }
+    a_.swap(A);
+}
+
+void DenseLdlt::Solve(const double* b, double* x) const {
+    const int64_t n = n_;
+    auto L = [&](int64_t i, int64_t j) { return a_[size_t(i * n + j)]; };
+    std::vector<double> y(static_cast<size_t>(n));
+    for (int64_t i = 0; i < n; ++i) y[size_t(i)] = b[perm_[size_t(i)]];
+    for (int64_t k = 0; k < n;) {   // L z = y
+        if (block_[size_t(k)] == 1) {
+            for (int64_t i = k + 1; i < n; ++i) y[size_t(i)] -= L(i, k) * y[size_t(k)];
+            k += 1;
+        } else {
+            for (int64_t i = k + 2; i < n; ++i) y[size_t(i)] -= L(i, k) * y[size_t(k)] + L(i, k + 1) * y[size_t(k) + 1];
+            k += 2;
+        }
+    }
+    for (int64_t k = 0; k < n;) {   // D w = z
+        if (block_[size_t(k)] == 1) {
+            y[size_t(k)] /= L(k, k);
+            k += 1;
+        } else {
+            const double d11 = L(k, k), d21 = L(k + 1, k), d22 = L(k + 1, k + 1);
+            const double det = d11 * d22 - d21 * d21;
+            const double r1 = y[size_t(k)], r2 = y[size_t(k) + 1];
+            y[size_t(k)] = (d22 * r1 - d21 * r2) / det;
+            y[size_t(k) + 1] = (d11 * r2 - d21 * r1) / det;
+            k += 2;
+        }
+    }
+    for (int64_t k = n - 1; k >= 0;) {   // L^T u = w
+        if (block_[size_t(k)] == 0) {   // second of a 2x2: the pair is (k-1, k)
+            const int64_t f = k - 1;
+            for (int64_t i = k + 1; i < n; ++i) {
+                y[size_t(f)] -= L(i, f) * y[size_t(i)];
+                y[size_t(k)] -= L(i, k) * y[size_t(i)];
+            }
+            k -= 2;
+        } else {
+            for (int64_t i = k + 1; i < n; ++i) y[size_t(k)] -= L(i, k) * y[size_t(i)];
+            k -= 1;
+        }
+    }
+    for (int64_t i = 0; i < n; ++i) x[perm_[size_t(i)]] = y[size_t(i)];
+}
+
+// ------------------------------------------------------- HessianLearner ----
+
+void HessianLearner::FinalizeCallback() {   // src/HessianLearner.cpp:19-26
+    const size_t n = size_t(GetNumberOfParameters()), k = size_t(GetNumberOfConstraints());
+    rhs.assign(n + k, 0.0);
+    expx.assign(n, 0.0);
+    grad.assign(n, 0.0);
+    lambda.assign(k, 1.0);   // _x.resize(n + k, 1.0)
+    hf_ready = false;
+}
+
+void HessianLearner::InitCallback(int flags) {   // :132-191
+    exponential_lambda = (flags & 32) != 0;
+    if (flags & 1) {
+        std::fill(_x.begin(), _x.end(), 0.0);
+        std::fill(lambda.begin(), lambda.end(), 1.0);
+    }
+    if (flags & 2) Renormalize();
+    if (flags & 4) InitSlackVariables();
+    include_Hf = (flags & 8) != 0;   // AssembleH(include_Hf)
+    if (include_Hf && !HasUniquePaths()) SetupHf();
+    // flags & 16 (METIS reordering) changes nothing in a dense factorisation
+    degenerate = false;
+}
+
+void HessianLearner::InitSlackVariables() {   // :554-563: lambda <- -C^T grad f
+    ComputeExpX();
+    ComputeGrad();
+    std::fill(lambda.begin(), lambda.end(), 0.0);
+    for (size_t i = 0; i < grad.size(); ++i) lambda[size_t(Ccol[i])] -= grad[i];
+}
+
+void HessianLearner::ComputeExpX() {
+    for (size_t i = 0; i < _x.size(); ++i) expx[i] = std::exp(_x[i]);
+}
+
+void HessianLearner::ComputeGrad() {   // :565-597, from the device
+    ComputeModeledProbs();
+    grad = grad_cache;
+}
+
+void HessianLearner::ComputeRhs() {   // :610-620: rhs <- [grad f + J_g lambda, C^T exp(x) - 1]
+    ComputeExpX();
+    ComputeGrad();
+    const size_t n = _x.size(), k = lambda.size();
+    for (size_t c = 0; c < k; ++c) rhs[n + c] = -1.0;
+    for (size_t i = 0; i < n; ++i) {
+        rhs[n + size_t(Ccol[i])] += expx[i];
+        rhs[i] = grad[i] + expx[i] * lambda[size_t(Ccol[i])];
+    }
+}
+
+void HessianLearner::SetupHf() {
+    if (hf_ready) return;
+    wfsa_dev* d = Device();
+    int64_t np = 0;
+    ThrowOnDevError(wfsa_dev_hf_setup(d, &np), "wfsa_dev_hf_setup");
+    std::vector<int32_t> pairs(size_t(2 * np));
+    ThrowOnDevError(wfsa_dev_hf_pairs(d, pairs.data()), "wfsa_dev_hf_pairs");
+    const auto& tw = GetTrimmedIndex();
+    hf_j.resize(size_t(np));
+    hf_k.resize(size_t(np));
+    for (int64_t t = 0; t < np; ++t) {
+        const int32_t a = tw[size_t(pairs[size_t(2 * t)])], b = tw[size_t(pairs[size_t(2 * t) + 1])];
+        hf_j[size_t(t)] = a >= 0 ? a : -1;
+        hf_k[size_t(t)] = b >= 0 ? b : -1;
+    }
+    hf_vals.resize(size_t(np));
+    hf_ready = true;
+}
+
+bool HessianLearner::AddHf(std::vector<double>& H, int64_t ld) {   // ComputeHf, :498-547
+    SetupHf();
+    const int32_t nf = GetNumberOfFullParameters();
+    w_hf.resize(size_t(nf));
+    for (int32_t j = 0; j < nf; ++j) w_hf[size_t(j)] = GetWeight(j);
+    ThrowOnDevError(wfsa_dev_hf_eval(Device(), w_hf.data(), hf_vals.data()), "wfsa_dev_hf_eval");
+    bool offdiag = false;
+    for (size_t t = 0; t < hf_vals.size(); ++t) {
+        const int64_t a = hf_j[t], b = hf_k[t];
+        if (a < 0 || b < 0) continue;
+        H[size_t(a * ld + b)] -= hf_vals[t];
+        if (a != b) {
+            H[size_t(b * ld + a)] -= hf_vals[t];
+            offdiag = true;
+        }
+    }
+    return offdiag;
+}
+
+void HessianLearner::OptimizationStep(double eta, bool) {   // :63-130
+    ComputeRhs();
+    ComputeObjective();
+    const int64_t n = int64_t(_x.size()), k = int64_t(lambda.size()), N = n + k;
+    if (N > kMaxDense)
+        throw LearnerError("HessianLearner: the augmented system has ", N, " unknowns; this build factors it densely "
+                           "up to ", kMaxDense, " (use -opt QuasiNewton)");
+    std::vector<double> H(size_t(N * N), 0.0);
+    if (include_Hf && !HasUniquePaths()) AddHf(H, N);
+    for (int64_t i = 0; i < n; ++i) {   // ComputeHg, :622-639
+        const int64_t c = n + Ccol[size_t(i)];
+        H[size_t(i * N + i)] += expx[size_t(i)] * lambda[size_t(Ccol[size_t(i)])];
+        H[size_t(i * N + c)] += expx[size_t(i)];
+        H[size_t(c * N + i)] += expx[size_t(i)];
+    }
+    lambda_min = k ? *std::min_element(lambda.begin(), lambda.end()) : 0.0;
+    DenseLdlt f;
+    f.Factor(H, N);
+    inertia_pos = f.positive;
+    inertia_neg = f.negative;
+    step.assign(size_t(N), 0.0);
+    f.Solve(rhs.data(), step.data());
+    const auto bad = [](double v) { return !std::isfinite(v); };
+    if (std::any_of(step.begin(), step.end(), bad)) {
+        degenerate = true;
+        std::fprintf(stderr,
+                     "Solution of Newton step is degenerate at %f%% of the parameters and %f%% of the constraints!\n",
+                     100.0 * double(std::count_if(step.begin(), step.begin() + n, bad)) / double(n),
+                     100.0 * double(std::count_if(step.begin() + n, step.end(), bad)) / double(std::max<int64_t>(k, 1)));
+    } else {
+        for (int64_t i = 0; i < n; ++i) _x[size_t(i)] -= eta * step[size_t(i)];
+        LambdaUpdate(step.data() + n, lambda.data(), eta, exponential_lambda);
+    }
+}
+
+std::string HessianLearner::GetOptimizationHeader() const {   // :272-282
+    return "       KL   graderr     g_min     g_max         +         - lambdamin      rmin";
+}
+
+// [KL, graderr, g_min, g_max, inertia +, inertia -, lambda_min, rmin, rmin
+// index] (:284-347); rmin (smallest relative path probability) needs an
+// explicit path list and is reported as 0
+std::vector<double> HessianLearner::GetOptimizationInfo() {
+    std::vector<double> r(9, 0.0);
+    const size_t n = _x.size();
+    r[0] = GetKLDistance();
+    for (size_t i = 0; i < n; ++i) r[1] = std::max(r[1], std::abs(rhs[i]));
+    if (rhs.size() > n) {
+        r[2] = *std::min_element(rhs.begin() + std::ptrdiff_t(n), rhs.end());
+        r[3] = *std::max_element(rhs.begin() + std::ptrdiff_t(n), rhs.end());
+    }
+    error = std::max(std::max(r[1], std::abs(r[2])), std::abs(r[3]));
+    if (!degenerate) {
+        r[4] = double(inertia_pos);
+        r[5] = double(inertia_neg);
+    }
+    r[6] = lambda_min;
+    return r;
+}
+
+bool HessianLearner::HaltCondition(double tol) {   // :374-379
+    if (degenerate) throw LearnerError("Unable to continue!");
+    return error <= tol;
+}
+
+// log det of the objective's Hessian in the weights w = exp(x):
+// (H_f - diag(grad f)) / (exp(x_j) exp(x_k)) (:219-260)
+double HessianLearner::ComputeLogDetHessian() {
+    const int64_t n = int64_t(_x.size());
+    if (n > kMaxDense)
+        throw LearnerError("HessianLearner: log det of ", n, " parameters exceeds the dense limit ", kMaxDense);
+    std::vector<double> H(size_t(n * n), 0.0);
+    ComputeExpX();
+    ComputeGrad();
+    const bool offdiag = !HasUniquePaths() && AddHf(H, n);
+    for (int64_t j = 0; j < n; ++j) H[size_t(j * n + j)] -= grad[size_t(j)];
+    for (int64_t j = 0; j < n; ++j)
+        for (int64_t k = 0; k < n; ++k) H[size_t(j * n + k)] /= expx[size_t(j)] * expx[size_t(k)];
+    const double inf = std::numeric_limits<double>::infinity();
+    if (!offdiag) {   // diagonal (src/Utils.cpp:300-311)
+        double r = 0.0;
+        for (int64_t i = 0; i < n; ++i) {
+            const double d = H[size_t(i * n + i)];
+            if (!(d > 0)) return inf;
+            r += std::log(d);
+        }
+        return r;
+    }
+    DenseLdlt f;
+    f.Factor(H, n);
+    if (f.det_sign <= 0) return inf;   // (:351-352)
+    return f.log_abs_det;
+}
+
+std::vector<double> HessianLearner::GetOptimizationResult(bool) {   // :349-372
+    ComputeModeledProbs();
+    ComputeObjective();
+    const double logdet = ComputeLogDetHessian();
+    const int64_t n = int64_t(_x.size());
+    int64_t nnz = n;
+    if (hf_ready)
+        for (size_t t = 0; t < hf_j.size(); ++t)
+            if (hf_j[t] >= 0 && hf_k[t] >= 0 && hf_j[t] != hf_k[t]) ++nnz;
+    std::fprintf(stderr, "Hessian:\n\trows: %lld\n\tnnz: %lld\n\tfill: %g\n", (long long)n, (long long)nnz,
+                 n ? double(nnz) / double(n) : 0.0);
+    return {GetKLDistance(),
+            mxlogx(GetCommonSupport()),
+            LogModelVolume(),
+            LogAuxiliaryVolume(),
+            logdet,
+            LogDetAuxiliaryHessian(),
+            double(GetNumberOfParameters() - GetNumberOfConstraints()),
+            double(std::max<int64_t>(0, GetNumberOfAuxParameters() - 1))};
+}
+
+}  // namespace wfsa

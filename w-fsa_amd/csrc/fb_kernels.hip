@@ -664,6 +664,121 @@ __global__ __launch_bounds__(kWideBlock) void wide_kernel(WideArgs a) {
     }
 }
 
+// Hessian second-order term per bubble (fb_kernels.hpp HfArgs).  The
+// bubble's local node ids are in position order, so its edges (listed by
+// source position) are already topologically sorted.
+__global__ __launch_bounds__(kHfBlock) void hf_kernel(HfArgs a) {
+    constexpr int NW = kHfBlock / kWave;
+    constexpr int NN = kMaxBubbleNodes;
+    __shared__ double s_w[NW][kMaxBubbleEdges + 1];
+    __shared__ int s_sd[NW][kMaxBubbleEdges + 1];
+    __shared__ int s_code[NW][kMaxBubbleEdges + 1];
+    __shared__ double s_R[NW][NN * NN];
+    __shared__ double s_ab[NW][2 * NN];
+    const int lane = lane_id(), w = int(threadIdx.x) / kWave;
+    const int b = int(blockIdx.x) * NW + w;
+    if (b >= a.n_bubbles) return;
+    const int32_t* rec = a.bub + a.bub_off[b];
+    const int nodes = rec[0] & 0xffff, edges = rec[0] >> 16;
+    const double p = __longlong_as_double((long long)(uint32_t(rec[2])) | ((long long)(uint32_t(rec[3])) << 32));
+    double* lw = s_w[w];
+    int* sd = s_sd[w];
+    int* code = s_code[w];
+    double* R = s_R[w];
+    double* A = s_ab[w];
+    double* B = s_ab[w] + NN;
+    for (int e = lane; e < edges; e += kWave) {
+        const int c = rec[4 + 2 * e];
+        sd[e] = rec[5 + 2 * e];
+        code[e] = c;
+        double wgt;
+        if (c >= 0) {
+            wgt = a.ewp[c];
+        } else {
+            const int g = -c - 2;
+            double t = 0.0;
+            for (int q = a.m.pptr[g]; q < a.m.pptr[g + 1]; ++q) t += a.w[a.m.pidx[q]];
+            wgt = exp(t);
+        }
+        lw[e] = wgt;
+    }
+    // R(u, v) = sum of the path weights from u to v: lane v owns column v
+    for (int u = 0; u < nodes; ++u)
+        if (lane < nodes) R[u * NN + lane] = u == lane ? 1.0 : 0.0;
+    wave_sync();
+    if (lane < nodes) {
+        for (int e = edges - 1; e >= 0; --e) {
+            const int src = sd[e] & 0xffff, dst = sd[e] >> 16;
+            R[src * NN + lane] += lw[e] * R[dst * NN + lane];
+        }
+    }
+    wave_sync();
+    if (lane < nodes) {   // alpha = R(0, .) (paths from the entry), beta = R(., end)
+        A[lane] = R[lane];
+        B[lane] = R[lane * NN + nodes - 1];
+    }
+    wave_sync();
+    const double Z = B[0];
+    const double inv_z = 1.0 / Z;
+    // slots: every ordered edge pair (e, f), every parameter pair (j in e,
+    // k in f) with j <= k, in nesting order; lanes take the (e, f) pairs
+    auto params = [&](int c, int* out) {   // the edge's parameters (in list order)
+        if (c >= 0) {
+            if (c < a.m.n_params) { out[0] = c; return 1; }
+            return 0;
+        }
+        const int g = -c - 2;
+        int n = 0;
+        for (int q = a.m.pptr[g]; q < a.m.pptr[g + 1] && n < 8; ++q) out[n++] = a.m.pidx[q];
+        return n;
+    };
+    // slot offsets of the ordered pairs are prefix sums over (e, f); lane 0
+    // walks them in order and the lanes fill pair by pair
+    int64_t slot = a.slot_base[b];
+    for (int ef0 = 0; ef0 < edges * edges; ef0 += kWave) {
+        const int ef = ef0 + lane;
+        int pe[8], pf[8], ne = 0, nf = 0, cnt = 0;
+        double v = 0.0;
+        if (ef < edges * edges) {
+            const int e = ef / edges, f = ef % edges;
+            ne = params(code[e], pe);
+            nf = params(code[f], pf);
+            for (int x = 0; x < ne; ++x)
+                for (int y = 0; y < nf; ++y) cnt += pe[x] <= pf[y];
+            const int se = sd[e] & 0xffff, de = sd[e] >> 16, sf = sd[f] & 0xffff, df = sd[f] >> 16;
+            const double Pe = A[se] * lw[e] * B[de] * inv_z;
+            const double Pf = A[sf] * lw[f] * B[df] * inv_z;
+            double both;
+            if (e == f) both = Pe;
+            else if (R[de * NN + sf] > 0.0) both = A[se] * lw[e] * R[de * NN + sf] * lw[f] * B[df] * inv_z;
+            else if (R[df * NN + se] > 0.0) both = A[sf] * lw[f] * R[df * NN + se] * lw[e] * B[de] * inv_z;
+            else both = 0.0;
+            v = p * (both - Pe * Pf);
+        }
+        // exclusive prefix of cnt over the lanes (pair order = lane order)
+        int incl = cnt;
+#pragma unroll
+        for (int o = 1; o < kWave; o <<= 1) {
+            const int t = __shfl_up(incl, o, kWave);
+            if (lane >= o) incl += t;
+        }
+        int64_t my = slot + (incl - cnt);
+        for (int x = 0; x < ne; ++x)
+            for (int y = 0; y < nf; ++y)
+                if (pe[x] <= pf[y]) a.slot_val[my++] = v;
+        slot += __shfl(incl, kWave - 1, kWave);
+    }
+}
+
+// pattern entry t = its slots' sum, in slot order (deterministic)
+__global__ __launch_bounds__(256) void hf_sum_kernel(HfArgs a) {
+    const int64_t t = int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+    if (t >= a.n_pattern) return;
+    double s = 0.0;
+    for (int64_t q = a.t_ptr[t]; q < a.t_ptr[t + 1]; ++q) s += a.slot_val[a.t_slot[q]];
+    a.out[t] = s;
+}
+
 // Main streams: one lane per string, 64 strings of similar stream length per
 // wavefront.  Every word is an edge on all of the string's paths (posterior
 // 1): log q accumulates its log-weight and its parameters get -p_s.  A
@@ -1324,6 +1439,15 @@ hipError_t launch_trav(TravMode mode, const TravArgs& a, int grid, hipStream_t s
             hipLaunchKernelGGL(trav_kernel<MODE_EMIT>, dim3(unsigned(grid)), block, lds, stream, a);
             break;
     }
+    return hipGetLastError();
+}
+
+hipError_t launch_hf(const HfArgs& a, hipStream_t stream) {
+    constexpr int NW = kHfBlock / kWave;
+    if (a.n_bubbles > 0)
+        hipLaunchKernelGGL(hf_kernel, dim3(unsigned((a.n_bubbles + NW - 1) / NW)), dim3(kHfBlock), 0, stream, a);
+    if (a.n_pattern > 0)
+        hipLaunchKernelGGL(hf_sum_kernel, dim3(unsigned((a.n_pattern + 255) / 256)), dim3(256), 0, stream, a);
     return hipGetLastError();
 }
 

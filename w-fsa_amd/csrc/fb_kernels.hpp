@@ -184,6 +184,34 @@ inline int64_t wide_scratch_stride(int32_t max_len, int32_t n_nodes) {
 }
 hipError_t launch_wide(bool counting, const WideArgs& a, int grid, hipStream_t stream);
 
+// Second-order term of the Hessian (HessianLearner::ComputeHf,
+// src/HessianLearner.cpp:498-547): sum_s p_s Cov_s(count_j, count_k).  The
+// segments of a compiled string are independent, so a string's covariance is
+// the sum of its bubbles' (trivial words have constant counts).  One
+// wavefront per bubble: alpha, beta, the node-to-node path sums R (<= 16 x 16)
+// and, for every ordered pair of its edges (e, f),
+//   v(e, f) = P(e and f on the path) - P(e) P(f),
+//   P(e and f) = alpha(src e) w_e R(dst e, src f) w_f beta(dst f) / Z (e before f),
+// written p-scaled into the bubble's slots: one slot per (e, f, j in e, k in
+// f, j <= k), in that nesting order (hf_slots counts them the same way).
+struct HfArgs {
+    ModelView m;
+    const int32_t* bub;        // bubble records (BubbleArgs)
+    const int32_t* bub_off;    // [n_bubbles]
+    const int64_t* slot_base;  // [n_bubbles + 1]
+    int32_t n_bubbles;
+    const double* w;           // [n_params + 1] weights (GetWeight form)
+    const double* ewp;         // [n_params + 1] exp(w)
+    double* slot_val;          // [slots]
+    // the pattern sums: entry t = sum of slot_val[t_slot[t_ptr[t] .. t_ptr[t+1])]
+    const int64_t* t_ptr;
+    const int64_t* t_slot;
+    int64_t n_pattern;
+    double* out;               // [n_pattern]
+};
+constexpr int kHfBlock = 256;   // four bubbles per block
+hipError_t launch_hf(const HfArgs& a, hipStream_t stream);
+
 // Device-resident QuasiNewton step (qn_kernel.hip): qn_update (wavefront per
 // constraint) updates x and lambda from out = [LL, grad_full] and writes the
 // next w_full; the finish (qn_finish_wave, qn_device.hpp) reduces the info

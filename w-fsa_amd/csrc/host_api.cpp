@@ -12,6 +12,7 @@
 
 #include "Corpus.hpp"
 #include "Fsa.hpp"
+#include "HessianLearner.hpp"
 #include "Learner.hpp"
 #include "QuasiNewtonLearner.hpp"
 #include "synth.hpp"
@@ -31,7 +32,10 @@ struct wfsa_corpus {
 };
 
 struct wfsa_learner {
-    std::unique_ptr<QuasiNewtonLearner> qn;
+    std::unique_ptr<Learner> base;
+    QuasiNewtonLearner* qn = nullptr;   // exactly one of these is set
+    HessianLearner* hs = nullptr;
+    int width() const { return hs ? 9 : 7; }   // GetOptimizationInfo values
 };
 
 struct wfsa_synth {
@@ -181,11 +185,17 @@ int wfsa_learner_create(const char* optimizer, int device, wfsa_learner** out) {
     if (!optimizer || !out) return null_arg("optimizer/out");
     *out = nullptr;
     return guarded([&] {
-        if (std::strcmp(optimizer, "QuasiNewton") != 0)
-            throw LearnerError("optimizer \"", optimizer, "\" is not available in this build (QuasiNewton only)");
         std::unique_ptr<wfsa_learner> l(new wfsa_learner());
-        l->qn.reset(new QuasiNewtonLearner());
-        l->qn->SetDevice(device);
+        if (std::strcmp(optimizer, "QuasiNewton") == 0) {
+            l->qn = new QuasiNewtonLearner();
+            l->base.reset(l->qn);
+        } else if (std::strcmp(optimizer, "Hessian") == 0) {
+            l->hs = new HessianLearner();
+            l->base.reset(l->hs);
+        } else {
+            throw LearnerError("unknown optimizer \"", optimizer, "\" (Hessian or QuasiNewton)");
+        }
+        l->base->SetDevice(device);
         *out = l.release();
     });
 }
@@ -194,7 +204,7 @@ void wfsa_learner_destroy(wfsa_learner* l) { delete l; }
 
 int wfsa_learner_set_comm(wfsa_learner* l, int nranks, int rank, const uint8_t id[WFSA_COMM_ID_BYTES]) {
     if (!l) return null_arg("learner");
-    return guarded([&] { l->qn->SetCommunicator(nranks, rank, id); });
+    return guarded([&] { l->base->SetCommunicator(nranks, rank, id); });
 }
 
 int wfsa_learner_build_packed(wfsa_learner* l, wfsa_fsa* f, const uint8_t* sym, const int64_t* off,
@@ -205,7 +215,7 @@ int wfsa_learner_build_packed(wfsa_learner* l, wfsa_fsa* f, const uint8_t* sym, 
         for (int64_t s = 0; s < n; ++s) sum += weights[s];
         std::vector<double> w(weights, weights + n);
         for (auto& v : w) v /= sum;   // Corpus::Renormalize (main.cpp:154)
-        l->qn->BuildFromPacked(f->fsa, sym, off, w.data(), n);
+        l->base->BuildFromPacked(f->fsa, sym, off, w.data(), n);
     });
 }
 
@@ -218,15 +228,15 @@ int wfsa_learner_build(wfsa_learner* l, wfsa_fsa* f, wfsa_corpus* c) {
 int wfsa_learner_finalize(wfsa_learner* l) {
     if (!l) return null_arg("learner");
     return guarded([&] {
-        if (l->qn->GetNumberOfParameters() == 0) throw LearnerError("Empty automaton!");
-        if (l->qn->GetNumberOfStrings() == 0) throw LearnerError("Automaton cannot generate any of the strings!");
-        l->qn->Finalize();
+        if (l->base->GetNumberOfParameters() == 0) throw LearnerError("Empty automaton!");
+        if (l->base->GetNumberOfStrings() == 0) throw LearnerError("Automaton cannot generate any of the strings!");
+        l->base->Finalize();
     });
 }
 
 int wfsa_learner_info_get(wfsa_learner* l, wfsa_learner_info* o) {
     if (!l || !o) return null_arg("learner/out");
-    QuasiNewtonLearner& q = *l->qn;
+    Learner& q = *l->base;
     o->n_strings = q.GetNumberOfStrings();
     o->n_local_strings = q.GetNumberOfLocalStrings();
     o->n_paths = q.GetNumberOfPaths();
@@ -248,17 +258,19 @@ int wfsa_learner_info_get(wfsa_learner* l, wfsa_learner_info* o) {
 
 int wfsa_learner_init(wfsa_learner* l, int flags, const double* x0) {
     if (!l) return null_arg("learner");
-    return guarded([&] { l->qn->Init(flags, x0); });
+    return guarded([&] { l->base->Init(flags, x0); });
 }
 
-int wfsa_learner_step(wfsa_learner* l, double eta, double tol, double info[7], int32_t* halt) {
+int wfsa_learner_info_width(wfsa_learner* l) { return l ? l->width() : 0; }
+
+int wfsa_learner_step(wfsa_learner* l, double eta, double tol, double* info, int32_t* halt) {
     if (!l) return null_arg("learner");
     return guarded([&] {
-        l->qn->OptimizationStep(eta, false);
-        const auto v = l->qn->GetOptimizationInfo();
+        l->base->OptimizationStep(eta, false);
+        const auto v = l->base->GetOptimizationInfo();
         if (info)
-            for (size_t i = 0; i < 7; ++i) info[i] = i < v.size() ? v[i] : 0.0;
-        if (halt) *halt = l->qn->HaltCondition(tol) ? 1 : 0;
+            for (size_t i = 0; i < size_t(l->width()); ++i) info[i] = i < v.size() ? v[i] : 0.0;
+        if (halt) *halt = l->base->HaltCondition(tol) ? 1 : 0;
     });
 }
 
@@ -266,20 +278,42 @@ int wfsa_learner_run(wfsa_learner* l, double eta, double tol, int32_t max_epochs
                      int32_t* epochs_done) {
     if (!l) return null_arg("learner");
     if (epochs_done) *epochs_done = 0;
-    return guarded([&] {   // src/main.cpp:276-303, device-resident
-        l->qn->RunDevice(eta, tol, max_epochs, info_rows, epochs_done);
+    return guarded([&] {   // src/main.cpp:276-303
+        if (l->qn) {   // device-resident
+            l->qn->RunDevice(eta, tol, max_epochs, info_rows, epochs_done);
+            return;
+        }
+        const int w = l->width();
+        for (int32_t e = 1; e <= max_epochs; ++e) {
+            l->base->OptimizationStep(eta, false);
+            const auto v = l->base->GetOptimizationInfo();
+            if (info_rows)
+                for (int i = 0; i < w; ++i) info_rows[size_t(e - 1) * size_t(w) + size_t(i)] = v[size_t(i)];
+            if (epochs_done) *epochs_done = e;
+            for (double x : v)
+                if (!std::isfinite(x)) throw LearnerError(x, " detected at epoch ", e);
+            if (l->base->HaltCondition(tol)) break;
+        }
     });
 }
 
 int wfsa_learner_objective_grad(wfsa_learner* l, double* kl, double* grad, double* logq) {
     if (!l) return null_arg("learner");
     return guarded([&] {
-        QuasiNewtonLearner& q = *l->qn;
-        q.ComputeExpX();
-        q.ComputeGrad();
+        const std::vector<double>* g;
+        if (l->qn) {
+            l->qn->ComputeExpX();
+            l->qn->ComputeGrad();
+            g = &l->qn->GetGradient();
+        } else {
+            l->hs->ComputeExpX();
+            l->hs->ComputeGrad();
+            g = &l->hs->GetGradient();
+        }
+        Learner& q = *l->base;
         q.ComputeObjective();
         if (kl) *kl = q.GetKLDistance();
-        if (grad) std::memcpy(grad, q.GetGradient().data(), q.GetGradient().size() * sizeof(double));
+        if (grad) std::memcpy(grad, g->data(), g->size() * sizeof(double));
         if (logq) {
             const auto& lq = q.GetLogQ();
             std::memcpy(logq, lq.data(), lq.size() * sizeof(double));
@@ -289,34 +323,34 @@ int wfsa_learner_objective_grad(wfsa_learner* l, double* kl, double* grad, doubl
 
 int wfsa_learner_get_x(wfsa_learner* l, double* x) {
     if (!l || !x) return null_arg("learner/x");
-    std::memcpy(x, l->qn->GetWeights(), size_t(l->qn->GetNumberOfParameters()) * sizeof(double));
+    std::memcpy(x, l->base->GetWeights(), size_t(l->base->GetNumberOfParameters()) * sizeof(double));
     return WFSA_OK;
 }
 
 int wfsa_learner_set_x(wfsa_learner* l, const double* x) {
     if (!l || !x) return null_arg("learner/x");
-    l->qn->SetWeights(x);
+    l->base->SetWeights(x);
     return WFSA_OK;
 }
 
 int wfsa_learner_get_p(wfsa_learner* l, double* p) {
     if (!l || !p) return null_arg("learner/p");
-    const auto& v = l->qn->GetP();
+    const auto& v = l->base->GetP();
     std::memcpy(p, v.data(), v.size() * sizeof(double));
     return WFSA_OK;
 }
 
 int wfsa_learner_trimmed_index(wfsa_learner* l, int32_t* out) {
     if (!l || !out) return null_arg("learner/out");
-    const auto& v = l->qn->GetTrimmedIndex();
+    const auto& v = l->base->GetTrimmedIndex();
     std::memcpy(out, v.data(), v.size() * sizeof(int32_t));
     return WFSA_OK;
 }
 
 int wfsa_learner_path_counts(wfsa_learner* l, double* out, uint8_t* recognized) {
     if (!l) return null_arg("learner");
-    const auto& pc = l->qn->GetPathCounts();
-    const auto& rc = l->qn->GetRecognized();
+    const auto& pc = l->base->GetPathCounts();
+    const auto& rc = l->base->GetRecognized();
     if (out) std::memcpy(out, pc.data(), pc.size() * sizeof(double));
     if (recognized) std::memcpy(recognized, rc.data(), rc.size());
     return WFSA_OK;
@@ -324,13 +358,13 @@ int wfsa_learner_path_counts(wfsa_learner* l, double* out, uint8_t* recognized) 
 
 int wfsa_learner_renormalize(wfsa_learner* l) {
     if (!l) return null_arg("learner");
-    return guarded([&] { l->qn->Renormalize(); });
+    return guarded([&] { l->base->Renormalize(); });
 }
 
 int wfsa_learner_dump(wfsa_learner* l, wfsa_fsa* f, const char* path) {
     if (!l || !f || !path) return null_arg("learner/fsa/path");
     return guarded([&] {
-        l->qn->RewriteWeights(f->fsa);
+        l->base->RewriteWeights(f->fsa);
         FILE* fp = std::fopen(path, "wb");
         if (!fp) throw LearnerError("Unable to open output file \"", path, "\" for writing!");
         f->fsa.Dump(fp);
@@ -338,14 +372,23 @@ int wfsa_learner_dump(wfsa_learner* l, wfsa_fsa* f, const char* path) {
     });
 }
 
+int wfsa_learner_result(wfsa_learner* l, double out[8]) {
+    if (!l || !out) return null_arg("learner/out");
+    return guarded([&] {
+        const auto v = l->base->GetOptimizationResult(false);
+        for (size_t i = 0; i < 8; ++i) out[i] = i < v.size() ? v[i] : 0.0;
+        if (v.empty()) throw LearnerError("this optimizer has no evaluation result");
+    });
+}
+
 int wfsa_learner_stats(wfsa_learner* l, wfsa_dev_stats* out) {
     if (!l || !out) return null_arg("learner/out");
-    if (!l->qn->Device()) {
+    if (!l->base->Device()) {
         g_host_error = "learner has no device context yet";
         return WFSA_ERR_ARG;
     }
-    const int rc = wfsa_dev_get_stats(l->qn->Device(), out);
-    if (rc == WFSA_OK) {
+    const int rc = wfsa_dev_get_stats(l->base->Device(), out);
+    if (rc == WFSA_OK && l->qn) {
         const auto& t = l->qn->StepTiming();
         out->host_steps = t.steps;
         out->host_begin_ms = t.begin_ms;

@@ -1,18 +1,21 @@
 // wfsa: command-line driver with the reference's flags (src/main.cpp:66-108)
-// for the QuasiNewton optimizer, running the objective/gradient on the GPU.
+// for both optimizers (Hessian, the default, and QuasiNewton), running the
+// objective/gradient (and the Hessian's count covariance) on the GPU.
 //
-//   wfsa -a A.wfsa -c C.corpus [-opt QuasiNewton] [-e epochs] [-l eta]
-//        [-tol t] [-i flags] [-n] [-eval] [-s] [-o out.wfsa] [-x] [-d device]
+//   wfsa -a A.wfsa -c C.corpus [-opt Hessian|QuasiNewton] [-e epochs] [-l eta]
+//        [-tol t] [-i flags] [-n] [-eval] [-s] [-o out.wfsa] [-x] [-p] [-d device]
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <iostream>
+#include <memory>
 #include <string>
 #include <vector>
 
 #include "Corpus.hpp"
 #include "Fsa.hpp"
+#include "HessianLearner.hpp"
 #include "QuasiNewtonLearner.hpp"
 
 using namespace wfsa;
@@ -40,19 +43,21 @@ void usage() {
                  "  -e, --epochs N         maximum optimization epochs (20)\n"
                  "  -l, --eta X            learning rate (1.0)\n"
                  "  -tol X                 halting tolerance (1e-6)\n"
-                 "  -i, --init FLAGS       1 uniform, 2 normalize, 4 Lagrange init, 32 exponential lambda\n"
+                 "  -i, --init FLAGS       1 uniform, 2 normalize, 4 Lagrange init, 8 Hessian of the objective,\n"
+                 "                         16 fill-reducing order (no effect: dense factorisation), 32 exponential lambda\n"
                  "  -n, --normalize        normalize the automaton after optimization\n"
                  "  -eval                  evaluate the model after optimization\n"
                  "  -s, --suppress         do not print the learned FSA\n"
                  "  -x, --initx            read the initial x vector from stdin\n"
-                 "  -opt NAME              QuasiNewton (Hessian is not part of this build)\n"
+                 "  -opt NAME              Hessian (default) or QuasiNewton\n"
+                 "  -p, --print            accepted (the reference prints its path matrices; no paths exist here)\n"
                  "  -d, --device N         GPU to use (0)\n";
 }
 
 }  // namespace
 
 int main(int argc, const char* argv[]) {
-    std::string automaton, corpus_file, output, optimizer = "QuasiNewton";
+    std::string automaton, corpus_file, output, optimizer = "Hessian";
     int epochs = 20, initflags = 0, device = 0;
     double eta = 1.0, tol = 1e-6;
     bool normalize = false, suppress = false, evaluate = false, initx = false;
@@ -80,10 +85,11 @@ int main(int argc, const char* argv[]) {
         else if (a == "-s" || a == "--suppress") suppress = true;
         else if (a == "-x" || a == "--initx" || a == "--initial") initx = true;
         else if (a == "-p" || a == "--print" || a == "-pr" || a == "--print-recognize") { /* no path listing */ }
+        else if (a == "-t" || a == "--thread" || a == "--threads" || a == "-r" || a == "--recognize") next();
         else { std::cerr << "unknown argument " << a << std::endl; usage(); return 1; }
     }
-    if (optimizer != "QuasiNewton") {
-        std::cerr << "optimizer \"" << optimizer << "\" is not available in this build (QuasiNewton only)" << std::endl;
+    if (optimizer != "QuasiNewton" && optimizer != "Hessian") {
+        std::cerr << "optimizer must be Hessian or QuasiNewton, not \"" << optimizer << "\"" << std::endl;
         return 1;
     }
     try {
@@ -112,7 +118,9 @@ int main(int argc, const char* argv[]) {
                   << "\n\tparameters: " << fsa.GetNumberOfParameters()
                   << "\n\tconstraints: " << fsa.GetNumberOfConstraints()
                   << "\n\tfree parameters: " << fsa.GetNumberOfFreeParameters() << std::endl;
-        QuasiNewtonLearner learner;
+        std::unique_ptr<Learner> owner(optimizer == "Hessian" ? static_cast<Learner*>(new HessianLearner())
+                                                               : static_cast<Learner*>(new QuasiNewtonLearner()));
+        Learner& learner = *owner;
         learner.SetDevice(device);
         learner.BuildFrom(fsa, corpus);
         std::cerr << "Recognize:\n\tstrings: " << learner.GetNumberOfStrings()
@@ -162,7 +170,7 @@ int main(int argc, const char* argv[]) {
         if (normalize) learner.Renormalize();
         if (evaluate) {
             const auto results = learner.GetOptimizationResult(false);
-            std::cerr.precision(15);
+            std::cerr.precision(15);   // DBL_DIG
             std::cerr << "Result:";
             for (double x : results) std::cerr << ' ' << x;
             std::cerr << std::endl;

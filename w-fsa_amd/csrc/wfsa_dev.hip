@@ -176,6 +176,7 @@ struct wfsa_dev {
 
     // traversal fallback: per tier string lists (tier 2: wide_kernel)
     int32_t n_fall[3] = {0, 0, 0};
+    std::vector<int8_t> h_tier;   // per string: -1 compiled, 0..2 traversal tier
     int fall_grid[3] = {0, 0, 0};
     DevBuf<int32_t> fall[3];
     // tier 2: byte-indexed in-edge lists and per-block scratch
@@ -229,6 +230,15 @@ struct wfsa_dev {
     std::unique_ptr<wfsa::DensePath> dense;
     int dense_mode = -1;
     bool dense_struct = false;   // the structural pass ran on the loaded corpus
+
+    // Hessian second-order term (wfsa_dev_hf_*): slots per bubble and the
+    // (j, k) pattern they sum into
+    bool hf_ready = false;
+    int hf_gen = -1;
+    std::vector<int32_t> hf_pairs;
+    DevBuf<int64_t> hf_slot_base, hf_t_ptr, hf_t_slot;
+    DevBuf<double> hf_slot_val, hf_out;
+    int64_t hf_n_slots = 0;
 
     // communicator
     ncclComm_t comm = nullptr;
@@ -896,6 +906,8 @@ int prepare(wfsa_dev* ctx, int level) {
     HIP_TRY(ctx->fixed_grad.alloc(size_t(std::max(ctx->n_params, 1))));
 
     // traversal fallback lists
+    ctx->h_tier.assign(size_t(ctx->n_strings), int8_t(-1));
+    for (int t = 0; t < 3; ++t) for (int32_t i : fb[t]) ctx->h_tier[size_t(i)] = int8_t(t);
     for (int t = 0; t < 3; ++t) {
         ctx->n_fall[t] = int32_t(fb[t].size());
         ctx->fall_grid[t] = fb[t].empty() ? 0
@@ -1525,6 +1537,20 @@ int wfsa_dev_recognize(wfsa_dev* ctx, uint8_t* recognized, double* path_count, u
     return WFSA_OK;
 }
 
+int wfsa_dev_string_tiers(wfsa_dev* ctx, int8_t* tier) {
+    if (int rc = check_ctx(ctx)) return rc;
+    if (!ctx->has_model || !ctx->has_corpus) return fail(WFSA_ERR_ARG, "load a model and a corpus first");
+    if (!tier) return fail(WFSA_ERR_ARG, "null output");
+    if (ctx->dense) {
+        std::memset(tier, 3, size_t(ctx->n_strings));
+        return WFSA_OK;
+    }
+    if (ctx->prep_level < 2)
+        if (int rc = prepare(ctx, 2)) return rc;
+    std::memcpy(tier, ctx->h_tier.data(), size_t(ctx->n_strings));
+    return WFSA_OK;
+}
+
 int wfsa_dev_objective_grad_begin(wfsa_dev* ctx, const double* w_full, int want_logq) {
     if (int rc = check_ctx(ctx)) return rc;
     if (!ctx->has_model || !ctx->has_corpus) return fail(WFSA_ERR_ARG, "load a model and a corpus first");
@@ -1747,6 +1773,122 @@ int wfsa_dev_qn_run(wfsa_dev* ctx, double eta, double tol, int32_t max_steps, do
     ctx->stats.compiled_kernel_ms += c_ms_sum;
     if (steps_done) *steps_done = done;
     if (status) *status = st;
+    return WFSA_OK;
+}
+
+int wfsa_dev_hf_setup(wfsa_dev* ctx, int64_t* n_pairs) {
+    if (int rc = check_ctx(ctx)) return rc;
+    if (!ctx->has_model || !ctx->has_corpus) return fail(WFSA_ERR_ARG, "load a model and a corpus first");
+    if (ctx->in_flight) return fail(WFSA_ERR_ARG, "an evaluation is in flight");
+    if (ctx->dense) return fail(WFSA_ERR_CAPACITY, "second-order terms: not available on the dense path");
+    if (ctx->comm) return fail(WFSA_ERR_ARG, "second-order terms: not available with a communicator");
+    if (ctx->prep_level < 2)
+        if (int rc = prepare(ctx, 2)) return rc;
+    const int64_t nfall = int64_t(ctx->n_fall[0]) + ctx->n_fall[1] + ctx->n_fall[2];
+    if (nfall > 0)
+        return fail(WFSA_ERR_CAPACITY, "second-order terms need every string compiled into bubbles; %lld strings "
+                    "are on the traversal tiers", (long long)nfall);
+    hipStream_t s = ctx->stream;
+    const int32_t np = ctx->n_params, nb = ctx->n_bubbles;
+    std::vector<int32_t> off(size_t(std::max(nb, 1)));
+    std::vector<int32_t> buf(ctx->bub.n);
+    if (nb > 0) {
+        HIP_TRY(ctx->bub_off.download(off.data(), size_t(nb), s));
+        HIP_TRY(ctx->bub.download(buf.data(), buf.size(), s));
+        HIP_TRY(hipStreamSynchronize(s));
+    }
+    auto params = [&](int32_t code, std::vector<int32_t>& out) {   // edge_code -> parameters
+        out.clear();
+        if (code >= 0) {
+            if (code < np) out.push_back(code);
+        } else {
+            const int32_t g = -code - 2;
+            for (int32_t q = ctx->h_pptr[size_t(g)]; q < ctx->h_pptr[size_t(g) + 1]; ++q) out.push_back(ctx->h_pidx[size_t(q)]);
+        }
+    };
+    // slots in the kernel's order: (e, f), j in e, k in f, j <= k
+    std::vector<int64_t> base(size_t(nb) + 1, 0), keys;
+    std::vector<std::vector<int32_t>> ep;
+    std::vector<int32_t> tmp;
+    for (int32_t b = 0; b < nb; ++b) {
+        const int32_t o = off[size_t(b)];
+        const int edges = buf[size_t(o)] >> 16;
+        ep.assign(size_t(edges), {});
+        for (int e = 0; e < edges; ++e) {
+            params(buf[size_t(o) + 4 + 2 * size_t(e)], tmp);
+            if (tmp.size() > 8)
+                return fail(WFSA_ERR_CAPACITY, "second-order terms: a bubble edge carries %zu parameters (max 8)",
+                            tmp.size());
+            ep[size_t(e)] = tmp;
+        }
+        for (int e = 0; e < edges; ++e)
+            for (int f = 0; f < edges; ++f)
+                for (int32_t j : ep[size_t(e)])
+                    for (int32_t k : ep[size_t(f)])
+                        if (j <= k) keys.push_back(int64_t(j) * np + k);
+        base[size_t(b) + 1] = int64_t(keys.size());
+    }
+    const int64_t ns = int64_t(keys.size());
+    std::vector<int64_t> order(static_cast<size_t>(ns));
+    for (int64_t i = 0; i < ns; ++i) order[size_t(i)] = i;
+    std::stable_sort(order.begin(), order.end(), [&](int64_t x, int64_t y) { return keys[size_t(x)] < keys[size_t(y)]; });
+    std::vector<int64_t> tptr(1, 0);
+    ctx->hf_pairs.clear();
+    for (int64_t i = 0; i < ns; ++i) {
+        const int64_t key = keys[size_t(order[size_t(i)])];
+        if (i == 0 || key != keys[size_t(order[size_t(i) - 1])]) {
+            if (i > 0) tptr.push_back(i);
+            ctx->hf_pairs.push_back(int32_t(key / np));
+            ctx->hf_pairs.push_back(int32_t(key % np));
+        }
+    }
+    tptr.push_back(ns);
+    if (ns == 0) tptr.assign(1, 0);
+    HIP_TRY(ctx->hf_slot_base.upload(base.data(), base.size(), s));
+    HIP_TRY(ctx->hf_t_ptr.upload(tptr.data(), tptr.size(), s));
+    HIP_TRY(ctx->hf_t_slot.upload(order.empty() ? base.data() : order.data(), std::max<size_t>(order.size(), 1), s));
+    HIP_TRY(ctx->hf_slot_val.alloc(size_t(std::max<int64_t>(ns, 1))));
+    HIP_TRY(ctx->hf_out.alloc(std::max<size_t>(ctx->hf_pairs.size() / 2, 1)));
+    HIP_TRY(hipStreamSynchronize(s));
+    ctx->hf_n_slots = ns;
+    ctx->hf_ready = true;
+    ctx->hf_gen = ctx->prep_gen;
+    if (n_pairs) *n_pairs = int64_t(ctx->hf_pairs.size() / 2);
+    return WFSA_OK;
+}
+
+int wfsa_dev_hf_pairs(wfsa_dev* ctx, int32_t* pairs) {
+    if (int rc = check_ctx(ctx)) return rc;
+    if (!ctx->hf_ready || ctx->hf_gen != ctx->prep_gen) return fail(WFSA_ERR_ARG, "wfsa_dev_hf_setup has not run");
+    if (pairs && !ctx->hf_pairs.empty()) std::memcpy(pairs, ctx->hf_pairs.data(), ctx->hf_pairs.size() * sizeof(int32_t));
+    return WFSA_OK;
+}
+
+int wfsa_dev_hf_eval(wfsa_dev* ctx, const double* w_full, double* values) {
+    if (int rc = check_ctx(ctx)) return rc;
+    if (!ctx->hf_ready || ctx->hf_gen != ctx->prep_gen) return fail(WFSA_ERR_ARG, "wfsa_dev_hf_setup has not run");
+    if (ctx->in_flight) return fail(WFSA_ERR_ARG, "an evaluation is in flight");
+    if (!w_full && ctx->n_params > 0) return fail(WFSA_ERR_ARG, "null weights");
+    hipStream_t s = ctx->stream;
+    const int32_t np = ctx->n_params;
+    if (np > 0) std::memcpy(ctx->pinned + weights_off(np), w_full, size_t(np) * sizeof(double));
+    HIP_TRY(wfsa::launch_stage(ctx->pinned_dev + weights_off(np), ctx->w_full.ptr, ctx->ewp.ptr, np, s));
+    wfsa::HfArgs a{};
+    a.m = model_view(ctx);
+    a.bub = ctx->bub.ptr;
+    a.bub_off = ctx->bub_off.ptr;
+    a.slot_base = ctx->hf_slot_base.ptr;
+    a.n_bubbles = ctx->n_bubbles;
+    a.w = ctx->w_full.ptr;
+    a.ewp = ctx->ewp.ptr;
+    a.slot_val = ctx->hf_slot_val.ptr;
+    a.t_ptr = ctx->hf_t_ptr.ptr;
+    a.t_slot = ctx->hf_t_slot.ptr;
+    a.n_pattern = int64_t(ctx->hf_pairs.size() / 2);
+    a.out = ctx->hf_out.ptr;
+    HIP_TRY(wfsa::launch_hf(a, s));
+    if (values && a.n_pattern > 0) HIP_TRY(ctx->hf_out.download(values, size_t(a.n_pattern), s));
+    HIP_TRY(hipStreamSynchronize(s));
     return WFSA_OK;
 }
 

@@ -152,13 +152,15 @@ class Synthetic:
 
 
 class QuasiNewtonLearner:
-    """inc/QuasiNewtonLearner.h: BuildFrom -> Finalize -> Init -> OptimizationStep*."""
+    """inc/QuasiNewtonLearner.h: BuildFrom -> Finalize -> Init -> OptimizationStep*.
+    optimizer="Hessian" gives the reference's HessianLearner (see HessianLearner)."""
 
     def __init__(self, device=0, optimizer="QuasiNewton"):
         h = C.c_void_p()
         check_host(load().wfsa_learner_create(_b(optimizer), device, C.byref(h)))
         self._h = h
         self._fsa = None
+        self.width = load().wfsa_learner_info_width(h)   # values per info row
 
     def __del__(self):
         if getattr(self, "_h", None):
@@ -198,7 +200,7 @@ class QuasiNewtonLearner:
         check_host(load().wfsa_learner_init(self._h, flags, _ptr(x0)))
 
     def OptimizationStep(self, eta=1.0, tol=1e-6):
-        info = np.zeros(7, dtype=np.float64)
+        info = np.zeros(self.width, dtype=np.float64)
         halt = C.c_int32()
         check_host(load().wfsa_learner_step(self._h, eta, tol, _ptr(info), C.byref(halt)))
         return info, bool(halt.value)
@@ -267,9 +269,16 @@ class QuasiNewtonLearner:
         self.Init(flags)
         return self.Run(epochs, eta, tol)
 
+    def result(self):
+        """GetOptimizationResult (the -eval line): KL, mxlogx(support),
+        LogModelVolume, LogAuxVolume, logdetHessian, LogDetAuxHessian, n-k, aux-1"""
+        out = np.zeros(8, dtype=np.float64)
+        check_host(load().wfsa_learner_result(self._h, _ptr(out)))
+        return out
+
     def Run(self, epochs, eta=1.0, tol=1e-6):
         """up to `epochs` OptimizationSteps in one native call (no Init)"""
-        rows = np.zeros((max(epochs, 0), 7))
+        rows = np.zeros((max(epochs, 0), self.width))
         done = C.c_int32(0)
         rc = load().wfsa_learner_run(self._h, eta, tol, int(epochs), _ptr(rows), C.byref(done))
         check_host(rc)
@@ -312,6 +321,12 @@ class Device:
         check_dev(load().wfsa_dev_recognize(self._h, _ptr(rec), _ptr(pc), _ptr(used)))
         return rec, pc, used[:self.n_params]
 
+    def string_tiers(self):
+        """per string: -1 compiled stream, 0/1 LDS traversal, 2 wide traversal, 3 dense"""
+        t = np.zeros(max(self.n_strings, 1), dtype=np.int8)
+        check_dev(load().wfsa_dev_string_tiers(self._h, _ptr(t)))
+        return t[:self.n_strings]
+
     def objective_grad(self, w_full, want_logq=True):
         w = np.ascontiguousarray(w_full, dtype=np.float64)
         grad = np.zeros(max(self.n_params, 1), dtype=np.float64)
@@ -333,6 +348,22 @@ class Device:
         check_dev(load().wfsa_dev_objective_grad_end(self._h, C.byref(ll), _ptr(grad), _ptr(logq)))
         return ll.value, grad[:self.n_params], logq
 
+    def hf_setup(self):
+        """pattern of the Hessian's second-order term: (j, k) Fsa parameter pairs"""
+        n = C.c_int64()
+        check_dev(load().wfsa_dev_hf_setup(self._h, C.byref(n)))
+        pairs = np.zeros(max(2 * n.value, 1), dtype=np.int32)
+        check_dev(load().wfsa_dev_hf_pairs(self._h, _ptr(pairs)))
+        self._hf_n = n.value
+        return pairs[:2 * n.value].reshape(-1, 2)
+
+    def hf_eval(self, w_full):
+        """sum_s p_s Cov_s(count_j, count_k) for the hf_setup pairs"""
+        w = np.ascontiguousarray(w_full, dtype=np.float64)
+        vals = np.zeros(max(self._hf_n, 1), dtype=np.float64)
+        check_dev(load().wfsa_dev_hf_eval(self._h, _ptr(w), _ptr(vals)))
+        return vals[:self._hf_n]
+
     def comm_init(self, nranks, rank, unique_id):
         buf = (C.c_uint8 * _lib.COMM_ID_BYTES).from_buffer_copy(bytes(unique_id))
         check_dev(load().wfsa_dev_comm_init(self._h, nranks, rank, buf))
@@ -352,3 +383,11 @@ class Device:
         s = _lib.DevStats()
         check_dev(load().wfsa_dev_get_stats(self._h, C.byref(s)))
         return {f: getattr(s, f) for f, _ in _lib.DevStats._fields_}
+
+
+class HessianLearner(QuasiNewtonLearner):
+    """inc/HessianLearner.h: the reference's default optimizer (augmented
+    Newton/KKT steps with the count covariance H_f from the device)."""
+
+    def __init__(self, device=0):
+        super().__init__(device, optimizer="Hessian")

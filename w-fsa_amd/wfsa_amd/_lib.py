@@ -65,6 +65,7 @@ _SIGS = {
     "wfsa_dev_load_model": (C.c_int, [vp, P(ModelDesc)]),
     "wfsa_dev_load_corpus": (C.c_int, [vp, vp, vp, vp, i64]),
     "wfsa_dev_recognize": (C.c_int, [vp, vp, vp, vp]),
+    "wfsa_dev_string_tiers": (C.c_int, [vp, vp]),
     "wfsa_dev_objective_grad": (C.c_int, [vp, vp, P(dbl), vp, vp]),
     "wfsa_dev_objective_grad_begin": (C.c_int, [vp, vp, C.c_int]),
     "wfsa_dev_objective_grad_end": (C.c_int, [vp, P(dbl), vp, vp]),
@@ -72,6 +73,9 @@ _SIGS = {
     "wfsa_dev_qn_set_state": (C.c_int, [vp, vp, vp]),
     "wfsa_dev_qn_get_state": (C.c_int, [vp, vp, vp, vp]),
     "wfsa_dev_qn_run": (C.c_int, [vp, dbl, dbl, i32, vp, P(i32), P(i32)]),
+    "wfsa_dev_hf_setup": (C.c_int, [vp, P(C.c_int64)]),
+    "wfsa_dev_hf_pairs": (C.c_int, [vp, vp]),
+    "wfsa_dev_hf_eval": (C.c_int, [vp, vp, vp]),
     "wfsa_dev_comm_unique_id": (C.c_int, [vp]),
     "wfsa_dev_comm_init": (C.c_int, [vp, C.c_int, C.c_int, vp]),
     "wfsa_dev_allreduce": (C.c_int, [vp, vp, i64]),
@@ -96,7 +100,9 @@ _SIGS = {
     "wfsa_learner_finalize": (C.c_int, [vp]),
     "wfsa_learner_info_get": (C.c_int, [vp, P(LearnerInfo)]),
     "wfsa_learner_init": (C.c_int, [vp, C.c_int, vp]),
+    "wfsa_learner_info_width": (C.c_int, [vp]),
     "wfsa_learner_step": (C.c_int, [vp, dbl, dbl, vp, P(i32)]),
+    "wfsa_learner_result": (C.c_int, [vp, vp]),
     "wfsa_learner_run": (C.c_int, [vp, dbl, dbl, i32, vp, P(i32)]),
     "wfsa_learner_objective_grad": (C.c_int, [vp, P(dbl), vp, vp]),
     "wfsa_learner_get_x": (C.c_int, [vp, vp]),
