@@ -125,6 +125,16 @@ int wfsa_dev_load_corpus(wfsa_dev* ctx, const uint8_t* sym, const int64_t* off,
 int wfsa_dev_recognize(wfsa_dev* ctx, uint8_t* recognized, double* path_count,
                        uint8_t* used_param);
 
+/* The rmin info column (QuasiNewtonLearner::GetOptimizationInfo,
+ * src/QuasiNewtonLearner.cpp:80-84; HessianLearner :313-317) at the weights
+ * of the last evaluation: *rmin = the smallest relative path probability
+ * exp(P x)_path / q_s over all paths of ambiguous strings (path count > 1),
+ * exact; *string_index = the loaded string holding that path (-1 when no
+ * string is ambiguous).  The reference reports the path's index in its BFS
+ * enumeration instead, which has no counterpart without enumerating paths.
+ * Not available on the dense path. */
+int wfsa_dev_rmin(wfsa_dev* ctx, double* rmin, int64_t* string_index);
+
 /* Where each loaded string runs (after compilation): tier[s] = -1 compiled
  * stream (trivial words + bubbles), 0 / 1 LDS-slab traversal, 2 wide
  * traversal (global scratch), 3 dense MFMA path. */
@@ -158,7 +168,7 @@ int wfsa_dev_objective_grad_end(wfsa_dev* ctx, double* loglik, double* grad_full
  *   qn_get_state: x, lambda and the last step's gradient (any may be NULL).
  *   qn_run:       up to max_steps steps; info_rows[7*s ..] gets step s's
  *                 GetOptimizationInfo row (KL, graderr, g_min, g_max, lambda_min,
- *                 0, 0); stops after the step whose HaltCondition(tol) holds
+ *                 rmin, rmin string -- both 0 unless info_rmin); stops after the step whose HaltCondition(tol) holds
  *                 (*status = 1) or whose info is not finite (*status = 2). */
 typedef struct {
     int32_t n_params;
@@ -167,6 +177,7 @@ typedef struct {
     const int32_t* ccol;       /* [n_params]                                 */
     double plogp;
     int32_t exponential_lambda;
+    int32_t info_rmin;         /* fill the rmin columns (wfsa_dev_rmin per step) */
 } wfsa_qn_desc;
 int wfsa_dev_qn_setup(wfsa_dev* ctx, const wfsa_qn_desc* desc);
 int wfsa_dev_qn_set_state(wfsa_dev* ctx, const double* x, const double* lambda);

@@ -168,6 +168,10 @@ def test_hessian_learner_epochs_match_restatement(case):
     np.testing.assert_allclose(got[:, 1:4], want[:, 1:4], rtol=1e-6, atol=1e-10)
     np.testing.assert_array_equal(got[:, 4:6], want[:, 4:6])
     np.testing.assert_allclose(got[:, 6], want[:, 6], rtol=1e-9, atol=1e-12)
+    # rmin: the value, and the string holding the reference's min path
+    np.testing.assert_allclose(got[:, 7], want[:, 7], rtol=1e-9, atol=1e-300)
+    strings = np.searchsorted(h.mrow, want[:, 8].astype(np.int64), side="right") - 1
+    np.testing.assert_array_equal(got[:, 8], np.where(h.unique, 0, strings))
     lrn.Renormalize()
     # same parameters, possibly another order: match them by name.  On a
     # singular Hessian (talk: a one-dimensional set of optima) the last Newton

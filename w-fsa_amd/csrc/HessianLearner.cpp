@@ -254,6 +254,7 @@ bool HessianLearner::AddHf(std::vector<double>& H, int64_t ld) {   // ComputeHf,
 void HessianLearner::OptimizationStep(double eta, bool) {   // :63-130
     ComputeRhs();
     ComputeObjective();
+    ComputeRmin(rmin);
     const int64_t n = int64_t(_x.size()), k = int64_t(lambda.size()), N = n + k;
     if (N > kMaxDense)
         throw LearnerError("HessianLearner: the augmented system has ", N, " unknowns; this build factors it densely "
@@ -308,6 +309,8 @@ std::vector<double> HessianLearner::GetOptimizationInfo() {
         r[5] = double(inertia_neg);
     }
     r[6] = lambda_min;
+    r[7] = rmin[0];   // :313-317 (index: the string holding the path, see QuasiNewtonLearner)
+    r[8] = rmin[1];
     return r;
 }
 

@@ -75,6 +75,7 @@ private:
     std::vector<double> hf_vals, w_hf;
     bool hf_ready = false, include_Hf = false, degenerate = false, exponential_lambda = false;
     double error = 0.0, lambda_min = 0.0;
+    double rmin[2] = {0.0, 0.0};   // rmin column at the step's x
     int64_t inertia_pos = 0, inertia_neg = 0;
 };
 

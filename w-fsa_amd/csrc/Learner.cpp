@@ -172,6 +172,23 @@ void Learner::BuildPaths(const Fsa& fsa, const uint8_t* sym, const int64_t* off,
     logq_valid = false;
 }
 
+bool Learner::RminAvailable() const {
+    if (unique_paths || nranks > 1 || !dev) return false;
+    wfsa_dev_stats st{};
+    if (wfsa_dev_get_stats(dev, &st) != WFSA_OK) return false;
+    return !st.dense;
+}
+
+void Learner::ComputeRmin(double* out) const {
+    out[0] = out[1] = 0.0;
+    if (!RminAvailable()) return;
+    double r = 0.0;
+    int64_t s = -1;
+    ThrowOnDevError(wfsa_dev_rmin(dev, &r, &s), "wfsa_dev_rmin");
+    out[0] = r;
+    out[1] = double(s);
+}
+
 // Learner::Trim (src/Learner.cpp:350-425) without the P matrix: a used
 // parameter alone in its constraint is fixed to log 1 (-1); the used ones
 // are renumbered, x and C follow.

@@ -76,6 +76,13 @@ public:
     int32_t GetNumberOfFullParameters() const { return n_full; }
 
     bool HasUniquePaths() const { return unique_paths; }
+    // the rmin info column (src/QuasiNewtonLearner.cpp:80-84): available with
+    // ambiguous strings on one rank off the dense path; otherwise (0, 0) as
+    // the reference reports for unique paths
+    bool RminAvailable() const;
+    // out[0] = smallest relative path probability at the last evaluation,
+    // out[1] = index of the string holding that path
+    void ComputeRmin(double* out) const;
     double GetKLDistance() const { return kl; }
     double gKLDistance() const { return kl + mxlogx(common_support); }
 

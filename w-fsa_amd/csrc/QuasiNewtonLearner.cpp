@@ -36,11 +36,13 @@ std::string QuasiNewtonLearner::GetOptimizationHeader() const {
     return "       KL   graderr     g_min     g_max lambdamin      rmin";
 }
 
-// [KL, graderr, g_min, g_max, lambda_min, rmin, rmin index].  The last two
-// (smallest relative path probability, src/QuasiNewtonLearner.cpp:80-84)
-// need an explicit path list and are reported as 0.
+// [KL, graderr, g_min, g_max, lambda_min, rmin, rmin index]: rmin is the
+// smallest relative path probability (src/QuasiNewtonLearner.cpp:80-84) at
+// the step's weights, from the device's (min, x) pass (wfsa_dev_rmin); its
+// index is the string holding that path (the reference's BFS path index has
+// no counterpart without enumerating paths).
 std::vector<double> QuasiNewtonLearner::GetOptimizationInfo() {
-    return {GetKLDistance(), grad_error, g_min, g_max, lambda_min, 0.0, 0.0};
+    return {GetKLDistance(), grad_error, g_min, g_max, lambda_min, rmin[0], rmin[1]};
 }
 
 bool QuasiNewtonLearner::HaltCondition(double tol) {   // :88-91
@@ -88,6 +90,7 @@ void QuasiNewtonLearner::OptimizationStep(double eta, bool) {   // :162-201
     ComputeG();
     const auto t2 = clk::now();
     EndModeledProbs(grad_cache);
+    ComputeRmin(rmin);
     const auto t3 = clk::now();
     grad = grad_cache;
     ComputeObjective();
@@ -129,6 +132,7 @@ void QuasiNewtonLearner::RunDevice(double eta, double tol, int32_t max_epochs, d
     desc.ccol = Ccol.data();
     desc.plogp = GetPLogP();
     desc.exponential_lambda = exponential_lambda ? 1 : 0;
+    desc.info_rmin = RminAvailable() ? 1 : 0;
     auto check = [](int rc, const char* what) {
         if (rc != WFSA_OK) throw LearnerError(what, ": ", wfsa_dev_last_error());
     };
@@ -150,6 +154,8 @@ void QuasiNewtonLearner::RunDevice(double eta, double tol, int32_t max_epochs, d
         g_min = r[2];
         g_max = r[3];
         lambda_min = r[4];
+        rmin[0] = r[5];
+        rmin[1] = r[6];
         SetEvaluated(GetPLogP() - r[0]);
         grad_cache = grad;
         timing.steps += done;

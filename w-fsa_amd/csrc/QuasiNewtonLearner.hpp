@@ -44,6 +44,7 @@ protected:
 private:
     std::vector<double> grad, expx, lambda, g, rhs;
     double grad_error = 0, lambda_min = 0, g_min = 0, g_max = 0;
+    double rmin[2] = {0, 0};   // rmin column of the last step
     bool exponential_lambda = false;
     bool dev_qn_ready = false, dev_qn_exp = false;   // wfsa_dev_qn_setup done for this build
     Timing timing;

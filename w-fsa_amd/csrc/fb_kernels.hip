@@ -76,6 +76,16 @@ __device__ __forceinline__ void global_add(double* p, double v) {
     __hip_atomic_fetch_add(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// Doubles as order-preserving 64-bit keys (an LDS atomicMin on the key is a
+// min on the value): sign bit set -> all bits flipped, else the sign bit set.
+__device__ __forceinline__ unsigned long long okey(double d) {
+    const unsigned long long u = (unsigned long long)__double_as_longlong(d);
+    return (u >> 63) ? ~u : (u | 0x8000000000000000ull);
+}
+__device__ __forceinline__ double odec(unsigned long long k) {
+    return __longlong_as_double((long long)((k >> 63) ? (k & 0x7fffffffffffffffull) : ~k));
+}
+
 __device__ __forceinline__ double wave_max(double v) {
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) v = fmax(v, __shfl_xor(v, o, kWave));
@@ -250,7 +260,8 @@ __device__ bool compile_walk(const Slab& sl, const ModelView& m, int L, int sidx
 
 template <int MODE>
 __global__ __launch_bounds__(256) void trav_kernel(TravArgs a) {
-    constexpr bool COUNTING = MODE != MODE_WEIGHTED;
+    constexpr bool COUNTING = MODE == MODE_COUNT || MODE == MODE_EMIT;
+    constexpr bool MINM = MODE == MODE_MIN;   // beta holds the (min, x) forward as okey(log)
     if (a.halted && *a.halted) return;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int lane = lane_id();
@@ -278,7 +289,8 @@ __global__ __launch_bounds__(256) void trav_kernel(TravArgs a) {
 
     const ModelView& m = a.m;
     const int cap_f = a.slab.cap_f, cap_e = a.slab.cap_e;
-    const bool want_back = !COUNTING || a.used || a.c_main || MODE == MODE_EMIT;
+    const bool want_back = !MINM && (!COUNTING || a.used || a.c_main || MODE == MODE_EMIT);
+    unsigned long long* fkey = reinterpret_cast<unsigned long long*>(fbeta);
 
     for (int j = lane; j < m.n_nodes; j += kWave) st_rlx(&slot[j], -1);
     wave_sync();
@@ -295,7 +307,8 @@ __global__ __launch_bounds__(256) void trav_kernel(TravArgs a) {
         if (lane == 0) {
             fstate[0] = m.start;
             falpha[0] = 1.0;
-            fbeta[0] = 0.0;
+            if (MINM) fkey[0] = okey(0.0);
+            else fbeta[0] = 0.0;
             sl.fpos[0] = 0;
             sl.fpos[1] = 1;
             sl.epos[0] = 0;
@@ -320,9 +333,10 @@ __global__ __launch_bounds__(256) void trav_kernel(TravArgs a) {
                 const int f = fbase + lane;
                 const bool act = f < fe;
                 int lo = 0, cnt = 0;
-                double af = 0.0;
+                double af = 0.0, mf = 0.0;
                 if (act) {
                     af = falpha[f];
+                    if (MINM) mf = odec(fkey[f]);
                     edge_range(m, fstate[f], c, lo, cnt);
                 }
                 const int maxc = wave_max_i(cnt);
@@ -352,13 +366,15 @@ __global__ __launch_bounds__(256) void trav_kernel(TravArgs a) {
                         st_rlx(&slot[d], idx);
                         fstate[idx] = d;
                         falpha[idx] = 0.0;
-                        fbeta[idx] = 0.0;
+                        if (MINM) fkey[idx] = okey(INFINITY);
+                        else fbeta[idx] = 0.0;
                     }
                     nF += nwon;
                     wave_sync();
                     if (need) slv = ld_rlx(&slot[d]);
                     if (has) {
                         lds_add(&falpha[slv], v);
+                        if (MINM && m.ew[g] > 0.0) atomicMin(&fkey[slv], okey(mf + log(m.ew[g])));
                         const int k = nE + rank_below(hm);
                         sl.e_g[k] = g;
                         sl.e_src[k] = f;
@@ -418,6 +434,15 @@ __global__ __launch_bounds__(256) void trav_kernel(TravArgs a) {
         }
         const double lq = qh > 0.0 ? log(qh) + kLn2 * double(esum) : -INFINITY;
         const double ps = COUNTING ? 0.0 : a.p[sidx];
+        if (MINM) {
+            double mn = INFINITY;
+            for (int j = fl0 + lane; j < fl1; j += kWave) {
+                const double we = end_weight(m, fstate[j]);
+                if (we > 0.0) mn = fmin(mn, odec(fkey[j]) + log(we));
+            }
+            mn = -wave_max(-mn);
+            if (lane == 0) a.rmin_log[sidx] = qh > 0.0 ? mn - lq : INFINITY;
+        }
         if (lane == 0) {
             if (MODE == MODE_COUNT) {
                 if (a.path_count) a.path_count[sidx] = qh > 0.0 ? ldexp(qh, esum) : 0.0;
@@ -427,7 +452,7 @@ __global__ __launch_bounds__(256) void trav_kernel(TravArgs a) {
                 a.logq[sidx] = lq;
             }
         }
-        if (!COUNTING) ll_acc += ps * lq;
+        if (!COUNTING && !MINM) ll_acc += ps * lq;
         edges_acc += (unsigned long long)nE;
         if (!(qh > 0.0) || !want_back) continue;
 
@@ -490,7 +515,7 @@ __global__ __launch_bounds__(256) void trav_kernel(TravArgs a) {
     }
 
     if (lane == 0) {
-        if (!COUNTING) a.ll_part[gw] = ll_acc;
+        if (!COUNTING && !MINM) a.ll_part[gw] = ll_acc;
         if (a.live_edges && edges_acc) atomicAdd(a.live_edges, edges_acc);
     }
 }
@@ -522,7 +547,7 @@ __device__ __forceinline__ double block_max(double v, double* red) {
 // the destinations of byte c_i (the list D_c), so the forward writes exactly
 // D_c and the backward visits exactly those nodes; the rows are zeroed per
 // string because an in-edge gather reads arbitrary sources.
-template <bool COUNTING>
+template <bool COUNTING, bool MINM = false>
 __global__ __launch_bounds__(kWideBlock) void wide_kernel(WideArgs a) {
     if (a.halted && *a.halted) return;
     extern __shared__ __attribute__((aligned(16))) double gl[];   // [n_params] (weighted, grad_lds)
@@ -534,7 +559,7 @@ __global__ __launch_bounds__(kWideBlock) void wide_kernel(WideArgs a) {
     double* A = a.scratch + int64_t(blockIdx.x) * a.scratch_stride;
     double* B = A + (int64_t(a.max_len) + 1) * N;             // [2][N]
     int* dsc = reinterpret_cast<int*>(B + 2 * int64_t(N));    // [max_len + 2]
-    const bool lgrad = !COUNTING && a.grad_lds;
+    const bool lgrad = !COUNTING && !MINM && a.grad_lds;
     if (lgrad)
         for (int j = tid; j < m.n_params; j += kWideBlock) gl[j] = 0.0;
     double ll = 0.0;
@@ -557,6 +582,7 @@ __global__ __launch_bounds__(kWideBlock) void wide_kernel(WideArgs a) {
         if (tid == 0) {
             A[m.start] = 1.0;
             dsc[0] = 0;
+            if (MINM) B[m.start] = 0.0;   // (min, x) forward in log form, rolling over B's two rows
         }
         __syncthreads();
         bool alive = true;
@@ -572,6 +598,15 @@ __global__ __launch_bounds__(kWideBlock) void wide_kernel(WideArgs a) {
                     v += COUNTING ? Ai[W.e_src[e]] : Ai[W.e_src[e]] * m.ew[W.e_g[e]];
                 An[W.dst[k]] = v;
                 mx = fmax(mx, v);
+                if (MINM) {
+                    const double* Mi = B + int64_t(i & 1) * N;
+                    double mn = INFINITY;
+                    for (int e = W.e_ptr[k]; e < W.e_ptr[k + 1]; ++e) {
+                        const double we = m.ew[W.e_g[e]];
+                        if (Ai[W.e_src[e]] > 0.0 && we > 0.0) mn = fmin(mn, Mi[W.e_src[e]] + log(we));
+                    }
+                    B[int64_t((i + 1) & 1) * N + W.dst[k]] = mn;
+                }
             }
             mx = block_max(mx, red);
             if (!(mx > 0.0)) {
@@ -602,6 +637,19 @@ __global__ __launch_bounds__(kWideBlock) void wide_kernel(WideArgs a) {
         }
         const double lq = qh > 0.0 ? log(qh) + kLn2 * double(esum) : -INFINITY;
         const double ps = COUNTING ? 1.0 : a.p[sidx];
+        if (MINM) {
+            double mn = INFINITY;
+            if (alive)
+                for (int k = fr_begin(L) + tid; k < fr_end(L); k += kWideBlock) {
+                    const int S = fr_node(L, k);
+                    const double we = end_weight(m, S);
+                    if (A[int64_t(L) * N + S] > 0.0 && we > 0.0) mn = fmin(mn, B[int64_t(L & 1) * N + S] + log(we));
+                }
+            mn = -block_max(-mn, red);
+            if (tid == 0) a.rmin_log[sidx] = qh > 0.0 ? mn - lq : INFINITY;
+            __syncthreads();
+            continue;
+        }
         if (tid == 0) {
             if (COUNTING) {
                 if (a.path_count) a.path_count[sidx] = qh > 0.0 ? ldexp(qh, esum) : 0.0;
@@ -656,7 +704,7 @@ __global__ __launch_bounds__(kWideBlock) void wide_kernel(WideArgs a) {
             __syncthreads();
         }
     }
-    if (!COUNTING && tid == 0) a.ll_part[blockIdx.x] = ll;
+    if (!COUNTING && !MINM && tid == 0) a.ll_part[blockIdx.x] = ll;
     if (lgrad) {
         __syncthreads();
         for (int j = tid; j < m.n_params; j += kWideBlock)
@@ -1393,6 +1441,7 @@ __global__ void node_end_kernel(const int32_t* __restrict__ x_ptr, const double*
 
 hipError_t configure_kernels(int max_dynamic_lds) {
     const void* fns[] = {reinterpret_cast<const void*>(&trav_kernel<MODE_WEIGHTED>),
+                         reinterpret_cast<const void*>(&trav_kernel<MODE_MIN>),
                          reinterpret_cast<const void*>(&trav_kernel<MODE_COUNT>),
                          reinterpret_cast<const void*>(&trav_kernel<MODE_EMIT>),
                          reinterpret_cast<const void*>(&fbc_kernel<0, false, true>),
@@ -1438,7 +1487,106 @@ hipError_t launch_trav(TravMode mode, const TravArgs& a, int grid, hipStream_t s
         case MODE_EMIT:
             hipLaunchKernelGGL(trav_kernel<MODE_EMIT>, dim3(unsigned(grid)), block, lds, stream, a);
             break;
+        case MODE_MIN:
+            hipLaunchKernelGGL(trav_kernel<MODE_MIN>, dim3(unsigned(grid)), block, lds, stream, a);
+            break;
     }
+    return hipGetLastError();
+}
+
+// rmin column (fb_kernels.hpp RminArgs).  Lane per bubble: sum forward and
+// (min, x) forward in log form over the bubble's topologically listed edges.
+__global__ __launch_bounds__(256) void rmin_bubble_kernel(RminArgs a) {
+    if (a.halted && *a.halted) return;
+    const int b = int(blockIdx.x) * int(blockDim.x) + int(threadIdx.x);
+    if (b >= a.n_bub) return;
+    const int32_t* rec = a.bub + a.bub_off[b];
+    const int nodes = rec[0] & 0xffff, edges = rec[0] >> 16;
+    double A[kMaxBubbleNodes], M[kMaxBubbleNodes];
+    for (int v = 0; v < kMaxBubbleNodes; ++v) {
+        A[v] = v == 0 ? 1.0 : 0.0;
+        M[v] = v == 0 ? 0.0 : INFINITY;
+    }
+    for (int e = 0; e < edges; ++e) {
+        const int code = rec[4 + 2 * e], sd = rec[5 + 2 * e];
+        double wgt;
+        if (code >= 0) {
+            wgt = a.ewp[code];
+        } else {
+            const int g = -code - 2;
+            double t = 0.0;
+            for (int q = a.m.pptr[g]; q < a.m.pptr[g + 1]; ++q) t += a.w[a.m.pidx[q]];
+            wgt = exp(t);
+        }
+        const int src = sd & 0xffff, dst = sd >> 16;
+        A[dst] += A[src] * wgt;
+        if (wgt > 0.0) M[dst] = fmin(M[dst], M[src] + log(wgt));
+    }
+    a.vb[b] = M[nodes - 1] - log(A[nodes - 1]);
+}
+
+// the lane of a string's first bubble sums the string's run, in order
+__global__ __launch_bounds__(256) void rmin_segment_kernel(RminArgs a) {
+    if (a.halted && *a.halted) return;
+    const int b = int(blockIdx.x) * int(blockDim.x) + int(threadIdx.x);
+    if (b >= a.n_bub) return;
+    const int str = a.bub[a.bub_off[b] + 1];
+    if (b > 0 && a.bub[a.bub_off[b - 1] + 1] == str) return;
+    double t = 0.0;
+    for (int c = b; c < a.n_bub && a.bub[a.bub_off[c] + 1] == str; ++c) t += a.vb[c];
+    a.rmin_log[str] = t;
+}
+
+// (value, index) minimum, ties to the lower index
+__device__ __forceinline__ void min_pair(double& v, double& i, double v2, double i2) {
+    if (v2 < v || (v2 == v && i2 < i)) {
+        v = v2;
+        i = i2;
+    }
+}
+
+__global__ __launch_bounds__(256) void rmin_reduce_kernel(RminArgs a) {
+    if (a.halted && *a.halted) return;
+    __shared__ double sv[256 / kWave], si[256 / kWave];
+    double v = INFINITY, idx = -1.0;
+    for (int64_t s = int64_t(blockIdx.x) * 256 + threadIdx.x; s < a.n_strings; s += int64_t(gridDim.x) * 256)
+        if (a.pcount[s] > 1.5) min_pair(v, idx, a.rmin_log[s], double(s));
+    for (int o = 32; o > 0; o >>= 1) min_pair(v, idx, __shfl_xor(v, o, 64), __shfl_xor(idx, o, 64));
+    const int w = int(threadIdx.x) >> 6;
+    if ((threadIdx.x & 63) == 0) {
+        sv[w] = v;
+        si[w] = idx;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        for (int k = 1; k < 256 / kWave; ++k) min_pair(v, idx, sv[k], si[k]);
+        a.part[2 * blockIdx.x] = v;
+        a.part[2 * blockIdx.x + 1] = idx;
+    }
+}
+
+__global__ __launch_bounds__(64) void rmin_final_kernel(RminArgs a) {
+    if (a.halted && *a.halted) return;
+    double v = INFINITY, idx = -1.0;
+    for (int k = int(threadIdx.x); k < kRminBlocks; k += 64) min_pair(v, idx, a.part[2 * k], a.part[2 * k + 1]);
+    for (int o = 32; o > 0; o >>= 1) min_pair(v, idx, __shfl_xor(v, o, 64), __shfl_xor(idx, o, 64));
+    if (threadIdx.x == 0) {
+        a.res[0] = idx >= 0.0 ? exp(v) : 0.0;
+        a.res[1] = idx;
+    }
+}
+
+hipError_t launch_rmin_bubbles(const RminArgs& a, hipStream_t stream) {
+    if (a.n_bub == 0) return hipSuccess;
+    const unsigned g = unsigned((a.n_bub + 255) / 256);
+    hipLaunchKernelGGL(rmin_bubble_kernel, dim3(g), dim3(256), 0, stream, a);
+    hipLaunchKernelGGL(rmin_segment_kernel, dim3(g), dim3(256), 0, stream, a);
+    return hipGetLastError();
+}
+
+hipError_t launch_rmin_reduce(const RminArgs& a, hipStream_t stream) {
+    hipLaunchKernelGGL(rmin_reduce_kernel, dim3(kRminBlocks), dim3(256), 0, stream, a);
+    hipLaunchKernelGGL(rmin_final_kernel, dim3(1), dim3(64), 0, stream, a);
     return hipGetLastError();
 }
 
@@ -1451,9 +1599,11 @@ hipError_t launch_hf(const HfArgs& a, hipStream_t stream) {
     return hipGetLastError();
 }
 
-hipError_t launch_wide(bool counting, const WideArgs& a, int grid, hipStream_t stream) {
-    const size_t lds = (!counting && a.grad_lds) ? size_t(a.m.n_params) * sizeof(double) : 0;
-    if (counting)
+hipError_t launch_wide(bool counting, const WideArgs& a, int grid, hipStream_t stream, bool min_mode) {
+    const size_t lds = (!counting && !min_mode && a.grad_lds) ? size_t(a.m.n_params) * sizeof(double) : 0;
+    if (min_mode)
+        hipLaunchKernelGGL((wide_kernel<false, true>), dim3(unsigned(grid)), dim3(kWideBlock), 0, stream, a);
+    else if (counting)
         hipLaunchKernelGGL(wide_kernel<true>, dim3(unsigned(grid)), dim3(kWideBlock), 0, stream, a);
     else
         hipLaunchKernelGGL(wide_kernel<false>, dim3(unsigned(grid)), dim3(kWideBlock), lds, stream, a);

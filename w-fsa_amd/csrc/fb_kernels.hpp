@@ -108,7 +108,9 @@ inline SlabLayout slab_layout(int32_t cap_f, int32_t cap_e, int32_t max_len, int
     return l;
 }
 
-enum TravMode { MODE_WEIGHTED = 0, MODE_COUNT = 1, MODE_EMIT = 2 };
+// MODE_MIN: the weighted forward plus the (min, x) forward of the rmin info
+// column -- log(min path weight / q) per string into rmin_log, no backward.
+enum TravMode { MODE_WEIGHTED = 0, MODE_COUNT = 1, MODE_EMIT = 2, MODE_MIN = 3 };
 
 struct TravArgs {
     ModelView m;
@@ -141,6 +143,7 @@ struct TravArgs {
     uint8_t* overflow;       // [S] string did not fit the slab
     unsigned long long* live_edges;
     const unsigned* halted;  // device-resident QN run: nonzero = skip (or null)
+    double* rmin_log;        // min mode: [S] log of the string's smallest relative path probability
 };
 
 // Tier 2 of the traversal: strings whose trellis overflows every LDS slab
@@ -177,12 +180,42 @@ struct WideArgs {
     uint8_t* recognized;
     uint8_t* used;
     const unsigned* halted;
+    double* rmin_log;        // min mode: [S] log(min path weight / q)
 };
 // doubles of scratch per block
 inline int64_t wide_scratch_stride(int32_t max_len, int32_t n_nodes) {
     return (int64_t(max_len) + 3) * int64_t(n_nodes) + (int64_t(max_len) + 3) / 2 + 2;
 }
-hipError_t launch_wide(bool counting, const WideArgs& a, int grid, hipStream_t stream);
+hipError_t launch_wide(bool counting, const WideArgs& a, int grid, hipStream_t stream, bool min_mode = false);
+
+// The rmin info column (QuasiNewtonLearner::GetOptimizationInfo,
+// src/QuasiNewtonLearner.cpp:80-84; HessianLearner :313-317): the smallest
+// relative path probability min_paths exp(P x)_path / q_s over every string.
+// A compiled string's path posterior factors over its bubbles, so its
+// smallest one is the product of each bubble's smallest (min, x) path over
+// the bubble's sum: rmin_bubble_kernel (lane per bubble) writes
+// log(min path / Z) per bubble, rmin_segment_kernel sums each string's run
+// of bubbles in order (deterministic, no atomics); traversal strings come
+// from trav_kernel<MODE_MIN> / wide_kernel min mode; rmin_reduce takes the
+// minimum over ambiguous strings (path count > 1), ties to the lower index.
+struct RminArgs {
+    ModelView m;
+    const int32_t* bub;
+    const int32_t* bub_off;  // [n_bub]
+    int32_t n_bub;
+    const double* w;         // [n_params + 1] weights (multi-parameter edges)
+    const double* ewp;       // [n_params + 1] exp(w)
+    double* vb;              // [n_bub] log(min path / Z) per bubble
+    double* rmin_log;        // [S]
+    const double* pcount;    // [S] path counts (structural pass)
+    int64_t n_strings;
+    double* part;            // [kRminBlocks][2]
+    double* res;             // [2]: rmin, string index (-1: no ambiguous string)
+    const unsigned* halted;
+};
+constexpr int kRminBlocks = 256;
+hipError_t launch_rmin_bubbles(const RminArgs& a, hipStream_t stream);
+hipError_t launch_rmin_reduce(const RminArgs& a, hipStream_t stream);
 
 // Second-order term of the Hessian (HessianLearner::ComputeHf,
 // src/HessianLearner.cpp:498-547): sum_s p_s Cov_s(count_j, count_k).  The
@@ -250,6 +283,7 @@ struct QnArgs {
     unsigned* seq;               // device sequence counter
     unsigned* host_flag;         // host-mapped completion flag
     double* host_ring;           // host-mapped [slots][kQnRow]
+    const double* rmin;          // [2] the step's rmin column (rmin, string index), or null (0, 0)
 };
 
 // Bubble evaluation.  Contributions (-p_s x edge posterior) go straight to

@@ -50,6 +50,10 @@ __device__ inline void qn_finish_wave(const QnArgs& a) {
             info[2] = gmin;
             info[3] = gmax;
             info[4] = lmin;
+            if (a.rmin) {
+                info[5] = a.rmin[0];
+                info[6] = a.rmin[1];
+            }
             bool finite = true;
             for (int i = 0; i < 7; ++i) finite = finite && isfinite(info[i]);
             const bool halt = gerr <= a.tol && fabs(gmin) <= a.tol && fabs(gmax) <= a.tol;

@@ -205,6 +205,11 @@ struct wfsa_dev {
 
     DevBuf<double> gpart;        // per-block partial gradients of the compiled kernel
 
+    // rmin info column: per-bubble / per-string logs, block partials, results
+    // (two halves: a QN step's finish reads its own while the next step writes)
+    DevBuf<double> rm_vb, rm_rs, rm_part, rm_res;
+    bool qn_rmin = false;        // the device QN loop fills the rmin columns
+
     // the per-iteration device sequence, captured once per prepared corpus
     hipGraph_t graph = nullptr;
     hipGraphExec_t graph_exec = nullptr;
@@ -1160,6 +1165,51 @@ int enqueue_evaluation(wfsa_dev* ctx, bool want_logq, const unsigned* halted, in
     return WFSA_OK;
 }
 
+// The rmin column at the weights of the evaluation just enqueued (w_full,
+// ewp and the per-edge weights on the device): bubbles, then the traversal
+// tiers in min mode, then the reduction into res[0..1].
+int enqueue_rmin(wfsa_dev* ctx, const unsigned* halted, double* res) {
+    hipStream_t s = ctx->stream;
+    const size_t S = size_t(std::max<int64_t>(ctx->n_strings, 1));
+    if (ctx->rm_rs.n < S) HIP_TRY(ctx->rm_rs.alloc(S));
+    if (ctx->rm_vb.n < size_t(std::max(ctx->n_bubbles, 1))) HIP_TRY(ctx->rm_vb.alloc(size_t(std::max(ctx->n_bubbles, 1))));
+    if (ctx->rm_part.n < size_t(2 * wfsa::kRminBlocks)) HIP_TRY(ctx->rm_part.alloc(size_t(2 * wfsa::kRminBlocks)));
+    wfsa::RminArgs r{};
+    r.m = model_view(ctx);
+    r.bub = ctx->bub.ptr;
+    r.bub_off = ctx->bub_off.ptr;
+    r.n_bub = ctx->n_bubbles;
+    r.w = ctx->w_full.ptr;
+    r.ewp = ctx->ewp.ptr;
+    r.vb = ctx->rm_vb.ptr;
+    r.rmin_log = ctx->rm_rs.ptr;
+    r.pcount = ctx->pcount.ptr;
+    r.n_strings = ctx->n_strings;
+    r.part = ctx->rm_part.ptr;
+    r.res = res;
+    r.halted = halted;
+    HIP_TRY(wfsa::launch_rmin_bubbles(r, s));
+    for (int t = 0; t < 2; ++t) {
+        if (!ctx->n_fall[t]) continue;
+        wfsa::TravArgs a = trav_args(ctx, t);
+        a.list = ctx->fall[t].ptr;
+        a.n_list = ctx->n_fall[t];
+        a.rmin_log = ctx->rm_rs.ptr;
+        a.halted = halted;
+        HIP_TRY(wfsa::launch_trav(wfsa::MODE_MIN, a, ctx->fall_grid[t], s));
+    }
+    if (ctx->n_fall[2]) {
+        wfsa::WideArgs a = wide_args(ctx);
+        a.list = ctx->fall[2].ptr;
+        a.n_list = ctx->n_fall[2];
+        a.rmin_log = ctx->rm_rs.ptr;
+        a.halted = halted;
+        HIP_TRY(wfsa::launch_wide(false, a, ctx->fall_grid[2], s, true));
+    }
+    HIP_TRY(wfsa::launch_rmin_reduce(r, s));
+    return WFSA_OK;
+}
+
 // One objective/gradient evaluation for the host: weights staged from the
 // host-mapped buffer, the evaluation, and -- without a communicator -- the
 // results published (with one, _begin all-reduces first).
@@ -1230,6 +1280,11 @@ int enqueue_qn_step(wfsa_dev* ctx, double eta, double tol, int64_t e, bool timed
     q.seq = ctx->counters.ptr;
     q.host_flag = ctx->flag_dev;
     q.host_ring = ctx->qn_ring_dev;
+    if (ctx->qn_rmin) {
+        double* res = ctx->rm_res.ptr + 2 * par;
+        if (int rc = enqueue_rmin(ctx, ctx->qn_halted.ptr, res)) return rc;
+        q.rmin = res;
+    }
     HIP_TRY(wfsa::launch_qn_update(q, s));
     *q_out = q;
     return WFSA_OK;
@@ -1537,6 +1592,22 @@ int wfsa_dev_recognize(wfsa_dev* ctx, uint8_t* recognized, double* path_count, u
     return WFSA_OK;
 }
 
+int wfsa_dev_rmin(wfsa_dev* ctx, double* rmin, int64_t* string_index) {
+    if (int rc = check_ctx(ctx)) return rc;
+    if (!ctx->has_model || !ctx->has_corpus) return fail(WFSA_ERR_ARG, "load a model and a corpus first");
+    if (ctx->in_flight) return fail(WFSA_ERR_ARG, "an evaluation is in flight");
+    if (ctx->dense) return fail(WFSA_ERR_CAPACITY, "rmin: not available on the dense path");
+    if (ctx->prep_level < 2) return fail(WFSA_ERR_ARG, "rmin: evaluate the objective first");
+    if (ctx->rm_res.n < 4) HIP_TRY(ctx->rm_res.alloc(4));
+    if (int rc = enqueue_rmin(ctx, nullptr, ctx->rm_res.ptr)) return rc;
+    double h[2];
+    HIP_TRY(ctx->rm_res.download(h, 2, ctx->stream));
+    HIP_TRY(hipStreamSynchronize(ctx->stream));
+    if (rmin) *rmin = h[0];
+    if (string_index) *string_index = int64_t(h[1]);
+    return WFSA_OK;
+}
+
 int wfsa_dev_string_tiers(wfsa_dev* ctx, int8_t* tier) {
     if (int rc = check_ctx(ctx)) return rc;
     if (!ctx->has_model || !ctx->has_corpus) return fail(WFSA_ERR_ARG, "load a model and a corpus first");
@@ -1665,6 +1736,10 @@ int wfsa_dev_qn_setup(wfsa_dev* ctx, const wfsa_qn_desc* d) {
     ctx->qn_k = k;
     ctx->qn_plogp = d->plogp;
     ctx->qn_exp_lambda = d->exponential_lambda ? 1 : 0;
+    if (d->info_rmin && (ctx->dense || ctx->comm))
+        return fail(WFSA_ERR_CAPACITY, "the rmin column is not available on the dense path or with a communicator");
+    ctx->qn_rmin = d->info_rmin != 0;
+    if (ctx->qn_rmin) HIP_TRY(ctx->rm_res.alloc(4));
     ctx->qn_ready = true;
     return WFSA_OK;
 }

@@ -364,6 +364,13 @@ class Device:
         check_dev(load().wfsa_dev_hf_eval(self._h, _ptr(w), _ptr(vals)))
         return vals[:self._hf_n]
 
+    def rmin(self):
+        """(smallest relative path probability, string holding it) at the
+        weights of the last objective_grad; string -1 when none is ambiguous"""
+        r, i = C.c_double(), C.c_int64()
+        check_dev(load().wfsa_dev_rmin(self._h, C.byref(r), C.byref(i)))
+        return r.value, i.value
+
     def comm_init(self, nranks, rank, unique_id):
         buf = (C.c_uint8 * _lib.COMM_ID_BYTES).from_buffer_copy(bytes(unique_id))
         check_dev(load().wfsa_dev_comm_init(self._h, nranks, rank, buf))

@@ -66,6 +66,7 @@ _SIGS = {
     "wfsa_dev_load_corpus": (C.c_int, [vp, vp, vp, vp, i64]),
     "wfsa_dev_recognize": (C.c_int, [vp, vp, vp, vp]),
     "wfsa_dev_string_tiers": (C.c_int, [vp, vp]),
+    "wfsa_dev_rmin": (C.c_int, [vp, vp, vp]),
     "wfsa_dev_objective_grad": (C.c_int, [vp, vp, P(dbl), vp, vp]),
     "wfsa_dev_objective_grad_begin": (C.c_int, [vp, vp, C.c_int]),
     "wfsa_dev_objective_grad_end": (C.c_int, [vp, P(dbl), vp, vp]),
