@@ -1494,50 +1494,8 @@ hipError_t launch_trav(TravMode mode, const TravArgs& a, int grid, hipStream_t s
     return hipGetLastError();
 }
 
-// rmin column (fb_kernels.hpp RminArgs).  Lane per bubble: sum forward and
-// (min, x) forward in log form over the bubble's topologically listed edges.
-__global__ __launch_bounds__(256) void rmin_bubble_kernel(RminArgs a) {
-    if (a.halted && *a.halted) return;
-    const int b = int(blockIdx.x) * int(blockDim.x) + int(threadIdx.x);
-    if (b >= a.n_bub) return;
-    const int32_t* rec = a.bub + a.bub_off[b];
-    const int nodes = rec[0] & 0xffff, edges = rec[0] >> 16;
-    double A[kMaxBubbleNodes], M[kMaxBubbleNodes];
-    for (int v = 0; v < kMaxBubbleNodes; ++v) {
-        A[v] = v == 0 ? 1.0 : 0.0;
-        M[v] = v == 0 ? 0.0 : INFINITY;
-    }
-    for (int e = 0; e < edges; ++e) {
-        const int code = rec[4 + 2 * e], sd = rec[5 + 2 * e];
-        double wgt;
-        if (code >= 0) {
-            wgt = a.ewp[code];
-        } else {
-            const int g = -code - 2;
-            double t = 0.0;
-            for (int q = a.m.pptr[g]; q < a.m.pptr[g + 1]; ++q) t += a.w[a.m.pidx[q]];
-            wgt = exp(t);
-        }
-        const int src = sd & 0xffff, dst = sd >> 16;
-        A[dst] += A[src] * wgt;
-        if (wgt > 0.0) M[dst] = fmin(M[dst], M[src] + log(wgt));
-    }
-    a.vb[b] = M[nodes - 1] - log(A[nodes - 1]);
-}
-
-// the lane of a string's first bubble sums the string's run, in order
-__global__ __launch_bounds__(256) void rmin_segment_kernel(RminArgs a) {
-    if (a.halted && *a.halted) return;
-    const int b = int(blockIdx.x) * int(blockDim.x) + int(threadIdx.x);
-    if (b >= a.n_bub) return;
-    const int str = a.bub[a.bub_off[b] + 1];
-    if (b > 0 && a.bub[a.bub_off[b - 1] + 1] == str) return;
-    double t = 0.0;
-    for (int c = b; c < a.n_bub && a.bub[a.bub_off[c] + 1] == str; ++c) t += a.vb[c];
-    a.rmin_log[str] = t;
-}
-
-// (value, index) minimum, ties to the lower index
+// rmin column (fb_kernels.hpp RminArgs).  (value, index) minimum, ties to
+// the lower index.
 __device__ __forceinline__ void min_pair(double& v, double& i, double v2, double i2) {
     if (v2 < v || (v2 == v && i2 < i)) {
         v = v2;
@@ -1545,48 +1503,99 @@ __device__ __forceinline__ void min_pair(double& v, double& i, double v2, double
     }
 }
 
-__global__ __launch_bounds__(256) void rmin_reduce_kernel(RminArgs a) {
+// Lane per bubble, 64-lane blocks: sum forward and (min, x) forward over the
+// bubble's topologically listed edges with the node vectors in LDS
+// ([node][lane], conflict-free); the min path never exceeds the sum, so both
+// stay linear and one log per bubble gives vb = log(min path / Z).
+__global__ __launch_bounds__(64) void rmin_bubble_kernel(RminArgs a) {
     if (a.halted && *a.halted) return;
-    __shared__ double sv[256 / kWave], si[256 / kWave];
+    __shared__ double sA[kMaxBubbleNodes][64], sM[kMaxBubbleNodes][64];
+    const int lane = int(threadIdx.x);
+    const int b = int(blockIdx.x) * 64 + lane;
+    if (b >= a.n_bub) return;
+    const int32_t* rec = a.bub + a.bub_off[b];
+    const int nodes = rec[0] & 0xffff, edges = rec[0] >> 16;
+    for (int u = 0; u < nodes; ++u) {
+        sA[u][lane] = u == 0 ? 1.0 : 0.0;
+        sM[u][lane] = u == 0 ? 1.0 : INFINITY;
+    }
+    const int2* ed = reinterpret_cast<const int2*>(rec + 4);   // (code, src | dst << 16), 8-byte aligned
+    for (int e = 0; e < edges; ++e) {
+        const int2 cs = ed[e];
+        double wgt;
+        if (cs.x >= 0) {
+            wgt = a.ewp[cs.x];
+        } else {
+            const int g = -cs.x - 2;
+            double t = 0.0;
+            for (int q = a.m.pptr[g]; q < a.m.pptr[g + 1]; ++q) t += a.w[a.m.pidx[q]];
+            wgt = exp(t);
+        }
+        const int src = cs.y & 0xffff, dst = cs.y >> 16;
+        sA[dst][lane] += sA[src][lane] * wgt;
+        if (wgt > 0.0) sM[dst][lane] = fmin(sM[dst][lane], sM[src][lane] * wgt);
+    }
+    a.vb[b] = log(sM[nodes - 1][lane] / sA[nodes - 1][lane]);
+}
+
+// Lane per ambiguous string: a compiled string sums its run of bubbles in
+// order (deterministic), a traversal string's value is already in rmin_log;
+// block minima to part[].
+__global__ __launch_bounds__(kRminBlock) void rmin_strings_kernel(RminArgs a) {
+    if (a.halted && *a.halted) return;
+    __shared__ double wv[kRminBlock / kWave], wi[kRminBlock / kWave];
+    const int lane = int(threadIdx.x);
+    const int64_t i = int64_t(blockIdx.x) * kRminBlock + lane;
     double v = INFINITY, idx = -1.0;
-    for (int64_t s = int64_t(blockIdx.x) * 256 + threadIdx.x; s < a.n_strings; s += int64_t(gridDim.x) * 256)
-        if (a.pcount[s] > 1.5) min_pair(v, idx, a.rmin_log[s], double(s));
+    if (i < a.n_amb) {
+        const int4 ent = a.amb[i];   // (string, first bubble, bubble count or -1, 0)
+        double r = 0.0;
+        if (ent.z < 0) r = a.rmin_log[ent.x];
+        else
+            for (int b = ent.y; b < ent.y + ent.z; ++b) r += a.vb[b];
+        v = r;
+        idx = double(ent.x);
+    }
     for (int o = 32; o > 0; o >>= 1) min_pair(v, idx, __shfl_xor(v, o, 64), __shfl_xor(idx, o, 64));
-    const int w = int(threadIdx.x) >> 6;
-    if ((threadIdx.x & 63) == 0) {
-        sv[w] = v;
-        si[w] = idx;
+    if ((lane & 63) == 0) {
+        wv[lane >> 6] = v;
+        wi[lane >> 6] = idx;
     }
     __syncthreads();
-    if (threadIdx.x == 0) {
-        for (int k = 1; k < 256 / kWave; ++k) min_pair(v, idx, sv[k], si[k]);
+    if (lane == 0) {
+        for (int k = 1; k < kRminBlock / kWave; ++k) min_pair(v, idx, wv[k], wi[k]);
         a.part[2 * blockIdx.x] = v;
         a.part[2 * blockIdx.x + 1] = idx;
     }
 }
 
-__global__ __launch_bounds__(64) void rmin_final_kernel(RminArgs a) {
+// the block minima -> res (a second launch: the kernel boundary orders the
+// partials; a device-scope fence per block costs an L2 write-back on gfx950)
+__global__ __launch_bounds__(256) void rmin_final_kernel(RminArgs a, int n_part) {
     if (a.halted && *a.halted) return;
+    __shared__ double wv[4], wi[4];
+    const int lane = int(threadIdx.x);
     double v = INFINITY, idx = -1.0;
-    for (int k = int(threadIdx.x); k < kRminBlocks; k += 64) min_pair(v, idx, a.part[2 * k], a.part[2 * k + 1]);
+    for (int k = lane; k < n_part; k += 256) min_pair(v, idx, a.part[2 * k], a.part[2 * k + 1]);
     for (int o = 32; o > 0; o >>= 1) min_pair(v, idx, __shfl_xor(v, o, 64), __shfl_xor(idx, o, 64));
-    if (threadIdx.x == 0) {
+    if ((lane & 63) == 0) {
+        wv[lane >> 6] = v;
+        wi[lane >> 6] = idx;
+    }
+    __syncthreads();
+    if (lane == 0) {
+        for (int k = 1; k < 4; ++k) min_pair(v, idx, wv[k], wi[k]);
         a.res[0] = idx >= 0.0 ? exp(v) : 0.0;
         a.res[1] = idx;
     }
 }
 
-hipError_t launch_rmin_bubbles(const RminArgs& a, hipStream_t stream) {
-    if (a.n_bub == 0) return hipSuccess;
-    const unsigned g = unsigned((a.n_bub + 255) / 256);
-    hipLaunchKernelGGL(rmin_bubble_kernel, dim3(g), dim3(256), 0, stream, a);
-    hipLaunchKernelGGL(rmin_segment_kernel, dim3(g), dim3(256), 0, stream, a);
-    return hipGetLastError();
-}
-
-hipError_t launch_rmin_reduce(const RminArgs& a, hipStream_t stream) {
-    hipLaunchKernelGGL(rmin_reduce_kernel, dim3(kRminBlocks), dim3(256), 0, stream, a);
-    hipLaunchKernelGGL(rmin_final_kernel, dim3(1), dim3(64), 0, stream, a);
+hipError_t launch_rmin(const RminArgs& a, hipStream_t stream) {
+    if (a.n_bub > 0)
+        hipLaunchKernelGGL(rmin_bubble_kernel, dim3(unsigned((a.n_bub + 63) / 64)), dim3(64), 0, stream, a);
+    const unsigned g = unsigned(std::max<int64_t>(1, (a.n_amb + kRminBlock - 1) / kRminBlock));
+    hipLaunchKernelGGL(rmin_strings_kernel, dim3(g), dim3(kRminBlock), 0, stream, a);
+    hipLaunchKernelGGL(rmin_final_kernel, dim3(1), dim3(256), 0, stream, a, int(g));
     return hipGetLastError();
 }
 

@@ -193,29 +193,28 @@ hipError_t launch_wide(bool counting, const WideArgs& a, int grid, hipStream_t s
 // relative path probability min_paths exp(P x)_path / q_s over every string.
 // A compiled string's path posterior factors over its bubbles, so its
 // smallest one is the product of each bubble's smallest (min, x) path over
-// the bubble's sum: rmin_bubble_kernel (lane per bubble) writes
-// log(min path / Z) per bubble, rmin_segment_kernel sums each string's run
-// of bubbles in order (deterministic, no atomics); traversal strings come
-// from trav_kernel<MODE_MIN> / wide_kernel min mode; rmin_reduce takes the
-// minimum over ambiguous strings (path count > 1), ties to the lower index.
+// the bubble's sum (rmin_bubble_kernel, lane per bubble); traversal strings
+// get log(min path / q) from trav_kernel<MODE_MIN> / wide_kernel min mode;
+// rmin_strings_kernel (lane per ambiguous string) sums each string's run and
+// takes the minimum, ties to the lower index; rmin_final_kernel merges the
+// block minima.
 struct RminArgs {
     ModelView m;
     const int32_t* bub;
     const int32_t* bub_off;  // [n_bub]
     int32_t n_bub;
+    double* vb;              // [n_bub] log(min path / Z) per bubble
     const double* w;         // [n_params + 1] weights (multi-parameter edges)
     const double* ewp;       // [n_params + 1] exp(w)
-    double* vb;              // [n_bub] log(min path / Z) per bubble
-    double* rmin_log;        // [S]
-    const double* pcount;    // [S] path counts (structural pass)
-    int64_t n_strings;
-    double* part;            // [kRminBlocks][2]
+    double* rmin_log;        // [S] traversal strings' values
+    const int4* amb;         // [n_amb] (string, first bubble, bubble count | -1 traversal, 0), ascending
+    int64_t n_amb;
+    double* part;            // [blocks][2]
     double* res;             // [2]: rmin, string index (-1: no ambiguous string)
     const unsigned* halted;
 };
-constexpr int kRminBlocks = 256;
-hipError_t launch_rmin_bubbles(const RminArgs& a, hipStream_t stream);
-hipError_t launch_rmin_reduce(const RminArgs& a, hipStream_t stream);
+constexpr int kRminBlock = 256;
+hipError_t launch_rmin(const RminArgs& a, hipStream_t stream);
 
 // Second-order term of the Hessian (HessianLearner::ComputeHf,
 // src/HessianLearner.cpp:498-547): sum_s p_s Cov_s(count_j, count_k).  The

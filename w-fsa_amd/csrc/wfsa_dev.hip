@@ -207,7 +207,11 @@ struct wfsa_dev {
 
     // rmin info column: per-bubble / per-string logs, block partials, results
     // (two halves: a QN step's finish reads its own while the next step writes)
-    DevBuf<double> rm_vb, rm_rs, rm_part, rm_res;
+    DevBuf<double> rm_rs, rm_vb, rm_part, rm_res;
+    DevBuf<int4> rm_amb;         // the ambiguous strings (path count > 1) with their bubble runs
+    std::vector<int32_t> h_bfirst, h_nbub;   // per string: first bubble ordinal, bubbles (compiled strings)
+    int64_t rm_n_amb = 0;
+    int rm_gen = -1;             // prep_gen the list was built for
     bool qn_rmin = false;        // the device QN loop fills the rmin columns
 
     // the per-iteration device sequence, captured once per prepared corpus
@@ -715,6 +719,8 @@ int prepare(wfsa_dev* ctx, int level) {
         bwords += h_bub[size_t(str)];
         nbub += h_nb[size_t(str)];
     }
+    ctx->h_bfirst = b_first;
+    ctx->h_nbub = h_nb;
     if (bwords >= (int64_t(1) << 31) - 2) return fail(WFSA_ERR_CAPACITY, "bubble buffer exceeds 2^31 words");
 
     // 3. emit the streams (same tier as counted)
@@ -1171,24 +1177,25 @@ int enqueue_evaluation(wfsa_dev* ctx, bool want_logq, const unsigned* halted, in
 int enqueue_rmin(wfsa_dev* ctx, const unsigned* halted, double* res) {
     hipStream_t s = ctx->stream;
     const size_t S = size_t(std::max<int64_t>(ctx->n_strings, 1));
-    if (ctx->rm_rs.n < S) HIP_TRY(ctx->rm_rs.alloc(S));
-    if (ctx->rm_vb.n < size_t(std::max(ctx->n_bubbles, 1))) HIP_TRY(ctx->rm_vb.alloc(size_t(std::max(ctx->n_bubbles, 1))));
-    if (ctx->rm_part.n < size_t(2 * wfsa::kRminBlocks)) HIP_TRY(ctx->rm_part.alloc(size_t(2 * wfsa::kRminBlocks)));
-    wfsa::RminArgs r{};
-    r.m = model_view(ctx);
-    r.bub = ctx->bub.ptr;
-    r.bub_off = ctx->bub_off.ptr;
-    r.n_bub = ctx->n_bubbles;
-    r.w = ctx->w_full.ptr;
-    r.ewp = ctx->ewp.ptr;
-    r.vb = ctx->rm_vb.ptr;
-    r.rmin_log = ctx->rm_rs.ptr;
-    r.pcount = ctx->pcount.ptr;
-    r.n_strings = ctx->n_strings;
-    r.part = ctx->rm_part.ptr;
-    r.res = res;
-    r.halted = halted;
-    HIP_TRY(wfsa::launch_rmin_bubbles(r, s));
+    if (ctx->rm_gen != ctx->prep_gen) {   // once per prepared corpus: the ambiguous strings
+        std::vector<double> pc(S);
+        HIP_TRY(ctx->pcount.download(pc.data(), size_t(ctx->n_strings), s));
+        HIP_TRY(hipStreamSynchronize(s));
+        std::vector<int4> amb;
+        for (int64_t i = 0; i < ctx->n_strings; ++i) {
+            if (!(pc[size_t(i)] > 1.5)) continue;
+            const bool comp = ctx->h_tier[size_t(i)] < 0;
+            amb.push_back(make_int4(int32_t(i), comp ? ctx->h_bfirst[size_t(i)] : 0, comp ? ctx->h_nbub[size_t(i)] : -1, 0));
+        }
+        ctx->rm_n_amb = int64_t(amb.size());
+        if (!amb.empty()) HIP_TRY(ctx->rm_amb.upload(amb.data(), amb.size(), s));
+        const size_t blocks = size_t(std::max<int64_t>(1, (ctx->rm_n_amb + wfsa::kRminBlock - 1) / wfsa::kRminBlock));
+        HIP_TRY(ctx->rm_part.alloc(2 * blocks));
+        HIP_TRY(ctx->rm_rs.alloc(S));
+        HIP_TRY(ctx->rm_vb.alloc(size_t(std::max(ctx->n_bubbles, 1))));
+        HIP_TRY(hipStreamSynchronize(s));   // amb is freed on return
+        ctx->rm_gen = ctx->prep_gen;
+    }
     for (int t = 0; t < 2; ++t) {
         if (!ctx->n_fall[t]) continue;
         wfsa::TravArgs a = trav_args(ctx, t);
@@ -1206,7 +1213,21 @@ int enqueue_rmin(wfsa_dev* ctx, const unsigned* halted, double* res) {
         a.halted = halted;
         HIP_TRY(wfsa::launch_wide(false, a, ctx->fall_grid[2], s, true));
     }
-    HIP_TRY(wfsa::launch_rmin_reduce(r, s));
+    wfsa::RminArgs r{};
+    r.m = model_view(ctx);
+    r.bub = ctx->bub.ptr;
+    r.bub_off = ctx->bub_off.ptr;
+    r.n_bub = ctx->n_bubbles;
+    r.vb = ctx->rm_vb.ptr;
+    r.w = ctx->w_full.ptr;
+    r.ewp = ctx->ewp.ptr;
+    r.rmin_log = ctx->rm_rs.ptr;
+    r.amb = ctx->rm_amb.ptr;
+    r.n_amb = ctx->rm_n_amb;
+    r.part = ctx->rm_part.ptr;
+    r.res = res;
+    r.halted = halted;
+    HIP_TRY(wfsa::launch_rmin(r, s));
     return WFSA_OK;
 }
 
