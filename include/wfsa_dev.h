@@ -125,19 +125,34 @@ int wfsa_dev_load_corpus(wfsa_dev* ctx, const uint8_t* sym, const int64_t* off,
 int wfsa_dev_recognize(wfsa_dev* ctx, uint8_t* recognized, double* path_count,
                        uint8_t* used_param);
 
+/* Matrix-file mode (Learner::LoadMatrices, src/Learner.cpp:125-199; main.cpp
+ * -m "<file"): instead of an automaton and strings, the path matrices the
+ * reference's BuildPaths builds.  P: n_paths x n_params CSR (prow[n_paths+1],
+ * pcol/pdata[prow[n_paths]], parameter counts); M: n_strings x n_paths CSR
+ * of ones (mrow[n_strings+1], mcol = path indices); p[n_strings].  Replaces
+ * any loaded model and corpus; objective_grad then takes w_full = x
+ * (n_params values, no trimming) and computes the reference's SpMV chain
+ * (logq = log M exp(P x), grad = -P^T (rpp (.) M^T p)); recognize reports
+ * the path counts of M and the parameters P uses; rmin reports the
+ * reference's path index.  Leave the mode with wfsa_dev_load_model. */
+int wfsa_dev_load_paths(wfsa_dev* ctx, int32_t n_params, int64_t n_paths, const int64_t* prow, const int32_t* pcol,
+                        const double* pdata, int64_t n_strings, const int64_t* mrow, const int64_t* mcol,
+                        const double* p);
+
 /* The rmin info column (QuasiNewtonLearner::GetOptimizationInfo,
  * src/QuasiNewtonLearner.cpp:80-84; HessianLearner :313-317) at the weights
  * of the last evaluation: *rmin = the smallest relative path probability
  * exp(P x)_path / q_s over all paths of ambiguous strings (path count > 1),
  * exact; *string_index = the loaded string holding that path (-1 when no
  * string is ambiguous).  The reference reports the path's index in its BFS
- * enumeration instead, which has no counterpart without enumerating paths.
- * Not available on the dense path. */
+ * enumeration instead, which has no counterpart without enumerating paths
+ * (in matrix-file mode, where paths are given, *string_index is that path
+ * index).  Not available on the dense path. */
 int wfsa_dev_rmin(wfsa_dev* ctx, double* rmin, int64_t* string_index);
 
 /* Where each loaded string runs (after compilation): tier[s] = -1 compiled
  * stream (trivial words + bubbles), 0 / 1 LDS-slab traversal, 2 wide
- * traversal (global scratch), 3 dense MFMA path. */
+ * traversal (global scratch), 3 dense MFMA path, 4 matrix-file mode. */
 int wfsa_dev_string_tiers(wfsa_dev* ctx, int8_t* tier);
 
 /* Per-iteration hot path.  w_full[n_params] = Learner::GetWeight(j)

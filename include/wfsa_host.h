@@ -68,6 +68,11 @@ int wfsa_learner_build(wfsa_learner* l, wfsa_fsa* fsa, wfsa_corpus* corpus);
 /* the same from packed strings + raw weights (renormalized here) */
 int wfsa_learner_build_packed(wfsa_learner* l, wfsa_fsa* fsa, const uint8_t* sym, const int64_t* off,
                               const double* weights, int64_t n_strings);
+/* Matrix-file mode: Learner::LoadMatrices / SaveMatrices (src/Learner.cpp:82-199),
+ * prefix.{C,M,P,prob,aux} in the reference's text CSR format; load replaces
+ * BuildFrom (no automaton); save works only for loaded matrices. */
+int wfsa_learner_load_matrices(wfsa_learner* l, const char* prefix);
+int wfsa_learner_save_matrices(wfsa_learner* l, const char* prefix);
 int wfsa_learner_finalize(wfsa_learner* l);                                 /* Learner::Finalize */
 int wfsa_learner_info_get(wfsa_learner* l, wfsa_learner_info* out);
 int wfsa_learner_init(wfsa_learner* l, int flags, const double* x0);       /* Learner::Init */

@@ -156,3 +156,25 @@ def test_hessian_restatement_covariance_is_gradient_derivative():
         gm = h.grad(h.modeled()[1])
         jac[:, k] = (gp - gm) / (2 * eps)
     np.testing.assert_allclose(hf, jac, atol=1e-8)
+
+
+def test_matrix_files_round_trip(tmp_path):
+    """the matrix-file writer (tests/matrix_io.py) and reader agree with the
+    oracle's path matrices (the files the -m mode loads)"""
+    from oracle import Oracle
+    from matrix_io import read_csr, write_matrices
+    o = Oracle.from_files(os.path.join(DATA, "test3.wfsa"), os.path.join(DATA, "test.corpus"))
+    prefix = str(tmp_path / "t3")
+    write_matrices(o, prefix)
+    prow, pcol, pdata, mrow = o.paths()
+    r, c, d = read_csr(prefix + ".P")
+    np.testing.assert_array_equal(r, prow)
+    np.testing.assert_array_equal(c, pcol)
+    np.testing.assert_array_equal(d, pdata)
+    r, c, _ = read_csr(prefix + ".M")
+    np.testing.assert_array_equal(r, mrow)
+    np.testing.assert_array_equal(c, np.arange(mrow[-1]))
+    r, c, _ = read_csr(prefix + ".C")
+    np.testing.assert_array_equal(c, o.ccol())
+    assert len(open(prefix + ".prob").read().split()) == o.info["n_strings"]
+    assert len(open(prefix + ".aux").read().split()) == 5

@@ -56,6 +56,7 @@ public:
     double ComputeLogDetHessian();
     const std::vector<double>& GetGradient() const { return grad; }
     const std::vector<double>& GetLambda() const { return lambda; }
+    std::vector<double> GetLagrangeMultipliers() const override { return lambda; }
     void SetLambda(const double* l) { lambda.assign(l, l + lambda.size()); }
 
 protected:

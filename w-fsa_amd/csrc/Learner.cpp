@@ -3,7 +3,10 @@
 #include <algorithm>
 #include <cmath>
 #include <limits>
+#include <fstream>
+#include <iomanip>
 #include <numeric>
+#include <sstream>
 
 namespace wfsa {
 
@@ -170,6 +173,135 @@ void Learner::BuildPaths(const Fsa& fsa, const uint8_t* sym, const int64_t* off,
     w_full.assign(size_t(n_full), 0.0);
     grad_full.assign(size_t(n_full), 0.0);
     logq_valid = false;
+}
+
+namespace {
+
+// ReadCsrMtx (src/Utils.cpp:184-202): a row per line, "col value" pairs
+// until the line stops parsing (a trailing half pair is dropped)
+void read_csr(std::istream& is, std::vector<double>& data, std::vector<int32_t>& rows, std::vector<int32_t>& cols) {
+    data.clear();
+    rows.clear();
+    cols.clear();
+    std::string line;
+    while (std::getline(is, line)) {
+        rows.push_back(int32_t(cols.size()));
+        std::istringstream iss(line);
+        int32_t c;
+        double d;
+        while (iss >> c >> d) {
+            cols.push_back(c);
+            data.push_back(d);
+        }
+    }
+    rows.push_back(int32_t(cols.size()));
+}
+
+// WriteCsrMtx (src/Utils.cpp:204-214)
+void write_csr(std::ostream& os, const std::vector<double>* data, const std::vector<int32_t>& rows,
+               const std::vector<int32_t>& cols) {
+    for (size_t r = 0; r + 1 < rows.size(); ++r) {
+        for (int32_t k = rows[r]; k < rows[r + 1]; ++k) os << cols[size_t(k)] << ' ' << (data ? (*data)[size_t(k)] : 1.0) << ' ';
+        os << '\n';
+    }
+}
+
+}  // namespace
+
+bool Learner::LoadMatrices(const std::string& prefix) {   // src/Learner.cpp:125-199
+    if (nranks > 1) throw LearnerError("matrix-file mode runs on one rank");
+    auto m = std::make_unique<Matrices>();
+    auto open = [&](const char* ext) {
+        std::ifstream ifs(prefix + ext);
+        if (!ifs) throw LearnerError("Unable to open \"", prefix + ext, "\"!");
+        return ifs;
+    };
+    {
+        auto ifs = open(".C");
+        read_csr(ifs, m->cdata, m->crow, m->ccol);
+    }
+    {
+        auto ifs = open(".M");
+        read_csr(ifs, m->mdata, m->mrow, m->mcol);
+    }
+    {
+        auto ifs = open(".P");
+        read_csr(ifs, m->pdata, m->prow, m->pcol);
+    }
+    std::vector<double> prob;
+    {
+        std::ifstream ifs(prefix + ".prob");
+        double v;
+        while (ifs >> v) prob.push_back(v);
+    }
+    {
+        auto ifs = open(".aux");
+        double cs, pl, mv, ah;
+        int64_t na;
+        if (!(ifs >> cs >> pl >> mv >> ah >> na)) throw LearnerError("Invalid data in \"", prefix + ".aux", "\"!");
+        common_support = cs;
+        plogp = pl;
+        model_volume = mv;
+        aux_hessian = ah;
+        auxiliary_parameters = na;
+    }
+    const int64_t n = int64_t(m->ccol.size());
+    const int64_t n_paths = int64_t(m->prow.size()) - 1, S = int64_t(prob.size());
+    if (S + 1 != int64_t(m->mrow.size())) throw LearnerError("Size mismatch: ", S + 1, " != ", m->mrow.size());
+    if (!m->pcol.empty() && *std::max_element(m->pcol.begin(), m->pcol.end()) >= n)
+        throw LearnerError("Size mismatch: more path indexes than parameters in the automaton!");
+    if (m->mcol.empty() || m->mcol.back() + 1 != n_paths) throw LearnerError("M cols != P rows");
+    for (size_t i = 1; i < m->ccol.size(); ++i)
+        if (m->ccol[i] < m->ccol[i - 1]) throw LearnerError("constraint columns must be non-decreasing");
+
+    Crow = m->crow;
+    Ccol = m->ccol;
+    p = prob;
+    _x.assign(size_t(n), 0.0);
+    n_full = int32_t(n);
+    trimmed_weights.resize(size_t(n));
+    std::iota(trimmed_weights.begin(), trimmed_weights.end(), 0);
+    n_strings_global = S;
+    n_paths_global = int64_t(m->mcol.size());
+    unique_paths = m->mrow.size() == m->mcol.size() + 1;   // Learner::HasUniquePaths (:585-588)
+    shard_begin = 0;
+    shard_end = S;
+    path_count_local.assign(size_t(S), 0.0);
+    recognized_local.assign(size_t(S), 1);
+    for (int64_t s = 0; s < S; ++s) path_count_local[size_t(s)] = double(m->mrow[size_t(s) + 1] - m->mrow[size_t(s)]);
+
+    EnsureDevice();
+    std::vector<int64_t> prow(m->prow.begin(), m->prow.end()), mrow(m->mrow.begin(), m->mrow.end()),
+        mcol(m->mcol.begin(), m->mcol.end());
+    ThrowOnDevError(wfsa_dev_load_paths(dev, int32_t(n), n_paths, prow.data(), m->pcol.data(), m->pdata.data(), S,
+                                        mrow.data(), mcol.data(), p.data()),
+                    "wfsa_dev_load_paths");
+    flat.reset();
+    w_full.assign(size_t(n), 0.0);
+    grad_full.assign(size_t(n), 0.0);
+    logq_valid = false;
+    matrices = std::move(m);
+    return true;
+}
+
+bool Learner::SaveMatrices(const std::string& prefix) const {   // src/Learner.cpp:82-123
+    if (!matrices) return false;   // no path matrices exist: this build never enumerates paths
+    auto put = [&](const char* ext, auto&& body) {
+        std::ofstream ofs(prefix + ext);
+        if (!ofs) return false;
+        ofs.precision(15);   // DBL_DIG
+        body(ofs);
+        return bool(ofs);
+    };
+    const Matrices& m = *matrices;
+    return put(".C", [&](std::ostream& o) { write_csr(o, nullptr, m.crow, m.ccol); }) &&
+           put(".M", [&](std::ostream& o) { write_csr(o, nullptr, m.mrow, m.mcol); }) &&
+           put(".P", [&](std::ostream& o) { write_csr(o, &m.pdata, m.prow, m.pcol); }) &&
+           put(".prob", [&](std::ostream& o) { for (double v : p) o << v << '\n'; }) &&
+           put(".aux", [&](std::ostream& o) {
+               o << common_support << '\n' << plogp << '\n' << model_volume << '\n' << aux_hessian << '\n'
+                 << auxiliary_parameters << '\n';
+           });
 }
 
 bool Learner::RminAvailable() const {

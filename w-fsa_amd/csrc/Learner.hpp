@@ -52,6 +52,16 @@ public:
     void BuildFromPacked(const Fsa& fsa, const uint8_t* sym, const int64_t* off, const double* weights,
                          int64_t n_strings);
 
+    // Matrix-file mode (src/Learner.cpp:82-199): LoadMatrices reads
+    // prefix.{C,M,P,prob,aux} in the reference's text CSR format
+    // (ReadCsrMtx, src/Utils.cpp:184-202) and hands P/M/p to the device
+    // (wfsa_dev_load_paths) instead of BuildFrom; throws LearnerError with the
+    // reference's messages.  SaveMatrices writes the same files -- possible
+    // only for matrices that were loaded: this build never enumerates paths.
+    bool LoadMatrices(const std::string& prefix);
+    bool SaveMatrices(const std::string& prefix) const;
+    bool FromMatrices() const { return matrices != nullptr; }
+
     void Renormalize();
     void RewriteWeights(Fsa& fsa) const;
     const double* GetWeights() const { return _x.data(); }
@@ -60,6 +70,8 @@ public:
     virtual std::string GetOptimizationHeader() const;
     virtual std::vector<double> GetOptimizationResult(bool verbose = false);
     virtual bool HaltCondition(double tol);
+    // the constraints' multipliers (the reference keeps them after x in _x)
+    virtual std::vector<double> GetLagrangeMultipliers() const { return {}; }
 
     double GetCommonSupport() const { return common_support; }
 
@@ -161,6 +173,11 @@ private:
     std::vector<uint8_t> comm_id;
     std::unique_ptr<FlatModel> flat;
     int64_t shard_begin = 0, shard_end = 0;
+    struct Matrices {   // the loaded path matrices (matrix-file mode)
+        std::vector<double> cdata, mdata, pdata;
+        std::vector<int32_t> crow, ccol, mrow, mcol, prow, pcol;
+    };
+    std::unique_ptr<Matrices> matrices;
 };
 
 void ThrowOnDevError(int rc, const char* what);

@@ -17,6 +17,7 @@ public:
 
     const std::vector<double>& GetGradient() const { return grad; }
     const std::vector<double>& GetLambda() const { return lambda; }
+    std::vector<double> GetLagrangeMultipliers() const override { return lambda; }
 
     void ComputeExpX();
     void ComputeG();

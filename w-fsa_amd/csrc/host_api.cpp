@@ -225,6 +225,19 @@ int wfsa_learner_build(wfsa_learner* l, wfsa_fsa* f, wfsa_corpus* c) {
                                      c->packed.size());
 }
 
+int wfsa_learner_load_matrices(wfsa_learner* l, const char* prefix) {
+    if (!l || !prefix) return null_arg("learner/prefix");
+    return guarded([&] { l->base->LoadMatrices(prefix); });
+}
+
+int wfsa_learner_save_matrices(wfsa_learner* l, const char* prefix) {
+    if (!l || !prefix) return null_arg("learner/prefix");
+    return guarded([&] {
+        if (!l->base->SaveMatrices(prefix))
+            throw LearnerError("no path matrices to save: only matrices that were loaded exist on this build");
+    });
+}
+
 int wfsa_learner_finalize(wfsa_learner* l) {
     if (!l) return null_arg("learner");
     return guarded([&] {

@@ -51,13 +51,15 @@ void usage() {
                  "  -x, --initx            read the initial x vector from stdin\n"
                  "  -opt NAME              Hessian (default) or QuasiNewton\n"
                  "  -p, --print            accepted (the reference prints its path matrices; no paths exist here)\n"
+                 "  -m, --matrix <FILE|>FILE  load the path matrices FILE.{C,M,P,prob,aux} instead of -a/-c,\n"
+                 "                         or save them (only matrices that were loaded: paths are never enumerated)\n"
                  "  -d, --device N         GPU to use (0)\n";
 }
 
 }  // namespace
 
 int main(int argc, const char* argv[]) {
-    std::string automaton, corpus_file, output, optimizer = "Hessian";
+    std::string automaton, corpus_file, output, optimizer = "Hessian", matrices;
     int epochs = 20, initflags = 0, device = 0;
     double eta = 1.0, tol = 1e-6;
     bool normalize = false, suppress = false, evaluate = false, initx = false;
@@ -80,6 +82,7 @@ int main(int argc, const char* argv[]) {
         else if (a == "-i" || a == "--init") initflags = std::atoi(next());
         else if (a == "-opt" || a == "--optimizer") optimizer = next();
         else if (a == "-d" || a == "--device") device = std::atoi(next());
+        else if (a == "-m" || a == "--matrix" || a == "--matrices") matrices = next();
         else if (a == "-n" || a == "--normalize") normalize = true;
         else if (a == "-eval" || a == "--eval" || a == "--evaluate") evaluate = true;
         else if (a == "-s" || a == "--suppress") suppress = true;
@@ -93,6 +96,24 @@ int main(int argc, const char* argv[]) {
         return 1;
     }
     try {
+        std::unique_ptr<Learner> owner(optimizer == "Hessian" ? static_cast<Learner*>(new HessianLearner())
+                                                               : static_cast<Learner*>(new QuasiNewtonLearner()));
+        Learner& learner = *owner;
+        learner.SetDevice(device);
+        Fsa fsa;
+        bool have_fsa = false;
+        if (!matrices.empty() && matrices.front() == '<') {   // src/main.cpp:123-137: skip Corpus and Fsa
+            std::cerr << "Loading matrices \"" << matrices.substr(1) << "\" ... ";
+            if (!learner.LoadMatrices(matrices.substr(1)))
+                throw LearnerError("Unable to load Learner from \"", matrices.substr(1), "\"");
+            std::cerr << "done" << std::endl;
+            std::cerr << "Info:\n\tparameters: " << learner.GetNumberOfParameters()
+                      << "\n\tconstraints: " << learner.GetNumberOfConstraints()
+                      << "\n\tstrings: " << learner.GetNumberOfStrings()
+                      << "\n\tpaths: " << learner.GetNumberOfPaths()
+                      << "\n\tcommon support: " << learner.GetCommonSupport()
+                      << "\n\tunique paths: " << (learner.HasUniquePaths() ? "true" : "false") << std::endl;
+        } else {
         Corpus corpus;
         if (FILE* f = std::fopen(corpus_file.c_str(), "rb")) {
             corpus.Read(f);
@@ -104,7 +125,6 @@ int main(int argc, const char* argv[]) {
         std::cerr << "Corpus:\n\tsize: " << corpus.size() << "\n\tsum: " << corpus.Sum();
         corpus.Renormalize();
         std::cerr << ", renormalized to " << corpus.Sum() << std::endl;
-        Fsa fsa;
         if (FILE* f = std::fopen(automaton.c_str(), "rb")) {
             fsa.Read(f);
             std::fclose(f);
@@ -112,16 +132,13 @@ int main(int argc, const char* argv[]) {
             std::cerr << "\nUnable to open \"" << automaton << "\"!" << std::endl;
             return 1;
         }
+        have_fsa = true;
         std::cerr << "Automaton:\n\tstates: " << fsa.GetNumberOfStates()
                   << "\n\ttransitions: " << fsa.GetNumberOfTransitions()
                   << "\n\temissions: " << fsa.GetNumberOfEmissions()
                   << "\n\tparameters: " << fsa.GetNumberOfParameters()
                   << "\n\tconstraints: " << fsa.GetNumberOfConstraints()
                   << "\n\tfree parameters: " << fsa.GetNumberOfFreeParameters() << std::endl;
-        std::unique_ptr<Learner> owner(optimizer == "Hessian" ? static_cast<Learner*>(new HessianLearner())
-                                                               : static_cast<Learner*>(new QuasiNewtonLearner()));
-        Learner& learner = *owner;
-        learner.SetDevice(device);
         learner.BuildFrom(fsa, corpus);
         std::cerr << "Recognize:\n\tstrings: " << learner.GetNumberOfStrings()
                   << "\n\tpaths: " << learner.GetNumberOfPaths()
@@ -129,6 +146,7 @@ int main(int argc, const char* argv[]) {
                   << "\n\tunique paths: " << (learner.HasUniquePaths() ? "true" : "false")
                   << "\nAfter trimming:\n\tparameters: " << learner.GetNumberOfParameters()
                   << "\n\tconstraints: " << learner.GetNumberOfConstraints() << std::endl;
+        }
         if (learner.GetNumberOfParameters() == 0) {
             std::cerr << "Empty automaton!" << std::endl;
             return 1;
@@ -138,6 +156,10 @@ int main(int argc, const char* argv[]) {
             return 1;
         }
         learner.Finalize();
+        if (!matrices.empty() && matrices.front() == '>') {   // src/main.cpp:241-249
+            std::cerr << "Saving matrices \"" << matrices.substr(1) << "\" ... ";
+            std::cerr << (learner.SaveMatrices(matrices.substr(1)) ? "Done" : "Failed!") << std::endl;
+        }
         std::cerr << "Initialize ... ";
         if (initx) {
             std::vector<double> x;
@@ -178,8 +200,17 @@ int main(int argc, const char* argv[]) {
         if (!suppress) {
             FILE* outf = output.empty() ? stdout : std::fopen(output.c_str(), "w");
             if (!outf) throw MyError("Unable to open output file \"", output, "\" for writing!");
-            learner.RewriteWeights(fsa);
-            fsa.Dump(outf);
+            if (have_fsa) {
+                learner.RewriteWeights(fsa);
+                fsa.Dump(outf);
+            } else {   // loaded from matrices (src/main.cpp:324-339): x, then lambda
+                const int32_t n = learner.GetNumberOfParameters();
+                const std::vector<double> lam = learner.GetLagrangeMultipliers();
+                for (int32_t i = 0; i < n; ++i) std::fprintf(outf, i ? " %g" : "%g", learner.GetWeights()[i]);
+                std::cout << std::endl;
+                for (size_t c = 0; c < lam.size(); ++c) std::fprintf(outf, c ? " %g" : "%g", lam[c]);
+                std::cout << std::endl;
+            }
             if (outf != stdout) std::fclose(outf);
         }
     } catch (const std::exception& e) {

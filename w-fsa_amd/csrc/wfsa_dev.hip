@@ -32,6 +32,7 @@
 #include <vector>
 
 #include "dense_path.hpp"
+#include "matrix_path.hpp"
 #include "fb_kernels.hpp"
 #include "trellis_model.hpp"
 
@@ -213,6 +214,7 @@ struct wfsa_dev {
     int64_t rm_n_amb = 0;
     int rm_gen = -1;             // prep_gen the list was built for
     bool qn_rmin = false;        // the device QN loop fills the rmin columns
+    std::unique_ptr<wfsa::MatrixPath> mpath;   // matrix-file mode (wfsa_dev_load_paths)
 
     // the per-iteration device sequence, captured once per prepared corpus
     hipGraph_t graph = nullptr;
@@ -497,6 +499,10 @@ int prepare_dense(wfsa_dev* ctx, int level) {
 
 int prepare(wfsa_dev* ctx, int level) {
     if (ctx->dense) return prepare_dense(ctx, level);
+    if (ctx->mpath) {   // nothing to compile: the structure came with the matrices
+        ctx->prep_level = 2;
+        return WFSA_OK;
+    }
     const auto t_start = std::chrono::steady_clock::now();
     drop_graph(ctx);
     hipStream_t s = ctx->stream;
@@ -1093,6 +1099,15 @@ int enqueue_evaluation(wfsa_dev* ctx, bool want_logq, const unsigned* halted, in
                        int32_t* n_ll = nullptr, const wfsa::QnArgs* fin = nullptr, bool* fin_done = nullptr) {
     hipStream_t s = ctx->stream;
     const int32_t np = ctx->n_params;
+    if (ctx->mpath) {   // matrix-file mode: out is complete when it returns
+        HIP_TRY(record(ctx, ctx->k0, slot, s));
+        HIP_TRY(ctx->mpath->enqueue(ctx->w_full.ptr, ctx->out.ptr, want_logq ? ctx->logq.ptr : nullptr, halted, s));
+        HIP_TRY(record(ctx, ctx->kc, slot, s));
+        HIP_TRY(record(ctx, ctx->k2, slot, s));
+        if (n_ll) *n_ll = 0;
+        if (fin_done) *fin_done = false;
+        return WFSA_OK;
+    }
     if (ctx->dense) {   // fp64 MFMA path: out is complete when it returns
         HIP_TRY(record(ctx, ctx->k0, slot, s));
         HIP_TRY(ctx->dense->enqueue(ctx->ewp.ptr, false, ctx->out.ptr, want_logq ? ctx->logq.ptr : nullptr, halted, s));
@@ -1176,6 +1191,10 @@ int enqueue_evaluation(wfsa_dev* ctx, bool want_logq, const unsigned* halted, in
 // tiers in min mode, then the reduction into res[0..1].
 int enqueue_rmin(wfsa_dev* ctx, const unsigned* halted, double* res) {
     hipStream_t s = ctx->stream;
+    if (ctx->mpath) {
+        HIP_TRY(ctx->mpath->enqueue_rmin(res, halted, s));
+        return WFSA_OK;
+    }
     const size_t S = size_t(std::max<int64_t>(ctx->n_strings, 1));
     if (ctx->rm_gen != ctx->prep_gen) {   // once per prepared corpus: the ambiguous strings
         std::vector<double> pc(S);
@@ -1260,7 +1279,7 @@ int enqueue_qn_step(wfsa_dev* ctx, double eta, double tol, int64_t e, bool timed
     ctx->ll_cur = ctx->ll_part.ptr + size_t(par) * ctx->ll_stride;
     // without the tail (no bubbles, no communicator) the QN kernels add the
     // constant gradient and sum the log-likelihood partials themselves
-    const bool tail = ctx->comm != nullptr || ctx->n_bubbles > 0 || ctx->dense != nullptr;
+    const bool tail = ctx->comm != nullptr || ctx->n_bubbles > 0 || ctx->dense != nullptr || ctx->mpath != nullptr;
     int32_t n_ll = 0;
     bool fin_done = false;
     if (int rc = enqueue_evaluation(ctx, false, ctx->qn_halted.ptr, timed ? slot : -1, tail, &n_ll, fin, &fin_done))
@@ -1465,6 +1484,10 @@ int wfsa_dev_load_model(wfsa_dev* ctx, const wfsa_model_desc* model) {
     if (int rc = check_ctx(ctx)) return rc;
     if (!model) return fail(WFSA_ERR_ARG, "null model");
     drop_graph(ctx);
+    if (ctx->mpath) {   // leaving matrix-file mode: the corpus went with the matrices
+        ctx->mpath.reset();
+        ctx->has_corpus = false;
+    }
     ctx->dense.reset();
     ctx->dense_struct = false;
     ctx->stats.dense = 0;
@@ -1562,6 +1585,7 @@ int wfsa_dev_load_model(wfsa_dev* ctx, const wfsa_model_desc* model) {
 
 int wfsa_dev_load_corpus(wfsa_dev* ctx, const uint8_t* sym, const int64_t* off, const double* p, int64_t n_strings) {
     if (int rc = check_ctx(ctx)) return rc;
+    if (ctx->mpath) return fail(WFSA_ERR_ARG, "matrix-file mode has no automaton: load a model first");
     if (n_strings < 0 || !off || (n_strings > 0 && !p)) return fail(WFSA_ERR_ARG, "bad corpus arguments");
     if (n_strings >= (int64_t(1) << 31) - 1) return fail(WFSA_ERR_ARG, "too many strings for one device (%lld)", (long long)n_strings);
     if (off[0] != 0) return fail(WFSA_ERR_ARG, "off[0] must be 0");
@@ -1613,6 +1637,57 @@ int wfsa_dev_recognize(wfsa_dev* ctx, uint8_t* recognized, double* path_count, u
     return WFSA_OK;
 }
 
+int wfsa_dev_load_paths(wfsa_dev* ctx, int32_t n_params, int64_t n_paths, const int64_t* prow, const int32_t* pcol,
+                        const double* pdata, int64_t n_strings, const int64_t* mrow, const int64_t* mcol,
+                        const double* p) {
+    if (int rc = check_ctx(ctx)) return rc;
+    if (n_params < 0 || n_paths < 0 || n_strings < 0 || !prow || !mrow || (n_strings > 0 && !p))
+        return fail(WFSA_ERR_ARG, "bad path matrices");
+    if (prow[0] != 0 || mrow[0] != 0) return fail(WFSA_ERR_ARG, "CSR rows must start at 0");
+    for (int64_t l = 0; l < n_paths; ++l)
+        if (prow[l + 1] < prow[l]) return fail(WFSA_ERR_ARG, "P rows not ascending at %lld", (long long)l);
+    for (int64_t k = 0; k < prow[n_paths]; ++k)
+        if (pcol[k] < 0 || pcol[k] >= n_params)
+            return fail(WFSA_ERR_ARG, "Size mismatch: more path indexes than parameters in the automaton!");
+    for (int64_t i = 0; i < n_strings; ++i)
+        if (mrow[i + 1] < mrow[i]) return fail(WFSA_ERR_ARG, "M rows not ascending at %lld", (long long)i);
+    for (int64_t k = 0; k < mrow[n_strings]; ++k)
+        if (mcol[k] < 0 || mcol[k] >= n_paths) return fail(WFSA_ERR_ARG, "M cols != P rows");
+    if (n_strings >= (int64_t(1) << 31) - 1) return fail(WFSA_ERR_ARG, "too many strings for one device");
+    drop_graph(ctx);
+    ctx->dense.reset();
+    ctx->dense_struct = false;
+    hipStream_t s = ctx->stream;
+    auto mp = std::make_unique<wfsa::MatrixPath>();
+    if (hipError_t e = mp->load(n_params, n_paths, prow, pcol, pdata, n_strings, mrow, mcol, p, s); e != hipSuccess)
+        return fail(WFSA_ERR_HIP, "matrix-file mode: upload failed (%s)", hipGetErrorString(e));
+    ctx->n_params = n_params;
+    ctx->n_nodes = ctx->n_edges = ctx->n_end = 0;
+    ctx->n_groups = 0;
+    ctx->n_bubbles = 0;
+    ctx->n_fall[0] = ctx->n_fall[1] = ctx->n_fall[2] = 0;
+    if (int rc = alloc_param_buffers(ctx)) return rc;
+    const size_t SZ = size_t(std::max<int64_t>(n_strings, 1));
+    std::vector<uint8_t> rec(SZ, 0);
+    for (int64_t i = 0; i < n_strings; ++i) rec[size_t(i)] = mp->path_counts()[size_t(i)] > 0 ? 1 : 0;
+    HIP_TRY(ctx->pcount.upload(mp->path_counts().data(), size_t(n_strings), s));
+    HIP_TRY(ctx->recog.upload(rec.data(), SZ, s));
+    HIP_TRY(ctx->used.upload(mp->used().data(), mp->used().size(), s));
+    HIP_TRY(ctx->logq.alloc(SZ));
+    HIP_TRY(hipStreamSynchronize(s));
+    ctx->mpath = std::move(mp);
+    ctx->n_strings = n_strings;
+    ctx->total_sym = 0;
+    ctx->max_len = 0;
+    ctx->has_model = true;
+    ctx->has_corpus = true;
+    ctx->prep_level = 2;
+    ctx->prep_gen++;
+    ctx->stats = wfsa_dev_stats{};
+    ctx->stats.n_strings = n_strings;
+    return WFSA_OK;
+}
+
 int wfsa_dev_rmin(wfsa_dev* ctx, double* rmin, int64_t* string_index) {
     if (int rc = check_ctx(ctx)) return rc;
     if (!ctx->has_model || !ctx->has_corpus) return fail(WFSA_ERR_ARG, "load a model and a corpus first");
@@ -1633,8 +1708,8 @@ int wfsa_dev_string_tiers(wfsa_dev* ctx, int8_t* tier) {
     if (int rc = check_ctx(ctx)) return rc;
     if (!ctx->has_model || !ctx->has_corpus) return fail(WFSA_ERR_ARG, "load a model and a corpus first");
     if (!tier) return fail(WFSA_ERR_ARG, "null output");
-    if (ctx->dense) {
-        std::memset(tier, 3, size_t(ctx->n_strings));
+    if (ctx->dense || ctx->mpath) {
+        std::memset(tier, ctx->dense ? 3 : 4, size_t(ctx->n_strings));
         return WFSA_OK;
     }
     if (ctx->prep_level < 2)
@@ -1877,6 +1952,14 @@ int wfsa_dev_hf_setup(wfsa_dev* ctx, int64_t* n_pairs) {
     if (!ctx->has_model || !ctx->has_corpus) return fail(WFSA_ERR_ARG, "load a model and a corpus first");
     if (ctx->in_flight) return fail(WFSA_ERR_ARG, "an evaluation is in flight");
     if (ctx->dense) return fail(WFSA_ERR_CAPACITY, "second-order terms: not available on the dense path");
+    if (ctx->mpath) {   // the pattern and the slots come from the path matrices
+        HIP_TRY(ctx->mpath->hf_setup(ctx->hf_pairs, ctx->stream));
+        HIP_TRY(ctx->hf_out.alloc(std::max<size_t>(ctx->hf_pairs.size() / 2, 1)));
+        ctx->hf_ready = true;
+        ctx->hf_gen = ctx->prep_gen;
+        if (n_pairs) *n_pairs = int64_t(ctx->hf_pairs.size() / 2);
+        return WFSA_OK;
+    }
     if (ctx->comm) return fail(WFSA_ERR_ARG, "second-order terms: not available with a communicator");
     if (ctx->prep_level < 2)
         if (int rc = prepare(ctx, 2)) return rc;
@@ -1969,6 +2052,13 @@ int wfsa_dev_hf_eval(wfsa_dev* ctx, const double* w_full, double* values) {
     const int32_t np = ctx->n_params;
     if (np > 0) std::memcpy(ctx->pinned + weights_off(np), w_full, size_t(np) * sizeof(double));
     HIP_TRY(wfsa::launch_stage(ctx->pinned_dev + weights_off(np), ctx->w_full.ptr, ctx->ewp.ptr, np, s));
+    if (ctx->mpath) {
+        const size_t n_pattern = ctx->hf_pairs.size() / 2;
+        HIP_TRY(ctx->mpath->hf_eval(ctx->w_full.ptr, ctx->hf_out.ptr, s));
+        if (values && n_pattern > 0) HIP_TRY(ctx->hf_out.download(values, n_pattern, s));
+        HIP_TRY(hipStreamSynchronize(s));
+        return WFSA_OK;
+    }
     wfsa::HfArgs a{};
     a.m = model_view(ctx);
     a.bub = ctx->bub.ptr;

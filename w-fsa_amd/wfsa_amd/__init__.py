@@ -7,6 +7,7 @@ include/wfsa_host.h, plus direct access to the device boundary
 libwfsa_amd.so on a gfx950 GPU; there is no CPU fallback.
 """
 import ctypes as C
+import os
 
 import numpy as np
 
@@ -175,6 +176,14 @@ class QuasiNewtonLearner:
         self._fsa = fsa
         check_host(load().wfsa_learner_build(self._h, fsa._h, corpus._h))
 
+    def LoadMatrices(self, prefix):
+        """matrix-file mode (Learner::LoadMatrices): prefix.{C,M,P,prob,aux}"""
+        self._fsa = None
+        check_host(load().wfsa_learner_load_matrices(self._h, os.fsencode(prefix)))
+
+    def SaveMatrices(self, prefix):
+        check_host(load().wfsa_learner_save_matrices(self._h, os.fsencode(prefix)))
+
     def BuildFromPacked(self, fsa, sym, off, weights):
         self._fsa = fsa
         sym = np.ascontiguousarray(sym, dtype=np.uint8)
@@ -320,6 +329,19 @@ class Device:
         used = np.zeros(max(self.n_params, 1), dtype=np.uint8)
         check_dev(load().wfsa_dev_recognize(self._h, _ptr(rec), _ptr(pc), _ptr(used)))
         return rec, pc, used[:self.n_params]
+
+    def load_paths(self, n_params, prow, pcol, pdata, mrow, mcol, p):
+        """matrix-file mode on the device: P (paths x params CSR), M (strings x paths)"""
+        prow = np.ascontiguousarray(prow, dtype=np.int64)
+        pcol = np.ascontiguousarray(pcol, dtype=np.int32)
+        pdata = np.ascontiguousarray(pdata, dtype=np.float64)
+        mrow = np.ascontiguousarray(mrow, dtype=np.int64)
+        mcol = np.ascontiguousarray(mcol, dtype=np.int64)
+        p = np.ascontiguousarray(p, dtype=np.float64)
+        check_dev(load().wfsa_dev_load_paths(self._h, int(n_params), len(prow) - 1, _ptr(prow), _ptr(pcol), _ptr(pdata),
+                                             len(mrow) - 1, _ptr(mrow), _ptr(mcol), _ptr(p)))
+        self.n_params = int(n_params)
+        self.n_strings = len(mrow) - 1
 
     def string_tiers(self):
         """per string: -1 compiled stream, 0/1 LDS traversal, 2 wide traversal, 3 dense"""
