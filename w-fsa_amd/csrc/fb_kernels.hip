@@ -1590,12 +1590,12 @@ __global__ __launch_bounds__(256) void rmin_final_kernel(RminArgs a, int n_part)
     }
 }
 
-hipError_t launch_rmin(const RminArgs& a, hipStream_t stream) {
+hipError_t launch_rmin(const RminArgs& a, hipStream_t stream, bool final) {
     if (a.n_bub > 0)
         hipLaunchKernelGGL(rmin_bubble_kernel, dim3(unsigned((a.n_bub + 63) / 64)), dim3(64), 0, stream, a);
     const unsigned g = unsigned(std::max<int64_t>(1, (a.n_amb + kRminBlock - 1) / kRminBlock));
     hipLaunchKernelGGL(rmin_strings_kernel, dim3(g), dim3(kRminBlock), 0, stream, a);
-    hipLaunchKernelGGL(rmin_final_kernel, dim3(1), dim3(256), 0, stream, a, int(g));
+    if (final) hipLaunchKernelGGL(rmin_final_kernel, dim3(1), dim3(256), 0, stream, a, int(g));
     return hipGetLastError();
 }
 

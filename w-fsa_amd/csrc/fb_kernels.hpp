@@ -214,7 +214,10 @@ struct RminArgs {
     const unsigned* halted;
 };
 constexpr int kRminBlock = 256;
-hipError_t launch_rmin(const RminArgs& a, hipStream_t stream);
+// final = false: leave the block minima in part[] (log values, string index)
+// for the QN finish to reduce (QnArgs::rmin_part)
+hipError_t launch_rmin(const RminArgs& a, hipStream_t stream, bool final = true);
+inline int rmin_blocks(int64_t n_amb) { return int(n_amb > 0 ? (n_amb + kRminBlock - 1) / kRminBlock : 1); }
 
 // Second-order term of the Hessian (HessianLearner::ComputeHf,
 // src/HessianLearner.cpp:498-547): sum_s p_s Cov_s(count_j, count_k).  The
@@ -283,6 +286,8 @@ struct QnArgs {
     unsigned* host_flag;         // host-mapped completion flag
     double* host_ring;           // host-mapped [slots][kQnRow]
     const double* rmin;          // [2] the step's rmin column (rmin, string index), or null (0, 0)
+    const double* rmin_part;     // or: [n][2] block minima (log rmin, string index) the finish reduces
+    int32_t rmin_n_part;
 };
 
 // Bubble evaluation.  Contributions (-p_s x edge posterior) go straight to

@@ -35,6 +35,22 @@ __device__ inline void qn_finish_wave(const QnArgs& a) {
         }
         if (a.ll_part) ll = strided_sum(a.ll_part, a.n_ll, lane, 64);
     }
+    double rv = INFINITY, ri = -1.0;   // rmin column from block minima, ties to the lower string
+    if (state == 0 && a.rmin_part)
+        for (int b = lane; b < a.rmin_n_part; b += 64) {
+            const double v = a.rmin_part[2 * b], i = a.rmin_part[2 * b + 1];
+            if (v < rv || (v == rv && i < ri)) {
+                rv = v;
+                ri = i;
+            }
+        }
+    for (int o = 32; o > 0; o >>= 1) {
+        const double v = __shfl_xor(rv, o, 64), i = __shfl_xor(ri, o, 64);
+        if (v < rv || (v == rv && i < ri)) {
+            rv = v;
+            ri = i;
+        }
+    }
     gmin = wave_reduce(gmin, 0);
     gmax = wave_reduce(gmax, 1);
     lmin = wave_reduce(lmin, 0);
@@ -50,7 +66,10 @@ __device__ inline void qn_finish_wave(const QnArgs& a) {
             info[2] = gmin;
             info[3] = gmax;
             info[4] = lmin;
-            if (a.rmin) {
+            if (a.rmin_part) {
+                info[5] = ri >= 0.0 ? exp(rv) : 0.0;
+                info[6] = ri;
+            } else if (a.rmin) {
                 info[5] = a.rmin[0];
                 info[6] = a.rmin[1];
             }

@@ -1189,7 +1189,7 @@ int enqueue_evaluation(wfsa_dev* ctx, bool want_logq, const unsigned* halted, in
 // The rmin column at the weights of the evaluation just enqueued (w_full,
 // ewp and the per-edge weights on the device): bubbles, then the traversal
 // tiers in min mode, then the reduction into res[0..1].
-int enqueue_rmin(wfsa_dev* ctx, const unsigned* halted, double* res) {
+int enqueue_rmin(wfsa_dev* ctx, const unsigned* halted, double* res, int par = 0, wfsa::QnArgs* q = nullptr) {
     hipStream_t s = ctx->stream;
     if (ctx->mpath) {
         HIP_TRY(ctx->mpath->enqueue_rmin(res, halted, s));
@@ -1208,8 +1208,7 @@ int enqueue_rmin(wfsa_dev* ctx, const unsigned* halted, double* res) {
         }
         ctx->rm_n_amb = int64_t(amb.size());
         if (!amb.empty()) HIP_TRY(ctx->rm_amb.upload(amb.data(), amb.size(), s));
-        const size_t blocks = size_t(std::max<int64_t>(1, (ctx->rm_n_amb + wfsa::kRminBlock - 1) / wfsa::kRminBlock));
-        HIP_TRY(ctx->rm_part.alloc(2 * blocks));
+        HIP_TRY(ctx->rm_part.alloc(4 * size_t(wfsa::rmin_blocks(ctx->rm_n_amb))));   // two halves (QN parity)
         HIP_TRY(ctx->rm_rs.alloc(S));
         HIP_TRY(ctx->rm_vb.alloc(size_t(std::max(ctx->n_bubbles, 1))));
         HIP_TRY(hipStreamSynchronize(s));   // amb is freed on return
@@ -1243,10 +1242,15 @@ int enqueue_rmin(wfsa_dev* ctx, const unsigned* halted, double* res) {
     r.rmin_log = ctx->rm_rs.ptr;
     r.amb = ctx->rm_amb.ptr;
     r.n_amb = ctx->rm_n_amb;
-    r.part = ctx->rm_part.ptr;
+    const int nb = wfsa::rmin_blocks(ctx->rm_n_amb);
+    r.part = ctx->rm_part.ptr + size_t(par) * 2 * size_t(nb);
     r.res = res;
     r.halted = halted;
-    HIP_TRY(wfsa::launch_rmin(r, s));
+    HIP_TRY(wfsa::launch_rmin(r, s, q == nullptr));
+    if (q) {   // the step's finish reduces the block minima (one launch fewer per step)
+        q->rmin_part = r.part;
+        q->rmin_n_part = nb;
+    }
     return WFSA_OK;
 }
 
@@ -1322,8 +1326,12 @@ int enqueue_qn_step(wfsa_dev* ctx, double eta, double tol, int64_t e, bool timed
     q.host_ring = ctx->qn_ring_dev;
     if (ctx->qn_rmin) {
         double* res = ctx->rm_res.ptr + 2 * par;
-        if (int rc = enqueue_rmin(ctx, ctx->qn_halted.ptr, res)) return rc;
-        q.rmin = res;
+        if (ctx->mpath) {
+            if (int rc = enqueue_rmin(ctx, ctx->qn_halted.ptr, res)) return rc;
+            q.rmin = res;
+        } else if (int rc = enqueue_rmin(ctx, ctx->qn_halted.ptr, res, par, &q)) {
+            return rc;
+        }
     }
     HIP_TRY(wfsa::launch_qn_update(q, s));
     *q_out = q;
