@@ -125,6 +125,17 @@ int wfsa_dev_load_corpus(wfsa_dev* ctx, const uint8_t* sym, const int64_t* off,
 int wfsa_dev_recognize(wfsa_dev* ctx, uint8_t* recognized, double* path_count,
                        uint8_t* used_param);
 
+/* Dense symmetric-indefinite factorisation in HBM for the HessianLearner's
+ * KKT system (MKL DSS in the reference: dss_factor_real / dss_statistics
+ * "Inertia", "Determinant" / dss_solve_real, src/HessianLearner.cpp:28-57,
+ * 100-113; RealSymmetricLogDet src/Utils.cpp:296-350): Bunch-Kaufman LDL^T
+ * (rocSOLVER dsytrf) of a[n*n] (symmetric, either layout); inertia =
+ * {positive, negative, zero} pivots of D, log|det| and its sign.  sym_solve
+ * overwrites b[n] with A^-1 b (one-workgroup dsytrs kernel). */
+int wfsa_dev_sym_factor(wfsa_dev* ctx, int64_t n, const double* a, int64_t inertia[3], double* log_abs_det,
+                        int32_t* det_sign);
+int wfsa_dev_sym_solve(wfsa_dev* ctx, double* b);
+
 /* Matrix-file mode (Learner::LoadMatrices, src/Learner.cpp:125-199; main.cpp
  * -m "<file"): instead of an automaton and strings, the path matrices the
  * reference's BuildPaths builds.  P: n_paths x n_params CSR (prow[n_paths+1],

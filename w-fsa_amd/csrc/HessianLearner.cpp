@@ -1,5 +1,7 @@
 #include "HessianLearner.hpp"
 
+#include <cstdlib>
+
 #include <algorithm>
 #include <cmath>
 #include <cstdio>
@@ -251,6 +253,50 @@ bool HessianLearner::AddHf(std::vector<double>& H, int64_t ld) {   // ComputeHf,
     return offdiag;
 }
 
+namespace {
+
+// host or device factorisation of an N x N system (HessianLearner::kHostDense)
+bool kkt_on_device(int64_t N) {
+    if (const char* e = std::getenv("WFSA_KKT"); e && e[0]) return std::string(e) == "device";
+    return N > HessianLearner::kHostDense;
+}
+
+struct Factored {
+    int64_t positive = 0, negative = 0;
+    double log_abs_det = 0.0;
+    int det_sign = 1;
+};
+
+// factors H (consumed on the host path) and, when rhs is given, solves
+// into x
+Factored factor_and_solve(wfsa_dev* dev, std::vector<double>& H, int64_t N, const double* rhs, double* x) {
+    Factored r;
+    if (!kkt_on_device(N)) {
+        DenseLdlt f;
+        f.Factor(H, N);
+        r.positive = f.positive;
+        r.negative = f.negative;
+        r.log_abs_det = f.log_abs_det;
+        r.det_sign = f.det_sign;
+        if (rhs) f.Solve(rhs, x);
+        return r;
+    }
+    if (!dev) throw LearnerError("no device for the KKT factorisation");
+    int64_t inertia[3] = {0, 0, 0};
+    int32_t sign = 1;
+    ThrowOnDevError(wfsa_dev_sym_factor(dev, N, H.data(), inertia, &r.log_abs_det, &sign), "wfsa_dev_sym_factor");
+    r.positive = inertia[0];
+    r.negative = inertia[1];
+    r.det_sign = sign;
+    if (rhs) {
+        std::copy(rhs, rhs + N, x);
+        ThrowOnDevError(wfsa_dev_sym_solve(dev, x), "wfsa_dev_sym_solve");
+    }
+    return r;
+}
+
+}  // namespace
+
 void HessianLearner::OptimizationStep(double eta, bool) {   // :63-130
     ComputeRhs();
     ComputeObjective();
@@ -258,7 +304,7 @@ void HessianLearner::OptimizationStep(double eta, bool) {   // :63-130
     const int64_t n = int64_t(_x.size()), k = int64_t(lambda.size()), N = n + k;
     if (N > kMaxDense)
         throw LearnerError("HessianLearner: the augmented system has ", N, " unknowns; this build factors it densely "
-                           "up to ", kMaxDense, " (use -opt QuasiNewton)");
+                           "in HBM up to ", kMaxDense, " (use -opt QuasiNewton)");
     std::vector<double> H(size_t(N * N), 0.0);
     if (include_Hf && !HasUniquePaths()) AddHf(H, N);
     for (int64_t i = 0; i < n; ++i) {   // ComputeHg, :622-639
@@ -268,12 +314,10 @@ void HessianLearner::OptimizationStep(double eta, bool) {   // :63-130
         H[size_t(c * N + i)] += expx[size_t(i)];
     }
     lambda_min = k ? *std::min_element(lambda.begin(), lambda.end()) : 0.0;
-    DenseLdlt f;
-    f.Factor(H, N);
+    step.assign(size_t(N), 0.0);
+    const Factored f = factor_and_solve(Device(), H, N, rhs.data(), step.data());
     inertia_pos = f.positive;
     inertia_neg = f.negative;
-    step.assign(size_t(N), 0.0);
-    f.Solve(rhs.data(), step.data());
     const auto bad = [](double v) { return !std::isfinite(v); };
     if (std::any_of(step.begin(), step.end(), bad)) {
         degenerate = true;
@@ -342,8 +386,7 @@ double HessianLearner::ComputeLogDetHessian() {
         }
         return r;
     }
-    DenseLdlt f;
-    f.Factor(H, n);
+    const Factored f = factor_and_solve(Device(), H, n, nullptr, nullptr);
     if (f.det_sign <= 0) return inf;   // (:351-352)
     return f.log_abs_det;
 }

@@ -8,9 +8,9 @@
 // (the count covariance of each string's paths) from the per-bubble
 // second-order kernel (wfsa_dev_hf_eval), and H_g / J_g are diagonal /
 // one-entry-per-row.  MKL DSS (symmetric indefinite factorisation, inertia,
-// determinant) is replaced by a dense Bunch-Kaufman LDL^T on the host, capped
-// at kMaxDense unknowns (a sparse factorisation is the next step for larger
-// automata).
+// determinant) is replaced by a dense Bunch-Kaufman LDL^T: on the host for
+// small systems, in HBM (wfsa_dev_sym_factor) for large ones up to kMaxDense
+// unknowns (a sparse factorisation is the next step beyond that).
 #pragma once
 
 #include <cstdint>
@@ -43,7 +43,12 @@ private:
 
 class HessianLearner : public Learner {
 public:
-    static constexpr int64_t kMaxDense = 4096;   // n + k of the augmented system
+    // n + k of the augmented system: factored on the host (Bunch-Kaufman
+    // LDL^T) up to kHostDense, above that in HBM (rocSOLVER dsytrf +
+    // wfsa_dev_sym_solve) up to kMaxDense (17 GB of fp64); WFSA_KKT=host /
+    // device forces one side
+    static constexpr int64_t kHostDense = 1024;
+    static constexpr int64_t kMaxDense = 46000;
 
     void OptimizationStep(double eta = 1.0, bool verbose = false) override;
     std::vector<double> GetOptimizationInfo() override;      // 9 values

@@ -33,6 +33,7 @@
 
 #include "dense_path.hpp"
 #include "matrix_path.hpp"
+#include "sym_solver.hpp"
 #include "fb_kernels.hpp"
 #include "trellis_model.hpp"
 
@@ -215,6 +216,7 @@ struct wfsa_dev {
     int rm_gen = -1;             // prep_gen the list was built for
     bool qn_rmin = false;        // the device QN loop fills the rmin columns
     std::unique_ptr<wfsa::MatrixPath> mpath;   // matrix-file mode (wfsa_dev_load_paths)
+    std::unique_ptr<wfsa::SymSolver> ldlt;     // dense LDL^T of the HessianLearner's KKT system
 
     // the per-iteration device sequence, captured once per prepared corpus
     hipGraph_t graph = nullptr;
@@ -1693,6 +1695,31 @@ int wfsa_dev_load_paths(wfsa_dev* ctx, int32_t n_params, int64_t n_paths, const 
     ctx->prep_gen++;
     ctx->stats = wfsa_dev_stats{};
     ctx->stats.n_strings = n_strings;
+    return WFSA_OK;
+}
+
+int wfsa_dev_sym_factor(wfsa_dev* ctx, int64_t n, const double* a, int64_t inertia[3], double* log_abs_det,
+                        int32_t* det_sign) {
+    if (int rc = check_ctx(ctx)) return rc;
+    if (n < 0 || (n > 0 && !a)) return fail(WFSA_ERR_ARG, "bad matrix");
+    if (ctx->in_flight) return fail(WFSA_ERR_ARG, "an evaluation is in flight");
+    if (!ctx->ldlt) ctx->ldlt = std::make_unique<wfsa::SymSolver>();
+    wfsa::SymFactor f;
+    if (const char* e = ctx->ldlt->factor(a, n, ctx->stream, &f)) return fail(WFSA_ERR_HIP, "sym_factor: %s", e);
+    if (inertia) {
+        inertia[0] = f.positive;
+        inertia[1] = f.negative;
+        inertia[2] = f.zero;
+    }
+    if (log_abs_det) *log_abs_det = f.log_abs_det;
+    if (det_sign) *det_sign = f.det_sign;
+    return WFSA_OK;
+}
+
+int wfsa_dev_sym_solve(wfsa_dev* ctx, double* b) {
+    if (int rc = check_ctx(ctx)) return rc;
+    if (!ctx->ldlt) return fail(WFSA_ERR_ARG, "sym_solve: no factorisation");
+    if (const char* e = ctx->ldlt->solve(b, ctx->stream)) return fail(WFSA_ERR_HIP, "sym_solve: %s", e);
     return WFSA_OK;
 }
 

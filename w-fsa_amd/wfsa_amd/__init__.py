@@ -330,6 +330,20 @@ class Device:
         check_dev(load().wfsa_dev_recognize(self._h, _ptr(rec), _ptr(pc), _ptr(used)))
         return rec, pc, used[:self.n_params]
 
+    def sym_factor(self, a):
+        """Bunch-Kaufman LDL^T of symmetric a in HBM: ((pos, neg, zero), log|det|, sign)"""
+        a = np.ascontiguousarray(a, dtype=np.float64)
+        n = a.shape[0]
+        inertia = np.zeros(3, dtype=np.int64)
+        lad, sign = C.c_double(), C.c_int32()
+        check_dev(load().wfsa_dev_sym_factor(self._h, n, _ptr(a), _ptr(inertia), C.byref(lad), C.byref(sign)))
+        return tuple(int(v) for v in inertia), lad.value, sign.value
+
+    def sym_solve(self, b):
+        x = np.array(b, dtype=np.float64)
+        check_dev(load().wfsa_dev_sym_solve(self._h, _ptr(x)))
+        return x
+
     def load_paths(self, n_params, prow, pcol, pdata, mrow, mcol, p):
         """matrix-file mode on the device: P (paths x params CSR), M (strings x paths)"""
         prow = np.ascontiguousarray(prow, dtype=np.int64)
