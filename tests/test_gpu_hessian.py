@@ -127,18 +127,23 @@ def test_hessian_learner_api_talk():
 
 
 HCASES = [("talk", "talk"), ("test3", "test"), ("test4", "test"), ("test.list", "test"), ("test2", "test"),
-          ("test.loop", "test")]
+          ("test.loop", "test"), ("test5", "test5"), ("test5_2", "test5")]
 
 
-@pytest.mark.parametrize("wfsa", ["test5", "test5_2"])
-def test_hessian_learner_fails_loudly_beyond_bubbles(wfsa):
-    """test5's one string is a single 20-node ambiguity region, wider than a
-    compiled bubble: the second-order term is not available for it and the
-    learner says so (WFSA_ERR_CAPACITY) instead of dropping H_f"""
+def test_hessian_learner_fails_loudly_beyond_bubbles():
+    """strings whose ambiguity region no compiled bubble (<= 32 nodes) holds
+    run on the traversal tiers, where no second-order term exists: the
+    learner says so (WFSA_ERR_CAPACITY) instead of dropping their H_f"""
     import wfsa_amd as W
+    syn = W.Synthetic(n_states=12, degree=3, vocab=3, emissions=2, n_strings=150, max_len=24, seed=3)
+    sym, off, wt = syn.corpus()
+    dev = W.Device(0)
+    dev.load_model(W.Fsa.read_text(syn.wfsa_text))
+    dev.load_corpus(sym, off, wt / wt.sum())
+    dev.recognize()
+    assert (dev.string_tiers() >= 0).any()
     lrn = W.HessianLearner(0)
-    lrn.BuildFrom(W.Fsa.read_file(os.path.join(DATA, wfsa + ".wfsa")),
-                  W.Corpus.read_file(os.path.join(DATA, "test5.corpus")))
+    lrn.BuildFromPacked(W.Fsa.read_text(syn.wfsa_text), sym, off, wt)
     lrn.Finalize()
     with pytest.raises(W.WfsaError, match="traversal tiers"):
         lrn.run(flags=31, epochs=20, tol=1e-6)

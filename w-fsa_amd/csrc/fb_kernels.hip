@@ -1509,7 +1509,9 @@ __device__ __forceinline__ void min_pair(double& v, double& i, double v2, double
 // stay linear and one log per bubble gives vb = log(min path / Z).
 __global__ __launch_bounds__(64) void rmin_bubble_kernel(RminArgs a) {
     if (a.halted && *a.halted) return;
-    __shared__ double sA[kMaxBubbleNodes][64], sM[kMaxBubbleNodes][64];
+    extern __shared__ double rmin_lds[];   // [max_nodes][64] sum, then [max_nodes][64] min
+    double (*sA)[64] = reinterpret_cast<double (*)[64]>(rmin_lds);
+    double (*sM)[64] = reinterpret_cast<double (*)[64]>(rmin_lds + size_t(a.max_nodes) * 64);
     const int lane = int(threadIdx.x);
     const int b = int(blockIdx.x) * 64 + lane;
     if (b >= a.n_bub) return;
@@ -1592,7 +1594,8 @@ __global__ __launch_bounds__(256) void rmin_final_kernel(RminArgs a, int n_part)
 
 hipError_t launch_rmin(const RminArgs& a, hipStream_t stream, bool final) {
     if (a.n_bub > 0)
-        hipLaunchKernelGGL(rmin_bubble_kernel, dim3(unsigned((a.n_bub + 63) / 64)), dim3(64), 0, stream, a);
+        hipLaunchKernelGGL(rmin_bubble_kernel, dim3(unsigned((a.n_bub + 63) / 64)), dim3(64),
+                           2 * size_t(a.max_nodes) * 64 * sizeof(double), stream, a);
     const unsigned g = unsigned(std::max<int64_t>(1, (a.n_amb + kRminBlock - 1) / kRminBlock));
     hipLaunchKernelGGL(rmin_strings_kernel, dim3(g), dim3(kRminBlock), 0, stream, a);
     if (final) hipLaunchKernelGGL(rmin_final_kernel, dim3(1), dim3(256), 0, stream, a, int(g));

@@ -19,7 +19,7 @@
 
 namespace wfsa {
 
-constexpr int kMaxBubbleNodes = 16;    // nodes of one compiled bubble
+constexpr int kMaxBubbleNodes = 32;    // nodes of one compiled bubble
 constexpr int kMaxBubbleEdges = 255;   // edges of one compiled bubble
 constexpr int kBubbleRegEdges = 8;     // bubbles up to this many edges run from registers
 constexpr int kBubbleRegNodes = 8;     // (and so at most this many nodes)
@@ -203,6 +203,7 @@ struct RminArgs {
     const int32_t* bub;
     const int32_t* bub_off;  // [n_bub]
     int32_t n_bub;
+    int32_t max_nodes;       // largest bubble: sizes the kernel's LDS node vectors
     double* vb;              // [n_bub] log(min path / Z) per bubble
     const double* w;         // [n_params + 1] weights (multi-parameter edges)
     const double* ewp;       // [n_params + 1] exp(w)

@@ -212,6 +212,7 @@ struct wfsa_dev {
     DevBuf<double> rm_rs, rm_vb, rm_part, rm_res;
     DevBuf<int4> rm_amb;         // the ambiguous strings (path count > 1) with their bubble runs
     std::vector<int32_t> h_bfirst, h_nbub;   // per string: first bubble ordinal, bubbles (compiled strings)
+    int max_bub_nodes = 1;                   // largest compiled bubble (nodes)
     int64_t rm_n_amb = 0;
     int rm_gen = -1;             // prep_gen the list was built for
     bool qn_rmin = false;        // the device QN loop fills the rmin columns
@@ -807,9 +808,11 @@ int prepare(wfsa_dev* ctx, int level) {
             }
         };
         std::vector<int32_t> small4, small, big;
+        ctx->max_bub_nodes = 1;
         for (int32_t o : h_off) {
             const int hdr = h_bubbuf[size_t(o)];
             const int nodes = hdr & 0xffff, edges = hdr >> 16;
+            ctx->max_bub_nodes = std::max(ctx->max_bub_nodes, nodes);
             bool sm = edges <= wfsa::kBubbleRegEdges && nodes <= wfsa::kBubbleRegNodes;
             for (int e = 0; sm && e < edges; ++e) sm = edge_code_at(o, e) >= 0;
             (!sm ? big : (edges <= 4 && nodes <= 4 ? small4 : small)).push_back(o);
@@ -1238,6 +1241,7 @@ int enqueue_rmin(wfsa_dev* ctx, const unsigned* halted, double* res, int par = 0
     r.bub = ctx->bub.ptr;
     r.bub_off = ctx->bub_off.ptr;
     r.n_bub = ctx->n_bubbles;
+    r.max_nodes = ctx->max_bub_nodes;
     r.vb = ctx->rm_vb.ptr;
     r.w = ctx->w_full.ptr;
     r.ewp = ctx->ewp.ptr;
