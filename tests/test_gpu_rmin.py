@@ -104,27 +104,37 @@ def test_rmin_synthetic(family, tier2, monkeypatch):
     _check(o, h, dev, seed=7)
 
 
-def test_rmin_column_in_quasinewton_device_loop():
+@pytest.mark.parametrize("source", ["test3", "family0", "family0_tier2"])
+def test_rmin_column_in_quasinewton_device_loop(source, monkeypatch):
     """the device-resident QN loop fills columns 5/6 at each step's x: the
-    oracle's QN trajectory (same steps) gives the x before each step"""
+    oracle's QN trajectory (same steps) gives the x before each step.
+    family0's strings run on the traversal tiers, whose weighted passes carry
+    the min forward in the loop (family0_tier2: all on the wide kernel)"""
     import wfsa_amd as W
     from oracle import Oracle
     from oracle.hessian import HessianOracle
-    wpath, cpath = os.path.join(DATA, "test3.wfsa"), os.path.join(DATA, "test.corpus")
-    o = Oracle.from_files(wpath, cpath)
+    monkeypatch.setenv("WFSA_TIER2", "1" if source.endswith("tier2") else "0")
+    lrn = W.QuasiNewtonLearner(0, optimizer="QuasiNewton")
+    if source == "test3":
+        wpath, cpath = os.path.join(DATA, "test3.wfsa"), os.path.join(DATA, "test.corpus")
+        o = Oracle.from_files(wpath, cpath)
+        lrn.BuildFrom(W.Fsa.read_file(wpath), W.Corpus.read_file(cpath))
+    else:
+        syn = W.Synthetic(n_states=12, degree=3, vocab=3, emissions=2, n_strings=150, max_len=8, seed=3)
+        sym, off, wt = syn.corpus()
+        o = Oracle.from_arrays(syn.wfsa_text, sym, off, wt)
+        lrn.BuildFromPacked(W.Fsa.read_text(syn.wfsa_text), sym, off, wt)
     h = HessianOracle(o)
     o.qn_init(7)
     want = []
-    for _ in range(20):
+    for _ in range(8):
         r, s, _ = _oracle_rmin(h, o.x())
         want.append((r, s))
         o.qn_step(1.0)
         if o.qn_halt(1e-6):
             break
-    lrn = W.QuasiNewtonLearner(0, optimizer="QuasiNewton")
-    lrn.BuildFrom(W.Fsa.read_file(wpath), W.Corpus.read_file(cpath))
     lrn.Finalize()
-    rows = np.array(lrn.run(flags=7, epochs=20, tol=1e-6))
+    rows = np.array(lrn.run(flags=7, epochs=len(want), tol=1e-6))
     assert len(rows) == len(want)
     np.testing.assert_allclose(rows[:, 5], [w[0] for w in want], rtol=1e-9)
     np.testing.assert_array_equal(rows[:, 6], [w[1] for w in want])

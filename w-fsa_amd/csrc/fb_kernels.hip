@@ -290,6 +290,9 @@ __global__ __launch_bounds__(256) void trav_kernel(TravArgs a) {
     const ModelView& m = a.m;
     const int cap_f = a.slab.cap_f, cap_e = a.slab.cap_e;
     const bool want_back = !MINM && (!COUNTING || a.used || a.c_main || MODE == MODE_EMIT);
+    // the (min, x) forward: min mode, or a weighted pass asked for the rmin
+    // column too (beta holds the keys until the backward re-zeroes it)
+    const bool track = MINM || (MODE == MODE_WEIGHTED && a.rmin_log != nullptr);
     unsigned long long* fkey = reinterpret_cast<unsigned long long*>(fbeta);
 
     for (int j = lane; j < m.n_nodes; j += kWave) st_rlx(&slot[j], -1);
@@ -307,7 +310,7 @@ __global__ __launch_bounds__(256) void trav_kernel(TravArgs a) {
         if (lane == 0) {
             fstate[0] = m.start;
             falpha[0] = 1.0;
-            if (MINM) fkey[0] = okey(0.0);
+            if (track) fkey[0] = okey(0.0);
             else fbeta[0] = 0.0;
             sl.fpos[0] = 0;
             sl.fpos[1] = 1;
@@ -336,7 +339,7 @@ __global__ __launch_bounds__(256) void trav_kernel(TravArgs a) {
                 double af = 0.0, mf = 0.0;
                 if (act) {
                     af = falpha[f];
-                    if (MINM) mf = odec(fkey[f]);
+                    if (track) mf = odec(fkey[f]);
                     edge_range(m, fstate[f], c, lo, cnt);
                 }
                 const int maxc = wave_max_i(cnt);
@@ -366,7 +369,7 @@ __global__ __launch_bounds__(256) void trav_kernel(TravArgs a) {
                         st_rlx(&slot[d], idx);
                         fstate[idx] = d;
                         falpha[idx] = 0.0;
-                        if (MINM) fkey[idx] = okey(INFINITY);
+                        if (track) fkey[idx] = okey(INFINITY);
                         else fbeta[idx] = 0.0;
                     }
                     nF += nwon;
@@ -374,7 +377,7 @@ __global__ __launch_bounds__(256) void trav_kernel(TravArgs a) {
                     if (need) slv = ld_rlx(&slot[d]);
                     if (has) {
                         lds_add(&falpha[slv], v);
-                        if (MINM && m.ew[g] > 0.0) atomicMin(&fkey[slv], okey(mf + log(m.ew[g])));
+                        if (track && m.lw[g] > -INFINITY) atomicMin(&fkey[slv], okey(mf + m.lw[g]));
                         const int k = nE + rank_below(hm);
                         sl.e_g[k] = g;
                         sl.e_src[k] = f;
@@ -434,7 +437,7 @@ __global__ __launch_bounds__(256) void trav_kernel(TravArgs a) {
         }
         const double lq = qh > 0.0 ? log(qh) + kLn2 * double(esum) : -INFINITY;
         const double ps = COUNTING ? 0.0 : a.p[sidx];
-        if (MINM) {
+        if (track) {
             double mn = INFINITY;
             for (int j = fl0 + lane; j < fl1; j += kWave) {
                 const double we = end_weight(m, fstate[j]);
@@ -442,6 +445,10 @@ __global__ __launch_bounds__(256) void trav_kernel(TravArgs a) {
             }
             mn = -wave_max(-mn);
             if (lane == 0) a.rmin_log[sidx] = qh > 0.0 ? mn - lq : INFINITY;
+            if (!MINM) {   // the backward accumulates into beta from zero
+                for (int j = lane; j < nF; j += kWave) fbeta[j] = 0.0;
+                wave_sync();
+            }
         }
         if (lane == 0) {
             if (MODE == MODE_COUNT) {
@@ -560,6 +567,7 @@ __global__ __launch_bounds__(kWideBlock) void wide_kernel(WideArgs a) {
     double* B = A + (int64_t(a.max_len) + 1) * N;             // [2][N]
     int* dsc = reinterpret_cast<int*>(B + 2 * int64_t(N));    // [max_len + 2]
     const bool lgrad = !COUNTING && !MINM && a.grad_lds;
+    const bool track = MINM || (!COUNTING && a.rmin_log != nullptr);   // (min, x) forward in B's rows
     if (lgrad)
         for (int j = tid; j < m.n_params; j += kWideBlock) gl[j] = 0.0;
     double ll = 0.0;
@@ -582,7 +590,7 @@ __global__ __launch_bounds__(kWideBlock) void wide_kernel(WideArgs a) {
         if (tid == 0) {
             A[m.start] = 1.0;
             dsc[0] = 0;
-            if (MINM) B[m.start] = 0.0;   // (min, x) forward in log form, rolling over B's two rows
+            if (track) B[m.start] = 0.0;   // (min, x) forward in log form, rolling over B's two rows
         }
         __syncthreads();
         bool alive = true;
@@ -598,12 +606,12 @@ __global__ __launch_bounds__(kWideBlock) void wide_kernel(WideArgs a) {
                     v += COUNTING ? Ai[W.e_src[e]] : Ai[W.e_src[e]] * m.ew[W.e_g[e]];
                 An[W.dst[k]] = v;
                 mx = fmax(mx, v);
-                if (MINM) {
+                if (track) {
                     const double* Mi = B + int64_t(i & 1) * N;
                     double mn = INFINITY;
                     for (int e = W.e_ptr[k]; e < W.e_ptr[k + 1]; ++e) {
-                        const double we = m.ew[W.e_g[e]];
-                        if (Ai[W.e_src[e]] > 0.0 && we > 0.0) mn = fmin(mn, Mi[W.e_src[e]] + log(we));
+                        const double lwe = m.lw[W.e_g[e]];
+                        if (Ai[W.e_src[e]] > 0.0 && lwe > -INFINITY) mn = fmin(mn, Mi[W.e_src[e]] + lwe);
                     }
                     B[int64_t((i + 1) & 1) * N + W.dst[k]] = mn;
                 }
@@ -637,7 +645,7 @@ __global__ __launch_bounds__(kWideBlock) void wide_kernel(WideArgs a) {
         }
         const double lq = qh > 0.0 ? log(qh) + kLn2 * double(esum) : -INFINITY;
         const double ps = COUNTING ? 1.0 : a.p[sidx];
-        if (MINM) {
+        if (track) {
             double mn = INFINITY;
             if (alive)
                 for (int k = fr_begin(L) + tid; k < fr_end(L); k += kWideBlock) {
@@ -648,7 +656,7 @@ __global__ __launch_bounds__(kWideBlock) void wide_kernel(WideArgs a) {
             mn = -block_max(-mn, red);
             if (tid == 0) a.rmin_log[sidx] = qh > 0.0 ? mn - lq : INFINITY;
             __syncthreads();
-            continue;
+            if (MINM) continue;
         }
         if (tid == 0) {
             if (COUNTING) {

@@ -216,6 +216,7 @@ struct wfsa_dev {
     int64_t rm_n_amb = 0;
     int rm_gen = -1;             // prep_gen the list was built for
     bool qn_rmin = false;        // the device QN loop fills the rmin columns
+    bool rm_eval = false;        // the evaluation being enqueued also runs the traversal min forward
     std::unique_ptr<wfsa::MatrixPath> mpath;   // matrix-file mode (wfsa_dev_load_paths)
     std::unique_ptr<wfsa::SymSolver> ldlt;     // dense LDL^T of the HessianLearner's KKT system
 
@@ -1155,6 +1156,7 @@ int enqueue_evaluation(wfsa_dev* ctx, bool want_logq, const unsigned* halted, in
         a.ll_part = ctx->ll_cur + wave_off;
         a.logq = want_logq ? ctx->logq.ptr : nullptr;
         a.halted = halted;
+        a.rmin_log = ctx->rm_eval ? ctx->rm_rs.ptr : nullptr;
         HIP_TRY(wfsa::launch_trav(wfsa::MODE_WEIGHTED, a, ctx->fall_grid[t], s));
         wave_off += ctx->fall_grid[t] * ctx->cfg[t].waves_per_block;
     }
@@ -1166,6 +1168,7 @@ int enqueue_evaluation(wfsa_dev* ctx, bool want_logq, const unsigned* halted, in
         a.ll_part = ctx->ll_cur + wave_off;
         a.logq = want_logq ? ctx->logq.ptr : nullptr;
         a.halted = halted;
+        a.rmin_log = ctx->rm_eval ? ctx->rm_rs.ptr : nullptr;
         HIP_TRY(wfsa::launch_wide(false, a, ctx->fall_grid[2], s));
         wave_off += ctx->fall_grid[2];
     }
@@ -1194,12 +1197,8 @@ int enqueue_evaluation(wfsa_dev* ctx, bool want_logq, const unsigned* halted, in
 // The rmin column at the weights of the evaluation just enqueued (w_full,
 // ewp and the per-edge weights on the device): bubbles, then the traversal
 // tiers in min mode, then the reduction into res[0..1].
-int enqueue_rmin(wfsa_dev* ctx, const unsigned* halted, double* res, int par = 0, wfsa::QnArgs* q = nullptr) {
+int rmin_prepare(wfsa_dev* ctx) {
     hipStream_t s = ctx->stream;
-    if (ctx->mpath) {
-        HIP_TRY(ctx->mpath->enqueue_rmin(res, halted, s));
-        return WFSA_OK;
-    }
     const size_t S = size_t(std::max<int64_t>(ctx->n_strings, 1));
     if (ctx->rm_gen != ctx->prep_gen) {   // once per prepared corpus: the ambiguous strings
         std::vector<double> pc(S);
@@ -1219,7 +1218,20 @@ int enqueue_rmin(wfsa_dev* ctx, const unsigned* halted, double* res, int par = 0
         HIP_TRY(hipStreamSynchronize(s));   // amb is freed on return
         ctx->rm_gen = ctx->prep_gen;
     }
-    for (int t = 0; t < 2; ++t) {
+    return WFSA_OK;
+}
+
+// trav_done: the evaluation just enqueued already wrote the traversal
+// strings' values (its weighted passes ran the min forward, ctx->rm_eval)
+int enqueue_rmin(wfsa_dev* ctx, const unsigned* halted, double* res, int par = 0, wfsa::QnArgs* q = nullptr,
+                 bool trav_done = false) {
+    hipStream_t s = ctx->stream;
+    if (ctx->mpath) {
+        HIP_TRY(ctx->mpath->enqueue_rmin(res, halted, s));
+        return WFSA_OK;
+    }
+    if (int rc = rmin_prepare(ctx)) return rc;
+    for (int t = 0; t < 2 && !trav_done; ++t) {
         if (!ctx->n_fall[t]) continue;
         wfsa::TravArgs a = trav_args(ctx, t);
         a.list = ctx->fall[t].ptr;
@@ -1228,7 +1240,7 @@ int enqueue_rmin(wfsa_dev* ctx, const unsigned* halted, double* res, int par = 0
         a.halted = halted;
         HIP_TRY(wfsa::launch_trav(wfsa::MODE_MIN, a, ctx->fall_grid[t], s));
     }
-    if (ctx->n_fall[2]) {
+    if (ctx->n_fall[2] && !trav_done) {
         wfsa::WideArgs a = wide_args(ctx);
         a.list = ctx->fall[2].ptr;
         a.n_list = ctx->n_fall[2];
@@ -1292,8 +1304,13 @@ int enqueue_qn_step(wfsa_dev* ctx, double eta, double tol, int64_t e, bool timed
     const bool tail = ctx->comm != nullptr || ctx->n_bubbles > 0 || ctx->dense != nullptr || ctx->mpath != nullptr;
     int32_t n_ll = 0;
     bool fin_done = false;
-    if (int rc = enqueue_evaluation(ctx, false, ctx->qn_halted.ptr, timed ? slot : -1, tail, &n_ll, fin, &fin_done))
-        return rc;
+    const bool fuse_rmin = ctx->qn_rmin && !ctx->mpath;   // traversal strings' rmin inside their weighted passes
+    if (fuse_rmin)
+        if (int rc = rmin_prepare(ctx)) return rc;
+    ctx->rm_eval = fuse_rmin;
+    const int erc = enqueue_evaluation(ctx, false, ctx->qn_halted.ptr, timed ? slot : -1, tail, &n_ll, fin, &fin_done);
+    ctx->rm_eval = false;
+    if (erc) return erc;
     if (fin && !fin_done) HIP_TRY(wfsa::launch_qn_finish(*fin, s));   // (no stream kernel to carry it)
     if (ctx->comm)
         RCCL_TRY(ncclAllReduce(ctx->out.ptr, ctx->out.ptr, size_t(np) + 1, ncclDouble, ncclSum, ctx->comm, s));
@@ -1335,7 +1352,7 @@ int enqueue_qn_step(wfsa_dev* ctx, double eta, double tol, int64_t e, bool timed
         if (ctx->mpath) {
             if (int rc = enqueue_rmin(ctx, ctx->qn_halted.ptr, res)) return rc;
             q.rmin = res;
-        } else if (int rc = enqueue_rmin(ctx, ctx->qn_halted.ptr, res, par, &q)) {
+        } else if (int rc = enqueue_rmin(ctx, ctx->qn_halted.ptr, res, par, &q, true)) {
             return rc;
         }
     }
