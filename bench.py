@@ -45,6 +45,9 @@ def parse():
     ap.add_argument("--emissions", type=int, default=None)
     ap.add_argument("--max-len", type=int, default=128)
     ap.add_argument("--seed", type=int, default=1)
+    ap.add_argument("--info-rmin", action="store_true",
+                    help="time the headline steps with the rmin info column on (default: measured in a "
+                         "second pass and reported as info_rmin; SURVEY 8d's timed region leaves it out)")
     ap.add_argument("--cpu-sample", type=int, default=None,
                     help="strings timed through the CPU oracle (0 = skip)")
     ap.add_argument("--profile-traffic", default=os.path.join(ROOT, "profiles", "traffic_latest.json"),
@@ -211,6 +214,7 @@ def main():
     t_build = time.perf_counter() - t0
     lrn.Finalize()
     lrn.Init(7)
+    lrn.set_info_rmin(args.info_rmin)
     info = lrn.info()
     local_sym = int(off[info["shard_end"]] - off[info["shard_begin"]])
     local_strings = info["n_local_strings"]
@@ -239,6 +243,23 @@ def main():
 
     strings_all = info["n_strings"]
     value = strings_all * args.steps / dt
+    # the same steps with the rmin info column (QuasiNewtonLearner::
+    # GetOptimizationInfo's smallest relative path probability), which the
+    # reference prints each epoch but computes outside OptimizationStep
+    rmin_pass = None
+    if not args.info_rmin and not distributed and not dense:
+        lrn.set_info_rmin(True)
+        lrn.Run(2, 1.0, -1.0)
+        barrier()
+        t1 = time.perf_counter()
+        rrows = lrn.Run(args.steps, 1.0, -1.0)
+        barrier()
+        dtr = time.perf_counter() - t1
+        rmin_pass = {"ms_per_step": dtr * 1e3 / args.steps, "value": strings_all * args.steps / dtr,
+                     "last_rmin": float(rrows[-1][5]) if len(rrows) else None,
+                     "note": "the headline steps plus the rmin info column (the (min, x) passes fused into "
+                             "the evaluation's bubble / traversal kernels)"}
+        lrn.set_info_rmin(False)
     # the device times a sample of the steps' kernels with HIP events (every
     # 4th step: an event between two kernels idles the device for a few us)
     timed = max(st1["fb_launches"] - st0["fb_launches"], 1)
@@ -320,7 +341,9 @@ def main():
             "strings_per_gpu": args.strings_per_gpu,
             "parallelism": f"dp{n_gpus}",
             "step": "QuasiNewtonLearner::OptimizationStep (H2D w, forward-backward, all-reduce, D2H grad, host update; epoch loop in wfsa_learner_run)",
+            "info_rmin": bool(args.info_rmin),
         },
+        "info_rmin": rmin_pass,
         "roofline": roofline,
         "host_ms_per_step": {k: (st1["host_" + k + "_ms"] - st0["host_" + k + "_ms"]) /
                              max(st1["host_steps"] - st0["host_steps"], 1)

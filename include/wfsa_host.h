@@ -68,6 +68,9 @@ int wfsa_learner_build(wfsa_learner* l, wfsa_fsa* fsa, wfsa_corpus* corpus);
 /* the same from packed strings + raw weights (renormalized here) */
 int wfsa_learner_build_packed(wfsa_learner* l, wfsa_fsa* fsa, const uint8_t* sym, const int64_t* off,
                               const double* weights, int64_t n_strings);
+/* The rmin info column (on by default, as the reference prints it every
+ * epoch); off: its two columns read 0 and no (min, x) pass runs. */
+int wfsa_learner_set_info_rmin(wfsa_learner* l, int on);
 /* Matrix-file mode: Learner::LoadMatrices / SaveMatrices (src/Learner.cpp:82-199),
  * prefix.{C,M,P,prob,aux} in the reference's text CSR format; load replaces
  * BuildFrom (no automaton); save works only for loaded matrices. */

@@ -92,6 +92,9 @@ public:
     // ambiguous strings on one rank off the dense path; otherwise (0, 0) as
     // the reference reports for unique paths
     bool RminAvailable() const;
+    // the rmin column is on by default (the reference prints it every epoch);
+    // off, columns rmin / index read 0 and no (min, x) pass runs
+    void SetInfoRmin(bool on) { info_rmin = on; }
     // out[0] = smallest relative path probability at the last evaluation,
     // out[1] = index of the string holding that path
     void ComputeRmin(double* out) const;
@@ -159,6 +162,7 @@ private:
     int64_t auxiliary_parameters = 0;
     int64_t n_strings_global = 0, n_paths_global = 0;
     bool unique_paths = true;
+    bool info_rmin = true;
     int32_t n_full = 0;
     std::vector<int32_t> trimmed_weights;
     std::vector<double> w_full, grad_full;

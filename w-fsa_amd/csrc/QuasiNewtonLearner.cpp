@@ -136,10 +136,11 @@ void QuasiNewtonLearner::RunDevice(double eta, double tol, int32_t max_epochs, d
     auto check = [](int rc, const char* what) {
         if (rc != WFSA_OK) throw LearnerError(what, ": ", wfsa_dev_last_error());
     };
-    if (!dev_qn_ready || dev_qn_exp != exponential_lambda) {   // once per Finalize (and lambda mode)
+    if (!dev_qn_ready || dev_qn_exp != exponential_lambda || dev_qn_rmin != desc.info_rmin) {   // once per Finalize (and mode)
         check(wfsa_dev_qn_setup(d, &desc), "wfsa_dev_qn_setup");
         dev_qn_ready = true;
         dev_qn_exp = exponential_lambda;
+        dev_qn_rmin = desc.info_rmin;
     }
     check(wfsa_dev_qn_set_state(d, _x.data(), lambda.data()), "wfsa_dev_qn_set_state");
     std::vector<double> rows(size_t(std::max(max_epochs, 0)) * 7);

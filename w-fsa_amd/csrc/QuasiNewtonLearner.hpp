@@ -48,6 +48,7 @@ private:
     double rmin[2] = {0, 0};   // rmin column of the last step
     bool exponential_lambda = false;
     bool dev_qn_ready = false, dev_qn_exp = false;   // wfsa_dev_qn_setup done for this build
+    int32_t dev_qn_rmin = -1;                        // ... with this info_rmin
     Timing timing;
 };
 

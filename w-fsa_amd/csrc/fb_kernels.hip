@@ -1015,7 +1015,7 @@ __device__ __forceinline__ void reg_add(double (&r)[N], int i, double v) {
 
 // A small bubble of class (N nodes, RE edges): quads of bubble b at
 // tbl[k * n + b] -- [header], RE/2 x [(code, sd) x 2], RE/4 x [slot x 4].
-template <int N, int RE>
+template <int N, int RE, bool RMIN = false>
 __device__ __forceinline__ double small_bubble(const BubbleArgs& a, const int4* __restrict__ tbl, int n, int b) {
     constexpr int NQ = 1 + RE / 2 + RE / 4;
     int4 q[NQ];
@@ -1052,6 +1052,22 @@ __device__ __forceinline__ double small_bubble(const BubbleArgs& a, const int4* 
         if (e < edges) reg_add(A, sd[e] >> 16, reg_get(A, sd[e] & 0xffff) * ew[e]);
     const double Z = reg_get(A, nodes - 1);
     const double scale = -p / Z;
+    if (RMIN && a.rmin_acc) {   // (min, x) forward for the rmin column in B's registers (re-zeroed
+                                // for the backward); the min path never exceeds Z
+#pragma unroll
+        for (int k = 0; k < N; ++k) B[k] = k == 0 ? 1.0 : INFINITY;
+#pragma unroll
+        for (int e = 0; e < RE; ++e)
+            if (e < edges && ew[e] > 0.0) {
+                const int dst = sd[e] >> 16;
+                const double v = reg_get(B, sd[e] & 0xffff) * ew[e];
+#pragma unroll
+                for (int k = 0; k < N; ++k) B[k] = dst == k ? fmin(B[k], v) : B[k];
+            }
+        global_add(&a.rmin_acc[q[0].y], log(reg_get(B, nodes - 1) / Z));
+#pragma unroll
+        for (int k = 0; k < N; ++k) B[k] = 0.0;
+    }
     reg_add(B, nodes - 1, 1.0);
 #pragma unroll
     for (int e = RE - 1; e >= 0; --e)
@@ -1103,6 +1119,13 @@ __device__ double big_bubble(const BubbleArgs& a, int i, int* lsd, double* lw, d
         for (int e = 0; e < edges; ++e) A[lsd[e] >> 16] += A[lsd[e] & 0xffff] * lw[e];
         const double Z = A[nodes - 1];
         const double scale = -p / Z;
+        if (a.rmin_acc) {   // (min, x) forward in B's storage, then B is re-zeroed
+            for (int v = 0; v < nodes; ++v) B[v] = v == 0 ? 1.0 : INFINITY;
+            for (int e = 0; e < edges; ++e)
+                if (lw[e] > 0.0) B[lsd[e] >> 16] = fmin(B[lsd[e] >> 16], B[lsd[e] & 0xffff] * lw[e]);
+            global_add(&a.rmin_acc[rec[1]], log(B[nodes - 1] / Z));
+            for (int v = 0; v < nodes; ++v) B[v] = 0.0;
+        }
         B[nodes - 1] = 1.0;
         for (int e = edges - 1; e >= 0; --e) {
             const int src = lsd[e] & 0xffff;
@@ -1121,6 +1144,7 @@ __device__ double big_bubble(const BubbleArgs& a, int i, int* lsd, double* lw, d
     return res;
 }
 
+template <bool RMIN>
 __global__ __launch_bounds__(kBubbleBlock) void bubble_kernel(BubbleArgs a) {
     if (a.halted && *a.halted) return;
     constexpr int WPB = kBubbleBlock / kWave;
@@ -1135,8 +1159,8 @@ __global__ __launch_bounds__(kBubbleBlock) void bubble_kernel(BubbleArgs a) {
     } else {
         // class A (4 nodes / 4 edges: most bubbles) first, then class B
         const int b = (gw - a.n_big) * kWave + lane;
-        if (b < a.n_small4) ll_acc = small_bubble<4, 4>(a, a.sm4_tbl, a.n_small4, b);
-        else if (b < a.n_small4 + a.n_small) ll_acc = small_bubble<8, 8>(a, a.sm_tbl, a.n_small, b - a.n_small4);
+        if (b < a.n_small4) ll_acc = small_bubble<4, 4, RMIN>(a, a.sm4_tbl, a.n_small4, b);
+        else if (b < a.n_small4 + a.n_small) ll_acc = small_bubble<8, 8, RMIN>(a, a.sm_tbl, a.n_small, b - a.n_small4);
     }
     ll_acc = wave_sum(ll_acc);
     if (lane == 0) a.ll_part[gw] = ll_acc;
@@ -1162,7 +1186,7 @@ __global__ __launch_bounds__(kBubbleBlock) void bubble_kernel(BubbleArgs a) {
 // DBG (timing experiments only, WFSA_FBS_DBG): 1 no table gathers, 3 no
 // stream pass at all, 4 neither stream pass nor table staging, 5 return at once, 6 / 7
 // prefetch sets of 2 / 6 rows, 8 no bubble code, 9 stream loads only
-template <bool WIDE, bool W_LDS, bool MULTI, int DBG = 0>
+template <bool WIDE, bool W_LDS, bool MULTI, int DBG = 0, bool RMIN = false>
 __global__ __launch_bounds__(1024) void fbs_kernel(CompiledArgs a) {
     extern __shared__ __attribute__((aligned(16))) double lds[];
     const int lane = lane_id();
@@ -1216,9 +1240,9 @@ __global__ __launch_bounds__(1024) void fbs_kernel(CompiledArgs a) {
         // block (spread over all CUs)
         if (w < a.bub.small_wpb) {   // small_wpb <= waves per block (bubbles_fused)
             const int b = (bid * a.bub.small_wpb + w) * kWave + lane;
-            if (b < a.bub.n_small4) ll_acc += small_bubble<4, 4>(a.bub, a.bub.sm4_tbl, a.bub.n_small4, b);
+            if (b < a.bub.n_small4) ll_acc += small_bubble<4, 4, RMIN>(a.bub, a.bub.sm4_tbl, a.bub.n_small4, b);
             else if (b < a.bub.n_small4 + a.bub.n_small)
-                ll_acc += small_bubble<8, 8>(a.bub, a.bub.sm_tbl, a.bub.n_small, b - a.bub.n_small4);
+                ll_acc += small_bubble<8, 8, RMIN>(a.bub, a.bub.sm_tbl, a.bub.n_small, b - a.bub.n_small4);
         }
         // big bubbles, one wavefront each, from the last blocks' last waves
         // down, staged in LDS after w
@@ -1462,6 +1486,10 @@ hipError_t configure_kernels(int max_dynamic_lds) {
                          reinterpret_cast<const void*>(&fbs_kernel<false, true, true>),
                          reinterpret_cast<const void*>(&fbs_kernel<true, true, false>),
                          reinterpret_cast<const void*>(&fbs_kernel<true, true, true>),
+                         reinterpret_cast<const void*>(&fbs_kernel<false, true, false, 0, true>),
+                         reinterpret_cast<const void*>(&fbs_kernel<false, true, true, 0, true>),
+                         reinterpret_cast<const void*>(&fbs_kernel<true, true, false, 0, true>),
+                         reinterpret_cast<const void*>(&fbs_kernel<true, true, true, 0, true>),
                          reinterpret_cast<const void*>(&fbs_kernel<false, true, false, 1>),
                          reinterpret_cast<const void*>(&fbs_kernel<false, true, false, 3>),
                          reinterpret_cast<const void*>(&fbs_kernel<false, true, false, 4>),
@@ -1560,9 +1588,14 @@ __global__ __launch_bounds__(kRminBlock) void rmin_strings_kernel(RminArgs a) {
     if (i < a.n_amb) {
         const int4 ent = a.amb[i];   // (string, first bubble, bubble count or -1, 0)
         double r = 0.0;
-        if (ent.z < 0) r = a.rmin_log[ent.x];
-        else
+        if (ent.z < 0) {
+            r = a.rmin_log[ent.x];
+        } else if (!a.vb) {   // accumulated by the evaluation's bubble passes: read, re-arm
+            r = a.rmin_log[ent.x];
+            a.rmin_log[ent.x] = 0.0;
+        } else {
             for (int b = ent.y; b < ent.y + ent.z; ++b) r += a.vb[b];
+        }
         v = r;
         idx = double(ent.x);
     }
@@ -1601,7 +1634,7 @@ __global__ __launch_bounds__(256) void rmin_final_kernel(RminArgs a, int n_part)
 }
 
 hipError_t launch_rmin(const RminArgs& a, hipStream_t stream, bool final) {
-    if (a.n_bub > 0)
+    if (a.n_bub > 0 && a.vb)
         hipLaunchKernelGGL(rmin_bubble_kernel, dim3(unsigned((a.n_bub + 63) / 64)), dim3(64),
                            2 * size_t(a.max_nodes) * 64 * sizeof(double), stream, a);
     const unsigned g = unsigned(std::max<int64_t>(1, (a.n_amb + kRminBlock - 1) / kRminBlock));
@@ -1683,6 +1716,19 @@ hipError_t launch_compiled(const CompiledArgs& a, int grid, int block, size_t ld
             return hipGetLastError();
         }
         const int key = (a.tables >= 1 ? 4 : 0) + (a.wide ? 2 : 0) + (a.multi ? 1 : 0);
+        if (a.bub_on && a.bub.rmin_acc) {   // the bubbles also feed the rmin column
+            switch (key) {
+                case 0: hipLaunchKernelGGL((fbs_kernel<false, false, false, 0, true>), g, b, 0, stream, a); break;
+                case 1: hipLaunchKernelGGL((fbs_kernel<false, false, true, 0, true>), g, b, 0, stream, a); break;
+                case 2: hipLaunchKernelGGL((fbs_kernel<true, false, false, 0, true>), g, b, 0, stream, a); break;
+                case 3: hipLaunchKernelGGL((fbs_kernel<true, false, true, 0, true>), g, b, 0, stream, a); break;
+                case 4: hipLaunchKernelGGL((fbs_kernel<false, true, false, 0, true>), g, b, lds, stream, a); break;
+                case 5: hipLaunchKernelGGL((fbs_kernel<false, true, true, 0, true>), g, b, lds, stream, a); break;
+                case 6: hipLaunchKernelGGL((fbs_kernel<true, true, false, 0, true>), g, b, lds, stream, a); break;
+                default: hipLaunchKernelGGL((fbs_kernel<true, true, true, 0, true>), g, b, lds, stream, a); break;
+            }
+            return hipGetLastError();
+        }
         switch (key) {
             case 0: hipLaunchKernelGGL((fbs_kernel<false, false, false>), g, b, 0, stream, a); break;
             case 1: hipLaunchKernelGGL((fbs_kernel<false, false, true>), g, b, 0, stream, a); break;
@@ -1713,7 +1759,10 @@ hipError_t launch_bubbles(const BubbleArgs& a, hipStream_t stream) {
     const int waves = bubble_waves(a.n_small4 + a.n_small, a.n_big);
     if (waves <= 0) return hipSuccess;
     constexpr int WPB = kBubbleBlock / kWave;
-    hipLaunchKernelGGL(bubble_kernel, dim3(unsigned((waves + WPB - 1) / WPB)), dim3(kBubbleBlock), 0, stream, a);
+    if (a.rmin_acc)
+        hipLaunchKernelGGL(bubble_kernel<true>, dim3(unsigned((waves + WPB - 1) / WPB)), dim3(kBubbleBlock), 0, stream, a);
+    else
+        hipLaunchKernelGGL(bubble_kernel<false>, dim3(unsigned((waves + WPB - 1) / WPB)), dim3(kBubbleBlock), 0, stream, a);
     return hipGetLastError();
 }
 

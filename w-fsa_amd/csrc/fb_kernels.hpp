@@ -204,7 +204,8 @@ struct RminArgs {
     const int32_t* bub_off;  // [n_bub]
     int32_t n_bub;
     int32_t max_nodes;       // largest bubble: sizes the kernel's LDS node vectors
-    double* vb;              // [n_bub] log(min path / Z) per bubble
+    double* vb;              // [n_bub] log(min path / Z) per bubble; null: the evaluation's bubble
+                             // passes accumulated them per string into rmin_log (read and re-zeroed)
     const double* w;         // [n_params + 1] weights (multi-parameter edges)
     const double* ewp;       // [n_params + 1] exp(w)
     double* rmin_log;        // [S] traversal strings' values
@@ -329,6 +330,8 @@ struct BubbleArgs {
     double* contrib;
     double* ll_part;         // [waves in grid]
     double* logq;            // [S] or null: log Z added to the string's entry
+    double* rmin_acc;        // [S] or null: log(min path / Z) added to the string's entry (rmin column;
+                             // small bubbles only in the RMIN kernel variants)
     const double* w;         // [n_params + 1] weights (GetWeight form) with the zero slot
     const double* ewp;       // [n_params + 1] exp(w), ewp[n_params] = 1 (per iteration)
     const unsigned* halted;

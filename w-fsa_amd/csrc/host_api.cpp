@@ -225,6 +225,11 @@ int wfsa_learner_build(wfsa_learner* l, wfsa_fsa* f, wfsa_corpus* c) {
                                      c->packed.size());
 }
 
+int wfsa_learner_set_info_rmin(wfsa_learner* l, int on) {
+    if (!l) return null_arg("learner");
+    return guarded([&] { l->base->SetInfoRmin(on != 0); });
+}
+
 int wfsa_learner_load_matrices(wfsa_learner* l, const char* prefix) {
     if (!l || !prefix) return null_arg("learner/prefix");
     return guarded([&] { l->base->LoadMatrices(prefix); });

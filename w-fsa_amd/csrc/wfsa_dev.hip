@@ -1057,6 +1057,7 @@ int enqueue_compiled(wfsa_dev* ctx, bool with_grad, bool want_logq, const unsign
 wfsa::BubbleArgs bubble_args(wfsa_dev* ctx, bool want_logq, const unsigned* halted, double* ll_part) {
     wfsa::BubbleArgs b{};
     b.m = model_view(ctx);
+    b.rmin_acc = ctx->rm_eval ? ctx->rm_rs.ptr : nullptr;
     b.sm4_tbl = ctx->sm4_tbl.ptr;
     b.n_small4 = ctx->n_small4;
     b.sm_tbl = ctx->sm_tbl.ptr;
@@ -1214,6 +1215,7 @@ int rmin_prepare(wfsa_dev* ctx) {
         if (!amb.empty()) HIP_TRY(ctx->rm_amb.upload(amb.data(), amb.size(), s));
         HIP_TRY(ctx->rm_part.alloc(4 * size_t(wfsa::rmin_blocks(ctx->rm_n_amb))));   // two halves (QN parity)
         HIP_TRY(ctx->rm_rs.alloc(S));
+        HIP_TRY(hipMemsetAsync(ctx->rm_rs.ptr, 0, S * sizeof(double), s));   // fused accumulation starts at 0
         HIP_TRY(ctx->rm_vb.alloc(size_t(std::max(ctx->n_bubbles, 1))));
         HIP_TRY(hipStreamSynchronize(s));   // amb is freed on return
         ctx->rm_gen = ctx->prep_gen;
@@ -1221,8 +1223,9 @@ int rmin_prepare(wfsa_dev* ctx) {
     return WFSA_OK;
 }
 
-// trav_done: the evaluation just enqueued already wrote the traversal
-// strings' values (its weighted passes ran the min forward, ctx->rm_eval)
+// trav_done: the evaluation just enqueued already produced every string's
+// value (ctx->rm_eval: its weighted traversal passes ran the min forward and
+// its bubble passes accumulated log(min path / Z) per string)
 int enqueue_rmin(wfsa_dev* ctx, const unsigned* halted, double* res, int par = 0, wfsa::QnArgs* q = nullptr,
                  bool trav_done = false) {
     hipStream_t s = ctx->stream;
@@ -1254,7 +1257,7 @@ int enqueue_rmin(wfsa_dev* ctx, const unsigned* halted, double* res, int par = 0
     r.bub_off = ctx->bub_off.ptr;
     r.n_bub = ctx->n_bubbles;
     r.max_nodes = ctx->max_bub_nodes;
-    r.vb = ctx->rm_vb.ptr;
+    r.vb = trav_done ? nullptr : ctx->rm_vb.ptr;   // fused: the evaluation accumulated the bubbles
     r.w = ctx->w_full.ptr;
     r.ewp = ctx->ewp.ptr;
     r.rmin_log = ctx->rm_rs.ptr;

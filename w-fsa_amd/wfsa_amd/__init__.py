@@ -176,6 +176,10 @@ class QuasiNewtonLearner:
         self._fsa = fsa
         check_host(load().wfsa_learner_build(self._h, fsa._h, corpus._h))
 
+    def set_info_rmin(self, on):
+        """the rmin info column on (default) / off"""
+        check_host(load().wfsa_learner_set_info_rmin(self._h, int(bool(on))))
+
     def LoadMatrices(self, prefix):
         """matrix-file mode (Learner::LoadMatrices): prefix.{C,M,P,prob,aux}"""
         self._fsa = None
