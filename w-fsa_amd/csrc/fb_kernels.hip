@@ -1187,7 +1187,7 @@ __global__ __launch_bounds__(kBubbleBlock) void bubble_kernel(BubbleArgs a) {
 // stream pass at all, 4 neither stream pass nor table staging, 5 return at once, 6 / 7
 // prefetch sets of 2 / 6 rows, 8 no bubble code, 9 stream loads only
 template <bool WIDE, bool W_LDS, bool MULTI, int DBG = 0, bool RMIN = false>
-__global__ __launch_bounds__(1024) void fbs_kernel(CompiledArgs a) {
+__global__ __launch_bounds__(1024, (DBG == 10 ? 8 : 1)) void fbs_kernel(CompiledArgs a) {
     extern __shared__ __attribute__((aligned(16))) double lds[];
     const int lane = lane_id();
     const int wpb = int(blockDim.x) / kWave;
@@ -1235,7 +1235,7 @@ __global__ __launch_bounds__(1024) void fbs_kernel(CompiledArgs a) {
     }
     const double* wsrc = W_LDS ? lds : a.w;
     double ll_acc = 0.0;
-    if (a.bub_on && DBG != 8) {   // this wave's bubbles, before its streams
+    if (a.bub_on && DBG != 8 && DBG != 10) {   // this wave's bubbles, before its streams
         // small ones, one per lane, from the first small_wpb waves of every
         // block (spread over all CUs)
         if (w < a.bub.small_wpb) {   // small_wpb <= waves per block (bubbles_fused)
@@ -1498,6 +1498,7 @@ hipError_t configure_kernels(int max_dynamic_lds) {
                          reinterpret_cast<const void*>(&fbs_kernel<false, true, false, 7>),
                          reinterpret_cast<const void*>(&fbs_kernel<false, true, false, 8>),
                          reinterpret_cast<const void*>(&fbs_kernel<false, true, false, 9>),
+                         reinterpret_cast<const void*>(&fbs_kernel<false, true, false, 10>),
                          reinterpret_cast<const void*>(&wide_kernel<false>)};
     for (const void* f : fns) {   // (static LDS counts against the same 160 KiB)
         hipFuncAttributes attr{};
@@ -1705,6 +1706,10 @@ hipError_t launch_compiled(const CompiledArgs& a, int grid, int block, size_t ld
         }
         if (dbg == 7) {
             hipLaunchKernelGGL((fbs_kernel<false, true, false, 7>), g, b, lds, stream, a);
+            return hipGetLastError();
+        }
+        if (dbg == 10) {   // no bubble code, two blocks per CU (<= 64 VGPRs): needs WFSA_FUSE_BUBBLES=0
+            hipLaunchKernelGGL((fbs_kernel<false, true, false, 10>), g, b, lds, stream, a);
             return hipGetLastError();
         }
         if (dbg == 8) {

@@ -642,7 +642,9 @@ int prepare(wfsa_dev* ctx, int level) {
         int i_per_cu = std::max(1, kIterWavesPerCu / i_wpb);
         if (ctx->i_tables)
             i_per_cu = std::min<int>(i_per_cu, int(size_t(kLdsPerCu) / std::max<size_t>(table_bytes, 1)));
-        if (const char* e = std::getenv("WFSA_IPERCU")) i_per_cu = std::min(i_per_cu, std::atoi(e));
+        if (const char* e = std::getenv("WFSA_IPERCU")) i_per_cu = std::atoi(e);   // experiments (LDS-capped below)
+        if (ctx->i_tables)
+            i_per_cu = std::min<int>(i_per_cu, int(size_t(kLdsPerCu) / std::max<size_t>(table_bytes, 1)));
         i_per_cu = std::max(1, i_per_cu);
         ctx->i_grid = int(std::max<int64_t>(1, std::min<int64_t>(int64_t(ctx->n_cu) * i_per_cu,
                                                                  (int64_t(G) + i_wpb - 1) / i_wpb)));
