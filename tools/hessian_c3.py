@@ -1,5 +1,5 @@
 """HessianLearner on the c3 workload (1024-state family A, 1M
-strings): n + k = 10,239 unknowns -- the KKT system factored in HBM
+strings): n + k = 10,249 unknowns -- the KKT system factored in HBM
 (rocSOLVER dsytrf + the dsytrs kernel), H_f from the compiled bubbles.
 Prints the time of each Newton epoch and its info row (GPU box)."""
 import os
