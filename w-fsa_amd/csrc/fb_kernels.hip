@@ -1196,10 +1196,15 @@ __global__ __launch_bounds__(1024, (DBG == 10 ? 8 : 1)) void fbs_kernel(Compiled
     const int bid = int(blockIdx.x);
     const int w = int(threadIdx.x) / kWave;
     const int gw = __builtin_amdgcn_readfirstlane(bid * wpb + w);
-    const unsigned halted = a.halted ? *a.halted : 0u;   // (before the finish below may set it)
-    if (a.fin_on && gw == a.fin_wave) qn_finish_wave(a.fin);   // the previous QN step's finish
-    if (halted) return;
-    if (DBG == 5) return;
+    const unsigned halted = a.halted ? *a.halted : 0u;   // (before the finish may set it)
+    // the previous QN step's finish runs after this wave's streams: at the
+    // start it held the whole block at the table staging barrier (~5 us on
+    // the kernel's critical path); the load balancer gives the wave fewer rows
+    const bool fin_here = a.fin_on && gw == a.fin_wave;
+    if (halted || DBG == 5) {
+        if (fin_here) qn_finish_wave(a.fin);
+        return;
+    }
     const uint32_t zslot = uint32_t(a.n_params);
     // this wave's run of chunk rows
     const int g0 = a.wave_first[gw], g1 = a.wave_first[gw + 1];
@@ -1347,6 +1352,7 @@ __global__ __launch_bounds__(1024, (DBG == 10 ? 8 : 1)) void fbs_kernel(Compiled
         for (int i = 0; i < wpb; ++i) t += wsum[i];
         a.ll_part[bid] = t;
     }
+    if (fin_here) qn_finish_wave(a.fin);   // reads the other half of ll_part (steps alternate)
     // this block's slice of the per-edge weights and the zeroed result, for
     // the kernels after this one (nothing in this launch reads them)
     if (W_LDS) edge_weight_slice(a, bid, nblk);
