@@ -637,6 +637,10 @@ int prepare(wfsa_dev* ctx, int level) {
         const size_t table_bytes = size_t(ctx->n_params) * sizeof(double);
         ctx->i_tables = table_bytes + 16 <= size_t(kLdsPerCu - 1024) ? 1 : 0;
         ctx->i_lds = ctx->i_tables ? table_bytes + 16 : 0;   // + the zero slot, even count
+        // two 512-thread blocks per CU when two tables fit in LDS (same 16
+        // waves per CU; c3: fbs 31.3 -> 30.1 us, profiles/r01/v19_block_sweep.txt),
+        // else one 1024-thread block
+        ctx->i_block = (ctx->i_tables && 2 * (table_bytes + 16) <= size_t(kLdsPerCu - 1024)) ? 512 : 1024;
         if (const char* e = std::getenv("WFSA_IBLOCK")) ctx->i_block = std::max(64, std::min(1024, std::atoi(e))) & ~63;
         const int i_wpb = ctx->i_block / kWave;
         int i_per_cu = std::max(1, kIterWavesPerCu / i_wpb);
