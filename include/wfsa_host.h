@@ -93,6 +93,9 @@ int wfsa_learner_run(wfsa_learner* l, double eta, double tol, int32_t max_epochs
  * kl, grad[n_params] (trimmed order), logq[n_local_strings] (nullable) */
 int wfsa_learner_objective_grad(wfsa_learner* l, double* kl, double* grad, double* logq);
 int wfsa_learner_get_x(wfsa_learner* l, double* x);
+/* the (trimmed) gradient of the last evaluation: after a device-resident
+ * run, the gradient of its last step (at the weights that step started from) */
+int wfsa_learner_get_grad(wfsa_learner* l, double* grad);
 int wfsa_learner_set_x(wfsa_learner* l, const double* x);
 int wfsa_learner_get_p(wfsa_learner* l, double* p);                 /* [n_local_strings] */
 int wfsa_learner_trimmed_index(wfsa_learner* l, int32_t* out);      /* [n_full]          */

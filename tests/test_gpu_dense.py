@@ -185,3 +185,97 @@ def test_dense_device_qn_large_groups_equals_host_update(monkeypatch):
         for u, v in zip(r[:5], q[:5]):
             assert _close(u, v, rel=1e-10, atol=1e-13)
     np.testing.assert_allclose(a.x(), b.x(), rtol=1e-10, atol=1e-12)
+
+
+def _dense_tables(fsa, w):
+    """exp-weights of a dense synthetic model from its flat description:
+    A[S][T] (transitions), E[T][c] (1-byte emissions), the start row and the
+    end column; kind of every Fsa parameter (0 emission, 1 start transition,
+    2 end transition, 3 interior transition).  Unequivocal groups (-1) weigh 1."""
+    import ctypes as C
+    d = fsa.desc()
+    ns = d.n_states
+
+    def arr(ptr, n, ct):
+        return np.ctypeslib.as_array(C.cast(ptr, C.POINTER(ct)), shape=(n,)).copy()
+
+    tr_ptr = arr(d.tr_ptr, ns + 1, C.c_int32)
+    tr_dst = arr(d.tr_dst, int(tr_ptr[-1]), C.c_int32)
+    tr_par = arr(d.tr_param, int(tr_ptr[-1]), C.c_int32)
+    em_ptr = arr(d.em_ptr, ns + 1, C.c_int32)
+    n_em = int(em_ptr[-1])
+    em_off = arr(d.em_off, n_em, C.c_int64)
+    em_len = arr(d.em_len, n_em, C.c_int32)
+    em_par = arr(d.em_param, n_em, C.c_int32)
+    em_bytes = arr(d.em_bytes, int((em_off + em_len).max()) if n_em else 1, C.c_uint8)
+    ew = np.where(np.asarray(tr_par) >= 0, np.exp(w[np.maximum(tr_par, 0)]), 1.0)
+    src = np.repeat(np.arange(ns), np.diff(tr_ptr))
+    A = np.zeros((ns, ns))
+    A[src, tr_dst] = ew
+    E = np.zeros((ns, 256))
+    esrc = np.repeat(np.arange(ns), np.diff(em_ptr))
+    one = em_len == 1
+    E[esrc[one], em_bytes[em_off[one]]] = np.where(em_par[one] >= 0, np.exp(w[np.maximum(em_par[one], 0)]), 1.0)
+    kind = np.full(len(w), -1)
+    kind[em_par[em_par >= 0]] = 0
+    tk = np.where(src == d.start, 1, np.where(tr_dst == d.end, 2, 3))
+    kind[tr_par[tr_par >= 0]] = tk[tr_par >= 0]
+    return A, E, d.start, d.end, kind
+
+
+def _dense_logq(A, E, start, end, s):
+    """scaled forward: alpha_1 = A[start] E[:, s0]; alpha_{i+1} = (alpha_i A) E[:, s_i]"""
+    a = A[start] * E[:, s[0]]
+    lg = 0.0
+    for c in s[1:]:
+        z = a.sum()
+        lg += np.log(z)
+        a = (a / z) @ A * E[:, c]
+    return lg + np.log(a @ A[:, end])
+
+
+def test_dense_c5_4096_states(monkeypatch):
+    """c5 at its BASELINE size (BASELINE.json configs[4]: 4096 states, full
+    transition matrix, every state emits every one of 16 symbols; 4096
+    strings, L ~ 32): the posterior count identities of the 1024-state test,
+    LL = p . log q, 8 strings against a numpy restatement of the forward
+    (the C oracle's trellis takes minutes per string at this size), and the
+    device-resident QN loop (4096 constraints of 4097 members: the strided
+    QN path) against the host QN update for two steps"""
+    import wfsa_amd as W
+    syn = W.Synthetic(n_states=4096, degree=1, vocab=16, emissions=16, dense=True, n_strings=4096, max_len=128,
+                      seed=2)
+    sym, off, wt = syn.corpus()
+    fsa = W.Fsa.read_text(syn.wfsa_text)
+    n_par = fsa.counts()["parameters"]
+    p = wt / wt.sum()
+    dev = _device(fsa, sym, off, p, monkeypatch, dense=True)
+    rec, pc, used = dev.recognize()
+    assert rec.all()
+    rng = np.random.default_rng(11)
+    w = rng.normal(-8.5, 1.0, size=n_par)
+    ll, grad, logq = dev.objective_grad(w)
+    assert np.isfinite(logq).all()
+    assert _close(ll, float(np.dot(p, logq)), rel=1e-12)
+    A, E, start, end, kind = _dense_tables(fsa, w)
+    assert (kind >= 0).all()
+    L = np.diff(off).astype(np.float64)
+    assert _close(grad[kind == 1].sum(), -1.0, rel=1e-10)
+    assert _close(grad[kind == 2].sum(), -1.0, rel=1e-10)
+    assert _close(grad[kind == 0].sum(), -float(np.dot(p, L)), rel=1e-10)
+    assert _close(grad[kind == 3].sum(), -float(np.dot(p, L - 1)), rel=1e-10)
+    for i in np.sort(rng.choice(len(wt), size=8, replace=False)):
+        assert _close(logq[i], _dense_logq(A, E, start, end, sym[off[i]:off[i + 1]]), rel=1e-11)
+    del dev, A, E
+    a, b = W.QuasiNewtonLearner(0), W.QuasiNewtonLearner(0)
+    for lrn in (a, b):
+        lrn.BuildFromPacked(fsa, sym, off, wt)
+        lrn.Finalize()
+        lrn.Init(7)
+        assert lrn.stats()["dense"] == 1
+    rows_a = a.Run(2, 1.0, -1.0)
+    rows_b = [b.OptimizationStep(1.0, -1.0)[0] for _ in range(2)]
+    for r, q in zip(rows_a, rows_b):
+        for u, v in zip(r[:5], q[:5]):
+            assert _close(u, v, rel=1e-9, atol=1e-12)
+    np.testing.assert_allclose(a.x(), b.x(), rtol=1e-9, atol=1e-11)

@@ -114,6 +114,7 @@ public:
 
     // accessors used by the C-ABI / tests
     const std::vector<double>& GetP() const { return p; }
+    const std::vector<double>& GetLastGradient() const { return grad_cache; }   // trimmed, last evaluation
     const std::vector<double>& GetLogQ();           // fetches log q from the device
     const std::vector<int32_t>& GetTrimmedIndex() const { return trimmed_weights; }
     const std::vector<double>& GetPathCounts() const { return path_count_local; }   // per local corpus string

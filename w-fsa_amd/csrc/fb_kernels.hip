@@ -890,17 +890,21 @@ __global__ __launch_bounds__(1024) void fbc_kernel(CompiledArgs a) {
     const uint4 pad = make_uint4(0xffffffffu, 0xffffffffu, 0xffffffffu, 0xffffffffu);
     double ll_acc = 0.0;
 
+    // the gradient pass runs one wavefront per block: its accumulation (LDS,
+    // or the block's own slab in HBM) sees one instruction stream, so the
+    // slabs -- summed in slab order afterwards -- are the same bits every time
+    double* gslab = a.gpart + size_t(blockIdx.x) * size_t(a.n_params);
     auto apply = [&](int j_single, int g_multi, double p, double& acc) {
         if (j_single >= 0) {
             acc += wsrc[j_single];
             if (G_LDS) block_add(&gacc[j_single], -p);
-            else if (GRAD) global_add(&a.grad[j_single], -p);
+            else if (GRAD) global_add(&gslab[j_single], -p);
         } else if (g_multi >= 0) {
             for (int q = a.m.pptr[g_multi]; q < a.m.pptr[g_multi + 1]; ++q) {
                 const int j = a.m.pidx[q];
                 acc += wsrc[j];
                 if (G_LDS) block_add(&gacc[j], -p);
-                else if (GRAD) global_add(&a.grad[j], -p);
+                else if (GRAD) global_add(&gslab[j], -p);
             }
         }
     };
@@ -955,10 +959,9 @@ __global__ __launch_bounds__(1024) void fbc_kernel(CompiledArgs a) {
     }
     ll_acc = wave_sum(ll_acc);
     if (lane == 0) a.ll_part[gw] = ll_acc;
-    if (G_LDS) {   // this block's partial gradient, summed by the tail kernel
+    if (G_LDS) {   // this block's partial gradient, summed by slab_sum_kernel
         __syncthreads();
-        double* slab = a.gpart + size_t(blockIdx.x) * size_t(a.n_params);
-        for (int j = int(threadIdx.x); j < a.n_params; j += int(blockDim.x)) slab[j] = gacc[j];
+        for (int j = int(threadIdx.x); j < a.n_params; j += int(blockDim.x)) gslab[j] = gacc[j];
     }
 }
 
@@ -1196,15 +1199,8 @@ __global__ __launch_bounds__(1024, (DBG == 10 ? 8 : 1)) void fbs_kernel(Compiled
     const int bid = int(blockIdx.x);
     const int w = int(threadIdx.x) / kWave;
     const int gw = __builtin_amdgcn_readfirstlane(bid * wpb + w);
-    const unsigned halted = a.halted ? *a.halted : 0u;   // (before the finish may set it)
-    // the previous QN step's finish runs after this wave's streams: at the
-    // start it held the whole block at the table staging barrier (~5 us on
-    // the kernel's critical path); the load balancer gives the wave fewer rows
-    const bool fin_here = a.fin_on && gw == a.fin_wave;
-    if (halted || DBG == 5) {
-        if (fin_here) qn_finish_wave(a.fin);
-        return;
-    }
+    // halted is written only by an earlier launch (the QN step's finish)
+    if ((a.halted && *a.halted) || DBG == 5) return;
     const uint32_t zslot = uint32_t(a.n_params);
     // this wave's run of chunk rows
     const int g0 = a.wave_first[gw], g1 = a.wave_first[gw + 1];
@@ -1352,7 +1348,6 @@ __global__ __launch_bounds__(1024, (DBG == 10 ? 8 : 1)) void fbs_kernel(Compiled
         for (int i = 0; i < wpb; ++i) t += wsum[i];
         a.ll_part[bid] = t;
     }
-    if (fin_here) qn_finish_wave(a.fin);   // reads the other half of ll_part (steps alternate)
     // this block's slice of the per-edge weights and the zeroed result, for
     // the kernels after this one (nothing in this launch reads them)
     if (W_LDS) edge_weight_slice(a, bid, nblk);
@@ -1383,7 +1378,14 @@ __global__ __launch_bounds__(256) void publish_kernel(const double* out, Publish
     const int n2 = (pub.n + 1) / 2;
     const double2* src = reinterpret_cast<const double2*>(out);
     double2* dst = reinterpret_cast<double2*>(pub.host_out);
-    for (int i = int(threadIdx.x); i < n2; i += int(blockDim.x)) dst[i] = src[i];
+    for (int i = int(threadIdx.x); i < n2; i += int(blockDim.x)) {
+        double2 v = src[i];
+        if (pub.add) {   // out[1 + j] += add[j]: add[2i - 1], add[2i]
+            if (2 * i >= 1 && 2 * i - 1 < pub.n - 1) v.x += pub.add[2 * i - 1];
+            if (2 * i < pub.n - 1) v.y += pub.add[2 * i];
+        }
+        dst[i] = v;
+    }
     __threadfence_system();
     __syncthreads();
     if (threadIdx.x == 0) {
@@ -1393,50 +1395,57 @@ __global__ __launch_bounds__(256) void publish_kernel(const double* out, Publish
     }
 }
 
-__global__ __launch_bounds__(256) void tail_kernel(TailArgs a) {
+// Per-iteration reduction (ReduceArgs): a block per tile of consecutive
+// parameters in slot order, one more for the log-likelihood.  No atomics.
+__global__ __launch_bounds__(kReduceBlock) void reduce_kernel(ReduceArgs a) {
     if (a.halted && *a.halted) return;
-    const int n_tiles = (a.n_params + 255) / 256;
-    const int n_slab_groups = (a.n_gpart + kTailSlabs - 1) / kTailSlabs;
-    const int n_param_blocks = n_tiles * n_slab_groups;
-    const int n_chunk_blocks = (a.n_chunks + 3) / 4;
-    const int b = int(blockIdx.x);
-    if (b < n_param_blocks) {             // column sums of kTailSlabs partial slabs
-        const int j = (b % n_tiles) * 256 + int(threadIdx.x);
-        const int k0 = (b / n_tiles) * kTailSlabs;
-        if (j < a.n_params) {
-            const int k1 = min(a.n_gpart, k0 + kTailSlabs);
-            double s = 0.0;
-            for (int k = k0; k < k1; ++k) s += a.gpart[size_t(k) * size_t(a.n_params) + size_t(j)];
-            if (s != 0.0) global_add(&a.out[1 + j], s);
-        }
-    } else if (b < n_param_blocks + n_chunk_blocks) {   // bubble contributions, contiguous runs
-        const int c = (b - n_param_blocks) * 4 + int(threadIdx.x) / kWave;
-        if (c < a.n_chunks) {
-            const int lane = lane_id();
-            const int k0 = a.chunk_ptr[c], k1 = a.chunk_ptr[c + 1];
-            static_assert(kBubbleGradChunk <= 8 * kWave, "run longer than one load round");
-            double v[8];
-#pragma unroll
-            for (int r = 0; r < 8; ++r) v[r] = a.contrib[min(k0 + lane + r * kWave, k1 - 1)];
-            double s = 0.0;
-#pragma unroll
-            for (int r = 0; r < 8; ++r)
-                if (k0 + lane + r * kWave < k1) s += v[r];
-            s = wave_sum(s);
-            if (lane == 0) global_add(&a.out[1 + a.chunk_param[c]], s);
-        }
-    } else {                              // log-likelihood, fixed order
-        __shared__ double red[256];
-        double s = 0.0;
-        s = strided_sum(a.ll_part, a.n_ll, int(threadIdx.x), 256);
-        red[threadIdx.x] = s;
+    const int t = int(threadIdx.x);
+    const int tb = int(blockIdx.x);
+    if (tb == a.n_tiles) {   // log-likelihood, fixed order
+        __shared__ double red[kReduceBlock];
+        red[t] = strided_sum(a.ll_part, a.n_ll, t, kReduceBlock);
         __syncthreads();
-        for (int w = 128; w > 0; w >>= 1) {
-            if (int(threadIdx.x) < w) red[threadIdx.x] += red[threadIdx.x + w];
+        for (int w = kReduceBlock / 2; w > 0; w >>= 1) {
+            if (t < w) red[t] += red[t + w];
             __syncthreads();
         }
-        if (threadIdx.x == 0) global_add(&a.out[0], red[0]);
+        if (t == 0) a.out[0] = red[0];
+        return;
     }
+    __shared__ int sp[kReduceTileParams + 1];
+    __shared__ double res[kReduceTileParams];
+    __shared__ SegScratch<kReduceBlock> sc;
+    const int p0 = a.tile_ptr[tb], ns = a.tile_ptr[tb + 1] - p0;
+    const int s0 = a.seg_ptr[p0];
+    if (a.contrib) {
+        for (int i = t; i <= ns; i += kReduceBlock) sp[i] = a.seg_ptr[p0 + i] - s0;
+        __syncthreads();
+        seg_sums<kReduceBlock>(a.contrib + s0, sp, ns, seg_piece(sp[ns], kReduceBlock), res, sc);
+    }
+    for (int i = t; i < ns; i += kReduceBlock) {
+        const int j = a.param_at[p0 + i];
+        double v = a.out[1 + j];
+        if (a.fixed) v += a.fixed[j];
+        if (a.contrib) v += res[i];
+        a.out[1 + j] = v;
+    }
+}
+
+// out[1 + j] = sum of the preparation-time gradient slabs, in slab order
+__global__ __launch_bounds__(256) void slab_sum_kernel(const double* __restrict__ gpart, int32_t n_slabs,
+                                                      int32_t n_params, double* __restrict__ out) {
+    const int j = int(blockIdx.x) * 256 + int(threadIdx.x);
+    if (j >= n_params) return;
+    double s = 0.0;
+    for (int k0 = 0; k0 < n_slabs; k0 += 8) {
+        double v[8];
+#pragma unroll
+        for (int b = 0; b < 8; ++b) v[b] = gpart[size_t(min(k0 + b, n_slabs - 1)) * size_t(n_params) + size_t(j)];
+#pragma unroll
+        for (int b = 0; b < 8; ++b)
+            if (k0 + b < n_slabs) s += v[b];
+    }
+    out[1 + j] = s;
 }
 
 // host-mapped weights -> device, 16-byte loads (both buffers padded to even)
@@ -1777,10 +1786,15 @@ hipError_t launch_bubbles(const BubbleArgs& a, hipStream_t stream) {
     return hipGetLastError();
 }
 
-hipError_t launch_tail(const TailArgs& a, hipStream_t stream) {
-    const int blocks = (a.n_params + 255) / 256 * ((a.n_gpart + kTailSlabs - 1) / kTailSlabs) +
-                       (a.n_chunks + 3) / 4 + 1;
-    hipLaunchKernelGGL(tail_kernel, dim3(unsigned(blocks)), dim3(256), 0, stream, a);
+hipError_t launch_reduce(const ReduceArgs& a, hipStream_t stream) {
+    hipLaunchKernelGGL(reduce_kernel, dim3(unsigned(a.n_tiles + 1)), dim3(kReduceBlock), 0, stream, a);
+    return hipGetLastError();
+}
+
+hipError_t launch_slab_sum(const double* gpart, int32_t n_slabs, int32_t n_params, double* out, hipStream_t stream) {
+    if (n_params <= 0 || n_slabs <= 0) return hipSuccess;
+    hipLaunchKernelGGL(slab_sum_kernel, dim3(unsigned((n_params + 255) / 256)), dim3(256), 0, stream, gpart, n_slabs,
+                       n_params, out);
     return hipGetLastError();
 }
 

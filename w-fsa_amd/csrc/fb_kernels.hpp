@@ -249,27 +249,29 @@ struct HfArgs {
 constexpr int kHfBlock = 256;   // four bubbles per block
 hipError_t launch_hf(const HfArgs& a, hipStream_t stream);
 
-// Device-resident QuasiNewton step (qn_kernel.hip): qn_update (wavefront per
-// constraint) updates x and lambda from out = [LL, grad_full] and writes the
-// next w_full; the finish (qn_finish_wave, qn_device.hpp) reduces the info
-// row [KL, graderr, g_min, g_max, lambda_min, 0, 0, status] into a
-// host-mapped ring slot and bumps the completion flag.  The finish of step k
-// runs in one wave of step k+1's stream kernel (or a trailing one-wave kernel).
+// Device-resident QuasiNewton step (qn_kernel.hip): qn_step_kernel, one
+// block per constraint, completes the gradient of the constraint's members
+// (the traversal tiers' part in out, the constant trivial-word part, and --
+// fused -- the sums of their bubble contribution slots in a fixed order),
+// updates x and lambda, writes the next w_full, and leaves its partial
+// (g, g, lambda, graderr) for the last block to arrive (an arrival ticket),
+// which reduces the info row [KL, graderr, g_min, g_max, lambda_min, rmin,
+// rmin string, status] into a host-mapped ring slot and bumps the flag.
 constexpr int kQnRow = 8;
 constexpr unsigned kQnRan = 0, kQnHalted = 1, kQnNonFinite = 2, kQnSkipped = 3;
+constexpr int kQnBlock = 256;
+constexpr int kQnMaxSeg = 1024;   // members of a constraint the fused kernel keeps in LDS
 struct QnArgs {
-    const double* out;           // [1 + n_full]
-    // without a communicator the tail kernel is skipped: the gradient is
-    // out[1+j] + fixed[j] (bubble/fallback atomics + the constant trivial
-    // part) and the log-likelihood the sum of ll_part[0, n_ll); else (null)
-    // out is final
-    const double* fixed;
-    const double* ll_part;
+    const double* out;           // [1 + n_full]: gradient parts accumulated so far; out[0] is the
+                                 // log-likelihood when ll_part is null
+    const double* fixed;         // [n_full] constant trivial-word gradient to add, or null
+    const double* contrib;       // fused: bubble contribution slots, or null
+    const int32_t* seg_ptr;      // fused: [n + 1] slot run of kept parameter i (trimmed order)
+    const double* ll_part;       // log-likelihood partials summed in a fixed order, or null
     int32_t n_ll;
     int32_t n_full, n, k;
     const int32_t* full_of;      // [n] full index of each kept parameter
     const int32_t* trim;         // [n_full] trimmed index / -1 / -2
-    const int32_t* ccol;         // [n] constraint of each parameter
     const int32_t* cptr;         // [k+1] constraint c owns parameters [cptr[c], cptr[c+1])
     double* x;
     double* lambda;
@@ -277,9 +279,8 @@ struct QnArgs {
     double* grad;
     double* w_full;              // [n_full + 1] (zero slot)
     double* ewp;                 // [n_full + 1] exp(w_full), for the bubble kernel
-    double* partial;             // [qn_update_blocks(k)][4]
-    int32_t n_partial;
-    double* ll_val;              // with the tail: out[0] (LL) copied by qn_update for the finish
+    double* partial;             // [max(k, 1)][4] block partials
+    unsigned* ticket;            // arrival counter (the last block resets it)
     double plogp, eta, tol;
     int32_t exp_lambda;
     int32_t ring_slot;           // ring slot of this step
@@ -366,14 +367,9 @@ struct CompiledArgs {
                              // else: >= 1 w staged in LDS, 0 global
     int32_t wide;
     int32_t with_grad;       // accumulate the (weight-independent) trivial-word gradient
-    // fin_on: wave fin_wave first runs the previous device-resident QN
-    // step's finish (given extra weight in the wave balance).  bub_on: the
-    // stream waves also evaluate the bubbles before their streams (no
-    // separate bubble kernel) -- the small ones one per lane from the first
-    // waves, the big ones one per wavefront from the last
-    QnArgs fin;
-    int32_t fin_on;
-    int32_t fin_wave;
+    // bub_on: the stream waves also evaluate the bubbles before their
+    // streams (no separate bubble kernel) -- the small ones one per lane from
+    // the first waves, the big ones one per wavefront from the last
     BubbleArgs bub;
     int32_t bub_on;
     int32_t multi;           // the automaton has multi-parameter (epsilon-composite) edges
@@ -394,35 +390,38 @@ struct CompiledArgs {
 };
 
 
-// The per-iteration tail, one launch: out[1+j] += sum over blocks of the
-// compiled kernel's partial gradients, += the bubble contributions of
-// parameter j (runs of at most kBubbleGradChunk contiguous slots, one
-// wavefront per run, so a hot parameter's long range is summed by many
-// waves), and out[0] = sum of the per-wave log-likelihood partials in a
-// fixed order.
-constexpr int kBubbleGradChunk = 512;
+// The per-iteration reduction, one launch, deterministic: parameters in
+// slot order are cut into tiles (consecutive positions, bounded slots); a
+// block per tile adds to out[1 + j] the constant trivial-word gradient (when
+// `fixed` is given) and the fixed-order sum of j's bubble contribution slots
+// (seg_sums, qn_device.hpp); one more block writes out[0] = the sum of the
+// log-likelihood partials in a fixed order.  No atomics: the same inputs give
+// the same bits on every launch.
+constexpr int kReduceBlock = 256;
+constexpr int kReduceTileParams = 1024;
+constexpr int kReduceTileSlots = 16384;
+struct ReduceArgs {
+    const double* contrib;       // bubble contribution slots, or null
+    const int32_t* seg_ptr;      // [n_pos + 1] slot run of the parameter at each position
+    const int32_t* param_at;     // [n_pos] full parameter index at each position
+    const int32_t* tile_ptr;     // [n_tiles + 1] position range of each tile
+    int32_t n_tiles;
+    const double* fixed;         // [n_params] added when non-null
+    const double* ll_part;
+    int32_t n_ll;
+    double* out;                 // [1 + n_params]
+    const unsigned* halted;
+};
 // Completion without a DMA copy or a stream synchronisation: a one-block
-// kernel copies out[0, n) into host-mapped memory, fences at system scope and
-// then stores the next sequence number into a host-mapped flag the host polls.
+// kernel copies out[0, n) into host-mapped memory (adding `add` to out[1..]
+// when given), fences at system scope and then stores the next sequence
+// number into a host-mapped flag the host polls.
 struct Publish {
     double* host_out;            // host-mapped [n rounded up to even]
     int32_t n;
+    const double* add;           // [n - 1] added to out[1 ..] (the all-reduced constant gradient), or null
     unsigned* seq;               // device sequence counter
     unsigned* host_flag;         // host-mapped: last published sequence number
-};
-constexpr int kTailSlabs = 8;    // partial slabs summed per thread
-struct TailArgs {
-    const double* gpart;         // [n_gpart][n_params]
-    int32_t n_gpart;
-    const int32_t* chunk_param;  // [n_chunks]
-    const int32_t* chunk_ptr;    // [n_chunks+1] contiguous runs of contrib
-    const double* contrib;
-    int32_t n_chunks;
-    const double* ll_part;
-    int32_t n_ll;
-    int32_t n_params;
-    double* out;                 // [1 + n_params]
-    const unsigned* halted;
 };
 
 // sum of p[t], p[t + nt], p[t + 2 nt], ... below n, in that order, with the
@@ -449,16 +448,17 @@ constexpr int kBubbleBlock = 128;
 // waves: n_big (one per big bubble) + ceil(n_small / 64)
 int bubble_waves(int32_t n_small, int32_t n_big);
 hipError_t launch_bubbles(const BubbleArgs& a, hipStream_t stream);
-hipError_t launch_tail(const TailArgs& a, hipStream_t stream);
+hipError_t launch_reduce(const ReduceArgs& a, hipStream_t stream);
+// out[1 + j] = sum over k of gpart[k][j] in k order (the preparation-time gradient slabs)
+hipError_t launch_slab_sum(const double* gpart, int32_t n_slabs, int32_t n_params, double* out, hipStream_t stream);
 // out[0, n) -> host-mapped memory, then the flag (one block)
 hipError_t launch_publish(const double* out, const Publish& pub, hipStream_t stream);
 // host-mapped weights w[0, n) and the zero slot w[n] -> device, with
 // ewp = exp(w) (all buffers padded to an even count)
 hipError_t launch_stage(const double* host_w, double* w, double* ewp, int32_t n, hipStream_t stream);
-// also zeroes out[0..n_out) (the accumulators of this iteration)
-int qn_update_blocks(int32_t k);
-hipError_t launch_qn_update(const QnArgs& a, hipStream_t stream);
-hipError_t launch_qn_finish(const QnArgs& a, hipStream_t stream);
+// fused: the member gradients include the bubble slot sums (every constraint
+// has at most kQnMaxSeg members); grid max(k, 1)
+hipError_t launch_qn_step(const QnArgs& a, bool fused, hipStream_t stream);
 hipError_t launch_qn_weights(const double* x, const int32_t* trim, int32_t n_full, double* w_full, double* ewp,
                              hipStream_t stream);
 hipError_t launch_edge_weights(const double* w_full, const int32_t* pptr, const int32_t* pidx, double* lw,

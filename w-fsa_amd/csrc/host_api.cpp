@@ -345,6 +345,13 @@ int wfsa_learner_get_x(wfsa_learner* l, double* x) {
     return WFSA_OK;
 }
 
+int wfsa_learner_get_grad(wfsa_learner* l, double* grad) {
+    if (!l || !grad) return null_arg("learner/grad");
+    const auto& g = l->base->GetLastGradient();
+    std::memcpy(grad, g.data(), g.size() * sizeof(double));
+    return WFSA_OK;
+}
+
 int wfsa_learner_set_x(wfsa_learner* l, const double* x) {
     if (!l || !x) return null_arg("learner/x");
     l->base->SetWeights(x);

@@ -1,6 +1,5 @@
-// Device helpers shared by the QN kernels and the stream kernel: wave
-// reductions and the finish of a device-resident QuasiNewton step (the info
-// row from qn_update's per-block partials, the halt decision, publication).
+// Device helpers shared by the QN step kernel and the reduction kernel: wave
+// reductions and the deterministic segmented sum of bubble contribution slots.
 #pragma once
 
 #include <hip/hip_runtime.h>
@@ -19,74 +18,80 @@ __device__ inline double wave_reduce(double v, int op) {   // op 0 min, 1 max, 2
     return v;
 }
 
-// The finish of one step by one wavefront (it runs inside the next step's
-// stream kernel, beside the streams, or as its own one-wave launch).
-__device__ inline void qn_finish_wave(const QnArgs& a) {
-    const int lane = int(threadIdx.x) & 63;
-    const unsigned state = *a.halted;
-    double gmin = INFINITY, gmax = -INFINITY, lmin = INFINITY, gerr = 0.0, ll = 0.0;
-    if (state == 0) {
-        for (int b = lane; b < a.n_partial; b += 64) {
-            const double* p = a.partial + size_t(b) * 4;
-            gmin = fmin(gmin, p[0]);
-            gmax = fmax(gmax, p[1]);
-            lmin = fmin(lmin, p[2]);
-            gerr = fmax(gerr, p[3]);
+// Deterministic per-segment sums over one contiguous run of bubble
+// contribution slots (the runs of consecutive parameters in slot order).
+// Segment q of nseg owns v[sp[q], sp[q+1]) (sp relative, sp[0] = 0, in LDS).
+// The block's NT threads cut the run into pieces of C consecutive slots,
+// thread t the t-th; a thread sums its piece segment by segment in slot
+// order (a segment wholly inside the piece is written at once), and a
+// segment that crosses pieces is completed by adding its piece partials in
+// thread order.  The order of every addition depends only on the segment
+// lengths and C, never on timing: the same inputs give the same bits.
+template <int NT>
+struct SegScratch {
+    double pf[NT], pl[NT];   // partial of the piece's first / last segment
+    int fs[NT], ls[NT];      // the piece's first / last segment (-1: empty piece)
+};
+
+// C: slots per piece, at least ceil(sp[nseg] / NT)
+__device__ inline int seg_piece(int total, int nt) { return max((total + nt - 1) / nt, 16); }
+
+template <int NT>
+__device__ void seg_sums(const double* __restrict__ v, const int* sp, int nseg, int C, double* res,
+                         SegScratch<NT>& sc) {
+    const int t = int(threadIdx.x);
+    const int total = sp[nseg];
+    for (int q = t; q < nseg; q += NT) res[q] = 0.0;
+    __syncthreads();
+    const int a0 = t * C, a1 = min(a0 + C, total);
+    int f = -1, q = -1;
+    double p0 = 0.0, acc = 0.0;
+    if (a0 < a1) {
+        int lo = 0, hi = nseg;   // the segment holding slot a0: last q with sp[q] <= a0
+        while (hi - lo > 1) {
+            const int mid = (lo + hi) >> 1;
+            if (sp[mid] <= a0) lo = mid; else hi = mid;
         }
-        if (a.ll_part) ll = strided_sum(a.ll_part, a.n_ll, lane, 64);
-    }
-    double rv = INFINITY, ri = -1.0;   // rmin column from block minima, ties to the lower string
-    if (state == 0 && a.rmin_part)
-        for (int b = lane; b < a.rmin_n_part; b += 64) {
-            const double v = a.rmin_part[2 * b], i = a.rmin_part[2 * b + 1];
-            if (v < rv || (v == rv && i < ri)) {
-                rv = v;
-                ri = i;
+        q = f = lo;
+        int nxt = sp[q + 1];
+        for (int s0 = a0; s0 < a1; s0 += 8) {
+            double x[8];
+#pragma unroll
+            for (int b = 0; b < 8; ++b) x[b] = v[min(s0 + b, a1 - 1)];
+#pragma unroll
+            for (int b = 0; b < 8; ++b) {
+                const int s = s0 + b;
+                if (s >= a1) break;
+                while (s >= nxt) {   // segment q ends inside this piece
+                    if (q == f) p0 = acc; else res[q] = acc;
+                    acc = 0.0;
+                    ++q;
+                    nxt = sp[q + 1];
+                }
+                acc += x[b];
             }
         }
-    for (int o = 32; o > 0; o >>= 1) {
-        const double v = __shfl_xor(rv, o, 64), i = __shfl_xor(ri, o, 64);
-        if (v < rv || (v == rv && i < ri)) {
-            rv = v;
-            ri = i;
+        if (q == f) p0 = acc;
+    }
+    sc.pf[t] = p0;
+    sc.pl[t] = acc;
+    sc.fs[t] = f;
+    sc.ls[t] = q;
+    __syncthreads();
+    for (int k = t; k < nseg; k += NT) {
+        const int b0 = sp[k], b1 = sp[k + 1];
+        if (b0 == b1) continue;
+        const int ta = b0 / C, tb = (b1 - 1) / C;
+        if (ta == tb) {
+            if (k == sc.fs[ta]) res[k] = sc.pf[ta];
+            else if (k == sc.ls[ta]) res[k] = sc.pl[ta];   // (else written by the piece itself)
+        } else {   // k is the last segment of piece ta and the first of tb
+            double s = sc.pl[ta];
+            for (int u = ta + 1; u < tb; ++u) s += sc.pf[u];
+            res[k] = s + sc.pf[tb];
         }
     }
-    gmin = wave_reduce(gmin, 0);
-    gmax = wave_reduce(gmax, 1);
-    lmin = wave_reduce(lmin, 0);
-    gerr = wave_reduce(gerr, 1);
-    ll = wave_reduce(ll, 2);
-    if (lane == 0) {
-        unsigned status = kQnSkipped;
-        double info[7] = {0, 0, 0, 0, 0, 0, 0};
-        if (state == 0) {
-            if (a.k == 0) gmin = gmax = lmin = 0.0;
-            info[0] = a.plogp - (a.ll_part ? ll : *a.ll_val);
-            info[1] = gerr;
-            info[2] = gmin;
-            info[3] = gmax;
-            info[4] = lmin;
-            if (a.rmin_part) {
-                info[5] = ri >= 0.0 ? exp(rv) : 0.0;
-                info[6] = ri;
-            } else if (a.rmin) {
-                info[5] = a.rmin[0];
-                info[6] = a.rmin[1];
-            }
-            bool finite = true;
-            for (int i = 0; i < 7; ++i) finite = finite && isfinite(info[i]);
-            const bool halt = gerr <= a.tol && fabs(gmin) <= a.tol && fabs(gmax) <= a.tol;
-            status = !finite ? kQnNonFinite : (halt ? kQnHalted : kQnRan);
-        }
-        double* row = a.host_ring + size_t(a.ring_slot) * kQnRow;
-        for (int i = 0; i < 7; ++i) row[i] = info[i];
-        row[7] = double(status);
-        if (status == kQnHalted || status == kQnNonFinite) *a.halted = status;
-        const unsigned v = *a.seq + 1u;
-        *a.seq = v;
-        // the system-scope release orders the row before the flag
-        __hip_atomic_store(a.host_flag, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-    }
+    __syncthreads();
 }
 
 }  // namespace wfsa

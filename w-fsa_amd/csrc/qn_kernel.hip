@@ -3,13 +3,19 @@
 // with ComputeExpX :53-56, ComputeG :148-160, ComputeLambdaNext :127-146,
 // Learner::LambdaUpdate src/Learner.cpp:438-462, HaltCondition :88-91 and
 // GetOptimizationInfo :68-86) after the objective/gradient kernels of the
-// same step: qn_update (wave per constraint) + qn_finish (one wave).  It keeps x, lambda and the next step's w_full in
-// HBM, so consecutive steps need nothing from the host; each step publishes
-// its info row to host-mapped memory and bumps the completion flag.
+// same step, in ONE launch: qn_step_kernel, one block per constraint, and the
+// step's finish by the last block to arrive.  It keeps x, lambda and the next
+// step's w_full in HBM, so consecutive steps need nothing from the host; each
+// step publishes its info row to host-mapped memory and bumps the flag.
+//
+// Fused form: the members' gradients are completed here from the bubble
+// contribution slots (the slots are laid out in trimmed-parameter order, so a
+// constraint's members own one contiguous run, summed by seg_sums in a fixed
+// order) -- no separate reduction launch.
 //
 // The arithmetic follows the host code operation for operation (the same
 // summation orders, no FMA contraction) so the device and host trajectories
-// agree to the last bits up to exp()'s rounding.
+// agree to the last bits up to exp()'s rounding and the gradient's summation.
 #include "fb_kernels.hpp"
 #include "qn_device.hpp"
 
@@ -25,86 +31,109 @@ namespace wfsa {
 
 namespace {
 
-constexpr int kQnUpdateBlock = 256;   // four constraints (one wavefront each) per block
+constexpr int kW = kQnBlock / 64;
 
-__device__ __forceinline__ void wave_sync() {
-    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+// the info row of a step into its host ring slot, then the flag; the
+// system-scope release orders the row before the flag
+__device__ void publish_row(const QnArgs& a, const double* info, unsigned status) {
+    double* row = a.host_ring + size_t(a.ring_slot) * kQnRow;
+    for (int i = 0; i < 7; ++i) row[i] = info ? info[i] : 0.0;
+    row[7] = double(status);
+    const unsigned v = *a.seq + 1u;
+    *a.seq = v;
+    __hip_atomic_store(a.host_flag, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
-// qn_update: one wavefront per constraint.  Every quantity of the update is
-// local to a constraint (its members are a contiguous, ascending range of
-// parameters), so waves are independent; each block writes its partial
-// (g_min, g_max, lambda_min, graderr) and qn_finish reduces them.  Up to 64
-// members: lane m owns member m (exp and the x update); g and the
-// lambda_next numerator are summed by lane 0 in member order, as the host
-// does.  Larger groups stride their members over the lanes.
-__global__ __launch_bounds__(kQnUpdateBlock) void qn_update_kernel(QnArgs a) {
-    if (*a.halted) return;
-    constexpr int W = kQnUpdateBlock / 64;
-    __shared__ double sh_ev[W][64], sh_gv[W][64];
-    __shared__ double sh_bc[W][2];
-    __shared__ double red[W][4];
-    const int lane = int(threadIdx.x) & 63, w = int(threadIdx.x) >> 6;
-    const int c = int(blockIdx.x) * W + w;
-    double gmin = INFINITY, gmax = -INFINITY, lmin = INFINITY, gerr = 0.0;
-    if (c < a.k) {
+__device__ double block_reduce(double v, int op, double* red) {   // fixed tree, every thread gets the result
+    const int t = int(threadIdx.x);
+    v = wave_reduce(v, op);
+    __syncthreads();
+    if ((t & 63) == 0) red[t >> 6] = v;
+    __syncthreads();
+    double r = red[0];
+    for (int i = 1; i < kW; ++i) r = op == 0 ? fmin(r, red[i]) : (op == 1 ? fmax(r, red[i]) : r + red[i]);
+    return r;
+}
+
+template <bool FUSED>
+__global__ __launch_bounds__(kQnBlock) void qn_step_kernel(QnArgs a) {
+    const int t = int(threadIdx.x);
+    const int c = int(blockIdx.x);
+    // halted is written only by an earlier launch's finish: every block of
+    // this launch sees the same value
+    if (*a.halted) {   // a step enqueued after the halt: published as skipped
+        if (c == 0 && t == 0) publish_row(a, nullptr, kQnSkipped);
+        return;
+    }
+    __shared__ double sg[kQnMaxSeg], se[kQnMaxSeg];
+    __shared__ int sp[kQnMaxSeg + 1];
+    __shared__ SegScratch<kQnBlock> sc;
+    __shared__ double bc[2], red[kW];
+    __shared__ unsigned last;
+    double gerr = 0.0, g = 0.0, lam = 0.0;
+    const bool have = c < a.k;
+    if (have) {
         const int b = a.cptr[c], e = a.cptr[c + 1], nm = e - b;
-        const double lam = a.lambda[c];
-        double g, laux;
-        if (nm <= 64) {
-            double xi = 0.0, gi = 0.0;
-            int fo = 0;
-            if (lane < nm) {
-                xi = a.x[b + lane];
-                fo = a.full_of[b + lane];
-                gi = a.out[1 + fo] + (a.fixed ? a.fixed[fo] : 0.0);
+        lam = a.lambda[c];
+        double laux;
+        const bool slots = FUSED && a.contrib;
+        if (slots) {   // the members' bubble slot sums (the host guarantees nm <= kQnMaxSeg)
+            const int s0 = a.seg_ptr[b];
+            for (int i = t; i <= nm; i += kQnBlock) sp[i] = a.seg_ptr[b + i] - s0;
+            __syncthreads();
+            seg_sums<kQnBlock>(a.contrib + s0, sp, nm, seg_piece(sp[nm], kQnBlock), sg, sc);
+        }
+        if (nm <= kQnMaxSeg) {
+            for (int m = t; m < nm; m += kQnBlock) {
+                const int fo = a.full_of[b + m];
+                double gi = a.out[1 + fo];
+                if (a.fixed) gi += a.fixed[fo];
+                if (slots) gi += sg[m];
+                sg[m] = gi;
+                se[m] = exp(a.x[b + m]);
             }
-            const double ei = lane < nm ? exp(xi) : 0.0;
-            sh_ev[w][lane] = ei;
-            sh_gv[w][lane] = gi;
-            wave_sync();
-            if (lane == 0) {   // ComputeG, ComputeLambdaNext in member order
+            __syncthreads();
+            if (t == 0) {   // ComputeG, ComputeLambdaNext in member order
                 double gg = -1.0;
-                for (int m = 0; m < nm; ++m) gg += sh_ev[w][m];
+                for (int m = 0; m < nm; ++m) gg += se[m];
                 double r = lam * gg;
-                for (int m = 0; m < nm; ++m) r -= sh_gv[w][m];
-                sh_bc[w][0] = gg;
-                sh_bc[w][1] = r / (gg + 1.0);
+                for (int m = 0; m < nm; ++m) r -= sg[m];
+                bc[0] = gg;
+                bc[1] = r / (gg + 1.0);
             }
-            wave_sync();
-            g = sh_bc[w][0];
-            laux = sh_bc[w][1];
-            if (lane < nm) {   // graderr (old lambda), x update (lambda_next), next weights
+            __syncthreads();
+            g = bc[0];
+            laux = bc[1];
+            for (int m = t; m < nm; m += kQnBlock) {   // graderr (old lambda), x update (lambda_next)
+                const double gi = sg[m], ei = se[m];
                 const double aux = ei * lam;
-                gerr = fabs(gi + aux);
-                const double xn = xi - a.eta * ((gi + ei * laux) / aux);
-                a.x[b + lane] = xn;
-                a.grad[b + lane] = gi;
+                gerr = fmax(gerr, fabs(gi + aux));
+                const double xn = a.x[b + m] - a.eta * ((gi + ei * laux) / aux);
+                const int fo = a.full_of[b + m];
+                a.x[b + m] = xn;
+                a.grad[b + m] = gi;
                 a.w_full[fo] = xn;   // GetWeight for the next step
                 a.ewp[fo] = exp(xn);
             }
-        } else {   // large groups (dense automata): members strided over the lanes,
-                   // lane sums combined by a fixed xor tree (deterministic; the
+        } else {   // large groups (dense automata; never fused): members strided
+                   // over the threads, sums by a fixed tree (deterministic; the
                    // host's member-order sums differ from it by rounding only)
             double gs = 0.0, gv = 0.0;
-            for (int i = b + lane; i < e; i += 64) {
+            for (int i = b + t; i < e; i += kQnBlock) {
                 const double ex = exp(a.x[i]);
                 const int fo = a.full_of[i];
-                const double gi = a.out[1 + fo] + (a.fixed ? a.fixed[fo] : 0.0);
+                double gi = a.out[1 + fo];
+                if (a.fixed) gi += a.fixed[fo];
                 a.expx[i] = ex;
                 a.grad[i] = gi;
                 gs += ex;
                 gv += gi;
             }
-            for (int o = 32; o > 0; o >>= 1) {
-                gs += __shfl_xor(gs, o, 64);
-                gv += __shfl_xor(gv, o, 64);
-            }
+            gs = block_reduce(gs, 2, red);
+            gv = block_reduce(gv, 2, red);
             g = -1.0 + gs;
             laux = (lam * g - gv) / (g + 1.0);
-            for (int i = b + lane; i < e; i += 64) {
+            for (int i = b + t; i < e; i += kQnBlock) {
                 const double ex = a.expx[i], gi = a.grad[i];
                 const double aux = ex * lam;
                 gerr = fmax(gerr, fabs(gi + aux));
@@ -114,43 +143,93 @@ __global__ __launch_bounds__(kQnUpdateBlock) void qn_update_kernel(QnArgs a) {
                 a.ewp[a.full_of[i]] = exp(xn);
             }
         }
-        if (lane == 0) {   // LambdaUpdate (src/Learner.cpp:438-462)
+        if (t == 0) {   // LambdaUpdate (src/Learner.cpp:438-462)
             const double d = lam - laux;
             a.lambda[c] = a.exp_lambda ? lam * exp(-a.eta * (d / lam)) : lam - a.eta * d;
         }
-        gmin = g;
-        gmax = g;
-        lmin = lam;
     }
-    for (int o = 32; o > 0; o >>= 1) gerr = fmax(gerr, __shfl_xor(gerr, o, 64));
-    if (lane == 0) {
-        red[w][0] = gmin;
-        red[w][1] = gmax;
-        red[w][2] = lmin;
-        red[w][3] = gerr;
+    gerr = block_reduce(gerr, 1, red);
+    // the block's partial, write-through, then the arrival ticket; the block
+    // whose arrival is the last finishes the step
+    if (t == 0) {
+        double* p = a.partial + size_t(c) * 4;
+        const double pv[4] = {have ? g : INFINITY, have ? g : -INFINITY, have ? lam : INFINITY, gerr};
+        for (int i = 0; i < 4; ++i) __hip_atomic_store(p + i, pv[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        const unsigned nb = gridDim.x;
+        last = __hip_atomic_fetch_add(a.ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == nb - 1u;
     }
     __syncthreads();
-    if (threadIdx.x == 0) {
-        if (blockIdx.x == 0 && !a.ll_part) *a.ll_val = a.out[0];   // the finish may run after out is reused
-        double r0 = red[0][0], r1 = red[0][1], r2 = red[0][2], r3 = red[0][3];
-        for (int v = 1; v < W; ++v) {
-            r0 = fmin(r0, red[v][0]);
-            r1 = fmax(r1, red[v][1]);
-            r2 = fmin(r2, red[v][2]);
-            r3 = fmax(r3, red[v][3]);
+    if (!last) return;
+    // finish: the info row from the block partials (write-through loads) and
+    // the log-likelihood partials (written by earlier launches), fixed order
+    double gmin = INFINITY, gmax = -INFINITY, lmin = INFINITY, ge = 0.0;
+    for (int j = t; j < int(gridDim.x); j += kQnBlock) {
+        const double* p = a.partial + size_t(j) * 4;
+        gmin = fmin(gmin, __hip_atomic_load(p + 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+        gmax = fmax(gmax, __hip_atomic_load(p + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+        lmin = fmin(lmin, __hip_atomic_load(p + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+        ge = fmax(ge, __hip_atomic_load(p + 3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+    }
+    gmin = block_reduce(gmin, 0, red);
+    gmax = block_reduce(gmax, 1, red);
+    lmin = block_reduce(lmin, 0, red);
+    ge = block_reduce(ge, 1, red);
+    double ll = a.ll_part ? strided_sum(a.ll_part, a.n_ll, t, kQnBlock) : 0.0;
+    ll = block_reduce(ll, 2, red);
+    double rv = INFINITY, ri = -1.0;   // rmin column from block minima, ties to the lower string
+    if (a.rmin_part)
+        for (int j = t; j < a.rmin_n_part; j += kQnBlock) {
+            const double v = a.rmin_part[2 * j], i = a.rmin_part[2 * j + 1];
+            if (v < rv || (v == rv && i < ri)) {
+                rv = v;
+                ri = i;
+            }
         }
-        double* p = a.partial + size_t(blockIdx.x) * 4;
-        p[0] = r0;
-        p[1] = r1;
-        p[2] = r2;
-        p[3] = r3;
+    for (int o = 32; o > 0; o >>= 1) {
+        const double v = __shfl_xor(rv, o, 64), i = __shfl_xor(ri, o, 64);
+        if (v < rv || (v == rv && i < ri)) {
+            rv = v;
+            ri = i;
+        }
+    }
+    __shared__ double rr[kW][2];
+    if ((t & 63) == 0) {
+        rr[t >> 6][0] = rv;
+        rr[t >> 6][1] = ri;
+    }
+    __syncthreads();
+    if (t == 0) {
+        for (int w = 1; w < kW; ++w)
+            if (rr[w][0] < rv || (rr[w][0] == rv && rr[w][1] < ri)) {
+                rv = rr[w][0];
+                ri = rr[w][1];
+            }
+        if (a.k == 0) gmin = gmax = lmin = 0.0;
+        double info[7];
+        info[0] = a.plogp - (a.ll_part ? ll : a.out[0]);
+        info[1] = ge;
+        info[2] = gmin;
+        info[3] = gmax;
+        info[4] = lmin;
+        info[5] = 0.0;
+        info[6] = 0.0;
+        if (a.rmin_part) {
+            info[5] = ri >= 0.0 ? exp(rv) : 0.0;
+            info[6] = ri;
+        } else if (a.rmin) {
+            info[5] = a.rmin[0];
+            info[6] = a.rmin[1];
+        }
+        bool finite = true;
+        for (int i = 0; i < 7; ++i) finite = finite && isfinite(info[i]);
+        const bool halt = ge <= a.tol && fabs(gmin) <= a.tol && fabs(gmax) <= a.tol;
+        const unsigned status = !finite ? kQnNonFinite : (halt ? kQnHalted : kQnRan);
+        if (status != kQnRan) *a.halted = status;   // read by the next launches only
+        *a.ticket = 0u;
+        publish_row(a, info, status);
     }
 }
-
-// qn_finish: the info row of the step (the reductions of qn_update's
-// partials and, without the tail kernel, of the per-wave log-likelihood
-// partials in a fixed order), the halt decision, then the publication.
-__global__ __launch_bounds__(64) void qn_finish_kernel(QnArgs a) { qn_finish_wave(a); }
 
 // initial w_full from x (qn_set_state)
 __global__ void qn_weights_kernel(const double* x, const int32_t* trim, int32_t n_full, double* w_full, double* ewp) {
@@ -168,18 +247,10 @@ __global__ void qn_weights_kernel(const double* x, const int32_t* trim, int32_t 
 
 }  // namespace
 
-int qn_update_blocks(int32_t k) {
-    constexpr int W = kQnUpdateBlock / 64;
-    return std::max(1, (k + W - 1) / W);
-}
-
-hipError_t launch_qn_update(const QnArgs& a, hipStream_t stream) {
-    hipLaunchKernelGGL(qn_update_kernel, dim3(unsigned(qn_update_blocks(a.k))), dim3(kQnUpdateBlock), 0, stream, a);
-    return hipGetLastError();
-}
-
-hipError_t launch_qn_finish(const QnArgs& a, hipStream_t stream) {
-    hipLaunchKernelGGL(qn_finish_kernel, dim3(1), dim3(64), 0, stream, a);
+hipError_t launch_qn_step(const QnArgs& a, bool fused, hipStream_t stream) {
+    const dim3 grid(unsigned(std::max(a.k, 1)));
+    if (fused) hipLaunchKernelGGL(qn_step_kernel<true>, grid, dim3(kQnBlock), 0, stream, a);
+    else hipLaunchKernelGGL(qn_step_kernel<false>, grid, dim3(kQnBlock), 0, stream, a);
     return hipGetLastError();
 }
 

@@ -99,7 +99,7 @@ struct DevBuf {
 constexpr int kLdsPerCu = 163840;
 constexpr int kNumCu = 256;
 constexpr int kWave = 64;
-constexpr int kCompiledBlock = 512;
+constexpr int kGradBlock = 64;   // the preparation-time gradient pass: one wavefront per block
 constexpr int kIterWavesPerCu = 16;   // per-iteration stream kernel
 constexpr int kQnDepth = 8;   // device-resident QN steps in flight
 constexpr int kTimingStride = 4;   // QN runs time every 4th step's kernels
@@ -165,13 +165,20 @@ struct wfsa_dev {
     DevBuf<double> fixed_grad;       // [n_params] gradient of the trivial words (constant)
     // bubbles
     int32_t n_bubbles = 0, n_small4 = 0, n_small = 0, n_big = 0, big_lds_edges = 2;
-    int32_t fin_wave = 0;   // the stream kernel's wave that runs the previous QN step's finish
     int b_waves = 0;
     DevBuf<int4> sm4_tbl, sm_tbl;
     DevBuf<int32_t> big_off, big_edge_base, big_eslot_ptr, big_eslot;
-    int32_t n_bg_chunks = 0;
-    DevBuf<int32_t> bub_off, bg_chunk_param, bg_chunk_ptr;
+    DevBuf<int32_t> bub_off;
     DevBuf<double> contrib;
+    // contribution slots: parameter-major in a slot order (position pos_of[j]
+    // of full parameter j; identity, or the trimmed order once the QN loop is
+    // set up, so a constraint's members own one contiguous run); seg_ptr by
+    // position, param_at its inverse, and the reduction's tiles
+    std::vector<int32_t> h_bubbuf, h_sm4_list, h_sm_list, h_big_list;   // host copies (re-layout)
+    std::vector<int32_t> slot_order;        // [n_params] pos_of used by the current layout
+    std::vector<int32_t> h_seg_ptr;
+    DevBuf<int32_t> seg_ptr, param_at, tile_ptr;
+    int32_t n_tiles = 0;
     std::vector<int32_t> h_pptr, h_pidx;   // host copy of the combined parameter lists
 
     size_t c_lds = 0;
@@ -235,7 +242,9 @@ struct wfsa_dev {
     DevBuf<int32_t> qn_trim, qn_full_of, qn_ccol, qn_cptr;
     int prep_gen = 0;
     DevBuf<double> qn_x, qn_lambda, qn_expx, qn_grad, qn_partial;
-    DevBuf<unsigned> qn_halted;
+    DevBuf<unsigned> qn_halted, qn_ticket;
+    std::vector<int32_t> qn_full_of_h, qn_cptr_h;
+    bool qn_fused = false;           // qn_step_kernel sums the members' bubble slots itself
     double* qn_ring = nullptr;       // host-mapped [kQnDepth][kQnRow]
     double* qn_ring_dev = nullptr;
 
@@ -394,7 +403,7 @@ int configure_tiers(wfsa_dev* ctx) {
 void drop_graph(wfsa_dev* ctx);
 
 int enqueue_compiled(wfsa_dev* ctx, bool with_grad, bool want_logq, const unsigned* halted = nullptr,
-                     int slot = -1, const wfsa::QnArgs* fin = nullptr);
+                     int slot = -1);
 wfsa::BubbleArgs bubble_args(wfsa_dev* ctx, bool want_logq, const unsigned* halted, double* ll_part);
 bool bubbles_fused(wfsa_dev* ctx, bool want_logq);
 // waves per block of the stream kernel that take the small bubbles (64 each)
@@ -460,6 +469,103 @@ int wait_published(wfsa_dev* ctx, unsigned want) {
         }
         __builtin_ia32_pause();
     }
+}
+
+// Contribution slots of the compiled bubbles in slot order pos_of (full
+// parameter j at position pos_of[j]): every (bubble edge, parameter) pair
+// gets a slot, parameter-major by position -- within a parameter small
+// bubbles, then big, in bubble order -- and the small-bubble tables / big
+// bubble slot lists are rebuilt to match; seg_ptr (by position), param_at and
+// the reduction's tiles follow.  Runs again when the QN loop moves the slots
+// into its trimmed order (wfsa_dev_qn_setup).
+int layout_slots(wfsa_dev* ctx, const std::vector<int32_t>& pos_of) {
+    hipStream_t s = ctx->stream;
+    const int32_t np = ctx->n_params;
+    const std::vector<int32_t>& bb = ctx->h_bubbuf;
+    auto edge_code_at = [&](int32_t o, int e) { return bb[size_t(o) + 4 + 2 * size_t(e)]; };
+    auto for_edge_params = [&](int32_t code, auto&& f) {   // the parameters of a bubble edge (edge_code)
+        if (code >= 0) {
+            if (code < np) f(code);
+        } else {
+            const int32_t g = -code - 2;
+            for (int32_t q = ctx->h_pptr[size_t(g)]; q < ctx->h_pptr[size_t(g) + 1]; ++q) f(ctx->h_pidx[size_t(q)]);
+        }
+    };
+    std::vector<int32_t> param_at(size_t(std::max(np, 1)), 0);
+    for (int32_t j = 0; j < np; ++j) param_at[size_t(pos_of[size_t(j)])] = j;
+    std::vector<int32_t> pc(size_t(np) + 1, 0);   // by position
+    for (const auto* list : {&ctx->h_sm4_list, &ctx->h_sm_list, &ctx->h_big_list})
+        for (int32_t o : *list)
+            for (int e = 0; e < (bb[size_t(o)] >> 16); ++e)
+                for_edge_params(edge_code_at(o, e), [&](int32_t jj) { pc[size_t(pos_of[size_t(jj)]) + 1]++; });
+    for (size_t q = 1; q < pc.size(); ++q) pc[q] += pc[q - 1];
+    std::vector<int32_t> fill(pc.begin(), pc.end() - 1);
+    if (ctx->n_bubbles > 0) {
+        // class tables: RE edges, quads = 1 + RE/2 + RE/4
+        auto build_table = [&](const std::vector<int32_t>& list, int RE, std::vector<int32_t>& tbl) {
+            const int Q = 1 + RE / 2 + RE / 4;
+            const size_t n = list.size();
+            tbl.assign(size_t(Q) * 4 * std::max<size_t>(n, 1), 0);
+            auto quad = [&](int k, size_t b) { return &tbl[(size_t(k) * n + b) * 4]; };
+            for (size_t b = 0; b < n; ++b) {
+                const int32_t o = list[b];
+                const int edges = bb[size_t(o)] >> 16;
+                for (int w = 0; w < 4; ++w) quad(0, b)[w] = bb[size_t(o) + size_t(w)];
+                for (int e = 0; e < RE; ++e) {
+                    int32_t code = np, sd = 0, sl = -1;   // padding edges: the zero-slot code
+                    if (e < edges) {
+                        code = edge_code_at(o, e);
+                        sd = bb[size_t(o) + 5 + 2 * size_t(e)];
+                        if (code < np) sl = fill[size_t(pos_of[size_t(code)])]++;
+                    }
+                    quad(1 + e / 2, b)[2 * (e & 1)] = code;
+                    quad(1 + e / 2, b)[2 * (e & 1) + 1] = sd;
+                    quad(1 + RE / 2 + e / 4, b)[e & 3] = sl;
+                }
+            }
+        };
+        std::vector<int32_t> tbl4, tbl;
+        build_table(ctx->h_sm4_list, 4, tbl4);
+        build_table(ctx->h_sm_list, wfsa::kBubbleRegEdges, tbl);
+        const int64_t nb = int64_t(ctx->h_big_list.size());
+        std::vector<int32_t> big_edge_base(size_t(std::max<int64_t>(nb, 1)), 0), eslot_ptr(1, 0), eslot;
+        for (int64_t i = 0; i < nb; ++i) {
+            const int32_t o = ctx->h_big_list[size_t(i)];
+            big_edge_base[size_t(i)] = int32_t(eslot_ptr.size()) - 1;
+            for (int e = 0; e < (bb[size_t(o)] >> 16); ++e) {
+                for_edge_params(edge_code_at(o, e), [&](int32_t jj) { eslot.push_back(fill[size_t(pos_of[size_t(jj)])]++); });
+                eslot_ptr.push_back(int32_t(eslot.size()));
+            }
+        }
+        if (eslot.empty()) eslot.push_back(0);
+        HIP_TRY(ctx->sm4_tbl.upload(reinterpret_cast<const int4*>(tbl4.data()), tbl4.size() / 4, s));
+        HIP_TRY(ctx->sm_tbl.upload(reinterpret_cast<const int4*>(tbl.data()), tbl.size() / 4, s));
+        const std::vector<int32_t>& bl = ctx->h_big_list;
+        HIP_TRY(ctx->big_off.upload(bl.empty() ? eslot.data() : bl.data(), std::max<size_t>(bl.size(), 1), s));
+        HIP_TRY(ctx->big_edge_base.upload(big_edge_base.data(), big_edge_base.size(), s));
+        HIP_TRY(ctx->big_eslot_ptr.upload(eslot_ptr.data(), eslot_ptr.size(), s));
+        HIP_TRY(ctx->big_eslot.upload(eslot.data(), eslot.size(), s));
+        HIP_TRY(ctx->contrib.alloc(size_t(std::max(pc.back(), 1))));
+        HIP_TRY(hipMemsetAsync(ctx->contrib.ptr, 0, size_t(std::max(pc.back(), 1)) * sizeof(double), s));
+    }
+    // tiles of consecutive positions: at most kReduceTileParams parameters and
+    // (unless one parameter alone has more) kReduceTileSlots slots
+    std::vector<int32_t> tiles(1, 0);
+    for (int32_t q = 0; q < np;) {
+        int32_t e = q + 1;
+        while (e < np && e - q < wfsa::kReduceTileParams && pc[size_t(e) + 1] - pc[size_t(q)] <= wfsa::kReduceTileSlots) ++e;
+        tiles.push_back(e);
+        q = e;
+    }
+    ctx->n_tiles = int32_t(tiles.size()) - 1;
+    HIP_TRY(ctx->seg_ptr.upload(pc.data(), pc.size(), s));
+    HIP_TRY(ctx->param_at.upload(param_at.data(), param_at.size(), s));
+    HIP_TRY(ctx->tile_ptr.upload(tiles.data(), tiles.size(), s));
+    HIP_TRY(hipStreamSynchronize(s));
+    ctx->h_seg_ptr = std::move(pc);
+    ctx->slot_order = pos_of;
+    drop_graph(ctx);   // a captured evaluation holds the old tables
+    return WFSA_OK;
 }
 
 // Dense automata: no compilation; level 1 is the structural pass, one
@@ -668,8 +774,6 @@ int prepare(wfsa_dev* ctx, int level) {
         double small_cost = 32.0, big_cost = 8.0;
         if (const char* e = std::getenv("WFSA_SMALL_COST")) small_cost = std::atof(e);
         if (const char* e = std::getenv("WFSA_BIG_COST")) big_cost = std::atof(e);
-        double fin_cost = 8.0;
-        if (const char* e = std::getenv("WFSA_FIN_COST")) fin_cost = std::atof(e);
         int64_t n_b = 0, n_big_est = 0;
         for (int32_t i : comp) {
             n_b += h_nb[size_t(i)];
@@ -684,13 +788,6 @@ int prepare(wfsa_dev* ctx, int level) {
             const int bid = w / i_wpb, wib = w % i_wpb;
             if (wib < small_wpb && int64_t(bid) * small_wpb + wib < small_waves) load[size_t(w)] += small_cost;
             if ((nblk - 1 - bid) + int64_t(nblk) * (i_wpb - 1 - wib) < n_big_est) load[size_t(w)] += big_cost;
-        }
-        // the QN finish: the wave after the big bubbles' (in their order)
-        {
-            const int64_t r = std::min<int64_t>(n_big_est, i_nw - 1);
-            const int bid = nblk - 1 - int(r % nblk), wib = i_wpb - 1 - int(r / nblk);
-            ctx->fin_wave = bid * i_wpb + wib;
-            load[size_t(ctx->fin_wave)] += fin_cost;
         }
         using Item = std::pair<double, int32_t>;
         std::priority_queue<Item, std::vector<Item>, std::greater<Item>> heap;
@@ -794,10 +891,9 @@ int prepare(wfsa_dev* ctx, int level) {
     ctx->n_groups = G;
     ctx->n_compiled = nc;
 
-    // bubbles: small ones into the structure-of-arrays table, big ones kept
+    // bubbles: small ones into the structure-of-arrays tables, big ones kept
     // as records; every (bubble edge, parameter) pair gets a slot in the
-    // parameter-major contribution array, and runs of at most
-    // kBubbleGradChunk slots of one parameter form the tail's chunks
+    // parameter-major contribution array (layout_slots)
     ctx->n_bubbles = int32_t(nbub);
     ctx->n_small4 = ctx->n_small = ctx->n_big = 0;
     if (nbub > 0) {
@@ -805,17 +901,7 @@ int prepare(wfsa_dev* ctx, int level) {
         HIP_TRY(ctx->bub.download(h_bubbuf.data(), size_t(bwords), s));
         HIP_TRY(ctx->bub_off.download(h_off.data(), size_t(nbub), s));
         HIP_TRY(hipStreamSynchronize(s));
-        const int32_t np = ctx->n_params;
         auto edge_code_at = [&](int32_t o, int e) { return h_bubbuf[size_t(o) + 4 + 2 * size_t(e)]; };
-        // the parameters of a bubble edge from its code (edge_code)
-        auto for_edge_params = [&](int32_t code, auto&& f) {
-            if (code >= 0) {
-                if (code < np) f(code);
-            } else {
-                const int32_t g = -code - 2;
-                for (int32_t q = ctx->h_pptr[size_t(g)]; q < ctx->h_pptr[size_t(g) + 1]; ++q) f(ctx->h_pidx[size_t(q)]);
-            }
-        };
         std::vector<int32_t> small4, small, big;
         ctx->max_bub_nodes = 1;
         for (int32_t o : h_off) {
@@ -841,99 +927,46 @@ int prepare(wfsa_dev* ctx, int level) {
                 if (hn[v]) std::fprintf(stderr, " %zu:%lld", v, (long long)hn[v]);
             std::fprintf(stderr, "\n");
         }
-        // slots, parameter-major; within a parameter: small bubbles, then big
-        std::vector<int32_t> pc(size_t(np) + 1, 0);
-        for (const auto* list : {&small4, &small, &big})
-            for (int32_t o : *list)
-                for (int e = 0; e < (h_bubbuf[size_t(o)] >> 16); ++e)
-                    for_edge_params(edge_code_at(o, e), [&](int32_t jj) { pc[size_t(jj) + 1]++; });
-        for (size_t jj = 1; jj < pc.size(); ++jj) pc[jj] += pc[jj - 1];
-        std::vector<int32_t> fill(pc.begin(), pc.end() - 1);
-        const int64_t nb = int64_t(big.size());
-        // class tables: RE edges, quads = 1 + RE/2 + RE/4
-        auto build_table = [&](const std::vector<int32_t>& list, int RE, std::vector<int32_t>& tbl) {
-            const int Q = 1 + RE / 2 + RE / 4;
-            const size_t n = list.size();
-            tbl.assign(size_t(Q) * 4 * std::max<size_t>(n, 1), 0);
-            auto quad = [&](int k, size_t b) { return &tbl[(size_t(k) * n + b) * 4]; };
-            for (size_t b = 0; b < n; ++b) {
-                const int32_t o = list[b];
-                const int edges = h_bubbuf[size_t(o)] >> 16;
-                for (int w = 0; w < 4; ++w) quad(0, b)[w] = h_bubbuf[size_t(o) + size_t(w)];
-                for (int e = 0; e < RE; ++e) {
-                    int32_t code = np, sd = 0, sl = -1;   // padding edges: the zero-slot code
-                    if (e < edges) {
-                        code = edge_code_at(o, e);
-                        sd = h_bubbuf[size_t(o) + 5 + 2 * size_t(e)];
-                        if (code < np) sl = fill[size_t(code)]++;
-                    }
-                    quad(1 + e / 2, b)[2 * (e & 1)] = code;
-                    quad(1 + e / 2, b)[2 * (e & 1) + 1] = sd;
-                    quad(1 + RE / 2 + e / 4, b)[e & 3] = sl;
-                }
-            }
-        };
-        std::vector<int32_t> tbl4, tbl;
-        build_table(small4, 4, tbl4);
-        build_table(small, wfsa::kBubbleRegEdges, tbl);
-        std::vector<int32_t> big_edge_base(size_t(std::max<int64_t>(nb, 1)), 0), eslot_ptr(1, 0), eslot;
-        for (int64_t i = 0; i < nb; ++i) {
-            const int32_t o = big[size_t(i)];
-            big_edge_base[size_t(i)] = int32_t(eslot_ptr.size()) - 1;
-            for (int e = 0; e < (h_bubbuf[size_t(o)] >> 16); ++e) {
-                for_edge_params(edge_code_at(o, e), [&](int32_t jj) { eslot.push_back(fill[size_t(jj)]++); });
-                eslot_ptr.push_back(int32_t(eslot.size()));
-            }
-        }
-        if (eslot.empty()) eslot.push_back(0);
-        HIP_TRY(ctx->sm4_tbl.upload(reinterpret_cast<const int4*>(tbl4.data()), tbl4.size() / 4, s));
-        HIP_TRY(ctx->sm_tbl.upload(reinterpret_cast<const int4*>(tbl.data()), tbl.size() / 4, s));
-        HIP_TRY(ctx->big_off.upload(big.empty() ? h_off.data() : big.data(), std::max<size_t>(big.size(), 1), s));
-        HIP_TRY(ctx->big_edge_base.upload(big_edge_base.data(), big_edge_base.size(), s));
-        HIP_TRY(ctx->big_eslot_ptr.upload(eslot_ptr.data(), eslot_ptr.size(), s));
-        HIP_TRY(ctx->big_eslot.upload(eslot.data(), eslot.size(), s));
-        ctx->n_small4 = int32_t(small4.size());
-        ctx->n_small = int32_t(small.size());
-        ctx->n_big = int32_t(nb);
+        ctx->h_bubbuf = std::move(h_bubbuf);
+        ctx->h_sm4_list = std::move(small4);
+        ctx->h_sm_list = std::move(small);
+        ctx->h_big_list = std::move(big);
+        ctx->n_small4 = int32_t(ctx->h_sm4_list.size());
+        ctx->n_small = int32_t(ctx->h_sm_list.size());
+        ctx->n_big = int32_t(ctx->h_big_list.size());
         ctx->big_lds_edges = 2;
-        for (int32_t o : big) ctx->big_lds_edges = std::max(ctx->big_lds_edges, (h_bubbuf[size_t(o)] >> 16) + 1);
+        for (int32_t o : ctx->h_big_list) ctx->big_lds_edges = std::max(ctx->big_lds_edges, (ctx->h_bubbuf[size_t(o)] >> 16) + 1);
         ctx->big_lds_edges &= ~1;   // even
-        std::vector<int32_t> cparam, cptr;
-        for (int32_t jj = 0; jj < np; ++jj)
-            for (int32_t b = pc[size_t(jj)]; b < pc[size_t(jj) + 1]; b += wfsa::kBubbleGradChunk) {
-                cparam.push_back(jj);
-                cptr.push_back(b);
-            }
-        cptr.push_back(pc.back());
-        ctx->n_bg_chunks = int32_t(cparam.size());
-        if (!cparam.empty()) HIP_TRY(ctx->bg_chunk_param.upload(cparam.data(), cparam.size(), s));
-        HIP_TRY(ctx->bg_chunk_ptr.upload(cptr.data(), cptr.size(), s));
-        HIP_TRY(ctx->contrib.alloc(size_t(std::max(pc.back(), 1))));
-        HIP_TRY(hipMemsetAsync(ctx->contrib.ptr, 0, size_t(std::max(pc.back(), 1)) * sizeof(double), s));
         ctx->b_waves = wfsa::bubble_waves(ctx->n_small4 + ctx->n_small, ctx->n_big);
         HIP_TRY(hipStreamSynchronize(s));
     } else {
         ctx->b_waves = 0;
+        ctx->h_bubbuf.clear();
+        ctx->h_sm4_list.clear();
+        ctx->h_sm_list.clear();
+        ctx->h_big_list.clear();
+    }
+    {   // slot layout: the QN loop's trimmed order when it is set up, else the identity
+        std::vector<int32_t> order = ctx->slot_order;
+        if (order.size() != size_t(ctx->n_params)) {
+            order.resize(size_t(ctx->n_params));
+            for (int32_t j = 0; j < ctx->n_params; ++j) order[size_t(j)] = j;
+        }
+        if (int rc = layout_slots(ctx, order)) return rc;
     }
 
-    // compiled kernel geometry: 16 waves per block, one block per CU; w and
-    // the gradient staged in LDS when both fit, else the gradient alone
+    // the preparation-time gradient pass: one wavefront per block (its
+    // accumulation is then deterministic), the gradient in LDS when it fits
+    // (else each block's own slab in HBM); the slabs are summed in order
     const size_t table_bytes = size_t(ctx->n_params) * sizeof(double);
-    if (2 * table_bytes <= size_t(kLdsPerCu - 1024)) {
-        ctx->c_tables = 2;
-        ctx->c_lds = 2 * table_bytes;
-    } else if (table_bytes <= size_t(kLdsPerCu - 1024)) {
-        ctx->c_tables = 1;
-        ctx->c_lds = table_bytes;
-    } else {
-        ctx->c_tables = 0;
-        ctx->c_lds = 0;
+    ctx->c_tables = table_bytes <= size_t(kLdsPerCu - 1024) ? 1 : 0;
+    ctx->c_lds = ctx->c_tables ? table_bytes : 0;
+    {
+        const int per_cu = ctx->c_tables ? std::max(1, std::min<int>(8, int(size_t(kLdsPerCu) / std::max<size_t>(table_bytes, 1))))
+                                         : 2;
+        ctx->c_grid = int(std::max<int64_t>(1, std::min<int64_t>(int64_t(ctx->n_cu) * per_cu, G)));
     }
-    const int waves_per_block = kCompiledBlock / kWave;
-    const int64_t want_blocks = (int64_t(G) + waves_per_block - 1) / waves_per_block;
-    const int per_cu = ctx->c_tables ? 1 : 2;
-    ctx->c_grid = int(std::max<int64_t>(1, std::min<int64_t>(int64_t(ctx->n_cu) * per_cu, want_blocks)));
-    if (ctx->c_tables >= 1) HIP_TRY(ctx->gpart.alloc(size_t(ctx->c_grid) * size_t(std::max(ctx->n_params, 1))));
+    HIP_TRY(ctx->gpart.alloc(size_t(ctx->c_grid) * size_t(std::max(ctx->n_params, 1))));
     HIP_TRY(ctx->fixed_grad.alloc(size_t(std::max(ctx->n_params, 1))));
 
     // traversal fallback lists
@@ -946,7 +979,7 @@ int prepare(wfsa_dev* ctx, int level) {
                                       : trav_grid(ctx->cfg[t], ctx->n_cu, int64_t(fb[t].size())));
         if (!fb[t].empty()) HIP_TRY(ctx->fall[t].upload(fb[t].data(), fb[t].size(), s));
     }
-    const size_t waves = std::max(size_t(ctx->c_grid) * waves_per_block, size_t(ctx->i_grid) * size_t(ctx->i_block / kWave)) +
+    const size_t waves = std::max(size_t(ctx->c_grid), size_t(ctx->i_grid) * size_t(ctx->i_block / kWave)) +
                          size_t(ctx->b_waves) +
                          size_t(ctx->fall_grid[0]) * size_t(ctx->cfg[0].waves_per_block) +
                          size_t(ctx->fall_grid[1]) * size_t(ctx->cfg[1].waves_per_block) + size_t(ctx->fall_grid[2]);
@@ -964,6 +997,16 @@ int prepare(wfsa_dev* ctx, int level) {
         if (int rc = enqueue_compiled(ctx, true, false)) return rc;
         HIP_TRY(hipMemcpyAsync(ctx->fixed_grad.ptr, ctx->out.ptr + 1, size_t(ctx->n_params) * sizeof(double),
                                hipMemcpyDeviceToDevice, s));
+        // with a communicator the constant part is summed over the ranks once
+        // here; the per-step all-reduce then carries only what varies
+        if (ctx->comm && ctx->n_params > 0)
+            RCCL_TRY(ncclAllReduce(ctx->fixed_grad.ptr, ctx->fixed_grad.ptr, size_t(ctx->n_params), ncclDouble, ncclSum,
+                                   ctx->comm, s));
+    } else {
+        HIP_TRY(hipMemsetAsync(ctx->fixed_grad.ptr, 0, size_t(std::max(ctx->n_params, 1)) * sizeof(double), s));
+        if (ctx->comm && ctx->n_params > 0)   // (every rank joins the collective)
+            RCCL_TRY(ncclAllReduce(ctx->fixed_grad.ptr, ctx->fixed_grad.ptr, size_t(ctx->n_params), ncclDouble, ncclSum,
+                                   ctx->comm, s));
     }
     HIP_TRY(hipStreamSynchronize(s));
 
@@ -987,8 +1030,7 @@ int prepare(wfsa_dev* ctx, int level) {
 // edge-weight kernel unless the kernel folds that into its prologue (it does
 // when it stages w in LDS).  with_grad: the preparation-time gradient pass
 // (followed by its slab reduction into out); else the per-iteration pass.
-int enqueue_compiled(wfsa_dev* ctx, bool with_grad, bool want_logq, const unsigned* halted, int slot,
-                     const wfsa::QnArgs* fin) {
+int enqueue_compiled(wfsa_dev* ctx, bool with_grad, bool want_logq, const unsigned* halted, int slot) {
     hipStream_t s = ctx->stream;
     const int32_t np = ctx->n_params;
     const int tables = with_grad ? ctx->c_tables : ctx->i_tables;
@@ -1025,11 +1067,6 @@ int enqueue_compiled(wfsa_dev* ctx, bool with_grad, bool want_logq, const unsign
         c.logq = want_logq ? ctx->logq.ptr : nullptr;
         c.halted = halted;
         size_t lds = with_grad ? ctx->c_lds : ctx->i_lds;
-        if (fin && !with_grad && tables >= 1) {
-            c.fin = *fin;
-            c.fin_on = 1;
-            c.fin_wave = ctx->fin_wave;
-        }
         if (!with_grad && bubbles_fused(ctx, want_logq)) {
             c.bub = bubble_args(ctx, false, halted, nullptr);
             c.bub_on = 1;
@@ -1040,19 +1077,15 @@ int enqueue_compiled(wfsa_dev* ctx, bool with_grad, bool want_logq, const unsign
                 lds = big_stage_off(ctx) + size_t(ctx->i_block / kWave) * size_t(wfsa::big_stage_bytes(ctx->big_lds_edges));
             }
         }
-        if (with_grad) HIP_TRY(wfsa::launch_compiled(c, ctx->c_grid, kCompiledBlock, lds, s));
+        if (with_grad && tables == 0)   // the blocks accumulate into their slabs
+            HIP_TRY(hipMemsetAsync(ctx->gpart.ptr, 0, size_t(ctx->c_grid) * size_t(np) * sizeof(double), s));
+        if (with_grad) HIP_TRY(wfsa::launch_compiled(c, ctx->c_grid, kGradBlock, lds, s));
         else HIP_TRY(wfsa::launch_compiled(c, ctx->i_grid, ctx->i_block, lds, s));
     }
     if (!with_grad) HIP_TRY(record(ctx, ctx->kc, slot, s));
     if (with_grad) {
-        wfsa::TailArgs t{};
-        t.gpart = ctx->gpart.ptr;
-        t.n_gpart = (ctx->n_groups > 0 && ctx->c_tables >= 1) ? ctx->c_grid : 0;
-        t.n_params = np;
-        t.ll_part = ctx->ll_cur;
-        t.n_ll = 0;
-        t.out = ctx->out.ptr;
-        HIP_TRY(wfsa::launch_tail(t, s));
+        if (ctx->n_groups > 0) HIP_TRY(wfsa::launch_slab_sum(ctx->gpart.ptr, ctx->c_grid, np, ctx->out.ptr, s));
+        else HIP_TRY(hipMemsetAsync(ctx->out.ptr, 0, (size_t(np) + 1) * sizeof(double), s));
     }
     return WFSA_OK;
 }
@@ -1109,18 +1142,34 @@ bool bubbles_fused(wfsa_dev* ctx, bool want_logq) {
 }
 
 // The evaluation kernels; with_tail: finish out = [LL, grad_full] with the
-// tail kernel (else the consumer adds fixed_grad and sums ll_part[0, *n_ll)).
+// reduction kernel -- adding the constant trivial-word gradient unless a
+// communicator is attached (its all-reduced copy is added after the
+// all-reduce) -- else the consumer (the fused QN step) sums the bubble slots,
+// adds fixed_grad and sums ll_part[0, *n_ll).
+wfsa::ReduceArgs reduce_args(wfsa_dev* ctx, const unsigned* halted, int32_t n_ll) {
+    wfsa::ReduceArgs r{};
+    r.contrib = ctx->n_bubbles > 0 ? ctx->contrib.ptr : nullptr;
+    r.seg_ptr = ctx->seg_ptr.ptr;
+    r.param_at = ctx->param_at.ptr;
+    r.tile_ptr = ctx->tile_ptr.ptr;
+    r.n_tiles = ctx->n_tiles;
+    r.fixed = (ctx->n_groups > 0 && !ctx->comm) ? ctx->fixed_grad.ptr : nullptr;
+    r.ll_part = ctx->ll_cur;
+    r.n_ll = n_ll;
+    r.out = ctx->out.ptr;
+    r.halted = halted;
+    return r;
+}
+
 int enqueue_evaluation(wfsa_dev* ctx, bool want_logq, const unsigned* halted, int slot, bool with_tail = true,
-                       int32_t* n_ll = nullptr, const wfsa::QnArgs* fin = nullptr, bool* fin_done = nullptr) {
+                       int32_t* n_ll = nullptr) {
     hipStream_t s = ctx->stream;
-    const int32_t np = ctx->n_params;
     if (ctx->mpath) {   // matrix-file mode: out is complete when it returns
         HIP_TRY(record(ctx, ctx->k0, slot, s));
         HIP_TRY(ctx->mpath->enqueue(ctx->w_full.ptr, ctx->out.ptr, want_logq ? ctx->logq.ptr : nullptr, halted, s));
         HIP_TRY(record(ctx, ctx->kc, slot, s));
         HIP_TRY(record(ctx, ctx->k2, slot, s));
         if (n_ll) *n_ll = 0;
-        if (fin_done) *fin_done = false;
         return WFSA_OK;
     }
     if (ctx->dense) {   // fp64 MFMA path: out is complete when it returns
@@ -1129,7 +1178,6 @@ int enqueue_evaluation(wfsa_dev* ctx, bool want_logq, const unsigned* halted, in
         HIP_TRY(record(ctx, ctx->kc, slot, s));
         HIP_TRY(record(ctx, ctx->k2, slot, s));
         if (n_ll) *n_ll = 0;
-        if (fin_done) *fin_done = false;
         return WFSA_OK;
     }
     // The bubble kernel reads only the weights (ewp, staged before this
@@ -1149,8 +1197,7 @@ int enqueue_evaluation(wfsa_dev* ctx, bool want_logq, const unsigned* halted, in
         if (int rc = enqueue_bubbles(ctx, want_logq, halted, wave_off, ctx->side_stream)) return rc;
         HIP_TRY(hipEventRecord(ctx->join, ctx->side_stream));
     }
-    if (int rc = enqueue_compiled(ctx, false, want_logq, halted, slot, fin)) return rc;
-    if (fin_done) *fin_done = fin && ctx->n_groups > 0 && ctx->i_tables >= 1;
+    if (int rc = enqueue_compiled(ctx, false, want_logq, halted, slot)) return rc;
     if (side) HIP_TRY(hipStreamWaitEvent(s, ctx->join, 0));
     if (ctx->n_bubbles > 0 && !side && !fusedb) {
         if (int rc = enqueue_bubbles(ctx, want_logq, halted, wave_off, s)) return rc;
@@ -1186,19 +1233,7 @@ int enqueue_evaluation(wfsa_dev* ctx, bool want_logq, const unsigned* halted, in
         HIP_TRY(record(ctx, ctx->k2, slot, s));
         return WFSA_OK;
     }
-    wfsa::TailArgs t{};
-    t.gpart = ctx->fixed_grad.ptr;
-    t.n_gpart = ctx->n_groups > 0 ? 1 : 0;
-    t.chunk_param = ctx->bg_chunk_param.ptr;
-    t.chunk_ptr = ctx->bg_chunk_ptr.ptr;
-    t.contrib = ctx->contrib.ptr;
-    t.n_chunks = ctx->n_bubbles > 0 ? ctx->n_bg_chunks : 0;
-    t.ll_part = ctx->ll_cur;
-    t.n_ll = wave_off;
-    t.n_params = np;
-    t.out = ctx->out.ptr;
-    t.halted = halted;
-    HIP_TRY(wfsa::launch_tail(t, s));
+    HIP_TRY(wfsa::launch_reduce(reduce_args(ctx, halted, wave_off), s));
     HIP_TRY(record(ctx, ctx->k2, slot, s));
     return WFSA_OK;
 }
@@ -1295,49 +1330,45 @@ int enqueue_iteration(wfsa_dev* ctx, bool want_logq) {
     return WFSA_OK;
 }
 
-// One device-resident QuasiNewton step: the evaluation at the device's
-// w_full, the all-reduce, the update (which writes the next w_full and
-// publishes the info row of ring slot `slot`).
 // One device-resident QuasiNewton step e: the evaluation at the device's
-// w_full (its stream kernel also runs `fin`, the previous step's finish,
-// in an extra block, when given), the all-reduce, the update.  *q receives
-// this step's finish arguments: the caller folds them into the next step or
-// launches them as a trailing kernel.
-int enqueue_qn_step(wfsa_dev* ctx, double eta, double tol, int64_t e, bool timed, const wfsa::QnArgs* fin,
-                    wfsa::QnArgs* q_out) {
+// w_full, then -- fused (one rank, bubbles laid out in trimmed order) -- the
+// QN step kernel that completes the members' gradients itself, or the
+// reduction, the all-reduce (communicator) and the QN step kernel.  The QN
+// kernel's last block publishes the step's info row (ring slot e % depth).
+int enqueue_qn_step(wfsa_dev* ctx, double eta, double tol, int64_t e, bool timed) {
     hipStream_t s = ctx->stream;
     const int32_t np = ctx->n_params;
     const int par = int(e & 1);
     const int slot = int(e % kQnDepth);
     ctx->ll_cur = ctx->ll_part.ptr + size_t(par) * ctx->ll_stride;
-    // without the tail (no bubbles, no communicator) the QN kernels add the
-    // constant gradient and sum the log-likelihood partials themselves
-    const bool tail = ctx->comm != nullptr || ctx->n_bubbles > 0 || ctx->dense != nullptr || ctx->mpath != nullptr;
+    const bool trellis = !ctx->dense && !ctx->mpath;
+    const bool fused = trellis && ctx->qn_fused && !ctx->comm;
     int32_t n_ll = 0;
-    bool fin_done = false;
     const bool fuse_rmin = ctx->qn_rmin && !ctx->mpath;   // traversal strings' rmin inside their weighted passes
     if (fuse_rmin)
         if (int rc = rmin_prepare(ctx)) return rc;
     ctx->rm_eval = fuse_rmin;
-    const int erc = enqueue_evaluation(ctx, false, ctx->qn_halted.ptr, timed ? slot : -1, tail, &n_ll, fin, &fin_done);
+    const int erc = enqueue_evaluation(ctx, false, ctx->qn_halted.ptr, timed ? slot : -1, !fused && trellis, &n_ll);
     ctx->rm_eval = false;
     if (erc) return erc;
-    if (fin && !fin_done) HIP_TRY(wfsa::launch_qn_finish(*fin, s));   // (no stream kernel to carry it)
     if (ctx->comm)
         RCCL_TRY(ncclAllReduce(ctx->out.ptr, ctx->out.ptr, size_t(np) + 1, ncclDouble, ncclSum, ctx->comm, s));
     wfsa::QnArgs q{};
     q.out = ctx->out.ptr;
-    if (!tail) {
+    if (fused) {
         q.fixed = ctx->n_groups > 0 ? ctx->fixed_grad.ptr : nullptr;
+        q.contrib = ctx->n_bubbles > 0 ? ctx->contrib.ptr : nullptr;
+        q.seg_ptr = ctx->seg_ptr.ptr;
         q.ll_part = ctx->ll_cur;
         q.n_ll = n_ll;
+    } else if (trellis && ctx->comm && ctx->n_groups > 0) {
+        q.fixed = ctx->fixed_grad.ptr;   // all-reduced once at preparation
     }
     q.n_full = np;
     q.n = ctx->qn_n;
     q.k = ctx->qn_k;
     q.full_of = ctx->qn_full_of.ptr;
     q.trim = ctx->qn_trim.ptr;
-    q.ccol = ctx->qn_ccol.ptr;
     q.cptr = ctx->qn_cptr.ptr;
     q.x = ctx->qn_x.ptr;
     q.lambda = ctx->qn_lambda.ptr;
@@ -1345,10 +1376,8 @@ int enqueue_qn_step(wfsa_dev* ctx, double eta, double tol, int64_t e, bool timed
     q.grad = ctx->qn_grad.ptr;
     q.w_full = ctx->w_full.ptr;
     q.ewp = ctx->ewp.ptr;
-    const int nbk = wfsa::qn_update_blocks(ctx->qn_k);
-    q.partial = ctx->qn_partial.ptr + size_t(par) * size_t(nbk) * 4;
-    q.n_partial = nbk;
-    q.ll_val = ctx->qn_partial.ptr + 2 * size_t(nbk) * 4 + size_t(par);
+    q.partial = ctx->qn_partial.ptr;
+    q.ticket = ctx->qn_ticket.ptr;
     q.plogp = ctx->qn_plogp;
     q.eta = eta;
     q.tol = tol;
@@ -1367,8 +1396,7 @@ int enqueue_qn_step(wfsa_dev* ctx, double eta, double tol, int64_t e, bool timed
             return rc;
         }
     }
-    HIP_TRY(wfsa::launch_qn_update(q, s));
-    *q_out = q;
+    HIP_TRY(wfsa::launch_qn_step(q, fused, s));
     return WFSA_OK;
 }
 
@@ -1526,6 +1554,8 @@ int wfsa_dev_load_model(wfsa_dev* ctx, const wfsa_model_desc* model) {
     if (int rc = check_ctx(ctx)) return rc;
     if (!model) return fail(WFSA_ERR_ARG, "null model");
     drop_graph(ctx);
+    ctx->slot_order.clear();   // (a QN set-up belongs to the previous model)
+    ctx->qn_fused = false;
     if (ctx->mpath) {   // leaving matrix-file mode: the corpus went with the matrices
         ctx->mpath.reset();
         ctx->has_corpus = false;
@@ -1822,7 +1852,9 @@ int wfsa_dev_objective_grad_begin(wfsa_dev* ctx, const double* w_full, int want_
     else if (int rc = enqueue_iteration(ctx, want_logq != 0)) return rc;
     if (ctx->comm) {
         RCCL_TRY(ncclAllReduce(ctx->out.ptr, ctx->out.ptr, size_t(np) + 1, ncclDouble, ncclSum, ctx->comm, s));
-        HIP_TRY(wfsa::launch_publish(ctx->out.ptr, publish_args(ctx), s));
+        wfsa::Publish pub = publish_args(ctx);   // + the constant gradient, all-reduced once at preparation
+        if (!ctx->dense && !ctx->mpath && ctx->n_groups > 0) pub.add = ctx->fixed_grad.ptr;
+        HIP_TRY(wfsa::launch_publish(ctx->out.ptr, pub, s));
     }
     HIP_TRY(hipEventRecord(ctx->ev1, s));
     ++ctx->seq;
@@ -1887,8 +1919,10 @@ int wfsa_dev_qn_setup(wfsa_dev* ctx, const wfsa_qn_desc* d) {
     HIP_TRY(ctx->qn_cptr.upload(cptr.data(), cptr.size(), s));
     for (DevBuf<double>* b : {&ctx->qn_x, &ctx->qn_expx, &ctx->qn_grad}) HIP_TRY(b->alloc(size_t(std::max(n, 1))));
     HIP_TRY(ctx->qn_lambda.alloc(size_t(std::max(k, 1))));
-    HIP_TRY(ctx->qn_partial.alloc(2 * size_t(wfsa::qn_update_blocks(k)) * 4 + 2));   // two halves + two LL slots
+    HIP_TRY(ctx->qn_partial.alloc(size_t(std::max(k, 1)) * 4));
     HIP_TRY(ctx->qn_halted.alloc(1));
+    HIP_TRY(ctx->qn_ticket.alloc(1));
+    HIP_TRY(hipMemsetAsync(ctx->qn_ticket.ptr, 0, sizeof(unsigned), s));
     if (!ctx->qn_ring) {
         HIP_TRY(hipHostMalloc(reinterpret_cast<void**>(&ctx->qn_ring), sizeof(double) * kQnDepth * wfsa::kQnRow,
                               hipHostMallocMapped | hipHostMallocCoherent));
@@ -1903,6 +1937,21 @@ int wfsa_dev_qn_setup(wfsa_dev* ctx, const wfsa_qn_desc* d) {
         return fail(WFSA_ERR_CAPACITY, "the rmin column is not available on the dense path or with a communicator");
     ctx->qn_rmin = d->info_rmin != 0;
     if (ctx->qn_rmin) HIP_TRY(ctx->rm_res.alloc(4));
+    // the contribution slots in trimmed order (kept parameters first, the
+    // rest after), so the fused QN step sums each constraint's run in place
+    int32_t max_nm = 0;
+    for (int32_t c = 0; c < k; ++c) max_nm = std::max(max_nm, cptr[size_t(c) + 1] - cptr[size_t(c)]);
+    ctx->qn_fused = max_nm <= wfsa::kQnMaxSeg && !ctx->comm;
+    if (ctx->qn_fused) {
+        std::vector<int32_t> pos_of(size_t(nf), -1);
+        for (int32_t i = 0; i < n; ++i) pos_of[size_t(full_of[size_t(i)])] = i;
+        int32_t nxt = n;
+        for (int32_t j = 0; j < nf; ++j)
+            if (pos_of[size_t(j)] < 0) pos_of[size_t(j)] = nxt++;
+        ctx->slot_order = pos_of;
+        if (ctx->prep_level >= 2 && !ctx->dense && !ctx->mpath)
+            if (int rc = layout_slots(ctx, pos_of)) return rc;
+    }
     ctx->qn_ready = true;
     return WFSA_OK;
 }
@@ -1950,31 +1999,13 @@ int wfsa_dev_qn_run(wfsa_dev* ctx, double eta, double tol, int32_t max_steps, do
     bool stop = false;
     double c_ms_sum = 0.0, fb_ms_sum = 0.0;
     int64_t timed = 0;
-    // step e's finish (its info row and flag) runs inside step e+1's stream
-    // kernel; the last enqueued step's finish is a trailing kernel
-    wfsa::QnArgs pending{};
-    bool has_pending = false;
-    auto flush_pending = [&]() -> int {
-        if (has_pending) {
-            HIP_TRY(wfsa::launch_qn_finish(pending, s));
-            has_pending = false;
-        }
-        return WFSA_OK;
-    };
     while (done < max_steps) {
         while (!stop && enq < max_steps && enq - done < kQnDepth) {
-            wfsa::QnArgs q{};
-            if (int rc = enqueue_qn_step(ctx, eta, tol, enq, enq % kTimingStride == 0,
-                                         has_pending ? &pending : nullptr, &q))
-                return rc;
-            pending = q;
-            has_pending = true;
+            if (int rc = enqueue_qn_step(ctx, eta, tol, enq, enq % kTimingStride == 0)) return rc;
             ++enq;
             ++ctx->seq;
         }
         if (done >= enq) break;
-        if (enq == done + 1)   // nothing after step `done` carries its finish
-            if (int rc = flush_pending()) return rc;
         if (int rc = wait_published(ctx, base + unsigned(done) + 1u)) return rc;
         const int slot = done % kQnDepth;
         const double* row = ctx->qn_ring + size_t(slot) * wfsa::kQnRow;
@@ -2002,7 +2033,6 @@ int wfsa_dev_qn_run(wfsa_dev* ctx, double eta, double tol, int32_t max_steps, do
         }
     }
     // drain the steps enqueued after a halt (they are no-ops)
-    if (int rc = flush_pending()) return rc;
     if (enq > done)
         if (int rc = wait_published(ctx, base + unsigned(enq))) return rc;
     HIP_TRY(hipStreamSynchronize(s));
@@ -2166,6 +2196,10 @@ int wfsa_dev_comm_init(wfsa_dev* ctx, int nranks, int rank, const uint8_t id[WFS
     RCCL_TRY(ncclCommInitRank(&ctx->comm, nranks, uid, rank));
     ctx->nranks = nranks;
     ctx->rank = rank;
+    // the compiled corpus' constant gradient is summed over the ranks at
+    // compilation: compile again (every rank does, in the same call order)
+    if (ctx->prep_level >= 2) ctx->prep_level = 1;
+    ctx->qn_fused = false;   // the per-step all-reduce needs the reduced vector
     return WFSA_OK;
 }
 

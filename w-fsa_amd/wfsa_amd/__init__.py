@@ -232,6 +232,12 @@ class QuasiNewtonLearner:
         check_host(load().wfsa_learner_get_x(self._h, _ptr(a)))
         return a
 
+    def last_grad(self):
+        """gradient (trimmed) of the last evaluation; after Run, of its last step"""
+        a = np.zeros(self.n, dtype=np.float64)
+        check_host(load().wfsa_learner_get_grad(self._h, _ptr(a)))
+        return a
+
     def set_x(self, x):
         x = np.ascontiguousarray(x, dtype=np.float64)
         assert x.shape == (self.n,)

@@ -113,6 +113,7 @@ _SIGS = {
     "wfsa_learner_run": (C.c_int, [vp, dbl, dbl, i32, vp, P(i32)]),
     "wfsa_learner_objective_grad": (C.c_int, [vp, P(dbl), vp, vp]),
     "wfsa_learner_get_x": (C.c_int, [vp, vp]),
+    "wfsa_learner_get_grad": (C.c_int, [vp, vp]),
     "wfsa_learner_set_x": (C.c_int, [vp, vp]),
     "wfsa_learner_get_p": (C.c_int, [vp, vp]),
     "wfsa_learner_trimmed_index": (C.c_int, [vp, vp]),
