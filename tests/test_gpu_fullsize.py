@@ -76,10 +76,28 @@ def test_c3_full_size_timed_path_matches_enum(c3):
     assert _close(kl2, kl1_o, rel=1e-11)
 
 
+def _compiled_only(W, fsa, sym, off, wt):
+    """the strings that compile (stream + bubbles): the traversal tiers still
+    scatter their gradient with fp64 atomics, whose order varies in the last
+    bits from run to run, so the bitwise tests keep to the
+    compiled path -- bubbles included, whose reduction is fixed-order"""
+    dev = W.Device(0)
+    dev.load_model(fsa)
+    dev.load_corpus(sym, off, wt / wt.sum())
+    dev.recognize()
+    dev.objective_grad(np.full(len(fsa.param_names()), -1.0), want_logq=False)
+    keep = np.flatnonzero(dev.string_tiers() < 0)
+    lens = np.diff(off)[keep]
+    noff = np.concatenate([[0], np.cumsum(lens)]).astype(np.int64)
+    nsym = np.concatenate([sym[off[i]:off[i + 1]] for i in keep]).astype(np.uint8)
+    return nsym, noff, wt[keep]
+
+
 def _ambiguous_learner(W, seed=4):
     syn = W.Synthetic(n_states=256, degree=8, vocab=16, emissions=1, n_strings=40_000, max_len=64, seed=seed)
     sym, off, wt = syn.corpus()
     fsa = W.Fsa.read_text(syn.wfsa_text)
+    sym, off, wt = _compiled_only(W, fsa, sym, off, wt)
     lrn = W.QuasiNewtonLearner(0)
     lrn.set_info_rmin(False)
     lrn.BuildFromPacked(fsa, sym, off, wt)
@@ -93,6 +111,7 @@ def test_evaluations_and_runs_are_bitwise_reproducible():
     lrn.Init(7)
     st = lrn.stats()
     assert st["n_bubbles"] > 1000
+    assert st["fallback_strings"] == 0 and st["tier1_strings"] == 0
     kl_a, g_a, _ = lrn.objective_grad()
     kl_b, g_b, _ = lrn.objective_grad()
     assert kl_a == kl_b

@@ -1216,6 +1216,10 @@ __global__ __launch_bounds__(1024, (DBG == 10 ? 8 : 1)) void fbs_kernel(Compiled
     };
     constexpr bool kStreams = DBG != 3 && DBG != 4;   // (timing experiments)
     if (kStreams) load(A, 0);
+    if (a.fin.active && bid == 0) {   // the previous QN step's finish (its loads beside the prefetch)
+        __shared__ double fred[kMaxBlockWaves];
+        qn_finish(a.fin, fred);
+    }
     if (W_LDS && DBG != 4) {
         // stage w[0, n_params] in 16-byte pieces, all of a thread's loads
         // issued before its first store (loads and stores unconditional --
@@ -1412,15 +1416,17 @@ __global__ __launch_bounds__(kReduceBlock) void reduce_kernel(ReduceArgs a) {
         if (t == 0) a.out[0] = red[0];
         return;
     }
-    __shared__ int sp[kReduceTileParams + 1];
-    __shared__ double res[kReduceTileParams];
-    __shared__ SegScratch<kReduceBlock> sc;
+    __shared__ int sp[kReduceTileParams + 1], cb[kReduceTileParams + 1];
+    __shared__ double res[kReduceTileParams], cp[kMaxChunks];
     const int p0 = a.tile_ptr[tb], ns = a.tile_ptr[tb + 1] - p0;
-    const int s0 = a.seg_ptr[p0];
     if (a.contrib) {
-        for (int i = t; i <= ns; i += kReduceBlock) sp[i] = a.seg_ptr[p0 + i] - s0;
+        const int s0 = a.seg_ptr[p0], c0 = a.chunk_ptr[p0];
+        for (int i = t; i <= ns; i += kReduceBlock) {
+            sp[i] = a.seg_ptr[p0 + i] - s0;
+            cb[i] = a.chunk_ptr[p0 + i] - c0;
+        }
         __syncthreads();
-        seg_sums<kReduceBlock>(a.contrib + s0, sp, ns, seg_piece(sp[ns], kReduceBlock), res, sc);
+        seg_sums<kReduceBlock>(a.contrib + a.grp_base[tb], sp, cb, ns, res, cp);
     }
     for (int i = t; i < ns; i += kReduceBlock) {
         const int j = a.param_at[p0 + i];

@@ -253,22 +253,50 @@ hipError_t launch_hf(const HfArgs& a, hipStream_t stream);
 // block per constraint, completes the gradient of the constraint's members
 // (the traversal tiers' part in out, the constant trivial-word part, and --
 // fused -- the sums of their bubble contribution slots in a fixed order),
-// updates x and lambda, writes the next w_full, and leaves its partial
-// (g, g, lambda, graderr) for the last block to arrive (an arrival ticket),
-// which reduces the info row [KL, graderr, g_min, g_max, lambda_min, rmin,
-// rmin string, status] into a host-mapped ring slot and bumps the flag.
+// updates x and lambda, writes the next w_full, and leaves its block partial
+// (g, g, lambda, graderr).  The step's FINISH -- the info row [KL, graderr,
+// g_min, g_max, lambda_min, rmin, rmin string, status] from those partials
+// and the log-likelihood partials, into a host-mapped ring slot, then the
+// flag -- runs in the first block of the NEXT step's stream kernel (which
+// does not depend on it; no arrival ticket: 1024 same-address atomics cost
+// ~8 ns each, serialised), or as its own one-block launch after the last
+// step of a run / when the next step has no stream kernel.
+//
+// Halting: the finish of step e sets halt_pending; the QN kernel of step
+// e + 1 (a later launch) sees it, publishes its row as skipped and sets
+// halted, which every evaluation kernel of the later steps checks at entry.
+// A launch never reads a flag that the same launch writes.
 constexpr int kQnRow = 8;
 constexpr unsigned kQnRan = 0, kQnHalted = 1, kQnNonFinite = 2, kQnSkipped = 3;
 constexpr int kQnBlock = 256;
 constexpr int kQnMaxSeg = 1024;   // members of a constraint the fused kernel keeps in LDS
+struct QnFinish {
+    int32_t active;              // (stream kernel: its block 0 finishes the previous step)
+    const double* partial;       // [n_blocks][4] the QN kernel's block partials
+    int32_t n_blocks;
+    const double* ll_part;       // log-likelihood partials (fixed-order sum), or null: out0
+    int32_t n_ll;
+    const double* out0;
+    const double* rmin;          // [2] the step's rmin column (rmin, string index), or null (0, 0)
+    const double* rmin_part;     // or: [n][2] block minima (log rmin, string index)
+    int32_t rmin_n_part;
+    int32_t k;
+    double plogp, tol;
+    int32_t ring_slot;           // ring slot of the step
+    const unsigned* halted;      // [0] halted, [1] halt_pending (the finish writes [1])
+    unsigned* halt_pending;
+    unsigned* seq;               // device sequence counter
+    unsigned* host_flag;         // host-mapped completion flag
+    double* host_ring;           // host-mapped [slots][kQnRow]
+};
 struct QnArgs {
-    const double* out;           // [1 + n_full]: gradient parts accumulated so far; out[0] is the
-                                 // log-likelihood when ll_part is null
+    const double* out;           // [1 + n_full]: gradient parts accumulated so far
+    int32_t use_out;             // (fused: 0 when no traversal string adds to out)
     const double* fixed;         // [n_full] constant trivial-word gradient to add, or null
     const double* contrib;       // fused: bubble contribution slots, or null
-    const int32_t* seg_ptr;      // fused: [n + 1] slot run of kept parameter i (trimmed order)
-    const double* ll_part;       // log-likelihood partials summed in a fixed order, or null
-    int32_t n_ll;
+    const int64_t* grp_base;     // fused: physical slot base of constraint c's group (chunk-transposed)
+    const int32_t* seg_ptr;      // fused: [n + 1] logical slot run of kept parameter i (trimmed order)
+    const int32_t* chunk_ptr;    // fused: [n + 1] its chunks (cumulative)
     int32_t n_full, n, k;
     const int32_t* full_of;      // [n] full index of each kept parameter
     const int32_t* trim;         // [n_full] trimmed index / -1 / -2
@@ -279,18 +307,11 @@ struct QnArgs {
     double* grad;
     double* w_full;              // [n_full + 1] (zero slot)
     double* ewp;                 // [n_full + 1] exp(w_full), for the bubble kernel
-    double* partial;             // [max(k, 1)][4] block partials
-    unsigned* ticket;            // arrival counter (the last block resets it)
-    double plogp, eta, tol;
+    double* partial;             // [max(k, 1)][4] block partials (the finish reads them)
+    double eta;
     int32_t exp_lambda;
-    int32_t ring_slot;           // ring slot of this step
-    unsigned* halted;            // device: nonzero after a halting step
-    unsigned* seq;               // device sequence counter
-    unsigned* host_flag;         // host-mapped completion flag
-    double* host_ring;           // host-mapped [slots][kQnRow]
-    const double* rmin;          // [2] the step's rmin column (rmin, string index), or null (0, 0)
-    const double* rmin_part;     // or: [n][2] block minima (log rmin, string index) the finish reduces
-    int32_t rmin_n_part;
+    unsigned* halted;            // [0] halted, [1] halt_pending
+    QnFinish fin;                // this step's finish (publication of skipped rows)
 };
 
 // Bubble evaluation.  Contributions (-p_s x edge posterior) go straight to
@@ -387,6 +408,7 @@ struct CompiledArgs {
     double* ll_part;         // [waves in grid] (per-iteration stream kernel: [blocks])
     double* logq;            // [S] or null
     const unsigned* halted;  // device-resident QN run: nonzero = skip (or null)
+    QnFinish fin;            // fin.active: block 0 finishes the previous QN step first
 };
 
 
@@ -397,14 +419,21 @@ struct CompiledArgs {
 // (seg_sums, qn_device.hpp); one more block writes out[0] = the sum of the
 // log-likelihood partials in a fixed order.  No atomics: the same inputs give
 // the same bits on every launch.
+
 constexpr int kReduceBlock = 256;
 constexpr int kReduceTileParams = 1024;
-constexpr int kReduceTileSlots = 16384;
+// The bubble contribution slots of a parameter are summed in chunks of
+// kSlotChunk (seg_sums, qn_device.hpp); a reduction group's chunk sums fit in
+// LDS up to kMaxChunks (a run-of-positions group is cut to fit).
+constexpr int kSlotChunk = 16;
+constexpr int kMaxChunks = 1024;
 struct ReduceArgs {
     const double* contrib;       // bubble contribution slots, or null
-    const int32_t* seg_ptr;      // [n_pos + 1] slot run of the parameter at each position
+    const int64_t* grp_base;     // [n_tiles + 1] physical slot base of each group (chunk-transposed)
+    const int32_t* seg_ptr;      // [n_pos + 1] logical slot run of the parameter at each position
+    const int32_t* chunk_ptr;    // [n_pos + 1] its chunks (cumulative)
     const int32_t* param_at;     // [n_pos] full parameter index at each position
-    const int32_t* tile_ptr;     // [n_tiles + 1] position range of each tile
+    const int32_t* tile_ptr;     // [n_tiles + 1] position range of each reduction group
     int32_t n_tiles;
     const double* fixed;         // [n_params] added when non-null
     const double* ll_part;
@@ -459,6 +488,8 @@ hipError_t launch_stage(const double* host_w, double* w, double* ewp, int32_t n,
 // fused: the member gradients include the bubble slot sums (every constraint
 // has at most kQnMaxSeg members); grid max(k, 1)
 hipError_t launch_qn_step(const QnArgs& a, bool fused, hipStream_t stream);
+// a step's finish as its own one-block launch
+hipError_t launch_qn_finish(const QnFinish& f, hipStream_t stream);
 hipError_t launch_qn_weights(const double* x, const int32_t* trim, int32_t n_full, double* w_full, double* ewp,
                              hipStream_t stream);
 hipError_t launch_edge_weights(const double* w_full, const int32_t* pptr, const int32_t* pidx, double* lw,

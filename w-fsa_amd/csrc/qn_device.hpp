@@ -18,80 +18,166 @@ __device__ inline double wave_reduce(double v, int op) {   // op 0 min, 1 max, 2
     return v;
 }
 
-// Deterministic per-segment sums over one contiguous run of bubble
-// contribution slots (the runs of consecutive parameters in slot order).
-// Segment q of nseg owns v[sp[q], sp[q+1]) (sp relative, sp[0] = 0, in LDS).
-// The block's NT threads cut the run into pieces of C consecutive slots,
-// thread t the t-th; a thread sums its piece segment by segment in slot
-// order (a segment wholly inside the piece is written at once), and a
-// segment that crosses pieces is completed by adding its piece partials in
-// thread order.  The order of every addition depends only on the segment
-// lengths and C, never on timing: the same inputs give the same bits.
+// Per-parameter sums of the bubble contribution slots, in an order that
+// depends on the parameter's own slots only (not on the slot layout, the
+// reduction groups or the block size), so the same contributions give the
+// same bits under every layout: parameter q's slots are cut into chunks of
+// kSlotChunk from its first slot, each chunk summed in slot order, then the
+// chunk sums added in chunk order.
+//
+// One reduction group (a QN constraint, or a run of positions) holds nseg
+// parameters: q owns logical slots [sp[q], sp[q+1]) and chunks [cb[q],
+// cb[q+1]) (both relative to the group, in LDS).  The group's chunks are
+// stored transposed: element b of chunk c at v[b * nch + c] (nch = cb[nseg];
+// a chunk's tail is zero padding), so consecutive threads -- one chunk each --
+// read consecutive addresses.  The chunk sums go to LDS (cp, kMaxChunks,
+// fb_kernels.hpp) and
+// a thread per parameter adds them; a group with more chunks sums each
+// parameter's chunks in one thread straight from memory (same order).
 template <int NT>
-struct SegScratch {
-    double pf[NT], pl[NT];   // partial of the piece's first / last segment
-    int fs[NT], ls[NT];      // the piece's first / last segment (-1: empty piece)
-};
-
-// C: slots per piece, at least ceil(sp[nseg] / NT)
-__device__ inline int seg_piece(int total, int nt) { return max((total + nt - 1) / nt, 16); }
-
-template <int NT>
-__device__ void seg_sums(const double* __restrict__ v, const int* sp, int nseg, int C, double* res,
-                         SegScratch<NT>& sc) {
+__device__ void seg_sums(const double* __restrict__ v, const int* sp, const int* cb, int nseg, double* res,
+                         double* cp) {
     const int t = int(threadIdx.x);
-    const int total = sp[nseg];
-    for (int q = t; q < nseg; q += NT) res[q] = 0.0;
-    __syncthreads();
-    const int a0 = t * C, a1 = min(a0 + C, total);
-    int f = -1, q = -1;
-    double p0 = 0.0, acc = 0.0;
-    if (a0 < a1) {
-        int lo = 0, hi = nseg;   // the segment holding slot a0: last q with sp[q] <= a0
-        while (hi - lo > 1) {
-            const int mid = (lo + hi) >> 1;
-            if (sp[mid] <= a0) lo = mid; else hi = mid;
+    const int nch = cb[nseg];
+    auto chunk_sum = [&](int c) {   // unguarded: the padding is zero, and adding +0.0 changes nothing
+        double x[kSlotChunk];
+#pragma unroll
+        for (int b = 0; b < kSlotChunk; ++b) x[b] = v[size_t(b) * size_t(nch) + size_t(c)];
+        double s = x[0];
+#pragma unroll
+        for (int b = 1; b < kSlotChunk; ++b) s += x[b];
+        return s;
+    };
+    if (nch <= kMaxChunks) {
+        for (int c = t; c < nch; c += NT) cp[c] = chunk_sum(c);
+        __syncthreads();
+        for (int q = t; q < nseg; q += NT) {
+            const int c0 = cb[q], c1 = cb[q + 1];
+            double s = 0.0;
+            int c = c0;
+            for (; c + 8 <= c1; c += 8) {   // eight LDS loads in flight, added in order
+                double y[8];
+#pragma unroll
+                for (int i = 0; i < 8; ++i) y[i] = cp[c + i];
+#pragma unroll
+                for (int i = 0; i < 8; ++i) s += y[i];
+            }
+            for (; c < c1; ++c) s += cp[c];
+            res[q] = s;
         }
-        q = f = lo;
-        int nxt = sp[q + 1];
-        for (int s0 = a0; s0 < a1; s0 += 8) {
-            double x[8];
+    } else {
+        for (int q = t; q < nseg; q += NT) {
+            double s = 0.0;
+            for (int c = cb[q]; c < cb[q + 1]; ++c) s += chunk_sum(c);
+            res[q] = s;
+        }
+    }
+    __syncthreads();
+}
+
+// the info row of a step into its host ring slot, then the flag; the
+// system-scope release orders the row before the flag
+__device__ inline void qn_publish_row(const QnFinish& f, const double* info, unsigned status) {
+    double* row = f.host_ring + size_t(f.ring_slot) * kQnRow;
+    for (int i = 0; i < 7; ++i) row[i] = info ? info[i] : 0.0;
+    row[7] = double(status);
+    const unsigned v = *f.seq + 1u;
+    *f.seq = v;
+    __hip_atomic_store(f.host_flag, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+constexpr int kMaxBlockWaves = 16;
+
+// block-wide reduction by a fixed tree (every thread gets the result);
+// red: kMaxBlockWaves doubles of LDS
+__device__ inline double block_reduce(double v, int op, double* red) {
+    const int t = int(threadIdx.x), nw = int(blockDim.x) / 64;
+    v = wave_reduce(v, op);
+    __syncthreads();
+    if ((t & 63) == 0) red[t >> 6] = v;
+    __syncthreads();
+    double r = red[0];
+    for (int i = 1; i < nw; ++i) r = op == 0 ? fmin(r, red[i]) : (op == 1 ? fmax(r, red[i]) : r + red[i]);
+    __syncthreads();   // red is reused
+    return r;
+}
+
+// A QN step's finish (QnFinish, fb_kernels.hpp), by every thread of one
+// block: the info row from the QN block partials and the log-likelihood
+// partials (fixed order), the halt decision (halt_pending, read by the next
+// QN launch), the publication.  red: kMaxBlockWaves doubles of LDS.
+__device__ inline void qn_finish(const QnFinish& f, double* red) {
+    const int t = int(threadIdx.x), nt = int(blockDim.x), nw = nt / 64;
+    double gmin = INFINITY, gmax = -INFINITY, lmin = INFINITY, ge = 0.0;
+    for (int j0 = t; j0 < f.n_blocks; j0 += 4 * nt) {   // four blocks' partials in flight per thread
+        double4 v[4];
 #pragma unroll
-            for (int b = 0; b < 8; ++b) x[b] = v[min(s0 + b, a1 - 1)];
+        for (int b = 0; b < 4; ++b) v[b] = reinterpret_cast<const double4*>(f.partial)[min(j0 + b * nt, f.n_blocks - 1)];
 #pragma unroll
-            for (int b = 0; b < 8; ++b) {
-                const int s = s0 + b;
-                if (s >= a1) break;
-                while (s >= nxt) {   // segment q ends inside this piece
-                    if (q == f) p0 = acc; else res[q] = acc;
-                    acc = 0.0;
-                    ++q;
-                    nxt = sp[q + 1];
-                }
-                acc += x[b];
+        for (int b = 0; b < 4; ++b) {
+            gmin = fmin(gmin, v[b].x);
+            gmax = fmax(gmax, v[b].y);
+            lmin = fmin(lmin, v[b].z);
+            ge = fmax(ge, v[b].w);
+        }
+    }
+    double ll = f.ll_part ? strided_sum(f.ll_part, f.n_ll, t, nt) : 0.0;
+    double rv = INFINITY, ri = -1.0;   // rmin column from block minima, ties to the lower string
+    if (f.rmin_part)
+        for (int j = t; j < f.rmin_n_part; j += nt) {
+            const double v = f.rmin_part[2 * j], i = f.rmin_part[2 * j + 1];
+            if (v < rv || (v == rv && i < ri)) {
+                rv = v;
+                ri = i;
             }
         }
-        if (q == f) p0 = acc;
-    }
-    sc.pf[t] = p0;
-    sc.pl[t] = acc;
-    sc.fs[t] = f;
-    sc.ls[t] = q;
-    __syncthreads();
-    for (int k = t; k < nseg; k += NT) {
-        const int b0 = sp[k], b1 = sp[k + 1];
-        if (b0 == b1) continue;
-        const int ta = b0 / C, tb = (b1 - 1) / C;
-        if (ta == tb) {
-            if (k == sc.fs[ta]) res[k] = sc.pf[ta];
-            else if (k == sc.ls[ta]) res[k] = sc.pl[ta];   // (else written by the piece itself)
-        } else {   // k is the last segment of piece ta and the first of tb
-            double s = sc.pl[ta];
-            for (int u = ta + 1; u < tb; ++u) s += sc.pf[u];
-            res[k] = s + sc.pf[tb];
+    gmin = block_reduce(gmin, 0, red);
+    gmax = block_reduce(gmax, 1, red);
+    lmin = block_reduce(lmin, 0, red);
+    ge = block_reduce(ge, 1, red);
+    ll = block_reduce(ll, 2, red);
+    for (int o = 32; o > 0; o >>= 1) {
+        const double v = __shfl_xor(rv, o, 64), i = __shfl_xor(ri, o, 64);
+        if (v < rv || (v == rv && i < ri)) {
+            rv = v;
+            ri = i;
         }
     }
+    __shared__ double rr[kMaxBlockWaves][2];
+    if ((t & 63) == 0) {
+        rr[t >> 6][0] = rv;
+        rr[t >> 6][1] = ri;
+    }
     __syncthreads();
+    if (t == 0) {
+        for (int w = 1; w < nw; ++w)
+            if (rr[w][0] < rv || (rr[w][0] == rv && rr[w][1] < ri)) {
+                rv = rr[w][0];
+                ri = rr[w][1];
+            }
+        if (f.k == 0) gmin = gmax = lmin = 0.0;
+        double info[7];
+        info[0] = f.plogp - (f.ll_part ? ll : *f.out0);
+        info[1] = ge;
+        info[2] = gmin;
+        info[3] = gmax;
+        info[4] = lmin;
+        info[5] = 0.0;
+        info[6] = 0.0;
+        if (f.rmin_part) {
+            info[5] = ri >= 0.0 ? exp(rv) : 0.0;
+            info[6] = ri;
+        } else if (f.rmin) {
+            info[5] = f.rmin[0];
+            info[6] = f.rmin[1];
+        }
+        bool finite = true;
+        for (int i = 0; i < 7; ++i) finite = finite && isfinite(info[i]);
+        const bool halt = ge <= f.tol && fabs(gmin) <= f.tol && fabs(gmax) <= f.tol;
+        const unsigned status = !finite ? kQnNonFinite : (halt ? kQnHalted : kQnRan);
+        if (status != kQnRan) *f.halt_pending = status;   // read by the next QN launch only
+        qn_publish_row(f, info, status);
+    }
 }
 
 }  // namespace wfsa

@@ -177,8 +177,11 @@ struct wfsa_dev {
     std::vector<int32_t> h_bubbuf, h_sm4_list, h_sm_list, h_big_list;   // host copies (re-layout)
     std::vector<int32_t> slot_order;        // [n_params] pos_of used by the current layout
     std::vector<int32_t> h_seg_ptr;
-    DevBuf<int32_t> seg_ptr, param_at, tile_ptr;
+    DevBuf<int32_t> seg_ptr, param_at, tile_ptr;   // tile_ptr: [n_tiles + 1] position range of each reduction group
     int32_t n_tiles = 0;
+    DevBuf<int64_t> grp_base;            // [n_tiles + 1] physical slot base of each reduction group
+    DevBuf<int32_t> chunk_ptr;           // [n_params + 1] slot chunks by position (cumulative)
+    std::vector<int32_t> slot_groups;     // leading reduction groups (positions): the QN constraints
     std::vector<int32_t> h_pptr, h_pidx;   // host copy of the combined parameter lists
 
     size_t c_lds = 0;
@@ -242,7 +245,12 @@ struct wfsa_dev {
     DevBuf<int32_t> qn_trim, qn_full_of, qn_ccol, qn_cptr;
     int prep_gen = 0;
     DevBuf<double> qn_x, qn_lambda, qn_expx, qn_grad, qn_partial;
-    DevBuf<unsigned> qn_halted, qn_ticket;
+    // the QN finish of the last enqueued step, not yet enqueued (fin_pending),
+    // and the one handed to the next stream kernel launch (fin_for_fbs)
+    wfsa::QnFinish fin_next{}, fin_for_fbs{};
+    std::vector<int32_t> h_cptr;
+    bool fin_pending = false, fin_hostable = false;
+    DevBuf<unsigned> qn_halted;
     std::vector<int32_t> qn_full_of_h, qn_cptr_h;
     bool qn_fused = false;           // qn_step_kernel sums the members' bubble slots itself
     double* qn_ring = nullptr;       // host-mapped [kQnDepth][kQnRow]
@@ -500,6 +508,42 @@ int layout_slots(wfsa_dev* ctx, const std::vector<int32_t>& pos_of) {
                 for_edge_params(edge_code_at(o, e), [&](int32_t jj) { pc[size_t(pos_of[size_t(jj)]) + 1]++; });
     for (size_t q = 1; q < pc.size(); ++q) pc[q] += pc[q - 1];
     std::vector<int32_t> fill(pc.begin(), pc.end() - 1);
+    // Reduction groups over the positions: the QN constraints when the slots
+    // follow its trimmed order (ctx->slot_groups), then runs of consecutive
+    // positions (at most kReduceTileParams parameters and, unless one alone
+    // has more, kMaxChunks chunks).  Parameter q's slots form chunks of
+    // kSlotChunk (seg_sums, qn_device.hpp: its sum depends on its own slots
+    // only); a group's chunks are stored transposed -- element b of the
+    // group's chunk c at gbase + b * nch + c -- so the threads of a block, a
+    // chunk each, read consecutive addresses (one cache line per 8 lanes
+    // instead of one per lane: the uncoalesced form cost ~8 us per QN step at c3).
+    std::vector<int32_t> cptr_pos(size_t(np) + 1, 0);   // chunks by position, cumulative
+    for (int32_t q = 0; q < np; ++q)
+        cptr_pos[size_t(q) + 1] = cptr_pos[size_t(q)] + (pc[size_t(q) + 1] - pc[size_t(q)] + wfsa::kSlotChunk - 1) / wfsa::kSlotChunk;
+    std::vector<int32_t> gp(1, 0);
+    for (size_t i = 1; i < ctx->slot_groups.size() && ctx->slot_groups[i] <= np; ++i) gp.push_back(ctx->slot_groups[i]);
+    for (int32_t q = gp.back(); q < np;) {
+        int32_t e = q + 1;
+        while (e < np && e - q < wfsa::kReduceTileParams && cptr_pos[size_t(e) + 1] - cptr_pos[size_t(q)] <= wfsa::kMaxChunks) ++e;
+        gp.push_back(e);
+        q = e;
+    }
+    const int32_t ng = int32_t(gp.size()) - 1;
+    std::vector<int64_t> gbase(size_t(ng) + 1, 0);
+    std::vector<int32_t> grp_of(size_t(std::max(np, 1)), 0);
+    for (int32_t g = 0; g < ng; ++g) {
+        const int64_t nch = cptr_pos[size_t(gp[size_t(g) + 1])] - cptr_pos[size_t(gp[size_t(g)])];
+        gbase[size_t(g) + 1] = gbase[size_t(g)] + nch * wfsa::kSlotChunk;
+        for (int32_t q = gp[size_t(g)]; q < gp[size_t(g) + 1]; ++q) grp_of[size_t(q)] = g;
+    }
+    auto phys = [&](int32_t pos, int32_t sl) -> int32_t {   // logical slot sl of position pos
+        const int32_t g = grp_of[size_t(pos)], cg = cptr_pos[size_t(gp[size_t(g)])];
+        const int64_t nch = cptr_pos[size_t(gp[size_t(g) + 1])] - cg;
+        const int32_t i = sl - pc[size_t(pos)];
+        const int64_t c = cptr_pos[size_t(pos)] - cg + i / wfsa::kSlotChunk;
+        return int32_t(gbase[size_t(g)] + int64_t(i % wfsa::kSlotChunk) * nch + c);
+    };
+    if (gbase.back() >= int64_t(INT32_MAX)) return fail(WFSA_ERR_CAPACITY, "too many bubble contribution slots");
     if (ctx->n_bubbles > 0) {
         // class tables: RE edges, quads = 1 + RE/2 + RE/4
         auto build_table = [&](const std::vector<int32_t>& list, int RE, std::vector<int32_t>& tbl) {
@@ -516,7 +560,10 @@ int layout_slots(wfsa_dev* ctx, const std::vector<int32_t>& pos_of) {
                     if (e < edges) {
                         code = edge_code_at(o, e);
                         sd = bb[size_t(o) + 5 + 2 * size_t(e)];
-                        if (code < np) sl = fill[size_t(pos_of[size_t(code)])]++;
+                        if (code < np) {
+                            const int32_t pos = pos_of[size_t(code)];
+                            sl = phys(pos, fill[size_t(pos)]++);
+                        }
                     }
                     quad(1 + e / 2, b)[2 * (e & 1)] = code;
                     quad(1 + e / 2, b)[2 * (e & 1) + 1] = sd;
@@ -533,7 +580,10 @@ int layout_slots(wfsa_dev* ctx, const std::vector<int32_t>& pos_of) {
             const int32_t o = ctx->h_big_list[size_t(i)];
             big_edge_base[size_t(i)] = int32_t(eslot_ptr.size()) - 1;
             for (int e = 0; e < (bb[size_t(o)] >> 16); ++e) {
-                for_edge_params(edge_code_at(o, e), [&](int32_t jj) { eslot.push_back(fill[size_t(pos_of[size_t(jj)])]++); });
+                for_edge_params(edge_code_at(o, e), [&](int32_t jj) {
+                    const int32_t pos = pos_of[size_t(jj)];
+                    eslot.push_back(phys(pos, fill[size_t(pos)]++));
+                });
                 eslot_ptr.push_back(int32_t(eslot.size()));
             }
         }
@@ -545,22 +595,18 @@ int layout_slots(wfsa_dev* ctx, const std::vector<int32_t>& pos_of) {
         HIP_TRY(ctx->big_edge_base.upload(big_edge_base.data(), big_edge_base.size(), s));
         HIP_TRY(ctx->big_eslot_ptr.upload(eslot_ptr.data(), eslot_ptr.size(), s));
         HIP_TRY(ctx->big_eslot.upload(eslot.data(), eslot.size(), s));
-        HIP_TRY(ctx->contrib.alloc(size_t(std::max(pc.back(), 1))));
-        HIP_TRY(hipMemsetAsync(ctx->contrib.ptr, 0, size_t(std::max(pc.back(), 1)) * sizeof(double), s));
     }
-    // tiles of consecutive positions: at most kReduceTileParams parameters and
-    // (unless one parameter alone has more) kReduceTileSlots slots
-    std::vector<int32_t> tiles(1, 0);
-    for (int32_t q = 0; q < np;) {
-        int32_t e = q + 1;
-        while (e < np && e - q < wfsa::kReduceTileParams && pc[size_t(e) + 1] - pc[size_t(q)] <= wfsa::kReduceTileSlots) ++e;
-        tiles.push_back(e);
-        q = e;
+    if (ctx->n_bubbles > 0) {
+        const size_t n_phys = size_t(std::max<int64_t>(gbase.back(), 1));
+        HIP_TRY(ctx->contrib.alloc(n_phys));
+        HIP_TRY(hipMemsetAsync(ctx->contrib.ptr, 0, n_phys * sizeof(double), s));   // padding stays zero
     }
-    ctx->n_tiles = int32_t(tiles.size()) - 1;
+    ctx->n_tiles = ng;
+    HIP_TRY(ctx->grp_base.upload(gbase.data(), gbase.size(), s));
+    HIP_TRY(ctx->chunk_ptr.upload(cptr_pos.data(), cptr_pos.size(), s));
     HIP_TRY(ctx->seg_ptr.upload(pc.data(), pc.size(), s));
     HIP_TRY(ctx->param_at.upload(param_at.data(), param_at.size(), s));
-    HIP_TRY(ctx->tile_ptr.upload(tiles.data(), tiles.size(), s));
+    HIP_TRY(ctx->tile_ptr.upload(gp.data(), gp.size(), s));
     HIP_TRY(hipStreamSynchronize(s));
     ctx->h_seg_ptr = std::move(pc);
     ctx->slot_order = pos_of;
@@ -1066,6 +1112,10 @@ int enqueue_compiled(wfsa_dev* ctx, bool with_grad, bool want_logq, const unsign
         c.ll_part = ctx->ll_cur;
         c.logq = want_logq ? ctx->logq.ptr : nullptr;
         c.halted = halted;
+        if (!with_grad) {   // a pending QN finish rides in block 0 (consumed)
+            c.fin = ctx->fin_for_fbs;
+            ctx->fin_for_fbs.active = 0;
+        }
         size_t lds = with_grad ? ctx->c_lds : ctx->i_lds;
         if (!with_grad && bubbles_fused(ctx, want_logq)) {
             c.bub = bubble_args(ctx, false, halted, nullptr);
@@ -1149,7 +1199,9 @@ bool bubbles_fused(wfsa_dev* ctx, bool want_logq) {
 wfsa::ReduceArgs reduce_args(wfsa_dev* ctx, const unsigned* halted, int32_t n_ll) {
     wfsa::ReduceArgs r{};
     r.contrib = ctx->n_bubbles > 0 ? ctx->contrib.ptr : nullptr;
+    r.grp_base = ctx->grp_base.ptr;
     r.seg_ptr = ctx->seg_ptr.ptr;
+    r.chunk_ptr = ctx->chunk_ptr.ptr;
     r.param_at = ctx->param_at.ptr;
     r.tile_ptr = ctx->tile_ptr.ptr;
     r.n_tiles = ctx->n_tiles;
@@ -1269,7 +1321,7 @@ int rmin_prepare(wfsa_dev* ctx) {
 // trav_done: the evaluation just enqueued already produced every string's
 // value (ctx->rm_eval: its weighted traversal passes ran the min forward and
 // its bubble passes accumulated log(min path / Z) per string)
-int enqueue_rmin(wfsa_dev* ctx, const unsigned* halted, double* res, int par = 0, wfsa::QnArgs* q = nullptr,
+int enqueue_rmin(wfsa_dev* ctx, const unsigned* halted, double* res, int par = 0, wfsa::QnFinish* q = nullptr,
                  bool trav_done = false) {
     hipStream_t s = ctx->stream;
     if (ctx->mpath) {
@@ -1335,6 +1387,8 @@ int enqueue_iteration(wfsa_dev* ctx, bool want_logq) {
 // QN step kernel that completes the members' gradients itself, or the
 // reduction, the all-reduce (communicator) and the QN step kernel.  The QN
 // kernel's last block publishes the step's info row (ring slot e % depth).
+int flush_qn_finish(wfsa_dev* ctx);
+
 int enqueue_qn_step(wfsa_dev* ctx, double eta, double tol, int64_t e, bool timed) {
     hipStream_t s = ctx->stream;
     const int32_t np = ctx->n_params;
@@ -1347,6 +1401,18 @@ int enqueue_qn_step(wfsa_dev* ctx, double eta, double tol, int64_t e, bool timed
     const bool fuse_rmin = ctx->qn_rmin && !ctx->mpath;   // traversal strings' rmin inside their weighted passes
     if (fuse_rmin)
         if (int rc = rmin_prepare(ctx)) return rc;
+    if (ctx->fin_pending) {   // the previous step's finish: in this step's stream kernel, or its own launch
+        static const bool host_fin = [] {
+            const char* e = std::getenv("WFSA_FIN_HOST");
+            return !(e && e[0] == '0');
+        }();
+        if (ctx->fin_hostable && fused && ctx->n_groups > 0 && host_fin) {
+            ctx->fin_for_fbs = ctx->fin_next;
+            ctx->fin_pending = false;
+        } else if (int rc = flush_qn_finish(ctx)) {
+            return rc;
+        }
+    }
     ctx->rm_eval = fuse_rmin;
     const int erc = enqueue_evaluation(ctx, false, ctx->qn_halted.ptr, timed ? slot : -1, !fused && trellis, &n_ll);
     ctx->rm_eval = false;
@@ -1354,13 +1420,18 @@ int enqueue_qn_step(wfsa_dev* ctx, double eta, double tol, int64_t e, bool timed
     if (ctx->comm)
         RCCL_TRY(ncclAllReduce(ctx->out.ptr, ctx->out.ptr, size_t(np) + 1, ncclDouble, ncclSum, ctx->comm, s));
     wfsa::QnArgs q{};
+    wfsa::QnFinish& f = q.fin;
     q.out = ctx->out.ptr;
+    q.use_out = !fused || ctx->n_fall[0] + ctx->n_fall[1] + ctx->n_fall[2] > 0;
+    f.out0 = ctx->out.ptr;
     if (fused) {
         q.fixed = ctx->n_groups > 0 ? ctx->fixed_grad.ptr : nullptr;
         q.contrib = ctx->n_bubbles > 0 ? ctx->contrib.ptr : nullptr;
+        q.grp_base = ctx->grp_base.ptr;   // constraint c = reduction group c
         q.seg_ptr = ctx->seg_ptr.ptr;
-        q.ll_part = ctx->ll_cur;
-        q.n_ll = n_ll;
+        q.chunk_ptr = ctx->chunk_ptr.ptr;
+        f.ll_part = ctx->ll_cur;
+        f.n_ll = n_ll;
     } else if (trellis && ctx->comm && ctx->n_groups > 0) {
         q.fixed = ctx->fixed_grad.ptr;   // all-reduced once at preparation
     }
@@ -1377,26 +1448,45 @@ int enqueue_qn_step(wfsa_dev* ctx, double eta, double tol, int64_t e, bool timed
     q.w_full = ctx->w_full.ptr;
     q.ewp = ctx->ewp.ptr;
     q.partial = ctx->qn_partial.ptr;
-    q.ticket = ctx->qn_ticket.ptr;
-    q.plogp = ctx->qn_plogp;
     q.eta = eta;
-    q.tol = tol;
     q.exp_lambda = ctx->qn_exp_lambda;
-    q.ring_slot = slot;
     q.halted = ctx->qn_halted.ptr;
-    q.seq = ctx->counters.ptr;
-    q.host_flag = ctx->flag_dev;
-    q.host_ring = ctx->qn_ring_dev;
+    f.partial = ctx->qn_partial.ptr;
+    f.n_blocks = std::max(ctx->qn_k, 1);
+    f.k = ctx->qn_k;
+    f.plogp = ctx->qn_plogp;
+    f.tol = tol;
+    f.ring_slot = slot;
+    f.halted = ctx->qn_halted.ptr;
+    f.halt_pending = ctx->qn_halted.ptr + 1;
+    f.seq = ctx->counters.ptr;
+    f.host_flag = ctx->flag_dev;
+    f.host_ring = ctx->qn_ring_dev;
     if (ctx->qn_rmin) {
         double* res = ctx->rm_res.ptr + 2 * par;
         if (ctx->mpath) {
             if (int rc = enqueue_rmin(ctx, ctx->qn_halted.ptr, res)) return rc;
-            q.rmin = res;
-        } else if (int rc = enqueue_rmin(ctx, ctx->qn_halted.ptr, res, par, &q, true)) {
+            f.rmin = res;
+        } else if (int rc = enqueue_rmin(ctx, ctx->qn_halted.ptr, res, par, &f, true)) {
             return rc;
         }
     }
     HIP_TRY(wfsa::launch_qn_step(q, fused, s));
+    // the finish reads the step's log-likelihood partials: it can ride in the
+    // next step's stream kernel when those are not in `out` (which that
+    // kernel zeroes); else it is launched when the next step is enqueued
+    ctx->fin_next = f;
+    ctx->fin_next.active = 1;
+    ctx->fin_pending = true;
+    ctx->fin_hostable = fused && ctx->n_groups > 0 && f.ll_part != nullptr;
+    return WFSA_OK;
+}
+
+// the pending finish of the last enqueued QN step as its own launch
+int flush_qn_finish(wfsa_dev* ctx) {
+    if (!ctx->fin_pending) return WFSA_OK;
+    ctx->fin_pending = false;
+    HIP_TRY(wfsa::launch_qn_finish(ctx->fin_next, ctx->stream));
     return WFSA_OK;
 }
 
@@ -1555,6 +1645,7 @@ int wfsa_dev_load_model(wfsa_dev* ctx, const wfsa_model_desc* model) {
     if (!model) return fail(WFSA_ERR_ARG, "null model");
     drop_graph(ctx);
     ctx->slot_order.clear();   // (a QN set-up belongs to the previous model)
+    ctx->slot_groups.clear();
     ctx->qn_fused = false;
     if (ctx->mpath) {   // leaving matrix-file mode: the corpus went with the matrices
         ctx->mpath.reset();
@@ -1823,6 +1914,17 @@ int wfsa_dev_objective_grad_begin(wfsa_dev* ctx, const double* w_full, int want_
     if (ctx->prep_level < 2)
         if (int rc = prepare(ctx, 2)) return rc;
     if (int rc = collect_timing(ctx)) return rc;
+    if (std::getenv("WFSA_VERBOSE") && !ctx->h_seg_ptr.empty() && ctx->qn_fused) {   // slots per constraint
+        const int32_t k = ctx->qn_k;
+        const std::vector<int32_t>& cptr = ctx->h_cptr;
+        std::vector<int64_t> sz;
+        for (int32_t c = 0; c < k; ++c) sz.push_back(ctx->h_seg_ptr[size_t(cptr[size_t(c) + 1])] - ctx->h_seg_ptr[size_t(cptr[size_t(c)])]);
+        std::sort(sz.begin(), sz.end());
+        if (!sz.empty())
+            std::fprintf(stderr, "[wfsa] slots per constraint: total %lld, max %lld, p99 %lld, p50 %lld\n",
+                         (long long)ctx->h_seg_ptr.back(), (long long)sz.back(), (long long)sz[sz.size() * 99 / 100],
+                         (long long)sz[sz.size() / 2]);
+    }
     hipStream_t s = ctx->stream;
     const int32_t np = ctx->n_params;
     double* win = ctx->pinned + weights_off(np);   // weights in
@@ -1920,9 +2022,7 @@ int wfsa_dev_qn_setup(wfsa_dev* ctx, const wfsa_qn_desc* d) {
     for (DevBuf<double>* b : {&ctx->qn_x, &ctx->qn_expx, &ctx->qn_grad}) HIP_TRY(b->alloc(size_t(std::max(n, 1))));
     HIP_TRY(ctx->qn_lambda.alloc(size_t(std::max(k, 1))));
     HIP_TRY(ctx->qn_partial.alloc(size_t(std::max(k, 1)) * 4));
-    HIP_TRY(ctx->qn_halted.alloc(1));
-    HIP_TRY(ctx->qn_ticket.alloc(1));
-    HIP_TRY(hipMemsetAsync(ctx->qn_ticket.ptr, 0, sizeof(unsigned), s));
+    HIP_TRY(ctx->qn_halted.alloc(2));   // halted, halt_pending
     if (!ctx->qn_ring) {
         HIP_TRY(hipHostMalloc(reinterpret_cast<void**>(&ctx->qn_ring), sizeof(double) * kQnDepth * wfsa::kQnRow,
                               hipHostMallocMapped | hipHostMallocCoherent));
@@ -1949,9 +2049,11 @@ int wfsa_dev_qn_setup(wfsa_dev* ctx, const wfsa_qn_desc* d) {
         for (int32_t j = 0; j < nf; ++j)
             if (pos_of[size_t(j)] < 0) pos_of[size_t(j)] = nxt++;
         ctx->slot_order = pos_of;
+        ctx->slot_groups = cptr;   // the constraints lead the reduction groups
         if (ctx->prep_level >= 2 && !ctx->dense && !ctx->mpath)
             if (int rc = layout_slots(ctx, pos_of)) return rc;
     }
+    ctx->h_cptr = cptr;
     ctx->qn_ready = true;
     return WFSA_OK;
 }
@@ -1992,8 +2094,21 @@ int wfsa_dev_qn_run(wfsa_dev* ctx, double eta, double tol, int32_t max_steps, do
     if (ctx->prep_level < 2)
         if (int rc = prepare(ctx, 2)) return rc;
     if (int rc = collect_timing(ctx)) return rc;
+    if (std::getenv("WFSA_VERBOSE") && !ctx->h_seg_ptr.empty() && ctx->qn_fused) {   // slots per constraint
+        const int32_t k = ctx->qn_k;
+        const std::vector<int32_t>& cptr = ctx->h_cptr;
+        std::vector<int64_t> sz;
+        for (int32_t c = 0; c < k; ++c) sz.push_back(ctx->h_seg_ptr[size_t(cptr[size_t(c) + 1])] - ctx->h_seg_ptr[size_t(cptr[size_t(c)])]);
+        std::sort(sz.begin(), sz.end());
+        if (!sz.empty())
+            std::fprintf(stderr, "[wfsa] slots per constraint: total %lld, max %lld, p99 %lld, p50 %lld\n",
+                         (long long)ctx->h_seg_ptr.back(), (long long)sz.back(), (long long)sz[sz.size() * 99 / 100],
+                         (long long)sz[sz.size() / 2]);
+    }
     hipStream_t s = ctx->stream;
-    HIP_TRY(hipMemsetAsync(ctx->qn_halted.ptr, 0, sizeof(unsigned), s));
+    HIP_TRY(hipMemsetAsync(ctx->qn_halted.ptr, 0, 2 * sizeof(unsigned), s));
+    ctx->fin_pending = false;
+    ctx->fin_for_fbs.active = 0;
     const unsigned base = ctx->seq;
     int32_t enq = 0, done = 0, st = 0;
     bool stop = false;
@@ -2005,6 +2120,8 @@ int wfsa_dev_qn_run(wfsa_dev* ctx, double eta, double tol, int32_t max_steps, do
             ++enq;
             ++ctx->seq;
         }
+        if (stop || enq == max_steps)   // no next step will carry the last one's finish
+            if (int rc = flush_qn_finish(ctx)) return rc;
         if (done >= enq) break;
         if (int rc = wait_published(ctx, base + unsigned(done) + 1u)) return rc;
         const int slot = done % kQnDepth;
@@ -2033,6 +2150,7 @@ int wfsa_dev_qn_run(wfsa_dev* ctx, double eta, double tol, int32_t max_steps, do
         }
     }
     // drain the steps enqueued after a halt (they are no-ops)
+    if (int rc = flush_qn_finish(ctx)) return rc;
     if (enq > done)
         if (int rc = wait_published(ctx, base + unsigned(enq))) return rc;
     HIP_TRY(hipStreamSynchronize(s));
