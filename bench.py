@@ -1,16 +1,30 @@
 #!/usr/bin/env python3
 """Benchmark of the MI355X forward-backward / objective-gradient path.
 
-Workload (BASELINE.json configs[2], SURVEY.md 8d "c3"): synthetic family-A
-automaton (1024 states, out-degree 8 + end, one symbol per state out of 64),
-1M distinct strings per GPU sampled from it (mean length ~32, capped at 128).
-One step = one QuasiNewtonLearner::OptimizationStep over the whole corpus:
-H2D of the weights, the forward-backward kernels, (RCCL all-reduce),
-D2H of [loglik, grad], the host O(n) update.  Inputs are resident in HBM.
+Headline workload (BASELINE.json configs[2], SURVEY.md 8d "c3"): synthetic
+family-A automaton (1024 states, out-degree 8 + end, one symbol per state out
+of 64), 1M distinct strings sampled from it (mean length ~36, capped at 128).
+With N > 1 GPUs the per-GPU shard is c4's (configs[3]: 10M strings over 8
+GPUs = 1.25M per GPU), weak scaling.
 
-Multi-GPU (weak scaling): launched by torch.distributed.run, one process per
-GPU; every rank builds the same global corpus and keeps a contiguous shard;
+One step = one QuasiNewtonLearner::OptimizationStep over the whole corpus,
+run DEVICE-RESIDENT: main.cpp's epoch loop is wfsa_learner_run ->
+wfsa_dev_qn_run, which enqueues per step the forward-backward kernels (stream
++ bubble + traversal tiers), [the RCCL all-reduce of the gradient], and the QN
+step kernel (x, lambda and the next weights stay in HBM; each step's info row
+lands in host-mapped memory).  Inputs are resident in HBM.  The same steps
+through the host binding of INTEGRATION.md section 2 (wfsa_dev_objective_grad
+per step: H2D weights, D2H [LL, grad], host QN update) are timed beside it
+(`boundary`).
+
+Multi-GPU: launched by torch.distributed.run, one process per GPU; every rank
+builds the same global corpus and keeps a contiguous shard (Learner::BuildFrom);
 the gradient + log-likelihood are summed with one RCCL all-reduce per step.
+
+After the headline (one GPU only) two sub-records run in the same process,
+each with its own roofline and CPU baseline: `dense_c5` (configs[4], the
+fp64 MFMA path) and `famB` (SURVEY 8d family B, the ambiguous automaton that
+runs on the traversal tiers).
 
 Prints ONE JSON line (rank 0).
 """
@@ -29,18 +43,29 @@ HBM_PEAK_GBS = 8000.0        # MI355X_MICROARCH.md: HBM3E 8 TB/s (spec)
 F64_MFMA_PEAK_TFS = 78.6     # MI355X spec: FP64 matrix (dense) 78.6 TF (= the FP64 vector rate)
 METRIC = "forward-backward strings/sec @1/2/4/8 GPU; log-lik rel-err vs MKL ref"
 
+# SURVEY.md 8d families: automaton, corpus size per GPU, default steps/warmup, CPU sample
+WORKLOADS = {
+    "c3": dict(states=1024, degree=8, vocab=64, emissions=1, dense=False, strings_per_gpu=1_000_000,
+               steps=200, warmup=10, cpu_sample=200_000),
+    "c5": dict(states=4096, degree=8, vocab=16, emissions=16, dense=True, strings_per_gpu=4096,
+               steps=10, warmup=2, cpu_sample=1),
+    "famB": dict(states=1024, degree=8, vocab=16, emissions=4, dense=False, strings_per_gpu=100_000,
+                 steps=10, warmup=2, cpu_sample=400),
+}
+C4_STRINGS_PER_GPU = 1_250_000   # configs[3]: 10M strings over 8 GPUs
+
 
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--workload", choices=("c3", "c5"), default="c3",
-                    help="c3: 1024-state sparse family A, 1M strings/GPU (the headline); "
-                         "c5: dense 4096-state automaton on the fp64 MFMA path")
+    ap.add_argument("--workload", choices=tuple(WORKLOADS), default="c3",
+                    help="c3: 1024-state sparse family A, 1M strings/GPU (the headline; c4 sizing with N > 1); "
+                         "c5: dense 4096-state automaton on the fp64 MFMA path; famB: SURVEY 8d family B")
     ap.add_argument("--steps", type=int, default=None)
     ap.add_argument("--warmup", type=int, default=None)
     ap.add_argument("--strings-per-gpu", type=int, default=None)
     ap.add_argument("--states", type=int, default=None)
-    ap.add_argument("--degree", type=int, default=8)
+    ap.add_argument("--degree", type=int, default=None)
     ap.add_argument("--vocab", type=int, default=None)
     ap.add_argument("--emissions", type=int, default=None)
     ap.add_argument("--max-len", type=int, default=128)
@@ -50,18 +75,29 @@ def parse():
                          "second pass and reported as info_rmin; SURVEY 8d's timed region leaves it out)")
     ap.add_argument("--cpu-sample", type=int, default=None,
                     help="strings timed through the CPU oracle (0 = skip)")
+    ap.add_argument("--no-sub", action="store_true", help="skip the dense_c5 / famB sub-records")
+    ap.add_argument("--boundary-steps", type=int, default=50,
+                    help="steps timed through the host binding (wfsa_dev_objective_grad per step; 0 = skip)")
     ap.add_argument("--profile-traffic", default=os.path.join(ROOT, "profiles", "traffic_latest.json"),
                     help="committed PMC traffic measurement to quote (if present)")
-    a = ap.parse_args()
-    dense = a.workload == "c5"
-    defaults = dict(steps=(10 if dense else 200), warmup=(2 if dense else 10),
-                    strings_per_gpu=(4096 if dense else 1_000_000), states=(4096 if dense else 1024),
-                    vocab=(16 if dense else 64), emissions=(16 if dense else 1),
-                    cpu_sample=(1 if dense else 200_000))
-    for k, v in defaults.items():
-        if getattr(a, k) is None:
-            setattr(a, k, v)
-    return a
+    return ap.parse_args()
+
+
+def workload_args(args, name, world):
+    """the workload's parameters, command-line overrides applied to the headline only"""
+    w = dict(WORKLOADS[name])
+    w["name"] = name
+    if name == "c3" and world > 1:
+        w["strings_per_gpu"] = C4_STRINGS_PER_GPU
+        w["name"] = "c4"
+    if name == args.workload:
+        for k in ("steps", "warmup", "strings_per_gpu", "states", "degree", "vocab", "emissions", "cpu_sample"):
+            v = getattr(args, k)
+            if v is not None:
+                w[k] = v
+    w["max_len"] = args.max_len
+    w["seed"] = args.seed
+    return w
 
 
 def host_cpu():
@@ -86,11 +122,11 @@ def host_cpu():
             "omp_threads": max(1, min(want, avail, 16))}
 
 
-def cpu_baseline(syn_text, sym, off, wt, n_sample):
+def cpu_baseline_enum(syn_text, sym, off, wt, n_sample):
     """Reference algorithm restated in C (oracle/): BFS path enumeration once,
     then the SpMV chain per iteration, one core.  Also the log-likelihood of
     the same sample through the device path, for the rel-err column."""
-    from oracle import ENUM, Oracle
+    from oracle import ENUM, Oracle, TRELLIS
     import wfsa_amd as W
     n = min(n_sample, len(wt))
     s_off = off[: n + 1].copy()
@@ -119,7 +155,6 @@ def cpu_baseline(syn_text, sym, off, wt, n_sample):
     # the trellis restatement (oracle TRELLIS: forward-backward per string,
     # OpenMP over strings) on a hundredth of the sample (it visits every state
     # at every position: ~1 ms per family-A string on one core)
-    from oracle import TRELLIS
     nt_s = max(1, n // 100)
     t_off = off[: nt_s + 1].copy()
     ot = Oracle.from_arrays(syn_text, sym[: t_off[-1]].copy(), t_off, wt[:nt_s].copy(), mode=TRELLIS)
@@ -135,7 +170,7 @@ def cpu_baseline(syn_text, sym, off, wt, n_sample):
     lrn.BuildFromPacked(fsa, s_sym, s_off, s_wt)
     lrn.Finalize()
     lrn.Init(7)
-    kl_dev, _, _ = lrn.objective_grad()
+    lrn.objective_grad()
     ll_dev = lrn.info()["loglik"]
     rel = abs(ll_dev - ll_ref) / abs(ll_ref)
     return {
@@ -151,14 +186,13 @@ def cpu_baseline(syn_text, sym, off, wt, n_sample):
                         "iteration_s": t_trel,
                         "sample": f"first {nt_s} strings, oracle TRELLIS forward-backward, {nt} OpenMP threads"},
         "host": host,
-    }, rel, ll_ref, ll_dev
+    }, rel
 
 
-def cpu_baseline_dense(syn_text, sym, off, wt, n_sample):
+def cpu_baseline_trellis(syn_text, sym, off, wt, n_sample, why):
     """The oracle's trellis restatement (oracle/wfsa_oracle.c TRELLIS: dense
-    float64 forward-backward, one core) on the first strings of the corpus.
-    The reference algorithm (BFS path enumeration) cannot run this model:
-    a length-32 string has ~4096^32 paths."""
+    float64 forward-backward per string, one core) on the first strings of the
+    corpus, for automata whose paths the reference algorithm cannot enumerate."""
     from oracle import Oracle, TRELLIS
     n = min(n_sample, len(wt))
     s_off = off[: n + 1].copy()
@@ -170,16 +204,154 @@ def cpu_baseline_dense(syn_text, sym, off, wt, n_sample):
     t0 = time.perf_counter()
     o.trellis_eval(w)
     t_eval = time.perf_counter() - t0
-    host = host_cpu()
     return {
         "value": n / t_eval, "unit": "strings/s", "cores": 1, "kind": "port",
         "sample": (f"first {n} string(s) ({int(s_off[-1])} symbols) of the same corpus through oracle/wfsa_oracle.c "
-                   f"TRELLIS (dense fp64 forward-backward, one core): {t_eval:.1f} s per evaluation; "
-                   f"build incl. its structural pass {t_build:.1f} s; path enumeration (the reference "
-                   f"algorithm) is infeasible here"),
+                   f"TRELLIS (dense fp64 forward-backward, one core): {t_eval:.2f} s per evaluation; "
+                   f"build incl. its structural pass {t_build:.1f} s; {why}"),
         "iteration_s": t_eval,
-        "host": host,
+        "host": host_cpu(),
     }
+
+
+def run_workload(wl, world, rank, local_rank, distributed, dist, torch, info_rmin=False):
+    """build, warm up, time `steps` device-resident QN steps; returns the
+    measurement and the objects the extras need"""
+    import wfsa_amd as W
+    total = wl["strings_per_gpu"] * world
+    syn = W.Synthetic(n_states=wl["states"], degree=wl["degree"], vocab=wl["vocab"], emissions=wl["emissions"],
+                      dense=wl["dense"], n_strings=total, max_len=wl["max_len"], seed=wl["seed"])
+    sym, off, wt = syn.corpus()
+    fsa = W.Fsa.read_text(syn.wfsa_text)
+    lrn = W.QuasiNewtonLearner(device=local_rank)
+    if distributed:
+        uid = [W.Device.comm_unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(uid, src=0)
+        lrn.SetCommunicator(world, rank, uid[0])
+    t0 = time.perf_counter()
+    lrn.BuildFromPacked(fsa, sym, off, wt)
+    t_build = time.perf_counter() - t0
+    lrn.Finalize()
+    lrn.Init(7)
+    lrn.set_info_rmin(info_rmin)
+    info = lrn.info()
+
+    def barrier():
+        if distributed:
+            dist.barrier()
+        torch.cuda.synchronize()
+
+    # main.cpp's epoch loop runs natively (wfsa_learner_run); tol < 0 never
+    # halts, so exactly `steps` OptimizationSteps run
+    if wl["warmup"]:
+        lrn.Run(wl["warmup"], 1.0, -1.0)
+    st0 = lrn.stats()
+    barrier()
+    t0 = time.perf_counter()
+    rows = lrn.Run(wl["steps"], 1.0, -1.0)
+    barrier()
+    dt = time.perf_counter() - t0
+    assert len(rows) == wl["steps"]
+    st1 = lrn.stats()
+    if distributed:
+        t = torch.tensor([dt], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+    return dict(wl=wl, syn=syn, sym=sym, off=off, wt=wt, fsa=fsa, lrn=lrn, info=info, st0=st0, st1=st1, dt=dt,
+                t_build=t_build, barrier=barrier,
+                value=info["n_strings"] * wl["steps"] / dt, ms_per_step=dt * 1e3 / wl["steps"],
+                local_sym=int(off[info["shard_end"]] - off[info["shard_begin"]]))
+
+
+def workload_label(wl, off):
+    mean = float(np.diff(off).mean())
+    if wl["dense"]:
+        return (f"{wl['name']} dense: {wl['states']}-state WFSA, full transition matrix (every S->T and S->$), every "
+                f"state emits every one of {wl['vocab']} symbols, {wl['strings_per_gpu']} distinct strings per GPU "
+                f"sampled from it (mean len {mean:.1f}, max {wl['max_len']})")
+    fam = "family A" if wl["emissions"] == 1 else "family B"
+    return (f"{wl['name']} {fam}: {wl['states']}-state sparse WFSA, out-degree {wl['degree']}+end, "
+            f"{wl['emissions']} of {wl['vocab']} symbols/state, {wl['strings_per_gpu']} distinct strings per GPU "
+            f"(mean len {mean:.1f}, max {wl['max_len']})")
+
+
+def roofline_of(m, traffic):
+    """the dominant kernel's roofline: fbs_kernel (compiled streams, c3/c4),
+    the dense GEMM evaluation (c5), the traversal tiers (family B)"""
+    wl, st0, st1 = m["wl"], m["st0"], m["st1"]
+    timed = max(st1["fb_launches"] - st0["fb_launches"], 1)
+    kern_ms = (st1["compiled_kernel_ms"] - st0["compiled_kernel_ms"]) / timed   # k0..kc: the stream kernel
+    fb_ms = (st1["fb_kernel_ms"] - st0["fb_kernel_ms"]) / timed                 # k0..k2: every evaluation kernel
+    local_strings = max(m["info"]["n_local_strings"], 1)
+    mean_sym = m["local_sym"] / local_strings
+    if wl["dense"]:
+        # SURVEY.md 8d (c5): 3 GEMM-equivalents of 2 N^2 flops per string
+        # position (forward, backward, gradient); every evaluation kernel is
+        # inside the timed span (weights, GEMMs, log q, reductions)
+        N = wl["states"]
+        alg_flops = 6.0 * N * N * m["local_sym"]
+        npd, R, T = st1["dense_np"], st1["dense_rows"], st1["dense_steps"]
+        tf = alg_flops / (fb_ms * 1e-3) / 1e12 if fb_ms > 0 else None
+        return {"bound": "mfma", "achieved": tf, "peak": F64_MFMA_PEAK_TFS, "unit": "TFLOP/s",
+                "frac": tf / F64_MFMA_PEAK_TFS if tf else None, "traffic": None,
+                "kernel": "dense_gemm_kernel<FWD/BWD/GRAD> (v_mfma_f64_16x16x4f64) + its epilogue kernels, one evaluation",
+                "timed_launches": timed, "evaluation_ms": fb_ms, "algorithmic_flops_per_evaluation": alg_flops,
+                "issued_flops_per_evaluation": 6.0 * npd * npd * R * max(T - 1, 0), "row_slots": R, "trellis_steps": T}
+    comp = st1["compiled_strings"]
+    trav = st1["fallback_strings"]
+    live = st1["last_live_edges"]
+    if comp >= trav:   # the stream kernel dominates (c3/c4)
+        alg_bytes = int(mean_sym * comp) + 16 * comp   # SURVEY 8d: string bytes + offset + p per string
+        achieved = alg_bytes / (kern_ms * 1e-3) / 1e9 if kern_ms > 0 else None   # None: WFSA_TIMING=0
+        return {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": achieved / HBM_PEAK_GBS if achieved else None, "traffic": traffic,
+                "kernel": "fbs_kernel (compiled-stream forward pass + fused bubbles, per step)",
+                "timed_launches": timed, "kernel_ms_per_launch": kern_ms, "all_fb_kernels_ms_per_step": fb_ms,
+                "algorithmic_bytes_per_launch": alg_bytes}
+    # family B: the traversal tiers (k_c..k_2 of the evaluation)
+    trav_ms = max(fb_ms - kern_ms, 1e-9)
+    alg_bytes = int(mean_sym * trav) + 16 * trav
+    achieved = alg_bytes / (trav_ms * 1e-3) / 1e9
+    out = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+           "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+           "kernel": "traversal tiers (trav_kernel<MODE_WEIGHTED> tiers 0/1 + wide_kernel tier 2), per step",
+           "timed_launches": timed, "kernel_ms_per_launch": trav_ms, "all_fb_kernels_ms_per_step": fb_ms,
+           "algorithmic_bytes_per_launch": alg_bytes, "traversal_strings": trav,
+           "note": "HBM is not the binding level here (SURVEY 8d: a dependent L-step chain + LDS/L2 gathers)"}
+    if live > 0:   # ~6 fp64 flops per live trellis edge (forward FMA, backward FMA, posterior mul+add)
+        eps = live / (fb_ms * 1e-3)
+        out.update({"live_edges_per_evaluation": live, "edge_ops_per_s": eps,
+                    "fp64_flops_frac": 6.0 * eps / (F64_MFMA_PEAK_TFS * 1e12)})
+    return out
+
+
+def boundary_steps(m, k):
+    """the same steps through the host binding (INTEGRATION.md section 2:
+    wfsa_dev_objective_grad per step, H2D weights, D2H [LL, grad], host QN update)"""
+    lrn = m["lrn"]
+    lrn.Init(7)
+    for _ in range(3):
+        lrn.OptimizationStep(1.0, -1.0)
+    m["barrier"]()
+    t0 = time.perf_counter()
+    for _ in range(k):
+        lrn.OptimizationStep(1.0, -1.0)
+    m["barrier"]()
+    dt = time.perf_counter() - t0
+    return {"ms_per_step": dt * 1e3 / k, "value": m["info"]["n_strings"] * k / dt, "steps": k,
+            "note": "QuasiNewtonLearner::OptimizationStep through the C ABI a maintainer binds (wfsa_dev_objective_grad: "
+                    "host weights in over PCIe, [LL, grad] out, the QN update on the host)"}
+
+
+def record(m, traffic, cpu):
+    wl = m["wl"]
+    return {"metric": METRIC, "value": m["value"], "unit": "strings/s", "steps": wl["steps"], "warmup": wl["warmup"],
+            "ms_per_step": m["ms_per_step"], "dtype": "f64",
+            "config": {"workload": workload_label(wl, m["off"]), "strings_per_gpu": wl["strings_per_gpu"],
+                       "step": "device-resident QN loop (wfsa_dev_qn_run: evaluation kernels + QN step kernel per step)"},
+            "roofline": roofline_of(m, traffic), "cpu_baseline": cpu,
+            "compiled_strings": m["st1"]["compiled_strings"], "fallback_strings": m["st1"]["fallback_strings"],
+            "tier2_strings": m["st1"]["tier2_strings"], "build_s": m["t_build"]}
 
 
 def main():
@@ -195,163 +367,65 @@ def main():
         dist.init_process_group("gloo")   # rendezvous / timing barrier only; the data path is RCCL
     torch.cuda.set_device(local_rank)
 
-    import wfsa_amd as W
-
-    total = args.strings_per_gpu * world
-    dense = args.workload == "c5"
-    syn = W.Synthetic(n_states=args.states, degree=args.degree, vocab=args.vocab, emissions=args.emissions,
-                      dense=dense, n_strings=total, max_len=args.max_len, seed=args.seed)
-    sym, off, wt = syn.corpus()
-    fsa = W.Fsa.read_text(syn.wfsa_text)
-
-    lrn = W.QuasiNewtonLearner(device=local_rank)
-    if distributed:
-        uid = [W.Device.comm_unique_id() if rank == 0 else None]
-        dist.broadcast_object_list(uid, src=0)
-        lrn.SetCommunicator(world, rank, uid[0])
-    t0 = time.perf_counter()
-    lrn.BuildFromPacked(fsa, sym, off, wt)
-    t_build = time.perf_counter() - t0
-    lrn.Finalize()
-    lrn.Init(7)
-    lrn.set_info_rmin(args.info_rmin)
-    info = lrn.info()
-    local_sym = int(off[info["shard_end"]] - off[info["shard_begin"]])
-    local_strings = info["n_local_strings"]
-
-    def barrier():
-        if distributed:
-            dist.barrier()
-        torch.cuda.synchronize()
-
-    # main.cpp's epoch loop runs natively (wfsa_learner_run); tol < 0 never
-    # halts, so exactly `steps` OptimizationSteps run
-    if args.warmup:
-        lrn.Run(args.warmup, 1.0, -1.0)
-    st0 = lrn.stats()
-    barrier()
-    t0 = time.perf_counter()
-    rows = lrn.Run(args.steps, 1.0, -1.0)
-    barrier()
-    assert len(rows) == args.steps
-    dt = time.perf_counter() - t0
-    st1 = lrn.stats()
-    if distributed:
-        t = torch.tensor([dt], dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        dt = float(t.item())
-
-    strings_all = info["n_strings"]
-    value = strings_all * args.steps / dt
-    # the same steps with the rmin info column (QuasiNewtonLearner::
-    # GetOptimizationInfo's smallest relative path probability), which the
-    # reference prints each epoch but computes outside OptimizationStep
-    rmin_pass = None
-    if not args.info_rmin and not distributed and not dense:
-        lrn.set_info_rmin(True)
-        lrn.Run(2, 1.0, -1.0)
-        barrier()
-        t1 = time.perf_counter()
-        rrows = lrn.Run(args.steps, 1.0, -1.0)
-        barrier()
-        dtr = time.perf_counter() - t1
-        rmin_pass = {"ms_per_step": dtr * 1e3 / args.steps, "value": strings_all * args.steps / dtr,
-                     "last_rmin": float(rrows[-1][5]) if len(rrows) else None,
-                     "note": "the headline steps plus the rmin info column (the (min, x) passes fused into "
-                             "the evaluation's bubble / traversal kernels)"}
-        lrn.set_info_rmin(False)
-    # the device times a sample of the steps' kernels with HIP events (every
-    # 4th step: an event between two kernels idles the device for a few us)
-    timed = max(st1["fb_launches"] - st0["fb_launches"], 1)
-    kern_ms = (st1["compiled_kernel_ms"] - st0["compiled_kernel_ms"]) / timed
-    fb_ms = (st1["fb_kernel_ms"] - st0["fb_kernel_ms"]) / timed
-    # algorithmic bytes: string bytes + offset + p per string,
-    # for the strings the compiled kernel serves
-    comp = st1["compiled_strings"]
-    alg_bytes = int(local_sym * comp / max(local_strings, 1)) + 16 * comp
-    achieved = alg_bytes / (kern_ms * 1e-3) / 1e9 if kern_ms > 0 else None   # None: WFSA_TIMING=0
+    wl = workload_args(args, args.workload, world)
+    m = run_workload(wl, world, rank, local_rank, distributed, dist, torch, info_rmin=args.info_rmin)
+    lrn, st1 = m["lrn"], m["st1"]
     traffic = None
-    if not dense and os.path.exists(args.profile_traffic):
+    if not wl["dense"] and wl["emissions"] == 1 and os.path.exists(args.profile_traffic):
         try:
             traffic = json.load(open(args.profile_traffic)).get("hbm_bytes_per_launch")
         except Exception:
             traffic = None
 
-    if dense:
-        # 3 GEMM-equivalents of 2 N^2 flops per string
-        # position (forward, backward, gradient); every evaluation kernel is
-        # inside the timed span (weights, GEMMs, log q, reductions)
-        N = args.states
-        alg_flops = 6.0 * N * N * local_sym
-        npd, R, T = st1["dense_np"], st1["dense_rows"], st1["dense_steps"]
-        issued = 6.0 * npd * npd * R * max(T - 1, 0)
-        tf = alg_flops / (fb_ms * 1e-3) / 1e12 if fb_ms > 0 else None
-        workload = (f"c5 dense: {N}-state WFSA, full transition matrix (every S->T and S->$), every state "
-                    f"emits every one of {args.vocab} symbols, {args.strings_per_gpu} distinct strings per GPU "
-                    f"sampled from it (mean len {np.diff(off).mean():.1f}, max {args.max_len})")
-        roofline = {
-            "bound": "mfma",
-            "achieved": tf,
-            "peak": F64_MFMA_PEAK_TFS,
-            "unit": "TFLOP/s",
-            "frac": tf / F64_MFMA_PEAK_TFS if tf else None,
-            "traffic": None,
-            "kernel": "dense_gemm_kernel<FWD/BWD/GRAD> (v_mfma_f64_16x16x4f64) + its epilogue kernels, one evaluation",
-            "timed_launches": timed,
-            "evaluation_ms": fb_ms,
-            "algorithmic_flops_per_evaluation": alg_flops,
-            "issued_flops_per_evaluation": issued,
-            "row_slots": R,
-            "trellis_steps": T,
-        }
-    else:
-        workload = (f"c3 family A: {args.states}-state sparse WFSA, out-degree {args.degree}+end, "
-                    f"{args.emissions} of {args.vocab} symbols/state, {args.strings_per_gpu} distinct "
-                    f"strings per GPU (mean len {np.diff(off).mean():.1f}, max {args.max_len})")
-        roofline = {
-            "bound": "hbm",
-            "achieved": achieved,
-            "peak": HBM_PEAK_GBS,
-            "unit": "GB/s",
-            "frac": achieved / HBM_PEAK_GBS if achieved else None,
-            "traffic": traffic,
-            "kernel": "fbs_kernel (compiled-stream forward pass, per-iteration)",
-            "timed_launches": timed,
-            "kernel_ms_per_launch": kern_ms,
-            "all_fb_kernels_ms_per_step": fb_ms,
-            "algorithmic_bytes_per_launch": alg_bytes,
-        }
+    # the same steps with the rmin info column (QuasiNewtonLearner::
+    # GetOptimizationInfo's smallest relative path probability), which the
+    # reference prints each epoch but computes outside OptimizationStep
+    rmin_pass = None
+    if not args.info_rmin and not distributed and not wl["dense"]:
+        lrn.set_info_rmin(True)
+        lrn.Run(2, 1.0, -1.0)
+        m["barrier"]()
+        t1 = time.perf_counter()
+        rrows = lrn.Run(wl["steps"], 1.0, -1.0)
+        m["barrier"]()
+        dtr = time.perf_counter() - t1
+        rmin_pass = {"ms_per_step": dtr * 1e3 / wl["steps"], "value": m["info"]["n_strings"] * wl["steps"] / dtr,
+                     "last_rmin": float(rrows[-1][5]) if len(rrows) else None,
+                     "note": "the headline steps plus the rmin info column (the (min, x) passes fused into "
+                             "the evaluation's bubble / traversal kernels)"}
+        lrn.set_info_rmin(False)
+    boundary = boundary_steps(m, args.boundary_steps) if args.boundary_steps > 0 else None
 
     out = {
         "metric": METRIC,
-        "value": value,
+        "value": m["value"],
         "unit": "strings/s",
         "n_gpus": n_gpus,
-        "steps": args.steps,
-        "warmup": args.warmup,
-        "ms_per_step": dt * 1e3 / args.steps,
+        "steps": wl["steps"],
+        "warmup": wl["warmup"],
+        "ms_per_step": m["ms_per_step"],
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "f64",
         "data": "synthetic",
         "config": {
-            "workload": workload,
-            "global_strings": strings_all,
-            "strings_per_gpu": args.strings_per_gpu,
+            "workload": workload_label(wl, m["off"]),
+            "global_strings": m["info"]["n_strings"],
+            "strings_per_gpu": wl["strings_per_gpu"],
             "parallelism": f"dp{n_gpus}",
-            "step": "QuasiNewtonLearner::OptimizationStep (H2D w, forward-backward, all-reduce, D2H grad, host update; epoch loop in wfsa_learner_run)",
+            "step": ("device-resident QN loop: wfsa_learner_run -> wfsa_dev_qn_run enqueues per step the "
+                     "forward-backward kernels, " + ("the RCCL all-reduce, " if distributed else "") +
+                     "and the QN step kernel (x, lambda, weights stay in HBM; info rows to host-mapped memory)"),
             "info_rmin": bool(args.info_rmin),
         },
+        "roofline": roofline_of(m, traffic),
         "info_rmin": rmin_pass,
-        "roofline": roofline,
-        "host_ms_per_step": {k: (st1["host_" + k + "_ms"] - st0["host_" + k + "_ms"]) /
-                             max(st1["host_steps"] - st0["host_steps"], 1)
-                             for k in ("begin", "overlap", "wait", "post")},
-        "device_call_ms_last": st1["last_call_ms"],
+        "boundary": boundary,
         "live_edges_per_step": st1["last_live_edges"],
-        "build_s": t_build,
+        "build_s": m["t_build"],
         "tier1_strings": st1["tier1_strings"],
+        "tier2_strings": st1["tier2_strings"],
         "compiled_strings": st1["compiled_strings"],
         "fallback_strings": st1["fallback_strings"],
         "stream_words": st1["stream_words"],
@@ -359,14 +433,37 @@ def main():
         "bubble_words": st1["bubble_words"],
         "prepare_ms": st1["prepare_ms"],
     }
-    if rank == 0 and world == 1 and args.cpu_sample > 0 and dense:
-        out["cpu_baseline"] = cpu_baseline_dense(syn.wfsa_text, sym, off, wt, args.cpu_sample)
-    elif rank == 0 and world == 1 and args.cpu_sample > 0:
-        cb, rel, ll_ref, ll_dev = cpu_baseline(syn.wfsa_text, sym, off, wt, args.cpu_sample)
-        out["cpu_baseline"] = cb
-        out["ll_rel_err_vs_reference_algorithm"] = rel
+    cpu_n = wl["cpu_sample"]
+    if rank == 0 and world == 1 and cpu_n > 0:
+        if wl["dense"]:
+            out["cpu_baseline"] = cpu_baseline_trellis(m["syn"].wfsa_text, m["sym"], m["off"], m["wt"], cpu_n,
+                                                       "path enumeration (the reference algorithm) is infeasible here")
+        elif wl["emissions"] == 1:
+            cb, rel = cpu_baseline_enum(m["syn"].wfsa_text, m["sym"], m["off"], m["wt"], cpu_n)
+            out["cpu_baseline"] = cb
+            out["ll_rel_err_vs_reference_algorithm"] = rel
+        else:
+            out["cpu_baseline"] = cpu_baseline_trellis(m["syn"].wfsa_text, m["sym"], m["off"], m["wt"], cpu_n,
+                                                       "the reference's BFS truncates or drops these ambiguous strings")
     else:
         out["cpu_baseline"] = None
+    del m, lrn
+    # the sub-records: configs[4] (dense, MFMA) and family B (traversal tiers)
+    if not distributed and not args.no_sub and args.workload == "c3":
+        for name in ("c5", "famB"):
+            sw = workload_args(args, name, 1)
+            try:
+                sm = run_workload(sw, 1, 0, local_rank, False, dist, torch)
+                cpu = None
+                if sw["cpu_sample"] > 0 and args.cpu_sample != 0:
+                    why = ("path enumeration (the reference algorithm) is infeasible here" if sw["dense"] else
+                           "the reference's BFS truncates or drops these ambiguous strings")
+                    cpu = cpu_baseline_trellis(sm["syn"].wfsa_text, sm["sym"], sm["off"], sm["wt"], sw["cpu_sample"],
+                                               why)
+                out["dense_c5" if name == "c5" else "famB"] = record(sm, None, cpu)
+                del sm
+            except Exception as e:   # a sub-record never takes the headline down
+                out["dense_c5" if name == "c5" else "famB"] = {"error": f"{type(e).__name__}: {e}"}
     if rank == 0:
         print(json.dumps(out), flush=True)
     if distributed:

@@ -594,6 +594,11 @@ __global__ __launch_bounds__(kWideBlock) void wide_kernel(WideArgs a) {
         }
         __syncthreads();
         bool alive = true;
+        if (COUNTING && a.live_edges && tid == 0) {   // the edges the forward gathers over, per position
+            unsigned long long ne = 0;
+            for (int i = 0; i < L; ++i) ne += (unsigned long long)(W.e_ptr[W.c_ptr[str[i] + 1]] - W.e_ptr[W.c_ptr[str[i]]]);
+            atomicAdd(a.live_edges, ne);
+        }
         for (int i = 0; i < L; ++i) {
             const int c = str[i];
             const double* Ai = A + int64_t(i) * N;
@@ -1216,9 +1221,15 @@ __global__ __launch_bounds__(1024, (DBG == 10 ? 8 : 1)) void fbs_kernel(Compiled
     };
     constexpr bool kStreams = DBG != 3 && DBG != 4;   // (timing experiments)
     if (kStreams) load(A, 0);
-    if (a.fin.active && bid == 0) {   // the previous QN step's finish (its loads beside the prefetch)
+    // the previous QN step's finish: reduced here (its loads beside the
+    // prefetch), published by thread 0 after the staging barrier (the
+    // system-scope release then holds up one wave, not the block)
+    double finfo[7];
+    unsigned fstat = kQnRan;
+    const bool fin = a.fin.active && bid == 0;
+    if (fin) {
         __shared__ double fred[kMaxBlockWaves];
-        qn_finish(a.fin, fred);
+        qn_finish_compute(a.fin, fred, finfo, fstat);
     }
     if (W_LDS && DBG != 4) {
         // stage w[0, n_params] in 16-byte pieces, all of a thread's loads
@@ -1238,6 +1249,7 @@ __global__ __launch_bounds__(1024, (DBG == 10 ? 8 : 1)) void fbs_kernel(Compiled
         }
         __syncthreads();
     }
+    if (fin && threadIdx.x == 0) qn_finish_publish(a.fin, finfo, fstat);
     const double* wsrc = W_LDS ? lds : a.w;
     double ll_acc = 0.0;
     if (a.bub_on && DBG != 8 && DBG != 10) {   // this wave's bubbles, before its streams

@@ -180,6 +180,7 @@ struct WideArgs {
     uint8_t* recognized;
     uint8_t* used;
     const unsigned* halted;
+    unsigned long long* live_edges;   // counting: += the edges the forward gathers over (or null)
     double* rmin_log;        // min mode: [S] log(min path weight / q)
 };
 // doubles of scratch per block

@@ -104,9 +104,10 @@ __device__ inline double block_reduce(double v, int op, double* red) {
 
 // A QN step's finish (QnFinish, fb_kernels.hpp), by every thread of one
 // block: the info row from the QN block partials and the log-likelihood
-// partials (fixed order), the halt decision (halt_pending, read by the next
-// QN launch), the publication.  red: kMaxBlockWaves doubles of LDS.
-__device__ inline void qn_finish(const QnFinish& f, double* red) {
+// partials (fixed order) into thread 0's info[7] and status; then
+// qn_finish_publish (thread 0): the halt decision (halt_pending, read by the
+// next QN launch) and the publication.  red: kMaxBlockWaves doubles of LDS.
+__device__ inline void qn_finish_compute(const QnFinish& f, double* red, double* info, unsigned& status) {
     const int t = int(threadIdx.x), nt = int(blockDim.x), nw = nt / 64;
     double gmin = INFINITY, gmax = -INFINITY, lmin = INFINITY, ge = 0.0;
     for (int j0 = t; j0 < f.n_blocks; j0 += 4 * nt) {   // four blocks' partials in flight per thread
@@ -156,7 +157,6 @@ __device__ inline void qn_finish(const QnFinish& f, double* red) {
                 ri = rr[w][1];
             }
         if (f.k == 0) gmin = gmax = lmin = 0.0;
-        double info[7];
         info[0] = f.plogp - (f.ll_part ? ll : *f.out0);
         info[1] = ge;
         info[2] = gmin;
@@ -174,10 +174,20 @@ __device__ inline void qn_finish(const QnFinish& f, double* red) {
         bool finite = true;
         for (int i = 0; i < 7; ++i) finite = finite && isfinite(info[i]);
         const bool halt = ge <= f.tol && fabs(gmin) <= f.tol && fabs(gmax) <= f.tol;
-        const unsigned status = !finite ? kQnNonFinite : (halt ? kQnHalted : kQnRan);
-        if (status != kQnRan) *f.halt_pending = status;   // read by the next QN launch only
-        qn_publish_row(f, info, status);
+        status = !finite ? kQnNonFinite : (halt ? kQnHalted : kQnRan);
     }
+}
+
+__device__ inline void qn_finish_publish(const QnFinish& f, const double* info, unsigned status) {
+    if (status != kQnRan) *f.halt_pending = status;   // read by the next QN launch only
+    qn_publish_row(f, info, status);
+}
+
+__device__ inline void qn_finish(const QnFinish& f, double* red) {
+    double info[7];
+    unsigned status = kQnRan;
+    qn_finish_compute(f, red, info, status);
+    if (threadIdx.x == 0) qn_finish_publish(f, info, status);
 }
 
 }  // namespace wfsa

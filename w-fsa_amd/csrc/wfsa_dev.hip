@@ -678,7 +678,10 @@ int prepare(wfsa_dev* ctx, int level) {
     HIP_TRY(hipMemsetAsync(c_bub.ptr, 0xff, SZ * sizeof(int32_t), s));   // -1: not compiled
     HIP_TRY(hipMemsetAsync(c_nbub.ptr, 0, SZ * sizeof(int32_t), s));
 
-    // 1. counting pass, tier 0 then tier 1 for strings that overflow
+    // 1. counting pass, tier 0 then tier 1 for strings that overflow; the
+    // live trellis edges of every string accumulate in ctx->live (a structural
+    // count: the work of one evaluation, whatever the weights)
+    HIP_TRY(hipMemsetAsync(ctx->live.ptr, 0, sizeof(unsigned long long), s));
     std::vector<uint8_t> ovf(SZ, 0);
     std::vector<uint8_t> tier(SZ, 0);
     auto count_pass = [&](int t, const int32_t* list, int64_t n) -> int {
@@ -730,11 +733,18 @@ int prepare(wfsa_dev* ctx, int level) {
         a.path_count = ctx->pcount.ptr;
         a.recognized = ctx->recog.ptr;
         a.used = ctx->used.ptr;
+        a.live_edges = ctx->live.ptr;
         HIP_TRY(wfsa::launch_wide(true, a, g2, s));
         HIP_TRY(hipStreamSynchronize(s));
     }
     ctx->tier2_strings = int32_t(l2.size());
     const int32_t n_tier1 = int32_t(l1.size() - l2.size());
+    {
+        unsigned long long live = 0;
+        HIP_TRY(ctx->live.download(&live, 1, s));
+        HIP_TRY(hipStreamSynchronize(s));
+        ctx->stats.last_live_edges = int64_t(live);
+    }
 
     if (level < 2) {
         ctx->stats.tier1_strings = n_tier1;
