@@ -129,7 +129,8 @@ int wfsa_dev_recognize(wfsa_dev* ctx, uint8_t* recognized, double* path_count,
  * KKT system (MKL DSS in the reference: dss_factor_real / dss_statistics
  * "Inertia", "Determinant" / dss_solve_real, src/HessianLearner.cpp:28-57,
  * 100-113; RealSymmetricLogDet src/Utils.cpp:296-350): Bunch-Kaufman LDL^T
- * (rocSOLVER dsytrf) of a[n*n] (symmetric, either layout); inertia =
+ * (our own right-looking kernels, sym_solver.hip, with LAPACK dsytf2's pivot rule
+ * and storage) of a[n*n] (symmetric, either layout); inertia =
  * {positive, negative, zero} pivots of D, log|det| and its sign.  sym_solve
  * overwrites b[n] with A^-1 b (one-workgroup dsytrs kernel). */
 int wfsa_dev_sym_factor(wfsa_dev* ctx, int64_t n, const double* a, int64_t inertia[3], double* log_abs_det,

@@ -18,38 +18,34 @@ void Corpus::ReadText(const char* text) {
     Parse(content);
 }
 
-// Line 1 is the separator (" " when empty).  Every later line is a string:
-// its tokens are concatenated and the last token is the weight
-// (src/Corpus.cpp:9-61); duplicates and weights that are not positive normal
-// numbers are errors.
+// Line 1 is the separator (" " when empty).  Every later line is a list of
+// tokens: all but the last, concatenated, form the string and the last is its
+// weight; a line of one token holds no string (src/Corpus.cpp:9-61).
+// Duplicates and weights that are not positive normal numbers are errors.
 void Corpus::Parse(std::vector<char>& content) {
     clear();
-    char* c = content.data();
-    auto result = get_word(c, "\n");
-    separator = result.first;
-    if (separator.empty()) separator = " ";
+    char* cursor = content.data();
+    const auto head = get_word(cursor, "\n");
+    separator = *head.first ? head.first : " ";
     std::unordered_set<std::string> seen;
-    std::string word;
-    while (result.second != '\0') {
-        word.clear();
-        bool empty = true;
+    std::vector<CStr> tokens;   // the current line's tokens (pointers into content)
+    for (char end = head.second; end != '\0';) {
+        tokens.clear();
         do {
-            result = get_word(c, separator.c_str());
-            if (result.second == '\n' || result.second == '\0') {
-                if (!empty) {
-                    if (!seen.insert(word).second) throw CorpusError("\"", word, "\" is duplicate!");
-                    emplace_back(word, std::atof(result.first));
-                }
-                break;
-            }
-            empty = false;
-            word += result.first;
-        } while (result.second);
+            const auto tok = get_word(cursor, separator.c_str());
+            tokens.push_back(tok.first);
+            end = tok.second;
+        } while (end != '\n' && end != '\0');
+        if (tokens.size() < 2) continue;
+        std::string str;
+        for (size_t i = 0; i + 1 < tokens.size(); ++i) str += tokens[i];
+        if (!seen.insert(str).second) throw CorpusError("\"", str, "\" is duplicate!");
+        const double weight = std::atof(tokens.back());
+        emplace_back(std::move(str), weight);
     }
-    for (const auto& w : *this) {
-        if (!std::isnormal(w.second) || w.second < 0)
-            throw CorpusError("\"", w.first, "\" has probability ", w.second, "!");
-    }
+    for (const auto& entry : *this)
+        if (!std::isnormal(entry.second) || entry.second < 0)
+            throw CorpusError("\"", entry.first, "\" has probability ", entry.second, "!");
 }
 
 void Corpus::Renormalize() {

@@ -75,52 +75,69 @@ void Fsa::Parse() {
     AssignIndices();
 }
 
+namespace {
+
+// The (key, value) tokens after a row's head, up to the line end: a state's
+// emission row "name e1 w1 e2 w2 ..." or its transition row "name t1 w1 ...".
+using Pairs = std::vector<std::pair<CStr, CStr>>;
+void read_pairs(char*& c, CStr sep, Pairs& out) {
+    out.clear();
+    std::pair<CStr, char> value;
+    do {
+        const CStr key = get_word(c, sep).first;
+        value = get_word(c, sep);
+        out.emplace_back(key, value.first);
+    } while (value.second != '\n' && value.second != '\0');
+}
+
+}  // namespace
+
+// One state: its emission row, then its transition row, which must name the
+// same state (src/Fsa.cpp:122-205).  A row starting blank or with the end
+// state's name is skipped.  The emissions / transitions are collected in
+// Keyed maps and copied out in their iteration order, and every successor is
+// entered into transition_probs before the state itself: both orders decide
+// the parameter numbering (AssignIndices), so they follow the reference's.
 void Fsa::ReadOneState(char*& c) {
-    auto result = get_word(c, separator);
-    const char* this_state = result.first;
-    if (is_empty(this_state) || contains_prefix(this_state, end_state)) {
-        get_word(c, "\n");   // comment / blank line: skip the rest of the line
+    const CStr name = get_word(c, separator).first;
+    if (is_empty(name) || contains_prefix(name, end_state)) {
+        get_word(c, "\n");
         return;
     }
-    Keyed<double> emissions, transitions;
-    do {
-        result = get_word(c, separator);
-        const char* word = result.first;
-        if (StrEq()(this_state, start_state) && !is_empty(word))
-            throw FsaError("Invalid FSA format! Start state should emit empty string instead of \"", word, "\"!");
-        auto ins = emissions.emplace(word, 0.0);
-        if (!ins.second)
-            throw FsaError("Invalid FSA format! Emission \"", word, "\" of state \"", this_state,
+    const bool is_start = StrEq()(name, start_state);
+    Pairs row;
+    read_pairs(c, separator, row);
+    Keyed<double> emissions;
+    for (const auto& kv : row) {
+        if (is_start && !is_empty(kv.first))
+            throw FsaError("Invalid FSA format! Start state should emit empty string instead of \"", kv.first, "\"!");
+        if (!emissions.emplace(kv.first, std::atof(kv.second)).second)
+            throw FsaError("Invalid FSA format! Emission \"", kv.first, "\" of state \"", name,
                            "\" appears more than once!");
-        result = get_word(c, separator);
-        ins.first->second = std::atof(result.first);
-    } while (result.second != '\n' && result.second != '\0');
+    }
     if (emissions.empty())
-        throw FsaError("Invalid FSA format! State \"", this_state,
+        throw FsaError("Invalid FSA format! State \"", name,
                        "\" should have positive number of emissions, even if empty emission!");
-    if (!StrEq()(this_state, get_word(c, separator).first))
-        throw FsaError("Invalid FSA format! You should enlist transitions of \"", this_state,
+    if (!StrEq()(name, get_word(c, separator).first))
+        throw FsaError("Invalid FSA format! You should enlist transitions of \"", name,
                        "\" after emissions of the same state!");
-    do {
-        result = get_word(c, separator);
-        const char* word = result.first;
-        auto ins = transitions.emplace(word, 0.0);
-        if (!ins.second)
-            throw FsaError("Invalid FSA format! Transition \"", this_state, "\" -> \"", word,
+    read_pairs(c, separator, row);
+    Keyed<double> transitions;
+    for (const auto& kv : row) {
+        if (!transitions.emplace(kv.first, std::atof(kv.second)).second)
+            throw FsaError("Invalid FSA format! Transition \"", name, "\" -> \"", kv.first,
                            "\" appears more than once!");
-        if (StrEq()(word, start_state))
-            throw FsaError("Invalid FSA format! \"", this_state, "\" connects to start state \"", start_state, "\"!");
-        result = get_word(c, separator);
-        ins.first->second = std::atof(result.first);
-    } while (result.second != '\n' && result.second != '\0');
+        if (StrEq()(kv.first, start_state))
+            throw FsaError("Invalid FSA format! \"", name, "\" connects to start state \"", start_state, "\"!");
+    }
     if (transitions.empty())
-        throw FsaError("Invalid FSA format! State \"", this_state, "\" should have positive number of transitions!");
+        throw FsaError("Invalid FSA format! State \"", name, "\" should have positive number of transitions!");
 
     State st;
     for (const auto& e : emissions) st.emissions.emplace_back(e.first, e.second);
     for (const auto& t : transitions)
         st.transitions.emplace_back(&(*transition_probs.emplace(t.first, State()).first), t.second);
-    transition_probs[this_state] = st;
+    transition_probs[name] = st;
 }
 
 void Fsa::AssignIndices() {

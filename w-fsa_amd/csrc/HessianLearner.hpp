@@ -44,7 +44,8 @@ private:
 class HessianLearner : public Learner {
 public:
     // n + k of the augmented system: factored on the host (Bunch-Kaufman
-    // LDL^T) up to kHostDense, above that in HBM (rocSOLVER dsytrf +
+    // LDL^T) up to kHostDense, above that in HBM (sym_solver.hip, our own
+    // Bunch-Kaufman kernels +
     // wfsa_dev_sym_solve) up to kMaxDense (17 GB of fp64); WFSA_KKT=host /
     // device forces one side
     static constexpr int64_t kHostDense = 1024;
