@@ -19,8 +19,9 @@
  *                              (src/QuasiNewtonLearner.cpp:93-125) ==
  *                              HessianLearner::ComputeGrad
  *                              (src/HessianLearner.cpp:565-597)
- *   wfsa_dev_comm_*         <- (new) one RCCL all-reduce per iteration when the
- *                              corpus is sharded over GPUs
+ *   wfsa_dev_comm_*         <- (new) one all-reduce per iteration when the
+ *                              corpus is sharded over GPUs (RCCL, or an
+ *                              in-process group of contexts)
  *
  * Conventions: plain pointers and sizes, host buffers caller-owned and only
  * touched during the call; all device memory belongs to the context.  Every
@@ -227,9 +228,15 @@ int wfsa_dev_hf_eval(wfsa_dev* ctx, const double* w_full, double* values);
 
 /* Multi-GPU: one process per GPU.  Rank 0 creates the id, the launcher
  * broadcasts the 128 bytes, every rank attaches.  wfsa_dev_allreduce sums
- * `count` doubles of a host buffer in place over the ranks. */
+ * `count` doubles of a host buffer in place over the ranks.
+ * wfsa_dev_comm_local_id makes the id of an in-process group instead: up to
+ * 16 contexts of ONE process, each driven by its own thread, on one device
+ * or on peer-enabled devices; comm_init with that id attaches a member.  The
+ * group combines the same values at the same points as RCCL (rank order,
+ * blocking), so one GPU runs every multi-rank branch of the path. */
 #define WFSA_COMM_ID_BYTES 128
 int wfsa_dev_comm_unique_id(uint8_t id[WFSA_COMM_ID_BYTES]);
+int wfsa_dev_comm_local_id(int nranks, uint8_t id[WFSA_COMM_ID_BYTES]);
 int wfsa_dev_comm_init(wfsa_dev* ctx, int nranks, int rank, const uint8_t id[WFSA_COMM_ID_BYTES]);
 int wfsa_dev_allreduce(wfsa_dev* ctx, double* host_buf, int64_t count);
 

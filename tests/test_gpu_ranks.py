@@ -1,0 +1,171 @@
+"""The product's multi-rank path on one GPU: K contexts of this process form
+an in-process group (wfsa_dev_comm_local_id), one thread per rank, and run
+exactly the branches an RCCL job runs on K GPUs -- the shard the rank keeps
+(Learner::BuildPaths' Sigma-length split), the corpus statistics all-reduce,
+the max-reduced used-parameter mask, the constant trivial gradient reduced
+once, the per-step all-reduce of [LL, grad] inside the device QN loop, the
+plogp all-reduce of Finalize.  Everything is compared with the one-context
+run and, for the first evaluation, with the ENUM oracle (the reference's
+algorithm, src/Learner.cpp:276-553).  All tests need a gfx950 device."""
+from concurrent.futures import ThreadPoolExecutor
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def _close(a, b, rel, atol=1e-13):
+    return abs(a - b) <= max(atol, rel * max(abs(a), abs(b)))
+
+
+def _with_unrecognized(sym, off, wt, n_bad=7, seed=0):
+    """append strings the automaton cannot produce (byte 0x01) at spread
+    positions, so several shards hold auxiliary parameters"""
+    rng = np.random.default_rng(seed)
+    strings = [bytes(sym[off[i]:off[i + 1]]) for i in range(len(wt))]
+    w = list(wt)
+    for k in range(n_bad):
+        pos = int(rng.integers(0, len(strings) + 1))
+        strings.insert(pos, b"\x01" * (1 + k % 3))
+        w.insert(pos, float(rng.uniform(0.5, 2.0)))
+    off2 = np.concatenate([[0], np.cumsum([len(s) for s in strings])]).astype(np.int64)
+    return np.frombuffer(b"".join(strings), dtype=np.uint8).copy(), off2, np.array(w)
+
+
+def _run_ranks(k, fn):
+    import wfsa_amd as W
+    gid = W.Device.comm_local_id(k)
+    with ThreadPoolExecutor(max_workers=k) as ex:
+        futs = [ex.submit(fn, k, r, gid) for r in range(k)]
+        return [f.result(timeout=300) for f in futs]
+
+
+FAMILIES = {
+    # compiled streams + bubbles
+    "bubbles": dict(n_states=64, degree=8, vocab=16, emissions=1, n_strings=3000, max_len=64, seed=9),
+    # ambiguous: traversal tiers 0/1 beside the compiled strings
+    "ambiguous": dict(n_states=48, degree=6, vocab=8, emissions=3, n_strings=1200, max_len=24, seed=4),
+}
+
+
+@pytest.mark.parametrize("family", sorted(FAMILIES))
+@pytest.mark.parametrize("k", [2, 3])
+def test_learner_ranks_equal_one_context(family, k):
+    import wfsa_amd as W
+    syn = W.Synthetic(**FAMILIES[family])
+    sym, off, wt = _with_unrecognized(*syn.corpus())
+    fsa = W.Fsa.read_text(syn.wfsa_text)
+
+    def learn(nranks, rank, gid):
+        lrn = W.QuasiNewtonLearner(0)
+        if nranks > 1:
+            lrn.SetCommunicator(nranks, rank, gid)
+        lrn.BuildFromPacked(fsa, sym, off, wt)
+        lrn.Finalize()
+        lrn.Init(7)
+        kl0, g0, _ = lrn.objective_grad()
+        rows = [lrn.OptimizationStep(1.0, -1.0)[0] for _ in range(3)]   # host QN update
+        rows += lrn.Run(6, 1.0, -1.0)                                   # device-resident loop
+        return lrn.info(), lrn.stats(), kl0, g0, rows, lrn.x(), lrn.trimmed_index()
+
+    one = learn(1, 0, None)
+    outs = _run_ranks(k, learn)
+    info1, _, kl1, g1, rows1, x1, trim1 = one
+    shards = []
+    for r, (info, st, kl, g, rows, x, trim) in enumerate(outs):
+        b, e = W.shard_range(off, k, r)
+        assert (info["shard_begin"], info["shard_end"]) == (b, e)
+        shards.append(e - b)
+        for key in ("n_params", "n_constraints", "n_strings", "n_paths", "n_full"):
+            assert info[key] == info1[key], key
+        for key in ("common_support", "plogp", "aux_hessian", "model_volume"):
+            assert _close(info[key], info1[key], rel=1e-12), key
+        np.testing.assert_array_equal(trim, trim1)           # the OR of the shards' used masks
+        assert _close(kl, kl1, rel=1e-12)
+        np.testing.assert_allclose(g, g1, rtol=1e-11, atol=1e-14)
+        assert len(rows) == len(rows1) == 9
+        for a, q in zip(rows, rows1):
+            for u, v in zip(a[:5], q[:5]):
+                assert _close(u, v, rel=1e-10, atol=1e-13)
+        np.testing.assert_allclose(x, x1, rtol=1e-10, atol=1e-12)
+    assert sum(shards) == len(wt) and min(shards) > 0
+    if family == "ambiguous":   # the traversal tiers ran on some rank
+        assert sum(o[1]["fallback_strings"] for o in outs) > 0
+
+
+def test_learner_ranks_match_enum_oracle():
+    """KL and gradient of the first evaluation, summed over 2 ranks, against
+    the reference algorithm on the whole corpus"""
+    import wfsa_amd as W
+    from oracle import ENUM, Oracle
+    syn = W.Synthetic(n_states=32, degree=4, vocab=6, emissions=2, n_strings=400, max_len=10, seed=9)
+    sym, off, wt = _with_unrecognized(*syn.corpus(), n_bad=3, seed=2)
+    fsa = W.Fsa.read_text(syn.wfsa_text)
+    o = Oracle.from_arrays(syn.wfsa_text, sym, off, wt, mode=ENUM, max_paths=10_000_000)
+    orows = o.qn_run(flags=7, epochs=6)
+
+    def learn(nranks, rank, gid):
+        lrn = W.QuasiNewtonLearner(0)
+        lrn.SetCommunicator(nranks, rank, gid)
+        lrn.BuildFromPacked(fsa, sym, off, wt)
+        lrn.Finalize()
+        return lrn.info(), lrn.run(flags=7, epochs=6), lrn.x(), lrn.param_names()
+
+    for info, rows, x, names in _run_ranks(2, learn):
+        assert info["n_strings"] == o.info["n_strings"]
+        assert info["n_paths"] == o.info["n_paths"]
+        assert info["n_params"] == o.info["n_params"]
+        assert len(rows) == len(orows)
+        for r, q in zip(rows, orows):
+            for a, b in zip(r[:5], q[:5]):
+                assert _close(a, b, rel=1e-8, atol=1e-11)
+        ox = dict(zip(o.param_names(), o.x()))
+        for n, v in zip(names, x):
+            assert _close(v, ox[n], rel=1e-8, atol=1e-10)
+
+
+def test_device_ranks_sum_to_the_whole():
+    """wfsa_dev_* with an in-process communicator: each context loads its
+    shard (p normalised over the whole corpus); objective_grad returns the
+    all-reduced [LL, grad] on every rank, recognize the max-reduced used
+    mask, allreduce sums host buffers -- all equal to one context"""
+    import wfsa_amd as W
+    syn = W.Synthetic(n_states=64, degree=8, vocab=16, emissions=2, n_strings=2000, max_len=40, seed=3)
+    sym, off, wt = syn.corpus()
+    p = wt / wt.sum()
+    fsa = W.Fsa.read_text(syn.wfsa_text)
+    w = np.random.default_rng(1).normal(-1.0, 0.5, size=len(fsa.param_names()))
+
+    def evaluate(nranks, rank, gid):
+        dev = W.Device(0)
+        if nranks > 1:
+            dev.comm_init(nranks, rank, gid)
+        b, e = W.shard_range(off, nranks, rank)
+        dev.load_model(fsa)
+        dev.load_corpus(sym[off[b]:off[e]], off[b:e + 1] - off[b], p[b:e])
+        rec, pc, used = dev.recognize()
+        ll, grad, logq = dev.objective_grad(w)
+        ll2, grad2, _ = dev.objective_grad(w, want_logq=False)   # the fused kernel path
+        s = dev.allreduce(np.array([float(e - b), rank + 1.0]))
+        return used, ll, grad, logq, ll2, grad2, s, (b, e)
+
+    used1, ll1, g1, logq1, _, _, _, _ = evaluate(1, 0, None)
+    outs = _run_ranks(4, evaluate)
+    logq_all = np.concatenate([o[3] for o in outs])
+    np.testing.assert_allclose(logq_all, logq1, rtol=1e-13)
+    for used, ll, grad, logq, ll2, grad2, s, _ in outs:
+        np.testing.assert_array_equal(used, used1)
+        assert _close(ll, ll1, rel=1e-12)
+        assert _close(ll2, ll1, rel=1e-12)
+        np.testing.assert_allclose(grad, g1, rtol=1e-11, atol=1e-15)
+        np.testing.assert_allclose(grad2, g1, rtol=1e-11, atol=1e-15)
+        assert s[0] == len(wt) and s[1] == 10.0
+    # a mismatched call is refused, not hung
+    def bad(nranks, rank, gid):
+        dev = W.Device(0)
+        dev.comm_init(nranks, rank, gid)
+        with pytest.raises(W.WfsaError):
+            dev.allreduce(np.zeros(1 + rank))
+        return True
+    assert all(_run_ranks(2, bad))

@@ -18,7 +18,6 @@
 #include "wfsa_dev.h"
 
 #include <hip/hip_runtime.h>
-#include <rccl/rccl.h>
 
 #include <algorithm>
 #include <chrono>
@@ -31,6 +30,7 @@
 #include <string>
 #include <vector>
 
+#include "collective.hpp"
 #include "dense_path.hpp"
 #include "matrix_path.hpp"
 #include "sym_solver.hpp"
@@ -57,10 +57,11 @@ int fail(int code, const char* fmt, ...) {
         if (e_ != hipSuccess) return fail(WFSA_ERR_HIP, "%s failed: %s", #expr, hipGetErrorString(e_)); \
     } while (0)
 
-#define RCCL_TRY(expr)                                                                                 \
+// an all-reduce over the context's communicator (collective.hpp)
+#define COMM_TRY(ctx, buf, n, op, s)                                                                      \
     do {                                                                                               \
-        ncclResult_t r_ = (expr);                                                                      \
-        if (r_ != ncclSuccess) return fail(WFSA_ERR_RCCL, "%s failed: %s", #expr, ncclGetErrorString(r_)); \
+        if ((ctx)->comm->allreduce((buf), (n), (op), (s)))                                             \
+            return fail(WFSA_ERR_RCCL, "%s all-reduce: %s", (ctx)->comm->kind(), (ctx)->comm->last_error()); \
     } while (0)
 
 // device buffer (RAII)
@@ -273,7 +274,7 @@ struct wfsa_dev {
     int64_t hf_n_slots = 0;
 
     // communicator
-    ncclComm_t comm = nullptr;
+    std::unique_ptr<wfsa::Collective> comm;
     int nranks = 1, rank = 0;
 
     wfsa_dev_stats stats{};
@@ -1056,13 +1057,11 @@ int prepare(wfsa_dev* ctx, int level) {
         // with a communicator the constant part is summed over the ranks once
         // here; the per-step all-reduce then carries only what varies
         if (ctx->comm && ctx->n_params > 0)
-            RCCL_TRY(ncclAllReduce(ctx->fixed_grad.ptr, ctx->fixed_grad.ptr, size_t(ctx->n_params), ncclDouble, ncclSum,
-                                   ctx->comm, s));
+            COMM_TRY(ctx, ctx->fixed_grad.ptr, size_t(ctx->n_params), wfsa::RedOp::SumF64, s);
     } else {
         HIP_TRY(hipMemsetAsync(ctx->fixed_grad.ptr, 0, size_t(std::max(ctx->n_params, 1)) * sizeof(double), s));
         if (ctx->comm && ctx->n_params > 0)   // (every rank joins the collective)
-            RCCL_TRY(ncclAllReduce(ctx->fixed_grad.ptr, ctx->fixed_grad.ptr, size_t(ctx->n_params), ncclDouble, ncclSum,
-                                   ctx->comm, s));
+            COMM_TRY(ctx, ctx->fixed_grad.ptr, size_t(ctx->n_params), wfsa::RedOp::SumF64, s);
     }
     HIP_TRY(hipStreamSynchronize(s));
 
@@ -1427,8 +1426,7 @@ int enqueue_qn_step(wfsa_dev* ctx, double eta, double tol, int64_t e, bool timed
     const int erc = enqueue_evaluation(ctx, false, ctx->qn_halted.ptr, timed ? slot : -1, !fused && trellis, &n_ll);
     ctx->rm_eval = false;
     if (erc) return erc;
-    if (ctx->comm)
-        RCCL_TRY(ncclAllReduce(ctx->out.ptr, ctx->out.ptr, size_t(np) + 1, ncclDouble, ncclSum, ctx->comm, s));
+    if (ctx->comm) COMM_TRY(ctx, ctx->out.ptr, size_t(np) + 1, wfsa::RedOp::SumF64, s);
     wfsa::QnArgs q{};
     wfsa::QnFinish& f = q.fin;
     q.out = ctx->out.ptr;
@@ -1633,7 +1631,7 @@ void wfsa_dev_destroy(wfsa_dev* ctx) {
     (void)hipSetDevice(ctx->device);
     if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
     drop_graph(ctx);
-    if (ctx->comm) (void)ncclCommDestroy(ctx->comm);
+    ctx->comm.reset();
     if (ctx->pinned) (void)hipHostFree(ctx->pinned);
     if (ctx->flag) (void)hipHostFree(ctx->flag);
     for (hipEvent_t ev : {ctx->ev0, ctx->ev1})
@@ -1802,7 +1800,7 @@ int wfsa_dev_recognize(wfsa_dev* ctx, uint8_t* recognized, double* path_count, u
     hipStream_t s = ctx->stream;
     const size_t S = size_t(ctx->n_strings);
     if (ctx->comm && ctx->n_params > 0)
-        RCCL_TRY(ncclAllReduce(ctx->used.ptr, ctx->used.ptr, size_t(ctx->n_params), ncclUint8, ncclMax, ctx->comm, s));
+        COMM_TRY(ctx, ctx->used.ptr, size_t(ctx->n_params), wfsa::RedOp::MaxU8, s);
     if (recognized) HIP_TRY(ctx->recog.download(recognized, S, s));
     if (path_count) HIP_TRY(ctx->pcount.download(path_count, S, s));
     if (used_param) HIP_TRY(ctx->used.download(used_param, size_t(ctx->n_params), s));
@@ -1963,7 +1961,7 @@ int wfsa_dev_objective_grad_begin(wfsa_dev* ctx, const double* w_full, int want_
     if (ctx->graph_exec) HIP_TRY(hipGraphLaunch(ctx->graph_exec, s));
     else if (int rc = enqueue_iteration(ctx, want_logq != 0)) return rc;
     if (ctx->comm) {
-        RCCL_TRY(ncclAllReduce(ctx->out.ptr, ctx->out.ptr, size_t(np) + 1, ncclDouble, ncclSum, ctx->comm, s));
+        COMM_TRY(ctx, ctx->out.ptr, size_t(np) + 1, wfsa::RedOp::SumF64, s);
         wfsa::Publish pub = publish_args(ctx);   // + the constant gradient, all-reduced once at preparation
         if (!ctx->dense && !ctx->mpath && ctx->n_groups > 0) pub.add = ctx->fixed_grad.ptr;
         HIP_TRY(wfsa::launch_publish(ctx->out.ptr, pub, s));
@@ -2305,23 +2303,27 @@ int wfsa_dev_hf_eval(wfsa_dev* ctx, const double* w_full, double* values) {
 
 int wfsa_dev_comm_unique_id(uint8_t id[WFSA_COMM_ID_BYTES]) {
     if (!id) return fail(WFSA_ERR_ARG, "null id");
-    static_assert(sizeof(ncclUniqueId) == WFSA_COMM_ID_BYTES, "ncclUniqueId size");
-    ncclUniqueId uid;
-    RCCL_TRY(ncclGetUniqueId(&uid));
-    std::memcpy(id, &uid, sizeof uid);
+    static_assert(wfsa::kCommIdBytes == WFSA_COMM_ID_BYTES, "communicator id size");
+    std::string err;
+    if (wfsa::rccl_unique_id(id, err)) return fail(WFSA_ERR_RCCL, "%s", err.c_str());
+    return WFSA_OK;
+}
+
+int wfsa_dev_comm_local_id(int nranks, uint8_t id[WFSA_COMM_ID_BYTES]) {
+    if (!id) return fail(WFSA_ERR_ARG, "null id");
+    if (nranks < 1 || nranks > wfsa::kLocalMaxRanks) return fail(WFSA_ERR_ARG, "an in-process group has 1..16 members");
+    wfsa::local_group_id(nranks, id);
     return WFSA_OK;
 }
 
 int wfsa_dev_comm_init(wfsa_dev* ctx, int nranks, int rank, const uint8_t id[WFSA_COMM_ID_BYTES]) {
     if (int rc = check_ctx(ctx)) return rc;
     if (nranks < 1 || rank < 0 || rank >= nranks || !id) return fail(WFSA_ERR_ARG, "bad communicator arguments");
-    if (ctx->comm) {
-        (void)ncclCommDestroy(ctx->comm);
-        ctx->comm = nullptr;
-    }
-    ncclUniqueId uid;
-    std::memcpy(&uid, id, sizeof uid);
-    RCCL_TRY(ncclCommInitRank(&ctx->comm, nranks, uid, rank));
+    ctx->comm.reset();
+    std::string err;
+    ctx->comm = wfsa::is_local_group_id(id) ? wfsa::make_local_collective(nranks, rank, id, ctx->device, err)
+                                            : wfsa::make_rccl_collective(nranks, rank, id, err);
+    if (!ctx->comm) return fail(WFSA_ERR_RCCL, "%s", err.c_str());
     ctx->nranks = nranks;
     ctx->rank = rank;
     // the compiled corpus' constant gradient is summed over the ranks at
@@ -2338,7 +2340,7 @@ int wfsa_dev_allreduce(wfsa_dev* ctx, double* host_buf, int64_t count) {
     if (!ctx->comm) return WFSA_OK;   // single rank: the sum is the input
     DevBuf<double> tmp;
     HIP_TRY(tmp.upload(host_buf, size_t(count), ctx->stream));
-    RCCL_TRY(ncclAllReduce(tmp.ptr, tmp.ptr, size_t(count), ncclDouble, ncclSum, ctx->comm, ctx->stream));
+    COMM_TRY(ctx, tmp.ptr, size_t(count), wfsa::RedOp::SumF64, ctx->stream);
     HIP_TRY(tmp.download(host_buf, size_t(count), ctx->stream));
     HIP_TRY(hipStreamSynchronize(ctx->stream));
     return WFSA_OK;

@@ -427,6 +427,14 @@ class Device:
         check_dev(load().wfsa_dev_comm_unique_id(buf))
         return bytes(buf)
 
+    @staticmethod
+    def comm_local_id(nranks):
+        """id of an in-process group: `nranks` contexts of this process, one
+        thread each (wfsa_dev_comm_local_id)"""
+        buf = (C.c_uint8 * _lib.COMM_ID_BYTES)()
+        check_dev(load().wfsa_dev_comm_local_id(nranks, buf))
+        return bytes(buf)
+
     def allreduce(self, values):
         a = np.ascontiguousarray(values, dtype=np.float64).copy()
         check_dev(load().wfsa_dev_allreduce(self._h, _ptr(a), len(a)))

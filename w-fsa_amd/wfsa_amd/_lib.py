@@ -85,6 +85,7 @@ _SIGS = {
     "wfsa_dev_hf_eval": (C.c_int, [vp, vp, vp]),
     "wfsa_dev_comm_unique_id": (C.c_int, [vp]),
     "wfsa_dev_comm_init": (C.c_int, [vp, C.c_int, C.c_int, vp]),
+    "wfsa_dev_comm_local_id": (C.c_int, [C.c_int, vp]),
     "wfsa_dev_allreduce": (C.c_int, [vp, vp, i64]),
     "wfsa_dev_get_stats": (C.c_int, [vp, P(DevStats)]),
     # host mirror (wfsa_host.h)
