@@ -218,7 +218,9 @@ int wfsa_dev_qn_run(wfsa_dev* ctx, double eta, double tol, int32_t max_steps, do
  *   hf_setup: builds the pattern -- the pairs (j, k), j <= k, of Fsa
  *             parameters whose counts vary together on some string -- after the
  *             corpus is compiled; fails (WFSA_ERR_CAPACITY) when a string is
- *             not compiled into bubbles, on the dense path, with a communicator.
+ *             not compiled into bubbles (on any rank), on the dense path.  With a
+ *             communicator the pattern is the union over the ranks and
+ *             hf_eval's values are all-reduced.
  *   hf_pairs: the pattern, pairs[2 t], pairs[2 t + 1] (ascending).
  *   hf_eval:  values[t] = sum_s p_s Cov_s(count_j, count_k) at w_full
  *             (HessianLearner adds -values to H). */

@@ -86,7 +86,7 @@ def test_learner_ranks_equal_one_context(family, k):
         np.testing.assert_allclose(g, g1, rtol=1e-11, atol=1e-14)
         assert len(rows) == len(rows1) == 9
         for a, q in zip(rows, rows1):
-            for u, v in zip(a[:5], q[:5]):
+            for u, v in zip(a[:7], q[:7]):
                 assert _close(u, v, rel=1e-10, atol=1e-13)
         np.testing.assert_allclose(x, x1, rtol=1e-10, atol=1e-12)
     assert sum(shards) == len(wt) and min(shards) > 0
@@ -169,3 +169,92 @@ def test_device_ranks_sum_to_the_whole():
             dev.allreduce(np.zeros(1 + rank))
         return True
     assert all(_run_ranks(2, bad))
+
+
+def _compiled_only(syn):
+    """the corpus cut to strings compiled into bubbles (second-order terms
+    exist for those only; see test_gpu_hessian.py)"""
+    import wfsa_amd as W
+    sym, off, wt = syn.corpus()
+    dev = W.Device(0)
+    dev.load_model(W.Fsa.read_text(syn.wfsa_text))
+    dev.load_corpus(sym, off, wt / wt.sum())
+    rec, pc, _ = dev.recognize()
+    keep = np.flatnonzero((dev.string_tiers() == -1) & (rec == 1))
+    strings = [bytes(sym[off[i]:off[i + 1]]) for i in keep]
+    sym2 = np.frombuffer(b"".join(strings), dtype=np.uint8).copy()
+    off2 = np.concatenate([[0], np.cumsum([len(x) for x in strings])]).astype(np.int64)
+    return sym2, off2, wt[keep] / wt[keep].sum()
+
+
+def test_rmin_column_across_ranks():
+    """the rmin info column (QuasiNewtonLearner::GetOptimizationInfo,
+    src/QuasiNewtonLearner.cpp:80-84) across ranks: value and the global
+    index of the string holding the path equal the one-context run, in the
+    host steps and the device-resident loop"""
+    import wfsa_amd as W
+    syn = W.Synthetic(**FAMILIES["ambiguous"])
+    sym, off, wt = _with_unrecognized(*syn.corpus())
+    fsa = W.Fsa.read_text(syn.wfsa_text)
+
+    def learn(nranks, rank, gid):
+        lrn = W.QuasiNewtonLearner(0)
+        if nranks > 1:
+            lrn.SetCommunicator(nranks, rank, gid)
+        lrn.BuildFromPacked(fsa, sym, off, wt)
+        lrn.Finalize()
+        lrn.Init(7)
+        rows = [lrn.OptimizationStep(1.0, -1.0)[0] for _ in range(2)]
+        return rows + lrn.Run(4, 1.0, -1.0)
+
+    rows1 = learn(1, 0, None)
+    assert all(r[6] >= 0 and 0 < r[5] < 1 for r in rows1)   # ambiguous strings exist
+    for rows in _run_ranks(3, learn):
+        for a, q in zip(rows, rows1):
+            for u, v in zip(a[:7], q[:7]):
+                assert _close(u, v, rel=1e-10, atol=1e-13)
+
+
+def test_hessian_across_ranks():
+    """HessianLearner with 2 and 3 ranks: the H_f pattern is the union of the
+    ranks' patterns, the values are all-reduced; device values and every
+    epoch row (KL, residuals, inertia, lambda_min, rmin) equal one context"""
+    import wfsa_amd as W
+    syn = W.Synthetic(seed=3, n_states=20, degree=4, vocab=6, emissions=2, n_strings=300, max_len=12)
+    sym, off, p = _compiled_only(syn)
+    fsa = W.Fsa.read_text(syn.wfsa_text)
+    w = np.random.default_rng(1).normal(-1.0, 0.3, size=len(fsa.param_names()))
+    syn2 = W.Synthetic(seed=3, n_states=16, degree=3, vocab=8, emissions=1, n_strings=2000, max_len=16)
+    sym2, off2, p2 = _compiled_only(syn2)
+    fsa2 = W.Fsa.read_text(syn2.wfsa_text)
+
+    def hf(nranks, rank, gid):
+        dev = W.Device(0)
+        if nranks > 1:
+            dev.comm_init(nranks, rank, gid)
+        b, e = W.shard_range(off, nranks, rank)
+        dev.load_model(fsa)
+        dev.load_corpus(sym[off[b]:off[e]], off[b:e + 1] - off[b], p[b:e])
+        dev.recognize()
+        pairs = dev.hf_setup()
+        return [tuple(x) for x in pairs], dev.hf_eval(w)
+
+    def learn(nranks, rank, gid):
+        lrn = W.HessianLearner(0)
+        if nranks > 1:
+            lrn.SetCommunicator(nranks, rank, gid)
+        lrn.BuildFromPacked(fsa2, sym2, off2, p2)
+        lrn.Finalize()
+        return np.array(lrn.run(flags=31, epochs=6, tol=1e-13)), lrn.x()
+
+    pairs1, vals1 = hf(1, 0, None)
+    rows1, x1 = learn(1, 0, None)
+    for k in (2, 3):
+        for pairs, vals in _run_ranks(k, hf):
+            assert pairs == pairs1
+            np.testing.assert_allclose(vals, vals1, rtol=1e-11, atol=1e-15)
+        for rows, x in _run_ranks(k, learn):
+            assert rows.shape == rows1.shape
+            assert len(rows1) == 6
+            np.testing.assert_allclose(rows, rows1, rtol=1e-8, atol=1e-10)
+            np.testing.assert_allclose(x, x1, rtol=1e-9, atol=1e-11)

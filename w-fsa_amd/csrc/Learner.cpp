@@ -305,7 +305,7 @@ bool Learner::SaveMatrices(const std::string& prefix) const {   // src/Learner.c
 }
 
 bool Learner::RminAvailable() const {
-    if (!info_rmin || unique_paths || nranks > 1 || !dev) return false;
+    if (!info_rmin || unique_paths || !dev) return false;
     wfsa_dev_stats st{};
     if (wfsa_dev_get_stats(dev, &st) != WFSA_OK) return false;
     return !st.dense;

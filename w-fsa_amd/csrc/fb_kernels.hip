@@ -1667,6 +1667,27 @@ __global__ __launch_bounds__(256) void rmin_final_kernel(RminArgs a, int n_part)
     }
 }
 
+// The rmin column across ranks, between two Min all-reduces of key
+// (phase 0: key[0] = this rank's value, +inf without an ambiguous string;
+// 1: key[1] = its global string index if it holds the global minimum, else
+// +inf -- ties to the lower string, as within a rank; 2: res = the result,
+// (0, -1) when no rank has an ambiguous string).
+__global__ void rmin_rank_kernel(double* res, double* key, double base, int phase) {
+    if (threadIdx.x != 0) return;
+    if (phase == 0) key[0] = res[1] >= 0.0 ? res[0] : INFINITY;
+    else if (phase == 1) key[1] = (res[1] >= 0.0 && res[0] == key[0]) ? res[1] + base : INFINITY;
+    else {
+        const bool any = key[1] < INFINITY;
+        res[0] = any ? key[0] : 0.0;
+        res[1] = any ? key[1] : -1.0;
+    }
+}
+
+hipError_t launch_rmin_rank(double* res, double* key, double base, int phase, hipStream_t stream) {
+    hipLaunchKernelGGL(rmin_rank_kernel, dim3(1), dim3(64), 0, stream, res, key, base, phase);
+    return hipGetLastError();
+}
+
 hipError_t launch_rmin(const RminArgs& a, hipStream_t stream, bool final) {
     if (a.n_bub > 0 && a.vb)
         hipLaunchKernelGGL(rmin_bubble_kernel, dim3(unsigned((a.n_bub + 63) / 64)), dim3(64),

@@ -220,6 +220,8 @@ constexpr int kRminBlock = 256;
 // final = false: leave the block minima in part[] (log values, string index)
 // for the QN finish to reduce (QnArgs::rmin_part)
 hipError_t launch_rmin(const RminArgs& a, hipStream_t stream, bool final = true);
+// rmin across ranks: the phases around the two Min all-reduces (fb_kernels.hip)
+hipError_t launch_rmin_rank(double* res, double* key, double base, int phase, hipStream_t stream);
 inline int rmin_blocks(int64_t n_amb) { return int(n_amb > 0 ? (n_amb + kRminBlock - 1) / kRminBlock : 1); }
 
 // Second-order term of the Hessian (HessianLearner::ComputeHf,

@@ -220,7 +220,8 @@ struct wfsa_dev {
 
     // rmin info column: per-bubble / per-string logs, block partials, results
     // (two halves: a QN step's finish reads its own while the next step writes)
-    DevBuf<double> rm_rs, rm_vb, rm_part, rm_res;
+    DevBuf<double> rm_rs, rm_vb, rm_part, rm_res, rm_key;
+    double rm_base = 0.0;        // across ranks: global index of this rank's first loaded string
     DevBuf<int4> rm_amb;         // the ambiguous strings (path count > 1) with their bubble runs
     std::vector<int32_t> h_bfirst, h_nbub;   // per string: first bubble ordinal, bubbles (compiled strings)
     int max_bub_nodes = 1;                   // largest compiled bubble (nodes)
@@ -1321,6 +1322,19 @@ int rmin_prepare(wfsa_dev* ctx) {
         HIP_TRY(ctx->rm_rs.alloc(S));
         HIP_TRY(hipMemsetAsync(ctx->rm_rs.ptr, 0, S * sizeof(double), s));   // fused accumulation starts at 0
         HIP_TRY(ctx->rm_vb.alloc(size_t(std::max(ctx->n_bubbles, 1))));
+        HIP_TRY(ctx->rm_key.alloc(2));
+        if (ctx->comm) {   // every rank's string count -> this rank's first global index
+            const int nr = ctx->comm->nranks();
+            std::vector<double> cnt(size_t(nr), 0.0);
+            cnt[size_t(ctx->comm->rank())] = double(ctx->n_strings);
+            DevBuf<double> t;
+            HIP_TRY(t.upload(cnt.data(), cnt.size(), s));
+            COMM_TRY(ctx, t.ptr, cnt.size(), wfsa::RedOp::SumF64, s);
+            HIP_TRY(t.download(cnt.data(), cnt.size(), s));
+            HIP_TRY(hipStreamSynchronize(s));
+            ctx->rm_base = 0.0;
+            for (int r = 0; r < ctx->comm->rank(); ++r) ctx->rm_base += cnt[size_t(r)];
+        }
         HIP_TRY(hipStreamSynchronize(s));   // amb is freed on return
         ctx->rm_gen = ctx->prep_gen;
     }
@@ -1330,6 +1344,18 @@ int rmin_prepare(wfsa_dev* ctx) {
 // trav_done: the evaluation just enqueued already produced every string's
 // value (ctx->rm_eval: its weighted traversal passes ran the min forward and
 // its bubble passes accumulated log(min path / Z) per string)
+// across ranks: res -> the global (rmin, string index); every rank calls it
+int combine_rmin(wfsa_dev* ctx, double* res, hipStream_t s) {
+    if (!ctx->comm) return WFSA_OK;
+    double* key = ctx->rm_key.ptr;
+    HIP_TRY(wfsa::launch_rmin_rank(res, key, ctx->rm_base, 0, s));
+    COMM_TRY(ctx, key, 1, wfsa::RedOp::MinF64, s);
+    HIP_TRY(wfsa::launch_rmin_rank(res, key, ctx->rm_base, 1, s));
+    COMM_TRY(ctx, key + 1, 1, wfsa::RedOp::MinF64, s);
+    HIP_TRY(wfsa::launch_rmin_rank(res, key, ctx->rm_base, 2, s));
+    return WFSA_OK;
+}
+
 int enqueue_rmin(wfsa_dev* ctx, const unsigned* halted, double* res, int par = 0, wfsa::QnFinish* q = nullptr,
                  bool trav_done = false) {
     hipStream_t s = ctx->stream;
@@ -1474,6 +1500,10 @@ int enqueue_qn_step(wfsa_dev* ctx, double eta, double tol, int64_t e, bool timed
         double* res = ctx->rm_res.ptr + 2 * par;
         if (ctx->mpath) {
             if (int rc = enqueue_rmin(ctx, ctx->qn_halted.ptr, res)) return rc;
+            f.rmin = res;
+        } else if (ctx->comm) {   // the rank's minimum, then the global one
+            if (int rc = enqueue_rmin(ctx, ctx->qn_halted.ptr, res, par, nullptr, true)) return rc;
+            if (int rc = combine_rmin(ctx, res, s)) return rc;
             f.rmin = res;
         } else if (int rc = enqueue_rmin(ctx, ctx->qn_halted.ptr, res, par, &f, true)) {
             return rc;
@@ -1892,6 +1922,7 @@ int wfsa_dev_rmin(wfsa_dev* ctx, double* rmin, int64_t* string_index) {
     if (ctx->prep_level < 2) return fail(WFSA_ERR_ARG, "rmin: evaluate the objective first");
     if (ctx->rm_res.n < 4) HIP_TRY(ctx->rm_res.alloc(4));
     if (int rc = enqueue_rmin(ctx, nullptr, ctx->rm_res.ptr)) return rc;
+    if (int rc = combine_rmin(ctx, ctx->rm_res.ptr, ctx->stream)) return rc;
     double h[2];
     HIP_TRY(ctx->rm_res.download(h, 2, ctx->stream));
     HIP_TRY(hipStreamSynchronize(ctx->stream));
@@ -2041,8 +2072,7 @@ int wfsa_dev_qn_setup(wfsa_dev* ctx, const wfsa_qn_desc* d) {
     ctx->qn_k = k;
     ctx->qn_plogp = d->plogp;
     ctx->qn_exp_lambda = d->exponential_lambda ? 1 : 0;
-    if (d->info_rmin && (ctx->dense || ctx->comm))
-        return fail(WFSA_ERR_CAPACITY, "the rmin column is not available on the dense path or with a communicator");
+    if (d->info_rmin && ctx->dense) return fail(WFSA_ERR_CAPACITY, "the rmin column is not available on the dense path");
     ctx->qn_rmin = d->info_rmin != 0;
     if (ctx->qn_rmin) HIP_TRY(ctx->rm_res.alloc(4));
     // the contribution slots in trimmed order (kept parameters first, the
@@ -2183,14 +2213,24 @@ int wfsa_dev_hf_setup(wfsa_dev* ctx, int64_t* n_pairs) {
         if (n_pairs) *n_pairs = int64_t(ctx->hf_pairs.size() / 2);
         return WFSA_OK;
     }
-    if (ctx->comm) return fail(WFSA_ERR_ARG, "second-order terms: not available with a communicator");
     if (ctx->prep_level < 2)
         if (int rc = prepare(ctx, 2)) return rc;
+    hipStream_t s = ctx->stream;
     const int64_t nfall = int64_t(ctx->n_fall[0]) + ctx->n_fall[1] + ctx->n_fall[2];
+    if (ctx->comm) {   // every rank learns whether any cannot build its part (no rank is left in a collective)
+        DevBuf<double> t;
+        double bad = nfall > 0 ? 1.0 : 0.0;
+        HIP_TRY(t.upload(&bad, 1, s));
+        COMM_TRY(ctx, t.ptr, 1, wfsa::RedOp::SumF64, s);
+        HIP_TRY(t.download(&bad, 1, s));
+        HIP_TRY(hipStreamSynchronize(s));
+        if (bad > 0 && nfall == 0)
+            return fail(WFSA_ERR_CAPACITY, "second-order terms need every string compiled into bubbles; "
+                        "another rank has strings on the traversal tiers");
+    }
     if (nfall > 0)
         return fail(WFSA_ERR_CAPACITY, "second-order terms need every string compiled into bubbles; %lld strings "
                     "are on the traversal tiers", (long long)nfall);
-    hipStream_t s = ctx->stream;
     const int32_t np = ctx->n_params, nb = ctx->n_bubbles;
     std::vector<int32_t> off(size_t(std::max(nb, 1)));
     std::vector<int32_t> buf(ctx->bub.n);
@@ -2246,6 +2286,53 @@ int wfsa_dev_hf_setup(wfsa_dev* ctx, int64_t* n_pairs) {
     }
     tptr.push_back(ns);
     if (ns == 0) tptr.assign(1, 0);
+    if (ctx->comm) {
+        // the pattern is the union over the ranks: every rank's pairs (keys
+        // j*np+k, exact in a double) gathered by a sum into per-rank segments;
+        // a global pair this rank never sees gets an empty slot run
+        const int nr = ctx->comm->nranks(), me = ctx->comm->rank();
+        const size_t nloc = ctx->hf_pairs.size() / 2;
+        std::vector<double> cnt(size_t(nr), 0.0);
+        cnt[size_t(me)] = double(nloc);
+        DevBuf<double> t;
+        HIP_TRY(t.upload(cnt.data(), cnt.size(), s));
+        COMM_TRY(ctx, t.ptr, cnt.size(), wfsa::RedOp::SumF64, s);
+        HIP_TRY(t.download(cnt.data(), cnt.size(), s));
+        HIP_TRY(hipStreamSynchronize(s));
+        size_t total = 0, mine = 0;
+        for (int r = 0; r < nr; ++r) {
+            if (r == me) mine = total;
+            total += size_t(cnt[size_t(r)]);
+        }
+        std::vector<double> all(std::max<size_t>(total, 1), 0.0);
+        for (size_t i = 0; i < nloc; ++i)
+            all[mine + i] = double(int64_t(ctx->hf_pairs[2 * i]) * np + ctx->hf_pairs[2 * i + 1]);
+        HIP_TRY(t.upload(all.data(), all.size(), s));
+        COMM_TRY(ctx, t.ptr, all.size(), wfsa::RedOp::SumF64, s);
+        HIP_TRY(t.download(all.data(), all.size(), s));
+        HIP_TRY(hipStreamSynchronize(s));
+        std::vector<int64_t> gk(total);
+        for (size_t i = 0; i < total; ++i) gk[i] = int64_t(all[i]);
+        std::sort(gk.begin(), gk.end());
+        gk.erase(std::unique(gk.begin(), gk.end()), gk.end());
+        std::vector<int64_t> gptr(gk.size() + 1, 0);
+        size_t li = 0;
+        int64_t pos = 0;
+        for (size_t g = 0; g < gk.size(); ++g) {
+            gptr[g] = pos;
+            if (li < nloc && int64_t(ctx->hf_pairs[2 * li]) * np + ctx->hf_pairs[2 * li + 1] == gk[g]) {
+                pos = tptr[li + 1];
+                ++li;
+            }
+        }
+        gptr[gk.size()] = pos;
+        tptr = gptr;
+        ctx->hf_pairs.clear();
+        for (int64_t key : gk) {
+            ctx->hf_pairs.push_back(int32_t(key / np));
+            ctx->hf_pairs.push_back(int32_t(key % np));
+        }
+    }
     HIP_TRY(ctx->hf_slot_base.upload(base.data(), base.size(), s));
     HIP_TRY(ctx->hf_t_ptr.upload(tptr.data(), tptr.size(), s));
     HIP_TRY(ctx->hf_t_slot.upload(order.empty() ? base.data() : order.data(), std::max<size_t>(order.size(), 1), s));
@@ -2296,6 +2383,7 @@ int wfsa_dev_hf_eval(wfsa_dev* ctx, const double* w_full, double* values) {
     a.n_pattern = int64_t(ctx->hf_pairs.size() / 2);
     a.out = ctx->hf_out.ptr;
     HIP_TRY(wfsa::launch_hf(a, s));
+    if (ctx->comm && a.n_pattern > 0) COMM_TRY(ctx, ctx->hf_out.ptr, size_t(a.n_pattern), wfsa::RedOp::SumF64, s);
     if (values && a.n_pattern > 0) HIP_TRY(ctx->hf_out.download(values, size_t(a.n_pattern), s));
     HIP_TRY(hipStreamSynchronize(s));
     return WFSA_OK;
