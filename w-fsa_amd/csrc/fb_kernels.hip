@@ -725,6 +725,226 @@ __global__ __launch_bounds__(kWideBlock) void wide_kernel(WideArgs a) {
     }
 }
 
+// Tier 2, weighted, one wavefront per string, over the byte-pair tables
+// (fb_kernels.hpp PairTables).  The trellis sums of wide_kernel<false>, laid
+// out for the gather rate that bounds this pass: a block's waves each take a
+// string from a work counter (16 strings per CU at once instead of one per
+// 256-thread block); a step (a, b) walks the pair's edge list one edge per
+// lane -- contiguous loads, no per-destination padding, only the edges whose
+// source is live -- and sums into the wave's LDS rows (LDS atomics, issued in
+// lane order within the wave: run-to-run stable); the forward keeps the
+// current row in LDS and writes each row once to HBM (compact, coalesced) for
+// the backward, which gathers alpha from that row and sums beta in LDS; no
+// block barriers; the gradient in one LDS table per block when it fits,
+// flushed once per launch.
+__device__ __forceinline__ void wave_fence() { __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup"); }
+
+template <bool TRACK>
+__global__ __launch_bounds__(kWide2Block) void wide2_kernel(WideArgs a) {
+    if (a.halted && *a.halted) return;
+    extern __shared__ __attribute__((aligned(16))) double lds2[];
+    __shared__ double llw[kWide2Block / kWave];
+    const int lane = lane_id(), wv = int(threadIdx.x) >> 6, nwv = int(blockDim.x) >> 6;
+    const ModelView& m = a.m;
+    const PairTables& P = a.pt;
+    const int K = P.K, MN = P.max_n;
+    const bool lgrad = a.grad_lds != 0;
+    double* gl = lds2;
+    double* rows = lds2 + (lgrad ? ((m.n_params + 1) & ~1) : 0) + int64_t(wv) * 2 * MN;
+    double* R0 = rows;              // the two rows (alternating)
+    double* R1 = rows + MN;
+    if (lgrad)
+        for (int j = int(threadIdx.x); j < m.n_params; j += int(blockDim.x)) gl[j] = 0.0;
+    __syncthreads();
+    double* H = a.scratch2 + (int64_t(blockIdx.x) * nwv + wv) * a.stride2;
+    double* Mg = H + 1 + int64_t(a.max_len) * MN;   // [2][max_n] min-forward rows (rmin column)
+    int* ex = reinterpret_cast<int*>(Mg + 2 * int64_t(MN));   // [max_len + 2]
+    double ll = 0.0;
+    auto credit = [&](int p0, int p1, int g, double v) {
+        if (p0 >= 0) {
+            if (lgrad) block_add(&gl[p0], v); else global_add(&a.grad[p0], v);
+            if (p1 >= 0) { if (lgrad) block_add(&gl[p1], v); else global_add(&a.grad[p1], v); }
+        } else if (p0 == -2) {
+            for (int q = m.pptr[g]; q < m.pptr[g + 1]; ++q) {
+                if (lgrad) block_add(&gl[m.pidx[q]], v); else global_add(&a.grad[m.pidx[q]], v);
+            }
+        }
+    };
+    for (;;) {
+        int li = 0;
+        if (lane == 0) li = int(__hip_atomic_fetch_add(a.ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+        li = __builtin_amdgcn_readfirstlane(__shfl(li, 0, kWave));
+        if (li >= a.n_list) break;
+        const int sidx = a.list[li];
+        const int64_t o0 = a.off[sidx];
+        const int L = int(a.off[sidx + 1] - o0);
+        const uint8_t* str = a.sym + o0;
+        auto byte_at = [&](int j) { return j == 0 ? K : P.bidx[str[j - 1]]; };   // D() of position j
+        // forward: the current row in A (LDS), every row also to H + roff (HBM)
+        double* A = R0;
+        double* Nx = R1;
+        if (lane == 0) {
+            A[0] = 1.0;
+            H[0] = 1.0;
+            ex[0] = 0;
+            if (TRACK) Mg[0] = 0.0;
+        }
+        wave_sync();
+        int exi = 0, esum = 0, ap = K;
+        int64_t roff = 0;
+        bool alive = true;
+        for (int i = 0; i < L; ++i) {
+            const int b = P.bidx[str[i]];
+            if (b < 0) {   // no edge consumes the byte
+                alive = false;
+                break;
+            }
+            const double sc = ldexp(1.0, -exi);
+            const int nb = P.n[b];
+            const int64_t rn = roff + P.n[ap];
+            for (int d = lane; d < nb; d += kWave) Nx[d] = 0.0;
+            wave_sync();
+            const int pair = ap * K + b;
+            const int eb = P.e_ptr[pair], ee = P.e_ptr[pair + 1];
+            for (int e = eb + lane; e < ee; e += kWave) {
+                const int4 en = P.ent[e];
+                const int src = en.x & 0xffff, dst = int(unsigned(en.x) >> 16);
+                lds_add(&Nx[dst], A[src] * P.w2[e].x);
+            }
+            wave_sync();
+            double mx = 0.0;
+            for (int d = lane; d < nb; d += kWave) {
+                const double v = Nx[d] * sc;
+                Nx[d] = v;
+                H[rn + d] = v;
+                mx = fmax(mx, v);
+            }
+            mx = wave_max(mx);
+            wave_sync();
+            double* t = A; A = Nx; Nx = t;
+            if (TRACK) {   // (min, x) forward: keys summed in the free row, sources' liveness from H
+                unsigned long long* KN = reinterpret_cast<unsigned long long*>(Nx);
+                const double* Mi = Mg + int64_t(i & 1) * MN;
+                double* Mn = Mg + int64_t((i + 1) & 1) * MN;
+                for (int d = lane; d < nb; d += kWave) KN[d] = ~0ull;
+                wave_sync();
+                for (int e = eb + lane; e < ee; e += kWave) {
+                    const int4 en = P.ent[e];
+                    const int src = en.x & 0xffff, dst = int(unsigned(en.x) >> 16);
+                    const double lwe = P.w2[e].y;
+                    if (H[roff + src] > 0.0 && lwe > -INFINITY) atomicMin(&KN[dst], okey(Mi[src] + lwe));
+                }
+                wave_sync();
+                for (int d = lane; d < nb; d += kWave) Mn[d] = odec(KN[d]);
+            }
+            roff = rn;
+            ap = b;
+            wave_fence();   // this row in H (and Mg) for every lane
+            if (!(mx > 0.0)) {
+                alive = false;
+                break;
+            }
+            exi = __builtin_amdgcn_frexp_exp(mx);
+            esum += exi;
+            if (lane == 0) ex[i + 1] = exi;
+        }
+        double qh = 0.0;
+        const double scL = ldexp(1.0, -exi);
+        const int nL = alive ? P.n[ap] : 0;
+        const int32_t* dL = P.dl_node + P.dl_ptr[ap];
+        for (int d = lane; d < nL; d += kWave) qh += A[d] * scL * end_weight(m, dL[d]);
+        qh = wave_sum(qh);
+        const double lq = qh > 0.0 ? log(qh) + kLn2 * double(esum) : -INFINITY;
+        const double ps = a.p[sidx];
+        if (TRACK) {
+            double mn = INFINITY;
+            for (int d = lane; d < nL; d += kWave) {
+                const double we = end_weight(m, dL[d]);
+                if (A[d] > 0.0 && we > 0.0) mn = fmin(mn, Mg[int64_t(L & 1) * MN + d] + log(we));
+            }
+            mn = -wave_max(-mn);
+            if (lane == 0) a.rmin_log[sidx] = qh > 0.0 ? mn - lq : INFINITY;
+        }
+        if (lane == 0) {
+            if (a.logq) a.logq[sidx] = lq;
+            ll += ps * lq;
+        }
+        if (!(qh > 0.0)) continue;
+        wave_fence();   // the rows in H are visible to every lane
+        // backward (beta scaled so that alpha_i beta_i is the node posterior):
+        // beta_{i+1} in Bn (LDS), beta_i summed into Bi (LDS)
+        const double inv_q = 1.0 / qh;
+        double* Bn = R1;
+        double* Bi = R0;
+        for (int d = lane; d < nL; d += kWave) {
+            const int S = dL[d];
+            const double af = A[d] * scL;
+            Bn[d] = end_weight(m, S) * inv_q;
+            if (!(af > 0.0)) continue;
+            for (int x = m.x_ptr[S]; x < m.x_ptr[S + 1]; ++x) {
+                const int gx = m.n_edges + x;
+                const double xi = af * m.ew[gx] * inv_q;
+                if (xi > 0.0) credit(-2, -1, gx, -ps * xi);
+            }
+        }
+        wave_sync();
+        int ex_next = exi, b = ap;
+        for (int i = L - 1; i >= 0; --i) {
+            const int ai = byte_at(i);
+            const int na = P.n[ai];
+            roff -= na;
+            const int ex_i = i == 0 ? 0 : ex[i];
+            const double sc = ldexp(1.0, -ex_next), sci = ldexp(1.0, -ex_i);
+            for (int d = lane; d < na; d += kWave) Bi[d] = 0.0;
+            wave_sync();
+            const int pair = ai * K + b;
+            const int eb = P.e_ptr[pair], ee = P.e_ptr[pair + 1];
+            for (int e = eb + lane; e < ee; e += kWave) {
+                const int4 en = P.ent[e];
+                const int src = en.x & 0xffff, dst = int(unsigned(en.x) >> 16);
+                const double af = H[roff + src] * sci;
+                if (!(af > 0.0)) continue;
+                const double bv = P.w2[e].x * Bn[dst] * sc;
+                lds_add(&Bi[src], bv);
+                const double xi = af * bv;
+                if (xi > 0.0) credit(en.z, en.w, en.y, -ps * xi);
+            }
+            wave_sync();
+            double* t = Bn; Bn = Bi; Bi = t;
+            ex_next = ex_i;
+            b = ai;
+        }
+        wave_sync();
+    }
+    if (lane == 0) {
+        llw[wv] = ll;
+        // the last wave out resets the counters for the next launch
+        const unsigned d = __hip_atomic_fetch_add(a.ctr + 1, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+        if (d + 1 == gridDim.x * unsigned(nwv)) {
+            __hip_atomic_store(a.ctr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(a.ctr + 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        double t = 0.0;
+        for (int w = 0; w < nwv; ++w) t += llw[w];
+        a.ll_part[blockIdx.x] = t;
+    }
+    if (lgrad)
+        for (int j = int(threadIdx.x); j < m.n_params; j += int(blockDim.x))
+            if (gl[j] != 0.0) global_add(&a.grad[j], gl[j]);
+}
+
+__global__ __launch_bounds__(256) void pair_weights_kernel(const int4* ent, int64_t n, const double* ew,
+                                                           const double* lw, double2* w2) {
+    const int64_t stride = int64_t(gridDim.x) * blockDim.x;
+    for (int64_t e = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; e < n; e += stride) {
+        const int g = ent[e].y;
+        w2[e] = make_double2(ew[g], lw[g]);
+    }
+}
+
 // Hessian second-order term per bubble (fb_kernels.hpp HfArgs).  The
 // bubble's local node ids are in position order, so its edges (listed by
 // source position) are already topologically sorted.
@@ -1715,6 +1935,22 @@ hipError_t launch_wide(bool counting, const WideArgs& a, int grid, hipStream_t s
         hipLaunchKernelGGL(wide_kernel<true>, dim3(unsigned(grid)), dim3(kWideBlock), 0, stream, a);
     else
         hipLaunchKernelGGL(wide_kernel<false>, dim3(unsigned(grid)), dim3(kWideBlock), lds, stream, a);
+    return hipGetLastError();
+}
+
+hipError_t launch_wide2(const WideArgs& a, int grid, int waves, size_t lds, hipStream_t stream) {
+    if (a.rmin_log)
+        hipLaunchKernelGGL(wide2_kernel<true>, dim3(unsigned(grid)), dim3(unsigned(waves * kWave)), lds, stream, a);
+    else
+        hipLaunchKernelGGL(wide2_kernel<false>, dim3(unsigned(grid)), dim3(unsigned(waves * kWave)), lds, stream, a);
+    return hipGetLastError();
+}
+
+hipError_t launch_pair_weights(const int4* ent, int64_t n, const double* ew, const double* lw, double2* w2,
+                               hipStream_t stream) {
+    if (n == 0) return hipSuccess;
+    const unsigned g = unsigned(std::min<int64_t>((n + 255) / 256, 4096));
+    hipLaunchKernelGGL(pair_weights_kernel, dim3(g), dim3(256), 0, stream, ent, n, ew, lw, w2);
     return hipGetLastError();
 }
 

@@ -153,6 +153,28 @@ struct TravArgs {
 // (each destination node summed by one thread: no atomics); beta rolls over
 // two vectors, gathered through the out-edges; the gradient accumulates in
 // LDS when n_params fits (else global atomics).
+// Byte-pair tables of the tier-2 wave kernel.  The nodes live at position i
+// are D(c_{i-1}) (the nodes a byte-c_{i-1} edge enters; at 0 the start node,
+// pseudo-byte K), so a trellis step (a = c_{i-1}, b = c_i) only ever joins
+// D(a) to D(b).  Rows are indexed by position in D (compact), and every pair
+// (a, b), a in [0, K], b in [0, K), owns the list of its edges -- the edges
+// consuming b whose source is in D(a) -- as
+//   ent = (src index | dst index << 16, edge id, param0, param1)
+// (param -1: none; param0 = -2: more than two, read pptr/pidx) and, rewritten
+// each evaluation, w2 = (ew, lw).  A wave walks a pair's list with one edge
+// per lane (contiguous loads, no padding) and sums into its LDS rows.
+struct PairTables {
+    int32_t K;               // compact alphabet (bytes some edge consumes)
+    const int32_t* bidx;     // [256] byte -> compact index, -1
+    const int32_t* n;        // [K + 1] |D(b)| (< 65536); n[K] = 1 (start)
+    const int32_t* dl_ptr;   // [K + 2] D(b) node list offsets into dl_node
+    const int32_t* dl_node;  // node ids
+    const int32_t* e_ptr;    // [(K + 1) K + 1] edge range of pair a K + b
+    const int4* ent;
+    const double2* w2;       // this evaluation's (ew, lw) per entry
+    int32_t max_n;
+};
+
 struct WideModel {
     const int32_t* c_ptr;    // [257] destination entries of byte c: [c_ptr[c], c_ptr[c+1])
     const int32_t* dst;      // [n_dst] the node (every destination of a byte-c edge, once)
@@ -182,12 +204,35 @@ struct WideArgs {
     const unsigned* halted;
     unsigned long long* live_edges;   // counting: += the edges the forward gathers over (or null)
     double* rmin_log;        // min mode: [S] log(min path weight / q)
+    // weighted mode, wave per string (wide2_kernel over the byte-pair tables)
+    PairTables pt;
+    double* scratch2;        // per wave: alpha rows (compact, 1 + max_len * max_n), min-forward rows
+                             // [2 max_n], exponents [max_len + 2]
+    int64_t stride2;         // doubles per wave
+    unsigned* ctr;           // [2] work and exit counters (zero between launches)
 };
 // doubles of scratch per block
 inline int64_t wide_scratch_stride(int32_t max_len, int32_t n_nodes) {
     return (int64_t(max_len) + 3) * int64_t(n_nodes) + (int64_t(max_len) + 3) / 2 + 2;
 }
 hipError_t launch_wide(bool counting, const WideArgs& a, int grid, hipStream_t stream, bool min_mode = false);
+// Tier 2 weighted pass, one wavefront per string (kWide2Block threads per
+// block, the blocks' waves take strings from a work counter): alpha rows in
+// HBM (zeroed behind the backward), gradient in one LDS table per block
+// when n_params fits.  grid: blocks.
+constexpr int kWide2Block = 1024;
+inline int64_t wide2_stride(int32_t max_len, int32_t max_n) {
+    return 1 + int64_t(max_len) * max_n + 2 * int64_t(max_n) + (int64_t(max_len) + 3) / 2 + 2;
+}
+// LDS of a block: the gradient table (grad_lds) + per wave 2 rows of max_n doubles
+inline size_t wide2_lds(int32_t n_params, bool grad_lds, int waves, int32_t max_n) {
+    return (grad_lds ? size_t((n_params + 1) & ~1) * 8 : 0) + size_t(waves) * 2 * size_t(max_n) * 8;
+}
+// waves: per block (blockDim = 64 waves); lds from wide2_lds
+hipError_t launch_wide2(const WideArgs& a, int grid, int waves, size_t lds, hipStream_t stream);
+// the pair tables' per-evaluation weights w2 from ew / lw
+hipError_t launch_pair_weights(const int4* ent, int64_t n, const double* ew, const double* lw, double2* w2,
+                               hipStream_t stream);
 
 // The rmin info column (QuasiNewtonLearner::GetOptimizationInfo,
 // src/QuasiNewtonLearner.cpp:80-84; HessianLearner :313-317): the smallest

@@ -198,6 +198,25 @@ struct wfsa_dev {
     int64_t w_stride = 0;
     int32_t tier2_strings = 0;
     bool force_tier2 = false;   // WFSA_TIER2=1: every string on tier 2 (tests)
+    // tier 2 weighted pass, wave per string (wide2_kernel; WFSA_WIDE2=0: the
+    // block-per-string wide_kernel): (node, byte) out-edge table, per-wave
+    // scratch (alpha rows zero between strings), work counters
+    bool use_wide2 = true;
+    bool has_pairs = false;   // the byte-pair tables were built (size cap)
+    int32_t pt_K = 0, pt_max_n = 0;
+    int64_t pt_ne = 0;
+    DevBuf<int32_t> pt_bidx, pt_n, pt_dlptr, pt_dlnode, pt_eptr;
+    DevBuf<int4> pt_ent;
+    DevBuf<double2> pt_w2;
+    int w2_waves = 16;           // waves per block
+    bool w2_lgrad = false;       // the gradient in LDS
+    DevBuf<double> w2_scratch;
+    int64_t w2_stride = 0;
+    int w2_grid = 0;
+    DevBuf<unsigned> w2_ctr;
+    bool w2_all = true;          // every traversal string on the wave kernel (WFSA_WIDE2_TIERS=2: tier 2 only)
+    DevBuf<int32_t> w2_list;     // its strings, longest first
+    int32_t w2_n = 0;
 
     // work buffers
     DevBuf<double> w_full, ewp, out, ll_part, logq;
@@ -381,7 +400,127 @@ wfsa::WideArgs wide_args(wfsa_dev* ctx) {
     a.scratch = ctx->w_scratch.ptr;
     a.scratch_stride = ctx->w_stride;
     a.grad_lds = size_t(ctx->n_params) * sizeof(double) <= size_t(96 * 1024) ? 1 : 0;
+    a.pt.K = ctx->pt_K;
+    a.pt.bidx = ctx->pt_bidx.ptr;
+    a.pt.n = ctx->pt_n.ptr;
+    a.pt.dl_ptr = ctx->pt_dlptr.ptr;
+    a.pt.dl_node = ctx->pt_dlnode.ptr;
+    a.pt.e_ptr = ctx->pt_eptr.ptr;
+    a.pt.ent = ctx->pt_ent.ptr;
+    a.pt.w2 = ctx->pt_w2.ptr;
+    a.pt.max_n = ctx->pt_max_n;
+    a.scratch2 = ctx->w2_scratch.ptr;
+    a.stride2 = ctx->w2_stride;
+    a.ctr = ctx->w2_ctr.ptr;
     return a;
+}
+
+// Waves per block and the gradient table of the tier-2 wave kernel: the
+// gradient table in LDS when at least 4 waves fit beside it (global fp64
+// atomics cost ~7x at family B), else the most waves with global atomics.
+bool wide2_config(wfsa_dev* ctx) {
+    const size_t cap = size_t(kLdsPerCu) - 1024;
+    int best = 0;
+    bool lg = false;
+    for (int w : {16, 12, 8, 4})
+        if (!best && wfsa::wide2_lds(ctx->n_params, true, w, ctx->pt_max_n) <= cap) {
+            best = w;
+            lg = true;
+        }
+    for (int w : {16, 12, 8, 4})
+        if (!best && wfsa::wide2_lds(ctx->n_params, false, w, ctx->pt_max_n) <= cap) best = w;
+    if (!best) return false;
+    ctx->w2_waves = best;
+    ctx->w2_lgrad = lg;
+    return true;
+}
+
+// The byte-pair tables of the tier-2 wave kernel (fb_kernels.hpp
+// PairTables), from the byte-indexed in-edge lists (cptr/dst/eptr/esrc/eg).
+// Skipped (has_pairs = false: tier 2 keeps the block-per-string kernel) when
+// the entries would exceed 2^27.
+int build_pair_tables(wfsa_dev* ctx, const wfsa::TrellisModel& tm, const std::vector<int32_t>& cptr,
+                      const std::vector<int32_t>& dst, const std::vector<int32_t>& eptr,
+                      const std::vector<int32_t>& esrc, const std::vector<int32_t>& eg,
+                      const std::vector<int32_t>& pptr, const std::vector<int32_t>& pidx) {
+    ctx->has_pairs = false;
+    hipStream_t s = ctx->stream;
+    std::vector<int32_t> bidx(256, -1), bytes;
+    for (int c = 0; c < 256; ++c)
+        if (cptr[size_t(c) + 1] > cptr[size_t(c)]) {
+            bidx[size_t(c)] = int32_t(bytes.size());
+            bytes.push_back(c);
+        }
+    const int K = int(bytes.size());
+    if (K == 0) return WFSA_OK;
+    // D(b) for b < K, then {start}
+    std::vector<int32_t> n(size_t(K) + 1), dl_ptr(size_t(K) + 2, 0), dl_node;
+    for (int b = 0; b < K; ++b) {
+        const int c = bytes[size_t(b)];
+        n[size_t(b)] = cptr[size_t(c) + 1] - cptr[size_t(c)];
+        for (int k = cptr[size_t(c)]; k < cptr[size_t(c) + 1]; ++k) dl_node.push_back(dst[size_t(k)]);
+        dl_ptr[size_t(b) + 1] = int32_t(dl_node.size());
+    }
+    n[size_t(K)] = 1;
+    dl_node.push_back(tm.start);
+    dl_ptr[size_t(K) + 1] = int32_t(dl_node.size());
+    int32_t max_n = 1;
+    for (int32_t v : n) max_n = std::max(max_n, v);
+    {   // build cost (and table index size) bounded: pairs x groups, pairs' in-edge scans
+        int64_t groups = 0;
+        for (int b = 0; b <= K; ++b) groups += (int64_t(n[size_t(b)]) + kWave - 1) / kWave;
+        if (int64_t(K + 1) * groups > (int64_t(1) << 22) || int64_t(K + 1) * int64_t(esrc.size()) > (int64_t(1) << 28))
+            return WFSA_OK;
+    }
+    // node -> index in D(a), one a at a time
+    if (max_n >= 65536) return WFSA_OK;   // indices are packed in 16 bits
+    const int32_t N = tm.n_nodes;
+    std::vector<int32_t> idx_a(size_t(N), -1), idx_b(size_t(N), -1);
+    auto fill = [&](std::vector<int32_t>& idx, int a, bool on) {
+        for (int32_t q = dl_ptr[size_t(a)]; q < dl_ptr[size_t(a) + 1]; ++q) idx[size_t(dl_node[size_t(q)])] = on ? q - dl_ptr[size_t(a)] : -1;
+    };
+    const int64_t n_pairs = int64_t(K + 1) * K;
+    std::vector<int32_t> e_ptr(size_t(n_pairs) + 1, 0);
+    std::vector<int4> ent;
+    constexpr int64_t kCap = int64_t(1) << 27;
+    for (int a = 0; a <= K; ++a) {
+        fill(idx_a, a, true);
+        for (int b = 0; b < K; ++b) {
+            const int c = bytes[size_t(b)];
+            fill(idx_b, b, true);
+            // the pair's edges, by destination (the in-edge lists of D(b)) with a source in D(a)
+            for (int32_t k = cptr[size_t(c)]; k < cptr[size_t(c) + 1]; ++k) {
+                const int32_t di = k - cptr[size_t(c)];
+                for (int32_t e = eptr[size_t(k)]; e < eptr[size_t(k) + 1]; ++e) {
+                    const int32_t si = idx_a[size_t(esrc[size_t(e)])];
+                    if (si < 0) continue;
+                    const int32_t g = eg[size_t(e)];
+                    const int32_t pc = pptr[size_t(g) + 1] - pptr[size_t(g)];
+                    const int32_t p0 = pc > 2 ? -2 : (pc >= 1 ? pidx[size_t(pptr[size_t(g)])] : -1);
+                    const int32_t p1 = pc == 2 ? pidx[size_t(pptr[size_t(g)]) + 1] : -1;
+                    ent.push_back(make_int4(int32_t(uint32_t(si) | (uint32_t(di) << 16)), g, p0, p1));
+                }
+            }
+            if (int64_t(ent.size()) > kCap) return WFSA_OK;
+            e_ptr[size_t(int64_t(a) * K + b) + 1] = int32_t(ent.size());
+            fill(idx_b, b, false);
+        }
+        fill(idx_a, a, false);
+    }
+    if (ent.empty()) ent.push_back(make_int4(0, 0, -1, -1));
+    HIP_TRY(ctx->pt_bidx.upload(bidx.data(), bidx.size(), s));
+    HIP_TRY(ctx->pt_n.upload(n.data(), n.size(), s));
+    HIP_TRY(ctx->pt_dlptr.upload(dl_ptr.data(), dl_ptr.size(), s));
+    HIP_TRY(ctx->pt_dlnode.upload(dl_node.data(), dl_node.size(), s));
+    HIP_TRY(ctx->pt_eptr.upload(e_ptr.data(), e_ptr.size(), s));
+    HIP_TRY(ctx->pt_ent.upload(ent.data(), ent.size(), s));
+    HIP_TRY(ctx->pt_w2.alloc(ent.size()));
+    HIP_TRY(hipStreamSynchronize(s));
+    ctx->pt_K = K;
+    ctx->pt_max_n = max_n;
+    ctx->pt_ne = int64_t(ent.size());
+    ctx->has_pairs = true;
+    return WFSA_OK;
 }
 
 int configure_tiers(wfsa_dev* ctx) {
@@ -1037,10 +1176,40 @@ int prepare(wfsa_dev* ctx, int level) {
                                       : trav_grid(ctx->cfg[t], ctx->n_cu, int64_t(fb[t].size())));
         if (!fb[t].empty()) HIP_TRY(ctx->fall[t].upload(fb[t].data(), fb[t].size(), s));
     }
+    ctx->w2_grid = 0;
+    ctx->w2_n = 0;
+    std::vector<int32_t> w2l = fb[2];
+    if (ctx->w2_all) {
+        w2l.insert(w2l.end(), fb[0].begin(), fb[0].end());
+        w2l.insert(w2l.end(), fb[1].begin(), fb[1].end());
+    }
+    if (!w2l.empty() && ctx->use_wide2 && ctx->has_pairs && wide2_config(ctx)) {   // wave per string, a block per CU
+        {   // longest first: the waves take strings from a counter, the short ones fill the tail
+            std::vector<int64_t> off(size_t(S) + 1);
+            HIP_TRY(ctx->off.download(off.data(), off.size(), s));
+            HIP_TRY(hipStreamSynchronize(s));
+            std::stable_sort(w2l.begin(), w2l.end(), [&](int32_t x, int32_t y) {
+                return off[size_t(x) + 1] - off[size_t(x)] > off[size_t(y) + 1] - off[size_t(y)];
+            });
+            HIP_TRY(ctx->w2_list.upload(w2l.data(), w2l.size(), s));
+            ctx->w2_n = int32_t(w2l.size());
+        }
+        const int wpb = ctx->w2_waves;
+        ctx->w2_stride = wfsa::wide2_stride(ctx->max_len, ctx->pt_max_n);
+        const int64_t budget = (int64_t(16) << 30) / 8;   // 16 GiB of alpha rows at most
+        int64_t g = std::min<int64_t>(ctx->n_cu, (int64_t(w2l.size()) + wpb - 1) / wpb);
+        g = std::min<int64_t>(g, budget / (int64_t(wpb) * ctx->w2_stride));
+        ctx->w2_grid = int(std::max<int64_t>(g, 1));
+        const size_t n2 = size_t(ctx->w2_grid) * wpb * size_t(ctx->w2_stride);
+        HIP_TRY(ctx->w2_scratch.alloc(n2));
+        HIP_TRY(ctx->w2_ctr.alloc(2));
+        HIP_TRY(hipMemsetAsync(ctx->w2_ctr.ptr, 0, 2 * sizeof(unsigned), s));
+    }
     const size_t waves = std::max(size_t(ctx->c_grid), size_t(ctx->i_grid) * size_t(ctx->i_block / kWave)) +
                          size_t(ctx->b_waves) +
                          size_t(ctx->fall_grid[0]) * size_t(ctx->cfg[0].waves_per_block) +
-                         size_t(ctx->fall_grid[1]) * size_t(ctx->cfg[1].waves_per_block) + size_t(ctx->fall_grid[2]);
+                         size_t(ctx->fall_grid[1]) * size_t(ctx->cfg[1].waves_per_block) +
+                         size_t(std::max(ctx->fall_grid[2], ctx->w2_grid));
     // two halves: a device-resident QN step's finish reads its partials
     // while the next step writes the other half
     HIP_TRY(ctx->ll_part.alloc(2 * waves));
@@ -1265,7 +1434,8 @@ int enqueue_evaluation(wfsa_dev* ctx, bool want_logq, const unsigned* halted, in
         if (int rc = enqueue_bubbles(ctx, want_logq, halted, wave_off, s)) return rc;
     }
     if (ctx->n_bubbles > 0 && !fusedb) wave_off += ctx->b_waves;
-    for (int t = 0; t < 2; ++t) {
+    const bool w2_covers_01 = ctx->w2_grid > 0 && ctx->w2_all;
+    for (int t = 0; t < 2 && !w2_covers_01; ++t) {
         if (!ctx->n_fall[t]) continue;
         wfsa::TravArgs a = trav_args(ctx, t);
         a.list = ctx->fall[t].ptr;
@@ -1278,7 +1448,7 @@ int enqueue_evaluation(wfsa_dev* ctx, bool want_logq, const unsigned* halted, in
         HIP_TRY(wfsa::launch_trav(wfsa::MODE_WEIGHTED, a, ctx->fall_grid[t], s));
         wave_off += ctx->fall_grid[t] * ctx->cfg[t].waves_per_block;
     }
-    if (ctx->n_fall[2]) {
+    if (ctx->n_fall[2] || w2_covers_01) {
         wfsa::WideArgs a = wide_args(ctx);
         a.list = ctx->fall[2].ptr;
         a.n_list = ctx->n_fall[2];
@@ -1287,8 +1457,18 @@ int enqueue_evaluation(wfsa_dev* ctx, bool want_logq, const unsigned* halted, in
         a.logq = want_logq ? ctx->logq.ptr : nullptr;
         a.halted = halted;
         a.rmin_log = ctx->rm_eval ? ctx->rm_rs.ptr : nullptr;
-        HIP_TRY(wfsa::launch_wide(false, a, ctx->fall_grid[2], s));
-        wave_off += ctx->fall_grid[2];
+        if (ctx->w2_grid > 0) {
+            a.list = ctx->w2_list.ptr;
+            a.n_list = ctx->w2_n;
+            a.grad_lds = ctx->w2_lgrad ? 1 : 0;
+            HIP_TRY(wfsa::launch_pair_weights(ctx->pt_ent.ptr, ctx->pt_ne, ctx->ew.ptr, ctx->lw.ptr, ctx->pt_w2.ptr, s));
+            const size_t lds = wfsa::wide2_lds(ctx->n_params, ctx->w2_lgrad, ctx->w2_waves, ctx->pt_max_n);
+            HIP_TRY(wfsa::launch_wide2(a, ctx->w2_grid, ctx->w2_waves, lds, s));
+            wave_off += ctx->w2_grid;
+        } else {
+            HIP_TRY(wfsa::launch_wide(false, a, ctx->fall_grid[2], s));
+            wave_off += ctx->fall_grid[2];
+        }
     }
     if (n_ll) *n_ll = wave_off;
     if (!with_tail) {
@@ -1632,6 +1812,8 @@ int wfsa_dev_create(int device, wfsa_dev** out) {
     if (const char* e = std::getenv("WFSA_FUSE_BUBBLES")) ctx->fuse_bubbles = e[0] != '0';
     if (const char* e = std::getenv("WFSA_DENSE"); e && e[0]) ctx->dense_mode = e[0] == '0' ? 0 : 1;
     if (const char* e = std::getenv("WFSA_TIER2")) ctx->force_tier2 = e[0] == '1';
+    if (const char* e = std::getenv("WFSA_WIDE2")) ctx->use_wide2 = e[0] != '0';
+    if (const char* e = std::getenv("WFSA_WIDE2_TIERS")) ctx->w2_all = std::strcmp(e, "2") != 0;
 
     HIP_TRY(hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking));
     // measured: the cross-stream fork/join costs more idle time (5-20 us)
@@ -1762,6 +1944,7 @@ int wfsa_dev_load_model(wfsa_dev* ctx, const wfsa_model_desc* model) {
         HIP_TRY(ctx->w_eptr.upload(eptr.data(), eptr.size(), s));
         HIP_TRY(ctx->w_esrc.upload(esrc.data(), std::max<size_t>(esrc.size(), 1), s));
         HIP_TRY(ctx->w_eg.upload(eg.data(), std::max<size_t>(eg.size(), 1), s));
+        if (int rc = build_pair_tables(ctx, tm, cptr, dst, eptr, esrc, eg, pptr, pidx)) return rc;
         HIP_TRY(hipStreamSynchronize(s));
     }
     HIP_TRY(ctx->lw.alloc(size_t(E + X)));
