@@ -738,6 +738,7 @@ __global__ __launch_bounds__(kWideBlock) void wide_kernel(WideArgs a) {
 // block barriers; the gradient in one LDS table per block when it fits,
 // flushed once per launch.
 __device__ __forceinline__ void wave_fence() { __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup"); }
+constexpr int kU = 4;   // wide2: edges per lane in flight
 
 template <bool TRACK>
 __global__ __launch_bounds__(kWide2Block) void wide2_kernel(WideArgs a) {
@@ -793,23 +794,42 @@ __global__ __launch_bounds__(kWide2Block) void wide2_kernel(WideArgs a) {
         int exi = 0, esum = 0, ap = K;
         int64_t roff = 0;
         bool alive = true;
+        // step i's byte, pair range and row size, loaded one step ahead
+        int b = L > 0 ? P.bidx[str[0]] : 0;
+        int eb = 0, ee = 0, nb = 0;
+        if (b >= 0) {
+            eb = P.e_ptr[ap * K + b];
+            ee = P.e_ptr[ap * K + b + 1];
+            nb = P.n[b];
+        }
         for (int i = 0; i < L; ++i) {
-            const int b = P.bidx[str[i]];
             if (b < 0) {   // no edge consumes the byte
                 alive = false;
                 break;
             }
+            const int b2 = i + 1 < L ? P.bidx[str[i + 1]] : -1;
+            int eb2 = 0, ee2 = 0, nb2 = 0;
+            if (b2 >= 0) {
+                eb2 = P.e_ptr[b * K + b2];
+                ee2 = P.e_ptr[b * K + b2 + 1];
+                nb2 = P.n[b2];
+            }
             const double sc = ldexp(1.0, -exi);
-            const int nb = P.n[b];
             const int64_t rn = roff + P.n[ap];
             for (int d = lane; d < nb; d += kWave) Nx[d] = 0.0;
             wave_sync();
-            const int pair = ap * K + b;
-            const int eb = P.e_ptr[pair], ee = P.e_ptr[pair + 1];
-            for (int e = eb + lane; e < ee; e += kWave) {
-                const int4 en = P.ent[e];
-                const int src = en.x & 0xffff, dst = int(unsigned(en.x) >> 16);
-                lds_add(&Nx[dst], A[src] * P.w2[e].x);
+            for (int e0 = eb + lane; e0 < ee; e0 += kU * kWave) {   // kU edges per lane in flight
+                int sd[kU];
+                double w[kU];
+#pragma unroll
+                for (int u = 0; u < kU; ++u) {
+                    const int e = e0 + u * kWave;
+                    sd[u] = e < ee ? P.sd[e] : -1;
+                    w[u] = e < ee ? P.w[e] : 0.0;
+                }
+#pragma unroll
+                for (int u = 0; u < kU; ++u)
+                    if (sd[u] >= 0) lds_add(&Nx[int(unsigned(sd[u]) >> 16)], A[sd[u] & 0xffff] * w[u]);
             }
             wave_sync();
             double mx = 0.0;
@@ -831,7 +851,7 @@ __global__ __launch_bounds__(kWide2Block) void wide2_kernel(WideArgs a) {
                 for (int e = eb + lane; e < ee; e += kWave) {
                     const int4 en = P.ent[e];
                     const int src = en.x & 0xffff, dst = int(unsigned(en.x) >> 16);
-                    const double lwe = P.w2[e].y;
+                    const double lwe = P.lw[e];
                     if (H[roff + src] > 0.0 && lwe > -INFINITY) atomicMin(&KN[dst], okey(Mi[src] + lwe));
                 }
                 wave_sync();
@@ -839,7 +859,11 @@ __global__ __launch_bounds__(kWide2Block) void wide2_kernel(WideArgs a) {
             }
             roff = rn;
             ap = b;
-            wave_fence();   // this row in H (and Mg) for every lane
+            b = b2;
+            eb = eb2;
+            ee = ee2;
+            nb = nb2;
+            if (TRACK) wave_fence();   // the next min pass reads this row from H
             if (!(mx > 0.0)) {
                 alive = false;
                 break;
@@ -888,31 +912,57 @@ __global__ __launch_bounds__(kWide2Block) void wide2_kernel(WideArgs a) {
             }
         }
         wave_sync();
-        int ex_next = exi, b = ap;
+        int ex_next = exi;
+        b = ap;
+        // step i's pair range, row size and exponent, loaded one step ahead
+        int ai = byte_at(L - 1);
+        eb = P.e_ptr[ai * K + b];
+        ee = P.e_ptr[ai * K + b + 1];
+        int na = P.n[ai];
+        int ex_i = L - 1 == 0 ? 0 : ex[L - 1];
         for (int i = L - 1; i >= 0; --i) {
-            const int ai = byte_at(i);
-            const int na = P.n[ai];
+            int ai2 = 0, eb2 = 0, ee2 = 0, na2 = 0, ex2 = 0;
+            if (i > 0) {
+                ai2 = byte_at(i - 1);
+                eb2 = P.e_ptr[ai2 * K + ai];
+                ee2 = P.e_ptr[ai2 * K + ai + 1];
+                na2 = P.n[ai2];
+                ex2 = i - 1 == 0 ? 0 : ex[i - 1];
+            }
             roff -= na;
-            const int ex_i = i == 0 ? 0 : ex[i];
             const double sc = ldexp(1.0, -ex_next), sci = ldexp(1.0, -ex_i);
             for (int d = lane; d < na; d += kWave) Bi[d] = 0.0;
             wave_sync();
-            const int pair = ai * K + b;
-            const int eb = P.e_ptr[pair], ee = P.e_ptr[pair + 1];
-            for (int e = eb + lane; e < ee; e += kWave) {
-                const int4 en = P.ent[e];
-                const int src = en.x & 0xffff, dst = int(unsigned(en.x) >> 16);
-                const double af = H[roff + src] * sci;
-                if (!(af > 0.0)) continue;
-                const double bv = P.w2[e].x * Bn[dst] * sc;
-                lds_add(&Bi[src], bv);
-                const double xi = af * bv;
-                if (xi > 0.0) credit(en.z, en.w, en.y, -ps * xi);
+            for (int e0 = eb + lane; e0 < ee; e0 += kU * kWave) {
+                int4 en[kU];
+                double w[kU], af[kU];
+#pragma unroll
+                for (int u = 0; u < kU; ++u) {
+                    const int e = e0 + u * kWave;
+                    en[u] = e < ee ? P.ent[e] : make_int4(-1, 0, -1, -1);
+                    w[u] = e < ee ? P.w[e] : 0.0;
+                }
+#pragma unroll
+                for (int u = 0; u < kU; ++u) af[u] = en[u].x >= 0 ? H[roff + (en[u].x & 0xffff)] * sci : 0.0;
+#pragma unroll
+                for (int u = 0; u < kU; ++u) {
+                    if (!(af[u] > 0.0)) continue;
+                    const int src = en[u].x & 0xffff, dst = int(unsigned(en[u].x) >> 16);
+                    const double bv = w[u] * Bn[dst] * sc;
+                    lds_add(&Bi[src], bv);
+                    const double xi = af[u] * bv;
+                    if (xi > 0.0) credit(en[u].z, en[u].w, en[u].y, -ps * xi);
+                }
             }
             wave_sync();
             double* t = Bn; Bn = Bi; Bi = t;
             ex_next = ex_i;
             b = ai;
+            ai = ai2;
+            eb = eb2;
+            ee = ee2;
+            na = na2;
+            ex_i = ex2;
         }
         wave_sync();
     }
@@ -937,11 +987,12 @@ __global__ __launch_bounds__(kWide2Block) void wide2_kernel(WideArgs a) {
 }
 
 __global__ __launch_bounds__(256) void pair_weights_kernel(const int4* ent, int64_t n, const double* ew,
-                                                           const double* lw, double2* w2) {
+                                                           const double* lw, double* pw) {
     const int64_t stride = int64_t(gridDim.x) * blockDim.x;
     for (int64_t e = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; e < n; e += stride) {
         const int g = ent[e].y;
-        w2[e] = make_double2(ew[g], lw[g]);
+        pw[e] = ew[g];
+        pw[n + e] = lw[g];
     }
 }
 
@@ -1946,11 +1997,11 @@ hipError_t launch_wide2(const WideArgs& a, int grid, int waves, size_t lds, hipS
     return hipGetLastError();
 }
 
-hipError_t launch_pair_weights(const int4* ent, int64_t n, const double* ew, const double* lw, double2* w2,
+hipError_t launch_pair_weights(const int4* ent, int64_t n, const double* ew, const double* lw, double* pw,
                                hipStream_t stream) {
     if (n == 0) return hipSuccess;
     const unsigned g = unsigned(std::min<int64_t>((n + 255) / 256, 4096));
-    hipLaunchKernelGGL(pair_weights_kernel, dim3(g), dim3(256), 0, stream, ent, n, ew, lw, w2);
+    hipLaunchKernelGGL(pair_weights_kernel, dim3(g), dim3(256), 0, stream, ent, n, ew, lw, pw);
     return hipGetLastError();
 }
 

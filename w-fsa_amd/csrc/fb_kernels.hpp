@@ -161,7 +161,7 @@ struct TravArgs {
 // consuming b whose source is in D(a) -- as
 //   ent = (src index | dst index << 16, edge id, param0, param1)
 // (param -1: none; param0 = -2: more than two, read pptr/pidx) and, rewritten
-// each evaluation, w2 = (ew, lw).  A wave walks a pair's list with one edge
+// each evaluation, its ew and lw.  A wave walks a pair's list with one edge
 // per lane (contiguous loads, no padding) and sums into its LDS rows.
 struct PairTables {
     int32_t K;               // compact alphabet (bytes some edge consumes)
@@ -170,8 +170,10 @@ struct PairTables {
     const int32_t* dl_ptr;   // [K + 2] D(b) node list offsets into dl_node
     const int32_t* dl_node;  // node ids
     const int32_t* e_ptr;    // [(K + 1) K + 1] edge range of pair a K + b
+    const int32_t* sd;       // [entries] the ent .x alone (the forward's contiguous loads)
     const int4* ent;
-    const double2* w2;       // this evaluation's (ew, lw) per entry
+    const double* w;         // this evaluation's ew per entry
+    const double* lw;        // and lw
     int32_t max_n;
 };
 
@@ -230,8 +232,8 @@ inline size_t wide2_lds(int32_t n_params, bool grad_lds, int waves, int32_t max_
 }
 // waves: per block (blockDim = 64 waves); lds from wide2_lds
 hipError_t launch_wide2(const WideArgs& a, int grid, int waves, size_t lds, hipStream_t stream);
-// the pair tables' per-evaluation weights w2 from ew / lw
-hipError_t launch_pair_weights(const int4* ent, int64_t n, const double* ew, const double* lw, double2* w2,
+// the pair tables' per-evaluation weights pw[0, n) = ew, pw[n, 2n) = lw
+hipError_t launch_pair_weights(const int4* ent, int64_t n, const double* ew, const double* lw, double* pw,
                                hipStream_t stream);
 
 // The rmin info column (QuasiNewtonLearner::GetOptimizationInfo,

@@ -207,7 +207,8 @@ struct wfsa_dev {
     int64_t pt_ne = 0;
     DevBuf<int32_t> pt_bidx, pt_n, pt_dlptr, pt_dlnode, pt_eptr;
     DevBuf<int4> pt_ent;
-    DevBuf<double2> pt_w2;
+    DevBuf<int32_t> pt_sd;
+    DevBuf<double> pt_w;   // [2 ne]: ew, lw per entry
     int w2_waves = 16;           // waves per block
     bool w2_lgrad = false;       // the gradient in LDS
     DevBuf<double> w2_scratch;
@@ -407,7 +408,9 @@ wfsa::WideArgs wide_args(wfsa_dev* ctx) {
     a.pt.dl_node = ctx->pt_dlnode.ptr;
     a.pt.e_ptr = ctx->pt_eptr.ptr;
     a.pt.ent = ctx->pt_ent.ptr;
-    a.pt.w2 = ctx->pt_w2.ptr;
+    a.pt.sd = ctx->pt_sd.ptr;
+    a.pt.w = ctx->pt_w.ptr;
+    a.pt.lw = ctx->pt_w.ptr + ctx->pt_ne;
     a.pt.max_n = ctx->pt_max_n;
     a.scratch2 = ctx->w2_scratch.ptr;
     a.stride2 = ctx->w2_stride;
@@ -514,7 +517,13 @@ int build_pair_tables(wfsa_dev* ctx, const wfsa::TrellisModel& tm, const std::ve
     HIP_TRY(ctx->pt_dlnode.upload(dl_node.data(), dl_node.size(), s));
     HIP_TRY(ctx->pt_eptr.upload(e_ptr.data(), e_ptr.size(), s));
     HIP_TRY(ctx->pt_ent.upload(ent.data(), ent.size(), s));
-    HIP_TRY(ctx->pt_w2.alloc(ent.size()));
+    {
+        std::vector<int32_t> sdv(ent.size());
+        for (size_t e = 0; e < ent.size(); ++e) sdv[e] = ent[e].x;
+        HIP_TRY(ctx->pt_sd.upload(sdv.data(), sdv.size(), s));
+        HIP_TRY(hipStreamSynchronize(s));
+    }
+    HIP_TRY(ctx->pt_w.alloc(2 * ent.size()));
     HIP_TRY(hipStreamSynchronize(s));
     ctx->pt_K = K;
     ctx->pt_max_n = max_n;
@@ -1461,7 +1470,7 @@ int enqueue_evaluation(wfsa_dev* ctx, bool want_logq, const unsigned* halted, in
             a.list = ctx->w2_list.ptr;
             a.n_list = ctx->w2_n;
             a.grad_lds = ctx->w2_lgrad ? 1 : 0;
-            HIP_TRY(wfsa::launch_pair_weights(ctx->pt_ent.ptr, ctx->pt_ne, ctx->ew.ptr, ctx->lw.ptr, ctx->pt_w2.ptr, s));
+            HIP_TRY(wfsa::launch_pair_weights(ctx->pt_ent.ptr, ctx->pt_ne, ctx->ew.ptr, ctx->lw.ptr, ctx->pt_w.ptr, s));
             const size_t lds = wfsa::wide2_lds(ctx->n_params, ctx->w2_lgrad, ctx->w2_waves, ctx->pt_max_n);
             HIP_TRY(wfsa::launch_wide2(a, ctx->w2_grid, ctx->w2_waves, lds, s));
             wave_off += ctx->w2_grid;
