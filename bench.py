@@ -308,16 +308,31 @@ def roofline_of(m, traffic):
                 "kernel": "fbs_kernel (compiled-stream forward pass + fused bubbles, per step)",
                 "timed_launches": timed, "kernel_ms_per_launch": kern_ms, "all_fb_kernels_ms_per_step": fb_ms,
                 "algorithmic_bytes_per_launch": alg_bytes}
-    # family B: the traversal tiers (k_c..k_2 of the evaluation)
+    # family B: the traversal strings (k_c..k_2 of the evaluation)
     trav_ms = max(fb_ms - kern_ms, 1e-9)
-    alg_bytes = int(mean_sym * trav) + 16 * trav
+    rows, pedges = st1.get("wave_row_entries", 0), st1.get("wave_pair_edges", 0)
+    if st1.get("wave_strings", 0) > 0:
+        # wide2_kernel: every alpha entry of every position is written to HBM
+        # once by the forward and read back once by the backward (16 B; the
+        # rows of one evaluation, 16 B x sum|D|, far exceed the caches), plus
+        # the strings (L + offset + p)
+        alg_bytes = 16 * rows + int(mean_sym * trav) + 16 * trav
+        kernel = "wide2_kernel (traversal strings: a wavefront per string over byte-pair edge lists, LDS rows)"
+        note = ("per-step latency chain (edge list -> LDS gather -> LDS atomic) with a 106 KB LDS gradient table "
+                "limiting the CU to 12 strings in flight; PMC: LDS array busy ~45%, waves waiting ~75% "
+                "(profiles/r02/v8_wide2_pmc.txt)")
+    else:
+        alg_bytes = int(mean_sym * trav) + 16 * trav
+        kernel = "traversal tiers (trav_kernel<MODE_WEIGHTED> tiers 0/1 + wide_kernel tier 2), per step"
+        note = "HBM is not the binding level here (SURVEY 8d: a dependent L-step chain + LDS/L2 gathers)"
     achieved = alg_bytes / (trav_ms * 1e-3) / 1e9
     out = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-           "frac": achieved / HBM_PEAK_GBS, "traffic": None,
-           "kernel": "traversal tiers (trav_kernel<MODE_WEIGHTED> tiers 0/1 + wide_kernel tier 2), per step",
+           "frac": achieved / HBM_PEAK_GBS, "traffic": None, "kernel": kernel,
            "timed_launches": timed, "kernel_ms_per_launch": trav_ms, "all_fb_kernels_ms_per_step": fb_ms,
-           "algorithmic_bytes_per_launch": alg_bytes, "traversal_strings": trav,
-           "note": "HBM is not the binding level here (SURVEY 8d: a dependent L-step chain + LDS/L2 gathers)"}
+           "algorithmic_bytes_per_launch": alg_bytes, "traversal_strings": trav, "note": note}
+    if pedges > 0:
+        out.update({"alpha_entries_per_evaluation": rows, "pair_edges_per_pass": pedges,
+                    "pair_edge_visits_per_s": 2.0 * pedges / (trav_ms * 1e-3)})
     if live > 0:   # ~6 fp64 flops per live trellis edge (forward FMA, backward FMA, posterior mul+add)
         eps = live / (fb_ms * 1e-3)
         out.update({"live_edges_per_evaluation": live, "edge_ops_per_s": eps,

@@ -104,6 +104,9 @@ typedef struct {
      * corpus; each evaluation runs 3 GEMMs of 2 np^2 R flops per step */
     int32_t dense_rows, dense_steps, dense_np;
     int32_t tier2_strings;     /* strings on the global-scratch traversal tier */
+    int32_t wave_strings;      /* traversal strings on the wave-per-string pair-table kernel */
+    int64_t wave_row_entries;  /* per evaluation: alpha entries it writes (and reads back), sum |D| */
+    int64_t wave_pair_edges;   /* per evaluation: pair-list edges one pass walks */
 } wfsa_dev_stats;
 
 /* context ---------------------------------------------------------------- */

@@ -739,6 +739,19 @@ __global__ __launch_bounds__(kWideBlock) void wide_kernel(WideArgs a) {
 // flushed once per launch.
 __device__ __forceinline__ void wave_fence() { __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup"); }
 constexpr int kU = 4;   // wide2: edges per lane in flight
+constexpr int kExpNone = -4096;   // below every frexp exponent of a double
+// wave max of frexp exponents (kExpNone where a lane has none) by 13 ballots
+// over the offset value's bits -- VALU compares, no LDS round trips
+__device__ __forceinline__ int wave_max_exp(int e) {
+    const unsigned u = unsigned(e - kExpNone);   // 0 .. 5120
+    unsigned r = 0;
+#pragma unroll
+    for (int bit = 12; bit >= 0; --bit) {
+        const unsigned c = r | (1u << bit);
+        if (__ballot(u >= c)) r = c;
+    }
+    return int(r) + kExpNone;
+}
 
 template <bool TRACK>
 __global__ __launch_bounds__(kWide2Block) void wide2_kernel(WideArgs a) {
@@ -751,11 +764,11 @@ __global__ __launch_bounds__(kWide2Block) void wide2_kernel(WideArgs a) {
     const int K = P.K, MN = P.max_n;
     const bool lgrad = a.grad_lds != 0;
     double* gl = lds2;
-    double* rows = lds2 + (lgrad ? ((m.n_params + 1) & ~1) : 0) + int64_t(wv) * 2 * MN;
+    double* rows = lds2 + (lgrad ? ((m.n_params + kWave + 1) & ~1) : 0) + int64_t(wv) * 2 * MN;
     double* R0 = rows;              // the two rows (alternating)
     double* R1 = rows + MN;
     if (lgrad)
-        for (int j = int(threadIdx.x); j < m.n_params; j += int(blockDim.x)) gl[j] = 0.0;
+        for (int j = int(threadIdx.x); j < m.n_params + kWave; j += int(blockDim.x)) gl[j] = 0.0;   // + spare slots
     __syncthreads();
     double* H = a.scratch2 + (int64_t(blockIdx.x) * nwv + wv) * a.stride2;
     double* Mg = H + 1 + int64_t(a.max_len) * MN;   // [2][max_n] min-forward rows (rmin column)
@@ -780,7 +793,26 @@ __global__ __launch_bounds__(kWide2Block) void wide2_kernel(WideArgs a) {
         const int64_t o0 = a.off[sidx];
         const int L = int(a.off[sidx + 1] - o0);
         const uint8_t* str = a.sym + o0;
-        auto byte_at = [&](int j) { return j == 0 ? K : P.bidx[str[j - 1]]; };   // D() of position j
+        // step info, 64 steps at a time in lane registers (lane j: step c*64+j):
+        // the pair (D of position p, byte p) range, |D(byte p)| (-1: no edge
+        // consumes the byte), |D of position p|; read per step with readlane
+        int veb = 0, vee = 0, vnb = 0, vna = 0;
+        auto load_chunk = [&](int c) {
+            const int p = c * kWave + lane;
+            veb = vee = vnb = vna = 0;
+            if (p < L) {
+                const int bp = P.bidx[str[p]];
+                const int apv = p == 0 ? K : P.bidx[str[p - 1]];
+                if (bp < 0 || apv < 0) {
+                    vnb = -1;
+                } else {
+                    veb = P.e_ptr[apv * K + bp];
+                    vee = P.e_ptr[apv * K + bp + 1];
+                    vnb = P.n[bp];
+                    vna = P.n[apv];
+                }
+            }
+        };
         // forward: the current row in A (LDS), every row also to H + roff (HBM)
         double* A = R0;
         double* Nx = R1;
@@ -791,55 +823,48 @@ __global__ __launch_bounds__(kWide2Block) void wide2_kernel(WideArgs a) {
             if (TRACK) Mg[0] = 0.0;
         }
         wave_sync();
-        int exi = 0, esum = 0, ap = K;
+        int exi = 0, esum = 0, last_n = 1;   // last_n: size of the current row
         int64_t roff = 0;
         bool alive = true;
-        // step i's byte, pair range and row size, loaded one step ahead
-        int b = L > 0 ? P.bidx[str[0]] : 0;
-        int eb = 0, ee = 0, nb = 0;
-        if (b >= 0) {
-            eb = P.e_ptr[ap * K + b];
-            ee = P.e_ptr[ap * K + b + 1];
-            nb = P.n[b];
-        }
         for (int i = 0; i < L; ++i) {
-            if (b < 0) {   // no edge consumes the byte
+            if ((i & (kWave - 1)) == 0) load_chunk(i / kWave);
+            const int nb = __builtin_amdgcn_readlane(vnb, i & (kWave - 1));
+            if (nb < 0) {   // no edge consumes the byte
                 alive = false;
                 break;
             }
-            const int b2 = i + 1 < L ? P.bidx[str[i + 1]] : -1;
-            int eb2 = 0, ee2 = 0, nb2 = 0;
-            if (b2 >= 0) {
-                eb2 = P.e_ptr[b * K + b2];
-                ee2 = P.e_ptr[b * K + b2 + 1];
-                nb2 = P.n[b2];
-            }
+            const int eb = __builtin_amdgcn_readlane(veb, i & (kWave - 1));
+            const int ee = __builtin_amdgcn_readlane(vee, i & (kWave - 1));
             const double sc = ldexp(1.0, -exi);
-            const int64_t rn = roff + P.n[ap];
+            const int64_t rn = roff + last_n;
             for (int d = lane; d < nb; d += kWave) Nx[d] = 0.0;
             wave_sync();
-            for (int e0 = eb + lane; e0 < ee; e0 += kU * kWave) {   // kU edges per lane in flight
+            for (int e0 = eb + lane; e0 < ((a.dbg & 2) ? eb : ee); e0 += kU * kWave) {   // kU edges per lane in flight
                 int sd[kU];
-                double w[kU];
+                double w[kU], r[kU];
 #pragma unroll
                 for (int u = 0; u < kU; ++u) {
                     const int e = e0 + u * kWave;
                     sd[u] = e < ee ? P.sd[e] : -1;
                     w[u] = e < ee ? P.w[e] : 0.0;
                 }
+                // branch-free: a padding lane adds 0 to its own entry (distinct banks)
+                const int own = lane < nb ? lane : 0;
+#pragma unroll
+                for (int u = 0; u < kU; ++u) r[u] = A[sd[u] >= 0 ? (sd[u] & 0xffff) : 0];
 #pragma unroll
                 for (int u = 0; u < kU; ++u)
-                    if (sd[u] >= 0) lds_add(&Nx[int(unsigned(sd[u]) >> 16)], A[sd[u] & 0xffff] * w[u]);
+                    lds_add(&Nx[sd[u] >= 0 ? int(unsigned(sd[u]) >> 16) : own], sd[u] >= 0 ? r[u] * w[u] : 0.0);
             }
             wave_sync();
-            double mx = 0.0;
+            int emx = kExpNone;   // the row's largest exponent (ballots, no LDS)
             for (int d = lane; d < nb; d += kWave) {
                 const double v = Nx[d] * sc;
                 Nx[d] = v;
                 H[rn + d] = v;
-                mx = fmax(mx, v);
+                if (v > 0.0) emx = max(emx, __builtin_amdgcn_frexp_exp(v));
             }
-            mx = wave_max(mx);
+            emx = wave_max_exp(emx);
             wave_sync();
             double* t = A; A = Nx; Nx = t;
             if (TRACK) {   // (min, x) forward: keys summed in the free row, sources' liveness from H
@@ -856,26 +881,23 @@ __global__ __launch_bounds__(kWide2Block) void wide2_kernel(WideArgs a) {
                 }
                 wave_sync();
                 for (int d = lane; d < nb; d += kWave) Mn[d] = odec(KN[d]);
+                wave_fence();   // the next min pass reads this row from H
             }
             roff = rn;
-            ap = b;
-            b = b2;
-            eb = eb2;
-            ee = ee2;
-            nb = nb2;
-            if (TRACK) wave_fence();   // the next min pass reads this row from H
-            if (!(mx > 0.0)) {
+            last_n = nb;
+            if (emx == kExpNone) {   // every node of the row is zero
                 alive = false;
                 break;
             }
-            exi = __builtin_amdgcn_frexp_exp(mx);
+            exi = emx;
             esum += exi;
             if (lane == 0) ex[i + 1] = exi;
         }
         double qh = 0.0;
         const double scL = ldexp(1.0, -exi);
-        const int nL = alive ? P.n[ap] : 0;
-        const int32_t* dL = P.dl_node + P.dl_ptr[ap];
+        const int aL = L > 0 ? P.bidx[str[L - 1]] : K;
+        const int nL = alive ? last_n : 0;
+        const int32_t* dL = P.dl_node + P.dl_ptr[alive ? aL : K];
         for (int d = lane; d < nL; d += kWave) qh += A[d] * scL * end_weight(m, dL[d]);
         qh = wave_sum(qh);
         const double lq = qh > 0.0 ? log(qh) + kLn2 * double(esum) : -INFINITY;
@@ -893,8 +915,8 @@ __global__ __launch_bounds__(kWide2Block) void wide2_kernel(WideArgs a) {
             if (a.logq) a.logq[sidx] = lq;
             ll += ps * lq;
         }
-        if (!(qh > 0.0)) continue;
-        wave_fence();   // the rows in H are visible to every lane
+        if (!(qh > 0.0) || (a.dbg & 1)) continue;
+        wave_fence();   // the rows in H (and ex) are visible to every lane
         // backward (beta scaled so that alpha_i beta_i is the node posterior):
         // beta_{i+1} in Bn (LDS), beta_i summed into Bi (LDS)
         const double inv_q = 1.0 / qh;
@@ -912,57 +934,55 @@ __global__ __launch_bounds__(kWide2Block) void wide2_kernel(WideArgs a) {
             }
         }
         wave_sync();
-        int ex_next = exi;
-        b = ap;
-        // step i's pair range, row size and exponent, loaded one step ahead
-        int ai = byte_at(L - 1);
-        eb = P.e_ptr[ai * K + b];
-        ee = P.e_ptr[ai * K + b + 1];
-        int na = P.n[ai];
-        int ex_i = L - 1 == 0 ? 0 : ex[L - 1];
+        int ex_next = exi, vex = 0;
         for (int i = L - 1; i >= 0; --i) {
-            int ai2 = 0, eb2 = 0, ee2 = 0, na2 = 0, ex2 = 0;
-            if (i > 0) {
-                ai2 = byte_at(i - 1);
-                eb2 = P.e_ptr[ai2 * K + ai];
-                ee2 = P.e_ptr[ai2 * K + ai + 1];
-                na2 = P.n[ai2];
-                ex2 = i - 1 == 0 ? 0 : ex[i - 1];
+            if (i == L - 1 || (i & (kWave - 1)) == kWave - 1) {   // this step's chunk (steps and row exponents)
+                load_chunk(i / kWave);
+                const int p = (i / kWave) * kWave + lane;
+                vex = p <= L ? ex[p] : 0;
             }
+            const int eb = __builtin_amdgcn_readlane(veb, i & (kWave - 1));
+            const int ee = __builtin_amdgcn_readlane(vee, i & (kWave - 1));
+            const int na = __builtin_amdgcn_readlane(vna, i & (kWave - 1));
+            const int ex_i = __builtin_amdgcn_readlane(vex, i & (kWave - 1));
             roff -= na;
             const double sc = ldexp(1.0, -ex_next), sci = ldexp(1.0, -ex_i);
             for (int d = lane; d < na; d += kWave) Bi[d] = 0.0;
             wave_sync();
-            for (int e0 = eb + lane; e0 < ee; e0 += kU * kWave) {
+            for (int e0 = eb + lane; e0 < ((a.dbg & 2) ? eb : ee); e0 += kU * kWave) {
                 int4 en[kU];
-                double w[kU], af[kU];
+                double w[kU], af[kU], bn[kU];
 #pragma unroll
                 for (int u = 0; u < kU; ++u) {
                     const int e = e0 + u * kWave;
                     en[u] = e < ee ? P.ent[e] : make_int4(-1, 0, -1, -1);
                     w[u] = e < ee ? P.w[e] : 0.0;
                 }
+                // branch-free: a padding / dead lane adds 0 to its own entries
+                const int own = lane < na ? lane : 0;
 #pragma unroll
                 for (int u = 0; u < kU; ++u) af[u] = en[u].x >= 0 ? H[roff + (en[u].x & 0xffff)] * sci : 0.0;
 #pragma unroll
+                for (int u = 0; u < kU; ++u) bn[u] = Bn[en[u].x >= 0 ? int(unsigned(en[u].x) >> 16) : 0];
+#pragma unroll
                 for (int u = 0; u < kU; ++u) {
-                    if (!(af[u] > 0.0)) continue;
-                    const int src = en[u].x & 0xffff, dst = int(unsigned(en[u].x) >> 16);
-                    const double bv = w[u] * Bn[dst] * sc;
-                    lds_add(&Bi[src], bv);
-                    const double xi = af[u] * bv;
-                    if (xi > 0.0) credit(en[u].z, en[u].w, en[u].y, -ps * xi);
+                    const bool on = af[u] > 0.0;
+                    const double bv = on ? w[u] * bn[u] * sc : 0.0;
+                    lds_add(&Bi[on ? (en[u].x & 0xffff) : own], bv);
+                    const double v = -ps * (af[u] * bv);
+                    if (lgrad) {   // two parameters per edge in one table; the rest to this lane's spare slot
+                        const int spare = m.n_params + lane;
+                        block_add(&gl[on && en[u].z >= 0 ? en[u].z : spare], on ? v : 0.0);
+                        block_add(&gl[on && en[u].w >= 0 ? en[u].w : spare], on ? v : 0.0);
+                        if (on && en[u].z == -2) credit(-2, -1, en[u].y, v);
+                    } else if (on && af[u] * bv > 0.0) {
+                        credit(en[u].z, en[u].w, en[u].y, v);
+                    }
                 }
             }
             wave_sync();
             double* t = Bn; Bn = Bi; Bi = t;
             ex_next = ex_i;
-            b = ai;
-            ai = ai2;
-            eb = eb2;
-            ee = ee2;
-            na = na2;
-            ex_i = ex2;
         }
         wave_sync();
     }

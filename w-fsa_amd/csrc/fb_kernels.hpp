@@ -197,6 +197,7 @@ struct WideArgs {
     double* scratch;         // per block: alpha [(max_len+1) n_nodes], beta [2 n_nodes], exponents
     int64_t scratch_stride;  // doubles per block
     int32_t grad_lds;        // weighted: the gradient accumulates in LDS (n_params doubles)
+    int32_t dbg;             // wide2 timing experiments (WFSA_W2_DBG): 1 no backward, 2 no edge loops, 3 both
     double* grad;            // [n_params]  -p_s E[count]
     double* ll_part;         // [grid]
     double* logq;            // [S] or null
@@ -226,9 +227,9 @@ constexpr int kWide2Block = 1024;
 inline int64_t wide2_stride(int32_t max_len, int32_t max_n) {
     return 1 + int64_t(max_len) * max_n + 2 * int64_t(max_n) + (int64_t(max_len) + 3) / 2 + 2;
 }
-// LDS of a block: the gradient table (grad_lds) + per wave 2 rows of max_n doubles
+// LDS of a block: the gradient table (grad_lds, + 64 spare slots) + per wave 2 rows of max_n doubles
 inline size_t wide2_lds(int32_t n_params, bool grad_lds, int waves, int32_t max_n) {
-    return (grad_lds ? size_t((n_params + 1) & ~1) * 8 : 0) + size_t(waves) * 2 * size_t(max_n) * 8;
+    return (grad_lds ? size_t((n_params + 64 + 1) & ~1) * 8 : 0) + size_t(waves) * 2 * size_t(max_n) * 8;
 }
 // waves: per block (blockDim = 64 waves); lds from wide2_lds
 hipError_t launch_wide2(const WideArgs& a, int grid, int waves, size_t lds, hipStream_t stream);

@@ -1197,6 +1197,29 @@ int prepare(wfsa_dev* ctx, int level) {
             std::vector<int64_t> off(size_t(S) + 1);
             HIP_TRY(ctx->off.download(off.data(), off.size(), s));
             HIP_TRY(hipStreamSynchronize(s));
+            {   // the pass's work, for the roofline: alpha entries and pair-list edges per evaluation
+                std::vector<uint8_t> sy(static_cast<size_t>(off[size_t(S)]));
+                std::vector<int32_t> bid(256), pn(size_t(ctx->pt_K) + 1), ep(size_t(int64_t(ctx->pt_K + 1) * ctx->pt_K) + 1);
+                HIP_TRY(ctx->sym.download(sy.data(), sy.size(), s));
+                HIP_TRY(ctx->pt_bidx.download(bid.data(), 256, s));
+                HIP_TRY(ctx->pt_n.download(pn.data(), pn.size(), s));
+                HIP_TRY(ctx->pt_eptr.download(ep.data(), ep.size(), s));
+                HIP_TRY(hipStreamSynchronize(s));
+                int64_t rows = 0, edges = 0;
+                const int K = ctx->pt_K;
+                for (int32_t i : w2l) {
+                    int a = K;
+                    for (int64_t q = off[size_t(i)]; q < off[size_t(i) + 1]; ++q) {
+                        const int b = bid[sy[size_t(q)]];
+                        if (b < 0) break;
+                        rows += pn[size_t(b)];
+                        edges += ep[size_t(a * K + b) + 1] - ep[size_t(a * K + b)];
+                        a = b;
+                    }
+                }
+                ctx->stats.wave_row_entries = rows;
+                ctx->stats.wave_pair_edges = edges;
+            }
             std::stable_sort(w2l.begin(), w2l.end(), [&](int32_t x, int32_t y) {
                 return off[size_t(x) + 1] - off[size_t(x)] > off[size_t(y) + 1] - off[size_t(y)];
             });
@@ -1247,6 +1270,8 @@ int prepare(wfsa_dev* ctx, int level) {
     ctx->stats.compiled_strings = nc;
     ctx->stats.fallback_strings = int64_t(fb[0].size() + fb[1].size() + fb[2].size());
     ctx->stats.tier2_strings = ctx->tier2_strings;
+    ctx->stats.wave_strings = ctx->w2_grid > 0 ? ctx->w2_n : 0;
+    if (ctx->w2_grid == 0) ctx->stats.wave_row_entries = ctx->stats.wave_pair_edges = 0;
     ctx->stats.stream_words = words;
     ctx->stats.stream_bytes = chunks * 16;
     ctx->stats.n_bubbles = nbub;
@@ -1470,6 +1495,11 @@ int enqueue_evaluation(wfsa_dev* ctx, bool want_logq, const unsigned* halted, in
             a.list = ctx->w2_list.ptr;
             a.n_list = ctx->w2_n;
             a.grad_lds = ctx->w2_lgrad ? 1 : 0;
+            static const int w2dbg = [] {
+                const char* e = std::getenv("WFSA_W2_DBG");
+                return e ? std::atoi(e) : 0;
+            }();
+            a.dbg = w2dbg;
             HIP_TRY(wfsa::launch_pair_weights(ctx->pt_ent.ptr, ctx->pt_ne, ctx->ew.ptr, ctx->lw.ptr, ctx->pt_w.ptr, s));
             const size_t lds = wfsa::wide2_lds(ctx->n_params, ctx->w2_lgrad, ctx->w2_waves, ctx->pt_max_n);
             HIP_TRY(wfsa::launch_wide2(a, ctx->w2_grid, ctx->w2_waves, lds, s));

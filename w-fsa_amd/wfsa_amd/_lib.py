@@ -43,6 +43,7 @@ class DevStats(C.Structure):
         ("host_steps", i64), ("host_begin_ms", dbl), ("host_overlap_ms", dbl), ("host_wait_ms", dbl),
         ("host_post_ms", dbl),
         ("dense_rows", i32), ("dense_steps", i32), ("dense_np", i32), ("tier2_strings", i32),
+        ("wave_strings", i32), ("wave_row_entries", i64), ("wave_pair_edges", i64),
     ]
 
 
