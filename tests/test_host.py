@@ -167,3 +167,12 @@ def test_cli_help_and_missing_input():
     assert r.returncode == 1 and "Unable to open" in r.stderr
     r = subprocess.run([CLI, "-opt", "Hessian", "-a", "x", "-c", "y"], capture_output=True, text=True)
     assert r.returncode == 1
+
+
+def test_crlf_automaton_fails_like_reference():
+    """data/test.wfsa.win (CRLF): the separator line is "\\r", so the start
+    line's emission runs into the next line; the parse stops at the reference's
+    "transitions after emissions" check (fails to parse)."""
+    import wfsa_amd as W
+    with pytest.raises(W.WfsaError, match='You should enlist transitions of "a" after emissions of the same state!'):
+        W.Fsa.read_file(os.path.join(DATA, "test.wfsa.win"))

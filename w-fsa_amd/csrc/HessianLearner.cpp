@@ -297,7 +297,43 @@ Factored factor_and_solve(wfsa_dev* dev, std::vector<double>& H, int64_t N, cons
 
 }  // namespace
 
-void HessianLearner::OptimizationStep(double eta, bool) {   // :63-130
+// The reference's sparse KKT layout (AssembleH, :381-467): row i < n holds
+// its diagonal, the equivocal pattern's columns j > i (with H_f), then the
+// constraint column n + C(i); rows n.. hold their (zero) diagonal.
+// with_jg = false: the n x n Hessian of ComputeLogDetHessian (:219-260), the
+// constraint column dropped.  Prints it as PrintCsrMtx does (PrintEq with rhs,
+// PrintH without, :262-270).
+void HessianLearner::PrintKkt(FILE* f, const std::vector<double>& H, int64_t ld, bool with_hf, bool with_jg,
+                              const std::vector<double>* rhs_print) {
+    const int64_t n = int64_t(_x.size()), k = with_jg ? int64_t(lambda.size()) : 0;
+    std::vector<std::vector<int32_t>> upper(static_cast<size_t>(n));
+    if (with_hf && !HasUniquePaths()) {
+        SetupHf();
+        for (size_t t = 0; t < hf_j.size(); ++t)
+            if (hf_j[t] >= 0 && hf_k[t] >= 0 && hf_j[t] != hf_k[t])
+                upper[size_t(std::min(hf_j[t], hf_k[t]))].push_back(std::max(hf_j[t], hf_k[t]));
+    }
+    std::vector<int32_t> rows(1, 0), cols;
+    std::vector<double> vals;
+    for (int64_t i = 0; i < n; ++i) {
+        auto& u = upper[size_t(i)];
+        std::sort(u.begin(), u.end());
+        u.erase(std::unique(u.begin(), u.end()), u.end());
+        cols.push_back(int32_t(i));
+        for (int32_t j : u) cols.push_back(j);
+        if (with_jg) cols.push_back(int32_t(n + Ccol[size_t(i)]));
+        rows.push_back(int32_t(cols.size()));
+    }
+    for (int64_t i = n; i < n + k; ++i) {
+        cols.push_back(int32_t(i));
+        rows.push_back(int32_t(cols.size()));
+    }
+    for (size_t r = 0; r + 1 < rows.size(); ++r)
+        for (int32_t q = rows[r]; q < rows[r + 1]; ++q) vals.push_back(H[size_t(int64_t(r) * ld + cols[size_t(q)])]);
+    print_csr(f, vals.data(), rows, cols, rhs_print);
+}
+
+void HessianLearner::OptimizationStep(double eta, bool verbose) {   // :63-130
     ComputeRhs();
     ComputeObjective();
     ComputeRmin(rmin);
@@ -312,6 +348,10 @@ void HessianLearner::OptimizationStep(double eta, bool) {   // :63-130
         H[size_t(i * N + i)] += expx[size_t(i)] * lambda[size_t(Ccol[size_t(i)])];
         H[size_t(i * N + c)] += expx[size_t(i)];
         H[size_t(c * N + i)] += expx[size_t(i)];
+    }
+    if (verbose) {   // (:76-80)
+        std::fputs("H:\n", stderr);
+        PrintKkt(stderr, H, N, include_Hf, true, &rhs);
     }
     lambda_min = k ? *std::min_element(lambda.begin(), lambda.end()) : 0.0;
     step.assign(size_t(N), 0.0);
@@ -365,7 +405,7 @@ bool HessianLearner::HaltCondition(double tol) {   // :374-379
 
 // log det of the objective's Hessian in the weights w = exp(x):
 // (H_f - diag(grad f)) / (exp(x_j) exp(x_k)) (:219-260)
-double HessianLearner::ComputeLogDetHessian() {
+double HessianLearner::ComputeLogDetHessian(bool verbose) {
     const int64_t n = int64_t(_x.size());
     if (n > kMaxDense)
         throw LearnerError("HessianLearner: log det of ", n, " parameters exceeds the dense limit ", kMaxDense);
@@ -376,6 +416,7 @@ double HessianLearner::ComputeLogDetHessian() {
     for (int64_t j = 0; j < n; ++j) H[size_t(j * n + j)] -= grad[size_t(j)];
     for (int64_t j = 0; j < n; ++j)
         for (int64_t k = 0; k < n; ++k) H[size_t(j * n + k)] /= expx[size_t(j)] * expx[size_t(k)];
+    if (verbose) log_det_h = H;   // for PrintH after the Hessian line (:360)
     const double inf = std::numeric_limits<double>::infinity();
     if (!offdiag) {   // diagonal (src/Utils.cpp:300-311)
         double r = 0.0;
@@ -391,10 +432,10 @@ double HessianLearner::ComputeLogDetHessian() {
     return f.log_abs_det;
 }
 
-std::vector<double> HessianLearner::GetOptimizationResult(bool) {   // :349-372
+std::vector<double> HessianLearner::GetOptimizationResult(bool verbose) {   // :349-372
     ComputeModeledProbs();
     ComputeObjective();
-    const double logdet = ComputeLogDetHessian();
+    const double logdet = ComputeLogDetHessian(verbose);
     const int64_t n = int64_t(_x.size());
     int64_t nnz = n;
     if (hf_ready)
@@ -402,6 +443,10 @@ std::vector<double> HessianLearner::GetOptimizationResult(bool) {   // :349-372
             if (hf_j[t] >= 0 && hf_k[t] >= 0 && hf_j[t] != hf_k[t]) ++nnz;
     std::fprintf(stderr, "Hessian:\n\trows: %lld\n\tnnz: %lld\n\tfill: %g\n", (long long)n, (long long)nnz,
                  n ? double(nnz) / double(n) : 0.0);
+    if (verbose && !log_det_h.empty()) {
+        PrintKkt(stderr, log_det_h, n, true, false, nullptr);
+        log_det_h.clear();
+    }
     return {GetKLDistance(),
             mxlogx(GetCommonSupport()),
             LogModelVolume(),

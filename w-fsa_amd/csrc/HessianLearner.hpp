@@ -59,7 +59,7 @@ public:
 
     void ComputeExpX();
     void ComputeGrad();
-    double ComputeLogDetHessian();
+    double ComputeLogDetHessian(bool verbose = false);
     const std::vector<double>& GetGradient() const { return grad; }
     const std::vector<double>& GetLambda() const { return lambda; }
     std::vector<double> GetLagrangeMultipliers() const override { return lambda; }
@@ -76,6 +76,9 @@ private:
     // H (ld x ld, row-major) -= sum_s p_s Cov_s at the current x, on the
     // trimmed parameters; returns whether the pattern has off-diagonal entries
     bool AddHf(std::vector<double>& H, int64_t ld);
+    void PrintKkt(FILE* f, const std::vector<double>& H, int64_t ld, bool with_hf, bool with_jg,
+                  const std::vector<double>* rhs_print);
+    std::vector<double> log_det_h;   // the last log-det Hessian, kept for PrintH (verbose)
 
     std::vector<double> rhs, expx, grad, lambda, step;
     std::vector<int32_t> hf_j, hf_k;   // trimmed indices of the pattern (-1: not a variable)

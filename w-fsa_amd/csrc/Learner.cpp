@@ -1,5 +1,7 @@
 #include "Learner.hpp"
 
+#include "Paths.hpp"
+
 #include <algorithm>
 #include <cmath>
 #include <limits>
@@ -7,6 +9,7 @@
 #include <iomanip>
 #include <numeric>
 #include <sstream>
+#include <cstring>
 
 namespace wfsa {
 
@@ -284,8 +287,78 @@ bool Learner::LoadMatrices(const std::string& prefix) {   // src/Learner.cpp:125
     return true;
 }
 
+void Learner::EnumeratePaths(const Fsa& fsa, const Corpus& corpus, bool bfs) {
+    if (nranks > 1) throw LearnerError("path enumeration runs on one rank");
+    auto m = std::make_unique<Matrices>();
+    typedef std::vector<std::pair<int32_t, double>> Path;   // (parameter, count), sorted
+    auto add = [](Path& h, int32_t j) {   // SortedInsert(history, j) += 1
+        auto it = std::lower_bound(h.begin(), h.end(), j, [](const auto& a, int32_t b) { return a.first < b; });
+        if (it == h.end() || it->first != j) it = h.insert(it, {j, 0.0});
+        it->second += 1.0;
+    };
+    const char* end_state = fsa.GetEndState();
+    bool has_path = false;
+    auto acc = [&](Path& h, const Fsa::NextState& t, const Fsa::NamedProb& e) {
+        if (t.index >= 0) add(h, t.index);
+        if (std::strcmp(t.next->first, end_state) != 0 && e.index >= 0) add(h, e.index);
+    };
+    auto done = [&](const Path& path) {
+        if (!has_path) m->mrow.push_back(int32_t(m->mcol.size()));
+        has_path = true;
+        m->prow.push_back(int32_t(m->pcol.size()));
+        for (const auto& v : path) {
+            m->pdata.push_back(v.second);
+            m->pcol.push_back(v.first);
+        }
+        m->mcol.push_back(int32_t(m->mcol.size()));
+    };
+    auto rec = make_recognizer<Path>(fsa, acc, done);
+    for (const auto& word : corpus) {
+        has_path = false;
+        rec.Recognize(word.first.c_str(), Path(), bfs);
+    }
+    m->mrow.push_back(int32_t(m->mcol.size()));
+    m->prow.push_back(int32_t(m->pcol.size()));
+    // Trim's renumbering of P (src/Learner.cpp:397-419): unused and fixed
+    // parameters drop out, the rest take their trimmed index
+    std::vector<int32_t> pcol;
+    std::vector<double> pdata;
+    int32_t start = m->prow[0];
+    for (size_t r = 0; r + 1 < m->prow.size(); ++r) {
+        const int32_t stop = m->prow[r + 1];
+        for (int32_t q = start; q < stop; ++q) {
+            const int32_t t = trimmed_weights[size_t(m->pcol[size_t(q)])];
+            if (t >= 0) {
+                pcol.push_back(t);
+                pdata.push_back(m->pdata[size_t(q)]);
+            }
+        }
+        start = stop;
+        m->prow[r + 1] = int32_t(pcol.size());
+    }
+    m->pcol.swap(pcol);
+    m->pdata.swap(pdata);
+    m->crow = Crow;
+    m->ccol = Ccol;
+    if (int64_t(m->mcol.size()) != n_paths_global || int64_t(m->mrow.size()) - 1 != n_strings_global)
+        throw LearnerError("path enumeration found ", m->mrow.size() - 1, " strings and ", m->mcol.size(),
+                           " paths; the device counted ", n_strings_global, " and ", n_paths_global);
+    enumerated = std::move(m);
+}
+
+// PrintC / PrintM / PrintP (src/Learner.cpp:60-80)
+void Learner::PrintC(FILE* f) const { print_csr(f, nullptr, Crow, Ccol); }
+
+void Learner::PrintM(FILE* f) const {
+    if (const Matrices* m = PathMatrices()) print_csr(f, nullptr, m->mrow, m->mcol);
+}
+
+void Learner::PrintP(FILE* f) const {
+    if (const Matrices* m = PathMatrices()) print_csr(f, m->pdata.data(), m->prow, m->pcol);
+}
+
 bool Learner::SaveMatrices(const std::string& prefix) const {   // src/Learner.cpp:82-123
-    if (!matrices) return false;   // no path matrices exist: this build never enumerates paths
+    if (!HasPathMatrices()) return false;   // after BuildFrom: EnumeratePaths first
     auto put = [&](const char* ext, auto&& body) {
         std::ofstream ofs(prefix + ext);
         if (!ofs) return false;
@@ -293,7 +366,7 @@ bool Learner::SaveMatrices(const std::string& prefix) const {   // src/Learner.c
         body(ofs);
         return bool(ofs);
     };
-    const Matrices& m = *matrices;
+    const Matrices& m = *PathMatrices();
     return put(".C", [&](std::ostream& o) { write_csr(o, nullptr, m.crow, m.ccol); }) &&
            put(".M", [&](std::ostream& o) { write_csr(o, nullptr, m.mrow, m.mcol); }) &&
            put(".P", [&](std::ostream& o) { write_csr(o, &m.pdata, m.prow, m.pcol); }) &&

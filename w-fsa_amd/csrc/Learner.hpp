@@ -61,6 +61,16 @@ public:
     bool LoadMatrices(const std::string& prefix);
     bool SaveMatrices(const std::string& prefix) const;
     bool FromMatrices() const { return matrices != nullptr; }
+    // The reference's P / M (paths x parameters counts, strings x paths) after
+    // BuildFrom + Trim, enumerated on the host in the reference's path order
+    // (Paths.hpp; src/Learner.cpp:276-348 and Trim's renumbering :397-419) --
+    // for -p and -m >prefix only, one rank.  Then PrintC/M/P
+    // (src/Learner.cpp:60-80) print them and SaveMatrices writes them.
+    void EnumeratePaths(const Fsa& fsa, const Corpus& corpus, bool bfs = true);
+    bool HasPathMatrices() const { return matrices != nullptr || enumerated != nullptr; }
+    void PrintC(FILE* f) const;
+    void PrintM(FILE* f) const;
+    void PrintP(FILE* f) const;
 
     void Renormalize();
     void RewriteWeights(Fsa& fsa) const;
@@ -183,6 +193,8 @@ private:
         std::vector<int32_t> crow, ccol, mrow, mcol, prow, pcol;
     };
     std::unique_ptr<Matrices> matrices;
+    std::unique_ptr<Matrices> enumerated;   // EnumeratePaths (after BuildFrom)
+    const Matrices* PathMatrices() const { return matrices ? matrices.get() : enumerated.get(); }
 };
 
 void ThrowOnDevError(int rc, const char* what);

@@ -16,24 +16,12 @@
 #include "Corpus.hpp"
 #include "Fsa.hpp"
 #include "HessianLearner.hpp"
+#include "Paths.hpp"
 #include "QuasiNewtonLearner.hpp"
 
 using namespace wfsa;
 
 namespace {
-
-// PrintFixedWidth (src/Utils.cpp:82-97): the epoch table's number format
-void print_fixed_width(FILE* out, double x, int width) {
-    const int mag = (x == 0) ? 0 : int(std::floor(std::log10(std::abs(x))));
-    if (mag <= width - 2 && mag >= 0) {
-        if (std::floor(x) == x) std::fprintf(out, "%*.0f", width, x);
-        else std::fprintf(out, "%*.*f", width, std::max(0, width - 3 - mag), x);
-    } else if (-4 < mag && mag < 0) {
-        std::fprintf(out, "%*.*f", width, width - 3, x);
-    } else {
-        std::fprintf(out, "%*.*e", width, width - 7, x);
-    }
-}
 
 void usage() {
     std::cerr << "usage: wfsa -a automaton.wfsa -c strings.corpus [options]\n"
@@ -50,9 +38,11 @@ void usage() {
                  "  -s, --suppress         do not print the learned FSA\n"
                  "  -x, --initx            read the initial x vector from stdin\n"
                  "  -opt NAME              Hessian (default) or QuasiNewton\n"
-                 "  -p, --print            accepted (the reference prints its path matrices; no paths exist here)\n"
+                 "  -p, --print            print the recognized paths, C, M, P and (Hessian) the KKT system to stderr\n"
+                 "  -pr, --print-recognize print the recognized paths to stderr\n"
+                 "  -r, --recognize N      path order of -p / -m >: 0 breadth-first (default), 1 depth-first\n"
                  "  -m, --matrix <FILE|>FILE  load the path matrices FILE.{C,M,P,prob,aux} instead of -a/-c,\n"
-                 "                         or save them (only matrices that were loaded: paths are never enumerated)\n"
+                 "                         or save them (after -a/-c: the paths enumerated on the host)\n"
                  "  -d, --device N         GPU to use (0)\n";
 }
 
@@ -63,6 +53,8 @@ int main(int argc, const char* argv[]) {
     int epochs = 20, initflags = 0, device = 0;
     double eta = 1.0, tol = 1e-6;
     bool normalize = false, suppress = false, evaluate = false, initx = false;
+    bool print = false, print_recognize = false;
+    int recognize = 0;   // 0: breadth-first, 1: depth-first (path order of -p / -m >)
     for (int i = 1; i < argc; ++i) {
         const std::string a = argv[i];
         auto next = [&]() -> const char* {
@@ -87,8 +79,16 @@ int main(int argc, const char* argv[]) {
         else if (a == "-eval" || a == "--eval" || a == "--evaluate") evaluate = true;
         else if (a == "-s" || a == "--suppress") suppress = true;
         else if (a == "-x" || a == "--initx" || a == "--initial") initx = true;
-        else if (a == "-p" || a == "--print" || a == "-pr" || a == "--print-recognize") { /* no path listing */ }
-        else if (a == "-t" || a == "--thread" || a == "--threads" || a == "-r" || a == "--recognize") next();
+        else if (a == "-p" || a == "--print") print = true;
+        else if (a == "-pr" || a == "--print-recognize") print_recognize = true;
+        else if (a == "-r" || a == "--recognize") {
+            recognize = std::atoi(next());
+            if (recognize != 0 && recognize != 1) {
+                std::cerr << "-r must be 0 (breadth-first) or 1 (depth-first)" << std::endl;
+                return 1;
+            }
+        }
+        else if (a == "-t" || a == "--thread" || a == "--threads") next();
         else { std::cerr << "unknown argument " << a << std::endl; usage(); return 1; }
     }
     if (optimizer != "QuasiNewton" && optimizer != "Hessian") {
@@ -139,7 +139,25 @@ int main(int argc, const char* argv[]) {
                   << "\n\tparameters: " << fsa.GetNumberOfParameters()
                   << "\n\tconstraints: " << fsa.GetNumberOfConstraints()
                   << "\n\tfree parameters: " << fsa.GetNumberOfFreeParameters() << std::endl;
+        if (print || print_recognize) {   // src/main.cpp:178-203: every recognized path, on the host
+            typedef std::pair<std::string, std::string> Path;   // (emitted string, state sequence)
+            auto acc = [&](Path& h, const Fsa::NextState& t, const Fsa::NamedProb& e) {
+                h.first += e.str;
+                h.second += " -> ";
+                h.second += t.next->first;
+                if (e.str[0]) {
+                    h.second += '"';
+                    h.second += e.str;
+                    h.second += '"';
+                }
+            };
+            auto done = [](const Path& path) { std::fprintf(stderr, "%s: %s\n", path.first.c_str(), path.second.c_str()); };
+            auto rec = make_recognizer<Path>(fsa, acc, done);
+            for (const auto& word : corpus) rec.Recognize(word.first.c_str(), Path("", fsa.GetStartState()), recognize == 0);
+        }
         learner.BuildFrom(fsa, corpus);
+        if (print || (!matrices.empty() && matrices.front() == '>'))   // P / M for -p and for saving
+            learner.EnumeratePaths(fsa, corpus, recognize == 0);
         std::cerr << "Recognize:\n\tstrings: " << learner.GetNumberOfStrings()
                   << "\n\tpaths: " << learner.GetNumberOfPaths()
                   << "\n\tcommon support: " << learner.GetCommonSupport()
@@ -156,6 +174,14 @@ int main(int argc, const char* argv[]) {
             return 1;
         }
         learner.Finalize();
+        if (print) {   // src/main.cpp:231-239
+            std::fputs("C:\n", stderr);
+            learner.PrintC(stderr);
+            std::fputs("M:\n", stderr);
+            learner.PrintM(stderr);
+            std::fputs("P:\n", stderr);
+            learner.PrintP(stderr);
+        }
         if (!matrices.empty() && matrices.front() == '>') {   // src/main.cpp:241-249
             std::cerr << "Saving matrices \"" << matrices.substr(1) << "\" ... ";
             std::cerr << (learner.SaveMatrices(matrices.substr(1)) ? "Done" : "Failed!") << std::endl;
@@ -177,7 +203,7 @@ int main(int argc, const char* argv[]) {
         if (epochs > 0) std::cerr << "Optimization:" << std::endl;
         for (int e = 1; e <= epochs; ++e) {
             if (e % 20 == 1) std::cerr << "epoch\t" << learner.GetOptimizationHeader() << std::endl;
-            learner.OptimizationStep(eta, false);
+            learner.OptimizationStep(eta, print);
             std::fprintf(stderr, "%0*d\t", width, e);
             const auto info = learner.GetOptimizationInfo();
             for (double x : info) {
@@ -191,7 +217,7 @@ int main(int argc, const char* argv[]) {
         }
         if (normalize) learner.Renormalize();
         if (evaluate) {
-            const auto results = learner.GetOptimizationResult(false);
+            const auto results = learner.GetOptimizationResult(print);
             std::cerr.precision(15);   // DBL_DIG
             std::cerr << "Result:";
             for (double x : results) std::cerr << ' ' << x;

@@ -1,5 +1,6 @@
 #include "text.hpp"
 
+#include <algorithm>
 #include <limits>
 
 namespace wfsa {
@@ -71,6 +72,39 @@ double mxlogx(double x) {
     if (x > 0) return -x * std::log(x);
     if (x == 0) return 0.0;
     return std::numeric_limits<double>::infinity();
+}
+
+void print_fixed_width(FILE* out, double x, int width) {
+    const int mag = (x == 0) ? 0 : int(std::floor(std::log10(std::abs(x))));
+    if (mag <= width - 2 && mag >= 0) {
+        if (std::floor(x) == x) std::fprintf(out, "%*.0f", width, x);
+        else std::fprintf(out, "%*.*f", width, std::max(0, width - 3 - mag), x);
+    } else if (-4 < mag && mag < 0) {
+        std::fprintf(out, "%*.*f", width, width - 3, x);
+    } else {
+        std::fprintf(out, "%*.*e", width, width - 7, x);
+    }
+}
+
+void print_csr(FILE* out, const double* data, const std::vector<int32_t>& rows, const std::vector<int32_t>& cols,
+               const std::vector<double>* rhs) {
+    if (rows.empty()) return;
+    const int64_t width = int64_t(rows.size()) - 1;
+    for (size_t r = 0; r + 1 < rows.size(); ++r) {
+        int64_t col = -1;   // the last column printed
+        for (int32_t q = rows[r]; q < rows[r + 1]; ++q) {
+            for (; col < int64_t(cols[size_t(q)]) - 1; ++col) std::fputs("        ", out);
+            col = cols[size_t(q)];
+            print_fixed_width(out, data ? data[q] : 1.0, 7);
+            std::fputs(" ", out);
+        }
+        if (rhs && rhs->size() > r) {
+            for (; col < width - 1; ++col) std::fputs("        ", out);
+            std::fputs("|", out);
+            print_fixed_width(out, (*rhs)[r], 7);
+        }
+        std::fputs("\n", out);
+    }
 }
 
 }  // namespace wfsa

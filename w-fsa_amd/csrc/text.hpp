@@ -68,4 +68,13 @@ bool read_content(FILE* input, std::vector<char>& content);
 double log_simplex_volume(size_t d);
 double mxlogx(double x);
 
+// PrintFixedWidth (src/Utils.cpp:82-97): the epoch table's and the matrix
+// printer's number format
+void print_fixed_width(FILE* out, double x, int width = 7);
+// PrintCsrMtx (src/Utils.cpp:157-182): one text row per matrix row, every
+// stored entry in its column (8 characters per column, blanks for the gaps),
+// optionally "|" and the row's right-hand side.  data == nullptr: all ones.
+void print_csr(FILE* out, const double* data, const std::vector<int32_t>& rows, const std::vector<int32_t>& cols,
+               const std::vector<double>* rhs = nullptr);
+
 }  // namespace wfsa
