@@ -275,6 +275,15 @@ struct wfsa_dev {
     DevBuf<unsigned> qn_halted;
     std::vector<int32_t> qn_full_of_h, qn_cptr_h;
     bool qn_fused = false;           // qn_step_kernel sums the members' bubble slots itself
+    // pipelined QN loop (qn_run, WFSA_PIPE=0 disables): the stream pass and
+    // the finish of step e on pipe_stream, beside the bubbles and QN update
+    // of the next steps on stream; weights double-buffered by step parity
+    bool use_pipe = true;
+    hipStream_t pipe_stream = nullptr;
+    hipEvent_t pq[kQnDepth] = {}, pf[kQnDepth] = {}, p_start = nullptr;
+    DevBuf<double> w_full2, ewp2;
+    double* w_cur = nullptr;         // the weights the evaluation kernels read (null: w_full / ewp)
+    double* ewp_cur = nullptr;
     double* qn_ring = nullptr;       // host-mapped [kQnDepth][kQnRow]
     double* qn_ring_dev = nullptr;
 
@@ -1314,7 +1323,7 @@ int enqueue_compiled(wfsa_dev* ctx, bool with_grad, bool want_logq, const unsign
         c.tables = tables;
         c.with_grad = with_grad ? 1 : 0;
         c.multi = ctx->n_multi > 0 ? 1 : 0;
-        c.w = ctx->w_full.ptr;
+        c.w = ctx->w_cur ? ctx->w_cur : ctx->w_full.ptr;
         c.grad = ctx->out.ptr + 1;
         c.gpart = ctx->gpart.ptr;
         c.n_comb = ctx->n_edges + ctx->n_end;
@@ -1373,8 +1382,8 @@ wfsa::BubbleArgs bubble_args(wfsa_dev* ctx, bool want_logq, const unsigned* halt
     b.big_eslot_ptr = ctx->big_eslot_ptr.ptr;
     b.big_eslot = ctx->big_eslot.ptr;
     b.contrib = ctx->contrib.ptr;
-    b.w = ctx->w_full.ptr;
-    b.ewp = ctx->ewp.ptr;
+    b.w = ctx->w_cur ? ctx->w_cur : ctx->w_full.ptr;
+    b.ewp = ctx->ewp_cur ? ctx->ewp_cur : ctx->ewp.ptr;
     b.ll_part = ll_part;
     b.logq = want_logq ? ctx->logq.ptr : nullptr;
     b.halted = halted;
@@ -1739,6 +1748,126 @@ int enqueue_qn_step(wfsa_dev* ctx, double eta, double tol, int64_t e, bool timed
     return WFSA_OK;
 }
 
+// The pipelined QN step e (qn_run when pipe_ok): the trivial words'
+// gradient is a constant, so the QN update needs only the bubbles; the
+// stream pass (the step's log-likelihood, for its info row) leaves the
+// update's critical path.
+//   stream:      bubbles(e) -> [finish(e-1) done] -> QN step(e) => pq[e]
+//   pipe_stream: [pq[e-1]] -> stream pass(e) -> [pq[e]] -> finish(e) => pf[e]
+// Step e reads the weights of parity e; QN step(e) writes parity e+1, which
+// stream pass(e-1) read -- done before finish(e-1), which QN step(e) waits
+// for (it also needs finish(e-1)'s halt decision).  ll partials and the QN
+// block partials alternate by parity; finish(e) reads both halves of step e
+// before QN step(e+2) / bubbles(e+2) rewrite them (they wait for finish(e+1)).
+bool pipe_ok(wfsa_dev* ctx) {
+    return ctx->use_pipe && ctx->pipe_stream && ctx->qn_fused && !ctx->comm && !ctx->dense && !ctx->mpath &&
+           !ctx->qn_rmin && ctx->n_groups > 0 && ctx->n_fall[0] + ctx->n_fall[1] + ctx->n_fall[2] == 0 &&
+           ctx->i_tables >= 1;
+}
+
+int enqueue_qn_step_piped(wfsa_dev* ctx, double eta, double tol, int64_t e, bool timed) {
+    hipStream_t M = ctx->stream, S = ctx->pipe_stream;
+    const int par = int(e & 1);
+    const int slot = int(e % kQnDepth), prev = int((e + kQnDepth - 1) % kQnDepth);
+    const int32_t np = ctx->n_params, k = std::max(ctx->qn_k, 1);
+    double* w_cur = par ? ctx->w_full2.ptr : ctx->w_full.ptr;
+    double* ewp_cur = par ? ctx->ewp2.ptr : ctx->ewp.ptr;
+    double* w_nxt = par ? ctx->w_full.ptr : ctx->w_full2.ptr;
+    double* ewp_nxt = par ? ctx->ewp.ptr : ctx->ewp2.ptr;
+    double* partial = ctx->qn_partial.ptr + size_t(par) * 4 * size_t(k);
+    ctx->ll_cur = ctx->ll_part.ptr + size_t(par) * ctx->ll_stride;
+    ctx->w_cur = w_cur;
+    ctx->ewp_cur = ewp_cur;
+    const unsigned* halted = ctx->qn_halted.ptr;
+    // stream: the bubbles of step e (ll partials after the stream kernel's blocks)
+    const int32_t wave_off = ctx->i_grid;
+    if (ctx->n_bubbles > 0)
+        if (int rc = enqueue_bubbles(ctx, false, halted, wave_off, M)) return rc;
+    if (e > 0) HIP_TRY(hipStreamWaitEvent(M, ctx->pf[prev], 0));
+    wfsa::QnArgs q{};
+    wfsa::QnFinish& f = q.fin;
+    q.out = ctx->out.ptr;
+    q.use_out = false;
+    q.fixed = ctx->fixed_grad.ptr;
+    q.contrib = ctx->n_bubbles > 0 ? ctx->contrib.ptr : nullptr;
+    q.grp_base = ctx->grp_base.ptr;
+    q.seg_ptr = ctx->seg_ptr.ptr;
+    q.chunk_ptr = ctx->chunk_ptr.ptr;
+    q.n_full = np;
+    q.n = ctx->qn_n;
+    q.k = ctx->qn_k;
+    q.full_of = ctx->qn_full_of.ptr;
+    q.trim = ctx->qn_trim.ptr;
+    q.cptr = ctx->qn_cptr.ptr;
+    q.x = ctx->qn_x.ptr;
+    q.lambda = ctx->qn_lambda.ptr;
+    q.expx = ctx->qn_expx.ptr;
+    q.grad = ctx->qn_grad.ptr;
+    q.w_full = w_nxt;
+    q.ewp = ewp_nxt;
+    q.partial = partial;
+    q.eta = eta;
+    q.exp_lambda = ctx->qn_exp_lambda;
+    q.halted = ctx->qn_halted.ptr;
+    f.out0 = ctx->out.ptr;
+    f.ll_part = ctx->ll_cur;
+    f.n_ll = ctx->i_grid + (ctx->n_bubbles > 0 ? ctx->b_waves : 0);
+    f.partial = partial;
+    f.n_blocks = k;
+    f.k = ctx->qn_k;
+    f.plogp = ctx->qn_plogp;
+    f.tol = tol;
+    f.ring_slot = slot;
+    f.halted = ctx->qn_halted.ptr;
+    f.halt_pending = ctx->qn_halted.ptr + 1;
+    f.seq = ctx->counters.ptr;
+    f.host_flag = ctx->flag_dev;
+    f.host_ring = ctx->qn_ring_dev;
+    HIP_TRY(wfsa::launch_qn_step(q, true, M));
+    HIP_TRY(hipEventRecord(ctx->pq[slot], M));
+    // pipe_stream: the stream pass of step e (weights of parity e, written by
+    // QN step e-1 or the set-up), then the finish once QN step e is done
+    HIP_TRY(hipStreamWaitEvent(S, e > 0 ? ctx->pq[prev] : ctx->p_start, 0));
+    if (timed) HIP_TRY(record(ctx, ctx->k0, slot, S));
+    {
+        wfsa::CompiledArgs c{};
+        c.m = model_view(ctx);
+        c.p = ctx->p.ptr;
+        c.stream = ctx->stream_w.ptr;
+        c.wide = ctx->wide;
+        c.g_base = ctx->g_base.ptr;
+        c.g_len = ctx->g_len.ptr;
+        c.l_str = ctx->l_str.ptr;
+        c.l_len = ctx->l_len.ptr;
+        c.wave_first = ctx->wave_first.ptr;
+        c.n_groups = ctx->n_groups;
+        c.n_params = np;
+        c.tables = ctx->i_tables;
+        c.with_grad = 0;
+        c.multi = ctx->n_multi > 0 ? 1 : 0;
+        c.w = w_cur;
+        c.grad = ctx->out.ptr + 1;
+        c.gpart = ctx->gpart.ptr;
+        c.n_comb = ctx->n_edges + ctx->n_end;
+        c.lw_out = ctx->lw.ptr;
+        c.ew_out = ctx->ew.ptr;
+        c.erec_out = ctx->erec.ptr;
+        c.out = ctx->out.ptr;
+        c.ll_part = ctx->ll_cur;
+        c.logq = nullptr;
+        c.halted = halted;
+        c.fin.active = 0;
+        c.bub_on = 0;
+        HIP_TRY(wfsa::launch_compiled(c, ctx->i_grid, ctx->i_block, ctx->i_lds, S));
+    }
+    if (timed) HIP_TRY(record(ctx, ctx->kc, slot, S));
+    HIP_TRY(hipStreamWaitEvent(S, ctx->pq[slot], 0));
+    HIP_TRY(wfsa::launch_qn_finish(f, S));
+    if (timed) HIP_TRY(record(ctx, ctx->k2, slot, S));
+    HIP_TRY(hipEventRecord(ctx->pf[slot], S));
+    return WFSA_OK;
+}
+
 // the pending finish of the last enqueued QN step as its own launch
 int flush_qn_finish(wfsa_dev* ctx) {
     if (!ctx->fin_pending) return WFSA_OK;
@@ -1855,6 +1984,13 @@ int wfsa_dev_create(int device, wfsa_dev** out) {
     if (const char* e = std::getenv("WFSA_WIDE2_TIERS")) ctx->w2_all = std::strcmp(e, "2") != 0;
 
     HIP_TRY(hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking));
+    if (const char* e = std::getenv("WFSA_PIPE")) ctx->use_pipe = e[0] != '0';
+    HIP_TRY(hipStreamCreateWithFlags(&ctx->pipe_stream, hipStreamNonBlocking));
+    HIP_TRY(hipEventCreateWithFlags(&ctx->p_start, hipEventDisableTiming));
+    for (int i = 0; i < kQnDepth; ++i) {
+        HIP_TRY(hipEventCreateWithFlags(&ctx->pq[i], hipEventDisableTiming));
+        HIP_TRY(hipEventCreateWithFlags(&ctx->pf[i], hipEventDisableTiming));
+    }
     // measured: the cross-stream fork/join costs more idle time (5-20 us)
     // than the overlap saves, so the side stream is opt-in
     if (const char* e = std::getenv("WFSA_SIDE_STREAM"); e && e[0] == '1') {
@@ -1895,6 +2031,14 @@ void wfsa_dev_destroy(wfsa_dev* ctx) {
     for (hipEvent_t ev : {ctx->fork, ctx->join})
         if (ev) (void)hipEventDestroy(ev);
     if (ctx->side_stream) (void)hipStreamDestroy(ctx->side_stream);
+    if (ctx->pipe_stream) {
+        (void)hipStreamSynchronize(ctx->pipe_stream);
+        (void)hipStreamDestroy(ctx->pipe_stream);
+    }
+    for (int i = 0; i < kQnDepth; ++i)
+        for (hipEvent_t ev : {ctx->pq[i], ctx->pf[i]})
+            if (ev) (void)hipEventDestroy(ev);
+    if (ctx->p_start) (void)hipEventDestroy(ctx->p_start);
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
     delete ctx;
 }
@@ -2282,7 +2426,7 @@ int wfsa_dev_qn_setup(wfsa_dev* ctx, const wfsa_qn_desc* d) {
     HIP_TRY(ctx->qn_cptr.upload(cptr.data(), cptr.size(), s));
     for (DevBuf<double>* b : {&ctx->qn_x, &ctx->qn_expx, &ctx->qn_grad}) HIP_TRY(b->alloc(size_t(std::max(n, 1))));
     HIP_TRY(ctx->qn_lambda.alloc(size_t(std::max(k, 1))));
-    HIP_TRY(ctx->qn_partial.alloc(size_t(std::max(k, 1)) * 4));
+    HIP_TRY(ctx->qn_partial.alloc(size_t(std::max(k, 1)) * 8));   // two halves: the pipelined loop
     HIP_TRY(ctx->qn_halted.alloc(2));   // halted, halt_pending
     if (!ctx->qn_ring) {
         HIP_TRY(hipHostMalloc(reinterpret_cast<void**>(&ctx->qn_ring), sizeof(double) * kQnDepth * wfsa::kQnRow,
@@ -2369,6 +2513,16 @@ int wfsa_dev_qn_run(wfsa_dev* ctx, double eta, double tol, int32_t max_steps, do
     HIP_TRY(hipMemsetAsync(ctx->qn_halted.ptr, 0, 2 * sizeof(unsigned), s));
     ctx->fin_pending = false;
     ctx->fin_for_fbs.active = 0;
+    const bool piped = pipe_ok(ctx);
+    if (piped) {   // the second weight buffer; the pipe stream starts after everything enqueued so far
+        HIP_TRY(ctx->w_full2.alloc(size_t(ctx->n_params) + 2));
+        HIP_TRY(ctx->ewp2.alloc(size_t(ctx->n_params) + 2));
+        HIP_TRY(hipMemcpyAsync(ctx->w_full2.ptr, ctx->w_full.ptr, (size_t(ctx->n_params) + 2) * sizeof(double),
+                               hipMemcpyDeviceToDevice, s));   // (the zero slot, for every parity)
+        HIP_TRY(hipMemcpyAsync(ctx->ewp2.ptr, ctx->ewp.ptr, (size_t(ctx->n_params) + 2) * sizeof(double),
+                               hipMemcpyDeviceToDevice, s));
+        HIP_TRY(hipEventRecord(ctx->p_start, s));
+    }
     const unsigned base = ctx->seq;
     int32_t enq = 0, done = 0, st = 0;
     bool stop = false;
@@ -2376,7 +2530,9 @@ int wfsa_dev_qn_run(wfsa_dev* ctx, double eta, double tol, int32_t max_steps, do
     int64_t timed = 0;
     while (done < max_steps) {
         while (!stop && enq < max_steps && enq - done < kQnDepth) {
-            if (int rc = enqueue_qn_step(ctx, eta, tol, enq, enq % kTimingStride == 0)) return rc;
+            if (int rc = piped ? enqueue_qn_step_piped(ctx, eta, tol, enq, enq % kTimingStride == 0)
+                               : enqueue_qn_step(ctx, eta, tol, enq, enq % kTimingStride == 0))
+                return rc;
             ++enq;
             ++ctx->seq;
         }
@@ -2413,6 +2569,13 @@ int wfsa_dev_qn_run(wfsa_dev* ctx, double eta, double tol, int32_t max_steps, do
     if (int rc = flush_qn_finish(ctx)) return rc;
     if (enq > done)
         if (int rc = wait_published(ctx, base + unsigned(enq))) return rc;
+    if (piped) {   // both streams drained; the weights of the final x back in the parity-0 buffers
+        HIP_TRY(hipStreamSynchronize(ctx->pipe_stream));
+        HIP_TRY(hipStreamSynchronize(s));
+        ctx->w_cur = ctx->ewp_cur = nullptr;
+        HIP_TRY(wfsa::launch_qn_weights(ctx->qn_x.ptr, ctx->qn_trim.ptr, ctx->n_params, ctx->w_full.ptr,
+                                        ctx->ewp.ptr, s));
+    }
     HIP_TRY(hipStreamSynchronize(s));
     ctx->stats.fb_launches += timed;
     ctx->stats.fb_kernel_ms += fb_ms_sum;
