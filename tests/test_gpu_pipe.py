@@ -14,7 +14,7 @@ pytestmark = pytest.mark.gpu
 
 def _learner(monkeypatch, pipe, syn, halt_tol=-1.0, steps=12):
     import wfsa_amd as W
-    monkeypatch.setenv("WFSA_PIPE", "1" if pipe else "0")
+    monkeypatch.setenv("WFSA_PIPE", "1" if pipe else "0")   # (opt-in path vs the default)
     sym, off, wt = syn.corpus()
     fsa = W.Fsa.read_text(syn.wfsa_text)
     lrn = W.QuasiNewtonLearner(0)

@@ -1510,7 +1510,7 @@ __global__ __launch_bounds__(1024, (DBG == 10 ? 8 : 1)) void fbs_kernel(Compiled
 #pragma unroll
         for (int d = 0; d < D; ++d) r[d] = st[int64_t(kWave) * min(c0 + d, last)];
     };
-    constexpr bool kStreams = DBG != 3 && DBG != 4;   // (timing experiments)
+    const bool kStreams = DBG != 3 && DBG != 4 && !a.no_streams;   // (timing experiments; bubbles-only launches)
     if (kStreams) load(A, 0);
     // the previous QN step's finish: reduced here (its loads beside the
     // prefetch), published by thread 0 after the staging barrier (the
@@ -1522,7 +1522,7 @@ __global__ __launch_bounds__(1024, (DBG == 10 ? 8 : 1)) void fbs_kernel(Compiled
         __shared__ double fred[kMaxBlockWaves];
         qn_finish_compute(a.fin, fred, finfo, fstat);
     }
-    if (W_LDS && DBG != 4) {
+    if (W_LDS && DBG != 4 && !a.no_streams) {
         // stage w[0, n_params] in 16-byte pieces, all of a thread's loads
         // issued before its first store (loads and stores unconditional --
         // an index past the end is clamped to the last piece, which is then
@@ -1657,7 +1657,7 @@ __global__ __launch_bounds__(1024, (DBG == 10 ? 8 : 1)) void fbs_kernel(Compiled
     }
     // this block's slice of the per-edge weights and the zeroed result, for
     // the kernels after this one (nothing in this launch reads them)
-    if (W_LDS) edge_weight_slice(a, bid, nblk);
+    if (W_LDS && !a.no_streams) edge_weight_slice(a, bid, nblk);
 }
 
 // Group headers (stream_hdr_words), written after the streams are emitted:

@@ -439,6 +439,8 @@ struct CompiledArgs {
                              // else: >= 1 w staged in LDS, 0 global
     int32_t wide;
     int32_t with_grad;       // accumulate the (weight-independent) trivial-word gradient
+    int32_t no_streams;      // bubbles only (the pipelined QN loop's update chain): no table
+                             // staging, no stream pass, no per-edge weight slice
     // bub_on: the stream waves also evaluate the bubbles before their
     // streams (no separate bubble kernel) -- the small ones one per lane from
     // the first waves, the big ones one per wavefront from the last

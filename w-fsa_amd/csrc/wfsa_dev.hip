@@ -275,10 +275,15 @@ struct wfsa_dev {
     DevBuf<unsigned> qn_halted;
     std::vector<int32_t> qn_full_of_h, qn_cptr_h;
     bool qn_fused = false;           // qn_step_kernel sums the members' bubble slots itself
-    // pipelined QN loop (qn_run, WFSA_PIPE=0 disables): the stream pass and
+    // pipelined QN loop (qn_run, opt-in: WFSA_PIPE=1): the stream pass and
     // the finish of step e on pipe_stream, beside the bubbles and QN update
-    // of the next steps on stream; weights double-buffered by step parity
-    bool use_pipe = true;
+    // of the next steps on stream; weights double-buffered by step parity.
+    // Measured slower at c3 (56 -> 79 us per step under rocprof, 45 -> 66
+    // us without): the concurrent kernels slow each other (QN step 10 ->
+    // 26 us beside the stream pass) and every cross-stream wait adds ~10 us
+    // of idle (profiles/r02/v9_pipe_timeline.txt)
+    bool use_pipe = false;
+    bool pipe_fbs_bubbles = true;    // the update chain's bubbles as the stream kernel's bubble waves
     hipStream_t pipe_stream = nullptr;
     hipEvent_t pq[kQnDepth] = {}, pf[kQnDepth] = {}, p_start = nullptr;
     DevBuf<double> w_full2, ewp2;
@@ -1779,10 +1784,44 @@ int enqueue_qn_step_piped(wfsa_dev* ctx, double eta, double tol, int64_t e, bool
     ctx->w_cur = w_cur;
     ctx->ewp_cur = ewp_cur;
     const unsigned* halted = ctx->qn_halted.ptr;
-    // stream: the bubbles of step e (ll partials after the stream kernel's blocks)
+    // stream: the bubbles of step e -- the stream kernel's fused bubble waves
+    // without its stream pass (ll partials in the second run of i_grid
+    // slots), or the lane-per-bubble kernel (after the block partials)
+    const bool bub_fused = bubbles_fused(ctx, false) && ctx->pipe_fbs_bubbles;
     const int32_t wave_off = ctx->i_grid;
-    if (ctx->n_bubbles > 0)
+    if (ctx->n_bubbles > 0 && bub_fused) {
+        wfsa::CompiledArgs c{};
+        c.m = model_view(ctx);
+        c.p = ctx->p.ptr;
+        c.stream = ctx->stream_w.ptr;
+        c.wide = ctx->wide;
+        c.g_base = ctx->g_base.ptr;
+        c.g_len = ctx->g_len.ptr;
+        c.l_str = ctx->l_str.ptr;
+        c.l_len = ctx->l_len.ptr;
+        c.wave_first = ctx->wave_first.ptr;
+        c.n_groups = ctx->n_groups;
+        c.n_params = ctx->n_params;
+        c.tables = ctx->i_tables;
+        c.multi = ctx->n_multi > 0 ? 1 : 0;
+        c.w = w_cur;
+        c.out = ctx->out.ptr;
+        c.ll_part = ctx->ll_cur + ctx->i_grid;
+        c.halted = halted;
+        c.no_streams = 1;
+        c.bub = bubble_args(ctx, false, halted, nullptr);
+        c.bub_on = 1;
+        c.bub.small_wpb = small_waves_per_block(ctx->n_small4 + ctx->n_small, ctx->i_grid);
+        size_t lds = ctx->i_lds;
+        if (ctx->n_big > 0) {
+            c.bub.big_lds_edges = ctx->big_lds_edges;
+            c.bub.big_lds_off = int32_t(big_stage_off(ctx));
+            lds = big_stage_off(ctx) + size_t(ctx->i_block / kWave) * size_t(wfsa::big_stage_bytes(ctx->big_lds_edges));
+        }
+        HIP_TRY(wfsa::launch_compiled(c, ctx->i_grid, ctx->i_block, lds, M));
+    } else if (ctx->n_bubbles > 0) {
         if (int rc = enqueue_bubbles(ctx, false, halted, wave_off, M)) return rc;
+    }
     if (e > 0) HIP_TRY(hipStreamWaitEvent(M, ctx->pf[prev], 0));
     wfsa::QnArgs q{};
     wfsa::QnFinish& f = q.fin;
@@ -1811,7 +1850,7 @@ int enqueue_qn_step_piped(wfsa_dev* ctx, double eta, double tol, int64_t e, bool
     q.halted = ctx->qn_halted.ptr;
     f.out0 = ctx->out.ptr;
     f.ll_part = ctx->ll_cur;
-    f.n_ll = ctx->i_grid + (ctx->n_bubbles > 0 ? ctx->b_waves : 0);
+    f.n_ll = ctx->i_grid + (ctx->n_bubbles == 0 ? 0 : bub_fused ? ctx->i_grid : ctx->b_waves);
     f.partial = partial;
     f.n_blocks = k;
     f.k = ctx->qn_k;
@@ -1984,7 +2023,8 @@ int wfsa_dev_create(int device, wfsa_dev** out) {
     if (const char* e = std::getenv("WFSA_WIDE2_TIERS")) ctx->w2_all = std::strcmp(e, "2") != 0;
 
     HIP_TRY(hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking));
-    if (const char* e = std::getenv("WFSA_PIPE")) ctx->use_pipe = e[0] != '0';
+    if (const char* e = std::getenv("WFSA_PIPE")) ctx->use_pipe = e[0] == '1';
+    if (const char* e = std::getenv("WFSA_PIPE_BUB")) ctx->pipe_fbs_bubbles = e[0] != '0';
     HIP_TRY(hipStreamCreateWithFlags(&ctx->pipe_stream, hipStreamNonBlocking));
     HIP_TRY(hipEventCreateWithFlags(&ctx->p_start, hipEventDisableTiming));
     for (int i = 0; i < kQnDepth; ++i) {
