@@ -130,23 +130,111 @@ HCASES = [("talk", "talk"), ("test3", "test"), ("test4", "test"), ("test.list", 
           ("test.loop", "test"), ("test5", "test5"), ("test5_2", "test5")]
 
 
-def test_hessian_learner_fails_loudly_beyond_bubbles():
+def _fd_check(dev, nf, used, seed=1):
+    pairs = dev.hf_setup()
+    w = np.random.default_rng(seed).normal(-1.0, 0.3, size=nf)
+    cov = dev.hf_eval(w)
+    assert len(pairs) > 0
+    h = 1e-5
+    jac = np.zeros((nf, nf))
+    for k in range(nf):
+        if not used[k]:
+            continue
+        wp, wm = w.copy(), w.copy()
+        wp[k] += h
+        wm[k] -= h
+        jac[:, k] = -(dev.objective_grad(wp, want_logq=False)[1] - dev.objective_grad(wm, want_logq=False)[1]) / (2 * h)
+    dense = np.zeros((nf, nf))
+    for (j, k), v in zip(pairs, cov):
+        dense[j, k] = v
+        dense[k, j] = v
+    scale = np.abs(jac).max()
+    np.testing.assert_allclose(dense, jac, rtol=0, atol=1e-7 * scale)
+
+
+TRAV_FAMILIES = [
+    dict(n_states=12, degree=3, vocab=3, emissions=2, n_strings=150, max_len=24, seed=3),
+    dict(n_states=16, degree=3, vocab=4, emissions=2, n_strings=100, max_len=12, seed=3),
+]
+
+
+@pytest.mark.parametrize("family", TRAV_FAMILIES)
+def test_count_covariance_on_traversal_strings(family):
     """strings whose ambiguity region no compiled bubble (<= 32 nodes) holds
-    run on the traversal tiers, where no second-order term exists: the
-    learner says so (WFSA_ERR_CAPACITY) instead of dropping their H_f"""
+    run on the traversal tiers; their second-order terms come from
+    hf_trav_kernel (E[c c^T] = D + A + A^T over the string's trellis, on its
+    equivocal parameters).  The whole recognized corpus, bubbles and
+    traversal strings together, against central differences of the gradient."""
     import wfsa_amd as W
-    syn = W.Synthetic(n_states=12, degree=3, vocab=3, emissions=2, n_strings=150, max_len=24, seed=3)
+    syn = W.Synthetic(**family)
     sym, off, wt = syn.corpus()
+    fsa = W.Fsa.read_text(syn.wfsa_text)
+    nf = len(fsa.param_names())
     dev = W.Device(0)
-    dev.load_model(W.Fsa.read_text(syn.wfsa_text))
+    dev.load_model(fsa)
     dev.load_corpus(sym, off, wt / wt.sum())
-    dev.recognize()
-    assert (dev.string_tiers() >= 0).any()
+    rec, _, _ = dev.recognize()
+    keep = np.flatnonzero(rec == 1)
+    strings = [bytes(sym[off[i]:off[i + 1]]) for i in keep]
+    sym2 = np.frombuffer(b"".join(strings), dtype=np.uint8).copy()
+    off2 = np.concatenate([[0], np.cumsum([len(x) for x in strings])]).astype(np.int64)
+    dev.load_corpus(sym2, off2, wt[keep] / wt.sum())
+    rec, pc, used = dev.recognize()
+    assert rec.all()
+    assert (dev.string_tiers() >= 0).sum() >= 5, np.bincount(dev.string_tiers() + 1)
+    _fd_check(dev, nf, used)
+
+
+def _trav_learner(fam):
+    import wfsa_amd as W
+    syn = W.Synthetic(**fam)
+    sym, off, wt = syn.corpus()
     lrn = W.HessianLearner(0)
     lrn.BuildFromPacked(W.Fsa.read_text(syn.wfsa_text), sym, off, wt)
     lrn.Finalize()
-    with pytest.raises(W.WfsaError, match="traversal tiers"):
+    return syn, (sym, off, wt), lrn
+
+
+def test_hessian_learner_on_traversal_strings_matches_restatement():
+    """HessianLearner epochs on a corpus with 16 traversal-tier strings (the
+    rest in bubbles), against oracle/hessian.py on the oracle's enumerated
+    paths (<= 144 per string)"""
+    from oracle import Oracle
+    from oracle.hessian import HessianOracle
+    fam = dict(n_states=16, degree=2, vocab=4, emissions=2, n_strings=200, max_len=16, seed=4)
+    syn, (sym, off, wt), lrn = _trav_learner(fam)
+    h = HessianOracle(Oracle.from_arrays(syn.wfsa_text, sym, off, wt, max_paths=3_000_000))
+    want = np.array(h.run(flags=31, epochs=20, tol=1e-6))
+    got = np.array(lrn.run(flags=31, epochs=20, tol=1e-6))
+    assert lrn.stats()["fallback_strings"] > 0
+    assert got.shape[0] == want.shape[0]
+    np.testing.assert_allclose(got[:, 0], want[:, 0], rtol=1e-10, atol=1e-13)
+    np.testing.assert_allclose(got[:, 1:4], want[:, 1:4], rtol=1e-6, atol=1e-10)
+    np.testing.assert_array_equal(got[:, 4:6], want[:, 4:6])
+    names = {n: i for i, n in enumerate(h.o.param_names())}
+    order = [names[n] for n in lrn.param_names()]
+    np.testing.assert_allclose(lrn.x(), h.x[order], rtol=0, atol=1e-8)
+
+
+def test_hessian_learner_degenerate_step_like_restatement():
+    """a family whose Newton step goes non-finite: both sides stop with
+    "Unable to continue!" (HaltCondition, src/HessianLearner.cpp:374-379)
+    after the same epochs; the factorisation of the NaN system stays in
+    bounds (a fresh learner runs after it)"""
+    import wfsa_amd as W
+    from oracle import Oracle
+    from oracle.hessian import HessianOracle
+    from oracle.oracle import OracleError
+    fam = dict(n_states=16, degree=3, vocab=4, emissions=2, n_strings=100, max_len=12, seed=3)
+    syn, (sym, off, wt), lrn = _trav_learner(fam)
+    h = HessianOracle(Oracle.from_arrays(syn.wfsa_text, sym, off, wt, max_paths=3_000_000))
+    with pytest.raises(OracleError, match="Unable to continue"):
+        h.run(flags=31, epochs=20, tol=1e-6)
+    with pytest.raises(W.WfsaError, match="Unable to continue"):
         lrn.run(flags=31, epochs=20, tol=1e-6)
+    del lrn
+    _, _, lrn2 = _trav_learner(dict(fam, seed=4))
+    lrn2.Init(31)
 
 
 @pytest.mark.parametrize("case", HCASES, ids=lambda c: f"{c[0]}+{c[1]}")

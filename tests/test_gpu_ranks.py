@@ -171,20 +171,21 @@ def test_device_ranks_sum_to_the_whole():
     assert all(_run_ranks(2, bad))
 
 
-def _compiled_only(syn):
-    """the corpus cut to strings compiled into bubbles (second-order terms
-    exist for those only; see test_gpu_hessian.py)"""
+def _recognized(syn):
+    """the corpus cut to recognized strings (bubbles and traversal tiers
+    alike), and how many of them run on the traversal tiers"""
     import wfsa_amd as W
     sym, off, wt = syn.corpus()
     dev = W.Device(0)
     dev.load_model(W.Fsa.read_text(syn.wfsa_text))
     dev.load_corpus(sym, off, wt / wt.sum())
     rec, pc, _ = dev.recognize()
-    keep = np.flatnonzero((dev.string_tiers() == -1) & (rec == 1))
+    keep = np.flatnonzero(rec == 1)
     strings = [bytes(sym[off[i]:off[i + 1]]) for i in keep]
     sym2 = np.frombuffer(b"".join(strings), dtype=np.uint8).copy()
     off2 = np.concatenate([[0], np.cumsum([len(x) for x in strings])]).astype(np.int64)
-    return sym2, off2, wt[keep] / wt[keep].sum()
+    n_trav = int((dev.string_tiers()[keep] >= 0).sum())
+    return sym2, off2, wt[keep] / wt[keep].sum(), n_trav
 
 
 def test_rmin_column_across_ranks():
@@ -217,15 +218,17 @@ def test_rmin_column_across_ranks():
 
 def test_hessian_across_ranks():
     """HessianLearner with 2 and 3 ranks: the H_f pattern is the union of the
-    ranks' patterns, the values are all-reduced; device values and every
+    ranks' patterns (bubbles and traversal strings), the values are
+    all-reduced; device values and every
     epoch row (KL, residuals, inertia, lambda_min, rmin) equal one context"""
     import wfsa_amd as W
     syn = W.Synthetic(seed=3, n_states=20, degree=4, vocab=6, emissions=2, n_strings=300, max_len=12)
-    sym, off, p = _compiled_only(syn)
+    sym, off, p, n_trav = _recognized(syn)
+    assert n_trav > 0
     fsa = W.Fsa.read_text(syn.wfsa_text)
     w = np.random.default_rng(1).normal(-1.0, 0.3, size=len(fsa.param_names()))
     syn2 = W.Synthetic(seed=3, n_states=16, degree=3, vocab=8, emissions=1, n_strings=2000, max_len=16)
-    sym2, off2, p2 = _compiled_only(syn2)
+    sym2, off2, p2, _ = _recognized(syn2)
     fsa2 = W.Fsa.read_text(syn2.wfsa_text)
 
     def hf(nranks, rank, gid):

@@ -52,7 +52,9 @@ void DenseLdlt::Factor(std::vector<double>& A, int64_t n) {
                 colmax = std::abs(at(i, k));
                 imax = i;
             }
-        if (std::max(absakk, colmax) == 0.0 || absakk >= alpha * colmax) {
+        // (imax == k: no nonzero below the diagonal -- also a NaN column, where
+        // a 2x2 pivot could reach past the last row)
+        if (imax == k || std::max(absakk, colmax) == 0.0 || absakk >= alpha * colmax) {
             kp = k;
         } else {
             double rowmax = 0.0;

@@ -1016,6 +1016,8 @@ __global__ __launch_bounds__(256) void pair_weights_kernel(const int4* ent, int6
     }
 }
 
+__device__ __forceinline__ void wave_fence_hf() { __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup"); }
+
 // Hessian second-order term per bubble (fb_kernels.hpp HfArgs).  The
 // bubble's local node ids are in position order, so its edges (listed by
 // source position) are already topologically sorted.
@@ -1123,6 +1125,213 @@ __global__ __launch_bounds__(kHfBlock) void hf_kernel(HfArgs a) {
 }
 
 // pattern entry t = its slots' sum, in slot order (deterministic)
+// weight of combined edge g (exp of its parameters' sum)
+__device__ __forceinline__ double hf_edge_weight(const ModelView& m, const double* wt, int g) {
+    double t = 0.0;
+    for (int q = m.pptr[g]; q < m.pptr[g + 1]; ++q) t += wt[m.pidx[q]];
+    return exp(t);
+}
+
+// (local index, count) of edge g's parameters in V (ascending), at most 8
+__device__ __forceinline__ int hf_local(const ModelView& m, const int32_t* V, int nV, int g, int* kk, double* cc) {
+    int n = 0;
+    for (int q = m.pptr[g]; q < m.pptr[g + 1] && n < 8; ++q) {
+        const int j = m.pidx[q];
+        int lo = 0, hi = nV;
+        while (lo < hi) {
+            const int mid = (lo + hi) >> 1;
+            if (V[mid] < j) lo = mid + 1; else hi = mid;
+        }
+        if (lo < nV && V[lo] == j) {
+            int t = 0;
+            while (t < n && kk[t] != lo) ++t;
+            if (t == n) {
+                kk[n] = lo;
+                cc[n] = 0.0;
+                ++n;
+            }
+            cc[t] += 1.0;
+        }
+    }
+    return n;
+}
+
+// hf_trav_kernel (fb_kernels.hpp HfTravArgs): one wavefront per string;
+// lane l owns the V columns l, l + 64, ... (R of them) of G and the rows of A.
+template <int R>
+__device__ void hf_trav_string(const HfTravArgs& a, int li, int lane, double* Bt) {
+    const ModelView& m = a.m;
+    const WideModel& W = a.w;
+    const int N = m.n_nodes;
+    const int VM = a.vm;
+    double* Be = Bt + (int64_t(a.max_len) + 1) * N;                // [max_len + 1] their exponents
+    double* Ar = Be + (a.max_len + 1);                             // [2][N] scaled alpha rows
+    double* Gr = Ar + 2 * int64_t(N);                              // [2][N][VM] scaled G rows
+    double* Am = Gr + 2 * int64_t(N) * VM;                         // [VM][VM]
+    double* Dm = Am + int64_t(VM) * VM;                            // [VM][VM]
+    double* Mv = Dm + int64_t(VM) * VM;                            // [VM]
+    const int4 it = a.list[li];
+    const int sidx = it.x, nV = it.z;
+    const int32_t* V = a.vlist + it.y;
+    const int64_t o0 = a.off[sidx];
+    const int L = int(a.off[sidx + 1] - o0);
+    const uint8_t* str = a.sym + o0;
+    // backward: beta rows, each scaled to a power of two (exponent kept)
+    for (int S = lane; S < N; S += kWave) {
+        double b = 0.0;
+        for (int x = m.x_ptr[S]; x < m.x_ptr[S + 1]; ++x) b += hf_edge_weight(m, a.wt, m.n_edges + x);
+        Bt[int64_t(L) * N + S] = b;
+    }
+    wave_fence_hf();
+    auto rescale = [&](double* row, int n) -> int {
+        double mx = 0.0;
+        for (int S = lane; S < n; S += kWave) mx = fmax(mx, row[S]);
+        mx = wave_max(mx);
+        const int e = mx > 0.0 ? __builtin_amdgcn_frexp_exp(mx) : 0;
+        if (e != 0)
+            for (int S = lane; S < n; S += kWave) row[S] = ldexp(row[S], -e);
+        wave_fence_hf();
+        return e;
+    };
+    int eb = rescale(Bt + int64_t(L) * N, N);
+    if (lane == 0) Be[L] = double(eb);
+    for (int i = L - 1; i >= 0; --i) {
+        const int c = str[i];
+        const double* Bn = Bt + int64_t(i + 1) * N;
+        for (int S = lane; S < N; S += kWave) {
+            int lo, cnt;
+            edge_range(m, S, c, lo, cnt);
+            double b = 0.0;
+            for (int g = lo; g < lo + cnt; ++g) b += hf_edge_weight(m, a.wt, g) * Bn[m.o_dst[g]];
+            Bt[int64_t(i) * N + S] = b;
+        }
+        wave_fence_hf();
+        eb += rescale(Bt + int64_t(i) * N, N);
+        if (lane == 0) Be[i] = double(eb);
+    }
+    wave_fence_hf();
+    // Z = beta_0(start); true beta_i = Bt_i 2^Be[i]
+    const double zt = Bt[m.start];
+    const int ez = int(Be[0]);
+    if (!(zt > 0.0)) return;   // not recognized (the host lists recognized strings only)
+    // forward: alpha and G rows (both scaled by 2^-ea), A, D, m
+    for (int64_t j = lane; j < int64_t(VM) * VM; j += kWave) {
+        Am[j] = 0.0;
+        Dm[j] = 0.0;
+    }
+    for (int j = lane; j < VM; j += kWave) Mv[j] = 0.0;
+    for (int S = lane; S < N; S += kWave) Ar[S] = S == m.start ? 1.0 : 0.0;
+    for (int64_t q = lane; q < int64_t(N) * VM; q += kWave) Gr[q] = 0.0;
+    wave_fence_hf();
+    int ea = 0;
+    int kk[8];
+    double cc[8];
+    // one edge: alpha / G into its destination (an, gn), A rows and D, m
+    auto edge = [&](const double* Gi, int S, double as, int g, double coef, double* gn) {
+        const int n = hf_local(m, V, nV, g, kk, cc);
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            const int j = lane + r * kWave;
+            const double gs = Gi[int64_t(S) * VM + j];
+            double cl = 0.0;
+            for (int t = 0; t < n; ++t) {
+                cl += kk[t] == j ? cc[t] : 0.0;
+                if (j < nV) Am[int64_t(j) * VM + kk[t]] += coef * gs * cc[t];
+            }
+            if (gn) gn[r] += gs + as * cl;   // (times the edge weight by the caller)
+        }
+        if (lane == 0) {
+            const double pe = coef * as;
+            for (int t = 0; t < n; ++t) {
+                Mv[kk[t]] += pe * cc[t];
+                for (int u = 0; u < n; ++u) Dm[int64_t(kk[t]) * VM + kk[u]] += pe * cc[t] * cc[u];
+            }
+        }
+    };
+    for (int i = 0; i < L; ++i) {
+        const int c = str[i];
+        const double* Ai = Ar + int64_t(i & 1) * N;
+        double* An = Ar + int64_t((i + 1) & 1) * N;
+        const double* Gi = Gr + int64_t(i & 1) * N * VM;
+        double* Gn = Gr + int64_t((i + 1) & 1) * N * VM;
+        const double* Bn = Bt + int64_t(i + 1) * N;
+        // P(e) = a~ w b~ 2^(ea + Be[i+1] - ez) / z~
+        const double f = ldexp(1.0, ea + int(Be[i + 1]) - ez) / zt;
+        for (int S = lane; S < N; S += kWave) An[S] = 0.0;
+        for (int64_t q = lane; q < int64_t(N) * VM; q += kWave) Gn[q] = 0.0;
+        wave_fence_hf();
+        for (int k = W.c_ptr[c]; k < W.c_ptr[c + 1]; ++k) {   // destinations of byte c, in order
+            const int T = W.dst[k];
+            double an = 0.0, gn[R];
+#pragma unroll
+            for (int r = 0; r < R; ++r) gn[r] = 0.0;
+            const double bT = Bn[T];
+            for (int e = W.e_ptr[k]; e < W.e_ptr[k + 1]; ++e) {
+                const int S = W.e_src[e], g = W.e_g[e];
+                const double as = Ai[S];
+                if (!(as > 0.0)) continue;
+                const double we = hf_edge_weight(m, a.wt, g);
+                double ge[R];
+#pragma unroll
+                for (int r = 0; r < R; ++r) ge[r] = 0.0;
+                edge(Gi, S, as, g, we * bT * f, ge);
+                an += we * as;
+#pragma unroll
+                for (int r = 0; r < R; ++r) gn[r] += we * ge[r];
+            }
+            if (lane == 0) An[T] = an;
+#pragma unroll
+            for (int r = 0; r < R; ++r) Gn[int64_t(T) * VM + lane + r * kWave] = gn[r];
+        }
+        wave_fence_hf();
+        // rescale alpha and G together
+        double mx = 0.0;
+        for (int S = lane; S < N; S += kWave) mx = fmax(mx, An[S]);
+        mx = wave_max(mx);
+        const int e = mx > 0.0 ? __builtin_amdgcn_frexp_exp(mx) : 0;
+        if (e != 0) {
+            for (int S = lane; S < N; S += kWave) An[S] = ldexp(An[S], -e);
+            for (int64_t q = lane; q < int64_t(N) * VM; q += kWave) Gn[q] = ldexp(Gn[q], -e);
+        }
+        ea += e;
+        wave_fence_hf();
+    }
+    {   // end edges (beta = 1 past them)
+        const double* Ai = Ar + int64_t(L & 1) * N;
+        const double* Gi = Gr + int64_t(L & 1) * N * VM;
+        const double f = ldexp(1.0, ea - ez) / zt;
+        for (int S = 0; S < N; ++S) {
+            const double as = Ai[S];
+            if (!(as > 0.0)) continue;
+            for (int x = m.x_ptr[S]; x < m.x_ptr[S + 1]; ++x) {
+                const int g = m.n_edges + x;
+                edge(Gi, S, as, g, hf_edge_weight(m, a.wt, g) * f, nullptr);
+            }
+        }
+    }
+    wave_fence_hf();
+    // slots (a <= b, row-major): p_s Cov(a, b)
+    const double ps = a.p[sidx];
+    const int64_t base = a.slot_base[li];
+    for (int ra = lane; ra < nV; ra += kWave) {
+        int64_t q = base + int64_t(ra) * nV - int64_t(ra) * (ra - 1) / 2;   // sum_{r < ra} (nV - r)
+        for (int rb = ra; rb < nV; ++rb, ++q) {
+            const double e2 = Dm[int64_t(ra) * VM + rb] + Am[int64_t(ra) * VM + rb] + Am[int64_t(rb) * VM + ra];
+            a.slot_val[q] = ps * (e2 - Mv[ra] * Mv[rb]);
+        }
+    }
+    wave_fence_hf();
+}
+
+template <int R>
+__global__ __launch_bounds__(kHfBlock) void hf_trav_kernel(HfTravArgs a) {
+    const int lane = lane_id();
+    const int gw = int(blockIdx.x) * (kHfBlock / kWave) + int(threadIdx.x) / kWave;
+    const int nwv = int(gridDim.x) * (kHfBlock / kWave);
+    double* Bt = a.scratch + int64_t(gw) * a.stride;               // [(max_len + 1)][N] scaled beta rows
+    for (int li = gw; li < a.n_list; li += nwv) hf_trav_string<R>(a, li, lane, Bt);
+}
+
 __global__ __launch_bounds__(256) void hf_sum_kernel(HfArgs a) {
     const int64_t t = int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
     if (t >= a.n_pattern) return;
@@ -1989,10 +2198,20 @@ hipError_t launch_rmin(const RminArgs& a, hipStream_t stream, bool final) {
     return hipGetLastError();
 }
 
-hipError_t launch_hf(const HfArgs& a, hipStream_t stream) {
+hipError_t launch_hf(const HfArgs& a, hipStream_t stream, const HfTravArgs* trav, int trav_grid) {
     constexpr int NW = kHfBlock / kWave;
     if (a.n_bubbles > 0)
         hipLaunchKernelGGL(hf_kernel, dim3(unsigned((a.n_bubbles + NW - 1) / NW)), dim3(kHfBlock), 0, stream, a);
+    if (trav && trav->n_list > 0)
+    {
+        const dim3 g(static_cast<unsigned>(trav_grid)), b(kHfBlock);
+        switch (trav->vm / kWave) {
+        case 1: hipLaunchKernelGGL(hf_trav_kernel<1>, g, b, 0, stream, *trav); break;
+        case 2: hipLaunchKernelGGL(hf_trav_kernel<2>, g, b, 0, stream, *trav); break;
+        case 4: hipLaunchKernelGGL(hf_trav_kernel<4>, g, b, 0, stream, *trav); break;
+        default: hipLaunchKernelGGL(hf_trav_kernel<8>, g, b, 0, stream, *trav); break;
+        }
+    }
     if (a.n_pattern > 0)
         hipLaunchKernelGGL(hf_sum_kernel, dim3(unsigned((a.n_pattern + 255) / 256)), dim3(256), 0, stream, a);
     return hipGetLastError();

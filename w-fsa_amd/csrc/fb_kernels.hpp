@@ -298,7 +298,41 @@ struct HfArgs {
     double* out;               // [n_pattern]
 };
 constexpr int kHfBlock = 256;   // four bubbles per block
-hipError_t launch_hf(const HfArgs& a, hipStream_t stream);
+
+// H_f of the strings the traversal kernels carry (no bubble decomposition):
+// per string s, over its equivocal parameters V_s (the parameters whose count
+// differs between its paths, at most kHfTravMaxV; the host finds them at set-up
+// from exact min / max counts), the count covariance from one backward and one
+// forward pass: with G_i(u)[j] the path-weighted count of parameter j over the
+// paths into node u at position i (G rolls forward with alpha),
+//   E[c c^T] = D + A + A^T,  D = sum_e P(e) c(e) c(e)^T,
+//   A[j][k] = sum_e (w_e beta(dst) / Z) G(src)[j] c_k(e)   (pairs strictly before e),
+//   E[c] = sum_e P(e) c(e);   slot (a <= b) = p_s Cov(a, b).
+// One wavefront per string: lanes over nodes for the alpha / beta rows, lanes
+// over j for G and A; every sum in a fixed order (deterministic).
+constexpr int kHfTravMaxV = 512;   // (8 columns per lane)
+struct HfTravArgs {
+    ModelView m;
+    WideModel w;             // in-edges by byte
+    const uint8_t* sym;
+    const int64_t* off;
+    const double* p;
+    const int4* list;        // (string, offset of V_s, |V_s|, 0)
+    const int32_t* vlist;    // V_s, ascending Fsa parameter ids
+    const int64_t* slot_base;   // [n_list] first slot of the string
+    int32_t n_list;
+    int32_t max_len;
+    const double* wt;        // [n_params + 1] weights (GetWeight form)
+    double* scratch;         // per wave: hf_trav_stride doubles
+    int64_t stride;
+    int32_t vm;              // columns of G / A / D: max |V_s| rounded up to 64, <= kHfTravMaxV
+    double* slot_val;
+};
+inline int64_t hf_trav_stride(int32_t max_len, int32_t n_nodes, int32_t vm) {
+    return (int64_t(max_len) + 1) * (n_nodes + 1) + 4 * int64_t(n_nodes) + 2 * int64_t(n_nodes) * vm +
+           2 * int64_t(vm) * vm + vm + 16;
+}
+hipError_t launch_hf(const HfArgs& a, hipStream_t stream, const HfTravArgs* trav = nullptr, int trav_grid = 0);
 
 // Device-resident QuasiNewton step (qn_kernel.hip): qn_step_kernel, one
 // block per constraint, completes the gradient of the constraint's members

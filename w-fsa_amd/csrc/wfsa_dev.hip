@@ -27,6 +27,7 @@
 #include <cstdio>
 #include <cstring>
 #include <memory>
+#include <limits>
 #include <string>
 #include <vector>
 
@@ -251,6 +252,7 @@ struct wfsa_dev {
     bool rm_eval = false;        // the evaluation being enqueued also runs the traversal min forward
     std::unique_ptr<wfsa::MatrixPath> mpath;   // matrix-file mode (wfsa_dev_load_paths)
     std::unique_ptr<wfsa::SymSolver> ldlt;     // dense LDL^T of the HessianLearner's KKT system
+    std::unique_ptr<wfsa::TrellisModel> h_tm;  // host copy of the trellis model (H_f set-up)
 
     // the per-iteration device sequence, captured once per prepared corpus
     hipGraph_t graph = nullptr;
@@ -307,6 +309,15 @@ struct wfsa_dev {
     DevBuf<int64_t> hf_slot_base, hf_t_ptr, hf_t_slot;
     DevBuf<double> hf_slot_val, hf_out;
     int64_t hf_n_slots = 0;
+    // traversal strings: (string, V offset, |V|), their equivocal parameters, first slots, scratch
+    DevBuf<int4> hft_list;
+    DevBuf<int32_t> hft_v;
+    DevBuf<int64_t> hft_base;
+    DevBuf<double> hft_scratch;
+    int32_t hft_n = 0;
+    int hft_grid = 0;
+    int64_t hft_stride = 0;
+    int32_t hft_vm = 0;
 
     // communicator
     std::unique_ptr<wfsa::Collective> comm;
@@ -544,6 +555,115 @@ int build_pair_tables(wfsa_dev* ctx, const wfsa::TrellisModel& tm, const std::ve
     ctx->pt_ne = int64_t(ent.size());
     ctx->has_pairs = true;
     return WFSA_OK;
+}
+
+// The equivocal parameters of one string (HessianLearner::AssembleH's
+// per-string sets, src/HessianLearner.cpp:388-437): those whose count is not
+// the same on every accepting path, from exact min / max counts over the
+// string's trellis.  false: the string has more than cap_p parameters on its
+// paths (the per-node count vectors would not fit).
+bool equivocal_params(const wfsa::TrellisModel& tm, const std::vector<int32_t>& pptr,
+                      const std::vector<int32_t>& pidx, const uint8_t* str, int L, std::vector<int32_t>& V,
+                      size_t cap_p) {
+    const int32_t N = tm.n_nodes, E = int32_t(tm.o_byte.size());
+    V.clear();
+    std::vector<std::vector<int32_t>> live(size_t(L) + 1);   // co-reachable (accepting) nodes per position
+    {
+        std::vector<std::vector<char>> fw(size_t(L) + 1, std::vector<char>(size_t(N), 0));
+        fw[0][size_t(tm.start)] = 1;
+        for (int i = 0; i < L; ++i)
+            for (int32_t S = 0; S < N; ++S)
+                if (fw[size_t(i)][size_t(S)])
+                    for (int32_t g = tm.o_ptr[size_t(S)]; g < tm.o_ptr[size_t(S) + 1]; ++g)
+                        if (tm.o_byte[size_t(g)] == str[i]) fw[size_t(i) + 1][size_t(tm.o_dst[size_t(g)])] = 1;
+        std::vector<char> bw(size_t(N), 0), nb(size_t(N), 0);
+        for (int32_t S = 0; S < N; ++S)
+            if (fw[size_t(L)][size_t(S)] && tm.x_ptr[size_t(S) + 1] > tm.x_ptr[size_t(S)]) {
+                bw[size_t(S)] = 1;
+                live[size_t(L)].push_back(S);
+            }
+        for (int i = L - 1; i >= 0; --i) {
+            std::fill(nb.begin(), nb.end(), 0);
+            for (int32_t S = 0; S < N; ++S) {
+                if (!fw[size_t(i)][size_t(S)]) continue;
+                for (int32_t g = tm.o_ptr[size_t(S)]; g < tm.o_ptr[size_t(S) + 1]; ++g)
+                    if (tm.o_byte[size_t(g)] == str[i] && bw[size_t(tm.o_dst[size_t(g)])]) nb[size_t(S)] = 1;
+                if (nb[size_t(S)]) live[size_t(i)].push_back(S);
+            }
+            bw.swap(nb);
+        }
+    }
+    // the parameters on accepting edges
+    std::vector<int32_t> P;
+    auto add_params = [&](int32_t g) {
+        for (int32_t q = pptr[size_t(g)]; q < pptr[size_t(g) + 1]; ++q) P.push_back(pidx[size_t(q)]);
+    };
+    std::vector<char> on(size_t(N), 0);
+    for (int i = 0; i < L; ++i) {
+        for (int32_t T : live[size_t(i) + 1]) on[size_t(T)] = 1;
+        for (int32_t S : live[size_t(i)])
+            for (int32_t g = tm.o_ptr[size_t(S)]; g < tm.o_ptr[size_t(S) + 1]; ++g)
+                if (tm.o_byte[size_t(g)] == str[i] && on[size_t(tm.o_dst[size_t(g)])]) add_params(g);
+        for (int32_t T : live[size_t(i) + 1]) on[size_t(T)] = 0;
+    }
+    for (int32_t S : live[size_t(L)])
+        for (int32_t x = tm.x_ptr[size_t(S)]; x < tm.x_ptr[size_t(S) + 1]; ++x) add_params(E + x);
+    std::sort(P.begin(), P.end());
+    P.erase(std::unique(P.begin(), P.end()), P.end());
+    if (P.empty()) return true;
+    if (P.size() > cap_p) return false;
+    const size_t np = P.size();
+    auto local = [&](int32_t j) { return size_t(std::lower_bound(P.begin(), P.end(), j) - P.begin()); };
+    // min / max count of every parameter over the paths into each live node,
+    // rows indexed by the node's place in live[i]
+    const int32_t kInf = std::numeric_limits<int32_t>::max() / 4;
+    std::vector<int32_t> at(size_t(N), -1);
+    std::vector<int32_t> mn(np, 0), mx(np, 0), mn2, mx2;   // position 0: the start node alone
+    std::vector<int32_t> cnt(np, 0);
+    auto edge_counts = [&](int32_t g, int sign) {
+        for (int32_t q = pptr[size_t(g)]; q < pptr[size_t(g) + 1]; ++q) cnt[local(pidx[size_t(q)])] += sign;
+    };
+    if (live[0].size() != 1 || live[0][0] != tm.start) return true;   // not recognized
+    for (int i = 0; i < L; ++i) {
+        const auto& cur = live[size_t(i)];
+        const auto& nxt = live[size_t(i) + 1];
+        mn2.assign(nxt.size() * np, kInf);
+        mx2.assign(nxt.size() * np, -kInf);
+        for (size_t t = 0; t < nxt.size(); ++t) at[size_t(nxt[t])] = int32_t(t);
+        for (size_t si = 0; si < cur.size(); ++si) {
+            const int32_t S = cur[si];
+            for (int32_t g = tm.o_ptr[size_t(S)]; g < tm.o_ptr[size_t(S) + 1]; ++g) {
+                const int32_t T = tm.o_dst[size_t(g)];
+                if (tm.o_byte[size_t(g)] != str[i] || at[size_t(T)] < 0) continue;
+                const size_t ti = size_t(at[size_t(T)]);
+                edge_counts(g, 1);
+                for (size_t j = 0; j < np; ++j) {
+                    mn2[ti * np + j] = std::min(mn2[ti * np + j], mn[si * np + j] + cnt[j]);
+                    mx2[ti * np + j] = std::max(mx2[ti * np + j], mx[si * np + j] + cnt[j]);
+                }
+                edge_counts(g, -1);
+            }
+        }
+        for (int32_t T : nxt) at[size_t(T)] = -1;
+        mn.swap(mn2);
+        mx.swap(mx2);
+    }
+    std::vector<int32_t> fmn(np, kInf), fmx(np, -kInf);
+    const auto& last = live[size_t(L)];
+    for (size_t si = 0; si < last.size(); ++si) {
+        const int32_t S = last[si];
+        for (int32_t x = tm.x_ptr[size_t(S)]; x < tm.x_ptr[size_t(S) + 1]; ++x) {
+            edge_counts(E + x, 1);
+            for (size_t j = 0; j < np; ++j) {
+                fmn[j] = std::min(fmn[j], mn[si * np + j] + cnt[j]);
+                fmx[j] = std::max(fmx[j], mx[si * np + j] + cnt[j]);
+            }
+            edge_counts(E + x, -1);
+        }
+    }
+    for (size_t j = 0; j < np; ++j)
+        if (fmn[j] != fmx[j]) V.push_back(P[j]);
+    return true;
 }
 
 int configure_tiers(wfsa_dev* ctx) {
@@ -2181,6 +2301,7 @@ int wfsa_dev_load_model(wfsa_dev* ctx, const wfsa_model_desc* model) {
     ctx->start = tm.start;
     if (int rc = alloc_param_buffers(ctx)) return rc;
     HIP_TRY(hipStreamSynchronize(s));
+    ctx->h_tm = std::make_unique<wfsa::TrellisModel>(std::move(tm));
     ctx->has_model = true;
     ctx->stats.n_nodes = ctx->n_nodes;
     ctx->stats.n_edges = ctx->n_edges;
@@ -2642,20 +2763,49 @@ int wfsa_dev_hf_setup(wfsa_dev* ctx, int64_t* n_pairs) {
         if (int rc = prepare(ctx, 2)) return rc;
     hipStream_t s = ctx->stream;
     const int64_t nfall = int64_t(ctx->n_fall[0]) + ctx->n_fall[1] + ctx->n_fall[2];
+    // traversal strings: their equivocal parameters, found on the host from
+    // exact min / max counts over each string's trellis (hf_trav_kernel)
+    std::vector<int4> tl;
+    std::vector<int32_t> tv;
+    int64_t bad_string = -1;
+    size_t bad_v = 0;
+    if (nfall > 0) {
+        std::vector<int64_t> off(size_t(ctx->n_strings) + 1);
+        HIP_TRY(ctx->off.download(off.data(), off.size(), s));
+        HIP_TRY(hipStreamSynchronize(s));
+        std::vector<uint8_t> sy(static_cast<size_t>(off.back()));
+        HIP_TRY(ctx->sym.download(sy.data(), sy.size(), s));
+        HIP_TRY(hipStreamSynchronize(s));
+        std::vector<int32_t> V;
+        for (int64_t i = 0; i < ctx->n_strings && bad_string < 0; ++i) {
+            if (ctx->h_tier[size_t(i)] < 0) continue;
+            const int L = int(off[size_t(i) + 1] - off[size_t(i)]);
+            if (!equivocal_params(*ctx->h_tm, ctx->h_pptr, ctx->h_pidx, sy.data() + off[size_t(i)], L, V, 4096) ||
+                V.size() > size_t(wfsa::kHfTravMaxV)) {
+                bad_string = i;
+                bad_v = V.size();
+                break;
+            }
+            if (V.empty()) continue;
+            tl.push_back(make_int4(int32_t(i), int32_t(tv.size()), int32_t(V.size()), 0));
+            tv.insert(tv.end(), V.begin(), V.end());
+        }
+    }
+    const bool local_bad = bad_string >= 0;
     if (ctx->comm) {   // every rank learns whether any cannot build its part (no rank is left in a collective)
         DevBuf<double> t;
-        double bad = nfall > 0 ? 1.0 : 0.0;
+        double bad = local_bad ? 1.0 : 0.0;
         HIP_TRY(t.upload(&bad, 1, s));
         COMM_TRY(ctx, t.ptr, 1, wfsa::RedOp::SumF64, s);
         HIP_TRY(t.download(&bad, 1, s));
         HIP_TRY(hipStreamSynchronize(s));
-        if (bad > 0 && nfall == 0)
-            return fail(WFSA_ERR_CAPACITY, "second-order terms need every string compiled into bubbles; "
-                        "another rank has strings on the traversal tiers");
+        if (bad > 0 && !local_bad)
+            return fail(WFSA_ERR_CAPACITY, "second-order terms: another rank has a string beyond their limits");
     }
-    if (nfall > 0)
-        return fail(WFSA_ERR_CAPACITY, "second-order terms need every string compiled into bubbles; %lld strings "
-                    "are on the traversal tiers", (long long)nfall);
+    if (local_bad)
+        return fail(WFSA_ERR_CAPACITY, "second-order terms: string %lld has %s equivocal parameters (at most %d, "
+                    "from at most 4096 parameters on its paths)", (long long)bad_string,
+                    bad_v ? std::to_string(bad_v).c_str() : "too many", wfsa::kHfTravMaxV);
     const int32_t np = ctx->n_params, nb = ctx->n_bubbles;
     std::vector<int32_t> off(size_t(std::max(nb, 1)));
     std::vector<int32_t> buf(ctx->bub.n);
@@ -2694,6 +2844,14 @@ int wfsa_dev_hf_setup(wfsa_dev* ctx, int64_t* n_pairs) {
                     for (int32_t k : ep[size_t(f)])
                         if (j <= k) keys.push_back(int64_t(j) * np + k);
         base[size_t(b) + 1] = int64_t(keys.size());
+    }
+    // the traversal strings' slots follow the bubbles': (a <= b) over V_s, row-major
+    std::vector<int64_t> tbase;
+    for (const int4& t : tl) {
+        tbase.push_back(int64_t(keys.size()));
+        const int32_t* V = tv.data() + t.y;
+        for (int a2 = 0; a2 < t.z; ++a2)
+            for (int b2 = a2; b2 < t.z; ++b2) keys.push_back(int64_t(V[a2]) * np + V[b2]);
     }
     const int64_t ns = int64_t(keys.size());
     std::vector<int64_t> order(static_cast<size_t>(ns));
@@ -2763,6 +2921,23 @@ int wfsa_dev_hf_setup(wfsa_dev* ctx, int64_t* n_pairs) {
     HIP_TRY(ctx->hf_t_slot.upload(order.empty() ? base.data() : order.data(), std::max<size_t>(order.size(), 1), s));
     HIP_TRY(ctx->hf_slot_val.alloc(size_t(std::max<int64_t>(ns, 1))));
     HIP_TRY(ctx->hf_out.alloc(std::max<size_t>(ctx->hf_pairs.size() / 2, 1)));
+    ctx->hft_n = int32_t(tl.size());
+    if (!tl.empty()) {
+        HIP_TRY(ctx->hft_list.upload(tl.data(), tl.size(), s));
+        HIP_TRY(ctx->hft_v.upload(tv.data(), tv.size(), s));
+        HIP_TRY(ctx->hft_base.upload(tbase.data(), tbase.size(), s));
+        int32_t vm = kWave, nv_max = 0;
+        for (const int4& t : tl) nv_max = std::max(nv_max, t.z);
+        while (vm < nv_max) vm *= 2;   // 64, 128, 256, 512: the kernel's column tiers
+        ctx->hft_vm = vm;
+        ctx->hft_stride = wfsa::hf_trav_stride(ctx->max_len, ctx->n_nodes, vm);
+        const int64_t budget = (int64_t(2) << 30) / 8;   // 2 GiB of per-wave scratch
+        constexpr int wpb = wfsa::kHfBlock / kWave;
+        int64_t waves = std::min<int64_t>(int64_t(tl.size()), int64_t(ctx->n_cu) * 8);
+        waves = std::max<int64_t>(1, std::min<int64_t>(waves, budget / ctx->hft_stride));
+        ctx->hft_grid = int((waves + wpb - 1) / wpb);
+        HIP_TRY(ctx->hft_scratch.alloc(size_t(ctx->hft_grid) * wpb * size_t(ctx->hft_stride)));
+    }
     HIP_TRY(hipStreamSynchronize(s));
     ctx->hf_n_slots = ns;
     ctx->hf_ready = true;
@@ -2807,7 +2982,29 @@ int wfsa_dev_hf_eval(wfsa_dev* ctx, const double* w_full, double* values) {
     a.t_slot = ctx->hf_t_slot.ptr;
     a.n_pattern = int64_t(ctx->hf_pairs.size() / 2);
     a.out = ctx->hf_out.ptr;
-    HIP_TRY(wfsa::launch_hf(a, s));
+    wfsa::HfTravArgs t{};
+    if (ctx->hft_n > 0) {
+        t.m = a.m;
+        t.w.c_ptr = ctx->w_cptr.ptr;
+        t.w.dst = ctx->w_dst.ptr;
+        t.w.e_ptr = ctx->w_eptr.ptr;
+        t.w.e_src = ctx->w_esrc.ptr;
+        t.w.e_g = ctx->w_eg.ptr;
+        t.sym = ctx->sym.ptr;
+        t.off = ctx->off.ptr;
+        t.p = ctx->p.ptr;
+        t.list = ctx->hft_list.ptr;
+        t.vlist = ctx->hft_v.ptr;
+        t.slot_base = ctx->hft_base.ptr;
+        t.n_list = ctx->hft_n;
+        t.max_len = ctx->max_len;
+        t.wt = ctx->w_full.ptr;
+        t.scratch = ctx->hft_scratch.ptr;
+        t.stride = ctx->hft_stride;
+        t.vm = ctx->hft_vm;
+        t.slot_val = ctx->hf_slot_val.ptr;
+    }
+    HIP_TRY(wfsa::launch_hf(a, s, ctx->hft_n > 0 ? &t : nullptr, ctx->hft_grid));
     if (ctx->comm && a.n_pattern > 0) COMM_TRY(ctx, ctx->hf_out.ptr, size_t(a.n_pattern), wfsa::RedOp::SumF64, s);
     if (values && a.n_pattern > 0) HIP_TRY(ctx->hf_out.download(values, size_t(a.n_pattern), s));
     HIP_TRY(hipStreamSynchronize(s));
