@@ -220,8 +220,10 @@ int wfsa_dev_qn_run(wfsa_dev* ctx, double eta, double tol, int32_t max_steps, do
  * (ComputeHf, src/HessianLearner.cpp:498-547; pattern as AssembleH :381-446):
  *   hf_setup: builds the pattern -- the pairs (j, k), j <= k, of Fsa
  *             parameters whose counts vary together on some string -- after the
- *             corpus is compiled; fails (WFSA_ERR_CAPACITY) when a string is
- *             not compiled into bubbles (on any rank), on the dense path.  With a
+ *             corpus is compiled (bubbles per bubble, traversal-tier strings
+ *             per string over their equivocal parameters); fails
+ *             (WFSA_ERR_CAPACITY) when a string has more than 512 equivocal
+ *             parameters (on any rank), and on the dense path.  With a
  *             communicator the pattern is the union over the ranks and
  *             hf_eval's values are all-reduced.
  *   hf_pairs: the pattern, pairs[2 t], pairs[2 t + 1] (ascending).
