@@ -119,6 +119,16 @@ int wfsa_shard_range(const int64_t* off, int64_t n, int nranks, int rank, int64_
  * Fails (WFSA_ERR_MODEL) e.g. on epsilon cycles. */
 int wfsa_trellis_compile_stats(const wfsa_model_desc* model, int64_t out[4]);
 
+/* The HessianLearner's sparse LDL^T (SparseLdlt.hpp) on a symmetric matrix
+ * given as upper-triangle coordinates (i[t] <= j[t], duplicates add): the
+ * order (0 identity, 1 minimum degree), factor, and -- when b is given --
+ * x = A^-1 b.  out_i = {positive pivots, negative pivots, nnz(L), ordering
+ * within its work bound}; out_d = {log|det|, det sign, min pivot ratio}.
+ * WFSA_ERR_ARG on a zero or non-finite pivot (no pivoting: the learner falls
+ * back to the dense factorisation then). */
+int wfsa_sym_sparse_solve(int64_t n, int64_t nnz, const int32_t* i, const int32_t* j, const double* v, int order,
+                          const double* b, double* x, int64_t out_i[4], double out_d[3]);
+
 /* ---- synthetic corpora (bench / tests) ---------------------------------- */
 /* family: N states, out-degree D (+ end), E distinct symbols per state out of
  * V printable bytes, stop probability 1/32 per step, lengths capped at

@@ -237,24 +237,29 @@ def test_hessian_learner_degenerate_step_like_restatement():
     lrn2.Init(31)
 
 
+@pytest.mark.parametrize("kkt,flags", [("", 31), ("sparse", 31), ("sparse", 15)], ids=["dense", "sparse-md", "sparse-id"])
 @pytest.mark.parametrize("case", HCASES, ids=lambda c: f"{c[0]}+{c[1]}")
-def test_hessian_learner_epochs_match_restatement(case):
+def test_hessian_learner_epochs_match_restatement(case, kkt, flags, monkeypatch):
     """HessianLearner through the C ABI, epoch by epoch (KL, graderr, g_min,
     g_max, inertia +/-, lambda_min) and its Result vector, against the dense
     restatement oracle/hessian.py on the oracle's enumerated paths.  logdetH is
-    compared where the Hessian is well conditioned (talk's is singular)."""
+    compared where the Hessian is well conditioned (talk's is singular).  The
+    KKT system through the dense Bunch-Kaufman LDL^T and through the sparse
+    LDL^T (WFSA_KKT=sparse) in minimum-degree order (flag 16, the reference's
+    METIS) and in the identity order (the reference's MKL_DSS_MY_ORDER)."""
     import wfsa_amd as W
+    monkeypatch.setenv("WFSA_KKT", kkt)
     from oracle import Oracle
     from oracle.hessian import HessianOracle
     wpath, cpath = os.path.join(DATA, case[0] + ".wfsa"), os.path.join(DATA, case[1] + ".corpus")
     h = HessianOracle(Oracle.from_files(wpath, cpath))
-    want = np.array(h.run(flags=31, epochs=20, tol=1e-6))
+    want = np.array(h.run(flags=flags, epochs=20, tol=1e-6))
     h.renormalize()
     want_res = h.result()
     lrn = W.HessianLearner(0)
     lrn.BuildFrom(W.Fsa.read_file(wpath), W.Corpus.read_file(cpath))
     lrn.Finalize()
-    got = np.array(lrn.run(flags=31, epochs=20, tol=1e-6))
+    got = np.array(lrn.run(flags=flags, epochs=20, tol=1e-6))
     assert got.shape[0] == want.shape[0]
     # KL and residuals; the residuals shrink to ~1e-12, so an absolute floor
     np.testing.assert_allclose(got[:, 0], want[:, 0], rtol=1e-10, atol=1e-13)

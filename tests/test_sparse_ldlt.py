@@ -1,0 +1,100 @@
+"""The HessianLearner's sparse LDL^T (w-fsa_amd/csrc/SparseLdlt.cpp, MKL DSS's
+role in src/HessianLearner.cpp:28-57,100-113) through the host C ABI
+(wfsa_sym_sparse_solve): solution, inertia and log|det| against numpy on
+KKT-shaped systems like the learner's (H_g + H_f over the parameters, one
+J_g entry per parameter row, the zero constraint block), in both orders (the
+identity -- the reference's MKL_DSS_MY_ORDER -- and minimum degree for init
+flag 16).  Host only: no device."""
+import numpy as np
+import pytest
+
+import wfsa_amd as W
+
+
+def _kkt(n, k, seed, indefinite=False, pairs=3):
+    rng = np.random.default_rng(seed)
+    C = rng.integers(0, k, size=n)
+    C[:k] = np.arange(k)                      # every constraint has a parameter
+    ex = np.exp(rng.normal(-1.0, 0.5, size=n))
+    lam = rng.uniform(0.5, 2.0, size=k)
+    ent = {}
+
+    def add(a, b, v):
+        a, b = min(a, b), max(a, b)
+        ent[(a, b)] = ent.get((a, b), 0.0) + v
+
+    for i in range(n):
+        add(i, i, ex[i] * lam[C[i]])
+        add(i, n + C[i], ex[i])
+    # H_f: -cov over random groups of parameters (negative semidefinite blocks)
+    for _ in range(pairs * n // 4):
+        g = rng.choice(n, size=4, replace=False)
+        c = rng.normal(size=4) * 0.3
+        for a in range(4):
+            for b in range(a, 4):
+                add(g[a], g[b], -(c[a] * c[b]) * (3.0 if indefinite else 0.2))
+    i, j = np.array([e[0] for e in ent], dtype=np.int32), np.array([e[1] for e in ent], dtype=np.int32)
+    v = np.array(list(ent.values()))
+    N = n + k
+    A = np.zeros((N, N))
+    A[i, j] += v
+    A[j, i] += np.where(i != j, v, 0.0)
+    return i, j, v, A
+
+
+@pytest.mark.parametrize("order", [0, 1])
+@pytest.mark.parametrize("n,k,seed,indef", [(40, 6, 1, False), (300, 30, 2, False), (300, 30, 3, True),
+                                             (1500, 120, 4, True)])
+def test_kkt_solve_inertia_logdet(order, n, k, seed, indef):
+    i, j, v, A = _kkt(n, k, seed, indef)
+    b = np.random.default_rng(seed + 100).normal(size=n + k)
+    x, st = W.sym_sparse_solve(i, j, v, n + k, b, order=order)
+    want = np.linalg.solve(A, b)
+    np.testing.assert_allclose(x, want, rtol=1e-8, atol=1e-10 * np.abs(want).max())
+    ev = np.linalg.eigvalsh(A)
+    assert (st["positive"], st["negative"]) == (int((ev > 0).sum()), int((ev < 0).sum()))
+    sign, logdet = np.linalg.slogdet(A)
+    assert st["det_sign"] == int(sign)
+    assert abs(st["log_abs_det"] - logdet) <= 1e-9 * max(1.0, abs(logdet))
+    assert st["ordered"]
+
+
+def test_minimum_degree_avoids_arrow_fill():
+    """an arrow matrix whose dense row comes first fills L completely in the
+    identity order; minimum degree eliminates the leaves first (no fill)"""
+    n = 200
+    i = np.concatenate([np.arange(n), np.zeros(n - 1)]).astype(np.int32)
+    j = np.concatenate([np.arange(n), np.arange(1, n)]).astype(np.int32)
+    v = np.concatenate([[float(n)], np.full(n - 1, 2.0), np.full(n - 1, 1.0)])
+    b = np.arange(n, dtype=float)
+    x0, s0 = W.sym_sparse_solve(i, j, v, n, b, order=0)
+    x1, s1 = W.sym_sparse_solve(i, j, v, n, b, order=1)
+    assert s0["nnz_l"] == n * (n - 1) // 2
+    assert s1["nnz_l"] == n - 1
+    np.testing.assert_allclose(x0, x1, rtol=1e-12)
+    A = np.zeros((n, n))
+    A[i, j] = v
+    A[j, i] = v
+    np.testing.assert_allclose(x1, np.linalg.solve(A, b), rtol=1e-10)
+
+
+def test_duplicates_add_and_factor_only():
+    i = np.array([0, 0, 1, 0, 1], dtype=np.int32)
+    j = np.array([0, 0, 1, 1, 1], dtype=np.int32)
+    v = np.array([1.0, 2.0, 1.0, 1.0, 3.0])           # A = [[3, 1], [1, 4]]
+    x, st = W.sym_sparse_solve(i, j, v, 2)
+    assert x is None
+    assert st["positive"] == 2 and abs(st["log_abs_det"] - np.log(11.0)) < 1e-14
+
+
+def test_zero_pivot_is_reported():
+    """[[0, 1], [1, 0]] needs a 2x2 pivot, which the static order has not:
+    the learner falls back to the dense Bunch-Kaufman factorisation then"""
+    with pytest.raises(W.WfsaError, match="pivot"):
+        W.sym_sparse_solve(np.array([0, 0, 1], np.int32), np.array([0, 1, 1], np.int32), np.array([0.0, 1.0, 0.0]),
+                           2, np.ones(2))
+    # minimum degree does not help here, but a nonzero diagonal does
+    x, st = W.sym_sparse_solve(np.array([0, 0, 1], np.int32), np.array([0, 1, 1], np.int32),
+                               np.array([1e-3, 1.0, 0.0]), 2, np.ones(2))
+    assert (st["positive"], st["negative"]) == (1, 1)
+    np.testing.assert_allclose(x, np.linalg.solve([[1e-3, 1.0], [1.0, 0.0]], np.ones(2)), rtol=1e-12)

@@ -1,7 +1,7 @@
 import sys, numpy as np
 sys.path.insert(0, "tests"); sys.path.insert(0, "w-fsa_amd"); sys.path.insert(0, ".")
 import wfsa_amd as W
-from test_gpu_ranks import _compiled_only
+from test_gpu_ranks import _recognized
 fams = [dict(n_states=20, degree=4, vocab=6, emissions=2, n_strings=300, max_len=12),
         dict(n_states=8, degree=2, vocab=4, emissions=1, n_strings=200, max_len=8),
         dict(n_states=64, degree=4, vocab=16, emissions=1, n_strings=400, max_len=10),
@@ -10,7 +10,7 @@ fams = [dict(n_states=20, degree=4, vocab=6, emissions=2, n_strings=300, max_len
 for f in fams:
     for flags in (31, 15, 7):
         syn = W.Synthetic(seed=3, **f)
-        sym, off, p = _compiled_only(syn)
+        sym, off, p, _ = _recognized(syn)
         fsa = W.Fsa.read_text(syn.wfsa_text)
         l = W.HessianLearner(0)
         l.BuildFromPacked(fsa, sym, off, p); l.Finalize()

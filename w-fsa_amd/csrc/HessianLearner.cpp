@@ -1,5 +1,7 @@
 #include "HessianLearner.hpp"
 
+#include <string>
+
 #include <cstdlib>
 
 #include <algorithm>
@@ -186,7 +188,7 @@ void HessianLearner::InitCallback(int flags) {   // :132-191
     if (flags & 4) InitSlackVariables();
     include_Hf = (flags & 8) != 0;   // AssembleH(include_Hf)
     if (include_Hf && !HasUniquePaths()) SetupHf();
-    // flags & 16 (METIS reordering) changes nothing in a dense factorisation
+    reorder = (flags & 16) != 0;   // METIS in the reference: our minimum degree for the sparse LDL^T
     degenerate = false;
 }
 
@@ -236,7 +238,7 @@ void HessianLearner::SetupHf() {
     hf_ready = true;
 }
 
-bool HessianLearner::AddHf(std::vector<double>& H, int64_t ld) {   // ComputeHf, :498-547
+bool HessianLearner::AddHf(SymEntries& A, bool per_weight) {   // ComputeHf, :498-547
     SetupHf();
     const int32_t nf = GetNumberOfFullParameters();
     w_hf.resize(size_t(nf));
@@ -246,34 +248,73 @@ bool HessianLearner::AddHf(std::vector<double>& H, int64_t ld) {   // ComputeHf,
     for (size_t t = 0; t < hf_vals.size(); ++t) {
         const int64_t a = hf_j[t], b = hf_k[t];
         if (a < 0 || b < 0) continue;
-        H[size_t(a * ld + b)] -= hf_vals[t];
-        if (a != b) {
-            H[size_t(b * ld + a)] -= hf_vals[t];
-            offdiag = true;
-        }
+        const double v = per_weight ? hf_vals[t] / (expx[size_t(a)] * expx[size_t(b)]) : hf_vals[t];
+        A.add(a, b, -v);
+        offdiag |= a != b;
     }
     return offdiag;
 }
 
 namespace {
 
-// host or device factorisation of an N x N system (HessianLearner::kHostDense)
-bool kkt_on_device(int64_t N) {
-    if (const char* e = std::getenv("WFSA_KKT"); e && e[0]) return std::string(e) == "device";
-    return N > HessianLearner::kHostDense;
+// WFSA_KKT=host / device / sparse forces one factorisation
+std::string kkt_forced() {
+    const char* e = std::getenv("WFSA_KKT");
+    return e ? std::string(e) : std::string();
 }
 
 struct Factored {
     int64_t positive = 0, negative = 0;
     double log_abs_det = 0.0;
     int det_sign = 1;
+    char kind = 'h';   // h: host dense, d: device dense, s: sparse
 };
 
-// factors H (consumed on the host path) and, when rhs is given, solves
-// into x
-Factored factor_and_solve(wfsa_dev* dev, std::vector<double>& H, int64_t N, const double* rhs, double* x) {
+// the sparse LDL^T where it pays (above kHostDense unknowns and within
+// kSparseFlops of work, or beyond the dense limit), else the dense
+// Bunch-Kaufman factorisation on the host or in HBM; a sparse factorisation
+// with a tiny pivot or a solve whose residual is off falls back to the dense
+// one (when it fits)
+Factored factor_and_solve(wfsa_dev* dev, const SymEntries& A, int order, const double* rhs, double* x) {
     Factored r;
-    if (!kkt_on_device(N)) {
+    const int64_t N = A.n;
+    const std::string forced = kkt_forced();
+    const bool dense_fits = N <= HessianLearner::kMaxDense;
+    if (forced == "sparse" || (forced.empty() && N > HessianLearner::kHostDense)) {
+        SparseLdlt s;
+        const bool ordered = s.Analyze(A, order);
+        if (std::getenv("WFSA_KKT_TRACE"))
+            std::fprintf(stderr, "[kkt] N %lld entries %zu order %d%s nnz(L) %lld flops %.3g\n", (long long)N,
+                         A.v.size(), order, ordered ? "" : " (work bound: identity)", (long long)s.nnz_l, s.flops);
+        if (forced == "sparse" || !dense_fits || s.flops <= HessianLearner::kSparseFlops) {
+            bool ok = s.Factor(A) && s.min_pivot_ratio > 1e-12;
+            if (ok && rhs) {
+                s.Solve(rhs, x);
+                std::vector<double> ax(static_cast<size_t>(N));
+                A.multiply(x, ax.data());
+                double res = 0.0, amax = 0.0, xmax = 0.0, bmax = 0.0;
+                for (int64_t i = 0; i < N; ++i) {
+                    res = std::max(res, std::abs(ax[size_t(i)] - rhs[i]));
+                    xmax = std::max(xmax, std::abs(x[i]));
+                    bmax = std::max(bmax, std::abs(rhs[i]));
+                }
+                for (double v : A.v) amax = std::max(amax, std::abs(v));
+                ok = std::isfinite(res) && res <= 1e-9 * (amax * xmax + bmax);
+            }
+            if (ok || !dense_fits) {
+                if (!ok && rhs) std::fill(x, x + N, std::numeric_limits<double>::quiet_NaN());   // degenerate
+                r.positive = s.positive;
+                r.negative = s.negative;
+                r.log_abs_det = ok ? s.log_abs_det : -std::numeric_limits<double>::infinity();
+                r.det_sign = ok ? s.det_sign : 0;
+                r.kind = 's';
+                return r;
+            }
+        }
+    }
+    std::vector<double> H = A.dense();
+    const bool device = forced == "device" || (forced != "host" && forced != "sparse" && N > HessianLearner::kHostDense);
+    if (!device) {
         DenseLdlt f;
         f.Factor(H, N);
         r.positive = f.positive;
@@ -290,6 +331,7 @@ Factored factor_and_solve(wfsa_dev* dev, std::vector<double>& H, int64_t N, cons
     r.positive = inertia[0];
     r.negative = inertia[1];
     r.det_sign = sign;
+    r.kind = 'd';
     if (rhs) {
         std::copy(rhs, rhs + N, x);
         ThrowOnDevError(wfsa_dev_sym_solve(dev, x), "wfsa_dev_sym_solve");
@@ -340,24 +382,20 @@ void HessianLearner::OptimizationStep(double eta, bool verbose) {   // :63-130
     ComputeObjective();
     ComputeRmin(rmin);
     const int64_t n = int64_t(_x.size()), k = int64_t(lambda.size()), N = n + k;
-    if (N > kMaxDense)
-        throw LearnerError("HessianLearner: the augmented system has ", N, " unknowns; this build factors it densely "
-                           "in HBM up to ", kMaxDense, " (use -opt QuasiNewton)");
-    std::vector<double> H(size_t(N * N), 0.0);
-    if (include_Hf && !HasUniquePaths()) AddHf(H, N);
+    SymEntries A(N);   // AssembleH's pattern (:381-467), upper triangle
+    if (include_Hf && !HasUniquePaths()) AddHf(A, false);
     for (int64_t i = 0; i < n; ++i) {   // ComputeHg, :622-639
-        const int64_t c = n + Ccol[size_t(i)];
-        H[size_t(i * N + i)] += expx[size_t(i)] * lambda[size_t(Ccol[size_t(i)])];
-        H[size_t(i * N + c)] += expx[size_t(i)];
-        H[size_t(c * N + i)] += expx[size_t(i)];
+        A.add(i, i, expx[size_t(i)] * lambda[size_t(Ccol[size_t(i)])]);
+        A.add(i, n + Ccol[size_t(i)], expx[size_t(i)]);
     }
     if (verbose) {   // (:76-80)
         std::fputs("H:\n", stderr);
-        PrintKkt(stderr, H, N, include_Hf, true, &rhs);
+        PrintKkt(stderr, A.dense(), N, include_Hf, true, &rhs);
     }
     lambda_min = k ? *std::min_element(lambda.begin(), lambda.end()) : 0.0;
     step.assign(size_t(N), 0.0);
-    const Factored f = factor_and_solve(Device(), H, N, rhs.data(), step.data());
+    const Factored f = factor_and_solve(Device(), A, reorder ? 1 : 0, rhs.data(), step.data());
+    kkt_kind = f.kind;
     inertia_pos = f.positive;
     inertia_neg = f.negative;
     const auto bad = [](double v) { return !std::isfinite(v); };
@@ -409,27 +447,25 @@ bool HessianLearner::HaltCondition(double tol) {   // :374-379
 // (H_f - diag(grad f)) / (exp(x_j) exp(x_k)) (:219-260)
 double HessianLearner::ComputeLogDetHessian(bool verbose) {
     const int64_t n = int64_t(_x.size());
-    if (n > kMaxDense)
-        throw LearnerError("HessianLearner: log det of ", n, " parameters exceeds the dense limit ", kMaxDense);
-    std::vector<double> H(size_t(n * n), 0.0);
+    SymEntries A(n);
     ComputeExpX();
     ComputeGrad();
-    const bool offdiag = !HasUniquePaths() && AddHf(H, n);
-    for (int64_t j = 0; j < n; ++j) H[size_t(j * n + j)] -= grad[size_t(j)];
-    for (int64_t j = 0; j < n; ++j)
-        for (int64_t k = 0; k < n; ++k) H[size_t(j * n + k)] /= expx[size_t(j)] * expx[size_t(k)];
-    if (verbose) log_det_h = H;   // for PrintH after the Hessian line (:360)
+    const bool offdiag = !HasUniquePaths() && AddHf(A, true);
+    for (int64_t j = 0; j < n; ++j) A.add(j, j, -grad[size_t(j)] / (expx[size_t(j)] * expx[size_t(j)]));
+    if (verbose) log_det_h = A.dense();   // for PrintH after the Hessian line (:360)
     const double inf = std::numeric_limits<double>::infinity();
     if (!offdiag) {   // diagonal (src/Utils.cpp:300-311)
+        std::vector<double> d(static_cast<size_t>(n), 0.0);
+        for (size_t t = 0; t < A.v.size(); ++t)
+            if (A.i[t] == A.j[t]) d[size_t(A.i[t])] += A.v[t];
         double r = 0.0;
         for (int64_t i = 0; i < n; ++i) {
-            const double d = H[size_t(i * n + i)];
-            if (!(d > 0)) return inf;
-            r += std::log(d);
+            if (!(d[size_t(i)] > 0)) return inf;
+            r += std::log(d[size_t(i)]);
         }
         return r;
     }
-    const Factored f = factor_and_solve(Device(), H, n, nullptr, nullptr);
+    const Factored f = factor_and_solve(Device(), A, reorder ? 1 : 0, nullptr, nullptr);
     if (f.det_sign <= 0) return inf;   // (:351-352)
     return f.log_abs_det;
 }

@@ -18,6 +18,7 @@
 #include <vector>
 
 #include "Learner.hpp"
+#include "SparseLdlt.hpp"
 
 namespace wfsa {
 
@@ -50,6 +51,13 @@ public:
     // device forces one side
     static constexpr int64_t kHostDense = 1024;
     static constexpr int64_t kMaxDense = 46000;
+    // above kHostDense the sparse LDL^T (SparseLdlt.hpp, scalar up-looking
+    // code at ~1 GFLOP/s) takes systems whose factor costs at most this many
+    // flops -- below the dense factorisation in HBM (0.5 s at N = 10k; c3's
+    // KKT system fills in too much for the sparse one) -- and every system
+    // beyond kMaxDense; WFSA_KKT=sparse forces it
+    static constexpr double kSparseFlops = 3e8;
+    char LastKktKind() const { return kkt_kind; }   // h / d / s: the last step's factorisation
 
     void OptimizationStep(double eta = 1.0, bool verbose = false) override;
     std::vector<double> GetOptimizationInfo() override;      // 9 values
@@ -73,9 +81,10 @@ private:
     void InitSlackVariables();
     void ComputeRhs();
     void SetupHf();
-    // H (ld x ld, row-major) -= sum_s p_s Cov_s at the current x, on the
-    // trimmed parameters; returns whether the pattern has off-diagonal entries
-    bool AddHf(std::vector<double>& H, int64_t ld);
+    // A += -sum_s p_s Cov_s at the current x, on the trimmed parameters
+    // (per_weight: over exp(x_j) exp(x_k), the weight-space Hessian); returns
+    // whether the pattern has off-diagonal entries
+    bool AddHf(SymEntries& A, bool per_weight);
     void PrintKkt(FILE* f, const std::vector<double>& H, int64_t ld, bool with_hf, bool with_jg,
                   const std::vector<double>* rhs_print);
     std::vector<double> log_det_h;   // the last log-det Hessian, kept for PrintH (verbose)
@@ -83,7 +92,8 @@ private:
     std::vector<double> rhs, expx, grad, lambda, step;
     std::vector<int32_t> hf_j, hf_k;   // trimmed indices of the pattern (-1: not a variable)
     std::vector<double> hf_vals, w_hf;
-    bool hf_ready = false, include_Hf = false, degenerate = false, exponential_lambda = false;
+    bool hf_ready = false, include_Hf = false, degenerate = false, exponential_lambda = false, reorder = false;
+    char kkt_kind = 0;
     double error = 0.0, lambda_min = 0.0;
     double rmin[2] = {0.0, 0.0};   // rmin column at the step's x
     int64_t inertia_pos = 0, inertia_neg = 0;

@@ -5,6 +5,7 @@
 #include <cmath>
 #include <cstdio>
 #include <cstring>
+#include <limits>
 #include <memory>
 #include <new>
 #include <string>
@@ -15,6 +16,7 @@
 #include "HessianLearner.hpp"
 #include "Learner.hpp"
 #include "QuasiNewtonLearner.hpp"
+#include "SparseLdlt.hpp"
 #include "synth.hpp"
 #include "trellis_model.hpp"
 
@@ -430,6 +432,38 @@ int wfsa_shard_range(const int64_t* off, int64_t n, int nranks, int rank, int64_
     *begin = r.begin;
     *end = r.end;
     return WFSA_OK;
+}
+
+int wfsa_sym_sparse_solve(int64_t n, int64_t nnz, const int32_t* i, const int32_t* j, const double* v, int order,
+                          const double* b, double* x, int64_t out_i[4], double out_d[3]) {
+    if (n < 0 || nnz < 0 || (nnz > 0 && (!i || !j || !v)) || (b && !x) || !out_i || !out_d) return null_arg("matrix");
+    if (n > std::numeric_limits<int32_t>::max()) return null_arg("n");
+    try {
+        SymEntries a(n);
+        for (int64_t t = 0; t < nnz; ++t) {
+            if (i[t] < 0 || j[t] < 0 || i[t] >= n || j[t] >= n) return null_arg("entry index");
+            a.add(i[t], j[t], v[t]);
+        }
+        SparseLdlt s;
+        const bool ordered = s.Analyze(a, order);
+        const bool ok = s.Factor(a);
+        out_i[0] = s.positive;
+        out_i[1] = s.negative;
+        out_i[2] = s.nnz_l;
+        out_i[3] = ordered ? 1 : 0;
+        out_d[0] = s.log_abs_det;
+        out_d[1] = s.det_sign;
+        out_d[2] = s.min_pivot_ratio;
+        if (!ok) {
+            g_host_error = "sparse LDL^T: zero or non-finite pivot";
+            return WFSA_ERR_ARG;
+        }
+        if (b) s.Solve(b, x);
+        return WFSA_OK;
+    } catch (const std::bad_alloc&) {
+        g_host_error = "out of host memory";
+        return WFSA_ERR_CAPACITY;
+    }
 }
 
 int wfsa_trellis_compile_stats(const wfsa_model_desc* model, int64_t out[4]) {

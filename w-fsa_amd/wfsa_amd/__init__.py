@@ -20,7 +20,7 @@ def _ptr(a):
 
 
 __all__ = ["Fsa", "Corpus", "QuasiNewtonLearner", "Device", "Synthetic", "WfsaError", "load", "shard_range",
-           "trellis_stats"]
+           "sym_sparse_solve", "trellis_stats"]
 
 
 def shard_range(off, nranks, rank):
@@ -29,6 +29,22 @@ def shard_range(off, nranks, rank):
     b, e = C.c_int64(), C.c_int64()
     check_host(load().wfsa_shard_range(_ptr(off), len(off) - 1, nranks, rank, C.byref(b), C.byref(e)))
     return b.value, e.value
+
+
+def sym_sparse_solve(i, j, v, n, b=None, order=0):
+    """the HessianLearner's sparse LDL^T on the upper-triangle coordinates
+    (i <= j): (x or None, dict of the factorisation's statistics)"""
+    i = np.ascontiguousarray(i, dtype=np.int32)
+    j = np.ascontiguousarray(j, dtype=np.int32)
+    v = np.ascontiguousarray(v, dtype=np.float64)
+    bb = None if b is None else np.ascontiguousarray(b, dtype=np.float64)
+    x = None if b is None else np.zeros(n)
+    oi = np.zeros(4, dtype=np.int64)
+    od = np.zeros(3)
+    check_host(load().wfsa_sym_sparse_solve(n, len(v), _ptr(i), _ptr(j), _ptr(v), order, _ptr(bb), _ptr(x),
+                                            _ptr(oi), _ptr(od)))
+    return x, dict(positive=int(oi[0]), negative=int(oi[1]), nnz_l=int(oi[2]), ordered=bool(oi[3]),
+                   log_abs_det=float(od[0]), det_sign=int(od[1]), min_pivot_ratio=float(od[2]))
 
 
 def trellis_stats(fsa):

@@ -124,6 +124,7 @@ _SIGS = {
     "wfsa_learner_dump": (C.c_int, [vp, vp, C.c_char_p]),
     "wfsa_learner_stats": (C.c_int, [vp, P(DevStats)]),
     "wfsa_shard_range": (C.c_int, [vp, i64, C.c_int, C.c_int, P(i64), P(i64)]),
+    "wfsa_sym_sparse_solve": (C.c_int, [i64, i64, vp, vp, vp, C.c_int, vp, vp, vp, vp]),
     "wfsa_trellis_compile_stats": (C.c_int, [P(ModelDesc), vp]),
     "wfsa_synth_make": (C.c_int, [i32, i32, i32, i32, i32, i64, i32, C.c_uint64, P(vp)]),
     "wfsa_synth_free": (None, [vp]),
