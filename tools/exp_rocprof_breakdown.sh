@@ -1,0 +1,26 @@
+#!/bin/bash
+# fbs breakdown from rocprof kernel durations (not events): the default
+# kernel against its timing variants (WFSA_FBS_DBG, fb_kernels.hip: 5 return
+# at once, 3 no stream pass, 8 no bubble code, 1 no table gathers, 9 stream
+# loads only).  Variant results are wrong by design; only durations matter.
+set -o pipefail
+R=${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}
+OUT=$R/gpurun_out/rbrk
+mkdir -p "$OUT"
+export TMPDIR=/tmp
+cd /tmp || exit 1
+for v in ${BRK_VARIANTS:-0 5 3 8 1 9}; do
+    WFSA_FBS_DBG=$v timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/v$v" -o run -- \
+        python3 "$R/bench.py" --no-sub --cpu-sample 0 --boundary-steps 0 --steps 200 --warmup 10 > "$OUT/v$v.log" 2>&1 || exit 1
+    f=$(find "$OUT/v$v" -name '*kernel_stats.csv' | head -1)
+    python3 - "$f" "$v" <<'PY'
+import csv, sys
+rows = list(csv.DictReader(open(sys.argv[1])))
+out = []
+for r in rows:
+    n = r["Name"]
+    if "fbs_kernel" in n or "qn_step" in n or "wide2" in n or "pair_weights" in n:
+        out.append(f"{n.split('(wfsa')[0].split('::')[-1][:48]} x{r['Calls']} avg {float(r['AverageNs'])/1e3:.2f} us")
+print(f"DBG={sys.argv[2]}: " + "; ".join(out), flush=True)
+PY
+done

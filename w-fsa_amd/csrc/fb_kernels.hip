@@ -1692,7 +1692,7 @@ __global__ __launch_bounds__(kBubbleBlock) void bubble_kernel(BubbleArgs a) {
 // The first set is issued before the weights are staged and the bubbles
 // evaluated, so its latency hides behind that work (both sets would spill).
 // DBG (timing experiments only, WFSA_FBS_DBG): 1 no table gathers, 3 no
-// stream pass at all, 4 neither stream pass nor table staging, 5 return at once, 6 / 7
+// stream pass at all, 4 neither stream pass nor table staging, 5 the QN finish only, 6 / 7
 // prefetch sets of 2 / 6 rows, 8 no bubble code, 9 stream loads only
 template <bool WIDE, bool W_LDS, bool MULTI, int DBG = 0, bool RMIN = false>
 __global__ __launch_bounds__(1024, (DBG == 10 ? 8 : 1)) void fbs_kernel(CompiledArgs a) {
@@ -1705,7 +1705,7 @@ __global__ __launch_bounds__(1024, (DBG == 10 ? 8 : 1)) void fbs_kernel(Compiled
     const int w = int(threadIdx.x) / kWave;
     const int gw = __builtin_amdgcn_readfirstlane(bid * wpb + w);
     // halted is written only by an earlier launch (the QN step's finish)
-    if ((a.halted && *a.halted) || DBG == 5) return;
+    if (a.halted && *a.halted) return;
     const uint32_t zslot = uint32_t(a.n_params);
     // this wave's run of chunk rows
     const int g0 = a.wave_first[gw], g1 = a.wave_first[gw + 1];
@@ -1721,15 +1721,21 @@ __global__ __launch_bounds__(1024, (DBG == 10 ? 8 : 1)) void fbs_kernel(Compiled
     };
     const bool kStreams = DBG != 3 && DBG != 4 && !a.no_streams;   // (timing experiments; bubbles-only launches)
     if (kStreams) load(A, 0);
-    // the previous QN step's finish: reduced here (its loads beside the
-    // prefetch), published by thread 0 after the staging barrier (the
-    // system-scope release then holds up one wave, not the block)
-    double finfo[7];
-    unsigned fstat = kQnRan;
-    const bool fin = a.fin.active && bid == 0;
-    if (fin) {
-        __shared__ double fred[kMaxBlockWaves];
-        qn_finish_compute(a.fin, fred, finfo, fstat);
+    // the previous QN step's finish runs in a wave of its own -- the last
+    // wave of block 0, which the host gives no groups and no bubbles -- after
+    // the staging barrier, beside the other waves' work
+    const bool fin_wave = bid == 0 && w == wpb - 1;
+    auto finish = [&]() {
+        if (fin_wave && a.fin.active) {
+            double finfo[7];
+            unsigned fstat = kQnRan;
+            qn_finish_compute<true>(a.fin, nullptr, finfo, fstat);
+            if (lane == 0) qn_finish_publish(a.fin, finfo, fstat);
+        }
+    };
+    if (DBG == 5) {   // the launch and the finish only
+        finish();
+        return;
     }
     if (W_LDS && DBG != 4 && !a.no_streams) {
         // stage w[0, n_params] in 16-byte pieces, all of a thread's loads
@@ -1749,10 +1755,10 @@ __global__ __launch_bounds__(1024, (DBG == 10 ? 8 : 1)) void fbs_kernel(Compiled
         }
         __syncthreads();
     }
-    if (fin && threadIdx.x == 0) qn_finish_publish(a.fin, finfo, fstat);
+    finish();
     const double* wsrc = W_LDS ? lds : a.w;
     double ll_acc = 0.0;
-    if (a.bub_on && DBG != 8 && DBG != 10) {   // this wave's bubbles, before its streams
+    if (a.bub_on && DBG != 8 && DBG != 10 && !fin_wave) {   // this wave's bubbles, before its streams
         // small ones, one per lane, from the first small_wpb waves of every
         // block (spread over all CUs)
         if (w < a.bub.small_wpb) {   // small_wpb <= waves per block (bubbles_fused)
@@ -1762,14 +1768,15 @@ __global__ __launch_bounds__(1024, (DBG == 10 ? 8 : 1)) void fbs_kernel(Compiled
                 ll_acc += small_bubble<8, 8, RMIN>(a.bub, a.bub.sm_tbl, a.bub.n_small, b - a.bub.n_small4);
         }
         // big bubbles, one wavefront each, from the last blocks' last waves
-        // down, staged in LDS after w
-        const int r = (nblk - 1 - bid) + nblk * (wpb - 1 - w);
+        // down (the finish wave's rank, nblk - 1, skipped), staged in LDS after w
+        int r = (nblk - 1 - bid) + nblk * (wpb - 1 - w);
+        r -= r > nblk - 1 ? 1 : 0;
         if (r < a.bub.n_big) {
             const int E = a.bub.big_lds_edges;
             char* stg = reinterpret_cast<char*>(lds) + a.bub.big_lds_off + w * big_stage_bytes(E);
             double* lw = reinterpret_cast<double*>(stg);
             int* lsd = reinterpret_cast<int*>(lw + E + 2 * kMaxBubbleNodes);
-            for (int i = r; i < a.bub.n_big; i += nw) ll_acc += big_bubble(a.bub, i, lsd, lw, lw, lw + E);
+            for (int i = r; i < a.bub.n_big; i += nw - 1) ll_acc += big_bubble(a.bub, i, lsd, lw, lw, lw + E);
         }
     }
     if (kStreams) load(B, D);

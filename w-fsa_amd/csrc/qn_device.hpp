@@ -107,8 +107,11 @@ __device__ inline double block_reduce(double v, int op, double* red) {
 // partials (fixed order) into thread 0's info[7] and status; then
 // qn_finish_publish (thread 0): the halt decision (halt_pending, read by the
 // next QN launch) and the publication.  red: kMaxBlockWaves doubles of LDS.
+// WAVE: one wavefront computes it alone (the stream kernel's reserved finish
+// wave; no block barriers), red unused
+template <bool WAVE = false>
 __device__ inline void qn_finish_compute(const QnFinish& f, double* red, double* info, unsigned& status) {
-    const int t = int(threadIdx.x), nt = int(blockDim.x), nw = nt / 64;
+    const int t = WAVE ? int(threadIdx.x) % 64 : int(threadIdx.x), nt = WAVE ? 64 : int(blockDim.x), nw = nt / 64;
     double gmin = INFINITY, gmax = -INFINITY, lmin = INFINITY, ge = 0.0;
     for (int j0 = t; j0 < f.n_blocks; j0 += 4 * nt) {   // four blocks' partials in flight per thread
         double4 v[4];
@@ -132,11 +135,19 @@ __device__ inline void qn_finish_compute(const QnFinish& f, double* red, double*
                 ri = i;
             }
         }
-    gmin = block_reduce(gmin, 0, red);
-    gmax = block_reduce(gmax, 1, red);
-    lmin = block_reduce(lmin, 0, red);
-    ge = block_reduce(ge, 1, red);
-    ll = block_reduce(ll, 2, red);
+    if (WAVE) {
+        gmin = wave_reduce(gmin, 0);
+        gmax = wave_reduce(gmax, 1);
+        lmin = wave_reduce(lmin, 0);
+        ge = wave_reduce(ge, 1);
+        ll = wave_reduce(ll, 2);
+    } else {
+        gmin = block_reduce(gmin, 0, red);
+        gmax = block_reduce(gmax, 1, red);
+        lmin = block_reduce(lmin, 0, red);
+        ge = block_reduce(ge, 1, red);
+        ll = block_reduce(ll, 2, red);
+    }
     for (int o = 32; o > 0; o >>= 1) {
         const double v = __shfl_xor(rv, o, 64), i = __shfl_xor(ri, o, 64);
         if (v < rv || (v == rv && i < ri)) {
@@ -145,11 +156,13 @@ __device__ inline void qn_finish_compute(const QnFinish& f, double* red, double*
         }
     }
     __shared__ double rr[kMaxBlockWaves][2];
-    if ((t & 63) == 0) {
-        rr[t >> 6][0] = rv;
-        rr[t >> 6][1] = ri;
+    if (!WAVE) {
+        if ((t & 63) == 0) {
+            rr[t >> 6][0] = rv;
+            rr[t >> 6][1] = ri;
+        }
+        __syncthreads();
     }
-    __syncthreads();
     if (t == 0) {
         for (int w = 1; w < nw; ++w)
             if (rr[w][0] < rv || (rr[w][0] == rv && rr[w][1] < ri)) {

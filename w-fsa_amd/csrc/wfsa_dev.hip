@@ -1126,8 +1126,14 @@ int prepare(wfsa_dev* ctx, int level) {
         std::vector<double> load(size_t(i_nw), 0.0);
         for (int w = 0; w < i_nw; ++w) {
             const int bid = w / i_wpb, wib = w % i_wpb;
+            if (bid == 0 && wib == i_wpb - 1) {   // the QN finish's wave (fbs_kernel): no groups
+                load[size_t(w)] = 1e300;
+                continue;
+            }
             if (wib < small_wpb && int64_t(bid) * small_wpb + wib < small_waves) load[size_t(w)] += small_cost;
-            if ((nblk - 1 - bid) + int64_t(nblk) * (i_wpb - 1 - wib) < n_big_est) load[size_t(w)] += big_cost;
+            int64_t r = (nblk - 1 - bid) + int64_t(nblk) * (i_wpb - 1 - wib);
+            r -= r > nblk - 1 ? 1 : 0;
+            if (r < n_big_est) load[size_t(w)] += big_cost;
         }
         using Item = std::pair<double, int32_t>;
         std::priority_queue<Item, std::vector<Item>, std::greater<Item>> heap;
@@ -1532,7 +1538,10 @@ bool bubbles_fused(wfsa_dev* ctx, bool want_logq) {
           ctx->fuse_bubbles))
         return false;
     // at most one chunk of 64 small bubbles per wave; the big bubbles' staging must fit beside w
-    if (small_waves_per_block(ctx->n_small4 + ctx->n_small, ctx->i_grid) > ctx->i_block / kWave) return false;
+    // (the last wave of block 0 is the QN finish's: no bubbles)
+    if (ctx->i_block / kWave < 2 ||
+        small_waves_per_block(ctx->n_small4 + ctx->n_small, ctx->i_grid) > ctx->i_block / kWave - 1)
+        return false;
     return ctx->n_big == 0 || big_stage_off(ctx) + size_t(ctx->i_block / kWave) *
                                                        size_t(wfsa::big_stage_bytes(ctx->big_lds_edges)) <=
                                   size_t(kLdsPerCu - 1024);
