@@ -8,9 +8,10 @@
 // (the count covariance of each string's paths) from the per-bubble
 // second-order kernel (wfsa_dev_hf_eval), and H_g / J_g are diagonal /
 // one-entry-per-row.  MKL DSS (symmetric indefinite factorisation, inertia,
-// determinant) is replaced by a dense Bunch-Kaufman LDL^T: on the host for
+// determinant) is replaced by a dense Bunch-Kaufman LDL^T -- on the host for
 // small systems, in HBM (wfsa_dev_sym_factor) for large ones up to kMaxDense
-// unknowns (a sparse factorisation is the next step beyond that).
+// unknowns -- and a sparse LDL^T (SparseLdlt.hpp) where its fill is small or
+// the system exceeds the dense limit.
 #pragma once
 
 #include <cstdint>

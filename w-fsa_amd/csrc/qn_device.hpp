@@ -22,34 +22,55 @@ __device__ inline double wave_reduce(double v, int op) {   // op 0 min, 1 max, 2
 // depends on the parameter's own slots only (not on the slot layout, the
 // reduction groups or the block size), so the same contributions give the
 // same bits under every layout: parameter q's slots are cut into chunks of
-// kSlotChunk from its first slot, each chunk summed in slot order, then the
-// chunk sums added in chunk order.
+// kSlotChunk (16) from its first slot, each chunk summed by a fixed tree
+// (chunk_tree: pairs, then pairs of pairs), then the chunk sums added in
+// chunk order.
 //
 // One reduction group (a QN constraint, or a run of positions) holds nseg
 // parameters: q owns logical slots [sp[q], sp[q+1]) and chunks [cb[q],
-// cb[q+1]) (both relative to the group, in LDS).  The group's chunks are
-// stored transposed: element b of chunk c at v[b * nch + c] (nch = cb[nseg];
-// a chunk's tail is zero padding), so consecutive threads -- one chunk each --
-// read consecutive addresses.  The chunk sums go to LDS (cp, kMaxChunks,
-// fb_kernels.hpp) and
-// a thread per parameter adds them; a group with more chunks sums each
-// parameter's chunks in one thread straight from memory (same order).
+// cb[q+1]) (both relative to the group, in LDS).  Chunk c of the group is
+// stored contiguously at v[16 c, 16 c + 16) (a chunk's tail is zero padding),
+// so the bubble kernels' stores -- lanes holding same-shaped bubbles write a
+// parameter's consecutive slots -- coalesce, and so do these loads: eight
+// lanes read a chunk as eight 16-byte pieces and reduce it by shuffles in the
+// tree's order.  The chunk sums go to LDS (cp, kMaxChunks, fb_kernels.hpp)
+// and a thread per parameter adds them; a group with more chunks sums each
+// parameter's chunks in one thread straight from memory (same tree).
+static_assert(kSlotChunk == 16, "chunk_tree and the 8-lane chunk loads assume 16-slot chunks");
+__device__ inline double chunk_tree(const double* x) {   // ((p0+p1)+(p2+p3)) + ((p4+p5)+(p6+p7)), pk = x2k + x2k+1
+    double p[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) p[k] = x[2 * k] + x[2 * k + 1];
+    return ((p[0] + p[1]) + (p[2] + p[3])) + ((p[4] + p[5]) + (p[6] + p[7]));
+}
 template <int NT>
 __device__ void seg_sums(const double* __restrict__ v, const int* sp, const int* cb, int nseg, double* res,
                          double* cp) {
     const int t = int(threadIdx.x);
     const int nch = cb[nseg];
-    auto chunk_sum = [&](int c) {   // unguarded: the padding is zero, and adding +0.0 changes nothing
-        double x[kSlotChunk];
-#pragma unroll
-        for (int b = 0; b < kSlotChunk; ++b) x[b] = v[size_t(b) * size_t(nch) + size_t(c)];
-        double s = x[0];
-#pragma unroll
-        for (int b = 1; b < kSlotChunk; ++b) s += x[b];
-        return s;
-    };
     if (nch <= kMaxChunks) {
-        for (int c = t; c < nch; c += NT) cp[c] = chunk_sum(c);
+        // a wave reads 8 chunks per round (lane: chunk lane / 8, piece lane % 8),
+        // kR rounds in flight; the shuffles follow chunk_tree's order
+        constexpr int kR = 4;
+        const int lane = t & 63, wv = t >> 6, sub = lane & 7;
+        constexpr int NW = NT / 64;
+        const double2* v2 = reinterpret_cast<const double2*>(v);
+        for (int c0 = wv * 8 * kR; c0 < nch; c0 += NW * 8 * kR) {
+            double2 x[kR];
+#pragma unroll
+            for (int r = 0; r < kR; ++r) {
+                const int c = c0 + 8 * r + (lane >> 3);
+                x[r] = c < nch ? v2[size_t(c) * 8 + sub] : make_double2(0.0, 0.0);
+            }
+#pragma unroll
+            for (int r = 0; r < kR; ++r) {
+                double sr = x[r].x + x[r].y;
+#pragma unroll
+                for (int o = 1; o < 8; o <<= 1) sr += __shfl_xor(sr, o, 64);
+                const int c = c0 + 8 * r + (lane >> 3);
+                if (sub == 0 && c < nch) cp[c] = sr;
+            }
+        }
         __syncthreads();
         for (int q = t; q < nseg; q += NT) {
             const int c0 = cb[q], c1 = cb[q + 1];
@@ -68,7 +89,12 @@ __device__ void seg_sums(const double* __restrict__ v, const int* sp, const int*
     } else {
         for (int q = t; q < nseg; q += NT) {
             double s = 0.0;
-            for (int c = cb[q]; c < cb[q + 1]; ++c) s += chunk_sum(c);
+            for (int c = cb[q]; c < cb[q + 1]; ++c) {
+                double x[kSlotChunk];
+#pragma unroll
+                for (int b = 0; b < kSlotChunk; ++b) x[b] = v[size_t(c) * kSlotChunk + size_t(b)];
+                s += chunk_tree(x);
+            }
             res[q] = s;
         }
     }

@@ -797,10 +797,9 @@ int layout_slots(wfsa_dev* ctx, const std::vector<int32_t>& pos_of) {
     // positions (at most kReduceTileParams parameters and, unless one alone
     // has more, kMaxChunks chunks).  Parameter q's slots form chunks of
     // kSlotChunk (seg_sums, qn_device.hpp: its sum depends on its own slots
-    // only); a group's chunks are stored transposed -- element b of the
-    // group's chunk c at gbase + b * nch + c -- so the threads of a block, a
-    // chunk each, read consecutive addresses (one cache line per 8 lanes
-    // instead of one per lane: the uncoalesced form cost ~8 us per QN step at c3).
+    // only), stored contiguously -- a parameter's slots are consecutive
+    // addresses, so the stores of lanes whose (sorted, same-shaped) bubbles
+    // share a parameter coalesce; seg_sums reads a chunk with eight lanes.
     std::vector<int32_t> cptr_pos(size_t(np) + 1, 0);   // chunks by position, cumulative
     for (int32_t q = 0; q < np; ++q)
         cptr_pos[size_t(q) + 1] = cptr_pos[size_t(q)] + (pc[size_t(q) + 1] - pc[size_t(q)] + wfsa::kSlotChunk - 1) / wfsa::kSlotChunk;
@@ -822,10 +821,8 @@ int layout_slots(wfsa_dev* ctx, const std::vector<int32_t>& pos_of) {
     }
     auto phys = [&](int32_t pos, int32_t sl) -> int32_t {   // logical slot sl of position pos
         const int32_t g = grp_of[size_t(pos)], cg = cptr_pos[size_t(gp[size_t(g)])];
-        const int64_t nch = cptr_pos[size_t(gp[size_t(g) + 1])] - cg;
         const int32_t i = sl - pc[size_t(pos)];
-        const int64_t c = cptr_pos[size_t(pos)] - cg + i / wfsa::kSlotChunk;
-        return int32_t(gbase[size_t(g)] + int64_t(i % wfsa::kSlotChunk) * nch + c);
+        return int32_t(gbase[size_t(g)] + int64_t(cptr_pos[size_t(pos)] - cg) * wfsa::kSlotChunk + i);
     };
     if (gbase.back() >= int64_t(INT32_MAX)) return fail(WFSA_ERR_CAPACITY, "too many bubble contribution slots");
     if (ctx->n_bubbles > 0) {
@@ -1257,6 +1254,21 @@ int prepare(wfsa_dev* ctx, int level) {
             bool sm = edges <= wfsa::kBubbleRegEdges && nodes <= wfsa::kBubbleRegNodes;
             for (int e = 0; sm && e < edges; ++e) sm = edge_code_at(o, e) >= 0;
             (!sm ? big : (edges <= 4 && nodes <= 4 ? small4 : small)).push_back(o);
+        }
+        // same-shaped bubbles (equal edge codes and structure) next to each
+        // other: the lanes of a wave then take the same branches and write a
+        // parameter's consecutive contribution slots (layout_slots)
+        auto shape_less = [&](int32_t x, int32_t y) {
+            const int ex = h_bubbuf[size_t(x)] >> 16, ey = h_bubbuf[size_t(y)] >> 16;
+            if (h_bubbuf[size_t(x)] != h_bubbuf[size_t(y)]) return h_bubbuf[size_t(x)] < h_bubbuf[size_t(y)];
+            for (int k = 0; k < 2 * std::min(ex, ey); ++k)
+                if (h_bubbuf[size_t(x) + 4 + size_t(k)] != h_bubbuf[size_t(y) + 4 + size_t(k)])
+                    return h_bubbuf[size_t(x) + 4 + size_t(k)] < h_bubbuf[size_t(y) + 4 + size_t(k)];
+            return false;
+        };
+        if (!(std::getenv("WFSA_BUB_SORT") && std::getenv("WFSA_BUB_SORT")[0] == '0')) {
+            std::stable_sort(small4.begin(), small4.end(), shape_less);
+            std::stable_sort(small.begin(), small.end(), shape_less);
         }
         if (std::getenv("WFSA_DEBUG_BUBBLES")) {   // size histogram (diagnostics)
             std::vector<int64_t> he(size_t(wfsa::kMaxBubbleEdges) + 1, 0), hn(size_t(wfsa::kMaxBubbleNodes) + 1, 0);
