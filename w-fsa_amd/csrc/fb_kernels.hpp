@@ -379,7 +379,8 @@ struct QnArgs {
     int32_t use_out;             // (fused: 0 when no traversal string adds to out)
     const double* fixed;         // [n_full] constant trivial-word gradient to add, or null
     const double* contrib;       // fused: bubble contribution slots, or null
-    const int64_t* grp_base;     // fused: physical slot base of constraint c's group (chunk-transposed)
+    const int64_t* grp_base;     // fused: physical slot base of constraint c's group
+    const int32_t* grp_nch;      // fused: its chunk count
     const int32_t* seg_ptr;      // fused: [n + 1] logical slot run of kept parameter i (trimmed order)
     const int32_t* chunk_ptr;    // fused: [n + 1] its chunks (cumulative)
     int32_t n_full, n, k;

@@ -43,12 +43,11 @@ __device__ inline double chunk_tree(const double* x) {   // ((p0+p1)+(p2+p3)) + 
     for (int k = 0; k < 8; ++k) p[k] = x[2 * k] + x[2 * k + 1];
     return ((p[0] + p[1]) + (p[2] + p[3])) + ((p[4] + p[5]) + (p[6] + p[7]));
 }
+// the chunk sums of a group (nch <= kMaxChunks) into cp; no barrier
 template <int NT>
-__device__ void seg_sums(const double* __restrict__ v, const int* sp, const int* cb, int nseg, double* res,
-                         double* cp) {
+__device__ inline void chunk_sums(const double* __restrict__ v, int nch, double* cp) {
     const int t = int(threadIdx.x);
-    const int nch = cb[nseg];
-    if (nch <= kMaxChunks) {
+    {
         // a wave reads 8 chunks per round (lane: chunk lane / 8, piece lane % 8),
         // kR rounds in flight; the shuffles follow chunk_tree's order
         constexpr int kR = 4;
@@ -71,7 +70,13 @@ __device__ void seg_sums(const double* __restrict__ v, const int* sp, const int*
                 if (sub == 0 && c < nch) cp[c] = sr;
             }
         }
-        __syncthreads();
+    }
+}
+// parameter q's sum from the chunk sums in cp (after a barrier); no barrier
+template <int NT>
+__device__ inline void member_sums(const int* cb, int nseg, const double* cp, double* res) {
+    const int t = int(threadIdx.x);
+    {
         for (int q = t; q < nseg; q += NT) {
             const int c0 = cb[q], c1 = cb[q + 1];
             double s = 0.0;
@@ -86,6 +91,17 @@ __device__ void seg_sums(const double* __restrict__ v, const int* sp, const int*
             for (; c < c1; ++c) s += cp[c];
             res[q] = s;
         }
+    }
+}
+template <int NT>
+__device__ void seg_sums(const double* __restrict__ v, const int* sp, const int* cb, int nseg, double* res,
+                         double* cp) {
+    const int t = int(threadIdx.x);
+    const int nch = cb[nseg];
+    if (nch <= kMaxChunks) {
+        chunk_sums<NT>(v, nch, cp);
+        __syncthreads();
+        member_sums<NT>(cb, nseg, cp, res);
     } else {
         for (int q = t; q < nseg; q += NT) {
             double s = 0.0;

@@ -41,16 +41,23 @@ __global__ __launch_bounds__(kQnBlock) void qn_step_kernel(QnArgs a) {
     __shared__ int sp[kQnMaxSeg + 1], cb[kQnMaxSeg + 1], sfo[kQnMaxSeg];
     __shared__ double cp[kMaxChunks];
     __shared__ double bc[2], red[kMaxBlockWaves];
-    // The loads are issued in three dependent rounds (the kernel is a chain
-    // of global-memory latencies): the flags with the constraint's extent;
-    // its members' slot runs, full indices and x; their slots and gradient parts.
+    // The loads are issued in dependent rounds (the kernel is a chain of
+    // global-memory latencies): the flags with the constraint's extent and its
+    // slot group; its members' slot runs, full indices and x together with the
+    // group's slot chunks; the members' constant gradient parts.
     const bool have = c < a.k;
-    int b = 0, e = 0;
+    const bool slots = FUSED && a.contrib;
+    int b = 0, e = 0, gnch = 0;
+    int64_t gb = 0;
     double lam = 0.0;
     if (have) {
         b = a.cptr[c];
         e = a.cptr[c + 1];
         lam = a.lambda[c];
+        if (slots) {
+            gb = a.grp_base[c];
+            gnch = a.grp_nch[c];
+        }
     }
     // halted and halt_pending are written only by earlier launches: every
     // block of this one sees the same values
@@ -65,7 +72,6 @@ __global__ __launch_bounds__(kQnBlock) void qn_step_kernel(QnArgs a) {
     if (have) {
         const int nm = e - b;
         double laux;
-        const bool slots = FUSED && a.contrib;
         if (nm <= kQnMaxSeg) {
             constexpr int PT = kQnMaxSeg / kQnBlock;   // members per thread (at most)
             double xr[PT];
@@ -83,6 +89,8 @@ __global__ __launch_bounds__(kQnBlock) void qn_step_kernel(QnArgs a) {
                     sp[i] = a.seg_ptr[b + i];
                     cb[i] = a.chunk_ptr[b + i];
                 }
+            const bool in_lds = slots && gnch <= kMaxChunks;
+            if (in_lds) chunk_sums<kQnBlock>(a.contrib + gb, gnch, cp);   // the group's chunks, this round
             __syncthreads();
             const int s0 = slots ? sp[0] : 0, c0 = slots ? cb[0] : 0;
             double gp[PT];   // this thread's members: trivial-word + traversal parts
@@ -104,7 +112,12 @@ __global__ __launch_bounds__(kQnBlock) void qn_step_kernel(QnArgs a) {
                     cb[i] -= c0;
                 }
                 __syncthreads();
-                seg_sums<kQnBlock>(a.contrib + a.grp_base[c], sp, cb, nm, sg, cp);
+                if (in_lds) {
+                    member_sums<kQnBlock>(cb, nm, cp, sg);
+                    __syncthreads();
+                } else {
+                    seg_sums<kQnBlock>(a.contrib + gb, sp, cb, nm, sg, cp);
+                }
             }
 #pragma unroll
             for (int i = 0; i < PT; ++i) {

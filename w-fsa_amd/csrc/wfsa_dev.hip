@@ -182,6 +182,7 @@ struct wfsa_dev {
     DevBuf<int32_t> seg_ptr, param_at, tile_ptr;   // tile_ptr: [n_tiles + 1] position range of each reduction group
     int32_t n_tiles = 0;
     DevBuf<int64_t> grp_base;            // [n_tiles + 1] physical slot base of each reduction group
+    DevBuf<int32_t> grp_nch;             // [n_tiles] its chunk count
     DevBuf<int32_t> chunk_ptr;           // [n_params + 1] slot chunks by position (cumulative)
     std::vector<int32_t> slot_groups;     // leading reduction groups (positions): the QN constraints
     std::vector<int32_t> h_pptr, h_pidx;   // host copy of the combined parameter lists
@@ -884,6 +885,11 @@ int layout_slots(wfsa_dev* ctx, const std::vector<int32_t>& pos_of) {
     }
     ctx->n_tiles = ng;
     HIP_TRY(ctx->grp_base.upload(gbase.data(), gbase.size(), s));
+    {
+        std::vector<int32_t> gn(size_t(std::max(ng, 1)), 0);
+        for (int32_t g = 0; g < ng; ++g) gn[size_t(g)] = cptr_pos[size_t(gp[size_t(g) + 1])] - cptr_pos[size_t(gp[size_t(g)])];
+        HIP_TRY(ctx->grp_nch.upload(gn.data(), gn.size(), s));
+    }
     HIP_TRY(ctx->chunk_ptr.upload(cptr_pos.data(), cptr_pos.size(), s));
     HIP_TRY(ctx->seg_ptr.upload(pc.data(), pc.size(), s));
     HIP_TRY(ctx->param_at.upload(param_at.data(), param_at.size(), s));
@@ -1836,6 +1842,7 @@ int enqueue_qn_step(wfsa_dev* ctx, double eta, double tol, int64_t e, bool timed
         q.fixed = ctx->n_groups > 0 ? ctx->fixed_grad.ptr : nullptr;
         q.contrib = ctx->n_bubbles > 0 ? ctx->contrib.ptr : nullptr;
         q.grp_base = ctx->grp_base.ptr;   // constraint c = reduction group c
+        q.grp_nch = ctx->grp_nch.ptr;
         q.seg_ptr = ctx->seg_ptr.ptr;
         q.chunk_ptr = ctx->chunk_ptr.ptr;
         f.ll_part = ctx->ll_cur;
@@ -1971,6 +1978,7 @@ int enqueue_qn_step_piped(wfsa_dev* ctx, double eta, double tol, int64_t e, bool
     q.fixed = ctx->fixed_grad.ptr;
     q.contrib = ctx->n_bubbles > 0 ? ctx->contrib.ptr : nullptr;
     q.grp_base = ctx->grp_base.ptr;
+    q.grp_nch = ctx->grp_nch.ptr;
     q.seg_ptr = ctx->seg_ptr.ptr;
     q.chunk_ptr = ctx->chunk_ptr.ptr;
     q.n_full = np;
