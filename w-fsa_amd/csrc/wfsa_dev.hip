@@ -1112,9 +1112,10 @@ int prepare(wfsa_dev* ctx, int level) {
     std::vector<int32_t> order;
     std::vector<int32_t> wave_first(size_t(i_nw) + 1, 0);
     {
-        // costs in stream rows; small 32: the middle of the 24-40 plateau of
-        // the sweep in profiles/r01/v18_cost_sweep.txt (fbs 31.9 -> 31.2 us at c3)
-        double small_cost = 32.0, big_cost = 8.0;
+        // costs in stream rows; small 18: the 16-20 optimum of the sweep after
+        // the slot stores became coalesced (profiles/r02/v12_small_cost_sweep.txt:
+        // fbs 24.6 -> 23.4 us at c3; it was 32 before, profiles/r01/v18_cost_sweep.txt)
+        double small_cost = 18.0, big_cost = 8.0;
         if (const char* e = std::getenv("WFSA_SMALL_COST")) small_cost = std::atof(e);
         if (const char* e = std::getenv("WFSA_BIG_COST")) big_cost = std::atof(e);
         int64_t n_b = 0, n_big_est = 0;
