@@ -378,6 +378,7 @@ struct QnArgs {
     const double* out;           // [1 + n_full]: gradient parts accumulated so far
     int32_t use_out;             // (fused: 0 when no traversal string adds to out)
     const double* fixed;         // [n_full] constant trivial-word gradient to add, or null
+    const double* fixed_t;       // fused: the same in trimmed order ([n]), or null (then fixed[full_of])
     const double* contrib;       // fused: bubble contribution slots, or null
     const int64_t* grp_base;     // fused: physical slot base of constraint c's group
     const int32_t* grp_nch;      // fused: its chunk count
@@ -398,6 +399,7 @@ struct QnArgs {
     int32_t exp_lambda;
     unsigned* halted;            // [0] halted, [1] halt_pending
     QnFinish fin;                // this step's finish (publication of skipped rows)
+    int32_t dbg;                 // timing experiments only (WFSA_QN_DBG)
 };
 
 // Bubble evaluation.  Contributions (-p_s x edge posterior) go straight to
@@ -576,6 +578,8 @@ hipError_t launch_stage(const double* host_w, double* w, double* ewp, int32_t n,
 // fused: the member gradients include the bubble slot sums (every constraint
 // has at most kQnMaxSeg members); grid max(k, 1)
 hipError_t launch_qn_step(const QnArgs& a, bool fused, hipStream_t stream);
+// dst[i] = src[idx[i]], i < n
+hipError_t launch_gather(const double* src, const int32_t* idx, int32_t n, double* dst, hipStream_t stream);
 // a step's finish as its own one-block launch
 hipError_t launch_qn_finish(const QnFinish& f, hipStream_t stream);
 hipError_t launch_qn_weights(const double* x, const int32_t* trim, int32_t n_full, double* w_full, double* ewp,

@@ -50,7 +50,7 @@ __device__ inline void chunk_sums(const double* __restrict__ v, int nch, double*
     {
         // a wave reads 8 chunks per round (lane: chunk lane / 8, piece lane % 8),
         // kR rounds in flight; the shuffles follow chunk_tree's order
-        constexpr int kR = 4;
+        constexpr int kR = NT >= 512 ? 2 : (NT >= 256 ? 4 : 8);
         const int lane = t & 63, wv = t >> 6, sub = lane & 7;
         constexpr int NW = NT / 64;
         const double2* v2 = reinterpret_cast<const double2*>(v);

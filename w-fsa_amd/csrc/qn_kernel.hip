@@ -26,6 +26,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdint>
+#include <cstdlib>
 
 #pragma clang fp contract(off)
 
@@ -33,8 +34,8 @@ namespace wfsa {
 
 namespace {
 
-template <bool FUSED>
-__global__ __launch_bounds__(kQnBlock) void qn_step_kernel(QnArgs a) {
+template <bool FUSED, int NT = kQnBlock>
+__global__ __launch_bounds__(NT) void qn_step_kernel(QnArgs a) {
     const int t = int(threadIdx.x);
     const int c = int(blockIdx.x);
     __shared__ double sg[kQnMaxSeg], se[kQnMaxSeg];
@@ -68,60 +69,64 @@ __global__ __launch_bounds__(kQnBlock) void qn_step_kernel(QnArgs a) {
         }
         return;
     }
+    if (a.dbg == 1) return;   // (timing experiments, WFSA_QN_DBG: the launch and first round only)
     double gerr = 0.0, g = 0.0;
     if (have) {
         const int nm = e - b;
         double laux;
         if (nm <= kQnMaxSeg) {
-            constexpr int PT = kQnMaxSeg / kQnBlock;   // members per thread (at most)
-            double xr[PT];
+            constexpr int PT = kQnMaxSeg / NT;   // members per thread (at most)
+            double xr[PT], ft[PT];
 #pragma unroll
             for (int i = 0; i < PT; ++i) {
-                const int m = t + i * kQnBlock;
+                const int m = t + i * NT;
                 xr[i] = 0.0;
+                ft[i] = 0.0;
                 if (m < nm) {
                     sfo[m] = a.full_of[b + m];
                     xr[i] = a.x[b + m];
+                    if (a.fixed_t) ft[i] = a.fixed_t[b + m];
                 }
             }
             if (slots)   // the members' bubble slot runs and chunks (the host guarantees nm <= kQnMaxSeg)
-                for (int i = t; i <= nm; i += kQnBlock) {
+                for (int i = t; i <= nm; i += NT) {
                     sp[i] = a.seg_ptr[b + i];
                     cb[i] = a.chunk_ptr[b + i];
                 }
             const bool in_lds = slots && gnch <= kMaxChunks;
-            if (in_lds) chunk_sums<kQnBlock>(a.contrib + gb, gnch, cp);   // the group's chunks, this round
+            if (in_lds) chunk_sums<NT>(a.contrib + gb, gnch, cp);   // the group's chunks, this round
             __syncthreads();
             const int s0 = slots ? sp[0] : 0, c0 = slots ? cb[0] : 0;
             double gp[PT];   // this thread's members: trivial-word + traversal parts
 #pragma unroll
             for (int i = 0; i < PT; ++i) {
-                const int m = t + i * kQnBlock;
+                const int m = t + i * NT;
                 double gi = 0.0;
                 if (m < nm) {
                     const int fo = sfo[m];
                     if (a.use_out) gi = a.out[1 + fo];
-                    if (a.fixed) gi += a.fixed[fo];
+                    if (a.fixed_t) gi += ft[i];
+                    else if (a.fixed) gi += a.fixed[fo];
                 }
                 gp[i] = gi;
             }
             if (slots) {
                 __syncthreads();   // every sp read as absolute above
-                for (int i = t; i <= nm; i += kQnBlock) {
+                for (int i = t; i <= nm; i += NT) {
                     sp[i] -= s0;
                     cb[i] -= c0;
                 }
                 __syncthreads();
                 if (in_lds) {
-                    member_sums<kQnBlock>(cb, nm, cp, sg);
+                    member_sums<NT>(cb, nm, cp, sg);
                     __syncthreads();
                 } else {
-                    seg_sums<kQnBlock>(a.contrib + gb, sp, cb, nm, sg, cp);
+                    seg_sums<NT>(a.contrib + gb, sp, cb, nm, sg, cp);
                 }
             }
 #pragma unroll
             for (int i = 0; i < PT; ++i) {
-                const int m = t + i * kQnBlock;
+                const int m = t + i * NT;
                 if (m < nm) {
                     sg[m] = slots ? gp[i] + sg[m] : gp[i];
                     se[m] = exp(xr[i]);
@@ -141,7 +146,7 @@ __global__ __launch_bounds__(kQnBlock) void qn_step_kernel(QnArgs a) {
             laux = bc[1];
 #pragma unroll
             for (int i = 0; i < PT; ++i) {   // graderr (old lambda), x update (lambda_next)
-                const int m = t + i * kQnBlock;
+                const int m = t + i * NT;
                 if (m >= nm) break;
                 const double gi = sg[m], ei = se[m];
                 const double aux = ei * lam;
@@ -157,7 +162,7 @@ __global__ __launch_bounds__(kQnBlock) void qn_step_kernel(QnArgs a) {
                    // over the threads, sums by a fixed tree (deterministic; the
                    // host's member-order sums differ from it by rounding only)
             double gs = 0.0, gv = 0.0;
-            for (int i = b + t; i < e; i += kQnBlock) {
+            for (int i = b + t; i < e; i += NT) {
                 const double ex = exp(a.x[i]);
                 const int fo = a.full_of[i];
                 double gi = a.out[1 + fo];
@@ -171,7 +176,7 @@ __global__ __launch_bounds__(kQnBlock) void qn_step_kernel(QnArgs a) {
             gv = block_reduce(gv, 2, red);
             g = -1.0 + gs;
             laux = (lam * g - gv) / (g + 1.0);
-            for (int i = b + t; i < e; i += kQnBlock) {
+            for (int i = b + t; i < e; i += NT) {
                 const double ex = a.expx[i], gi = a.grad[i];
                 const double aux = ex * lam;
                 gerr = fmax(gerr, fabs(gi + aux));
@@ -219,10 +224,33 @@ __global__ void qn_weights_kernel(const double* x, const int32_t* trim, int32_t 
 
 }  // namespace
 
-hipError_t launch_qn_step(const QnArgs& a, bool fused, hipStream_t stream) {
+hipError_t launch_qn_step(const QnArgs& a_in, bool fused, hipStream_t stream) {
+    static const int dbg = [] {
+        const char* e = std::getenv("WFSA_QN_DBG");
+        return e ? std::atoi(e) : 0;
+    }();
+    QnArgs a = a_in;
+    a.dbg = dbg;
     const dim3 grid(unsigned(std::max(a.k, 1)));
-    if (fused) hipLaunchKernelGGL(qn_step_kernel<true>, grid, dim3(kQnBlock), 0, stream, a);
-    else hipLaunchKernelGGL(qn_step_kernel<false>, grid, dim3(kQnBlock), 0, stream, a);
+    static const int nt = [] {   // (experiments: WFSA_QN_BLOCK = 128 / 256)
+        const char* e = std::getenv("WFSA_QN_BLOCK");
+        return e && std::atoi(e) == 128 ? 128 : (e && std::atoi(e) == 512 ? 512 : kQnBlock);
+    }();
+    if (fused && nt == 128) hipLaunchKernelGGL((qn_step_kernel<true, 128>), grid, dim3(128), 0, stream, a);
+    else if (fused && nt == 512) hipLaunchKernelGGL((qn_step_kernel<true, 512>), grid, dim3(512), 0, stream, a);
+    else if (fused) hipLaunchKernelGGL((qn_step_kernel<true>), grid, dim3(kQnBlock), 0, stream, a);
+    else hipLaunchKernelGGL((qn_step_kernel<false>), grid, dim3(kQnBlock), 0, stream, a);
+    return hipGetLastError();
+}
+
+__global__ void gather_kernel(const double* src, const int32_t* idx, int32_t n, double* dst) {
+    const int i = int(blockIdx.x * blockDim.x + threadIdx.x);
+    if (i < n) dst[i] = src[idx[i]];
+}
+
+hipError_t launch_gather(const double* src, const int32_t* idx, int32_t n, double* dst, hipStream_t stream) {
+    if (n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(gather_kernel, dim3(unsigned((n + 255) / 256)), dim3(256), 0, stream, src, idx, n, dst);
     return hipGetLastError();
 }
 

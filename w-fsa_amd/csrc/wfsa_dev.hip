@@ -165,6 +165,8 @@ struct wfsa_dev {
     int i_block = 1024;
     size_t i_lds = 0;
     DevBuf<double> fixed_grad;       // [n_params] gradient of the trivial words (constant)
+    DevBuf<double> fixed_t;          // [qn_n] the same in trimmed order (QN runs)
+    bool fixed_t_on = false;
     // bubbles
     int32_t n_bubbles = 0, n_small4 = 0, n_small = 0, n_big = 0, big_lds_edges = 2;
     int b_waves = 0;
@@ -1841,6 +1843,7 @@ int enqueue_qn_step(wfsa_dev* ctx, double eta, double tol, int64_t e, bool timed
     f.out0 = ctx->out.ptr;
     if (fused) {
         q.fixed = ctx->n_groups > 0 ? ctx->fixed_grad.ptr : nullptr;
+        q.fixed_t = ctx->fixed_t_on ? ctx->fixed_t.ptr : nullptr;
         q.contrib = ctx->n_bubbles > 0 ? ctx->contrib.ptr : nullptr;
         q.grp_base = ctx->grp_base.ptr;   // constraint c = reduction group c
         q.grp_nch = ctx->grp_nch.ptr;
@@ -2704,6 +2707,14 @@ int wfsa_dev_qn_run(wfsa_dev* ctx, double eta, double tol, int32_t max_steps, do
     HIP_TRY(hipMemsetAsync(ctx->qn_halted.ptr, 0, 2 * sizeof(unsigned), s));
     ctx->fin_pending = false;
     ctx->fin_for_fbs.active = 0;
+    // the constant trivial-word gradient in trimmed order, so the fused QN
+    // step loads it with its members' x (no load round on their full index)
+    ctx->fixed_t_on = false;
+    if (ctx->qn_fused && !ctx->dense && !ctx->mpath && ctx->n_groups > 0 && ctx->qn_n > 0) {
+        HIP_TRY(ctx->fixed_t.alloc(size_t(ctx->qn_n)));
+        HIP_TRY(wfsa::launch_gather(ctx->fixed_grad.ptr, ctx->qn_full_of.ptr, ctx->qn_n, ctx->fixed_t.ptr, s));
+        ctx->fixed_t_on = true;
+    }
     const bool piped = pipe_ok(ctx);
     if (piped) {   // the second weight buffer; the pipe stream starts after everything enqueued so far
         HIP_TRY(ctx->w_full2.alloc(size_t(ctx->n_params) + 2));
