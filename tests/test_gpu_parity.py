@@ -300,3 +300,40 @@ def test_single_rank_communicator_path():
         for u, v in zip(r[:5], q[:5]):
             assert _close(u, v, rel=1e-11, atol=1e-14)
     np.testing.assert_allclose(comm.x(), plain.x(), rtol=1e-11, atol=1e-13)
+
+
+def test_popular_parameters_chunked_sums(capfd, monkeypatch):
+    """A small automaton under a large corpus: a constraint's bubble slots
+    exceed what the fused QN step keeps in LDS (kMaxChunks x 16), so both its
+    sums and the host binding's reduction take the per-thread chunk path; the
+    device loop still equals the host QN steps, and the first gradient equals
+    the trellis oracle's."""
+    import wfsa_amd as W
+    from oracle import TRELLIS, Oracle
+    monkeypatch.setenv("WFSA_VERBOSE", "1")
+    syn = W.Synthetic(n_states=4, degree=2, vocab=2, emissions=1, n_strings=30000, max_len=24, seed=2)
+    sym, off, wt = syn.corpus()
+    fsa = W.Fsa.read_text(syn.wfsa_text)
+    a, b = W.QuasiNewtonLearner(0), W.QuasiNewtonLearner(0)
+    for lrn in (a, b):
+        lrn.BuildFromPacked(fsa, sym, off, wt)
+        lrn.Finalize()
+        lrn.Init(7)
+    kl0, g0, _ = a.objective_grad()
+    rows_a = a.Run(5, 1.0, -1.0)
+    err = capfd.readouterr().err
+    line = [ln for ln in err.splitlines() if "slots per constraint" in ln][-1]
+    assert int(line.split("max ")[1].split(",")[0]) > 16 * 1024, line
+    rows_b = [b.OptimizationStep(1.0, -1.0)[0] for _ in range(5)]
+    for r, q in zip(rows_a, rows_b):
+        for u, v in zip(r[:5], q[:5]):
+            assert _close(u, v, rel=1e-11, atol=1e-14)
+    np.testing.assert_allclose(a.x(), b.x(), rtol=1e-11, atol=1e-13)
+    o = Oracle.from_arrays(syn.wfsa_text, sym, off, wt, mode=TRELLIS)
+    o.qn_init(7)
+    ko = o.objective_grad()[0]
+    go = o.grad()
+    assert _close(kl0, ko, rel=1e-11)
+    dn, on = a.param_names(), o.param_names()
+    want = dict(zip(on, go))
+    np.testing.assert_allclose(g0, [want[n] for n in dn], rtol=1e-10, atol=1e-14)
