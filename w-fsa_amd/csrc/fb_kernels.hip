@@ -1873,7 +1873,7 @@ __global__ __launch_bounds__(1024, (DBG == 10 ? 8 : 1)) void fbs_kernel(Compiled
     }
     // this block's slice of the per-edge weights and the zeroed result, for
     // the kernels after this one (nothing in this launch reads them)
-    if (W_LDS && !a.no_streams) edge_weight_slice(a, bid, nblk);
+    if (W_LDS && !a.no_streams && !a.no_slice) edge_weight_slice(a, bid, nblk);
 }
 
 // Group headers (stream_hdr_words), written after the streams are emitted:

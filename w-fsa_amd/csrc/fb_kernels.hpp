@@ -476,6 +476,7 @@ struct CompiledArgs {
                              // else: >= 1 w staged in LDS, 0 global
     int32_t wide;
     int32_t with_grad;       // accumulate the (weight-independent) trivial-word gradient
+    int32_t no_slice;        // skip edge_weight_slice (nothing after this launch reads it)
     int32_t no_streams;      // bubbles only (the pipelined QN loop's update chain): no table
                              // staging, no stream pass, no per-edge weight slice
     // bub_on: the stream waves also evaluate the bubbles before their

@@ -167,6 +167,7 @@ struct wfsa_dev {
     DevBuf<double> fixed_grad;       // [n_params] gradient of the trivial words (constant)
     DevBuf<double> fixed_t;          // [qn_n] the same in trimmed order (QN runs)
     bool fixed_t_on = false;
+    bool eval_no_slice = false;      // this evaluation's stream kernel skips edge_weight_slice
     // bubbles
     int32_t n_bubbles = 0, n_small4 = 0, n_small = 0, n_big = 0, big_lds_edges = 2;
     int b_waves = 0;
@@ -1483,6 +1484,7 @@ int enqueue_compiled(wfsa_dev* ctx, bool with_grad, bool want_logq, const unsign
         c.ew_out = ctx->ew.ptr;
         c.erec_out = ctx->erec.ptr;
         c.out = ctx->out.ptr;
+        c.no_slice = (!with_grad && ctx->eval_no_slice) ? 1 : 0;
         c.ll_part = ctx->ll_cur;
         c.logq = want_logq ? ctx->logq.ptr : nullptr;
         c.halted = halted;
@@ -1626,7 +1628,13 @@ int enqueue_evaluation(wfsa_dev* ctx, bool want_logq, const unsigned* halted, in
         if (int rc = enqueue_bubbles(ctx, want_logq, halted, wave_off, ctx->side_stream)) return rc;
         HIP_TRY(hipEventRecord(ctx->join, ctx->side_stream));
     }
-    if (int rc = enqueue_compiled(ctx, false, want_logq, halted, slot)) return rc;
+    // the per-edge weights and the zeroed result are for the traversal
+    // kernels and the reduction: the fused QN step over compiled strings
+    // alone reads neither, so the stream kernel skips writing them
+    ctx->eval_no_slice = !with_tail && ctx->n_fall[0] + ctx->n_fall[1] + ctx->n_fall[2] == 0;
+    const int crc = enqueue_compiled(ctx, false, want_logq, halted, slot);
+    ctx->eval_no_slice = false;
+    if (crc) return crc;
     if (side) HIP_TRY(hipStreamWaitEvent(s, ctx->join, 0));
     if (ctx->n_bubbles > 0 && !side && !fusedb) {
         if (int rc = enqueue_bubbles(ctx, want_logq, halted, wave_off, s)) return rc;
