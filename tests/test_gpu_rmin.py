@@ -138,3 +138,33 @@ def test_rmin_column_in_quasinewton_device_loop(source, monkeypatch):
     assert len(rows) == len(want)
     np.testing.assert_allclose(rows[:, 5], [w[0] for w in want], rtol=1e-9)
     np.testing.assert_array_equal(rows[:, 6], [w[1] for w in want])
+
+
+def test_rmin_column_bitwise_reproducible_on_bubbles():
+    """the fused stream kernel stores each bubble's log(min path / Z) at its
+    list position and the strings kernel sums them per string in bubble order
+    (no atomics): two device-loop runs give the same rmin column bit for bit,
+    equal to the separate rmin pass (host steps) to rounding"""
+    import wfsa_amd as W
+    syn = W.Synthetic(n_states=64, degree=8, vocab=16, emissions=1, n_strings=3000, max_len=64, seed=5)
+    sym, off, wt = syn.corpus()
+    fsa = W.Fsa.read_text(syn.wfsa_text)
+    runs = []
+    for _ in range(2):
+        lrn = W.QuasiNewtonLearner(0)
+        lrn.set_info_rmin(True)
+        lrn.BuildFromPacked(fsa, sym, off, wt)
+        lrn.Finalize()
+        lrn.Init(7)
+        runs.append(np.array(lrn.Run(6, 1.0, -1.0)))
+    assert lrn.stats()["n_bubbles"] > 0 and lrn.stats()["fallback_strings"] == 0
+    assert (runs[0][:, 6] >= 0).all()
+    np.testing.assert_array_equal(runs[0][:, 5:7], runs[1][:, 5:7])
+    host = W.QuasiNewtonLearner(0)
+    host.set_info_rmin(True)
+    host.BuildFromPacked(fsa, sym, off, wt)
+    host.Finalize()
+    host.Init(7)
+    rows = np.array([host.OptimizationStep(1.0, -1.0)[0] for _ in range(6)])
+    np.testing.assert_allclose(rows[:, 5], runs[0][:, 5], rtol=1e-11)
+    np.testing.assert_array_equal(rows[:, 6], runs[0][:, 6])

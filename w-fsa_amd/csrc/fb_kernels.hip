@@ -1524,7 +1524,8 @@ __device__ __forceinline__ void reg_add(double (&r)[N], int i, double v) {
 // A small bubble of class (N nodes, RE edges): quads of bubble b at
 // tbl[k * n + b] -- [header], RE/2 x [(code, sd) x 2], RE/4 x [slot x 4].
 template <int N, int RE, bool RMIN = false>
-__device__ __forceinline__ double small_bubble(const BubbleArgs& a, const int4* __restrict__ tbl, int n, int b) {
+__device__ __forceinline__ double small_bubble(const BubbleArgs& a, const int4* __restrict__ tbl, int n, int b,
+                                               int pos) {
     constexpr int NQ = 1 + RE / 2 + RE / 4;
     int4 q[NQ];
 #pragma unroll
@@ -1572,7 +1573,9 @@ __device__ __forceinline__ double small_bubble(const BubbleArgs& a, const int4* 
 #pragma unroll
                 for (int k = 0; k < N; ++k) B[k] = dst == k ? fmin(B[k], v) : B[k];
             }
-        global_add(&a.rmin_acc[q[0].y], log(reg_get(B, nodes - 1) / Z));
+        const double rv = log(reg_get(B, nodes - 1) / Z);
+        if (a.rmin_sv) a.rmin_sv[pos] = rv;
+        else global_add(&a.rmin_acc[q[0].y], rv);
 #pragma unroll
         for (int k = 0; k < N; ++k) B[k] = 0.0;
     }
@@ -1631,7 +1634,9 @@ __device__ double big_bubble(const BubbleArgs& a, int i, int* lsd, double* lw, d
             for (int v = 0; v < nodes; ++v) B[v] = v == 0 ? 1.0 : INFINITY;
             for (int e = 0; e < edges; ++e)
                 if (lw[e] > 0.0) B[lsd[e] >> 16] = fmin(B[lsd[e] >> 16], B[lsd[e] & 0xffff] * lw[e]);
-            global_add(&a.rmin_acc[rec[1]], log(B[nodes - 1] / Z));
+            const double rv = log(B[nodes - 1] / Z);
+            if (a.rmin_sv) a.rmin_sv[a.n_small4 + a.n_small + i] = rv;
+            else global_add(&a.rmin_acc[rec[1]], rv);
             for (int v = 0; v < nodes; ++v) B[v] = 0.0;
         }
         B[nodes - 1] = 1.0;
@@ -1667,8 +1672,9 @@ __global__ __launch_bounds__(kBubbleBlock) void bubble_kernel(BubbleArgs a) {
     } else {
         // class A (4 nodes / 4 edges: most bubbles) first, then class B
         const int b = (gw - a.n_big) * kWave + lane;
-        if (b < a.n_small4) ll_acc = small_bubble<4, 4, RMIN>(a, a.sm4_tbl, a.n_small4, b);
-        else if (b < a.n_small4 + a.n_small) ll_acc = small_bubble<8, 8, RMIN>(a, a.sm_tbl, a.n_small, b - a.n_small4);
+        if (b < a.n_small4) ll_acc = small_bubble<4, 4, RMIN>(a, a.sm4_tbl, a.n_small4, b, b);
+        else if (b < a.n_small4 + a.n_small)
+            ll_acc = small_bubble<8, 8, RMIN>(a, a.sm_tbl, a.n_small, b - a.n_small4, b);
     }
     ll_acc = wave_sum(ll_acc);
     if (lane == 0) a.ll_part[gw] = ll_acc;
@@ -1763,9 +1769,9 @@ __global__ __launch_bounds__(1024, (DBG == 10 ? 8 : 1)) void fbs_kernel(Compiled
         // block (spread over all CUs)
         if (w < a.bub.small_wpb) {   // small_wpb <= waves per block (bubbles_fused)
             const int b = (bid * a.bub.small_wpb + w) * kWave + lane;
-            if (b < a.bub.n_small4) ll_acc += small_bubble<4, 4, RMIN>(a.bub, a.bub.sm4_tbl, a.bub.n_small4, b);
+            if (b < a.bub.n_small4) ll_acc += small_bubble<4, 4, RMIN>(a.bub, a.bub.sm4_tbl, a.bub.n_small4, b, b);
             else if (b < a.bub.n_small4 + a.bub.n_small)
-                ll_acc += small_bubble<8, 8, RMIN>(a.bub, a.bub.sm_tbl, a.bub.n_small, b - a.bub.n_small4);
+                ll_acc += small_bubble<8, 8, RMIN>(a.bub, a.bub.sm_tbl, a.bub.n_small, b - a.bub.n_small4, b);
         }
         // big bubbles, one wavefront each, from the last blocks' last waves
         // down (the finish wave's rank, nblk - 1, skipped), staged in LDS after w
@@ -2131,6 +2137,8 @@ __global__ __launch_bounds__(kRminBlock) void rmin_strings_kernel(RminArgs a) {
         double r = 0.0;
         if (ent.z < 0) {
             r = a.rmin_log[ent.x];
+        } else if (a.sv) {   // stored per bubble by the evaluation: summed in bubble order
+            for (int b = ent.y; b < ent.y + ent.z; ++b) r += a.sv[a.bpos[b]];
         } else if (!a.vb) {   // accumulated by the evaluation's bubble passes: read, re-arm
             r = a.rmin_log[ent.x];
             a.rmin_log[ent.x] = 0.0;

@@ -258,6 +258,8 @@ struct RminArgs {
     const double* w;         // [n_params + 1] weights (multi-parameter edges)
     const double* ewp;       // [n_params + 1] exp(w)
     double* rmin_log;        // [S] traversal strings' values
+    const double* sv;        // [n_bub] or null: per-bubble values at list positions (BubbleArgs::rmin_sv)
+    const int32_t* bpos;     // [n_bub] list position of bubble b
     const int4* amb;         // [n_amb] (string, first bubble, bubble count | -1 traversal, 0), ascending
     int64_t n_amb;
     double* part;            // [blocks][2]
@@ -442,6 +444,9 @@ struct BubbleArgs {
     double* logq;            // [S] or null: log Z added to the string's entry
     double* rmin_acc;        // [S] or null: log(min path / Z) added to the string's entry (rmin column;
                              // small bubbles only in the RMIN kernel variants)
+    double* rmin_sv;         // [n_bubbles] or null: the same value stored per bubble at its list position
+                             // (small4, small, big) instead of added -- coalesced, summed per string in
+                             // bubble order by rmin_strings_kernel (deterministic)
     const double* w;         // [n_params + 1] weights (GetWeight form) with the zero slot
     const double* ewp;       // [n_params + 1] exp(w), ewp[n_params] = 1 (per iteration)
     const unsigned* halted;

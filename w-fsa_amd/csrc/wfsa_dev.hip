@@ -29,6 +29,7 @@
 #include <memory>
 #include <limits>
 #include <string>
+#include <unordered_map>
 #include <vector>
 
 #include "collective.hpp"
@@ -246,6 +247,9 @@ struct wfsa_dev {
     // rmin info column: per-bubble / per-string logs, block partials, results
     // (two halves: a QN step's finish reads its own while the next step writes)
     DevBuf<double> rm_rs, rm_vb, rm_part, rm_res, rm_key;
+    DevBuf<double> rm_sv;           // [n_bubbles] per-bubble rmin values at list positions (fused kernel)
+    DevBuf<int32_t> rm_bpos;        // [n_bubbles] list position of each bubble
+    bool rm_sv_used = false;        // the last evaluation stored per-bubble values into rm_sv
     double rm_base = 0.0;        // across ranks: global index of this rank's first loaded string
     DevBuf<int4> rm_amb;         // the ambiguous strings (path count > 1) with their bubble runs
     std::vector<int32_t> h_bfirst, h_nbub;   // per string: first bubble ordinal, bubbles (compiled strings)
@@ -1295,6 +1299,17 @@ int prepare(wfsa_dev* ctx, int level) {
                 if (hn[v]) std::fprintf(stderr, " %zu:%lld", v, (long long)hn[v]);
             std::fprintf(stderr, "\n");
         }
+        {   // list position of every bubble (the fused rmin values are stored there)
+            std::unordered_map<int32_t, int32_t> idx_of;
+            idx_of.reserve(h_off.size());
+            for (size_t i = 0; i < h_off.size(); ++i) idx_of[h_off[i]] = int32_t(i);
+            std::vector<int32_t> bpos(h_off.size(), 0);
+            int32_t pos = 0;
+            for (const auto* list : {&small4, &small, &big})
+                for (int32_t o : *list) bpos[size_t(idx_of.at(o))] = pos++;
+            HIP_TRY(ctx->rm_bpos.upload(bpos.data(), bpos.size(), s));
+            HIP_TRY(ctx->rm_sv.alloc(bpos.size()));
+        }
         ctx->h_bubbuf = std::move(h_bubbuf);
         ctx->h_sm4_list = std::move(small4);
         ctx->h_sm_list = std::move(small);
@@ -1493,8 +1508,13 @@ int enqueue_compiled(wfsa_dev* ctx, bool with_grad, bool want_logq, const unsign
             ctx->fin_for_fbs.active = 0;
         }
         size_t lds = with_grad ? ctx->c_lds : ctx->i_lds;
+        ctx->rm_sv_used = false;
         if (!with_grad && bubbles_fused(ctx, want_logq)) {
             c.bub = bubble_args(ctx, false, halted, nullptr);
+            if (c.bub.rmin_acc) {
+                c.bub.rmin_sv = ctx->rm_sv.ptr;
+                ctx->rm_sv_used = true;
+            }
             c.bub_on = 1;
             c.bub.small_wpb = small_waves_per_block(ctx->n_small4 + ctx->n_small, ctx->i_grid);
             if (ctx->n_big > 0) {
@@ -1616,6 +1636,7 @@ int enqueue_evaluation(wfsa_dev* ctx, bool want_logq, const unsigned* halted, in
     // stream beside the stream kernel (not with log q, where both write the
     // strings' entries, nor with bubble atomics into out, which the stream
     // kernel zeroes).
+    ctx->rm_sv_used = false;   // (set by the stream kernel's launch when it stores the bubbles' rmin values)
     const bool side = ctx->n_bubbles > 0 && ctx->side_stream && !want_logq;
     if (side) {
         HIP_TRY(hipEventRecord(ctx->fork, s));
@@ -1779,6 +1800,10 @@ int enqueue_rmin(wfsa_dev* ctx, const unsigned* halted, double* res, int par = 0
     r.n_bub = ctx->n_bubbles;
     r.max_nodes = ctx->max_bub_nodes;
     r.vb = trav_done ? nullptr : ctx->rm_vb.ptr;   // fused: the evaluation accumulated the bubbles
+    if (trav_done && ctx->rm_sv_used) {            // ... or stored them per bubble
+        r.sv = ctx->rm_sv.ptr;
+        r.bpos = ctx->rm_bpos.ptr;
+    }
     r.w = ctx->w_full.ptr;
     r.ewp = ctx->ewp.ptr;
     r.rmin_log = ctx->rm_rs.ptr;
