@@ -141,9 +141,10 @@ def test_rmin_column_in_quasinewton_device_loop(source, monkeypatch):
 
 
 def test_rmin_column_bitwise_reproducible_on_bubbles():
-    """the fused stream kernel stores each bubble's log(min path / Z) at its
-    list position and the strings kernel sums them per string in bubble order
-    (no atomics): two device-loop runs give the same rmin column bit for bit,
+    """the bubble passes (fused into the stream kernel, or the bubble kernel
+    beside it, as here) store each bubble's log(min path / Z) at its list
+    position and the strings kernel sums them per string in bubble order (no
+    atomics): two device-loop runs give the same rmin column bit for bit,
     equal to the separate rmin pass (host steps) to rounding"""
     import wfsa_amd as W
     syn = W.Synthetic(n_states=64, degree=8, vocab=16, emissions=1, n_strings=3000, max_len=64, seed=5)

@@ -1508,7 +1508,6 @@ int enqueue_compiled(wfsa_dev* ctx, bool with_grad, bool want_logq, const unsign
             ctx->fin_for_fbs.active = 0;
         }
         size_t lds = with_grad ? ctx->c_lds : ctx->i_lds;
-        ctx->rm_sv_used = false;
         if (!with_grad && bubbles_fused(ctx, want_logq)) {
             c.bub = bubble_args(ctx, false, halted, nullptr);
             if (c.bub.rmin_acc) {
@@ -1570,7 +1569,12 @@ wfsa::BubbleArgs bubble_args(wfsa_dev* ctx, bool want_logq, const unsigned* halt
 }
 
 int enqueue_bubbles(wfsa_dev* ctx, bool want_logq, const unsigned* halted, int32_t wave_off, hipStream_t s) {
-    HIP_TRY(wfsa::launch_bubbles(bubble_args(ctx, want_logq, halted, ctx->ll_cur + wave_off), s));
+    wfsa::BubbleArgs b = bubble_args(ctx, want_logq, halted, ctx->ll_cur + wave_off);
+    if (b.rmin_acc) {   // the rmin values per bubble, as the fused form stores them
+        b.rmin_sv = ctx->rm_sv.ptr;
+        ctx->rm_sv_used = true;
+    }
+    HIP_TRY(wfsa::launch_bubbles(b, s));
     return WFSA_OK;
 }
 
@@ -1804,6 +1808,9 @@ int enqueue_rmin(wfsa_dev* ctx, const unsigned* halted, double* res, int par = 0
         r.sv = ctx->rm_sv.ptr;
         r.bpos = ctx->rm_bpos.ptr;
     }
+    if (std::getenv("WFSA_RMIN_TRACE"))
+        std::fprintf(stderr, "[rmin] trav_done %d sv %d par %d finish %d\n", int(trav_done), int(r.sv != nullptr), par,
+                     int(q != nullptr));
     r.w = ctx->w_full.ptr;
     r.ewp = ctx->ewp.ptr;
     r.rmin_log = ctx->rm_rs.ptr;
