@@ -402,6 +402,8 @@ struct QnArgs {
     unsigned* halted;            // [0] halted, [1] halt_pending
     QnFinish fin;                // this step's finish (publication of skipped rows)
     int32_t dbg;                 // timing experiments only (WFSA_QN_DBG)
+    int32_t seg_cap;             // LDS capacity: members of the largest constraint (<= kQnMaxSeg; 0: that)
+    int32_t chunk_cap;           // ... and its slot chunks (<= kMaxChunks; 0: that)
 };
 
 // Bubble evaluation.  Contributions (-p_s x edge posterior) go straight to

@@ -93,12 +93,13 @@ __device__ inline void member_sums(const int* cb, int nseg, const double* cp, do
         }
     }
 }
+// cp holds cap chunk sums (kMaxChunks unless the caller sized it smaller)
 template <int NT>
 __device__ void seg_sums(const double* __restrict__ v, const int* sp, const int* cb, int nseg, double* res,
-                         double* cp) {
+                         double* cp, int cap = kMaxChunks) {
     const int t = int(threadIdx.x);
     const int nch = cb[nseg];
-    if (nch <= kMaxChunks) {
+    if (nch <= cap) {
         chunk_sums<NT>(v, nch, cp);
         __syncthreads();
         member_sums<NT>(cb, nseg, cp, res);

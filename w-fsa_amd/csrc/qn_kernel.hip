@@ -38,9 +38,15 @@ template <bool FUSED, int NT = kQnBlock>
 __global__ __launch_bounds__(NT) void qn_step_kernel(QnArgs a) {
     const int t = int(threadIdx.x);
     const int c = int(blockIdx.x);
-    __shared__ double sg[kQnMaxSeg], se[kQnMaxSeg];
-    __shared__ int sp[kQnMaxSeg + 1], cb[kQnMaxSeg + 1], sfo[kQnMaxSeg];
-    __shared__ double cp[kMaxChunks];
+    // LDS sized by the host to the largest constraint (a.seg_cap members,
+    // a.chunk_cap slot chunks), so every block of the grid is resident at once
+    extern __shared__ __attribute__((aligned(16))) double qlds[];
+    double* sg = qlds;
+    double* se = sg + a.seg_cap;
+    double* cp = se + a.seg_cap;
+    int* sp = reinterpret_cast<int*>(cp + a.chunk_cap);
+    int* cb = sp + a.seg_cap + 1;
+    int* sfo = cb + a.seg_cap + 1;
     __shared__ double bc[2], red[kMaxBlockWaves];
     // The loads are issued in dependent rounds (the kernel is a chain of
     // global-memory latencies): the flags with the constraint's extent and its
@@ -74,7 +80,7 @@ __global__ __launch_bounds__(NT) void qn_step_kernel(QnArgs a) {
     if (have) {
         const int nm = e - b;
         double laux;
-        if (nm <= kQnMaxSeg) {
+        if (nm <= a.seg_cap) {
             constexpr int PT = kQnMaxSeg / NT;   // members per thread (at most)
             double xr[PT], ft[PT];
 #pragma unroll
@@ -93,7 +99,7 @@ __global__ __launch_bounds__(NT) void qn_step_kernel(QnArgs a) {
                     sp[i] = a.seg_ptr[b + i];
                     cb[i] = a.chunk_ptr[b + i];
                 }
-            const bool in_lds = slots && gnch <= kMaxChunks;
+            const bool in_lds = slots && gnch <= a.chunk_cap;   // (else more than kMaxChunks: seg_sums from memory)
             if (in_lds) chunk_sums<NT>(a.contrib + gb, gnch, cp);   // the group's chunks, this round
             __syncthreads();
             const int s0 = slots ? sp[0] : 0, c0 = slots ? cb[0] : 0;
@@ -121,7 +127,7 @@ __global__ __launch_bounds__(NT) void qn_step_kernel(QnArgs a) {
                     member_sums<NT>(cb, nm, cp, sg);
                     __syncthreads();
                 } else {
-                    seg_sums<NT>(a.contrib + gb, sp, cb, nm, sg, cp);
+                    seg_sums<NT>(a.contrib + gb, sp, cb, nm, sg, cp, a.chunk_cap);
                 }
             }
 #pragma unroll
@@ -231,15 +237,19 @@ hipError_t launch_qn_step(const QnArgs& a_in, bool fused, hipStream_t stream) {
     }();
     QnArgs a = a_in;
     a.dbg = dbg;
+    if (a.seg_cap <= 0 || a.seg_cap > kQnMaxSeg) a.seg_cap = kQnMaxSeg;
+    if (a.chunk_cap <= 0 || a.chunk_cap > kMaxChunks) a.chunk_cap = kMaxChunks;
+    const size_t lds = (2 * size_t(a.seg_cap) + size_t(a.chunk_cap)) * sizeof(double) +
+                       (3 * size_t(a.seg_cap) + 2) * sizeof(int);
     const dim3 grid(unsigned(std::max(a.k, 1)));
     static const int nt = [] {   // (experiments: WFSA_QN_BLOCK = 128 / 256)
         const char* e = std::getenv("WFSA_QN_BLOCK");
         return e && std::atoi(e) == 128 ? 128 : (e && std::atoi(e) == 512 ? 512 : kQnBlock);
     }();
-    if (fused && nt == 128) hipLaunchKernelGGL((qn_step_kernel<true, 128>), grid, dim3(128), 0, stream, a);
-    else if (fused && nt == 512) hipLaunchKernelGGL((qn_step_kernel<true, 512>), grid, dim3(512), 0, stream, a);
-    else if (fused) hipLaunchKernelGGL((qn_step_kernel<true>), grid, dim3(kQnBlock), 0, stream, a);
-    else hipLaunchKernelGGL((qn_step_kernel<false>), grid, dim3(kQnBlock), 0, stream, a);
+    if (fused && nt == 128) hipLaunchKernelGGL((qn_step_kernel<true, 128>), grid, dim3(128), lds, stream, a);
+    else if (fused && nt == 512) hipLaunchKernelGGL((qn_step_kernel<true, 512>), grid, dim3(512), lds, stream, a);
+    else if (fused) hipLaunchKernelGGL((qn_step_kernel<true>), grid, dim3(kQnBlock), lds, stream, a);
+    else hipLaunchKernelGGL((qn_step_kernel<false>), grid, dim3(kQnBlock), lds, stream, a);
     return hipGetLastError();
 }
 

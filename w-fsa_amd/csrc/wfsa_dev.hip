@@ -169,6 +169,8 @@ struct wfsa_dev {
     DevBuf<double> fixed_t;          // [qn_n] the same in trimmed order (QN runs)
     bool fixed_t_on = false;
     bool eval_no_slice = false;      // this evaluation's stream kernel skips edge_weight_slice
+    int32_t lead_grp_nch = 1;        // chunks of the largest constraint-led slot group
+    int32_t qn_max_nm = 1;           // members of the largest constraint
     // bubbles
     int32_t n_bubbles = 0, n_small4 = 0, n_small = 0, n_big = 0, big_lds_edges = 2;
     int b_waves = 0;
@@ -896,6 +898,9 @@ int layout_slots(wfsa_dev* ctx, const std::vector<int32_t>& pos_of) {
         std::vector<int32_t> gn(size_t(std::max(ng, 1)), 0);
         for (int32_t g = 0; g < ng; ++g) gn[size_t(g)] = cptr_pos[size_t(gp[size_t(g) + 1])] - cptr_pos[size_t(gp[size_t(g)])];
         HIP_TRY(ctx->grp_nch.upload(gn.data(), gn.size(), s));
+        ctx->lead_grp_nch = 1;   // the largest constraint-led group's chunk count (the QN step's LDS)
+        for (size_t g = 0; g + 1 < ctx->slot_groups.size() && int32_t(g) < ng; ++g)
+            ctx->lead_grp_nch = std::max(ctx->lead_grp_nch, gn[g]);
     }
     HIP_TRY(ctx->chunk_ptr.upload(cptr_pos.data(), cptr_pos.size(), s));
     HIP_TRY(ctx->seg_ptr.upload(pc.data(), pc.size(), s));
@@ -1910,6 +1915,8 @@ int enqueue_qn_step(wfsa_dev* ctx, double eta, double tol, int64_t e, bool timed
     q.eta = eta;
     q.exp_lambda = ctx->qn_exp_lambda;
     q.halted = ctx->qn_halted.ptr;
+    q.seg_cap = ctx->qn_max_nm;
+    q.chunk_cap = (fused && ctx->n_bubbles > 0) ? std::min(ctx->lead_grp_nch, wfsa::kMaxChunks) : 1;
     f.partial = ctx->qn_partial.ptr;
     f.n_blocks = std::max(ctx->qn_k, 1);
     f.k = ctx->qn_k;
@@ -2041,6 +2048,8 @@ int enqueue_qn_step_piped(wfsa_dev* ctx, double eta, double tol, int64_t e, bool
     q.eta = eta;
     q.exp_lambda = ctx->qn_exp_lambda;
     q.halted = ctx->qn_halted.ptr;
+    q.seg_cap = ctx->qn_max_nm;
+    q.chunk_cap = ctx->n_bubbles > 0 ? std::min(ctx->lead_grp_nch, wfsa::kMaxChunks) : 1;
     f.out0 = ctx->out.ptr;
     f.ll_part = ctx->ll_cur;
     f.n_ll = ctx->i_grid + (ctx->n_bubbles == 0 ? 0 : bub_fused ? ctx->i_grid : ctx->b_waves);
@@ -2680,6 +2689,7 @@ int wfsa_dev_qn_setup(wfsa_dev* ctx, const wfsa_qn_desc* d) {
     int32_t max_nm = 0;
     for (int32_t c = 0; c < k; ++c) max_nm = std::max(max_nm, cptr[size_t(c) + 1] - cptr[size_t(c)]);
     ctx->qn_fused = max_nm <= wfsa::kQnMaxSeg && !ctx->comm;
+    ctx->qn_max_nm = std::max(1, std::min(max_nm, wfsa::kQnMaxSeg));
     if (ctx->qn_fused) {
         std::vector<int32_t> pos_of(size_t(nf), -1);
         for (int32_t i = 0; i < n; ++i) pos_of[size_t(full_of[size_t(i)])] = i;
