@@ -613,6 +613,7 @@ void DensePath::free_corpus() {
 
 hipError_t DensePath::load_model(const DenseModel& m, hipStream_t s) {
     if (const char* e = std::getenv("WFSA_DENSE_GRAD_CFG")) grad_cfg_ = std::atoi(e);   // timing experiments
+    if (const char* e = std::getenv("WFSA_DENSE_STEP_CFG")) step_cfg_ = std::atoi(e);
     free_corpus();
     free_model();
     n_params_ = m.n_params;
@@ -812,7 +813,9 @@ hipError_t DensePath::enqueue(const double* ewp, bool structural, double* out, d
         f.out = alpha_ + size_t(t + 1) * step;
         f.la_in = t < 0 ? la_ : la_ + size_t(t) * R;
         f.la_out = la_ + size_t(t + 1) * R;
-        dense_gemm_kernel<FWD, kBkStep, kNwStep><<<fb_blocks, kNwStep * 64, 0, s>>>(f);
+        if (step_cfg_ == 1) dense_gemm_kernel<FWD, kBkStep, 4><<<fb_blocks, 4 * 64, 0, s>>>(f);
+        else if (step_cfg_ == 2) dense_gemm_kernel<FWD, kBkGrad, kNwStep><<<fb_blocks, kNwStep * 64, 0, s>>>(f);
+        else dense_gemm_kernel<FWD, kBkStep, kNwStep><<<fb_blocks, kNwStep * 64, 0, s>>>(f);
         DTRY(hipGetLastError());
     }
     {
@@ -841,7 +844,9 @@ hipError_t DensePath::enqueue(const double* ewp, bool structural, double* out, d
         b.alpha_t = alpha_ + size_t(t) * step;
         b.gam = gam_ + size_t(t) * step;
         b.z = z_ + size_t(t) * step;
-        dense_gemm_kernel<BWD, kBkStep, kNwStep><<<fb_blocks, kNwStep * 64, 0, s>>>(b);
+        if (step_cfg_ == 1) dense_gemm_kernel<BWD, kBkStep, 4><<<fb_blocks, 4 * 64, 0, s>>>(b);
+        else if (step_cfg_ == 2) dense_gemm_kernel<BWD, kBkGrad, kNwStep><<<fb_blocks, kNwStep * 64, 0, s>>>(b);
+        else dense_gemm_kernel<BWD, kBkStep, kNwStep><<<fb_blocks, kNwStep * 64, 0, s>>>(b);
         DTRY(hipGetLastError());
     }
     if (T_ >= 2) {
