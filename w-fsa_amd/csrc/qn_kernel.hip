@@ -116,26 +116,43 @@ __global__ __launch_bounds__(NT) void qn_step_kernel(QnArgs a) {
                 }
                 gp[i] = gi;
             }
-            if (slots) {
-                __syncthreads();   // every sp read as absolute above
-                for (int i = t; i <= nm; i += NT) {
-                    sp[i] -= s0;
-                    cb[i] -= c0;
+            if (in_lds) {   // each thread its members' chunk sums, in chunk order (member_sums' order)
+#pragma unroll
+                for (int i = 0; i < PT; ++i) {
+                    const int m = t + i * NT;
+                    if (m < nm) {
+                        const int q0 = cb[m] - c0, q1 = cb[m + 1] - c0;
+                        double sm = 0.0;
+                        int q = q0;
+                        for (; q + 8 <= q1; q += 8) {
+                            double y[8];
+#pragma unroll
+                            for (int k = 0; k < 8; ++k) y[k] = cp[q + k];
+#pragma unroll
+                            for (int k = 0; k < 8; ++k) sm += y[k];
+                        }
+                        for (; q < q1; ++q) sm += cp[q];
+                        sg[m] = gp[i] + sm;
+                        se[m] = exp(xr[i]);
+                    }
                 }
-                __syncthreads();
-                if (in_lds) {
-                    member_sums<NT>(cb, nm, cp, sg);
+            } else {
+                if (slots) {
+                    __syncthreads();   // every sp read as absolute above
+                    for (int i = t; i <= nm; i += NT) {
+                        sp[i] -= s0;
+                        cb[i] -= c0;
+                    }
                     __syncthreads();
-                } else {
                     seg_sums<NT>(a.contrib + gb, sp, cb, nm, sg, cp, a.chunk_cap);
                 }
-            }
 #pragma unroll
-            for (int i = 0; i < PT; ++i) {
-                const int m = t + i * NT;
-                if (m < nm) {
-                    sg[m] = slots ? gp[i] + sg[m] : gp[i];
-                    se[m] = exp(xr[i]);
+                for (int i = 0; i < PT; ++i) {
+                    const int m = t + i * NT;
+                    if (m < nm) {
+                        sg[m] = slots ? gp[i] + sg[m] : gp[i];
+                        se[m] = exp(xr[i]);
+                    }
                 }
             }
             __syncthreads();
@@ -197,7 +214,8 @@ __global__ __launch_bounds__(NT) void qn_step_kernel(QnArgs a) {
             a.lambda[c] = a.exp_lambda ? lam * exp(-a.eta * (d / lam)) : lam - a.eta * d;
         }
     }
-    gerr = block_reduce(gerr, 1, red);
+    // (max is exact in any order: members in wave 0 alone need no block barrier)
+    gerr = (e - b <= 64) ? wave_reduce(gerr, 1) : block_reduce(gerr, 1, red);
     if (t == 0) {   // the block's partial for the step's finish (a later launch)
         double4 pv;
         pv.x = have ? g : INFINITY;
