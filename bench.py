@@ -348,12 +348,16 @@ def boundary_steps(m, k):
     for _ in range(3):
         lrn.OptimizationStep(1.0, -1.0)
     m["barrier"]()
+    s0 = lrn.stats()
     t0 = time.perf_counter()
     for _ in range(k):
         lrn.OptimizationStep(1.0, -1.0)
     m["barrier"]()
     dt = time.perf_counter() - t0
+    s1 = lrn.stats()
+    host = {f: (s1[f] - s0[f]) / k for f in ("host_begin_ms", "host_overlap_ms", "host_wait_ms", "host_post_ms")}
     return {"ms_per_step": dt * 1e3 / k, "value": m["info"]["n_strings"] * k / dt, "steps": k,
+            "host_ms_per_step": host,
             "note": "QuasiNewtonLearner::OptimizationStep through the C ABI a maintainer binds (wfsa_dev_objective_grad: "
                     "host weights in over PCIe, [LL, grad] out, the QN update on the host)"}
 
