@@ -52,6 +52,7 @@ __global__ __launch_bounds__(NT) void qn_step_kernel(QnArgs a) {
     // global-memory latencies): the flags with the constraint's extent and its
     // slot group; its members' slot runs, full indices and x together with the
     // group's slot chunks; the members' constant gradient parts.
+    if (a.dbg == 3) return;   // (timing experiments: the launch alone)
     const bool have = c < a.k;
     const bool slots = FUSED && a.contrib;
     int b = 0, e = 0, gnch = 0;
@@ -259,7 +260,11 @@ hipError_t launch_qn_step(const QnArgs& a_in, bool fused, hipStream_t stream) {
     if (a.chunk_cap <= 0 || a.chunk_cap > kMaxChunks) a.chunk_cap = kMaxChunks;
     const size_t lds = (2 * size_t(a.seg_cap) + size_t(a.chunk_cap)) * sizeof(double) +
                        (3 * size_t(a.seg_cap) + 2) * sizeof(int);
-    const dim3 grid(unsigned(std::max(a.k, 1)));
+    dim3 grid(unsigned(std::max(a.k, 1)));
+    if (dbg == 4) {   // (timing experiments: an empty launch of a quarter of the blocks)
+        grid = dim3(unsigned(std::max((a.k + 3) / 4, 1)));
+        a.dbg = 3;
+    }
     static const int nt = [] {   // (experiments: WFSA_QN_BLOCK = 128 / 256)
         const char* e = std::getenv("WFSA_QN_BLOCK");
         return e && std::atoi(e) == 128 ? 128 : (e && std::atoi(e) == 512 ? 512 : kQnBlock);
