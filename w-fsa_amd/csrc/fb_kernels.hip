@@ -2077,15 +2077,6 @@ hipError_t launch_trav(TravMode mode, const TravArgs& a, int grid, hipStream_t s
     return hipGetLastError();
 }
 
-// rmin column (fb_kernels.hpp RminArgs).  (value, index) minimum, ties to
-// the lower index.
-__device__ __forceinline__ void min_pair(double& v, double& i, double v2, double i2) {
-    if (v2 < v || (v2 == v && i2 < i)) {
-        v = v2;
-        i = i2;
-    }
-}
-
 // Lane per bubble, 64-lane blocks: sum forward and (min, x) forward over the
 // bubble's topologically listed edges with the node vectors in LDS
 // ([node][lane], conflict-free); the min path never exceeds the sum, so both
@@ -2123,42 +2114,11 @@ __global__ __launch_bounds__(64) void rmin_bubble_kernel(RminArgs a) {
     a.vb[b] = log(sM[nodes - 1][lane] / sA[nodes - 1][lane]);
 }
 
-// Lane per ambiguous string: a compiled string sums its run of bubbles in
-// order (deterministic), a traversal string's value is already in rmin_log;
-// block minima to part[].
+// Lane per ambiguous string (rmin_strings_block, qn_device.hpp): block minima to part[].
 __global__ __launch_bounds__(kRminBlock) void rmin_strings_kernel(RminArgs a) {
     if (a.halted && *a.halted) return;
     __shared__ double wv[kRminBlock / kWave], wi[kRminBlock / kWave];
-    const int lane = int(threadIdx.x);
-    const int64_t i = int64_t(blockIdx.x) * kRminBlock + lane;
-    double v = INFINITY, idx = -1.0;
-    if (i < a.n_amb) {
-        const int4 ent = a.amb[i];   // (string, first bubble, bubble count or -1, 0)
-        double r = 0.0;
-        if (ent.z < 0) {
-            r = a.rmin_log[ent.x];
-        } else if (a.sv) {   // stored per bubble by the evaluation: summed in bubble order
-            for (int b = ent.y; b < ent.y + ent.z; ++b) r += a.sv[a.bpos[b]];
-        } else if (!a.vb) {   // accumulated by the evaluation's bubble passes: read, re-arm
-            r = a.rmin_log[ent.x];
-            a.rmin_log[ent.x] = 0.0;
-        } else {
-            for (int b = ent.y; b < ent.y + ent.z; ++b) r += a.vb[b];
-        }
-        v = r;
-        idx = double(ent.x);
-    }
-    for (int o = 32; o > 0; o >>= 1) min_pair(v, idx, __shfl_xor(v, o, 64), __shfl_xor(idx, o, 64));
-    if ((lane & 63) == 0) {
-        wv[lane >> 6] = v;
-        wi[lane >> 6] = idx;
-    }
-    __syncthreads();
-    if (lane == 0) {
-        for (int k = 1; k < kRminBlock / kWave; ++k) min_pair(v, idx, wv[k], wi[k]);
-        a.part[2 * blockIdx.x] = v;
-        a.part[2 * blockIdx.x + 1] = idx;
-    }
+    rmin_strings_block(a, int(blockIdx.x), wv, wi);
 }
 
 // the block minima -> res (a second launch: the kernel boundary orders the

@@ -404,6 +404,8 @@ struct QnArgs {
     int32_t dbg;                 // timing experiments only (WFSA_QN_DBG)
     int32_t seg_cap;             // LDS capacity: members of the largest constraint (<= kQnMaxSeg; 0: that)
     int32_t chunk_cap;           // ... and its slot chunks (<= kMaxChunks; 0: that)
+    RminArgs rm;                 // rm_on: the rmin strings pass folded into this launch (its block c runs
+    int32_t rm_on, rm_blocks;    // the pass's block c, c < rm_blocks; the grid covers both)
 };
 
 // Bubble evaluation.  Contributions (-p_s x edge posterior) go straight to

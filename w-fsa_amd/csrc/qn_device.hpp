@@ -131,6 +131,54 @@ __device__ inline void qn_publish_row(const QnFinish& f, const double* info, uns
 
 constexpr int kMaxBlockWaves = 16;
 
+// rmin column (fb_kernels.hpp RminArgs).  (value, index) minimum, ties to
+// the lower index.
+__device__ __forceinline__ void min_pair(double& v, double& i, double v2, double i2) {
+    if (v2 < v || (v2 == v && i2 < i)) {
+        v = v2;
+        i = i2;
+    }
+}
+
+// Block bid of the rmin strings pass (kRminBlock threads): lane per ambiguous
+// string -- a compiled string sums its run of bubbles in order
+// (deterministic), a traversal string's value is already in rmin_log -- and
+// the block minimum to part[2 bid].  Run by rmin_strings_kernel, or folded
+// into the QN step kernel's blocks (QnArgs::rm_on).  wv, wi: LDS, one per wave.
+__device__ inline void rmin_strings_block(const RminArgs& a, int bid, double* wv, double* wi) {
+    const int lane = int(threadIdx.x);
+    const int64_t i = int64_t(bid) * kRminBlock + lane;
+    double v = INFINITY, idx = -1.0;
+    if (i < a.n_amb) {
+        const int4 ent = a.amb[i];   // (string, first bubble, bubble count or -1, 0)
+        double r = 0.0;
+        if (ent.z < 0) {
+            r = a.rmin_log[ent.x];
+        } else if (a.sv) {   // stored per bubble by the evaluation: summed in bubble order
+            for (int b = ent.y; b < ent.y + ent.z; ++b) r += a.sv[a.bpos[b]];
+        } else if (!a.vb) {   // accumulated by the evaluation's bubble passes: read, re-arm
+            r = a.rmin_log[ent.x];
+            a.rmin_log[ent.x] = 0.0;
+        } else {
+            for (int b = ent.y; b < ent.y + ent.z; ++b) r += a.vb[b];
+        }
+        v = r;
+        idx = double(ent.x);
+    }
+    for (int o = 32; o > 0; o >>= 1) min_pair(v, idx, __shfl_xor(v, o, 64), __shfl_xor(idx, o, 64));
+    if ((lane & 63) == 0) {
+        wv[lane >> 6] = v;
+        wi[lane >> 6] = idx;
+    }
+    __syncthreads();
+    if (lane == 0) {
+        for (int k = 1; k < kRminBlock / 64; ++k) min_pair(v, idx, wv[k], wi[k]);
+        a.part[2 * bid] = v;
+        a.part[2 * bid + 1] = idx;
+    }
+    __syncthreads();   // (wv, wi reused by the caller)
+}
+
 // block-wide reduction by a fixed tree (every thread gets the result);
 // red: kMaxBlockWaves doubles of LDS
 __device__ inline double block_reduce(double v, int op, double* red) {

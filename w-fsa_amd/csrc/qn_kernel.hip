@@ -76,6 +76,11 @@ __global__ __launch_bounds__(NT) void qn_step_kernel(QnArgs a) {
         }
         return;
     }
+    if (a.rm_on && c < a.rm_blocks) {   // the rmin strings pass's block c (one launch fewer per step)
+        static_assert(kRminBlock == kQnBlock, "the folded rmin pass runs in the QN step's blocks");
+        rmin_strings_block(a.rm, c, red, red + kMaxBlockWaves / 2);
+    }
+    if (c >= max(a.k, 1)) return;   // (blocks beyond the constraints: the rmin pass only)
     if (a.dbg == 1) return;   // (timing experiments, WFSA_QN_DBG: the launch and first round only)
     double gerr = 0.0, g = 0.0;
     if (have) {
@@ -260,7 +265,7 @@ hipError_t launch_qn_step(const QnArgs& a_in, bool fused, hipStream_t stream) {
     if (a.chunk_cap <= 0 || a.chunk_cap > kMaxChunks) a.chunk_cap = kMaxChunks;
     const size_t lds = (2 * size_t(a.seg_cap) + size_t(a.chunk_cap)) * sizeof(double) +
                        (3 * size_t(a.seg_cap) + 2) * sizeof(int);
-    dim3 grid(unsigned(std::max(a.k, 1)));
+    dim3 grid(unsigned(std::max({a.k, 1, a.rm_on ? a.rm_blocks : 0})));
     if (dbg == 4) {   // (timing experiments: an empty launch of a quarter of the blocks)
         grid = dim3(unsigned(std::max((a.k + 3) / 4, 1)));
         a.dbg = 3;

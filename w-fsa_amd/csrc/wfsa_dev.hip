@@ -1778,7 +1778,7 @@ int combine_rmin(wfsa_dev* ctx, double* res, hipStream_t s) {
 }
 
 int enqueue_rmin(wfsa_dev* ctx, const unsigned* halted, double* res, int par = 0, wfsa::QnFinish* q = nullptr,
-                 bool trav_done = false) {
+                 bool trav_done = false, wfsa::QnArgs* fold = nullptr) {
     hipStream_t s = ctx->stream;
     if (ctx->mpath) {
         HIP_TRY(ctx->mpath->enqueue_rmin(res, halted, s));
@@ -1825,7 +1825,13 @@ int enqueue_rmin(wfsa_dev* ctx, const unsigned* halted, double* res, int par = 0
     r.part = ctx->rm_part.ptr + size_t(par) * 2 * size_t(nb);
     r.res = res;
     r.halted = halted;
-    HIP_TRY(wfsa::launch_rmin(r, s, q == nullptr));
+    if (fold && q && trav_done && !r.vb) {   // the strings pass rides in the QN step kernel's blocks
+        fold->rm = r;
+        fold->rm_on = 1;
+        fold->rm_blocks = wfsa::rmin_blocks(ctx->rm_n_amb);
+    } else {
+        HIP_TRY(wfsa::launch_rmin(r, s, q == nullptr));
+    }
     if (q) {   // the step's finish reduces the block minima (one launch fewer per step)
         q->rmin_part = r.part;
         q->rmin_n_part = nb;
@@ -1929,6 +1935,10 @@ int enqueue_qn_step(wfsa_dev* ctx, double eta, double tol, int64_t e, bool timed
     f.host_flag = ctx->flag_dev;
     f.host_ring = ctx->qn_ring_dev;
     if (ctx->qn_rmin) {
+        static const bool fold_rmin = [] {   // WFSA_RMIN_FOLD=0: the strings pass as its own launch
+            const char* e = std::getenv("WFSA_RMIN_FOLD");
+            return !(e && e[0] == '0');
+        }();
         double* res = ctx->rm_res.ptr + 2 * par;
         if (ctx->mpath) {
             if (int rc = enqueue_rmin(ctx, ctx->qn_halted.ptr, res)) return rc;
@@ -1937,7 +1947,7 @@ int enqueue_qn_step(wfsa_dev* ctx, double eta, double tol, int64_t e, bool timed
             if (int rc = enqueue_rmin(ctx, ctx->qn_halted.ptr, res, par, nullptr, true)) return rc;
             if (int rc = combine_rmin(ctx, res, s)) return rc;
             f.rmin = res;
-        } else if (int rc = enqueue_rmin(ctx, ctx->qn_halted.ptr, res, par, &f, true)) {
+        } else if (int rc = enqueue_rmin(ctx, ctx->qn_halted.ptr, res, par, &f, true, fold_rmin ? &q : nullptr)) {
             return rc;
         }
     }
