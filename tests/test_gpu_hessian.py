@@ -287,3 +287,36 @@ def test_hessian_learner_epochs_match_restatement(case, kkt, flags, monkeypatch)
             assert np.isinf(res[4])
         else:
             np.testing.assert_allclose(res[4], want_res[4], rtol=1e-8, atol=1e-10)
+
+
+def test_hessian_learner_sparse_and_dense_kkt_agree(monkeypatch):
+    """a mid-size sparse family (n + k > 1024, so the host-dense size is
+    exceeded): the default choice between the sparse LDL^T and the dense
+    factorisation in HBM against WFSA_KKT=device -- the same epochs (inertia
+    exactly, the rest to rounding) and the same Result vector"""
+    import wfsa_amd as W
+    syn = W.Synthetic(n_states=256, degree=8, vocab=64, emissions=1, n_strings=20000, max_len=64, seed=2)
+    sym, off, wt = syn.corpus()
+    fsa = W.Fsa.read_text(syn.wfsa_text)
+
+    def run(kkt):
+        monkeypatch.setenv("WFSA_KKT", kkt)
+        lrn = W.HessianLearner(0)
+        lrn.BuildFromPacked(fsa, sym, off, wt)
+        lrn.Finalize()
+        inf = lrn.info()
+        rows = np.array(lrn.run(flags=31, epochs=4, tol=1e-12))
+        lrn.Renormalize()
+        return inf, rows, np.array(lrn.result())
+
+    inf, ra, resa = run("")
+    assert inf["n_params"] + inf["n_constraints"] > 1024
+    _, rb, resb = run("device")
+    assert ra.shape == rb.shape
+    np.testing.assert_allclose(ra[:, 0], rb[:, 0], rtol=1e-10)
+    np.testing.assert_allclose(ra[:, 1:4], rb[:, 1:4], rtol=1e-6, atol=1e-10)
+    np.testing.assert_array_equal(ra[:, 4:6], rb[:, 4:6])
+    keep = [0, 1, 2, 3, 5, 6, 7]
+    np.testing.assert_allclose(resa[keep], resb[keep], rtol=1e-9, atol=1e-12)
+    if np.isfinite(resb[4]):
+        np.testing.assert_allclose(resa[4], resb[4], rtol=1e-8)
