@@ -105,7 +105,6 @@ constexpr int kWave = 64;
 constexpr int kGradBlock = 64;   // the preparation-time gradient pass: one wavefront per block
 constexpr int kIterWavesPerCu = 16;   // per-iteration stream kernel
 constexpr int kQnDepth = 8;   // device-resident QN steps in flight
-constexpr int kTimingStride = 4;   // QN runs time every 4th step's kernels
 
 // weights after the results in the host-mapped buffer, 16-byte aligned
 inline size_t weights_off(int32_t np) { return (size_t(np) + 3) & ~size_t(1); }
@@ -121,6 +120,10 @@ struct wfsa_dev {
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     // per in-flight step: before the stream kernel, after it, after the tail
     hipEvent_t k0[kQnDepth] = {}, kc[kQnDepth] = {}, k2[kQnDepth] = {};
+    // nothing was enqueued between kc and the tail's end: k2 is kc (each
+    // timing marker costs the step ~1 us, profiles/r02/v23_timing_ab.txt)
+    bool k2_kc[kQnDepth] = {};
+    int timing_stride = 16;   // QN runs time every 16th step's kernels (WFSA_TIMING_STRIDE)
 
     // model
     bool has_model = false;
@@ -720,6 +723,7 @@ size_t big_stage_off(const wfsa_dev* ctx) { return (ctx->i_lds + 15) & ~size_t(1
 // WFSA_TIMING=0 leaves them all out).  An event between two kernels costs a
 // few microseconds of idle device, so QN runs time a sample of their steps.
 hipError_t record(wfsa_dev* ctx, hipEvent_t* evs, int slot, hipStream_t s) {
+    if (evs == ctx->k2 && slot >= 0) ctx->k2_kc[slot] = false;
     return ctx->kernel_timing && slot >= 0 ? hipEventRecord(evs[slot], s) : hipSuccess;
 }
 
@@ -740,7 +744,7 @@ int collect_timing(wfsa_dev* ctx) {
     float c_ms = 0.f, fb_ms = 0.f, all_ms = 0.f;
     if (!ctx->graph_exec && ctx->kernel_timing) {   // events inside a captured graph are not timeable
         HIP_TRY(hipEventElapsedTime(&c_ms, ctx->k0[0], ctx->kc[0]));
-        HIP_TRY(hipEventElapsedTime(&fb_ms, ctx->k0[0], ctx->k2[0]));
+        HIP_TRY(hipEventElapsedTime(&fb_ms, ctx->k0[0], ctx->k2_kc[0] ? ctx->kc[0] : ctx->k2[0]));
     }
     HIP_TRY(hipEventElapsedTime(&all_ms, ctx->ev0, ctx->ev1));
     const double fb = double(fb_ms);
@@ -1713,7 +1717,10 @@ int enqueue_evaluation(wfsa_dev* ctx, bool want_logq, const unsigned* halted, in
     }
     if (n_ll) *n_ll = wave_off;
     if (!with_tail) {
-        HIP_TRY(record(ctx, ctx->k2, slot, s));
+        const bool after_kc = side || (ctx->n_bubbles > 0 && !fusedb) || ctx->n_fall[0] || ctx->n_fall[1] ||
+                              ctx->n_fall[2] || w2_covers_01;
+        if (!after_kc && slot >= 0) ctx->k2_kc[slot] = true;
+        else HIP_TRY(record(ctx, ctx->k2, slot, s));
         return WFSA_OK;
     }
     HIP_TRY(wfsa::launch_reduce(reduce_args(ctx, halted, wave_off), s));
@@ -2228,6 +2235,7 @@ int wfsa_dev_create(int device, wfsa_dev** out) {
     ctx->n_cu = prop.multiProcessorCount > 0 ? prop.multiProcessorCount : kNumCu;
     if (const char* e = std::getenv("WFSA_GRAPH")) ctx->use_graph = e[0] == '1';
     if (const char* e = std::getenv("WFSA_TIMING")) ctx->kernel_timing = e[0] != '0';
+    if (const char* e = std::getenv("WFSA_TIMING_STRIDE")) ctx->timing_stride = std::max(1, std::atoi(e));
     if (const char* e = std::getenv("WFSA_FUSE_BUBBLES")) ctx->fuse_bubbles = e[0] != '0';
     if (const char* e = std::getenv("WFSA_DENSE"); e && e[0]) ctx->dense_mode = e[0] == '0' ? 0 : 1;
     if (const char* e = std::getenv("WFSA_TIER2")) ctx->force_tier2 = e[0] == '1';
@@ -2792,8 +2800,8 @@ int wfsa_dev_qn_run(wfsa_dev* ctx, double eta, double tol, int32_t max_steps, do
     int64_t timed = 0;
     while (done < max_steps) {
         while (!stop && enq < max_steps && enq - done < kQnDepth) {
-            if (int rc = piped ? enqueue_qn_step_piped(ctx, eta, tol, enq, enq % kTimingStride == 0)
-                               : enqueue_qn_step(ctx, eta, tol, enq, enq % kTimingStride == 0))
+            const bool tm = enq % ctx->timing_stride == 0;
+            if (int rc = piped ? enqueue_qn_step_piped(ctx, eta, tol, enq, tm) : enqueue_qn_step(ctx, eta, tol, enq, tm))
                 return rc;
             ++enq;
             ++ctx->seq;
@@ -2805,11 +2813,12 @@ int wfsa_dev_qn_run(wfsa_dev* ctx, double eta, double tol, int32_t max_steps, do
         const int slot = done % kQnDepth;
         const double* row = ctx->qn_ring + size_t(slot) * wfsa::kQnRow;
         const unsigned rs = unsigned(row[7]);
-        if (ctx->kernel_timing && done % kTimingStride == 0) {
+        if (ctx->kernel_timing && done % ctx->timing_stride == 0) {
             float c = 0.f, f = 0.f;
-            if (hipEventSynchronize(ctx->k2[slot]) == hipSuccess &&
+            const hipEvent_t end = ctx->k2_kc[slot] ? ctx->kc[slot] : ctx->k2[slot];
+            if (hipEventSynchronize(end) == hipSuccess &&
                 hipEventElapsedTime(&c, ctx->k0[slot], ctx->kc[slot]) == hipSuccess &&
-                hipEventElapsedTime(&f, ctx->k0[slot], ctx->k2[slot]) == hipSuccess) {
+                hipEventElapsedTime(&f, ctx->k0[slot], end) == hipSuccess) {
                 c_ms_sum += c;
                 fb_ms_sum += f;
                 ++timed;
