@@ -54,7 +54,7 @@ __global__ __launch_bounds__(NT) void qn_step_kernel(QnArgs a) {
     // group's slot chunks; the members' constant gradient parts.
     if (a.dbg == 3) return;   // (timing experiments: the launch alone)
     const bool have = c < a.k;
-    const bool slots = FUSED && a.contrib;
+    const bool slots = FUSED && a.contrib && a.dbg != 5;   // (5: timing experiments, no slot sums)
     int b = 0, e = 0, gnch = 0;
     int64_t gb = 0;
     double lam = 0.0;
