@@ -594,6 +594,9 @@ hipError_t launch_gather(const double* src, const int32_t* idx, int32_t n, doubl
 hipError_t launch_qn_finish(const QnFinish& f, hipStream_t stream);
 hipError_t launch_qn_weights(const double* x, const int32_t* trim, int32_t n_full, double* w_full, double* ewp,
                              hipStream_t stream);
+// n doubles src -> dst by a kernel (host-mapped memory on either side: no
+// staging copy of pageable memory)
+hipError_t launch_copy(const double* src, double* dst, int64_t n, hipStream_t stream);
 hipError_t launch_edge_weights(const double* w_full, const int32_t* pptr, const int32_t* pidx, double* lw,
                                double* ew, EdgeRec* erec, int64_t n_edges, double* out, int64_t n_out,
                                hipStream_t stream);

@@ -281,6 +281,11 @@ hipError_t launch_qn_step(const QnArgs& a_in, bool fused, hipStream_t stream) {
     return hipGetLastError();
 }
 
+__global__ void copy_kernel(const double* __restrict__ src, double* __restrict__ dst, int64_t n) {
+    const int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+    if (i < n) dst[i] = src[i];
+}
+
 __global__ void gather_kernel(const double* src, const int32_t* idx, int32_t n, double* dst) {
     const int i = int(blockIdx.x * blockDim.x + threadIdx.x);
     if (i < n) dst[i] = src[idx[i]];
@@ -294,6 +299,12 @@ hipError_t launch_gather(const double* src, const int32_t* idx, int32_t n, doubl
 
 hipError_t launch_qn_finish(const QnFinish& f, hipStream_t stream) {
     hipLaunchKernelGGL(qn_finish_kernel, dim3(1), dim3(kQnBlock), 0, stream, f);
+    return hipGetLastError();
+}
+
+hipError_t launch_copy(const double* src, double* dst, int64_t n, hipStream_t stream) {
+    if (n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(copy_kernel, dim3(unsigned((n + 255) / 256)), dim3(256), 0, stream, src, dst, n);
     return hipGetLastError();
 }
 

@@ -123,6 +123,11 @@ struct wfsa_dev {
     // nothing was enqueued between kc and the tail's end: k2 is kc (each
     // timing marker costs the step ~1 us, profiles/r02/v23_timing_ab.txt)
     bool k2_kc[kQnDepth] = {};
+    // host-mapped QN state (x | lambda | grad) for set_state / get_state:
+    // kernels move it, where pageable copies cost ~25 us each
+    double* qst = nullptr;
+    double* qst_dev = nullptr;
+    size_t qst_n = 0;
     int timing_stride = 16;   // QN runs time every 16th step's kernels (WFSA_TIMING_STRIDE)
 
     // model
@@ -2287,6 +2292,7 @@ void wfsa_dev_destroy(wfsa_dev* ctx) {
         for (hipEvent_t ev : {ctx->k0[i], ctx->kc[i], ctx->k2[i]})
             if (ev) (void)hipEventDestroy(ev);
     if (ctx->qn_ring) (void)hipHostFree(ctx->qn_ring);
+    if (ctx->qst) (void)hipHostFree(ctx->qst);
     if (ctx->side_stream) (void)hipStreamSynchronize(ctx->side_stream);
     for (hipEvent_t ev : {ctx->fork, ctx->join})
         if (ev) (void)hipEventDestroy(ev);
@@ -2724,14 +2730,35 @@ int wfsa_dev_qn_setup(wfsa_dev* ctx, const wfsa_qn_desc* d) {
     return WFSA_OK;
 }
 
+namespace {
+int ensure_qst(wfsa_dev* ctx) {
+    const size_t need = 2 * size_t(ctx->qn_n) + size_t(ctx->qn_k) + 1;
+    if (ctx->qst_n >= need) return WFSA_OK;
+    if (ctx->qst) (void)hipHostFree(ctx->qst);
+    ctx->qst = nullptr;
+    ctx->qst_n = 0;
+    HIP_TRY(hipHostMalloc(reinterpret_cast<void**>(&ctx->qst), need * sizeof(double),
+                          hipHostMallocMapped | hipHostMallocCoherent));
+    HIP_TRY(hipHostGetDevicePointer(reinterpret_cast<void**>(&ctx->qst_dev), ctx->qst, 0));
+    ctx->qst_n = need;
+    return WFSA_OK;
+}
+}  // namespace
+
 int wfsa_dev_qn_set_state(wfsa_dev* ctx, const double* x, const double* lambda) {
     if (int rc = check_ctx(ctx)) return rc;
     if (!ctx->qn_ready) return fail(WFSA_ERR_ARG, "wfsa_dev_qn_setup has not run");
     if ((ctx->qn_n > 0 && !x) || (ctx->qn_k > 0 && !lambda)) return fail(WFSA_ERR_ARG, "null state");
     if (ctx->in_flight) return fail(WFSA_ERR_ARG, "an evaluation is in flight");
     hipStream_t s = ctx->stream;
-    if (ctx->qn_n > 0) HIP_TRY(ctx->qn_x.upload(x, size_t(ctx->qn_n), s));
-    if (ctx->qn_k > 0) HIP_TRY(ctx->qn_lambda.upload(lambda, size_t(ctx->qn_k), s));
+    if (int rc = ensure_qst(ctx)) return rc;
+    const size_t n = size_t(ctx->qn_n), k = size_t(ctx->qn_k);
+    HIP_TRY(ctx->qn_x.alloc(n));
+    HIP_TRY(ctx->qn_lambda.alloc(k));
+    if (n) std::memcpy(ctx->qst, x, n * sizeof(double));
+    if (k) std::memcpy(ctx->qst + n, lambda, k * sizeof(double));
+    HIP_TRY(wfsa::launch_copy(ctx->qst_dev, ctx->qn_x.ptr, int64_t(n), s));
+    HIP_TRY(wfsa::launch_copy(ctx->qst_dev + n, ctx->qn_lambda.ptr, int64_t(k), s));
     HIP_TRY(wfsa::launch_qn_weights(ctx->qn_x.ptr, ctx->qn_trim.ptr, ctx->n_params, ctx->w_full.ptr, ctx->ewp.ptr, s));
     HIP_TRY(hipStreamSynchronize(s));
     return WFSA_OK;
@@ -2741,10 +2768,17 @@ int wfsa_dev_qn_get_state(wfsa_dev* ctx, double* x, double* lambda, double* grad
     if (int rc = check_ctx(ctx)) return rc;
     if (!ctx->qn_ready) return fail(WFSA_ERR_ARG, "wfsa_dev_qn_setup has not run");
     hipStream_t s = ctx->stream;
-    if (x && ctx->qn_n > 0) HIP_TRY(ctx->qn_x.download(x, size_t(ctx->qn_n), s));
-    if (lambda && ctx->qn_k > 0) HIP_TRY(ctx->qn_lambda.download(lambda, size_t(ctx->qn_k), s));
-    if (grad && ctx->qn_n > 0) HIP_TRY(ctx->qn_grad.download(grad, size_t(ctx->qn_n), s));
+    if (int rc = ensure_qst(ctx)) return rc;
+    const size_t n = size_t(ctx->qn_n), k = size_t(ctx->qn_k);
+    if ((n && (!ctx->qn_x.ptr || !ctx->qn_grad.ptr)) || (k && !ctx->qn_lambda.ptr))
+        return fail(WFSA_ERR_ARG, "the QN state has not been set");
+    if (x && n) HIP_TRY(wfsa::launch_copy(ctx->qn_x.ptr, ctx->qst_dev, int64_t(n), s));
+    if (lambda && k) HIP_TRY(wfsa::launch_copy(ctx->qn_lambda.ptr, ctx->qst_dev + n, int64_t(k), s));
+    if (grad && n) HIP_TRY(wfsa::launch_copy(ctx->qn_grad.ptr, ctx->qst_dev + n + k, int64_t(n), s));
     HIP_TRY(hipStreamSynchronize(s));
+    if (x && n) std::memcpy(x, ctx->qst, n * sizeof(double));
+    if (lambda && k) std::memcpy(lambda, ctx->qst + n, k * sizeof(double));
+    if (grad && n) std::memcpy(grad, ctx->qst + n + k, n * sizeof(double));
     return WFSA_OK;
 }
 

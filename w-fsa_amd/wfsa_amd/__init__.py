@@ -317,7 +317,7 @@ class QuasiNewtonLearner:
         done = C.c_int32(0)
         rc = load().wfsa_learner_run(self._h, eta, tol, int(epochs), _ptr(rows), C.byref(done))
         check_host(rc)
-        return [list(r) for r in rows[:done.value]]
+        return rows[:done.value].tolist()
 
 
 class Device:
