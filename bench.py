@@ -373,12 +373,41 @@ def record(m, traffic, cpu):
             "tier2_strings": m["st1"]["tier2_strings"], "build_s": m["t_build"]}
 
 
+def launch_ranks(n):
+    """`bench.py --gpus N` (N > 1) started without a launcher: start the N rank
+    processes as fresh children through torch.distributed.run, before this
+    process touches the GPU, and exit with their status.  Refuses (exit 2)
+    when the node has fewer than N GPUs -- it never reports N GPUs from one."""
+    import socket
+    import subprocess
+    import torch   # device_count() does not initialise the GPU on this image
+    have = torch.cuda.device_count()
+    if have < n:
+        print(f"bench.py: --gpus {n} needs {n} GPUs on this node, {have} visible; refusing", file=sys.stderr)
+        sys.exit(2)
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + sys.argv[1:]
+    sys.exit(subprocess.call(cmd))
+
+
 def main():
     args = parse()
+    knobs = sorted(k for k in os.environ if k.startswith("WFSA_") and k.endswith("_DBG"))
+    if knobs:   # timing experiments that skip work: never inside a measurement
+        print(f"bench.py: refusing to measure with {', '.join(knobs)} set", file=sys.stderr)
+        sys.exit(2)
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        launch_ranks(args.gpus)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    n_gpus = max(args.gpus, world)
+    if args.gpus not in (1, world):   # (a launcher without --gpus: the default 1 means "one per rank")
+        print(f"bench.py: --gpus {args.gpus} but {world} rank process(es); refusing", file=sys.stderr)
+        sys.exit(2)
+    n_gpus = world   # the rank processes actually running, one GPU each
     import torch
     import torch.distributed as dist
     distributed = world > 1

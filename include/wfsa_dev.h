@@ -107,6 +107,8 @@ typedef struct {
     int32_t wave_strings;      /* traversal strings on the wave-per-string pair-table kernel */
     int64_t wave_row_entries;  /* per evaluation: alpha entries it writes (and reads back), sum |D| */
     int64_t wave_pair_edges;   /* per evaluation: pair-list edges one pass walks */
+    int32_t comm_ranks;        /* communicator size (1: none) */
+    int32_t comm_peer;         /* the one-shot peer all-reduce: 1 on, 0 off / untried, -1 its set-up check failed */
 } wfsa_dev_stats;
 
 /* context ---------------------------------------------------------------- */
@@ -246,6 +248,25 @@ int wfsa_dev_comm_unique_id(uint8_t id[WFSA_COMM_ID_BYTES]);
 int wfsa_dev_comm_local_id(int nranks, uint8_t id[WFSA_COMM_ID_BYTES]);
 int wfsa_dev_comm_init(wfsa_dev* ctx, int nranks, int rank, const uint8_t id[WFSA_COMM_ID_BYTES]);
 int wfsa_dev_allreduce(wfsa_dev* ctx, double* host_buf, int64_t count);
+
+/* A communicator over a host callback instead of RCCL (one process per rank,
+ * several may share a GPU; e.g. torch.distributed over gloo, or MPI):
+ * fn(user, buf, count, op) all-reduces a HOST buffer in place -- op 0: sum
+ * of doubles, 1: min of doubles, 2: max of bytes -- and returns 0 on
+ * success.  Called from the thread that drives ctx.  (New; the reference
+ * has no multi-process path.)
+ *
+ * Sums of up to 65536 doubles (the per-iteration [LL, grad] and the other
+ * small vectors) take the one-shot peer all-reduce when it is on: one
+ * kernel stores the rank's vector into every member's receive slot over
+ * xGMI (IPC-mapped device memory; the pointer itself in an in-process
+ * group), raises a flag per chunk and sums the members' slots in rank
+ * order -- stream-ordered, no host step.  On by default over RCCL, off
+ * otherwise; WFSA_PEER=1 / 0 overrides.  The first such sum checks the
+ * path on every rank and all ranks fall back to the transport when any
+ * check fails (stats.comm_peer = -1). */
+typedef int (*wfsa_host_allreduce_fn)(void* user, void* buf, int64_t count, int32_t op);
+int wfsa_dev_comm_init_host(wfsa_dev* ctx, int nranks, int rank, wfsa_host_allreduce_fn fn, void* user);
 
 int wfsa_dev_get_stats(wfsa_dev* ctx, wfsa_dev_stats* out);
 

@@ -62,6 +62,8 @@ int wfsa_learner_create(const char* optimizer, int device, wfsa_learner** out);
 int wfsa_learner_info_width(wfsa_learner* l);
 void wfsa_learner_destroy(wfsa_learner* l);
 int wfsa_learner_set_comm(wfsa_learner* l, int nranks, int rank, const uint8_t id[WFSA_COMM_ID_BYTES]);
+/* the same over a host all-reduce callback (wfsa_dev_comm_init_host) */
+int wfsa_learner_set_comm_host(wfsa_learner* l, int nranks, int rank, wfsa_host_allreduce_fn fn, void* user);
 /* Learner::BuildFrom on (Fsa, Corpus); the corpus is renormalized first as
  * main.cpp does.  With a communicator each rank keeps its shard. */
 int wfsa_learner_build(wfsa_learner* l, wfsa_fsa* fsa, wfsa_corpus* corpus);

@@ -740,33 +740,77 @@ static learner_t* build_common(learner_t* L, int mode, int64_t max_paths, char* 
         /* no transition reaches the end state: nothing is recognized */
         for (int64_t i = 0; i < NC; ++i) { L->aux_params++; L->aux_hessian -= log(cp->w.a[i]); }
     } else if (mode == 0) {
-        bfs_ws_t ws = {0};
+        /* BuildPaths (src/Learner.cpp:276-348): strings enumerated in chunks
+         * on OpenMP threads, each into its own arrays, then concatenated in
+         * string order -- the same P, M and numbering as one thread */
+        int nt = omp_get_max_threads();
+        const char* bt = getenv("ORACLE_BUILD_THREADS");   /* (tests: force a split) */
+        if (bt && atoi(bt) > 0) nt = atoi(bt);
+        else if (NC < 4096) nt = 1;
+        if (nt < 1) nt = 1;
+        paths_out_t* po_t = calloc((size_t)nt, sizeof(paths_out_t));
+        int64_t* np_of = calloc((size_t)(NC + 1), sizeof(int64_t));
+        int failed = 0;
+        int64_t fail_at = -1;
+#pragma omp parallel num_threads(nt) if (nt > 1)
+        {
+            const int t = omp_get_thread_num();
+            const int64_t b = NC * t / nt, e = NC * (t + 1) / nt;
+            bfs_ws_t ws = {0};
+            for (int64_t i = b; i < e && !failed; ++i) {
+                int64_t np = bfs_paths(f, cp->words.a[i], &ws, &po_t[t], L->max_paths);
+                np_of[i] = np;
+                if (np < 0) {
+#pragma omp critical
+                    { if (!failed || i < fail_at) fail_at = i; failed = 1; }
+                }
+            }
+            VFREE(ws.q); VFREE(ws.hist);
+        }
+        if (failed) {
+            snprintf(err, errlen, "string %lld exceeds max_paths", (long long)fail_at);
+            for (int t = 0; t < nt; ++t) { VFREE(po_t[t].prow); VFREE(po_t[t].pcol); VFREE(po_t[t].pdata); }
+            free(po_t); free(np_of); free(x_full); free(Ccol_full); return NULL;
+        }
         paths_out_t po = {0};
         VEC(int64_t) mrow = {0};
+        int64_t tot_rows = 0, tot_nz = 0;
+        for (int t = 0; t < nt; ++t) { tot_rows += po_t[t].prow.n; tot_nz += po_t[t].pcol.n; }
+        po.prow.a = xrealloc(NULL, sizeof(int64_t) * (size_t)(tot_rows + 1)); po.prow.cap = tot_rows + 1;
+        po.pcol.a = xrealloc(NULL, sizeof(int) * (size_t)(tot_nz + 1)); po.pcol.cap = tot_nz + 1;
+        po.pdata.a = xrealloc(NULL, sizeof(double) * (size_t)(tot_nz + 1)); po.pdata.cap = tot_nz + 1;
+        for (int t = 0; t < nt; ++t) {
+            const int64_t row0 = po.prow.n, nz0 = po.pcol.n;
+            for (int64_t r = 0; r < po_t[t].prow.n; ++r) po.prow.a[row0 + r] = po_t[t].prow.a[r] + nz0;
+            po.prow.n += po_t[t].prow.n;
+            memcpy(po.pcol.a + nz0, po_t[t].pcol.a, sizeof(int) * (size_t)po_t[t].pcol.n);
+            memcpy(po.pdata.a + nz0, po_t[t].pdata.a, sizeof(double) * (size_t)po_t[t].pdata.n);
+            po.pcol.n += po_t[t].pcol.n;
+            po.pdata.n += po_t[t].pdata.n;
+            VFREE(po_t[t].prow); VFREE(po_t[t].pcol); VFREE(po_t[t].pdata);
+        }
+        free(po_t);
+        int64_t row = 0;
         for (int64_t i = 0; i < NC; ++i) {
-            int64_t before = po.prow.n;
-            int64_t np = bfs_paths(f, cp->words.a[i], &ws, &po, L->max_paths);
-            if (np < 0) {
-                snprintf(err, errlen, "string %lld exceeds max_paths", (long long)i);
-                VFREE(ws.q); VFREE(ws.hist); VFREE(po.prow); VFREE(po.pcol); VFREE(po.pdata); VFREE(mrow);
-                free(x_full); free(Ccol_full); return NULL;
-            }
+            const int64_t np = np_of[i];
             L->path_count[i] = np;
             if (np > 0) {
-                VPUSH(mrow, before);
+                VPUSH(mrow, row);
                 L->common_support += cp->w.a[i];
                 L->str_of[S] = i; L->p[S] = cp->w.a[i]; ++S;
-                for (int64_t k = po.prow.a[before]; k < po.pcol.n; ++k) L->trimmed[po.pcol.a[k]] = 0;
+                const int64_t k_end = row + np < po.prow.n ? po.prow.a[row + np] : po.pcol.n;
+                for (int64_t k = po.prow.a[row]; k < k_end; ++k) L->trimmed[po.pcol.a[k]] = 0;
+                row += np;
             } else {
                 L->aux_params++; L->aux_hessian -= log(cp->w.a[i]);
             }
         }
+        free(np_of);
         VPUSH(mrow, po.prow.n);
         VPUSH(po.prow, po.pcol.n);
         L->n_paths = po.prow.n - 1;
         L->Prow = po.prow.a; L->Pcol = po.pcol.a; L->Pdata = po.pdata.a;
         L->Mrow = mrow.a;
-        VFREE(ws.q); VFREE(ws.hist);
     } else {
         trellis_ws_t ws = {0};
         ws.N = (int)f->st.n;

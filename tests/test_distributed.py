@@ -1,9 +1,14 @@
 """Data parallelism on CPU (gloo, world_size 2): every rank keeps the shard
 the product assigns it (wfsa_shard_range, as Learner::BuildFrom does), its
-partial [loglik, grad] is computed with globally normalized weights, and one
-all-reduce sums them -- the same decomposition the device path performs with
-one RCCL all-reduce per iteration.  The sum must equal the single-process
-result."""
+partial [loglik, grad] is computed with globally normalized weights (the CPU
+oracle stands in for the device evaluation, which needs a GPU), and the sum
+goes through the product's host transport -- the wfsa_host_allreduce_fn
+wrapper (wfsa_amd._host_callback around wfsa_amd.torch_allreduce) that
+wfsa_dev_comm_init_host calls, invoked here through ctypes exactly as the
+library invokes it: a host buffer address, a count and an op code (sum of
+doubles for [LL, grad], max of bytes for the used-parameter mask).  The sum
+must equal the single-process result.  tests/test_gpu_multiprocess.py runs
+the device path itself over the same transport."""
 import os
 import socket
 
@@ -50,11 +55,16 @@ def _worker(rank, world, port, q):
     names_w = dict(zip(names, np.random.default_rng(0).normal(-1.2, 0.4, size=len(names))))
     b, e = W.shard_range(off, world, rank)
     ll, g = _eval_shard(syn.wfsa_text, sym, off, wt, names_w, b, e)
-    vec = torch.tensor([ll] + [g[n] for n in names] + [float(e - b)], dtype=torch.float64)
-    dist.all_reduce(vec)
+    vec = np.array([ll] + [g[n] for n in names] + [float(e - b)], dtype=np.float64)
+    cb = W._host_callback(W.torch_allreduce)          # the product's wfsa_host_allreduce_fn
+    assert cb(None, vec.ctypes.data, len(vec), 0) == 0          # op 0: sum of doubles
+    used = np.zeros(len(names), dtype=np.uint8)                  # a rank's used-parameter mask
+    used[rank::world] = 1
+    assert cb(None, used.ctypes.data, len(used), 2) == 0        # op 2: max of bytes
+    assert used.all()
     if rank == 0:
         full_ll, full_g = _eval_shard(syn.wfsa_text, sym, off, wt, names_w, 0, len(wt))
-        q.put((vec.numpy(), full_ll, np.array([full_g[n] for n in names]), len(wt)))
+        q.put((vec, full_ll, np.array([full_g[n] for n in names]), len(wt)))
     dist.destroy_process_group()
 
 

@@ -187,7 +187,7 @@ def test_dense_device_qn_large_groups_equals_host_update(monkeypatch):
     np.testing.assert_allclose(a.x(), b.x(), rtol=1e-10, atol=1e-12)
 
 
-def _dense_tables(fsa, w):
+def _dense_tables(fsa, w, with_index=False):
     """exp-weights of a dense synthetic model from its flat description:
     A[S][T] (transitions), E[T][c] (1-byte emissions), the start row and the
     end column; kind of every Fsa parameter (0 emission, 1 start transition,
@@ -220,7 +220,11 @@ def _dense_tables(fsa, w):
     kind[em_par[em_par >= 0]] = 0
     tk = np.where(src == d.start, 1, np.where(tr_dst == d.end, 2, 3))
     kind[tr_par[tr_par >= 0]] = tk[tr_par >= 0]
-    return A, E, d.start, d.end, kind
+    if not with_index:
+        return A, E, d.start, d.end, kind
+    # every parameter's (row, column) in A or E
+    index = dict(tr=(src, tr_dst, tr_par), em=(esrc[one], em_bytes[em_off[one]], em_par[one]))
+    return A, E, d.start, d.end, kind, index
 
 
 def _dense_logq(A, E, start, end, s):
@@ -279,3 +283,74 @@ def test_dense_c5_4096_states(monkeypatch):
         for u, v in zip(r[:5], q[:5]):
             assert _close(u, v, rel=1e-9, atol=1e-12)
     np.testing.assert_allclose(a.x(), b.x(), rtol=1e-9, atol=1e-11)
+
+
+def _dense_expected_counts(A, E, start, end, s):
+    """log q and the expected transition / emission counts of one string
+    (numpy forward-backward, per-position scaling):
+    C_A[S][T] = sum_i P(S at i, T at i+1), C_E[T][c] = sum_i P(T at i) [s_i = c]"""
+    L = len(s)
+    al = np.zeros((L, A.shape[0]))
+    z = np.zeros(L)
+    a = A[start] * E[:, s[0]]
+    for i in range(L):
+        if i > 0:
+            a = al[i - 1] @ A * E[:, s[i]]
+        z[i] = a.sum()
+        al[i] = a / z[i]
+    fin = al[L - 1] @ A[:, end]
+    logq = np.log(z).sum() + np.log(fin)
+    be = A[:, end] / fin          # beta_{L-1}, in the scale where al[i] * be[i] sums to 1
+    CA = np.zeros_like(A)
+    CE = np.zeros_like(E)
+    CA[:, end] += al[L - 1] * A[:, end] / fin
+    for i in range(L - 1, -1, -1):
+        g = al[i] * be
+        CE[:, s[i]] += g
+        if i == 0:
+            CA[start] += g
+            break
+        nxt = E[:, s[i]] * be / z[i]   # message into T at position i
+        CA += np.outer(al[i - 1], nxt) * A
+        be = A @ nxt
+    return logq, CA, CE
+
+
+def test_dense_c5_4096_gradient_per_element(monkeypatch):
+    """per-parameter gradient at the c5 size (4096 states, full transition
+    matrix, 16 symbols): 6 strings as their own corpus on the dense MFMA path
+    against a numpy forward-backward of the same strings -- every transition
+    (start, interior, end) and emission parameter, rel 1e-9"""
+    import wfsa_amd as W
+    syn = W.Synthetic(n_states=4096, degree=1, vocab=16, emissions=16, dense=True, n_strings=6, max_len=40, seed=5)
+    sym, off, wt = syn.corpus()
+    fsa = W.Fsa.read_text(syn.wfsa_text)
+    n_par = fsa.counts()["parameters"]
+    p = wt / wt.sum()
+    w = np.random.default_rng(12).normal(-8.5, 1.0, size=n_par)
+    dev = _device(fsa, sym, off, p, monkeypatch, dense=True)
+    rec, _, _ = dev.recognize()
+    assert rec.all()
+    ll, grad, logq = dev.objective_grad(w)
+    A, E, start, end, kind, index = _dense_tables(fsa, w, with_index=True)
+    CA = np.zeros_like(A)
+    CE = np.zeros_like(E)
+    ll_ref = 0.0
+    for i in range(len(wt)):
+        lq, ca, ce = _dense_expected_counts(A, E, start, end, sym[off[i]:off[i + 1]])
+        assert _close(logq[i], lq, rel=1e-11)
+        ll_ref += p[i] * lq
+        CA += p[i] * ca
+        CE += p[i] * ce
+    assert _close(ll, ll_ref, rel=1e-11)
+    ref = np.zeros(n_par)
+    src, dst, par = index["tr"]
+    ok = par >= 0
+    ref[par[ok]] -= CA[src[ok], dst[ok]]
+    es, ec, ep = index["em"]
+    ok = ep >= 0
+    ref[ep[ok]] -= CE[es[ok], ec[ok]]
+    assert (kind >= 0).all()
+    for k in range(4):   # start, interior, end transitions and emissions all compared
+        assert (kind == k).any()
+    np.testing.assert_allclose(grad, ref, rtol=1e-9, atol=1e-15)

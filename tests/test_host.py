@@ -176,3 +176,27 @@ def test_crlf_automaton_fails_like_reference():
     import wfsa_amd as W
     with pytest.raises(W.WfsaError, match='You should enlist transitions of "a" after emissions of the same state!'):
         W.Fsa.read_file(os.path.join(DATA, "test.wfsa.win"))
+
+
+def test_bench_never_reports_more_gpus_than_rank_processes():
+    """bench.py --gpus N (N > 1) without a launcher starts its own ranks or
+    refuses; on a node with fewer GPUs it refuses (exit 2) instead of
+    reporting N GPUs from one process"""
+    import subprocess
+    import sys
+    env = dict(os.environ, CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="")
+    env.pop("WORLD_SIZE", None)
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "1"],
+                       capture_output=True, text=True, env=env, timeout=120)
+    assert r.returncode == 2, r.stderr
+    assert "refusing" in r.stderr and r.stdout.strip() == ""
+    # a launcher's WORLD_SIZE that disagrees with --gpus is refused too
+    env2 = dict(env, WORLD_SIZE="2", RANK="0", LOCAL_RANK="0")
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "4"],
+                       capture_output=True, text=True, env=env2, timeout=120)
+    assert r.returncode == 2 and "refusing" in r.stderr
+    # work-skipping experiment knobs are refused
+    env3 = dict(env, WFSA_FBS_DBG="1")
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py")], capture_output=True, text=True, env=env3,
+                       timeout=120)
+    assert r.returncode == 2 and "WFSA_FBS_DBG" in r.stderr

@@ -178,3 +178,25 @@ def test_matrix_files_round_trip(tmp_path):
     np.testing.assert_array_equal(c, o.ccol())
     assert len(open(prefix + ".prob").read().split()) == o.info["n_strings"]
     assert len(open(prefix + ".aux").read().split()) == 5
+
+
+def test_enum_threaded_enumeration_equals_one_thread(monkeypatch):
+    """the oracle's BuildPaths on OpenMP threads (chunks of strings,
+    concatenated in string order) builds the same P, M, numbering and
+    objective as one thread"""
+    import numpy as np
+    import wfsa_amd as W
+    from oracle import ENUM, Oracle
+    syn = W.Synthetic(n_states=48, degree=6, vocab=16, emissions=1, n_strings=3000, max_len=20, seed=7)
+    sym, off, wt = syn.corpus()
+    res = []
+    for nt in ("1", "5"):
+        monkeypatch.setenv("ORACLE_BUILD_THREADS", nt)
+        o = Oracle.from_arrays(syn.wfsa_text, sym, off, wt, mode=ENUM)
+        o.qn_init(7)
+        kl, ll = o.objective_grad()
+        res.append((o.info, kl, ll, o.grad(), o.param_names(), o.path_counts()))
+    a, b = res
+    assert a[0] == b[0] and a[1] == b[1] and a[2] == b[2] and a[4] == b[4]
+    np.testing.assert_array_equal(a[3], b[3])
+    np.testing.assert_array_equal(a[5], b[5])

@@ -1,0 +1,201 @@
+// Stream formats for the trivial words of compiled strings, measured in
+// isolation (c3-like: 1M strings of 36 edges, 1024 nodes x 9 out-slots):
+//   A  16-bit slot index per edge (the current stream): an independent LDS
+//      gather of the edge weight per edge, 2 B of stream per edge;
+//   B  4-bit out-edge choice per edge: a chain through LDS (slot = base of the
+//      current node + choice; weight and the next node's base per slot),
+//      0.5 B of stream per edge;
+//   B2 B with two strings per lane (two chains in flight).
+// Prints the kernel time of each and checks that all three sum the same
+// log-likelihood.
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <cstdio>
+#include <random>
+#include <vector>
+
+#define CK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { printf("%s line %d\n", hipGetErrorString(e_), __LINE__); return 1; } } while (0)
+
+constexpr int kWave = 64;
+constexpr int kNodes = 1024, kDeg = 9, kSlots = kNodes * kDeg;
+constexpr int kLen = 36;
+constexpr int kChA = (kLen + 7) / 8;    // 16-byte chunks per string, 16-bit words
+constexpr int kChB = (kLen + 31) / 32;  // ... nibbles
+
+__device__ inline double wave_sum(double v) {
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+    return v;
+}
+
+// one wave per group of 64 strings, groups dealt round-robin over the waves
+__global__ __launch_bounds__(512) void walk_a(const uint4* __restrict__ st, int n_groups, const double* __restrict__ w,
+                                              const double* __restrict__ p, double* ll_part) {
+    __shared__ double lw[kSlots];
+    for (int j = threadIdx.x; j < kSlots; j += blockDim.x) lw[j] = w[j];
+    __syncthreads();
+    const int lane = threadIdx.x % kWave;
+    const int gw = blockIdx.x * (blockDim.x / kWave) + threadIdx.x / kWave;
+    const int nw = gridDim.x * (blockDim.x / kWave);
+    double ll = 0.0;
+    for (int g = gw; g < n_groups; g += nw) {
+        const uint4* s = st + size_t(g) * kChA * kWave + lane;
+        uint4 r[kChA];
+#pragma unroll
+        for (int c = 0; c < kChA; ++c) r[c] = s[c * kWave];
+        double a0 = 0.0, a1 = 0.0;
+#pragma unroll
+        for (int c = 0; c < kChA; ++c) {
+            const uint32_t v[4] = {r[c].x, r[c].y, r[c].z, r[c].w};
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const uint32_t lo = v[i] & 0xffffu, hi = v[i] >> 16;
+                a0 += lw[min(lo, uint32_t(kSlots - 1))] * (lo != 0xffffu);
+                a1 += lw[min(hi, uint32_t(kSlots - 1))] * (hi != 0xffffu);
+            }
+        }
+        ll += p[g * kWave + lane] * (a0 + a1);
+    }
+    ll = wave_sum(ll);
+    if (lane == 0) ll_part[gw] = ll;
+}
+
+template <int K>   // strings per lane in flight
+__global__ __launch_bounds__(1024) void walk_b(const uint4* __restrict__ st, int n_groups, const double* __restrict__ sw,
+                                               const uint16_t* __restrict__ nb, const double* __restrict__ p,
+                                               double* ll_part) {
+    __shared__ double lw[kSlots];
+    __shared__ uint16_t lnb[kSlots];
+    for (int j = threadIdx.x; j < kSlots; j += blockDim.x) {
+        lw[j] = sw[j];
+        lnb[j] = nb[j];
+    }
+    __syncthreads();
+    const int lane = threadIdx.x % kWave;
+    const int gw = blockIdx.x * (blockDim.x / kWave) + threadIdx.x / kWave;
+    const int nw = gridDim.x * (blockDim.x / kWave);
+    double ll = 0.0;
+    for (int g0 = gw * K; g0 < n_groups; g0 += nw * K) {
+        uint4 r[K][kChB];
+        double acc[K];
+        int base[K];
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            const int g = min(g0 + k, n_groups - 1);
+            const uint4* s = st + size_t(g) * kChB * kWave + lane;
+#pragma unroll
+            for (int c = 0; c < kChB; ++c) r[k][c] = s[c * kWave];
+            acc[k] = 0.0;
+            base[k] = 0;
+        }
+#pragma unroll
+        for (int c = 0; c < kChB; ++c) {
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+#pragma unroll
+                for (int h = 0; h < 8; ++h) {
+                    if (c * 32 + i * 8 + h >= kLen) break;
+#pragma unroll
+                    for (int k = 0; k < K; ++k) {
+                        const uint32_t v = (i == 0 ? r[k][c].x : i == 1 ? r[k][c].y : i == 2 ? r[k][c].z : r[k][c].w);
+                        const int slot = base[k] + int((v >> (4 * h)) & 0xfu);
+                        acc[k] += lw[slot];
+                        base[k] = lnb[slot];
+                    }
+                }
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < K; ++k)
+            if (g0 + k < n_groups) ll += p[(g0 + k) * kWave + lane] * acc[k];
+    }
+    ll = wave_sum(ll);
+    if (lane == 0) ll_part[gw] = ll;
+}
+
+int main() {
+    const int S = 1 << 20, G = S / kWave;
+    std::mt19937_64 rng(7);
+    std::vector<int> succ(kSlots);
+    std::vector<double> sw(kSlots), p(S);
+    std::vector<uint16_t> nb(kSlots);
+    for (int u = 0; u < kNodes; ++u)
+        for (int d = 0; d < kDeg; ++d) {
+            succ[u * kDeg + d] = int(rng() % kNodes);
+            sw[u * kDeg + d] = -1.0 - double(rng() % 1000) * 1e-3;
+            nb[u * kDeg + d] = uint16_t(succ[u * kDeg + d] * kDeg);
+        }
+    for (int s = 0; s < S; ++s) p[s] = 1.0 / S;
+    std::vector<uint32_t> A(size_t(G) * kChA * kWave * 4, 0xffffffffu), B(size_t(G) * kChB * kWave * 4, 0u);
+    double ref = 0.0;
+    for (int s = 0; s < S; ++s) {
+        const int g = s / kWave, l = s % kWave;
+        int u = 0;
+        double acc = 0.0;
+        for (int e = 0; e < kLen; ++e) {
+            const int d = int(rng() % 8);
+            const int slot = u * kDeg + d;
+            acc += sw[slot];
+            // A: word e of the string at chunk e/8, u32 (e%8)/2, half e%2
+            uint32_t& wa = A[((size_t(g) * kChA + e / 8) * kWave + l) * 4 + (e % 8) / 2];
+            wa = (e % 2) ? ((wa & 0xffffu) | (uint32_t(slot) << 16)) : ((wa & 0xffff0000u) | uint32_t(slot));
+            uint32_t& wb = B[((size_t(g) * kChB + e / 32) * kWave + l) * 4 + (e % 32) / 8];
+            wb |= uint32_t(d) << (4 * (e % 8));
+            u = succ[slot];
+        }
+        ref += p[s] * acc;
+    }
+    uint4 *dA, *dB;
+    double *dsw, *dp, *dll;
+    uint16_t* dnb;
+    CK(hipMalloc(&dA, A.size() * 4));
+    CK(hipMalloc(&dB, B.size() * 4));
+    CK(hipMalloc(&dsw, kSlots * 8));
+    CK(hipMalloc(&dnb, kSlots * 2));
+    CK(hipMalloc(&dp, size_t(S) * 8));
+    CK(hipMalloc(&dll, 1 << 20));
+    CK(hipMemcpy(dA, A.data(), A.size() * 4, hipMemcpyHostToDevice));
+    CK(hipMemcpy(dB, B.data(), B.size() * 4, hipMemcpyHostToDevice));
+    CK(hipMemcpy(dsw, sw.data(), kSlots * 8, hipMemcpyHostToDevice));
+    CK(hipMemcpy(dnb, nb.data(), kSlots * 2, hipMemcpyHostToDevice));
+    CK(hipMemcpy(dp, p.data(), size_t(S) * 8, hipMemcpyHostToDevice));
+    hipEvent_t e0, e1;
+    CK(hipEventCreate(&e0));
+    CK(hipEventCreate(&e1));
+    auto run = [&](const char* name, auto launch, int nwaves, double bytes) -> int {
+        for (int r = 0; r < 3; ++r) launch();
+        CK(hipDeviceSynchronize());
+        const int reps = 50;
+        CK(hipEventRecord(e0, 0));
+        for (int r = 0; r < reps; ++r) launch();
+        CK(hipEventRecord(e1, 0));
+        CK(hipEventSynchronize(e1));
+        float ms = 0.f;
+        CK(hipEventElapsedTime(&ms, e0, e1));
+        std::vector<double> part(nwaves);
+        CK(hipMemcpy(part.data(), dll, size_t(nwaves) * 8, hipMemcpyDeviceToHost));
+        double ll = 0.0;
+        for (double v : part) ll += v;
+        const double us = ms * 1e3 / reps;
+        printf("%-28s %8.2f us  stream %6.1f MB  %7.1f GB/s  ll %.15g (ref %.15g, rel %.1e)\n", name, us, bytes / 1e6,
+               bytes / us / 1e3, ll, ref, std::abs(ll - ref) / std::abs(ref));
+        return 0;
+    };
+    const double bA = double(A.size()) * 4, bB = double(B.size()) * 4;
+    for (int bpc : {1, 2, 4}) {   // blocks of 512 threads per CU
+        const int grid = 256 * bpc;
+        char nm[64];
+        snprintf(nm, sizeof nm, "A 16-bit, %d x 512 / CU", bpc);
+        if (run(nm, [&] { hipLaunchKernelGGL(walk_a, dim3(grid), dim3(512), 0, 0, dA, G, dsw, dp, dll); }, grid * 8, bA)) return 1;
+    }
+    for (int bpc : {1}) {
+        const int grid = 256 * bpc;
+        if (run("B nibble, K=1", [&] { hipLaunchKernelGGL(walk_b<1>, dim3(grid), dim3(1024), 0, 0, dB, G, dsw, dnb, dp, dll); },
+                grid * 16, bB)) return 1;
+        if (run("B nibble, K=2", [&] { hipLaunchKernelGGL(walk_b<2>, dim3(grid), dim3(1024), 0, 0, dB, G, dsw, dnb, dp, dll); },
+                grid * 16, bB)) return 1;
+        if (run("B nibble, K=4", [&] { hipLaunchKernelGGL(walk_b<4>, dim3(grid), dim3(1024), 0, 0, dB, G, dsw, dnb, dp, dll); },
+                grid * 16, bB)) return 1;
+    }
+    return 0;
+}

@@ -1,5 +1,7 @@
 #include "HessianLearner.hpp"
 
+#include <unordered_map>
+
 #include <string>
 
 #include <cstdlib>
@@ -281,37 +283,53 @@ Factored factor_and_solve(wfsa_dev* dev, const SymEntries& A, int order, const d
     const std::string forced = kkt_forced();
     const bool dense_fits = N <= HessianLearner::kMaxDense;
     if (forced == "sparse" || (forced.empty() && N > HessianLearner::kHostDense)) {
-        SparseLdlt s;
-        const bool ordered = s.Analyze(A, order);
-        if (std::getenv("WFSA_KKT_TRACE"))
-            std::fprintf(stderr, "[kkt] N %lld entries %zu order %d%s nnz(L) %lld flops %.3g\n", (long long)N,
-                         A.v.size(), order, ordered ? "" : " (work bound: identity)", (long long)s.nnz_l, s.flops);
-        if (forced == "sparse" || !dense_fits || s.flops <= HessianLearner::kSparseFlops) {
+        // the requested ordering first; when its factorisation fails, the other
+        // one before giving up (a different elimination order meets different
+        // pivots)
+        for (int attempt = 0; attempt < 2; ++attempt) {
+            const int ord = attempt == 0 ? order : 1 - order;
+            SparseLdlt s;
+            const bool ordered = s.Analyze(A, ord);
+            if (std::getenv("WFSA_KKT_TRACE"))
+                std::fprintf(stderr, "[kkt] N %lld entries %zu order %d%s nnz(L) %lld flops %.3g\n", (long long)N,
+                             A.v.size(), ord, ordered ? "" : " (work bound: identity)", (long long)s.nnz_l, s.flops);
+            if (!(forced == "sparse" || !dense_fits || s.flops <= HessianLearner::kSparseFlops)) break;
             bool ok = s.Factor(A) && s.min_pivot_ratio > 1e-12;
-            if (ok && rhs) {
+            if (ok && rhs) {   // normwise backward error per row: |Ax - b|_i <= tol (|A||x| + |b|)_i
                 s.Solve(rhs, x);
-                std::vector<double> ax(static_cast<size_t>(N));
+                std::vector<double> ax(static_cast<size_t>(N)), mag(static_cast<size_t>(N), 0.0);
                 A.multiply(x, ax.data());
-                double res = 0.0, amax = 0.0, xmax = 0.0, bmax = 0.0;
-                for (int64_t i = 0; i < N; ++i) {
-                    res = std::max(res, std::abs(ax[size_t(i)] - rhs[i]));
-                    xmax = std::max(xmax, std::abs(x[i]));
-                    bmax = std::max(bmax, std::abs(rhs[i]));
+                for (size_t t = 0; t < A.v.size(); ++t) {
+                    const double v = std::abs(A.v[t]);
+                    mag[size_t(A.i[t])] += v * std::abs(x[A.j[t]]);
+                    if (A.i[t] != A.j[t]) mag[size_t(A.j[t])] += v * std::abs(x[A.i[t]]);
                 }
-                for (double v : A.v) amax = std::max(amax, std::abs(v));
-                ok = std::isfinite(res) && res <= 1e-9 * (amax * xmax + bmax);
+                for (int64_t i = 0; i < N && ok; ++i) {
+                    const double res = std::abs(ax[size_t(i)] - rhs[i]);
+                    ok = std::isfinite(res) && res <= 1e-9 * (mag[size_t(i)] + std::abs(rhs[i]));
+                }
             }
-            if (ok || !dense_fits) {
-                if (!ok && rhs) std::fill(x, x + N, std::numeric_limits<double>::quiet_NaN());   // degenerate
+            if (ok) {
                 r.positive = s.positive;
                 r.negative = s.negative;
-                r.log_abs_det = ok ? s.log_abs_det : -std::numeric_limits<double>::infinity();
-                r.det_sign = ok ? s.det_sign : 0;
+                r.log_abs_det = s.log_abs_det;
+                r.det_sign = s.det_sign;
                 r.kind = 's';
                 return r;
             }
         }
+        if (!dense_fits) {   // degenerate: no inertia from a partial factorisation
+            if (rhs) std::fill(x, x + N, std::numeric_limits<double>::quiet_NaN());
+            r.positive = r.negative = 0;
+            r.log_abs_det = -std::numeric_limits<double>::infinity();
+            r.det_sign = 0;
+            r.kind = 's';
+            return r;
+        }
     }
+    if (!dense_fits)   // only a forced dense factorisation gets here
+        throw LearnerError("KKT system of ", N, " unknowns: beyond the dense factorisation's ", HessianLearner::kMaxDense,
+                           " (WFSA_KKT=", forced, ")");
     std::vector<double> H = A.dense();
     const bool device = forced == "device" || (forced != "host" && forced != "sparse" && N > HessianLearner::kHostDense);
     if (!device) {
@@ -347,9 +365,16 @@ Factored factor_and_solve(wfsa_dev* dev, const SymEntries& A, int order, const d
 // with_jg = false: the n x n Hessian of ComputeLogDetHessian (:219-260), the
 // constraint column dropped.  Prints it as PrintCsrMtx does (PrintEq with rhs,
 // PrintH without, :262-270).
-void HessianLearner::PrintKkt(FILE* f, const std::vector<double>& H, int64_t ld, bool with_hf, bool with_jg,
+void HessianLearner::PrintKkt(FILE* f, const SymEntries& A, bool with_hf, bool with_jg,
                               const std::vector<double>* rhs_print) {
     const int64_t n = int64_t(_x.size()), k = with_jg ? int64_t(lambda.size()) : 0;
+    std::unordered_map<int64_t, double> H;   // (row, col) of the upper triangle -> value, duplicates summed
+    H.reserve(A.v.size());
+    for (size_t t = 0; t < A.v.size(); ++t) H[int64_t(A.i[t]) * A.n + A.j[t]] += A.v[t];
+    auto at = [&](int64_t r, int64_t c) {
+        const auto it = H.find(r * A.n + c);
+        return it == H.end() ? 0.0 : it->second;
+    };
     std::vector<std::vector<int32_t>> upper(static_cast<size_t>(n));
     if (with_hf && !HasUniquePaths()) {
         SetupHf();
@@ -373,7 +398,7 @@ void HessianLearner::PrintKkt(FILE* f, const std::vector<double>& H, int64_t ld,
         rows.push_back(int32_t(cols.size()));
     }
     for (size_t r = 0; r + 1 < rows.size(); ++r)
-        for (int32_t q = rows[r]; q < rows[r + 1]; ++q) vals.push_back(H[size_t(int64_t(r) * ld + cols[size_t(q)])]);
+        for (int32_t q = rows[r]; q < rows[r + 1]; ++q) vals.push_back(at(int64_t(r), cols[size_t(q)]));
     print_csr(f, vals.data(), rows, cols, rhs_print);
 }
 
@@ -390,7 +415,7 @@ void HessianLearner::OptimizationStep(double eta, bool verbose) {   // :63-130
     }
     if (verbose) {   // (:76-80)
         std::fputs("H:\n", stderr);
-        PrintKkt(stderr, A.dense(), N, include_Hf, true, &rhs);
+        PrintKkt(stderr, A, include_Hf, true, &rhs);
     }
     lambda_min = k ? *std::min_element(lambda.begin(), lambda.end()) : 0.0;
     step.assign(size_t(N), 0.0);
@@ -452,7 +477,7 @@ double HessianLearner::ComputeLogDetHessian(bool verbose) {
     ComputeGrad();
     const bool offdiag = !HasUniquePaths() && AddHf(A, true);
     for (int64_t j = 0; j < n; ++j) A.add(j, j, -grad[size_t(j)] / (expx[size_t(j)] * expx[size_t(j)]));
-    if (verbose) log_det_h = A.dense();   // for PrintH after the Hessian line (:360)
+    if (verbose) log_det_h = A;   // for PrintH after the Hessian line (:360)
     const double inf = std::numeric_limits<double>::infinity();
     if (!offdiag) {   // diagonal (src/Utils.cpp:300-311)
         std::vector<double> d(static_cast<size_t>(n), 0.0);
@@ -481,9 +506,9 @@ std::vector<double> HessianLearner::GetOptimizationResult(bool verbose) {   // :
             if (hf_j[t] >= 0 && hf_k[t] >= 0 && hf_j[t] != hf_k[t]) ++nnz;
     std::fprintf(stderr, "Hessian:\n\trows: %lld\n\tnnz: %lld\n\tfill: %g\n", (long long)n, (long long)nnz,
                  n ? double(nnz) / double(n) : 0.0);
-    if (verbose && !log_det_h.empty()) {
-        PrintKkt(stderr, log_det_h, n, true, false, nullptr);
-        log_det_h.clear();
+    if (verbose && log_det_h.n > 0) {
+        PrintKkt(stderr, log_det_h, true, false, nullptr);
+        log_det_h = SymEntries();
     }
     return {GetKLDistance(),
             mxlogx(GetCommonSupport()),

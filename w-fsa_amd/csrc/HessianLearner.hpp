@@ -86,9 +86,9 @@ private:
     // (per_weight: over exp(x_j) exp(x_k), the weight-space Hessian); returns
     // whether the pattern has off-diagonal entries
     bool AddHf(SymEntries& A, bool per_weight);
-    void PrintKkt(FILE* f, const std::vector<double>& H, int64_t ld, bool with_hf, bool with_jg,
+    void PrintKkt(FILE* f, const SymEntries& A, bool with_hf, bool with_jg,
                   const std::vector<double>* rhs_print);
-    std::vector<double> log_det_h;   // the last log-det Hessian, kept for PrintH (verbose)
+    SymEntries log_det_h;   // the last log-det Hessian, kept for PrintH (verbose)
 
     std::vector<double> rhs, expx, grad, lambda, step;
     std::vector<int32_t> hf_j, hf_k;   // trimmed indices of the pattern (-1: not a variable)

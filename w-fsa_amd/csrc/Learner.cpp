@@ -49,12 +49,25 @@ void Learner::SetCommunicator(int n, int r, const uint8_t* id) {
         if (!id) throw LearnerError("null communicator id");
         comm_id.assign(id, id + WFSA_COMM_ID_BYTES);
     }
+    host_fn = nullptr;
+}
+
+void Learner::SetHostCommunicator(int n, int r, wfsa_host_allreduce_fn fn, void* user) {
+    if (dev) throw LearnerError("SetCommunicator must come before BuildFrom");
+    if (n < 1 || r < 0 || r >= n || (n > 1 && !fn)) throw LearnerError("bad communicator: rank ", r, " of ", n);
+    nranks = n;
+    rank = r;
+    host_fn = fn;
+    host_user = user;
 }
 
 void Learner::EnsureDevice() {
     if (dev) return;
     ThrowOnDevError(wfsa_dev_create(device, &dev), "wfsa_dev_create");
-    if (nranks > 1) ThrowOnDevError(wfsa_dev_comm_init(dev, nranks, rank, comm_id.data()), "wfsa_dev_comm_init");
+    if (nranks > 1) {
+        if (host_fn) ThrowOnDevError(wfsa_dev_comm_init_host(dev, nranks, rank, host_fn, host_user), "wfsa_dev_comm_init_host");
+        else ThrowOnDevError(wfsa_dev_comm_init(dev, nranks, rank, comm_id.data()), "wfsa_dev_comm_init");
+    }
 }
 
 double Learner::AllReduceSum(double v) const {

@@ -42,6 +42,8 @@ public:
     // Device / sharding setup (new; call before BuildFrom).
     void SetDevice(int device);
     void SetCommunicator(int nranks, int rank, const uint8_t* unique_id);
+    // the same over a host callback (wfsa_dev_comm_init_host)
+    void SetHostCommunicator(int nranks, int rank, wfsa_host_allreduce_fn fn, void* user);
 
     // `corpus` weights must already be normalized over the whole corpus
     // (main.cpp renormalizes before BuildFrom).  With a communicator, every
@@ -186,6 +188,8 @@ private:
     wfsa_dev* dev = nullptr;
     int nranks = 1, rank = 0;
     std::vector<uint8_t> comm_id;
+    wfsa_host_allreduce_fn host_fn = nullptr;
+    void* host_user = nullptr;
     std::unique_ptr<FlatModel> flat;
     int64_t shard_begin = 0, shard_end = 0;
     struct Matrices {   // the loaded path matrices (matrix-file mode)

@@ -3,6 +3,8 @@
 #include <algorithm>
 #include <chrono>
 #include <cmath>
+#include <cstdio>
+#include <cstdlib>
 
 namespace wfsa {
 
@@ -14,6 +16,7 @@ void QuasiNewtonLearner::FinalizeCallback() {   // src/QuasiNewtonLearner.cpp:17
     lambda.assign(k, 1.0);
     g.assign(k, 0.0);
     dev_qn_ready = false;
+    dev_state_valid = host_state_stale = false;
 }
 
 void QuasiNewtonLearner::InitCallback(int flags) {   // :29-51
@@ -137,16 +140,32 @@ void QuasiNewtonLearner::RunDevice(double eta, double tol, int32_t max_epochs, d
         if (rc != WFSA_OK) throw LearnerError(what, ": ", wfsa_dev_last_error());
     };
     if (!dev_qn_ready || dev_qn_exp != exponential_lambda || dev_qn_rmin != desc.info_rmin) {   // once per Finalize (and mode)
+        PullDeviceState();   // (the set-up may move the device buffers)
         check(wfsa_dev_qn_setup(d, &desc), "wfsa_dev_qn_setup");
         dev_qn_ready = true;
         dev_qn_exp = exponential_lambda;
         dev_qn_rmin = desc.info_rmin;
+        dev_state_valid = false;
     }
-    check(wfsa_dev_qn_set_state(d, _x.data(), lambda.data()), "wfsa_dev_qn_set_state");
-    std::vector<double> rows(size_t(std::max(max_epochs, 0)) * 7);
+    using clk = std::chrono::steady_clock;
+    static const bool trace = std::getenv("WFSA_RUN_TRACE") != nullptr;
+    const auto t0 = clk::now();
+    if (!dev_state_valid) {
+        check(wfsa_dev_qn_set_state(d, _x.data(), lambda.data()), "wfsa_dev_qn_set_state");
+        dev_state_valid = true;
+    }
+    const auto t1 = clk::now();
+    rows_buf.resize(size_t(std::max(max_epochs, 0)) * 7);
+    std::vector<double>& rows = rows_buf;
     int32_t done = 0, status = 0;
-    check(wfsa_dev_qn_run(d, eta, tol, max_epochs, rows.data(), &done, &status), "wfsa_dev_qn_run");
-    check(wfsa_dev_qn_get_state(d, _x.data(), lambda.data(), grad.data()), "wfsa_dev_qn_get_state");
+    const int rc = wfsa_dev_qn_run(d, eta, tol, max_epochs, rows.data(), &done, &status);
+    host_state_stale = true;   // even a failed run may have moved the device state
+    check(rc, "wfsa_dev_qn_run");
+    if (trace) {
+        const auto t2 = clk::now();
+        auto us = [](clk::time_point a, clk::time_point b) { return std::chrono::duration<double, std::micro>(b - a).count(); };
+        std::fprintf(stderr, "[wfsa] RunDevice: set_state %.1f us, qn_run %.1f\n", us(t0, t1), us(t1, t2));
+    }
     if (info_rows) std::copy(rows.begin(), rows.begin() + std::ptrdiff_t(done) * 7, info_rows);
     if (epochs_done) *epochs_done = done;
     if (done > 0) {
@@ -158,12 +177,21 @@ void QuasiNewtonLearner::RunDevice(double eta, double tol, int32_t max_epochs, d
         rmin[0] = r[5];
         rmin[1] = r[6];
         SetEvaluated(GetPLogP() - r[0]);
-        grad_cache = grad;
         timing.steps += done;
         if (status == 2)
             for (int i = 0; i < 7; ++i)
                 if (!std::isfinite(r[i])) throw LearnerError(r[i], " detected at epoch ", done);
     }
+}
+
+void QuasiNewtonLearner::PullDeviceState() {
+    if (!host_state_stale) return;
+    wfsa_dev* d = Device();
+    if (!d) return;
+    if (wfsa_dev_qn_get_state(d, _x.data(), lambda.data(), grad.data()) != WFSA_OK)
+        throw LearnerError("wfsa_dev_qn_get_state: ", wfsa_dev_last_error());
+    grad_cache = grad;
+    host_state_stale = false;
 }
 
 }  // namespace wfsa

@@ -31,6 +31,15 @@ public:
     // any throw).
     void RunDevice(double eta, double tol, int32_t max_epochs, double* info_rows, int32_t* epochs_done);
 
+    // RunDevice leaves (x, lambda, grad) on the device: consecutive runs pass
+    // them on without a host round trip.  Every other use of the learner
+    // first pulls them back (PullDeviceState); one that may change x or
+    // lambda on the host then marks the device copy out of date
+    // (HostStateChanged), so the next run uploads it.  The C ABI
+    // (host_api.cpp) does both at its entry points.
+    void PullDeviceState();
+    void HostStateChanged() { dev_state_valid = false; }
+
     struct Timing {
         int64_t steps = 0;
         double begin_ms = 0, overlap_ms = 0, wait_ms = 0, post_ms = 0;
@@ -49,7 +58,10 @@ private:
     bool exponential_lambda = false;
     bool dev_qn_ready = false, dev_qn_exp = false;   // wfsa_dev_qn_setup done for this build
     int32_t dev_qn_rmin = -1;                        // ... with this info_rmin
+    bool dev_state_valid = false;   // the device holds this learner's (x, lambda)
+    bool host_state_stale = false;  // the device's (x, lambda, grad) are newer than the host's
     Timing timing;
+    std::vector<double> rows_buf;   // RunDevice's info rows
 };
 
 }  // namespace wfsa

@@ -839,7 +839,7 @@ __global__ __launch_bounds__(kWide2Block) void wide2_kernel(WideArgs a) {
             const int64_t rn = roff + last_n;
             for (int d = lane; d < nb; d += kWave) Nx[d] = 0.0;
             wave_sync();
-            for (int e0 = eb + lane; e0 < ((a.dbg & 2) ? eb : ee); e0 += kU * kWave) {   // kU edges per lane in flight
+            for (int e0 = eb + lane; e0 < ((WFSA_KDBG(a.dbg) & 2) ? eb : ee); e0 += kU * kWave) {   // kU edges per lane in flight
                 int sd[kU];
                 double w[kU], r[kU];
 #pragma unroll
@@ -915,7 +915,7 @@ __global__ __launch_bounds__(kWide2Block) void wide2_kernel(WideArgs a) {
             if (a.logq) a.logq[sidx] = lq;
             ll += ps * lq;
         }
-        if (!(qh > 0.0) || (a.dbg & 1)) continue;
+        if (!(qh > 0.0) || (WFSA_KDBG(a.dbg) & 1)) continue;
         wave_fence();   // the rows in H (and ex) are visible to every lane
         // backward (beta scaled so that alpha_i beta_i is the node posterior):
         // beta_{i+1} in Bn (LDS), beta_i summed into Bi (LDS)
@@ -949,7 +949,7 @@ __global__ __launch_bounds__(kWide2Block) void wide2_kernel(WideArgs a) {
             const double sc = ldexp(1.0, -ex_next), sci = ldexp(1.0, -ex_i);
             for (int d = lane; d < na; d += kWave) Bi[d] = 0.0;
             wave_sync();
-            for (int e0 = eb + lane; e0 < ((a.dbg & 2) ? eb : ee); e0 += kU * kWave) {
+            for (int e0 = eb + lane; e0 < ((WFSA_KDBG(a.dbg) & 2) ? eb : ee); e0 += kU * kWave) {
                 int4 en[kU];
                 double w[kU], af[kU], bn[kU];
 #pragma unroll
@@ -1549,7 +1549,7 @@ __device__ __forceinline__ double small_bubble(const BubbleArgs& a, const int4* 
     }
     double ew[RE];
 #pragma unroll
-    for (int e = 0; e < RE; ++e) ew[e] = (a.dbg & 2) ? 1.0 + 1e-3 * code[e] : a.ewp[code[e]];   // padding edges carry the zero-slot code
+    for (int e = 0; e < RE; ++e) ew[e] = (WFSA_KDBG(a.dbg) & 2) ? 1.0 + 1e-3 * code[e] : a.ewp[code[e]];   // padding edges carry the zero-slot code
     double A[N], B[N];
 #pragma unroll
     for (int k = 0; k < N; ++k) {
@@ -1586,7 +1586,7 @@ __device__ __forceinline__ double small_bubble(const BubbleArgs& a, const int4* 
             const int src = sd[e] & 0xffff;
             const double bb = ew[e] * reg_get(B, sd[e] >> 16);
             reg_add(B, src, bb);
-            if (slot[e] >= 0 && !(a.dbg & 1)) a.contrib[slot[e]] = reg_get(A, src) * bb * scale;
+            if (slot[e] >= 0 && !(WFSA_KDBG(a.dbg) & 1)) a.contrib[slot[e]] = reg_get(A, src) * bb * scale;
         }
     const double lz = log(Z);
     if (a.logq) global_add(&a.logq[q[0].y], lz);
@@ -2231,10 +2231,8 @@ hipError_t launch_stream_headers(uint4* stream, const int64_t* g_base, const int
 hipError_t launch_compiled(const CompiledArgs& a, int grid, int block, size_t lds, hipStream_t stream) {
     const dim3 g{unsigned(grid), 1, 1}, b{unsigned(block), 1, 1};
     if (!a.with_grad) {   // per-iteration form: w staged in LDS or read from global
-        static const int dbg = [] {
-            const char* e = std::getenv("WFSA_FBS_DBG");
-            return e ? std::atoi(e) : 0;
-        }();
+#ifdef WFSA_EXPERIMENTS
+        static const int dbg = experiment_knob("WFSA_FBS_DBG");
         if (dbg == 1) {
             hipLaunchKernelGGL((fbs_kernel<false, true, false, 1>), g, b, lds, stream, a);
             return hipGetLastError();
@@ -2275,6 +2273,7 @@ hipError_t launch_compiled(const CompiledArgs& a, int grid, int block, size_t ld
             hipLaunchKernelGGL((fbs_kernel<false, true, false, 9>), g, b, lds, stream, a);
             return hipGetLastError();
         }
+#endif
         const int key = (a.tables >= 1 ? 4 : 0) + (a.wide ? 2 : 0) + (a.multi ? 1 : 0);
         if (a.bub_on && a.bub.rmin_acc) {   // the bubbles also feed the rmin column
             switch (key) {

@@ -16,6 +16,22 @@
 
 #include <cstddef>
 #include <cstdint>
+#include <cstdlib>
+
+// Timing experiments that skip work on purpose (WFSA_FBS_DBG, WFSA_BUB_DBG,
+// WFSA_QN_DBG, WFSA_W2_DBG) exist only in a build made with
+// `make EXPERIMENTS=1`; the release library ignores those variables and its
+// kernels carry no such branch.
+#ifdef WFSA_EXPERIMENTS
+#define WFSA_KDBG(x) (x)
+inline int experiment_knob(const char* name) {
+    const char* e = std::getenv(name);
+    return e ? std::atoi(e) : 0;
+}
+#else
+#define WFSA_KDBG(x) 0
+inline int experiment_knob(const char*) { return 0; }
+#endif
 
 namespace wfsa {
 

@@ -38,6 +38,16 @@ struct wfsa_learner {
     QuasiNewtonLearner* qn = nullptr;   // exactly one of these is set
     HessianLearner* hs = nullptr;
     int width() const { return hs ? 9 : 7; }   // GetOptimizationInfo values
+    // the learner for a host-side use: (x, lambda, grad) the device-resident
+    // loop left on the device come back first; a use that may change x or
+    // lambda (writes) makes the next wfsa_learner_run upload them again
+    Learner& host(bool writes) {
+        if (qn) {
+            qn->PullDeviceState();
+            if (writes) qn->HostStateChanged();
+        }
+        return *base;
+    }
 };
 
 struct wfsa_synth {
@@ -206,7 +216,12 @@ void wfsa_learner_destroy(wfsa_learner* l) { delete l; }
 
 int wfsa_learner_set_comm(wfsa_learner* l, int nranks, int rank, const uint8_t id[WFSA_COMM_ID_BYTES]) {
     if (!l) return null_arg("learner");
-    return guarded([&] { l->base->SetCommunicator(nranks, rank, id); });
+    return guarded([&] { l->host(true).SetCommunicator(nranks, rank, id); });
+}
+
+int wfsa_learner_set_comm_host(wfsa_learner* l, int nranks, int rank, wfsa_host_allreduce_fn fn, void* user) {
+    if (!l) return null_arg("learner");
+    return guarded([&] { l->host(true).SetHostCommunicator(nranks, rank, fn, user); });
 }
 
 int wfsa_learner_build_packed(wfsa_learner* l, wfsa_fsa* f, const uint8_t* sym, const int64_t* off,
@@ -217,7 +232,7 @@ int wfsa_learner_build_packed(wfsa_learner* l, wfsa_fsa* f, const uint8_t* sym, 
         for (int64_t s = 0; s < n; ++s) sum += weights[s];
         std::vector<double> w(weights, weights + n);
         for (auto& v : w) v /= sum;   // Corpus::Renormalize (main.cpp:154)
-        l->base->BuildFromPacked(f->fsa, sym, off, w.data(), n);
+        l->host(true).BuildFromPacked(f->fsa, sym, off, w.data(), n);
     });
 }
 
@@ -234,13 +249,13 @@ int wfsa_learner_set_info_rmin(wfsa_learner* l, int on) {
 
 int wfsa_learner_load_matrices(wfsa_learner* l, const char* prefix) {
     if (!l || !prefix) return null_arg("learner/prefix");
-    return guarded([&] { l->base->LoadMatrices(prefix); });
+    return guarded([&] { l->host(true).LoadMatrices(prefix); });
 }
 
 int wfsa_learner_save_matrices(wfsa_learner* l, const char* prefix) {
     if (!l || !prefix) return null_arg("learner/prefix");
     return guarded([&] {
-        if (!l->base->SaveMatrices(prefix))
+        if (!l->host(false).SaveMatrices(prefix))
             throw LearnerError("no path matrices to save: only matrices that were loaded exist on this build");
     });
 }
@@ -248,6 +263,7 @@ int wfsa_learner_save_matrices(wfsa_learner* l, const char* prefix) {
 int wfsa_learner_finalize(wfsa_learner* l) {
     if (!l) return null_arg("learner");
     return guarded([&] {
+        l->host(true);
         if (l->base->GetNumberOfParameters() == 0) throw LearnerError("Empty automaton!");
         if (l->base->GetNumberOfStrings() == 0) throw LearnerError("Automaton cannot generate any of the strings!");
         l->base->Finalize();
@@ -278,7 +294,7 @@ int wfsa_learner_info_get(wfsa_learner* l, wfsa_learner_info* o) {
 
 int wfsa_learner_init(wfsa_learner* l, int flags, const double* x0) {
     if (!l) return null_arg("learner");
-    return guarded([&] { l->base->Init(flags, x0); });
+    return guarded([&] { l->host(true).Init(flags, x0); });
 }
 
 int wfsa_learner_info_width(wfsa_learner* l) { return l ? l->width() : 0; }
@@ -286,7 +302,7 @@ int wfsa_learner_info_width(wfsa_learner* l) { return l ? l->width() : 0; }
 int wfsa_learner_step(wfsa_learner* l, double eta, double tol, double* info, int32_t* halt) {
     if (!l) return null_arg("learner");
     return guarded([&] {
-        l->base->OptimizationStep(eta, false);
+        l->host(true).OptimizationStep(eta, false);
         const auto v = l->base->GetOptimizationInfo();
         if (info)
             for (size_t i = 0; i < size_t(l->width()); ++i) info[i] = i < v.size() ? v[i] : 0.0;
@@ -321,6 +337,7 @@ int wfsa_learner_objective_grad(wfsa_learner* l, double* kl, double* grad, doubl
     if (!l) return null_arg("learner");
     return guarded([&] {
         const std::vector<double>* g;
+        l->host(false);
         if (l->qn) {
             l->qn->ComputeExpX();
             l->qn->ComputeGrad();
@@ -343,21 +360,22 @@ int wfsa_learner_objective_grad(wfsa_learner* l, double* kl, double* grad, doubl
 
 int wfsa_learner_get_x(wfsa_learner* l, double* x) {
     if (!l || !x) return null_arg("learner/x");
-    std::memcpy(x, l->base->GetWeights(), size_t(l->base->GetNumberOfParameters()) * sizeof(double));
-    return WFSA_OK;
+    return guarded([&] {
+        std::memcpy(x, l->host(false).GetWeights(), size_t(l->base->GetNumberOfParameters()) * sizeof(double));
+    });
 }
 
 int wfsa_learner_get_grad(wfsa_learner* l, double* grad) {
     if (!l || !grad) return null_arg("learner/grad");
-    const auto& g = l->base->GetLastGradient();
-    std::memcpy(grad, g.data(), g.size() * sizeof(double));
-    return WFSA_OK;
+    return guarded([&] {
+        const auto& g = l->host(false).GetLastGradient();
+        std::memcpy(grad, g.data(), g.size() * sizeof(double));
+    });
 }
 
 int wfsa_learner_set_x(wfsa_learner* l, const double* x) {
     if (!l || !x) return null_arg("learner/x");
-    l->base->SetWeights(x);
-    return WFSA_OK;
+    return guarded([&] { l->host(true).SetWeights(x); });
 }
 
 int wfsa_learner_get_p(wfsa_learner* l, double* p) {
@@ -385,13 +403,13 @@ int wfsa_learner_path_counts(wfsa_learner* l, double* out, uint8_t* recognized) 
 
 int wfsa_learner_renormalize(wfsa_learner* l) {
     if (!l) return null_arg("learner");
-    return guarded([&] { l->base->Renormalize(); });
+    return guarded([&] { l->host(true).Renormalize(); });
 }
 
 int wfsa_learner_dump(wfsa_learner* l, wfsa_fsa* f, const char* path) {
     if (!l || !f || !path) return null_arg("learner/fsa/path");
     return guarded([&] {
-        l->base->RewriteWeights(f->fsa);
+        l->host(false).RewriteWeights(f->fsa);
         FILE* fp = std::fopen(path, "wb");
         if (!fp) throw LearnerError("Unable to open output file \"", path, "\" for writing!");
         f->fsa.Dump(fp);
@@ -402,7 +420,7 @@ int wfsa_learner_dump(wfsa_learner* l, wfsa_fsa* f, const char* path) {
 int wfsa_learner_result(wfsa_learner* l, double out[8]) {
     if (!l || !out) return null_arg("learner/out");
     return guarded([&] {
-        const auto v = l->base->GetOptimizationResult(false);
+        const auto v = l->host(true).GetOptimizationResult(false);
         for (size_t i = 0; i < 8; ++i) out[i] = i < v.size() ? v[i] : 0.0;
         if (v.empty()) throw LearnerError("this optimizer has no evaluation result");
     });

@@ -32,7 +32,7 @@ void usage() {
                  "  -l, --eta X            learning rate (1.0)\n"
                  "  -tol X                 halting tolerance (1e-6)\n"
                  "  -i, --init FLAGS       1 uniform, 2 normalize, 4 Lagrange init, 8 Hessian of the objective,\n"
-                 "                         16 fill-reducing order (no effect: dense factorisation), 32 exponential lambda\n"
+                 "                         16 fill-reducing (minimum-degree) order of the sparse KKT factorisation, 32 exponential lambda\n"
                  "  -n, --normalize        normalize the automaton after optimization\n"
                  "  -eval                  evaluate the model after optimization\n"
                  "  -s, --suppress         do not print the learned FSA\n"

@@ -52,9 +52,9 @@ __global__ __launch_bounds__(NT) void qn_step_kernel(QnArgs a) {
     // global-memory latencies): the flags with the constraint's extent and its
     // slot group; its members' slot runs, full indices and x together with the
     // group's slot chunks; the members' constant gradient parts.
-    if (a.dbg == 3) return;   // (timing experiments: the launch alone)
+    if (WFSA_KDBG(a.dbg) == 3) return;   // (timing experiments: the launch alone)
     const bool have = c < a.k;
-    const bool slots = FUSED && a.contrib && a.dbg != 5;   // (5: timing experiments, no slot sums)
+    const bool slots = FUSED && a.contrib && WFSA_KDBG(a.dbg) != 5;   // (5: timing experiments, no slot sums)
     int b = 0, e = 0, gnch = 0;
     int64_t gb = 0;
     double lam = 0.0;
@@ -81,7 +81,7 @@ __global__ __launch_bounds__(NT) void qn_step_kernel(QnArgs a) {
         rmin_strings_block(a.rm, c, red, red + kMaxBlockWaves / 2);
     }
     if (c >= max(a.k, 1)) return;   // (blocks beyond the constraints: the rmin pass only)
-    if (a.dbg == 1) return;   // (timing experiments, WFSA_QN_DBG: the launch and first round only)
+    if (WFSA_KDBG(a.dbg) == 1) return;   // (timing experiments, WFSA_QN_DBG: the launch and first round only)
     double gerr = 0.0, g = 0.0;
     if (have) {
         const int nm = e - b;
@@ -255,10 +255,7 @@ __global__ void qn_weights_kernel(const double* x, const int32_t* trim, int32_t 
 }  // namespace
 
 hipError_t launch_qn_step(const QnArgs& a_in, bool fused, hipStream_t stream) {
-    static const int dbg = [] {
-        const char* e = std::getenv("WFSA_QN_DBG");
-        return e ? std::atoi(e) : 0;
-    }();
+    static const int dbg = experiment_knob("WFSA_QN_DBG");
     QnArgs a = a_in;
     a.dbg = dbg;
     if (a.seg_cap <= 0 || a.seg_cap > kQnMaxSeg) a.seg_cap = kQnMaxSeg;

@@ -128,7 +128,10 @@ struct wfsa_dev {
     double* qst = nullptr;
     double* qst_dev = nullptr;
     size_t qst_n = 0;
-    int timing_stride = 16;   // QN runs time every 16th step's kernels (WFSA_TIMING_STRIDE)
+    // QN runs time the kernels of every 16th step (WFSA_TIMING_STRIDE), steps
+    // stride-1, 2*stride-1, ...: not the first, whose launch latency the
+    // event markers would lengthen
+    int timing_stride = 16;
 
     // model
     bool has_model = false;
@@ -176,6 +179,9 @@ struct wfsa_dev {
     DevBuf<double> fixed_grad;       // [n_params] gradient of the trivial words (constant)
     DevBuf<double> fixed_t;          // [qn_n] the same in trimmed order (QN runs)
     bool fixed_t_on = false;
+    int64_t fixed_t_key = -1;        // (prep_gen, qn setup) the gather above was made for
+    int64_t qn_setup_gen = 0;
+    bool qn_flags_clear = false;     // halted / halt_pending are 0 (the last run did not halt)
     bool eval_no_slice = false;      // this evaluation's stream kernel skips edge_weight_slice
     int32_t lead_grp_nch = 1;        // chunks of the largest constraint-led slot group
     int32_t qn_max_nm = 1;           // members of the largest constraint
@@ -1574,10 +1580,7 @@ wfsa::BubbleArgs bubble_args(wfsa_dev* ctx, bool want_logq, const unsigned* halt
     b.ll_part = ll_part;
     b.logq = want_logq ? ctx->logq.ptr : nullptr;
     b.halted = halted;
-    static const int dbg = [] {
-        const char* e = std::getenv("WFSA_BUB_DBG");
-        return e ? std::atoi(e) : 0;
-    }();
+    static const int dbg = experiment_knob("WFSA_BUB_DBG");
     b.dbg = dbg;
     return b;
 }
@@ -1706,10 +1709,7 @@ int enqueue_evaluation(wfsa_dev* ctx, bool want_logq, const unsigned* halted, in
             a.list = ctx->w2_list.ptr;
             a.n_list = ctx->w2_n;
             a.grad_lds = ctx->w2_lgrad ? 1 : 0;
-            static const int w2dbg = [] {
-                const char* e = std::getenv("WFSA_W2_DBG");
-                return e ? std::atoi(e) : 0;
-            }();
+            static const int w2dbg = experiment_knob("WFSA_W2_DBG");
             a.dbg = w2dbg;
             HIP_TRY(wfsa::launch_pair_weights(ctx->pt_ent.ptr, ctx->pt_ne, ctx->ew.ptr, ctx->lw.ptr, ctx->pt_w.ptr, s));
             const size_t lds = wfsa::wide2_lds(ctx->n_params, ctx->w2_lgrad, ctx->w2_waves, ctx->pt_max_n);
@@ -2553,6 +2553,8 @@ int wfsa_dev_rmin(wfsa_dev* ctx, double* rmin, int64_t* string_index) {
     if (ctx->in_flight) return fail(WFSA_ERR_ARG, "an evaluation is in flight");
     if (ctx->dense) return fail(WFSA_ERR_CAPACITY, "rmin: not available on the dense path");
     if (ctx->prep_level < 2) return fail(WFSA_ERR_ARG, "rmin: evaluate the objective first");
+    if (ctx->mpath && ctx->comm)   // its index is a path of this rank's matrices: no global counterpart
+        return fail(WFSA_ERR_ARG, "rmin: matrix-file mode runs the rmin column on one rank only");
     if (ctx->rm_res.n < 4) HIP_TRY(ctx->rm_res.alloc(4));
     if (int rc = enqueue_rmin(ctx, nullptr, ctx->rm_res.ptr)) return rc;
     if (int rc = combine_rmin(ctx, ctx->rm_res.ptr, ctx->stream)) return rc;
@@ -2706,6 +2708,8 @@ int wfsa_dev_qn_setup(wfsa_dev* ctx, const wfsa_qn_desc* d) {
     ctx->qn_plogp = d->plogp;
     ctx->qn_exp_lambda = d->exponential_lambda ? 1 : 0;
     if (d->info_rmin && ctx->dense) return fail(WFSA_ERR_CAPACITY, "the rmin column is not available on the dense path");
+    if (d->info_rmin && ctx->mpath && ctx->comm)
+        return fail(WFSA_ERR_ARG, "rmin: matrix-file mode runs the rmin column on one rank only");
     ctx->qn_rmin = d->info_rmin != 0;
     if (ctx->qn_rmin) HIP_TRY(ctx->rm_res.alloc(4));
     // the contribution slots in trimmed order (kept parameters first, the
@@ -2726,6 +2730,8 @@ int wfsa_dev_qn_setup(wfsa_dev* ctx, const wfsa_qn_desc* d) {
             if (int rc = layout_slots(ctx, pos_of)) return rc;
     }
     ctx->h_cptr = cptr;
+    ctx->qn_setup_gen++;
+    ctx->qn_flags_clear = false;
     ctx->qn_ready = true;
     return WFSA_OK;
 }
@@ -2791,6 +2797,11 @@ int wfsa_dev_qn_run(wfsa_dev* ctx, double eta, double tol, int32_t max_steps, do
     if (!ctx->has_corpus) return fail(WFSA_ERR_ARG, "load a corpus first");
     if (ctx->in_flight) return fail(WFSA_ERR_ARG, "an evaluation is in flight");
     if (max_steps <= 0) return WFSA_OK;
+    using clk = std::chrono::steady_clock;
+    static const bool trace = std::getenv("WFSA_RUN_TRACE") != nullptr;
+    const auto tr0 = clk::now();
+    auto tr_ms = [&](clk::time_point t) { return std::chrono::duration<double, std::micro>(t - tr0).count(); };
+    clk::time_point tr_pro{}, tr_first{}, tr_last{}, tr_end{};
     if (ctx->prep_level < 2)
         if (int rc = prepare(ctx, 2)) return rc;
     if (int rc = collect_timing(ctx)) return rc;
@@ -2806,16 +2817,23 @@ int wfsa_dev_qn_run(wfsa_dev* ctx, double eta, double tol, int32_t max_steps, do
                          (long long)sz[sz.size() / 2]);
     }
     hipStream_t s = ctx->stream;
-    HIP_TRY(hipMemsetAsync(ctx->qn_halted.ptr, 0, 2 * sizeof(unsigned), s));
+    if (!ctx->qn_flags_clear) HIP_TRY(hipMemsetAsync(ctx->qn_halted.ptr, 0, 2 * sizeof(unsigned), s));
+    ctx->qn_flags_clear = false;
     ctx->fin_pending = false;
     ctx->fin_for_fbs.active = 0;
     // the constant trivial-word gradient in trimmed order, so the fused QN
-    // step loads it with its members' x (no load round on their full index)
-    ctx->fixed_t_on = false;
+    // step loads it with its members' x (no load round on their full index);
+    // made once per preparation and QN set-up
+    const int64_t ft_key = ctx->prep_gen * 1000003 + ctx->qn_setup_gen;
     if (ctx->qn_fused && !ctx->dense && !ctx->mpath && ctx->n_groups > 0 && ctx->qn_n > 0) {
-        HIP_TRY(ctx->fixed_t.alloc(size_t(ctx->qn_n)));
-        HIP_TRY(wfsa::launch_gather(ctx->fixed_grad.ptr, ctx->qn_full_of.ptr, ctx->qn_n, ctx->fixed_t.ptr, s));
-        ctx->fixed_t_on = true;
+        if (!ctx->fixed_t_on || ctx->fixed_t_key != ft_key) {
+            HIP_TRY(ctx->fixed_t.alloc(size_t(ctx->qn_n)));
+            HIP_TRY(wfsa::launch_gather(ctx->fixed_grad.ptr, ctx->qn_full_of.ptr, ctx->qn_n, ctx->fixed_t.ptr, s));
+            ctx->fixed_t_on = true;
+            ctx->fixed_t_key = ft_key;
+        }
+    } else {
+        ctx->fixed_t_on = false;
     }
     const bool piped = pipe_ok(ctx);
     if (piped) {   // the second weight buffer; the pipe stream starts after everything enqueued so far
@@ -2827,14 +2845,21 @@ int wfsa_dev_qn_run(wfsa_dev* ctx, double eta, double tol, int32_t max_steps, do
                                hipMemcpyDeviceToDevice, s));
         HIP_TRY(hipEventRecord(ctx->p_start, s));
     }
+    // steps whose kernels are timed: every stride-th (not the first), or the
+    // last of a run shorter than the stride
+    auto timed_step = [&](int32_t e) {
+        const int32_t k = ctx->timing_stride;
+        return e % k == k - 1 || (max_steps < k && e == max_steps - 1);
+    };
     const unsigned base = ctx->seq;
     int32_t enq = 0, done = 0, st = 0;
     bool stop = false;
     double c_ms_sum = 0.0, fb_ms_sum = 0.0;
     int64_t timed = 0;
+    if (trace) tr_pro = clk::now();
     while (done < max_steps) {
         while (!stop && enq < max_steps && enq - done < kQnDepth) {
-            const bool tm = enq % ctx->timing_stride == 0;
+            const bool tm = timed_step(enq);
             if (int rc = piped ? enqueue_qn_step_piped(ctx, eta, tol, enq, tm) : enqueue_qn_step(ctx, eta, tol, enq, tm))
                 return rc;
             ++enq;
@@ -2844,10 +2869,11 @@ int wfsa_dev_qn_run(wfsa_dev* ctx, double eta, double tol, int32_t max_steps, do
             if (int rc = flush_qn_finish(ctx)) return rc;
         if (done >= enq) break;
         if (int rc = wait_published(ctx, base + unsigned(done) + 1u)) return rc;
+        if (trace) (done == 0 ? tr_first : tr_last) = clk::now();
         const int slot = done % kQnDepth;
         const double* row = ctx->qn_ring + size_t(slot) * wfsa::kQnRow;
         const unsigned rs = unsigned(row[7]);
-        if (ctx->kernel_timing && done % ctx->timing_stride == 0) {
+        if (ctx->kernel_timing && timed_step(done)) {
             float c = 0.f, f = 0.f;
             const hipEvent_t end = ctx->k2_kc[slot] ? ctx->kc[slot] : ctx->k2[slot];
             if (hipEventSynchronize(end) == hipSuccess &&
@@ -2881,7 +2907,20 @@ int wfsa_dev_qn_run(wfsa_dev* ctx, double eta, double tol, int32_t max_steps, do
         HIP_TRY(wfsa::launch_qn_weights(ctx->qn_x.ptr, ctx->qn_trim.ptr, ctx->n_params, ctx->w_full.ptr,
                                         ctx->ewp.ptr, s));
     }
-    HIP_TRY(hipStreamSynchronize(s));
+    // the last step's row is in: wait for the stream's tail by polling (a
+    // blocking synchronize costs a wake-up of ~10 us on this system)
+    for (;;) {
+        const hipError_t e = hipStreamQuery(s);
+        if (e == hipSuccess) break;
+        if (e != hipErrorNotReady) return fail(WFSA_ERR_HIP, "device failure: %s", hipGetErrorString(e));
+        __builtin_ia32_pause();
+    }
+    if (trace) {
+        tr_end = clk::now();
+        std::fprintf(stderr, "[wfsa] qn_run %d steps: prologue %.1f us, first row %.1f, last row %.1f, end %.1f\n",
+                     done, tr_ms(tr_pro), tr_ms(tr_first), done > 1 ? tr_ms(tr_last) : tr_ms(tr_first), tr_ms(tr_end));
+    }
+    ctx->qn_flags_clear = st == 0;
     ctx->stats.fb_launches += timed;
     ctx->stats.fb_kernel_ms += fb_ms_sum;
     ctx->stats.compiled_kernel_ms += c_ms_sum;
@@ -2895,6 +2934,7 @@ int wfsa_dev_hf_setup(wfsa_dev* ctx, int64_t* n_pairs) {
     if (!ctx->has_model || !ctx->has_corpus) return fail(WFSA_ERR_ARG, "load a model and a corpus first");
     if (ctx->in_flight) return fail(WFSA_ERR_ARG, "an evaluation is in flight");
     if (ctx->dense) return fail(WFSA_ERR_CAPACITY, "second-order terms: not available on the dense path");
+    if (ctx->mpath && ctx->comm) return fail(WFSA_ERR_ARG, "second-order terms: matrix-file mode runs on one rank only");
     if (ctx->mpath) {   // the pattern and the slots come from the path matrices
         HIP_TRY(ctx->mpath->hf_setup(ctx->hf_pairs, ctx->stream));
         HIP_TRY(ctx->hf_out.alloc(std::max<size_t>(ctx->hf_pairs.size() / 2, 1)));
@@ -2935,21 +2975,6 @@ int wfsa_dev_hf_setup(wfsa_dev* ctx, int64_t* n_pairs) {
             tv.insert(tv.end(), V.begin(), V.end());
         }
     }
-    const bool local_bad = bad_string >= 0;
-    if (ctx->comm) {   // every rank learns whether any cannot build its part (no rank is left in a collective)
-        DevBuf<double> t;
-        double bad = local_bad ? 1.0 : 0.0;
-        HIP_TRY(t.upload(&bad, 1, s));
-        COMM_TRY(ctx, t.ptr, 1, wfsa::RedOp::SumF64, s);
-        HIP_TRY(t.download(&bad, 1, s));
-        HIP_TRY(hipStreamSynchronize(s));
-        if (bad > 0 && !local_bad)
-            return fail(WFSA_ERR_CAPACITY, "second-order terms: another rank has a string beyond their limits");
-    }
-    if (local_bad)
-        return fail(WFSA_ERR_CAPACITY, "second-order terms: string %lld has %s equivocal parameters (at most %d, "
-                    "from at most 4096 parameters on its paths)", (long long)bad_string,
-                    bad_v ? std::to_string(bad_v).c_str() : "too many", wfsa::kHfTravMaxV);
     const int32_t np = ctx->n_params, nb = ctx->n_bubbles;
     std::vector<int32_t> off(size_t(std::max(nb, 1)));
     std::vector<int32_t> buf(ctx->bub.n);
@@ -2971,15 +2996,14 @@ int wfsa_dev_hf_setup(wfsa_dev* ctx, int64_t* n_pairs) {
     std::vector<int64_t> base(size_t(nb) + 1, 0), keys;
     std::vector<std::vector<int32_t>> ep;
     std::vector<int32_t> tmp;
-    for (int32_t b = 0; b < nb; ++b) {
+    size_t bad_edge_params = 0;   // a bubble edge with more than 8 parameters
+    for (int32_t b = 0; b < nb && bad_edge_params == 0; ++b) {
         const int32_t o = off[size_t(b)];
         const int edges = buf[size_t(o)] >> 16;
         ep.assign(size_t(edges), {});
         for (int e = 0; e < edges; ++e) {
             params(buf[size_t(o) + 4 + 2 * size_t(e)], tmp);
-            if (tmp.size() > 8)
-                return fail(WFSA_ERR_CAPACITY, "second-order terms: a bubble edge carries %zu parameters (max 8)",
-                            tmp.size());
+            if (tmp.size() > 8 && bad_edge_params == 0) bad_edge_params = tmp.size();
             ep[size_t(e)] = tmp;
         }
         for (int e = 0; e < edges; ++e)
@@ -2989,6 +3013,26 @@ int wfsa_dev_hf_setup(wfsa_dev* ctx, int64_t* n_pairs) {
                         if (j <= k) keys.push_back(int64_t(j) * np + k);
         base[size_t(b) + 1] = int64_t(keys.size());
     }
+    // every limit is checked before the status all-reduce below, so a rank
+    // that fails never leaves the others waiting in a later collective
+    const bool local_bad = bad_string >= 0 || bad_edge_params > 0;
+    if (ctx->comm) {   // every rank learns whether any cannot build its part (no rank is left in a collective)
+        DevBuf<double> t;
+        double bad = local_bad ? 1.0 : 0.0;
+        HIP_TRY(t.upload(&bad, 1, s));
+        COMM_TRY(ctx, t.ptr, 1, wfsa::RedOp::SumF64, s);
+        HIP_TRY(t.download(&bad, 1, s));
+        HIP_TRY(hipStreamSynchronize(s));
+        if (bad > 0 && !local_bad)
+            return fail(WFSA_ERR_CAPACITY, "second-order terms: another rank has a string beyond their limits");
+    }
+    if (bad_edge_params > 0)
+        return fail(WFSA_ERR_CAPACITY, "second-order terms: a bubble edge carries %zu parameters (max 8)",
+                    bad_edge_params);
+    if (local_bad)
+        return fail(WFSA_ERR_CAPACITY, "second-order terms: string %lld has %s equivocal parameters (at most %d, "
+                    "from at most 4096 parameters on its paths)", (long long)bad_string,
+                    bad_v ? std::to_string(bad_v).c_str() : "too many", wfsa::kHfTravMaxV);
     // the traversal strings' slots follow the bubbles': (a <= b) over V_s, row-major
     std::vector<int64_t> tbase;
     for (const int4& t : tl) {
@@ -3187,6 +3231,20 @@ int wfsa_dev_comm_init(wfsa_dev* ctx, int nranks, int rank, const uint8_t id[WFS
     return WFSA_OK;
 }
 
+int wfsa_dev_comm_init_host(wfsa_dev* ctx, int nranks, int rank, wfsa_host_allreduce_fn fn, void* user) {
+    if (int rc = check_ctx(ctx)) return rc;
+    if (nranks < 1 || rank < 0 || rank >= nranks || !fn) return fail(WFSA_ERR_ARG, "bad communicator arguments");
+    ctx->comm.reset();
+    std::string err;
+    ctx->comm = wfsa::make_host_collective(nranks, rank, fn, user, err);
+    if (!ctx->comm) return fail(WFSA_ERR_RCCL, "%s", err.c_str());
+    ctx->nranks = nranks;
+    ctx->rank = rank;
+    if (ctx->prep_level >= 2) ctx->prep_level = 1;   // (as wfsa_dev_comm_init)
+    ctx->qn_fused = false;
+    return WFSA_OK;
+}
+
 int wfsa_dev_allreduce(wfsa_dev* ctx, double* host_buf, int64_t count) {
     if (int rc = check_ctx(ctx)) return rc;
     if (count <= 0) return WFSA_OK;
@@ -3205,6 +3263,9 @@ int wfsa_dev_get_stats(wfsa_dev* ctx, wfsa_dev_stats* out) {
     if (!ctx->in_flight)
         if (int rc = collect_timing(ctx)) return rc;
     *out = ctx->stats;
+    out->comm_ranks = ctx->comm ? ctx->comm->nranks() : 1;
+    const char* ps = ctx->comm ? ctx->comm->peer_state() : "off";
+    out->comm_peer = std::strcmp(ps, "on") == 0 ? 1 : std::strcmp(ps, "failed") == 0 ? -1 : 0;
     return WFSA_OK;
 }
 

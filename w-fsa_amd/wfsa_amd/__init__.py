@@ -204,6 +204,14 @@ class QuasiNewtonLearner:
     def SaveMatrices(self, prefix):
         check_host(load().wfsa_learner_save_matrices(self._h, os.fsencode(prefix)))
 
+    def SetHostCommunicator(self, nranks, rank, allreduce):
+        """a communicator over a host callback (wfsa_learner_set_comm_host):
+        allreduce(array, op) reduces a numpy array in place over the ranks,
+        op "sum" / "min" (float64) or "max" (uint8) -- e.g. torch_allreduce
+        over a gloo process group"""
+        self._host_cb = _host_callback(allreduce)
+        check_host(load().wfsa_learner_set_comm_host(self._h, nranks, rank, self._host_cb, None))
+
     def BuildFromPacked(self, fsa, sym, off, weights):
         self._fsa = fsa
         sym = np.ascontiguousarray(sym, dtype=np.uint8)
@@ -318,6 +326,34 @@ class QuasiNewtonLearner:
         rc = load().wfsa_learner_run(self._h, eta, tol, int(epochs), _ptr(rows), C.byref(done))
         check_host(rc)
         return rows[:done.value].tolist()
+
+
+_OPS = ("sum", "min", "max")
+
+
+def _host_callback(allreduce):
+    """wrap a Python all-reduce as a wfsa_host_allreduce_fn"""
+    def cb(user, buf, count, op):
+        try:
+            ct = C.c_uint8 if op == 2 else C.c_double
+            arr = np.ctypeslib.as_array((ct * int(count)).from_address(buf))
+            allreduce(arr, _OPS[op])
+            return 0
+        except Exception:   # reported to the library as a failed transport
+            import traceback
+            traceback.print_exc()
+            return 1
+    return _lib.HOST_ALLREDUCE_FN(cb)
+
+
+def torch_allreduce(arr, op):
+    """all-reduce a numpy array in place over the default torch.distributed
+    process group (gloo for host buffers)"""
+    import torch
+    import torch.distributed as dist
+    red = {"sum": dist.ReduceOp.SUM, "min": dist.ReduceOp.MIN, "max": dist.ReduceOp.MAX}[op]
+    t = torch.from_numpy(arr)
+    dist.all_reduce(t, op=red)
 
 
 class Device:
@@ -450,6 +486,11 @@ class Device:
         buf = (C.c_uint8 * _lib.COMM_ID_BYTES)()
         check_dev(load().wfsa_dev_comm_local_id(nranks, buf))
         return bytes(buf)
+
+    def comm_init_host(self, nranks, rank, allreduce):
+        """wfsa_dev_comm_init_host (see QuasiNewtonLearner.SetHostCommunicator)"""
+        self._host_cb = _host_callback(allreduce)
+        check_dev(load().wfsa_dev_comm_init_host(self._h, nranks, rank, self._host_cb, None))
 
     def allreduce(self, values):
         a = np.ascontiguousarray(values, dtype=np.float64).copy()

@@ -44,7 +44,12 @@ class DevStats(C.Structure):
         ("host_post_ms", dbl),
         ("dense_rows", i32), ("dense_steps", i32), ("dense_np", i32), ("tier2_strings", i32),
         ("wave_strings", i32), ("wave_row_entries", i64), ("wave_pair_edges", i64),
+        ("comm_ranks", i32), ("comm_peer", i32),
     ]
+
+
+# int fn(void* user, void* buf, int64_t count, int32_t op) (wfsa_host_allreduce_fn)
+HOST_ALLREDUCE_FN = C.CFUNCTYPE(C.c_int, vp, vp, i64, i32)
 
 
 class LearnerInfo(C.Structure):
@@ -88,6 +93,7 @@ _SIGS = {
     "wfsa_dev_comm_init": (C.c_int, [vp, C.c_int, C.c_int, vp]),
     "wfsa_dev_comm_local_id": (C.c_int, [C.c_int, vp]),
     "wfsa_dev_allreduce": (C.c_int, [vp, vp, i64]),
+    "wfsa_dev_comm_init_host": (C.c_int, [vp, C.c_int, C.c_int, vp, vp]),
     "wfsa_dev_get_stats": (C.c_int, [vp, P(DevStats)]),
     # host mirror (wfsa_host.h)
     "wfsa_host_last_error": (C.c_char_p, []),
@@ -104,6 +110,7 @@ _SIGS = {
     "wfsa_learner_create": (C.c_int, [C.c_char_p, C.c_int, P(vp)]),
     "wfsa_learner_destroy": (None, [vp]),
     "wfsa_learner_set_comm": (C.c_int, [vp, C.c_int, C.c_int, vp]),
+    "wfsa_learner_set_comm_host": (C.c_int, [vp, C.c_int, C.c_int, vp, vp]),
     "wfsa_learner_build": (C.c_int, [vp, vp, vp]),
     "wfsa_learner_build_packed": (C.c_int, [vp, vp, vp, vp, vp, i64]),
     "wfsa_learner_finalize": (C.c_int, [vp]),
