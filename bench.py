@@ -133,7 +133,11 @@ def cpu_baseline_enum(syn_text, sym, off, wt, n_sample):
     s_sym = sym[: s_off[-1]].copy()
     s_wt = wt[:n].copy()
     t0 = time.perf_counter()
-    o = Oracle.from_arrays(syn_text, s_sym, s_off, s_wt, mode=ENUM, max_paths=1_000_000)
+    os.environ["ORACLE_BUILD_THREADS"] = "1"   # the reference's enumeration is sequential (mkl_sequential build)
+    try:
+        o = Oracle.from_arrays(syn_text, s_sym, s_off, s_wt, mode=ENUM, max_paths=1_000_000)
+    finally:
+        os.environ.pop("ORACLE_BUILD_THREADS", None)
     t_build = time.perf_counter() - t0
     o.qn_init(7)
     iters = 3
@@ -395,7 +399,7 @@ def launch_ranks(n):
 
 def main():
     args = parse()
-    knobs = sorted(k for k in os.environ if k.startswith("WFSA_") and k.endswith("_DBG"))
+    knobs = sorted(k for k in os.environ if (k.startswith("WFSA_") and k.endswith("_DBG")) or k == "WFSA_LIB")
     if knobs:   # timing experiments that skip work: never inside a measurement
         print(f"bench.py: refusing to measure with {', '.join(knobs)} set", file=sys.stderr)
         sys.exit(2)

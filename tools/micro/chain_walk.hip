@@ -113,6 +113,190 @@ __global__ __launch_bounds__(1024) void walk_b(const uint4* __restrict__ st, int
     if (lane == 0) ll_part[gw] = ll;
 }
 
+// the same with the next group's chunks loaded before the current group is
+// applied (software pipelining across groups, as the real stream kernel does)
+template <bool GATHER>
+__global__ __launch_bounds__(1024) void walk_a_pf(const uint4* __restrict__ st, int n_groups, const double* __restrict__ w,
+                                                  const double* __restrict__ p, double* ll_part) {
+    __shared__ double lw[kSlots];
+    for (int j = threadIdx.x; j < kSlots; j += blockDim.x) lw[j] = w[j];
+    __syncthreads();
+    const int lane = threadIdx.x % kWave;
+    const int gw = blockIdx.x * (blockDim.x / kWave) + threadIdx.x / kWave;
+    const int nw = gridDim.x * (blockDim.x / kWave);
+    double ll = 0.0;
+    uint4 r[kChA], nx[kChA];
+    auto ld = [&](uint4 (&d)[kChA], int g) {
+        const uint4* s = st + size_t(min(g, n_groups - 1)) * kChA * kWave + lane;
+#pragma unroll
+        for (int c = 0; c < kChA; ++c) d[c] = s[c * kWave];
+    };
+    if (gw < n_groups) ld(r, gw);
+    for (int g = gw; g < n_groups; g += nw) {
+        ld(nx, g + nw);
+        double a0 = 0.0, a1 = 0.0;
+#pragma unroll
+        for (int c = 0; c < kChA; ++c) {
+            const uint32_t v[4] = {r[c].x, r[c].y, r[c].z, r[c].w};
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const uint32_t lo = v[i] & 0xffffu, hi = v[i] >> 16;
+                if (GATHER) {
+                    a0 += lw[min(lo, uint32_t(kSlots - 1))] * (lo != 0xffffu);
+                    a1 += lw[min(hi, uint32_t(kSlots - 1))] * (hi != 0xffffu);
+                } else {
+                    a0 += double(lo ^ hi);
+                }
+            }
+        }
+        ll += p[g * kWave + lane] * (a0 + a1);
+#pragma unroll
+        for (int c = 0; c < kChA; ++c) r[c] = nx[c];
+    }
+    ll = wave_sum(ll);
+    if (lane == 0) ll_part[gw] = ll;
+}
+
+template <int K>
+__global__ __launch_bounds__(1024) void walk_b_pf(const uint4* __restrict__ st, int n_groups, const double* __restrict__ sw,
+                                                  const uint16_t* __restrict__ nb, const double* __restrict__ p,
+                                                  double* ll_part) {
+    __shared__ double lw[kSlots];
+    __shared__ uint16_t lnb[kSlots];
+    for (int j = threadIdx.x; j < kSlots; j += blockDim.x) {
+        lw[j] = sw[j];
+        lnb[j] = nb[j];
+    }
+    __syncthreads();
+    const int lane = threadIdx.x % kWave;
+    const int gw = blockIdx.x * (blockDim.x / kWave) + threadIdx.x / kWave;
+    const int nw = gridDim.x * (blockDim.x / kWave);
+    double ll = 0.0;
+    uint4 r[K][kChB], nx[K][kChB];
+    auto ld = [&](uint4 (&d)[K][kChB], int g0) {
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            const uint4* s = st + size_t(min(g0 + k, n_groups - 1)) * kChB * kWave + lane;
+#pragma unroll
+            for (int c = 0; c < kChB; ++c) d[k][c] = s[c * kWave];
+        }
+    };
+    if (gw * K < n_groups) ld(r, gw * K);
+    for (int g0 = gw * K; g0 < n_groups; g0 += nw * K) {
+        ld(nx, g0 + nw * K);
+        double acc[K];
+        int base[K];
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            acc[k] = 0.0;
+            base[k] = 0;
+        }
+#pragma unroll
+        for (int c = 0; c < kChB; ++c) {
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+#pragma unroll
+                for (int h = 0; h < 8; ++h) {
+                    if (c * 32 + i * 8 + h >= kLen) break;
+#pragma unroll
+                    for (int k = 0; k < K; ++k) {
+                        const uint32_t v = (i == 0 ? r[k][c].x : i == 1 ? r[k][c].y : i == 2 ? r[k][c].z : r[k][c].w);
+                        const int slot = base[k] + int((v >> (4 * h)) & 0xfu);
+                        acc[k] += lw[slot];
+                        base[k] = lnb[slot];
+                    }
+                }
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < K; ++k)
+            if (g0 + k < n_groups) ll += p[(g0 + k) * kWave + lane] * acc[k];
+#pragma unroll
+        for (int k = 0; k < K; ++k)
+#pragma unroll
+            for (int c = 0; c < kChB; ++c) r[k][c] = nx[k][c];
+    }
+    ll = wave_sum(ll);
+    if (lane == 0) ll_part[gw] = ll;
+}
+
+// both formats in one kernel: the first nb waves of each block walk nibble
+// groups [0, GB), the others 16-bit groups [GB, G) -- HBM and LDS at once
+__global__ __launch_bounds__(1024) void walk_mix(const uint4* __restrict__ stA, const uint4* __restrict__ stB, int GB,
+                                                 int G, int nbw, const double* __restrict__ w,
+                                                 const double* __restrict__ sw, const uint16_t* __restrict__ nb,
+                                                 const double* __restrict__ p, double* ll_part) {
+    __shared__ double lw[kSlots];
+    __shared__ uint16_t lnb[kSlots];
+    for (int j = threadIdx.x; j < kSlots; j += blockDim.x) {
+        lw[j] = sw[j];
+        lnb[j] = nb[j];
+    }
+    __syncthreads();
+    const int lane = threadIdx.x % kWave;
+    const int wv = threadIdx.x / kWave, wpb = blockDim.x / kWave;
+    double ll = 0.0;
+    if (wv < nbw) {   // nibble waves
+        const int gw = blockIdx.x * nbw + wv, nw = gridDim.x * nbw;
+        uint4 r[kChB], nx[kChB];
+        auto ld = [&](uint4 (&d)[kChB], int g) {
+            const uint4* s = stB + size_t(min(g, GB - 1)) * kChB * kWave + lane;
+#pragma unroll
+            for (int c = 0; c < kChB; ++c) d[c] = s[c * kWave];
+        };
+        if (gw < GB) ld(r, gw);
+        for (int g = gw; g < GB; g += nw) {
+            ld(nx, g + nw);
+            double acc = 0.0;
+            int base = 0;
+#pragma unroll
+            for (int c = 0; c < kChB; ++c)
+#pragma unroll
+                for (int i = 0; i < 4; ++i)
+#pragma unroll
+                    for (int h = 0; h < 8; ++h) {
+                        if (c * 32 + i * 8 + h >= kLen) break;
+                        const uint32_t v = (i == 0 ? r[c].x : i == 1 ? r[c].y : i == 2 ? r[c].z : r[c].w);
+                        const int slot = base + int((v >> (4 * h)) & 0xfu);
+                        acc += lw[slot];
+                        base = lnb[slot];
+                    }
+            ll += p[g * kWave + lane] * acc;
+#pragma unroll
+            for (int c = 0; c < kChB; ++c) r[c] = nx[c];
+        }
+    } else {   // 16-bit waves
+        const int na = wpb - nbw;
+        const int gw = blockIdx.x * na + (wv - nbw), nw = gridDim.x * na;
+        uint4 r[kChA], nx[kChA];
+        auto ld = [&](uint4 (&d)[kChA], int g) {
+            const uint4* s = stA + size_t(min(g, G - 1)) * kChA * kWave + lane;
+#pragma unroll
+            for (int c = 0; c < kChA; ++c) d[c] = s[c * kWave];
+        };
+        if (GB + gw < G) ld(r, GB + gw);
+        for (int g = GB + gw; g < G; g += nw) {
+            ld(nx, g + nw);
+            double a0 = 0.0, a1 = 0.0;
+#pragma unroll
+            for (int c = 0; c < kChA; ++c) {
+                const uint32_t v[4] = {r[c].x, r[c].y, r[c].z, r[c].w};
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    const uint32_t lo = v[i] & 0xffffu, hi = v[i] >> 16;
+                    a0 += lw[min(lo, uint32_t(kSlots - 1))] * (lo != 0xffffu);
+                    a1 += lw[min(hi, uint32_t(kSlots - 1))] * (hi != 0xffffu);
+                }
+            }
+            ll += p[g * kWave + lane] * (a0 + a1);
+#pragma unroll
+            for (int c = 0; c < kChA; ++c) r[c] = nx[c];
+        }
+    }
+    ll = wave_sum(ll);
+    if (lane == 0) ll_part[blockIdx.x * wpb + wv] = ll;
+}
+
 int main() {
     const int S = 1 << 20, G = S / kWave;
     std::mt19937_64 rng(7);
@@ -196,6 +380,30 @@ int main() {
                 grid * 16, bB)) return 1;
         if (run("B nibble, K=4", [&] { hipLaunchKernelGGL(walk_b<4>, dim3(grid), dim3(1024), 0, 0, dB, G, dsw, dnb, dp, dll); },
                 grid * 16, bB)) return 1;
+    }
+    {
+        const int grid = 256;
+        if (run("A 16-bit prefetch, 16 w/CU", [&] { hipLaunchKernelGGL(walk_a_pf<true>, dim3(grid), dim3(1024), 0, 0, dA, G, dsw, dp, dll); },
+                grid * 16, bA)) return 1;
+        if (run("B nibble prefetch, K=1", [&] { hipLaunchKernelGGL(walk_b_pf<1>, dim3(grid), dim3(1024), 0, 0, dB, G, dsw, dnb, dp, dll); },
+                grid * 16, bB)) return 1;
+        if (run("B nibble prefetch, K=2", [&] { hipLaunchKernelGGL(walk_b_pf<2>, dim3(grid), dim3(1024), 0, 0, dB, G, dsw, dnb, dp, dll); },
+                grid * 16, bB)) return 1;
+    }
+    for (int nbw : {4, 5, 6, 8}) {   // mixed: nibble waves per block / 16, groups split in the same ratio
+        for (double f : {0.25, 0.3, 0.35, 0.4}) {
+            const int GB = int(G * f);
+            char nm[64];
+            snprintf(nm, sizeof nm, "mix %d/16 waves nibble, %.2f", nbw, f);
+            const double bytes = bA * (1.0 - f) + bB * f;
+            if (run(nm, [&] { hipLaunchKernelGGL(walk_mix, dim3(256), dim3(1024), 0, 0, dA, dB, GB, G, nbw, dsw, dsw, dnb,
+                                                 dp, dll); }, 256 * 16, bytes)) return 1;
+        }
+    }
+    {   // stream loads alone: the HBM floor of each format
+        const int grid = 256;
+        if (run("A loads only (no LDS)", [&] { hipLaunchKernelGGL(walk_a_pf<false>, dim3(grid), dim3(1024), 0, 0, dA, G, dsw, dp, dll); },
+                grid * 16, bA)) return 1;
     }
     return 0;
 }

@@ -2036,6 +2036,7 @@ hipError_t configure_kernels(int max_dynamic_lds) {
                          reinterpret_cast<const void*>(&fbs_kernel<false, true, true, 0, true>),
                          reinterpret_cast<const void*>(&fbs_kernel<true, true, false, 0, true>),
                          reinterpret_cast<const void*>(&fbs_kernel<true, true, true, 0, true>),
+#ifdef WFSA_EXPERIMENTS
                          reinterpret_cast<const void*>(&fbs_kernel<false, true, false, 1>),
                          reinterpret_cast<const void*>(&fbs_kernel<false, true, false, 3>),
                          reinterpret_cast<const void*>(&fbs_kernel<false, true, false, 4>),
@@ -2045,6 +2046,7 @@ hipError_t configure_kernels(int max_dynamic_lds) {
                          reinterpret_cast<const void*>(&fbs_kernel<false, true, false, 8>),
                          reinterpret_cast<const void*>(&fbs_kernel<false, true, false, 9>),
                          reinterpret_cast<const void*>(&fbs_kernel<false, true, false, 10>),
+#endif
                          reinterpret_cast<const void*>(&wide_kernel<false>)};
     for (const void* f : fns) {   // (static LDS counts against the same 160 KiB)
         hipFuncAttributes attr{};

@@ -394,6 +394,9 @@ struct QnFinish {
 };
 struct QnArgs {
     const double* out;           // [1 + n_full]: gradient parts accumulated so far
+    double* ll_stash;            // non-null (across ranks): out[0], the step's all-reduced log-likelihood,
+                                 // copied here for the step's finish (which rides in the next stream kernel,
+                                 // which zeroes out)
     int32_t use_out;             // (fused: 0 when no traversal string adds to out)
     const double* fixed;         // [n_full] constant trivial-word gradient to add, or null
     const double* fixed_t;       // fused: the same in trimmed order ([n]), or null (then fixed[full_of])

@@ -76,6 +76,7 @@ __global__ __launch_bounds__(NT) void qn_step_kernel(QnArgs a) {
         }
         return;
     }
+    if (a.ll_stash && c == 0 && t == 0) *a.ll_stash = a.out[0];
     if (a.rm_on && c < a.rm_blocks) {   // the rmin strings pass's block c (one launch fewer per step)
         static_assert(kRminBlock == kQnBlock, "the folded rmin pass runs in the QN step's blocks");
         rmin_strings_block(a.rm, c, red, red + kMaxBlockWaves / 2);

@@ -296,6 +296,7 @@ struct wfsa_dev {
     // the QN finish of the last enqueued step, not yet enqueued (fin_pending),
     // and the one handed to the next stream kernel launch (fin_for_fbs)
     wfsa::QnFinish fin_next{}, fin_for_fbs{};
+    DevBuf<double> ll_stash;   // [2] the all-reduced log-likelihood of a multi-rank step, by parity
     std::vector<int32_t> h_cptr;
     bool fin_pending = false, fin_hostable = false;
     DevBuf<unsigned> qn_halted;
@@ -1887,7 +1888,7 @@ int enqueue_qn_step(wfsa_dev* ctx, double eta, double tol, int64_t e, bool timed
             const char* e = std::getenv("WFSA_FIN_HOST");
             return !(e && e[0] == '0');
         }();
-        if (ctx->fin_hostable && fused && ctx->n_groups > 0 && host_fin) {
+        if (ctx->fin_hostable && trellis && ctx->n_groups > 0 && host_fin) {
             ctx->fin_for_fbs = ctx->fin_next;
             ctx->fin_pending = false;
         } else if (int rc = flush_qn_finish(ctx)) {
@@ -1916,6 +1917,12 @@ int enqueue_qn_step(wfsa_dev* ctx, double eta, double tol, int64_t e, bool timed
         f.n_ll = n_ll;
     } else if (trellis && ctx->comm && ctx->n_groups > 0) {
         q.fixed = ctx->fixed_grad.ptr;   // all-reduced once at preparation
+    }
+    if (trellis && ctx->comm) {   // the step's log-likelihood for its finish, which then rides in the next stream kernel
+        if (ctx->ll_stash.n < 2) HIP_TRY(ctx->ll_stash.alloc(2));
+        q.ll_stash = ctx->ll_stash.ptr + par;
+        f.ll_part = ctx->ll_stash.ptr + par;
+        f.n_ll = 1;
     }
     q.n_full = np;
     q.n = ctx->qn_n;
@@ -1970,7 +1977,7 @@ int enqueue_qn_step(wfsa_dev* ctx, double eta, double tol, int64_t e, bool timed
     ctx->fin_next = f;
     ctx->fin_next.active = 1;
     ctx->fin_pending = true;
-    ctx->fin_hostable = fused && ctx->n_groups > 0 && f.ll_part != nullptr;
+    ctx->fin_hostable = (fused || (trellis && ctx->comm)) && ctx->n_groups > 0 && f.ll_part != nullptr;
     return WFSA_OK;
 }
 

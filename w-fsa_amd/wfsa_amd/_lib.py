@@ -8,7 +8,9 @@ import ctypes as C
 import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libwfsa_amd.so")
+# WFSA_LIB: the timing-experiment build (make -C w-fsa_amd/csrc exp) for tools/;
+# bench.py refuses to measure with it
+LIB_PATH = os.environ.get("WFSA_LIB") or os.path.join(HERE, "libwfsa_amd.so")
 
 WFSA_OK = 0
 WFSA_ERR_ARG = -1
