@@ -142,6 +142,18 @@ int wfsa_dev_recognize(wfsa_dev* ctx, uint8_t* recognized, double* path_count,
 int wfsa_dev_sym_factor(wfsa_dev* ctx, int64_t n, const double* a, int64_t inertia[3], double* log_abs_det,
                         int32_t* det_sign);
 int wfsa_dev_sym_solve(wfsa_dev* ctx, double* b);
+/* The same from the matrix's entries -- upper-triangle coordinates
+ * (i[t] <= j[t]; duplicates add), no dense host copy -- assembled in HBM and
+ * factored blockwise: Bunch-Kaufman pivots within 128-column diagonal blocks
+ * (MKL DSS's supernode-restricted pivoting), the trailing updates as fp64
+ * library GEMMs (rocBLAS dsyrkx on MFMA); b (nullable) is solved in place and
+ * refined against the entries.  When a block pivot falls under 1e-12 max|A|,
+ * L grows past 1e8, or the refined solve misses a backward error of 1e-12,
+ * the full Bunch-Kaufman factorisation above is used instead.  *method = 1
+ * blocked, 2 full.  sym_solve works after either. */
+int wfsa_dev_sym_factor_coo(wfsa_dev* ctx, int64_t n, int64_t nnz, const int32_t* i, const int32_t* j,
+                            const double* v, double* b, int64_t inertia[3], double* log_abs_det, int32_t* det_sign,
+                            int32_t* method);
 
 /* Matrix-file mode (Learner::LoadMatrices, src/Learner.cpp:125-199; main.cpp
  * -m "<file"): instead of an automaton and strings, the path matrices the

@@ -77,3 +77,66 @@ def test_hessian_learner_host_and_device_factorisations_agree(monkeypatch):
     assert rows["host"].shape == rows["device"].shape == (3, 9)
     np.testing.assert_allclose(rows["device"][:, 0], rows["host"][:, 0], rtol=1e-9)
     np.testing.assert_array_equal(rows["device"][:, 4:6], rows["host"][:, 4:6])
+
+
+def _upper_entries(a, rng):
+    """upper-triangle coordinates of a (i <= j); a tenth of the entries split
+    in two parts (duplicates add, as SymEntries emits them)"""
+    i, j = np.nonzero(np.triu(a))
+    v = a[i, j]
+    dup = np.flatnonzero(rng.random(len(v)) < 0.1)
+    part = rng.uniform(0.2, 0.8, size=len(dup))
+    extra = v[dup] * (1 - part)
+    v = v.copy()
+    v[dup] *= part
+    return np.concatenate([i, i[dup]]), np.concatenate([j, j[dup]]), np.concatenate([v, extra])
+
+
+@pytest.mark.parametrize("n,k", [(5, 2), (120, 10), (300, 30), (1000, 100), (2600, 300)])
+def test_blocked_factor_from_entries(n, k):
+    """wfsa_dev_sym_factor_coo: KKT-shaped systems (zero-diagonal constraint
+    rows, several 128-column panels) factored blockwise -- inertia, log|det|,
+    sign against numpy, the refined solve against numpy.linalg.solve"""
+    import wfsa_amd as W
+    rng = np.random.default_rng(100 + n)
+    a = _kkt(rng, n, k)
+    i, j, v = _upper_entries(a, rng)
+    dev = W.Device(0)
+    b = rng.normal(size=a.shape[0])
+    (pos, neg, zero), lad, sign, method, x = dev.sym_factor_coo(a.shape[0], i, j, v, b)
+    assert method == 1   # the blocked factorisation held up
+    ev = np.linalg.eigvalsh(a)
+    assert (pos, neg, zero) == (int(np.sum(ev > 0)), int(np.sum(ev < 0)), 0)
+    s, l = np.linalg.slogdet(a)
+    assert sign == int(s)
+    assert abs(lad - l) <= 1e-8 * max(1.0, abs(l))
+    want = np.linalg.solve(a, b)
+    np.testing.assert_allclose(x, want, rtol=1e-8, atol=1e-9 * np.abs(want).max())
+    # sym_solve after it: the same factor, refined
+    b2 = rng.normal(size=a.shape[0])
+    np.testing.assert_allclose(dev.sym_solve(b2), np.linalg.solve(a, b2), rtol=1e-8,
+                               atol=1e-9 * np.abs(np.linalg.solve(a, b2)).max())
+
+
+def test_blocked_factor_falls_back_to_full_pivoting():
+    """a diagonal block no pivot inside it can serve (zero block, coupled only
+    to rows below): the restricted pivoting gives up and the full
+    Bunch-Kaufman answers"""
+    import wfsa_amd as W
+    rng = np.random.default_rng(7)
+    n = 300
+    a = np.zeros((n, n))
+    a[128:, 128:] = rng.normal(size=(n - 128, n - 128))
+    a[128:, 128:] = (a[128:, 128:] + a[128:, 128:].T) / 2
+    c = rng.normal(size=(n - 128, 128))
+    a[128:, :128] = c
+    a[:128, 128:] = c.T
+    i, j = np.nonzero(np.triu(a))
+    b = rng.normal(size=n)
+    dev = W.Device(0)
+    (pos, neg, zero), lad, sign, method, x = dev.sym_factor_coo(n, i, j, a[i, j], b)
+    assert method == 2
+    ev = np.linalg.eigvalsh(a)
+    assert (pos, neg, zero) == (int(np.sum(ev > 0)), int(np.sum(ev < 0)), 0)
+    want = np.linalg.solve(a, b)
+    np.testing.assert_allclose(x, want, rtol=1e-7, atol=1e-8 * np.abs(want).max())

@@ -25,12 +25,13 @@ def main():
     lrn.BuildFromPacked(fsa, sym, off, wt)
     lrn.Finalize()
     lrn.Init(7)
-    ks = [1, 2, 5, 20, 50, 200]
-    for rmin in (False, True):
+    ks = [int(k) for k in os.environ.get("RC_KS", "1,2,5,20,50,200").split(",")]
+    reps = int(os.environ.get("RC_REPS", "3"))
+    for rmin in [bool(int(v)) for v in os.environ.get("RC_RMIN", "0,1").split(",")]:
         lrn.set_info_rmin(rmin)
         lrn.Run(10, 1.0, -1.0)
         res = {}
-        for rep in range(3):
+        for rep in range(reps):
             for k in ks:
                 torch.cuda.synchronize()
                 t0 = time.perf_counter()
@@ -41,7 +42,7 @@ def main():
                 res.setdefault(k, []).append(dt * 1e6)
         x = np.array(ks, dtype=float)
         y = np.array([min(res[k]) for k in ks])
-        b, a = np.polyfit(x, y, 1)
+        b, a = np.polyfit(x, y, 1) if len(ks) > 1 else (y[0] / x[0], 0.0)
         print(f"rmin={rmin}: " + ", ".join(f"K={k}: {min(res[k]):.0f} us ({min(res[k]) / k:.1f}/step)" for k in ks))
         print(f"rmin={rmin}: fit fixed {a:.1f} us + {b:.2f} us/step", flush=True)
 

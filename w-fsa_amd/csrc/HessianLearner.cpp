@@ -269,7 +269,7 @@ struct Factored {
     int64_t positive = 0, negative = 0;
     double log_abs_det = 0.0;
     int det_sign = 1;
-    char kind = 'h';   // h: host dense, d: device dense, s: sparse
+    char kind = 'h';   // h: host dense, b: device blocked, d: device full Bunch-Kaufman, s: sparse
 };
 
 // the sparse LDL^T where it pays (above kHostDense unknowns and within
@@ -330,9 +330,9 @@ Factored factor_and_solve(wfsa_dev* dev, const SymEntries& A, int order, const d
     if (!dense_fits)   // only a forced dense factorisation gets here
         throw LearnerError("KKT system of ", N, " unknowns: beyond the dense factorisation's ", HessianLearner::kMaxDense,
                            " (WFSA_KKT=", forced, ")");
-    std::vector<double> H = A.dense();
     const bool device = forced == "device" || (forced != "host" && forced != "sparse" && N > HessianLearner::kHostDense);
     if (!device) {
+        std::vector<double> H = A.dense();
         DenseLdlt f;
         f.Factor(H, N);
         r.positive = f.positive;
@@ -343,17 +343,20 @@ Factored factor_and_solve(wfsa_dev* dev, const SymEntries& A, int order, const d
         return r;
     }
     if (!dev) throw LearnerError("no device for the KKT factorisation");
+    // assembled in HBM from the entries (no dense host copy): the blocked
+    // factorisation, or the full Bunch-Kaufman when it does not hold up
     int64_t inertia[3] = {0, 0, 0};
-    int32_t sign = 1;
-    ThrowOnDevError(wfsa_dev_sym_factor(dev, N, H.data(), inertia, &r.log_abs_det, &sign), "wfsa_dev_sym_factor");
+    int32_t sign = 1, method = 0;
+    if (rhs) std::copy(rhs, rhs + N, x);
+    ThrowOnDevError(wfsa_dev_sym_factor_coo(dev, N, int64_t(A.v.size()), A.i.data(), A.j.data(), A.v.data(),
+                                            rhs ? x : nullptr, inertia, &r.log_abs_det, &sign, &method),
+                    "wfsa_dev_sym_factor_coo");
     r.positive = inertia[0];
     r.negative = inertia[1];
     r.det_sign = sign;
-    r.kind = 'd';
-    if (rhs) {
-        std::copy(rhs, rhs + N, x);
-        ThrowOnDevError(wfsa_dev_sym_solve(dev, x), "wfsa_dev_sym_solve");
-    }
+    r.kind = method == 1 ? 'b' : 'd';
+    if (std::getenv("WFSA_KKT_TRACE"))
+        std::fprintf(stderr, "[kkt] N %lld device %s\n", (long long)N, method == 1 ? "blocked" : "full Bunch-Kaufman");
     return r;
 }
 

@@ -1,8 +1,11 @@
 // Dense symmetric-indefinite LDL^T on the device (sym_solver.hpp).
 #include "sym_solver.hpp"
 
+#include <rocblas/rocblas.h>
+
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
 
 namespace wfsa {
 namespace {
@@ -324,37 +327,50 @@ __global__ __launch_bounds__(kSolveBlock) void sytrs_lower_kernel(const double* 
 
 SymSolver::~SymSolver() {
     for (void* p : {static_cast<void*>(a_), static_cast<void*>(b_), static_cast<void*>(diag_),
+                    static_cast<void*>(ipiv_), static_cast<void*>(ctl_), static_cast<void*>(y_),
+                    static_cast<void*>(bd_), static_cast<void*>(gmax_), static_cast<void*>(x_),
+                    static_cast<void*>(perm_), static_cast<void*>(bpiv_), static_cast<void*>(bstat_), coo_})
+        if (p) (void)hipFree(p);
+    if (blas_) (void)rocblas_destroy_handle(static_cast<rocblas_handle>(blas_));
+}
+
+const char* SymSolver::alloc(int64_t n) {
+    if (n >= (int64_t(1) << 31)) return "matrix too large";
+    if (n <= cap_) return nullptr;
+    for (void* p : {static_cast<void*>(a_), static_cast<void*>(b_), static_cast<void*>(diag_),
                     static_cast<void*>(ipiv_), static_cast<void*>(ctl_)})
         if (p) (void)hipFree(p);
+    a_ = b_ = diag_ = nullptr;
+    ipiv_ = nullptr;
+    ctl_ = nullptr;
+    cap_ = 0;
+    if (hipMalloc(reinterpret_cast<void**>(&a_), size_t(n) * size_t(n) * sizeof(double)) != hipSuccess ||
+        hipMalloc(reinterpret_cast<void**>(&b_), size_t(n) * sizeof(double)) != hipSuccess ||
+        hipMalloc(reinterpret_cast<void**>(&diag_), 2 * size_t(n) * sizeof(double)) != hipSuccess ||
+        hipMalloc(reinterpret_cast<void**>(&ipiv_), size_t(n) * sizeof(int32_t)) != hipSuccess ||
+        hipMalloc(&ctl_, sizeof(BkCtl)) != hipSuccess)
+        return "device allocation failed";
+    cap_ = n;
+    return nullptr;
 }
 
 const char* SymSolver::factor(const double* a, int64_t n, hipStream_t s, SymFactor* out) {
     factored_ = false;
+    blocked_ok_ = false;
     if (n <= 0) {
         *out = SymFactor{};
         return nullptr;
     }
-    if (n >= (int64_t(1) << 31)) return "matrix too large";
-    if (n > cap_) {
-        for (void* p : {static_cast<void*>(a_), static_cast<void*>(b_), static_cast<void*>(diag_),
-                        static_cast<void*>(ipiv_), static_cast<void*>(ctl_)})
-            if (p) (void)hipFree(p);
-        a_ = b_ = diag_ = nullptr;
-        ipiv_ = nullptr;
-        ctl_ = nullptr;
-        cap_ = 0;
-        if (hipMalloc(reinterpret_cast<void**>(&a_), size_t(n) * size_t(n) * sizeof(double)) != hipSuccess ||
-            hipMalloc(reinterpret_cast<void**>(&b_), size_t(n) * sizeof(double)) != hipSuccess ||
-            hipMalloc(reinterpret_cast<void**>(&diag_), 2 * size_t(n) * sizeof(double)) != hipSuccess ||
-            hipMalloc(reinterpret_cast<void**>(&ipiv_), size_t(n) * sizeof(int32_t)) != hipSuccess ||
-            hipMalloc(&ctl_, sizeof(BkCtl)) != hipSuccess)
-            return "device allocation failed";
-        cap_ = n;
-    }
+    if (const char* e = alloc(n)) return e;
     n_ = n;
-    if (hipMemcpyAsync(a_, a, size_t(n) * size_t(n) * sizeof(double), hipMemcpyHostToDevice, s) != hipSuccess ||
-        hipMemsetAsync(ctl_, 0, sizeof(BkCtl), s) != hipSuccess)
+    if (hipMemcpyAsync(a_, a, size_t(n) * size_t(n) * sizeof(double), hipMemcpyHostToDevice, s) != hipSuccess)
         return "upload failed";
+    return bk_factor_device(s, out);
+}
+
+const char* SymSolver::bk_factor_device(hipStream_t s, SymFactor* out) {
+    const int64_t n = n_;
+    if (hipMemsetAsync(ctl_, 0, sizeof(BkCtl), s) != hipSuccess) return "memset failed";
     BkCtl* ctl = static_cast<BkCtl*>(ctl_);
     for (int64_t step = 0; step < n; ++step) {   // each step takes >= 1 column: n steps suffice
         hipLaunchKernelGGL(bk_pivot_kernel, dim3(1), dim3(kPivBlock), 0, s, a_, n, ipiv_, ctl);
@@ -400,7 +416,135 @@ const char* SymSolver::factor(const double* a, int64_t n, hipStream_t s, SymFact
     return nullptr;
 }
 
+bool SymSolver::residual(const double* b, const double* x, double* r, double tol) const {
+    const int64_t n = n_;
+    std::vector<double> mag(static_cast<size_t>(n), 0.0);
+    for (int64_t i = 0; i < n; ++i) r[i] = b[i];
+    for (size_t t = 0; t < cval_.size(); ++t) {
+        const int64_t i = crow_[t], j = ccol_[t];
+        const double v = cval_[t];
+        r[i] -= v * x[j];
+        mag[size_t(i)] += std::fabs(v * x[j]);
+        if (i != j) {
+            r[j] -= v * x[i];
+            mag[size_t(j)] += std::fabs(v * x[i]);
+        }
+    }
+    bool ok = true;
+    for (int64_t i = 0; i < n && ok; ++i) ok = std::isfinite(r[i]) && std::fabs(r[i]) <= tol * (mag[size_t(i)] + std::fabs(b[i]));
+    return ok;
+}
+
+const char* SymSolver::factor_coo(int64_t n, int64_t nnz, const int32_t* ei, const int32_t* ej, const double* ev,
+                                  double* b, hipStream_t s, SymFactor* out, int* method) {
+    factored_ = false;
+    blocked_ok_ = false;
+    if (method) *method = 0;
+    if (n <= 0) {
+        *out = SymFactor{};
+        return nullptr;
+    }
+    if (const char* e = alloc(n)) return e;
+    n_ = n;
+    // unique lower entries (row = max, col = min), duplicates summed in a fixed order
+    {
+        std::vector<int64_t> key(static_cast<size_t>(nnz));
+        std::vector<int64_t> ord(static_cast<size_t>(nnz));
+        for (int64_t t = 0; t < nnz; ++t) {
+            const int64_t r = std::max(ei[t], ej[t]), c = std::min(ei[t], ej[t]);
+            if (c < 0 || r >= n) return "entry out of range";
+            key[size_t(t)] = c * n + r;
+            ord[size_t(t)] = t;
+        }
+        std::stable_sort(ord.begin(), ord.end(), [&](int64_t x, int64_t y) { return key[size_t(x)] < key[size_t(y)]; });
+        crow_.clear();
+        ccol_.clear();
+        cval_.clear();
+        for (int64_t q = 0; q < nnz; ++q) {
+            const int64_t t = ord[size_t(q)];
+            if (q > 0 && key[size_t(t)] == key[size_t(ord[size_t(q) - 1])]) {
+                cval_.back() += ev[t];
+            } else {
+                crow_.push_back(int32_t(key[size_t(t)] % n));
+                ccol_.push_back(int32_t(key[size_t(t)] / n));
+                cval_.push_back(ev[t]);
+            }
+        }
+    }
+    static const bool only_bk = [] {   // WFSA_KKT_BLOCKED=0: the full Bunch-Kaufman only
+        const char* e = std::getenv("WFSA_KKT_BLOCKED");
+        return e && e[0] == '0';
+    }();
+    if (!only_bk) {
+        if (const char* e = ensure_blocked(n, s)) return e;
+        if (const char* e = assemble(s)) return e;
+        bool exact = false;
+        SymFactor f;
+        if (const char* e = blocked_factor(s, &f, &exact)) return e;
+        if (exact) {
+            bool ok = true;
+            if (b) {   // solve, refine (up to 3 corrections) and check
+                std::vector<double> rhs(b, b + n), x(static_cast<size_t>(n)), r(static_cast<size_t>(n));
+                auto dev_solve = [&](const double* in, double* outv) -> const char* {
+                    if (hipMemcpyAsync(b_, in, size_t(n) * sizeof(double), hipMemcpyHostToDevice, s) != hipSuccess)
+                        return "upload failed";
+                    if (const char* e = blocked_solve(s)) return e;
+                    if (hipMemcpyAsync(outv, b_, size_t(n) * sizeof(double), hipMemcpyDeviceToHost, s) != hipSuccess ||
+                        hipStreamSynchronize(s) != hipSuccess)
+                        return "download failed";
+                    return nullptr;
+                };
+                if (const char* e = dev_solve(rhs.data(), x.data())) return e;
+                ok = residual(rhs.data(), x.data(), r.data(), 1e-12);
+                for (int it = 0; it < 3 && !ok; ++it) {
+                    std::vector<double> dx(static_cast<size_t>(n));
+                    if (const char* e = dev_solve(r.data(), dx.data())) return e;
+                    for (int64_t q = 0; q < n; ++q) x[size_t(q)] += dx[size_t(q)];
+                    ok = residual(rhs.data(), x.data(), r.data(), 1e-12);
+                }
+                if (ok) std::copy(x.begin(), x.end(), b);
+            }
+            if (ok) {
+                *out = f;
+                if (method) *method = 1;
+                blocked_ok_ = true;
+                return nullptr;
+            }
+        }
+    }
+    // the full Bunch-Kaufman (LAPACK dsytf2 semantics) on the assembled matrix
+    if (const char* e = ensure_blocked(n, s)) return e;
+    if (const char* e = assemble(s)) return e;
+    if (const char* e = bk_factor_device(s, out)) return e;
+    if (method) *method = 2;
+    if (b) return solve(b, s);
+    return nullptr;
+}
+
 const char* SymSolver::solve(double* b, hipStream_t s) {
+    if (blocked_ok_) {   // the blocked factor: solve, then refine against the entries
+        const int64_t n = n_;
+        std::vector<double> rhs(b, b + n), x(static_cast<size_t>(n)), r(static_cast<size_t>(n));
+        auto dev_solve = [&](const double* in, double* outv) -> const char* {
+            if (hipMemcpyAsync(b_, in, size_t(n) * sizeof(double), hipMemcpyHostToDevice, s) != hipSuccess)
+                return "upload failed";
+            if (const char* e = blocked_solve(s)) return e;
+            if (hipMemcpyAsync(outv, b_, size_t(n) * sizeof(double), hipMemcpyDeviceToHost, s) != hipSuccess ||
+                hipStreamSynchronize(s) != hipSuccess)
+                return "download failed";
+            return nullptr;
+        };
+        if (const char* e = dev_solve(rhs.data(), x.data())) return e;
+        bool ok = residual(rhs.data(), x.data(), r.data(), 1e-12);
+        for (int it = 0; it < 3 && !ok; ++it) {
+            std::vector<double> dx(static_cast<size_t>(n));
+            if (const char* e = dev_solve(r.data(), dx.data())) return e;
+            for (int64_t q = 0; q < n; ++q) x[size_t(q)] += dx[size_t(q)];
+            ok = residual(rhs.data(), x.data(), r.data(), 1e-12);
+        }
+        std::copy(x.begin(), x.end(), b);
+        return nullptr;
+    }
     if (!factored_) return "no factorisation";
     if (n_ == 0) return nullptr;
     if (hipMemcpyAsync(b_, b, size_t(n_) * sizeof(double), hipMemcpyHostToDevice, s) != hipSuccess) return "upload failed";

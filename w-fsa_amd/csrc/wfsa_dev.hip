@@ -2547,6 +2547,28 @@ int wfsa_dev_sym_factor(wfsa_dev* ctx, int64_t n, const double* a, int64_t inert
     return WFSA_OK;
 }
 
+int wfsa_dev_sym_factor_coo(wfsa_dev* ctx, int64_t n, int64_t nnz, const int32_t* i, const int32_t* j,
+                            const double* v, double* b, int64_t inertia[3], double* log_abs_det, int32_t* det_sign,
+                            int32_t* method) {
+    if (int rc = check_ctx(ctx)) return rc;
+    if (n < 0 || nnz < 0 || (nnz > 0 && (!i || !j || !v))) return fail(WFSA_ERR_ARG, "bad matrix entries");
+    if (ctx->in_flight) return fail(WFSA_ERR_ARG, "an evaluation is in flight");
+    if (!ctx->ldlt) ctx->ldlt = std::make_unique<wfsa::SymSolver>();
+    wfsa::SymFactor f;
+    int m = 0;
+    if (const char* e = ctx->ldlt->factor_coo(n, nnz, i, j, v, b, ctx->stream, &f, &m))
+        return fail(WFSA_ERR_HIP, "sym_factor_coo: %s", e);
+    if (inertia) {
+        inertia[0] = f.positive;
+        inertia[1] = f.negative;
+        inertia[2] = f.zero;
+    }
+    if (log_abs_det) *log_abs_det = f.log_abs_det;
+    if (det_sign) *det_sign = f.det_sign;
+    if (method) *method = m;
+    return WFSA_OK;
+}
+
 int wfsa_dev_sym_solve(wfsa_dev* ctx, double* b) {
     if (int rc = check_ctx(ctx)) return rc;
     if (!ctx->ldlt) return fail(WFSA_ERR_ARG, "sym_solve: no factorisation");

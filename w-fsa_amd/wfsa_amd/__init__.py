@@ -401,6 +401,19 @@ class Device:
         check_dev(load().wfsa_dev_sym_factor(self._h, n, _ptr(a), _ptr(inertia), C.byref(lad), C.byref(sign)))
         return tuple(int(v) for v in inertia), lad.value, sign.value
 
+    def sym_factor_coo(self, n, i, j, v, b=None):
+        """the blocked LDL^T from upper-triangle entries (wfsa_dev_sym_factor_coo):
+        ((pos, neg, zero), log|det|, sign, method (1 blocked, 2 full BK), x or None)"""
+        i = np.ascontiguousarray(i, dtype=np.int32)
+        j = np.ascontiguousarray(j, dtype=np.int32)
+        v = np.ascontiguousarray(v, dtype=np.float64)
+        x = None if b is None else np.array(b, dtype=np.float64)
+        inertia = np.zeros(3, dtype=np.int64)
+        lad, sign, method = C.c_double(), C.c_int32(), C.c_int32()
+        check_dev(load().wfsa_dev_sym_factor_coo(self._h, int(n), len(v), _ptr(i), _ptr(j), _ptr(v), _ptr(x),
+                                                 _ptr(inertia), C.byref(lad), C.byref(sign), C.byref(method)))
+        return tuple(int(q) for q in inertia), lad.value, sign.value, method.value, x
+
     def sym_solve(self, b):
         x = np.array(b, dtype=np.float64)
         check_dev(load().wfsa_dev_sym_solve(self._h, _ptr(x)))

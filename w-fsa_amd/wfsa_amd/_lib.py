@@ -77,6 +77,7 @@ _SIGS = {
     "wfsa_dev_rmin": (C.c_int, [vp, vp, vp]),
     "wfsa_dev_sym_factor": (C.c_int, [vp, C.c_int64, vp, vp, vp, vp]),
     "wfsa_dev_sym_solve": (C.c_int, [vp, vp]),
+    "wfsa_dev_sym_factor_coo": (C.c_int, [vp, C.c_int64, C.c_int64, vp, vp, vp, vp, vp, vp, vp, vp]),
     "wfsa_dev_load_paths": (C.c_int, [vp, C.c_int32, C.c_int64, vp, vp, vp, C.c_int64, vp, vp, vp]),
     "wfsa_learner_load_matrices": (C.c_int, [vp, C.c_char_p]),
     "wfsa_learner_set_info_rmin": (C.c_int, [vp, C.c_int]),
