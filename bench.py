@@ -17,9 +17,13 @@ through the host binding of INTEGRATION.md section 2 (wfsa_dev_objective_grad
 per step: H2D weights, D2H [LL, grad], host QN update) are timed beside it
 (`boundary`).
 
-Multi-GPU: launched by torch.distributed.run, one process per GPU; every rank
-builds the same global corpus and keeps a contiguous shard (Learner::BuildFrom);
-the gradient + log-likelihood are summed with one RCCL all-reduce per step.
+Multi-GPU: launched by torch.distributed.run, one process per GPU (`--gpus N`
+without a launcher starts the N ranks itself, or refuses when the node has
+fewer GPUs); every rank builds the same global corpus and keeps a contiguous
+shard (Learner::BuildFrom); the gradient + log-likelihood are summed once per
+step by the one-shot peer all-reduce over xGMI (RCCL communicator; RCCL's own
+all-reduce if the peer path's set-up check fails -- `comm` in the line says
+which).
 
 After the headline (one GPU only) two sub-records run in the same process,
 each with its own roofline and CPU baseline: `dense_c5` (configs[4], the
@@ -474,6 +478,11 @@ def main():
         "roofline": roofline_of(m, traffic),
         "info_rmin": rmin_pass,
         "boundary": boundary,
+        "comm": ({"transport": "rccl", "ranks": st1.get("comm_ranks", world),
+                  "per_step_sum": {1: "one-shot peer all-reduce (xGMI)", 0: "ncclAllReduce",
+                                   -1: "ncclAllReduce (peer set-up check failed)"}.get(st1.get("comm_peer", 0))}
+                 if distributed else None),
+        "experiment_knobs": "none (WFSA_*_DBG refused; compiled out of the release library)",
         "live_edges_per_step": st1["last_live_edges"],
         "build_s": m["t_build"],
         "tier1_strings": st1["tier1_strings"],

@@ -261,3 +261,43 @@ def test_hessian_across_ranks():
             assert len(rows1) == 6
             np.testing.assert_allclose(rows, rows1, rtol=1e-8, atol=1e-10)
             np.testing.assert_allclose(x, x1, rtol=1e-9, atol=1e-11)
+
+
+_LONG_EDGE_WFSA = "\n".join(
+    ["", "^", "$", "^  0", "^ P0 0 Q 0 S 0"]
+    + [line for i in range(9) for line in (f"P{i}  0 z 0", f"P{i} P{i + 1} 0 $ 0")]
+    + ["P9 a 0 z 0", "P9 R 0 $ 0", "Q a 0 c 0", "Q R 0 $ 0", "R b 0 d 0", "R $ 0 S 0", "S c 0 d 0", "S R 0 $ 0"]
+) + "\n"
+
+
+def test_hf_setup_capacity_on_one_shard_fails_every_rank():
+    """the H_f set-up's limit on one shard only: a bubble edge
+    through an epsilon chain carries ~20 parameters (more than 8) in the
+    last rank's strings alone; every rank fails with WFSA_ERR_CAPACITY and
+    none is left waiting in a later collective"""
+    import wfsa_amd as W
+    fsa = W.Fsa.read_text(_LONG_EDGE_WFSA)
+    strings = [b"cb", b"cd", b"db", b"dd", b"ab"]
+    sym = np.frombuffer(b"".join(strings), dtype=np.uint8).copy()
+    off = np.concatenate([[0], np.cumsum([len(s) for s in strings])]).astype(np.int64)
+    p = np.full(len(strings), 1.0 / len(strings))
+    assert W.shard_range(off, 2, 1)[0] > 0 and W.shard_range(off, 2, 1)[1] == len(strings)   # "ab" on rank 1
+
+    def hf(nranks, rank, gid):
+        dev = W.Device(0)
+        dev.comm_init(nranks, rank, gid)
+        b, e = W.shard_range(off, nranks, rank)
+        dev.load_model(fsa)
+        dev.load_corpus(sym[off[b]:off[e]], off[b:e + 1] - off[b], p[b:e])
+        dev.recognize()
+        with pytest.raises(W.WfsaError) as err:
+            dev.hf_setup()
+        return err.value.code, str(err.value)
+
+    import time
+    t0 = time.time()
+    outs = _run_ranks(2, hf)
+    assert time.time() - t0 < 60
+    codes = [c for c, _ in outs]
+    assert codes[0] == codes[1] and codes[0] != 0
+    assert "another rank" in outs[0][1] and "parameters" in outs[1][1]
