@@ -354,3 +354,21 @@ def test_dense_c5_4096_gradient_per_element(monkeypatch):
     for k in range(4):   # start, interior, end transitions and emissions all compared
         assert (kind == k).any()
     np.testing.assert_allclose(grad, ref, rtol=1e-9, atol=1e-15)
+
+
+def test_dense_evaluation_is_bitwise_reproducible(monkeypatch):
+    """the dense path's sums run in a fixed order -- the library GEMMs with
+    atomics off, the epilogue row sums as fixed block trees: two evaluations
+    of the same weights agree bit for bit"""
+    import wfsa_amd as W
+    syn = W.Synthetic(n_states=512, degree=1, vocab=16, emissions=16, dense=True, n_strings=600, max_len=40, seed=6)
+    sym, off, wt = syn.corpus()
+    fsa = W.Fsa.read_text(syn.wfsa_text)
+    dev = _device(fsa, sym, off, wt / wt.sum(), monkeypatch, dense=True)
+    dev.recognize()
+    w = np.random.default_rng(3).normal(-6.0, 1.0, size=len(fsa.param_names()))
+    ll1, g1, lq1 = dev.objective_grad(w)
+    ll2, g2, lq2 = dev.objective_grad(w)
+    assert ll1 == ll2
+    np.testing.assert_array_equal(g1, g2)
+    np.testing.assert_array_equal(lq1, lq2)

@@ -23,6 +23,8 @@
 // L2).
 #include "dense_path.hpp"
 
+#include <rocblas/rocblas.h>
+
 #include <algorithm>
 #include <cmath>
 #include <cstdlib>
@@ -501,6 +503,125 @@ __global__ __launch_bounds__(256) void dense_scatter_kernel(ScatterArgs a) {
     }
 }
 
+// ---- epilogues of the library GEMMs (enqueue_blas) ------------------------
+// One block per row slot r of the step; the row's new values and their sum
+// (a fixed-order block reduction: deterministic) for the next step's scale.
+
+constexpr int kEpiThreads = 256;
+
+__device__ __forceinline__ double epi_block_sum(double v, double* red) {
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+    const int w = int(threadIdx.x) >> 6;
+    if ((threadIdx.x & 63) == 0) red[w] = v;
+    __syncthreads();
+    double t = 0.0;
+    for (int i = 0; i < kEpiThreads / 64; ++i) t += red[i];
+    return t;
+}
+
+struct EpiArgs {
+    int32_t np, ldx;
+    int32_t first;             // FWD: step 0 (every row starts) / BWD: step T-1 (every row ends)
+    const int32_t* meta;       // [R] of the output step
+    const int32_t* sid;        // [R] (BWD)
+    const double* sum_in;      // [R] row sums of the input step
+    double* sum_out;           // [R] of the output step
+    const double* et;
+    const double* a0;
+    const double* aend;
+    double* io;                // FWD: alpha[t+1] (the GEMM's alpha[t] A in, the values out); BWD: Y[t] likewise
+    const double* la_in;       // FWD
+    double* la_out;
+    const double* lb_in;       // BWD
+    double* lb_out;
+    const double* la_t;
+    const double* la_prev;
+    const double* alpha_t;
+    double* gam;
+    double* z;
+    const double* p;
+    const double* logq;
+    const unsigned* halted;
+};
+
+// alpha[t+1] = (alpha[t] A / rowsum(alpha[t])) (.) E[sym], a0 (.) E[sym] where a string starts
+__global__ __launch_bounds__(kEpiThreads) void dense_fwd_epi_kernel(EpiArgs a) {
+    if (a.halted && *a.halted) return;
+    __shared__ double red[kEpiThreads / 64];
+    const int r = int(blockIdx.x);
+    const int m = a.meta[r];
+    const bool start = (m >> 9) & 1;
+    double inv = 0.0, la = 0.0;
+    if (!a.first) {
+        const double s = a.sum_in[r];
+        inv = s > 0.0 ? 1.0 / s : 0.0;
+        la = start ? 0.0 : a.la_in[r] + log(s);
+    }
+    if (threadIdx.x == 0) a.la_out[r] = la;
+    const double* erow = a.et + int64_t(m & 511) * a.np;
+    double* row = a.io + int64_t(r) * a.ldx;
+    double acc = 0.0;
+    for (int c = int(threadIdx.x); c < a.np; c += kEpiThreads) {
+        const double v = (start ? a.a0[c] : (a.first ? 0.0 : row[c] * inv)) * erow[c];
+        row[c] = v;
+        acc += v;
+    }
+    acc = epi_block_sum(acc, red);
+    if (threadIdx.x == 0) a.sum_out[r] = acc;
+}
+
+// beta[t] = Y[t+1] A^T / rowsum(Y[t+1]) (e where a string ends); Y[t] = E (.)
+// beta, z[t] = Y[t] f2, gamma[t] = alpha[t] beta f1 (the fused kernel's epilogue)
+__global__ __launch_bounds__(kEpiThreads) void dense_bwd_epi_kernel(EpiArgs a) {
+    if (a.halted && *a.halted) return;
+    __shared__ double red[kEpiThreads / 64];
+    const int r = int(blockIdx.x);
+    const int m = a.meta[r];
+    const bool start = (m >> 9) & 1, end = (m >> 10) & 1;
+    double inv = 0.0, lb = 0.0;
+    if (!end && !a.first) {
+        const double u = a.sum_in[r];
+        inv = u > 0.0 ? 1.0 / u : 0.0;
+        lb = a.lb_in[r] + log(u);
+    }
+    if (threadIdx.x == 0) a.lb_out[r] = lb;
+    double f1 = 0.0, f2 = 0.0;
+    const int s = a.sid[r];
+    if (s >= 0) {
+        const double lq = a.logq[s];
+        if (lq > -INFINITY) {
+            f1 = a.p[s] * exp(a.la_t[r] + lb - lq);
+            if (!start && a.la_prev) f2 = a.p[s] * exp(a.la_prev[r] + lb - lq);
+        }
+    }
+    const double* erow = a.et + int64_t(m & 511) * a.np;
+    const int64_t o0 = int64_t(r) * a.ldx;
+    double* row = a.io + o0;
+    double acc = 0.0;
+    for (int c = int(threadIdx.x); c < a.np; c += kEpiThreads) {
+        const double beta = end ? a.aend[c] : (a.first ? 0.0 : row[c] * inv);
+        a.gam[o0 + c] = a.alpha_t[o0 + c] * beta * f1;
+        const double v = erow[c] * beta;
+        row[c] = v;
+        a.z[o0 + c] = v * f2;
+        acc += v;
+    }
+    acc = epi_block_sum(acc, red);
+    if (threadIdx.x == 0) a.sum_out[r] = acc;
+}
+
+// grad(S -> T) = -A(S, T) G(S, T) for the transition parameters
+__global__ __launch_bounds__(256) void dense_grad_scatter_kernel(const double* __restrict__ g, const double* __restrict__ amat,
+                                                                 const int32_t* __restrict__ code_a, int64_t n,
+                                                                 int32_t n_params, double* grad, const unsigned* halted) {
+    if (halted && *halted) return;
+    const int64_t stride = int64_t(gridDim.x) * blockDim.x;
+    for (int64_t o = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; o < n; o += stride) {
+        const int32_t code = code_a[o];
+        if (code >= 0 && code < n_params) grad[code] = -amat[o] * g[o];
+    }
+}
+
 template <typename T>
 hipError_t dalloc(T*& p, size_t n) {
     if (p) (void)hipFree(p);
@@ -600,7 +721,9 @@ DensePath::~DensePath() {
 
 void DensePath::free_model() {
     dfree(code_a_); dfree(code_s_); dfree(code_e_); dfree(code_em_);
-    dfree(amat_); dfree(amat_t_); dfree(et_); dfree(a0_); dfree(aend_); dfree(ones_);
+    dfree(amat_); dfree(amat_t_); dfree(et_); dfree(a0_); dfree(aend_); dfree(ones_); dfree(gbuf_);
+    if (blas_) (void)rocblas_destroy_handle(static_cast<rocblas_handle>(blas_));
+    blas_ = nullptr;
 }
 
 void DensePath::free_corpus() {
@@ -639,6 +762,16 @@ hipError_t DensePath::load_model(const DenseModel& m, hipStream_t s) {
     std::vector<double> ones(size_t(n_params_) + 2, 1.0);
     DTRY(dalloc(ones_, ones.size()));
     DTRY(hipMemcpyAsync(ones_, ones.data(), ones.size() * 8, hipMemcpyHostToDevice, s));
+    if (const char* e = std::getenv("WFSA_DENSE_BLAS")) use_blas_ = e[0] != '0';
+    if (use_blas_) {
+        rocblas_handle h = nullptr;
+        if (rocblas_create_handle(&h) != rocblas_status_success) return hipErrorNotInitialized;
+        blas_ = h;
+        // no atomics: every GEMM's sums in a fixed order (deterministic results)
+        if (rocblas_set_atomics_mode(h, rocblas_atomics_not_allowed) != rocblas_status_success)
+            return hipErrorNotInitialized;
+        DTRY(dalloc(gbuf_, np * np));
+    }
     return hipStreamSynchronize(s);
 }
 
@@ -760,6 +893,7 @@ hipError_t DensePath::enqueue(const double* ewp, bool structural, double* out, d
     const size_t np = size_t(np_), R = size_t(R_);
     const double* w = structural ? ones_ : ewp;
     const double* p = structural ? pones_ : p_;
+    if (use_blas_ && blas_ && n_strings_ > 0 && total_sym_ > 0) return enqueue_blas(w, p, structural, out, logq, halted, s);
     {
         WeightsArgs a{};
         a.ewp = w;
@@ -862,6 +996,118 @@ hipError_t DensePath::enqueue(const double* ewp, bool structural, double* out, d
             dense_gemm_kernel<GRAD, kBkStep, kNwStep><<<int((np / kT) * (np / kT)), kNwStep * 64, 0, s>>>(q);
         else
             dense_gemm_kernel<GRAD, kBkGrad, kNwGrad><<<int((np / kT) * (np / kT)), kNwGrad * 64, 0, s>>>(q);
+        DTRY(hipGetLastError());
+    }
+    {
+        ReduceArgs r{};
+        r.gam = gam_; r.meta = meta_;
+        r.rows = int64_t(T_) * int64_t(R);
+        r.rows_per_chunk = (r.rows + reduce_chunks_ - 1) / reduce_chunks_;
+        r.np = np_; r.vocab = vocab_; r.ldx = ldx_; r.red = red_; r.halted = halted;
+        dim3 grid(unsigned(np / kRedThreads), unsigned(reduce_chunks_));
+        dense_reduce_kernel<<<grid, kRedThreads, 0, s>>>(r);
+        DTRY(hipGetLastError());
+    }
+    {
+        ScatterArgs c{};
+        c.red = red_; c.chunks = reduce_chunks_; c.np = np_; c.vocab = vocab_;
+        c.code_em = code_em_; c.code_s = code_s_; c.code_e = code_e_; c.code_se = code_se_;
+        c.n_params = n_params_; c.empty_p = structural ? n0_ : p0_sum_;
+        c.ll_part = ll_part_; c.n_ll = n_ll_; c.out = out; c.halted = halted;
+        const int64_t n = int64_t(vocab_ + 2) * int64_t(np);
+        dense_scatter_kernel<<<unsigned((n + 255) / 256), 256, 0, s>>>(c);
+        DTRY(hipGetLastError());
+    }
+    return hipSuccess;
+}
+
+// The same evaluation with the GEMMs as plain rocBLAS dgemm calls (fp64 MFMA)
+// and the fused kernels' epilogues as their own per-row kernels: the row
+// slot buffers are row-major [R][ldx]; seen column-major they are np x R
+// (ld = ldx), so alpha[t+1]^T = A^T alpha[t]^T is dgemm(N, N) with the
+// row-major A as its column-major transpose, Y[t+1] A^T likewise with op T,
+// and G = alpha[0..T-2]^T z[1..T-1] as (G^T)^T = dgemm(N, T) over K = (T-1) R
+// rows.  Row sums: one full sum per row ([R], nct = 1).
+hipError_t DensePath::enqueue_blas(const double* w, const double* p, bool structural, double* out, double* logq,
+                                   const unsigned* halted, hipStream_t s) {
+    const size_t np = size_t(np_), R = size_t(R_);
+    rocblas_handle h = static_cast<rocblas_handle>(blas_);
+    if (rocblas_set_stream(h, s) != rocblas_status_success) return hipErrorInvalidHandle;
+    auto rb = [](rocblas_status st) { return st == rocblas_status_success ? hipSuccess : hipErrorLaunchFailure; };
+    {
+        WeightsArgs a{};
+        a.ewp = w;
+        a.code_a = code_a_; a.code_em = code_em_; a.code_s = code_s_; a.code_e = code_e_;
+        a.amat = amat_; a.et = et_; a.a0 = a0_; a.aend = aend_;
+        a.n_a = int64_t(np * np);
+        a.n_em = int64_t(size_t(vocab_ + 1) * np);
+        a.np = np_;
+        a.out = out;
+        a.n_out = n_params_ + 1;
+        a.halted = halted;
+        dense_weights_kernel<<<1024, 256, 0, s>>>(a);
+        DTRY(hipGetLastError());
+    }
+    const size_t step = R * size_t(ldx_);
+    const double one = 1.0, zero = 0.0;
+    const rocblas_int inp = rocblas_int(np_), iR = rocblas_int(R_), ild = rocblas_int(ldx_);
+    EpiArgs g{};
+    g.np = np_; g.ldx = ldx_; g.et = et_; g.a0 = a0_; g.aend = aend_; g.p = p; g.logq = logq_; g.halted = halted;
+    // forward
+    for (int64_t t = -1; t + 1 < T_; ++t) {
+        double* nxt = alpha_ + size_t(t + 1) * step;
+        if (t >= 0)   // alpha[t+1]^T = A^T alpha[t]^T (raw products; the epilogue scales)
+            DTRY(rb(rocblas_dgemm(h, rocblas_operation_none, rocblas_operation_none, inp, iR, inp, &one, amat_, inp,
+                                  alpha_ + size_t(t) * step, ild, &zero, nxt, ild)));
+        EpiArgs f = g;
+        f.first = t < 0;
+        f.meta = meta_ + size_t(t + 1) * R;
+        f.sum_in = part_ + size_t(t & 1) * R;
+        f.sum_out = part_ + size_t((t + 1) & 1) * R;
+        f.io = nxt;
+        f.la_in = t < 0 ? la_ : la_ + size_t(t) * R;
+        f.la_out = la_ + size_t(t + 1) * R;
+        dense_fwd_epi_kernel<<<unsigned(R), kEpiThreads, 0, s>>>(f);
+        DTRY(hipGetLastError());
+    }
+    {
+        FinalArgs f{};
+        f.alpha = alpha_; f.la = la_; f.aend = aend_; f.end_at = end_at_; f.p = p; f.ewp = w;
+        f.code_se = code_se_; f.n_strings = n_strings_; f.np = np_; f.ldx = ldx_; f.logq = logq_; f.logq_user = logq;
+        f.ll_part = ll_part_; f.halted = halted;
+        dense_final_kernel<<<n_ll_, 256, 0, s>>>(f);
+        DTRY(hipGetLastError());
+    }
+    // backward
+    for (int64_t t = T_ - 1; t >= 0; --t) {
+        double* cur = y_ + size_t(t & 1) * step;
+        if (t < T_ - 1)   // beta[t]^T = A Y[t+1]^T (raw)
+            DTRY(rb(rocblas_dgemm(h, rocblas_operation_transpose, rocblas_operation_none, inp, iR, inp, &one, amat_, inp,
+                                  y_ + size_t((t + 1) & 1) * step, ild, &zero, cur, ild)));
+        EpiArgs b = g;
+        b.first = t == T_ - 1;
+        b.meta = meta_ + size_t(t) * R;
+        b.sid = sid_ + size_t(t) * R;
+        b.sum_in = part_ + size_t((t + 1) & 1) * R;
+        b.sum_out = part_ + size_t(t & 1) * R;
+        b.io = cur;
+        b.lb_in = lb_ + size_t(std::min<int64_t>(t + 1, T_ - 1)) * R;
+        b.lb_out = lb_ + size_t(t) * R;
+        b.la_t = la_ + size_t(t) * R;
+        b.la_prev = t > 0 ? la_ + size_t(t - 1) * R : nullptr;
+        b.alpha_t = alpha_ + size_t(t) * step;
+        b.gam = gam_ + size_t(t) * step;
+        b.z = z_ + size_t(t) * step;
+        dense_bwd_epi_kernel<<<unsigned(R), kEpiThreads, 0, s>>>(b);
+        DTRY(hipGetLastError());
+    }
+    if (T_ >= 2) {   // G^T = z[1..]^T alpha[0..] over K = (T-1) R rows: g[S np + T] = G(S, T)
+        const int64_t K = int64_t(T_ - 1) * int64_t(R);
+        if (K >= (int64_t(1) << 31)) return hipErrorInvalidValue;
+        DTRY(rb(rocblas_dgemm(h, rocblas_operation_none, rocblas_operation_transpose, inp, inp, rocblas_int(K), &one,
+                              z_ + step, ild, alpha_, ild, &zero, gbuf_, inp)));
+        dense_grad_scatter_kernel<<<1024, 256, 0, s>>>(gbuf_, amat_, code_a_, int64_t(np * np), n_params_, out + 1,
+                                                        halted);
         DTRY(hipGetLastError());
     }
     {

@@ -128,6 +128,14 @@ private:
     double* ll_part_ = nullptr;
     int32_t n_ll_ = 0;
     double* red_ = nullptr;    // [chunks][vocab+2][np]
+    // the GEMMs as plain fp64 library GEMMs (rocBLAS, atomics off:
+    // deterministic) with our epilogue kernels; WFSA_DENSE_BLAS=0: the fused
+    // MFMA kernels above
+    bool use_blas_ = true;
+    void* blas_ = nullptr;     // rocblas_handle
+    double* gbuf_ = nullptr;   // [np][np] the gradient GEMM's product
+    hipError_t enqueue_blas(const double* w, const double* p, bool structural, double* out, double* logq,
+                            const unsigned* halted, hipStream_t s);
     void free_corpus();
     void free_model();
 };

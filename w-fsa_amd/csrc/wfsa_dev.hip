@@ -2887,7 +2887,9 @@ int wfsa_dev_qn_run(wfsa_dev* ctx, double eta, double tol, int32_t max_steps, do
     int64_t timed = 0;
     if (trace) tr_pro = clk::now();
     while (done < max_steps) {
-        while (!stop && enq < max_steps && enq - done < kQnDepth) {
+        // dense steps take ~0.2 s each: two in flight keep the device busy, and
+        // after a halt fewer no-op steps remain queued (their library GEMMs do not skip)
+        while (!stop && enq < max_steps && enq - done < (ctx->dense ? 2 : kQnDepth)) {
             const bool tm = timed_step(enq);
             if (int rc = piped ? enqueue_qn_step_piped(ctx, eta, tol, enq, tm) : enqueue_qn_step(ctx, eta, tol, enq, tm))
                 return rc;
