@@ -132,3 +132,38 @@ def test_in_process_group_peer_path(monkeypatch):
     for res in outs:
         assert res["stats"]["comm_peer"] == 1
         _compare(res, one)
+
+
+def _family_a_eval(W):
+    syn = W.Synthetic(n_states=1024, degree=8, vocab=64, emissions=1, n_strings=2000, max_len=128, seed=11)
+    sym, off, wt = syn.corpus()
+    fsa = W.Fsa.read_text(syn.wfsa_text)
+    w = np.random.default_rng(7).normal(-1.5, 0.7, size=len(fsa.param_names()))
+    dev = W.Device(0)
+    dev.load_model(fsa)
+    dev.load_corpus(sym, off, wt / wt.sum())
+    dev.recognize()
+    ll, grad, _ = dev.objective_grad(w)
+    return ll, np.array(grad)
+
+
+def test_context_after_peer_group_is_exact(monkeypatch):
+    """a context made after an in-process peer group is gone evaluates to the
+    same bits as one made before it (the group's uncached areas must not
+    reach later contexts' allocations: fp64 atomics into them were lost)"""
+    import wfsa_amd as W
+    ll0, g0 = _family_a_eval(W)
+    monkeypatch.setenv("WFSA_PEER", "1")
+    syn = W.Synthetic(**SPEC)
+    sym, off, wt = syn.corpus()
+    fsa = W.Fsa.read_text(syn.wfsa_text)
+    for _ in range(2):   # two groups one after the other: the second reuses the first's areas
+        gid = W.Device.comm_local_id(2)
+        with ThreadPoolExecutor(max_workers=2) as ex:
+            futs = [ex.submit(_learn, W, fsa, sym, off, wt, lambda l, r=r: l.SetCommunicator(2, r, gid)) for r in range(2)]
+            outs = [f.result(timeout=300) for f in futs]
+        assert all(o["stats"]["comm_peer"] == 1 for o in outs)
+    for _ in range(3):
+        ll1, g1 = _family_a_eval(W)
+        assert ll1 == ll0
+        np.testing.assert_array_equal(g1, g0)

@@ -87,6 +87,27 @@ def _oracle_eval(wfsa_text, sym, off, weights, w_full_by_name):
     return ll, logq, dict(zip(names, grad)), o
 
 
+def _dirty_device_memory(gib=8):
+    """hipMalloc'd, filled with 0xff bytes (NaN doubles) and freed again, in
+    the HIP runtime the library uses, so its next allocations are likely
+    handed these pages"""
+    import ctypes
+    import wfsa_amd as W
+    W.Device(0)   # the library's HIP runtime up
+    libs = sorted({ln.split()[-1] for ln in open("/proc/self/maps") if "libamdhip64" in ln})
+    assert libs
+    hip = ctypes.CDLL(libs[0]) if len(libs) == 1 else ctypes.CDLL("libamdhip64.so.7")
+    ptrs = []
+    for _ in range(gib):
+        p = ctypes.c_void_p()
+        assert hip.hipMalloc(ctypes.byref(p), ctypes.c_size_t(1 << 30)) == 0
+        assert hip.hipMemset(p, 0xff, ctypes.c_size_t(1 << 30)) == 0
+        ptrs.append(p)
+    assert hip.hipDeviceSynchronize() == 0
+    for p in ptrs:
+        assert hip.hipFree(p) == 0
+
+
 def _device_eval(wfsa_text, sym, off, p, rng):
     import wfsa_amd as W
     fsa = W.Fsa.read_text(wfsa_text)
@@ -105,8 +126,13 @@ def _device_eval(wfsa_text, sym, off, p, rng):
     dict(n_states=48, degree=6, vocab=8, emissions=3, n_strings=800, max_len=24),   # ambiguous (family B-like)
     dict(n_states=1024, degree=8, vocab=64, emissions=1, n_strings=2000, max_len=128),  # family A
 ])
-def test_device_matches_oracle_trellis_random_weights(family):
+@pytest.mark.parametrize("dirty", [False, True], ids=["fresh", "dirty"])
+def test_device_matches_oracle_trellis_random_weights(family, dirty):
+    """dirty: the device memory the context will be handed was just written
+    with NaN (no buffer may rely on hipMalloc returning zeros)"""
     import wfsa_amd as W
+    if dirty:
+        _dirty_device_memory()
     rng = np.random.default_rng(7)
     syn = W.Synthetic(seed=11, **family)
     sym, off, wt = syn.corpus()

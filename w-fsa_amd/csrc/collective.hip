@@ -369,6 +369,39 @@ struct PeerBlob {   // what a rank publishes at set-up
 };
 static_assert(sizeof(hipIpcMemHandle_t) <= 64, "IPC handle size");
 
+// Uncached areas are kept for the life of the process and reused by later
+// groups, never handed back to HIP: freed, their pages went on (still mapped
+// uncached) to ordinary allocations of later contexts, where the evaluation
+// kernels' fp64 atomic adds were lost -- a context made after an in-process
+// peer group summed gradients short (tests/test_gpu_multiprocess.py,
+// test_context_after_peer_group_is_exact).
+std::mutex g_uncached_mu;
+std::multimap<size_t, void*> g_uncached_free;
+
+void* uncached_get(size_t bytes) {
+    {
+        std::lock_guard<std::mutex> lk(g_uncached_mu);
+        auto it = g_uncached_free.find(bytes);
+        if (it != g_uncached_free.end()) {
+            void* p = it->second;
+            g_uncached_free.erase(it);
+            return p;
+        }
+    }
+    void* p = nullptr;
+    if (hipExtMallocWithFlags(&p, bytes, hipDeviceMallocUncached) != hipSuccess) {
+        (void)hipGetLastError();
+        return nullptr;
+    }
+    return p;
+}
+
+void uncached_put(void* p, size_t bytes) {
+    if (!p) return;
+    std::lock_guard<std::mutex> lk(g_uncached_mu);
+    g_uncached_free.emplace(bytes, p);
+}
+
 }  // namespace
 
 class PeerSum {
@@ -376,7 +409,10 @@ public:
     ~PeerSum() {
         for (int r = 0; r < n_; ++r)
             if (opened_[r]) (void)hipIpcCloseMemHandle(args_.area[r]);
-        if (own_) (void)hipFree(own_);
+        if (own_) {   // (no kernel of this group is in flight: its users synchronised first)
+            (void)hipDeviceSynchronize();
+            uncached_put(own_, own_bytes_);
+        }
         if (status_) (void)hipFree(status_);
     }
 
@@ -389,8 +425,9 @@ public:
         me_ = c.rank();
         const size_t bytes = 2 * size_t(n_) * kPeerCap * sizeof(double) +
                              2 * size_t(n_) * kPeerMaxChunks * sizeof(uint64_t);
-        bool ok = hipExtMallocWithFlags(reinterpret_cast<void**>(&own_), bytes, hipDeviceMallocUncached) == hipSuccess &&
-                  hipMemsetAsync(own_, 0, bytes, s) == hipSuccess &&
+        own_ = static_cast<double*>(uncached_get(bytes));
+        own_bytes_ = bytes;
+        bool ok = own_ != nullptr && hipMemsetAsync(own_, 0, bytes, s) == hipSuccess &&
                   hipMalloc(reinterpret_cast<void**>(&status_), sizeof(unsigned)) == hipSuccess &&
                   hipMemsetAsync(status_, 0, sizeof(unsigned), s) == hipSuccess &&
                   hipStreamSynchronize(s) == hipSuccess;
@@ -477,6 +514,7 @@ public:
 private:
     int n_ = 0, me_ = 0;
     double* own_ = nullptr;
+    size_t own_bytes_ = 0;
     unsigned* status_ = nullptr;
     bool opened_[kLocalMaxRanks] = {};
     uint64_t seq_ = 0;

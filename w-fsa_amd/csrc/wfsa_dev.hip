@@ -86,6 +86,12 @@ struct DevBuf {
         const size_t c = std::max<size_t>(count, 1);
         hipError_t e = hipMalloc(reinterpret_cast<void**>(&ptr), c * sizeof(T));
         if (e == hipSuccess) n = c;
+        // test hook: every fresh buffer filled with 0xff bytes (NaN doubles,
+        // -1 integers), so a read before the first write shows in the results
+        if (e == hipSuccess && std::getenv("WFSA_POISON_ALLOC")) {
+            e = hipMemset(ptr, 0xff, c * sizeof(T));
+            if (e == hipSuccess) e = hipDeviceSynchronize();
+        }
         return e;
     }
     hipError_t upload(const T* src, size_t count, hipStream_t s) {
