@@ -109,6 +109,9 @@ typedef struct {
     int64_t wave_pair_edges;   /* per evaluation: pair-list edges one pass walks */
     int32_t comm_ranks;        /* communicator size (1: none) */
     int32_t comm_peer;         /* the one-shot peer all-reduce: 1 on, 0 off / untried, -1 its set-up check failed */
+    int64_t slot_chunks;       /* bubble contribution slots, in 16-slot chunks (8 B a slot) */
+    int32_t max_group_chunks;  /* chunks of the largest constraint's slot group (one QN block sums it) */
+    int32_t pad_;
 } wfsa_dev_stats;
 
 /* context ---------------------------------------------------------------- */

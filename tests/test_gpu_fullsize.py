@@ -77,10 +77,8 @@ def test_c3_full_size_timed_path_matches_enum(c3):
 
 
 def _compiled_only(W, fsa, sym, off, wt):
-    """the strings that compile (stream + bubbles): the traversal tiers still
-    scatter their gradient with fp64 atomics, whose order varies in the last
-    bits from run to run, so the bitwise tests keep to the
-    compiled path -- bubbles included, whose reduction is fixed-order"""
+    """the strings that compile (stream + bubbles; the traversal strings have
+    their own bitwise test below)"""
     dev = W.Device(0)
     dev.load_model(fsa)
     dev.load_corpus(sym, off, wt / wt.sum())
@@ -145,3 +143,40 @@ def test_halting_run_leaves_consistent_state():
     fresh.set_x(x)
     kl_f, g_f, _ = fresh.objective_grad()
     assert kl == kl_f and np.array_equal(g, g_f)
+
+
+def test_traversal_strings_are_bitwise_reproducible():
+    """family B strings run on the wave kernel, whose waves draw strings from a
+    work counter; its gradient and log-likelihood are fixed-point sums, so the
+    evaluation and a QN run give the same bits every time and in a second
+    context"""
+    import wfsa_amd as W
+    syn = W.Synthetic(n_states=1024, degree=8, vocab=16, emissions=4, n_strings=3000, max_len=128, seed=2)
+    sym, off, wt = syn.corpus()
+    fsa = W.Fsa.read_text(syn.wfsa_text)
+
+    def learner():
+        lrn = W.QuasiNewtonLearner(0)
+        lrn.set_info_rmin(False)
+        lrn.BuildFromPacked(fsa, sym, off, wt)
+        lrn.Finalize()
+        lrn.Init(7)
+        return lrn
+
+    lrn = learner()
+    st = lrn.stats()
+    assert st["wave_strings"] > 1000
+    evals = [lrn.objective_grad() for _ in range(3)]
+    for kl, g, _ in evals[1:]:
+        assert kl == evals[0][0]
+        assert np.array_equal(g, evals[0][1])
+    runs = []
+    for _ in range(2):
+        lrn.Init(7)
+        rows = lrn.Run(5, 1.0, -1.0)
+        runs.append((np.array(rows), lrn.x()))
+    assert np.array_equal(runs[0][0], runs[1][0])
+    assert np.array_equal(runs[0][1], runs[1][1])
+    other = learner()
+    kl_c, g_c, _ = other.objective_grad()
+    assert kl_c == evals[0][0] and np.array_equal(g_c, evals[0][1])

@@ -76,6 +76,54 @@ __device__ __forceinline__ void global_add(double* p, double v) {
     __hip_atomic_fetch_add(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// Fixed-point sums whose bits do not depend on the order of the adds (integer
+// addition is associative): the wave kernel's gradient and log-likelihood,
+// whose strings go to waves through a work counter.  A value is rounded once
+// to a multiple of 2^-frac; a 128-bit accumulator {lo, hi} in global memory
+// takes a signed 64-bit (or a 128-bit) addend with an atomic add on the low
+// word whose returned old value gives the carry into the high word.
+constexpr unsigned long long kFixLlNegInf = 1, kFixLlPosInf = 2, kFixLlNan = 4, kFixGradBad = 8;
+__device__ __forceinline__ long long fix_of(double v, int frac) { return (long long)rint(ldexp(v, frac)); }
+__device__ __forceinline__ void fix128_add(unsigned long long* acc, unsigned long long lo, long long hi) {
+    const unsigned long long old = __hip_atomic_fetch_add(acc, lo, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    hi += (old + lo < old) ? 1 : 0;   // carry out of the low word
+    if (hi) __hip_atomic_fetch_add(acc + 1, (unsigned long long)hi, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void fix128_add(unsigned long long* acc, long long v) {
+    fix128_add(acc, (unsigned long long)v, v < 0 ? -1ll : 0ll);
+}
+// v * 2^64 rounded to an integer, as {lo, hi} (|v| < 2^63)
+__device__ __forceinline__ void fix128_of(double v, unsigned long long& lo, long long& hi) {
+    const double r = rint(ldexp(v, 64));
+    if (fabs(r) < 0x1p63) {
+        const long long i = (long long)r;
+        lo = (unsigned long long)i;
+        hi = i < 0 ? -1 : 0;
+    } else {   // r is a multiple of 2^11: r - h 2^64 is exact
+        const double h = floor(ldexp(r, -64));
+        hi = (long long)h;
+        lo = (unsigned long long)(r - ldexp(h, 64));
+    }
+}
+__device__ __forceinline__ double fix128_value(unsigned long long lo, long long hi, int frac) {
+    const long long s = (long long)lo;
+    if (hi == (s < 0 ? -1 : 0)) return ldexp(double(s), -frac);   // fits 64 bits: one rounding
+    return ldexp(double(hi), 64 - frac) + ldexp(double(lo), -frac);
+}
+__device__ __forceinline__ void block_add_fix(long long* p, long long v) {
+    __hip_atomic_fetch_add(reinterpret_cast<unsigned long long*>(p), (unsigned long long)v, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ unsigned long long ld_agent(const unsigned long long* p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void st_agent(unsigned long long* p, unsigned long long v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void flag_agent(unsigned long long* p, unsigned long long bits) {
+    __hip_atomic_fetch_or(p, bits, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 // Doubles as order-preserving 64-bit keys (an LDS atomicMin on the key is a
 // min on the value): sign bit set -> all bits flipped, else the sign bit set.
 __device__ __forceinline__ unsigned long long okey(double d) {
@@ -736,7 +784,10 @@ __global__ __launch_bounds__(kWideBlock) void wide_kernel(WideArgs a) {
 // current row in LDS and writes each row once to HBM (compact, coalesced) for
 // the backward, which gathers alpha from that row and sums beta in LDS; no
 // block barriers; the gradient in one LDS table per block when it fits,
-// flushed once per launch.
+// flushed once per launch.  The gradient and the log-likelihood are summed in
+// fixed point (fix128_*): which wave drew which string changes the order of
+// the adds, not their result, so an evaluation gives the same bits every run;
+// the last block out turns the accumulators into doubles.
 __device__ __forceinline__ void wave_fence() { __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup"); }
 constexpr int kU = 4;   // wide2: edges per lane in flight
 constexpr int kExpNone = -4096;   // below every frexp exponent of a double
@@ -757,31 +808,36 @@ template <bool TRACK>
 __global__ __launch_bounds__(kWide2Block) void wide2_kernel(WideArgs a) {
     if (a.halted && *a.halted) return;
     extern __shared__ __attribute__((aligned(16))) double lds2[];
-    __shared__ double llw[kWide2Block / kWave];
+    __shared__ int last_block;
     const int lane = lane_id(), wv = int(threadIdx.x) >> 6, nwv = int(blockDim.x) >> 6;
     const ModelView& m = a.m;
     const PairTables& P = a.pt;
     const int K = P.K, MN = P.max_n;
     const bool lgrad = a.grad_lds != 0;
-    double* gl = lds2;
+    long long* gl = reinterpret_cast<long long*>(lds2);   // fixed point, a.fix_frac fraction bits
+    const int F = a.fix_frac;
+    unsigned long long* gfix = a.fix;                       // [2 n_params]
+    unsigned long long* llfix = a.fix + 2 * int64_t(m.n_params);
     double* rows = lds2 + (lgrad ? ((m.n_params + kWave + 1) & ~1) : 0) + int64_t(wv) * 2 * MN;
     double* R0 = rows;              // the two rows (alternating)
     double* R1 = rows + MN;
     if (lgrad)
-        for (int j = int(threadIdx.x); j < m.n_params + kWave; j += int(blockDim.x)) gl[j] = 0.0;   // + spare slots
+        for (int j = int(threadIdx.x); j < m.n_params + kWave; j += int(blockDim.x)) gl[j] = 0;   // + spare slots
     __syncthreads();
     double* H = a.scratch2 + (int64_t(blockIdx.x) * nwv + wv) * a.stride2;
     double* Mg = H + 1 + int64_t(a.max_len) * MN;   // [2][max_n] min-forward rows (rmin column)
     int* ex = reinterpret_cast<int*>(Mg + 2 * int64_t(MN));   // [max_len + 2]
-    double ll = 0.0;
+    auto add_fix = [&](int j, long long iv) {
+        if (lgrad) block_add_fix(&gl[j], iv); else fix128_add(gfix + 2 * int64_t(j), iv);
+    };
     auto credit = [&](int p0, int p1, int g, double v) {
+        if (!(fabs(v) < INFINITY)) flag_agent(llfix + 2, kFixGradBad);
+        const long long iv = fix_of(v, F);
         if (p0 >= 0) {
-            if (lgrad) block_add(&gl[p0], v); else global_add(&a.grad[p0], v);
-            if (p1 >= 0) { if (lgrad) block_add(&gl[p1], v); else global_add(&a.grad[p1], v); }
+            add_fix(p0, iv);
+            if (p1 >= 0) add_fix(p1, iv);
         } else if (p0 == -2) {
-            for (int q = m.pptr[g]; q < m.pptr[g + 1]; ++q) {
-                if (lgrad) block_add(&gl[m.pidx[q]], v); else global_add(&a.grad[m.pidx[q]], v);
-            }
+            for (int q = m.pptr[g]; q < m.pptr[g + 1]; ++q) add_fix(m.pidx[q], iv);
         }
     };
     for (;;) {
@@ -913,7 +969,15 @@ __global__ __launch_bounds__(kWide2Block) void wide2_kernel(WideArgs a) {
         }
         if (lane == 0) {
             if (a.logq) a.logq[sidx] = lq;
-            ll += ps * lq;
+            const double c = ps * lq;
+            if (fabs(c) < 0x1p62) {
+                unsigned long long lo;
+                long long hi;
+                fix128_of(c, lo, hi);
+                fix128_add(llfix, lo, hi);
+            } else {
+                flag_agent(llfix + 2, c != c ? kFixLlNan : (c < 0.0 ? kFixLlNegInf : kFixLlPosInf));
+            }
         }
         if (!(qh > 0.0) || (WFSA_KDBG(a.dbg) & 1)) continue;
         wave_fence();   // the rows in H (and ex) are visible to every lane
@@ -972,8 +1036,10 @@ __global__ __launch_bounds__(kWide2Block) void wide2_kernel(WideArgs a) {
                     const double v = -ps * (af[u] * bv);
                     if (lgrad) {   // two parameters per edge in one table; the rest to this lane's spare slot
                         const int spare = m.n_params + lane;
-                        block_add(&gl[on && en[u].z >= 0 ? en[u].z : spare], on ? v : 0.0);
-                        block_add(&gl[on && en[u].w >= 0 ? en[u].w : spare], on ? v : 0.0);
+                        if (on && !(fabs(v) < INFINITY)) flag_agent(llfix + 2, kFixGradBad);
+                        const long long iv = on ? fix_of(v, F) : 0;
+                        block_add_fix(&gl[on && en[u].z >= 0 ? en[u].z : spare], iv);
+                        block_add_fix(&gl[on && en[u].w >= 0 ? en[u].w : spare], iv);
                         if (on && en[u].z == -2) credit(-2, -1, en[u].y, v);
                     } else if (on && af[u] * bv > 0.0) {
                         credit(en[u].z, en[u].w, en[u].y, v);
@@ -986,24 +1052,46 @@ __global__ __launch_bounds__(kWide2Block) void wide2_kernel(WideArgs a) {
         }
         wave_sync();
     }
-    if (lane == 0) {
-        llw[wv] = ll;
-        // the last wave out resets the counters for the next launch
+    __syncthreads();   // every wave of the block is past its last string
+    if (lgrad)
+        for (int j = int(threadIdx.x); j < m.n_params; j += int(blockDim.x))
+            if (gl[j] != 0) fix128_add(gfix + 2 * int64_t(j), gl[j]);
+    __threadfence();   // this thread's accumulator adds before the block's arrival
+    __syncthreads();
+    if (threadIdx.x == 0) {
         const unsigned d = __hip_atomic_fetch_add(a.ctr + 1, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
-        if (d + 1 == gridDim.x * unsigned(nwv)) {
+        last_block = d + 1 == gridDim.x;
+    }
+    __syncthreads();
+    if (!last_block) return;
+    // the last block out: the sums into doubles, the accumulators and
+    // counters zeroed for the next launch
+    __threadfence();
+    const unsigned long long flags = ld_agent(llfix + 2);
+    for (int j = int(threadIdx.x); j < m.n_params; j += int(blockDim.x)) {
+        unsigned long long* q = gfix + 2 * int64_t(j);
+        const unsigned long long lo = ld_agent(q), hi = ld_agent(q + 1);
+        if (flags & kFixGradBad) a.grad[j] = __builtin_nan("");
+        else if (lo | hi) a.grad[j] += fix128_value(lo, (long long)hi, F);
+        if (lo | hi) {
+            st_agent(q, 0);
+            st_agent(q + 1, 0);
+        }
+    }
+    for (int b = int(threadIdx.x); b < int(gridDim.x); b += int(blockDim.x)) {
+        double v = 0.0;
+        if (b == 0) {
+            const bool ninf = flags & kFixLlNegInf, pinf = flags & kFixLlPosInf;
+            v = (flags & kFixLlNan) || (ninf && pinf) ? __builtin_nan("")
+                : ninf ? -INFINITY : pinf ? INFINITY : fix128_value(ld_agent(llfix), (long long)ld_agent(llfix + 1), 64);
+            st_agent(llfix, 0);
+            st_agent(llfix + 1, 0);
+            st_agent(llfix + 2, 0);
             __hip_atomic_store(a.ctr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             __hip_atomic_store(a.ctr + 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
+        a.ll_part[b] = v;   // the log-likelihood in the first slot
     }
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        double t = 0.0;
-        for (int w = 0; w < nwv; ++w) t += llw[w];
-        a.ll_part[blockIdx.x] = t;
-    }
-    if (lgrad)
-        for (int j = int(threadIdx.x); j < m.n_params; j += int(blockDim.x))
-            if (gl[j] != 0.0) global_add(&a.grad[j], gl[j]);
 }
 
 __global__ __launch_bounds__(256) void pair_weights_kernel(const int4* ent, int64_t n, const double* ew,
@@ -1751,7 +1839,7 @@ __global__ __launch_bounds__(1024, (DBG == 10 ? 8 : 1)) void fbs_kernel(Compiled
         const int n2 = (a.n_params + 2) / 2;
         const double2* src = reinterpret_cast<const double2*>(a.w);
         double2* dst = reinterpret_cast<double2*>(lds);
-        constexpr int kB = 8;
+        constexpr int kB = 12;   // one round for tables up to 12k params at 512 threads
         for (int j0 = int(threadIdx.x); j0 < n2; j0 += kB * int(blockDim.x)) {
             double2 t[kB];
 #pragma unroll

@@ -228,7 +228,13 @@ struct WideArgs {
     double* scratch2;        // per wave: alpha rows (compact, 1 + max_len * max_n), min-forward rows
                              // [2 max_n], exponents [max_len + 2]
     int64_t stride2;         // doubles per wave
-    unsigned* ctr;           // [2] work and exit counters (zero between launches)
+    unsigned* ctr;           // [2] work and block-exit counters (zero between launches)
+    // wide2_kernel's order-independent sums (fixed point, fix128_* in
+    // fb_kernels.hip): [2 n_params] gradient accumulators (lo, hi words, fix_frac
+    // fraction bits), [2] the log-likelihood's (64 fraction bits), [1] flags
+    // (kFix*); zero between launches
+    unsigned long long* fix;
+    int32_t fix_frac;
 };
 // doubles of scratch per block
 inline int64_t wide_scratch_stride(int32_t max_len, int32_t n_nodes) {

@@ -107,7 +107,7 @@ __global__ __launch_bounds__(NT) void qn_step_kernel(QnArgs a) {
                     cb[i] = a.chunk_ptr[b + i];
                 }
             const bool in_lds = slots && gnch <= a.chunk_cap;   // (else more than kMaxChunks: seg_sums from memory)
-            if (in_lds) chunk_sums<NT>(a.contrib + gb, gnch, cp);   // the group's chunks, this round
+            if (in_lds && WFSA_KDBG(a.dbg) != 7) chunk_sums<NT>(a.contrib + gb, gnch, cp);   // the group's chunks, this round (7: timing, skipped)
             __syncthreads();
             const int s0 = slots ? sp[0] : 0, c0 = slots ? cb[0] : 0;
             double gp[PT];   // this thread's members: trivial-word + traversal parts
@@ -128,7 +128,7 @@ __global__ __launch_bounds__(NT) void qn_step_kernel(QnArgs a) {
                 for (int i = 0; i < PT; ++i) {
                     const int m = t + i * NT;
                     if (m < nm) {
-                        const int q0 = cb[m] - c0, q1 = cb[m + 1] - c0;
+                        const int q0 = cb[m] - c0, q1 = WFSA_KDBG(a.dbg) == 6 ? q0 : cb[m + 1] - c0;   // (6: timing, no sums)
                         double sm = 0.0;
                         int q = q0;
                         for (; q + 8 <= q1; q += 8) {

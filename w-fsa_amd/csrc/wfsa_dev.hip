@@ -243,6 +243,8 @@ struct wfsa_dev {
     int64_t w2_stride = 0;
     int w2_grid = 0;
     DevBuf<unsigned> w2_ctr;
+    DevBuf<unsigned long long> w2_fix;   // the wave kernel's fixed-point sums (WideArgs::fix)
+    int32_t w2_fix_frac = 52;
     bool w2_all = true;          // every traversal string on the wave kernel (WFSA_WIDE2_TIERS=2: tier 2 only)
     DevBuf<int32_t> w2_list;     // its strings, longest first
     int32_t w2_n = 0;
@@ -471,6 +473,8 @@ wfsa::WideArgs wide_args(wfsa_dev* ctx) {
     a.scratch2 = ctx->w2_scratch.ptr;
     a.stride2 = ctx->w2_stride;
     a.ctr = ctx->w2_ctr.ptr;
+    a.fix = ctx->w2_fix.ptr;
+    a.fix_frac = ctx->w2_fix_frac;
     return a;
 }
 
@@ -923,6 +927,8 @@ int layout_slots(wfsa_dev* ctx, const std::vector<int32_t>& pos_of) {
         ctx->lead_grp_nch = 1;   // the largest constraint-led group's chunk count (the QN step's LDS)
         for (size_t g = 0; g + 1 < ctx->slot_groups.size() && int32_t(g) < ng; ++g)
             ctx->lead_grp_nch = std::max(ctx->lead_grp_nch, gn[g]);
+        ctx->stats.max_group_chunks = ctx->lead_grp_nch;
+        ctx->stats.slot_chunks = ctx->n_bubbles > 0 ? int64_t(gbase.back()) / wfsa::kSlotChunk : 0;
     }
     HIP_TRY(ctx->chunk_ptr.upload(cptr_pos.data(), cptr_pos.size(), s));
     HIP_TRY(ctx->seg_ptr.upload(pc.data(), pc.size(), s));
@@ -1440,6 +1446,18 @@ int prepare(wfsa_dev* ctx, int level) {
         HIP_TRY(ctx->w2_scratch.alloc(n2));
         HIP_TRY(ctx->w2_ctr.alloc(2));
         HIP_TRY(hipMemsetAsync(ctx->w2_ctr.ptr, 0, 2 * sizeof(unsigned), s));
+        // fixed-point gradient: a parameter's sum over strings is at most
+        // (max_len + 2) x (parameters per edge) in magnitude (sum p = 1; every
+        // position's edge and the end weight, each parameter once per
+        // occurrence), so a block's partial fits a signed 64-bit word with
+        // the rest as fraction (c3-like max_len 128: 2^-54)
+        int32_t pe = 1;
+        for (size_t g = 0; g + 1 < ctx->h_pptr.size(); ++g) pe = std::max(pe, ctx->h_pptr[g + 1] - ctx->h_pptr[g]);
+        const double bound = (double(ctx->max_len) + 2.0) * double(pe);
+        ctx->w2_fix_frac = std::max(20, std::min(60, 63 - int(std::ceil(std::log2(bound)))));
+        const size_t nfix = 2 * size_t(std::max(ctx->n_params, 1)) + 3;
+        HIP_TRY(ctx->w2_fix.alloc(nfix));
+        HIP_TRY(hipMemsetAsync(ctx->w2_fix.ptr, 0, nfix * sizeof(unsigned long long), s));
     }
     const size_t waves = std::max(size_t(ctx->c_grid), size_t(ctx->i_grid) * size_t(ctx->i_block / kWave)) +
                          size_t(ctx->b_waves) +
