@@ -226,6 +226,12 @@ def run_workload(wl, world, rank, local_rank, distributed, dist, torch, info_rmi
     """build, warm up, time `steps` device-resident QN steps; returns the
     measurement and the objects the extras need"""
     import wfsa_amd as W
+    # torch's own HIP start-up (its first CUDA call) here rather than in the
+    # barrier between the warmup and the timed steps: it idles the GPU for
+    # long enough that the timed steps start at a lower clock (measured: a
+    # 50 ms pause before the timed Run costs 35 -> 45 us per c3 step,
+    # tools/bench_like.py)
+    torch.cuda.synchronize()
     total = wl["strings_per_gpu"] * world
     syn = W.Synthetic(n_states=wl["states"], degree=wl["degree"], vocab=wl["vocab"], emissions=wl["emissions"],
                       dense=wl["dense"], n_strings=total, max_len=wl["max_len"], seed=wl["seed"])
