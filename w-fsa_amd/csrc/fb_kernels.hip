@@ -1094,6 +1094,378 @@ __global__ __launch_bounds__(kWide2Block) void wide2_kernel(WideArgs a) {
     }
 }
 
+// Tier 2, weighted, one wavefront per string, pulling (fb_kernels.hpp
+// PullTables): the forward sums each destination of D(b) over its in-edges
+// and the backward each source of D(a) over its out-edges, a lane per node
+// -- no LDS atomics on the rows, each node's sum in one fixed order -- and a
+// wave needs one LDS row, not two: a lane keeps its finished node sums in a
+// shift register (the newest in acc[0]) until the whole wave has read the
+// row, then writes them over it.  With the gradient table that fits 16 waves
+// per block where wide2_kernel fits 12.  The backward reads alpha of an
+// edge's source from the row the forward wrote to HBM (the lane's consecutive
+// entries share a source: one row read per source: the pair's first entry row
+// lists each lane's sources).  Scaling, alpha history, fixed-point
+// gradient / log-likelihood and the last block's conversion as wide2_kernel.
+#ifndef WFSA_PULL_UF
+#define WFSA_PULL_UF 4   // forward entries per lane in flight
+#endif
+#ifndef WFSA_PULL_UB
+#define WFSA_PULL_UB 2   // backward entries per lane in flight
+#endif
+// timing variants only (make var, never the release build): 1 no alpha
+// gather in the backward, 2 no gradient credits
+#ifndef WFSA_PULL_EXP
+#define WFSA_PULL_EXP 0
+#endif
+template <bool TRACK>
+__global__ __launch_bounds__(kWide2Block) void wave_pull_kernel(WideArgs a) {
+    constexpr int kUF = WFSA_PULL_UF, kUB = WFSA_PULL_UB;
+    if (a.halted && *a.halted) return;
+    extern __shared__ __attribute__((aligned(16))) double lds2[];
+    __shared__ int last_block;
+    const int lane = lane_id(), wv = int(threadIdx.x) >> 6, nwv = int(blockDim.x) >> 6;
+    const ModelView& m = a.m;
+    const PairTables& P = a.pt;
+    const PullTables& Q = a.pl;
+    const int K = P.K, MN = P.max_n;
+    const bool lgrad = a.grad_lds != 0;
+    long long* gl = reinterpret_cast<long long*>(lds2);   // fixed point, a.fix_frac fraction bits
+    const int F = a.fix_frac;
+    unsigned long long* gfix = a.fix;                       // [2 n_params]
+    unsigned long long* llfix = a.fix + 2 * int64_t(m.n_params);
+    double* R = lds2 + (lgrad ? ((m.n_params + kWave + 1) & ~1) : 0) + int64_t(wv) * MN;   // the wave's row
+    if (lgrad)
+        for (int j = int(threadIdx.x); j < m.n_params + kWave; j += int(blockDim.x)) gl[j] = 0;   // + spare slots
+    __syncthreads();
+    double* H = a.scratch2 + (int64_t(blockIdx.x) * nwv + wv) * a.stride2;
+    double* Mg = H + 1 + int64_t(a.max_len) * MN;   // [2][max_n] min-forward rows (rmin column)
+    int* ex = reinterpret_cast<int*>(Mg + 2 * int64_t(MN));   // [max_len + 2]
+    auto add_fix = [&](int j, long long iv) {
+        if (lgrad) block_add_fix(&gl[j], iv); else fix128_add(gfix + 2 * int64_t(j), iv);
+    };
+    auto credit = [&](int p0, int p1, int g, double v) {
+        if (!(fabs(v) < INFINITY)) flag_agent(llfix + 2, kFixGradBad);
+        const long long iv = fix_of(v, F);
+        if (p0 >= 0) {
+            add_fix(p0, iv);
+            if (p1 >= 0) add_fix(p1, iv);
+        } else if (p0 == -2) {
+            for (int q = m.pptr[g]; q < m.pptr[g + 1]; ++q) add_fix(m.pidx[q], iv);
+        }
+    };
+    for (;;) {
+        int li = 0;
+        if (lane == 0) li = int(__hip_atomic_fetch_add(a.ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+        li = __builtin_amdgcn_readfirstlane(__shfl(li, 0, kWave));
+        if (li >= a.n_list) break;
+        const int sidx = a.list[li];
+        const int64_t o0 = a.off[sidx];
+        const int L = int(a.off[sidx + 1] - o0);
+        const uint8_t* str = a.sym + o0;
+        // step info, 64 steps at a time in lane registers (lane j: step c*64+j):
+        // the pair's forward base / T and backward base / T, |D(byte p)| (-1:
+        // no edge consumes the byte), |D of position p|; read with readlane
+        int vfb = 0, vft = 0, vbb = 0, vbt = 0, vnb = 0, vna = 0;
+        auto load_chunk = [&](int c) {
+            const int p = c * kWave + lane;
+            vfb = vft = vbb = vbt = vnb = vna = 0;
+            if (p < L) {
+                const int bp = P.bidx[str[p]];
+                const int apv = p == 0 ? K : P.bidx[str[p - 1]];
+                if (bp < 0 || apv < 0) {
+                    vnb = -1;
+                } else {
+                    const int4 inf = Q.info[apv * K + bp];
+                    vfb = inf.x;
+                    vft = inf.y;
+                    vbb = inf.z;
+                    vbt = inf.w;
+                    vnb = P.n[bp];
+                    vna = P.n[apv];
+                }
+            }
+        };
+        if (lane == 0) {
+            R[0] = 1.0;
+            H[0] = 1.0;
+            ex[0] = 0;
+            if (TRACK) Mg[0] = 0.0;
+        }
+        wave_sync();
+        int exi = 0, esum = 0, last_n = 1;   // last_n: size of the current row
+        int64_t roff = 0;
+        bool alive = true;
+        for (int i = 0; i < L; ++i) {
+            if ((i & (kWave - 1)) == 0) load_chunk(i / kWave);
+            const int ii = i & (kWave - 1);
+            const int nb = __builtin_amdgcn_readlane(vnb, ii);
+            if (nb < 0) {   // no edge consumes the byte
+                alive = false;
+                break;
+            }
+            const int fb = __builtin_amdgcn_readlane(vfb, ii);
+            const int T = __builtin_amdgcn_readlane(vft, ii);
+            const double sc = ldexp(1.0, -exi);
+            const int64_t rn = roff + last_n;
+            const double* Mi = Mg + int64_t(i & 1) * MN;
+            double* Mn = Mg + int64_t((i + 1) & 1) * MN;
+            double acc[kPullItems], amin[kPullItems];
+            int dd[kPullItems];
+#pragma unroll
+            for (int k = 0; k < kPullItems; ++k) {
+                acc[k] = 0.0;
+                amin[k] = INFINITY;
+                dd[k] = -1;
+            }
+            double s = 0.0, smin = INFINITY;
+            for (int t0 = 0; t0 < T; t0 += kUF) {
+                int cd[kUF];
+                double w[kUF], r[kUF], lwv[kUF], mv[kUF];
+#pragma unroll
+                for (int u = 0; u < kUF; ++u) {
+                    const int t = t0 + u;
+                    const int64_t e = int64_t(fb) + int64_t(t) * kWave + lane;
+                    cd[u] = t < T ? Q.fcode[e] : 0;
+                    w[u] = t < T ? Q.fw[e] : 0.0;
+                    if (TRACK) lwv[u] = t < T ? Q.flw[e] : -INFINITY;
+                }
+#pragma unroll
+                for (int u = 0; u < kUF; ++u) r[u] = R[cd[u] & 0xffff];
+                if (TRACK) {
+#pragma unroll
+                    for (int u = 0; u < kUF; ++u) mv[u] = Mi[cd[u] & 0xffff];
+                }
+#pragma unroll
+                for (int u = 0; u < kUF; ++u) {
+                    if (t0 + u >= T) break;   // uniform
+                    s += r[u] * w[u];
+                    if (TRACK && r[u] > 0.0 && lwv[u] > -INFINITY) smin = fmin(smin, mv[u] + lwv[u]);
+                    const bool f = cd[u] < 0;   // the node's last entry
+#pragma unroll
+                    for (int k = kPullItems - 1; k > 0; --k) {
+                        acc[k] = f ? acc[k - 1] : acc[k];
+                        dd[k] = f ? dd[k - 1] : dd[k];
+                        if (TRACK) amin[k] = f ? amin[k - 1] : amin[k];
+                    }
+                    acc[0] = f ? s : acc[0];
+                    dd[0] = f ? ((cd[u] >> 16) & 0x7fff) : dd[0];
+                    s = f ? 0.0 : s;
+                    if (TRACK) {
+                        amin[0] = f ? smin : amin[0];
+                        smin = f ? INFINITY : smin;
+                    }
+                }
+            }
+            wave_sync();   // every lane has read the row
+            int emx = kExpNone;   // the row's largest exponent (ballots, no LDS)
+#pragma unroll
+            for (int k = 0; k < kPullItems; ++k) {
+                if (dd[k] < 0) continue;
+                const double v = acc[k] * sc;
+                R[dd[k]] = v;
+                H[rn + dd[k]] = v;
+                if (v > 0.0) emx = max(emx, __builtin_amdgcn_frexp_exp(v));
+                if (TRACK) Mn[dd[k]] = amin[k];
+            }
+            emx = wave_max_exp(emx);
+            wave_sync();
+            if (TRACK) wave_fence();   // the next step reads the min row from HBM
+            roff = rn;
+            last_n = nb;
+            if (emx == kExpNone) {   // every node of the row is zero
+                alive = false;
+                break;
+            }
+            exi = emx;
+            esum += exi;
+            if (lane == 0) ex[i + 1] = exi;
+        }
+        double qh = 0.0;
+        const double scL = ldexp(1.0, -exi);
+        const int aL = L > 0 ? P.bidx[str[L - 1]] : K;
+        const int nL = alive ? last_n : 0;
+        const int32_t* dL = P.dl_node + P.dl_ptr[alive ? aL : K];
+        for (int d = lane; d < nL; d += kWave) qh += R[d] * scL * end_weight(m, dL[d]);
+        qh = wave_sum(qh);
+        const double lq = qh > 0.0 ? log(qh) + kLn2 * double(esum) : -INFINITY;
+        const double ps = a.p[sidx];
+        if (TRACK) {
+            double mn = INFINITY;
+            for (int d = lane; d < nL; d += kWave) {
+                const double we = end_weight(m, dL[d]);
+                if (R[d] > 0.0 && we > 0.0) mn = fmin(mn, Mg[int64_t(L & 1) * MN + d] + log(we));
+            }
+            mn = -wave_max(-mn);
+            if (lane == 0) a.rmin_log[sidx] = qh > 0.0 ? mn - lq : INFINITY;
+        }
+        if (lane == 0) {
+            if (a.logq) a.logq[sidx] = lq;
+            const double c = ps * lq;
+            if (fabs(c) < 0x1p62) {
+                unsigned long long lo;
+                long long hi;
+                fix128_of(c, lo, hi);
+                fix128_add(llfix, lo, hi);
+            } else {
+                flag_agent(llfix + 2, c != c ? kFixLlNan : (c < 0.0 ? kFixLlNegInf : kFixLlPosInf));
+            }
+        }
+        if (!(qh > 0.0)) continue;
+        wave_fence();   // the rows in H (and ex) are visible to every lane
+        // backward (beta scaled so that alpha_i beta_i is the node posterior):
+        // beta_L from the end weights, over the last alpha row (each lane
+        // reads, then overwrites, its own entries)
+        const double inv_q = 1.0 / qh;
+        for (int d = lane; d < nL; d += kWave) {
+            const int S = dL[d];
+            const double af = R[d] * scL;
+            R[d] = end_weight(m, S) * inv_q;
+            if (!(af > 0.0)) continue;
+            for (int x = m.x_ptr[S]; x < m.x_ptr[S + 1]; ++x) {
+                const int gx = m.n_edges + x;
+                const double xi = af * m.ew[gx] * inv_q;
+                if (xi > 0.0) credit(-2, -1, gx, -ps * xi);
+            }
+        }
+        wave_sync();
+        int ex_next = exi, vex = 0;
+        for (int i = L - 1; i >= 0; --i) {
+            if (i == L - 1 || (i & (kWave - 1)) == kWave - 1) {   // this step's chunk (steps and row exponents)
+                load_chunk(i / kWave);
+                const int p = (i / kWave) * kWave + lane;
+                vex = p <= L ? ex[p] : 0;
+            }
+            const int ii = i & (kWave - 1);
+            const int bb = __builtin_amdgcn_readlane(vbb, ii);
+            const int T = __builtin_amdgcn_readlane(vbt, ii);
+            const int na = __builtin_amdgcn_readlane(vna, ii);
+            const int ex_i = __builtin_amdgcn_readlane(vex, ii);
+            roff -= na;
+            const double sc = ldexp(1.0, -ex_next), sci = ldexp(1.0, -ex_i);
+            double acc[kPullItems], av[kPullItems];
+            int dd[kPullItems];
+            {   // alpha of the lane's sources, in its item order (row 0 of the pair's entries)
+                const int4 sl = Q.bent[int64_t(bb) + lane];
+                const unsigned sw[4] = {unsigned(sl.x), unsigned(sl.y), unsigned(sl.z), unsigned(sl.w)};
+#pragma unroll
+                for (int k = 0; k < kPullItems; ++k) {
+                    const unsigned u = (sw[k >> 1] >> (16 * (k & 1))) & 0xffffu;
+                    av[k] = WFSA_PULL_EXP == 1 ? (u != 0xffffu ? 1e-3 * sci : 0.0)
+                                               : (u != 0xffffu ? H[roff + int(u)] * sci : 0.0);
+                }
+            }
+#pragma unroll
+            for (int k = 0; k < kPullItems; ++k) {
+                acc[k] = 0.0;
+                dd[k] = -1;
+            }
+            double s = 0.0;
+            for (int t0 = 0; t0 < T; t0 += kUB) {
+                int4 en[kUB];
+                double w[kUB], bn[kUB];
+#pragma unroll
+                for (int u = 0; u < kUB; ++u) {
+                    const int t = t0 + u;
+                    const int64_t e = int64_t(bb) + int64_t(t + 1) * kWave + lane;   // (row 0: the lane's sources)
+                    en[u] = t < T ? Q.bent[e] : make_int4(0, -1, -1, -1);
+                    w[u] = t < T ? Q.bw[e] : 0.0;
+                }
+#pragma unroll
+                for (int u = 0; u < kUB; ++u) bn[u] = R[en[u].x & 0xffff];
+#pragma unroll
+                for (int u = 0; u < kUB; ++u) {
+                    if (t0 + u >= T) break;   // uniform
+                    const double afu = av[0];   // alpha of the lane's current source
+                    const bool on = afu > 0.0;
+                    const double bv = on ? w[u] * bn[u] * sc : 0.0;
+                    s += bv;
+                    const double v = -ps * (afu * bv);
+                    if (WFSA_PULL_EXP == 2) {
+                    } else if (lgrad) {   // two parameters per edge in one table; the rest to this lane's spare slot
+                        const int spare = m.n_params + lane;
+                        if (on && !(fabs(v) < INFINITY)) flag_agent(llfix + 2, kFixGradBad);
+                        const long long iv = on ? fix_of(v, F) : 0;
+                        block_add_fix(&gl[on && en[u].z >= 0 ? en[u].z : spare], iv);
+                        block_add_fix(&gl[on && en[u].w >= 0 ? en[u].w : spare], iv);
+                        if (on && en[u].z == -2) credit(-2, -1, en[u].y, v);
+                    } else if (on && afu * bv > 0.0) {
+                        credit(en[u].z, en[u].w, en[u].y, v);
+                    }
+                    const bool f = en[u].x < 0;   // the source's last entry
+#pragma unroll
+                    for (int k = kPullItems - 1; k > 0; --k) {
+                        acc[k] = f ? acc[k - 1] : acc[k];
+                        dd[k] = f ? dd[k - 1] : dd[k];
+                    }
+#pragma unroll
+                    for (int k = 0; k + 1 < kPullItems; ++k) av[k] = f ? av[k + 1] : av[k];
+                    av[kPullItems - 1] = f ? 0.0 : av[kPullItems - 1];
+                    acc[0] = f ? s : acc[0];
+                    dd[0] = f ? ((en[u].x >> 16) & 0x7fff) : dd[0];
+                    s = f ? 0.0 : s;
+                }
+            }
+            wave_sync();   // every lane has read the row
+#pragma unroll
+            for (int k = 0; k < kPullItems; ++k)
+                if (dd[k] >= 0) R[dd[k]] = acc[k];
+            wave_sync();
+            ex_next = ex_i;
+        }
+        wave_sync();
+    }
+    __syncthreads();   // every wave of the block is past its last string
+    if (lgrad)
+        for (int j = int(threadIdx.x); j < m.n_params; j += int(blockDim.x))
+            if (gl[j] != 0) fix128_add(gfix + 2 * int64_t(j), gl[j]);
+    __threadfence();   // this thread's accumulator adds before the block's arrival
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const unsigned d = __hip_atomic_fetch_add(a.ctr + 1, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+        last_block = d + 1 == gridDim.x;
+    }
+    __syncthreads();
+    if (!last_block) return;
+    __threadfence();
+    const unsigned long long flags = ld_agent(llfix + 2);
+    for (int j = int(threadIdx.x); j < m.n_params; j += int(blockDim.x)) {
+        unsigned long long* q = gfix + 2 * int64_t(j);
+        const unsigned long long lo = ld_agent(q), hi = ld_agent(q + 1);
+        if (flags & kFixGradBad) a.grad[j] = __builtin_nan("");
+        else if (lo | hi) a.grad[j] += fix128_value(lo, (long long)hi, F);
+        if (lo | hi) {
+            st_agent(q, 0);
+            st_agent(q + 1, 0);
+        }
+    }
+    for (int b = int(threadIdx.x); b < int(gridDim.x); b += int(blockDim.x)) {
+        double v = 0.0;
+        if (b == 0) {
+            const bool ninf = flags & kFixLlNegInf, pinf = flags & kFixLlPosInf;
+            v = (flags & kFixLlNan) || (ninf && pinf) ? __builtin_nan("")
+                : ninf ? -INFINITY : pinf ? INFINITY : fix128_value(ld_agent(llfix), (long long)ld_agent(llfix + 1), 64);
+            st_agent(llfix, 0);
+            st_agent(llfix + 1, 0);
+            st_agent(llfix + 2, 0);
+            __hip_atomic_store(a.ctr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(a.ctr + 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        a.ll_part[b] = v;   // the log-likelihood in the first slot
+    }
+}
+
+__global__ __launch_bounds__(256) void pull_weights_kernel(const int32_t* __restrict__ g, int64_t n, int64_t n_lw,
+                                                           const double* __restrict__ ew,
+                                                           const double* __restrict__ lw, double* __restrict__ w,
+                                                           double* __restrict__ lw_out) {
+    const int64_t stride = int64_t(gridDim.x) * blockDim.x;
+    for (int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < n; i += stride) {
+        const int32_t k = g[i];
+        w[i] = k >= 0 ? ew[k] : 0.0;
+        if (i < n_lw) lw_out[i] = k >= 0 ? lw[k] : -INFINITY;
+    }
+}
+
 __global__ __launch_bounds__(256) void pair_weights_kernel(const int4* ent, int64_t n, const double* ew,
                                                            const double* lw, double* pw) {
     const int64_t stride = int64_t(gridDim.x) * blockDim.x;
@@ -2298,6 +2670,22 @@ hipError_t launch_wide2(const WideArgs& a, int grid, int waves, size_t lds, hipS
         hipLaunchKernelGGL(wide2_kernel<true>, dim3(unsigned(grid)), dim3(unsigned(waves * kWave)), lds, stream, a);
     else
         hipLaunchKernelGGL(wide2_kernel<false>, dim3(unsigned(grid)), dim3(unsigned(waves * kWave)), lds, stream, a);
+    return hipGetLastError();
+}
+
+hipError_t launch_wave_pull(const WideArgs& a, int grid, int waves, size_t lds, hipStream_t stream) {
+    if (a.rmin_log)
+        hipLaunchKernelGGL(wave_pull_kernel<true>, dim3(unsigned(grid)), dim3(unsigned(waves * kWave)), lds, stream, a);
+    else
+        hipLaunchKernelGGL(wave_pull_kernel<false>, dim3(unsigned(grid)), dim3(unsigned(waves * kWave)), lds, stream, a);
+    return hipGetLastError();
+}
+
+hipError_t launch_pull_weights(const int32_t* g, int64_t n, int64_t n_lw, const double* ew, const double* lw,
+                               double* w, double* lw_out, hipStream_t stream) {
+    if (n == 0) return hipSuccess;
+    const unsigned nb = unsigned(std::min<int64_t>((n + 255) / 256, 4096));
+    hipLaunchKernelGGL(pull_weights_kernel, dim3(nb), dim3(256), 0, stream, g, n, n_lw, ew, lw, w, lw_out);
     return hipGetLastError();
 }
 

@@ -193,6 +193,32 @@ struct PairTables {
     int32_t max_n;
 };
 
+// The same steps laid out for pulling (wave_pull_kernel): the forward sums
+// each destination of D(b) over its in-edges, the backward each source of
+// D(a) over its out-edges, one lane per node -- no LDS atomics, each node's
+// sum in a fixed order, one LDS row per wave (a lane holds its nodes' sums in
+// registers until every lane has read the row, then overwrites it).  Per
+// pair the nodes are dealt to the 64 lanes (largest first, to the least
+// loaded lane, at most kPullItems per lane) and each lane's entries are its
+// nodes' edge lists back to back, lane-strided: entry t of lane l at
+// base + 64 t + l, T entries per lane (the most loaded lane; the rest padded).
+// A node's last entry carries the flag bit and the node; a node without edges
+// gets one empty flagged entry (its sum is 0).  The backward's entries start
+// with one more row: per lane its sources in item order, 16 bits each
+// (0xffff: none), so a lane loads their alpha at the step's start.
+//   forward code:  src index | dst index << 16 | last << 31
+//   backward code: dst index | src index << 16 | last << 31
+// (src in D(a), dst in D(b), both < 2^15).
+constexpr int kPullItems = 8;
+struct PullTables {
+    const int4* info;        // [(K + 1) K] per pair: forward base, forward T, backward base, backward T
+    const int32_t* fcode;    // forward entries
+    const double* fw;        // their ew this evaluation (0: padding / empty node)
+    const double* flw;       // their lw (rmin column; -inf: padding)
+    const int4* bent;        // backward entries: code, edge id, param0, param1 (as PairTables::ent)
+    const double* bw;        // their ew this evaluation
+};
+
 struct WideModel {
     const int32_t* c_ptr;    // [257] destination entries of byte c: [c_ptr[c], c_ptr[c+1])
     const int32_t* dst;      // [n_dst] the node (every destination of a byte-c edge, once)
@@ -225,7 +251,8 @@ struct WideArgs {
     double* rmin_log;        // min mode: [S] log(min path weight / q)
     // weighted mode, wave per string (wide2_kernel over the byte-pair tables)
     PairTables pt;
-    double* scratch2;        // per wave: alpha rows (compact, 1 + max_len * max_n), min-forward rows
+    PullTables pl;           // wave_pull_kernel (info null: not built)
+    double* scratch2;       // per wave: alpha rows (compact, 1 + max_len * max_n), min-forward rows
                              // [2 max_n], exponents [max_len + 2]
     int64_t stride2;         // doubles per wave
     unsigned* ctr;           // [2] work and block-exit counters (zero between launches)
@@ -255,6 +282,15 @@ inline size_t wide2_lds(int32_t n_params, bool grad_lds, int waves, int32_t max_
 }
 // waves: per block (blockDim = 64 waves); lds from wide2_lds
 hipError_t launch_wide2(const WideArgs& a, int grid, int waves, size_t lds, hipStream_t stream);
+// LDS of a wave_pull_kernel block: the gradient table + one row per wave
+inline size_t pull_lds(int32_t n_params, bool grad_lds, int waves, int32_t max_n) {
+    return (grad_lds ? size_t((n_params + 64 + 1) & ~1) * 8 : 0) + size_t(waves) * size_t(max_n) * 8;
+}
+hipError_t launch_wave_pull(const WideArgs& a, int grid, int waves, size_t lds, hipStream_t stream);
+// the pull tables' per-evaluation weights: w[i] = ew[g[i]] (0 where g < 0),
+// and for i < n_lw, lw_out[i] = lw[g[i]] (-inf where g < 0)
+hipError_t launch_pull_weights(const int32_t* g, int64_t n, int64_t n_lw, const double* ew, const double* lw,
+                               double* w, double* lw_out, hipStream_t stream);
 // the pair tables' per-evaluation weights pw[0, n) = ew, pw[n, 2n) = lw
 hipError_t launch_pair_weights(const int4* ent, int64_t n, const double* ew, const double* lw, double* pw,
                                hipStream_t stream);

@@ -237,6 +237,14 @@ struct wfsa_dev {
     DevBuf<int4> pt_ent;
     DevBuf<int32_t> pt_sd;
     DevBuf<double> pt_w;   // [2 ne]: ew, lw per entry
+    // the same pairs laid out for wave_pull_kernel (PullTables; WFSA_PULL=0: wide2_kernel)
+    bool use_pull = true;
+    bool has_pull = false;
+    bool w2_pull = false;           // this preparation runs wave_pull_kernel
+    int64_t pl_nf = 0, pl_nb = 0;   // forward / backward entries
+    DevBuf<int4> pl_info, pl_bent;
+    DevBuf<int32_t> pl_fcode, pl_g;   // pl_g: edge id per forward then per backward entry
+    DevBuf<double> pl_w;              // [nf + nb + nf]: forward ew, backward ew, forward lw
     int w2_waves = 16;           // waves per block
     bool w2_lgrad = false;       // the gradient in LDS
     DevBuf<double> w2_scratch;
@@ -470,6 +478,14 @@ wfsa::WideArgs wide_args(wfsa_dev* ctx) {
     a.pt.w = ctx->pt_w.ptr;
     a.pt.lw = ctx->pt_w.ptr + ctx->pt_ne;
     a.pt.max_n = ctx->pt_max_n;
+    if (ctx->has_pull) {
+        a.pl.info = ctx->pl_info.ptr;
+        a.pl.fcode = ctx->pl_fcode.ptr;
+        a.pl.bent = ctx->pl_bent.ptr;
+        a.pl.fw = ctx->pl_w.ptr;
+        a.pl.bw = ctx->pl_w.ptr + ctx->pl_nf;
+        a.pl.flw = ctx->pl_w.ptr + ctx->pl_nf + ctx->pl_nb;
+    }
     a.scratch2 = ctx->w2_scratch.ptr;
     a.stride2 = ctx->w2_stride;
     a.ctr = ctx->w2_ctr.ptr;
@@ -483,19 +499,158 @@ wfsa::WideArgs wide_args(wfsa_dev* ctx) {
 // atomics cost ~7x at family B), else the most waves with global atomics.
 bool wide2_config(wfsa_dev* ctx) {
     const size_t cap = size_t(kLdsPerCu) - 1024;
+    const bool pull = ctx->has_pull && ctx->use_pull;
+    auto lds = [&](bool lg, int w) {
+        return pull ? wfsa::pull_lds(ctx->n_params, lg, w, ctx->pt_max_n) : wfsa::wide2_lds(ctx->n_params, lg, w, ctx->pt_max_n);
+    };
     int best = 0;
     bool lg = false;
     for (int w : {16, 12, 8, 4})
-        if (!best && wfsa::wide2_lds(ctx->n_params, true, w, ctx->pt_max_n) <= cap) {
+        if (!best && lds(true, w) <= cap) {
             best = w;
             lg = true;
         }
     for (int w : {16, 12, 8, 4})
-        if (!best && wfsa::wide2_lds(ctx->n_params, false, w, ctx->pt_max_n) <= cap) best = w;
+        if (!best && lds(false, w) <= cap) best = w;
     if (!best) return false;
     ctx->w2_waves = best;
     ctx->w2_lgrad = lg;
+    ctx->w2_pull = pull;
     return true;
+}
+
+// The pull layout of the pair tables (fb_kernels.hpp PullTables) from the
+// pairs' edge lists: per pair, the forward's items are the destinations of
+// D(b) with their in-edges, the backward's the sources of D(a) with their
+// out-edges (both in the lists' order); items dealt to the 64 lanes largest
+// first, each to the least loaded lane holding fewer than kPullItems.
+// Skipped (has_pull = false) when a D(b) exceeds 64 kPullItems nodes.
+int build_pull_tables(wfsa_dev* ctx, int K, const std::vector<int32_t>& n, const std::vector<int32_t>& e_ptr,
+                      const std::vector<int4>& ent) {
+    ctx->has_pull = false;
+    int32_t max_n = 0;
+    for (int32_t v : n) max_n = std::max(max_n, v);
+    if (max_n > kWave * wfsa::kPullItems || max_n >= 32768) return WFSA_OK;
+    const int64_t n_pairs = int64_t(K + 1) * K;
+    std::vector<int4> info(static_cast<size_t>(n_pairs));
+    std::vector<int32_t> fcode, fg, bg;
+    std::vector<int4> bent;
+    std::vector<std::vector<int32_t>> items;   // per node: its entries (indices into ent)
+    std::vector<int32_t> order;
+    std::vector<int64_t> load(kWave);
+    std::vector<int32_t> cnt(kWave);
+    std::vector<std::vector<int32_t>> lane_items(kWave);
+    // deal items [0, n_items) to the lanes; returns T (entries of the most loaded lane)
+    auto deal = [&](int n_items) -> int64_t {
+        order.resize(size_t(n_items));
+        for (int i = 0; i < n_items; ++i) order[size_t(i)] = i;
+        std::stable_sort(order.begin(), order.end(),
+                         [&](int32_t x, int32_t y) { return items[size_t(x)].size() > items[size_t(y)].size(); });
+        std::fill(load.begin(), load.end(), 0);
+        std::fill(cnt.begin(), cnt.end(), 0);
+        for (auto& v : lane_items) v.clear();
+        for (int32_t it : order) {
+            int best = -1;
+            for (int l = 0; l < kWave; ++l)
+                if (cnt[size_t(l)] < wfsa::kPullItems && (best < 0 || load[size_t(l)] < load[size_t(best)])) best = l;
+            lane_items[size_t(best)].push_back(it);
+            load[size_t(best)] += std::max<int64_t>(1, int64_t(items[size_t(it)].size()));
+            ++cnt[size_t(best)];
+        }
+        int64_t T = 0;
+        for (int64_t v : load) T = std::max(T, v);
+        return T;
+    };
+    for (int a = 0; a <= K; ++a) {
+        for (int b = 0; b < K; ++b) {
+            const int64_t q = int64_t(a) * K + b;
+            const int na = n[size_t(a)], nb = n[size_t(b)];
+            const int32_t e0 = e_ptr[size_t(q)], e1 = e_ptr[size_t(q) + 1];
+            // forward: destinations
+            items.assign(size_t(nb), {});
+            for (int32_t e = e0; e < e1; ++e) items[size_t(uint32_t(ent[size_t(e)].x) >> 16)].push_back(e);
+            int64_t T = deal(nb);
+            const int64_t fbase = int64_t(fcode.size());
+            fcode.resize(size_t(fbase + T * kWave), 0);
+            fg.resize(size_t(fbase + T * kWave), -1);
+            for (int l = 0; l < kWave; ++l) {
+                int64_t t = 0;
+                for (int32_t d : lane_items[size_t(l)]) {
+                    const auto& it = items[size_t(d)];
+                    const size_t at0 = size_t(fbase + t * kWave + l);
+                    if (it.empty()) {
+                        fcode[at0] = int32_t((uint32_t(d) << 16) | 0x80000000u);
+                        ++t;
+                        continue;
+                    }
+                    for (size_t k = 0; k < it.size(); ++k, ++t) {
+                        const int4& en = ent[size_t(it[k])];
+                        const size_t at = size_t(fbase + t * kWave + l);
+                        fcode[at] = int32_t((uint32_t(en.x) & 0xffffu) | (uint32_t(d) << 16) |
+                                            (k + 1 == it.size() ? 0x80000000u : 0u));
+                        fg[at] = en.y;
+                    }
+                }
+            }
+            const int64_t fT = T;
+            // backward: sources
+            items.assign(size_t(na), {});
+            for (int32_t e = e0; e < e1; ++e) items[size_t(uint32_t(ent[size_t(e)].x) & 0xffffu)].push_back(e);
+            T = deal(na);
+            const int64_t bbase = int64_t(bent.size());
+            bent.resize(size_t(bbase + (T + 1) * kWave), make_int4(0, -1, -1, -1));
+            bg.resize(bent.size(), -1);
+            for (int l = 0; l < kWave; ++l) {   // row 0: the lane's sources
+                uint32_t sw[4] = {~0u, ~0u, ~0u, ~0u};
+                for (size_t k = 0; k < lane_items[size_t(l)].size(); ++k) {
+                    const uint32_t u = uint32_t(lane_items[size_t(l)][k]);
+                    sw[k >> 1] = (sw[k >> 1] & ~(0xffffu << (16 * (k & 1)))) | (u << (16 * (k & 1)));
+                }
+                bent[size_t(bbase + l)] = make_int4(int32_t(sw[0]), int32_t(sw[1]), int32_t(sw[2]), int32_t(sw[3]));
+            }
+            for (int l = 0; l < kWave; ++l) {
+                int64_t t = 1;
+                for (int32_t u : lane_items[size_t(l)]) {
+                    const auto& it = items[size_t(u)];
+                    if (it.empty()) {
+                        bent[size_t(bbase + t * kWave + l)] = make_int4(int32_t((uint32_t(u) << 16) | 0x80000000u), -1, -1, -1);
+                        ++t;
+                        continue;
+                    }
+                    for (size_t k = 0; k < it.size(); ++k, ++t) {
+                        const int4& en = ent[size_t(it[k])];
+                        bent[size_t(bbase + t * kWave + l)] =
+                            make_int4(int32_t((uint32_t(en.x) >> 16) | (uint32_t(u) << 16) |
+                                              (k + 1 == it.size() ? 0x80000000u : 0u)),
+                                      en.y, en.z, en.w);
+                        bg[size_t(bbase + t * kWave + l)] = en.y;
+                    }
+                }
+            }
+            if (fbase + fT * kWave >= (int64_t(1) << 31) || bbase + (T + 1) * kWave >= (int64_t(1) << 31)) return WFSA_OK;
+            info[size_t(q)] = make_int4(int32_t(fbase), int32_t(fT), int32_t(bbase), int32_t(T));
+        }
+    }
+    if (fcode.empty()) {
+        fcode.push_back(0);
+        fg.push_back(-1);
+    }
+    if (bent.empty()) {
+        bent.push_back(make_int4(0, -1, -1, -1));
+        bg.push_back(-1);
+    }
+    hipStream_t s = ctx->stream;
+    HIP_TRY(ctx->pl_info.upload(info.data(), info.size(), s));
+    HIP_TRY(ctx->pl_fcode.upload(fcode.data(), fcode.size(), s));
+    HIP_TRY(ctx->pl_bent.upload(bent.data(), bent.size(), s));
+    fg.insert(fg.end(), bg.begin(), bg.end());
+    HIP_TRY(ctx->pl_g.upload(fg.data(), fg.size(), s));
+    ctx->pl_nf = int64_t(fcode.size());
+    ctx->pl_nb = int64_t(bent.size());
+    HIP_TRY(ctx->pl_w.alloc(size_t(2 * ctx->pl_nf + ctx->pl_nb)));
+    HIP_TRY(hipStreamSynchronize(s));
+    ctx->has_pull = true;
+    return WFSA_OK;
 }
 
 // The byte-pair tables of the tier-2 wave kernel (fb_kernels.hpp
@@ -588,6 +743,7 @@ int build_pair_tables(wfsa_dev* ctx, const wfsa::TrellisModel& tm, const std::ve
     ctx->pt_K = K;
     ctx->pt_max_n = max_n;
     ctx->pt_ne = int64_t(ent.size());
+    if (int rc = build_pull_tables(ctx, K, n, e_ptr, ent)) return rc;
     ctx->has_pairs = true;
     return WFSA_OK;
 }
@@ -1736,9 +1892,16 @@ int enqueue_evaluation(wfsa_dev* ctx, bool want_logq, const unsigned* halted, in
             a.grad_lds = ctx->w2_lgrad ? 1 : 0;
             static const int w2dbg = experiment_knob("WFSA_W2_DBG");
             a.dbg = w2dbg;
-            HIP_TRY(wfsa::launch_pair_weights(ctx->pt_ent.ptr, ctx->pt_ne, ctx->ew.ptr, ctx->lw.ptr, ctx->pt_w.ptr, s));
-            const size_t lds = wfsa::wide2_lds(ctx->n_params, ctx->w2_lgrad, ctx->w2_waves, ctx->pt_max_n);
-            HIP_TRY(wfsa::launch_wide2(a, ctx->w2_grid, ctx->w2_waves, lds, s));
+            if (ctx->w2_pull) {
+                HIP_TRY(wfsa::launch_pull_weights(ctx->pl_g.ptr, ctx->pl_nf + ctx->pl_nb, ctx->pl_nf, ctx->ew.ptr,
+                                                  ctx->lw.ptr, ctx->pl_w.ptr, ctx->pl_w.ptr + ctx->pl_nf + ctx->pl_nb, s));
+                const size_t lds = wfsa::pull_lds(ctx->n_params, ctx->w2_lgrad, ctx->w2_waves, ctx->pt_max_n);
+                HIP_TRY(wfsa::launch_wave_pull(a, ctx->w2_grid, ctx->w2_waves, lds, s));
+            } else {
+                HIP_TRY(wfsa::launch_pair_weights(ctx->pt_ent.ptr, ctx->pt_ne, ctx->ew.ptr, ctx->lw.ptr, ctx->pt_w.ptr, s));
+                const size_t lds = wfsa::wide2_lds(ctx->n_params, ctx->w2_lgrad, ctx->w2_waves, ctx->pt_max_n);
+                HIP_TRY(wfsa::launch_wide2(a, ctx->w2_grid, ctx->w2_waves, lds, s));
+            }
             wave_off += ctx->w2_grid;
         } else {
             HIP_TRY(wfsa::launch_wide(false, a, ctx->fall_grid[2], s));
@@ -2276,6 +2439,7 @@ int wfsa_dev_create(int device, wfsa_dev** out) {
     if (const char* e = std::getenv("WFSA_DENSE"); e && e[0]) ctx->dense_mode = e[0] == '0' ? 0 : 1;
     if (const char* e = std::getenv("WFSA_TIER2")) ctx->force_tier2 = e[0] == '1';
     if (const char* e = std::getenv("WFSA_WIDE2")) ctx->use_wide2 = e[0] != '0';
+    if (const char* e = std::getenv("WFSA_PULL")) ctx->use_pull = e[0] != '0';
     if (const char* e = std::getenv("WFSA_WIDE2_TIERS")) ctx->w2_all = std::strcmp(e, "2") != 0;
 
     HIP_TRY(hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking));
