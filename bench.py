@@ -325,25 +325,26 @@ def roofline_of(m, traffic):
     # family B: the traversal strings (k_c..k_2 of the evaluation)
     trav_ms = max(fb_ms - kern_ms, 1e-9)
     rows, pedges = st1.get("wave_row_entries", 0), st1.get("wave_pair_edges", 0)
+    alg_bytes = int(mean_sym * trav) + 16 * trav   # string bytes + offset + p per string
+    extra = {}
     if st1.get("wave_strings", 0) > 0:
-        # wide2_kernel: every alpha entry of every position is written to HBM
-        # once by the forward and read back once by the backward (16 B; the
-        # rows of one evaluation, 16 B x sum|D|, far exceed the caches), plus
-        # the strings (L + offset + p)
-        alg_bytes = 16 * rows + int(mean_sym * trav) + 16 * trav
-        kernel = "wide2_kernel (traversal strings: a wavefront per string over byte-pair edge lists, LDS rows)"
-        note = ("per-step latency chain (edge list -> LDS gather -> LDS atomic) with a 106 KB LDS gradient table "
-                "limiting the CU to 12 strings in flight; PMC: LDS array busy ~45%, waves waiting ~75% "
-                "(profiles/r02/v8_wide2_pmc.txt)")
+        pull = st1.get("wave_pull", 0)
+        kernel = ("wave_pull_kernel (traversal strings: a wavefront per string, each step's nodes pulled lane by "
+                  "lane over the byte-pair edge lists)" if pull else
+                  "wide2_kernel (traversal strings: a wavefront per string over byte-pair edge lists, LDS rows)")
+        note = ("HBM is not this pass's bound (SURVEY 8d): a dependent per-position chain of L2 loads, LDS "
+                "gathers and LDS fixed-point gradient adds per string, 16 strings in flight per CU; its honest "
+                "efficiency figure is fp64_flops_frac.  The implementation also writes every alpha row to HBM "
+                "and reads it back (alpha_history_bytes).  PMC: profiles/r03/famb_pull_pmc.txt")
+        extra = {"alpha_history_bytes": 16 * rows, "nodes_per_lane": pull}
     else:
-        alg_bytes = int(mean_sym * trav) + 16 * trav
         kernel = "traversal tiers (trav_kernel<MODE_WEIGHTED> tiers 0/1 + wide_kernel tier 2), per step"
         note = "HBM is not the binding level here (SURVEY 8d: a dependent L-step chain + LDS/L2 gathers)"
     achieved = alg_bytes / (trav_ms * 1e-3) / 1e9
     out = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
            "frac": achieved / HBM_PEAK_GBS, "traffic": None, "kernel": kernel,
            "timed_launches": timed, "kernel_ms_per_launch": trav_ms, "all_fb_kernels_ms_per_step": fb_ms,
-           "algorithmic_bytes_per_launch": alg_bytes, "traversal_strings": trav, "note": note}
+           "algorithmic_bytes_per_launch": alg_bytes, "traversal_strings": trav, "note": note, **extra}
     if pedges > 0:
         out.update({"alpha_entries_per_evaluation": rows, "pair_edges_per_pass": pedges,
                     "pair_edge_visits_per_s": 2.0 * pedges / (trav_ms * 1e-3)})
@@ -445,7 +446,7 @@ def main():
     rmin_pass = None
     if not args.info_rmin and not distributed and not wl["dense"]:
         lrn.set_info_rmin(True)
-        lrn.Run(2, 1.0, -1.0)
+        lrn.Run(max(wl["warmup"], 10), 1.0, -1.0)   # (its set-up, then the clock back up: as the headline's warmup)
         m["barrier"]()
         t1 = time.perf_counter()
         rrows = lrn.Run(wl["steps"], 1.0, -1.0)

@@ -111,7 +111,7 @@ typedef struct {
     int32_t comm_peer;         /* the one-shot peer all-reduce: 1 on, 0 off / untried, -1 its set-up check failed */
     int64_t slot_chunks;       /* bubble contribution slots, in 16-slot chunks (8 B a slot) */
     int32_t max_group_chunks;  /* chunks of the largest constraint's slot group (one QN block sums it) */
-    int32_t pad_;
+    int32_t wave_pull;         /* the wave kernel pulls (wave_pull_kernel): nodes per lane (4, 6, 8); 0: it pushes (wide2_kernel) */
 } wfsa_dev_stats;
 
 /* context ---------------------------------------------------------------- */

@@ -1117,7 +1117,7 @@ __global__ __launch_bounds__(kWide2Block) void wide2_kernel(WideArgs a) {
 #ifndef WFSA_PULL_EXP
 #define WFSA_PULL_EXP 0
 #endif
-template <bool TRACK>
+template <int NI, bool TRACK>
 __global__ __launch_bounds__(kWide2Block) void wave_pull_kernel(WideArgs a) {
     constexpr int kUF = WFSA_PULL_UF, kUB = WFSA_PULL_UB;
     if (a.halted && *a.halted) return;
@@ -1165,17 +1165,18 @@ __global__ __launch_bounds__(kWide2Block) void wave_pull_kernel(WideArgs a) {
         // step info, 64 steps at a time in lane registers (lane j: step c*64+j):
         // the pair's forward base / T and backward base / T, |D(byte p)| (-1:
         // no edge consumes the byte), |D of position p|; read with readlane
-        int vfb = 0, vft = 0, vbb = 0, vbt = 0, vnb = 0, vna = 0;
+        int vfb = 0, vft = 0, vbb = 0, vbt = 0, vnb = 0, vna = 0, vq = 0;
         auto load_chunk = [&](int c) {
             const int p = c * kWave + lane;
-            vfb = vft = vbb = vbt = vnb = vna = 0;
+            vfb = vft = vbb = vbt = vnb = vna = vq = 0;
             if (p < L) {
                 const int bp = P.bidx[str[p]];
                 const int apv = p == 0 ? K : P.bidx[str[p - 1]];
                 if (bp < 0 || apv < 0) {
                     vnb = -1;
                 } else {
-                    const int4 inf = Q.info[apv * K + bp];
+                    vq = apv * K + bp;
+                    const int4 inf = Q.info[vq];
                     vfb = inf.x;
                     vft = inf.y;
                     vbb = inf.z;
@@ -1205,17 +1206,16 @@ __global__ __launch_bounds__(kWide2Block) void wave_pull_kernel(WideArgs a) {
             }
             const int fb = __builtin_amdgcn_readlane(vfb, ii);
             const int T = __builtin_amdgcn_readlane(vft, ii);
+            const int4 dh = Q.fhdr[int64_t(__builtin_amdgcn_readlane(vq, ii)) * kWave + lane];   // the lane's destinations
             const double sc = ldexp(1.0, -exi);
             const int64_t rn = roff + last_n;
             const double* Mi = Mg + int64_t(i & 1) * MN;
             double* Mn = Mg + int64_t((i + 1) & 1) * MN;
-            double acc[kPullItems], amin[kPullItems];
-            int dd[kPullItems];
+            double acc[NI], amin[NI];
 #pragma unroll
-            for (int k = 0; k < kPullItems; ++k) {
+            for (int k = 0; k < NI; ++k) {
                 acc[k] = 0.0;
                 amin[k] = INFINITY;
-                dd[k] = -1;
             }
             double s = 0.0, smin = INFINITY;
             for (int t0 = 0; t0 < T; t0 += kUF) {
@@ -1242,30 +1242,46 @@ __global__ __launch_bounds__(kWide2Block) void wave_pull_kernel(WideArgs a) {
                     if (TRACK && r[u] > 0.0 && lwv[u] > -INFINITY) smin = fmin(smin, mv[u] + lwv[u]);
                     const bool f = cd[u] < 0;   // the node's last entry
 #pragma unroll
-                    for (int k = kPullItems - 1; k > 0; --k) {
-                        acc[k] = f ? acc[k - 1] : acc[k];
-                        dd[k] = f ? dd[k - 1] : dd[k];
-                        if (TRACK) amin[k] = f ? amin[k - 1] : amin[k];
+                    for (int k = 0; k + 1 < NI; ++k) {   // (a queue: the lane's first node ends up in acc[0])
+                        acc[k] = f ? acc[k + 1] : acc[k];
+                        if (TRACK) amin[k] = f ? amin[k + 1] : amin[k];
                     }
-                    acc[0] = f ? s : acc[0];
-                    dd[0] = f ? ((cd[u] >> 16) & 0x7fff) : dd[0];
+                    acc[NI - 1] = f ? s : acc[NI - 1];
                     s = f ? 0.0 : s;
                     if (TRACK) {
-                        amin[0] = f ? smin : amin[0];
+                        amin[NI - 1] = f ? smin : amin[NI - 1];
                         smin = f ? INFINITY : smin;
                     }
                 }
             }
             wave_sync();   // every lane has read the row
             int emx = kExpNone;   // the row's largest exponent (ballots, no LDS)
+            {
+                // the lane's n nodes sit in acc[NI - n .. NI) in its item order: node k
+                // (header slot k) in acc[NI - n + k]; shift them down to acc[k]
+                const unsigned hw[4] = {unsigned(dh.x), unsigned(dh.y), unsigned(dh.z), unsigned(dh.w)};
+                int n = 0;
 #pragma unroll
-            for (int k = 0; k < kPullItems; ++k) {
-                if (dd[k] < 0) continue;
-                const double v = acc[k] * sc;
-                R[dd[k]] = v;
-                H[rn + dd[k]] = v;
-                if (v > 0.0) emx = max(emx, __builtin_amdgcn_frexp_exp(v));
-                if (TRACK) Mn[dd[k]] = amin[k];
+                for (int k = 0; k < NI; ++k) n += ((hw[k >> 1] >> (16 * (k & 1))) & 0xffffu) != 0xffffu ? 1 : 0;
+#pragma unroll
+                for (int r = 0; r < NI; ++r) {   // NI - n rounds of a one-place shift
+                    const bool sh = r < NI - n;
+#pragma unroll
+                    for (int k = 0; k + 1 < NI; ++k) {
+                        acc[k] = sh ? acc[k + 1] : acc[k];
+                        if (TRACK) amin[k] = sh ? amin[k + 1] : amin[k];
+                    }
+                }
+#pragma unroll
+                for (int k = 0; k < NI; ++k) {
+                    const unsigned d = (hw[k >> 1] >> (16 * (k & 1))) & 0xffffu;
+                    if (d == 0xffffu) continue;
+                    const double v = acc[k] * sc;
+                    R[d] = v;
+                    H[rn + d] = v;
+                    if (v > 0.0) emx = max(emx, __builtin_amdgcn_frexp_exp(v));
+                    if (TRACK) Mn[d] = amin[k];
+                }
             }
             emx = wave_max_exp(emx);
             wave_sync();
@@ -1342,20 +1358,20 @@ __global__ __launch_bounds__(kWide2Block) void wave_pull_kernel(WideArgs a) {
             const int ex_i = __builtin_amdgcn_readlane(vex, ii);
             roff -= na;
             const double sc = ldexp(1.0, -ex_next), sci = ldexp(1.0, -ex_i);
-            double acc[kPullItems], av[kPullItems];
-            int dd[kPullItems];
+            double acc[NI], av[NI];
+            int dd[NI];
             {   // alpha of the lane's sources, in its item order (row 0 of the pair's entries)
                 const int4 sl = Q.bent[int64_t(bb) + lane];
                 const unsigned sw[4] = {unsigned(sl.x), unsigned(sl.y), unsigned(sl.z), unsigned(sl.w)};
 #pragma unroll
-                for (int k = 0; k < kPullItems; ++k) {
+                for (int k = 0; k < NI; ++k) {
                     const unsigned u = (sw[k >> 1] >> (16 * (k & 1))) & 0xffffu;
                     av[k] = WFSA_PULL_EXP == 1 ? (u != 0xffffu ? 1e-3 * sci : 0.0)
                                                : (u != 0xffffu ? H[roff + int(u)] * sci : 0.0);
                 }
             }
 #pragma unroll
-            for (int k = 0; k < kPullItems; ++k) {
+            for (int k = 0; k < NI; ++k) {
                 acc[k] = 0.0;
                 dd[k] = -1;
             }
@@ -1393,13 +1409,13 @@ __global__ __launch_bounds__(kWide2Block) void wave_pull_kernel(WideArgs a) {
                     }
                     const bool f = en[u].x < 0;   // the source's last entry
 #pragma unroll
-                    for (int k = kPullItems - 1; k > 0; --k) {
+                    for (int k = NI - 1; k > 0; --k) {
                         acc[k] = f ? acc[k - 1] : acc[k];
                         dd[k] = f ? dd[k - 1] : dd[k];
                     }
 #pragma unroll
-                    for (int k = 0; k + 1 < kPullItems; ++k) av[k] = f ? av[k + 1] : av[k];
-                    av[kPullItems - 1] = f ? 0.0 : av[kPullItems - 1];
+                    for (int k = 0; k + 1 < NI; ++k) av[k] = f ? av[k + 1] : av[k];
+                    av[NI - 1] = f ? 0.0 : av[NI - 1];
                     acc[0] = f ? s : acc[0];
                     dd[0] = f ? ((en[u].x >> 16) & 0x7fff) : dd[0];
                     s = f ? 0.0 : s;
@@ -1407,7 +1423,7 @@ __global__ __launch_bounds__(kWide2Block) void wave_pull_kernel(WideArgs a) {
             }
             wave_sync();   // every lane has read the row
 #pragma unroll
-            for (int k = 0; k < kPullItems; ++k)
+            for (int k = 0; k < NI; ++k)
                 if (dd[k] >= 0) R[dd[k]] = acc[k];
             wave_sync();
             ex_next = ex_i;
@@ -2673,11 +2689,21 @@ hipError_t launch_wide2(const WideArgs& a, int grid, int waves, size_t lds, hipS
     return hipGetLastError();
 }
 
-hipError_t launch_wave_pull(const WideArgs& a, int grid, int waves, size_t lds, hipStream_t stream) {
+template <int NI>
+void launch_wave_pull_ni(const WideArgs& a, int grid, int waves, size_t lds, hipStream_t stream) {
     if (a.rmin_log)
-        hipLaunchKernelGGL(wave_pull_kernel<true>, dim3(unsigned(grid)), dim3(unsigned(waves * kWave)), lds, stream, a);
+        hipLaunchKernelGGL((wave_pull_kernel<NI, true>), dim3(unsigned(grid)), dim3(unsigned(waves * kWave)), lds, stream, a);
     else
-        hipLaunchKernelGGL(wave_pull_kernel<false>, dim3(unsigned(grid)), dim3(unsigned(waves * kWave)), lds, stream, a);
+        hipLaunchKernelGGL((wave_pull_kernel<NI, false>), dim3(unsigned(grid)), dim3(unsigned(waves * kWave)), lds, stream, a);
+}
+
+hipError_t launch_wave_pull(const WideArgs& a, int grid, int waves, size_t lds, hipStream_t stream) {
+    switch (a.pl.items) {
+    case 4: launch_wave_pull_ni<4>(a, grid, waves, lds, stream); break;
+    case 6: launch_wave_pull_ni<6>(a, grid, waves, lds, stream); break;
+    case 8: launch_wave_pull_ni<8>(a, grid, waves, lds, stream); break;
+    default: return hipErrorInvalidValue;
+    }
     return hipGetLastError();
 }
 

@@ -199,19 +199,22 @@ struct PairTables {
 // sum in a fixed order, one LDS row per wave (a lane holds its nodes' sums in
 // registers until every lane has read the row, then overwrites it).  Per
 // pair the nodes are dealt to the 64 lanes (largest first, to the least
-// loaded lane, at most kPullItems per lane) and each lane's entries are its
+// loaded lane, at most `items` per lane) and each lane's entries are its
 // nodes' edge lists back to back, lane-strided: entry t of lane l at
 // base + 64 t + l, T entries per lane (the most loaded lane; the rest padded).
 // A node's last entry carries the flag bit and the node; a node without edges
 // gets one empty flagged entry (its sum is 0).  The backward's entries start
 // with one more row: per lane its sources in item order, 16 bits each
-// (0xffff: none), so a lane loads their alpha at the step's start.
+// (0xffff: none), so a lane loads their alpha at the step's start; the
+// forward's destinations are listed the same way in fhdr (per pair, per lane).
 //   forward code:  src index | dst index << 16 | last << 31
 //   backward code: dst index | src index << 16 | last << 31
 // (src in D(a), dst in D(b), both < 2^15).
-constexpr int kPullItems = 8;
+constexpr int kPullItemsMax = 8;
 struct PullTables {
+    int32_t items;           // nodes per lane at most: 4, 6 or 8 (the kernel's register queues)
     const int4* info;        // [(K + 1) K] per pair: forward base, forward T, backward base, backward T
+    const int4* fhdr;        // [(K + 1) K][64] each lane's destinations, 16 bits each (0xffff: none)
     const int32_t* fcode;    // forward entries
     const double* fw;        // their ew this evaluation (0: padding / empty node)
     const double* flw;       // their lw (rmin column; -inf: padding)

@@ -242,7 +242,8 @@ struct wfsa_dev {
     bool has_pull = false;
     bool w2_pull = false;           // this preparation runs wave_pull_kernel
     int64_t pl_nf = 0, pl_nb = 0;   // forward / backward entries
-    DevBuf<int4> pl_info, pl_bent;
+    DevBuf<int4> pl_info, pl_fhdr, pl_bent;
+    int32_t pl_items = 8;
     DevBuf<int32_t> pl_fcode, pl_g;   // pl_g: edge id per forward then per backward entry
     DevBuf<double> pl_w;              // [nf + nb + nf]: forward ew, backward ew, forward lw
     int w2_waves = 16;           // waves per block
@@ -479,7 +480,9 @@ wfsa::WideArgs wide_args(wfsa_dev* ctx) {
     a.pt.lw = ctx->pt_w.ptr + ctx->pt_ne;
     a.pt.max_n = ctx->pt_max_n;
     if (ctx->has_pull) {
+        a.pl.items = ctx->pl_items;
         a.pl.info = ctx->pl_info.ptr;
+        a.pl.fhdr = ctx->pl_fhdr.ptr;
         a.pl.fcode = ctx->pl_fcode.ptr;
         a.pl.bent = ctx->pl_bent.ptr;
         a.pl.fw = ctx->pl_w.ptr;
@@ -523,16 +526,22 @@ bool wide2_config(wfsa_dev* ctx) {
 // pairs' edge lists: per pair, the forward's items are the destinations of
 // D(b) with their in-edges, the backward's the sources of D(a) with their
 // out-edges (both in the lists' order); items dealt to the 64 lanes largest
-// first, each to the least loaded lane holding fewer than kPullItems.
-// Skipped (has_pull = false) when a D(b) exceeds 64 kPullItems nodes.
+// first, each to the least loaded lane holding fewer than `items` (4, 6 or
+// 8: the fewest that hold the largest D).  Skipped (has_pull = false) when a
+// D(b) exceeds 64 x 8 nodes.
 int build_pull_tables(wfsa_dev* ctx, int K, const std::vector<int32_t>& n, const std::vector<int32_t>& e_ptr,
                       const std::vector<int4>& ent) {
     ctx->has_pull = false;
     int32_t max_n = 0;
     for (int32_t v : n) max_n = std::max(max_n, v);
-    if (max_n > kWave * wfsa::kPullItems || max_n >= 32768) return WFSA_OK;
+    if (max_n > kWave * wfsa::kPullItemsMax || max_n >= 32768) return WFSA_OK;
+#ifdef WFSA_PULL_NI   // (layout-variant builds: make var)
+    const int NI = std::max(WFSA_PULL_NI, max_n <= 4 * kWave ? 4 : (max_n <= 6 * kWave ? 6 : 8));
+#else
+    const int NI = max_n <= 4 * kWave ? 4 : (max_n <= 6 * kWave ? 6 : 8);
+#endif
     const int64_t n_pairs = int64_t(K + 1) * K;
-    std::vector<int4> info(static_cast<size_t>(n_pairs));
+    std::vector<int4> info(static_cast<size_t>(n_pairs)), fhdr(static_cast<size_t>(n_pairs * kWave));
     std::vector<int32_t> fcode, fg, bg;
     std::vector<int4> bent;
     std::vector<std::vector<int32_t>> items;   // per node: its entries (indices into ent)
@@ -552,7 +561,7 @@ int build_pull_tables(wfsa_dev* ctx, int K, const std::vector<int32_t>& n, const
         for (int32_t it : order) {
             int best = -1;
             for (int l = 0; l < kWave; ++l)
-                if (cnt[size_t(l)] < wfsa::kPullItems && (best < 0 || load[size_t(l)] < load[size_t(best)])) best = l;
+                if (cnt[size_t(l)] < NI && (best < 0 || load[size_t(l)] < load[size_t(best)])) best = l;
             lane_items[size_t(best)].push_back(it);
             load[size_t(best)] += std::max<int64_t>(1, int64_t(items[size_t(it)].size()));
             ++cnt[size_t(best)];
@@ -570,6 +579,14 @@ int build_pull_tables(wfsa_dev* ctx, int K, const std::vector<int32_t>& n, const
             items.assign(size_t(nb), {});
             for (int32_t e = e0; e < e1; ++e) items[size_t(uint32_t(ent[size_t(e)].x) >> 16)].push_back(e);
             int64_t T = deal(nb);
+            for (int l = 0; l < kWave; ++l) {   // the lane's destinations
+                uint32_t sw[4] = {~0u, ~0u, ~0u, ~0u};
+                for (size_t k = 0; k < lane_items[size_t(l)].size(); ++k) {
+                    const uint32_t d = uint32_t(lane_items[size_t(l)][k]);
+                    sw[k >> 1] = (sw[k >> 1] & ~(0xffffu << (16 * (k & 1)))) | (d << (16 * (k & 1)));
+                }
+                fhdr[size_t(q * kWave + l)] = make_int4(int32_t(sw[0]), int32_t(sw[1]), int32_t(sw[2]), int32_t(sw[3]));
+            }
             const int64_t fbase = int64_t(fcode.size());
             fcode.resize(size_t(fbase + T * kWave), 0);
             fg.resize(size_t(fbase + T * kWave), -1);
@@ -641,6 +658,8 @@ int build_pull_tables(wfsa_dev* ctx, int K, const std::vector<int32_t>& n, const
     }
     hipStream_t s = ctx->stream;
     HIP_TRY(ctx->pl_info.upload(info.data(), info.size(), s));
+    HIP_TRY(ctx->pl_fhdr.upload(fhdr.data(), fhdr.size(), s));
+    ctx->pl_items = NI;
     HIP_TRY(ctx->pl_fcode.upload(fcode.data(), fcode.size(), s));
     HIP_TRY(ctx->pl_bent.upload(bent.data(), bent.size(), s));
     fg.insert(fg.end(), bg.begin(), bg.end());
@@ -1649,6 +1668,7 @@ int prepare(wfsa_dev* ctx, int level) {
     ctx->stats.fallback_strings = int64_t(fb[0].size() + fb[1].size() + fb[2].size());
     ctx->stats.tier2_strings = ctx->tier2_strings;
     ctx->stats.wave_strings = ctx->w2_grid > 0 ? ctx->w2_n : 0;
+    ctx->stats.wave_pull = ctx->w2_grid > 0 && ctx->w2_pull ? ctx->pl_items : 0;
     if (ctx->w2_grid == 0) ctx->stats.wave_row_entries = ctx->stats.wave_pair_edges = 0;
     ctx->stats.stream_words = words;
     ctx->stats.stream_bytes = chunks * 16;

@@ -47,7 +47,7 @@ class DevStats(C.Structure):
         ("dense_rows", i32), ("dense_steps", i32), ("dense_np", i32), ("tier2_strings", i32),
         ("wave_strings", i32), ("wave_row_entries", i64), ("wave_pair_edges", i64),
         ("comm_ranks", i32), ("comm_peer", i32),
-        ("slot_chunks", i64), ("max_group_chunks", i32), ("pad_", i32),
+        ("slot_chunks", i64), ("max_group_chunks", i32), ("wave_pull", i32),
     ]
 
 
