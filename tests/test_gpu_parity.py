@@ -328,15 +328,19 @@ def test_single_rank_communicator_path():
     np.testing.assert_allclose(comm.x(), plain.x(), rtol=1e-11, atol=1e-13)
 
 
-def test_popular_parameters_chunked_sums(capfd, monkeypatch):
-    """A small automaton under a large corpus: a constraint's bubble slots
+@pytest.mark.parametrize("merge", ["0", "1"])
+def test_popular_parameters_chunked_sums(capfd, monkeypatch, merge):
+    """A small automaton under a large corpus.  Without the wavefront merge of
+    same-parameter small-bubble slots (WFSA_SLOT_MERGE=0) a constraint's slots
     exceed what the fused QN step keeps in LDS (kMaxChunks x 16), so both its
-    sums and the host binding's reduction take the per-thread chunk path; the
-    device loop still equals the host QN steps, and the first gradient equals
-    the trellis oracle's."""
+    sums and the host binding's reduction take the per-thread chunk path; with
+    it (the default) the same bubbles collapse into a few slots per wavefront.
+    Either way the device loop equals the host QN steps and the first
+    gradient equals the trellis oracle's."""
     import wfsa_amd as W
     from oracle import TRELLIS, Oracle
     monkeypatch.setenv("WFSA_VERBOSE", "1")
+    monkeypatch.setenv("WFSA_SLOT_MERGE", merge)
     syn = W.Synthetic(n_states=4, degree=2, vocab=2, emissions=1, n_strings=30000, max_len=24, seed=2)
     sym, off, wt = syn.corpus()
     fsa = W.Fsa.read_text(syn.wfsa_text)
@@ -349,7 +353,10 @@ def test_popular_parameters_chunked_sums(capfd, monkeypatch):
     rows_a = a.Run(5, 1.0, -1.0)
     err = capfd.readouterr().err
     line = [ln for ln in err.splitlines() if "slots per constraint" in ln][-1]
-    assert int(line.split("max ")[1].split(",")[0]) > 16 * 1024, line
+    if merge == "0":
+        assert int(line.split("max ")[1].split(",")[0]) > 16 * 1024, line
+    else:
+        assert int(line.split("total ")[1].split(",")[0]) < 30000, line
     rows_b = [b.OptimizationStep(1.0, -1.0)[0] for _ in range(5)]
     for r, q in zip(rows_a, rows_b):
         for u, v in zip(r[:5], q[:5]):

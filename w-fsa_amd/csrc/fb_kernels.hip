@@ -2056,13 +2056,31 @@ __device__ __forceinline__ double small_bubble(const BubbleArgs& a, const int4* 
         for (int k = 0; k < N; ++k) B[k] = 0.0;
     }
     reg_add(B, nodes - 1, 1.0);
+    // lanes of an aligned 2^k group sharing edge e's parameter (slot field
+    // level k, layout_slots) sum their contributions by a butterfly -- every
+    // lane of the group gets the same bits, in a fixed order -- and the
+    // group's first lane stores the one slot; the partners of a grouped lane
+    // are active (their edge e exists), the rest ignore what they read
+    int kl = 0, kmax = 0;   // (ballots: over the active lanes only -- this runs inside the class branch)
+#pragma unroll
+    for (int e = 0; e < RE; ++e) kl = max(kl, slot[e] >= 0 ? (slot[e] >> 28) : 0);
+#pragma unroll
+    for (int t = 1; t <= 6; ++t) kmax = __ballot(kl >= t) ? t : kmax;
+    const int lane = lane_id();
 #pragma unroll
     for (int e = RE - 1; e >= 0; --e)
         if (e < edges) {
             const int src = sd[e] & 0xffff;
             const double bb = ew[e] * reg_get(B, sd[e] >> 16);
             reg_add(B, src, bb);
-            if (slot[e] >= 0 && !(WFSA_KDBG(a.dbg) & 1)) a.contrib[slot[e]] = reg_get(A, src) * bb * scale;
+            double v = reg_get(A, src) * bb * scale;
+            const int k = slot[e] >= 0 ? (slot[e] >> 28) : 0;
+            for (int d = 1; d < (1 << kmax); d <<= 1) {
+                const double t = __shfl_xor(v, d, kWave);
+                if (d < (1 << k)) v += t;
+            }
+            if (slot[e] >= 0 && (lane & ((1 << k) - 1)) == 0 && !(WFSA_KDBG(a.dbg) & 1))
+                a.contrib[slot[e] & 0x0fffffff] = v;
         }
     const double lz = log(Z);
     if (a.logq) global_add(&a.logq[q[0].y], lz);

@@ -996,11 +996,47 @@ int layout_slots(wfsa_dev* ctx, const std::vector<int32_t>& pos_of) {
     };
     std::vector<int32_t> param_at(size_t(std::max(np, 1)), 0);
     for (int32_t j = 0; j < np; ++j) param_at[size_t(pos_of[size_t(j)])] = j;
+    // Small bubbles run one per lane, 64 consecutive list entries (class A
+    // then class B) per wavefront, sorted by shape: where an aligned group of
+    // 2^k lanes of one class all carry parameter j on edge e, the lanes sum
+    // their contributions by a butterfly and the group's first lane stores
+    // one slot (fb_kernels.hip small_bubble); lvl[b * 8 + e] = k
+    const int64_t n4 = int64_t(ctx->h_sm4_list.size()), nsm = n4 + int64_t(ctx->h_sm_list.size());
+    auto small_o = [&](int64_t b) { return b < n4 ? ctx->h_sm4_list[size_t(b)] : ctx->h_sm_list[size_t(b - n4)]; };
+    auto small_code = [&](int64_t b, int e) -> int32_t {   // its parameter on edge e, or -1
+        const int32_t o = small_o(b);
+        if (e >= (bb[size_t(o)] >> 16)) return -1;
+        const int32_t c = edge_code_at(o, e);
+        return c >= 0 && c < np ? c : -1;
+    };
+    std::vector<uint8_t> lvl(size_t(std::max<int64_t>(nsm, 1)) * 8, 0);
+    const bool merge = [] {   // WFSA_SLOT_MERGE=0: a slot per small-bubble edge (read at each layout)
+        const char* e = std::getenv("WFSA_SLOT_MERGE");
+        return !(e && e[0] == '0');
+    }();
+    for (int64_t g0 = 0; merge && g0 < nsm; g0 += kWave)
+        for (int e = 0; e < wfsa::kBubbleRegEdges; ++e)
+            for (int k = 6; k >= 1; --k) {   // largest aligned groups first
+                const int64_t G = int64_t(1) << k;
+                for (int64_t b0 = g0; b0 + G <= std::min(g0 + kWave, nsm); b0 += G) {
+                    if (lvl[size_t(b0) * 8 + size_t(e)]) continue;   // inside a larger group
+                    const int32_t c = small_code(b0, e);
+                    bool same = c >= 0 && (b0 < n4) == (b0 + G - 1 < n4);
+                    for (int64_t b = b0 + 1; same && b < b0 + G; ++b) same = small_code(b, e) == c && !lvl[size_t(b) * 8 + size_t(e)];
+                    if (same)
+                        for (int64_t b = b0; b < b0 + G; ++b) lvl[size_t(b) * 8 + size_t(e)] = uint8_t(k);
+                }
+            }
+    auto leader = [&](int64_t b, int e) { return (b & ((int64_t(1) << lvl[size_t(b) * 8 + size_t(e)]) - 1)) == 0; };
     std::vector<int32_t> pc(size_t(np) + 1, 0);   // by position
-    for (const auto* list : {&ctx->h_sm4_list, &ctx->h_sm_list, &ctx->h_big_list})
-        for (int32_t o : *list)
-            for (int e = 0; e < (bb[size_t(o)] >> 16); ++e)
-                for_edge_params(edge_code_at(o, e), [&](int32_t jj) { pc[size_t(pos_of[size_t(jj)]) + 1]++; });
+    for (int64_t b = 0; b < nsm; ++b)
+        for (int e = 0; e < wfsa::kBubbleRegEdges; ++e) {
+            const int32_t c = small_code(b, e);
+            if (c >= 0 && leader(b, e)) pc[size_t(pos_of[size_t(c)]) + 1]++;
+        }
+    for (int32_t o : ctx->h_big_list)
+        for (int e = 0; e < (bb[size_t(o)] >> 16); ++e)
+            for_edge_params(edge_code_at(o, e), [&](int32_t jj) { pc[size_t(pos_of[size_t(jj)]) + 1]++; });
     for (size_t q = 1; q < pc.size(); ++q) pc[q] += pc[q - 1];
     std::vector<int32_t> fill(pc.begin(), pc.end() - 1);
     // Reduction groups over the positions: the QN constraints when the slots
@@ -1035,10 +1071,22 @@ int layout_slots(wfsa_dev* ctx, const std::vector<int32_t>& pos_of) {
         const int32_t i = sl - pc[size_t(pos)];
         return int32_t(gbase[size_t(g)] + int64_t(cptr_pos[size_t(pos)] - cg) * wfsa::kSlotChunk + i);
     };
-    if (gbase.back() >= int64_t(INT32_MAX)) return fail(WFSA_ERR_CAPACITY, "too many bubble contribution slots");
+    if (gbase.back() >= int64_t(1) << 28) return fail(WFSA_ERR_CAPACITY, "too many bubble contribution slots");
     if (ctx->n_bubbles > 0) {
+        // the small bubbles' slot fields: slot | group level << 28 (every lane
+        // of a group carries the group's slot; its first lane stores)
+        std::vector<int32_t> sfield(size_t(std::max<int64_t>(nsm, 1)) * 8, -1);
+        for (int64_t b = 0; b < nsm; ++b)
+            for (int e = 0; e < wfsa::kBubbleRegEdges; ++e) {
+                const int32_t c = small_code(b, e);
+                if (c < 0 || !leader(b, e)) continue;
+                const int32_t pos = pos_of[size_t(c)];
+                const int k = lvl[size_t(b) * 8 + size_t(e)];
+                const int32_t f = phys(pos, fill[size_t(pos)]++) | (int32_t(k) << 28);
+                for (int64_t q = b; q < b + (int64_t(1) << k); ++q) sfield[size_t(q) * 8 + size_t(e)] = f;
+            }
         // class tables: RE edges, quads = 1 + RE/2 + RE/4
-        auto build_table = [&](const std::vector<int32_t>& list, int RE, std::vector<int32_t>& tbl) {
+        auto build_table = [&](const std::vector<int32_t>& list, int RE, std::vector<int32_t>& tbl, int64_t b_first) {
             const int Q = 1 + RE / 2 + RE / 4;
             const size_t n = list.size();
             tbl.assign(size_t(Q) * 4 * std::max<size_t>(n, 1), 0);
@@ -1052,10 +1100,7 @@ int layout_slots(wfsa_dev* ctx, const std::vector<int32_t>& pos_of) {
                     if (e < edges) {
                         code = edge_code_at(o, e);
                         sd = bb[size_t(o) + 5 + 2 * size_t(e)];
-                        if (code < np) {
-                            const int32_t pos = pos_of[size_t(code)];
-                            sl = phys(pos, fill[size_t(pos)]++);
-                        }
+                        sl = sfield[size_t(b_first + int64_t(b)) * 8 + size_t(e)];
                     }
                     quad(1 + e / 2, b)[2 * (e & 1)] = code;
                     quad(1 + e / 2, b)[2 * (e & 1) + 1] = sd;
@@ -1064,8 +1109,8 @@ int layout_slots(wfsa_dev* ctx, const std::vector<int32_t>& pos_of) {
             }
         };
         std::vector<int32_t> tbl4, tbl;
-        build_table(ctx->h_sm4_list, 4, tbl4);
-        build_table(ctx->h_sm_list, wfsa::kBubbleRegEdges, tbl);
+        build_table(ctx->h_sm4_list, 4, tbl4, 0);
+        build_table(ctx->h_sm_list, wfsa::kBubbleRegEdges, tbl, n4);
         const int64_t nb = int64_t(ctx->h_big_list.size());
         std::vector<int32_t> big_edge_base(size_t(std::max<int64_t>(nb, 1)), 0), eslot_ptr(1, 0), eslot;
         for (int64_t i = 0; i < nb; ++i) {
