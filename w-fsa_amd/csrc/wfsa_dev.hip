@@ -3083,7 +3083,7 @@ int wfsa_dev_qn_run(wfsa_dev* ctx, double eta, double tol, int32_t max_steps, do
     static const bool trace = std::getenv("WFSA_RUN_TRACE") != nullptr;
     const auto tr0 = clk::now();
     auto tr_ms = [&](clk::time_point t) { return std::chrono::duration<double, std::micro>(t - tr0).count(); };
-    clk::time_point tr_pro{}, tr_first{}, tr_last{}, tr_end{};
+    clk::time_point tr_pro{}, tr_first{}, tr_last{}, tr_end{}, tr_enq1{};
     if (ctx->prep_level < 2)
         if (int rc = prepare(ctx, 2)) return rc;
     if (int rc = collect_timing(ctx)) return rc;
@@ -3148,6 +3148,7 @@ int wfsa_dev_qn_run(wfsa_dev* ctx, double eta, double tol, int32_t max_steps, do
                 return rc;
             ++enq;
             ++ctx->seq;
+            if (trace && enq == 1) tr_enq1 = clk::now();
         }
         if (stop || enq == max_steps)   // no next step will carry the last one's finish
             if (int rc = flush_qn_finish(ctx)) return rc;
@@ -3160,7 +3161,11 @@ int wfsa_dev_qn_run(wfsa_dev* ctx, double eta, double tol, int32_t max_steps, do
         if (ctx->kernel_timing && timed_step(done)) {
             float c = 0.f, f = 0.f;
             const hipEvent_t end = ctx->k2_kc[slot] ? ctx->kc[slot] : ctx->k2[slot];
-            if (hipEventSynchronize(end) == hipSuccess &&
+            // (complete by now: the row was published by a later kernel; a
+            // query, not a synchronize, which may sleep the thread for a wake-up)
+            hipError_t q;
+            while ((q = hipEventQuery(end)) == hipErrorNotReady) __builtin_ia32_pause();
+            if (q == hipSuccess &&
                 hipEventElapsedTime(&c, ctx->k0[slot], ctx->kc[slot]) == hipSuccess &&
                 hipEventElapsedTime(&f, ctx->k0[slot], end) == hipSuccess) {
                 c_ms_sum += c;
@@ -3201,8 +3206,10 @@ int wfsa_dev_qn_run(wfsa_dev* ctx, double eta, double tol, int32_t max_steps, do
     }
     if (trace) {
         tr_end = clk::now();
-        std::fprintf(stderr, "[wfsa] qn_run %d steps: prologue %.1f us, first row %.1f, last row %.1f, end %.1f\n",
-                     done, tr_ms(tr_pro), tr_ms(tr_first), done > 1 ? tr_ms(tr_last) : tr_ms(tr_first), tr_ms(tr_end));
+        std::fprintf(stderr, "[wfsa] qn_run %d steps: prologue %.1f us, first step enqueued %.1f, first row %.1f, "
+                     "last row %.1f, end %.1f (start at %lld ns)\n",
+                     done, tr_ms(tr_pro), tr_ms(tr_enq1), tr_ms(tr_first), done > 1 ? tr_ms(tr_last) : tr_ms(tr_first),
+                     tr_ms(tr_end), (long long)std::chrono::duration_cast<std::chrono::nanoseconds>(tr0.time_since_epoch()).count());
     }
     ctx->qn_flags_clear = st == 0;
     ctx->stats.fb_launches += timed;
