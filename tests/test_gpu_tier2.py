@@ -85,3 +85,38 @@ def test_tier2_path_counts_match_enumeration(monkeypatch):
     np.testing.assert_array_equal(pc, o.path_counts().astype(np.float64))
     oused = {n for n, t in zip(o.full_param_names(), o.trimmed_index()) if t != -2}
     assert {n for n, u in zip(names, used) if u} == oused
+
+
+@pytest.mark.parametrize("family", [
+    dict(n_states=256, degree=8, vocab=16, emissions=4, n_strings=600, max_len=48),    # D up to ~80: 4 nodes/lane
+    dict(n_states=1024, degree=8, vocab=16, emissions=4, n_strings=300, max_len=40),   # famB shape: 6 nodes/lane
+])
+def test_wave_pull_equals_push_and_repeats(family, monkeypatch):
+    """the traversal strings' pull kernel (wave_pull_kernel, the default) and
+    round 2's push kernel (wide2_kernel, WFSA_PULL=0) give the same log q,
+    log-likelihood and gradient; the pull kernel's evaluation repeats bit for
+    bit (fixed-order node sums, fixed-point gradient)"""
+    import wfsa_amd as W
+    syn = W.Synthetic(seed=23, **family)
+    sym, off, wt = syn.corpus()
+    p = wt / wt.sum()
+    names = W.Fsa.read_text(syn.wfsa_text).param_names()
+    w = np.random.default_rng(8).normal(-1.4, 0.4, size=len(names))
+    monkeypatch.setenv("WFSA_PULL", "0")
+    *_, llp, gp, lqp, stp = _eval(syn.wfsa_text, sym, off, p, w, monkeypatch, False)
+    assert stp["wave_strings"] > 0 and stp["wave_pull"] == 0
+    monkeypatch.setenv("WFSA_PULL", "1")
+    import wfsa_amd as W2
+    fsa = W2.Fsa.read_text(syn.wfsa_text)
+    dev = W2.Device(0)
+    dev.load_model(fsa)
+    dev.load_corpus(sym, off, p)
+    dev.recognize()
+    ll1, g1, lq1 = dev.objective_grad(w)
+    ll2, g2, lq2 = dev.objective_grad(w)
+    st = dev.stats()
+    assert st["wave_strings"] == stp["wave_strings"] and st["wave_pull"] in (4, 6, 8)
+    assert ll1 == ll2 and np.array_equal(g1, g2) and np.array_equal(lq1, lq2)
+    np.testing.assert_allclose(lq1, lqp, rtol=1e-12)
+    assert _close(ll1, llp, rel=1e-12)
+    np.testing.assert_allclose(g1, gp, rtol=1e-10, atol=1e-16)

@@ -1107,7 +1107,7 @@ __global__ __launch_bounds__(kWide2Block) void wide2_kernel(WideArgs a) {
 // lists each lane's sources).  Scaling, alpha history, fixed-point
 // gradient / log-likelihood and the last block's conversion as wide2_kernel.
 #ifndef WFSA_PULL_UF
-#define WFSA_PULL_UF 4   // forward entries per lane in flight
+#define WFSA_PULL_UF 8   // forward entries per lane in flight
 #endif
 #ifndef WFSA_PULL_UB
 #define WFSA_PULL_UB 2   // backward entries per lane in flight
@@ -1119,7 +1119,7 @@ __global__ __launch_bounds__(kWide2Block) void wide2_kernel(WideArgs a) {
 #endif
 template <int NI, bool TRACK>
 __global__ __launch_bounds__(kWide2Block) void wave_pull_kernel(WideArgs a) {
-    constexpr int kUF = WFSA_PULL_UF, kUB = WFSA_PULL_UB;
+    constexpr int kUF = TRACK && WFSA_PULL_UF > 4 ? 4 : WFSA_PULL_UF, kUB = WFSA_PULL_UB;   // (the min forward's registers)
     if (a.halted && *a.halted) return;
     extern __shared__ __attribute__((aligned(16))) double lds2[];
     __shared__ int last_block;
@@ -1345,6 +1345,8 @@ __global__ __launch_bounds__(kWide2Block) void wave_pull_kernel(WideArgs a) {
         }
         wave_sync();
         int ex_next = exi, vex = 0;
+        int4 sl_next = make_int4(-1, -1, -1, -1);   // the next (lower) step's source list, loaded a step early
+        bool have_next = false;
         for (int i = L - 1; i >= 0; --i) {
             if (i == L - 1 || (i & (kWave - 1)) == kWave - 1) {   // this step's chunk (steps and row exponents)
                 load_chunk(i / kWave);
@@ -1361,7 +1363,13 @@ __global__ __launch_bounds__(kWide2Block) void wave_pull_kernel(WideArgs a) {
             double acc[NI], av[NI];
             int dd[NI];
             {   // alpha of the lane's sources, in its item order (row 0 of the pair's entries)
-                const int4 sl = Q.bent[int64_t(bb) + lane];
+                const int4 sl = have_next ? sl_next : Q.bent[int64_t(bb) + lane];
+#ifdef WFSA_PULL_NOPF   // (layout-variant builds: no prefetch)
+                have_next = false;
+#else
+                have_next = (ii & (kWave - 1)) != 0;   // step i - 1 in this chunk of step registers
+#endif
+                if (have_next) sl_next = Q.bent[int64_t(__builtin_amdgcn_readlane(vbb, ii - 1)) + lane];
                 const unsigned sw[4] = {unsigned(sl.x), unsigned(sl.y), unsigned(sl.z), unsigned(sl.w)};
 #pragma unroll
                 for (int k = 0; k < NI; ++k) {
