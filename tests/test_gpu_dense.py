@@ -372,3 +372,97 @@ def test_dense_evaluation_is_bitwise_reproducible(monkeypatch):
     assert ll1 == ll2
     np.testing.assert_array_equal(g1, g2)
     np.testing.assert_array_equal(lq1, lq2)
+
+
+def _dense_min_rpp(A, E, start, end, s, logq):
+    """the string's smallest relative path probability: a (min, +) forward
+    in the log domain (missing edges +inf) over the same model"""
+    with np.errstate(divide="ignore"):
+        lA = np.where(A > 0, np.log(np.where(A > 0, A, 1.0)), np.inf)
+        lE = np.where(E > 0, np.log(np.where(E > 0, E, 1.0)), np.inf)
+    m = lA[start] + lE[:, s[0]]
+    for c in s[1:]:
+        m = np.min(m[:, None] + lA, axis=0) + lE[:, c]
+    return float(np.exp(np.min(m + lA[:, end]) - logq))
+
+
+def test_dense_rmin_matches_path_enumeration(monkeypatch):
+    """the rmin info column on the dense path (its (min, +) trellis) against
+    the oracle's enumerated paths (src/QuasiNewtonLearner.cpp:80-84, the
+    reference's idamin over relative_path_probs), a 5-state model forced
+    dense: value and the string holding the path"""
+    from test_gpu_rmin import _check, _setup
+    import wfsa_amd as W
+    syn = W.Synthetic(n_states=5, degree=1, vocab=3, emissions=2, dense=True, n_strings=60, max_len=5, seed=9)
+    sym, off, wt = syn.corpus()
+    monkeypatch.setenv("WFSA_DENSE", "1")
+    o, h, dev = _setup(syn.wfsa_text, sym, off, wt, monkeypatch)
+    assert dev.stats()["dense"] == 1
+    _check(o, h, dev, seed=3)
+
+
+def test_dense_rmin_equals_sparse_kernels(monkeypatch):
+    """same model and strings: the dense path's rmin equals the trellis
+    kernels' (min, x) passes (traversal tiers), value and string"""
+    import wfsa_amd as W
+    syn = W.Synthetic(n_states=16, degree=1, vocab=6, emissions=2, dense=True, n_strings=400, max_len=9, seed=4)
+    sym, off, wt = syn.corpus()
+    fsa = W.Fsa.read_text(syn.wfsa_text)
+    names = fsa.param_names()
+    p = wt / wt.sum()
+    sp = _device(fsa, sym, off, p, monkeypatch, dense=False)
+    dn = _device(fsa, sym, off, p, monkeypatch, dense=True)
+    rec, _, _ = dn.recognize()
+    assert rec.all()
+    with pytest.raises(Exception):   # structural pass only: no weights yet
+        dn.rmin()
+    rng = np.random.default_rng(6)
+    for _ in range(3):
+        w = rng.normal(-0.8, 0.6, size=len(names))
+        sp.objective_grad(w)
+        dn.objective_grad(w)
+        (rs, ss), (rd, sd) = sp.rmin(), dn.rmin()
+        assert _close(rd, rs, rel=1e-12) and 0.0 < rd < 1.0
+        assert sd == ss
+
+
+def test_dense_rmin_two_column_tiles_against_numpy(monkeypatch):
+    """200 states (np 256: two column tiles, padded states), ragged row
+    slots: the device's rmin equals a numpy (min, +) restatement per string"""
+    import wfsa_amd as W
+    syn = W.Synthetic(n_states=200, degree=1, vocab=5, emissions=2, dense=True, n_strings=300, max_len=40, seed=12)
+    sym, off, wt = syn.corpus()
+    fsa = W.Fsa.read_text(syn.wfsa_text)
+    p = wt / wt.sum()
+    dev = _device(fsa, sym, off, p, monkeypatch, dense=True)
+    dev.recognize()
+    w = np.random.default_rng(8).normal(-1.5, 0.9, size=len(fsa.param_names()))
+    _, _, logq = dev.objective_grad(w)
+    r, s = dev.rmin()
+    A, E, start, end, _ = _dense_tables(fsa, w)
+    want = np.array([_dense_min_rpp(A, E, start, end, sym[off[i]:off[i + 1]], logq[i]) for i in range(len(wt))])
+    i = int(np.argmin(want))
+    assert _close(r, want[i], rel=1e-11)
+    assert s == i or _close(want[s], want[i], rel=1e-11)
+
+
+def test_dense_rmin_column_in_quasinewton_device_loop(monkeypatch):
+    """QuasiNewtonLearner with the rmin column on: the dense path's device
+    loop fills columns 5/6 as the trellis kernels' loop does"""
+    import wfsa_amd as W
+    syn = W.Synthetic(n_states=16, degree=1, vocab=8, emissions=2, dense=True, n_strings=300, max_len=9, seed=21)
+    sym, off, wt = syn.corpus()
+    fsa = W.Fsa.read_text(syn.wfsa_text)
+    rows = {}
+    for dense in (False, True):
+        monkeypatch.setenv("WFSA_DENSE", "1" if dense else "0")
+        lrn = W.QuasiNewtonLearner(0)
+        lrn.set_info_rmin(True)
+        lrn.BuildFromPacked(fsa, sym, off, wt)
+        lrn.Finalize()
+        lrn.Init(7)
+        assert lrn.stats()["dense"] == (1 if dense else 0)
+        rows[dense] = np.array([lrn.OptimizationStep(1.0, -1.0)[0] for _ in range(2)] + lrn.Run(4, 1.0, -1.0))
+    assert (rows[True][:, 6] >= 0).all() and (rows[True][:, 5] < 1.0).all()
+    np.testing.assert_allclose(rows[True][:, 5], rows[False][:, 5], rtol=1e-9)
+    np.testing.assert_array_equal(rows[True][:, 6], rows[False][:, 6])

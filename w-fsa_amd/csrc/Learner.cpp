@@ -392,9 +392,7 @@ bool Learner::SaveMatrices(const std::string& prefix) const {   // src/Learner.c
 
 bool Learner::RminAvailable() const {
     if (!info_rmin || unique_paths || !dev) return false;
-    wfsa_dev_stats st{};
-    if (wfsa_dev_get_stats(dev, &st) != WFSA_OK) return false;
-    return !st.dense;
+    return true;   // every tier, the dense path included (its (min, +) trellis)
 }
 
 void Learner::ComputeRmin(double* out) const {

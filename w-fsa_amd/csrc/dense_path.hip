@@ -622,6 +622,196 @@ __global__ __launch_bounds__(256) void dense_grad_scatter_kernel(const double* _
     }
 }
 
+// ---- the rmin info column: a (min, +) trellis in the log domain ----------
+//
+// m_1[T] = log a[T] + log E[T][c_0],  m_{j+1}[T] = min_S (m_j[S] + log A[S][T])
+// + log E[T][c_j], and the string's smallest path weight is min_T (m_L[T] +
+// log e[T]); its relative probability divides by q (log q from the
+// evaluation).  Missing edges are +inf, so they never win a minimum.
+
+// log tables of the evaluation's exp-weight tables (+inf where the weight is 0)
+__global__ __launch_bounds__(256) void dense_log_kernel(const double* __restrict__ amat, const double* __restrict__ et,
+                                                        const double* __restrict__ a0, const double* __restrict__ aend,
+                                                        double* lmat, double* let, double* l0, double* lend,
+                                                        int64_t n_a, int64_t n_e, int32_t np, const unsigned* halted) {
+    if (halted && *halted) return;
+    const int64_t n = n_a + n_e + 2 * int64_t(np);
+    for (int64_t i = int64_t(blockIdx.x) * 256 + threadIdx.x; i < n; i += int64_t(gridDim.x) * 256) {
+        const double* src;
+        double* dst;
+        int64_t j = i;
+        if (j < n_a) { src = amat; dst = lmat; }
+        else if ((j -= n_a) < n_e) { src = et; dst = let; }
+        else if ((j -= n_e) < np) { src = a0; dst = l0; }
+        else { j -= np; src = aend; dst = lend; }
+        const double v = src[j];
+        dst[j] = v > 0.0 ? log(v) : INFINITY;
+    }
+}
+
+struct MinPlusArgs {
+    const double* x;        // [R][np] the previous step's log minima (unused at step 0)
+    const double* lmat;     // [np][np]
+    const double* let;      // [vocab+1][np]
+    const double* l0;       // [np]
+    const double* lend;     // [np]
+    const int32_t* meta;    // [R] this step
+    const int32_t* sid;     // [R] this step
+    double* y;              // [R][np] this step's log minima
+    double* spart;          // [nct][S] per column tile: a string's end minimum
+    int64_t n_strings;
+    int32_t np, vocab;
+    const unsigned* halted;
+};
+
+constexpr int kMpK = 16;   // K slice of the min-plus tile
+
+// One step of the (min, +) trellis for all R row slots: y = (x (min,+) lA)
+// + lE[sym] on a 128 x 128 tile per block (256 threads, 8 x 8 per thread at
+// stride 16: the LDS reads of a slice broadcast within each 16-lane row
+// group), K staged through LDS in slices of 16 with the next slice's global
+// loads in registers during the current one's arithmetic.  Rows that start a
+// string take log a + lE instead; rows that end one reduce min_T (y + log e)
+// over the tile's columns into spart.
+template <bool FIRST>
+__global__ __launch_bounds__(256) void dense_minplus_kernel(MinPlusArgs a) {
+    if (a.halted && *a.halted) return;
+    __shared__ double xs[kMpK][kT + 1];   // [k][row]
+    __shared__ double ls[kMpK][kT];       // [k][column]
+    const int tid = int(threadIdx.x), tx = tid & 15, ty = tid >> 4;
+    const int c0 = int(blockIdx.x) * kT, r0 = int(blockIdx.y) * kT;
+    const size_t np = size_t(a.np);
+    double acc[8][8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) acc[i][j] = INFINITY;
+    if (!FIRST) {
+        // loaders: x row tid/2, k half (tid&1)*8; lA k row tid/16, columns (tid&15)*8
+        const int xr = tid >> 1, xk = (tid & 1) * 8, lk = tid >> 4, lc = (tid & 15) * 8;
+        const double2* xp = reinterpret_cast<const double2*>(a.x + size_t(r0 + xr) * np + size_t(xk));
+        const double2* lp = reinterpret_cast<const double2*>(a.lmat + size_t(lk) * np + size_t(c0 + lc));
+        const size_t lstep = kMpK * np / 2;   // double2 per K slice of lA
+        double2 xv[4], lv[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            xv[q] = xp[q];
+            lv[q] = lp[q];
+        }
+        for (int k0 = 0; k0 < a.np; k0 += kMpK) {
+            __syncthreads();   // the previous slice's reads are done
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                xs[xk + 2 * q][xr] = xv[q].x;
+                xs[xk + 2 * q + 1][xr] = xv[q].y;
+                ls[lk][lc + 2 * q] = lv[q].x;
+                ls[lk][lc + 2 * q + 1] = lv[q].y;
+            }
+            __syncthreads();
+            if (k0 + kMpK < a.np) {
+                xp += kMpK / 2;
+                lp += lstep;
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    xv[q] = xp[q];
+                    lv[q] = lp[q];
+                }
+            }
+#pragma unroll 4
+            for (int kk = 0; kk < kMpK; ++kk) {
+                double xa[8], lb[8];
+#pragma unroll
+                for (int i = 0; i < 8; ++i) xa[i] = xs[kk][ty + 16 * i];
+#pragma unroll
+                for (int j = 0; j < 8; ++j) lb[j] = ls[kk][tx + 16 * j];
+#pragma unroll
+                for (int i = 0; i < 8; ++i)
+#pragma unroll
+                    for (int j = 0; j < 8; ++j) acc[i][j] = fmin(acc[i][j], xa[i] + lb[j]);
+            }
+        }
+    }
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        const int r = r0 + ty + 16 * i;
+        const int32_t m = a.meta[r];
+        const int sym = m & 0x1ff;
+        const bool idle = sym >= a.vocab, start = (m >> 9) & 1, end = (m >> 10) & 1;
+        double endmin = INFINITY;
+        double* yr = a.y + size_t(r) * np;
+        const double* le = a.let + size_t(idle ? a.vocab : sym) * np;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const int T = c0 + tx + 16 * j;
+            const double v = idle ? INFINITY : ((start || FIRST) ? a.l0[T] : acc[i][j]) + le[T];
+            yr[T] = v;
+            endmin = fmin(endmin, v + a.lend[T]);
+        }
+        // the 16 lanes of this row (one row group of the wavefront)
+#pragma unroll
+        for (int o = 8; o >= 1; o >>= 1) endmin = fmin(endmin, __shfl_xor(endmin, o, 64));
+        if (end && !idle && tx == 0) a.spart[size_t(blockIdx.x) * size_t(a.n_strings) + size_t(a.sid[r])] = endmin;
+    }
+}
+
+__device__ __forceinline__ void dense_min_pair(double& v, double& i, double v2, double i2) {
+    if (v2 < v || (v2 == v && i2 < i)) {
+        v = v2;
+        i = i2;
+    }
+}
+
+// per string: log(min path / q) = min over column tiles - log q; block minima
+// (value, string), ties to the lower string
+__global__ __launch_bounds__(256) void dense_rmin_strings_kernel(const double* __restrict__ spart, int32_t nct,
+                                                                 const int32_t* __restrict__ end_at,
+                                                                 const double* __restrict__ logq, int64_t n_strings,
+                                                                 double* rpart, const unsigned* halted) {
+    if (halted && *halted) return;
+    __shared__ double wv[4], wi[4];
+    const int64_t s = int64_t(blockIdx.x) * 256 + threadIdx.x;
+    double v = INFINITY, idx = -1.0;
+    if (s < n_strings && end_at[s] >= 0) {
+        double m = INFINITY;
+        for (int c = 0; c < nct; ++c) m = fmin(m, spart[size_t(c) * size_t(n_strings) + size_t(s)]);
+        v = m - logq[s];
+        idx = double(s);
+    }
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) dense_min_pair(v, idx, __shfl_xor(v, o, 64), __shfl_xor(idx, o, 64));
+    if ((threadIdx.x & 63) == 0) {
+        wv[threadIdx.x >> 6] = v;
+        wi[threadIdx.x >> 6] = idx;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        for (int k = 1; k < 4; ++k) dense_min_pair(v, idx, wv[k], wi[k]);
+        rpart[2 * blockIdx.x] = v;
+        rpart[2 * blockIdx.x + 1] = idx;
+    }
+}
+
+// the block minima -> res = (exp(value), string), (0, -1) without a string
+__global__ __launch_bounds__(256) void dense_rmin_final_kernel(const double* __restrict__ rpart, int n_part, double* res,
+                                                               const unsigned* halted) {
+    if (halted && *halted) return;
+    __shared__ double wv[4], wi[4];
+    double v = INFINITY, idx = -1.0;
+    for (int k = int(threadIdx.x); k < n_part; k += 256) dense_min_pair(v, idx, rpart[2 * k], rpart[2 * k + 1]);
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) dense_min_pair(v, idx, __shfl_xor(v, o, 64), __shfl_xor(idx, o, 64));
+    if ((threadIdx.x & 63) == 0) {
+        wv[threadIdx.x >> 6] = v;
+        wi[threadIdx.x >> 6] = idx;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        for (int k = 1; k < 4; ++k) dense_min_pair(v, idx, wv[k], wi[k]);
+        res[0] = idx >= 0.0 ? exp(v) : 0.0;
+        res[1] = idx;
+    }
+}
+
 template <typename T>
 hipError_t dalloc(T*& p, size_t n) {
     if (p) (void)hipFree(p);
@@ -730,8 +920,10 @@ void DensePath::free_corpus() {
     dfree(meta_); dfree(sid_); dfree(end_at_); dfree(p_); dfree(pones_); dfree(logq_);
     dfree(la_); dfree(lb_); dfree(alpha_); dfree(gam_); dfree(z_); dfree(y_); dfree(part_);
     dfree(ll_part_); dfree(red_);
+    dfree(lmat_); dfree(let_); dfree(l0_); dfree(lend_); dfree(mrow_); dfree(spart_); dfree(rpart_);
     n_strings_ = 0;
     R_ = T_ = 0;
+    weighted_ = false;
 }
 
 hipError_t DensePath::load_model(const DenseModel& m, hipStream_t s) {
@@ -893,6 +1085,7 @@ hipError_t DensePath::enqueue(const double* ewp, bool structural, double* out, d
     const size_t np = size_t(np_), R = size_t(R_);
     const double* w = structural ? ones_ : ewp;
     const double* p = structural ? pones_ : p_;
+    weighted_ = !structural;
     if (use_blas_ && blas_ && n_strings_ > 0 && total_sym_ > 0) return enqueue_blas(w, p, structural, out, logq, halted, s);
     {
         WeightsArgs a{};
@@ -1131,6 +1324,51 @@ hipError_t DensePath::enqueue_blas(const double* w, const double* p, bool struct
         DTRY(hipGetLastError());
     }
     return hipSuccess;
+}
+
+hipError_t DensePath::enqueue_rmin(double* res, const unsigned* halted, hipStream_t s) {
+    const size_t np = size_t(np_), R = size_t(R_), S = size_t(std::max<int64_t>(n_strings_, 1));
+    const int nb = int((S + 255) / 256);
+    if (!lmat_) {   // first call: the pass's buffers
+        DTRY(dalloc(lmat_, np * np));
+        DTRY(dalloc(let_, size_t(vocab_ + 1) * np));
+        DTRY(dalloc(l0_, np));
+        DTRY(dalloc(lend_, np));
+    }
+    if (!mrow_ && R > 0) {
+        DTRY(dalloc(mrow_, 2 * R * np));
+        DTRY(dalloc(spart_, size_t(nct_) * S));
+        DTRY(dalloc(rpart_, 2 * size_t(nb)));
+    }
+    if (n_strings_ == 0 || total_sym_ == 0 || R == 0) {   // no string with a path of positive length
+        static const double none[2] = {0.0, -1.0};
+        return hipMemcpyAsync(res, none, sizeof none, hipMemcpyHostToDevice, s);
+    }
+    dense_log_kernel<<<1024, 256, 0, s>>>(amat_, et_, a0_, aend_, lmat_, let_, l0_, lend_, int64_t(np * np),
+                                          int64_t(size_t(vocab_ + 1) * np), np_, halted);
+    DTRY(hipGetLastError());
+    MinPlusArgs g{};
+    g.lmat = lmat_; g.let = let_; g.l0 = l0_; g.lend = lend_;
+    g.spart = spart_;
+    g.n_strings = n_strings_;
+    g.np = np_;
+    g.vocab = vocab_;
+    g.halted = halted;
+    const dim3 grid(unsigned(np / kT), unsigned(R / kT));
+    for (int64_t t = 0; t < T_; ++t) {
+        MinPlusArgs f = g;
+        f.x = mrow_ + size_t((t + 1) & 1) * R * np;
+        f.y = mrow_ + size_t(t & 1) * R * np;
+        f.meta = meta_ + size_t(t) * R;
+        f.sid = sid_ + size_t(t) * R;
+        if (t == 0) dense_minplus_kernel<true><<<grid, 256, 0, s>>>(f);
+        else dense_minplus_kernel<false><<<grid, 256, 0, s>>>(f);
+        DTRY(hipGetLastError());
+    }
+    dense_rmin_strings_kernel<<<unsigned(nb), 256, 0, s>>>(spart_, nct_, end_at_, logq_, n_strings_, rpart_, halted);
+    DTRY(hipGetLastError());
+    dense_rmin_final_kernel<<<1, 256, 0, s>>>(rpart_, nb, res, halted);
+    return hipGetLastError();
 }
 
 }  // namespace wfsa

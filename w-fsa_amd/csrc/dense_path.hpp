@@ -75,7 +75,17 @@ public:
     // parameters, wfsa_dev_recognize).  halted (nullable): nonzero = skip.
     hipError_t enqueue(const double* ewp, bool structural, double* out, double* logq, const unsigned* halted,
                        hipStream_t s);
+    // The rmin info column at the weights of the evaluation just enqueued
+    // (src/QuasiNewtonLearner.cpp:80-84): res[0] = min over strings and
+    // their paths of path probability / q, res[1] = the string holding it
+    // (lowest index on ties), by a (min, +) trellis pass in the log domain
+    // over the same row slots -- one tiled min-plus product per step on the
+    // fp64 VALU (a semiring MFMA does not compute).  Empty strings (one path,
+    // relative probability 1) are not candidates.
+    hipError_t enqueue_rmin(double* res, const unsigned* halted, hipStream_t s);
 
+    // the last evaluation ran at real weights (not the structural pass)
+    bool weighted() const { return weighted_; }
     int64_t n_strings() const { return n_strings_; }
     int32_t rows() const { return R_; }
     int32_t steps() const { return T_; }
@@ -96,6 +106,7 @@ private:
     int16_t sym_of_byte_[256] = {};
     int64_t n_strings_ = 0, total_sym_ = 0;
     int32_t R_ = 0, T_ = 0;
+    bool weighted_ = false;
     int32_t ldx_ = 0;                  // row pitch of alpha / gamma / z / Y
     double p0_sum_ = 0.0, n0_ = 0.0;   // sum of p / count of empty strings
     int32_t reduce_chunks_ = 0;
@@ -134,6 +145,16 @@ private:
     bool use_blas_ = true;
     void* blas_ = nullptr;     // rocblas_handle
     double* gbuf_ = nullptr;   // [np][np] the gradient GEMM's product
+    // rmin pass (allocated by its first call): log tables (+inf: no edge),
+    // two row-slot buffers of log min-path weights, per column tile and
+    // string the end minima, per block the string minima
+    double* lmat_ = nullptr;   // [np][np] log A
+    double* let_ = nullptr;    // [vocab+1][np] log E^T
+    double* l0_ = nullptr;     // [np] log a
+    double* lend_ = nullptr;   // [np] log e
+    double* mrow_ = nullptr;   // [2][R][np]
+    double* spart_ = nullptr;  // [nct][S]
+    double* rpart_ = nullptr;  // [2 * blocks]
     hipError_t enqueue_blas(const double* w, const double* p, bool structural, double* out, double* logq,
                             const unsigned* halted, hipStream_t s);
     void free_corpus();

@@ -1986,6 +1986,26 @@ int enqueue_evaluation(wfsa_dev* ctx, bool want_logq, const unsigned* halted, in
     return WFSA_OK;
 }
 
+// Across ranks, once per prepared corpus: the combine's key pair and every
+// rank's string count -> this rank's first global string index.
+int rmin_rank_base(wfsa_dev* ctx) {
+    hipStream_t s = ctx->stream;
+    HIP_TRY(ctx->rm_key.alloc(2));
+    if (ctx->comm) {
+        const int nr = ctx->comm->nranks();
+        std::vector<double> cnt(size_t(nr), 0.0);
+        cnt[size_t(ctx->comm->rank())] = double(ctx->n_strings);
+        DevBuf<double> t;
+        HIP_TRY(t.upload(cnt.data(), cnt.size(), s));
+        COMM_TRY(ctx, t.ptr, cnt.size(), wfsa::RedOp::SumF64, s);
+        HIP_TRY(t.download(cnt.data(), cnt.size(), s));
+        HIP_TRY(hipStreamSynchronize(s));
+        ctx->rm_base = 0.0;
+        for (int r = 0; r < ctx->comm->rank(); ++r) ctx->rm_base += cnt[size_t(r)];
+    }
+    return WFSA_OK;
+}
+
 // The rmin column at the weights of the evaluation just enqueued (w_full,
 // ewp and the per-edge weights on the device): bubbles, then the traversal
 // tiers in min mode, then the reduction into res[0..1].
@@ -2008,19 +2028,7 @@ int rmin_prepare(wfsa_dev* ctx) {
         HIP_TRY(ctx->rm_rs.alloc(S));
         HIP_TRY(hipMemsetAsync(ctx->rm_rs.ptr, 0, S * sizeof(double), s));   // fused accumulation starts at 0
         HIP_TRY(ctx->rm_vb.alloc(size_t(std::max(ctx->n_bubbles, 1))));
-        HIP_TRY(ctx->rm_key.alloc(2));
-        if (ctx->comm) {   // every rank's string count -> this rank's first global index
-            const int nr = ctx->comm->nranks();
-            std::vector<double> cnt(size_t(nr), 0.0);
-            cnt[size_t(ctx->comm->rank())] = double(ctx->n_strings);
-            DevBuf<double> t;
-            HIP_TRY(t.upload(cnt.data(), cnt.size(), s));
-            COMM_TRY(ctx, t.ptr, cnt.size(), wfsa::RedOp::SumF64, s);
-            HIP_TRY(t.download(cnt.data(), cnt.size(), s));
-            HIP_TRY(hipStreamSynchronize(s));
-            ctx->rm_base = 0.0;
-            for (int r = 0; r < ctx->comm->rank(); ++r) ctx->rm_base += cnt[size_t(r)];
-        }
+        if (int rc = rmin_rank_base(ctx)) return rc;
         HIP_TRY(hipStreamSynchronize(s));   // amb is freed on return
         ctx->rm_gen = ctx->prep_gen;
     }
@@ -2047,6 +2055,14 @@ int enqueue_rmin(wfsa_dev* ctx, const unsigned* halted, double* res, int par = 0
     hipStream_t s = ctx->stream;
     if (ctx->mpath) {
         HIP_TRY(ctx->mpath->enqueue_rmin(res, halted, s));
+        return WFSA_OK;
+    }
+    if (ctx->dense) {   // the (min, +) trellis over the evaluation's row slots (dense_path.hip)
+        if (ctx->rm_gen != ctx->prep_gen) {
+            if (int rc = rmin_rank_base(ctx)) return rc;
+            ctx->rm_gen = ctx->prep_gen;
+        }
+        HIP_TRY(ctx->dense->enqueue_rmin(res, halted, s));
         return WFSA_OK;
     }
     if (int rc = rmin_prepare(ctx)) return rc;
@@ -2132,7 +2148,7 @@ int enqueue_qn_step(wfsa_dev* ctx, double eta, double tol, int64_t e, bool timed
     const bool trellis = !ctx->dense && !ctx->mpath;
     const bool fused = trellis && ctx->qn_fused && !ctx->comm;
     int32_t n_ll = 0;
-    const bool fuse_rmin = ctx->qn_rmin && !ctx->mpath;   // traversal strings' rmin inside their weighted passes
+    const bool fuse_rmin = ctx->qn_rmin && trellis;   // traversal strings' rmin inside their weighted passes
     if (fuse_rmin)
         if (int rc = rmin_prepare(ctx)) return rc;
     if (ctx->fin_pending) {   // the previous step's finish: in this step's stream kernel, or its own launch
@@ -2211,7 +2227,7 @@ int enqueue_qn_step(wfsa_dev* ctx, double eta, double tol, int64_t e, bool timed
             return !(e && e[0] == '0');
         }();
         double* res = ctx->rm_res.ptr + 2 * par;
-        if (ctx->mpath) {
+        if (ctx->mpath || (ctx->dense && !ctx->comm)) {
             if (int rc = enqueue_rmin(ctx, ctx->qn_halted.ptr, res)) return rc;
             f.rmin = res;
         } else if (ctx->comm) {   // the rank's minimum, then the global one
@@ -2433,6 +2449,7 @@ int dense_load_corpus(wfsa_dev* ctx, const uint8_t* sym, const int64_t* off, con
                     hipGetErrorString(e));
     ctx->dense_struct = false;
     ctx->prep_level = 0;
+    ctx->prep_gen++;   // (the rmin pass's rank base is per corpus)
     ctx->stats.dense_rows = ctx->dense->rows();
     ctx->stats.dense_steps = ctx->dense->steps();
     ctx->stats.dense_np = ctx->dense->np();
@@ -2833,8 +2850,8 @@ int wfsa_dev_rmin(wfsa_dev* ctx, double* rmin, int64_t* string_index) {
     if (int rc = check_ctx(ctx)) return rc;
     if (!ctx->has_model || !ctx->has_corpus) return fail(WFSA_ERR_ARG, "load a model and a corpus first");
     if (ctx->in_flight) return fail(WFSA_ERR_ARG, "an evaluation is in flight");
-    if (ctx->dense) return fail(WFSA_ERR_CAPACITY, "rmin: not available on the dense path");
-    if (ctx->prep_level < 2) return fail(WFSA_ERR_ARG, "rmin: evaluate the objective first");
+    if (ctx->dense ? !ctx->dense->weighted() : ctx->prep_level < 2)
+        return fail(WFSA_ERR_ARG, "rmin: evaluate the objective first");
     if (ctx->mpath && ctx->comm)   // its index is a path of this rank's matrices: no global counterpart
         return fail(WFSA_ERR_ARG, "rmin: matrix-file mode runs the rmin column on one rank only");
     if (ctx->rm_res.n < 4) HIP_TRY(ctx->rm_res.alloc(4));
@@ -2989,7 +3006,6 @@ int wfsa_dev_qn_setup(wfsa_dev* ctx, const wfsa_qn_desc* d) {
     ctx->qn_k = k;
     ctx->qn_plogp = d->plogp;
     ctx->qn_exp_lambda = d->exponential_lambda ? 1 : 0;
-    if (d->info_rmin && ctx->dense) return fail(WFSA_ERR_CAPACITY, "the rmin column is not available on the dense path");
     if (d->info_rmin && ctx->mpath && ctx->comm)
         return fail(WFSA_ERR_ARG, "rmin: matrix-file mode runs the rmin column on one rank only");
     ctx->qn_rmin = d->info_rmin != 0;
