@@ -116,11 +116,27 @@ def test_two_processes_over_gloo_equal_one_context(peer):
         _compare(got[r], one)
 
 
-def test_in_process_group_peer_path(monkeypatch):
-    """the same peer kernel between two contexts of one process (the
-    pointers themselves instead of IPC handles)"""
+def _in_child(body):
+    """run `body` (a function of this module) in a fresh Python process: two
+    contexts of one process whose peer kernels spin on each other's flags
+    need their streams on distinct hardware queues, which a process that has
+    already made and dropped many contexts (this test session) does not
+    guarantee -- HIP spreads streams over GPU_MAX_HW_QUEUES queues, and two
+    streams on one queue run in order, so one rank's spinning kernel would
+    hold back the other's (the wait then gives up: NaN).  The child starts
+    with 4 streams on 8 queues."""
+    import subprocess
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    code = (f"import sys; sys.path[:0] = [{here!r}, {ROOT!r}, {os.path.join(ROOT, 'w-fsa_amd')!r}]\n"
+            f"import test_gpu_multiprocess as t; t.{body}()")
+    env = dict(os.environ, WFSA_PEER="1", GPU_MAX_HW_QUEUES="8")
+    r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=400)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-6000:]
+
+
+def _peer_group_body():
     import wfsa_amd as W
-    monkeypatch.setenv("WFSA_PEER", "1")
     syn = W.Synthetic(**SPEC)
     sym, off, wt = syn.corpus()
     fsa = W.Fsa.read_text(syn.wfsa_text)
@@ -132,6 +148,12 @@ def test_in_process_group_peer_path(monkeypatch):
     for res in outs:
         assert res["stats"]["comm_peer"] == 1
         _compare(res, one)
+
+
+def test_in_process_group_peer_path():
+    """the same peer kernel between two contexts of one process (the
+    pointers themselves instead of IPC handles)"""
+    _in_child("_peer_group_body")
 
 
 def _family_a_eval(W):
@@ -147,13 +169,11 @@ def _family_a_eval(W):
     return ll, np.array(grad)
 
 
-def test_context_after_peer_group_is_exact(monkeypatch):
-    """a context made after an in-process peer group is gone evaluates to the
-    same bits as one made before it (the group's uncached areas must not
-    reach later contexts' allocations: fp64 atomics into them were lost)"""
+def _after_group_body():
     import wfsa_amd as W
+    os.environ["WFSA_PEER"] = "0"
     ll0, g0 = _family_a_eval(W)
-    monkeypatch.setenv("WFSA_PEER", "1")
+    os.environ["WFSA_PEER"] = "1"
     syn = W.Synthetic(**SPEC)
     sym, off, wt = syn.corpus()
     fsa = W.Fsa.read_text(syn.wfsa_text)
@@ -167,3 +187,10 @@ def test_context_after_peer_group_is_exact(monkeypatch):
         ll1, g1 = _family_a_eval(W)
         assert ll1 == ll0
         np.testing.assert_array_equal(g1, g0)
+
+
+def test_context_after_peer_group_is_exact():
+    """a context made after an in-process peer group is gone evaluates to the
+    same bits as one made before it (the group's uncached areas must not
+    reach later contexts' allocations: fp64 atomics into them were lost)"""
+    _in_child("_after_group_body")
