@@ -301,3 +301,36 @@ def test_hf_setup_capacity_on_one_shard_fails_every_rank():
     codes = [c for c, _ in outs]
     assert codes[0] == codes[1] and codes[0] != 0
     assert "another rank" in outs[0][1] and "parameters" in outs[1][1]
+
+
+def test_dense_path_across_ranks_with_rmin(monkeypatch):
+    """the dense fp64 path across 2 ranks (each rank's row slots hold its
+    shard; [LL, grad] summed per step) with the rmin column on -- its (min, +)
+    pass per rank, then the global minimum and string index: the host steps
+    and the device loop equal one context"""
+    import wfsa_amd as W
+    monkeypatch.setenv("WFSA_DENSE", "1")
+    syn = W.Synthetic(n_states=16, degree=1, vocab=8, emissions=2, dense=True, n_strings=300, max_len=9, seed=21)
+    sym, off, wt = syn.corpus()
+    fsa = W.Fsa.read_text(syn.wfsa_text)
+
+    def learn(nranks, rank, gid):
+        lrn = W.QuasiNewtonLearner(0)
+        if nranks > 1:
+            lrn.SetCommunicator(nranks, rank, gid)
+        lrn.set_info_rmin(True)
+        lrn.BuildFromPacked(fsa, sym, off, wt)
+        lrn.Finalize()
+        lrn.Init(7)
+        assert lrn.stats()["dense"] == 1
+        rows = [lrn.OptimizationStep(1.0, -1.0)[0] for _ in range(2)]
+        return rows + lrn.Run(4, 1.0, -1.0), lrn.x()
+
+    rows1, x1 = learn(1, 0, None)
+    assert all(r[6] >= 0 and 0 < r[5] < 1 for r in rows1)
+    for rows, x in _run_ranks(2, learn):
+        assert len(rows) == len(rows1) == 6
+        for a, q in zip(rows, rows1):
+            for u, v in zip(a[:7], q[:7]):
+                assert _close(u, v, rel=1e-10, atol=1e-13)
+        np.testing.assert_allclose(x, x1, rtol=1e-10, atol=1e-12)
