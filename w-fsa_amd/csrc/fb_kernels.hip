@@ -83,19 +83,7 @@ __device__ __forceinline__ void global_add(double* p, double v) {
 // takes a signed 64-bit (or a 128-bit) addend with an atomic add on the low
 // word whose returned old value gives the carry into the high word.
 constexpr unsigned long long kFixLlNegInf = 1, kFixLlPosInf = 2, kFixLlNan = 4, kFixGradBad = 8;
-// v * 2^frac rounded to the nearest integer (ties to even, as rint).  Below
-// 2^51 in magnitude, x + 1.5 * 2^52 lands in [2^52, 2^53), whose unit in
-// the last place is 1: the sum is exact after rounding x, and its bits less
-// those of 1.5 * 2^52 are the integer -- an add and a 64-bit subtract instead
-// of the emulated double -> int64 conversion (the same value, bit for bit)
-__device__ __forceinline__ long long fix_of(double v, int frac) {
-    const double x = ldexp(v, frac);
-#ifndef WFSA_FIX_RINT   // (layout-variant builds: the conversion alone)
-    if (__builtin_expect(fabs(x) < 0x1p51, 1))
-        return __double_as_longlong(x + 0x1.8p52) - __double_as_longlong(0x1.8p52);
-#endif
-    return (long long)rint(x);
-}
+__device__ __forceinline__ long long fix_of(double v, int frac) { return (long long)rint(ldexp(v, frac)); }
 __device__ __forceinline__ void fix128_add(unsigned long long* acc, unsigned long long lo, long long hi) {
     const unsigned long long old = __hip_atomic_fetch_add(acc, lo, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     hi += (old + lo < old) ? 1 : 0;   // carry out of the low word
