@@ -180,7 +180,9 @@ int wfsa_dev_load_paths(wfsa_dev* ctx, int32_t n_params, int64_t n_paths, const 
  * string is ambiguous).  The reference reports the path's index in its BFS
  * enumeration instead, which has no counterpart without enumerating paths
  * (in matrix-file mode, where paths are given, *string_index is that path
- * index).  Not available on the dense path. */
+ * index).  On the dense path the candidates are every non-empty string
+ * (a (min, +) trellis over its row slots; WFSA_ERR_ARG until an evaluation
+ * at real weights has run). */
 int wfsa_dev_rmin(wfsa_dev* ctx, double* rmin, int64_t* string_index);
 
 /* Where each loaded string runs (after compilation): tier[s] = -1 compiled
