@@ -457,7 +457,8 @@ def main():
                      "note": "the headline steps plus the rmin info column (the (min, x) passes fused into "
                              "the evaluation's bubble / traversal kernels)"}
         lrn.set_info_rmin(False)
-    boundary = boundary_steps(m, args.boundary_steps) if args.boundary_steps > 0 else None
+    # (one GPU only: a sub-record must never leave ranks waiting in a collective)
+    boundary = boundary_steps(m, args.boundary_steps) if args.boundary_steps > 0 and not distributed else None
 
     out = {
         "metric": METRIC,
