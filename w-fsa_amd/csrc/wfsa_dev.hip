@@ -937,11 +937,7 @@ wfsa::Publish publish_args(wfsa_dev* ctx) {
 int collect_timing(wfsa_dev* ctx) {
     if (!ctx->timing_pending) return WFSA_OK;
     ctx->timing_pending = false;
-    // the results were published before the stream's tail event completes:
-    // poll it (a blocking synchronize sleeps the thread for a ~10 us wake-up)
-    hipError_t q;
-    while ((q = hipEventQuery(ctx->ev1)) == hipErrorNotReady) __builtin_ia32_pause();
-    HIP_TRY(q);
+    HIP_TRY(hipEventSynchronize(ctx->ev1));
     float c_ms = 0.f, fb_ms = 0.f, all_ms = 0.f;
     if (!ctx->graph_exec && ctx->kernel_timing) {   // events inside a captured graph are not timeable
         HIP_TRY(hipEventElapsedTime(&c_ms, ctx->k0[0], ctx->kc[0]));
