@@ -5,12 +5,14 @@
 //   B  4-bit out-edge choice per edge: a chain through LDS (slot = base of the
 //      current node + choice; weight and the next node's base per slot),
 //      0.5 B of stream per edge;
-//   B2 B with two strings per lane (two chains in flight).
+//   B2 B with two strings per lane (two chains in flight);
+//   C  B with the weight and the next base in one 16-byte LDS entry.
 // Prints the kernel time of each and checks that all three sum the same
 // log-likelihood.
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <cstring>
 #include <cstdio>
 #include <random>
 #include <vector>
@@ -220,6 +222,66 @@ __global__ __launch_bounds__(1024) void walk_b_pf(const uint4* __restrict__ st, 
     if (lane == 0) ll_part[gw] = ll;
 }
 
+// C: B's chain with the weight and the next node's base in ONE 16-byte LDS
+// entry (one ds_read_b128 per edge instead of an 8-byte and a 2-byte read);
+// the table (147 KB) takes the CU's LDS: one 1024-thread block per CU
+template <int K>
+__global__ __launch_bounds__(1024) void walk_c_pf(const uint4* __restrict__ st, int n_groups,
+                                                  const double2* __restrict__ tab, const double* __restrict__ p,
+                                                  double* ll_part) {
+    extern __shared__ double2 lt[];
+    for (int j = threadIdx.x; j < kSlots; j += blockDim.x) lt[j] = tab[j];
+    __syncthreads();
+    const int lane = threadIdx.x % kWave;
+    const int gw = blockIdx.x * (blockDim.x / kWave) + threadIdx.x / kWave;
+    const int nw = gridDim.x * (blockDim.x / kWave);
+    double ll = 0.0;
+    uint4 r[K][kChB], nx[K][kChB];
+    auto ld = [&](uint4 (&d)[K][kChB], int g0) {
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            const uint4* s = st + size_t(min(g0 + k, n_groups - 1)) * kChB * kWave + lane;
+#pragma unroll
+            for (int c = 0; c < kChB; ++c) d[k][c] = s[c * kWave];
+        }
+    };
+    if (gw * K < n_groups) ld(r, gw * K);
+    for (int g0 = gw * K; g0 < n_groups; g0 += nw * K) {
+        ld(nx, g0 + nw * K);
+        double acc[K];
+        int base[K];
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            acc[k] = 0.0;
+            base[k] = 0;
+        }
+#pragma unroll
+        for (int c = 0; c < kChB; ++c)
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+#pragma unroll
+                for (int h = 0; h < 8; ++h) {
+                    if (c * 32 + i * 8 + h >= kLen) break;
+#pragma unroll
+                    for (int k = 0; k < K; ++k) {
+                        const uint32_t v = (i == 0 ? r[k][c].x : i == 1 ? r[k][c].y : i == 2 ? r[k][c].z : r[k][c].w);
+                        const double2 e = lt[base[k] + int((v >> (4 * h)) & 0xfu)];
+                        acc[k] += e.x;
+                        base[k] = int(__double_as_longlong(e.y));
+                    }
+                }
+#pragma unroll
+        for (int k = 0; k < K; ++k)
+            if (g0 + k < n_groups) ll += p[(g0 + k) * kWave + lane] * acc[k];
+#pragma unroll
+        for (int k = 0; k < K; ++k)
+#pragma unroll
+            for (int c = 0; c < kChB; ++c) r[k][c] = nx[k][c];
+    }
+    ll = wave_sum(ll);
+    if (lane == 0) ll_part[gw] = ll;
+}
+
 // both formats in one kernel: the first nb waves of each block walk nibble
 // groups [0, GB), the others 16-bit groups [GB, G) -- HBM and LDS at once
 __global__ __launch_bounds__(1024) void walk_mix(const uint4* __restrict__ stA, const uint4* __restrict__ stB, int GB,
@@ -399,6 +461,25 @@ int main() {
             if (run(nm, [&] { hipLaunchKernelGGL(walk_mix, dim3(256), dim3(1024), 0, 0, dA, dB, GB, G, nbw, dsw, dsw, dnb,
                                                  dp, dll); }, 256 * 16, bytes)) return 1;
         }
+    }
+    {   // C: one 16-byte LDS entry per edge (weight, next base)
+        std::vector<double2> tab(kSlots);
+        for (int j = 0; j < kSlots; ++j) {
+            long long nbv = nb[j];
+            double nbd;
+            memcpy(&nbd, &nbv, 8);
+            tab[j] = make_double2(sw[j], nbd);
+        }
+        double2* dtab;
+        CK(hipMalloc(&dtab, kSlots * sizeof(double2)));
+        CK(hipMemcpy(dtab, tab.data(), kSlots * sizeof(double2), hipMemcpyHostToDevice));
+        const size_t lds = kSlots * sizeof(double2);
+        CK(hipFuncSetAttribute(reinterpret_cast<const void*>(&walk_c_pf<1>), hipFuncAttributeMaxDynamicSharedMemorySize, int(lds)));
+        CK(hipFuncSetAttribute(reinterpret_cast<const void*>(&walk_c_pf<2>), hipFuncAttributeMaxDynamicSharedMemorySize, int(lds)));
+        if (run("C nibble, 16-B entry, K=1", [&] { hipLaunchKernelGGL(walk_c_pf<1>, dim3(256), dim3(1024), lds, 0, dB, G, dtab, dp, dll); },
+                256 * 16, bB)) return 1;
+        if (run("C nibble, 16-B entry, K=2", [&] { hipLaunchKernelGGL(walk_c_pf<2>, dim3(256), dim3(1024), lds, 0, dB, G, dtab, dp, dll); },
+                256 * 16, bB)) return 1;
     }
     {   // stream loads alone: the HBM floor of each format
         const int grid = 256;
