@@ -282,6 +282,54 @@ __global__ __launch_bounds__(1024) void walk_c_pf(const uint4* __restrict__ st, 
     if (lane == 0) ll_part[gw] = ll;
 }
 
+// A with the weight table split into its high and low 32-bit words (two
+// tables, two 4-byte gathers per word instead of one 8-byte gather): the
+// bank-conflict pattern of random ds_read_b32 vs ds_read_b64
+__global__ __launch_bounds__(1024) void walk_a_split(const uint4* __restrict__ st, int n_groups,
+                                                     const double* __restrict__ w, const double* __restrict__ p,
+                                                     double* ll_part) {
+    __shared__ uint32_t lhi[kSlots], llo[kSlots];
+    for (int j = threadIdx.x; j < kSlots; j += blockDim.x) {
+        const long long b = __double_as_longlong(w[j]);
+        lhi[j] = uint32_t(b >> 32);
+        llo[j] = uint32_t(b);
+    }
+    __syncthreads();
+    const int lane = threadIdx.x % kWave;
+    const int gw = blockIdx.x * (blockDim.x / kWave) + threadIdx.x / kWave;
+    const int nw = gridDim.x * (blockDim.x / kWave);
+    double ll = 0.0;
+    uint4 r[kChA], nx[kChA];
+    auto ld = [&](uint4 (&d)[kChA], int g) {
+        const uint4* s = st + size_t(min(g, n_groups - 1)) * kChA * kWave + lane;
+#pragma unroll
+        for (int c = 0; c < kChA; ++c) d[c] = s[c * kWave];
+    };
+    auto wt = [&](uint32_t x) {
+        const uint32_t i = min(x, uint32_t(kSlots - 1));
+        return x != 0xffffu ? __hiloint2double(int(lhi[i]), int(llo[i])) : 0.0;
+    };
+    if (gw < n_groups) ld(r, gw);
+    for (int g = gw; g < n_groups; g += nw) {
+        ld(nx, g + nw);
+        double a0 = 0.0, a1 = 0.0;
+#pragma unroll
+        for (int c = 0; c < kChA; ++c) {
+            const uint32_t v[4] = {r[c].x, r[c].y, r[c].z, r[c].w};
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                a0 += wt(v[i] & 0xffffu);
+                a1 += wt(v[i] >> 16);
+            }
+        }
+        ll += p[g * kWave + lane] * (a0 + a1);
+#pragma unroll
+        for (int c = 0; c < kChA; ++c) r[c] = nx[c];
+    }
+    ll = wave_sum(ll);
+    if (lane == 0) ll_part[gw] = ll;
+}
+
 // both formats in one kernel: the first nb waves of each block walk nibble
 // groups [0, GB), the others 16-bit groups [GB, G) -- HBM and LDS at once
 __global__ __launch_bounds__(1024) void walk_mix(const uint4* __restrict__ stA, const uint4* __restrict__ stB, int GB,
@@ -462,6 +510,8 @@ int main() {
                                                  dp, dll); }, 256 * 16, bytes)) return 1;
         }
     }
+    if (run("A 16-bit prefetch, split hi/lo", [&] { hipLaunchKernelGGL(walk_a_split, dim3(256), dim3(1024), 0, 0, dA, G, dsw, dp, dll); },
+            256 * 16, bA)) return 1;
     {   // C: one 16-byte LDS entry per edge (weight, next base)
         std::vector<double2> tab(kSlots);
         for (int j = 0; j < kSlots; ++j) {
