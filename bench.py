@@ -308,7 +308,10 @@ def roofline_of(m, traffic):
         tf = alg_flops / (fb_ms * 1e-3) / 1e12 if fb_ms > 0 else None
         return {"bound": "mfma", "achieved": tf, "peak": F64_MFMA_PEAK_TFS, "unit": "TFLOP/s",
                 "frac": tf / F64_MFMA_PEAK_TFS if tf else None, "traffic": None,
-                "kernel": "dense_gemm_kernel<FWD/BWD/GRAD> (v_mfma_f64_16x16x4f64) + its epilogue kernels, one evaluation",
+                "kernel": ("rocblas_dgemm (library fp64 MFMA GEMMs) + our epilogue kernels, one evaluation"
+                           if st1.get("dense_blas") else
+                           "dense_gemm_kernel<FWD/BWD/GRAD> (hand-written v_mfma_f64_16x16x4f64, epilogues fused), "
+                           "one evaluation"),
                 "timed_launches": timed, "evaluation_ms": fb_ms, "algorithmic_flops_per_evaluation": alg_flops,
                 "issued_flops_per_evaluation": 6.0 * npd * npd * R * max(T - 1, 0), "row_slots": R, "trellis_steps": T}
     comp = st1["compiled_strings"]

@@ -112,6 +112,7 @@ typedef struct {
     int64_t slot_chunks;       /* bubble contribution slots, in 16-slot chunks (8 B a slot) */
     int32_t max_group_chunks;  /* chunks of the largest constraint's slot group (one QN block sums it) */
     int32_t wave_pull;         /* the wave kernel pulls (wave_pull_kernel): nodes per lane (4, 6, 8); 0: it pushes (wide2_kernel) */
+    int32_t dense_blas;        /* dense path GEMM engine: 0 our fused MFMA kernels (default), 1 rocBLAS dgemm (WFSA_DENSE_BLAS=1) */
 } wfsa_dev_stats;
 
 /* context ---------------------------------------------------------------- */
@@ -266,6 +267,28 @@ int wfsa_dev_comm_local_id(int nranks, uint8_t id[WFSA_COMM_ID_BYTES]);
 int wfsa_dev_comm_init(wfsa_dev* ctx, int nranks, int rank, const uint8_t id[WFSA_COMM_ID_BYTES]);
 int wfsa_dev_allreduce(wfsa_dev* ctx, double* host_buf, int64_t count);
 
+/* Failure semantics across ranks.  A call that takes part in
+ * collectives (recognize, objective_grad_begin/_end, qn_setup, qn_run,
+ * hf_setup, hf_eval, rmin, allreduce) and fails on one rank for any reason
+ * but a bad argument aborts that rank's communicator: the in-process group
+ * is poisoned (every waiting member wakes with WFSA_ERR_RCCL now), every
+ * member's peer area gets its poison word (their next peer sum fails at
+ * entry), an RCCL communicator is aborted (ncclCommAbort).  A peer sum whose
+ * wait gives up (WFSA_PEER_TIMEOUT_S, default 120 s) poisons every area too
+ * and is reported as WFSA_ERR_RCCL at the next host sync point, never as a
+ * NaN result.  wfsa_dev_comm_abort does the same for a failure outside the
+ * library (the caller's own work between collectives). */
+int wfsa_dev_comm_abort(wfsa_dev* ctx, const char* why);
+
+/* Test entry: the peer all-reduce kernel on one device, the other members'
+ * areas local and written beforehand (no second process, no concurrency
+ * needed).  mode 0: every member present, out[0] = max |sum - rank-order
+ * sum|; 1: the last member never arrives, out[0] = NaN results (the call
+ * must give up after timeout_s); 2: the area poisoned before the call, which
+ * must fail at entry.  out[1] = status word, out[2] = poisoned areas,
+ * out[3] = seconds the call took. */
+int wfsa_dev_peer_selftest(int device, int nranks, int64_t n, double timeout_s, int mode, double out[4]);
+
 /* A communicator over a host callback instead of RCCL (one process per rank,
  * several may share a GPU; e.g. torch.distributed over gloo, or MPI):
  * fn(user, buf, count, op) all-reduces a HOST buffer in place -- op 0: sum
@@ -281,7 +304,9 @@ int wfsa_dev_allreduce(wfsa_dev* ctx, double* host_buf, int64_t count);
  * order -- stream-ordered, no host step.  On by default over RCCL, off
  * otherwise; WFSA_PEER=1 / 0 overrides.  The first such sum checks the
  * path on every rank and all ranks fall back to the transport when any
- * check fails (stats.comm_peer = -1). */
+ * check fails (stats.comm_peer = -1).  Refused (stats.comm_peer = 0) for an
+ * in-process group whose members share a device: nothing guarantees their
+ * spinning kernels run concurrently there. */
 typedef int (*wfsa_host_allreduce_fn)(void* user, void* buf, int64_t count, int32_t op);
 int wfsa_dev_comm_init_host(wfsa_dev* ctx, int nranks, int rank, wfsa_host_allreduce_fn fn, void* user);
 

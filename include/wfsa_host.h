@@ -62,6 +62,11 @@ int wfsa_learner_create(const char* optimizer, int device, wfsa_learner** out);
 int wfsa_learner_info_width(wfsa_learner* l);
 void wfsa_learner_destroy(wfsa_learner* l);
 int wfsa_learner_set_comm(wfsa_learner* l, int nranks, int rank, const uint8_t id[WFSA_COMM_ID_BYTES]);
+/* this rank failed outside the library: every other rank's current or next
+ * collective fails at once (wfsa_dev_comm_abort).  The learner calls that
+ * sit between collectives (build, finalize, init, step, run, objective_grad,
+ * load_matrices) do this themselves when they fail. */
+int wfsa_learner_comm_abort(wfsa_learner* l, const char* why);
 /* the same over a host all-reduce callback (wfsa_dev_comm_init_host) */
 int wfsa_learner_set_comm_host(wfsa_learner* l, int nranks, int rank, wfsa_host_allreduce_fn fn, void* user);
 /* Learner::BuildFrom on (Fsa, Corpus); the corpus is renormalized first as

@@ -8,6 +8,15 @@ import pytest
 pytestmark = pytest.mark.gpu
 
 
+@pytest.fixture(autouse=True, params=["mfma", "rocblas"])
+def gemm_engine(request, monkeypatch):
+    """every test on both GEMM engines of the dense path: our fused
+    v_mfma_f64_16x16x4f64 kernels (WFSA_DENSE_BLAS=0) and rocBLAS dgemm
+    with our epilogue kernels (=1)"""
+    monkeypatch.setenv("WFSA_DENSE_BLAS", "0" if request.param == "mfma" else "1")
+    return request.param
+
+
 def _close(a, b, rel, atol=1e-13):
     return abs(a - b) <= max(atol, rel * max(abs(a), abs(b)))
 

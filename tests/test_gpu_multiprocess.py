@@ -49,11 +49,13 @@ def _learn(W, fsa, sym, off, wt, setup=None):
     return dict(kl=kl, grad=g, rows=[list(r) for r in rows], x=lrn.x(), info=lrn.info(), stats=lrn.stats())
 
 
-def _worker(rank, world, port, peer, q):
+def _worker(rank, world, port, peer, q, late_s=0.0):
     import sys
     sys.path.insert(0, ROOT)
     sys.path.insert(0, os.path.join(ROOT, "w-fsa_amd"))
     os.environ["WFSA_PEER"] = "1" if peer else "0"
+    if late_s:
+        os.environ["WFSA_PEER_TIMEOUT_S"] = "3"
     import torch.distributed as dist
     import wfsa_amd as W
     try:
@@ -62,6 +64,10 @@ def _worker(rank, world, port, peer, q):
         syn = W.Synthetic(**SPEC)
         sym, off, wt = syn.corpus()
         fsa = W.Fsa.read_text(syn.wfsa_text)
+        if late_s:   # rank 1 arrives at the device loop after the others' peer waits gave up
+            res = _late_learn(W, fsa, sym, off, wt, world, rank, late_s)
+            q.put((rank, res))
+            return
         res = _learn(W, fsa, sym, off, wt, lambda l: l.SetHostCommunicator(world, rank, W.torch_allreduce))
         dist.barrier()
         dist.destroy_process_group()
@@ -69,6 +75,29 @@ def _worker(rank, world, port, peer, q):
     except Exception as e:   # reported to the parent, never a hang
         import traceback
         q.put((rank, {"error": f"{type(e).__name__}: {e}\n{traceback.format_exc()}"}))
+
+
+def _late_learn(W, fsa, sym, off, wt, world, rank, late_s):
+    """the device QN loop with rank 1 late by late_s: every rank must raise
+    (WFSA_ERR_RCCL) -- rank 0 when its peer wait gives up, rank 1 at entry
+    of its first peer sum (its area was poisoned) -- and neither may report
+    a non-finite halt"""
+    import time
+    lrn = W.QuasiNewtonLearner(0)
+    lrn.SetHostCommunicator(world, rank, W.torch_allreduce)
+    lrn.BuildFromPacked(fsa, sym, off, wt)
+    lrn.Finalize()
+    lrn.Init(7)
+    lrn.objective_grad()   # the peer path set up and checked while both ranks are here
+    assert lrn.stats()["comm_peer"] == 1
+    if rank == 1:
+        time.sleep(late_s)
+    t0 = time.time()
+    try:
+        rows = lrn.Run(5, 1.0, -1.0)
+        return {"raised": None, "rows": [list(r) for r in rows], "s": time.time() - t0}
+    except W.WfsaError as e:
+        return {"raised": str(e), "code": e.code, "s": time.time() - t0}
 
 
 def _one_context():
@@ -88,13 +117,11 @@ def _compare(res, one):
     np.testing.assert_allclose(res["x"], one["x"], rtol=1e-10, atol=1e-12)
 
 
-@pytest.mark.parametrize("peer", [True, False])
-def test_two_processes_over_gloo_equal_one_context(peer):
-    world = 2
+def _spawn(world, peer, late_s=0.0):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, peer, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, peer, q, late_s)) for r in range(world)]
     for p in procs:
         p.start()
     got = {}
@@ -109,6 +136,13 @@ def test_two_processes_over_gloo_equal_one_context(peer):
                 p.kill()
     for r in range(world):
         assert "error" not in got[r], got[r].get("error")
+    return got
+
+
+@pytest.mark.parametrize("peer", [True, False])
+def test_two_processes_over_gloo_equal_one_context(peer):
+    world = 2
+    got = _spawn(world, peer)
     one = _one_context()
     for r in range(world):
         assert got[r]["stats"]["comm_ranks"] == world
@@ -116,44 +150,44 @@ def test_two_processes_over_gloo_equal_one_context(peer):
         _compare(got[r], one)
 
 
-def _in_child(body):
-    """run `body` (a function of this module) in a fresh Python process: two
-    contexts of one process whose peer kernels spin on each other's flags
-    need their streams on distinct hardware queues, which a process that has
-    already made and dropped many contexts (this test session) does not
-    guarantee -- HIP spreads streams over GPU_MAX_HW_QUEUES queues, and two
-    streams on one queue run in order, so one rank's spinning kernel would
-    hold back the other's (the wait then gives up: NaN).  The child starts
-    with 4 streams on 8 queues."""
-    import subprocess
-    import sys
-    here = os.path.dirname(os.path.abspath(__file__))
-    code = (f"import sys; sys.path[:0] = [{here!r}, {ROOT!r}, {os.path.join(ROOT, 'w-fsa_amd')!r}]\n"
-            f"import test_gpu_multiprocess as t; t.{body}()")
-    env = dict(os.environ, WFSA_PEER="1", GPU_MAX_HW_QUEUES="8")
-    r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=400)
-    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-6000:]
+def test_two_processes_late_rank_fails_every_rank():
+    """rank 1 reaches the device QN loop 8 s late, past WFSA_PEER_TIMEOUT_S
+    (3 s): rank 0's peer wait gives up, poisons both areas and raises; rank
+    1 raises at its first peer sum without waiting (the timeout
+    used to become a NaN gradient and a non-finite halt)"""
+    got = _spawn(2, True, late_s=8.0)
+    for r in range(2):
+        assert got[r]["raised"], f"rank {r} did not fail: {got[r]}"
+        assert "peer all-reduce" in got[r]["raised"], got[r]["raised"]
+    assert got[0]["s"] < 30          # the 3 s timeout, not a hang
+    assert got[1]["s"] < 5           # poisoned: fails at entry
 
 
-def _peer_group_body():
+# ---- the peer kernel on one device, the other members simulated ----------
+
+@pytest.mark.parametrize("nranks,n", [(2, 1), (2, 3000), (3, 1025), (8, 65536)])
+def test_peer_kernel_sums_in_rank_order(nranks, n):
     import wfsa_amd as W
-    syn = W.Synthetic(**SPEC)
-    sym, off, wt = syn.corpus()
-    fsa = W.Fsa.read_text(syn.wfsa_text)
-    gid = W.Device.comm_local_id(2)
-    with ThreadPoolExecutor(max_workers=2) as ex:
-        futs = [ex.submit(_learn, W, fsa, sym, off, wt, lambda l, r=r: l.SetCommunicator(2, r, gid)) for r in range(2)]
-        outs = [f.result(timeout=300) for f in futs]
-    one = _one_context()
-    for res in outs:
-        assert res["stats"]["comm_peer"] == 1
-        _compare(res, one)
+    err, status, poisoned, secs = W.Device.peer_selftest(nranks, n, 5.0, 0)
+    assert err == 0.0                 # bit for bit the rank-order sum
+    assert status == 0 and poisoned == 0
+    assert secs < 2
 
 
-def test_in_process_group_peer_path():
-    """the same peer kernel between two contexts of one process (the
-    pointers themselves instead of IPC handles)"""
-    _in_child("_peer_group_body")
+def test_peer_kernel_gives_up_and_poisons_every_area():
+    import wfsa_amd as W
+    nan, status, poisoned, secs = W.Device.peer_selftest(4, 3000, 0.5, 1)
+    assert nan == 3000                # NaN results, never a partial sum
+    assert status == 1                # the host-mapped status word (Collective::check)
+    assert poisoned == 4              # every member's next call fails at entry
+    assert 0.4 < secs < 5
+
+
+def test_peer_kernel_fails_at_entry_when_poisoned():
+    import wfsa_amd as W
+    nan, status, poisoned, secs = W.Device.peer_selftest(4, 3000, 10.0, 2)
+    assert nan == 3000 and status == 1 and poisoned == 4
+    assert secs < 1                   # no wait
 
 
 def _family_a_eval(W):
@@ -169,28 +203,110 @@ def _family_a_eval(W):
     return ll, np.array(grad)
 
 
-def _after_group_body():
+def test_context_after_peer_selftest_is_exact():
+    """contexts made after peer areas were used and handed back evaluate to
+    the same bits as one made before (the uncached areas must never reach
+    later contexts' allocations: fp64 atomics into them were lost, round 3)"""
     import wfsa_amd as W
-    os.environ["WFSA_PEER"] = "0"
     ll0, g0 = _family_a_eval(W)
-    os.environ["WFSA_PEER"] = "1"
-    syn = W.Synthetic(**SPEC)
-    sym, off, wt = syn.corpus()
-    fsa = W.Fsa.read_text(syn.wfsa_text)
-    for _ in range(2):   # two groups one after the other: the second reuses the first's areas
-        gid = W.Device.comm_local_id(2)
-        with ThreadPoolExecutor(max_workers=2) as ex:
-            futs = [ex.submit(_learn, W, fsa, sym, off, wt, lambda l, r=r: l.SetCommunicator(2, r, gid)) for r in range(2)]
-            outs = [f.result(timeout=300) for f in futs]
-        assert all(o["stats"]["comm_peer"] == 1 for o in outs)
     for _ in range(3):
+        W.Device.peer_selftest(2, 65536, 5.0, 0)
+        W.Device.peer_selftest(8, 65536, 5.0, 0)
         ll1, g1 = _family_a_eval(W)
         assert ll1 == ll0
         np.testing.assert_array_equal(g1, g0)
 
 
-def test_context_after_peer_group_is_exact():
-    """a context made after an in-process peer group is gone evaluates to the
-    same bits as one made before it (the group's uncached areas must not
-    reach later contexts' allocations: fp64 atomics into them were lost)"""
-    _in_child("_after_group_body")
+# ---- in-process groups: the peer path refused, failures propagate ---------
+
+def _group(k, fn):
+    """run fn(k, rank, gid) on k threads; every rank's result or exception"""
+    import wfsa_amd as W
+    gid = W.Device.comm_local_id(k)
+    with ThreadPoolExecutor(max_workers=k) as ex:
+        futs = [ex.submit(fn, k, r, gid) for r in range(k)]
+        out = []
+        for f in futs:
+            try:
+                out.append(f.result(timeout=100))
+            except Exception as e:   # (a product error, not a test timeout)
+                out.append(e)
+    return out
+
+
+def test_in_process_group_on_one_device_refuses_peer(monkeypatch):
+    """WFSA_PEER=1 on an in-process group whose members share a device: the
+    path is refused (their spinning kernels need not run concurrently), the
+    transport carries every sum, and the result equals one context"""
+    import wfsa_amd as W
+    monkeypatch.setenv("WFSA_PEER", "1")
+    syn = W.Synthetic(**SPEC)
+    sym, off, wt = syn.corpus()
+    fsa = W.Fsa.read_text(syn.wfsa_text)
+    outs = _group(2, lambda k, r, gid: _learn(W, fsa, sym, off, wt, lambda l: l.SetCommunicator(k, r, gid)))
+    one = _one_context()
+    for res in outs:
+        assert not isinstance(res, Exception), res
+        assert res["stats"]["comm_peer"] == 0
+        _compare(res, one)
+
+
+def _prepared(W, k, r, gid):
+    syn = W.Synthetic(**SPEC)
+    sym, off, wt = syn.corpus()
+    lrn = W.QuasiNewtonLearner(0)
+    lrn.SetCommunicator(k, r, gid)
+    lrn.BuildFromPacked(W.Fsa.read_text(syn.wfsa_text), sym, off, wt)
+    lrn.Finalize()
+    lrn.Init(7)
+    return lrn
+
+
+def test_aborted_rank_fails_every_rank_promptly():
+    """rank 1 fails outside the library and aborts; rank 0, already waiting
+    in the device loop's per-step sum, fails at once with the reason"""
+    import time
+    import wfsa_amd as W
+
+    def body(k, r, gid):
+        lrn = _prepared(W, k, r, gid)
+        t0 = time.time()
+        if r == 1:
+            time.sleep(1.0)   # rank 0 is inside Run by now
+            lrn.AbortCommunicator("rank 1: injected failure")
+            with pytest.raises(W.WfsaError):
+                lrn.Run(5, 1.0, -1.0)
+            return time.time() - t0
+        with pytest.raises(W.WfsaError) as e:
+            lrn.Run(5, 1.0, -1.0)
+        assert "injected failure" in str(e.value) or "failed" in str(e.value)
+        return time.time() - t0
+
+    outs = _group(2, body)
+    for o in outs:
+        assert not isinstance(o, Exception), o
+        assert o < 10
+
+
+def test_late_rank_times_out_every_rank(monkeypatch):
+    """WFSA_GROUP_TIMEOUT_S=2 and rank 1 six seconds late: rank 0's barrier
+    gives up after ~2 s and poisons the group; rank 1 fails at its first
+    collective without waiting"""
+    import time
+    import wfsa_amd as W
+    monkeypatch.setenv("WFSA_GROUP_TIMEOUT_S", "2")
+
+    def body(k, r, gid):
+        lrn = _prepared(W, k, r, gid)
+        if r == 1:
+            time.sleep(6.0)
+        t0 = time.time()
+        with pytest.raises(W.WfsaError) as e:
+            lrn.Run(5, 1.0, -1.0)
+        return time.time() - t0, str(e.value)
+
+    outs = _group(2, body)
+    for o in outs:
+        assert not isinstance(o, Exception), o
+    assert 1.5 < outs[0][0] < 10 and "WFSA_GROUP_TIMEOUT_S" in outs[0][1]
+    assert outs[1][0] < 2

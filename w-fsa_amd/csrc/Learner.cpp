@@ -61,6 +61,10 @@ void Learner::SetHostCommunicator(int n, int r, wfsa_host_allreduce_fn fn, void*
     host_user = user;
 }
 
+void Learner::AbortCommunicator(const char* why) {
+    if (dev && nranks > 1) (void)wfsa_dev_comm_abort(dev, why);
+}
+
 void Learner::EnsureDevice() {
     if (dev) return;
     ThrowOnDevError(wfsa_dev_create(device, &dev), "wfsa_dev_create");

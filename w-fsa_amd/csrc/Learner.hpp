@@ -44,6 +44,9 @@ public:
     void SetCommunicator(int nranks, int rank, const uint8_t* unique_id);
     // the same over a host callback (wfsa_dev_comm_init_host)
     void SetHostCommunicator(int nranks, int rank, wfsa_host_allreduce_fn fn, void* user);
+    // this rank failed: the other ranks' current or next collective fails at
+    // once (wfsa_dev_comm_abort); a no-op before BuildFrom or on one rank
+    void AbortCommunicator(const char* why);
 
     // `corpus` weights must already be normalized over the whole corpus
     // (main.cpp renormalizes before BuildFrom).  With a communicator, every

@@ -4,8 +4,11 @@
 
 #include <rccl/rccl.h>
 
+#include <algorithm>
 #include <atomic>
 #include <chrono>
+#include <cmath>
+#include <cstdio>
 #include <condition_variable>
 #include <cstdlib>
 #include <cstring>
@@ -27,11 +30,21 @@ public:
         n_ = n;
         r_ = r;
     }
-    ~RcclCollective() override { (void)ncclCommDestroy(comm_); }
+    ~RcclCollective() override {
+        if (comm_) (void)ncclCommDestroy(comm_);
+    }
     const char* kind() const override { return "rccl"; }
     bool peer_default() const override { return true; }
+    void abort_transport(const std::string&) override {   // the other members' pending RCCL calls see a broken ring
+        if (comm_) (void)ncclCommAbort(comm_);
+        comm_ = nullptr;
+    }
     int transport_allreduce(void* buf, size_t n, RedOp op, hipStream_t s) override {
         if (n == 0) return 0;
+        if (!comm_) {
+            err_ = "the RCCL communicator was aborted";
+            return 1;
+        }
         ncclDataType_t t = op == RedOp::MaxU8 ? ncclUint8 : ncclDouble;
         ncclRedOp_t o = op == RedOp::SumF64 ? ncclSum : op == RedOp::MinF64 ? ncclMin : ncclMax;
         ncclResult_t r = ncclAllReduce(buf, buf, n, t, o, comm_, s);
@@ -62,21 +75,21 @@ struct LocalGroup {
     int op[kLocalMaxRanks] = {};
     int dev[kLocalMaxRanks] = {};
 
-    bool poisoned = false;   // a member timed out: the group is out of step for good
+    bool poisoned = false;   // a member timed out or failed: the group is out of step for good
+    std::string why;         // (under m) what poisoned it
+    int limit_s = 120;       // WFSA_GROUP_TIMEOUT_S when the group was made
 
-    // false on a timeout (a member that never arrives: a bug upstream,
-    // reported instead of hanging the process) or once the group is poisoned.
-    // A timeout poisons the group -- the late member's arrival would
-    // otherwise release a later barrier at the wrong count and combine
-    // buffers from different calls -- so every later call fails at once.
-    // WFSA_GROUP_TIMEOUT_S sets the limit (default 600 s: a healthy rank may
-    // do long host work, e.g. a sparse factorisation, between collectives).
+    // false on a timeout (a member that never arrives: a bug upstream, or a
+    // member that failed without aborting) or once the group is poisoned.  A
+    // timeout poisons the group -- the late member's arrival would otherwise
+    // release a later barrier at the wrong count and combine buffers from
+    // different calls -- so every later call fails at once.  A member that
+    // fails anywhere poisons it too (Collective::abort), which wakes every
+    // waiting member now.  WFSA_GROUP_TIMEOUT_S sets the limit (default 120 s,
+    // inside a test's limit; a healthy rank's host work between collectives,
+    // e.g. a sparse factorisation, is replicated on every rank, so members
+    // arrive together).
     bool barrier() {
-        static const int limit_s = [] {
-            const char* e = std::getenv("WFSA_GROUP_TIMEOUT_S");
-            const int v = e ? std::atoi(e) : 0;
-            return v > 0 ? v : 600;
-        }();
         std::unique_lock<std::mutex> lk(m);
         if (poisoned) return false;
         const uint64_t g0 = gen;
@@ -88,9 +101,20 @@ struct LocalGroup {
         }
         if (cv.wait_for(lk, std::chrono::seconds(limit_s), [&] { return gen != g0 || poisoned; }) && !poisoned)
             return true;
+        if (!poisoned) why = "a member did not arrive within WFSA_GROUP_TIMEOUT_S";
         poisoned = true;
         cv.notify_all();
         return false;
+    }
+    void poison(const std::string& w) {
+        std::lock_guard<std::mutex> lk(m);
+        if (!poisoned) why = w;
+        poisoned = true;
+        cv.notify_all();
+    }
+    std::string reason() {
+        std::lock_guard<std::mutex> lk(m);
+        return why;
     }
 };
 
@@ -132,6 +156,8 @@ public:
     }
     const char* kind() const override { return "local"; }
     bool same_process() const override { return true; }
+    int device() const override { return device_; }
+    void abort_transport(const std::string& why) override { g_->poison("member " + std::to_string(r_) + " aborted: " + why); }
     int transport_allreduce(void* buf, size_t n, RedOp op, hipStream_t s) override {
         const size_t esz = op == RedOp::MaxU8 ? 1 : 8;
         if (n * esz > tmp_bytes_) {
@@ -146,7 +172,7 @@ public:
         g_->count[r_] = n;
         g_->op[r_] = int(op);
         g_->dev[r_] = device_;
-        if (!g_->barrier()) return fail("in-process group: a member did not arrive in time (WFSA_GROUP_TIMEOUT_S), or the group failed before");
+        if (!g_->barrier()) return fail_group();
         Ptrs src{};
         for (int r = 0; r < n_; ++r) {
             if (g_->count[r] != n || g_->op[r] != int(op))   // every member must make the same call
@@ -170,15 +196,20 @@ public:
             if (hipGetLastError() != hipSuccess || hipStreamSynchronize(s) != hipSuccess)
                 return fail("rank reduction kernel failed");
         }
-        if (!g_->barrier()) return fail("in-process group: a member did not arrive in time (WFSA_GROUP_TIMEOUT_S), or the group failed before");
+        if (!g_->barrier()) return fail_group();
         if (n > 0 && hipMemcpyAsync(buf, tmp_, n * esz, hipMemcpyDeviceToDevice, s) != hipSuccess)
             return fail("copy of the reduced values failed");
         return 0;
     }
 
 private:
-    int fail(const char* m) {
+    int fail(const char* m) {   // the members are out of step now: poison the group
         err_ = m;
+        g_->poison(std::string("member ") + std::to_string(r_) + ": " + m);
+        return 1;
+    }
+    int fail_group() {
+        err_ = "in-process group failed: " + g_->reason();
         return 1;
     }
     std::shared_ptr<LocalGroup> g_;
@@ -232,6 +263,9 @@ std::unique_ptr<Collective> make_local_collective(int nranks, int rank, const ui
         if (!slot) {
             slot = std::make_shared<LocalGroup>();
             slot->n = n;
+            const char* e = std::getenv("WFSA_GROUP_TIMEOUT_S");
+            const int v = e ? std::atoi(e) : 0;
+            if (v > 0) slot->limit_s = v;
         }
         g = slot;
         if (++g->joined == n) g_reg.erase(serial);   // every member holds the group now
@@ -313,11 +347,23 @@ struct PeerArgs {
     int nranks, me;
     uint64_t seq;
     uint64_t timeout;   // s_memrealtime ticks (100 MHz)
-    unsigned* status;   // set to 1 on a timeout
+    unsigned* status;   // host-mapped: set to 1 when the call failed
 };
 
+// area layout: [2][nranks][kPeerCap] doubles, [2][nranks][kPeerMaxChunks]
+// flags, then the poison word (padded to 16 bytes)
+__host__ __device__ inline size_t peer_area_bytes(int nranks) {
+    return 2 * size_t(nranks) * kPeerCap * sizeof(double) + 2 * size_t(nranks) * kPeerMaxChunks * sizeof(uint64_t) + 16;
+}
 __device__ __forceinline__ uint64_t* peer_flags(double* area, int nranks) {
     return reinterpret_cast<uint64_t*>(area + 2 * size_t(nranks) * kPeerCap);
+}
+__device__ __forceinline__ uint64_t* peer_poison(double* area, int nranks) {
+    return peer_flags(area, nranks) + 2 * size_t(nranks) * kPeerMaxChunks;
+}
+
+__device__ __forceinline__ bool poisoned(double* area, int nranks) {
+    return __hip_atomic_load(peer_poison(area, nranks), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0;
 }
 
 __global__ __launch_bounds__(256) void peer_sum_kernel(PeerArgs a) {
@@ -325,41 +371,56 @@ __global__ __launch_bounds__(256) void peer_sum_kernel(PeerArgs a) {
     const int64_t b = int64_t(c) * kPeerChunk, e = min(a.n, b + kPeerChunk);
     const int par = int(a.seq & 1);
     const size_t my_slot = (size_t(par) * a.nranks + a.me) * kPeerCap;
-    // this rank's chunk into its slot of every member's area
-    for (int64_t i = b + threadIdx.x; i < e; i += blockDim.x) {
-        const double v = a.src[i];
-        for (int r = 0; r < a.nranks; ++r) a.area[r][my_slot + i] = v;
-    }
-    __threadfence_system();   // the slots before the flags, on every member
-    __syncthreads();
-    const size_t fl = (size_t(par) * a.nranks + a.me) * kPeerMaxChunks + c;
-    if (int(threadIdx.x) < a.nranks)
-        __hip_atomic_store(peer_flags(a.area[threadIdx.x], a.nranks) + fl, a.seq, __ATOMIC_RELEASE,
-                           __HIP_MEMORY_SCOPE_SYSTEM);
-    // every member's chunk c in this rank's area
     __shared__ int late;
-    if (threadIdx.x == 0) late = 0;
+    if (threadIdx.x == 0) late = poisoned(a.area[a.me], a.nranks) ? 1 : 0;   // a member failed before: no wait
     __syncthreads();
-    if (int(threadIdx.x) < a.nranks) {
-        const uint64_t* f = peer_flags(a.area[a.me], a.nranks) + (size_t(par) * a.nranks + threadIdx.x) * kPeerMaxChunks + c;
-        const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-        while (__hip_atomic_load(f, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) < a.seq) {
-            if (__builtin_amdgcn_s_memrealtime() - t0 > a.timeout) {
-                atomicOr(&late, 1);
-                break;
-            }
-            __builtin_amdgcn_s_sleep(2);
+    if (!late) {
+        // this rank's chunk into its slot of every member's area
+        for (int64_t i = b + threadIdx.x; i < e; i += blockDim.x) {
+            const double v = a.src[i];
+            for (int r = 0; r < a.nranks; ++r) a.area[r][my_slot + i] = v;
         }
+        __threadfence_system();   // the slots before the flags, on every member
+        __syncthreads();
+        const size_t fl = (size_t(par) * a.nranks + a.me) * kPeerMaxChunks + c;
+        if (int(threadIdx.x) < a.nranks)
+            __hip_atomic_store(peer_flags(a.area[threadIdx.x], a.nranks) + fl, a.seq, __ATOMIC_RELEASE,
+                               __HIP_MEMORY_SCOPE_SYSTEM);
+        // every member's chunk c in this rank's area; a poisoned area ends the wait
+        if (int(threadIdx.x) < a.nranks) {
+            const uint64_t* f = peer_flags(a.area[a.me], a.nranks) + (size_t(par) * a.nranks + threadIdx.x) * kPeerMaxChunks + c;
+            const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+            while (__hip_atomic_load(f, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) < a.seq) {
+                if (__builtin_amdgcn_s_memrealtime() - t0 > a.timeout || poisoned(a.area[a.me], a.nranks)) {
+                    atomicOr(&late, 1);
+                    break;
+                }
+                __builtin_amdgcn_s_sleep(2);
+            }
+        }
+        __threadfence_system();
+        __syncthreads();
     }
-    __threadfence_system();
-    __syncthreads();
-    if (late && threadIdx.x == 0) __hip_atomic_store(a.status, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    if (late) {   // every member's next call fails at entry; the host sees the status
+        if (int(threadIdx.x) < a.nranks)
+            __hip_atomic_store(peer_poison(a.area[threadIdx.x], a.nranks), uint64_t(1), __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_SYSTEM);
+        if (threadIdx.x == 0) __hip_atomic_store(a.status, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
     const double* mine = a.area[a.me] + size_t(par) * a.nranks * kPeerCap;
     for (int64_t i = b + threadIdx.x; i < e; i += blockDim.x) {
         double t = 0.0;
-        for (int r = 0; r < a.nranks; ++r) t += mine[size_t(r) * kPeerCap + i];   // rank order: deterministic
+        if (!late)
+            for (int r = 0; r < a.nranks; ++r) t += mine[size_t(r) * kPeerCap + i];   // rank order: deterministic
         a.dst[i] = late ? __builtin_nan("") : t;
     }
+}
+
+// the poison word of every area (Collective::abort)
+__global__ void peer_poison_kernel(PeerArgs a) {
+    if (int(threadIdx.x) < a.nranks)
+        __hip_atomic_store(peer_poison(a.area[threadIdx.x], a.nranks), uint64_t(1), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 struct PeerBlob {   // what a rank publishes at set-up
@@ -373,8 +434,8 @@ static_assert(sizeof(hipIpcMemHandle_t) <= 64, "IPC handle size");
 // groups, never handed back to HIP: freed, their pages went on (still mapped
 // uncached) to ordinary allocations of later contexts, where the evaluation
 // kernels' fp64 atomic adds were lost -- a context made after an in-process
-// peer group summed gradients short (tests/test_gpu_multiprocess.py,
-// test_context_after_peer_group_is_exact).
+// peer group summed gradients short (round 3; tests/test_gpu_multiprocess.py,
+// test_context_after_peer_selftest_is_exact).
 std::mutex g_uncached_mu;
 std::multimap<size_t, void*> g_uncached_free;
 
@@ -402,6 +463,12 @@ void uncached_put(void* p, size_t bytes) {
     g_uncached_free.emplace(bytes, p);
 }
 
+double peer_timeout_s() {
+    const char* e = std::getenv("WFSA_PEER_TIMEOUT_S");   // (read per set-up: tests shorten it)
+    const double v = e ? std::atof(e) : 0.0;
+    return v > 0 ? v : 120.0;
+}
+
 }  // namespace
 
 class PeerSum {
@@ -413,25 +480,41 @@ public:
             (void)hipDeviceSynchronize();
             uncached_put(own_, own_bytes_);
         }
-        if (status_) (void)hipFree(status_);
+        if (status_h_) (void)hipHostFree(status_h_);
+        if (aux_) (void)hipStreamDestroy(aux_);
     }
 
-    // maps every member's area; the transport carries the exchange.  Every
-    // member makes the same calls (false: err says why; the caller agrees
-    // with the others before using the path)
-    bool setup(Collective& c, bool same_process, hipStream_t s,
-               const std::function<int(void*, size_t, RedOp)>& xfer, std::string& err) {
-        n_ = c.nranks();
-        me_ = c.rank();
-        const size_t bytes = 2 * size_t(n_) * kPeerCap * sizeof(double) +
-                             2 * size_t(n_) * kPeerMaxChunks * sizeof(uint64_t);
-        own_ = static_cast<double*>(uncached_get(bytes));
-        own_bytes_ = bytes;
-        bool ok = own_ != nullptr && hipMemsetAsync(own_, 0, bytes, s) == hipSuccess &&
-                  hipMalloc(reinterpret_cast<void**>(&status_), sizeof(unsigned)) == hipSuccess &&
-                  hipMemsetAsync(status_, 0, sizeof(unsigned), s) == hipSuccess &&
+    // this rank's area and status word (false: err says why).  Always safe to
+    // follow with exchange(): a failed set-up still takes part in it.
+    bool alloc(int nranks, int me, hipStream_t s, std::string& err) {
+        n_ = nranks;
+        me_ = me;
+        own_bytes_ = peer_area_bytes(n_);
+        own_ = static_cast<double*>(uncached_get(own_bytes_));
+        bool ok = own_ != nullptr && hipMemsetAsync(own_, 0, own_bytes_, s) == hipSuccess &&
+                  hipHostMalloc(reinterpret_cast<void**>(&status_h_), sizeof(unsigned),
+                                hipHostMallocMapped | hipHostMallocCoherent | hipHostMallocPortable) == hipSuccess &&
+                  hipHostGetDevicePointer(reinterpret_cast<void**>(&status_d_), status_h_, 0) == hipSuccess &&
+                  hipStreamCreateWithFlags(&aux_, hipStreamNonBlocking) == hipSuccess &&
                   hipStreamSynchronize(s) == hipSuccess;
-        if (!ok) (void)hipGetLastError();
+        if (!ok) {
+            (void)hipGetLastError();
+            err = "peer set-up: allocation of the receive area failed";
+        } else {
+            *status_h_ = 0;
+        }
+        args_.nranks = n_;
+        args_.me = me_;
+        args_.status = status_d_;
+        args_.timeout = uint64_t(peer_timeout_s() * 1e8);
+        return ok;
+    }
+
+    // maps every member's area; xfer carries the exchange (a byte max-
+    // reduction over the transport, dbuf its device buffer).  Every member
+    // makes the same calls whatever happened before (ok in/out).
+    bool exchange(bool ok, bool same_process, hipStream_t s, void* dbuf,
+                  const std::function<int(void*, size_t, RedOp)>& xfer, std::string& err) {
         std::vector<PeerBlob> blobs(static_cast<size_t>(n_));
         std::memset(blobs.data(), 0, blobs.size() * sizeof(PeerBlob));
         PeerBlob& mine = blobs[size_t(me_)];
@@ -440,27 +523,24 @@ public:
             ok = hipIpcGetMemHandle(&h, own_) == hipSuccess;
             if (ok) std::memcpy(mine.handle, &h, sizeof h);
             else (void)hipGetLastError();
+            if (!ok) err = "peer set-up: hipIpcGetMemHandle failed";
         }
         mine.ptr = reinterpret_cast<uint64_t>(own_);
         mine.pid = int32_t(getpid());
-        // exchange: every rank's blob in its own slot, the rest zero, max-reduced
-        void* dbuf = nullptr;
+        mine.pad = ok ? 0 : 1;   // (a member whose area is unusable says so)
         const size_t bb = blobs.size() * sizeof(PeerBlob);
-        if (hipMalloc(&dbuf, bb) != hipSuccess) {
-            err = "peer set-up: allocation failed";
-            return false;
-        }
         if (hipMemcpyAsync(dbuf, blobs.data(), bb, hipMemcpyHostToDevice, s) != hipSuccess ||
             xfer(dbuf, bb, RedOp::MaxU8) != 0 ||
             hipMemcpyAsync(blobs.data(), dbuf, bb, hipMemcpyDeviceToHost, s) != hipSuccess ||
             hipStreamSynchronize(s) != hipSuccess) {
-            (void)hipFree(dbuf);
             err = "peer set-up: exchange failed";
-            return false;
+            return false;   // (the transport itself failed: the caller reports it)
         }
-        (void)hipFree(dbuf);
         for (int r = 0; r < n_ && ok; ++r) {
-            if (r == me_) {
+            if (blobs[size_t(r)].pad) {
+                ok = false;
+                err = "peer set-up: another member's area is unusable";
+            } else if (r == me_) {
                 args_.area[r] = own_;
             } else if (same_process) {
                 args_.area[r] = reinterpret_cast<double*>(blobs[size_t(r)].ptr);
@@ -474,21 +554,14 @@ public:
                     opened_[r] = true;
                 } else {
                     (void)hipGetLastError();
+                    err = "peer set-up: a member's area could not be mapped";
                 }
             }
         }
-        if (!ok) err = "peer set-up: a member's area could not be mapped";
-        static const double limit_s = [] {
-            const char* e = std::getenv("WFSA_PEER_TIMEOUT_S");
-            const double v = e ? std::atof(e) : 0.0;
-            return v > 0 ? v : 10.0;
-        }();
-        args_.nranks = n_;
-        args_.me = me_;
-        args_.status = status_;
-        args_.timeout = uint64_t(limit_s * 1e8);
-        return ok;
+        mapped_ = ok;
+        return true;
     }
+    bool mapped() const { return mapped_; }
 
     int run(double* buf, size_t n, hipStream_t s) {
         PeerArgs a = args_;
@@ -502,21 +575,32 @@ public:
         return hipGetLastError() == hipSuccess ? 0 : 1;
     }
 
-    // a wait that gave up since the set-up (reads the status word)
-    bool timed_out(hipStream_t s) {
-        unsigned h = 0;
-        if (hipMemcpyAsync(&h, status_, sizeof h, hipMemcpyDeviceToHost, s) != hipSuccess ||
-            hipStreamSynchronize(s) != hipSuccess)
-            return true;
-        return h != 0;
+    // a call failed (this rank's wait gave up, or it found its area poisoned)
+    bool failed() const { return __atomic_load_n(status_h_, __ATOMIC_ACQUIRE) != 0; }
+
+    // poison every member's area from the host side (on a stream of its own,
+    // not waited for: the member's own stream may hold a waiting kernel)
+    void poison_all() {
+        if (!mapped_) return;
+        hipLaunchKernelGGL(peer_poison_kernel, dim3(1), dim3(64), 0, aux_, args_);
+        (void)hipGetLastError();
     }
+
+    // selftest access
+    PeerArgs& args() { return args_; }
+    double* own() const { return own_; }
+    unsigned* status_host() const { return status_h_; }
+    uint64_t seq() const { return seq_; }
 
 private:
     int n_ = 0, me_ = 0;
     double* own_ = nullptr;
     size_t own_bytes_ = 0;
-    unsigned* status_ = nullptr;
+    unsigned* status_h_ = nullptr;
+    unsigned* status_d_ = nullptr;
+    hipStream_t aux_ = nullptr;
     bool opened_[kLocalMaxRanks] = {};
+    bool mapped_ = false;
     uint64_t seq_ = 0;
     PeerArgs args_{};
 };
@@ -527,63 +611,128 @@ const char* Collective::peer_state() const {
     return peer_st_ == 1 ? "on" : peer_st_ == -1 ? "off" : peer_st_ == -2 ? "failed" : "untried";
 }
 
-// Decides once, on the first sum that fits, whether the peer path is used:
-// the set-up on every rank, then a check sum (rank r contributes (r + 1)(i + 1))
-// through it, then the ranks agree over the transport -- any failure anywhere
-// and every rank stays on the transport.
+// Decides once, on the first sum that fits, whether the peer path is used.
+// Every member makes the same transport calls whatever fails locally (a
+// local failure is carried as its "bad" byte), so no member is left waiting:
+// (1) the members' devices (the path is refused when two share a device in
+// one process, see collective.hpp), (2) the areas' set-up and exchange, (3) a
+// check sum (rank r contributes (r + 1)(i + 1)) through the path, (4) the
+// ranks agree -- any failure anywhere and every rank stays on the transport.
 int Collective::try_peer(hipStream_t s) {
     const char* pe = std::getenv("WFSA_PEER");   // (read per communicator: tests switch it)
     const int want = pe && pe[0] ? (pe[0] == '0' ? 0 : 1) : -1;
     const bool on = want < 0 ? peer_default() : want == 1;
     if (!on || n_ < 2 || n_ > kLocalMaxRanks) {
         peer_st_ = -1;
+        peer_why_ = !on ? "not requested (WFSA_PEER)" : "group size";
         return 0;
     }
-    auto xfer = [&](void* b, size_t n, RedOp op) { return transport_allreduce(b, n, op, s); };
-    auto p = std::make_unique<PeerSum>();
-    std::string why;
-    bool ok = p->setup(*this, same_process(), s, xfer, why);
     constexpr size_t kCheck = 3000;   // spans three chunks
-    std::vector<double> h(kCheck);
-    double* d = nullptr;
-    if (hipMalloc(reinterpret_cast<void**>(&d), kCheck * sizeof(double)) != hipSuccess) return 1;
+    const size_t dbytes = std::max(kCheck * sizeof(double), size_t(kLocalMaxRanks) * sizeof(PeerBlob));
+    uint8_t* d = nullptr;
+    if (hipMalloc(reinterpret_cast<void**>(&d), dbytes) != hipSuccess) {
+        (void)hipGetLastError();
+        err_ = "peer set-up: no device memory for the agreement";
+        return 1;   // (the caller fails and aborts the communicator: every member hears of it)
+    }
+    auto xfer = [&](void* b, size_t n, RedOp op) { return transport_allreduce(b, n, op, s); };
+    auto agree = [&](bool mine_ok, bool& all_ok) {   // a byte per rank, max-reduced
+        std::vector<uint8_t> bad(size_t(n_), 0);
+        bad[size_t(r_)] = mine_ok ? 0 : 1;
+        if (hipMemcpyAsync(d, bad.data(), bad.size(), hipMemcpyHostToDevice, s) != hipSuccess) return 1;
+        if (transport_allreduce(d, bad.size(), RedOp::MaxU8, s)) return 1;
+        if (hipMemcpyAsync(bad.data(), d, bad.size(), hipMemcpyDeviceToHost, s) != hipSuccess ||
+            hipStreamSynchronize(s) != hipSuccess)
+            return 1;
+        all_ok = true;
+        for (uint8_t b : bad) all_ok &= b == 0;
+        return 0;
+    };
+    auto done = [&](int rc) {
+        (void)hipFree(d);
+        return rc;
+    };
+    std::string why;
+    // (1) devices: a byte per rank holding its device + 1
+    {
+        std::vector<uint8_t> dv(size_t(n_), 0);
+        dv[size_t(r_)] = uint8_t(std::max(0, device()) + 1);
+        if (hipMemcpyAsync(d, dv.data(), dv.size(), hipMemcpyHostToDevice, s) != hipSuccess ||
+            transport_allreduce(d, dv.size(), RedOp::MaxU8, s) != 0 ||
+            hipMemcpyAsync(dv.data(), d, dv.size(), hipMemcpyDeviceToHost, s) != hipSuccess ||
+            hipStreamSynchronize(s) != hipSuccess)
+            return done(1);
+        if (same_process())
+            for (int a = 0; a < n_; ++a)
+                for (int b = a + 1; b < n_; ++b)
+                    if (dv[size_t(a)] == dv[size_t(b)]) {
+                        peer_st_ = -1;
+                        peer_why_ = "members share a device in one process (their kernels need not run concurrently)";
+                        if (std::getenv("WFSA_VERBOSE"))
+                            std::fprintf(stderr, "[wfsa] rank %d: peer all-reduce off: %s\n", r_, peer_why_.c_str());
+                        return done(0);
+                    }
+    }
+    // (2) areas
+    auto p = std::make_unique<PeerSum>();
+    bool ok = p->alloc(n_, r_, s, why);
+    if (!p->exchange(ok, same_process(), s, d, xfer, why)) return done(1);
+    ok = p->mapped();
+    // (3) the check sum
     if (ok) {
+        std::vector<double> h(kCheck);
         for (size_t i = 0; i < kCheck; ++i) h[i] = double(r_ + 1) * double(i + 1);
-        ok = hipMemcpyAsync(d, h.data(), kCheck * sizeof(double), hipMemcpyHostToDevice, s) == hipSuccess &&
-             p->run(d, kCheck, s) == 0 &&
-             hipMemcpyAsync(h.data(), d, kCheck * sizeof(double), hipMemcpyDeviceToHost, s) == hipSuccess &&
-             hipStreamSynchronize(s) == hipSuccess && !p->timed_out(s);
+        double* dd = reinterpret_cast<double*>(d);
+        ok = hipMemcpyAsync(dd, h.data(), kCheck * sizeof(double), hipMemcpyHostToDevice, s) == hipSuccess &&
+             p->run(dd, kCheck, s) == 0 &&
+             hipMemcpyAsync(h.data(), dd, kCheck * sizeof(double), hipMemcpyDeviceToHost, s) == hipSuccess &&
+             hipStreamSynchronize(s) == hipSuccess && !p->failed();
         const double tri = double(n_) * double(n_ + 1) / 2.0;
         for (size_t i = 0; i < kCheck && ok; ++i) ok = h[i] == tri * double(i + 1);
+        if (!ok && why.empty()) why = "the check sum through the peer path was wrong or timed out";
     }
-    // agree: a byte per rank, max-reduced over the transport
-    std::vector<uint8_t> bad(size_t(n_), 0);
-    bad[size_t(r_)] = ok ? 0 : 1;
-    int rc = hipMemcpyAsync(d, bad.data(), bad.size(), hipMemcpyHostToDevice, s) == hipSuccess ? 0 : 1;
-    if (!rc) rc = transport_allreduce(d, bad.size(), RedOp::MaxU8, s);
-    if (!rc)
-        rc = (hipMemcpyAsync(bad.data(), d, bad.size(), hipMemcpyDeviceToHost, s) == hipSuccess &&
-              hipStreamSynchronize(s) == hipSuccess) ? 0 : 1;
-    (void)hipFree(d);
-    if (rc) return 1;
-    bool all = true;
-    for (uint8_t b : bad) all &= b == 0;
+    // (4) agree
+    bool all = false;
+    if (agree(ok, all)) return done(1);
     if (std::getenv("WFSA_VERBOSE"))
         std::fprintf(stderr, "[wfsa] rank %d: peer all-reduce %s%s%s\n", r_, all ? "on" : "failed",
                      why.empty() ? "" : ": ", why.c_str());
     if (all) {
         peer_ = std::move(p);
         peer_st_ = 1;
+        peer_why_.clear();
     } else {
         peer_st_ = -2;
+        peer_why_ = why.empty() ? "another member's set-up or check failed" : why;
+    }
+    return done(0);
+}
+
+int Collective::check() {
+    if (aborted_) {
+        err_ = "communicator aborted: " + abort_why_;
+        return 1;
+    }
+    if (peer_ && peer_->failed()) {
+        err_ = "peer all-reduce: a member did not arrive within WFSA_PEER_TIMEOUT_S, or failed";
+        return 1;
     }
     return 0;
 }
 
+void Collective::abort(const char* why) {
+    if (aborted_) return;
+    aborted_ = true;
+    abort_why_ = why ? why : "";
+    if (peer_) peer_->poison_all();
+    abort_transport(abort_why_);
+}
+
 int Collective::allreduce(void* buf, size_t n, RedOp op, hipStream_t s) {
+    if (check()) return 1;
     if (op == RedOp::SumF64 && n > 0 && n <= kPeerCap) {
         if (peer_st_ == 0 && try_peer(s)) {
-            err_ = "peer all-reduce set-up failed";
+            if (err_.empty()) err_ = "peer all-reduce set-up failed";
             return 1;
         }
         if (peer_st_ == 1) {
@@ -595,6 +744,117 @@ int Collective::allreduce(void* buf, size_t n, RedOp op, hipStream_t s) {
         }
     }
     return transport_allreduce(buf, n, op, s);
+}
+
+// ---- the peer kernel on one device (collective.hpp: peer_selftest) --------
+
+namespace {
+
+__global__ void selftest_fill_kernel(PeerArgs a, int rank, uint64_t seq, int with_flags) {
+    // what member `rank` would have stored into this rank's area: its slot
+    // (value (rank + 1) * (i + 1) + i * 1e-3) and the flags of every chunk
+    const int par = int(seq & 1);
+    double* area = a.area[a.me];
+    const size_t slot = (size_t(par) * a.nranks + rank) * kPeerCap;
+    for (int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < a.n; i += int64_t(gridDim.x) * blockDim.x)
+        area[slot + size_t(i)] = double(rank + 1) * double(i + 1) + double(i) * 1e-3;
+    if (with_flags && blockIdx.x == 0) {
+        const int chunks = int((a.n + kPeerChunk - 1) / kPeerChunk);
+        for (int c = int(threadIdx.x); c < chunks; c += int(blockDim.x))
+            __hip_atomic_store(peer_flags(area, a.nranks) + (size_t(par) * a.nranks + rank) * kPeerMaxChunks + c, seq,
+                               __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+}
+
+}  // namespace
+
+int peer_selftest(int nranks, int64_t n, double timeout_s, int mode, double out[4], std::string& err) {
+    if (nranks < 2 || nranks > kLocalMaxRanks || n < 1 || n > int64_t(kPeerCap) || mode < 0 || mode > 2 ||
+        !(timeout_s > 0)) {
+        err = "peer selftest: bad arguments";
+        return 1;
+    }
+    hipStream_t s = nullptr;
+    if (hipStreamCreate(&s) != hipSuccess) {
+        err = "peer selftest: no stream";
+        return 1;
+    }
+    // rank 0's PeerSum; the other members' areas are plain local areas of the
+    // same layout (only their poison words and rank 0's stores land there)
+    PeerSum p;
+    std::vector<void*> others;
+    auto cleanup = [&](int rc) {
+        (void)hipStreamSynchronize(s);
+        for (void* o : others) uncached_put(o, peer_area_bytes(nranks));
+        (void)hipStreamDestroy(s);
+        return rc;
+    };
+    if (!p.alloc(nranks, 0, s, err)) return cleanup(1);
+    PeerArgs& a = p.args();
+    a.area[0] = p.own();
+    for (int r = 1; r < nranks; ++r) {
+        void* o = uncached_get(peer_area_bytes(nranks));
+        if (!o || hipMemsetAsync(o, 0, peer_area_bytes(nranks), s) != hipSuccess) {
+            err = "peer selftest: allocation failed";
+            return cleanup(1);
+        }
+        others.push_back(o);
+        a.area[r] = static_cast<double*>(o);
+    }
+    a.timeout = uint64_t(timeout_s * 1e8);
+    double* buf = nullptr;
+    if (hipMalloc(reinterpret_cast<void**>(&buf), size_t(n) * sizeof(double)) != hipSuccess) {
+        err = "peer selftest: allocation failed";
+        return cleanup(1);
+    }
+    std::vector<double> h(static_cast<size_t>(n));
+    for (int64_t i = 0; i < n; ++i) h[size_t(i)] = double(i + 1) + double(i) * 1e-3;   // rank 0's own values
+    const uint64_t seq = p.seq() + 1;
+    PeerArgs fa = a;
+    fa.n = n;
+    bool ok = hipMemcpyAsync(buf, h.data(), size_t(n) * sizeof(double), hipMemcpyHostToDevice, s) == hipSuccess;
+    for (int r = 1; r < nranks && ok; ++r) {
+        const int flags = mode == 1 && r == nranks - 1 ? 0 : 1;   // mode 1: the last member never arrives
+        hipLaunchKernelGGL(selftest_fill_kernel, dim3(64), dim3(256), 0, s, fa, r, seq, flags);
+        ok = hipGetLastError() == hipSuccess;
+    }
+    if (ok && mode == 2) {   // another member failed before this call
+        hipLaunchKernelGGL(peer_poison_kernel, dim3(1), dim3(64), 0, s, a);
+        ok = hipGetLastError() == hipSuccess;
+    }
+    ok = ok && hipStreamSynchronize(s) == hipSuccess;
+    const auto t0 = std::chrono::steady_clock::now();
+    ok = ok && p.run(buf, size_t(n), s) == 0 && hipStreamSynchronize(s) == hipSuccess;
+    const double el = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    std::vector<double> got(static_cast<size_t>(n));
+    ok = ok && hipMemcpy(got.data(), buf, size_t(n) * sizeof(double), hipMemcpyDeviceToHost) == hipSuccess;
+    int poisoned_areas = 0;
+    for (int r = 0; r < nranks && ok; ++r) {
+        uint64_t w = 0;
+        const uint8_t* base = reinterpret_cast<const uint8_t*>(a.area[r]) + peer_area_bytes(nranks) - 16;
+        ok = hipMemcpy(&w, base, sizeof w, hipMemcpyDeviceToHost) == hipSuccess;
+        poisoned_areas += w != 0;
+    }
+    (void)hipFree(buf);
+    if (!ok) {
+        err = "peer selftest: a HIP call failed";
+        return cleanup(1);
+    }
+    double metric = 0.0;
+    if (mode == 0) {
+        for (int64_t i = 0; i < n; ++i) {
+            double want = 0.0;   // rank order, as the kernel sums
+            for (int r = 0; r < nranks; ++r) want += double(r + 1) * double(i + 1) + double(i) * 1e-3;
+            metric = std::max(metric, std::fabs(got[size_t(i)] - want));
+        }
+    } else {
+        for (double v : got) metric += std::isnan(v) ? 1.0 : 0.0;
+    }
+    out[0] = metric;
+    out[1] = double(*p.status_host());
+    out[2] = double(poisoned_areas);
+    out[3] = el;
+    return cleanup(0);
 }
 
 }  // namespace wfsa

@@ -45,12 +45,31 @@ public:
     // the one-shot peer all-reduce: "on", "off", "failed" (its set-up check
     // disagreed on some rank: the transport is used), "untried"
     const char* peer_state() const;
+    // why the peer path is off or failed ("" when on or untried)
+    const char* peer_reason() const { return peer_why_.c_str(); }
+
+    // 0 while the group is healthy; 1 (last_error() says why) once a peer
+    // wait gave up, another member poisoned the group, or abort() ran.  Free
+    // to call at any host sync point: the peer kernels report through
+    // host-mapped memory.
+    int check();
+    // this member failed: make every other member's next collective (or the
+    // one it is waiting in) fail at once instead of waiting for its timeout.
+    // The in-process group is poisoned, the peer areas of every member get
+    // their poison word, an RCCL communicator is aborted.  Every later call
+    // on this communicator fails.
+    void abort(const char* why);
+    bool aborted() const { return aborted_; }
 
 protected:
     // the transport's own all-reduce
     virtual int transport_allreduce(void* buf, size_t n, RedOp op, hipStream_t s) = 0;
+    // the transport's part of abort()
+    virtual void abort_transport(const std::string& why) {}
     // the members share this process's address space (no IPC mapping)
     virtual bool same_process() const { return false; }
+    // the device ordinal this member's kernels run on
+    virtual int device() const { return -1; }
     // the peer path by default (WFSA_PEER=1 / 0 overrides)
     virtual bool peer_default() const { return false; }
     int n_ = 1, r_ = 0;
@@ -60,6 +79,9 @@ private:
     int try_peer(hipStream_t s);
     std::unique_ptr<PeerSum> peer_;
     int peer_st_ = 0;   // 0 untried, 1 on, -1 off, -2 failed
+    std::string peer_why_;
+    bool aborted_ = false;
+    std::string abort_why_;
 };
 
 // One-shot peer all-reduce of doubles: every rank owns an area
@@ -71,14 +93,33 @@ private:
 // chunk's flags of all ranks in its own area and sums the slots in rank
 // order -- deterministic, stream-ordered, no host step.  The parity (call
 // sequence & 1) keeps a fast rank from overwriting slots a slow one still
-// reads.  A wait gives up after WFSA_PEER_TIMEOUT_S (default 10 s): the
-// result becomes NaN and the status word is set, never a hang.
+// reads.  A wait gives up after WFSA_PEER_TIMEOUT_S (default 120 s, the
+// in-process group's barrier limit): the result becomes NaN, the rank's
+// host-mapped status word is set and a poison word goes into EVERY member's
+// area, so every member's next peer call fails at entry without waiting;
+// Collective::check() turns the status into an error at the next host sync
+// point -- an error on every rank, never a hang and never a silent NaN.
+// The peer kernels of the members must run concurrently: members on distinct
+// devices, or in distinct processes (distinct hardware queues).  Two contexts
+// of one process on one device have no such guarantee -- HIP may put their
+// streams on one hardware queue, where a spinning kernel holds back the
+// other -- so an in-process group on one device keeps the transport.
 constexpr size_t kPeerCap = size_t(1) << 16;      // doubles per rank slot (512 KiB)
 constexpr int kPeerChunk = 1024;                  // doubles per block
 constexpr int kPeerMaxChunks = int(kPeerCap / kPeerChunk);
 
 constexpr int kCommIdBytes = 128;   // WFSA_COMM_ID_BYTES
 constexpr int kLocalMaxRanks = 16;
+
+// Checks the peer kernel on one device without a second process: the other
+// members' areas are local and their contributions / flags are written
+// beforehand (mode 0: all present, the sum must equal the rank-order sum;
+// mode 1: member `nranks-1` never arrives, the call must give up after
+// timeout_s with NaN, the status set and every area poisoned; mode 2: the
+// own area poisoned before the call, which must fail at entry, well inside
+// timeout_s).  out[0..3] = {max |error| (mode 0) or NaN count, status,
+// poisoned areas, elapsed seconds}.  0 = ran (the caller judges out), else err.
+int peer_selftest(int nranks, int64_t n, double timeout_s, int mode, double out[4], std::string& err);
 
 // a fresh in-process group id (magic prefix, serial, size)
 void local_group_id(int nranks, uint8_t id[kCommIdBytes]);

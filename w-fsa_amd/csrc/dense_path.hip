@@ -48,10 +48,21 @@ constexpr int kBkStep = 32, kBkGrad = 16;
 // SIMD hide each other's LDS and barrier time), 4 for the gradient GEMM (two
 // blocks per CU do that)
 constexpr int kNwStep = 8, kNwGrad = 4;
-// padded LDS row (doubles): BK + 2 == 2 (mod 32) keeps a 64-lane fragment
-// read conflict free
+// LDS images of an operand slice (128 rows r x BK k), never transposed on
+// the way in, so every store is a plain conflict-free 16-byte write:
+//  * KC (the operand's rows contiguous along k in memory): [r][k], padded
+//    row of BK + 2 doubles (BK + 2 == 2 mod 32: a 64-lane fragment read
+//    (16 r x 4 k) is conflict free);
+//  * RC (memory rows run along r): [k][r], padded row of kLdn = 144
+//    doubles (2 kLdn == 32 mod 64: the fragment read's two k rows of a
+//    32-lane group fall on the two bank halves).
+// (Round 2's kernels stored RC slices transposed into [r][k]: 8-byte
+// stores four-way conflicted, a burst at every slice end while the MFMA
+// pipe idled -- 0.67 of the fp64 peak.)
 template <int BK> constexpr int ldk() { return BK + 2; }
-template <int BK> constexpr int stage() { return 2 * kT * ldk<BK>(); }   // doubles per stage (A and B)
+constexpr int kLdn = kDenseTile + 16;
+template <bool KC, int BK> constexpr int op_size() { return KC ? kT * ldk<BK>() : BK * kLdn; }
+template <int MODE, int BK> constexpr int stage();   // doubles per stage (A and B), below
 constexpr int kRedThreads = 128;      // dense_reduce: one column per thread
 // row pitch of the row-slot buffers = np + 16 doubles: a 128-row tile read
 // along k then spreads over memory channels and L2 sets (a power-of-two pitch
@@ -97,7 +108,7 @@ struct GemmArgs {
 // Global -> registers -> LDS staging of one 128 x 16 operand slice.  KC: the
 // operand's row r is contiguous along k (element (r, k) at base[r ld + k]);
 // RC: rows of memory run along the operand's rows (element (r, k) at
-// base[k ld + r]).  Either way LDS holds [r][k] (kLdk stride).
+// base[k ld + r]).  LDS holds KC slices as [r][k], RC slices as [k][r].
 // chunks of 16 bytes per thread for one 128 x BK slice
 template <int BK, int NT> constexpr int slice_chunks() { return kT * BK / 2 / NT; }
 
@@ -129,11 +140,12 @@ __device__ __forceinline__ void store_slice(double* __restrict__ s, int tid, con
             *reinterpret_cast<double2*>(s + row * L + 2 * kp) = v[c];
         } else {
             const int kk = idx >> 6, rp = idx & 63;
-            s[(2 * rp) * L + kk] = v[c].x;
-            s[(2 * rp + 1) * L + kk] = v[c].y;
+            *reinterpret_cast<double2*>(s + kk * kLdn + 2 * rp) = v[c];
         }
     }
 }
+
+template <int MODE, int BK> constexpr int stage() { return op_size<MODE != 2, BK>() + op_size<false, BK>(); }
 
 // NW waves per 128 x 128 block: 2 x (NW / 2), each a 64 x (256 / NW) tile
 // of 16 x 16 MFMA tiles (NJ of them per row of tiles)
@@ -141,7 +153,7 @@ template <int MODE, int BK, int NW>
 __global__ __launch_bounds__(NW * 64, 2) void dense_gemm_kernel(GemmArgs a) {
     if (a.halted && *a.halted) return;
     constexpr int NT = NW * 64, NWN = NW / 2, NJ = 16 / NW, WCOLS = 16 * NJ;
-    constexpr int kLdk = ldk<BK>(), kStage = stage<BK>();
+    constexpr int kLdk = ldk<BK>(), kStage = stage<MODE, BK>();
     constexpr int CH = slice_chunks<BK, NT>();
     __shared__ __attribute__((aligned(16))) double lds[2 * kStage];
     __shared__ double red[NWN][kT];
@@ -218,7 +230,7 @@ __global__ __launch_bounds__(NW * 64, 2) void dense_gemm_kernel(GemmArgs a) {
         load_slice<B_KC, BK, NT>(xb, ldb, c0, 0, tid, vb);
         row_scalars();   // its loads overlap the first slice's
         store_slice<A_KC, BK, NT>(lds, tid, va);
-        store_slice<B_KC, BK, NT>(lds + kT * kLdk, tid, vb);
+        store_slice<B_KC, BK, NT>(lds + op_size<A_KC, BK>(), tid, vb);
         __syncthreads();
         for (int64_t kt = 0; kt < nk; ++kt) {
             const bool more = kt + 1 < nk;
@@ -227,14 +239,16 @@ __global__ __launch_bounds__(NW * 64, 2) void dense_gemm_kernel(GemmArgs a) {
                 load_slice<B_KC, BK, NT>(xb, ldb, c0, (kt + 1) * BK, tid, vb);
             }
             const double* As = lds + (kt & 1) * kStage;
-            const double* Bs = As + kT * kLdk;
+            const double* Bs = As + op_size<A_KC, BK>();
 #pragma unroll
             for (int kk = 0; kk < BK / 4; ++kk) {
                 double av[4], bv[NJ];
 #pragma unroll
-                for (int i = 0; i < 4; ++i) av[i] = As[(wm * 64 + i * 16 + (lane & 15)) * kLdk + kk * 4 + (lane >> 4)];
+                for (int i = 0; i < 4; ++i)
+                    av[i] = A_KC ? As[(wm * 64 + i * 16 + (lane & 15)) * kLdk + kk * 4 + (lane >> 4)]
+                                 : As[(kk * 4 + (lane >> 4)) * kLdn + wm * 64 + i * 16 + (lane & 15)];
 #pragma unroll
-                for (int j = 0; j < NJ; ++j) bv[j] = Bs[(wn * WCOLS + j * 16 + (lane & 15)) * kLdk + kk * 4 + (lane >> 4)];
+                for (int j = 0; j < NJ; ++j) bv[j] = Bs[(kk * 4 + (lane >> 4)) * kLdn + wn * WCOLS + j * 16 + (lane & 15)];
 #pragma unroll
                 for (int i = 0; i < 4; ++i)
 #pragma unroll
@@ -244,7 +258,7 @@ __global__ __launch_bounds__(NW * 64, 2) void dense_gemm_kernel(GemmArgs a) {
             if (more) {
                 double* s = lds + ((kt + 1) & 1) * kStage;
                 store_slice<A_KC, BK, NT>(s, tid, va);
-                store_slice<B_KC, BK, NT>(s + kT * kLdk, tid, vb);
+                store_slice<B_KC, BK, NT>(s + op_size<A_KC, BK>(), tid, vb);
             }
             __syncthreads();
         }

@@ -90,6 +90,7 @@ public:
     int32_t rows() const { return R_; }
     int32_t steps() const { return T_; }
     int32_t np() const { return np_; }
+    bool blas() const { return use_blas_ && blas_; }
     int64_t total_symbols() const { return total_sym_; }
     // algorithmic fp64 flops of one evaluation: three GEMMs of 2 np^2 per
     // string position (forward, backward, gradient)

@@ -71,6 +71,16 @@ int guarded(F&& f) {
     return WFSA_ERR_ARG;
 }
 
+// guarded() for a learner call that may sit between rank collectives: a
+// failure on this rank aborts its communicator (wfsa_dev_comm_abort), so the
+// other ranks fail at their current or next collective instead of waiting
+template <class F>
+int rank_guarded(wfsa_learner* l, F&& f) {
+    const int rc = guarded(std::forward<F>(f));
+    if (rc != WFSA_OK) l->base->AbortCommunicator(g_host_error.c_str());
+    return rc;
+}
+
 int null_arg(const char* what) {
     g_host_error = std::string("null argument: ") + what;
     return WFSA_ERR_ARG;
@@ -219,6 +229,12 @@ int wfsa_learner_set_comm(wfsa_learner* l, int nranks, int rank, const uint8_t i
     return guarded([&] { l->host(true).SetCommunicator(nranks, rank, id); });
 }
 
+int wfsa_learner_comm_abort(wfsa_learner* l, const char* why) {
+    if (!l) return null_arg("learner");
+    l->base->AbortCommunicator(why ? why : "wfsa_learner_comm_abort");
+    return WFSA_OK;
+}
+
 int wfsa_learner_set_comm_host(wfsa_learner* l, int nranks, int rank, wfsa_host_allreduce_fn fn, void* user) {
     if (!l) return null_arg("learner");
     return guarded([&] { l->host(true).SetHostCommunicator(nranks, rank, fn, user); });
@@ -227,7 +243,7 @@ int wfsa_learner_set_comm_host(wfsa_learner* l, int nranks, int rank, wfsa_host_
 int wfsa_learner_build_packed(wfsa_learner* l, wfsa_fsa* f, const uint8_t* sym, const int64_t* off,
                               const double* weights, int64_t n) {
     if (!l || !f || !off || (n > 0 && (!weights || !sym))) return null_arg("learner/fsa/corpus");
-    return guarded([&] {
+    return rank_guarded(l, [&] {
         double sum = 0.0;
         for (int64_t s = 0; s < n; ++s) sum += weights[s];
         std::vector<double> w(weights, weights + n);
@@ -249,7 +265,7 @@ int wfsa_learner_set_info_rmin(wfsa_learner* l, int on) {
 
 int wfsa_learner_load_matrices(wfsa_learner* l, const char* prefix) {
     if (!l || !prefix) return null_arg("learner/prefix");
-    return guarded([&] { l->host(true).LoadMatrices(prefix); });
+    return rank_guarded(l, [&] { l->host(true).LoadMatrices(prefix); });
 }
 
 int wfsa_learner_save_matrices(wfsa_learner* l, const char* prefix) {
@@ -262,7 +278,7 @@ int wfsa_learner_save_matrices(wfsa_learner* l, const char* prefix) {
 
 int wfsa_learner_finalize(wfsa_learner* l) {
     if (!l) return null_arg("learner");
-    return guarded([&] {
+    return rank_guarded(l, [&] {
         l->host(true);
         if (l->base->GetNumberOfParameters() == 0) throw LearnerError("Empty automaton!");
         if (l->base->GetNumberOfStrings() == 0) throw LearnerError("Automaton cannot generate any of the strings!");
@@ -294,14 +310,14 @@ int wfsa_learner_info_get(wfsa_learner* l, wfsa_learner_info* o) {
 
 int wfsa_learner_init(wfsa_learner* l, int flags, const double* x0) {
     if (!l) return null_arg("learner");
-    return guarded([&] { l->host(true).Init(flags, x0); });
+    return rank_guarded(l, [&] { l->host(true).Init(flags, x0); });
 }
 
 int wfsa_learner_info_width(wfsa_learner* l) { return l ? l->width() : 0; }
 
 int wfsa_learner_step(wfsa_learner* l, double eta, double tol, double* info, int32_t* halt) {
     if (!l) return null_arg("learner");
-    return guarded([&] {
+    return rank_guarded(l, [&] {
         l->host(true).OptimizationStep(eta, false);
         const auto v = l->base->GetOptimizationInfo();
         if (info)
@@ -314,7 +330,7 @@ int wfsa_learner_run(wfsa_learner* l, double eta, double tol, int32_t max_epochs
                      int32_t* epochs_done) {
     if (!l) return null_arg("learner");
     if (epochs_done) *epochs_done = 0;
-    return guarded([&] {   // src/main.cpp:276-303
+    return rank_guarded(l, [&] {   // src/main.cpp:276-303
         if (l->qn) {   // device-resident
             l->qn->RunDevice(eta, tol, max_epochs, info_rows, epochs_done);
             return;
@@ -335,7 +351,7 @@ int wfsa_learner_run(wfsa_learner* l, double eta, double tol, int32_t max_epochs
 
 int wfsa_learner_objective_grad(wfsa_learner* l, double* kl, double* grad, double* logq) {
     if (!l) return null_arg("learner");
-    return guarded([&] {
+    return rank_guarded(l, [&] {
         const std::vector<double>* g;
         l->host(false);
         if (l->qn) {

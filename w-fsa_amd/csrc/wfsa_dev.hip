@@ -66,6 +66,14 @@ int fail(int code, const char* fmt, ...) {
             return fail(WFSA_ERR_RCCL, "%s all-reduce: %s", (ctx)->comm->kind(), (ctx)->comm->last_error()); \
     } while (0)
 
+// after a host sync: a peer all-reduce of this call that gave up (NaN
+// results) is reported as the error it is
+#define COMM_CHECK(ctx)                                                                               \
+    do {                                                                                               \
+        if ((ctx)->comm && (ctx)->comm->check())                                                       \
+            return fail(WFSA_ERR_RCCL, "%s all-reduce: %s", (ctx)->comm->kind(), (ctx)->comm->last_error()); \
+    } while (0)
+
 // device buffer (RAII)
 template <class T>
 struct DevBuf {
@@ -961,7 +969,11 @@ int collect_timing(wfsa_dev* ctx) {
 int wait_published(wfsa_dev* ctx, unsigned want) {
     auto reached = [&] { return int(__atomic_load_n(ctx->flag, __ATOMIC_ACQUIRE) - want) >= 0; };
     for (uint64_t spin = 1;; ++spin) {
-        if (reached()) return WFSA_OK;
+        if (reached()) {   // (a failed peer all-reduce publishes NaN: say why instead)
+            if (ctx->comm && ctx->comm->check())
+                return fail(WFSA_ERR_RCCL, "%s all-reduce: %s", ctx->comm->kind(), ctx->comm->last_error());
+            return WFSA_OK;
+        }
         if ((spin & 0x3fff) == 0) {
             const hipError_t e = hipStreamQuery(ctx->stream);
             if (e == hipSuccess) {
@@ -2453,6 +2465,7 @@ int dense_load_corpus(wfsa_dev* ctx, const uint8_t* sym, const int64_t* off, con
     ctx->stats.dense_rows = ctx->dense->rows();
     ctx->stats.dense_steps = ctx->dense->steps();
     ctx->stats.dense_np = ctx->dense->np();
+    ctx->stats.dense_blas = ctx->dense->blas() ? 1 : 0;
     return WFSA_OK;
 }
 
@@ -2732,7 +2745,7 @@ int wfsa_dev_load_corpus(wfsa_dev* ctx, const uint8_t* sym, const int64_t* off, 
     return WFSA_OK;
 }
 
-int wfsa_dev_recognize(wfsa_dev* ctx, uint8_t* recognized, double* path_count, uint8_t* used_param) {
+static int recognize_impl(wfsa_dev* ctx, uint8_t* recognized, double* path_count, uint8_t* used_param) {
     if (int rc = check_ctx(ctx)) return rc;
     if (!ctx->has_model || !ctx->has_corpus) return fail(WFSA_ERR_ARG, "load a model and a corpus first");
     if (ctx->dense ? !ctx->dense_struct : ctx->prep_level < 1)
@@ -2846,7 +2859,7 @@ int wfsa_dev_sym_solve(wfsa_dev* ctx, double* b) {
     return WFSA_OK;
 }
 
-int wfsa_dev_rmin(wfsa_dev* ctx, double* rmin, int64_t* string_index) {
+static int rmin_impl(wfsa_dev* ctx, double* rmin, int64_t* string_index) {
     if (int rc = check_ctx(ctx)) return rc;
     if (!ctx->has_model || !ctx->has_corpus) return fail(WFSA_ERR_ARG, "load a model and a corpus first");
     if (ctx->in_flight) return fail(WFSA_ERR_ARG, "an evaluation is in flight");
@@ -2879,7 +2892,7 @@ int wfsa_dev_string_tiers(wfsa_dev* ctx, int8_t* tier) {
     return WFSA_OK;
 }
 
-int wfsa_dev_objective_grad_begin(wfsa_dev* ctx, const double* w_full, int want_logq) {
+static int objective_grad_begin_impl(wfsa_dev* ctx, const double* w_full, int want_logq) {
     if (int rc = check_ctx(ctx)) return rc;
     if (!ctx->has_model || !ctx->has_corpus) return fail(WFSA_ERR_ARG, "load a model and a corpus first");
     if (!w_full && ctx->n_params > 0) return fail(WFSA_ERR_ARG, "null weights");
@@ -2938,7 +2951,7 @@ int wfsa_dev_objective_grad_begin(wfsa_dev* ctx, const double* w_full, int want_
     return WFSA_OK;
 }
 
-int wfsa_dev_objective_grad_end(wfsa_dev* ctx, double* loglik, double* grad_full, double* logq) {
+static int objective_grad_end_impl(wfsa_dev* ctx, double* loglik, double* grad_full, double* logq) {
     if (int rc = check_ctx(ctx)) return rc;
     if (!ctx->in_flight) return fail(WFSA_ERR_ARG, "objective_grad_end without _begin");
     ctx->in_flight = false;
@@ -2962,7 +2975,7 @@ int wfsa_dev_objective_grad(wfsa_dev* ctx, const double* w_full, double* loglik,
     return wfsa_dev_objective_grad_end(ctx, loglik, grad_full, logq);
 }
 
-int wfsa_dev_qn_setup(wfsa_dev* ctx, const wfsa_qn_desc* d) {
+static int qn_setup_impl(wfsa_dev* ctx, const wfsa_qn_desc* d) {
     if (int rc = check_ctx(ctx)) return rc;
     if (!d || d->n_params < 0 || d->n_constraints < 0) return fail(WFSA_ERR_ARG, "bad QN description");
     if (!ctx->has_model) return fail(WFSA_ERR_ARG, "load a model first");
@@ -3086,7 +3099,7 @@ int wfsa_dev_qn_get_state(wfsa_dev* ctx, double* x, double* lambda, double* grad
     return WFSA_OK;
 }
 
-int wfsa_dev_qn_run(wfsa_dev* ctx, double eta, double tol, int32_t max_steps, double* info_rows,
+static int qn_run_impl(wfsa_dev* ctx, double eta, double tol, int32_t max_steps, double* info_rows,
                     int32_t* steps_done, int32_t* status) {
     if (int rc = check_ctx(ctx)) return rc;
     if (steps_done) *steps_done = 0;
@@ -3236,7 +3249,7 @@ int wfsa_dev_qn_run(wfsa_dev* ctx, double eta, double tol, int32_t max_steps, do
     return WFSA_OK;
 }
 
-int wfsa_dev_hf_setup(wfsa_dev* ctx, int64_t* n_pairs) {
+static int hf_setup_impl(wfsa_dev* ctx, int64_t* n_pairs) {
     if (int rc = check_ctx(ctx)) return rc;
     if (!ctx->has_model || !ctx->has_corpus) return fail(WFSA_ERR_ARG, "load a model and a corpus first");
     if (ctx->in_flight) return fail(WFSA_ERR_ARG, "an evaluation is in flight");
@@ -3448,7 +3461,7 @@ int wfsa_dev_hf_pairs(wfsa_dev* ctx, int32_t* pairs) {
     return WFSA_OK;
 }
 
-int wfsa_dev_hf_eval(wfsa_dev* ctx, const double* w_full, double* values) {
+static int hf_eval_impl(wfsa_dev* ctx, const double* w_full, double* values) {
     if (int rc = check_ctx(ctx)) return rc;
     if (!ctx->hf_ready || ctx->hf_gen != ctx->prep_gen) return fail(WFSA_ERR_ARG, "wfsa_dev_hf_setup has not run");
     if (ctx->in_flight) return fail(WFSA_ERR_ARG, "an evaluation is in flight");
@@ -3503,6 +3516,7 @@ int wfsa_dev_hf_eval(wfsa_dev* ctx, const double* w_full, double* values) {
     if (ctx->comm && a.n_pattern > 0) COMM_TRY(ctx, ctx->hf_out.ptr, size_t(a.n_pattern), wfsa::RedOp::SumF64, s);
     if (values && a.n_pattern > 0) HIP_TRY(ctx->hf_out.download(values, size_t(a.n_pattern), s));
     HIP_TRY(hipStreamSynchronize(s));
+    COMM_CHECK(ctx);
     return WFSA_OK;
 }
 
@@ -3552,7 +3566,7 @@ int wfsa_dev_comm_init_host(wfsa_dev* ctx, int nranks, int rank, wfsa_host_allre
     return WFSA_OK;
 }
 
-int wfsa_dev_allreduce(wfsa_dev* ctx, double* host_buf, int64_t count) {
+static int allreduce_impl(wfsa_dev* ctx, double* host_buf, int64_t count) {
     if (int rc = check_ctx(ctx)) return rc;
     if (count <= 0) return WFSA_OK;
     if (!host_buf) return fail(WFSA_ERR_ARG, "null buffer");
@@ -3562,6 +3576,7 @@ int wfsa_dev_allreduce(wfsa_dev* ctx, double* host_buf, int64_t count) {
     COMM_TRY(ctx, tmp.ptr, size_t(count), wfsa::RedOp::SumF64, ctx->stream);
     HIP_TRY(tmp.download(host_buf, size_t(count), ctx->stream));
     HIP_TRY(hipStreamSynchronize(ctx->stream));
+    COMM_CHECK(ctx);
     return WFSA_OK;
 }
 
@@ -3576,4 +3591,39 @@ int wfsa_dev_get_stats(wfsa_dev* ctx, wfsa_dev_stats* out) {
     return WFSA_OK;
 }
 
+
+// Entry points that take part in rank collectives: a failure on this rank
+// (anything but a bad argument, which fails before any collective) aborts
+// the communicator, so the other ranks' current or next collective fails at
+// once instead of waiting for a member that will not come.
+static int rank_guard(wfsa_dev* ctx, int rc) {
+    if (rc != WFSA_OK && rc != WFSA_ERR_ARG && ctx && ctx->comm) ctx->comm->abort(g_last_error.c_str());
+    return rc;
+}
+int wfsa_dev_recognize(wfsa_dev* ctx, uint8_t* recognized, double* path_count, uint8_t* used_param) { return rank_guard(ctx, recognize_impl(ctx, recognized, path_count, used_param)); }
+int wfsa_dev_rmin(wfsa_dev* ctx, double* rmin, int64_t* string_index) { return rank_guard(ctx, rmin_impl(ctx, rmin, string_index)); }
+int wfsa_dev_objective_grad_begin(wfsa_dev* ctx, const double* w_full, int want_logq) { return rank_guard(ctx, objective_grad_begin_impl(ctx, w_full, want_logq)); }
+int wfsa_dev_objective_grad_end(wfsa_dev* ctx, double* loglik, double* grad_full, double* logq) { return rank_guard(ctx, objective_grad_end_impl(ctx, loglik, grad_full, logq)); }
+int wfsa_dev_qn_setup(wfsa_dev* ctx, const wfsa_qn_desc* d) { return rank_guard(ctx, qn_setup_impl(ctx, d)); }
+int wfsa_dev_qn_run(wfsa_dev* ctx, double eta, double tol, int32_t max_steps, double* info_rows, int32_t* steps_done, int32_t* status) { return rank_guard(ctx, qn_run_impl(ctx, eta, tol, max_steps, info_rows, steps_done, status)); }
+int wfsa_dev_hf_setup(wfsa_dev* ctx, int64_t* n_pairs) { return rank_guard(ctx, hf_setup_impl(ctx, n_pairs)); }
+int wfsa_dev_hf_eval(wfsa_dev* ctx, const double* w_full, double* values) { return rank_guard(ctx, hf_eval_impl(ctx, w_full, values)); }
+int wfsa_dev_allreduce(wfsa_dev* ctx, double* host_buf, int64_t count) { return rank_guard(ctx, allreduce_impl(ctx, host_buf, count)); }
+
+int wfsa_dev_comm_abort(wfsa_dev* ctx, const char* why) {
+    if (int rc = check_ctx(ctx)) return rc;
+    if (ctx->comm) ctx->comm->abort(why ? why : "wfsa_dev_comm_abort");
+    return WFSA_OK;
+}
+
+int wfsa_dev_peer_selftest(int device, int nranks, int64_t n, double timeout_s, int mode, double out[4]) {
+    if (!out) return fail(WFSA_ERR_ARG, "null output");
+    const hipError_t e = hipSetDevice(device);
+    if (e != hipSuccess) return fail(WFSA_ERR_HIP, "hipSetDevice: %s", hipGetErrorString(e));
+    std::string err;
+    if (wfsa::peer_selftest(nranks, n, timeout_s, mode, out, err)) return fail(WFSA_ERR_HIP, "%s", err.c_str());
+    return WFSA_OK;
+}
+
 }  // extern "C"
+

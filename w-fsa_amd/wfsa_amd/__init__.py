@@ -188,6 +188,11 @@ class QuasiNewtonLearner:
         buf = (C.c_uint8 * _lib.COMM_ID_BYTES).from_buffer_copy(bytes(unique_id))
         check_host(load().wfsa_learner_set_comm(self._h, nranks, rank, buf))
 
+    def AbortCommunicator(self, why="aborted by the caller"):
+        """this rank failed: the other ranks' current or next collective
+        fails at once (wfsa_learner_comm_abort)"""
+        check_host(load().wfsa_learner_comm_abort(self._h, why.encode()))
+
     def BuildFrom(self, fsa, corpus):
         self._fsa = fsa
         check_host(load().wfsa_learner_build(self._h, fsa._h, corpus._h))
@@ -504,6 +509,19 @@ class Device:
         """wfsa_dev_comm_init_host (see QuasiNewtonLearner.SetHostCommunicator)"""
         self._host_cb = _host_callback(allreduce)
         check_dev(load().wfsa_dev_comm_init_host(self._h, nranks, rank, self._host_cb, None))
+
+    def comm_abort(self, why="aborted by the caller"):
+        """wfsa_dev_comm_abort: every other member's current or next
+        collective fails at once"""
+        check_dev(load().wfsa_dev_comm_abort(self._h, why.encode()))
+
+    @staticmethod
+    def peer_selftest(nranks, n, timeout_s, mode, device=0):
+        """the peer all-reduce kernel on one device (wfsa_dev_peer_selftest):
+        returns (metric, status, poisoned areas, seconds)"""
+        out = (C.c_double * 4)()
+        check_dev(load().wfsa_dev_peer_selftest(device, nranks, n, timeout_s, mode, out))
+        return tuple(out)
 
     def allreduce(self, values):
         a = np.ascontiguousarray(values, dtype=np.float64).copy()

@@ -48,6 +48,7 @@ class DevStats(C.Structure):
         ("wave_strings", i32), ("wave_row_entries", i64), ("wave_pair_edges", i64),
         ("comm_ranks", i32), ("comm_peer", i32),
         ("slot_chunks", i64), ("max_group_chunks", i32), ("wave_pull", i32),
+        ("dense_blas", i32),
     ]
 
 
@@ -97,6 +98,8 @@ _SIGS = {
     "wfsa_dev_comm_init": (C.c_int, [vp, C.c_int, C.c_int, vp]),
     "wfsa_dev_comm_local_id": (C.c_int, [C.c_int, vp]),
     "wfsa_dev_allreduce": (C.c_int, [vp, vp, i64]),
+    "wfsa_dev_comm_abort": (C.c_int, [vp, C.c_char_p]),
+    "wfsa_dev_peer_selftest": (C.c_int, [C.c_int, C.c_int, i64, C.c_double, C.c_int, vp]),
     "wfsa_dev_comm_init_host": (C.c_int, [vp, C.c_int, C.c_int, vp, vp]),
     "wfsa_dev_get_stats": (C.c_int, [vp, P(DevStats)]),
     # host mirror (wfsa_host.h)
@@ -115,6 +118,7 @@ _SIGS = {
     "wfsa_learner_destroy": (None, [vp]),
     "wfsa_learner_set_comm": (C.c_int, [vp, C.c_int, C.c_int, vp]),
     "wfsa_learner_set_comm_host": (C.c_int, [vp, C.c_int, C.c_int, vp, vp]),
+    "wfsa_learner_comm_abort": (C.c_int, [vp, C.c_char_p]),
     "wfsa_learner_build": (C.c_int, [vp, vp, vp]),
     "wfsa_learner_build_packed": (C.c_int, [vp, vp, vp, vp, vp, i64]),
     "wfsa_learner_finalize": (C.c_int, [vp]),
