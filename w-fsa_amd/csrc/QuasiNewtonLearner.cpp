@@ -15,6 +15,18 @@ void QuasiNewtonLearner::FinalizeCallback() {   // src/QuasiNewtonLearner.cpp:17
     rhs.assign(n, 0.0);
     lambda.assign(k, 1.0);
     g.assign(k, 0.0);
+    // the constraints' member runs, when Ccol is non-decreasing (the host
+    // update's fast form)
+    ccol_runs = true;
+    cptr_runs.assign(k + 1, 0);
+    for (size_t i = 0; i < n; ++i) {
+        if ((i > 0 && Ccol[i] < Ccol[i - 1]) || Ccol[i] < 0 || size_t(Ccol[i]) >= k) {
+            ccol_runs = false;
+            break;
+        }
+        cptr_runs[size_t(Ccol[i]) + 1]++;
+    }
+    for (size_t c = 0; c < k && ccol_runs; ++c) cptr_runs[c + 1] += cptr_runs[c];
     dev_qn_ready = false;
     dev_state_valid = host_state_stale = false;
 }
@@ -81,6 +93,88 @@ void QuasiNewtonLearner::ComputeG() {   // :148-160: g = C^T exp(x) - 1
     g_max = *std::max_element(g.begin(), g.end());
 }
 
+namespace {
+
+// OptimizationStep's O(n + k) update after the gradient (:170-199): aux,
+// rhs and graderr, the next lambda (ComputeLambdaNext), x and LambdaUpdate's
+// argument.  Every value is formed by the same operations in the same order
+// as the plain loops (Ccol is non-decreasing -- BuildConstraints numbers a
+// group's members consecutively -- so a constraint's members are one run,
+// subtracted in ascending order), so the results are the same bits; the max
+// runs in four accumulators (NaN is never selected, as with std::max).
+// Compiled twice, the AVX2 clone picked at load time (AVX2 alone has no FMA,
+// so nothing is contracted).
+struct QnHostUpdate {
+    size_t n, k;
+    const int32_t* ccol;
+    const int32_t* cptr;
+    const double* grad;
+    const double* expx;
+    const double* lambda;
+    double* g;
+    double* aux;
+    double* rhs;
+    double* x;
+    double* laux;   // k: lambda - lambda_next on return
+    double* lx;     // n: scratch
+    double eta;
+};
+
+__attribute__((target_clones("avx2", "default"))) double qn_host_update(const QnHostUpdate& u) {
+    const size_t n = u.n, k = u.k;
+    const int32_t* __restrict ccol = u.ccol;
+    const int32_t* __restrict cptr = u.cptr;
+    const double* __restrict grad = u.grad;
+    const double* __restrict expx = u.expx;
+    const double* __restrict lambda = u.lambda;
+    double* __restrict g = u.g;
+    double* __restrict aux = u.aux;
+    double* __restrict rhs = u.rhs;
+    double* __restrict x = u.x;
+    double* __restrict laux = u.laux;
+    double* __restrict lx = u.lx;
+    for (size_t i = 0; i < n; ++i) lx[i] = lambda[ccol[i]];
+    double m[4] = {0.0, 0.0, 0.0, 0.0};
+    size_t i = 0;
+    for (; i + 4 <= n; i += 4)
+        for (int q = 0; q < 4; ++q) {
+            const double a = expx[i + q] * lx[i + q];   // J_g . lambda
+            aux[i + q] = a;
+            const double r = grad[i + q] + a;
+            rhs[i + q] = r;
+            const double ar = std::fabs(r);
+            m[q] = m[q] < ar ? ar : m[q];
+        }
+    for (; i < n; ++i) {
+        const double a = expx[i] * lx[i];
+        aux[i] = a;
+        const double r = grad[i] + a;
+        rhs[i] = r;
+        const double ar = std::fabs(r);
+        m[0] = m[0] < ar ? ar : m[0];
+    }
+    m[0] = m[0] < m[1] ? m[1] : m[0];
+    m[2] = m[2] < m[3] ? m[3] : m[2];
+    const double graderr = m[0] < m[2] ? m[2] : m[0];
+    for (size_t c = 0; c < k; ++c) {   // ComputeLambdaNext (:127-146)
+        double v = lambda[c] * g[c];
+        for (int32_t j = cptr[c]; j < cptr[c + 1]; ++j) v -= grad[j];
+        const double gc = g[c] + 1.0;
+        g[c] = gc;
+        laux[c] = v / gc;
+    }
+    for (size_t j = 0; j < n; ++j) lx[j] = laux[ccol[j]];
+    for (size_t j = 0; j < n; ++j) {
+        const double r = (grad[j] + expx[j] * lx[j]) / aux[j];
+        rhs[j] = r;
+        x[j] -= u.eta * r;
+    }
+    for (size_t c = 0; c < k; ++c) laux[c] = lambda[c] - laux[c];
+    return graderr;
+}
+
+}  // namespace
+
 void QuasiNewtonLearner::OptimizationStep(double eta, bool) {   // :162-201
     // ComputeExpX and ComputeG do not depend on the gradient: run them on
     // the host while the device evaluates (same results as the reference's
@@ -99,21 +193,28 @@ void QuasiNewtonLearner::OptimizationStep(double eta, bool) {   // :162-201
     ComputeObjective();
     const size_t n = _x.size(), k = lambda.size();
     aux.resize(n);
-    grad_error = 0.0;
-    for (size_t i = 0; i < n; ++i) {
-        aux[i] = expx[i] * lambda[size_t(Ccol[i])];   // J_g . lambda
-        rhs[i] = grad[i] + aux[i];
-        grad_error = std::max(grad_error, std::abs(rhs[i]));
-    }
     lambda_min = k ? *std::min_element(lambda.begin(), lambda.end()) : 0.0;
-    std::vector<double> laux;
-    ComputeLambdaNext(laux);
-    for (size_t i = 0; i < n; ++i) {
-        rhs[i] = (grad[i] + expx[i] * laux[size_t(Ccol[i])]) / aux[i];
-        _x[i] -= eta * rhs[i];
+    if (ccol_runs) {
+        laux_buf.resize(k);
+        lx_buf.resize(n);
+        const QnHostUpdate u{n, k, Ccol.data(), cptr_runs.data(), grad.data(), expx.data(), lambda.data(), g.data(),
+                             aux.data(), rhs.data(), _x.data(), laux_buf.data(), lx_buf.data(), eta};
+        grad_error = qn_host_update(u);
+    } else {   // the plain loops (any constraint numbering)
+        grad_error = 0.0;
+        for (size_t i = 0; i < n; ++i) {
+            aux[i] = expx[i] * lambda[size_t(Ccol[i])];   // J_g . lambda
+            rhs[i] = grad[i] + aux[i];
+            grad_error = std::max(grad_error, std::abs(rhs[i]));
+        }
+        ComputeLambdaNext(laux_buf);
+        for (size_t i = 0; i < n; ++i) {
+            rhs[i] = (grad[i] + expx[i] * laux_buf[size_t(Ccol[i])]) / aux[i];
+            _x[i] -= eta * rhs[i];
+        }
+        for (size_t c = 0; c < k; ++c) laux_buf[c] = lambda[c] - laux_buf[c];
     }
-    for (size_t c = 0; c < k; ++c) laux[c] = lambda[c] - laux[c];
-    LambdaUpdate(laux.data(), lambda.data(), eta, exponential_lambda);
+    LambdaUpdate(laux_buf.data(), lambda.data(), eta, exponential_lambda);
     const auto t4 = clk::now();
     auto ms = [](clk::time_point a, clk::time_point b) { return std::chrono::duration<double, std::milli>(b - a).count(); };
     timing.steps += 1;

@@ -62,6 +62,9 @@ private:
     bool host_state_stale = false;  // the device's (x, lambda, grad) are newer than the host's
     Timing timing;
     std::vector<double> rows_buf;   // RunDevice's info rows
+    std::vector<double> laux_buf, lx_buf;   // OptimizationStep scratch (k, n)
+    std::vector<int32_t> cptr_runs;         // constraint c's members: [cptr_runs[c], cptr_runs[c + 1])
+    bool ccol_runs = false;                 // Ccol non-decreasing: cptr_runs is valid
 };
 
 }  // namespace wfsa

@@ -38,6 +38,10 @@ namespace wfsa {
 namespace {
 
 typedef double d4 __attribute__((ext_vector_type(4)));
+// staging registers of the operand slices: a native vector, not HIP's double2
+// class (whose assignment is a struct memcpy that SROA leaves in scratch: the
+// prefetch then went through scratch stores waited for right after issue)
+typedef double d2 __attribute__((ext_vector_type(2)));
 
 constexpr int kT = kDenseTile;        // 128
 // K slice per LDS stage: 32 for the per-step GEMMs (one block per CU, the
@@ -114,33 +118,33 @@ template <int BK, int NT> constexpr int slice_chunks() { return kT * BK / 2 / NT
 
 template <bool KC, int BK, int NT>
 __device__ __forceinline__ void load_slice(const double* __restrict__ base, int64_t ld, int r0, int64_t k0, int tid,
-                                           double2 (&v)[slice_chunks<BK, NT>()]) {
+                                           d2 (&v)[slice_chunks<BK, NT>()]) {
     constexpr int kPairs = BK / 2;   // 16-byte chunks per row of the slice
 #pragma unroll
     for (int c = 0; c < slice_chunks<BK, NT>(); ++c) {
         const int idx = c * NT + tid;
         if (KC) {
             const int row = idx / kPairs, kp = idx % kPairs;
-            v[c] = *reinterpret_cast<const double2*>(base + int64_t(r0 + row) * ld + k0 + 2 * kp);
+            v[c] = *reinterpret_cast<const d2*>(base + int64_t(r0 + row) * ld + k0 + 2 * kp);
         } else {
             const int kk = idx >> 6, rp = idx & 63;
-            v[c] = *reinterpret_cast<const double2*>(base + (k0 + kk) * ld + r0 + 2 * rp);
+            v[c] = *reinterpret_cast<const d2*>(base + (k0 + kk) * ld + r0 + 2 * rp);
         }
     }
 }
 
 template <bool KC, int BK, int NT>
-__device__ __forceinline__ void store_slice(double* __restrict__ s, int tid, const double2 (&v)[slice_chunks<BK, NT>()]) {
+__device__ __forceinline__ void store_slice(double* __restrict__ s, int tid, const d2 (&v)[slice_chunks<BK, NT>()]) {
     constexpr int kPairs = BK / 2, L = ldk<BK>();
 #pragma unroll
     for (int c = 0; c < slice_chunks<BK, NT>(); ++c) {
         const int idx = c * NT + tid;
         if (KC) {
             const int row = idx / kPairs, kp = idx % kPairs;
-            *reinterpret_cast<double2*>(s + row * L + 2 * kp) = v[c];
+            *reinterpret_cast<d2*>(s + row * L + 2 * kp) = v[c];
         } else {
             const int kk = idx >> 6, rp = idx & 63;
-            *reinterpret_cast<double2*>(s + kk * kLdn + 2 * rp) = v[c];
+            *reinterpret_cast<d2*>(s + kk * kLdn + 2 * rp) = v[c];
         }
     }
 }
@@ -150,7 +154,7 @@ template <int MODE, int BK> constexpr int stage() { return op_size<MODE != 2, BK
 // NW waves per 128 x 128 block: 2 x (NW / 2), each a 64 x (256 / NW) tile
 // of 16 x 16 MFMA tiles (NJ of them per row of tiles)
 template <int MODE, int BK, int NW>
-__global__ __launch_bounds__(NW * 64, 2) void dense_gemm_kernel(GemmArgs a) {
+__global__ __launch_bounds__(NW * 64, (MODE == 2 && NW == 4 ? 2 : 1)) void dense_gemm_kernel(GemmArgs a) {
     if (a.halted && *a.halted) return;
     constexpr int NT = NW * 64, NWN = NW / 2, NJ = 16 / NW, WCOLS = 16 * NJ;
     constexpr int kLdk = ldk<BK>(), kStage = stage<MODE, BK>();
@@ -224,7 +228,7 @@ __global__ __launch_bounds__(NW * 64, 2) void dense_gemm_kernel(GemmArgs a) {
         const int64_t nk = (MODE == GRAD ? a.kg : int64_t(np)) / BK;
         const double* xa = a.x;
         const double* xb = a.bm;
-        double2 va[CH], vb[CH];
+        d2 va[CH], vb[CH];
         const int ldb = MODE == GRAD ? ldx : np;   // z / A, A^T
         load_slice<A_KC, BK, NT>(xa, ldx, r0, 0, tid, va);
         load_slice<B_KC, BK, NT>(xb, ldb, c0, 0, tid, vb);
