@@ -246,6 +246,16 @@ __global__ __launch_bounds__(NW * 64, (MODE == 2 && NW == 4 ? 2 : 1)) void dense
             const double* Bs = As + op_size<A_KC, BK>();
 #pragma unroll
             for (int kk = 0; kk < BK / 4; ++kk) {
+                // the next slice into the other stage half-way through this
+                // one (its loads have landed by then; every wave finished
+                // reading that stage before the last barrier): the stores
+                // then overlap this wave's MFMAs instead of idling the matrix
+                // pipe before the barrier
+                if (kk == BK / 8 && more) {
+                    double* s = lds + ((kt + 1) & 1) * kStage;
+                    store_slice<A_KC, BK, NT>(s, tid, va);
+                    store_slice<B_KC, BK, NT>(s + op_size<A_KC, BK>(), tid, vb);
+                }
                 double av[4], bv[NJ];
 #pragma unroll
                 for (int i = 0; i < 4; ++i)
@@ -258,11 +268,6 @@ __global__ __launch_bounds__(NW * 64, (MODE == 2 && NW == 4 ? 2 : 1)) void dense
 #pragma unroll
                     for (int j = 0; j < NJ; ++j)
                         acc[i][j] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[i], bv[j], acc[i][j], 0, 0, 0);
-            }
-            if (more) {
-                double* s = lds + ((kt + 1) & 1) * kStage;
-                store_slice<A_KC, BK, NT>(s, tid, va);
-                store_slice<B_KC, BK, NT>(s + op_size<A_KC, BK>(), tid, vb);
             }
             __syncthreads();
         }

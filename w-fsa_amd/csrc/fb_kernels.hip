@@ -2202,7 +2202,38 @@ __global__ __launch_bounds__(kBubbleBlock) void bubble_kernel(BubbleArgs a) {
 // DBG (timing experiments only, WFSA_FBS_DBG): 1 no table gathers, 3 no
 // stream pass at all, 4 neither stream pass nor table staging, 5 the QN finish only, 6 / 7
 // prefetch sets of 2 / 6 rows, 8 no bubble code, 9 stream loads only
-template <bool WIDE, bool W_LDS, bool MULTI, int DBG = 0, bool RMIN = false>
+// One delta-format row (kDeltaBits fields, fb_kernels.hpp) of a lane: each
+// field steps the lane's index forward and gathers that entry of the staged
+// table; HDR: the group's first row, whose fields 0-7 hold p and the row
+// count.  The index is clamped to the table (a corrupt stream reads a zero
+// slot, never past LDS).
+template <bool HDR>
+__device__ __forceinline__ void delta_row(const uint4 v, uint32_t& cur, const double* __restrict__ tab, uint32_t tmax,
+                                          double& a0, double& a1) {
+    constexpr uint32_t M = kDeltaMax;
+    uint32_t f[kDeltaFields];
+    f[0] = v.x & M;
+    f[1] = (v.x >> 10) & M;
+    f[2] = (v.x >> 20) & M;
+    f[3] = __builtin_amdgcn_alignbit(v.y, v.x, 30) & M;
+    f[4] = (v.y >> 8) & M;
+    f[5] = (v.y >> 18) & M;
+    f[6] = __builtin_amdgcn_alignbit(v.z, v.y, 28) & M;
+    f[7] = (v.z >> 6) & M;
+    f[8] = (v.z >> 16) & M;
+    f[9] = __builtin_amdgcn_alignbit(v.w, v.z, 26) & M;
+    f[10] = (v.w >> 4) & M;
+    f[11] = (v.w >> 14) & M;
+#pragma unroll
+    for (int i = HDR ? kDeltaFields - kDeltaHdrFields : 0; i < kDeltaFields; ++i) {
+        cur += f[i];
+        const double t = tab[min(cur, tmax)];
+        if (i & 1) a1 += t;
+        else a0 += t;
+    }
+}
+
+template <bool WIDE, bool W_LDS, bool MULTI, int DBG = 0, bool RMIN = false, bool DELTA = false>
 __global__ __launch_bounds__(1024, (DBG == 10 ? 8 : 1)) void fbs_kernel(CompiledArgs a) {
     extern __shared__ __attribute__((aligned(16))) double lds[];
     const int lane = lane_id();
@@ -2245,7 +2276,30 @@ __global__ __launch_bounds__(1024, (DBG == 10 ? 8 : 1)) void fbs_kernel(Compiled
         finish();
         return;
     }
-    if (W_LDS && DBG != 4 && !a.no_streams) {
+    if (DELTA && !a.no_streams) {
+        // the delta format's remapped table: slot s holds weight
+        // s - 1 - s / kDeltaPeriod, or zero on a multiple of kDeltaPeriod
+        // (and past the last weight); all of a thread's loads first
+        constexpr int kB = 12;
+        const int T = a.d_tab;
+        for (int s0 = int(threadIdx.x); s0 < T; s0 += kB * int(blockDim.x)) {
+            double t[kB];
+#pragma unroll
+            for (int b = 0; b < kB; ++b) {
+                const int s = s0 + b * int(blockDim.x);
+                const int j = s - 1 - s / kDeltaPeriod;
+                const bool z = (s % kDeltaPeriod) == 0 || j >= a.n_params;
+                const double v = a.w[min(max(j, 0), a.n_params - 1)];
+                t[b] = z ? 0.0 : v;
+            }
+#pragma unroll
+            for (int b = 0; b < kB; ++b) {
+                const int s = s0 + b * int(blockDim.x);
+                if (s < T) lds[s] = t[b];
+            }
+        }
+        __syncthreads();
+    } else if (W_LDS && DBG != 4 && !a.no_streams) {
         // stage w[0, n_params] in 16-byte pieces, all of a thread's loads
         // issued before its first store (loads and stores unconditional --
         // an index past the end is clamped to the last piece, which is then
@@ -2298,12 +2352,29 @@ __global__ __launch_bounds__(1024, (DBG == 10 ? 8 : 1)) void fbs_kernel(Compiled
             if (s >= 0) a.logq[s] = acc;
         }
     };
+    uint32_t cur = 0;   // DELTA: the lane's index into the remapped table
+    const uint32_t tmax = uint32_t(max(a.d_tab - 1, 0));
     auto apply = [&](const uint4 (&r)[D], int c0) {
 #pragma unroll
         for (int d = 0; d < D; ++d) {
             const int c = c0 + d;
             if (c >= rows) break;
             uint4 v = r[d];
+            if constexpr (DELTA) {
+                if (c == hdr) {   // uniform: the first row of the next group
+                    flush();
+                    acc0 = 0.0;
+                    acc1 = 0.0;
+                    p = __longlong_as_double((long long)(v.x) | ((long long)(v.y) << 32));
+                    hdr += __builtin_amdgcn_readfirstlane(int(v.z & 0xffffu));
+                    ++grp;
+                    cur = 0;
+                    delta_row<true>(v, cur, wsrc, tmax, acc0, acc1);
+                } else {
+                    delta_row<false>(v, cur, wsrc, tmax, acc0, acc1);
+                }
+                continue;
+            }
             if (c == hdr) {   // uniform: the first row of the next group
                 flush();
                 acc0 = 0.0;
@@ -2538,6 +2609,8 @@ hipError_t configure_kernels(int max_dynamic_lds) {
                          reinterpret_cast<const void*>(&fbs_kernel<false, true, true, 0, true>),
                          reinterpret_cast<const void*>(&fbs_kernel<true, true, false, 0, true>),
                          reinterpret_cast<const void*>(&fbs_kernel<true, true, true, 0, true>),
+                         reinterpret_cast<const void*>(&fbs_kernel<false, true, false, 0, false, true>),
+                         reinterpret_cast<const void*>(&fbs_kernel<false, true, false, 0, true, true>),
 #ifdef WFSA_EXPERIMENTS
                          reinterpret_cast<const void*>(&fbs_kernel<false, true, false, 1>),
                          reinterpret_cast<const void*>(&fbs_kernel<false, true, false, 3>),
@@ -2804,6 +2877,13 @@ hipError_t launch_compiled(const CompiledArgs& a, int grid, int block, size_t ld
             return hipGetLastError();
         }
 #endif
+        if (a.d_tab > 0) {   // delta stream: narrow words, no composites, w staged (the host checks)
+            if (a.bub_on && a.bub.rmin_acc)
+                hipLaunchKernelGGL((fbs_kernel<false, true, false, 0, true, true>), g, b, lds, stream, a);
+            else
+                hipLaunchKernelGGL((fbs_kernel<false, true, false, 0, false, true>), g, b, lds, stream, a);
+            return hipGetLastError();
+        }
         const int key = (a.tables >= 1 ? 4 : 0) + (a.wide ? 2 : 0) + (a.multi ? 1 : 0);
         if (a.bub_on && a.bub.rmin_acc) {   // the bubbles also feed the rmin column
             switch (key) {

@@ -52,6 +52,30 @@ constexpr int kStreamTailChunks = 64 * 8;
 // the string's words follow.
 __host__ __device__ inline int stream_hdr_words(int wide) { return wide ? 3 : 5; }
 
+// Delta stream (the per-iteration stream kernel's format when the weights
+// are staged in LDS and no word is a multi-parameter composite): a string's
+// trivial words as a multiset -- their sum does not depend on the order --
+// sorted, each a 10-bit step forward from the previous index.  The staged
+// table is remapped with a zero-weight slot every kDeltaPeriod entries
+// (slot 0 included): a gap longer than a step is bridged by steps onto zero
+// slots, the lane starts each string on slot 0 and ends it on a zero slot,
+// so padding fields (0) add nothing.  Row layout (16 bytes per lane): field
+// i at bits [10 i, 10 i + 10), 12 fields; the lane's first row of a group
+// carries p (bits 0-63) and the group's row count (bits 64-79) in place of
+// fields 0-7.  c3: 10.5 bits per word against 16 (profiles/r04/
+// stream_format_micro_v4b.txt).
+constexpr int kDeltaBits = 10;
+constexpr uint32_t kDeltaMax = (1u << kDeltaBits) - 1u;
+constexpr int kDeltaPeriod = 512;   // <= kDeltaMax: a zero slot is always within one step
+constexpr int kDeltaFields = 12, kDeltaHdrFields = 4;
+__host__ __device__ inline int32_t delta_slot(int32_t j) { return j + 1 + j / (kDeltaPeriod - 1); }
+// table entries: every weight's slot and one zero slot after the last (an
+// index past it -- the end step of a string whose last word is the last
+// weight -- is clamped onto it)
+__host__ __device__ inline int32_t delta_table(int32_t n_params) {
+    return n_params > 0 ? delta_slot(n_params - 1) + 2 : 1;
+}
+
 // Per-iteration record of a combined edge, one 16-byte gather in the
 // compiled kernel: its log-weight and its parameter list (p0 when np == 1).
 struct alignas(16) EdgeRec {
@@ -545,6 +569,7 @@ struct CompiledArgs {
                                  // wave w: [wave_first[w], wave_first[w + 1]), contiguous
     int32_t n_groups;
     int32_t n_params;
+    int32_t d_tab;           // > 0: the stream is in the delta format, its LDS table has d_tab entries
     int32_t tables;          // with_grad: 2 w and grad staged in LDS, 1 grad in LDS, 0 global;
                              // else: >= 1 w staged in LDS, 0 global
     int32_t wide;

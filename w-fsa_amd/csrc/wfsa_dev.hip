@@ -29,6 +29,7 @@
 #include <memory>
 #include <limits>
 #include <string>
+#include <thread>
 #include <unordered_map>
 #include <vector>
 
@@ -186,6 +187,15 @@ struct wfsa_dev {
     DevBuf<int32_t> bub, g_len, l_str, l_len;
     DevBuf<int32_t> wave_first;   // [stream waves + 1] the per-iteration kernel's groups of each wave
     DevBuf<int64_t> g_base;
+    // the per-iteration stream kernel's copy of the streams in the delta
+    // format (fb_kernels.hpp): its own groups, dealing and layout; the 16-bit
+    // streams above stay for the preparation-time gradient pass
+    bool delta_on = false;
+    int32_t d_tab = 0;
+    DevBuf<uint4> dstream;
+    DevBuf<int64_t> d_g_base;
+    DevBuf<int32_t> d_g_len, d_l_str, d_wave_first;
+    int64_t d_stream_bytes = 0;
     int c_grid = 0, c_tables = 0;    // gradient pass (once, at preparation)
     int i_grid = 0, i_tables = 0;    // per-iteration pass (log-weights only)
     int i_block = 1024;
@@ -282,6 +292,7 @@ struct wfsa_dev {
     bool timing_pending = false; // events of the last call not yet read
     bool kernel_timing = true;
     bool fuse_bubbles = true;    // WFSA_FUSE_BUBBLES=0: separate bubble kernel
+    bool use_delta = true;       // WFSA_DELTA=0: the per-iteration pass reads the 16-bit streams
 
     DevBuf<double> gpart;        // per-block partial gradients of the compiled kernel
 
@@ -1212,6 +1223,168 @@ int prepare_dense(wfsa_dev* ctx, int level) {
     return WFSA_OK;
 }
 
+// fn(begin, end) over [0, n) on up to 16 host threads (the GPU box's CPU share)
+template <class F>
+void parallel_for(int64_t n, F&& fn) {
+    const int64_t hc = std::max<int64_t>(1, int64_t(std::thread::hardware_concurrency()));
+    const int nt = int(std::max<int64_t>(1, std::min<int64_t>({16, hc, n / 4096 + 1})));
+    if (nt == 1) {
+        fn(int64_t(0), n);
+        return;
+    }
+    std::vector<std::thread> th;
+    for (int t = 0; t < nt; ++t) th.emplace_back([&fn, n, t, nt] { fn(n * t / nt, n * (t + 1) / nt); });
+    for (auto& x : th) x.join();
+}
+
+// The per-iteration kernel's delta-format streams (fb_kernels.hpp): every
+// compiled string's trivial words read back from the 16-bit streams,
+// remapped (delta_slot), sorted and written as 10-bit steps; the strings
+// regrouped by their delta rows (longest first, 64 per group) and the groups
+// dealt to the waves by the same rule as the 16-bit groups.
+template <class Deal>
+int build_delta(wfsa_dev* ctx, const std::vector<int32_t>& comp, const std::vector<int32_t>& h_main,
+                const std::vector<int64_t>& s_base, const std::vector<double>& h_p, int64_t chunks, int32_t G,
+                Deal&& deal) {
+    hipStream_t s = ctx->stream;
+    const int64_t nc = int64_t(comp.size());
+    std::vector<uint16_t> h16(size_t(chunks) * 8);
+    HIP_TRY(ctx->stream_w.download(reinterpret_cast<uint4*>(h16.data()), size_t(chunks), s));
+    HIP_TRY(hipStreamSynchronize(s));
+    const int hdr16 = wfsa::stream_hdr_words(0);
+    auto words_of = [&](int32_t str, std::vector<uint32_t>& r) {
+        r.clear();
+        const int64_t c0 = s_base[size_t(str)] / 8;   // the lane's first chunk
+        for (int k = 0; k < h_main[size_t(str)]; ++k) {
+            const int slot = hdr16 + k;
+            const uint16_t wd = h16[size_t(c0 + int64_t(kWave) * (slot / 8)) * 8 + size_t(slot % 8)];
+            r.push_back(uint32_t(wfsa::delta_slot(int32_t(wd))));
+        }
+        std::sort(r.begin(), r.end());
+    };
+    auto encode = [](const std::vector<uint32_t>& r, auto&& emit) {
+        constexpr uint32_t M = wfsa::kDeltaMax, P = wfsa::kDeltaPeriod;
+        uint32_t cur = 0;
+        for (uint32_t t : r) {
+            while (t - cur > M) {   // onto the farthest zero slot within one step
+                const uint32_t z = (cur + M) / P * P;
+                emit(z - cur);
+                cur = z;
+            }
+            emit(t - cur);
+            cur = t;
+        }
+        if (cur % P) emit((cur / P + 1) * P - cur);   // end on a zero slot: the padding adds nothing
+    };
+    auto rows_of = [](int64_t nf) {
+        return nf <= wfsa::kDeltaHdrFields
+                   ? 1
+                   : 1 + int32_t((nf - wfsa::kDeltaHdrFields + wfsa::kDeltaFields - 1) / wfsa::kDeltaFields);
+    };
+    std::vector<int32_t> drows(size_t(std::max<int64_t>(nc, 1)));
+    parallel_for(nc, [&](int64_t b, int64_t e) {
+        std::vector<uint32_t> r;
+        for (int64_t i = b; i < e; ++i) {
+            words_of(comp[size_t(i)], r);
+            int64_t nf = 0;
+            encode(r, [&](uint32_t) { ++nf; });
+            drows[size_t(i)] = rows_of(nf);
+        }
+    });
+    // regroup, longest first (stable counting sort over the rows)
+    int32_t max_rows = 1;
+    for (int64_t i = 0; i < nc; ++i) max_rows = std::max(max_rows, drows[size_t(i)]);
+    if (max_rows > 0xffff) return fail(WFSA_ERR_CAPACITY, "delta stream: %d rows exceed the group header", max_rows);
+    std::vector<int64_t> cnt(size_t(max_rows) + 2, 0);
+    for (int64_t i = 0; i < nc; ++i) cnt[size_t(max_rows - drows[size_t(i)])]++;
+    int64_t acc = 0;
+    for (auto& c : cnt) {
+        const int64_t t = c;
+        c = acc;
+        acc += t;
+    }
+    std::vector<int32_t> dcomp(size_t(std::max<int64_t>(nc, 1))), drow_of(size_t(std::max<int64_t>(nc, 1)));
+    for (int64_t i = 0; i < nc; ++i) {
+        const int64_t k = cnt[size_t(max_rows - drows[size_t(i)])]++;
+        dcomp[size_t(k)] = comp[size_t(i)];
+        drow_of[size_t(k)] = drows[size_t(i)];
+    }
+    std::vector<int32_t> grows(size_t(std::max(G, 1)), 0);
+    for (int32_t g = 0; g < G; ++g) grows[size_t(g)] = drow_of[size_t(g) * kWave];
+    std::vector<int32_t> dorder, dwf;
+    deal(grows, dorder, dwf);
+    std::vector<int64_t> dg_base(size_t(G) + 1, 0);
+    std::vector<int32_t> dg_len(size_t(std::max(G, 1)), 0), dl_str(size_t(std::max(G, 1)) * kWave, -1);
+    int64_t dch = 0;
+    for (int32_t g = 0; g < G; ++g) {
+        const int32_t src = dorder[size_t(g)];
+        dg_base[size_t(g)] = dch;
+        dg_len[size_t(g)] = grows[size_t(src)];
+        for (int l = 0; l < kWave; ++l) {
+            const int64_t ks = int64_t(src) * kWave + l;
+            if (ks < nc) dl_str[size_t(g) * kWave + size_t(l)] = dcomp[size_t(ks)];
+        }
+        dch += int64_t(kWave) * dg_len[size_t(g)];
+    }
+    dg_base[size_t(G)] = dch;
+    std::vector<uint32_t> hd(size_t(std::max<int64_t>(dch, 1)) * 4, 0u);
+    parallel_for(int64_t(G), [&](int64_t b, int64_t e) {
+        std::vector<uint32_t> r;
+        for (int64_t g = b; g < e; ++g)
+            for (int l = 0; l < kWave; ++l) {
+                const int64_t base = dg_base[size_t(g)] + l;   // the lane's first row (chunk units)
+                const int32_t str = dl_str[size_t(g) * kWave + size_t(l)];
+                uint32_t* h = &hd[size_t(base) * 4];
+                const double pv = str >= 0 ? h_p[size_t(str)] : 0.0;
+                uint64_t pb;
+                std::memcpy(&pb, &pv, sizeof pb);
+                h[0] = uint32_t(pb);
+                h[1] = uint32_t(pb >> 32);
+                h[2] = uint32_t(dg_len[size_t(g)]);
+                if (str < 0) continue;
+                words_of(str, r);
+                int64_t q = 0;
+                encode(r, [&](uint32_t f) {
+                    const int64_t row =
+                        q < wfsa::kDeltaHdrFields ? 0 : 1 + (q - wfsa::kDeltaHdrFields) / wfsa::kDeltaFields;
+                    const int slot = q < wfsa::kDeltaHdrFields
+                                         ? int(wfsa::kDeltaFields - wfsa::kDeltaHdrFields + q)
+                                         : int((q - wfsa::kDeltaHdrFields) % wfsa::kDeltaFields);
+                    uint32_t* d = &hd[size_t(base + int64_t(kWave) * row) * 4];
+                    const int bit = wfsa::kDeltaBits * slot, wd = bit / 32, sh = bit % 32;
+                    d[wd] |= f << sh;
+                    if (sh + wfsa::kDeltaBits > 32) d[wd + 1] |= f >> (32 - sh);
+                    ++q;
+                });
+            }
+    });
+    HIP_TRY(ctx->dstream.upload(reinterpret_cast<const uint4*>(hd.data()), size_t(std::max<int64_t>(dch, 1)), s));
+    HIP_TRY(ctx->d_g_base.upload(dg_base.data(), dg_base.size(), s));
+    HIP_TRY(ctx->d_g_len.upload(dg_len.data(), dg_len.size(), s));
+    HIP_TRY(ctx->d_l_str.upload(dl_str.data(), dl_str.size(), s));
+    HIP_TRY(ctx->d_wave_first.upload(dwf.data(), dwf.size(), s));
+    HIP_TRY(hipStreamSynchronize(s));
+    ctx->delta_on = true;
+    ctx->d_tab = wfsa::delta_table(ctx->n_params);
+    ctx->d_stream_bytes = dch * 16;
+    return WFSA_OK;
+}
+
+// The per-iteration (or, per_iteration false, the preparation-time) stream
+// kernel's view of the compiled streams
+void stream_args(const wfsa_dev* ctx, wfsa::CompiledArgs& c, bool per_iteration) {
+    const bool d = per_iteration && ctx->delta_on;
+    c.stream = d ? ctx->dstream.ptr : ctx->stream_w.ptr;
+    c.g_base = d ? ctx->d_g_base.ptr : ctx->g_base.ptr;
+    c.g_len = d ? ctx->d_g_len.ptr : ctx->g_len.ptr;
+    c.l_str = d ? ctx->d_l_str.ptr : ctx->l_str.ptr;
+    c.l_len = ctx->l_len.ptr;   // (the 16-bit layout's: only the gradient pass reads it)
+    c.wave_first = d ? ctx->d_wave_first.ptr : ctx->wave_first.ptr;
+    c.wide = ctx->wide;
+    c.n_groups = ctx->n_groups;
+    c.d_tab = d ? ctx->d_tab : 0;
+}
+
 int prepare(wfsa_dev* ctx, int level) {
     if (ctx->dense) return prepare_dense(ctx, level);
     if (ctx->mpath) {   // nothing to compile: the structure came with the matrices
@@ -1354,22 +1527,27 @@ int prepare(wfsa_dev* ctx, int level) {
     // the per-iteration kernel's geometry: w staged in LDS when it fits, 16
     // waves per block, one block per CU (every block stages the whole table,
     // so fewer blocks stage less: measured 1/CU beats 2/CU at c3)
+    // the per-iteration kernel reads the delta format (fb_kernels.hpp) when it
+    // stages the weights and no stream word is a multi-parameter composite
+    const bool delta_want = ctx->use_delta && !ctx->wide && ctx->n_multi == 0 && nc > 0;
     {
         const size_t table_bytes = size_t(ctx->n_params) * sizeof(double);
-        ctx->i_tables = table_bytes + 16 <= size_t(kLdsPerCu - 1024) ? 1 : 0;
-        ctx->i_lds = ctx->i_tables ? table_bytes + 16 : 0;   // + the zero slot, even count
+        size_t stage_bytes = table_bytes + 16;   // + the zero slot, even count
+        if (delta_want) stage_bytes = std::max(stage_bytes, size_t(wfsa::delta_table(ctx->n_params)) * sizeof(double));
+        ctx->i_tables = stage_bytes <= size_t(kLdsPerCu - 1024) ? 1 : 0;
+        ctx->i_lds = ctx->i_tables ? stage_bytes : 0;
         // two 512-thread blocks per CU when two tables fit in LDS (same 16
         // waves per CU; c3: fbs 31.3 -> 30.1 us, profiles/r01/v19_block_sweep.txt),
         // else one 1024-thread block
-        ctx->i_block = (ctx->i_tables && 2 * (table_bytes + 16) <= size_t(kLdsPerCu - 1024)) ? 512 : 1024;
+        ctx->i_block = (ctx->i_tables && 2 * stage_bytes <= size_t(kLdsPerCu - 1024)) ? 512 : 1024;
         if (const char* e = std::getenv("WFSA_IBLOCK")) ctx->i_block = std::max(64, std::min(1024, std::atoi(e))) & ~63;
         const int i_wpb = ctx->i_block / kWave;
         int i_per_cu = std::max(1, kIterWavesPerCu / i_wpb);
         if (ctx->i_tables)
-            i_per_cu = std::min<int>(i_per_cu, int(size_t(kLdsPerCu) / std::max<size_t>(table_bytes, 1)));
+            i_per_cu = std::min<int>(i_per_cu, int(size_t(kLdsPerCu) / std::max<size_t>(stage_bytes, 1)));
         if (const char* e = std::getenv("WFSA_IPERCU")) i_per_cu = std::atoi(e);   // experiments (LDS-capped below)
         if (ctx->i_tables)
-            i_per_cu = std::min<int>(i_per_cu, int(size_t(kLdsPerCu) / std::max<size_t>(table_bytes, 1)));
+            i_per_cu = std::min<int>(i_per_cu, int(size_t(kLdsPerCu) / std::max<size_t>(stage_bytes, 1)));
         i_per_cu = std::max(1, i_per_cu);
         ctx->i_grid = int(std::max<int64_t>(1, std::min<int64_t>(int64_t(ctx->n_cu) * i_per_cu,
                                                                  (int64_t(G) + i_wpb - 1) / i_wpb)));
@@ -1383,6 +1561,30 @@ int prepare(wfsa_dev* ctx, int level) {
     const int i_wpb = ctx->i_block / kWave, i_nw = ctx->i_grid * i_wpb;
     std::vector<int32_t> order;
     std::vector<int32_t> wave_first(size_t(i_nw) + 1, 0);
+    std::vector<double> load0(size_t(i_nw), 0.0);   // each wave's bubble work, in stream rows
+    // groups (row counts in sorted order) to waves: longest first, each to the
+    // least loaded wave; each wave's groups then lie contiguously
+    auto deal = [&](const std::vector<int32_t>& grows, std::vector<int32_t>& ord, std::vector<int32_t>& wf) {
+        using Item = std::pair<double, int32_t>;
+        std::priority_queue<Item, std::vector<Item>, std::greater<Item>> heap;
+        for (int w = 0; w < i_nw; ++w) heap.push({load0[size_t(w)], w});
+        std::vector<std::vector<int32_t>> lists(static_cast<size_t>(i_nw));
+        for (int32_t g = 0; g < G; ++g) {
+            Item it = heap.top();
+            heap.pop();
+            lists[size_t(it.second)].push_back(g);
+            it.first += grows[size_t(g)];
+            heap.push(it);
+        }
+        ord.clear();
+        ord.reserve(size_t(G));
+        wf.assign(size_t(i_nw) + 1, 0);
+        for (int w = 0; w < i_nw; ++w) {
+            wf[size_t(w)] = int32_t(ord.size());
+            ord.insert(ord.end(), lists[size_t(w)].begin(), lists[size_t(w)].end());
+        }
+        wf[size_t(i_nw)] = G;
+    };
     {
         // costs in stream rows; small 18: the 16-20 optimum of the sweep after
         // the slot stores became coalesced (profiles/r02/v12_small_cost_sweep.txt:
@@ -1399,35 +1601,18 @@ int prepare(wfsa_dev* ctx, int level) {
         const int nblk = ctx->i_grid;
         const int small_wpb = small_waves_per_block(n_b - n_big_est, nblk);
         const int64_t small_waves = (n_b - n_big_est + kWave - 1) / kWave;
-        std::vector<double> load(size_t(i_nw), 0.0);
         for (int w = 0; w < i_nw; ++w) {
             const int bid = w / i_wpb, wib = w % i_wpb;
             if (bid == 0 && wib == i_wpb - 1) {   // the QN finish's wave (fbs_kernel): no groups
-                load[size_t(w)] = 1e300;
+                load0[size_t(w)] = 1e300;
                 continue;
             }
-            if (wib < small_wpb && int64_t(bid) * small_wpb + wib < small_waves) load[size_t(w)] += small_cost;
+            if (wib < small_wpb && int64_t(bid) * small_wpb + wib < small_waves) load0[size_t(w)] += small_cost;
             int64_t r = (nblk - 1 - bid) + int64_t(nblk) * (i_wpb - 1 - wib);
             r -= r > nblk - 1 ? 1 : 0;
-            if (r < n_big_est) load[size_t(w)] += big_cost;
+            if (r < n_big_est) load0[size_t(w)] += big_cost;
         }
-        using Item = std::pair<double, int32_t>;
-        std::priority_queue<Item, std::vector<Item>, std::greater<Item>> heap;
-        for (int w = 0; w < i_nw; ++w) heap.push({load[size_t(w)], w});
-        std::vector<std::vector<int32_t>> lists(static_cast<size_t>(i_nw));
-        for (int32_t g = 0; g < G; ++g) {
-            Item it = heap.top();
-            heap.pop();
-            lists[size_t(it.second)].push_back(g);
-            it.first += rows0[size_t(g)];
-            heap.push(it);
-        }
-        order.reserve(size_t(G));
-        for (int w = 0; w < i_nw; ++w) {
-            wave_first[size_t(w)] = int32_t(order.size());
-            order.insert(order.end(), lists[size_t(w)].begin(), lists[size_t(w)].end());
-        }
-        wave_first[size_t(i_nw)] = G;
+        deal(rows0, order, wave_first);
     }
     std::vector<int64_t> g_base(size_t(G) + 1, 0), s_base(SZ, 0), b_base(SZ, 0);
     std::vector<int32_t> g_len(size_t(std::max(G, 1)), 0), l_str(size_t(G) * kWave, -1), l_len(size_t(G) * kWave, 0);
@@ -1509,6 +1694,10 @@ int prepare(wfsa_dev* ctx, int level) {
         HIP_TRY(wfsa::launch_stream_headers(ctx->stream_w.ptr, ctx->g_base.ptr, ctx->g_len.ptr, d_pl.ptr, G,
                                             ctx->wide, s));
         HIP_TRY(hipStreamSynchronize(s));
+        ctx->delta_on = false;
+        ctx->d_tab = 0;
+        if (delta_want && ctx->i_tables)
+            if (int rc = build_delta(ctx, comp, h_main, s_base, h_p, chunks, G, deal)) return rc;
     }
     ctx->n_groups = G;
     ctx->n_compiled = nc;
@@ -1728,7 +1917,7 @@ int prepare(wfsa_dev* ctx, int level) {
     ctx->stats.wave_pull = ctx->w2_grid > 0 && ctx->w2_pull ? ctx->pl_items : 0;
     if (ctx->w2_grid == 0) ctx->stats.wave_row_entries = ctx->stats.wave_pair_edges = 0;
     ctx->stats.stream_words = words;
-    ctx->stats.stream_bytes = chunks * 16;
+    ctx->stats.stream_bytes = ctx->delta_on ? ctx->d_stream_bytes : chunks * 16;   // what the per-iteration pass reads
     ctx->stats.n_bubbles = nbub;
     ctx->stats.bubble_words = bwords;
     ctx->stats.tier1_strings = n_tier1;
@@ -1757,14 +1946,7 @@ int enqueue_compiled(wfsa_dev* ctx, bool with_grad, bool want_logq, const unsign
         wfsa::CompiledArgs c{};
         c.m = model_view(ctx);
         c.p = ctx->p.ptr;
-        c.stream = ctx->stream_w.ptr;
-        c.wide = ctx->wide;
-        c.g_base = ctx->g_base.ptr;
-        c.g_len = ctx->g_len.ptr;
-        c.l_str = ctx->l_str.ptr;
-        c.l_len = ctx->l_len.ptr;
-        c.wave_first = ctx->wave_first.ptr;
-        c.n_groups = ctx->n_groups;
+        stream_args(ctx, c, !with_grad);
         c.n_params = np;
         c.tables = tables;
         c.with_grad = with_grad ? 1 : 0;
@@ -2301,14 +2483,7 @@ int enqueue_qn_step_piped(wfsa_dev* ctx, double eta, double tol, int64_t e, bool
         wfsa::CompiledArgs c{};
         c.m = model_view(ctx);
         c.p = ctx->p.ptr;
-        c.stream = ctx->stream_w.ptr;
-        c.wide = ctx->wide;
-        c.g_base = ctx->g_base.ptr;
-        c.g_len = ctx->g_len.ptr;
-        c.l_str = ctx->l_str.ptr;
-        c.l_len = ctx->l_len.ptr;
-        c.wave_first = ctx->wave_first.ptr;
-        c.n_groups = ctx->n_groups;
+        stream_args(ctx, c, true);
         c.n_params = ctx->n_params;
         c.tables = ctx->i_tables;
         c.multi = ctx->n_multi > 0 ? 1 : 0;
@@ -2383,14 +2558,7 @@ int enqueue_qn_step_piped(wfsa_dev* ctx, double eta, double tol, int64_t e, bool
         wfsa::CompiledArgs c{};
         c.m = model_view(ctx);
         c.p = ctx->p.ptr;
-        c.stream = ctx->stream_w.ptr;
-        c.wide = ctx->wide;
-        c.g_base = ctx->g_base.ptr;
-        c.g_len = ctx->g_len.ptr;
-        c.l_str = ctx->l_str.ptr;
-        c.l_len = ctx->l_len.ptr;
-        c.wave_first = ctx->wave_first.ptr;
-        c.n_groups = ctx->n_groups;
+        stream_args(ctx, c, true);
         c.n_params = np;
         c.tables = ctx->i_tables;
         c.with_grad = 0;
@@ -2531,6 +2699,7 @@ int wfsa_dev_create(int device, wfsa_dev** out) {
     if (const char* e = std::getenv("WFSA_TIMING")) ctx->kernel_timing = e[0] != '0';
     if (const char* e = std::getenv("WFSA_TIMING_STRIDE")) ctx->timing_stride = std::max(1, std::atoi(e));
     if (const char* e = std::getenv("WFSA_FUSE_BUBBLES")) ctx->fuse_bubbles = e[0] != '0';
+    if (const char* e = std::getenv("WFSA_DELTA")) ctx->use_delta = e[0] != '0';
     if (const char* e = std::getenv("WFSA_DENSE"); e && e[0]) ctx->dense_mode = e[0] == '0' ? 0 : 1;
     if (const char* e = std::getenv("WFSA_TIER2")) ctx->force_tier2 = e[0] == '1';
     if (const char* e = std::getenv("WFSA_WIDE2")) ctx->use_wide2 = e[0] != '0';
