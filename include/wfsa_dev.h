@@ -205,6 +205,12 @@ int wfsa_dev_objective_grad(wfsa_dev* ctx, const double* w_full, double* loglik,
  * _end waits and writes the outputs.  Exactly one _end per _begin. */
 int wfsa_dev_objective_grad_begin(wfsa_dev* ctx, const double* w_full, int want_logq);
 int wfsa_dev_objective_grad_end(wfsa_dev* ctx, double* loglik, double* grad_full, double* logq);
+/* The host-mapped area _begin copies w_full into (n_params doubles; NULL
+ * before a model is loaded; valid until the next load).  A caller may write
+ * the weights there itself and pass w_full = NULL to _begin: one copy of
+ * the weights fewer per evaluation (the host QN binding does).  Not while an
+ * evaluation is in flight. */
+double* wfsa_dev_weights_staging(wfsa_dev* ctx);
 
 /* Device-resident QuasiNewton: QuasiNewtonLearner::OptimizationStep
  * (src/QuasiNewtonLearner.cpp:162-201) and the epoch loop (src/main.cpp:276-303)

@@ -120,3 +120,33 @@ def test_wave_pull_equals_push_and_repeats(family, monkeypatch):
     np.testing.assert_allclose(lq1, lqp, rtol=1e-12)
     assert _close(ll1, llp, rel=1e-12)
     np.testing.assert_allclose(g1, gp, rtol=1e-10, atol=1e-16)
+
+
+@pytest.mark.parametrize("n_strings,max_len", [(10_000, 128), (2_000, 600)])
+def test_wave_pull_fixed_point_gradient_at_scale(n_strings, max_len, monkeypatch):
+    """family B at scale: the pull kernel's 64-bit fixed-point gradient
+    (resolution 2^-F, F from max_len and parameters per edge) against tier 2's
+    fp64 sums (WFSA_WIDE2=0: block per string, pinned to the oracle by the
+    tests above) element by element.  Every credit is -p * posterior <= 0, so
+    no entry cancels: a relative bound holds for each nonzero entry, and the
+    zero entries must agree exactly."""
+    import wfsa_amd as W
+    syn = W.Synthetic(n_states=1024, degree=8, vocab=16, emissions=4, n_strings=n_strings, max_len=max_len, seed=31)
+    sym, off, wt = syn.corpus()
+    p = wt / wt.sum()
+    names = W.Fsa.read_text(syn.wfsa_text).param_names()
+    w = np.random.default_rng(9).normal(-1.5, 0.5, size=len(names))
+    monkeypatch.setenv("WFSA_WIDE2", "0")
+    *_, ll0, g0, lq0, st0 = _eval(syn.wfsa_text, sym, off, p, w, monkeypatch, False)
+    monkeypatch.setenv("WFSA_WIDE2", "1")
+    *_, ll1, g1, lq1, st1 = _eval(syn.wfsa_text, sym, off, p, w, monkeypatch, False)
+    assert st0["wave_strings"] == 0 and st1["wave_strings"] > 0.9 * n_strings
+    assert (g0 <= 0).all() and (g1 <= 0).all()
+    nz = g0 != 0
+    np.testing.assert_array_equal(g1[~nz], 0.0)
+    rel = np.abs(g1[nz] - g0[nz]) / np.abs(g0[nz])
+    print(f"{n_strings} strings, max len {int(np.diff(off).max())}: worst rel {rel.max():.2e}, "
+          f"{int(nz.sum())} nonzero entries, smallest |g| {np.abs(g0[nz]).min():.2e}")
+    assert rel.max() <= 1e-9
+    np.testing.assert_allclose(lq1, lq0, rtol=1e-12)
+    assert _close(ll1, ll0, rel=1e-12)

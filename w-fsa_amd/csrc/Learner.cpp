@@ -501,17 +501,29 @@ void Learner::Init(int flags, const double* initialx) {
     InitCallback(flags);
 }
 
+namespace {
+// GetWeight(j) for every full parameter (src/Learner.cpp:427-436): x of its
+// trimmed index, log 1 for a fixed singleton (-1), -inf for an unused one (-2)
+__attribute__((target_clones("avx2", "default"))) void get_weights(int32_t n, const int32_t* __restrict tw,
+                                                                   const double* __restrict x, double* __restrict w) {
+    const double ninf = -std::numeric_limits<double>::infinity();
+    for (int32_t j = 0; j < n; ++j) {
+        const int32_t t = tw[j];
+        const double xv = x[t >= 0 ? t : 0];
+        w[j] = t >= 0 ? xv : (t == -1 ? 0.0 : ninf);
+    }
+}
+}  // namespace
+
 void Learner::BeginModeledProbs(bool want_logq) {
     if (!dev) throw LearnerError("BuildFrom has not run");
     if (eval_in_flight) throw LearnerError("an evaluation is already in flight");
-    const int32_t* tw = trimmed_weights.data();
-    const double* x = _x.data();
-    double* w = w_full.data();
-    for (int32_t j = 0; j < n_full; ++j) {   // GetWeight(j), src/Learner.cpp:427-436
-        const int32_t t = tw[j];
-        w[j] = t >= 0 ? x[t] : (t == -1 ? 0.0 : -std::numeric_limits<double>::infinity());
-    }
-    ThrowOnDevError(wfsa_dev_objective_grad_begin(dev, w, want_logq ? 1 : 0),
+    // straight into the device's host-mapped staging area (one copy fewer)
+    double* staged = n_full > 0 ? wfsa_dev_weights_staging(dev) : nullptr;
+    double* w = staged ? staged : w_full.data();
+    const double none = 0.0;   // (no kept parameter: every index is negative, x is never read)
+    get_weights(n_full, trimmed_weights.data(), _x.empty() ? &none : _x.data(), w);
+    ThrowOnDevError(wfsa_dev_objective_grad_begin(dev, staged ? nullptr : w, want_logq ? 1 : 0),
                     "wfsa_dev_objective_grad_begin");
     eval_in_flight = true;
     eval_logq = want_logq;

@@ -2252,7 +2252,7 @@ __global__ __launch_bounds__(1024, (DBG == 10 ? 8 : 1)) void fbs_kernel(Compiled
     const int rows = int((a.g_base[g1] - cb) / kWave);
     const int last = max(rows - 1, 0);   // no groups: row 0 of the slack after the last group
     const uint4* st = a.stream + cb + lane;
-    constexpr int D = DBG == 6 ? 2 : (DBG == 7 ? 6 : kStreamPrefetch);
+    constexpr int D = DELTA ? kDeltaPrefetch : (DBG == 6 ? 2 : (DBG == 7 ? 6 : kStreamPrefetch));
     uint4 A[D], B[D];
     auto load = [&](uint4 (&r)[D], int c0) {
 #pragma unroll

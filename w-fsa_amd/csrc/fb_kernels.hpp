@@ -68,6 +68,13 @@ constexpr int kDeltaBits = 10;
 constexpr uint32_t kDeltaMax = (1u << kDeltaBits) - 1u;
 constexpr int kDeltaPeriod = 512;   // <= kDeltaMax: a zero slot is always within one step
 constexpr int kDeltaFields = 12, kDeltaHdrFields = 4;
+// rows per register set of the delta pass (two sets in flight): 12 gathers
+// per row, so fewer rows than the 16-bit pass's kStreamPrefetch (the stream
+// micro: D = 2 17.9 us, D = 3 19.0 us)
+#ifndef WFSA_DELTA_D
+#define WFSA_DELTA_D 2
+#endif
+constexpr int kDeltaPrefetch = WFSA_DELTA_D;
 __host__ __device__ inline int32_t delta_slot(int32_t j) { return j + 1 + j / (kDeltaPeriod - 1); }
 // table entries: every weight's slot and one zero slot after the last (an
 // index past it -- the end step of a string whose last word is the last

@@ -5,6 +5,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstdio>
 #include <cstdlib>
 
 namespace wfsa {
@@ -435,6 +436,11 @@ bool SymSolver::residual(const double* b, const double* x, double* r, double tol
     return ok;
 }
 
+// componentwise backward error the blocked factor's refined solve must meet
+// (the bar HessianLearner.cpp sets for the host sparse LDL^T); a factor that misses it is
+// replaced by the full Bunch-Kaufman (WFSA_KKT_TRACE logs that)
+constexpr double kRefineTol = 1e-9;
+
 const char* SymSolver::factor_coo(int64_t n, int64_t nnz, const int32_t* ei, const int32_t* ej, const double* ev,
                                   double* b, hipStream_t s, SymFactor* out, int* method) {
     factored_ = false;
@@ -495,12 +501,12 @@ const char* SymSolver::factor_coo(int64_t n, int64_t nnz, const int32_t* ei, con
                     return nullptr;
                 };
                 if (const char* e = dev_solve(rhs.data(), x.data())) return e;
-                ok = residual(rhs.data(), x.data(), r.data(), 1e-12);
+                ok = residual(rhs.data(), x.data(), r.data(), kRefineTol);
                 for (int it = 0; it < 3 && !ok; ++it) {
                     std::vector<double> dx(static_cast<size_t>(n));
                     if (const char* e = dev_solve(r.data(), dx.data())) return e;
                     for (int64_t q = 0; q < n; ++q) x[size_t(q)] += dx[size_t(q)];
-                    ok = residual(rhs.data(), x.data(), r.data(), 1e-12);
+                    ok = residual(rhs.data(), x.data(), r.data(), kRefineTol);
                 }
                 if (ok) std::copy(x.begin(), x.end(), b);
             }
@@ -511,6 +517,9 @@ const char* SymSolver::factor_coo(int64_t n, int64_t nnz, const int32_t* ei, con
                 return nullptr;
             }
         }
+        if (std::getenv("WFSA_KKT_TRACE"))
+            std::fprintf(stderr, "[kkt] n %lld: blocked factor %s; the full Bunch-Kaufman instead\n", (long long)n,
+                         exact ? "missed the refined residual bound" : "hit a pivot it cannot take");
     }
     // the full Bunch-Kaufman (LAPACK dsytf2 semantics) on the assembled matrix
     if (const char* e = ensure_blocked(n, s)) return e;
@@ -535,12 +544,12 @@ const char* SymSolver::solve(double* b, hipStream_t s) {
             return nullptr;
         };
         if (const char* e = dev_solve(rhs.data(), x.data())) return e;
-        bool ok = residual(rhs.data(), x.data(), r.data(), 1e-12);
+        bool ok = residual(rhs.data(), x.data(), r.data(), kRefineTol);
         for (int it = 0; it < 3 && !ok; ++it) {
             std::vector<double> dx(static_cast<size_t>(n));
             if (const char* e = dev_solve(r.data(), dx.data())) return e;
             for (int64_t q = 0; q < n; ++q) x[size_t(q)] += dx[size_t(q)];
-            ok = residual(rhs.data(), x.data(), r.data(), 1e-12);
+            ok = residual(rhs.data(), x.data(), r.data(), kRefineTol);
         }
         std::copy(x.begin(), x.end(), b);
         return nullptr;

@@ -1823,7 +1823,14 @@ int prepare(wfsa_dev* ctx, int level) {
         w2l.insert(w2l.end(), fb[0].begin(), fb[0].end());
         w2l.insert(w2l.end(), fb[1].begin(), fb[1].end());
     }
-    if (!w2l.empty() && ctx->use_wide2 && ctx->has_pairs && wide2_config(ctx)) {   // wave per string, a block per CU
+    // the wave kernel's fixed-point gradient holds a block's partial in 64
+    // bits with at least 20 fraction bits (below): longer strings than that
+    // bound allows stay on the fp64 tiers
+    int32_t fix_pe = 1;
+    for (size_t g = 0; g + 1 < ctx->h_pptr.size(); ++g) fix_pe = std::max(fix_pe, ctx->h_pptr[g + 1] - ctx->h_pptr[g]);
+    const double fix_bound = (double(ctx->max_len) + 2.0) * double(fix_pe);
+    if (!w2l.empty() && ctx->use_wide2 && ctx->has_pairs && fix_bound <= std::ldexp(1.0, 63 - 20) &&
+        wide2_config(ctx)) {   // wave per string, a block per CU
         {   // longest first: the waves take strings from a counter, the short ones fill the tail
             std::vector<int64_t> off(size_t(S) + 1);
             HIP_TRY(ctx->off.download(off.data(), off.size(), s));
@@ -1872,10 +1879,7 @@ int prepare(wfsa_dev* ctx, int level) {
         // position's edge and the end weight, each parameter once per
         // occurrence), so a block's partial fits a signed 64-bit word with
         // the rest as fraction (c3-like max_len 128: 2^-54)
-        int32_t pe = 1;
-        for (size_t g = 0; g + 1 < ctx->h_pptr.size(); ++g) pe = std::max(pe, ctx->h_pptr[g + 1] - ctx->h_pptr[g]);
-        const double bound = (double(ctx->max_len) + 2.0) * double(pe);
-        ctx->w2_fix_frac = std::max(20, std::min(60, 63 - int(std::ceil(std::log2(bound)))));
+        ctx->w2_fix_frac = std::max(20, std::min(60, 63 - int(std::ceil(std::log2(fix_bound)))));
         const size_t nfix = 2 * size_t(std::max(ctx->n_params, 1)) + 3;
         HIP_TRY(ctx->w2_fix.alloc(nfix));
         HIP_TRY(hipMemsetAsync(ctx->w2_fix.ptr, 0, nfix * sizeof(unsigned long long), s));
@@ -3064,7 +3068,6 @@ int wfsa_dev_string_tiers(wfsa_dev* ctx, int8_t* tier) {
 static int objective_grad_begin_impl(wfsa_dev* ctx, const double* w_full, int want_logq) {
     if (int rc = check_ctx(ctx)) return rc;
     if (!ctx->has_model || !ctx->has_corpus) return fail(WFSA_ERR_ARG, "load a model and a corpus first");
-    if (!w_full && ctx->n_params > 0) return fail(WFSA_ERR_ARG, "null weights");
     if (ctx->in_flight) return fail(WFSA_ERR_ARG, "objective_grad_begin called twice without _end");
     if (ctx->prep_level < 2)
         if (int rc = prepare(ctx, 2)) return rc;
@@ -3082,8 +3085,8 @@ static int objective_grad_begin_impl(wfsa_dev* ctx, const double* w_full, int wa
     }
     hipStream_t s = ctx->stream;
     const int32_t np = ctx->n_params;
-    double* win = ctx->pinned + weights_off(np);   // weights in
-    if (np > 0) std::memcpy(win, w_full, size_t(np) * sizeof(double));
+    double* win = ctx->pinned + weights_off(np);   // weights in (w_full == NULL: already written there)
+    if (np > 0 && w_full) std::memcpy(win, w_full, size_t(np) * sizeof(double));
     HIP_TRY(hipEventRecord(ctx->ev0, s));
     if (ctx->use_graph && !ctx->graph_exec && !ctx->graph_failed) {
         // capture once; a capture the runtime rejects falls back to eager launches
@@ -3139,7 +3142,13 @@ static int objective_grad_end_impl(wfsa_dev* ctx, double* loglik, double* grad_f
     return WFSA_OK;
 }
 
+double* wfsa_dev_weights_staging(wfsa_dev* ctx) {
+    if (!ctx || !ctx->has_model || !ctx->pinned || ctx->in_flight) return nullptr;
+    return ctx->pinned + weights_off(ctx->n_params);
+}
+
 int wfsa_dev_objective_grad(wfsa_dev* ctx, const double* w_full, double* loglik, double* grad_full, double* logq) {
+    if (!w_full && ctx && ctx->n_params > 0) return fail(WFSA_ERR_ARG, "null weights");   // (only _begin takes staged weights)
     if (int rc = wfsa_dev_objective_grad_begin(ctx, w_full, logq != nullptr)) return rc;
     return wfsa_dev_objective_grad_end(ctx, loglik, grad_full, logq);
 }

@@ -86,6 +86,7 @@ _SIGS = {
     "wfsa_learner_save_matrices": (C.c_int, [vp, C.c_char_p]),
     "wfsa_dev_objective_grad": (C.c_int, [vp, vp, P(dbl), vp, vp]),
     "wfsa_dev_objective_grad_begin": (C.c_int, [vp, vp, C.c_int]),
+    "wfsa_dev_weights_staging": (vp, [vp]),
     "wfsa_dev_objective_grad_end": (C.c_int, [vp, P(dbl), vp, vp]),
     "wfsa_dev_qn_setup": (C.c_int, [vp, vp]),
     "wfsa_dev_qn_set_state": (C.c_int, [vp, vp, vp]),
