@@ -127,10 +127,14 @@ def _device_eval(wfsa_text, sym, off, p, rng):
     dict(n_states=1024, degree=8, vocab=64, emissions=1, n_strings=2000, max_len=128),  # family A
 ])
 @pytest.mark.parametrize("dirty", [False, True], ids=["fresh", "dirty"])
-def test_device_matches_oracle_trellis_random_weights(family, dirty):
+@pytest.mark.parametrize("fmt", ["delta", "b16"])
+def test_device_matches_oracle_trellis_random_weights(family, dirty, fmt, monkeypatch):
     """dirty: the device memory the context will be handed was just written
-    with NaN (no buffer may rely on hipMalloc returning zeros)"""
+    with NaN (no buffer may rely on hipMalloc returning zeros); fmt: the
+    per-iteration stream kernel on the delta format (WFSA_DELTA=1) or the
+    16-bit words (=0)"""
     import wfsa_amd as W
+    monkeypatch.setenv("WFSA_DELTA", "1" if fmt == "delta" else "0")
     if dirty:
         _dirty_device_memory()
     rng = np.random.default_rng(7)

@@ -55,15 +55,23 @@ constexpr int kNwStep = 8, kNwGrad = 4;
 // LDS images of an operand slice (128 rows r x BK k), never transposed on
 // the way in, so every store is a plain conflict-free 16-byte write:
 //  * KC (the operand's rows contiguous along k in memory): [r][k], padded
-//    row of BK + 2 doubles (BK + 2 == 2 mod 32: a 64-lane fragment read
-//    (16 r x 4 k) is conflict free);
+//    row of BK + 1 doubles: the compiler pairs a fragment's reads for kk and
+//    kk + 1 into ds_read2_b64, banked per 16 lanes mod 32 dwords, where an
+//    odd pitch puts the 16 rows on distinct bank pairs (round 3's BK + 2,
+//    conflict-free for single ds_read_b64, left a third of the A reads'
+//    LDS cycles in conflicts: SQ_LDS_BANK_CONFLICT, profiles/r04/
+//    gemm_pmc.txt); the pitch is odd, so its stores are 8 bytes wide;
 //  * RC (memory rows run along r): [k][r], padded row of kLdn = 144
 //    doubles (2 kLdn == 32 mod 64: the fragment read's two k rows of a
 //    32-lane group fall on the two bank halves).
 // (Round 2's kernels stored RC slices transposed into [r][k]: 8-byte
 // stores four-way conflicted, a burst at every slice end while the MFMA
 // pipe idled -- 0.67 of the fp64 peak.)
+#ifdef WFSA_GEMM_LDK_EVEN   // (layout-variant builds: round 3's padding)
 template <int BK> constexpr int ldk() { return BK + 2; }
+#else
+template <int BK> constexpr int ldk() { return BK + 1; }
+#endif
 constexpr int kLdn = kDenseTile + 16;
 template <bool KC, int BK> constexpr int op_size() { return KC ? kT * ldk<BK>() : BK * kLdn; }
 template <int MODE, int BK> constexpr int stage();   // doubles per stage (A and B), below
@@ -139,9 +147,10 @@ __device__ __forceinline__ void store_slice(double* __restrict__ s, int tid, con
 #pragma unroll
     for (int c = 0; c < slice_chunks<BK, NT>(); ++c) {
         const int idx = c * NT + tid;
-        if (KC) {
+        if (KC) {   // (an odd row pitch: 8-byte stores)
             const int row = idx / kPairs, kp = idx % kPairs;
-            *reinterpret_cast<d2*>(s + row * L + 2 * kp) = v[c];
+            s[row * L + 2 * kp] = v[c].x;
+            s[row * L + 2 * kp + 1] = v[c].y;
         } else {
             const int kk = idx >> 6, rp = idx & 63;
             *reinterpret_cast<d2*>(s + kk * kLdn + 2 * rp) = v[c];
@@ -251,7 +260,11 @@ __global__ __launch_bounds__(NW * 64, (MODE == 2 && NW == 4 ? 2 : 1)) void dense
                 // reading that stage before the last barrier): the stores
                 // then overlap this wave's MFMAs instead of idling the matrix
                 // pipe before the barrier
+#ifdef WFSA_GEMM_STORE_END   // (layout-variant builds: the stores after the slice's MFMAs)
+                if (kk == BK / 4 - 1 && more) {
+#else
                 if (kk == BK / 8 && more) {
+#endif
                     double* s = lds + ((kt + 1) & 1) * kStage;
                     store_slice<A_KC, BK, NT>(s, tid, va);
                     store_slice<B_KC, BK, NT>(s + op_size<A_KC, BK>(), tid, vb);

@@ -2202,32 +2202,37 @@ __global__ __launch_bounds__(kBubbleBlock) void bubble_kernel(BubbleArgs a) {
 // DBG (timing experiments only, WFSA_FBS_DBG): 1 no table gathers, 3 no
 // stream pass at all, 4 neither stream pass nor table staging, 5 the QN finish only, 6 / 7
 // prefetch sets of 2 / 6 rows, 8 no bubble code, 9 stream loads only
-// One delta-format row (kDeltaBits fields, fb_kernels.hpp) of a lane: each
-// field steps the lane's index forward and gathers that entry of the staged
-// table; HDR: the group's first row, whose fields 0-7 hold p and the row
-// count.  The index is clamped to the table (a corrupt stream reads a zero
-// slot, never past LDS).
+// One delta-format row (fb_kernels.hpp) of a lane: three 10-bit fields per
+// dword; each steps the lane's LDS address in the staged table forward and
+// gathers that entry -- three VALU per field (extract, shift-add, f64 add).
+// HDR: the group's first row, whose fields 0-7 hold p and the row count.  A
+// valid stream never leaves the table (its last step lands on the final zero
+// slot); a corrupt one reads zeros past the allocation, never faults.
+typedef __attribute__((address_space(3))) const double lds_double;
+// the LDS address of the staged table (32-bit; the lane's cursor is kept as
+// one, so a gather needs no base add)
+__device__ __forceinline__ uint32_t lds_addr(const double* p) {
+    return uint32_t(reinterpret_cast<uintptr_t>((lds_double*)p));   // (an address-space cast)
+}
+// field k (0..2) of a dword: one v_bfe_u32 (written out: the compiler turns
+// a bfe followed by the << 3 into a shift and a mask, an instruction more)
+__device__ __forceinline__ uint32_t delta_field(uint32_t d, int k) {   // (k a constant after unrolling)
+    uint32_t f;
+    if (k == 0) asm("v_bfe_u32 %0, %1, 0, 10" : "=v"(f) : "v"(d));
+    else if (k == 1) asm("v_bfe_u32 %0, %1, 10, 10" : "=v"(f) : "v"(d));
+    else asm("v_bfe_u32 %0, %1, 20, 10" : "=v"(f) : "v"(d));
+    return f;
+}
 template <bool HDR>
-__device__ __forceinline__ void delta_row(const uint4 v, uint32_t& cur, const double* __restrict__ tab, uint32_t tmax,
-                                          double& a0, double& a1) {
-    constexpr uint32_t M = kDeltaMax;
-    uint32_t f[kDeltaFields];
-    f[0] = v.x & M;
-    f[1] = (v.x >> 10) & M;
-    f[2] = (v.x >> 20) & M;
-    f[3] = __builtin_amdgcn_alignbit(v.y, v.x, 30) & M;
-    f[4] = (v.y >> 8) & M;
-    f[5] = (v.y >> 18) & M;
-    f[6] = __builtin_amdgcn_alignbit(v.z, v.y, 28) & M;
-    f[7] = (v.z >> 6) & M;
-    f[8] = (v.z >> 16) & M;
-    f[9] = __builtin_amdgcn_alignbit(v.w, v.z, 26) & M;
-    f[10] = (v.w >> 4) & M;
-    f[11] = (v.w >> 14) & M;
+__device__ __forceinline__ void delta_row(const uint4 v, uint32_t& cur, double& a0, double& a1) {
+    const uint32_t d[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
     for (int i = HDR ? kDeltaFields - kDeltaHdrFields : 0; i < kDeltaFields; ++i) {
-        cur += f[i];
-        const double t = tab[min(cur, tmax)];
+        const uint32_t f = delta_field(d[i / 3], i % 3);
+        // (written out too: the compiler reassociates cur + (f << 3) into
+        // prefix sums of the fields plus a shift-add each, a third VALU)
+        asm("v_lshl_add_u32 %0, %1, 3, %2" : "=v"(cur) : "v"(f), "v"(cur));
+        const double t = *(lds_double*)uintptr_t(cur);
         if (i & 1) a1 += t;
         else a0 += t;
     }
@@ -2277,25 +2282,28 @@ __global__ __launch_bounds__(1024, (DBG == 10 ? 8 : 1)) void fbs_kernel(Compiled
         return;
     }
     if (DELTA && !a.no_streams) {
-        // the delta format's remapped table: slot s holds weight
-        // s - 1 - s / kDeltaPeriod, or zero on a multiple of kDeltaPeriod
-        // (and past the last weight); all of a thread's loads first
+        // the delta format's remapped table in 16-byte pieces: slots (s, s+1),
+        // s even, hold weights (j, j + 1), j = s - 1 - s / kDeltaPeriod
+        // (slot s is a zero slot when s is a multiple of kDeltaPeriod; s + 1,
+        // odd, never is), zero past the last weight; loads first
         constexpr int kB = 12;
-        const int T = a.d_tab;
-        for (int s0 = int(threadIdx.x); s0 < T; s0 += kB * int(blockDim.x)) {
-            double t[kB];
+        const int T2 = (a.d_tab + 1) / 2;
+        const int last = a.n_params - 1;
+        double2* dst = reinterpret_cast<double2*>(lds);
+        for (int q0 = int(threadIdx.x); q0 < T2; q0 += kB * int(blockDim.x)) {
+            double2 t[kB];
 #pragma unroll
             for (int b = 0; b < kB; ++b) {
-                const int s = s0 + b * int(blockDim.x);
-                const int j = s - 1 - s / kDeltaPeriod;
-                const bool z = (s % kDeltaPeriod) == 0 || j >= a.n_params;
-                const double v = a.w[min(max(j, 0), a.n_params - 1)];
-                t[b] = z ? 0.0 : v;
+                const int s2 = 2 * (q0 + b * int(blockDim.x));
+                const int j = s2 - 1 - s2 / kDeltaPeriod;
+                const double lo = a.w[min(max(j, 0), last)], hi = a.w[min(j + 1, last)];
+                t[b].x = (s2 % kDeltaPeriod) == 0 || j > last ? 0.0 : lo;
+                t[b].y = j + 1 > last ? 0.0 : hi;
             }
 #pragma unroll
             for (int b = 0; b < kB; ++b) {
-                const int s = s0 + b * int(blockDim.x);
-                if (s < T) lds[s] = t[b];
+                const int q = q0 + b * int(blockDim.x);
+                if (q < T2) dst[q] = t[b];
             }
         }
         __syncthreads();
@@ -2352,8 +2360,9 @@ __global__ __launch_bounds__(1024, (DBG == 10 ? 8 : 1)) void fbs_kernel(Compiled
             if (s >= 0) a.logq[s] = acc;
         }
     };
-    uint32_t cur = 0;   // DELTA: the lane's index into the remapped table
-    const uint32_t tmax = uint32_t(max(a.d_tab - 1, 0));
+    // DELTA: the lane's LDS address in the remapped table (its slot 0 at a group start)
+    const uint32_t tab0 = lds_addr(lds);
+    uint32_t cur = tab0;
     auto apply = [&](const uint4 (&r)[D], int c0) {
 #pragma unroll
         for (int d = 0; d < D; ++d) {
@@ -2368,10 +2377,10 @@ __global__ __launch_bounds__(1024, (DBG == 10 ? 8 : 1)) void fbs_kernel(Compiled
                     p = __longlong_as_double((long long)(v.x) | ((long long)(v.y) << 32));
                     hdr += __builtin_amdgcn_readfirstlane(int(v.z & 0xffffu));
                     ++grp;
-                    cur = 0;
-                    delta_row<true>(v, cur, wsrc, tmax, acc0, acc1);
+                    cur = tab0;
+                    delta_row<true>(v, cur, acc0, acc1);
                 } else {
-                    delta_row<false>(v, cur, wsrc, tmax, acc0, acc1);
+                    delta_row<false>(v, cur, acc0, acc1);
                 }
                 continue;
             }

@@ -59,10 +59,11 @@ __host__ __device__ inline int stream_hdr_words(int wide) { return wide ? 3 : 5;
 // table is remapped with a zero-weight slot every kDeltaPeriod entries
 // (slot 0 included): a gap longer than a step is bridged by steps onto zero
 // slots, the lane starts each string on slot 0 and ends it on a zero slot,
-// so padding fields (0) add nothing.  Row layout (16 bytes per lane): field
-// i at bits [10 i, 10 i + 10), 12 fields; the lane's first row of a group
-// carries p (bits 0-63) and the group's row count (bits 64-79) in place of
-// fields 0-7.  c3: 10.5 bits per word against 16 (profiles/r04/
+// so padding fields (0) add nothing.  Row layout (16 bytes per lane): three
+// 10-bit fields per dword (field i in dword i / 3 at bit 10 (i % 3); no
+// field straddles a dword), 12 fields; the lane's first row of a group
+// carries p (dwords 0-1) and the group's row count (bits 0-15 of dword 2) in
+// place of fields 0-7.  c3: 10.5 bits per word against 16 (profiles/r04/
 // stream_format_micro_v4b.txt).
 constexpr int kDeltaBits = 10;
 constexpr uint32_t kDeltaMax = (1u << kDeltaBits) - 1u;
@@ -76,12 +77,13 @@ constexpr int kDeltaFields = 12, kDeltaHdrFields = 4;
 #endif
 constexpr int kDeltaPrefetch = WFSA_DELTA_D;
 __host__ __device__ inline int32_t delta_slot(int32_t j) { return j + 1 + j / (kDeltaPeriod - 1); }
-// table entries: every weight's slot and one zero slot after the last (an
-// index past it -- the end step of a string whose last word is the last
-// weight -- is clamped onto it)
-__host__ __device__ inline int32_t delta_table(int32_t n_params) {
-    return n_params > 0 ? delta_slot(n_params - 1) + 2 : 1;
+// the zero slot after the last weight's: a string whose words end in the
+// last period steps onto it (not onto the next multiple of kDeltaPeriod)
+__host__ __device__ inline int32_t delta_end_slot(int32_t n_params) {
+    return n_params > 0 ? delta_slot(n_params - 1) + 1 : 0;
 }
+// table entries (even: the kernel stages 16-byte pieces)
+__host__ __device__ inline int32_t delta_table(int32_t n_params) { return (delta_end_slot(n_params) + 2) & ~1; }
 
 // Per-iteration record of a combined edge, one 16-byte gather in the
 // compiled kernel: its log-weight and its parameter list (p0 when np == 1).

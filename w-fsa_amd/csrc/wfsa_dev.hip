@@ -1262,7 +1262,8 @@ int build_delta(wfsa_dev* ctx, const std::vector<int32_t>& comp, const std::vect
         }
         std::sort(r.begin(), r.end());
     };
-    auto encode = [](const std::vector<uint32_t>& r, auto&& emit) {
+    const uint32_t z_end = uint32_t(wfsa::delta_end_slot(ctx->n_params));
+    auto encode = [z_end](const std::vector<uint32_t>& r, auto&& emit) {
         constexpr uint32_t M = wfsa::kDeltaMax, P = wfsa::kDeltaPeriod;
         uint32_t cur = 0;
         for (uint32_t t : r) {
@@ -1274,7 +1275,7 @@ int build_delta(wfsa_dev* ctx, const std::vector<int32_t>& comp, const std::vect
             emit(t - cur);
             cur = t;
         }
-        if (cur % P) emit((cur / P + 1) * P - cur);   // end on a zero slot: the padding adds nothing
+        if (cur % P) emit(std::min((cur / P + 1) * P, z_end) - cur);   // end on a zero slot: the padding adds nothing
     };
     auto rows_of = [](int64_t nf) {
         return nf <= wfsa::kDeltaHdrFields
@@ -1351,9 +1352,7 @@ int build_delta(wfsa_dev* ctx, const std::vector<int32_t>& comp, const std::vect
                                          ? int(wfsa::kDeltaFields - wfsa::kDeltaHdrFields + q)
                                          : int((q - wfsa::kDeltaHdrFields) % wfsa::kDeltaFields);
                     uint32_t* d = &hd[size_t(base + int64_t(kWave) * row) * 4];
-                    const int bit = wfsa::kDeltaBits * slot, wd = bit / 32, sh = bit % 32;
-                    d[wd] |= f << sh;
-                    if (sh + wfsa::kDeltaBits > 32) d[wd + 1] |= f >> (32 - sh);
+                    d[slot / 3] |= f << (wfsa::kDeltaBits * (slot % 3));   // three fields per dword
                     ++q;
                 });
             }
