@@ -14,6 +14,7 @@ for r in csv.DictReader(open(sys.argv[1])):
 PY
 }
 run odd WFSA_DENSE_BLAS=0 && run even WFSA_DENSE_BLAS=0 WFSA_LIB=w-fsa_amd/build_var/ldkeven/libwfsa_amd.so || exit 1
+run grad0 WFSA_DENSE_BLAS=0 WFSA_DENSE_GRAD_CFG=0 && run step2 WFSA_DENSE_BLAS=0 WFSA_DENSE_STEP_CFG=2 || exit 1
 WFSA_DENSE_BLAS=0 TD_EVALS=1 timeout -s KILL 180 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_WAIT_ANY --output-format csv -d gpurun_out/r4i/pmc/odd -o run -- python tools/time_dense.py > gpurun_out/r4i/pmc.log 2>&1 || { tail -5 gpurun_out/r4i/pmc.log; exit 1; }
 python tools/pmc_summary.py gpurun_out/r4i/pmc dense_gemm
 timeout -k 10 500 python -u -m pytest tests/test_gpu_dense.py -q -x --timeout 180 --timeout-method thread > gpurun_out/r4i/dense_tests.log 2>&1 || { tail -30 gpurun_out/r4i/dense_tests.log; exit 1; }

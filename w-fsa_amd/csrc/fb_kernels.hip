@@ -2282,23 +2282,27 @@ __global__ __launch_bounds__(1024, (DBG == 10 ? 8 : 1)) void fbs_kernel(Compiled
         return;
     }
     if (DELTA && !a.no_streams) {
-        // the delta format's remapped table in 16-byte pieces: slots (s, s+1),
-        // s even, hold weights (j, j + 1), j = s - 1 - s / kDeltaPeriod
-        // (slot s is a zero slot when s is a multiple of kDeltaPeriod; s + 1,
-        // odd, never is), zero past the last weight; loads first
+        // the delta format's remapped table in 16-byte pieces: slot s holds
+        // weight s - 1 - s / kDeltaPeriod, or zero on a multiple of
+        // kDeltaPeriod and past the last weight; loads first
         constexpr int kB = 12;
         const int T2 = (a.d_tab + 1) / 2;
         const int last = a.n_params - 1;
         double2* dst = reinterpret_cast<double2*>(lds);
+        auto wslot = [&](int s, bool& zero) {
+            const int j = s - 1 - s / kDeltaPeriod;
+            zero = (s % kDeltaPeriod) == 0 || j > last;
+            return min(max(j, 0), last);
+        };
         for (int q0 = int(threadIdx.x); q0 < T2; q0 += kB * int(blockDim.x)) {
             double2 t[kB];
 #pragma unroll
             for (int b = 0; b < kB; ++b) {
                 const int s2 = 2 * (q0 + b * int(blockDim.x));
-                const int j = s2 - 1 - s2 / kDeltaPeriod;
-                const double lo = a.w[min(max(j, 0), last)], hi = a.w[min(j + 1, last)];
-                t[b].x = (s2 % kDeltaPeriod) == 0 || j > last ? 0.0 : lo;
-                t[b].y = j + 1 > last ? 0.0 : hi;
+                bool z0, z1;
+                const double lo = a.w[wslot(s2, z0)], hi = a.w[wslot(s2 + 1, z1)];
+                t[b].x = z0 ? 0.0 : lo;
+                t[b].y = z1 ? 0.0 : hi;
             }
 #pragma unroll
             for (int b = 0; b < kB; ++b) {

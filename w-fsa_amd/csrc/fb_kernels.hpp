@@ -67,7 +67,11 @@ __host__ __device__ inline int stream_hdr_words(int wide) { return wide ? 3 : 5;
 // stream_format_micro_v4b.txt).
 constexpr int kDeltaBits = 10;
 constexpr uint32_t kDeltaMax = (1u << kDeltaBits) - 1u;
-constexpr int kDeltaPeriod = 512;   // <= kDeltaMax: a zero slot is always within one step
+// zero slots at the multiples of kDeltaPeriod (<= kDeltaMax: a zero slot is
+// always within one step); odd, so the zero slots fall on different LDS
+// banks -- the lanes whose strings have ended sit on them, as do the steps
+// bridging long gaps (at 512 every zero slot was on bank 0: N-way conflicts)
+constexpr int kDeltaPeriod = 511;
 constexpr int kDeltaFields = 12, kDeltaHdrFields = 4;
 // rows per register set of the delta pass (two sets in flight): 12 gathers
 // per row, so fewer rows than the 16-bit pass's kStreamPrefetch (the stream

@@ -1245,7 +1245,7 @@ void parallel_for(int64_t n, F&& fn) {
 template <class Deal>
 int build_delta(wfsa_dev* ctx, const std::vector<int32_t>& comp, const std::vector<int32_t>& h_main,
                 const std::vector<int64_t>& s_base, const std::vector<double>& h_p, int64_t chunks, int32_t G,
-                Deal&& deal) {
+                const std::vector<int32_t>& rows16_of, Deal&& deal) {
     hipStream_t s = ctx->stream;
     const int64_t nc = int64_t(comp.size());
     std::vector<uint16_t> h16(size_t(chunks) * 8);
@@ -1312,8 +1312,15 @@ int build_delta(wfsa_dev* ctx, const std::vector<int32_t>& comp, const std::vect
     }
     std::vector<int32_t> grows(size_t(std::max(G, 1)), 0);
     for (int32_t g = 0; g < G; ++g) grows[size_t(g)] = drow_of[size_t(g) * kWave];
+    // the bubble charges in delta rows: a wave's stream time goes with its
+    // bytes, so scale by the two formats' total rows
+    double rows16 = 0.0, rowsd = 0.0;
+    for (int32_t g = 0; g < G; ++g) {
+        rows16 += double(rows16_of[size_t(g)]);
+        rowsd += double(grows[size_t(g)]);
+    }
     std::vector<int32_t> dorder, dwf;
-    deal(grows, dorder, dwf);
+    deal(grows, dorder, dwf, rows16 > 0.0 ? rowsd / rows16 : 1.0);
     std::vector<int64_t> dg_base(size_t(G) + 1, 0);
     std::vector<int32_t> dg_len(size_t(std::max(G, 1)), 0), dl_str(size_t(std::max(G, 1)) * kWave, -1);
     int64_t dch = 0;
@@ -1563,10 +1570,13 @@ int prepare(wfsa_dev* ctx, int level) {
     std::vector<double> load0(size_t(i_nw), 0.0);   // each wave's bubble work, in stream rows
     // groups (row counts in sorted order) to waves: longest first, each to the
     // least loaded wave; each wave's groups then lie contiguously
-    auto deal = [&](const std::vector<int32_t>& grows, std::vector<int32_t>& ord, std::vector<int32_t>& wf) {
+    // (scale: the bubble work in this format's rows -- the costs below are
+    // in 16-bit rows)
+    auto deal = [&](const std::vector<int32_t>& grows, std::vector<int32_t>& ord, std::vector<int32_t>& wf,
+                    double scale) {
         using Item = std::pair<double, int32_t>;
         std::priority_queue<Item, std::vector<Item>, std::greater<Item>> heap;
-        for (int w = 0; w < i_nw; ++w) heap.push({load0[size_t(w)], w});
+        for (int w = 0; w < i_nw; ++w) heap.push({load0[size_t(w)] * scale, w});
         std::vector<std::vector<int32_t>> lists(static_cast<size_t>(i_nw));
         for (int32_t g = 0; g < G; ++g) {
             Item it = heap.top();
@@ -1611,7 +1621,7 @@ int prepare(wfsa_dev* ctx, int level) {
             r -= r > nblk - 1 ? 1 : 0;
             if (r < n_big_est) load0[size_t(w)] += big_cost;
         }
-        deal(rows0, order, wave_first);
+        deal(rows0, order, wave_first, 1.0);
     }
     std::vector<int64_t> g_base(size_t(G) + 1, 0), s_base(SZ, 0), b_base(SZ, 0);
     std::vector<int32_t> g_len(size_t(std::max(G, 1)), 0), l_str(size_t(G) * kWave, -1), l_len(size_t(G) * kWave, 0);
@@ -1696,7 +1706,7 @@ int prepare(wfsa_dev* ctx, int level) {
         ctx->delta_on = false;
         ctx->d_tab = 0;
         if (delta_want && ctx->i_tables)
-            if (int rc = build_delta(ctx, comp, h_main, s_base, h_p, chunks, G, deal)) return rc;
+            if (int rc = build_delta(ctx, comp, h_main, s_base, h_p, chunks, G, rows0, deal)) return rc;
     }
     ctx->n_groups = G;
     ctx->n_compiled = nc;
