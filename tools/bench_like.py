@@ -22,7 +22,9 @@ def main():
     lrn.set_info_rmin(False)
     k = int(os.environ.get("BL_STEPS", "20"))
     for rep in range(int(os.environ.get("BL_REPS", "6"))):
-        lrn.Run(10, 1.0, -1.0)
+        if os.environ.get("BL_PRESLEEP"):   # an idle device before the warm-up (as after the preparation)
+            time.sleep(float(os.environ["BL_PRESLEEP"]))
+        lrn.Run(int(os.environ.get("BL_WARM", "10")), 1.0, -1.0)
         if os.environ.get("BL_STATS", "1") == "1":
             lrn.stats()
         torch.cuda.synchronize()
