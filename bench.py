@@ -308,10 +308,12 @@ def roofline_of(m, traffic):
         tf = alg_flops / (fb_ms * 1e-3) / 1e12 if fb_ms > 0 else None
         return {"bound": "mfma", "achieved": tf, "peak": F64_MFMA_PEAK_TFS, "unit": "TFLOP/s",
                 "frac": tf / F64_MFMA_PEAK_TFS if tf else None, "traffic": None,
-                "kernel": ("rocblas_dgemm (library fp64 MFMA GEMMs) + our epilogue kernels, one evaluation"
-                           if st1.get("dense_blas") else
-                           "dense_gemm_kernel<FWD/BWD/GRAD> (hand-written v_mfma_f64_16x16x4f64, epilogues fused), "
-                           "one evaluation"),
+                "kernel": {1: "rocblas_dgemm (library fp64 MFMA GEMMs) + our epilogue kernels, one evaluation",
+                           2: "dense_gemm_kernel<RAW> (hand-written v_mfma_f64_16x16x4f64, K in two halves) + "
+                              "dense_gemm_kernel<GRAD> + our epilogue kernels, one evaluation"}.get(
+                               st1.get("dense_blas", 0),
+                               "dense_gemm_kernel<FWD/BWD/GRAD> (hand-written v_mfma_f64_16x16x4f64, epilogues "
+                               "fused), one evaluation"),
                 "timed_launches": timed, "evaluation_ms": fb_ms, "algorithmic_flops_per_evaluation": alg_flops,
                 "issued_flops_per_evaluation": 6.0 * npd * npd * R * max(T - 1, 0), "row_slots": R, "trellis_steps": T}
     comp = st1["compiled_strings"]
@@ -524,21 +526,32 @@ def main():
         out["cpu_baseline"] = None
     del m, lrn
     # the sub-records: configs[4] (dense, MFMA) and family B (traversal tiers)
+    # (dense_c5_rocblas: the same c5 run with rocBLAS dgemm for the GEMMs, the
+    # library reference for the hand-written engine's roofline fraction)
     if not distributed and not args.no_sub and args.workload == "c3":
-        for name in ("c5", "famB"):
+        for key in ("dense_c5", "famB", "dense_c5_rocblas"):
+            name = "famB" if key == "famB" else "c5"
             sw = workload_args(args, name, 1)
+            engine = os.environ.get("WFSA_DENSE_ENGINE")
+            if key == "dense_c5_rocblas":
+                os.environ["WFSA_DENSE_ENGINE"] = "blas"
             try:
                 sm = run_workload(sw, 1, 0, local_rank, False, dist, torch)
                 cpu = None
-                if sw["cpu_sample"] > 0 and args.cpu_sample != 0:
+                if sw["cpu_sample"] > 0 and args.cpu_sample != 0 and key != "dense_c5_rocblas":
                     why = ("path enumeration (the reference algorithm) is infeasible here" if sw["dense"] else
                            "the reference's BFS truncates or drops these ambiguous strings")
                     cpu = cpu_baseline_trellis(sm["syn"].wfsa_text, sm["sym"], sm["off"], sm["wt"], sw["cpu_sample"],
                                                why)
-                out["dense_c5" if name == "c5" else "famB"] = record(sm, None, cpu)
+                out[key] = record(sm, None, cpu)
                 del sm
             except Exception as e:   # a sub-record never takes the headline down
-                out["dense_c5" if name == "c5" else "famB"] = {"error": f"{type(e).__name__}: {e}"}
+                out[key] = {"error": f"{type(e).__name__}: {e}"}
+            finally:
+                if engine is None:
+                    os.environ.pop("WFSA_DENSE_ENGINE", None)
+                else:
+                    os.environ["WFSA_DENSE_ENGINE"] = engine
     if rank == 0:
         print(json.dumps(out), flush=True)
     if distributed:

@@ -8,12 +8,13 @@ import pytest
 pytestmark = pytest.mark.gpu
 
 
-@pytest.fixture(autouse=True, params=["mfma", "rocblas"])
+@pytest.fixture(autouse=True, params=["fused", "split", "blas"])
 def gemm_engine(request, monkeypatch):
-    """every test on both GEMM engines of the dense path: our fused
-    v_mfma_f64_16x16x4f64 kernels (WFSA_DENSE_BLAS=0) and rocBLAS dgemm
-    with our epilogue kernels (=1)"""
-    monkeypatch.setenv("WFSA_DENSE_BLAS", "0" if request.param == "mfma" else "1")
+    """every test on the three GEMM engines of the dense path: our fused
+    v_mfma_f64_16x16x4f64 kernels, our split-K RAW kernels with the epilogue
+    kernels, and rocBLAS dgemm with the epilogue kernels (WFSA_DENSE_ENGINE)"""
+    monkeypatch.delenv("WFSA_DENSE_BLAS", raising=False)
+    monkeypatch.setenv("WFSA_DENSE_ENGINE", request.param)
     return request.param
 
 

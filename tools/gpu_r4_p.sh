@@ -1,0 +1,16 @@
+# round 4: split-K RAW GEMM variants -- next-slice store mid-slice (default) vs at the slice end, K slices of 16 (2 blocks/CU) vs 32 (1 block/CU)
+set -o pipefail
+mkdir -p gpurun_out/r4p
+cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
+run() {   # name, env...
+  local n=$1; shift
+  env "$@" TD_EVALS=2 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/r4p/$n -o run -- python tools/time_dense.py > gpurun_out/r4p/$n.log 2>&1 || { tail -20 gpurun_out/r4p/$n.log; return 1; }
+  echo "== $n: $(grep eval gpurun_out/r4p/$n.log | tr '\n' ' ')"
+  python - $(find gpurun_out/r4p/$n -name "*kernel_stats.csv") <<'PY'
+import csv, sys
+for r in csv.DictReader(open(sys.argv[1])):
+    if any(k in r["Name"] for k in ("gemm", "epi")):
+        print(r["Name"][:64], r["Calls"], round(float(r["AverageNs"]) / 1e3, 1), round(float(r["TotalDurationNs"]) / 1e6, 1))
+PY
+}
+run mid && run end WFSA_LIB=w-fsa_amd/build_var/gend/libwfsa_amd.so && run bk32 WFSA_DENSE_STEP_CFG=3 || exit 1

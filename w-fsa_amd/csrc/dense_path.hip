@@ -32,6 +32,7 @@
 #include <limits>
 #include <numeric>
 #include <queue>
+#include <string>
 
 namespace wfsa {
 
@@ -52,6 +53,9 @@ constexpr int kBkStep = 32, kBkGrad = 16;
 // SIMD hide each other's LDS and barrier time), 4 for the gradient GEMM (two
 // blocks per CU do that)
 constexpr int kNwStep = 8, kNwGrad = 4;
+// engine 2's step GEMMs: K in two halves, 4-wave blocks, slices of 16 --
+// twice the blocks of a step's tile grid, two per CU (the gradient GEMM's shape)
+constexpr int kSplitK = 2;
 // LDS images of an operand slice (128 rows r x BK k), never transposed on
 // the way in, so every store is a plain conflict-free 16-byte write:
 //  * KC (the operand's rows contiguous along k in memory): [r][k], padded
@@ -82,7 +86,10 @@ constexpr int kRedThreads = 128;      // dense_reduce: one column per thread
 constexpr int kRowPad = 16;
 constexpr int kRedWindow = 64;        // symbols per LDS pass of dense_reduce
 
-enum GemmMode { FWD = 0, BWD = 1, GRAD = 2 };
+// RAW: a plain product (the forward's or the backward's operand layouts)
+// into out (K split s: into out2 for s = 1), the epilogue left to the
+// epilogue kernels -- split-K gives the 256-tile step GEMMs two blocks per CU
+enum GemmMode { FWD = 0, BWD = 1, GRAD = 2, RAW = 3 };
 
 struct GemmArgs {
     int32_t R, np, nct;
@@ -115,6 +122,8 @@ struct GemmArgs {
     double* grad;              // GRAD: out + 1
     int32_t n_params;
     const unsigned* halted;
+    double* out2;              // RAW: the second K half's product
+    int32_t splits;            // RAW: K halves (1 or 2); else 1
 };
 
 // Global -> registers -> LDS staging of one 128 x 16 operand slice.  KC: the
@@ -163,7 +172,7 @@ template <int MODE, int BK> constexpr int stage() { return op_size<MODE != 2, BK
 // NW waves per 128 x 128 block: 2 x (NW / 2), each a 64 x (256 / NW) tile
 // of 16 x 16 MFMA tiles (NJ of them per row of tiles)
 template <int MODE, int BK, int NW>
-__global__ __launch_bounds__(NW * 64, (MODE == 2 && NW == 4 ? 2 : 1)) void dense_gemm_kernel(GemmArgs a) {
+__global__ __launch_bounds__(NW * 64, ((MODE == GRAD || MODE == RAW) && NW == 4 && BK == 16 ? 2 : 1)) void dense_gemm_kernel(GemmArgs a) {
     if (a.halted && *a.halted) return;
     constexpr int NT = NW * 64, NWN = NW / 2, NJ = 16 / NW, WCOLS = 16 * NJ;
     constexpr int kLdk = ldk<BK>(), kStage = stage<MODE, BK>();
@@ -179,15 +188,16 @@ __global__ __launch_bounds__(NW * 64, (MODE == 2 && NW == 4 ? 2 : 1)) void dense
     const int wm = wave / NWN, wn = wave % NWN;
     const int np = a.np, ldx = a.ldx;
     const int mtiles = (MODE == GRAD ? np : a.R) / kT, ntiles = np / kT;
-    const int nb = mtiles * ntiles;
+    const int nb = mtiles * ntiles, splits = MODE == RAW ? a.splits : 1, total = nb * splits;
     int bid = int(blockIdx.x);
-    if ((nb & 7) == 0) bid = (bid & 7) * (nb >> 3) + (bid >> 3);   // XCD x: tiles [x nb/8, (x+1) nb/8)
-    const int mt_ = bid % mtiles, nt_ = bid / mtiles;
+    if ((total & 7) == 0) bid = (bid & 7) * (total >> 3) + (bid >> 3);   // XCD x: tiles [x total/8, (x+1) total/8)
+    const int sidx = bid / nb, tile = bid % nb;   // (RAW: K half sidx)
+    const int mt_ = tile % mtiles, nt_ = tile / mtiles;
     const int r0 = mt_ * kT, c0 = nt_ * kT;
 
     // per-row scalars of the block's output rows (read by the epilogue)
     auto row_scalars = [&]() {
-    if (MODE != GRAD && tid < kT) {
+    if ((MODE == FWD || MODE == BWD) && tid < kT) {
         const int r = r0 + tid;
         const int m = a.meta[r];
         const bool start = (m >> 9) & 1, end = (m >> 10) & 1;
@@ -234,13 +244,14 @@ __global__ __launch_bounds__(NW * 64, (MODE == 2 && NW == 4 ? 2 : 1)) void dense
         for (int j = 0; j < NJ; ++j) acc[i][j] = d4{0.0, 0.0, 0.0, 0.0};
 
     if (!a.no_mma) {
-        const int64_t nk = (MODE == GRAD ? a.kg : int64_t(np)) / BK;
+        const int64_t klen = (MODE == GRAD ? a.kg : int64_t(np)) / splits, kofs = int64_t(sidx) * klen;
+        const int64_t nk = klen / BK;
         const double* xa = a.x;
         const double* xb = a.bm;
         d2 va[CH], vb[CH];
         const int ldb = MODE == GRAD ? ldx : np;   // z / A, A^T
-        load_slice<A_KC, BK, NT>(xa, ldx, r0, 0, tid, va);
-        load_slice<B_KC, BK, NT>(xb, ldb, c0, 0, tid, vb);
+        load_slice<A_KC, BK, NT>(xa, ldx, r0, kofs, tid, va);
+        load_slice<B_KC, BK, NT>(xb, ldb, c0, kofs, tid, vb);
         row_scalars();   // its loads overlap the first slice's
         store_slice<A_KC, BK, NT>(lds, tid, va);
         store_slice<B_KC, BK, NT>(lds + op_size<A_KC, BK>(), tid, vb);
@@ -248,8 +259,8 @@ __global__ __launch_bounds__(NW * 64, (MODE == 2 && NW == 4 ? 2 : 1)) void dense
         for (int64_t kt = 0; kt < nk; ++kt) {
             const bool more = kt + 1 < nk;
             if (more) {
-                load_slice<A_KC, BK, NT>(xa, ldx, r0, (kt + 1) * BK, tid, va);
-                load_slice<B_KC, BK, NT>(xb, ldb, c0, (kt + 1) * BK, tid, vb);
+                load_slice<A_KC, BK, NT>(xa, ldx, r0, kofs + (kt + 1) * BK, tid, va);
+                load_slice<B_KC, BK, NT>(xb, ldb, c0, kofs + (kt + 1) * BK, tid, vb);
             }
             const double* As = lds + (kt & 1) * kStage;
             const double* Bs = As + op_size<A_KC, BK>();
@@ -291,6 +302,20 @@ __global__ __launch_bounds__(NW * 64, (MODE == 2 && NW == 4 ? 2 : 1)) void dense
 
     // epilogue: element (i, j, e) of this lane is row wm*64 + 16 i + (lane>>4)
     // + 4 e, column wn*WCOLS + 16 j + (lane & 15) of the block tile
+    if (MODE == RAW) {   // the raw product (4 rows x 16 columns = 128-byte runs per store)
+        double* o = sidx ? a.out2 : a.out;
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int j = 0; j < NJ; ++j)
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    const int row = r0 + wm * 64 + 16 * i + (lane >> 4) + 4 * e;
+                    const int col = c0 + wn * WCOLS + 16 * j + (lane & 15);
+                    o[int64_t(row) * ldx + col] = acc[i][j][e];
+                }
+        return;
+    }
     if (MODE == GRAD) {
 #pragma unroll
         for (int i = 0; i < 4; ++i)
@@ -566,6 +591,7 @@ struct EpiArgs {
     const double* a0;
     const double* aend;
     double* io;                // FWD: alpha[t+1] (the GEMM's alpha[t] A in, the values out); BWD: Y[t] likewise
+    const double* io2;         // a split-K GEMM's second product (added to io's), or null
     const double* la_in;       // FWD
     double* la_out;
     const double* lb_in;       // BWD
@@ -596,9 +622,11 @@ __global__ __launch_bounds__(kEpiThreads) void dense_fwd_epi_kernel(EpiArgs a) {
     if (threadIdx.x == 0) a.la_out[r] = la;
     const double* erow = a.et + int64_t(m & 511) * a.np;
     double* row = a.io + int64_t(r) * a.ldx;
+    const double* row2 = a.io2 ? a.io2 + int64_t(r) * a.ldx : nullptr;
     double acc = 0.0;
     for (int c = int(threadIdx.x); c < a.np; c += kEpiThreads) {
-        const double v = (start ? a.a0[c] : (a.first ? 0.0 : row[c] * inv)) * erow[c];
+        const double raw = a.first ? 0.0 : (row2 ? row[c] + row2[c] : row[c]);
+        const double v = (start ? a.a0[c] : raw * inv) * erow[c];
         row[c] = v;
         acc += v;
     }
@@ -633,9 +661,11 @@ __global__ __launch_bounds__(kEpiThreads) void dense_bwd_epi_kernel(EpiArgs a) {
     const double* erow = a.et + int64_t(m & 511) * a.np;
     const int64_t o0 = int64_t(r) * a.ldx;
     double* row = a.io + o0;
+    const double* row2 = a.io2 ? a.io2 + o0 : nullptr;
     double acc = 0.0;
     for (int c = int(threadIdx.x); c < a.np; c += kEpiThreads) {
-        const double beta = end ? a.aend[c] : (a.first ? 0.0 : row[c] * inv);
+        const double raw = a.first ? 0.0 : (row2 ? row[c] + row2[c] : row[c]);
+        const double beta = end ? a.aend[c] : raw * inv;
         a.gam[o0 + c] = a.alpha_t[o0 + c] * beta * f1;
         const double v = erow[c] * beta;
         row[c] = v;
@@ -954,7 +984,7 @@ void DensePath::free_model() {
 
 void DensePath::free_corpus() {
     dfree(meta_); dfree(sid_); dfree(end_at_); dfree(p_); dfree(pones_); dfree(logq_);
-    dfree(la_); dfree(lb_); dfree(alpha_); dfree(gam_); dfree(z_); dfree(y_); dfree(part_);
+    dfree(la_); dfree(lb_); dfree(alpha_); dfree(gam_); dfree(z_); dfree(y_); dfree(ysplit_); dfree(part_);
     dfree(ll_part_); dfree(red_);
     dfree(lmat_); dfree(let_); dfree(l0_); dfree(lend_); dfree(mrow_); dfree(spart_); dfree(rpart_);
     n_strings_ = 0;
@@ -990,8 +1020,15 @@ hipError_t DensePath::load_model(const DenseModel& m, hipStream_t s) {
     std::vector<double> ones(size_t(n_params_) + 2, 1.0);
     DTRY(dalloc(ones_, ones.size()));
     DTRY(hipMemcpyAsync(ones_, ones.data(), ones.size() * 8, hipMemcpyHostToDevice, s));
-    if (const char* e = std::getenv("WFSA_DENSE_BLAS")) use_blas_ = e[0] != '0';
-    if (use_blas_) {
+    if (const char* e = std::getenv("WFSA_DENSE_BLAS")) engine_ = e[0] != '0' ? 1 : 0;
+    if (const char* e = std::getenv("WFSA_DENSE_ENGINE")) {
+        const std::string v(e);
+        if (v == "fused") engine_ = 0;
+        else if (v == "blas") engine_ = 1;
+        else if (v == "split") engine_ = 2;
+        else return hipErrorInvalidValue;
+    }
+    if (engine_ == 1) {
         rocblas_handle h = nullptr;
         if (rocblas_create_handle(&h) != rocblas_status_success) return hipErrorNotInitialized;
         blas_ = h;
@@ -1099,6 +1136,7 @@ hipError_t DensePath::load_corpus(const uint8_t* sym, const int64_t* off, const 
     DTRY(dalloc(gam_, TR * ld));
     DTRY(dalloc(z_, TR * ld));
     DTRY(dalloc(y_, 2 * size_t(R) * ld));
+    if (engine_ == 2) DTRY(dalloc(ysplit_, size_t(R) * ld));
     DTRY(dalloc(part_, 2 * size_t(nct_) * size_t(R)));
     n_ll_ = int32_t((S + 3) / 4);
     DTRY(dalloc(ll_part_, size_t(std::max(n_ll_, 1))));
@@ -1122,7 +1160,7 @@ hipError_t DensePath::enqueue(const double* ewp, bool structural, double* out, d
     const double* w = structural ? ones_ : ewp;
     const double* p = structural ? pones_ : p_;
     weighted_ = !structural;
-    if (use_blas_ && blas_ && n_strings_ > 0 && total_sym_ > 0) return enqueue_blas(w, p, structural, out, logq, halted, s);
+    if (engine() != 0 && n_strings_ > 0 && total_sym_ > 0) return enqueue_lib(w, p, structural, out, logq, halted, s);
     {
         WeightsArgs a{};
         a.ewp = w;
@@ -1250,19 +1288,26 @@ hipError_t DensePath::enqueue(const double* ewp, bool structural, double* out, d
     return hipSuccess;
 }
 
-// The same evaluation with the GEMMs as plain rocBLAS dgemm calls (fp64 MFMA)
-// and the fused kernels' epilogues as their own per-row kernels: the row
-// slot buffers are row-major [R][ldx]; seen column-major they are np x R
-// (ld = ldx), so alpha[t+1]^T = A^T alpha[t]^T is dgemm(N, N) with the
-// row-major A as its column-major transpose, Y[t+1] A^T likewise with op T,
-// and G = alpha[0..T-2]^T z[1..T-1] as (G^T)^T = dgemm(N, T) over K = (T-1) R
-// rows.  Row sums: one full sum per row ([R], nct = 1).
-hipError_t DensePath::enqueue_blas(const double* w, const double* p, bool structural, double* out, double* logq,
-                                   const unsigned* halted, hipStream_t s) {
+// The same evaluation with the GEMMs as plain products and the fused
+// kernels' epilogues as their own per-row kernels.  Engine 1: rocBLAS dgemm
+// calls (fp64 MFMA): the row slot buffers are row-major [R][ldx]; seen
+// column-major they are np x R (ld = ldx), so alpha[t+1]^T = A^T alpha[t]^T
+// is dgemm(N, N) with the row-major A as its column-major transpose, Y[t+1]
+// A^T likewise with op T, and G = alpha[0..T-2]^T z[1..T-1] as (G^T)^T =
+// dgemm(N, T) over K = (T-1) R rows.  Engine 2: dense_gemm_kernel<RAW> with
+// K in two halves (the second into ysplit_, summed by the epilogue) and the
+// fused gradient kernel.  Row sums: one full sum per row ([R], nct = 1).
+hipError_t DensePath::enqueue_lib(const double* w, const double* p, bool structural, double* out, double* logq,
+                                  const unsigned* halted, hipStream_t s) {
     const size_t np = size_t(np_), R = size_t(R_);
+    const bool ours = engine() == 2;
     rocblas_handle h = static_cast<rocblas_handle>(blas_);
-    if (rocblas_set_stream(h, s) != rocblas_status_success) return hipErrorInvalidHandle;
+    if (!ours && rocblas_set_stream(h, s) != rocblas_status_success) return hipErrorInvalidHandle;
     auto rb = [](rocblas_status st) { return st == rocblas_status_success ? hipSuccess : hipErrorLaunchFailure; };
+    GemmArgs raw{};
+    raw.R = R_; raw.np = np_; raw.nct = nct_; raw.ldx = ldx_; raw.halted = halted;
+    raw.out2 = ysplit_; raw.splits = kSplitK;
+    const int raw_blocks = int((R / kT) * (np / kT)) * kSplitK;
     {
         WeightsArgs a{};
         a.ewp = w;
@@ -1276,6 +1321,10 @@ hipError_t DensePath::enqueue_blas(const double* w, const double* p, bool struct
         a.halted = halted;
         dense_weights_kernel<<<1024, 256, 0, s>>>(a);
         DTRY(hipGetLastError());
+        if (ours) {
+            dense_transpose_kernel<<<dim3(unsigned(np / 32), unsigned(np / 32)), 256, 0, s>>>(amat_, amat_t_, np_, halted);
+            DTRY(hipGetLastError());
+        }
     }
     const size_t step = R * size_t(ldx_);
     const double one = 1.0, zero = 0.0;
@@ -1285,10 +1334,20 @@ hipError_t DensePath::enqueue_blas(const double* w, const double* p, bool struct
     // forward
     for (int64_t t = -1; t + 1 < T_; ++t) {
         double* nxt = alpha_ + size_t(t + 1) * step;
-        if (t >= 0)   // alpha[t+1]^T = A^T alpha[t]^T (raw products; the epilogue scales)
+        if (t >= 0 && ours) {   // alpha[t+1] = alpha[t] A (raw products; the epilogue scales)
+            GemmArgs m = raw;
+            m.x = alpha_ + size_t(t) * step;
+            m.bm = amat_;
+            m.out = nxt;
+            if (step_cfg_ == 3) dense_gemm_kernel<RAW, kBkStep, 4><<<raw_blocks, 4 * 64, 0, s>>>(m);
+            else dense_gemm_kernel<RAW, kBkGrad, kNwGrad><<<raw_blocks, kNwGrad * 64, 0, s>>>(m);
+            DTRY(hipGetLastError());
+        } else if (t >= 0) {   // alpha[t+1]^T = A^T alpha[t]^T
             DTRY(rb(rocblas_dgemm(h, rocblas_operation_none, rocblas_operation_none, inp, iR, inp, &one, amat_, inp,
                                   alpha_ + size_t(t) * step, ild, &zero, nxt, ild)));
+        }
         EpiArgs f = g;
+        f.io2 = ours && t >= 0 ? ysplit_ : nullptr;
         f.first = t < 0;
         f.meta = meta_ + size_t(t + 1) * R;
         f.sum_in = part_ + size_t(t & 1) * R;
@@ -1310,10 +1369,20 @@ hipError_t DensePath::enqueue_blas(const double* w, const double* p, bool struct
     // backward
     for (int64_t t = T_ - 1; t >= 0; --t) {
         double* cur = y_ + size_t(t & 1) * step;
-        if (t < T_ - 1)   // beta[t]^T = A Y[t+1]^T (raw)
+        if (t < T_ - 1 && ours) {   // beta[t] = Y[t+1] A^T (raw)
+            GemmArgs m = raw;
+            m.x = y_ + size_t((t + 1) & 1) * step;
+            m.bm = amat_t_;
+            m.out = cur;
+            if (step_cfg_ == 3) dense_gemm_kernel<RAW, kBkStep, 4><<<raw_blocks, 4 * 64, 0, s>>>(m);
+            else dense_gemm_kernel<RAW, kBkGrad, kNwGrad><<<raw_blocks, kNwGrad * 64, 0, s>>>(m);
+            DTRY(hipGetLastError());
+        } else if (t < T_ - 1) {   // beta[t]^T = A Y[t+1]^T
             DTRY(rb(rocblas_dgemm(h, rocblas_operation_transpose, rocblas_operation_none, inp, iR, inp, &one, amat_, inp,
                                   y_ + size_t((t + 1) & 1) * step, ild, &zero, cur, ild)));
+        }
         EpiArgs b = g;
+        b.io2 = ours && t < T_ - 1 ? ysplit_ : nullptr;
         b.first = t == T_ - 1;
         b.meta = meta_ + size_t(t) * R;
         b.sid = sid_ + size_t(t) * R;
@@ -1330,7 +1399,18 @@ hipError_t DensePath::enqueue_blas(const double* w, const double* p, bool struct
         dense_bwd_epi_kernel<<<unsigned(R), kEpiThreads, 0, s>>>(b);
         DTRY(hipGetLastError());
     }
-    if (T_ >= 2) {   // G^T = z[1..]^T alpha[0..] over K = (T-1) R rows: g[S np + T] = G(S, T)
+    if (T_ >= 2 && ours) {   // G = alpha[0..T-2]^T z[1..T-1], scattered into the gradient by the kernel
+        GemmArgs q{};
+        q.R = R_; q.np = np_; q.nct = nct_; q.ldx = ldx_; q.halted = halted; q.n_params = n_params_; q.splits = 1;
+        q.kg = int64_t(T_ - 1) * int64_t(R);
+        q.x = alpha_;
+        q.bm = z_ + step;
+        q.code_a = code_a_;
+        q.amat = amat_;
+        q.grad = out + 1;
+        dense_gemm_kernel<GRAD, kBkGrad, kNwGrad><<<int((np / kT) * (np / kT)), kNwGrad * 64, 0, s>>>(q);
+        DTRY(hipGetLastError());
+    } else if (T_ >= 2) {   // G^T = z[1..]^T alpha[0..] over K = (T-1) R rows: g[S np + T] = G(S, T)
         const int64_t K = int64_t(T_ - 1) * int64_t(R);
         if (K >= (int64_t(1) << 31)) return hipErrorInvalidValue;
         DTRY(rb(rocblas_dgemm(h, rocblas_operation_none, rocblas_operation_transpose, inp, inp, rocblas_int(K), &one,

@@ -90,7 +90,9 @@ public:
     int32_t rows() const { return R_; }
     int32_t steps() const { return T_; }
     int32_t np() const { return np_; }
-    bool blas() const { return use_blas_ && blas_; }
+    // the GEMM engine the evaluations run: 0 fused MFMA kernels, 1 rocBLAS
+    // dgemm + epilogue kernels, 2 split-K MFMA kernels + epilogue kernels
+    int engine() const { return engine_ == 1 && !blas_ ? 0 : engine_; }
     int64_t total_symbols() const { return total_sym_; }
     // algorithmic fp64 flops of one evaluation: three GEMMs of 2 np^2 per
     // string position (forward, backward, gradient)
@@ -101,7 +103,7 @@ public:
 private:
     int n_cu_ = 256;
     int grad_cfg_ = 0;   // gradient GEMM: 4-wave blocks, K slices of 16, two blocks per CU (WFSA_DENSE_GRAD_CFG=1: 8-wave, 32; 65.7 vs 69.8 ms, profiles/r04/gemm_cfg_ab.txt)
-    int step_cfg_ = 0;   // WFSA_DENSE_STEP_CFG (timing experiments): 1 per-step GEMMs with 4-wave blocks, 2 K slices of 16
+    int step_cfg_ = 0;   // WFSA_DENSE_STEP_CFG (timing experiments): 1 per-step GEMMs with 4-wave blocks, 2 K slices of 16, 3 engine 2 with K slices of 32
     int32_t n_params_ = 0, np_ = 0, vocab_ = 0, nct_ = 0;
     int32_t code_se_ = kCodeNone;
     int16_t sym_of_byte_[256] = {};
@@ -140,12 +142,15 @@ private:
     double* ll_part_ = nullptr;
     int32_t n_ll_ = 0;
     double* red_ = nullptr;    // [chunks][vocab+2][np]
-    // the GEMMs as plain fp64 library GEMMs (rocBLAS, atomics off:
-    // deterministic) with our epilogue kernels; WFSA_DENSE_BLAS=0: the fused
-    // MFMA kernels above
-    bool use_blas_ = true;
+    // GEMM engine (WFSA_DENSE_ENGINE=fused|blas|split, default split;
+    // WFSA_DENSE_BLAS=0/1 = fused/blas): 1 the GEMMs as plain fp64 library GEMMs (rocBLAS, atomics
+    // off: deterministic) with our epilogue kernels; 2 the same flow with our
+    // RAW GEMM kernel (K split in two halves: 2 blocks per CU) for the step
+    // GEMMs and the fused gradient kernel; 0 the fused MFMA kernels above
+    int engine_ = 2;
     void* blas_ = nullptr;     // rocblas_handle
-    double* gbuf_ = nullptr;   // [np][np] the gradient GEMM's product
+    double* gbuf_ = nullptr;   // [np][np] the gradient GEMM's product (engine 1)
+    double* ysplit_ = nullptr; // [R][ldx] the second K half's products (engine 2)
     // rmin pass (allocated by its first call): log tables (+inf: no edge),
     // two row-slot buffers of log min-path weights, per column tile and
     // string the end minima, per block the string minima
@@ -156,8 +161,8 @@ private:
     double* mrow_ = nullptr;   // [2][R][np]
     double* spart_ = nullptr;  // [nct][S]
     double* rpart_ = nullptr;  // [2 * blocks]
-    hipError_t enqueue_blas(const double* w, const double* p, bool structural, double* out, double* logq,
-                            const unsigned* halted, hipStream_t s);
+    hipError_t enqueue_lib(const double* w, const double* p, bool structural, double* out, double* logq,
+                           const unsigned* halted, hipStream_t s);
     void free_corpus();
     void free_model();
 };

@@ -1118,7 +1118,7 @@ __global__ __launch_bounds__(kWide2Block) void wide2_kernel(WideArgs a) {
 #define WFSA_PULL_EXP 0
 #endif
 template <int NI, bool TRACK>
-__global__ __launch_bounds__(kWide2Block) void wave_pull_kernel(WideArgs a) {
+__global__ __launch_bounds__(kPullBlock) void wave_pull_kernel(WideArgs a) {
     constexpr int kUF = TRACK && WFSA_PULL_UF > 4 ? 4 : WFSA_PULL_UF, kUB = WFSA_PULL_UB;   // (the min forward's registers)
     if (a.halted && *a.halted) return;
     extern __shared__ __attribute__((aligned(16))) double lds2[];
@@ -1196,8 +1196,39 @@ __global__ __launch_bounds__(kWide2Block) void wave_pull_kernel(WideArgs a) {
         int exi = 0, esum = 0, last_n = 1;   // last_n: size of the current row
         int64_t roff = 0;
         bool alive = true;
+        // a step's header and first kUF entries per lane are loaded during the
+        // step before (they depend only on the string's bytes), so the step's
+        // chain starts at its LDS gathers, not at a global load
+        int pcd[kUF];
+        double pw[kUF], plw[kUF];
+        int4 pdh = make_int4(-1, -1, -1, -1);
+        auto load_entries = [&](int fb, int T, int t0, int* cd, double* w, double* lwv) {
+#pragma unroll
+            for (int u = 0; u < kUF; ++u) {
+                const int t = t0 + u;
+                const int64_t e = int64_t(fb) + int64_t(t) * kWave + lane;
+                cd[u] = t < T ? Q.fcode[e] : 0;
+                w[u] = t < T ? Q.fw[e] : 0.0;
+                if (TRACK) lwv[u] = t < T ? Q.flw[e] : -INFINITY;
+            }
+        };
+        auto prefetch = [&](int i) {   // step i's info is in the chunk registers
+            const int ii = i & (kWave - 1);
+            if (__builtin_amdgcn_readlane(vnb, ii) < 0) return;
+            pdh = Q.fhdr[int64_t(__builtin_amdgcn_readlane(vq, ii)) * kWave + lane];
+            load_entries(__builtin_amdgcn_readlane(vfb, ii), __builtin_amdgcn_readlane(vft, ii), 0, pcd, pw, plw);
+        };
+#ifndef WFSA_PULL_NOSTEPPF
+        if (L > 0) {
+            load_chunk(0);
+            prefetch(0);
+        }
+#endif
         for (int i = 0; i < L; ++i) {
+#ifdef WFSA_PULL_NOSTEPPF
             if ((i & (kWave - 1)) == 0) load_chunk(i / kWave);
+            prefetch(i);
+#endif
             const int ii = i & (kWave - 1);
             const int nb = __builtin_amdgcn_readlane(vnb, ii);
             if (nb < 0) {   // no edge consumes the byte
@@ -1206,7 +1237,7 @@ __global__ __launch_bounds__(kWide2Block) void wave_pull_kernel(WideArgs a) {
             }
             const int fb = __builtin_amdgcn_readlane(vfb, ii);
             const int T = __builtin_amdgcn_readlane(vft, ii);
-            const int4 dh = Q.fhdr[int64_t(__builtin_amdgcn_readlane(vq, ii)) * kWave + lane];   // the lane's destinations
+            const int4 dh = pdh;   // the lane's destinations
             const double sc = ldexp(1.0, -exi);
             const int64_t rn = roff + last_n;
             const double* Mi = Mg + int64_t(i & 1) * MN;
@@ -1221,13 +1252,15 @@ __global__ __launch_bounds__(kWide2Block) void wave_pull_kernel(WideArgs a) {
             for (int t0 = 0; t0 < T; t0 += kUF) {
                 int cd[kUF];
                 double w[kUF], r[kUF], lwv[kUF], mv[kUF];
+                if (t0 == 0) {
 #pragma unroll
-                for (int u = 0; u < kUF; ++u) {
-                    const int t = t0 + u;
-                    const int64_t e = int64_t(fb) + int64_t(t) * kWave + lane;
-                    cd[u] = t < T ? Q.fcode[e] : 0;
-                    w[u] = t < T ? Q.fw[e] : 0.0;
-                    if (TRACK) lwv[u] = t < T ? Q.flw[e] : -INFINITY;
+                    for (int u = 0; u < kUF; ++u) {
+                        cd[u] = pcd[u];
+                        w[u] = pw[u];
+                        lwv[u] = plw[u];
+                    }
+                } else {
+                    load_entries(fb, T, t0, cd, w, lwv);
                 }
 #pragma unroll
                 for (int u = 0; u < kUF; ++u) r[u] = R[cd[u] & 0xffff];
@@ -1254,6 +1287,12 @@ __global__ __launch_bounds__(kWide2Block) void wave_pull_kernel(WideArgs a) {
                     }
                 }
             }
+#ifndef WFSA_PULL_NOSTEPPF
+            if (i + 1 < L) {   // the next step's header and entries, in flight over this step's row write
+                if (((i + 1) & (kWave - 1)) == 0) load_chunk((i + 1) / kWave);
+                prefetch(i + 1);
+            }
+#endif
             wave_sync();   // every lane has read the row
             int emx = kExpNone;   // the row's largest exponent (ballots, no LDS)
             {
@@ -1347,6 +1386,21 @@ __global__ __launch_bounds__(kWide2Block) void wave_pull_kernel(WideArgs a) {
         int ex_next = exi, vex = 0;
         int4 sl_next = make_int4(-1, -1, -1, -1);   // the next (lower) step's source list, loaded a step early
         bool have_next = false;
+        // entries: each round's loads issued before the round before it is
+        // summed, the next step's first round during this step's row write
+        // (within a chunk of step registers)
+        int4 ben[kUB];
+        double bwn[kUB];
+        bool have_ent = false;
+        auto load_b = [&](int bb, int T, int t0, int4* en, double* w) {
+#pragma unroll
+            for (int u = 0; u < kUB; ++u) {
+                const int t = t0 + u;
+                const int64_t e = int64_t(bb) + int64_t(t + 1) * kWave + lane;   // (row 0: the lane's sources)
+                en[u] = t < T ? Q.bent[e] : make_int4(0, -1, -1, -1);
+                w[u] = t < T ? Q.bw[e] : 0.0;
+            }
+        };
         for (int i = L - 1; i >= 0; --i) {
             if (i == L - 1 || (i & (kWave - 1)) == kWave - 1) {   // this step's chunk (steps and row exponents)
                 load_chunk(i / kWave);
@@ -1384,16 +1438,24 @@ __global__ __launch_bounds__(kWide2Block) void wave_pull_kernel(WideArgs a) {
                 dd[k] = -1;
             }
             double s = 0.0;
+#ifdef WFSA_PULL_NOSTEPPF
+            have_ent = false;
+#endif
+            if (!have_ent) load_b(bb, T, 0, ben, bwn);
             for (int t0 = 0; t0 < T; t0 += kUB) {
                 int4 en[kUB];
                 double w[kUB], bn[kUB];
+#ifdef WFSA_PULL_NOSTEPPF   // (A/B variant: round 3's load, gather, sum)
+                if (t0 > 0) load_b(bb, T, t0, ben, bwn);
+#endif
 #pragma unroll
                 for (int u = 0; u < kUB; ++u) {
-                    const int t = t0 + u;
-                    const int64_t e = int64_t(bb) + int64_t(t + 1) * kWave + lane;   // (row 0: the lane's sources)
-                    en[u] = t < T ? Q.bent[e] : make_int4(0, -1, -1, -1);
-                    w[u] = t < T ? Q.bw[e] : 0.0;
+                    en[u] = ben[u];
+                    w[u] = bwn[u];
                 }
+#ifndef WFSA_PULL_NOSTEPPF
+                if (t0 + kUB < T) load_b(bb, T, t0 + kUB, ben, bwn);
+#endif
 #pragma unroll
                 for (int u = 0; u < kUB; ++u) bn[u] = R[en[u].x & 0xffff];
 #pragma unroll
@@ -1429,6 +1491,11 @@ __global__ __launch_bounds__(kWide2Block) void wave_pull_kernel(WideArgs a) {
                     s = f ? 0.0 : s;
                 }
             }
+#ifndef WFSA_PULL_NOSTEPPF
+            have_ent = ii != 0;   // step i - 1 in this chunk of step registers
+#endif
+            if (have_ent)
+                load_b(__builtin_amdgcn_readlane(vbb, ii - 1), __builtin_amdgcn_readlane(vbt, ii - 1), 0, ben, bwn);
             wave_sync();   // every lane has read the row
 #pragma unroll
             for (int k = 0; k < NI; ++k)

@@ -313,6 +313,12 @@ hipError_t launch_wide(bool counting, const WideArgs& a, int grid, hipStream_t s
 // HBM (zeroed behind the backward), gradient in one LDS table per block
 // when n_params fits.  grid: blocks.
 constexpr int kWide2Block = 1024;
+// wave_pull_kernel's largest block: its launch bound sets the register budget
+// (1024 threads: 4 waves per SIMD, 128 VGPRs)
+#ifndef WFSA_PULL_BLOCK
+#define WFSA_PULL_BLOCK 1024
+#endif
+constexpr int kPullBlock = WFSA_PULL_BLOCK;
 inline int64_t wide2_stride(int32_t max_len, int32_t max_n) {
     return 1 + int64_t(max_len) * max_n + 2 * int64_t(max_n) + (int64_t(max_len) + 3) / 2 + 2;
 }

@@ -527,13 +527,14 @@ bool wide2_config(wfsa_dev* ctx) {
     };
     int best = 0;
     bool lg = false;
+    const int wmax = pull ? wfsa::kPullBlock / kWave : 16;
     for (int w : {16, 12, 8, 4})
-        if (!best && lds(true, w) <= cap) {
+        if (!best && w <= wmax && lds(true, w) <= cap) {
             best = w;
             lg = true;
         }
     for (int w : {16, 12, 8, 4})
-        if (!best && lds(false, w) <= cap) best = w;
+        if (!best && w <= wmax && lds(false, w) <= cap) best = w;
     if (!best) return false;
     ctx->w2_waves = best;
     ctx->w2_lgrad = lg;
@@ -2646,7 +2647,7 @@ int dense_load_corpus(wfsa_dev* ctx, const uint8_t* sym, const int64_t* off, con
     ctx->stats.dense_rows = ctx->dense->rows();
     ctx->stats.dense_steps = ctx->dense->steps();
     ctx->stats.dense_np = ctx->dense->np();
-    ctx->stats.dense_blas = ctx->dense->blas() ? 1 : 0;
+    ctx->stats.dense_blas = ctx->dense->engine();
     return WFSA_OK;
 }
 
