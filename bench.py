@@ -327,9 +327,11 @@ def roofline_of(m, traffic):
                 "kernel": "fbs_kernel (compiled-stream forward pass + fused bubbles, per step)",
                 "timed_launches": timed, "kernel_ms_per_launch": kern_ms, "all_fb_kernels_ms_per_step": fb_ms,
                 "algorithmic_bytes_per_launch": alg_bytes,
-                "note": ("the stream pass is bound by LDS random gathers (one weight per trivial word), not HBM: "
-                         "every stream format measured runs 17-18 us on its own, the 16-bit stream's loads alone "
-                         "16.6 us (profiles/r03/stream_format_micro_v2.txt, DESIGN 3)")}
+                "note": ("the pass reads the compiled stream (10-bit delta words, 1.62x the algorithmic bytes in "
+                         "PMC traffic) and is bound by those bytes: the delta stream's loads alone take 15.4 us of "
+                         "the micro's 17.9 us pass (profiles/r04/stream_format_micro_v4b.txt); HIP events around "
+                         "the launch include its ~3 us launch gap (rocprof's kernel average is the tighter figure, "
+                         "profiles/r04/, DESIGN 3)")}
     # family B: the traversal strings (k_c..k_2 of the evaluation)
     trav_ms = max(fb_ms - kern_ms, 1e-9)
     rows, pedges = st1.get("wave_row_entries", 0), st1.get("wave_pair_edges", 0)

@@ -13,4 +13,18 @@ for r in csv.DictReader(open(sys.argv[1])):
         print(r["Name"][:64], r["Calls"], round(float(r["AverageNs"]) / 1e3, 1), round(float(r["TotalDurationNs"]) / 1e6, 1))
 PY
 }
-run mid && run end WFSA_LIB=w-fsa_amd/build_var/gend/libwfsa_amd.so && run bk32 WFSA_DENSE_STEP_CFG=3 || exit 1
+run mid && run end WFSA_LIB=w-fsa_amd/build_var/gend/libwfsa_amd.so && run bk32 WFSA_DENSE_STEP_CFG=3 && run frag WFSA_LIB=w-fsa_amd/build_var/gfrag/libwfsa_amd.so && run prio WFSA_LIB=w-fsa_amd/build_var/gprio/libwfsa_amd.so || exit 1
+# family B: the next step's source alpha loaded a step early too (variant avpf) vs the default
+famb() {   # name, env...
+  local n=$1; shift
+  env "$@" timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/r4p/$n -o run -- python tools/time_famb.py > gpurun_out/r4p/$n.log 2>&1 || { tail -20 gpurun_out/r4p/$n.log; return 1; }
+  echo "== $n: $(grep evaluation gpurun_out/r4p/$n.log)"
+  python - $(find gpurun_out/r4p/$n -name "*kernel_stats.csv") <<'PY'
+import csv, sys
+for r in csv.DictReader(open(sys.argv[1])):
+    if "wave_pull" in r["Name"]:
+        print(r["Name"][:64], r["Calls"], round(float(r["AverageNs"]) / 1e3, 1), "min", round(float(r["MinNs"]) / 1e3, 1))
+PY
+}
+famb fb_pf && famb fb_avpf WFSA_LIB=w-fsa_amd/build_var/avpf/libwfsa_amd.so || exit 1
+bash tools/gpu_r4_q.sh

@@ -264,6 +264,18 @@ __global__ __launch_bounds__(NW * 64, ((MODE == GRAD || MODE == RAW) && NW == 4 
             }
             const double* As = lds + (kt & 1) * kStage;
             const double* Bs = As + op_size<A_KC, BK>();
+            // a wave's fragments of k-step kk: 4 A values (its 64 rows) and NJ B values
+            auto frag = [&](int kk, double (&av)[4], double (&bv)[NJ]) {
+#pragma unroll
+                for (int i = 0; i < 4; ++i)
+                    av[i] = A_KC ? As[(wm * 64 + i * 16 + (lane & 15)) * kLdk + kk * 4 + (lane >> 4)]
+                                 : As[(kk * 4 + (lane >> 4)) * kLdn + wm * 64 + i * 16 + (lane & 15)];
+#pragma unroll
+                for (int j = 0; j < NJ; ++j) bv[j] = Bs[(kk * 4 + (lane >> 4)) * kLdn + wn * WCOLS + j * 16 + (lane & 15)];
+            };
+#ifdef WFSA_GEMM_FRAG_PF
+            double fa[2][4], fb[2][NJ];
+#endif
 #pragma unroll
             for (int kk = 0; kk < BK / 4; ++kk) {
                 // the next slice into the other stage half-way through this
@@ -280,18 +292,26 @@ __global__ __launch_bounds__(NW * 64, ((MODE == GRAD || MODE == RAW) && NW == 4 
                     store_slice<A_KC, BK, NT>(s, tid, va);
                     store_slice<B_KC, BK, NT>(s + op_size<A_KC, BK>(), tid, vb);
                 }
+#ifdef WFSA_GEMM_FRAG_PF   // (variant builds: fragments of k-step kk + 1 read before kk's MFMAs)
+                if (kk == 0) frag(0, fa[0], fb[0]);
+                if (kk + 1 < BK / 4) frag(kk + 1, fa[(kk + 1) & 1], fb[(kk + 1) & 1]);
+                double (&av)[4] = fa[kk & 1];
+                double (&bv)[NJ] = fb[kk & 1];
+#else
                 double av[4], bv[NJ];
-#pragma unroll
-                for (int i = 0; i < 4; ++i)
-                    av[i] = A_KC ? As[(wm * 64 + i * 16 + (lane & 15)) * kLdk + kk * 4 + (lane >> 4)]
-                                 : As[(kk * 4 + (lane >> 4)) * kLdn + wm * 64 + i * 16 + (lane & 15)];
-#pragma unroll
-                for (int j = 0; j < NJ; ++j) bv[j] = Bs[(kk * 4 + (lane >> 4)) * kLdn + wn * WCOLS + j * 16 + (lane & 15)];
+                frag(kk, av, bv);
+#endif
+#ifdef WFSA_GEMM_PRIO
+                __builtin_amdgcn_s_setprio(1);
+#endif
 #pragma unroll
                 for (int i = 0; i < 4; ++i)
 #pragma unroll
                     for (int j = 0; j < NJ; ++j)
                         acc[i][j] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[i], bv[j], acc[i][j], 0, 0, 0);
+#ifdef WFSA_GEMM_PRIO
+                __builtin_amdgcn_s_setprio(0);
+#endif
             }
             __syncthreads();
         }
