@@ -14,6 +14,9 @@ for r in csv.DictReader(open(sys.argv[1])):
 PY
 }
 run mid && run end WFSA_LIB=w-fsa_amd/build_var/gend/libwfsa_amd.so && run bk32 WFSA_DENSE_STEP_CFG=3 && run frag WFSA_LIB=w-fsa_amd/build_var/gfrag/libwfsa_amd.so && run prio WFSA_LIB=w-fsa_amd/build_var/gprio/libwfsa_amd.so || exit 1
+# counters of the RAW GEMM (one evaluation)
+TD_EVALS=1 timeout -s KILL 180 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_LDS SQ_WAIT_ANY SQ_WAVE_CYCLES SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE --output-format csv -d gpurun_out/r4p/pmc -o run -- python tools/time_dense.py > gpurun_out/r4p/pmc.log 2>&1 || { tail -5 gpurun_out/r4p/pmc.log; exit 1; }
+python tools/pmc_summary.py gpurun_out/r4p/pmc dense_gemm
 # family B: the next step's source alpha loaded a step early too (variant avpf) vs the default
 famb() {   # name, env...
   local n=$1; shift

@@ -629,11 +629,22 @@ int Collective::try_peer(hipStream_t s) {
     }
     constexpr size_t kCheck = 3000;   // spans three chunks
     const size_t dbytes = std::max(kCheck * sizeof(double), size_t(kLocalMaxRanks) * sizeof(PeerBlob));
+    // the agreement's buffer: device memory, else host-mapped memory (so a
+    // member short of device memory still takes part in every exchange below
+    // and reports its failure as its "bad" byte)
     uint8_t* d = nullptr;
+    uint8_t* dh = nullptr;
     if (hipMalloc(reinterpret_cast<void**>(&d), dbytes) != hipSuccess) {
         (void)hipGetLastError();
-        err_ = "peer set-up: no device memory for the agreement";
-        return 1;   // (the caller fails and aborts the communicator: every member hears of it)
+        d = nullptr;
+        if (hipHostMalloc(reinterpret_cast<void**>(&dh), dbytes, hipHostMallocMapped | hipHostMallocCoherent) !=
+                hipSuccess ||
+            hipHostGetDevicePointer(reinterpret_cast<void**>(&d), dh, 0) != hipSuccess) {
+            (void)hipGetLastError();
+            if (dh) (void)hipHostFree(dh);
+            err_ = "peer set-up: no memory for the agreement";
+            return 1;   // (the caller fails and aborts the communicator: every member hears of it)
+        }
     }
     auto xfer = [&](void* b, size_t n, RedOp op) { return transport_allreduce(b, n, op, s); };
     auto agree = [&](bool mine_ok, bool& all_ok) {   // a byte per rank, max-reduced
@@ -649,7 +660,8 @@ int Collective::try_peer(hipStream_t s) {
         return 0;
     };
     auto done = [&](int rc) {
-        (void)hipFree(d);
+        if (dh) (void)hipHostFree(dh);
+        else (void)hipFree(d);
         return rc;
     };
     std::string why;
