@@ -31,3 +31,12 @@ PY
 }
 famb fb_pf && famb fb_avpf WFSA_LIB=w-fsa_amd/build_var/avpf/libwfsa_amd.so || exit 1
 bash tools/gpu_r4_q.sh
+# the QN loop's Run prologue / tail changes: pipe and parity tests
+timeout -k 10 600 python -u -m pytest tests/test_gpu_pipe.py tests/test_gpu_parity.py -x -q --timeout 180 --timeout-method thread > gpurun_out/r4p/pipe_tests.log 2>&1 || { tail -30 gpurun_out/r4p/pipe_tests.log; exit 1; }
+tail -2 gpurun_out/r4p/pipe_tests.log
+for i in 1 2; do
+  timeout -k 10 300 python -u bench.py --steps 20 --warmup 5 --cpu-sample 0 --boundary-steps 0 --no-sub > gpurun_out/r4p/drv$i.json 2> gpurun_out/r4p/drv$i.err || { tail -20 gpurun_out/r4p/drv$i.err; exit 1; }
+  python -c "import json;d=json.load(open('gpurun_out/r4p/drv$i.json'));print('driver setting', $i, round(d['ms_per_step']*1e3,2), 'us/step')"
+done
+timeout -k 10 300 python -u bench.py --cpu-sample 0 --boundary-steps 0 --no-sub > gpurun_out/r4p/d200.json 2> gpurun_out/r4p/d200.err || { tail -20 gpurun_out/r4p/d200.err; exit 1; }
+python -c "import json;d=json.load(open('gpurun_out/r4p/d200.json'));print('200 steps', round(d['ms_per_step']*1e3,2), 'us/step')"
