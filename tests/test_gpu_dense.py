@@ -8,11 +8,12 @@ import pytest
 pytestmark = pytest.mark.gpu
 
 
-@pytest.fixture(autouse=True, params=["fused", "split", "blas"])
+@pytest.fixture(autouse=True, params=["fused", "split", "dma", "blas"])
 def gemm_engine(request, monkeypatch):
-    """every test on the three GEMM engines of the dense path: our fused
-    v_mfma_f64_16x16x4f64 kernels, our split-K RAW kernels with the epilogue
-    kernels, and rocBLAS dgemm with the epilogue kernels (WFSA_DENSE_ENGINE)"""
+    """every test on the four GEMM engines of the dense path: our fused
+    v_mfma_f64_16x16x4f64 kernels, our split-K RAW kernels and our LDS-DMA
+    pipelined kernels with the epilogue kernels, and rocBLAS dgemm with the
+    epilogue kernels (WFSA_DENSE_ENGINE)"""
     monkeypatch.delenv("WFSA_DENSE_BLAS", raising=False)
     monkeypatch.setenv("WFSA_DENSE_ENGINE", request.param)
     return request.param

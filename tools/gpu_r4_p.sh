@@ -13,7 +13,9 @@ for r in csv.DictReader(open(sys.argv[1])):
         print(r["Name"][:64], r["Calls"], round(float(r["AverageNs"]) / 1e3, 1), round(float(r["TotalDurationNs"]) / 1e6, 1))
 PY
 }
-run mid && run end WFSA_LIB=w-fsa_amd/build_var/gend/libwfsa_amd.so && run bk32 WFSA_DENSE_STEP_CFG=3 && run frag WFSA_LIB=w-fsa_amd/build_var/gfrag/libwfsa_amd.so && run prio WFSA_LIB=w-fsa_amd/build_var/gprio/libwfsa_amd.so || exit 1
+timeout -k 10 300 python -u -m pytest tests/test_gpu_dense.py -k dma -x -q --timeout 120 --timeout-method thread > gpurun_out/r4p/dma_tests.log 2>&1 || { tail -30 gpurun_out/r4p/dma_tests.log; exit 1; }
+tail -2 gpurun_out/r4p/dma_tests.log
+run dma WFSA_DENSE_ENGINE=dma && run mid && run end WFSA_LIB=w-fsa_amd/build_var/gend/libwfsa_amd.so && run bk32 WFSA_DENSE_STEP_CFG=3 && run frag WFSA_LIB=w-fsa_amd/build_var/gfrag/libwfsa_amd.so && run prio WFSA_LIB=w-fsa_amd/build_var/gprio/libwfsa_amd.so || exit 1
 # counters of the RAW GEMM (one evaluation)
 TD_EVALS=1 timeout -s KILL 180 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_LDS SQ_WAIT_ANY SQ_WAVE_CYCLES SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE --output-format csv -d gpurun_out/r4p/pmc -o run -- python tools/time_dense.py > gpurun_out/r4p/pmc.log 2>&1 || { tail -5 gpurun_out/r4p/pmc.log; exit 1; }
 python tools/pmc_summary.py gpurun_out/r4p/pmc dense_gemm

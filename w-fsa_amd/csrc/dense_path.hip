@@ -584,6 +584,161 @@ __global__ __launch_bounds__(256) void dense_scatter_kernel(ScatterArgs a) {
     }
 }
 
+// ---- the staged-pipeline GEMM (engine 3) -----------------------------------
+// One 4-wave block per 128 x 128 tile (64 x 64 per wave), K in slices of 16
+// moved global -> LDS by global_load_lds_dwordx4 (LDS-DMA: no staging
+// registers, no LDS store instructions) into four LDS stages, three slices
+// ahead.  Each wave waits (counted vmcnt, never 0 in the loop) for its own
+// pieces of the next slice half-way through the current one, then a raw
+// s_barrier -- past it every wave's pieces of that slice are in LDS and every
+// wave has finished the slice before, whose stage the next issue refills.
+// The LDS images are lane-linear per 1 KiB DMA piece:
+//  * [k][r] rows of 144 doubles for an operand whose memory rows run along r
+//    (B always; A in the gradient GEMM) -- one piece per k row;
+//  * [r][k] rows of 16 doubles for the step GEMMs' A (alpha / Y rows run
+//    along k): 16-byte chunk c of row r stored at chunk c ^ ((r >> 1) & 7) --
+//    the permutation applied to the pieces' global source addresses and
+//    undone by the fragment reads, so a fragment read (16 rows x 2 k per
+//    32 lanes) touches 64 distinct banks.
+// Epilogue: RAW the plain product into out; GRADEPI the gradient's scatter
+// -A (.) G by parameter code (as dense_gemm_kernel<GRAD>).
+constexpr int kMmBK = 16, kMmStages = 4;
+constexpr int kMmKc = kT * kMmBK;     // doubles of a swizzled [r][k] image
+constexpr int kMmRc = kMmBK * kLdn;   // doubles of a padded [k][r] image
+template <bool AKC> constexpr int mm_stage() { return (AKC ? kMmKc : kMmRc) + kMmRc; }
+typedef __attribute__((address_space(3))) void lds_void;
+typedef __attribute__((address_space(1))) void glb_void;
+
+template <bool AKC, bool GRADEPI>
+__global__ __launch_bounds__(256, 1) void dense_mm_kernel(GemmArgs a) {
+    if (a.halted && *a.halted) return;
+    constexpr int kStage = mm_stage<AKC>(), kBOff = AKC ? kMmKc : kMmRc;
+    __shared__ __attribute__((aligned(16))) double lds[kMmStages * kStage];
+    const int tid = int(threadIdx.x), lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int wm = wave >> 1, wn = wave & 1;
+    const int np = a.np, ldx = a.ldx;
+    const int mtiles = (GRADEPI ? np : a.R) / kT, ntiles = np / kT, nb = mtiles * ntiles;
+    int bid = int(blockIdx.x);
+    if ((nb & 7) == 0) bid = (bid & 7) * (nb >> 3) + (bid >> 3);   // XCD x: tiles [x nb/8, (x+1) nb/8)
+    const int mt_ = bid % mtiles, nt_ = bid / mtiles;
+    const int r0 = mt_ * kT, c0 = nt_ * kT;
+    const int nk = int((GRADEPI ? a.kg : int64_t(np)) / kMmBK);
+    const int ldb = GRADEPI ? ldx : np;   // z / A, A^T
+    const double* xa = a.x;
+    const double* xb = a.bm;
+    // slice s into stage s % 4: 4 A pieces and 4 B pieces of 1 KiB per wave
+    auto issue = [&](int s) {
+        double* st = lds + (s % kMmStages) * kStage;
+        const int64_t k0 = int64_t(s) * kMmBK;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int q = wave * 4 + i;
+            const double* ga;
+            double* la;
+            if (AKC) {   // rows 8q .. 8q + 7; lane l fills chunk l % 8 of row 8q + l / 8
+                const int row = 8 * q + (lane >> 3);
+                const int c = (lane & 7) ^ ((row >> 1) & 7);
+                ga = xa + int64_t(r0 + row) * ldx + k0 + 2 * c;
+                la = st + q * 128;
+            } else {     // k row q
+                ga = xa + (k0 + q) * ldx + r0 + 2 * lane;
+                la = st + q * kLdn;
+            }
+            __builtin_amdgcn_global_load_lds((glb_void*)ga, (lds_void*)la, 16, 0, 0);
+            const double* gb = xb + (k0 + q) * ldb + c0 + 2 * lane;
+            __builtin_amdgcn_global_load_lds((glb_void*)gb, (lds_void*)(st + kBOff + q * kLdn), 16, 0, 0);
+        }
+    };
+    d4 acc[4][4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = d4{0.0, 0.0, 0.0, 0.0};
+    // a wave's fragments of k-step kk of slice s (4 A, 4 B values), and the
+    // k-step's 16 MFMAs: the fragments of the next k-step are read before
+    // this one's MFMAs are issued (one wave per SIMD: nothing else hides the
+    // LDS latency), across the mid-slice barrier too
+    auto frag = [&](int s, int kk, double (&av)[4], double (&bv)[4]) {
+        const double* As = lds + (s % kMmStages) * kStage;
+        const double* Bs = As + kBOff;
+        const int kr = kk * 4 + (lane >> 4);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int row = wm * 64 + i * 16 + (lane & 15);
+            av[i] = AKC ? As[row * kMmBK + ((((kr >> 1) ^ ((row >> 1) & 7))) << 1) + (kr & 1)]
+                        : As[kr * kLdn + row];
+        }
+#pragma unroll
+        for (int j = 0; j < 4; ++j) bv[j] = Bs[kr * kLdn + wn * 64 + j * 16 + (lane & 15)];
+    };
+    auto mma = [&](const double (&av)[4], const double (&bv)[4], int i0 = 0, int i1 = 4) {   // A rows i0 .. i1 - 1
+#pragma unroll
+        for (int i = i0; i < i1; ++i)
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+                acc[i][j] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[i], bv[j], acc[i][j], 0, 0, 0);
+    };
+    // (every wave issues 8 DMA pieces per slice: "slice t landed" = at most
+    // 8 x (slices issued after t) still outstanding)
+    auto barrier = [] {
+        asm volatile("" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+    };
+    issue(0);
+    if (nk > 1) issue(1);
+    if (nk > 2) issue(2);
+    if (nk > 2) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+    else if (nk > 1) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    barrier();
+    double a0[4], b0[4], a1[4], b1[4];
+    frag(0, 0, a0, b0);
+    for (int t = 0; t < nk; ++t) {
+        frag(t, 1, a1, b1);
+        mma(a0, b0);
+        frag(t, 2, a0, b0);
+        mma(a1, b1);
+        // slice t + 1 in LDS (past the last slice: every DMA done); stage
+        // (t + 3) % 4 = (t - 1) % 4 free.  (Unconditional barrier and reads:
+        // one LDS-counter state on every path, so the compiler's waits for
+        // the fragments stay counted, not drained.)
+        if (t + 2 < nk) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        barrier();
+        if (t + 3 < nk) issue(t + 3);
+        frag(t, 3, a1, b1);
+        mma(a0, b0);
+        // the next slice's first fragments read half-way through the last
+        // k-step (pinned there: hoisted above it, the wait for k-step 3's
+        // fragments drained them too, with no MFMA in between)
+        mma(a1, b1, 0, 2);
+        __builtin_amdgcn_sched_barrier(0);
+        frag(t + 1, 0, a0, b0);   // (past the last slice: a stale stage, unused)
+        __builtin_amdgcn_sched_barrier(0);
+        mma(a1, b1, 2, 4);
+    }
+    // epilogue: element (i, j, e) of this lane is row wm*64 + 16 i + (lane>>4)
+    // + 4 e, column wn*64 + 16 j + (lane & 15) of the block tile
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const int row = r0 + wm * 64 + 16 * i + (lane >> 4) + 4 * e;
+                const int col = c0 + wn * 64 + 16 * j + (lane & 15);
+                if (GRADEPI) {
+                    const int64_t o = int64_t(row) * np + col;
+                    const int32_t code = a.code_a[o];
+                    if (code >= 0 && code < a.n_params) a.grad[code] = -a.amat[o] * acc[i][j][e];
+                } else {
+                    a.out[int64_t(row) * ldx + col] = acc[i][j][e];
+                }
+            }
+}
+
 // ---- epilogues of the library GEMMs (enqueue_blas) ------------------------
 // One block per row slot r of the step; the row's new values and their sum
 // (a fixed-order block reduction: deterministic) for the next step's scale.
@@ -1046,6 +1201,7 @@ hipError_t DensePath::load_model(const DenseModel& m, hipStream_t s) {
         if (v == "fused") engine_ = 0;
         else if (v == "blas") engine_ = 1;
         else if (v == "split") engine_ = 2;
+        else if (v == "dma") engine_ = 3;
         else return hipErrorInvalidValue;
     }
     if (engine_ == 1) {
@@ -1156,7 +1312,7 @@ hipError_t DensePath::load_corpus(const uint8_t* sym, const int64_t* off, const 
     DTRY(dalloc(gam_, TR * ld));
     DTRY(dalloc(z_, TR * ld));
     DTRY(dalloc(y_, 2 * size_t(R) * ld));
-    if (engine_ == 2) DTRY(dalloc(ysplit_, size_t(R) * ld));
+    if (engine_ == 2) DTRY(dalloc(ysplit_, size_t(R) * ld));   // (engine 3: no split)
     DTRY(dalloc(part_, 2 * size_t(nct_) * size_t(R)));
     n_ll_ = int32_t((S + 3) / 4);
     DTRY(dalloc(ll_part_, size_t(std::max(n_ll_, 1))));
@@ -1320,14 +1476,14 @@ hipError_t DensePath::enqueue(const double* ewp, bool structural, double* out, d
 hipError_t DensePath::enqueue_lib(const double* w, const double* p, bool structural, double* out, double* logq,
                                   const unsigned* halted, hipStream_t s) {
     const size_t np = size_t(np_), R = size_t(R_);
-    const bool ours = engine() == 2;
+    const bool ours = engine() >= 2, dma = engine() == 3;
     rocblas_handle h = static_cast<rocblas_handle>(blas_);
     if (!ours && rocblas_set_stream(h, s) != rocblas_status_success) return hipErrorInvalidHandle;
     auto rb = [](rocblas_status st) { return st == rocblas_status_success ? hipSuccess : hipErrorLaunchFailure; };
     GemmArgs raw{};
     raw.R = R_; raw.np = np_; raw.nct = nct_; raw.ldx = ldx_; raw.halted = halted;
     raw.out2 = ysplit_; raw.splits = kSplitK;
-    const int raw_blocks = int((R / kT) * (np / kT)) * kSplitK;
+    const int raw_blocks = int((R / kT) * (np / kT)) * kSplitK, mm_blocks = int((R / kT) * (np / kT));
     {
         WeightsArgs a{};
         a.ewp = w;
@@ -1359,7 +1515,8 @@ hipError_t DensePath::enqueue_lib(const double* w, const double* p, bool structu
             m.x = alpha_ + size_t(t) * step;
             m.bm = amat_;
             m.out = nxt;
-            if (step_cfg_ == 3) dense_gemm_kernel<RAW, kBkStep, 4><<<raw_blocks, 4 * 64, 0, s>>>(m);
+            if (dma) dense_mm_kernel<true, false><<<mm_blocks, 256, 0, s>>>(m);
+            else if (step_cfg_ == 3) dense_gemm_kernel<RAW, kBkStep, 4><<<raw_blocks, 4 * 64, 0, s>>>(m);
             else dense_gemm_kernel<RAW, kBkGrad, kNwGrad><<<raw_blocks, kNwGrad * 64, 0, s>>>(m);
             DTRY(hipGetLastError());
         } else if (t >= 0) {   // alpha[t+1]^T = A^T alpha[t]^T
@@ -1367,7 +1524,7 @@ hipError_t DensePath::enqueue_lib(const double* w, const double* p, bool structu
                                   alpha_ + size_t(t) * step, ild, &zero, nxt, ild)));
         }
         EpiArgs f = g;
-        f.io2 = ours && t >= 0 ? ysplit_ : nullptr;
+        f.io2 = ours && !dma && t >= 0 ? ysplit_ : nullptr;
         f.first = t < 0;
         f.meta = meta_ + size_t(t + 1) * R;
         f.sum_in = part_ + size_t(t & 1) * R;
@@ -1394,7 +1551,8 @@ hipError_t DensePath::enqueue_lib(const double* w, const double* p, bool structu
             m.x = y_ + size_t((t + 1) & 1) * step;
             m.bm = amat_t_;
             m.out = cur;
-            if (step_cfg_ == 3) dense_gemm_kernel<RAW, kBkStep, 4><<<raw_blocks, 4 * 64, 0, s>>>(m);
+            if (dma) dense_mm_kernel<true, false><<<mm_blocks, 256, 0, s>>>(m);
+            else if (step_cfg_ == 3) dense_gemm_kernel<RAW, kBkStep, 4><<<raw_blocks, 4 * 64, 0, s>>>(m);
             else dense_gemm_kernel<RAW, kBkGrad, kNwGrad><<<raw_blocks, kNwGrad * 64, 0, s>>>(m);
             DTRY(hipGetLastError());
         } else if (t < T_ - 1) {   // beta[t]^T = A Y[t+1]^T
@@ -1402,7 +1560,7 @@ hipError_t DensePath::enqueue_lib(const double* w, const double* p, bool structu
                                   y_ + size_t((t + 1) & 1) * step, ild, &zero, cur, ild)));
         }
         EpiArgs b = g;
-        b.io2 = ours && t < T_ - 1 ? ysplit_ : nullptr;
+        b.io2 = ours && !dma && t < T_ - 1 ? ysplit_ : nullptr;
         b.first = t == T_ - 1;
         b.meta = meta_ + size_t(t) * R;
         b.sid = sid_ + size_t(t) * R;
@@ -1428,7 +1586,8 @@ hipError_t DensePath::enqueue_lib(const double* w, const double* p, bool structu
         q.code_a = code_a_;
         q.amat = amat_;
         q.grad = out + 1;
-        dense_gemm_kernel<GRAD, kBkGrad, kNwGrad><<<int((np / kT) * (np / kT)), kNwGrad * 64, 0, s>>>(q);
+        if (dma) dense_mm_kernel<false, true><<<int((np / kT) * (np / kT)), 256, 0, s>>>(q);
+        else dense_gemm_kernel<GRAD, kBkGrad, kNwGrad><<<int((np / kT) * (np / kT)), kNwGrad * 64, 0, s>>>(q);
         DTRY(hipGetLastError());
     } else if (T_ >= 2) {   // G^T = z[1..]^T alpha[0..] over K = (T-1) R rows: g[S np + T] = G(S, T)
         const int64_t K = int64_t(T_ - 1) * int64_t(R);

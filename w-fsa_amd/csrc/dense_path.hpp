@@ -91,7 +91,8 @@ public:
     int32_t steps() const { return T_; }
     int32_t np() const { return np_; }
     // the GEMM engine the evaluations run: 0 fused MFMA kernels, 1 rocBLAS
-    // dgemm + epilogue kernels, 2 split-K MFMA kernels + epilogue kernels
+    // dgemm + epilogue kernels, 2 split-K MFMA kernels + epilogue kernels,
+    // 3 LDS-DMA pipelined MFMA kernels + epilogue kernels
     int engine() const { return engine_ == 1 && !blas_ ? 0 : engine_; }
     int64_t total_symbols() const { return total_sym_; }
     // algorithmic fp64 flops of one evaluation: three GEMMs of 2 np^2 per
@@ -142,7 +143,7 @@ private:
     double* ll_part_ = nullptr;
     int32_t n_ll_ = 0;
     double* red_ = nullptr;    // [chunks][vocab+2][np]
-    // GEMM engine (WFSA_DENSE_ENGINE=fused|blas|split, default split;
+    // GEMM engine (WFSA_DENSE_ENGINE=fused|blas|split|dma, default split;
     // WFSA_DENSE_BLAS=0/1 = fused/blas): 1 the GEMMs as plain fp64 library GEMMs (rocBLAS, atomics
     // off: deterministic) with our epilogue kernels; 2 the same flow with our
     // RAW GEMM kernel (K split in two halves: 2 blocks per CU) for the step
