@@ -301,7 +301,7 @@ __global__ __launch_bounds__(NW * 64, ((MODE == GRAD || MODE == RAW) && NW == 4 
                 double av[4], bv[NJ];
                 frag(kk, av, bv);
 #endif
-#ifdef WFSA_GEMM_PRIO
+#ifndef WFSA_GEMM_NOPRIO   // (MFMA clusters at raised priority: 537 -> 528 us per step GEMM, profiles/r04/gemm_variants.txt)
                 __builtin_amdgcn_s_setprio(1);
 #endif
 #pragma unroll
@@ -309,7 +309,7 @@ __global__ __launch_bounds__(NW * 64, ((MODE == GRAD || MODE == RAW) && NW == 4 
 #pragma unroll
                     for (int j = 0; j < NJ; ++j)
                         acc[i][j] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[i], bv[j], acc[i][j], 0, 0, 0);
-#ifdef WFSA_GEMM_PRIO
+#ifndef WFSA_GEMM_NOPRIO
                 __builtin_amdgcn_s_setprio(0);
 #endif
             }
