@@ -33,6 +33,7 @@ runs on the traversal tiers).
 Prints ONE JSON line (rank 0).
 """
 import argparse
+import gc
 import json
 import os
 import sys
@@ -260,11 +261,22 @@ def run_workload(wl, world, rank, local_rank, distributed, dist, torch, info_rmi
     if wl["warmup"]:
         lrn.Run(wl["warmup"], 1.0, -1.0)
     st0 = lrn.stats()
+    # no cyclic garbage collection inside the timed region (a collection
+    # pass over torch's heap costs tens of microseconds of host time)
+    gc.collect()
+    gc.disable()
     barrier()
     t0 = time.perf_counter()
+    ns0 = time.monotonic_ns()
     rows = lrn.Run(wl["steps"], 1.0, -1.0)
+    ns1 = time.monotonic_ns()
+    t_run = time.perf_counter()
     barrier()
     dt = time.perf_counter() - t0
+    gc.enable()
+    if os.environ.get("WFSA_BENCH_TRACE"):   # (diagnostics: where the timed region's wall time goes)
+        print(f"[bench] timed region {dt * 1e6:.1f} us: Run {1e6 * (t_run - t0):.1f}, barrier {1e6 * (t0 + dt - t_run):.1f}"
+              f" (Run call at {ns0} ns, returned at {ns1} ns)", file=sys.stderr, flush=True)
     assert len(rows) == wl["steps"]
     st1 = lrn.stats()
     if distributed:

@@ -226,6 +226,8 @@ void QuasiNewtonLearner::OptimizationStep(double eta, bool) {   // :162-201
 
 void QuasiNewtonLearner::RunDevice(double eta, double tol, int32_t max_epochs, double* info_rows,
                                    int32_t* epochs_done) {
+    using clk = std::chrono::steady_clock;
+    const auto te = clk::now();
     if (epochs_done) *epochs_done = 0;
     wfsa_dev* d = Device();
     if (!d) throw LearnerError("BuildFrom has not run");
@@ -248,7 +250,6 @@ void QuasiNewtonLearner::RunDevice(double eta, double tol, int32_t max_epochs, d
         dev_qn_rmin = desc.info_rmin;
         dev_state_valid = false;
     }
-    using clk = std::chrono::steady_clock;
     static const bool trace = std::getenv("WFSA_RUN_TRACE") != nullptr;
     const auto t0 = clk::now();
     if (!dev_state_valid) {
@@ -265,7 +266,9 @@ void QuasiNewtonLearner::RunDevice(double eta, double tol, int32_t max_epochs, d
     if (trace) {
         const auto t2 = clk::now();
         auto us = [](clk::time_point a, clk::time_point b) { return std::chrono::duration<double, std::micro>(b - a).count(); };
-        std::fprintf(stderr, "[wfsa] RunDevice: set_state %.1f us, qn_run %.1f\n", us(t0, t1), us(t1, t2));
+        std::fprintf(stderr, "[wfsa] RunDevice: entry at %lld ns, set-up %.1f us, set_state %.1f us, qn_run %.1f\n",
+                     (long long)std::chrono::duration_cast<std::chrono::nanoseconds>(te.time_since_epoch()).count(),
+                     us(te, t0), us(t0, t1), us(t1, t2));
     }
     if (info_rows) std::copy(rows.begin(), rows.begin() + std::ptrdiff_t(done) * 7, info_rows);
     if (epochs_done) *epochs_done = done;

@@ -3424,8 +3424,11 @@ static int qn_run_impl(wfsa_dev* ctx, double eta, double tol, int32_t max_steps,
         // and the poll below then covers both
         HIP_TRY(hipStreamWaitEvent(s, ctx->pf[(enq + kQnDepth - 1) % kQnDepth], 0));
         ctx->w_cur = ctx->ewp_cur = nullptr;
-        HIP_TRY(wfsa::launch_qn_weights(ctx->qn_x.ptr, ctx->qn_trim.ptr, ctx->n_params, ctx->w_full.ptr,
-                                        ctx->ewp.ptr, s));
+        // step e writes the weights of parity e + 1: after an even number of
+        // steps, none skipped by a halt, they are in the parity-0 buffers already
+        if (st != 0 || (enq & 1))
+            HIP_TRY(wfsa::launch_qn_weights(ctx->qn_x.ptr, ctx->qn_trim.ptr, ctx->n_params, ctx->w_full.ptr,
+                                            ctx->ewp.ptr, s));
     }
     // the last step's row is in: wait for the stream's tail by polling (a
     // blocking synchronize costs a wake-up of ~10 us on this system)

@@ -8,11 +8,15 @@ libwfsa_amd.so on a gfx950 GPU; there is no CPU fallback.
 """
 import ctypes as C
 import os
+import sys
+import time
 
 import numpy as np
 
 from . import _lib
 from ._lib import WfsaError, check_dev, check_host, load
+
+_RUN_TRACE = bool(os.environ.get("WFSA_RUN_TRACE"))   # (diagnostics: Run's host-side timestamps on stderr)
 
 
 def _ptr(a):
@@ -326,11 +330,23 @@ class QuasiNewtonLearner:
 
     def Run(self, epochs, eta=1.0, tol=1e-6):
         """up to `epochs` OptimizationSteps in one native call (no Init)"""
-        rows = np.zeros((max(epochs, 0), self.width))
-        done = C.c_int32(0)
-        rc = load().wfsa_learner_run(self._h, eta, tol, int(epochs), _ptr(rows), C.byref(done))
+        t0 = time.monotonic_ns() if _RUN_TRACE else 0
+        n = max(int(epochs), 0)
+        rb = self.__dict__.get("_run_rows")
+        if rb is None or rb[0].shape[0] < n:   # (one rows buffer per learner, grown on demand: no allocation per Run)
+            rows = np.zeros((max(n, 1), self.width))
+            done = C.c_int32(0)
+            rb = self._run_rows = (rows, _ptr(rows), done, C.byref(done), load().wfsa_learner_run)
+        rows, ptr, done, done_ref, fn = rb
+        t1 = time.monotonic_ns() if _RUN_TRACE else 0
+        rc = fn(self._h, eta, tol, n, ptr, done_ref)
+        t2 = time.monotonic_ns() if _RUN_TRACE else 0
         check_host(rc)
-        return rows[:done.value].tolist()
+        out = rows[:done.value].tolist()
+        if _RUN_TRACE:
+            print(f"[wfsa.py] Run: entry {t0} ns, native call at {t1}, back at {t2}, out at {time.monotonic_ns()}",
+                  file=sys.stderr, flush=True)
+        return out
 
 
 _OPS = ("sum", "min", "max")
