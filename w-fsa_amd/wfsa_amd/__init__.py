@@ -334,7 +334,7 @@ class QuasiNewtonLearner:
         n = max(int(epochs), 0)
         rb = self.__dict__.get("_run_rows")
         if rb is None or rb[0].shape[0] < n:   # (one rows buffer per learner, grown on demand: no allocation per Run)
-            rows = np.zeros((max(n, 1), self.width))
+            rows = np.zeros((max(n, 256), self.width))
             done = C.c_int32(0)
             rb = self._run_rows = (rows, _ptr(rows), done, C.byref(done), load().wfsa_learner_run)
         rows, ptr, done, done_ref, fn = rb
