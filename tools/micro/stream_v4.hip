@@ -16,6 +16,8 @@
 // against the host's.  Run under rocprofv3 --pmc for the LDS counters.
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
+
 #include <algorithm>
 #include <cstdint>
 #include <cstdio>
@@ -363,7 +365,8 @@ int main() {
     std::iota(ordr.begin(), ordr.end(), 0);
     std::stable_sort(ordr.begin(), ordr.end(), [&](int a, int b) { return str[a].size() > str[b].size(); });
     // groups dealt to waves in snake order, then laid out wave-contiguous
-    const int nwaves = 256 * 16;
+    // STREAM_WAVES=8192: the layout for two 1024-thread blocks per CU (32 waves)
+    const int nwaves = std::getenv("STREAM_WAVES") ? std::atoi(std::getenv("STREAM_WAVES")) : 256 * 16;
     std::vector<std::vector<int>> wg(nwaves);
     for (int g = 0; g < G; ++g) {
         const int round = g / nwaves, k = g % nwaves;
@@ -470,7 +473,13 @@ int main() {
         printf("\n");
         return 0;
     };
-    const int b1 = 256;   // one 1024-thread block per CU (16 waves); the waves' runs assume 4096 waves
+    const int b1 = nwaves / 16;   // 1024-thread blocks: 256 (one per CU, 16 waves) or 512 (two per CU)
+    if (nwaves == 8192) {   // the 32-waves-per-CU form of the delta pass (64 VGPRs)
+        if (run("delta 10-bit D2 gather occ2", pass<110, 2, 0, 2>, dd[2], b1, true)) return 1;
+        if (run("delta 10-bit D3 gather occ2", pass<110, 3, 0, 2>, dd[2], b1, true)) return 1;
+        if (run("delta 10-bit D2 loads occ2", pass<110, 2, 1, 2>, dd[2], b1, false)) return 1;
+        return 0;
+    }
     if (run("16-bit rand  D4 gather", pass<16, 4, 0, 1>, d16r, b1, true)) return 1;
     if (run("16-bit sched D4 gather", pass<16, 4, 0, 1>, d16s, b1, true)) return 1;
     if (run("14-bit rand  D4 gather", pass<14, 4, 0, 1>, d14r, b1, true)) return 1;

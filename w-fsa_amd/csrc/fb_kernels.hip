@@ -2306,7 +2306,12 @@ __device__ __forceinline__ void delta_row(const uint4 v, uint32_t& cur, double& 
 }
 
 template <bool WIDE, bool W_LDS, bool MULTI, int DBG = 0, bool RMIN = false, bool DELTA = false>
-__global__ __launch_bounds__(1024, (DBG == 10 ? 8 : 1)) void fbs_kernel(CompiledArgs a) {
+#ifdef WFSA_FBS_VGPR64   // (variant builds: a 64-VGPR budget, two 1024-thread blocks per CU)
+#define WFSA_FBS_ATTR __attribute__((amdgpu_num_vgpr(64)))
+#else
+#define WFSA_FBS_ATTR
+#endif
+__global__ __launch_bounds__(1024, (DBG == 10 ? 8 : 1)) WFSA_FBS_ATTR void fbs_kernel(CompiledArgs a) {
     extern __shared__ __attribute__((aligned(16))) double lds[];
     const int lane = lane_id();
     const int wpb = int(blockDim.x) / kWave;
