@@ -673,11 +673,17 @@ __global__ __launch_bounds__(256, 1) void dense_mm_kernel(GemmArgs a) {
         for (int j = 0; j < 4; ++j) bv[j] = Bs[kr * kLdn + wn * 64 + j * 16 + (lane & 15)];
     };
     auto mma = [&](const double (&av)[4], const double (&bv)[4], int i0 = 0, int i1 = 4) {   // A rows i0 .. i1 - 1
+#ifdef WFSA_MM_PRIO
+        __builtin_amdgcn_s_setprio(1);
+#endif
 #pragma unroll
         for (int i = i0; i < i1; ++i)
 #pragma unroll
             for (int j = 0; j < 4; ++j)
                 acc[i][j] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[i], bv[j], acc[i][j], 0, 0, 0);
+#ifdef WFSA_MM_PRIO
+        __builtin_amdgcn_s_setprio(0);
+#endif
     };
     // (every wave issues 8 DMA pieces per slice: "slice t landed" = at most
     // 8 x (slices issued after t) still outstanding)
@@ -1586,7 +1592,7 @@ hipError_t DensePath::enqueue_lib(const double* w, const double* p, bool structu
         q.code_a = code_a_;
         q.amat = amat_;
         q.grad = out + 1;
-        if (dma) dense_mm_kernel<false, true><<<int((np / kT) * (np / kT)), 256, 0, s>>>(q);
+        if (dma && step_cfg_ == 4) dense_mm_kernel<false, true><<<int((np / kT) * (np / kT)), 256, 0, s>>>(q);
         else dense_gemm_kernel<GRAD, kBkGrad, kNwGrad><<<int((np / kT) * (np / kT)), kNwGrad * 64, 0, s>>>(q);
         DTRY(hipGetLastError());
     } else if (T_ >= 2) {   // G^T = z[1..]^T alpha[0..] over K = (T-1) R rows: g[S np + T] = G(S, T)
