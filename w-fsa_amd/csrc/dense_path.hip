@@ -85,6 +85,8 @@ constexpr int kRedThreads = 128;      // dense_reduce: one column per thread
 // puts every row of the tile on the same ones)
 constexpr int kRowPad = 16;
 constexpr int kRedWindow = 64;        // symbols per LDS pass of dense_reduce
+constexpr int kRedBatch = 8;          // dense_reduce: rows whose loads are in flight together
+constexpr int kEpiBatch = 4;          // epilogues: columns per thread loaded before the stores
 
 // RAW: a plain product (the forward's or the backward's operand layouts)
 // into out (K split s: into out2 for s = 1), the epilogue left to the
@@ -527,18 +529,29 @@ __global__ __launch_bounds__(kRedThreads) void dense_reduce_kernel(ReduceArgs a)
         const int wv = min(kRedWindow, V - vb);
         for (int k = 0; k < kRedWindow + 2; ++k) acc[k * kRedThreads + t] = 0.0;
         double st = 0.0, en = 0.0;
-        for (int64_t r = rbeg; r < rend; ++r) {
-            const int m = a.meta[r];
+        auto add = [&](int m, double g) {
             const int sym = m & 511;
-            if (sym >= V) continue;   // idle slot
-            const double g = a.gam[r * a.ldx + col];
+            if (sym >= V) return;   // idle slot
             const int k = sym - vb;
             if (k >= 0 && k < wv) acc[k * kRedThreads + t] += g;
             if (vb == 0) {
                 if ((m >> 9) & 1) st += g;
                 if ((m >> 10) & 1) en += g;
             }
+        };
+        int64_t r = rbeg;
+        for (; r + kRedBatch <= rend; r += kRedBatch) {   // a batch of rows' loads in flight, then the adds in row order
+            int mb[kRedBatch];
+            double gb[kRedBatch];
+#pragma unroll
+            for (int u = 0; u < kRedBatch; ++u) {
+                mb[u] = a.meta[r + u];
+                gb[u] = a.gam[(r + u) * a.ldx + col];   // (an idle slot's row is read and skipped)
+            }
+#pragma unroll
+            for (int u = 0; u < kRedBatch; ++u) add(mb[u], gb[u]);
         }
+        for (; r < rend; ++r) add(a.meta[r], a.gam[r * a.ldx + col]);
         for (int k = 0; k < wv; ++k) outp[int64_t(vb + k) * a.np + col] = acc[k * kRedThreads + t];
         if (vb == 0) {
             outp[int64_t(V) * a.np + col] = st;
@@ -805,11 +818,27 @@ __global__ __launch_bounds__(kEpiThreads) void dense_fwd_epi_kernel(EpiArgs a) {
     double* row = a.io + int64_t(r) * a.ldx;
     const double* row2 = a.io2 ? a.io2 + int64_t(r) * a.ldx : nullptr;
     double acc = 0.0;
-    for (int c = int(threadIdx.x); c < a.np; c += kEpiThreads) {
-        const double raw = a.first ? 0.0 : (row2 ? row[c] + row2[c] : row[c]);
-        const double v = (start ? a.a0[c] : raw * inv) * erow[c];
-        row[c] = v;
-        acc += v;
+    // kEpiBatch columns per thread loaded before any is stored (the stores
+    // into the row would otherwise order every later load behind them);
+    // the sum runs over the thread's columns in the same ascending order
+    for (int c0 = int(threadIdx.x); c0 < a.np; c0 += kEpiBatch * kEpiThreads) {
+        double raw[kEpiBatch], e[kEpiBatch], s0[kEpiBatch];
+#pragma unroll
+        for (int u = 0; u < kEpiBatch; ++u) {
+            const int c = c0 + u * kEpiThreads;
+            const bool in = c < a.np;
+            raw[u] = in && !a.first ? (row2 ? row[c] + row2[c] : row[c]) : 0.0;
+            e[u] = in ? erow[c] : 0.0;
+            s0[u] = in && start ? a.a0[c] : 0.0;
+        }
+#pragma unroll
+        for (int u = 0; u < kEpiBatch; ++u) {
+            const int c = c0 + u * kEpiThreads;
+            if (c >= a.np) break;
+            const double v = (start ? s0[u] : raw[u] * inv) * e[u];
+            row[c] = v;
+            acc += v;
+        }
     }
     acc = epi_block_sum(acc, red);
     if (threadIdx.x == 0) a.sum_out[r] = acc;
@@ -844,14 +873,28 @@ __global__ __launch_bounds__(kEpiThreads) void dense_bwd_epi_kernel(EpiArgs a) {
     double* row = a.io + o0;
     const double* row2 = a.io2 ? a.io2 + o0 : nullptr;
     double acc = 0.0;
-    for (int c = int(threadIdx.x); c < a.np; c += kEpiThreads) {
-        const double raw = a.first ? 0.0 : (row2 ? row[c] + row2[c] : row[c]);
-        const double beta = end ? a.aend[c] : raw * inv;
-        a.gam[o0 + c] = a.alpha_t[o0 + c] * beta * f1;
-        const double v = erow[c] * beta;
-        row[c] = v;
-        a.z[o0 + c] = v * f2;
-        acc += v;
+    for (int c0 = int(threadIdx.x); c0 < a.np; c0 += kEpiBatch * kEpiThreads) {   // (batched as the forward's)
+        double raw[kEpiBatch], e[kEpiBatch], al[kEpiBatch], ae[kEpiBatch];
+#pragma unroll
+        for (int u = 0; u < kEpiBatch; ++u) {
+            const int c = c0 + u * kEpiThreads;
+            const bool in = c < a.np;
+            raw[u] = in && !a.first ? (row2 ? row[c] + row2[c] : row[c]) : 0.0;
+            e[u] = in ? erow[c] : 0.0;
+            al[u] = in ? a.alpha_t[o0 + c] : 0.0;
+            ae[u] = in && end ? a.aend[c] : 0.0;
+        }
+#pragma unroll
+        for (int u = 0; u < kEpiBatch; ++u) {
+            const int c = c0 + u * kEpiThreads;
+            if (c >= a.np) break;
+            const double beta = end ? ae[u] : raw[u] * inv;
+            a.gam[o0 + c] = al[u] * beta * f1;
+            const double v = e[u] * beta;
+            row[c] = v;
+            a.z[o0 + c] = v * f2;
+            acc += v;
+        }
     }
     acc = epi_block_sum(acc, red);
     if (threadIdx.x == 0) a.sum_out[r] = acc;
