@@ -85,8 +85,14 @@ constexpr int kRedThreads = 128;      // dense_reduce: one column per thread
 // puts every row of the tile on the same ones)
 constexpr int kRowPad = 16;
 constexpr int kRedWindow = 64;        // symbols per LDS pass of dense_reduce
-constexpr int kRedBatch = 8;          // dense_reduce: rows whose loads are in flight together
-constexpr int kEpiBatch = 4;          // epilogues: columns per thread loaded before the stores
+#ifndef WFSA_RED_BATCH   // (variant builds: batch sizes)
+#define WFSA_RED_BATCH 8
+#endif
+#ifndef WFSA_EPI_BATCH
+#define WFSA_EPI_BATCH 4
+#endif
+constexpr int kRedBatch = WFSA_RED_BATCH;   // dense_reduce: rows whose loads are in flight together (4.35 -> 1.68 ms per c5 evaluation)
+constexpr int kEpiBatch = WFSA_EPI_BATCH;   // epilogues: columns per thread loaded before the stores (29.1 / 47.7 -> 24.7 / 45.5 us)
 
 // RAW: a plain product (the forward's or the backward's operand layouts)
 // into out (K split s: into out2 for s = 1), the epilogue left to the
