@@ -86,12 +86,12 @@ constexpr int kRedThreads = 128;      // dense_reduce: one column per thread
 constexpr int kRowPad = 16;
 constexpr int kRedWindow = 64;        // symbols per LDS pass of dense_reduce
 #ifndef WFSA_RED_BATCH   // (variant builds: batch sizes)
-#define WFSA_RED_BATCH 16
+#define WFSA_RED_BATCH 32
 #endif
 #ifndef WFSA_EPI_BATCH
 #define WFSA_EPI_BATCH 4
 #endif
-constexpr int kRedBatch = WFSA_RED_BATCH;   // dense_reduce: rows whose loads are in flight together (batch 8 / 16: 4.35 -> 1.68 / 1.27 ms per c5 evaluation)
+constexpr int kRedBatch = WFSA_RED_BATCH;   // dense_reduce: rows whose loads are in flight together (batch 8 / 16 / 32: 4.35 -> 1.68 / 1.27 / 1.12 ms per c5 evaluation)
 constexpr int kEpiBatch = WFSA_EPI_BATCH;   // epilogues: columns per thread loaded before the stores (29.1 / 47.7 -> 24.7 / 45.5 us)
 
 // RAW: a plain product (the forward's or the backward's operand layouts)
