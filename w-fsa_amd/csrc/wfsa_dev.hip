@@ -3430,13 +3430,14 @@ static int qn_run_impl(wfsa_dev* ctx, double eta, double tol, int32_t max_steps,
             HIP_TRY(wfsa::launch_qn_weights(ctx->qn_x.ptr, ctx->qn_trim.ptr, ctx->n_params, ctx->w_full.ptr,
                                             ctx->ewp.ptr, s));
     }
-    // the last step's row is in: wait for the stream's tail by polling (a
-    // blocking synchronize costs a wake-up of ~10 us on this system)
-    for (;;) {
+    // the last step's row is in: the stream's tail (the end of the kernel
+    // that published it) is left to run beside the caller's return -- every
+    // later use of the device state is ordered behind it on this stream, and
+    // a failure surfaces at the next call; here only an error already known
+    {
         const hipError_t e = hipStreamQuery(s);
-        if (e == hipSuccess) break;
-        if (e != hipErrorNotReady) return fail(WFSA_ERR_HIP, "device failure: %s", hipGetErrorString(e));
-        __builtin_ia32_pause();
+        if (e != hipSuccess && e != hipErrorNotReady)
+            return fail(WFSA_ERR_HIP, "device failure: %s", hipGetErrorString(e));
     }
     if (trace) {
         tr_end = clk::now();
