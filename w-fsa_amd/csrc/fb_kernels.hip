@@ -33,6 +33,7 @@
 #include "qn_device.hpp"
 
 #include <hip/hip_runtime.h>
+#include <hip/hip_ext.h>
 
 #include <algorithm>
 #include <cmath>
@@ -2916,7 +2917,28 @@ hipError_t launch_stream_headers(uint4* stream, const int64_t* g_base, const int
     return hipGetLastError();
 }
 
-hipError_t launch_compiled(const CompiledArgs& a, int grid, int block, size_t lds, hipStream_t stream) {
+static hipError_t launch_compiled_impl(const CompiledArgs& a, int grid, int block, size_t lds, hipStream_t stream);
+
+hipError_t launch_compiled(const CompiledArgs& a, int grid, int block, size_t lds, hipStream_t stream, hipEvent_t ev0,
+                           hipEvent_t ev1) {
+    if (!a.with_grad && a.d_tab > 0 && (ev0 || ev1)) {   // the delta stream kernel with dispatch timestamps
+        const dim3 g{unsigned(grid), 1, 1}, b{unsigned(block), 1, 1};
+        if (a.bub_on && a.bub.rmin_acc)
+            hipExtLaunchKernelGGL((fbs_kernel<false, true, false, 0, true, true>), g, b, uint32_t(lds), stream, ev0, ev1, 0u, a);
+        else
+            hipExtLaunchKernelGGL((fbs_kernel<false, true, false, 0, false, true>), g, b, uint32_t(lds), stream, ev0, ev1, 0u, a);
+        return hipGetLastError();
+    }
+    if (ev0) {
+        const hipError_t e = hipEventRecord(ev0, stream);
+        if (e != hipSuccess) return e;
+    }
+    const hipError_t e = launch_compiled_impl(a, grid, block, lds, stream);
+    if (e != hipSuccess || !ev1) return e;
+    return hipEventRecord(ev1, stream);
+}
+
+static hipError_t launch_compiled_impl(const CompiledArgs& a, int grid, int block, size_t lds, hipStream_t stream) {
     const dim3 g{unsigned(grid), 1, 1}, b{unsigned(block), 1, 1};
     if (!a.with_grad) {   // per-iteration form: w staged in LDS or read from global
 #ifdef WFSA_EXPERIMENTS

@@ -680,7 +680,10 @@ hipError_t configure_kernels(int max_dynamic_lds);
 hipError_t launch_trav(TravMode mode, const TravArgs& a, int grid, hipStream_t stream);
 hipError_t launch_stream_headers(uint4* stream, const int64_t* g_base, const int32_t* g_len, const double* p_lane,
                                 int32_t n_groups, int32_t wide, hipStream_t s);
-hipError_t launch_compiled(const CompiledArgs& a, int grid, int block, size_t lds, hipStream_t stream);
+// ev0 / ev1 (optional, timing events): the stream kernel's dispatch start and
+// end (hipExtLaunchKernel's profiling timestamps, the launch gap excluded)
+hipError_t launch_compiled(const CompiledArgs& a, int grid, int block, size_t lds, hipStream_t stream,
+                           hipEvent_t ev0 = nullptr, hipEvent_t ev1 = nullptr);
 constexpr int kBubbleBlock = 128;
 // waves: n_big (one per big bubble) + ceil(n_small / 64)
 int bubble_waves(int32_t n_small, int32_t n_big);

@@ -1958,7 +1958,10 @@ int enqueue_compiled(wfsa_dev* ctx, bool with_grad, bool want_logq, const unsign
     if (!fused)
         HIP_TRY(wfsa::launch_edge_weights(ctx->w_full.ptr, ctx->pptr.ptr, ctx->pidx.ptr, ctx->lw.ptr, ctx->ew.ptr,
                                           ctx->erec.ptr, ctx->n_edges + ctx->n_end, ctx->out.ptr, int64_t(np) + 1, s));
-    if (!with_grad) HIP_TRY(record(ctx, ctx->k0, slot, s));
+    // the stream kernel's timing: events attached to its dispatch (start and
+    // end of the kernel itself), else recorded around it
+    const bool ktimed = !with_grad && ctx->kernel_timing && slot >= 0;
+    if (ktimed && ctx->n_groups == 0) HIP_TRY(record(ctx, ctx->k0, slot, s));
     if (ctx->n_groups > 0) {
         wfsa::CompiledArgs c{};
         c.m = model_view(ctx);
@@ -2002,9 +2005,10 @@ int enqueue_compiled(wfsa_dev* ctx, bool with_grad, bool want_logq, const unsign
         if (with_grad && tables == 0)   // the blocks accumulate into their slabs
             HIP_TRY(hipMemsetAsync(ctx->gpart.ptr, 0, size_t(ctx->c_grid) * size_t(np) * sizeof(double), s));
         if (with_grad) HIP_TRY(wfsa::launch_compiled(c, ctx->c_grid, kGradBlock, lds, s));
-        else HIP_TRY(wfsa::launch_compiled(c, ctx->i_grid, ctx->i_block, lds, s));
+        else HIP_TRY(wfsa::launch_compiled(c, ctx->i_grid, ctx->i_block, lds, s, ktimed ? ctx->k0[slot] : nullptr,
+                                           ktimed ? ctx->kc[slot] : nullptr));
     }
-    if (!with_grad) HIP_TRY(record(ctx, ctx->kc, slot, s));
+    if (ktimed && ctx->n_groups == 0) HIP_TRY(record(ctx, ctx->kc, slot, s));
     if (with_grad) {
         if (ctx->n_groups > 0) HIP_TRY(wfsa::launch_slab_sum(ctx->gpart.ptr, ctx->c_grid, np, ctx->out.ptr, s));
         else HIP_TRY(hipMemsetAsync(ctx->out.ptr, 0, (size_t(np) + 1) * sizeof(double), s));
