@@ -341,9 +341,9 @@ def roofline_of(m, traffic):
                 "algorithmic_bytes_per_launch": alg_bytes,
                 "note": ("the pass reads the compiled stream (10-bit delta words, 1.62x the algorithmic bytes in "
                          "PMC traffic) and is bound by those bytes: the delta stream's loads alone take 15.4 us of "
-                         "the micro's 17.9 us pass (profiles/r04/stream_format_micro_v4b.txt); HIP events around "
-                         "the launch include its ~3 us launch gap (rocprof's kernel average is the tighter figure, "
-                         "profiles/r04/, DESIGN 3)")}
+                         "the micro's 17.9 us pass (profiles/r04/stream_format_micro_v4b.txt); the kernel time is from "
+                         "HIP events attached to the kernel's dispatch (hipExtLaunchKernelGGL start/stop), within "
+                         "~1.5 us of rocprof's kernel average (profiles/r04/, DESIGN 3)")}
     # family B: the traversal strings (k_c..k_2 of the evaluation)
     trav_ms = max(fb_ms - kern_ms, 1e-9)
     rows, pedges = st1.get("wave_row_entries", 0), st1.get("wave_pair_edges", 0)
