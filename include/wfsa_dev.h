@@ -112,7 +112,9 @@ typedef struct {
     int64_t slot_chunks;       /* bubble contribution slots, in 16-slot chunks (8 B a slot) */
     int32_t max_group_chunks;  /* chunks of the largest constraint's slot group (one QN block sums it) */
     int32_t wave_pull;         /* the wave kernel pulls (wave_pull_kernel): nodes per lane (4, 6, 8); 0: it pushes (wide2_kernel) */
-    int32_t dense_blas;        /* dense path GEMM engine (WFSA_DENSE_ENGINE): 0 our fused MFMA kernels, 1 rocBLAS dgemm + our epilogues, 2 our split-K MFMA kernels + epilogues */
+    int32_t dense_blas;        /* dense path GEMM engine (WFSA_DENSE_ENGINE): 0 our fused MFMA kernels, 1 rocBLAS dgemm + our epilogues, 2 our split-K MFMA kernels + epilogues, 3 our LDS-DMA pipelined MFMA kernels + epilogues */
+    int32_t qn_inkernel_waves; /* last device QN run: its update ran inside the stream kernel on this many waves (0: the separate QN step kernel) */
+    int32_t qn_batches;        /* ... in this many batches of constraints (at most 64 members each) */
 } wfsa_dev_stats;
 
 /* context ---------------------------------------------------------------- */

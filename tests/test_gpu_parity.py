@@ -1,5 +1,7 @@
-"""GPU parity: the HIP path (through the C ABI) against the oracle and the
-reference's recorded outputs.  All tests here need a gfx950 device."""
+"""GPU parity: the HIP path (through the C ABI) against the oracle and
+SURVEY.md Appendix A (values from a stand-in-MKL-header build of the
+reference sources, SURVEY.md Appendix B: parity is unpinned, see
+tests/golden/appendix_a.json).  All tests here need a gfx950 device."""
 import json
 import os
 

@@ -1,0 +1,123 @@
+"""The QN update inside the stream kernel (fb_kernels.hpp QnWave).
+
+The device-resident QN loop (src/main.cpp:276-303 run natively; one
+QuasiNewtonLearner::OptimizationStep per step, src/QuasiNewtonLearner.cpp:
+162-201) runs each step's update in the stream kernel's QN waves, which wait
+for every block's bubble slots by an arrival counter and read them
+write-through.  It must give the same bits as the separate qn_step_kernel
+(WFSA_QN_INKERNEL=0) -- rows, x, lambda-dependent trajectory, the last
+gradient -- over runs of any length (the weights alternate between two
+buffers by step parity), across consecutive runs, and through a halt.
+"""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def _learner(W, fsa, sym, off, wt, monkeypatch, inkernel):
+    monkeypatch.setenv("WFSA_QN_INKERNEL", "1" if inkernel else "0")
+    lrn = W.QuasiNewtonLearner(0)
+    lrn.set_info_rmin(False)
+    lrn.BuildFromPacked(fsa, sym, off, wt)
+    lrn.Finalize()
+    lrn.Init(7)
+    return lrn
+
+
+def _corpus(W, compiled_only=False, **kw):
+    syn = W.Synthetic(**kw)
+    sym, off, wt = syn.corpus()
+    fsa = W.Fsa.read_text(syn.wfsa_text)
+    if compiled_only:   # the strings that compile (the others make the loop take the separate kernel)
+        dev = W.Device(0)
+        dev.load_model(fsa)
+        dev.load_corpus(sym, off, wt / wt.sum())
+        dev.recognize()
+        dev.objective_grad(np.full(len(fsa.param_names()), -1.0), want_logq=False)
+        keep = np.flatnonzero(dev.string_tiers() < 0)
+        lens = np.diff(off)[keep]
+        off_k = np.concatenate([[0], np.cumsum(lens)]).astype(np.int64)
+        sym = np.concatenate([sym[off[i]:off[i + 1]] for i in keep]).astype(np.uint8)
+        off, wt = off_k, wt[keep]
+    return fsa, sym, off, wt
+
+
+FAMILIES = {
+    # family A at c3's shape, fewer strings: every string compiles, bubbles at cuts
+    "familyA": dict(n_states=1024, degree=8, vocab=64, emissions=1, n_strings=200_000, max_len=128, seed=1),
+    # many bubbles per string and popular parameters (large slot chunks per member)
+    "ambiguous": dict(n_states=256, degree=8, vocab=16, emissions=1, n_strings=8_000, max_len=64, seed=4,
+                      compiled_only=True),
+}
+
+
+@pytest.mark.parametrize("family", sorted(FAMILIES))
+def test_inkernel_update_equals_qn_step_kernel(family, monkeypatch):
+    import wfsa_amd as W
+    fsa, sym, off, wt = _corpus(W, **FAMILIES[family])
+    a = _learner(W, fsa, sym, off, wt, monkeypatch, True)
+    b = _learner(W, fsa, sym, off, wt, monkeypatch, False)
+    # runs of odd and even length, back to back: the weight parity and the
+    # arrival counters carry across runs
+    # one step first: the gradient the update used and the updated x
+    r1a, r1b = a.Run(1, 1.0, -1.0), b.Run(1, 1.0, -1.0)
+    np.testing.assert_array_equal(a.last_grad(), b.last_grad())
+    np.testing.assert_array_equal(a.x(), b.x())
+    np.testing.assert_array_equal(np.array(r1a), np.array(r1b))
+    a.Init(7)
+    b.Init(7)
+    ra = a.Run(3, 1.0, -1.0) + a.Run(4, 1.0, -1.0) + a.Run(1, 1.0, -1.0) + a.Run(12, 1.0, -1.0)
+    sa = a.stats()
+    rb = b.Run(20, 1.0, -1.0)
+    assert sa["qn_inkernel_waves"] > 0 and sa["qn_batches"] > 0, "the in-kernel update did not run"
+    assert b.stats()["qn_inkernel_waves"] == 0
+    ra, rb = np.array(ra), np.array(rb)
+    bad = sorted(set(int(r) for r, _ in np.argwhere(ra != rb)))
+    assert not bad, f"rows {bad} differ: {ra[bad].tolist()} vs {rb[bad].tolist()}"
+    np.testing.assert_array_equal(a.x(), b.x())
+    np.testing.assert_array_equal(a.last_grad(), b.last_grad())
+    # the weights after the run (parity buffers folded back): the next
+    # evaluation agrees with the other learner's bit for bit
+    kl_a, g_a, _ = a.objective_grad()
+    kl_b, g_b, _ = b.objective_grad()
+    assert kl_a == kl_b and np.array_equal(g_a, g_b)
+
+
+def test_inkernel_update_matches_host_steps(monkeypatch):
+    """the in-kernel loop against the host QN update (OptimizationStep one by
+    one: wfsa_dev_objective_grad + QuasiNewtonLearner.cpp's update on the host)"""
+    import wfsa_amd as W
+    fsa, sym, off, wt = _corpus(W, **FAMILIES["ambiguous"])
+    a = _learner(W, fsa, sym, off, wt, monkeypatch, True)
+    b = _learner(W, fsa, sym, off, wt, monkeypatch, True)
+    rows_a = a.Run(8, 1.0, -1.0)
+    assert a.stats()["qn_inkernel_waves"] > 0
+    rows_b = [b.OptimizationStep(1.0, -1.0)[0] for _ in range(8)]
+    for r, q in zip(rows_a, rows_b):
+        for u, v in zip(r[:5], q[:5]):
+            assert abs(u - v) <= max(1e-14, 1e-11 * max(abs(u), abs(v)))
+    np.testing.assert_allclose(a.x(), b.x(), rtol=1e-11, atol=1e-13)
+
+
+def test_inkernel_halting_run(monkeypatch):
+    """a halting run stops at the same epoch with the same rows and state as
+    the separate kernel; the steps enqueued after the halt are skipped and
+    the next run starts cleanly"""
+    import wfsa_amd as W
+    fsa, sym, off, wt = _corpus(W, **FAMILIES["ambiguous"])
+    a = _learner(W, fsa, sym, off, wt, monkeypatch, True)
+    b = _learner(W, fsa, sym, off, wt, monkeypatch, False)
+    ra = a.Run(200, 1.0, 1e-3)
+    rb = b.Run(200, 1.0, 1e-3)
+    assert 0 < len(ra) < 200
+    assert np.array_equal(np.array(ra), np.array(rb))
+    assert np.array_equal(a.x(), b.x())
+    kl_a, g_a, _ = a.objective_grad()
+    kl_b, g_b, _ = b.objective_grad()
+    assert kl_a == kl_b and np.array_equal(g_a, g_b)
+    # after the halt: a fresh start runs in-kernel again and matches
+    a.Init(7)
+    b.Init(7)
+    assert np.array_equal(np.array(a.Run(5, 1.0, -1.0)), np.array(b.Run(5, 1.0, -1.0)))
+    assert np.array_equal(a.x(), b.x())

@@ -1,7 +1,10 @@
-"""The CPU oracle (oracle/wfsa_oracle.c) pinned against the reference's own
-recorded outputs (SURVEY.md Appendix A -> tests/golden/appendix_a.json) and
-its CTest outcomes; its two engines (path enumeration = the reference
-algorithm, dense trellis) checked against each other."""
+"""The CPU oracle (oracle/wfsa_oracle.c) against the reference's CTest
+outcomes (CMakeLists.txt:34-57, the only outputs the reference itself holds)
+and against SURVEY.md Appendix A (tests/golden/appendix_a.json: values from a
+stand-in-MKL-header build of the reference sources, SURVEY.md Appendix B -- a
+consistency check, not a pin: parity is unpinned); its two engines (path
+enumeration = the reference algorithm, dense trellis) checked against each
+other."""
 import json
 import os
 

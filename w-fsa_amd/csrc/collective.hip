@@ -24,11 +24,45 @@ namespace {
 
 // ---- RCCL ----------------------------------------------------------------
 
+// A non-blocking communicator's call that returned ncclInProgress: poll its
+// state until it settles; ncclInProgress after limit_s = timed out
+ncclResult_t rccl_settle(ncclComm_t c, double limit_s) {
+    const auto t0 = std::chrono::steady_clock::now();
+    for (;;) {
+        ncclResult_t st = ncclInProgress;
+        if (ncclCommGetAsyncError(c, &st) != ncclSuccess) return ncclInternalError;
+        if (st != ncclInProgress) return st;
+        if (std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() > limit_s) return ncclInProgress;
+        usleep(20);
+    }
+}
+
+// WFSA_RCCL_BLOCKING=1: a blocking communicator (RCCL's default mode)
+bool rccl_blocking() {
+    const char* e = std::getenv("WFSA_RCCL_BLOCKING");
+    return e && e[0] == '1';
+}
+
 class RcclCollective final : public Collective {
 public:
-    RcclCollective(ncclComm_t c, int n, int r) : comm_(c) {
+    RcclCollective(ncclComm_t c, int n, int r) : comm_(c), timeout_s_(comm_timeout_s()) {
         n_ = n;
         r_ = r;
+    }
+    // the communicator's asynchronous error, or a host wait past the limit:
+    // abort it (its pending kernels on this rank end) and report
+    int watchdog(double waited_s) override {
+        if (check()) return 1;
+        std::string why;
+        ncclResult_t st = ncclSuccess;
+        if (comm_ && ncclCommGetAsyncError(comm_, &st) == ncclSuccess && st != ncclSuccess && st != ncclInProgress)
+            why = std::string("RCCL asynchronous error: ") + ncclGetErrorString(st);
+        else if (waited_s > timeout_s_)
+            why = "no progress within WFSA_COMM_TIMEOUT_S (a member failed or stalled)";
+        if (why.empty()) return 0;
+        abort(why.c_str());
+        err_ = why;
+        return 1;
     }
     ~RcclCollective() override {
         if (comm_) (void)ncclCommDestroy(comm_);
@@ -48,8 +82,10 @@ public:
         ncclDataType_t t = op == RedOp::MaxU8 ? ncclUint8 : ncclDouble;
         ncclRedOp_t o = op == RedOp::SumF64 ? ncclSum : op == RedOp::MinF64 ? ncclMin : ncclMax;
         ncclResult_t r = ncclAllReduce(buf, buf, n, t, o, comm_, s);
+        if (r == ncclInProgress) r = rccl_settle(comm_, timeout_s_);   // (enqueued once it settles)
         if (r != ncclSuccess) {
-            err_ = std::string("ncclAllReduce failed: ") + ncclGetErrorString(r);
+            err_ = r == ncclInProgress ? std::string("ncclAllReduce did not settle within WFSA_COMM_TIMEOUT_S")
+                                       : std::string("ncclAllReduce failed: ") + ncclGetErrorString(r);
             return 1;
         }
         return 0;
@@ -57,6 +93,7 @@ public:
 
 private:
     ncclComm_t comm_;
+    double timeout_s_;
 };
 
 // ---- in-process group ----------------------------------------------------
@@ -238,12 +275,21 @@ std::unique_ptr<Collective> make_rccl_collective(int nranks, int rank, const uin
     ncclUniqueId uid;
     std::memcpy(&uid, id, sizeof uid);
     ncclComm_t c = nullptr;
-    ncclResult_t r = ncclCommInitRank(&c, nranks, uid, rank);
+    // non-blocking: a member that never joins ends the set-up after
+    // WFSA_COMM_TIMEOUT_S instead of blocking this thread for good
+    ncclConfig_t cfg = NCCL_CONFIG_INITIALIZER;
+    cfg.blocking = rccl_blocking() ? 1 : 0;
+    ncclResult_t r = ncclCommInitRankConfig(&c, nranks, uid, rank, &cfg);
+    if (c && (r == ncclInProgress || (r == ncclSuccess && !cfg.blocking))) r = rccl_settle(c, comm_timeout_s());
     if (r != ncclSuccess) {
-        err = std::string("ncclCommInitRank failed: ") + ncclGetErrorString(r);
+        err = r == ncclInProgress ? std::string("ncclCommInitRankConfig: the members did not all join within WFSA_COMM_TIMEOUT_S")
+                                  : std::string("ncclCommInitRankConfig failed: ") + ncclGetErrorString(r);
+        if (c) (void)ncclCommAbort(c);
         return nullptr;
     }
-    return std::make_unique<RcclCollective>(c, nranks, rank);
+    auto col = std::make_unique<RcclCollective>(c, nranks, rank);
+    if (!col->reserve_agreement(err)) return nullptr;
+    return col;
 }
 
 std::unique_ptr<Collective> make_local_collective(int nranks, int rank, const uint8_t id[kCommIdBytes],
@@ -270,7 +316,9 @@ std::unique_ptr<Collective> make_local_collective(int nranks, int rank, const ui
         g = slot;
         if (++g->joined == n) g_reg.erase(serial);   // every member holds the group now
     }
-    return std::make_unique<LocalCollective>(g, rank, device);
+    auto col = std::make_unique<LocalCollective>(g, rank, device);
+    if (!col->reserve_agreement(err)) return nullptr;
+    return col;
 }
 
 int rccl_unique_id(uint8_t id[kCommIdBytes], std::string& err) {
@@ -332,7 +380,9 @@ std::unique_ptr<Collective> make_host_collective(int nranks, int rank, HostAllre
         err = "host transport: bad arguments";
         return nullptr;
     }
-    return std::make_unique<HostCollective>(nranks, rank, fn, user);
+    auto col = std::make_unique<HostCollective>(nranks, rank, fn, user);
+    if (!col->reserve_agreement(err)) return nullptr;
+    return col;
 }
 
 // ---- one-shot peer all-reduce (collective.hpp) ----------------------------
@@ -605,7 +655,27 @@ private:
     PeerArgs args_{};
 };
 
-Collective::~Collective() = default;
+double comm_timeout_s() {
+    const char* e = std::getenv("WFSA_COMM_TIMEOUT_S");   // (read per communicator: tests shorten it)
+    const double v = e ? std::atof(e) : 0.0;
+    return v > 0 ? v : 300.0;
+}
+
+constexpr size_t kAgreeBytes = std::max(size_t(3000) * sizeof(double), size_t(kLocalMaxRanks) * 88);
+
+bool Collective::reserve_agreement(std::string& err) {
+    if (hipMalloc(&agree_buf_, kAgreeBytes) != hipSuccess) {
+        (void)hipGetLastError();
+        agree_buf_ = nullptr;
+        err = "communicator set-up: no device memory for the peer path's agreement";
+        return false;
+    }
+    return true;
+}
+
+Collective::~Collective() {
+    if (agree_buf_) (void)hipFree(agree_buf_);
+}
 
 const char* Collective::peer_state() const {
     return peer_st_ == 1 ? "on" : peer_st_ == -1 ? "off" : peer_st_ == -2 ? "failed" : "untried";
@@ -628,23 +698,15 @@ int Collective::try_peer(hipStream_t s) {
         return 0;
     }
     constexpr size_t kCheck = 3000;   // spans three chunks
-    const size_t dbytes = std::max(kCheck * sizeof(double), size_t(kLocalMaxRanks) * sizeof(PeerBlob));
-    // the agreement's buffer: device memory, else host-mapped memory (so a
-    // member short of device memory still takes part in every exchange below
-    // and reports its failure as its "bad" byte)
-    uint8_t* d = nullptr;
-    uint8_t* dh = nullptr;
-    if (hipMalloc(reinterpret_cast<void**>(&d), dbytes) != hipSuccess) {
-        (void)hipGetLastError();
-        d = nullptr;
-        if (hipHostMalloc(reinterpret_cast<void**>(&dh), dbytes, hipHostMallocMapped | hipHostMallocCoherent) !=
-                hipSuccess ||
-            hipHostGetDevicePointer(reinterpret_cast<void**>(&d), dh, 0) != hipSuccess) {
-            (void)hipGetLastError();
-            if (dh) (void)hipHostFree(dh);
-            err_ = "peer set-up: no memory for the agreement";
-            return 1;   // (the caller fails and aborts the communicator: every member hears of it)
-        }
+    static_assert(kCheck * sizeof(double) <= kAgreeBytes && kLocalMaxRanks * sizeof(PeerBlob) <= kAgreeBytes,
+                  "the agreement buffer holds the check sum and the set-up blobs");
+    // the agreement's buffer, reserved with the communicator: no allocation
+    // here can fail, so every member takes part in every exchange below and a
+    // local failure travels as its "bad" byte
+    uint8_t* d = static_cast<uint8_t*>(agree_buf_);
+    if (!d) {   // (never: the communicator is not made without it)
+        err_ = "peer set-up: no agreement buffer";
+        return 1;
     }
     auto xfer = [&](void* b, size_t n, RedOp op) { return transport_allreduce(b, n, op, s); };
     auto agree = [&](bool mine_ok, bool& all_ok) {   // a byte per rank, max-reduced
@@ -659,11 +721,7 @@ int Collective::try_peer(hipStream_t s) {
         for (uint8_t b : bad) all_ok &= b == 0;
         return 0;
     };
-    auto done = [&](int rc) {
-        if (dh) (void)hipHostFree(dh);
-        else (void)hipFree(d);
-        return rc;
-    };
+    auto done = [&](int rc) { return rc; };
     std::string why;
     // (1) devices: a byte per rank holding its device + 1
     {

@@ -53,11 +53,22 @@ public:
     // to call at any host sync point: the peer kernels report through
     // host-mapped memory.
     int check();
-    // this member failed: make every other member's next collective (or the
-    // one it is waiting in) fail at once instead of waiting for its timeout.
-    // The in-process group is poisoned, the peer areas of every member get
-    // their poison word, an RCCL communicator is aborted.  Every later call
-    // on this communicator fails.
+    // check() plus the transport's own liveness, for a host that has been
+    // waiting `waited_s` seconds for device work that includes collectives:
+    // an RCCL communicator with an asynchronous error, or a wait longer than
+    // WFSA_COMM_TIMEOUT_S (default 300 s), is aborted here and reported (1)
+    virtual int watchdog(double waited_s) { return check(); }
+    // this member failed: every later call on this communicator fails, and
+    // the members hear of it as follows (failure semantics):
+    //  * in-process group: poisoned -- every member waiting in, or later
+    //    entering, a collective fails at once;
+    //  * peer all-reduce (the per-step [LL, grad] sums): every member's area
+    //    gets its poison word -- their current or next peer call fails at once;
+    //  * RCCL: the communicator is aborted (ncclCommAbort).  The other
+    //    processes' pending RCCL calls are NOT woken by that: each rank's own
+    //    watchdog ends them (its asynchronous error, or WFSA_COMM_TIMEOUT_S);
+    //  * host callback (gloo, MPI): nothing to abort -- the other members end
+    //    by the callback transport's own timeout.
     void abort(const char* why);
     bool aborted() const { return aborted_; }
 
@@ -74,6 +85,14 @@ protected:
     virtual bool peer_default() const { return false; }
     int n_ = 1, r_ = 0;
     std::string err_;
+
+    // device memory for the peer set-up's exchanges, reserved when the
+    // communicator is made, so the set-up never lacks a buffer for its
+    // agreement (every member then takes part in every exchange)
+    void* agree_buf_ = nullptr;
+public:
+    bool reserve_agreement(std::string& err);   // (the make_*_collective functions call it)
+protected:
 
 private:
     int try_peer(hipStream_t s);
@@ -131,6 +150,8 @@ std::unique_ptr<Collective> make_rccl_collective(int nranks, int rank, const uin
 std::unique_ptr<Collective> make_local_collective(int nranks, int rank, const uint8_t id[kCommIdBytes],
                                                   int device, std::string& err);
 int rccl_unique_id(uint8_t id[kCommIdBytes], std::string& err);
+// the host watchdog's limit (WFSA_COMM_TIMEOUT_S, default 300 s)
+double comm_timeout_s();
 
 // a transport over a host callback (e.g. torch.distributed over gloo, MPI):
 // fn(user, host buffer, count, op) all-reduces in place, op 0 = sum of

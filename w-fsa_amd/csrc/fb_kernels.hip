@@ -2075,13 +2075,58 @@ __device__ __forceinline__ void reg_add(double (&r)[N], int i, double v) {
 
 // A small bubble of class (N nodes, RE edges): quads of bubble b at
 // tbl[k * n + b] -- [header], RE/2 x [(code, sd) x 2], RE/4 x [slot x 4].
+// The partner's value at butterfly level d (1, 2, ..., 32) of an aligned
+// group sum, without the LDS crossbar (ds_bpermute): DPP within a 16-lane
+// row, the gfx950 permlane swaps across rows.  At level d every aligned
+// d-lane group already holds one value, so the half-row / row mirrors pair
+// the same groups as xor 4 / xor 8 (tools/micro/permlane_probe.hip: the swaps'
+// lane mapping).
+template <int D>
+__device__ __forceinline__ double bfly_partner(double v) {
+    const int lo = __double2loint(v), hi = __double2hiint(v);
+    if constexpr (D == 16 || D == 32) {
+        const auto l = D == 16 ? __builtin_amdgcn_permlane16_swap(lo, lo, false, false)
+                               : __builtin_amdgcn_permlane32_swap(lo, lo, false, false);
+        const auto h = D == 16 ? __builtin_amdgcn_permlane16_swap(hi, hi, false, false)
+                               : __builtin_amdgcn_permlane32_swap(hi, hi, false, false);
+        const bool up = (lane_id() & D) != 0;   // (out[0]: the lower row's lanes, out[1]: the upper row's)
+        return __hiloint2double(up ? h[0] : h[1], up ? l[0] : l[1]);
+    } else {
+        constexpr int ctrl = D == 1 ? 0xB1 : D == 2 ? 0x4E : D == 4 ? 0x141 : 0x140;   // quad_perm / half mirror / mirror
+        return __hiloint2double(__builtin_amdgcn_mov_dpp(hi, ctrl, 0xF, 0xF, false),
+                                __builtin_amdgcn_mov_dpp(lo, ctrl, 0xF, 0xF, false));
+    }
+}
+// v summed over the lane's aligned group of 2^k lanes, levels below kmax
+// (wave-uniform) exchanged: every lane of the group ends with the same bits
+__device__ __forceinline__ double group_sum(double v, int k, int kmax) {
+    if (kmax >= 1) { const double t = bfly_partner<1>(v); if (k >= 1) v += t; }
+    if (kmax >= 2) { const double t = bfly_partner<2>(v); if (k >= 2) v += t; }
+    if (kmax >= 3) { const double t = bfly_partner<4>(v); if (k >= 3) v += t; }
+    if (kmax >= 4) { const double t = bfly_partner<8>(v); if (k >= 4) v += t; }
+    if (kmax >= 5) { const double t = bfly_partner<16>(v); if (k >= 5) v += t; }
+    if (kmax >= 6) { const double t = bfly_partner<32>(v); if (k >= 6) v += t; }
+    return v;
+}
+
+#ifndef WFSA_UNI_BUBBLES   // (variant builds: the uniform-structure path of small bubbles)
+#define WFSA_UNI_BUBBLES 0
+#endif
+// (tr: timing experiments only, stamps 8..11 of the wave's trace row)
+#define WFSA_BSTAMP(k)                                                   \
+    if (tr) {                                                            \
+        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");     \
+        if (lane_id() == 0) tr[k] = __builtin_amdgcn_s_memrealtime();    \
+    }
 template <int N, int RE, bool RMIN = false>
 __device__ __forceinline__ double small_bubble(const BubbleArgs& a, const int4* __restrict__ tbl, int n, int b,
-                                               int pos) {
+                                               int pos, unsigned long long* tr = nullptr) {
+#pragma clang fp contract(off)   // (both forms below: the same bits)
     constexpr int NQ = 1 + RE / 2 + RE / 4;
     int4 q[NQ];
 #pragma unroll
     for (int k = 0; k < NQ; ++k) q[k] = tbl[size_t(k) * size_t(n) + size_t(b)];
+    WFSA_BSTAMP(8)
     const int nodes = q[0].x & 0xffff, edges = q[0].x >> 16;
     const double p = __longlong_as_double((long long)(uint32_t(q[0].z)) | ((long long)(uint32_t(q[0].w)) << 32));
     int code[RE], sd[RE], slot[RE];
@@ -2102,17 +2147,38 @@ __device__ __forceinline__ double small_bubble(const BubbleArgs& a, const int4* 
     double ew[RE];
 #pragma unroll
     for (int e = 0; e < RE; ++e) ew[e] = (WFSA_KDBG(a.dbg) & 2) ? 1.0 + 1e-3 * code[e] : a.ewp[code[e]];   // padding edges carry the zero-slot code
+    WFSA_BSTAMP(9)
     double A[N], B[N];
 #pragma unroll
     for (int k = 0; k < N; ++k) {
         A[k] = k == 0 ? 1.0 : 0.0;
         B[k] = 0.0;
     }
+    // Bubbles are sorted by shape, so the lanes of a wave mostly share one
+    // structure (header and every edge's nodes): then the node indices are
+    // wave-uniform and address the registers directly (s_set_gpr_idx), else
+    // every access is a tree of selects (reg_get / reg_add)
+    bool same = q[0].x == __builtin_amdgcn_readfirstlane(q[0].x);
 #pragma unroll
-    for (int e = 0; e < RE; ++e)
-        if (e < edges) reg_add(A, sd[e] >> 16, reg_get(A, sd[e] & 0xffff) * ew[e]);
-    const double Z = reg_get(A, nodes - 1);
+    for (int e = 0; e < RE; ++e) same = same && sd[e] == __builtin_amdgcn_readfirstlane(sd[e]);
+    const bool uni = WFSA_UNI_BUBBLES && !RMIN && __all(same);
+    if (uni) {
+        const int eu = __builtin_amdgcn_readfirstlane(edges);
+#pragma unroll
+        for (int e = 0; e < RE; ++e)
+            if (e < eu) {
+                const int s = __builtin_amdgcn_readfirstlane(sd[e]);
+                const double v = A[s & 0xffff] * ew[e];
+                A[s >> 16] = A[s >> 16] + v;
+            }
+    } else {
+#pragma unroll
+        for (int e = 0; e < RE; ++e)
+            if (e < edges) reg_add(A, sd[e] >> 16, reg_get(A, sd[e] & 0xffff) * ew[e]);
+    }
+    const double Z = uni ? A[__builtin_amdgcn_readfirstlane(nodes) - 1] : reg_get(A, nodes - 1);
     const double scale = -p / Z;
+    WFSA_BSTAMP(10)
     if (RMIN && a.rmin_acc) {   // (min, x) forward for the rmin column in B's registers (re-zeroed
                                 // for the backward); the min path never exceeds Z
 #pragma unroll
@@ -2131,7 +2197,8 @@ __device__ __forceinline__ double small_bubble(const BubbleArgs& a, const int4* 
 #pragma unroll
         for (int k = 0; k < N; ++k) B[k] = 0.0;
     }
-    reg_add(B, nodes - 1, 1.0);
+    if (uni) B[__builtin_amdgcn_readfirstlane(nodes) - 1] = 0.0 + 1.0;
+    else reg_add(B, nodes - 1, 1.0);
     // lanes of an aligned 2^k group sharing edge e's parameter (slot field
     // level k, layout_slots) sum their contributions by a butterfly -- every
     // lane of the group gets the same bits, in a fixed order -- and the
@@ -2143,25 +2210,40 @@ __device__ __forceinline__ double small_bubble(const BubbleArgs& a, const int4* 
 #pragma unroll
     for (int t = 1; t <= 6; ++t) kmax = __ballot(kl >= t) ? t : kmax;
     const int lane = lane_id();
-#pragma unroll
-    for (int e = RE - 1; e >= 0; --e)
-        if (e < edges) {
-            const int src = sd[e] & 0xffff;
-            const double bb = ew[e] * reg_get(B, sd[e] >> 16);
-            reg_add(B, src, bb);
-            double v = reg_get(A, src) * bb * scale;
-            const int k = slot[e] >= 0 ? (slot[e] >> 28) : 0;
-            for (int d = 1; d < (1 << kmax); d <<= 1) {
-                const double t = __shfl_xor(v, d, kWave);
-                if (d < (1 << k)) v += t;
-            }
-            if (slot[e] >= 0 && (lane & ((1 << k) - 1)) == 0 && !(WFSA_KDBG(a.dbg) & 1))
-                a.contrib[slot[e] & 0x0fffffff] = v;
+    auto contribute = [&](int e, double v) {   // edge e's slot (its group's sum, by the group's first lane)
+        const int k = slot[e] >= 0 ? (slot[e] >> 28) : 0;
+        v = group_sum(v, k, kmax);
+        if (slot[e] >= 0 && (lane & ((1 << k) - 1)) == 0 && !(WFSA_KDBG(a.dbg) & 1)) {
+            if (a.wt) store_wt(&a.contrib[slot[e] & 0x0fffffff], v);
+            else a.contrib[slot[e] & 0x0fffffff] = v;
         }
+    };
+    if (uni) {
+        const int eu = __builtin_amdgcn_readfirstlane(edges);
+#pragma unroll
+        for (int e = RE - 1; e >= 0; --e)
+            if (e < eu) {
+                const int s = __builtin_amdgcn_readfirstlane(sd[e]);
+                const double bb = ew[e] * B[s >> 16];
+                B[s & 0xffff] = B[s & 0xffff] + bb;
+                contribute(e, A[s & 0xffff] * bb * scale);
+            }
+    } else {
+#pragma unroll
+        for (int e = RE - 1; e >= 0; --e)
+            if (e < edges) {
+                const int src = sd[e] & 0xffff;
+                const double bb = ew[e] * reg_get(B, sd[e] >> 16);
+                reg_add(B, src, bb);
+                contribute(e, reg_get(A, src) * bb * scale);
+            }
+    }
+    WFSA_BSTAMP(11)
     const double lz = log(Z);
     if (a.logq) global_add(&a.logq[q[0].y], lz);
     return p * lz;
 }
+#undef WFSA_BSTAMP
 
 // Big bubbles, one wavefront each: the lanes stage the edges (code, nodes,
 // weight) in LDS in parallel, lane 0 runs the two sweeps over the staged
@@ -2223,7 +2305,10 @@ __device__ double big_bubble(const BubbleArgs& a, int i, int* lsd, double* lw, d
     wave_sync();
     const int base = a.big_edge_base[i];
     for (int e = lane; e < edges; e += kWave)
-        for (int q = a.big_eslot_ptr[base + e]; q < a.big_eslot_ptr[base + e + 1]; ++q) a.contrib[a.big_eslot[q]] = lv[e];
+        for (int q = a.big_eslot_ptr[base + e]; q < a.big_eslot_ptr[base + e + 1]; ++q) {
+            if (a.wt) store_wt(&a.contrib[a.big_eslot[q]], lv[e]);
+            else a.contrib[a.big_eslot[q]] = lv[e];
+        }
     return res;
 }
 
@@ -2269,7 +2354,9 @@ __global__ __launch_bounds__(kBubbleBlock) void bubble_kernel(BubbleArgs a) {
 // evaluated, so its latency hides behind that work (both sets would spill).
 // DBG (timing experiments only, WFSA_FBS_DBG): 1 no table gathers, 3 no
 // stream pass at all, 4 neither stream pass nor table staging, 5 the QN finish only, 6 / 7
-// prefetch sets of 2 / 6 rows, 8 no bubble code, 9 stream loads only
+// prefetch sets of 2 / 6 rows, 8 no bubble code, 9 stream loads only; the
+// delta kernel also: 11 no table staging, 12 no QN finish, 13 neither bubbles
+// nor finish (the stream pass and the staging alone)
 // One delta-format row (fb_kernels.hpp) of a lane: three 10-bit fields per
 // dword; each steps the lane's LDS address in the staged table forward and
 // gathers that entry -- three VALU per field (extract, shift-add, f64 add).
@@ -2306,7 +2393,180 @@ __device__ __forceinline__ void delta_row(const uint4 v, uint32_t& cur, double& 
     }
 }
 
-template <bool WIDE, bool W_LDS, bool MULTI, int DBG = 0, bool RMIN = false, bool DELTA = false>
+// The QuasiNewton update of one batch of constraints (QnWave) by one
+// wavefront, a lane per member: the arithmetic and the summation orders of
+// qn_step_kernel<true> (qn_kernel.hip: ComputeExpX, ComputeG,
+// ComputeLambdaNext, the x update, LambdaUpdate -- src/QuasiNewtonLearner.cpp:
+// 53-56,127-201, src/Learner.cpp:438-462), so the trajectory is the same bit
+// for bit.  The per-constraint sums run in member order on the constraint's
+// first lane, which reads its members' values by shuffles.  ok == false (the
+// arrival poll gave up): NaN partials, no update.
+// a batch's member data: loaded before the QN wave's poll (none of it is
+// written in this launch)
+struct QnBatchIn {
+    int c0, nc, m0, m1, nchunk;
+    int64_t cbase;
+    int con, fo, nch, fc, cpl;
+    double x, ft, laml;
+};
+__device__ __forceinline__ QnBatchIn qn_wave_load(const QnWave& q, int b) {
+    const int lane = lane_id();
+    const int4 bd = q.batch[2 * b], bc = q.batch[2 * b + 1];
+    QnBatchIn in;
+    in.c0 = bd.x;
+    in.nc = bd.y - bd.x;
+    in.m0 = bd.z;
+    in.m1 = bd.w;
+    in.nchunk = bc.x;
+    in.cbase = int64_t(uint32_t(bc.y)) | (int64_t(bc.z) << 32);
+    const int m = in.m0 + lane;
+    in.con = in.c0;
+    in.fo = in.nch = in.fc = in.cpl = 0;
+    in.x = in.ft = in.laml = 0.0;
+    if (m < in.m1) {
+        in.con = q.con_of[m];
+        in.fo = q.full_of[m];
+        in.x = q.x[m];
+        in.ft = q.fixed_t[m];
+        in.fc = q.mfirst[m];
+        in.nch = q.mnch[m];
+    }
+    if (lane < in.nc) {
+        in.cpl = q.cptr[in.c0 + lane];
+        in.laml = q.lambda[in.c0 + lane];
+    }
+    return in;
+}
+
+__device__ __forceinline__ void qn_wave_batch(const QnWave& q, const QnBatchIn& in, bool ok) {
+#pragma clang fp contract(off)
+    const int lane = lane_id();
+    const int c0 = in.c0, nc = in.nc, m0 = in.m0, m1 = in.m1, nchunk = in.nchunk;
+    const int64_t cbase = in.cbase;
+    const int m = m0 + lane;
+    const bool valid = m < m1;
+    const int con = in.con, fo = in.fo, nch = in.nch, fc = in.fc, cpl = in.cpl;
+    const double x = in.x, ft = in.ft, laml = in.laml;
+    const int j = con - c0;                        // the member's constraint within the batch
+    const int first = __shfl(cpl, j, kWave);       // its first member
+    const int nxt = __shfl(cpl, min(j + 1, kWave - 1), kWave);
+    const int end = j + 1 < nc ? nxt : m1;
+    const double lam = __shfl(laml, j, kWave);
+    const int nm = end - first, ld = first - m0;   // members, and the first member's lane
+    const bool leader = valid && m == first;
+    int maxnm = valid ? nm : 0, maxnch = valid ? nch : 0;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        maxnm = max(maxnm, __shfl_xor(maxnm, o, kWave));
+        maxnch = max(maxnch, __shfl_xor(maxnch, o, kWave));
+    }
+    // the batch's bubble contribution chunks (stored write-through by this
+    // launch's bubble waves: sc1 loads), one per lane per round, each summed
+    // by chunk_tree; then every member adds its chunks' sums in chunk order
+    double cs[kQnWaveChunkRounds];
+#pragma unroll
+    for (int r = 0; r < kQnWaveChunkRounds; ++r) {
+        cs[r] = 0.0;
+        const int qc = r * kWave + lane;
+        if (r * kWave < nchunk && qc < nchunk) {
+            double v[kSlotChunk];
+#pragma unroll
+            for (int k = 0; k < kSlotChunk; ++k) v[k] = load_wt(q.contrib + cbase + int64_t(kSlotChunk) * qc + k);
+            cs[r] = chunk_tree(v);
+        }
+    }
+    double sm = 0.0;
+    for (int t = 0; t < maxnch; ++t) {
+        const int qc = fc + t, src = qc & (kWave - 1), rr = qc >> 6;
+        double v = 0.0;
+#pragma unroll
+        for (int r = 0; r < kQnWaveChunkRounds; ++r) {
+            if (r * kWave >= nchunk) break;   // (uniform)
+            const double s = __shfl(cs[r], src, kWave);
+            if (rr == r) v = s;
+        }
+        if (t < nch) sm += v;
+    }
+    double gi = 0.0;
+    gi += ft;
+    const double sg = gi + sm;
+    const double e = exp(x);
+    double gg = -1.0;   // ComputeG: -1 + sum exp(x) in member order
+    for (int t = 0; t < maxnm; ++t) {
+        const double v = __shfl(e, min(lane + t, kWave - 1), kWave);
+        if (leader && t < nm) gg += v;
+    }
+    double r = lam * gg;   // ComputeLambdaNext
+    for (int t = 0; t < maxnm; ++t) {
+        const double v = __shfl(sg, min(lane + t, kWave - 1), kWave);
+        if (leader && t < nm) r -= v;
+    }
+    const double laux_l = r / (gg + 1.0);
+    const double g = __shfl(gg, ld, kWave), laux = __shfl(laux_l, ld, kWave);
+    double gerr = 0.0;
+    if (valid && ok) {
+        const double aux = e * lam;
+        gerr = fabs(sg + aux);
+        const double xn = x - q.eta * ((sg + e * laux) / aux);
+        q.x[m] = xn;
+        q.grad[m] = sg;
+        q.w_next[fo] = xn;   // GetWeight for the next step
+        q.ewp_next[fo] = exp(xn);
+    }
+    double ge = 0.0;
+    for (int t = 0; t < maxnm; ++t) {
+        const double v = __shfl(gerr, min(lane + t, kWave - 1), kWave);
+        if (leader && t < nm) ge = fmax(ge, v);
+    }
+    if (leader) {
+        double4 pv;
+        if (ok) {
+            const double d = lam - laux_l;   // LambdaUpdate (src/Learner.cpp:438-462)
+            q.lambda[con] = q.exp_lambda ? lam * exp(-q.eta * (d / lam)) : lam - q.eta * d;
+            pv.x = g;
+            pv.y = g;
+            pv.z = lam;
+            pv.w = ge;
+        } else {
+            pv.x = pv.y = pv.z = pv.w = NAN;
+        }
+        reinterpret_cast<double4*>(q.partial)[con] = pv;
+    }
+}
+
+// QN wave r of the launch: wait for every block's arrival (its bubble slots
+// and the finish wave's halt decision), then its batches r, r + n_waves, ...
+constexpr unsigned kQnPollLimit = 1u << 20;   // x s_sleep 4 (~0.1 us): ~0.1 s, then give up
+__device__ __forceinline__ void qn_wave_run(const QnWave& q, int r, unsigned long long* tr) {
+    const int lane = lane_id();
+    QnBatchIn first{};
+    if (r < q.n_batches) first = qn_wave_load(q, r);   // (in flight during the poll)
+    int ok = 1;
+    if (lane == 0) {
+        unsigned it = 0;
+        while (load_wt(q.arrive + q.parity) < unsigned(q.n_arrive)) {
+            __builtin_amdgcn_s_sleep(4);
+            if (++it > kQnPollLimit) {
+                ok = 0;
+                break;
+            }
+        }
+    }
+    ok = __shfl(ok, 0, kWave);
+    if (tr && lane == 0) tr[5] = __builtin_amdgcn_s_memrealtime();   // (timing experiments)
+    if (ok && load_wt(q.halted + 1) != 0u) {   // the previous step halted: this one is skipped
+        if (r == 0 && lane == 0) {
+            q.halted[0] = 1u;   // for the later launches
+            qn_publish_row(q.fin, nullptr, kQnSkipped);
+        }
+        return;
+    }
+    if (r < q.n_batches) qn_wave_batch(q, first, ok != 0);
+    for (int b = r + q.n_waves; b < q.n_batches; b += q.n_waves) qn_wave_batch(q, qn_wave_load(q, b), ok != 0);
+    if (tr && lane == 0) tr[6] = __builtin_amdgcn_s_memrealtime();
+}
+
+template <bool WIDE, bool W_LDS, bool MULTI, int DBG = 0, bool RMIN = false, bool DELTA = false, bool QN = false>
 #ifdef WFSA_FBS_VGPR64   // (variant builds: a 64-VGPR budget, two 1024-thread blocks per CU)
 #define WFSA_FBS_ATTR __attribute__((amdgpu_num_vgpr(64)))
 #else
@@ -2321,8 +2581,37 @@ __global__ __launch_bounds__(1024, (DBG == 10 ? 8 : 1)) WFSA_FBS_ATTR void fbs_k
     const int bid = int(blockIdx.x);
     const int w = int(threadIdx.x) / kWave;
     const int gw = __builtin_amdgcn_readfirstlane(bid * wpb + w);
+#ifdef WFSA_EXPERIMENTS
+    unsigned long long* tr = a.trace ? a.trace + size_t(gw) * 16 : nullptr;   // (timing experiments)
+#define WFSA_STAMP(k) \
+    if (tr && lane == 0) tr[k] = __builtin_amdgcn_s_memrealtime();
+#else
+#define WFSA_STAMP(k)
+#endif
+    WFSA_STAMP(0)
+    if (QN && bid == 0 && threadIdx.x == 0) a.qw.arrive[a.qw.parity ^ 1] = 0u;   // for the next launch
     // halted is written only by an earlier launch (the QN step's finish)
-    if (a.halted && *a.halted) return;
+    if (a.halted && *a.halted) {
+        if (QN && bid == 0 && threadIdx.x == 0) qn_publish_row(a.qw.fin, nullptr, kQnSkipped);   // (no QN kernel)
+        return;
+    }
+    __shared__ unsigned q_arrived;   // QN: this block's waves whose bubble slots have retired
+    // Early bubbles (delta kernel): the small-bubble waves evaluate their
+    // bubbles at entry -- they need no LDS table -- while the other waves
+    // stage the table and announce it by an LDS counter; every wave waits for
+    // that counter before its stream pass (no block barrier on the way)
+    __shared__ unsigned staged_waves;
+    const bool early = DELTA && a.early_bub && a.bub_on && a.bub.small_wpb > 0 && a.bub.small_wpb < wpb &&
+                       DBG != 4 && DBG != 8 && DBG != 10 && DBG != 11 && DBG != 13 && !a.no_streams;
+    if (early) {
+        if (threadIdx.x == 0) {
+            q_arrived = 0u;
+            staged_waves = 0u;
+        }
+        __syncthreads();
+    } else if (QN && threadIdx.x == 0) {
+        q_arrived = 0u;   // (ordered by the staging barrier)
+    }
     const uint32_t zslot = uint32_t(a.n_params);
     // this wave's run of chunk rows
     const int g0 = a.wave_first[gw], g1 = a.wave_first[gw + 1];
@@ -2332,18 +2621,32 @@ __global__ __launch_bounds__(1024, (DBG == 10 ? 8 : 1)) WFSA_FBS_ATTR void fbs_k
     const uint4* st = a.stream + cb + lane;
     constexpr int D = DELTA ? kDeltaPrefetch : (DBG == 6 ? 2 : (DBG == 7 ? 6 : kStreamPrefetch));
     uint4 A[D], B[D];
+    typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+    const bool nt = a.stream_nt != 0;   // once-read stream rows: non-temporal, keep the L2 for the table
     auto load = [&](uint4 (&r)[D], int c0) {
+        if (nt) {
 #pragma unroll
-        for (int d = 0; d < D; ++d) r[d] = st[int64_t(kWave) * min(c0 + d, last)];
+            for (int d = 0; d < D; ++d) {
+                const u32x4 v = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(st + int64_t(kWave) * min(c0 + d, last)));
+                r[d] = make_uint4(v.x, v.y, v.z, v.w);
+            }
+        } else {
+#pragma unroll
+            for (int d = 0; d < D; ++d) r[d] = st[int64_t(kWave) * min(c0 + d, last)];
+        }
     };
     const bool kStreams = DBG != 3 && DBG != 4 && !a.no_streams;   // (timing experiments; bubbles-only launches)
-    if (kStreams) load(A, 0);
+    // the first row set in flight from the start (its latency hides behind
+    // the staging and the bubbles; but the table loads then return behind it),
+    // or issued once the wave's table / bubble loads are out (defer_prefetch)
+    const bool defer = DELTA && DBG != 4 && DBG != 11 && a.defer_prefetch != 0;
+    if (kStreams && !defer) load(A, 0);
     // the previous QN step's finish runs in a wave of its own -- the last
     // wave of block 0, which the host gives no groups and no bubbles -- after
     // the staging barrier, beside the other waves' work
     const bool fin_wave = bid == 0 && w == wpb - 1;
     auto finish = [&]() {
-        if (fin_wave && a.fin.active) {
+        if (fin_wave && a.fin.active && DBG != 12 && DBG != 13) {
             double finfo[7];
             unsigned fstat = kQnRan;
             qn_finish_compute<true>(a.fin, nullptr, finfo, fstat);
@@ -2354,7 +2657,31 @@ __global__ __launch_bounds__(1024, (DBG == 10 ? 8 : 1)) WFSA_FBS_ATTR void fbs_k
         finish();
         return;
     }
-    if (DELTA && !a.no_streams) {
+    double ll_acc = 0.0;
+    bool stored = fin_wave;   // (QN: this wave's stores must retire before it arrives)
+    const bool small_wave = a.bub_on && DBG != 8 && DBG != 10 && DBG != 13 && !fin_wave && w < a.bub.small_wpb;
+    auto small_bubbles = [&]() {   // one per lane, from the first small_wpb waves of every block (spread over all CUs)
+        stored = true;
+        // chunk w * nblk + bid: consecutive chunks (one class, one cost) on
+        // different blocks, so the costly class-B chunks spread over the CUs
+        const int b = (w * nblk + bid) * kWave + lane;
+#ifdef WFSA_EXPERIMENTS
+        unsigned long long* btr = tr;
+#else
+        unsigned long long* btr = nullptr;
+#endif
+        // (the bubbles are on the QN update's critical path; the stream waves
+        // beside them mostly wait for memory: the bubble waves issue first)
+        if (a.bub.prio) __builtin_amdgcn_s_setprio(2);
+        if (b < a.bub.n_small4) ll_acc += small_bubble<4, 4, RMIN>(a.bub, a.bub.sm4_tbl, a.bub.n_small4, b, b, btr);
+        else if (b < a.bub.n_small4 + a.bub.n_small)
+            ll_acc += small_bubble<8, 8, RMIN>(a.bub, a.bub.sm_tbl, a.bub.n_small, b - a.bub.n_small4, b, btr);
+        if (a.bub.prio) __builtin_amdgcn_s_setprio(0);
+    };
+    if (early && small_wave) small_bubbles();
+    if (kStreams && defer && early && small_wave) load(A, 0);
+    const int stage_w0 = early ? a.bub.small_wpb : 0;   // the staging waves: [stage_w0, wpb)
+    if (DELTA && !a.no_streams && DBG != 4 && DBG != 11 && w >= stage_w0) {
         // the delta format's remapped table in 16-byte pieces: slot s holds
         // weight s - 1 - s / kDeltaPeriod, or zero on a multiple of
         // kDeltaPeriod and past the last weight; loads first
@@ -2367,24 +2694,36 @@ __global__ __launch_bounds__(1024, (DBG == 10 ? 8 : 1)) WFSA_FBS_ATTR void fbs_k
             zero = (s % kDeltaPeriod) == 0 || j > last;
             return min(max(j, 0), last);
         };
-        for (int q0 = int(threadIdx.x); q0 < T2; q0 += kB * int(blockDim.x)) {
+        const int nthr = int(blockDim.x) - stage_w0 * kWave;
+        bool pf = kStreams && defer;   // the deferred first row set: after this wave's first table loads
+        for (int q0 = int(threadIdx.x) - stage_w0 * kWave; q0 < T2; q0 += kB * nthr) {
             double2 t[kB];
 #pragma unroll
             for (int b = 0; b < kB; ++b) {
-                const int s2 = 2 * (q0 + b * int(blockDim.x));
+                const int s2 = 2 * (q0 + b * nthr);
                 bool z0, z1;
                 const double lo = a.w[wslot(s2, z0)], hi = a.w[wslot(s2 + 1, z1)];
                 t[b].x = z0 ? 0.0 : lo;
                 t[b].y = z1 ? 0.0 : hi;
             }
+            if (pf) {
+                load(A, 0);
+                pf = false;
+            }
 #pragma unroll
             for (int b = 0; b < kB; ++b) {
-                const int q = q0 + b * int(blockDim.x);
+                const int q = q0 + b * nthr;
                 if (q < T2) dst[q] = t[b];
             }
         }
-        __syncthreads();
-    } else if (W_LDS && DBG != 4 && !a.no_streams) {
+        if (pf) load(A, 0);   // (a wave with no table piece)
+        if (early) {   // this wave's part is in LDS: announce it
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+            if (lane == 0) atomicAdd(&staged_waves, 1u);
+        } else {
+            __syncthreads();
+        }
+    } else if (!DELTA && W_LDS && DBG != 4 && !a.no_streams) {
         // stage w[0, n_params] in 16-byte pieces, all of a thread's loads
         // issued before its first store (loads and stores unconditional --
         // an index past the end is clamped to the last piece, which is then
@@ -2402,29 +2741,40 @@ __global__ __launch_bounds__(1024, (DBG == 10 ? 8 : 1)) WFSA_FBS_ATTR void fbs_k
         }
         __syncthreads();
     }
+    WFSA_STAMP(1)
     finish();
     const double* wsrc = W_LDS ? lds : a.w;
-    double ll_acc = 0.0;
-    if (a.bub_on && DBG != 8 && DBG != 10 && !fin_wave) {   // this wave's bubbles, before its streams
-        // small ones, one per lane, from the first small_wpb waves of every
-        // block (spread over all CUs)
-        if (w < a.bub.small_wpb) {   // small_wpb <= waves per block (bubbles_fused)
-            const int b = (bid * a.bub.small_wpb + w) * kWave + lane;
-            if (b < a.bub.n_small4) ll_acc += small_bubble<4, 4, RMIN>(a.bub, a.bub.sm4_tbl, a.bub.n_small4, b, b);
-            else if (b < a.bub.n_small4 + a.bub.n_small)
-                ll_acc += small_bubble<8, 8, RMIN>(a.bub, a.bub.sm_tbl, a.bub.n_small, b - a.bub.n_small4, b);
-        }
+    if (a.bub_on && DBG != 8 && DBG != 10 && DBG != 13 && !fin_wave) {   // this wave's bubbles, before its streams
+        if (small_wave && !early) small_bubbles();   // (small_wpb <= waves per block: bubbles_fused)
         // big bubbles, one wavefront each, from the last blocks' last waves
         // down (the finish wave's rank, nblk - 1, skipped), staged in LDS after w
         int r = (nblk - 1 - bid) + nblk * (wpb - 1 - w);
         r -= r > nblk - 1 ? 1 : 0;
         if (r < a.bub.n_big) {
+            stored = true;
             const int E = a.bub.big_lds_edges;
             char* stg = reinterpret_cast<char*>(lds) + a.bub.big_lds_off + w * big_stage_bytes(E);
             double* lw = reinterpret_cast<double*>(stg);
             int* lsd = reinterpret_cast<int*>(lw + E + 2 * kMaxBubbleNodes);
             for (int i = r; i < a.bub.n_big; i += nw - 1) ll_acc += big_bubble(a.bub, i, lsd, lw, lw, lw + E);
         }
+    }
+    WFSA_STAMP(2)
+    if (QN) {   // this wave's slot stores (and the finish wave's halt decision) retired: arrive
+        if (stored) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        unsigned prev = 0u;
+        if (lane == 0) prev = atomicAdd(&q_arrived, 1u);
+        prev = __shfl(prev, 0, kWave);
+        if (lane == 0 && prev == unsigned(wpb - 1))   // the block's last wave: one arrival for all its stores
+            __hip_atomic_fetch_add(a.qw.arrive + a.qw.parity, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        WFSA_STAMP(3)
+    }
+    if (early) {   // the table must be complete before the stream pass reads it
+        const unsigned nst = unsigned(wpb - stage_w0);
+        if (lane == 0)
+            while (__hip_atomic_load(&staged_waves, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < nst)
+                __builtin_amdgcn_s_sleep(1);
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
     }
     if (kStreams) load(B, D);
     double p = 0.0, acc0 = 0.0, acc1 = 0.0;
@@ -2447,6 +2797,28 @@ __global__ __launch_bounds__(1024, (DBG == 10 ? 8 : 1)) WFSA_FBS_ATTR void fbs_k
             if (c >= rows) break;
             uint4 v = r[d];
             if constexpr (DELTA) {
+                if (DBG == 9 || DBG == 1) {   // (timing variants: loads only / no table gathers)
+                    if (c == hdr) {
+                        flush();
+                        acc0 = 0.0;
+                        acc1 = 0.0;
+                        hdr += __builtin_amdgcn_readfirstlane(int(v.z & 0xffffu));
+                        ++grp;
+                    }
+                    if (DBG == 9) {
+                        acc0 += double(v.x ^ v.y ^ v.z ^ v.w);
+                    } else {
+                        const uint32_t d[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+                        for (int i = 0; i < kDeltaFields; ++i) {
+                            const uint32_t f = delta_field(d[i / 3], i % 3);
+                            asm("v_lshl_add_u32 %0, %1, 3, %2" : "=v"(cur) : "v"(f), "v"(cur));
+                            if (i & 1) acc1 += double(cur);
+                            else acc0 += double(cur);
+                        }
+                    }
+                    continue;
+                }
                 if (c == hdr) {   // uniform: the first row of the next group
                     flush();
                     acc0 = 0.0;
@@ -2526,6 +2898,7 @@ __global__ __launch_bounds__(1024, (DBG == 10 ? 8 : 1)) WFSA_FBS_ATTR void fbs_k
         }
     }
     flush();
+    WFSA_STAMP(4)
     // one log-likelihood partial per block (the QN finish sums them)
     __shared__ double wsum[1024 / kWave];
     ll_acc = wave_sum(ll_acc);
@@ -2539,6 +2912,16 @@ __global__ __launch_bounds__(1024, (DBG == 10 ? 8 : 1)) WFSA_FBS_ATTR void fbs_k
     // this block's slice of the per-edge weights and the zeroed result, for
     // the kernels after this one (nothing in this launch reads them)
     if (W_LDS && !a.no_streams && !a.no_slice) edge_weight_slice(a, bid, nblk);
+    // the QN waves, their stream share done: this step's QN update
+    if (QN && w == wpb - 2 && bid < a.qw.n_waves) {
+#ifdef WFSA_EXPERIMENTS
+        qn_wave_run(a.qw, bid, tr);
+#else
+        qn_wave_run(a.qw, bid, nullptr);
+#endif
+    }
+    WFSA_STAMP(7)
+#undef WFSA_STAMP
 }
 
 // Group headers (stream_hdr_words), written after the streams are emitted:
@@ -2576,9 +2959,8 @@ __global__ __launch_bounds__(256) void publish_kernel(const double* out, Publish
     }
     __threadfence_system();
     __syncthreads();
-    if (threadIdx.x == 0) {
-        const unsigned v = *pub.seq + 1u;
-        *pub.seq = v;
+    if (threadIdx.x == 0) {   // (the sequence counter is an agent-scope atomic everywhere: qn_publish_row)
+        const unsigned v = __hip_atomic_fetch_add(pub.seq, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u;
         __hip_atomic_store(pub.host_flag, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
     }
 }
@@ -2697,6 +3079,7 @@ hipError_t configure_kernels(int max_dynamic_lds) {
                          reinterpret_cast<const void*>(&fbs_kernel<true, true, true, 0, true>),
                          reinterpret_cast<const void*>(&fbs_kernel<false, true, false, 0, false, true>),
                          reinterpret_cast<const void*>(&fbs_kernel<false, true, false, 0, true, true>),
+                         reinterpret_cast<const void*>(&fbs_kernel<false, true, false, 0, false, true, true>),
 #ifdef WFSA_EXPERIMENTS
                          reinterpret_cast<const void*>(&fbs_kernel<false, true, false, 1>),
                          reinterpret_cast<const void*>(&fbs_kernel<false, true, false, 3>),
@@ -2707,6 +3090,15 @@ hipError_t configure_kernels(int max_dynamic_lds) {
                          reinterpret_cast<const void*>(&fbs_kernel<false, true, false, 8>),
                          reinterpret_cast<const void*>(&fbs_kernel<false, true, false, 9>),
                          reinterpret_cast<const void*>(&fbs_kernel<false, true, false, 10>),
+                         reinterpret_cast<const void*>(&fbs_kernel<false, true, false, 1, false, true>),
+                         reinterpret_cast<const void*>(&fbs_kernel<false, true, false, 3, false, true>),
+                         reinterpret_cast<const void*>(&fbs_kernel<false, true, false, 4, false, true>),
+                         reinterpret_cast<const void*>(&fbs_kernel<false, true, false, 5, false, true>),
+                         reinterpret_cast<const void*>(&fbs_kernel<false, true, false, 8, false, true>),
+                         reinterpret_cast<const void*>(&fbs_kernel<false, true, false, 9, false, true>),
+                         reinterpret_cast<const void*>(&fbs_kernel<false, true, false, 11, false, true>),
+                         reinterpret_cast<const void*>(&fbs_kernel<false, true, false, 12, false, true>),
+                         reinterpret_cast<const void*>(&fbs_kernel<false, true, false, 13, false, true>),
 #endif
                          reinterpret_cast<const void*>(&wide_kernel<false>)};
     for (const void* f : fns) {   // (static LDS counts against the same 160 KiB)
@@ -2919,15 +3311,45 @@ hipError_t launch_stream_headers(uint4* stream, const int64_t* g_base, const int
 
 static hipError_t launch_compiled_impl(const CompiledArgs& a, int grid, int block, size_t lds, hipStream_t stream);
 
+// one launch of a stream-kernel instance, with dispatch timestamps when
+// events are given (hipExtLaunchKernelGGL: the kernel itself, as rocprof
+// measures it)
+template <typename K>
+static hipError_t go(K k, int grid, int block, size_t lds, hipStream_t stream, hipEvent_t ev0, hipEvent_t ev1,
+                     const CompiledArgs& a) {
+    const dim3 g{unsigned(grid), 1, 1}, b{unsigned(block), 1, 1};
+    if (ev0 || ev1) hipExtLaunchKernelGGL(k, g, b, uint32_t(lds), stream, ev0, ev1, 0u, a);
+    else hipLaunchKernelGGL(k, g, b, lds, stream, a);
+    return hipGetLastError();
+}
+
 hipError_t launch_compiled(const CompiledArgs& a, int grid, int block, size_t lds, hipStream_t stream, hipEvent_t ev0,
                            hipEvent_t ev1) {
-    if (!a.with_grad && a.d_tab > 0 && (ev0 || ev1)) {   // the delta stream kernel with dispatch timestamps
-        const dim3 g{unsigned(grid), 1, 1}, b{unsigned(block), 1, 1};
+    if (ev0 || ev1) {   // no dispatch events inside a stream capture (the graph path records none)
+        hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+        if (hipStreamIsCapturing(stream, &cs) == hipSuccess && cs != hipStreamCaptureStatusNone) ev0 = ev1 = nullptr;
+    }
+    if (!a.with_grad && a.d_tab > 0) {   // the delta stream kernel: narrow words, no composites, w staged (the host checks)
+#ifdef WFSA_EXPERIMENTS
+        static const int dbg = experiment_knob("WFSA_FBS_DBG");
+        switch (dbg) {   // timing variants of the delta kernel (results wrong by design)
+        case 1: return go(fbs_kernel<false, true, false, 1, false, true>, grid, block, lds, stream, ev0, ev1, a);
+        case 3: return go(fbs_kernel<false, true, false, 3, false, true>, grid, block, lds, stream, ev0, ev1, a);
+        case 4: return go(fbs_kernel<false, true, false, 4, false, true>, grid, block, lds, stream, ev0, ev1, a);
+        case 5: return go(fbs_kernel<false, true, false, 5, false, true>, grid, block, lds, stream, ev0, ev1, a);
+        case 8: return go(fbs_kernel<false, true, false, 8, false, true>, grid, block, lds, stream, ev0, ev1, a);
+        case 9: return go(fbs_kernel<false, true, false, 9, false, true>, grid, block, lds, stream, ev0, ev1, a);
+        case 11: return go(fbs_kernel<false, true, false, 11, false, true>, grid, block, lds, stream, ev0, ev1, a);
+        case 12: return go(fbs_kernel<false, true, false, 12, false, true>, grid, block, lds, stream, ev0, ev1, a);
+        case 13: return go(fbs_kernel<false, true, false, 13, false, true>, grid, block, lds, stream, ev0, ev1, a);
+        default: break;
+        }
+#endif
+        if (a.qw.on)   // with this step's QN update (the host checks: no rmin, bubbles fused or none)
+            return go(fbs_kernel<false, true, false, 0, false, true, true>, grid, block, lds, stream, ev0, ev1, a);
         if (a.bub_on && a.bub.rmin_acc)
-            hipExtLaunchKernelGGL((fbs_kernel<false, true, false, 0, true, true>), g, b, uint32_t(lds), stream, ev0, ev1, 0u, a);
-        else
-            hipExtLaunchKernelGGL((fbs_kernel<false, true, false, 0, false, true>), g, b, uint32_t(lds), stream, ev0, ev1, 0u, a);
-        return hipGetLastError();
+            return go(fbs_kernel<false, true, false, 0, true, true>, grid, block, lds, stream, ev0, ev1, a);
+        return go(fbs_kernel<false, true, false, 0, false, true>, grid, block, lds, stream, ev0, ev1, a);
     }
     if (ev0) {
         const hipError_t e = hipEventRecord(ev0, stream);
@@ -2984,13 +3406,6 @@ static hipError_t launch_compiled_impl(const CompiledArgs& a, int grid, int bloc
             return hipGetLastError();
         }
 #endif
-        if (a.d_tab > 0) {   // delta stream: narrow words, no composites, w staged (the host checks)
-            if (a.bub_on && a.bub.rmin_acc)
-                hipLaunchKernelGGL((fbs_kernel<false, true, false, 0, true, true>), g, b, lds, stream, a);
-            else
-                hipLaunchKernelGGL((fbs_kernel<false, true, false, 0, false, true>), g, b, lds, stream, a);
-            return hipGetLastError();
-        }
         const int key = (a.tables >= 1 ? 4 : 0) + (a.wide ? 2 : 0) + (a.multi ? 1 : 0);
         if (a.bub_on && a.bub.rmin_acc) {   // the bubbles also feed the rmin column
             switch (key) {

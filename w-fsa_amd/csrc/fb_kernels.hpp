@@ -562,6 +562,8 @@ struct BubbleArgs {
     const double* ewp;       // [n_params + 1] exp(w), ewp[n_params] = 1 (per iteration)
     const unsigned* halted;
     int32_t dbg;             // timing experiments only (WFSA_BUB_DBG): 1 no slot stores, 2 no weight gathers
+    int32_t wt;              // contribution slots stored write-through (sc1): read in the same launch (QnWave)
+    int32_t prio;            // fused small bubbles at raised wave priority (s_setprio 2)
 };
 
 // Compiled streams of the per-iteration kernels.
@@ -576,6 +578,55 @@ struct BubbleArgs {
 //     (edge code, src | dst << 16) x edges] (edge_code above), 16-byte aligned
 //     (padded), so edge e of the bubble at word offset o owns contribution
 //     slot o / 2 + 2 + e.
+// The QN update inside the stream kernel (one rank, every string compiled,
+// delta stream, no rmin column): the bubble waves store their contribution
+// slots write-through (sc1), and each block, once all its waves' stores have
+// retired (the last wave of the block by an LDS counter), adds one arrival to
+// a per-launch counter (agent-scope atomic).  The QN waves -- wave wpb - 2 of
+// blocks [0, n_waves), charged by the dealer -- stream their (shorter) share
+// of rows, then poll the counter (sc1 loads) until every block has arrived,
+// read the slots with sc1 loads and run the QuasiNewton update of their
+// batches of constraints: a batch is a run of consecutive constraints with at
+// most 64 members, a lane per member, the per-constraint sums in member order
+// by lane shuffles (the host's order: bitwise the same update as
+// qn_step_kernel).  The finish wave of the same launch (the previous step's
+// info row and halt decision) arrives like the bubble waves, so the QN waves
+// read its halt_pending (stored sc1) after the same poll.  The updated weights
+// go to the other parity's buffers (w_next, ewp_next): the blocks of this
+// launch still read the current ones.  Launch e uses arrive[e & 1] and zeroes
+// arrive[(e + 1) & 1] for the next launch.  A poll that outlasts its limit
+// writes NaN partials (the step's row then reports non-finite) instead of
+// hanging.
+constexpr int kQnWaveMembers = 64;
+constexpr int kQnWaveChunkRounds = 4;   // a batch's slot chunks, one per lane per round: at most 256
+struct QnWave {
+    int32_t on;
+    int32_t n_batches;
+    int32_t n_waves;             // QN waves: wave wpb - 2 of blocks [0, n_waves)
+    int32_t parity;
+    int32_t n_arrive;            // arrivals to wait for (the grid's blocks)
+    const int4* batch;           // [n_batches][2] (first constraint, end constraint, first member, end member),
+                                 // (slot chunks, their first slot: low, high word, 0)
+    const int32_t* con_of;       // [n] constraint of each member (trimmed order)
+    const int32_t* mfirst;       // [n] the member's first chunk within its batch
+    const int32_t* mnch;         // [n] its chunk count
+    const int32_t* cptr;         // [k + 1]
+    const int32_t* full_of;      // [n]
+    const double* fixed_t;       // [n] constant trivial-word gradient, trimmed order
+    const double* contrib;
+    double* x;
+    double* lambda;
+    double* grad;
+    double* w_next;              // [n_full + 1] the next step's weights (the other parity)
+    double* ewp_next;
+    double* partial;             // [k][4] (g, g, lambda, graderr), read by the next finish
+    double eta;
+    int32_t exp_lambda;
+    unsigned* arrive;            // [2] per-parity arrival counters
+    unsigned* halted;            // [0] halted (earlier launches), [1] halt_pending (this launch's finish, sc1)
+    QnFinish fin;                // this step's publication (a skipped row after a halt)
+};
+
 struct CompiledArgs {
     ModelView m;
     const double* p;         // [S]
@@ -617,6 +668,11 @@ struct CompiledArgs {
     double* logq;            // [S] or null
     const unsigned* halted;  // device-resident QN run: nonzero = skip (or null)
     QnFinish fin;            // fin.active: block 0 finishes the previous QN step first
+    QnWave qw;               // qw.on: this step's QN update runs in this launch
+    unsigned long long* trace;   // timing experiments only (WFSA_FBS_TRACE): [waves][8] s_memrealtime stamps
+    int32_t early_bub;       // delta kernel: the small-bubble waves start at entry, the others stage the table
+    int32_t stream_nt;       // stream rows loaded non-temporal
+    int32_t defer_prefetch;  // delta kernel: the first row set issued after the wave's table / bubble loads
 };
 
 

@@ -118,14 +118,31 @@ __device__ void seg_sums(const double* __restrict__ v, const int* sp, const int*
     __syncthreads();
 }
 
+// Write-through (sc1) 8-byte stores and sc1 loads: the hand-off inside one
+// launch across CUs and XCDs (MI355X_MICROARCH.md, inter-workgroup
+// visibility: sc1 stores, every storing wave's vmcnt(0) before its arrival,
+// sc1 loads by the consumer after its poll has matched)
+__device__ __forceinline__ void store_wt(double* p, double v) {
+    __hip_atomic_store(reinterpret_cast<unsigned long long*>(p), (unsigned long long)(__double_as_longlong(v)),
+                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ double load_wt(const double* p) {
+    return __longlong_as_double((long long)(__hip_atomic_load(reinterpret_cast<unsigned long long*>(const_cast<double*>(p)),
+                                                              __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)));
+}
+__device__ __forceinline__ unsigned load_wt(const unsigned* p) {
+    return __hip_atomic_load(const_cast<unsigned*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 // the info row of a step into its host ring slot, then the flag; the
-// system-scope release orders the row before the flag
+// system-scope release orders the row before the flag.  The sequence counter
+// is an agent-scope atomic: two rows of one launch (a finish and a skipped
+// step) may be published from different CUs.
 __device__ inline void qn_publish_row(const QnFinish& f, const double* info, unsigned status) {
     double* row = f.host_ring + size_t(f.ring_slot) * kQnRow;
     for (int i = 0; i < 7; ++i) row[i] = info ? info[i] : 0.0;
     row[7] = double(status);
-    const unsigned v = *f.seq + 1u;
-    *f.seq = v;
+    const unsigned v = __hip_atomic_fetch_add(f.seq, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u;
     __hip_atomic_store(f.host_flag, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
@@ -216,7 +233,12 @@ __device__ inline void qn_finish_compute(const QnFinish& f, double* red, double*
             ge = fmax(ge, v[b].w);
         }
     }
-    double ll = f.ll_part ? strided_sum(f.ll_part, f.n_ll, t, nt) : 0.0;
+    // the log-likelihood partials in one order whichever form runs (the
+    // first wavefront's strided sums, then its shuffle tree): a run's last
+    // row (the one-block finish) and the others (the stream kernel's finish
+    // wave) sum the same way
+    double ll = (f.ll_part && t < 64) ? strided_sum(f.ll_part, f.n_ll, t, 64) : 0.0;
+    ll = wave_reduce(ll, 2);
     double rv = INFINITY, ri = -1.0;   // rmin column from block minima, ties to the lower string
     if (f.rmin_part)
         for (int j = t; j < f.rmin_n_part; j += nt) {
@@ -231,13 +253,11 @@ __device__ inline void qn_finish_compute(const QnFinish& f, double* red, double*
         gmax = wave_reduce(gmax, 1);
         lmin = wave_reduce(lmin, 0);
         ge = wave_reduce(ge, 1);
-        ll = wave_reduce(ll, 2);
     } else {
         gmin = block_reduce(gmin, 0, red);
         gmax = block_reduce(gmax, 1, red);
         lmin = block_reduce(lmin, 0, red);
         ge = block_reduce(ge, 1, red);
-        ll = block_reduce(ll, 2, red);
     }
     for (int o = 32; o > 0; o >>= 1) {
         const double v = __shfl_xor(rv, o, 64), i = __shfl_xor(ri, o, 64);
@@ -283,7 +303,9 @@ __device__ inline void qn_finish_compute(const QnFinish& f, double* red, double*
 }
 
 __device__ inline void qn_finish_publish(const QnFinish& f, const double* info, unsigned status) {
-    if (status != kQnRan) *f.halt_pending = status;   // read by the next QN launch only
+    // read by the next QN launch, or (write-through) by the QN waves of the
+    // stream kernel this finish runs in
+    if (status != kQnRan) __hip_atomic_store(f.halt_pending, status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     qn_publish_row(f, info, status);
 }
 

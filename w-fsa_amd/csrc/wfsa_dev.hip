@@ -357,6 +357,32 @@ struct wfsa_dev {
     double* ewp_cur = nullptr;
     double* qn_ring = nullptr;       // host-mapped [kQnDepth][kQnRow]
     double* qn_ring_dev = nullptr;
+    // the QN update inside the stream kernel (fb_kernels.hpp QnWave; one
+    // rank, every string compiled, delta stream, no rmin column;
+    // WFSA_QN_INKERNEL=0: the separate qn_step_kernel): QN waves reserved by
+    // the dealer (qw_waves, wave wpb - 2 of blocks [0, qw_waves)), batches of
+    // constraints built at QN set-up, per-parity arrival counters and the
+    // weights double-buffered by step parity (w_full2 / ewp2 above)
+    bool use_qw = true;
+    bool early_bub = true;           // WFSA_EARLY_BUB=0: every wave stages the table before any bubble
+    bool stream_nt = false;          // WFSA_STREAM_NT=1: the stream kernel's rows loaded non-temporal
+    bool defer_prefetch = false;     // WFSA_DEFER_PREFETCH=1: the first row set after the table / bubble loads
+    bool bub_prio = true;            // WFSA_BUB_PRIO=0: the fused small bubbles at normal wave priority
+    int32_t qw_waves = 0;            // reserved at preparation
+    double qw_cost = 8.0;            // the dealer's charge per QN wave, in stream rows (WFSA_QN_COST)
+    bool qw_ok = false;              // batches built for the current preparation and QN set-up
+    int32_t qw_nbatch = 0;
+    DevBuf<int4> qw_batch;
+    DevBuf<int32_t> qw_con_of, qw_mnch, qw_mfirst;
+    std::vector<int64_t> h_mchunk;   // [n_params] first contribution slot of each position's chunks (layout_slots)
+    std::vector<int32_t> h_mnch;     // [n_params] its chunk count
+    int64_t layout_gen = 0;          // layout_slots runs
+    int64_t qw_key = -1;             // (qn set-up, layout) the batches were built for
+    std::vector<int4> h_qw_batch;    // host copy of the batches (diagnostics)
+    DevBuf<unsigned> qw_arrive;      // [2], zero between launches (each launch zeroes the next one's)
+    uint64_t qw_seq = 0;             // in-kernel QN launches enqueued (their parity)
+    wfsa::QnWave qw_next{};          // picked up by the next stream kernel launch (qw_next.on)
+    DevBuf<unsigned long long> fbs_trace;   // timing experiments (WFSA_FBS_TRACE): per-wave stamps of the last launch
 
     // dense automata: the fp64 MFMA path (dense_path.hpp) replaces the
     // trellis kernels; WFSA_DENSE=0 never, =1 whenever the model qualifies
@@ -983,6 +1009,7 @@ int collect_timing(wfsa_dev* ctx) {
 // failed launch surfaces as an error.
 int wait_published(wfsa_dev* ctx, unsigned want) {
     auto reached = [&] { return int(__atomic_load_n(ctx->flag, __ATOMIC_ACQUIRE) - want) >= 0; };
+    const auto t0 = std::chrono::steady_clock::now();
     for (uint64_t spin = 1;; ++spin) {
         if (reached()) {   // (a failed peer all-reduce publishes NaN: say why instead)
             if (ctx->comm && ctx->comm->check())
@@ -996,6 +1023,11 @@ int wait_published(wfsa_dev* ctx, unsigned want) {
                 return fail(WFSA_ERR_HIP, "device finished without publishing (sequence %u)", want);
             }
             if (e != hipErrorNotReady) return fail(WFSA_ERR_HIP, "device failure: %s", hipGetErrorString(e));
+            // the communicator's liveness (an RCCL error or a stalled member
+            // aborts it; its pending kernels on this rank then end)
+            if (ctx->comm &&
+                ctx->comm->watchdog(std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count()))
+                return fail(WFSA_ERR_RCCL, "%s all-reduce: %s", ctx->comm->kind(), ctx->comm->last_error());
         }
         __builtin_ia32_pause();
     }
@@ -1176,6 +1208,18 @@ int layout_slots(wfsa_dev* ctx, const std::vector<int32_t>& pos_of) {
             ctx->lead_grp_nch = std::max(ctx->lead_grp_nch, gn[g]);
         ctx->stats.max_group_chunks = ctx->lead_grp_nch;
         ctx->stats.slot_chunks = ctx->n_bubbles > 0 ? int64_t(gbase.back()) / wfsa::kSlotChunk : 0;
+    }
+    {   // per position: the first contribution slot of its chunks and their count (the in-kernel QN update)
+        std::vector<int64_t> mchunk(size_t(std::max(np, 1)), 0);
+        std::vector<int32_t> mnch(size_t(std::max(np, 1)), 0);
+        for (int32_t q = 0; q < np; ++q) {
+            const int32_t g = grp_of[size_t(q)];
+            mchunk[size_t(q)] = gbase[size_t(g)] + int64_t(cptr_pos[size_t(q)] - cptr_pos[size_t(gp[size_t(g)])]) * wfsa::kSlotChunk;
+            mnch[size_t(q)] = cptr_pos[size_t(q) + 1] - cptr_pos[size_t(q)];
+        }
+        ctx->h_mchunk = std::move(mchunk);
+        ctx->h_mnch = std::move(mnch);
+        ++ctx->layout_gen;
     }
     HIP_TRY(ctx->chunk_ptr.upload(cptr_pos.data(), cptr_pos.size(), s));
     HIP_TRY(ctx->seg_ptr.upload(pc.data(), pc.size(), s));
@@ -1614,13 +1658,22 @@ int prepare(wfsa_dev* ctx, int level) {
         const int nblk = ctx->i_grid;
         const int small_wpb = small_waves_per_block(n_b - n_big_est, nblk);
         const int64_t small_waves = (n_b - n_big_est + kWave - 1) / kWave;
+        // the in-kernel QN update's waves (wave i_wpb - 2 of the first
+        // blocks; fb_kernels.hpp QnWave): about one per 48 parameters (a
+        // batch holds at most 64 members), each charged qw_cost rows so its
+        // stream share ends early
+        // (reserved whatever WFSA_QN_INKERNEL says: the layout, and so every
+        // fixed-order sum, is then the same with the update in or out)
+        ctx->qw_waves = (i_wpb >= 3 && delta_want && ctx->i_tables)
+                            ? int(std::min<int64_t>(nblk, (int64_t(ctx->n_params) + 47) / 48)) : 0;
         for (int w = 0; w < i_nw; ++w) {
             const int bid = w / i_wpb, wib = w % i_wpb;
             if (bid == 0 && wib == i_wpb - 1) {   // the QN finish's wave (fbs_kernel): no groups
                 load0[size_t(w)] = 1e300;
                 continue;
             }
-            if (wib < small_wpb && int64_t(bid) * small_wpb + wib < small_waves) load0[size_t(w)] += small_cost;
+            if (wib == i_wpb - 2 && bid < ctx->qw_waves) load0[size_t(w)] += ctx->qw_cost;
+            if (wib < small_wpb && int64_t(wib) * nblk + bid < small_waves) load0[size_t(w)] += small_cost;   // (fbs_kernel's chunk order)
             int64_t r = (nblk - 1 - bid) + int64_t(nblk) * (i_wpb - 1 - wib);
             r -= r > nblk - 1 ? 1 : 0;
             if (r < n_big_est) load0[size_t(w)] += big_cost;
@@ -1696,25 +1749,6 @@ int prepare(wfsa_dev* ctx, int level) {
     HIP_TRY(ctx->l_str.upload(l_str.data(), l_str.size(), s));
     HIP_TRY(ctx->l_len.upload(l_len.data(), l_len.size(), s));
     HIP_TRY(ctx->wave_first.upload(wave_first.data(), wave_first.size(), s));
-    {   // the group headers: p of each lane's string and the group's rows
-        std::vector<double> h_p(S > 0 ? size_t(S) : 1, 0.0), pl(std::max<size_t>(l_str.size(), 1), 0.0);
-        if (S > 0) HIP_TRY(ctx->p.download(h_p.data(), size_t(S), s));
-        HIP_TRY(hipStreamSynchronize(s));
-        for (size_t k = 0; k < l_str.size(); ++k)
-            if (l_str[k] >= 0) pl[k] = h_p[size_t(l_str[k])];
-        DevBuf<double> d_pl;
-        HIP_TRY(d_pl.upload(pl.data(), pl.size(), s));
-        HIP_TRY(wfsa::launch_stream_headers(ctx->stream_w.ptr, ctx->g_base.ptr, ctx->g_len.ptr, d_pl.ptr, G,
-                                            ctx->wide, s));
-        HIP_TRY(hipStreamSynchronize(s));
-        ctx->delta_on = false;
-        ctx->d_tab = 0;
-        if (delta_want && ctx->i_tables)
-            if (int rc = build_delta(ctx, comp, h_main, s_base, h_p, chunks, G, rows0, deal)) return rc;
-    }
-    ctx->n_groups = G;
-    ctx->n_compiled = nc;
-
     // bubbles: small ones into the structure-of-arrays tables, big ones kept
     // as records; every (bubble edge, parameter) pair gets a slot in the
     // parameter-major contribution array (layout_slots)
@@ -1796,6 +1830,49 @@ int prepare(wfsa_dev* ctx, int level) {
         ctx->h_sm_list.clear();
         ctx->h_big_list.clear();
     }
+    // the delta deal's bubble charges from the classified bubbles: a wave of
+    // class-B small bubbles (8 nodes / edges: about twice a class-A wave's
+    // time, profiles/r05) costs more stream rows than a class-A one
+    {
+        double small_cost = 18.0, small_cost_b = 36.0, big_cost = 8.0;
+        if (const char* e = std::getenv("WFSA_SMALL_COST")) small_cost = std::atof(e);
+        if (const char* e = std::getenv("WFSA_SMALL_COST_B")) small_cost_b = std::atof(e);
+        if (const char* e = std::getenv("WFSA_BIG_COST")) big_cost = std::atof(e);
+        const int nblk = ctx->i_grid;
+        const int64_t ns = int64_t(ctx->n_small4) + ctx->n_small;
+        const int small_wpb = small_waves_per_block(ns, nblk);
+        for (int w = 0; w < i_nw; ++w) {
+            const int bid = w / i_wpb, wib = w % i_wpb;
+            if (bid == 0 && wib == i_wpb - 1) continue;   // the finish wave (charged 1e300 above)
+            double c = 0.0;
+            if (wib == i_wpb - 2 && bid < ctx->qw_waves) c += ctx->qw_cost;
+            const int64_t b0 = (int64_t(wib) * nblk + bid) * kWave;   // fbs_kernel's chunk of this wave
+            if (wib < small_wpb && b0 < ns) c += (b0 + kWave > ctx->n_small4) ? small_cost_b : small_cost;
+            int64_t r = (nblk - 1 - bid) + int64_t(nblk) * (i_wpb - 1 - wib);
+            r -= r > nblk - 1 ? 1 : 0;
+            if (r < ctx->n_big) c += big_cost;
+            load0[size_t(w)] = c;
+        }
+    }
+    {   // the group headers: p of each lane's string and the group's rows
+        std::vector<double> h_p(S > 0 ? size_t(S) : 1, 0.0), pl(std::max<size_t>(l_str.size(), 1), 0.0);
+        if (S > 0) HIP_TRY(ctx->p.download(h_p.data(), size_t(S), s));
+        HIP_TRY(hipStreamSynchronize(s));
+        for (size_t k = 0; k < l_str.size(); ++k)
+            if (l_str[k] >= 0) pl[k] = h_p[size_t(l_str[k])];
+        DevBuf<double> d_pl;
+        HIP_TRY(d_pl.upload(pl.data(), pl.size(), s));
+        HIP_TRY(wfsa::launch_stream_headers(ctx->stream_w.ptr, ctx->g_base.ptr, ctx->g_len.ptr, d_pl.ptr, G,
+                                            ctx->wide, s));
+        HIP_TRY(hipStreamSynchronize(s));
+        ctx->delta_on = false;
+        ctx->d_tab = 0;
+        if (delta_want && ctx->i_tables)
+            if (int rc = build_delta(ctx, comp, h_main, s_base, h_p, chunks, G, rows0, deal)) return rc;
+    }
+    ctx->n_groups = G;
+    ctx->n_compiled = nc;
+
     {   // slot layout: the QN loop's trimmed order when it is set up, else the identity
         std::vector<int32_t> order = ctx->slot_order;
         if (order.size() != size_t(ctx->n_params)) {
@@ -1980,6 +2057,8 @@ int enqueue_compiled(wfsa_dev* ctx, bool with_grad, bool want_logq, const unsign
         c.erec_out = ctx->erec.ptr;
         c.out = ctx->out.ptr;
         c.no_slice = (!with_grad && ctx->eval_no_slice) ? 1 : 0;
+        c.stream_nt = ctx->stream_nt ? 1 : 0;
+        c.defer_prefetch = ctx->defer_prefetch ? 1 : 0;
         c.ll_part = ctx->ll_cur;
         c.logq = want_logq ? ctx->logq.ptr : nullptr;
         c.halted = halted;
@@ -1995,12 +2074,27 @@ int enqueue_compiled(wfsa_dev* ctx, bool with_grad, bool want_logq, const unsign
                 ctx->rm_sv_used = true;
             }
             c.bub_on = 1;
+            c.bub.prio = ctx->bub_prio ? 1 : 0;
+            c.early_bub = ctx->early_bub ? 1 : 0;
             c.bub.small_wpb = small_waves_per_block(ctx->n_small4 + ctx->n_small, ctx->i_grid);
             if (ctx->n_big > 0) {
                 c.bub.big_lds_edges = ctx->big_lds_edges;
                 c.bub.big_lds_off = int32_t(big_stage_off(ctx));
                 lds = big_stage_off(ctx) + size_t(ctx->i_block / kWave) * size_t(wfsa::big_stage_bytes(ctx->big_lds_edges));
             }
+        }
+#ifdef WFSA_EXPERIMENTS
+        if (!with_grad && std::getenv("WFSA_FBS_TRACE")) {   // per-wave stamps (fb_kernels.hip WFSA_STAMP)
+            const size_t nw = size_t(ctx->i_grid) * size_t(ctx->i_block / kWave) * 16;
+            HIP_TRY(ctx->fbs_trace.alloc(nw));
+            HIP_TRY(hipMemsetAsync(ctx->fbs_trace.ptr, 0, nw * sizeof(unsigned long long), ctx->stream));
+            c.trace = ctx->fbs_trace.ptr;
+        }
+#endif
+        if (!with_grad && ctx->qw_next.on) {   // this step's QN update rides in this launch
+            c.qw = ctx->qw_next;
+            ctx->qw_next.on = 0;
+            c.bub.wt = 1;   // the QN waves read the slots in this launch
         }
         if (with_grad && tables == 0)   // the blocks accumulate into their slabs
             HIP_TRY(hipMemsetAsync(ctx->gpart.ptr, 0, size_t(ctx->c_grid) * size_t(np) * sizeof(double), s));
@@ -2135,11 +2229,16 @@ int enqueue_evaluation(wfsa_dev* ctx, bool want_logq, const unsigned* halted, in
     // kernels and the reduction: the fused QN step over compiled strings
     // alone reads neither, so the stream kernel skips writing them
     ctx->eval_no_slice = !with_tail && ctx->n_fall[0] + ctx->n_fall[1] + ctx->n_fall[2] == 0;
+    // the QN update in the stream kernel reads the bubble slots: a separate
+    // bubble kernel then runs before it (its slots visible at the boundary)
+    const bool bub_first = ctx->qw_next.on && ctx->n_bubbles > 0 && !side && !fusedb;
+    if (bub_first)
+        if (int rc = enqueue_bubbles(ctx, want_logq, halted, wave_off, s)) return rc;
     const int crc = enqueue_compiled(ctx, false, want_logq, halted, slot);
     ctx->eval_no_slice = false;
     if (crc) return crc;
     if (side) HIP_TRY(hipStreamWaitEvent(s, ctx->join, 0));
-    if (ctx->n_bubbles > 0 && !side && !fusedb) {
+    if (ctx->n_bubbles > 0 && !side && !fusedb && !bub_first) {
         if (int rc = enqueue_bubbles(ctx, want_logq, halted, wave_off, s)) return rc;
     }
     if (ctx->n_bubbles > 0 && !fusedb) wave_off += ctx->b_waves;
@@ -2190,7 +2289,7 @@ int enqueue_evaluation(wfsa_dev* ctx, bool want_logq, const unsigned* halted, in
     }
     if (n_ll) *n_ll = wave_off;
     if (!with_tail) {
-        const bool after_kc = side || (ctx->n_bubbles > 0 && !fusedb) || ctx->n_fall[0] || ctx->n_fall[1] ||
+        const bool after_kc = side || (ctx->n_bubbles > 0 && !fusedb && !bub_first) || ctx->n_fall[0] || ctx->n_fall[1] ||
                               ctx->n_fall[2] || w2_covers_01;
         if (!after_kc && slot >= 0) ctx->k2_kc[slot] = true;
         else HIP_TRY(record(ctx, ctx->k2, slot, s));
@@ -2354,7 +2453,82 @@ int enqueue_iteration(wfsa_dev* ctx, bool want_logq) {
 // kernel's last block publishes the step's info row (ring slot e % depth).
 int flush_qn_finish(wfsa_dev* ctx);
 
-int enqueue_qn_step(wfsa_dev* ctx, double eta, double tol, int64_t e, bool timed) {
+// The in-kernel QN update's batches (fb_kernels.hpp QnWave): runs of
+// consecutive constraints of at most kQnWaveMembers members and
+// 64 * kQnWaveChunkRounds slot chunks (their chunks are consecutive in the
+// contribution array: constraint c's group follows c - 1's).  qw_ok = false
+// when a constraint alone exceeds either, or has no member.
+int build_qw_batches(wfsa_dev* ctx) {
+    const int64_t key = ctx->qn_setup_gen * 1000003 + ctx->layout_gen;
+    if (ctx->qw_key == key) return WFSA_OK;
+    ctx->qw_key = key;
+    ctx->qw_ok = false;
+    ctx->qw_nbatch = 0;
+    const int32_t n = ctx->qn_n, k = ctx->qn_k;
+    const std::vector<int32_t>& cptr = ctx->h_cptr;
+    const int32_t cap = kWave * wfsa::kQnWaveChunkRounds;
+    if (!ctx->qn_fused || k <= 0 || n <= 0 || int64_t(cptr.size()) != int64_t(k) + 1 ||
+        int64_t(ctx->h_mchunk.size()) < n || ctx->slot_order.size() != size_t(ctx->n_params))
+        return WFSA_OK;
+    auto chunks = [&](int32_t c0, int32_t c1) {   // slot chunks of constraints [c0, c1)
+        int64_t t = 0;
+        for (int32_t i = cptr[size_t(c0)]; i < cptr[size_t(c1)]; ++i) t += ctx->h_mnch[size_t(i)];
+        return t;
+    };
+    for (int32_t c = 0; c < k; ++c) {
+        const int32_t nm = cptr[size_t(c) + 1] - cptr[size_t(c)];
+        if (nm < 1 || nm > wfsa::kQnWaveMembers || chunks(c, c + 1) > cap) return WFSA_OK;
+    }
+    std::vector<int4> batch;
+    std::vector<int32_t> con_of(size_t(n), 0), mfirst(size_t(n), 0);
+    for (int32_t c0 = 0; c0 < k;) {
+        int32_t c1 = c0 + 1;
+        int64_t nch = chunks(c0, c1);
+        while (c1 < k && cptr[size_t(c1) + 1] - cptr[size_t(c0)] <= wfsa::kQnWaveMembers) {
+            const int64_t more = chunks(c1, c1 + 1);
+            if (nch + more > cap) break;
+            nch += more;
+            ++c1;
+        }
+        const int32_t m0 = cptr[size_t(c0)], m1 = cptr[size_t(c1)];
+        const int64_t base = ctx->h_mchunk[size_t(m0)];
+        int64_t q = 0;
+        for (int32_t c = c0; c < c1; ++c)
+            for (int32_t i = cptr[size_t(c)]; i < cptr[size_t(c) + 1]; ++i) {
+                if (ctx->h_mnch[size_t(i)] > 0 && ctx->h_mchunk[size_t(i)] != base + q * wfsa::kSlotChunk)
+                    return WFSA_OK;   // (never: the layout keeps a batch's chunks consecutive)
+                con_of[size_t(i)] = c;
+                mfirst[size_t(i)] = int32_t(q);
+                q += ctx->h_mnch[size_t(i)];
+            }
+        batch.push_back(make_int4(c0, c1, m0, m1));
+        batch.push_back(make_int4(int32_t(nch), int32_t(uint32_t(uint64_t(base))), int32_t(uint64_t(base) >> 32), 0));
+        c0 = c1;
+    }
+    hipStream_t s = ctx->stream;
+    HIP_TRY(ctx->qw_batch.upload(batch.data(), batch.size(), s));
+    HIP_TRY(ctx->qw_con_of.upload(con_of.data(), con_of.size(), s));
+    HIP_TRY(ctx->qw_mfirst.upload(mfirst.data(), mfirst.size(), s));
+    HIP_TRY(ctx->qw_mnch.upload(ctx->h_mnch.data(), size_t(n), s));
+    HIP_TRY(hipStreamSynchronize(s));
+    ctx->qw_nbatch = int32_t(batch.size() / 2);
+    ctx->h_qw_batch = batch;
+    ctx->qw_ok = true;
+    return WFSA_OK;
+}
+
+// The QN update rides in the stream kernel (fb_kernels.hpp QnWave) when the
+// step is exactly: one rank, every string compiled into the delta stream, no
+// rmin column, every constraint of 1..64 members (bubbles not fused into the
+// stream kernel run in their own kernel before it)
+bool qw_usable(wfsa_dev* ctx) {
+    return ctx->use_qw && ctx->qw_ok && ctx->qw_waves > 0 && ctx->qn_fused && !ctx->comm && !ctx->dense &&
+           !ctx->mpath && !ctx->qn_rmin && ctx->n_groups > 0 && ctx->delta_on && ctx->i_tables >= 1 &&
+           ctx->n_fall[0] + ctx->n_fall[1] + ctx->n_fall[2] == 0 && ctx->fixed_t_on && ctx->qn_k > 0 &&
+           !ctx->side_stream && ctx->i_block / kWave >= 3;
+}
+
+int enqueue_qn_step(wfsa_dev* ctx, double eta, double tol, int64_t e, bool timed, bool inkern) {
     hipStream_t s = ctx->stream;
     const int32_t np = ctx->n_params;
     const int par = int(e & 1);
@@ -2378,11 +2552,6 @@ int enqueue_qn_step(wfsa_dev* ctx, double eta, double tol, int64_t e, bool timed
             return rc;
         }
     }
-    ctx->rm_eval = fuse_rmin;
-    const int erc = enqueue_evaluation(ctx, false, ctx->qn_halted.ptr, timed ? slot : -1, !fused && trellis, &n_ll);
-    ctx->rm_eval = false;
-    if (erc) return erc;
-    if (ctx->comm) COMM_TRY(ctx, ctx->out.ptr, size_t(np) + 1, wfsa::RedOp::SumF64, s);
     wfsa::QnArgs q{};
     wfsa::QnFinish& f = q.fin;
     q.out = ctx->out.ptr;
@@ -2397,7 +2566,6 @@ int enqueue_qn_step(wfsa_dev* ctx, double eta, double tol, int64_t e, bool timed
         q.seg_ptr = ctx->seg_ptr.ptr;
         q.chunk_ptr = ctx->chunk_ptr.ptr;
         f.ll_part = ctx->ll_cur;
-        f.n_ll = n_ll;
     } else if (trellis && ctx->comm && ctx->n_groups > 0) {
         q.fixed = ctx->fixed_grad.ptr;   // all-reduced once at preparation
     }
@@ -2436,6 +2604,44 @@ int enqueue_qn_step(wfsa_dev* ctx, double eta, double tol, int64_t e, bool timed
     f.seq = ctx->counters.ptr;
     f.host_flag = ctx->flag_dev;
     f.host_ring = ctx->qn_ring_dev;
+    if (inkern) {   // the update in the stream kernel: step e reads the weights of parity e, writes parity e + 1
+        ctx->w_cur = par ? ctx->w_full2.ptr : ctx->w_full.ptr;
+        ctx->ewp_cur = par ? ctx->ewp2.ptr : ctx->ewp.ptr;
+        wfsa::QnWave& w = ctx->qw_next;
+        w = wfsa::QnWave{};
+        w.on = 1;
+        w.n_batches = ctx->qw_nbatch;
+        w.n_waves = ctx->qw_waves;
+        w.parity = int32_t(ctx->qw_seq & 1u);
+        w.n_arrive = ctx->i_grid;
+        w.batch = ctx->qw_batch.ptr;
+        w.con_of = ctx->qw_con_of.ptr;
+        w.mfirst = ctx->qw_mfirst.ptr;
+        w.mnch = ctx->qw_mnch.ptr;
+        w.cptr = ctx->qn_cptr.ptr;
+        w.full_of = ctx->qn_full_of.ptr;
+        w.fixed_t = ctx->fixed_t.ptr;
+        w.contrib = ctx->n_bubbles > 0 ? ctx->contrib.ptr : nullptr;
+        w.x = ctx->qn_x.ptr;
+        w.lambda = ctx->qn_lambda.ptr;
+        w.grad = ctx->qn_grad.ptr;
+        w.w_next = par ? ctx->w_full.ptr : ctx->w_full2.ptr;
+        w.ewp_next = par ? ctx->ewp.ptr : ctx->ewp2.ptr;
+        w.partial = ctx->qn_partial.ptr;
+        w.eta = eta;
+        w.exp_lambda = ctx->qn_exp_lambda;
+        w.arrive = ctx->qw_arrive.ptr;
+        w.halted = ctx->qn_halted.ptr;
+        w.fin = f;
+        ++ctx->qw_seq;
+    }
+    ctx->rm_eval = fuse_rmin;
+    const int erc = enqueue_evaluation(ctx, false, ctx->qn_halted.ptr, timed ? slot : -1, !fused && trellis, &n_ll);
+    ctx->rm_eval = false;
+    if (erc) return erc;
+    if (ctx->qw_next.on) return fail(WFSA_ERR_HIP, "the in-kernel QN update was not launched");
+    if (fused) f.n_ll = n_ll;
+    if (ctx->comm) COMM_TRY(ctx, ctx->out.ptr, size_t(np) + 1, wfsa::RedOp::SumF64, s);
     if (ctx->qn_rmin) {
         static const bool fold_rmin = [] {   // WFSA_RMIN_FOLD=0: the strings pass as its own launch
             const char* e = std::getenv("WFSA_RMIN_FOLD");
@@ -2453,7 +2659,7 @@ int enqueue_qn_step(wfsa_dev* ctx, double eta, double tol, int64_t e, bool timed
             return rc;
         }
     }
-    HIP_TRY(wfsa::launch_qn_step(q, fused, s));
+    if (!inkern) HIP_TRY(wfsa::launch_qn_step(q, fused, s));
     // the finish reads the step's log-likelihood partials: it can ride in the
     // next step's stream kernel when those are not in `out` (which that
     // kernel zeroes); else it is launched when the next step is enqueued
@@ -2726,6 +2932,12 @@ int wfsa_dev_create(int device, wfsa_dev** out) {
     if (const char* e = std::getenv("WFSA_WIDE2")) ctx->use_wide2 = e[0] != '0';
     if (const char* e = std::getenv("WFSA_PULL")) ctx->use_pull = e[0] != '0';
     if (const char* e = std::getenv("WFSA_WIDE2_TIERS")) ctx->w2_all = std::strcmp(e, "2") != 0;
+    if (const char* e = std::getenv("WFSA_QN_INKERNEL")) ctx->use_qw = e[0] != '0';
+    if (const char* e = std::getenv("WFSA_EARLY_BUB")) ctx->early_bub = e[0] != '0';
+    if (const char* e = std::getenv("WFSA_STREAM_NT")) ctx->stream_nt = e[0] == '1';
+    if (const char* e = std::getenv("WFSA_DEFER_PREFETCH")) ctx->defer_prefetch = e[0] == '1';
+    if (const char* e = std::getenv("WFSA_BUB_PRIO")) ctx->bub_prio = e[0] != '0';
+    if (const char* e = std::getenv("WFSA_QN_COST")) ctx->qw_cost = std::atof(e);
 
     HIP_TRY(hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking));
     if (const char* e = std::getenv("WFSA_PIPE")) ctx->use_pipe = e[0] == '1';
@@ -2753,6 +2965,8 @@ int wfsa_dev_create(int device, wfsa_dev** out) {
     *ctx->flag = 0;
     HIP_TRY(ctx->counters.alloc(1));
     HIP_TRY(hipMemsetAsync(ctx->counters.ptr, 0, sizeof(unsigned), ctx->stream));
+    HIP_TRY(ctx->qw_arrive.alloc(2));
+    HIP_TRY(hipMemsetAsync(ctx->qw_arrive.ptr, 0, 2 * sizeof(unsigned), ctx->stream));
     HIP_TRY(hipStreamSynchronize(ctx->stream));
     *out = ctx.release();
     return WFSA_OK;
@@ -3235,6 +3449,7 @@ static int qn_setup_impl(wfsa_dev* ctx, const wfsa_qn_desc* d) {
         if (ctx->prep_level >= 2 && !ctx->dense && !ctx->mpath)
             if (int rc = layout_slots(ctx, pos_of)) return rc;
     }
+    ctx->qw_ok = false;   // (its batches are built at the next run: build_qw_batches)
     ctx->h_cptr = cptr;
     ctx->qn_setup_gen++;
     ctx->qn_flags_clear = false;
@@ -3342,7 +3557,18 @@ static int qn_run_impl(wfsa_dev* ctx, double eta, double tol, int32_t max_steps,
         ctx->fixed_t_on = false;
     }
     const bool piped = pipe_ok(ctx);
-    if (piped) {   // the second weight buffer; the pipe stream starts after everything enqueued so far
+    if (!piped && ctx->use_qw && ctx->qw_waves > 0)
+        if (int rc = build_qw_batches(ctx)) return rc;
+    const bool inkern = !piped && qw_usable(ctx);
+    if (!inkern && !piped && ctx->use_qw && std::getenv("WFSA_VERBOSE"))
+        std::fprintf(stderr, "[wfsa] QN update as its own kernel: batches %d waves %d fused %d comm %d rmin %d delta %d "
+                     "fallback %d bubbles fused %d fixed_t %d k %d\n", int(ctx->qw_ok), ctx->qw_waves, int(ctx->qn_fused),
+                     int(ctx->comm != nullptr), int(ctx->qn_rmin), int(ctx->delta_on),
+                     ctx->n_fall[0] + ctx->n_fall[1] + ctx->n_fall[2],
+                     int(ctx->n_bubbles == 0 || bubbles_fused(ctx, false)), int(ctx->fixed_t_on), ctx->qn_k);
+    ctx->stats.qn_inkernel_waves = inkern ? ctx->qw_waves : 0;
+    ctx->stats.qn_batches = inkern ? ctx->qw_nbatch : 0;
+    if (piped || inkern) {   // the second weight buffer; the pipe stream starts after everything enqueued so far
         HIP_TRY(ctx->w_full2.alloc(size_t(ctx->n_params) + 2));
         HIP_TRY(ctx->ewp2.alloc(size_t(ctx->n_params) + 2));
         // its entries the QN steps never write (the trimmed-away parameters'
@@ -3358,7 +3584,7 @@ static int qn_run_impl(wfsa_dev* ctx, double eta, double tol, int32_t max_steps,
             ctx->pipe_init_w = ctx->w_full2.ptr;
             ctx->pipe_init_e = ctx->ewp2.ptr;
         }
-        HIP_TRY(hipEventRecord(ctx->p_start, s));
+        if (piped) HIP_TRY(hipEventRecord(ctx->p_start, s));
     }
     // steps whose kernels are timed: every stride-th (not the first), or the
     // last of a run shorter than the stride
@@ -3377,7 +3603,7 @@ static int qn_run_impl(wfsa_dev* ctx, double eta, double tol, int32_t max_steps,
         // after a halt fewer no-op steps remain queued (their library GEMMs do not skip)
         while (!stop && enq < max_steps && enq - done < (ctx->dense ? 2 : kQnDepth)) {
             const bool tm = timed_step(enq);
-            if (int rc = piped ? enqueue_qn_step_piped(ctx, eta, tol, enq, tm) : enqueue_qn_step(ctx, eta, tol, enq, tm))
+            if (int rc = piped ? enqueue_qn_step_piped(ctx, eta, tol, enq, tm) : enqueue_qn_step(ctx, eta, tol, enq, tm, inkern))
                 return rc;
             ++enq;
             ++ctx->seq;
@@ -3409,6 +3635,7 @@ static int qn_run_impl(wfsa_dev* ctx, double eta, double tol, int32_t max_steps,
             }
         }
         if (rs == wfsa::kQnSkipped) return fail(WFSA_ERR_HIP, "QN step %d skipped before a halt", done);
+        if (rs > wfsa::kQnSkipped) return fail(WFSA_ERR_HIP, "QN step %d: malformed info row (status %u)", done, rs);
         if (info_rows)
             for (int i = 0; i < 7; ++i) info_rows[size_t(done) * 7 + size_t(i)] = row[i];
         ++done;
@@ -3422,11 +3649,11 @@ static int qn_run_impl(wfsa_dev* ctx, double eta, double tol, int32_t max_steps,
     if (int rc = flush_qn_finish(ctx)) return rc;
     if (enq > done)
         if (int rc = wait_published(ctx, base + unsigned(enq))) return rc;
-    if (piped) {   // the weights of the final x back in the parity-0 buffers, after both streams' work:
+    if (piped || inkern) {   // the weights of the final x back in the parity-0 buffers, after both streams' work:
         // the main stream waits on the device for the pipe stream's last
         // finish (two blocking synchronizes here cost a host wake-up each),
         // and the poll below then covers both
-        HIP_TRY(hipStreamWaitEvent(s, ctx->pf[(enq + kQnDepth - 1) % kQnDepth], 0));
+        if (piped) HIP_TRY(hipStreamWaitEvent(s, ctx->pf[(enq + kQnDepth - 1) % kQnDepth], 0));
         ctx->w_cur = ctx->ewp_cur = nullptr;
         // step e writes the weights of parity e + 1: after an even number of
         // steps, none skipped by a halt, they are in the parity-0 buffers already
@@ -3443,6 +3670,88 @@ static int qn_run_impl(wfsa_dev* ctx, double eta, double tol, int32_t max_steps,
         if (e != hipSuccess && e != hipErrorNotReady)
             return fail(WFSA_ERR_HIP, "device failure: %s", hipGetErrorString(e));
     }
+#ifdef WFSA_EXPERIMENTS
+    if (std::getenv("WFSA_FBS_TRACE") && ctx->fbs_trace.ptr) {   // the last launch's per-wave stamps
+        const int wpb = ctx->i_block / kWave, nw = ctx->i_grid * wpb;
+        std::vector<unsigned long long> t(size_t(nw) * 16);
+        HIP_TRY(hipStreamSynchronize(s));
+        HIP_TRY(ctx->fbs_trace.download(t.data(), t.size(), s));
+        HIP_TRY(hipStreamSynchronize(s));
+        unsigned long long t0 = ~0ull;
+        for (int w = 0; w < nw; ++w)
+            if (t[size_t(w) * 16]) t0 = std::min(t0, t[size_t(w) * 16]);
+        const int small_wpb = small_waves_per_block(ctx->n_small4 + ctx->n_small, ctx->i_grid);
+        const char* names[8] = {"entry", "staged", "bubbles", "arrived", "stream", "qn-poll", "qn-done", "exit"};
+        for (int grp = 0; grp < 3; ++grp) {
+            for (int k = 0; k < 8; ++k) {
+                std::vector<double> v;
+                for (int w = 0; w < nw; ++w) {
+                    const int wib = w % wpb, bid = w / wpb;
+                    const bool qn = wib == wpb - 2 && bid < ctx->qw_waves, sb = wib < small_wpb;
+                    if ((grp == 1 && !sb) || (grp == 2 && !qn)) continue;
+                    const unsigned long long x = t[size_t(w) * 16 + size_t(k)];
+                    if (x) v.push_back(double(x - t0) / 100.0);   // 100 MHz -> us
+                }
+                if (v.empty()) continue;
+                std::sort(v.begin(), v.end());
+                auto q = [&](double f) { return v[std::min(v.size() - 1, size_t(f * double(v.size())))]; };
+                std::fprintf(stderr, "[fbs-trace] %-12s %-8s n %5zu  min %6.2f p10 %6.2f p50 %6.2f p90 %6.2f max %6.2f us\n",
+                             grp == 0 ? "all waves" : grp == 1 ? "small-bubble" : "qn waves", names[k], v.size(), v[0],
+                             q(0.1), q(0.5), q(0.9), v.back());
+            }
+        }
+        // small-bubble phases (stamps 8..11: quads loaded, weights gathered,
+        // forward done, backward done), by class (A: chunk below n_small4)
+        for (int cls = 0; cls < 2; ++cls) {
+            std::vector<double> ph[4];
+            for (int w = 0; w < nw; ++w) {
+                const int wib = w % wpb, bid = w / wpb;
+                if (wib >= small_wpb) continue;
+                const int64_t b0 = (int64_t(wib) * ctx->i_grid + bid) * kWave;
+                if (b0 >= ctx->n_small4 + ctx->n_small || (b0 < ctx->n_small4) != (cls == 0)) continue;
+                const unsigned long long* r = &t[size_t(w) * 16];
+                const unsigned long long st = r[1] ? r[1] : r[0];
+                const unsigned long long pts[5] = {st, r[8], r[9], r[10], r[11]};
+                for (int k = 0; k < 4; ++k)
+                    if (pts[k] && pts[k + 1]) ph[k].push_back(double(pts[k + 1] - pts[k]) / 100.0);
+            }
+            const char* pn[4] = {"quads", "gathers", "forward", "backward"};
+            std::fprintf(stderr, "[fbs-trace] class %c small-bubble phases (p50 / p90 / max us):", cls ? 'B' : 'A');
+            for (int k = 0; k < 4; ++k) {
+                if (ph[k].empty()) continue;
+                std::sort(ph[k].begin(), ph[k].end());
+                std::fprintf(stderr, " %s %.2f / %.2f / %.2f;", pn[k], ph[k][ph[k].size() / 2], ph[k][ph[k].size() * 9 / 10],
+                             ph[k].back());
+            }
+            std::fprintf(stderr, "\n");
+        }
+        // the slowest bubble waves and QN waves
+        auto dt = [&](int w, int a, int b) {
+            const unsigned long long x = t[size_t(w) * 16 + size_t(a)], y = t[size_t(w) * 16 + size_t(b)];
+            return x && y ? double(y - x) / 100.0 : -1.0;
+        };
+        std::vector<std::pair<double, int>> bw, qw;
+        for (int w = 0; w < nw; ++w) {
+            bw.push_back({dt(w, 1, 2), w});
+            if (w % wpb == wpb - 2 && w / wpb < ctx->qw_waves) qw.push_back({dt(w, 5, 6), w});
+        }
+        std::sort(bw.rbegin(), bw.rend());
+        std::sort(qw.rbegin(), qw.rend());
+        std::fprintf(stderr, "[fbs-trace] small %d/%d big %d, small waves per block %d; slowest bubble phases:", ctx->n_small4,
+                     ctx->n_small, ctx->n_big, small_wpb);
+        for (size_t i = 0; i < std::min<size_t>(8, bw.size()); ++i)
+            std::fprintf(stderr, " (b%d w%d %.2f)", bw[i].second / wpb, bw[i].second % wpb, bw[i].first);
+        std::fprintf(stderr, "\n[fbs-trace] slowest QN waves (batch: constraints members chunks):");
+        for (size_t i = 0; i < std::min<size_t>(8, qw.size()); ++i) {
+            const int b = qw[i].second / wpb;
+            if (size_t(2 * b + 1) < ctx->h_qw_batch.size()) {
+                const int4 x = ctx->h_qw_batch[size_t(2 * b)], y = ctx->h_qw_batch[size_t(2 * b + 1)];
+                std::fprintf(stderr, " (%.2f us: %d %d %d)", qw[i].first, x.y - x.x, x.w - x.z, y.x);
+            }
+        }
+        std::fprintf(stderr, "\n");
+    }
+#endif
     if (trace) {
         tr_end = clk::now();
         std::fprintf(stderr, "[wfsa] qn_run %d steps: prologue %.1f us, first step enqueued %.1f, first row %.1f, "

@@ -48,7 +48,7 @@ class DevStats(C.Structure):
         ("wave_strings", i32), ("wave_row_entries", i64), ("wave_pair_edges", i64),
         ("comm_ranks", i32), ("comm_peer", i32),
         ("slot_chunks", i64), ("max_group_chunks", i32), ("wave_pull", i32),
-        ("dense_blas", i32),
+        ("dense_blas", i32), ("qn_inkernel_waves", i32), ("qn_batches", i32),
     ]
 
 
