@@ -211,7 +211,8 @@ int wfsa_dev_objective_grad_end(wfsa_dev* ctx, double* loglik, double* grad_full
  * before a model is loaded; valid until the next load).  A caller may write
  * the weights there itself and pass w_full = NULL to _begin: one copy of
  * the weights fewer per evaluation (the host QN binding does).  Not while an
- * evaluation is in flight. */
+ * evaluation is in flight.  _begin accepts w_full = NULL only when this was
+ * called since the previous _begin (else WFSA_ERR_ARG). */
 double* wfsa_dev_weights_staging(wfsa_dev* ctx);
 
 /* Device-resident QuasiNewton: QuasiNewtonLearner::OptimizationStep

@@ -126,15 +126,20 @@ int wfsa_shard_range(const int64_t* off, int64_t n, int nranks, int rank, int64_
  * Fails (WFSA_ERR_MODEL) e.g. on epsilon cycles. */
 int wfsa_trellis_compile_stats(const wfsa_model_desc* model, int64_t out[4]);
 
-/* The HessianLearner's sparse LDL^T (SparseLdlt.hpp) on a symmetric matrix
- * given as upper-triangle coordinates (i[t] <= j[t], duplicates add): the
- * order (0 identity, 1 minimum degree), factor, and -- when b is given --
- * x = A^-1 b.  out_i = {positive pivots, negative pivots, nnz(L), ordering
- * within its work bound}; out_d = {log|det|, det sign, min pivot ratio}.
- * WFSA_ERR_ARG on a zero or non-finite pivot (no pivoting: the learner falls
- * back to the dense factorisation then). */
+/* The HessianLearner's sparse LDL^T (SparseLdlt.hpp; MKL DSS's role,
+ * src/HessianLearner.cpp:28-57,100-113) on a symmetric matrix given as
+ * upper-triangle coordinates (i[t] <= j[t], duplicates add): the order (0
+ * identity -- MKL_DSS_MY_ORDER --, 1 exact minimum degree, 2 approximate
+ * minimum degree -- init flag 16, the reference's METIS), the multifrontal
+ * supernodal Bunch-Kaufman factorisation, and -- when b is given -- x = A^-1 b.
+ * out_i = {positive pivots, negative pivots, nnz(L), ordering within its work
+ * bound, supernodes, 2x2 pivots, largest front, delayed columns}; out_d = {log|det|, det sign,
+ * min pivot ratio}.  Pivots pass a threshold test or their columns are
+ * delayed to the parent front; the solve adds up to two steps of iterative
+ * refinement.  WFSA_ERR_ARG when singular (a zero column, or no nonsingular
+ * pivot left at a root). */
 int wfsa_sym_sparse_solve(int64_t n, int64_t nnz, const int32_t* i, const int32_t* j, const double* v, int order,
-                          const double* b, double* x, int64_t out_i[4], double out_d[3]);
+                          const double* b, double* x, int64_t out_i[8], double out_d[3]);
 
 /* ---- synthetic corpora (bench / tests) ---------------------------------- */
 /* family: N states, out-degree D (+ end), E distinct symbols per state out of

@@ -376,3 +376,28 @@ def test_popular_parameters_chunked_sums(capfd, monkeypatch, merge):
     dn, on = a.param_names(), o.param_names()
     want = dict(zip(on, go))
     np.testing.assert_allclose(g0, [want[n] for n in dn], rtol=1e-10, atol=1e-14)
+
+
+def test_graph_replay_is_instantiated_and_equal(monkeypatch):
+    """WFSA_GRAPH=1: the host binding's evaluation is captured once into a
+    hipGraph and replayed (no dispatch-timestamp launch inside the capture);
+    the replay must actually be a graph (stats.graph == 1) and equal the
+    eager evaluation bit for bit."""
+    import wfsa_amd as W
+    syn = W.Synthetic(n_states=64, degree=8, vocab=16, emissions=1, n_strings=3000, max_len=64, seed=5)
+    sym, off, wt = syn.corpus()
+    fsa = W.Fsa.read_text(syn.wfsa_text)
+    w = np.random.default_rng(3).normal(-1.5, 0.5, size=len(fsa.param_names()))
+    res = {}
+    for mode in ("0", "1"):
+        monkeypatch.setenv("WFSA_GRAPH", mode)
+        dev = W.Device(0)
+        dev.load_model(fsa)
+        dev.load_corpus(sym, off, wt / wt.sum())
+        dev.recognize()
+        runs = [dev.objective_grad(w, want_logq=False) for _ in range(3)]
+        res[mode] = (runs, dev.stats()["graph"])
+    assert res["1"][1] == 1, "WFSA_GRAPH=1 did not replay a graph"
+    assert res["0"][1] == 0
+    for (ll_a, g_a, _), (ll_b, g_b, _) in zip(res["0"][0], res["1"][0]):
+        assert ll_a == ll_b and np.array_equal(g_a, g_b)

@@ -190,7 +190,7 @@ void HessianLearner::InitCallback(int flags) {   // :132-191
     if (flags & 4) InitSlackVariables();
     include_Hf = (flags & 8) != 0;   // AssembleH(include_Hf)
     if (include_Hf && !HasUniquePaths()) SetupHf();
-    reorder = (flags & 16) != 0;   // METIS in the reference: our minimum degree for the sparse LDL^T
+    reorder = (flags & 16) != 0;   // METIS in the reference: approximate minimum degree for the sparse LDL^T
     degenerate = false;
 }
 
@@ -285,18 +285,20 @@ Factored factor_and_solve(wfsa_dev* dev, const SymEntries& A, int order, const d
     if (forced == "sparse" || (forced.empty() && N > HessianLearner::kHostDense)) {
         // the requested ordering first; when its factorisation fails, the other
         // one before giving up (a different elimination order meets different
-        // pivots)
+        // pivots and supernodes)
         for (int attempt = 0; attempt < 2; ++attempt) {
-            const int ord = attempt == 0 ? order : 1 - order;
+            const int other = order == SparseLdlt::kIdentity ? SparseLdlt::kApproxMinimumDegree : SparseLdlt::kIdentity;
+            const int ord = attempt == 0 ? order : other;
             SparseLdlt s;
             const bool ordered = s.Analyze(A, ord);
             if (std::getenv("WFSA_KKT_TRACE"))
-                std::fprintf(stderr, "[kkt] N %lld entries %zu order %d%s nnz(L) %lld flops %.3g\n", (long long)N,
-                             A.v.size(), ord, ordered ? "" : " (work bound: identity)", (long long)s.nnz_l, s.flops);
+                std::fprintf(stderr, "[kkt] N %lld entries %zu order %d%s nnz(L) %lld flops %.3g supernodes %lld front %lld\n",
+                             (long long)N, A.v.size(), ord, ordered ? "" : " (work bound: identity)", (long long)s.nnz_l,
+                             s.flops, (long long)s.supernodes, (long long)s.max_front);
             if (!(forced == "sparse" || !dense_fits || s.flops <= HessianLearner::kSparseFlops)) break;
             bool ok = s.Factor(A) && s.min_pivot_ratio > 1e-12;
             if (ok && rhs) {   // normwise backward error per row: |Ax - b|_i <= tol (|A||x| + |b|)_i
-                s.Solve(rhs, x);
+                s.SolveRefined(A, rhs, x);
                 std::vector<double> ax(static_cast<size_t>(N)), mag(static_cast<size_t>(N), 0.0);
                 A.multiply(x, ax.data());
                 for (size_t t = 0; t < A.v.size(); ++t) {
@@ -422,7 +424,7 @@ void HessianLearner::OptimizationStep(double eta, bool verbose) {   // :63-130
     }
     lambda_min = k ? *std::min_element(lambda.begin(), lambda.end()) : 0.0;
     step.assign(size_t(N), 0.0);
-    const Factored f = factor_and_solve(Device(), A, reorder ? 1 : 0, rhs.data(), step.data());
+    const Factored f = factor_and_solve(Device(), A, reorder ? SparseLdlt::kApproxMinimumDegree : SparseLdlt::kIdentity, rhs.data(), step.data());
     kkt_kind = f.kind;
     inertia_pos = f.positive;
     inertia_neg = f.negative;
@@ -493,7 +495,7 @@ double HessianLearner::ComputeLogDetHessian(bool verbose) {
         }
         return r;
     }
-    const Factored f = factor_and_solve(Device(), A, reorder ? 1 : 0, nullptr, nullptr);
+    const Factored f = factor_and_solve(Device(), A, reorder ? SparseLdlt::kApproxMinimumDegree : SparseLdlt::kIdentity, nullptr, nullptr);
     if (f.det_sign <= 0) return inf;   // (:351-352)
     return f.log_abs_det;
 }

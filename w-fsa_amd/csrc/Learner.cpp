@@ -36,13 +36,13 @@ Learner::~Learner() {
 }
 
 void Learner::SetDevice(int d) {
-    if (dev) throw LearnerError("SetDevice must come before BuildFrom");
+    if (dev) throw LearnerUsageError("SetDevice must come before BuildFrom");
     device = d;
 }
 
 void Learner::SetCommunicator(int n, int r, const uint8_t* id) {
-    if (dev) throw LearnerError("SetCommunicator must come before BuildFrom");
-    if (n < 1 || r < 0 || r >= n) throw LearnerError("bad communicator: rank ", r, " of ", n);
+    if (dev) throw LearnerUsageError("SetCommunicator must come before BuildFrom");
+    if (n < 1 || r < 0 || r >= n) throw LearnerUsageError("bad communicator: rank ", r, " of ", n);
     nranks = n;
     rank = r;
     if (n > 1) {
@@ -53,7 +53,7 @@ void Learner::SetCommunicator(int n, int r, const uint8_t* id) {
 }
 
 void Learner::SetHostCommunicator(int n, int r, wfsa_host_allreduce_fn fn, void* user) {
-    if (dev) throw LearnerError("SetCommunicator must come before BuildFrom");
+    if (dev) throw LearnerUsageError("SetCommunicator must come before BuildFrom");
     if (n < 1 || r < 0 || r >= n || (n > 1 && !fn)) throw LearnerError("bad communicator: rank ", r, " of ", n);
     nranks = n;
     rank = r;
@@ -516,8 +516,8 @@ __attribute__((target_clones("avx2", "default"))) void get_weights(int32_t n, co
 }  // namespace
 
 void Learner::BeginModeledProbs(bool want_logq) {
-    if (!dev) throw LearnerError("BuildFrom has not run");
-    if (eval_in_flight) throw LearnerError("an evaluation is already in flight");
+    if (!dev) throw LearnerUsageError("BuildFrom has not run");
+    if (eval_in_flight) throw LearnerUsageError("an evaluation is already in flight");
     // straight into the device's host-mapped staging area (one copy fewer)
     double* staged = n_full > 0 ? wfsa_dev_weights_staging(dev) : nullptr;
     double* w = staged ? staged : w_full.data();
@@ -530,7 +530,7 @@ void Learner::BeginModeledProbs(bool want_logq) {
 }
 
 void Learner::EndModeledProbs(std::vector<double>& grad_out) {
-    if (!eval_in_flight) throw LearnerError("no evaluation in flight");
+    if (!eval_in_flight) throw LearnerUsageError("no evaluation in flight");
     eval_in_flight = false;
     if (eval_logq) logq.resize(p.size());
     ThrowOnDevError(wfsa_dev_objective_grad_end(dev, &loglik, grad_full.data(),

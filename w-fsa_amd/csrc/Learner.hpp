@@ -31,6 +31,11 @@ namespace wfsa {
 struct LearnerError : public MyError {
     using MyError::MyError;
 };
+// a call made out of order or with bad arguments, found before any rank
+// collective: it fails this call only (the communicator is not aborted)
+struct LearnerUsageError : public LearnerError {
+    using LearnerError::LearnerError;
+};
 
 class Learner {
 public:

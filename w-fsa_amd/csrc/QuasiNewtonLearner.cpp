@@ -230,7 +230,7 @@ void QuasiNewtonLearner::RunDevice(double eta, double tol, int32_t max_epochs, d
     const auto te = clk::now();
     if (epochs_done) *epochs_done = 0;
     wfsa_dev* d = Device();
-    if (!d) throw LearnerError("BuildFrom has not run");
+    if (!d) throw LearnerUsageError("BuildFrom has not run");
     wfsa_qn_desc desc{};
     desc.n_params = GetNumberOfParameters();
     desc.n_constraints = GetNumberOfConstraints();

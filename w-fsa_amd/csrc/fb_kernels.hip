@@ -2438,7 +2438,7 @@ __device__ __forceinline__ QnBatchIn qn_wave_load(const QnWave& q, int b) {
     return in;
 }
 
-__device__ __forceinline__ void qn_wave_batch(const QnWave& q, const QnBatchIn& in, bool ok) {
+__device__ __forceinline__ void qn_wave_batch(const QnWave& q, const QnBatchIn& in, bool ok, const unsigned& halt) {
 #pragma clang fp contract(off)
     const int lane = lane_id();
     const int c0 = in.c0, nc = in.nc, m0 = in.m0, m1 = in.m1, nchunk = in.nchunk;
@@ -2503,6 +2503,9 @@ __device__ __forceinline__ void qn_wave_batch(const QnWave& q, const QnBatchIn& 
     }
     const double laux_l = r / (gg + 1.0);
     const double g = __shfl(gg, ld, kWave), laux = __shfl(laux_l, ld, kWave);
+    // the previous step's halt decision (loaded beside the chunks): a halted
+    // run skips this step -- no update at all (qn_wave_run publishes it)
+    if (halt != 0u) return;
     double gerr = 0.0;
     if (valid && ok) {
         const double aux = e * lam;
@@ -2536,7 +2539,7 @@ __device__ __forceinline__ void qn_wave_batch(const QnWave& q, const QnBatchIn& 
 
 // QN wave r of the launch: wait for every block's arrival (its bubble slots
 // and the finish wave's halt decision), then its batches r, r + n_waves, ...
-constexpr unsigned kQnPollLimit = 1u << 20;   // x s_sleep 4 (~0.1 us): ~0.1 s, then give up
+constexpr unsigned kQnPollLimit = 1u << 22;   // polls of ~0.5 us under load (s_sleep 1 + an sc1 load): ~1 s, then give up
 __device__ __forceinline__ void qn_wave_run(const QnWave& q, int r, unsigned long long* tr) {
     const int lane = lane_id();
     QnBatchIn first{};
@@ -2545,7 +2548,7 @@ __device__ __forceinline__ void qn_wave_run(const QnWave& q, int r, unsigned lon
     if (lane == 0) {
         unsigned it = 0;
         while (load_wt(q.arrive + q.parity) < unsigned(q.n_arrive)) {
-            __builtin_amdgcn_s_sleep(4);
+            __builtin_amdgcn_s_sleep(1);
             if (++it > kQnPollLimit) {
                 ok = 0;
                 break;
@@ -2554,15 +2557,16 @@ __device__ __forceinline__ void qn_wave_run(const QnWave& q, int r, unsigned lon
     }
     ok = __shfl(ok, 0, kWave);
     if (tr && lane == 0) tr[5] = __builtin_amdgcn_s_memrealtime();   // (timing experiments)
-    if (ok && load_wt(q.halted + 1) != 0u) {   // the previous step halted: this one is skipped
-        if (r == 0 && lane == 0) {
-            q.halted[0] = 1u;   // for the later launches
-            qn_publish_row(q.fin, nullptr, kQnSkipped);
-        }
-        return;
+    // the halt decision of this launch's finish wave: issued now, waited for
+    // only before the first store (beside the batch's chunk loads)
+    const unsigned halt = ok ? load_wt(q.halted + 1) : 0u;
+    if (r < q.n_batches) qn_wave_batch(q, first, ok != 0, halt);
+    for (int b = r + q.n_waves; b < q.n_batches && halt == 0u; b += q.n_waves)
+        qn_wave_batch(q, qn_wave_load(q, b), ok != 0, halt);
+    if (halt != 0u && r == 0 && lane == 0) {   // the previous step halted: this one is skipped
+        q.halted[0] = 1u;   // for the later launches
+        qn_publish_row(q.fin, nullptr, kQnSkipped);
     }
-    if (r < q.n_batches) qn_wave_batch(q, first, ok != 0);
-    for (int b = r + q.n_waves; b < q.n_batches; b += q.n_waves) qn_wave_batch(q, qn_wave_load(q, b), ok != 0);
     if (tr && lane == 0) tr[6] = __builtin_amdgcn_s_memrealtime();
 }
 
@@ -2589,6 +2593,31 @@ __global__ __launch_bounds__(1024, (DBG == 10 ? 8 : 1)) WFSA_FBS_ATTR void fbs_k
 #define WFSA_STAMP(k)
 #endif
     WFSA_STAMP(0)
+    const bool early = DELTA && a.early_bub && a.bub_on && a.bub.small_wpb > 0 && a.bub.small_wpb < wpb &&
+                       DBG != 4 && DBG != 8 && DBG != 10 && DBG != 11 && DBG != 13 && !a.no_streams;
+    // The delta table's first round of loads before anything else is waited
+    // for (the halted flag, the wave's stream setup, the first row set): at
+    // entry these scalar load chains took ~2 us ahead of the table's loads
+    constexpr int kTB = 12;   // 16-byte pieces per thread and round (one round for 12k-entry tables at 512 threads)
+    const bool pre = DELTA && !a.no_streams && DBG != 4 && DBG != 11 && !early;
+    const int tlast = a.n_params - 1;
+    auto wslot = [&](int s, bool& zero) {   // slot s of the remapped table: weight s - 1 - s / kDeltaPeriod, or zero
+        const int j = s - 1 - s / kDeltaPeriod;
+        zero = (s % kDeltaPeriod) == 0 || j > tlast;
+        return min(max(j, 0), tlast);
+    };
+    auto table_round = [&](int q0, int nthr, double2 (&t)[kTB]) {
+#pragma unroll
+        for (int b = 0; b < kTB; ++b) {
+            const int s2 = 2 * (q0 + b * nthr);
+            bool z0, z1;
+            const double lo = a.w[wslot(s2, z0)], hi = a.w[wslot(s2 + 1, z1)];
+            t[b].x = z0 ? 0.0 : lo;
+            t[b].y = z1 ? 0.0 : hi;
+        }
+    };
+    double2 t0[kTB];
+    if (pre) table_round(int(threadIdx.x), int(blockDim.x), t0);
     if (QN && bid == 0 && threadIdx.x == 0) a.qw.arrive[a.qw.parity ^ 1] = 0u;   // for the next launch
     // halted is written only by an earlier launch (the QN step's finish)
     if (a.halted && *a.halted) {
@@ -2601,8 +2630,6 @@ __global__ __launch_bounds__(1024, (DBG == 10 ? 8 : 1)) WFSA_FBS_ATTR void fbs_k
     // stage the table and announce it by an LDS counter; every wave waits for
     // that counter before its stream pass (no block barrier on the way)
     __shared__ unsigned staged_waves;
-    const bool early = DELTA && a.early_bub && a.bub_on && a.bub.small_wpb > 0 && a.bub.small_wpb < wpb &&
-                       DBG != 4 && DBG != 8 && DBG != 10 && DBG != 11 && DBG != 13 && !a.no_streams;
     if (early) {
         if (threadIdx.x == 0) {
             q_arrived = 0u;
@@ -2639,8 +2666,27 @@ __global__ __launch_bounds__(1024, (DBG == 10 ? 8 : 1)) WFSA_FBS_ATTR void fbs_k
     // the first row set in flight from the start (its latency hides behind
     // the staging and the bubbles; but the table loads then return behind it),
     // or issued once the wave's table / bubble loads are out (defer_prefetch)
-    const bool defer = DELTA && DBG != 4 && DBG != 11 && a.defer_prefetch != 0;
+    const bool defer = DELTA && DBG != 4 && DBG != 11 && a.defer_prefetch != 0 && !pre;
     if (kStreams && !defer) load(A, 0);
+    if (pre) {   // the table: the first round's pieces (loaded at entry), then any further rounds
+        const int T2 = (a.d_tab + 1) / 2, nthr = int(blockDim.x);
+        double2* dst = reinterpret_cast<double2*>(lds);
+#pragma unroll
+        for (int b = 0; b < kTB; ++b) {
+            const int q = int(threadIdx.x) + b * nthr;
+            if (q < T2) dst[q] = t0[b];
+        }
+        for (int q0 = int(threadIdx.x) + kTB * nthr; q0 < T2; q0 += kTB * nthr) {
+            double2 t[kTB];
+            table_round(q0, nthr, t);
+#pragma unroll
+            for (int b = 0; b < kTB; ++b) {
+                const int q = q0 + b * nthr;
+                if (q < T2) dst[q] = t[b];
+            }
+        }
+        __syncthreads();
+    }
     // the previous QN step's finish runs in a wave of its own -- the last
     // wave of block 0, which the host gives no groups and no bubbles -- after
     // the staging barrier, beside the other waves' work
@@ -2681,31 +2727,18 @@ __global__ __launch_bounds__(1024, (DBG == 10 ? 8 : 1)) WFSA_FBS_ATTR void fbs_k
     if (early && small_wave) small_bubbles();
     if (kStreams && defer && early && small_wave) load(A, 0);
     const int stage_w0 = early ? a.bub.small_wpb : 0;   // the staging waves: [stage_w0, wpb)
-    if (DELTA && !a.no_streams && DBG != 4 && DBG != 11 && w >= stage_w0) {
+    if (DELTA && !a.no_streams && DBG != 4 && DBG != 11 && !pre && w >= stage_w0) {
         // the delta format's remapped table in 16-byte pieces: slot s holds
         // weight s - 1 - s / kDeltaPeriod, or zero on a multiple of
         // kDeltaPeriod and past the last weight; loads first
-        constexpr int kB = 12;
+        constexpr int kB = kTB;
         const int T2 = (a.d_tab + 1) / 2;
-        const int last = a.n_params - 1;
         double2* dst = reinterpret_cast<double2*>(lds);
-        auto wslot = [&](int s, bool& zero) {
-            const int j = s - 1 - s / kDeltaPeriod;
-            zero = (s % kDeltaPeriod) == 0 || j > last;
-            return min(max(j, 0), last);
-        };
         const int nthr = int(blockDim.x) - stage_w0 * kWave;
         bool pf = kStreams && defer;   // the deferred first row set: after this wave's first table loads
         for (int q0 = int(threadIdx.x) - stage_w0 * kWave; q0 < T2; q0 += kB * nthr) {
             double2 t[kB];
-#pragma unroll
-            for (int b = 0; b < kB; ++b) {
-                const int s2 = 2 * (q0 + b * nthr);
-                bool z0, z1;
-                const double lo = a.w[wslot(s2, z0)], hi = a.w[wslot(s2 + 1, z1)];
-                t[b].x = z0 ? 0.0 : lo;
-                t[b].y = z1 ? 0.0 : hi;
-            }
+            table_round(q0, nthr, t);
             if (pf) {
                 load(A, 0);
                 pf = false;

@@ -74,11 +74,24 @@ int guarded(F&& f) {
 // guarded() for a learner call that may sit between rank collectives: a
 // failure on this rank aborts its communicator (wfsa_dev_comm_abort), so the
 // other ranks fail at their current or next collective instead of waiting
+// (a LearnerUsageError -- a call out of order or with bad arguments, found
+// before any collective -- fails the call only, as wfsa_dev's rank guard
+// exempts WFSA_ERR_ARG)
 template <class F>
 int rank_guarded(wfsa_learner* l, F&& f) {
-    const int rc = guarded(std::forward<F>(f));
-    if (rc != WFSA_OK) l->base->AbortCommunicator(g_host_error.c_str());
-    return rc;
+    try {
+        f();
+        return WFSA_OK;
+    } catch (const wfsa::LearnerUsageError& e) {
+        g_host_error = e.what();
+        return WFSA_ERR_ARG;
+    } catch (const std::bad_alloc&) {
+        g_host_error = "out of memory";
+    } catch (const std::exception& e) {
+        g_host_error = e.what();
+    }
+    l->base->AbortCommunicator(g_host_error.c_str());
+    return WFSA_ERR_ARG;
 }
 
 int null_arg(const char* what) {
@@ -469,7 +482,7 @@ int wfsa_shard_range(const int64_t* off, int64_t n, int nranks, int rank, int64_
 }
 
 int wfsa_sym_sparse_solve(int64_t n, int64_t nnz, const int32_t* i, const int32_t* j, const double* v, int order,
-                          const double* b, double* x, int64_t out_i[4], double out_d[3]) {
+                          const double* b, double* x, int64_t out_i[8], double out_d[3]) {
     if (n < 0 || nnz < 0 || (nnz > 0 && (!i || !j || !v)) || (b && !x) || !out_i || !out_d) return null_arg("matrix");
     if (n > std::numeric_limits<int32_t>::max()) return null_arg("n");
     try {
@@ -485,14 +498,18 @@ int wfsa_sym_sparse_solve(int64_t n, int64_t nnz, const int32_t* i, const int32_
         out_i[1] = s.negative;
         out_i[2] = s.nnz_l;
         out_i[3] = ordered ? 1 : 0;
+        out_i[4] = s.supernodes;
+        out_i[5] = s.two_by_two;
+        out_i[6] = s.max_front;
+        out_i[7] = s.delayed;
         out_d[0] = s.log_abs_det;
         out_d[1] = s.det_sign;
         out_d[2] = s.min_pivot_ratio;
         if (!ok) {
-            g_host_error = "sparse LDL^T: zero or non-finite pivot";
+            g_host_error = "sparse LDL^T: singular (a zero column or a zero / non-finite pivot)";
             return WFSA_ERR_ARG;
         }
-        if (b) s.Solve(b, x);
+        if (b) s.SolveRefined(a, b, x);
         return WFSA_OK;
     } catch (const std::bad_alloc&) {
         g_host_error = "out of host memory";

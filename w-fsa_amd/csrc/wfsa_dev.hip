@@ -320,6 +320,7 @@ struct wfsa_dev {
     bool graph_failed = false;
     bool use_graph = false;    // WFSA_GRAPH=1: replay a captured graph (no per-kernel timing)
     bool in_flight = false;    // between objective_grad_begin and _end
+    bool weights_staged = false;   // wfsa_dev_weights_staging handed out the staging area since the last _begin
     bool logq_ready = false;   // the call in flight computes log q
 
     // device-resident QuasiNewton (wfsa_dev_qn_*)
@@ -364,7 +365,7 @@ struct wfsa_dev {
     // constraints built at QN set-up, per-parity arrival counters and the
     // weights double-buffered by step parity (w_full2 / ewp2 above)
     bool use_qw = true;
-    bool early_bub = true;           // WFSA_EARLY_BUB=0: every wave stages the table before any bubble
+    bool early_bub = false;          // WFSA_EARLY_BUB=1: the small-bubble waves start at entry, the others stage (slower: the few stagers take longer)
     bool stream_nt = false;          // WFSA_STREAM_NT=1: the stream kernel's rows loaded non-temporal
     bool defer_prefetch = false;     // WFSA_DEFER_PREFETCH=1: the first row set after the table / bubble loads
     bool bub_prio = true;            // WFSA_BUB_PRIO=0: the fused small bubbles at normal wave priority
@@ -2933,7 +2934,7 @@ int wfsa_dev_create(int device, wfsa_dev** out) {
     if (const char* e = std::getenv("WFSA_PULL")) ctx->use_pull = e[0] != '0';
     if (const char* e = std::getenv("WFSA_WIDE2_TIERS")) ctx->w2_all = std::strcmp(e, "2") != 0;
     if (const char* e = std::getenv("WFSA_QN_INKERNEL")) ctx->use_qw = e[0] != '0';
-    if (const char* e = std::getenv("WFSA_EARLY_BUB")) ctx->early_bub = e[0] != '0';
+    if (const char* e = std::getenv("WFSA_EARLY_BUB")) ctx->early_bub = e[0] == '1';
     if (const char* e = std::getenv("WFSA_STREAM_NT")) ctx->stream_nt = e[0] == '1';
     if (const char* e = std::getenv("WFSA_DEFER_PREFETCH")) ctx->defer_prefetch = e[0] == '1';
     if (const char* e = std::getenv("WFSA_BUB_PRIO")) ctx->bub_prio = e[0] != '0';
@@ -3317,6 +3318,9 @@ static int objective_grad_begin_impl(wfsa_dev* ctx, const double* w_full, int wa
     hipStream_t s = ctx->stream;
     const int32_t np = ctx->n_params;
     double* win = ctx->pinned + weights_off(np);   // weights in (w_full == NULL: already written there)
+    if (!w_full && np > 0 && !ctx->weights_staged)
+        return fail(WFSA_ERR_ARG, "null weights, and none written through wfsa_dev_weights_staging since the last call");
+    ctx->weights_staged = false;
     if (np > 0 && w_full) std::memcpy(win, w_full, size_t(np) * sizeof(double));
     HIP_TRY(hipEventRecord(ctx->ev0, s));
     if (ctx->use_graph && !ctx->graph_exec && !ctx->graph_failed) {
@@ -3375,6 +3379,7 @@ static int objective_grad_end_impl(wfsa_dev* ctx, double* loglik, double* grad_f
 
 double* wfsa_dev_weights_staging(wfsa_dev* ctx) {
     if (!ctx || !ctx->has_model || !ctx->pinned || ctx->in_flight) return nullptr;
+    ctx->weights_staged = true;   // (the next _begin may take its weights from here)
     return ctx->pinned + weights_off(ctx->n_params);
 }
 

@@ -43,11 +43,12 @@ def sym_sparse_solve(i, j, v, n, b=None, order=0):
     v = np.ascontiguousarray(v, dtype=np.float64)
     bb = None if b is None else np.ascontiguousarray(b, dtype=np.float64)
     x = None if b is None else np.zeros(n)
-    oi = np.zeros(4, dtype=np.int64)
+    oi = np.zeros(8, dtype=np.int64)
     od = np.zeros(3)
     check_host(load().wfsa_sym_sparse_solve(n, len(v), _ptr(i), _ptr(j), _ptr(v), order, _ptr(bb), _ptr(x),
                                             _ptr(oi), _ptr(od)))
     return x, dict(positive=int(oi[0]), negative=int(oi[1]), nnz_l=int(oi[2]), ordered=bool(oi[3]),
+                   supernodes=int(oi[4]), two_by_two=int(oi[5]), max_front=int(oi[6]), delayed=int(oi[7]),
                    log_abs_det=float(od[0]), det_sign=int(od[1]), min_pivot_ratio=float(od[2]))
 
 
