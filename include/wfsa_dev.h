@@ -279,14 +279,24 @@ int wfsa_dev_allreduce(wfsa_dev* ctx, double* host_buf, int64_t count);
 /* Failure semantics across ranks.  A call that takes part in
  * collectives (recognize, objective_grad_begin/_end, qn_setup, qn_run,
  * hf_setup, hf_eval, rmin, allreduce) and fails on one rank for any reason
- * but a bad argument aborts that rank's communicator: the in-process group
- * is poisoned (every waiting member wakes with WFSA_ERR_RCCL now), every
- * member's peer area gets its poison word (their next peer sum fails at
- * entry), an RCCL communicator is aborted (ncclCommAbort).  A peer sum whose
- * wait gives up (WFSA_PEER_TIMEOUT_S, default 120 s) poisons every area too
- * and is reported as WFSA_ERR_RCCL at the next host sync point, never as a
- * NaN result.  wfsa_dev_comm_abort does the same for a failure outside the
- * library (the caller's own work between collectives). */
+ * but a bad argument aborts that rank's communicator.  How the others hear
+ * of it depends on the transport:
+ *   - in-process group: poisoned -- every waiting member wakes with
+ *     WFSA_ERR_RCCL now, a later one fails at entry;
+ *   - peer sums (the per-step [LL, grad]): every member's peer area gets its
+ *     poison word -- their next peer sum fails at entry;
+ *   - host callback (gloo, MPI): a poisoned header exchange -- every member
+ *     waiting in, or later entering, any collective fails at once;
+ *   - RCCL: the communicator is aborted (ncclCommAbort), which does NOT wake
+ *     the other processes' pending RCCL calls: each rank's host watchdog
+ *     ends them (an asynchronous error, or no progress within
+ *     WFSA_COMM_TIMEOUT_S, default 300 s), unless the peer path carried the
+ *     call.
+ * A peer sum whose wait gives up (WFSA_PEER_TIMEOUT_S, default 120 s)
+ * poisons every area too and is reported as WFSA_ERR_RCCL at the next host
+ * sync point, never as a NaN result.  wfsa_dev_comm_abort does the same for
+ * a failure outside the library (the caller's own work between
+ * collectives). */
 int wfsa_dev_comm_abort(wfsa_dev* ctx, const char* why);
 
 /* Test entry: the peer all-reduce kernel on one device, the other members'

@@ -245,7 +245,7 @@ def test_hessian_learner_epochs_match_restatement(case, kkt, flags, monkeypatch)
     restatement oracle/hessian.py on the oracle's enumerated paths.  logdetH is
     compared where the Hessian is well conditioned (talk's is singular).  The
     KKT system through the dense Bunch-Kaufman LDL^T and through the sparse
-    LDL^T (WFSA_KKT=sparse) in minimum-degree order (flag 16, the reference's
+    LDL^T (WFSA_KKT=sparse) in approximate-minimum-degree order (flag 16, the reference's
     METIS) and in the identity order (the reference's MKL_DSS_MY_ORDER)."""
     import wfsa_amd as W
     monkeypatch.setenv("WFSA_KKT", kkt)

@@ -49,7 +49,7 @@ def _learn(W, fsa, sym, off, wt, setup=None):
     return dict(kl=kl, grad=g, rows=[list(r) for r in rows], x=lrn.x(), info=lrn.info(), stats=lrn.stats())
 
 
-def _worker(rank, world, port, peer, q, late_s=0.0):
+def _worker(rank, world, port, peer, q, late_s=0.0, abort=False):
     import sys
     sys.path.insert(0, ROOT)
     sys.path.insert(0, os.path.join(ROOT, "w-fsa_amd"))
@@ -64,6 +64,9 @@ def _worker(rank, world, port, peer, q, late_s=0.0):
         syn = W.Synthetic(**SPEC)
         sym, off, wt = syn.corpus()
         fsa = W.Fsa.read_text(syn.wfsa_text)
+        if abort:
+            q.put((rank, _abort_learn(W, fsa, sym, off, wt, world, rank)))
+            return
         if late_s:   # rank 1 arrives at the device loop after the others' peer waits gave up
             res = _late_learn(W, fsa, sym, off, wt, world, rank, late_s)
             q.put((rank, res))
@@ -100,6 +103,36 @@ def _late_learn(W, fsa, sym, off, wt, world, rank, late_s):
         return {"raised": str(e), "code": e.code, "s": time.time() - t0}
 
 
+def _abort_learn(W, fsa, sym, off, wt, world, rank):
+    """the host transport (gloo) with the peer path off: rank 1 fails outside
+    the library and aborts while rank 0 waits in the per-step gradient sum
+    (a non-peer collective); rank 0 must fail at once with the reason, not at
+    gloo's 30-minute timeout"""
+    import time
+    lrn = W.QuasiNewtonLearner(0)
+    lrn.SetHostCommunicator(world, rank, W.torch_allreduce)
+    lrn.BuildFromPacked(fsa, sym, off, wt)
+    lrn.Finalize()
+    lrn.Init(7)
+    lrn.objective_grad()   # both ranks here, healthy
+    assert lrn.stats()["comm_peer"] == 0
+    t0 = time.time()
+    if rank == 1:
+        time.sleep(2.0)    # rank 0 is inside Run by now
+        lrn.AbortCommunicator("rank 1: injected failure")
+        t_abort = time.time() - t0
+        try:
+            lrn.Run(5, 1.0, -1.0)
+            return {"raised": None}
+        except W.WfsaError as e:
+            return {"raised": str(e), "s": time.time() - t0, "abort_s": t_abort}
+    try:
+        rows = lrn.Run(50, 1.0, -1.0)
+        return {"raised": None, "rows": len(rows)}
+    except W.WfsaError as e:
+        return {"raised": str(e), "s": time.time() - t0}
+
+
 def _one_context():
     import wfsa_amd as W
     syn = W.Synthetic(**SPEC)
@@ -117,11 +150,11 @@ def _compare(res, one):
     np.testing.assert_allclose(res["x"], one["x"], rtol=1e-10, atol=1e-12)
 
 
-def _spawn(world, peer, late_s=0.0):
+def _spawn(world, peer, late_s=0.0, abort=False):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, peer, q, late_s)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, peer, q, late_s, abort)) for r in range(world)]
     for p in procs:
         p.start()
     got = {}
@@ -161,6 +194,18 @@ def test_two_processes_late_rank_fails_every_rank():
         assert "peer all-reduce" in got[r]["raised"], got[r]["raised"]
     assert got[0]["s"] < 30          # the 3 s timeout, not a hang
     assert got[1]["s"] < 5           # poisoned: fails at entry
+
+
+def test_two_processes_abort_over_gloo_fails_every_rank():
+    """an abort must reach the other processes over the host
+    transport too.  Rank 1 aborts 2 s in; rank 0, waiting in a gloo sum of
+    the QN loop, fails within seconds with "aborted the group"; rank 1's own
+    next collective fails at entry"""
+    got = _spawn(2, False, abort=True)
+    assert got[0]["raised"] and "aborted the group" in got[0]["raised"], got[0]
+    assert got[0]["s"] < 20, got[0]
+    assert got[1]["raised"], got[1]
+    assert got[1]["abort_s"] < 20, got[1]
 
 
 # ---- the peer kernel on one device, the other members simulated ----------

@@ -296,7 +296,7 @@ Factored factor_and_solve(wfsa_dev* dev, const SymEntries& A, int order, const d
                              (long long)N, A.v.size(), ord, ordered ? "" : " (work bound: identity)", (long long)s.nnz_l,
                              s.flops, (long long)s.supernodes, (long long)s.max_front);
             if (!(forced == "sparse" || !dense_fits || s.flops <= HessianLearner::kSparseFlops)) break;
-            bool ok = s.Factor(A) && s.min_pivot_ratio > 1e-12;
+            bool ok = s.Factor(A) && (s.min_pivot_ratio > HessianLearner::kSparsePivotFloor || !dense_fits);
             if (ok && rhs) {   // normwise backward error per row: |Ax - b|_i <= tol (|A||x| + |b|)_i
                 s.SolveRefined(A, rhs, x);
                 std::vector<double> ax(static_cast<size_t>(N)), mag(static_cast<size_t>(N), 0.0);

@@ -52,12 +52,17 @@ public:
     // device forces one side
     static constexpr int64_t kHostDense = 1024;
     static constexpr int64_t kMaxDense = 46000;
-    // above kHostDense the sparse LDL^T (SparseLdlt.hpp, scalar up-looking
-    // code at ~1 GFLOP/s) takes systems whose factor costs at most this many
-    // flops -- below the dense factorisation in HBM (0.5 s at N = 10k; c3's
-    // KKT system fills in too much for the sparse one) -- and every system
-    // beyond kMaxDense; WFSA_KKT=sparse forces it
+    // above kHostDense the sparse LDL^T (SparseLdlt.hpp, multifrontal with
+    // scalar host fronts at ~1 GFLOP/s) takes systems whose factor costs at
+    // most this many flops -- below the dense factorisation in HBM (0.5 s at
+    // N = 10k; c3's KKT system fills in too much for the sparse one) -- and
+    // every system beyond kMaxDense; WFSA_KKT=sparse forces it
     static constexpr double kSparseFlops = 3e8;
+    // a sparse factorisation whose smallest pivot is below this fraction of
+    // its row's largest entry leaves the inertia's sign there to rounding
+    // (threshold pivots allow more growth than full Bunch-Kaufman): such a
+    // system goes to the dense factorisation when it fits
+    static constexpr double kSparsePivotFloor = 1e-9;
     char LastKktKind() const { return kkt_kind; }   // h / d / s: the last step's factorisation
 
     void OptimizationStep(double eta = 1.0, bool verbose = false) override;

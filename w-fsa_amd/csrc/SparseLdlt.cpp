@@ -228,7 +228,7 @@ bool approximate_minimum_degree_order(const SymEntries& a, std::vector<int32_t>&
 namespace {
 
 constexpr double kBkAlpha = 0.6403882032022076;   // (1 + sqrt(17)) / 8: Bunch-Kaufman's growth bound
-constexpr double kPivotThreshold = 0.01;           // a pivot's multipliers at most 1 / u (u: MA57's default)
+constexpr double kPivotThreshold = 0.1;           // a pivot's multipliers at most 1 / u (MA57 allows 0.01 .. 0.1)
 
 }  // namespace
 

@@ -17,7 +17,7 @@
 //     entries and the children's update matrices (extend-add), partially
 //     factorised with Bunch-Kaufman 1x1 / 2x2 pivots chosen among its fully
 //     summed columns and accepted under a threshold test over the whole
-//     front column (multipliers at most 1 / u, u = 0.01); columns with no
+//     front column (multipliers at most 1 / u, u = 0.1); columns with no
 //     acceptable pivot are delayed -- handed, with the Schur complement, to
 //     the parent's front, where they are fully summed again (MA57's
 //     threshold pivoting with delayed pivots; PARDISO perturbs such pivots

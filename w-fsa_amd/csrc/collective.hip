@@ -337,6 +337,15 @@ int rccl_unique_id(uint8_t id[kCommIdBytes], std::string& err) {
 
 namespace {
 
+// Every all-reduce is two callback calls: a fixed 8-byte header (max of
+// bytes; byte 0 = poisoned), then the payload.  abort() on a member standing
+// between collectives sends the header alone with the poison byte set: the
+// other members are waiting in (or will enter) a header exchange of the same
+// size whatever collective they are in, so theirs completes with the poison
+// and fails at once -- the abort reaches every rank through the transport
+// itself.  The aborting call returns once every member has entered a
+// collective (or the transport reports a closed peer).  A member that dies
+// without aborting leaves the others to the callback transport's own timeout.
 class HostCollective final : public Collective {
 public:
     HostCollective(int n, int r, HostAllreduceFn fn, void* user) : fn_(fn), user_(user) {
@@ -344,8 +353,28 @@ public:
         r_ = r;
     }
     const char* kind() const override { return "host"; }
+    void abort_transport(const std::string&) override {
+        if (phase_ != 0 || broken_) return;   // (inside a callback: the exchange is out of step already)
+        uint8_t hdr[8] = {1, 0, 0, 0, 0, 0, 0, 0};
+        broken_ = true;
+        (void)fn_(user_, hdr, 8, 2);
+    }
     int transport_allreduce(void* buf, size_t n, RedOp op, hipStream_t s) override {
         if (n == 0) return 0;
+        if (broken_) {
+            err_ = "host transport: the group was aborted";
+            return 1;
+        }
+        uint8_t hdr[8] = {};
+        phase_ = 1;
+        const int hr = fn_(user_, hdr, 8, 2);
+        phase_ = 0;
+        if (hr != 0 || hdr[0] != 0) {
+            broken_ = true;
+            err_ = hr != 0 ? "host transport: the all-reduce callback failed"
+                           : "host transport: another member aborted the group";
+            return 1;
+        }
         const size_t bytes = n * (op == RedOp::MaxU8 ? 1 : 8);
         if (host_.size() < bytes) host_.resize(bytes);
         if (hipMemcpyAsync(host_.data(), buf, bytes, hipMemcpyDeviceToHost, s) != hipSuccess ||
@@ -354,7 +383,11 @@ public:
             return 1;
         }
         const int32_t code = op == RedOp::SumF64 ? 0 : op == RedOp::MinF64 ? 1 : 2;
-        if (fn_(user_, host_.data(), int64_t(n), code) != 0) {
+        phase_ = 2;
+        const int pr = fn_(user_, host_.data(), int64_t(n), code);
+        phase_ = 0;
+        if (pr != 0) {
+            broken_ = true;
             err_ = "host transport: the all-reduce callback failed";
             return 1;
         }
@@ -370,6 +403,8 @@ private:
     HostAllreduceFn fn_;
     void* user_;
     std::vector<uint8_t> host_;
+    int phase_ = 0;         // 1 / 2: inside the header / payload callback
+    bool broken_ = false;   // aborted, poisoned or a failed callback: the exchange is out of step
 };
 
 }  // namespace

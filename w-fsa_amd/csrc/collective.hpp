@@ -67,8 +67,10 @@ public:
     //  * RCCL: the communicator is aborted (ncclCommAbort).  The other
     //    processes' pending RCCL calls are NOT woken by that: each rank's own
     //    watchdog ends them (its asynchronous error, or WFSA_COMM_TIMEOUT_S);
-    //  * host callback (gloo, MPI): nothing to abort -- the other members end
-    //    by the callback transport's own timeout.
+    //  * host callback (gloo, MPI): a poisoned header exchange (every call
+    //    starts with one) -- every member waiting in, or later entering, a
+    //    collective fails at once.  A member that dies without aborting
+    //    leaves the others to the callback transport's own timeout.
     void abort(const char* why);
     bool aborted() const { return aborted_; }
 
