@@ -257,14 +257,16 @@ def run_workload(wl, world, rank, local_rank, distributed, dist, torch, info_rmi
         torch.cuda.synchronize()
 
     # main.cpp's epoch loop runs natively (wfsa_learner_run); tol < 0 never
-    # halts, so exactly `steps` OptimizationSteps run
+    # halts, so exactly `steps` OptimizationSteps run.  No cyclic garbage
+    # collection from the warmup to the end of the timed region: a collection
+    # pass over torch's heap costs tens of microseconds of host time inside it,
+    # and milliseconds between the warmup and the timed steps idle the GPU
+    # long enough for its clock to drop (the timed steps then start slow)
+    gc.collect()
+    gc.disable()
     if wl["warmup"]:
         lrn.Run(wl["warmup"], 1.0, -1.0)
     st0 = lrn.stats()
-    # no cyclic garbage collection inside the timed region (a collection
-    # pass over torch's heap costs tens of microseconds of host time)
-    gc.collect()
-    gc.disable()
     barrier()
     t0 = time.perf_counter()
     ns0 = time.monotonic_ns()

@@ -65,7 +65,9 @@ def _worker(rank, world, port, peer, q, late_s=0.0, abort=False):
         sym, off, wt = syn.corpus()
         fsa = W.Fsa.read_text(syn.wfsa_text)
         if abort:
-            q.put((rank, _abort_learn(W, fsa, sym, off, wt, world, rank)))
+            if abort == "stall":
+                os.environ["WFSA_COMM_TIMEOUT_S"] = "3"
+            q.put((rank, _abort_learn(W, fsa, sym, off, wt, world, rank, abort == "stall")))
             return
         if late_s:   # rank 1 arrives at the device loop after the others' peer waits gave up
             res = _late_learn(W, fsa, sym, off, wt, world, rank, late_s)
@@ -103,11 +105,12 @@ def _late_learn(W, fsa, sym, off, wt, world, rank, late_s):
         return {"raised": str(e), "code": e.code, "s": time.time() - t0}
 
 
-def _abort_learn(W, fsa, sym, off, wt, world, rank):
+def _abort_learn(W, fsa, sym, off, wt, world, rank, stall=False):
     """the host transport (gloo) with the peer path off: rank 1 fails outside
     the library and aborts while rank 0 waits in the per-step gradient sum
     (a non-peer collective); rank 0 must fail at once with the reason, not at
-    gloo's 30-minute timeout"""
+    gloo's 30-minute timeout.  stall: rank 1 stalls instead (no abort) and
+    rank 0's wait gives up at WFSA_COMM_TIMEOUT_S (3 s)"""
     import time
     lrn = W.QuasiNewtonLearner(0)
     lrn.SetHostCommunicator(world, rank, W.torch_allreduce)
@@ -117,6 +120,13 @@ def _abort_learn(W, fsa, sym, off, wt, world, rank):
     lrn.objective_grad()   # both ranks here, healthy
     assert lrn.stats()["comm_peer"] == 0
     t0 = time.time()
+    if rank == 1 and stall:
+        time.sleep(8.0)    # past rank 0's 3 s limit, without a word
+        try:
+            lrn.Run(5, 1.0, -1.0)
+            return {"raised": None}
+        except W.WfsaError as e:
+            return {"raised": str(e), "s": time.time() - t0 - 8.0}
     if rank == 1:
         time.sleep(2.0)    # rank 0 is inside Run by now
         lrn.AbortCommunicator("rank 1: injected failure")
@@ -206,6 +216,18 @@ def test_two_processes_abort_over_gloo_fails_every_rank():
     assert got[0]["s"] < 20, got[0]
     assert got[1]["raised"], got[1]
     assert got[1]["abort_s"] < 20, got[1]
+
+
+def test_two_processes_stalled_rank_times_out_over_gloo():
+    """ADVICE/VERDICT r4 item 6: a member that stalls without aborting.  Rank
+    0 waits in a gloo sum; its wait gives up at WFSA_COMM_TIMEOUT_S (3 s) and
+    the call fails (the transport is then broken for good); rank 1, back
+    8 s later, fails too (rank 0 is gone or its limit ends the wait)"""
+    got = _spawn(2, False, abort="stall")
+    assert got[0]["raised"] and "callback failed" in got[0]["raised"], got[0]
+    assert 2.5 < got[0]["s"] < 15, got[0]
+    assert got[1]["raised"], got[1]
+    assert got[1]["s"] < 15, got[1]
 
 
 # ---- the peer kernel on one device, the other members simulated ----------

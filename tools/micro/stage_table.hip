@@ -1,0 +1,119 @@
+// The stream kernel's table staging alone: every block copies the delta
+// format's weight table (c3: ~9.4k doubles, 74 KB) from HBM into its LDS,
+// then ends.  Variants (time each under rocprofv3 --kernel-trace --stats):
+//   gather  -- as fbs_kernel stages it: per 16-byte piece two 8-byte loads of
+//              the weight vector through the slot remap (zero slots)
+//   contig  -- one 16-byte load per piece from a table already laid out in
+//              slot order (the QN update writing it)
+//   dma     -- global_load_lds_dwordx4 from the slot-ordered table (no VGPRs,
+//              no ds_write)
+// each at 512 blocks x 512 threads (2 blocks per CU, as fbs_kernel) and at
+// 256 blocks x 1024 threads (1 per CU: the table once per CU).
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <cstdio>
+#include <vector>
+
+#define CK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { printf("%s line %d\n", hipGetErrorString(e_), __LINE__); return 1; } } while (0)
+
+constexpr int kPeriod = 511;
+constexpr int kTB = 12;
+typedef __attribute__((address_space(3))) void lds_void;
+typedef __attribute__((address_space(1))) void glb_void;
+
+__device__ __forceinline__ int wslot(int s, int tlast, bool& zero) {
+    const int j = s - 1 - s / kPeriod;
+    zero = (s % kPeriod) == 0 || j > tlast;
+    return min(max(j, 0), tlast);
+}
+
+template <int V>
+__global__ __launch_bounds__(1024, 1) void stage(const double* __restrict__ w, const double2* __restrict__ tab, int n_params,
+                                                 int d_tab, double* out) {
+    extern __shared__ __attribute__((aligned(16))) double lds[];
+    const int T2 = (d_tab + 1) / 2, nthr = int(blockDim.x);
+    double2* dst = reinterpret_cast<double2*>(lds);
+    if (V == 0) {
+        for (int q0 = int(threadIdx.x); q0 < T2; q0 += kTB * nthr) {
+            double2 t[kTB];
+#pragma unroll
+            for (int b = 0; b < kTB; ++b) {
+                const int s2 = 2 * (q0 + b * nthr);
+                bool z0, z1;
+                const double lo = w[wslot(s2, n_params - 1, z0)], hi = w[wslot(s2 + 1, n_params - 1, z1)];
+                t[b].x = z0 ? 0.0 : lo;
+                t[b].y = z1 ? 0.0 : hi;
+            }
+#pragma unroll
+            for (int b = 0; b < kTB; ++b)
+                if (q0 + b * nthr < T2) dst[q0 + b * nthr] = t[b];
+        }
+    } else if (V == 1) {
+        for (int q0 = int(threadIdx.x); q0 < T2; q0 += kTB * nthr) {
+            double2 t[kTB];
+#pragma unroll
+            for (int b = 0; b < kTB; ++b) t[b] = tab[min(q0 + b * nthr, T2 - 1)];
+#pragma unroll
+            for (int b = 0; b < kTB; ++b)
+                if (q0 + b * nthr < T2) dst[q0 + b * nthr] = t[b];
+        }
+    } else {
+        const int lane = int(threadIdx.x) % 64, wv = int(threadIdx.x) / 64, nwv = nthr / 64;
+        for (int p = wv; p * 64 < T2; p += nwv) {   // 1 KiB pieces, one per wave in turn
+            const int q = min(p * 64 + lane, T2 - 1);
+            __builtin_amdgcn_global_load_lds((glb_void*)(tab + q), (lds_void*)(dst + p * 64), 16, 0, 0);
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __syncthreads();
+    if (lds[(threadIdx.x * 7) % d_tab] == 1234.5) out[blockIdx.x] = 1.0;
+}
+
+int main() {
+    const int n_params = 9216 + 200;
+    const int d_tab = n_params + n_params / (kPeriod - 1) + 2;
+    const int T2 = (d_tab + 1) / 2;
+    std::vector<double> hw(n_params), ht(size_t(T2) * 2, 0.0);
+    for (int j = 0; j < n_params; ++j) hw[j] = 0.001 * j;
+    for (int s = 0; s < 2 * T2; ++s) {
+        const int j = s - 1 - s / kPeriod;
+        if (s % kPeriod != 0 && j < n_params) ht[s] = hw[j];
+    }
+    double *w, *out;
+    double2* tab;
+    CK(hipMalloc(&w, n_params * 8));
+    CK(hipMalloc(&tab, T2 * 16));
+    CK(hipMalloc(&out, 4096 * 8));
+    CK(hipMemcpy(w, hw.data(), n_params * 8, hipMemcpyHostToDevice));
+    CK(hipMemcpy(tab, ht.data(), T2 * 16, hipMemcpyHostToDevice));
+    const size_t lds = size_t(T2) * 16;
+    printf("table %d slots, %zu bytes of LDS\n", d_tab, lds);
+    CK(hipFuncSetAttribute((const void*)stage<0>, hipFuncAttributeMaxDynamicSharedMemorySize, int(lds)));
+    CK(hipFuncSetAttribute((const void*)stage<1>, hipFuncAttributeMaxDynamicSharedMemorySize, int(lds)));
+    CK(hipFuncSetAttribute((const void*)stage<2>, hipFuncAttributeMaxDynamicSharedMemorySize, int(lds)));
+    hipEvent_t e0, e1;
+    CK(hipEventCreate(&e0));
+    CK(hipEventCreate(&e1));
+    const char* names[3] = {"gather", "contig", "dma"};
+    for (int v = 0; v < 3; ++v)
+        for (int shape = 0; shape < 2; ++shape) {
+            const int blocks = shape == 0 ? 512 : 256, thr = shape == 0 ? 512 : 1024;
+            auto go = [&] {
+                if (v == 0) hipLaunchKernelGGL(stage<0>, dim3(blocks), dim3(thr), lds, 0, w, tab, n_params, d_tab, out);
+                if (v == 1) hipLaunchKernelGGL(stage<1>, dim3(blocks), dim3(thr), lds, 0, w, tab, n_params, d_tab, out);
+                if (v == 2) hipLaunchKernelGGL(stage<2>, dim3(blocks), dim3(thr), lds, 0, w, tab, n_params, d_tab, out);
+            };
+            for (int r = 0; r < 20; ++r) go();
+            CK(hipDeviceSynchronize());
+            CK(hipEventRecord(e0, 0));
+            for (int r = 0; r < 100; ++r) go();
+            CK(hipEventRecord(e1, 0));
+            CK(hipEventSynchronize(e1));
+            float ms = 0;
+            CK(hipEventElapsedTime(&ms, e0, e1));
+            printf("%-7s %3d x %4d: %.2f us per launch (events over 100 back-to-back launches)\n", names[v], blocks, thr,
+                   ms * 10.0);
+        }
+    return 0;
+}

@@ -3730,6 +3730,76 @@ static int qn_run_impl(wfsa_dev* ctx, double eta, double tol, int32_t max_steps,
             }
             std::fprintf(stderr, "\n");
         }
+        // the deal's calibration: each wave's stream-phase end (stamp 4, from
+        // its staging stamp) against its delta rows and its extra work, by
+        // least squares: end = c0 + c1 rows + cA [class A] + cB [class B] +
+        // cG [big] + cQ [QN wave]; the implied charges in rows are cX / c1
+        if (ctx->delta_on && ctx->d_wave_first.ptr && ctx->d_g_base.ptr) {
+            std::vector<int32_t> wf(size_t(nw) + 1);
+            std::vector<int64_t> gb(size_t(ctx->n_groups) + 1);
+            HIP_TRY(ctx->d_wave_first.download(wf.data(), wf.size(), s));
+            HIP_TRY(ctx->d_g_base.download(gb.data(), gb.size(), s));
+            HIP_TRY(hipStreamSynchronize(s));
+            const int64_t ns = int64_t(ctx->n_small4) + ctx->n_small;
+            double M[6][6] = {}, v[6] = {};
+            double sums[5][3] = {};   // per kind: n, rows, end
+            for (int w = 0; w < nw; ++w) {
+                const int wib = w % wpb, bid = w / wpb;
+                const unsigned long long* r = &t[size_t(w) * 16];
+                if (!r[1] || !r[4] || (bid == 0 && wib == wpb - 1)) continue;
+                const double end = double(r[4] - r[1]) / 100.0;
+                const double rows = double(gb[size_t(wf[size_t(w) + 1])] - gb[size_t(wf[size_t(w)])]) / kWave;
+                double x[6] = {1.0, rows, 0, 0, 0, 0};
+                const int64_t b0 = (int64_t(wib) * ctx->i_grid + bid) * kWave;
+                int kind = 0;
+                if (wib < small_wpb && b0 < ns) {
+                    kind = b0 + kWave > ctx->n_small4 ? 2 : 1;
+                    x[kind + 1] = 1.0;
+                }
+                int64_t rb = (ctx->i_grid - 1 - bid) + int64_t(ctx->i_grid) * (wpb - 1 - wib);
+                rb -= rb > ctx->i_grid - 1 ? 1 : 0;
+                if (rb < ctx->n_big) {
+                    x[4] = 1.0;
+                    kind = kind ? kind : 3;
+                }
+                if (wib == wpb - 2 && bid < ctx->qw_waves) {
+                    x[5] = 1.0;
+                    kind = 4;
+                }
+                sums[kind][0] += 1;
+                sums[kind][1] += rows;
+                sums[kind][2] += end;
+                for (int i = 0; i < 6; ++i) {
+                    v[i] += x[i] * end;
+                    for (int j = 0; j < 6; ++j) M[i][j] += x[i] * x[j];
+                }
+            }
+            for (int i = 0; i < 6; ++i) M[i][i] += 1e-9;   // (a kind absent: its coefficient 0)
+            for (int c = 0; c < 6; ++c) {   // Gauss-Jordan
+                int p = c;
+                for (int i = c + 1; i < 6; ++i)
+                    if (std::abs(M[i][c]) > std::abs(M[p][c])) p = i;
+                for (int j = 0; j < 6; ++j) std::swap(M[c][j], M[p][j]);
+                std::swap(v[c], v[p]);
+                for (int i = 0; i < 6; ++i) {
+                    if (i == c || M[c][c] == 0.0) continue;
+                    const double f = M[i][c] / M[c][c];
+                    for (int j = 0; j < 6; ++j) M[i][j] -= f * M[c][j];
+                    v[i] -= f * v[c];
+                }
+            }
+            double cf[6];
+            for (int i = 0; i < 6; ++i) cf[i] = M[i][i] != 0.0 ? v[i] / M[i][i] : 0.0;
+            const char* kn[5] = {"stream only", "class A", "class B", "big", "QN"};
+            std::fprintf(stderr, "[fbs-trace] deal fit: end = %.2f + %.4f rows us; charges in rows: A %.1f B %.1f big %.1f "
+                         "QN %.1f\n[fbs-trace] deal by kind (n, mean rows, mean end us):", cf[0], cf[1], cf[2] / cf[1],
+                         cf[3] / cf[1], cf[4] / cf[1], cf[5] / cf[1]);
+            for (int k = 0; k < 5; ++k)
+                if (sums[k][0] > 0)
+                    std::fprintf(stderr, " %s (%.0f, %.1f, %.2f)", kn[k], sums[k][0], sums[k][1] / sums[k][0],
+                                 sums[k][2] / sums[k][0]);
+            std::fprintf(stderr, "\n");
+        }
         // the slowest bubble waves and QN waves
         auto dt = [&](int w, int a, int b) {
             const unsigned long long x = t[size_t(w) * 16 + size_t(a)], y = t[size_t(w) * 16 + size_t(b)];

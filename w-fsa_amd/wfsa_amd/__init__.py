@@ -370,12 +370,17 @@ def _host_callback(allreduce):
 
 def torch_allreduce(arr, op):
     """all-reduce a numpy array in place over the default torch.distributed
-    process group (gloo for host buffers)"""
+    process group (gloo for host buffers).  A member that stalls without
+    aborting: the wait gives up after WFSA_COMM_TIMEOUT_S (default 300 s, the
+    library's host watchdog limit) and raises -- the library then fails the
+    call and treats the group as broken (collective.hip HostCollective)"""
+    import datetime
     import torch
     import torch.distributed as dist
     red = {"sum": dist.ReduceOp.SUM, "min": dist.ReduceOp.MIN, "max": dist.ReduceOp.MAX}[op]
     t = torch.from_numpy(arr)
-    dist.all_reduce(t, op=red)
+    limit = float(os.environ.get("WFSA_COMM_TIMEOUT_S", "300"))
+    dist.all_reduce(t, op=red, async_op=True).wait(timeout=datetime.timedelta(seconds=limit))
 
 
 class Device:
