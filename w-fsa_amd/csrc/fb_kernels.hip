@@ -2601,19 +2601,25 @@ __global__ __launch_bounds__(1024, (DBG == 10 ? 8 : 1)) WFSA_FBS_ATTR void fbs_k
     constexpr int kTB = 12;   // 16-byte pieces per thread and round (one round for 12k-entry tables at 512 threads)
     const bool pre = DELTA && !a.no_streams && DBG != 4 && DBG != 11 && !early;
     const int tlast = a.n_params - 1;
-    auto wslot = [&](int s, bool& zero) {   // slot s of the remapped table: weight s - 1 - s / kDeltaPeriod, or zero
-        const int j = s - 1 - s / kDeltaPeriod;
-        zero = (s % kDeltaPeriod) == 0 || j > tlast;
-        return min(max(j, 0), tlast);
-    };
+    // A piece is slots (s2, s2 + 1): weights j0 = s2 - 1 - s2 / kDeltaPeriod
+    // and j0 + 1 whenever neither slot is a zero slot, and on a period
+    // boundary one of the two is zero and the other is still w[j0] or
+    // w[j0 + 1] -- so one 16-byte load of (w[j0], w[j0 + 1]) serves every
+    // piece (8-byte aligned; w holds n_params + 2 doubles, so j0 + 1 <=
+    // tlast + 1 stays inside), the zeros by selects: half the load
+    // instructions of two 8-byte gathers (the staging 5.4 -> ~3.4 us in
+    // tools/micro/stage_table.hip, profiles/r05)
     auto table_round = [&](int q0, int nthr, double2 (&t)[kTB]) {
 #pragma unroll
         for (int b = 0; b < kTB; ++b) {
             const int s2 = 2 * (q0 + b * nthr);
-            bool z0, z1;
-            const double lo = a.w[wslot(s2, z0)], hi = a.w[wslot(s2 + 1, z1)];
-            t[b].x = z0 ? 0.0 : lo;
-            t[b].y = z1 ? 0.0 : hi;
+            const int j0 = s2 - 1 - s2 / kDeltaPeriod;
+            const int jc = min(max(j0, 0), tlast);
+            const double2 v = *reinterpret_cast<const double2*>(a.w + jc);
+            const bool z0 = (s2 % kDeltaPeriod) == 0 || j0 > tlast;
+            const bool z1 = ((s2 + 1) % kDeltaPeriod) == 0 || j0 + 1 > tlast;
+            t[b].x = z0 ? 0.0 : v.x;
+            t[b].y = z1 ? 0.0 : (j0 < 0 ? v.x : v.y);
         }
     };
     double2 t0[kTB];
