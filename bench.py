@@ -340,6 +340,10 @@ def roofline_of(m, traffic):
         achieved = alg_bytes / (kern_ms * 1e-3) / 1e9 if kern_ms > 0 else None   # None: WFSA_TIMING=0
         return {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": achieved / HBM_PEAK_GBS if achieved else None, "traffic": traffic,
+                "traffic_source": ("a committed lease measurement, not taken in this run: "
+                                   "profiles/traffic_latest.json (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes "
+                                   "over bench.py on this kernel, corrected per MI355X_MICROARCH.md, per launch)")
+                if traffic else None,
                 "kernel": "fbs_kernel (compiled-stream forward pass + fused bubbles, per step)",
                 "timed_launches": timed, "kernel_ms_per_launch": kern_ms, "all_fb_kernels_ms_per_step": fb_ms,
                 "algorithmic_bytes_per_launch": alg_bytes,
@@ -462,7 +466,8 @@ def main():
     traffic = None
     if not wl["dense"] and wl["emissions"] == 1 and os.path.exists(args.profile_traffic):
         try:
-            traffic = json.load(open(args.profile_traffic)).get("hbm_bytes_per_launch")
+            tj = json.load(open(args.profile_traffic))
+            traffic = tj.get("hbm_bytes_per_launch")
         except Exception:
             traffic = None
 

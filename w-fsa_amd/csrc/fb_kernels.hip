@@ -2942,6 +2942,19 @@ __global__ __launch_bounds__(1024, (DBG == 10 ? 8 : 1)) WFSA_FBS_ATTR void fbs_k
     __shared__ double wsum[1024 / kWave];
     ll_acc = wave_sum(ll_acc);
     if (lane == 0) wsum[w] = ll_acc;
+    // the QN waves, their stream share done: this step's QN update, after
+    // the block barrier, or (qw.pre_barrier) before it -- then it polls while
+    // the block's other waves still stream, which measured far slower unless
+    // the QN waves carry a full stream share (profiles/r05/qn_order_sweep.txt)
+    const bool qn_wave = QN && w == wpb - 2 && bid < a.qw.n_waves;
+    auto qn_run = [&]() {
+#ifdef WFSA_EXPERIMENTS
+        qn_wave_run(a.qw, bid, tr);
+#else
+        qn_wave_run(a.qw, bid, nullptr);
+#endif
+    };
+    if (qn_wave && a.qw.pre_barrier) qn_run();
     __syncthreads();
     if (threadIdx.x == 0) {
         double t = 0.0;
@@ -2951,14 +2964,7 @@ __global__ __launch_bounds__(1024, (DBG == 10 ? 8 : 1)) WFSA_FBS_ATTR void fbs_k
     // this block's slice of the per-edge weights and the zeroed result, for
     // the kernels after this one (nothing in this launch reads them)
     if (W_LDS && !a.no_streams && !a.no_slice) edge_weight_slice(a, bid, nblk);
-    // the QN waves, their stream share done: this step's QN update
-    if (QN && w == wpb - 2 && bid < a.qw.n_waves) {
-#ifdef WFSA_EXPERIMENTS
-        qn_wave_run(a.qw, bid, tr);
-#else
-        qn_wave_run(a.qw, bid, nullptr);
-#endif
-    }
+    if (qn_wave && !a.qw.pre_barrier) qn_run();
     WFSA_STAMP(7)
 #undef WFSA_STAMP
 }

@@ -371,6 +371,7 @@ struct wfsa_dev {
     bool bub_prio = true;            // WFSA_BUB_PRIO=0: the fused small bubbles at normal wave priority
     int32_t qw_waves = 0;            // reserved at preparation
     double qw_cost = 8.0;            // the dealer's charge per QN wave, in stream rows (WFSA_QN_COST)
+    bool qw_pre_barrier = false;     // the QN waves before the block's end barrier (WFSA_QN_PRE_BARRIER=1)
     bool qw_ok = false;              // batches built for the current preparation and QN set-up
     int32_t qw_nbatch = 0;
     DevBuf<int4> qw_batch;
@@ -2615,6 +2616,7 @@ int enqueue_qn_step(wfsa_dev* ctx, double eta, double tol, int64_t e, bool timed
         w.n_waves = ctx->qw_waves;
         w.parity = int32_t(ctx->qw_seq & 1u);
         w.n_arrive = ctx->i_grid;
+        w.pre_barrier = ctx->qw_pre_barrier ? 1 : 0;
         w.batch = ctx->qw_batch.ptr;
         w.con_of = ctx->qw_con_of.ptr;
         w.mfirst = ctx->qw_mfirst.ptr;
@@ -2939,6 +2941,7 @@ int wfsa_dev_create(int device, wfsa_dev** out) {
     if (const char* e = std::getenv("WFSA_DEFER_PREFETCH")) ctx->defer_prefetch = e[0] == '1';
     if (const char* e = std::getenv("WFSA_BUB_PRIO")) ctx->bub_prio = e[0] != '0';
     if (const char* e = std::getenv("WFSA_QN_COST")) ctx->qw_cost = std::atof(e);
+    if (const char* e = std::getenv("WFSA_QN_PRE_BARRIER")) ctx->qw_pre_barrier = e[0] == '1';
 
     HIP_TRY(hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking));
     if (const char* e = std::getenv("WFSA_PIPE")) ctx->use_pipe = e[0] == '1';
