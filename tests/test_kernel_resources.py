@@ -1,0 +1,46 @@
+"""Register budget of the stream kernel (fb_kernels.hip fbs_kernel): every
+variant the device QN loop launches must fit 128 VGPRs without spilling.
+A spill put the in-kernel QN variant's scratch at 1,184 bytes per lane and
+the c3 step from 29 to 116 us (round 5), with every parity test still green
+-- so the compiler's own resource report is checked here, on the CPU
+(hipcc cross-compiles gfx950)."""
+import os
+import re
+import shutil
+import subprocess
+
+import pytest
+
+from conftest import ROOT
+
+CSRC = os.path.join(ROOT, "w-fsa_amd", "csrc")
+
+
+@pytest.mark.skipif(shutil.which("hipcc") is None, reason="hipcc not installed")
+def test_stream_kernel_variants_do_not_spill(tmp_path):
+    cmd = ["hipcc", "-O3", "-std=c++17", "-fPIC", "-I" + os.path.join(ROOT, "include"), "--offload-arch=gfx950",
+           "-munsafe-fp-atomics", "-c", os.path.join(CSRC, "fb_kernels.hip"), "-o", str(tmp_path / "fb.o"),
+           "-Rpass-analysis=kernel-resource-usage"]
+    out = subprocess.run(cmd, capture_output=True, text=True, timeout=900)
+    assert out.returncode == 0, out.stderr[-2000:]
+    kernels = {}
+    name = None
+    for line in out.stderr.splitlines():
+        m = re.search(r"Function Name: (\S+)", line)
+        if m:
+            name = m.group(1)
+            kernels[name] = {}
+            continue
+        m = re.search(r"remark:\s+(VGPRs Spill|ScratchSize \[bytes/lane\]): (\d+)", line)
+        if m and name:
+            kernels[name][m.group(1)] = int(m.group(2))
+    # fbs_kernel<WIDE, W_LDS, MULTI, DBG=0, RMIN, DELTA, QN>: the release variants
+    fbs = {k: v for k, v in kernels.items() if "fbs_kernel" in k and "Li0E" in k}
+    assert len(fbs) >= 8, sorted(kernels)
+    bad = {k: v for k, v in fbs.items() if v.get("VGPRs Spill", 0) > 0}
+    assert not bad, f"stream kernel variants spilling VGPRs: {bad}"
+    # the delta-format variants without the rmin column (the c3 headline, with and without the QN
+    # waves) use no scratch at all (the rmin ones keep 80 bytes of indexed arrays there)
+    delta = {k: v for k, v in fbs.items() if re.search(r"Li0ELb0ELb1ELb[01]E", k)}
+    assert delta, sorted(fbs)
+    assert all(v.get("ScratchSize [bytes/lane]", 0) == 0 for v in delta.values()), delta

@@ -2547,6 +2547,8 @@ __device__ __forceinline__ void qn_wave_run(const QnWave& q, int r, unsigned lon
     int ok = 1;
     if (lane == 0) {
         unsigned it = 0;
+        // (every QN wave polls the one counter: a go token per wave's own
+        // line, written by the last arrival, measured no faster, r05)
         while (load_wt(q.arrive + q.parity) < unsigned(q.n_arrive)) {
             __builtin_amdgcn_s_sleep(1);
             if (++it > kQnPollLimit) {
@@ -2942,19 +2944,6 @@ __global__ __launch_bounds__(1024, (DBG == 10 ? 8 : 1)) WFSA_FBS_ATTR void fbs_k
     __shared__ double wsum[1024 / kWave];
     ll_acc = wave_sum(ll_acc);
     if (lane == 0) wsum[w] = ll_acc;
-    // the QN waves, their stream share done: this step's QN update, after
-    // the block barrier, or (qw.pre_barrier) before it -- then it polls while
-    // the block's other waves still stream, which measured far slower unless
-    // the QN waves carry a full stream share (profiles/r05/qn_order_sweep.txt)
-    const bool qn_wave = QN && w == wpb - 2 && bid < a.qw.n_waves;
-    auto qn_run = [&]() {
-#ifdef WFSA_EXPERIMENTS
-        qn_wave_run(a.qw, bid, tr);
-#else
-        qn_wave_run(a.qw, bid, nullptr);
-#endif
-    };
-    if (qn_wave && a.qw.pre_barrier) qn_run();
     __syncthreads();
     if (threadIdx.x == 0) {
         double t = 0.0;
@@ -2964,7 +2953,16 @@ __global__ __launch_bounds__(1024, (DBG == 10 ? 8 : 1)) WFSA_FBS_ATTR void fbs_k
     // this block's slice of the per-edge weights and the zeroed result, for
     // the kernels after this one (nothing in this launch reads them)
     if (W_LDS && !a.no_streams && !a.no_slice) edge_weight_slice(a, bid, nblk);
-    if (qn_wave && !a.qw.pre_barrier) qn_run();
+    // the QN waves, their stream share done: this step's QN update (after
+    // the block barrier; a second call site before it, as an option, made
+    // the kernel spill 96 VGPRs)
+    if (QN && w == wpb - 2 && bid < a.qw.n_waves) {
+#ifdef WFSA_EXPERIMENTS
+        qn_wave_run(a.qw, bid, tr);
+#else
+        qn_wave_run(a.qw, bid, nullptr);
+#endif
+    }
     WFSA_STAMP(7)
 #undef WFSA_STAMP
 }

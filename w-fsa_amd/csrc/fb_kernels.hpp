@@ -605,7 +605,6 @@ struct QnWave {
     int32_t n_waves;             // QN waves: wave wpb - 2 of blocks [0, n_waves)
     int32_t parity;
     int32_t n_arrive;            // arrivals to wait for (the grid's blocks)
-    int32_t pre_barrier;         // run before the block's end barrier (WFSA_QN_PRE_BARRIER=1), else after it
     const int4* batch;           // [n_batches][2] (first constraint, end constraint, first member, end member),
                                  // (slot chunks, their first slot: low, high word, 0)
     const int32_t* con_of;       // [n] constraint of each member (trimmed order)

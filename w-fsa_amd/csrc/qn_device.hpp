@@ -133,6 +133,9 @@ __device__ __forceinline__ double load_wt(const double* p) {
 __device__ __forceinline__ unsigned load_wt(const unsigned* p) {
     return __hip_atomic_load(const_cast<unsigned*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
+__device__ __forceinline__ void store_wt(unsigned* p, unsigned v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
 
 // the info row of a step into its host ring slot, then the flag; the
 // system-scope release orders the row before the flag.  The sequence counter

@@ -370,8 +370,7 @@ struct wfsa_dev {
     bool defer_prefetch = false;     // WFSA_DEFER_PREFETCH=1: the first row set after the table / bubble loads
     bool bub_prio = true;            // WFSA_BUB_PRIO=0: the fused small bubbles at normal wave priority
     int32_t qw_waves = 0;            // reserved at preparation
-    double qw_cost = 8.0;            // the dealer's charge per QN wave, in stream rows (WFSA_QN_COST)
-    bool qw_pre_barrier = false;     // the QN waves before the block's end barrier (WFSA_QN_PRE_BARRIER=1)
+    double qw_cost = 6.0;            // the dealer's charge per QN wave, in stream rows (WFSA_QN_COST)
     bool qw_ok = false;              // batches built for the current preparation and QN set-up
     int32_t qw_nbatch = 0;
     DevBuf<int4> qw_batch;
@@ -1832,11 +1831,14 @@ int prepare(wfsa_dev* ctx, int level) {
         ctx->h_sm_list.clear();
         ctx->h_big_list.clear();
     }
-    // the delta deal's bubble charges from the classified bubbles: a wave of
-    // class-B small bubbles (8 nodes / edges: about twice a class-A wave's
-    // time, profiles/r05) costs more stream rows than a class-A one
+    // the delta deal's bubble charges from the classified bubbles, in delta
+    // rows: fitted to the waves' measured stream-phase ends (the experiments
+    // build's deal fit: end = c0 + c1 rows + a charge per kind of extra work)
+    // and then swept round-robin on one box (profiles/r05/dealer_fit.txt):
+    // class A 9, class B 17, big 13, the QN wave 6 -- c3 29.6 -> 28.1 us per
+    // step against the earlier 18 / 36 / 8 / 8
     {
-        double small_cost = 18.0, small_cost_b = 36.0, big_cost = 8.0;
+        double small_cost = 9.0, small_cost_b = 17.0, big_cost = 13.0;
         if (const char* e = std::getenv("WFSA_SMALL_COST")) small_cost = std::atof(e);
         if (const char* e = std::getenv("WFSA_SMALL_COST_B")) small_cost_b = std::atof(e);
         if (const char* e = std::getenv("WFSA_BIG_COST")) big_cost = std::atof(e);
@@ -2616,7 +2618,6 @@ int enqueue_qn_step(wfsa_dev* ctx, double eta, double tol, int64_t e, bool timed
         w.n_waves = ctx->qw_waves;
         w.parity = int32_t(ctx->qw_seq & 1u);
         w.n_arrive = ctx->i_grid;
-        w.pre_barrier = ctx->qw_pre_barrier ? 1 : 0;
         w.batch = ctx->qw_batch.ptr;
         w.con_of = ctx->qw_con_of.ptr;
         w.mfirst = ctx->qw_mfirst.ptr;
@@ -2941,7 +2942,6 @@ int wfsa_dev_create(int device, wfsa_dev** out) {
     if (const char* e = std::getenv("WFSA_DEFER_PREFETCH")) ctx->defer_prefetch = e[0] == '1';
     if (const char* e = std::getenv("WFSA_BUB_PRIO")) ctx->bub_prio = e[0] != '0';
     if (const char* e = std::getenv("WFSA_QN_COST")) ctx->qw_cost = std::atof(e);
-    if (const char* e = std::getenv("WFSA_QN_PRE_BARRIER")) ctx->qw_pre_barrier = e[0] == '1';
 
     HIP_TRY(hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking));
     if (const char* e = std::getenv("WFSA_PIPE")) ctx->use_pipe = e[0] == '1';
