@@ -2463,17 +2463,40 @@ __device__ __forceinline__ void qn_wave_batch(const QnWave& q, const QnBatchIn& 
     // the batch's bubble contribution chunks (stored write-through by this
     // launch's bubble waves: sc1 loads), one per lane per round, each summed
     // by chunk_tree; then every member adds its chunks' sums in chunk order
+    // Eight lanes read a chunk (lane piece = two consecutive slots, so a load
+    // instruction covers eight whole chunks, 1 KiB, instead of 64 lanes each
+    // on its own chunk's line) and reduce it by xor shuffles in chunk_tree's
+    // order; chunk 64 r + l's sum then moves to lane l of round r
     double cs[kQnWaveChunkRounds];
 #pragma unroll
-    for (int r = 0; r < kQnWaveChunkRounds; ++r) {
-        cs[r] = 0.0;
-        const int qc = r * kWave + lane;
-        if (r * kWave < nchunk && qc < nchunk) {
-            double v[kSlotChunk];
+    for (int r = 0; r < kQnWaveChunkRounds; ++r) cs[r] = 0.0;
+    const int sub = lane & 7;
+#pragma nounroll
+    for (int r = 0; r < kQnWaveChunkRounds; ++r) {   // (a round at a time: 16 loads in flight, no spills)
+        if (r * kWave >= nchunk) break;   // (uniform)
+        double s8[8];
 #pragma unroll
-            for (int k = 0; k < kSlotChunk; ++k) v[k] = load_wt(q.contrib + cbase + int64_t(kSlotChunk) * qc + k);
-            cs[r] = chunk_tree(v);
+        for (int k = 0; k < 8; ++k) {
+            const int c = r * kWave + 8 * k + (lane >> 3);
+            const double* p = q.contrib + cbase + int64_t(kSlotChunk) * c + 2 * sub;
+            s8[k] = c < nchunk ? load_wt(p) : 0.0;
+            const double hi = c < nchunk ? load_wt(p + 1) : 0.0;
+            s8[k] += hi;   // p_sub = x[2 sub] + x[2 sub + 1]
         }
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+#pragma unroll
+            for (int o = 1; o < 8; o <<= 1) s8[k] += __shfl_xor(s8[k], o, kWave);
+        }
+        double v = 0.0;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            const double t = __shfl(s8[k], sub * 8, kWave);
+            if (k == (lane >> 3)) v = t;
+        }
+#pragma unroll
+        for (int i = 0; i < kQnWaveChunkRounds; ++i)   // (static indices: the array stays in registers)
+            if (i == r) cs[i] = v;
     }
     double sm = 0.0;
     for (int t = 0; t < maxnch; ++t) {
