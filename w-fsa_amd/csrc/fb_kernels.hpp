@@ -564,6 +564,7 @@ struct BubbleArgs {
     int32_t dbg;             // timing experiments only (WFSA_BUB_DBG): 1 no slot stores, 2 no weight gathers
     int32_t wt;              // contribution slots stored write-through (sc1): read in the same launch (QnWave)
     int32_t prio;            // fused small bubbles at raised wave priority (s_setprio 2)
+    int32_t early_big;       // the stream kernel's big-bubble waves run their bubble at entry, beside the staging
 };
 
 // Compiled streams of the per-iteration kernels.

@@ -369,6 +369,7 @@ struct wfsa_dev {
     bool stream_nt = false;          // WFSA_STREAM_NT=1: the stream kernel's rows loaded non-temporal
     bool defer_prefetch = false;     // WFSA_DEFER_PREFETCH=1: the first row set after the table / bubble loads
     bool bub_prio = true;            // WFSA_BUB_PRIO=0: the fused small bubbles at normal wave priority
+    bool early_big = false;          // WFSA_EARLY_BIG=1: the big-bubble waves start at entry (fb_kernels.hip)
     int32_t qw_waves = 0;            // reserved at preparation
     double qw_cost = 6.0;            // the dealer's charge per QN wave, in stream rows (WFSA_QN_COST)
     bool qw_ok = false;              // batches built for the current preparation and QN set-up
@@ -2079,6 +2080,7 @@ int enqueue_compiled(wfsa_dev* ctx, bool with_grad, bool want_logq, const unsign
             }
             c.bub_on = 1;
             c.bub.prio = ctx->bub_prio ? 1 : 0;
+            c.bub.early_big = ctx->early_big ? 1 : 0;
             c.early_bub = ctx->early_bub ? 1 : 0;
             c.bub.small_wpb = small_waves_per_block(ctx->n_small4 + ctx->n_small, ctx->i_grid);
             if (ctx->n_big > 0) {
@@ -2941,6 +2943,7 @@ int wfsa_dev_create(int device, wfsa_dev** out) {
     if (const char* e = std::getenv("WFSA_STREAM_NT")) ctx->stream_nt = e[0] == '1';
     if (const char* e = std::getenv("WFSA_DEFER_PREFETCH")) ctx->defer_prefetch = e[0] == '1';
     if (const char* e = std::getenv("WFSA_BUB_PRIO")) ctx->bub_prio = e[0] != '0';
+    if (const char* e = std::getenv("WFSA_EARLY_BIG")) ctx->early_big = e[0] == '1';
     if (const char* e = std::getenv("WFSA_QN_COST")) ctx->qw_cost = std::atof(e);
 
     HIP_TRY(hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking));
