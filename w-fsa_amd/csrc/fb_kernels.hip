@@ -2326,9 +2326,9 @@ __global__ __launch_bounds__(kBubbleBlock) void bubble_kernel(BubbleArgs a) {
         ll_acc = big_bubble(a, gw, lsd[wib], lw[wib], lv[wib], lab[wib]);
     } else {
         // class A (4 nodes / 4 edges: most bubbles) first, then class B
-        const int b = (gw - a.n_big) * kWave + lane;
-        if (b < a.n_small4) ll_acc = small_bubble<4, 4, RMIN>(a, a.sm4_tbl, a.n_small4, b, b);
-        else if (b < a.n_small4 + a.n_small)
+        const int b = int(small_entry(gw - a.n_big, lane, a.n_small4, a.n_small));
+        if (b >= 0 && b < a.n_small4) ll_acc = small_bubble<4, 4, RMIN>(a, a.sm4_tbl, a.n_small4, b, b);
+        else if (b >= a.n_small4)
             ll_acc = small_bubble<8, 8, RMIN>(a, a.sm_tbl, a.n_small, b - a.n_small4, b);
     }
     ll_acc = wave_sum(ll_acc);
@@ -2438,7 +2438,8 @@ __device__ __forceinline__ QnBatchIn qn_wave_load(const QnWave& q, int b) {
     return in;
 }
 
-__device__ __forceinline__ void qn_wave_batch(const QnWave& q, const QnBatchIn& in, bool ok, const unsigned& halt) {
+__device__ __forceinline__ void qn_wave_batch(const QnWave& q, const QnBatchIn& in, bool ok, const unsigned& halt,
+                                              unsigned long long* tr = nullptr) {   // (tr: timing experiments, stamps 8-11)
 #pragma clang fp contract(off)
     const int lane = lane_id();
     const int c0 = in.c0, nc = in.nc, m0 = in.m0, m1 = in.m1, nchunk = in.nchunk;
@@ -2498,6 +2499,7 @@ __device__ __forceinline__ void qn_wave_batch(const QnWave& q, const QnBatchIn& 
         for (int i = 0; i < kQnWaveChunkRounds; ++i)   // (static indices: the array stays in registers)
             if (i == r) cs[i] = v;
     }
+    if (tr && lane_id() == 0) tr[8] = __builtin_amdgcn_s_memrealtime();
     double sm = 0.0;   // the member's chunk sums in chunk order, four chunks' shuffles per round
     for (int t0 = 0; t0 < maxnch; t0 += 4) {
         double v[4];
@@ -2544,6 +2546,7 @@ __device__ __forceinline__ void qn_wave_batch(const QnWave& q, const QnBatchIn& 
     }
     const double laux_l = r / (gg + 1.0);
     const double g = __shfl(gg, ld, kWave), laux = __shfl(laux_l, ld, kWave);
+    if (tr && lane == 0) tr[9] = __builtin_amdgcn_s_memrealtime();
     // the previous step's halt decision (loaded beside the chunks): a halted
     // run skips this step -- no update at all (qn_wave_run publishes it)
     if (halt != 0u) return;
@@ -2557,6 +2560,7 @@ __device__ __forceinline__ void qn_wave_batch(const QnWave& q, const QnBatchIn& 
         q.w_next[fo] = xn;   // GetWeight for the next step
         q.ewp_next[fo] = exp(xn);
     }
+    if (tr && lane == 0) tr[10] = __builtin_amdgcn_s_memrealtime();
     double ge = 0.0;
     for (int t0 = 0; t0 < maxnm; t0 += 8) {
         double v[8];
@@ -2607,7 +2611,7 @@ __device__ __forceinline__ void qn_wave_run(const QnWave& q, int r, unsigned lon
     // the halt decision of this launch's finish wave: issued now, waited for
     // only before the first store (beside the batch's chunk loads)
     const unsigned halt = ok ? load_wt(q.halted + 1) : 0u;
-    if (r < q.n_batches) qn_wave_batch(q, first, ok != 0, halt);
+    if (r < q.n_batches) qn_wave_batch(q, first, ok != 0, halt, tr);
     for (int b = r + q.n_waves; b < q.n_batches && halt == 0u; b += q.n_waves)
         qn_wave_batch(q, qn_wave_load(q, b), ok != 0, halt);
     if (halt != 0u && r == 0 && lane == 0) {   // the previous step halted: this one is skipped
@@ -2785,7 +2789,7 @@ __global__ __launch_bounds__(1024, (DBG == 10 ? 8 : 1)) WFSA_FBS_ATTR void fbs_k
         stored = true;
         // chunk w * nblk + bid: consecutive chunks (one class, one cost) on
         // different blocks, so the costly class-B chunks spread over the CUs
-        const int b = (w * nblk + bid) * kWave + lane;
+        const int b = int(small_entry(int64_t(w) * nblk + bid, lane, a.bub.n_small4, a.bub.n_small));
 #ifdef WFSA_EXPERIMENTS
         unsigned long long* btr = tr;
 #else
@@ -2794,8 +2798,8 @@ __global__ __launch_bounds__(1024, (DBG == 10 ? 8 : 1)) WFSA_FBS_ATTR void fbs_k
         // (the bubbles are on the QN update's critical path; the stream waves
         // beside them mostly wait for memory: the bubble waves issue first)
         if (a.bub.prio) __builtin_amdgcn_s_setprio(2);
-        if (b < a.bub.n_small4) ll_acc += small_bubble<4, 4, RMIN>(a.bub, a.bub.sm4_tbl, a.bub.n_small4, b, b, btr);
-        else if (b < a.bub.n_small4 + a.bub.n_small)
+        if (b >= 0 && b < a.bub.n_small4) ll_acc += small_bubble<4, 4, RMIN>(a.bub, a.bub.sm4_tbl, a.bub.n_small4, b, b, btr);
+        else if (b >= a.bub.n_small4)
             ll_acc += small_bubble<8, 8, RMIN>(a.bub, a.bub.sm_tbl, a.bub.n_small, b - a.bub.n_small4, b, btr);
         if (a.bub.prio) __builtin_amdgcn_s_setprio(0);
     };
@@ -3556,10 +3560,10 @@ static hipError_t launch_compiled_impl(const CompiledArgs& a, int grid, int bloc
     return hipGetLastError();
 }
 
-int bubble_waves(int32_t n_small, int32_t n_big) { return n_big + (n_small + kWave - 1) / kWave; }
+int bubble_waves(int32_t n_small4, int32_t n_small, int32_t n_big) { return n_big + int(small_chunks(n_small4, n_small)); }
 
 hipError_t launch_bubbles(const BubbleArgs& a, hipStream_t stream) {
-    const int waves = bubble_waves(a.n_small4 + a.n_small, a.n_big);
+    const int waves = bubble_waves(a.n_small4, a.n_small, a.n_big);
     if (waves <= 0) return hipSuccess;
     constexpr int WPB = kBubbleBlock / kWave;
     if (a.rmin_acc)

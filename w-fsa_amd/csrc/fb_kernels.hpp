@@ -743,7 +743,24 @@ hipError_t launch_compiled(const CompiledArgs& a, int grid, int block, size_t ld
                            hipEvent_t ev0 = nullptr, hipEvent_t ev1 = nullptr);
 constexpr int kBubbleBlock = 128;
 // waves: n_big (one per big bubble) + ceil(n_small / 64)
-int bubble_waves(int32_t n_small, int32_t n_big);
+// Small bubbles run 64 to a wavefront: the class-A chunks first (the last
+// one partial), then the class-B chunks from list entry n4 on -- so no
+// wavefront holds both classes (a mixed one ran both code paths, twice a
+// wave's time, and was the launch's last bubble arrival, profiles/r05).
+// Chunk c, lane l -> small-list entry b (class A: b < n4, class B: b >= n4),
+// or -1 for an idle lane; b is also the bubble's position (rmin, the slot
+// layout's lane groups, which are aligned within each class's chunks)
+__host__ __device__ inline int64_t small_chunks(int64_t n4, int64_t ns) { return (n4 + 63) / 64 + (ns + 63) / 64; }
+__host__ __device__ inline int64_t small_entry(int64_t c, int l, int64_t n4, int64_t ns) {
+    const int64_t na = (n4 + 63) / 64;
+    if (c < na) {
+        const int64_t b = c * 64 + l;
+        return b < n4 ? b : -1;
+    }
+    const int64_t b = n4 + (c - na) * 64 + l;
+    return b < n4 + ns ? b : -1;
+}
+int bubble_waves(int32_t n_small4, int32_t n_small, int32_t n_big);
 hipError_t launch_bubbles(const BubbleArgs& a, hipStream_t stream);
 hipError_t launch_reduce(const ReduceArgs& a, hipStream_t stream);
 // out[1 + j] = sum over k of gpart[k][j] in k order (the preparation-time gradient slabs)

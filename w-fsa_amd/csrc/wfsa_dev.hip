@@ -1075,20 +1075,27 @@ int layout_slots(wfsa_dev* ctx, const std::vector<int32_t>& pos_of) {
         const char* e = std::getenv("WFSA_SLOT_MERGE");
         return !(e && e[0] == '0');
     }();
-    for (int64_t g0 = 0; merge && g0 < nsm; g0 += kWave)
+    // (a wavefront's lanes: 64 consecutive entries of one class, from the
+    // class's first entry -- wfsa::small_entry -- so lane = (b - base) & 63)
+    auto wave_base = [&](int64_t b) { return b < n4 ? int64_t(0) : n4; };
+    for (int64_t g0 = 0; merge && g0 < nsm; g0 = std::min(g0 + kWave, g0 < n4 ? n4 : nsm)) {
+        const int64_t gend = std::min(g0 + kWave, g0 < n4 ? n4 : nsm);
         for (int e = 0; e < wfsa::kBubbleRegEdges; ++e)
             for (int k = 6; k >= 1; --k) {   // largest aligned groups first
                 const int64_t G = int64_t(1) << k;
-                for (int64_t b0 = g0; b0 + G <= std::min(g0 + kWave, nsm); b0 += G) {
+                for (int64_t b0 = g0; b0 + G <= gend; b0 += G) {
                     if (lvl[size_t(b0) * 8 + size_t(e)]) continue;   // inside a larger group
                     const int32_t c = small_code(b0, e);
-                    bool same = c >= 0 && (b0 < n4) == (b0 + G - 1 < n4);
+                    bool same = c >= 0;
                     for (int64_t b = b0 + 1; same && b < b0 + G; ++b) same = small_code(b, e) == c && !lvl[size_t(b) * 8 + size_t(e)];
                     if (same)
                         for (int64_t b = b0; b < b0 + G; ++b) lvl[size_t(b) * 8 + size_t(e)] = uint8_t(k);
                 }
             }
-    auto leader = [&](int64_t b, int e) { return (b & ((int64_t(1) << lvl[size_t(b) * 8 + size_t(e)]) - 1)) == 0; };
+    }
+    auto leader = [&](int64_t b, int e) {
+        return ((b - wave_base(b)) & ((int64_t(1) << lvl[size_t(b) * 8 + size_t(e)]) - 1)) == 0;
+    };
     std::vector<int32_t> pc(size_t(np) + 1, 0);   // by position
     for (int64_t b = 0; b < nsm; ++b)
         for (int e = 0; e < wfsa::kBubbleRegEdges; ++e) {
@@ -1823,7 +1830,7 @@ int prepare(wfsa_dev* ctx, int level) {
         ctx->big_lds_edges = 2;
         for (int32_t o : ctx->h_big_list) ctx->big_lds_edges = std::max(ctx->big_lds_edges, (ctx->h_bubbuf[size_t(o)] >> 16) + 1);
         ctx->big_lds_edges &= ~1;   // even
-        ctx->b_waves = wfsa::bubble_waves(ctx->n_small4 + ctx->n_small, ctx->n_big);
+        ctx->b_waves = wfsa::bubble_waves(ctx->n_small4, ctx->n_small, ctx->n_big);
         HIP_TRY(hipStreamSynchronize(s));
     } else {
         ctx->b_waves = 0;
@@ -1844,15 +1851,15 @@ int prepare(wfsa_dev* ctx, int level) {
         if (const char* e = std::getenv("WFSA_SMALL_COST_B")) small_cost_b = std::atof(e);
         if (const char* e = std::getenv("WFSA_BIG_COST")) big_cost = std::atof(e);
         const int nblk = ctx->i_grid;
-        const int64_t ns = int64_t(ctx->n_small4) + ctx->n_small;
-        const int small_wpb = small_waves_per_block(ns, nblk);
+        const int64_t nch = wfsa::small_chunks(ctx->n_small4, ctx->n_small), na = (int64_t(ctx->n_small4) + kWave - 1) / kWave;
+        const int small_wpb = small_waves_per_block(nch * kWave, nblk);
         for (int w = 0; w < i_nw; ++w) {
             const int bid = w / i_wpb, wib = w % i_wpb;
             if (bid == 0 && wib == i_wpb - 1) continue;   // the finish wave (charged 1e300 above)
             double c = 0.0;
             if (wib == i_wpb - 2 && bid < ctx->qw_waves) c += ctx->qw_cost;
-            const int64_t b0 = (int64_t(wib) * nblk + bid) * kWave;   // fbs_kernel's chunk of this wave
-            if (wib < small_wpb && b0 < ns) c += (b0 + kWave > ctx->n_small4) ? small_cost_b : small_cost;
+            const int64_t ch = int64_t(wib) * nblk + bid;   // fbs_kernel's chunk of this wave (wfsa::small_entry)
+            if (wib < small_wpb && ch < nch) c += ch >= na ? small_cost_b : small_cost;
             int64_t r = (nblk - 1 - bid) + int64_t(nblk) * (i_wpb - 1 - wib);
             r -= r > nblk - 1 ? 1 : 0;
             if (r < ctx->n_big) c += big_cost;
@@ -2082,7 +2089,7 @@ int enqueue_compiled(wfsa_dev* ctx, bool with_grad, bool want_logq, const unsign
             c.bub.prio = ctx->bub_prio ? 1 : 0;
             c.bub.early_big = ctx->early_big ? 1 : 0;
             c.early_bub = ctx->early_bub ? 1 : 0;
-            c.bub.small_wpb = small_waves_per_block(ctx->n_small4 + ctx->n_small, ctx->i_grid);
+            c.bub.small_wpb = small_waves_per_block(wfsa::small_chunks(ctx->n_small4, ctx->n_small) * kWave, ctx->i_grid);
             if (ctx->n_big > 0) {
                 c.bub.big_lds_edges = ctx->big_lds_edges;
                 c.bub.big_lds_off = int32_t(big_stage_off(ctx));
@@ -2165,7 +2172,7 @@ bool bubbles_fused(wfsa_dev* ctx, bool want_logq) {
     // at most one chunk of 64 small bubbles per wave; the big bubbles' staging must fit beside w
     // (the last wave of block 0 is the QN finish's: no bubbles)
     if (ctx->i_block / kWave < 2 ||
-        small_waves_per_block(ctx->n_small4 + ctx->n_small, ctx->i_grid) > ctx->i_block / kWave - 1)
+        small_waves_per_block(wfsa::small_chunks(ctx->n_small4, ctx->n_small) * kWave, ctx->i_grid) > ctx->i_block / kWave - 1)
         return false;
     return ctx->n_big == 0 || big_stage_off(ctx) + size_t(ctx->i_block / kWave) *
                                                        size_t(wfsa::big_stage_bytes(ctx->big_lds_edges)) <=
@@ -2727,7 +2734,7 @@ int enqueue_qn_step_piped(wfsa_dev* ctx, double eta, double tol, int64_t e, bool
         c.no_streams = 1;
         c.bub = bubble_args(ctx, false, halted, nullptr);
         c.bub_on = 1;
-        c.bub.small_wpb = small_waves_per_block(ctx->n_small4 + ctx->n_small, ctx->i_grid);
+        c.bub.small_wpb = small_waves_per_block(wfsa::small_chunks(ctx->n_small4, ctx->n_small) * kWave, ctx->i_grid);
         size_t lds = ctx->i_lds;
         if (ctx->n_big > 0) {
             c.bub.big_lds_edges = ctx->big_lds_edges;
@@ -3691,7 +3698,7 @@ static int qn_run_impl(wfsa_dev* ctx, double eta, double tol, int32_t max_steps,
         unsigned long long t0 = ~0ull;
         for (int w = 0; w < nw; ++w)
             if (t[size_t(w) * 16]) t0 = std::min(t0, t[size_t(w) * 16]);
-        const int small_wpb = small_waves_per_block(ctx->n_small4 + ctx->n_small, ctx->i_grid);
+        const int small_wpb = small_waves_per_block(wfsa::small_chunks(ctx->n_small4, ctx->n_small) * kWave, ctx->i_grid);
         const char* names[8] = {"entry", "staged", "bubbles", "arrived", "stream", "qn-poll", "qn-done", "exit"};
         for (int grp = 0; grp < 3; ++grp) {
             for (int k = 0; k < 8; ++k) {
@@ -3718,8 +3725,9 @@ static int qn_run_impl(wfsa_dev* ctx, double eta, double tol, int32_t max_steps,
             for (int w = 0; w < nw; ++w) {
                 const int wib = w % wpb, bid = w / wpb;
                 if (wib >= small_wpb) continue;
-                const int64_t b0 = (int64_t(wib) * ctx->i_grid + bid) * kWave;
-                if (b0 >= ctx->n_small4 + ctx->n_small || (b0 < ctx->n_small4) != (cls == 0)) continue;
+                const int64_t ch = int64_t(wib) * ctx->i_grid + bid;   // (wfsa::small_entry's chunks)
+                const int64_t na = (int64_t(ctx->n_small4) + kWave - 1) / kWave;
+                if (ch >= wfsa::small_chunks(ctx->n_small4, ctx->n_small) || (ch < na) != (cls == 0)) continue;
                 const unsigned long long* r = &t[size_t(w) * 16];
                 const unsigned long long st = r[1] ? r[1] : r[0];
                 const unsigned long long pts[5] = {st, r[8], r[9], r[10], r[11]};
@@ -3728,6 +3736,26 @@ static int qn_run_impl(wfsa_dev* ctx, double eta, double tol, int32_t max_steps,
             }
             const char* pn[4] = {"quads", "gathers", "forward", "backward"};
             std::fprintf(stderr, "[fbs-trace] class %c small-bubble phases (p50 / p90 / max us):", cls ? 'B' : 'A');
+            for (int k = 0; k < 4; ++k) {
+                if (ph[k].empty()) continue;
+                std::sort(ph[k].begin(), ph[k].end());
+                std::fprintf(stderr, " %s %.2f / %.2f / %.2f;", pn[k], ph[k][ph[k].size() / 2], ph[k][ph[k].size() * 9 / 10],
+                             ph[k].back());
+            }
+            std::fprintf(stderr, "\n");
+        }
+        {   // the QN waves' phases: poll done (5) -> halt flag + slot chunks summed (8) -> member and
+            // constraint sums (9) -> x / weight stores (10) -> done (6)
+            std::vector<double> ph[4];
+            for (int w = 0; w < nw; ++w) {
+                if (!(w % wpb == wpb - 2 && w / wpb < ctx->qw_waves)) continue;
+                const unsigned long long* r = &t[size_t(w) * 16];
+                const unsigned long long pts[5] = {r[5], r[8], r[9], r[10], r[6]};
+                for (int k = 0; k < 4; ++k)
+                    if (pts[k] && pts[k + 1] && pts[k + 1] >= pts[k]) ph[k].push_back(double(pts[k + 1] - pts[k]) / 100.0);
+            }
+            const char* pn[4] = {"chunks", "sums", "stores", "tail"};
+            std::fprintf(stderr, "[fbs-trace] QN wave phases (p50 / p90 / max us):");
             for (int k = 0; k < 4; ++k) {
                 if (ph[k].empty()) continue;
                 std::sort(ph[k].begin(), ph[k].end());
@@ -3746,7 +3774,8 @@ static int qn_run_impl(wfsa_dev* ctx, double eta, double tol, int32_t max_steps,
             HIP_TRY(ctx->d_wave_first.download(wf.data(), wf.size(), s));
             HIP_TRY(ctx->d_g_base.download(gb.data(), gb.size(), s));
             HIP_TRY(hipStreamSynchronize(s));
-            const int64_t ns = int64_t(ctx->n_small4) + ctx->n_small;
+            const int64_t nch = wfsa::small_chunks(ctx->n_small4, ctx->n_small);
+            const int64_t na = (int64_t(ctx->n_small4) + kWave - 1) / kWave;
             double M[6][6] = {}, v[6] = {};
             double sums[5][3] = {};   // per kind: n, rows, end
             for (int w = 0; w < nw; ++w) {
@@ -3756,10 +3785,10 @@ static int qn_run_impl(wfsa_dev* ctx, double eta, double tol, int32_t max_steps,
                 const double end = double(r[4] - r[1]) / 100.0;
                 const double rows = double(gb[size_t(wf[size_t(w) + 1])] - gb[size_t(wf[size_t(w)])]) / kWave;
                 double x[6] = {1.0, rows, 0, 0, 0, 0};
-                const int64_t b0 = (int64_t(wib) * ctx->i_grid + bid) * kWave;
+                const int64_t ch = int64_t(wib) * ctx->i_grid + bid;
                 int kind = 0;
-                if (wib < small_wpb && b0 < ns) {
-                    kind = b0 + kWave > ctx->n_small4 ? 2 : 1;
+                if (wib < small_wpb && ch < nch) {
+                    kind = ch >= na ? 2 : 1;
                     x[kind + 1] = 1.0;
                 }
                 int64_t rb = (ctx->i_grid - 1 - bid) + int64_t(ctx->i_grid) * (wpb - 1 - wib);
