@@ -2582,7 +2582,15 @@ __device__ __forceinline__ void qn_wave_batch(const QnWave& q, const QnBatchIn& 
         } else {
             pv.x = pv.y = pv.z = pv.w = NAN;
         }
-        reinterpret_cast<double4*>(q.partial)[con] = pv;
+        if (q.self_finish) {   // read by this launch's finisher
+            double* pp = q.partial + 4 * size_t(con);
+            store_wt(pp, pv.x);
+            store_wt(pp + 1, pv.y);
+            store_wt(pp + 2, pv.z);
+            store_wt(pp + 3, pv.w);
+        } else {
+            reinterpret_cast<double4*>(q.partial)[con] = pv;
+        }
     }
 }
 
@@ -2692,7 +2700,10 @@ __global__ __launch_bounds__(1024, (DBG == 10 ? 8 : 1)) WFSA_FBS_ATTR void fbs_k
     };
     double2 t0[kTB];
     if (pre && !big_early) table_round(int(threadIdx.x), n_stage, t0);
-    if (QN && bid == 0 && threadIdx.x == 0) a.qw.arrive[a.qw.parity ^ 1] = 0u;   // for the next launch
+    if (QN && bid == 0 && threadIdx.x == 0) {   // for the next launch
+        a.qw.arrive[a.qw.parity ^ 1] = 0u;
+        if (a.qw.self_finish) a.qw.done[a.qw.parity ^ 1] = 0u;
+    }
     // halted is written only by an earlier launch (the QN step's finish)
     if (a.halted && *a.halted) {
         if (QN && bid == 0 && threadIdx.x == 0) qn_publish_row(a.qw.fin, nullptr, kQnSkipped);   // (no QN kernel)
@@ -2813,7 +2824,9 @@ __global__ __launch_bounds__(1024, (DBG == 10 ? 8 : 1)) WFSA_FBS_ATTR void fbs_k
             char* stg = reinterpret_cast<char*>(lds) + a.bub.big_lds_off + w * big_stage_bytes(E);
             double* lw = reinterpret_cast<double*>(stg);
             int* lsd = reinterpret_cast<int*>(lw + E + 2 * kMaxBubbleNodes);
+            if (a.bub.prio > 1) __builtin_amdgcn_s_setprio(2);   // (prio 2: the big bubbles raised too)
             for (int i = r; i < a.bub.n_big; i += nw - 1) ll_acc += big_bubble(a.bub, i, lsd, lw, lw, lw + E);
+            if (a.bub.prio > 1) __builtin_amdgcn_s_setprio(0);
         }
     };
     if (early && small_wave) small_bubbles();
@@ -3018,10 +3031,12 @@ __global__ __launch_bounds__(1024, (DBG == 10 ? 8 : 1)) WFSA_FBS_ATTR void fbs_k
     ll_acc = wave_sum(ll_acc);
     if (lane == 0) wsum[w] = ll_acc;
     __syncthreads();
+    const bool self_fin = QN && a.qw.self_finish;
     if (threadIdx.x == 0) {
         double t = 0.0;
         for (int i = 0; i < wpb; ++i) t += wsum[i];
-        a.ll_part[bid] = t;
+        if (self_fin) store_wt(a.ll_part + bid, t);   // (read by this launch's finisher)
+        else a.ll_part[bid] = t;
     }
     // this block's slice of the per-edge weights and the zeroed result, for
     // the kernels after this one (nothing in this launch reads them)
@@ -3030,11 +3045,31 @@ __global__ __launch_bounds__(1024, (DBG == 10 ? 8 : 1)) WFSA_FBS_ATTR void fbs_k
     // the block barrier; a second call site before it, as an option, made
     // the kernel spill 96 VGPRs)
     if (QN && w == wpb - 2 && bid < a.qw.n_waves) {
+        if (a.bub.prio > 2) __builtin_amdgcn_s_setprio(3);   // (prio 3: the QN waves raised above the stream)
 #ifdef WFSA_EXPERIMENTS
         qn_wave_run(a.qw, bid, tr);
 #else
         qn_wave_run(a.qw, bid, nullptr);
 #endif
+    }
+    // Self-finish: every block's wave 0 (its log-likelihood partial) and
+    // every QN wave (its constraints' partials) arrive once their stores
+    // retired; the last arrival runs this step's finish (the wave form,
+    // write-through loads, the same sums as the next launch's finish wave)
+    // and publishes the row -- no finish left for the next launch, and the
+    // Run's last row needs no finish kernel of its own.  A step the previous
+    // finish halted publishes its skipped row from its QN waves instead.
+    if (self_fin && (w == 0 || (w == wpb - 2 && bid < a.qw.n_waves))) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        unsigned before = 0u;
+        if (lane == 0) before = __hip_atomic_fetch_add(a.qw.done + a.qw.parity, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        before = __shfl(before, 0, kWave);
+        if (before + 1u == unsigned(nblk + a.qw.n_waves) && load_wt(a.qw.halted + 1) == 0u) {
+            double info[7];
+            unsigned st = kQnRan;
+            qn_finish_compute<true, true>(a.qw.fin, nullptr, info, st);
+            if (lane == 0) qn_finish_publish(a.qw.fin, info, st);
+        }
     }
     WFSA_STAMP(7)
 #undef WFSA_STAMP

@@ -563,7 +563,7 @@ struct BubbleArgs {
     const unsigned* halted;
     int32_t dbg;             // timing experiments only (WFSA_BUB_DBG): 1 no slot stores, 2 no weight gathers
     int32_t wt;              // contribution slots stored write-through (sc1): read in the same launch (QnWave)
-    int32_t prio;            // fused small bubbles at raised wave priority (s_setprio 2)
+    int32_t prio;            // fused small bubbles at raised wave priority (s_setprio 2); 2: the big ones too
     int32_t early_big;       // the stream kernel's big-bubble waves run their bubble at entry, beside the staging
 };
 
@@ -625,7 +625,10 @@ struct QnWave {
     int32_t exp_lambda;
     unsigned* arrive;            // [2] per-parity arrival counters
     unsigned* halted;            // [0] halted (earlier launches), [1] halt_pending (this launch's finish, sc1)
-    QnFinish fin;                // this step's publication (a skipped row after a halt)
+    QnFinish fin;                // this step's publication (a skipped row after a halt; with self_finish, its row)
+    int32_t self_finish;         // the launch's last finisher (after every block's log-likelihood partial and
+                                 // every QN wave's partials, write-through) runs this step's finish itself
+    unsigned* done;              // [2] per-parity counters of those arrivals (each launch zeroes the other's)
 };
 
 struct CompiledArgs {

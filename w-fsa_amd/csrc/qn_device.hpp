@@ -220,14 +220,21 @@ __device__ inline double block_reduce(double v, int op, double* red) {
 // next QN launch) and the publication.  red: kMaxBlockWaves doubles of LDS.
 // WAVE: one wavefront computes it alone (the stream kernel's reserved finish
 // wave; no block barriers), red unused
-template <bool WAVE = false>
+template <bool WAVE = false, bool WT = false>   // WT: the partials read write-through (sc1): inside the launch that wrote them
 __device__ inline void qn_finish_compute(const QnFinish& f, double* red, double* info, unsigned& status) {
     const int t = WAVE ? int(threadIdx.x) % 64 : int(threadIdx.x), nt = WAVE ? 64 : int(blockDim.x), nw = nt / 64;
     double gmin = INFINITY, gmax = -INFINITY, lmin = INFINITY, ge = 0.0;
     for (int j0 = t; j0 < f.n_blocks; j0 += 4 * nt) {   // four blocks' partials in flight per thread
         double4 v[4];
 #pragma unroll
-        for (int b = 0; b < 4; ++b) v[b] = reinterpret_cast<const double4*>(f.partial)[min(j0 + b * nt, f.n_blocks - 1)];
+        for (int b = 0; b < 4; ++b) {
+            if constexpr (WT) {
+                const double* p = f.partial + 4 * size_t(min(j0 + b * nt, f.n_blocks - 1));
+                v[b] = make_double4(load_wt(p), load_wt(p + 1), load_wt(p + 2), load_wt(p + 3));
+            } else {
+                v[b] = reinterpret_cast<const double4*>(f.partial)[min(j0 + b * nt, f.n_blocks - 1)];
+            }
+        }
 #pragma unroll
         for (int b = 0; b < 4; ++b) {
             gmin = fmin(gmin, v[b].x);
@@ -240,7 +247,20 @@ __device__ inline void qn_finish_compute(const QnFinish& f, double* red, double*
     // first wavefront's strided sums, then its shuffle tree): a run's last
     // row (the one-block finish) and the others (the stream kernel's finish
     // wave) sum the same way
-    double ll = (f.ll_part && t < 64) ? strided_sum(f.ll_part, f.n_ll, t, 64) : 0.0;
+    double ll = 0.0;
+    if constexpr (WT) {   // strided_sum's order, write-through loads
+        if (f.ll_part && t < 64)
+            for (int i0 = t; i0 < f.n_ll; i0 += 8 * 64) {
+                double v[8];
+#pragma unroll
+                for (int b = 0; b < 8; ++b) v[b] = load_wt(f.ll_part + min(i0 + b * 64, f.n_ll - 1));
+#pragma unroll
+                for (int b = 0; b < 8; ++b)
+                    if (i0 + b * 64 < f.n_ll) ll += v[b];
+            }
+    } else {
+        ll = (f.ll_part && t < 64) ? strided_sum(f.ll_part, f.n_ll, t, 64) : 0.0;
+    }
     ll = wave_reduce(ll, 2);
     double rv = INFINITY, ri = -1.0;   // rmin column from block minima, ties to the lower string
     if (f.rmin_part)

@@ -369,6 +369,8 @@ struct wfsa_dev {
     bool stream_nt = false;          // WFSA_STREAM_NT=1: the stream kernel's rows loaded non-temporal
     bool defer_prefetch = false;     // WFSA_DEFER_PREFETCH=1: the first row set after the table / bubble loads
     bool bub_prio = true;            // WFSA_BUB_PRIO=0: the fused small bubbles at normal wave priority
+    bool bub_prio_big = false;       // WFSA_BUB_PRIO=2: the big ones at raised priority too
+    bool qn_prio = false;            // WFSA_BUB_PRIO=3: and the QN waves above the stream
     bool early_big = false;          // WFSA_EARLY_BIG=1: the big-bubble waves start at entry (fb_kernels.hip)
     int32_t qw_waves = 0;            // reserved at preparation
     double qw_cost = 6.0;            // the dealer's charge per QN wave, in stream rows (WFSA_QN_COST)
@@ -382,6 +384,8 @@ struct wfsa_dev {
     int64_t qw_key = -1;             // (qn set-up, layout) the batches were built for
     std::vector<int4> h_qw_batch;    // host copy of the batches (diagnostics)
     DevBuf<unsigned> qw_arrive;      // [2], zero between launches (each launch zeroes the next one's)
+    DevBuf<unsigned> qw_done;        // [2] the self-finish's arrivals, likewise
+    bool qw_self_finish = false;     // WFSA_QN_SELF_FINISH=1: each launch finishes its own step (fb_kernels.hip)
     uint64_t qw_seq = 0;             // in-kernel QN launches enqueued (their parity)
     wfsa::QnWave qw_next{};          // picked up by the next stream kernel launch (qw_next.on)
     DevBuf<unsigned long long> fbs_trace;   // timing experiments (WFSA_FBS_TRACE): per-wave stamps of the last launch
@@ -2086,7 +2090,7 @@ int enqueue_compiled(wfsa_dev* ctx, bool with_grad, bool want_logq, const unsign
                 ctx->rm_sv_used = true;
             }
             c.bub_on = 1;
-            c.bub.prio = ctx->bub_prio ? 1 : 0;
+            c.bub.prio = ctx->bub_prio ? (ctx->qn_prio ? 3 : ctx->bub_prio_big ? 2 : 1) : 0;
             c.bub.early_big = ctx->early_big ? 1 : 0;
             c.early_bub = ctx->early_bub ? 1 : 0;
             c.bub.small_wpb = small_waves_per_block(wfsa::small_chunks(ctx->n_small4, ctx->n_small) * kWave, ctx->i_grid);
@@ -2646,6 +2650,12 @@ int enqueue_qn_step(wfsa_dev* ctx, double eta, double tol, int64_t e, bool timed
         w.arrive = ctx->qw_arrive.ptr;
         w.halted = ctx->qn_halted.ptr;
         w.fin = f;
+        if (ctx->qw_self_finish) {   // this launch finishes its own step (its stream kernel's blocks' ll partials)
+            w.self_finish = 1;
+            w.done = ctx->qw_done.ptr;
+            w.fin.ll_part = ctx->ll_cur;
+            w.fin.n_ll = ctx->i_grid;
+        }
         ++ctx->qw_seq;
     }
     ctx->rm_eval = fuse_rmin;
@@ -2654,6 +2664,12 @@ int enqueue_qn_step(wfsa_dev* ctx, double eta, double tol, int64_t e, bool timed
     if (erc) return erc;
     if (ctx->qw_next.on) return fail(WFSA_ERR_HIP, "the in-kernel QN update was not launched");
     if (fused) f.n_ll = n_ll;
+    if (inkern && ctx->qw_self_finish) {   // the step published its own row: no finish pending
+        if (n_ll != ctx->i_grid) return fail(WFSA_ERR_HIP, "self-finish: %d log-likelihood partials, not %d", n_ll, ctx->i_grid);
+        ctx->fin_pending = false;
+        ctx->fin_next.active = 0;
+        return WFSA_OK;
+    }
     if (ctx->comm) COMM_TRY(ctx, ctx->out.ptr, size_t(np) + 1, wfsa::RedOp::SumF64, s);
     if (ctx->qn_rmin) {
         static const bool fold_rmin = [] {   // WFSA_RMIN_FOLD=0: the strings pass as its own launch
@@ -2949,9 +2965,14 @@ int wfsa_dev_create(int device, wfsa_dev** out) {
     if (const char* e = std::getenv("WFSA_EARLY_BUB")) ctx->early_bub = e[0] == '1';
     if (const char* e = std::getenv("WFSA_STREAM_NT")) ctx->stream_nt = e[0] == '1';
     if (const char* e = std::getenv("WFSA_DEFER_PREFETCH")) ctx->defer_prefetch = e[0] == '1';
-    if (const char* e = std::getenv("WFSA_BUB_PRIO")) ctx->bub_prio = e[0] != '0';
+    if (const char* e = std::getenv("WFSA_BUB_PRIO")) {
+        ctx->bub_prio = e[0] != '0';
+        ctx->bub_prio_big = e[0] == '2' || e[0] == '3';
+        ctx->qn_prio = e[0] == '3';
+    }
     if (const char* e = std::getenv("WFSA_EARLY_BIG")) ctx->early_big = e[0] == '1';
     if (const char* e = std::getenv("WFSA_QN_COST")) ctx->qw_cost = std::atof(e);
+    if (const char* e = std::getenv("WFSA_QN_SELF_FINISH")) ctx->qw_self_finish = e[0] == '1';
 
     HIP_TRY(hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking));
     if (const char* e = std::getenv("WFSA_PIPE")) ctx->use_pipe = e[0] == '1';
@@ -2981,6 +3002,8 @@ int wfsa_dev_create(int device, wfsa_dev** out) {
     HIP_TRY(hipMemsetAsync(ctx->counters.ptr, 0, sizeof(unsigned), ctx->stream));
     HIP_TRY(ctx->qw_arrive.alloc(2));
     HIP_TRY(hipMemsetAsync(ctx->qw_arrive.ptr, 0, 2 * sizeof(unsigned), ctx->stream));
+    HIP_TRY(ctx->qw_done.alloc(2));
+    HIP_TRY(hipMemsetAsync(ctx->qw_done.ptr, 0, 2 * sizeof(unsigned), ctx->stream));
     HIP_TRY(hipStreamSynchronize(ctx->stream));
     *out = ctx.release();
     return WFSA_OK;
