@@ -2654,7 +2654,9 @@ int enqueue_qn_step(wfsa_dev* ctx, double eta, double tol, int64_t e, bool timed
             w.self_finish = 1;
             w.done = ctx->qw_done.ptr;
             w.fin.ll_part = ctx->ll_cur;
-            w.fin.n_ll = ctx->i_grid;
+            // the stream kernel's blocks, then (bubbles not fused: the bubble
+            // kernel ran first) the bubble kernel's waves -- enqueue_evaluation's order
+            w.fin.n_ll = ctx->i_grid + ((ctx->n_bubbles > 0 && !bubbles_fused(ctx, false)) ? ctx->b_waves : 0);
         }
         ++ctx->qw_seq;
     }
@@ -2665,7 +2667,8 @@ int enqueue_qn_step(wfsa_dev* ctx, double eta, double tol, int64_t e, bool timed
     if (ctx->qw_next.on) return fail(WFSA_ERR_HIP, "the in-kernel QN update was not launched");
     if (fused) f.n_ll = n_ll;
     if (inkern && ctx->qw_self_finish) {   // the step published its own row: no finish pending
-        if (n_ll != ctx->i_grid) return fail(WFSA_ERR_HIP, "self-finish: %d log-likelihood partials, not %d", n_ll, ctx->i_grid);
+        const int32_t want = ctx->i_grid + ((ctx->n_bubbles > 0 && !bubbles_fused(ctx, false)) ? ctx->b_waves : 0);
+        if (n_ll != want) return fail(WFSA_ERR_HIP, "self-finish: %d log-likelihood partials, not %d", n_ll, want);
         ctx->fin_pending = false;
         ctx->fin_next.active = 0;
         return WFSA_OK;
