@@ -11,8 +11,10 @@ One step = one QuasiNewtonLearner::OptimizationStep over the whole corpus,
 run DEVICE-RESIDENT: main.cpp's epoch loop is wfsa_learner_run ->
 wfsa_dev_qn_run, which enqueues per step the forward-backward kernels (stream
 + bubble + traversal tiers), [the RCCL all-reduce of the gradient], and the QN
-step kernel (x, lambda and the next weights stay in HBM; each step's info row
-lands in host-mapped memory).  Inputs are resident in HBM.  The same steps
+update (x, lambda and the next weights stay in HBM; each step's info row lands
+in host-mapped memory).  On one GPU at c3 that is ONE launch per step: the
+stream kernel with the bubbles and the QN update inside; across
+ranks the QN update is its own kernel after the all-reduce.  Inputs are resident in HBM.  The same steps
 through the host binding of INTEGRATION.md section 2 (wfsa_dev_objective_grad
 per step: H2D weights, D2H [LL, grad], host QN update) are timed beside it
 (`boundary`).
@@ -347,11 +349,15 @@ def roofline_of(m, traffic):
                 "kernel": "fbs_kernel (compiled-stream forward pass + fused bubbles, per step)",
                 "timed_launches": timed, "kernel_ms_per_launch": kern_ms, "all_fb_kernels_ms_per_step": fb_ms,
                 "algorithmic_bytes_per_launch": alg_bytes,
-                "note": ("the pass reads the compiled stream (10-bit delta words, 1.62x the algorithmic bytes in "
-                         "PMC traffic) and is bound by those bytes: the delta stream's loads alone take 15.4 us of "
-                         "the micro's 17.9 us pass (profiles/r04/stream_format_micro_v4b.txt); the kernel time is from "
-                         "HIP events attached to the kernel's dispatch (hipExtLaunchKernelGGL start/stop), within "
-                         "~1.5 us of rocprof's kernel average (profiles/r04/, DESIGN 3)")}
+                "note": ("one launch per QN step: staging of the weight table (~4.3 us), the fused bubbles "
+                         "(write-through slots, an arrival counter), the delta-format stream pass, and the QN "
+                         "update's waves after the last bubble arrival (profiles/r05/fbs_trace_fit.log).  PMC "
+                         "(profiles/r05/profile/pmc.txt, profiles/traffic_latest.json): 86.2 MB of HBM traffic "
+                         "per launch (1.67x the algorithmic bytes), waves waiting 66% of their cycles, LDS bank "
+                         "conflicts 53% of LDS-active cycles; the launch's end is the QN tail and the slowest "
+                         "stream waves, not the stream's bytes.  The kernel time is from HIP events attached to "
+                         "its dispatch (hipExtLaunchKernelGGL start/stop); rocprof's average is ~1-3 us lower "
+                         "(DESIGN 6)")}
     # family B: the traversal strings (k_c..k_2 of the evaluation)
     trav_ms = max(fb_ms - kern_ms, 1e-9)
     rows, pedges = st1.get("wave_row_entries", 0), st1.get("wave_pair_edges", 0)
@@ -412,7 +418,7 @@ def record(m, traffic, cpu):
     return {"metric": METRIC, "value": m["value"], "unit": "strings/s", "steps": wl["steps"], "warmup": wl["warmup"],
             "ms_per_step": m["ms_per_step"], "dtype": "f64",
             "config": {"workload": workload_label(wl, m["off"]), "strings_per_gpu": wl["strings_per_gpu"],
-                       "step": "device-resident QN loop (wfsa_dev_qn_run: evaluation kernels + QN step kernel per step)"},
+                       "step": "device-resident QN loop (wfsa_dev_qn_run: evaluation kernels + the QN update per step)"},
             "roofline": roofline_of(m, traffic), "cpu_baseline": cpu,
             "compiled_strings": m["st1"]["compiled_strings"], "fallback_strings": m["st1"]["fallback_strings"],
             "tier2_strings": m["st1"]["tier2_strings"], "build_s": m["t_build"]}
@@ -475,7 +481,7 @@ def main():
     # GetOptimizationInfo's smallest relative path probability), which the
     # reference prints each epoch but computes outside OptimizationStep
     rmin_pass = None
-    if not args.info_rmin and not distributed and not wl["dense"]:
+    if not args.info_rmin and not distributed and not wl["dense"] and not args.no_sub:
         lrn.set_info_rmin(True)
         lrn.Run(max(wl["warmup"], 10), 1.0, -1.0)   # (its set-up, then the clock back up: as the headline's warmup)
         m["barrier"]()
@@ -509,9 +515,12 @@ def main():
             "global_strings": m["info"]["n_strings"],
             "strings_per_gpu": wl["strings_per_gpu"],
             "parallelism": f"dp{n_gpus}",
-            "step": ("device-resident QN loop: wfsa_learner_run -> wfsa_dev_qn_run enqueues per step the "
-                     "forward-backward kernels, " + ("the RCCL all-reduce, " if distributed else "") +
-                     "and the QN step kernel (x, lambda, weights stay in HBM; info rows to host-mapped memory)"),
+            "step": ("device-resident QN loop: wfsa_learner_run -> wfsa_dev_qn_run enqueues per step " +
+                     ("the forward-backward kernels, the RCCL all-reduce and the QN step kernel"
+                      if distributed or not st1.get("qn_inkernel_waves") else
+                      "ONE stream kernel with the bubbles and the QN update inside (%d QN waves)"
+                      % st1.get("qn_inkernel_waves", 0)) +
+                     " (x, lambda, weights stay in HBM; info rows to host-mapped memory)"),
             "info_rmin": bool(args.info_rmin),
         },
         "roofline": roofline_of(m, traffic),

@@ -21,7 +21,10 @@ def main():
     out = sys.argv[2] if len(sys.argv) > 2 else os.path.join(os.path.dirname(os.path.dirname(
         os.path.abspath(__file__))), "profiles", "traffic_latest.json")
     res = summarise(d)
-    kern = next(k for k in res if k.startswith("fbs_kernel"))
+    # the headline's stream kernel: the in-kernel QN variant (its last
+    # template argument true) when the run launched it, else the first one
+    fbs = [k for k in res if k.startswith("fbs_kernel")]
+    kern = next((k for k in fbs if k.replace(" ", "").endswith(",true>")), fbs[0])
     fetch_kib = res[kern]["FETCH_SIZE"]
     write_kib = res[kern]["WRITE_SIZE"]
     cal_r = res["stream_read"]["FETCH_SIZE"] * 1024.0
