@@ -7,6 +7,9 @@
 //              slot order (the QN update writing it)
 //   dma     -- global_load_lds_dwordx4 from the slot-ordered table (no VGPRs,
 //              no ds_write)
+//   dmaw    -- global_load_lds_dwordx4 straight from the weight vector at the
+//              remapped (8-byte aligned) addresses, then the zero slots fixed
+//              up in LDS; its LDS image is checked against the table
 // each at 512 blocks x 512 threads (2 blocks per CU, as fbs_kernel) and at
 // 256 blocks x 1024 threads (1 per CU: the table once per CU).
 #include <hip/hip_runtime.h>
@@ -58,15 +61,35 @@ __global__ __launch_bounds__(1024, 1) void stage(const double* __restrict__ w, c
             for (int b = 0; b < kTB; ++b)
                 if (q0 + b * nthr < T2) dst[q0 + b * nthr] = t[b];
         }
-    } else {
+    } else if (V == 2) {
         const int lane = int(threadIdx.x) % 64, wv = int(threadIdx.x) / 64, nwv = nthr / 64;
         for (int p = wv; p * 64 < T2; p += nwv) {   // 1 KiB pieces, one per wave in turn
             const int q = min(p * 64 + lane, T2 - 1);
             __builtin_amdgcn_global_load_lds((glb_void*)(tab + q), (lds_void*)(dst + p * 64), 16, 0, 0);
         }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    } else {
+        const int lane = int(threadIdx.x) % 64, wv = int(threadIdx.x) / 64, nwv = nthr / 64, tlast = n_params - 1;
+        for (int p = wv; p * 64 < T2; p += nwv) {
+            const int s2 = 2 * (p * 64 + lane);
+            const int j0 = s2 - 1 - s2 / kPeriod;
+            const int jc = min(max(j0, 0), tlast);
+            __builtin_amdgcn_global_load_lds((glb_void*)(w + jc), (lds_void*)(dst + p * 64), 16, 0, 0);
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        for (int p = wv; p * 64 < T2; p += nwv) {   // this wave's pieces: the zero slots, the first slot pair
+            const int q = p * 64 + lane, s2 = 2 * q;
+            if (q >= T2) continue;
+            const int j0 = s2 - 1 - s2 / kPeriod;
+            const bool z0 = (s2 % kPeriod) == 0 || j0 > tlast, z1 = ((s2 + 1) % kPeriod) == 0 || j0 + 1 > tlast;
+            if (z0) lds[s2] = 0.0;
+            if (z1) lds[s2 + 1] = 0.0;
+            else if (j0 < 0) lds[s2 + 1] = w[0];
+        }
     }
     __syncthreads();
+    if (V == 3 && blockIdx.x == 0)   // the image, for the host's check
+        for (int i = int(threadIdx.x); i < 2 * T2; i += int(blockDim.x)) out[4096 + i] = lds[i];
     if (lds[(threadIdx.x * 7) % d_tab] == 1234.5) out[blockIdx.x] = 1.0;
 }
 
@@ -84,7 +107,7 @@ int main() {
     double2* tab;
     CK(hipMalloc(&w, n_params * 8));
     CK(hipMalloc(&tab, T2 * 16));
-    CK(hipMalloc(&out, 4096 * 8));
+    CK(hipMalloc(&out, (4096 + 2 * size_t(T2)) * 8));
     CK(hipMemcpy(w, hw.data(), n_params * 8, hipMemcpyHostToDevice));
     CK(hipMemcpy(tab, ht.data(), T2 * 16, hipMemcpyHostToDevice));
     const size_t lds = size_t(T2) * 16;
@@ -92,17 +115,19 @@ int main() {
     CK(hipFuncSetAttribute((const void*)stage<0>, hipFuncAttributeMaxDynamicSharedMemorySize, int(lds)));
     CK(hipFuncSetAttribute((const void*)stage<1>, hipFuncAttributeMaxDynamicSharedMemorySize, int(lds)));
     CK(hipFuncSetAttribute((const void*)stage<2>, hipFuncAttributeMaxDynamicSharedMemorySize, int(lds)));
+    CK(hipFuncSetAttribute((const void*)stage<3>, hipFuncAttributeMaxDynamicSharedMemorySize, int(lds)));
     hipEvent_t e0, e1;
     CK(hipEventCreate(&e0));
     CK(hipEventCreate(&e1));
-    const char* names[3] = {"gather", "contig", "dma"};
-    for (int v = 0; v < 3; ++v)
+    const char* names[4] = {"gather", "contig", "dma", "dmaw"};
+    for (int v = 0; v < 4; ++v)
         for (int shape = 0; shape < 2; ++shape) {
             const int blocks = shape == 0 ? 512 : 256, thr = shape == 0 ? 512 : 1024;
             auto go = [&] {
                 if (v == 0) hipLaunchKernelGGL(stage<0>, dim3(blocks), dim3(thr), lds, 0, w, tab, n_params, d_tab, out);
                 if (v == 1) hipLaunchKernelGGL(stage<1>, dim3(blocks), dim3(thr), lds, 0, w, tab, n_params, d_tab, out);
                 if (v == 2) hipLaunchKernelGGL(stage<2>, dim3(blocks), dim3(thr), lds, 0, w, tab, n_params, d_tab, out);
+                if (v == 3) hipLaunchKernelGGL(stage<3>, dim3(blocks), dim3(thr), lds, 0, w, tab, n_params, d_tab, out);
             };
             for (int r = 0; r < 20; ++r) go();
             CK(hipDeviceSynchronize());
@@ -115,5 +140,12 @@ int main() {
             printf("%-7s %3d x %4d: %.2f us per launch (events over 100 back-to-back launches)\n", names[v], blocks, thr,
                    ms * 10.0);
         }
+    {   // the dmaw image against the table
+        std::vector<double> img(size_t(T2) * 2);
+        CK(hipMemcpy(img.data(), out + 4096, img.size() * 8, hipMemcpyDeviceToHost));
+        size_t bad = 0;
+        for (size_t i = 0; i < img.size(); ++i) bad += img[i] != ht[i];
+        printf("dmaw image: %zu of %zu slots differ from the table\n", bad, img.size());
+    }
     return 0;
 }

@@ -2438,6 +2438,8 @@ __device__ __forceinline__ QnBatchIn qn_wave_load(const QnWave& q, int b) {
     return in;
 }
 
+typedef __attribute__((address_space(3))) void lds_void;   // (LDS-DMA operands)
+typedef __attribute__((address_space(1))) void glb_void;
 __device__ __forceinline__ void qn_wave_batch(const QnWave& q, const QnBatchIn& in, bool ok, const unsigned& halt,
                                               unsigned long long* tr = nullptr) {   // (tr: timing experiments, stamps 8-11)
 #pragma clang fp contract(off)
@@ -2841,7 +2843,41 @@ __global__ __launch_bounds__(1024, (DBG == 10 ? 8 : 1)) WFSA_FBS_ATTR void fbs_k
         double2* dst = reinterpret_cast<double2*>(lds);
         const int nthr = int(blockDim.x) - stage_w0 * kWave;
         bool pf = kStreams && defer;   // the deferred first row set: after this wave's first table loads
-        for (int q0 = int(threadIdx.x) - stage_w0 * kWave; q0 < T2; q0 += kB * nthr) {
+        if (a.dma_stage) {
+            // LDS-DMA (global_load_lds_dwordx4): each 1 KiB piece straight from
+            // the weight vector at the pieces' 8-byte aligned addresses -- no
+            // registers, no LDS stores, so a few stager waves issue the whole
+            // table at once -- then, once this wave's DMA retired, its pieces'
+            // zero slots (and slot 1, weight 0) written over; the partial last
+            // piece by plain loads (a DMA writes all 64 lanes' 16 bytes)
+            const int sw = w - stage_w0, nsw = wpb - stage_w0, full = T2 / kWave;
+            for (int p = sw; p < full; p += nsw) {
+                const int s2 = 2 * (p * kWave + lane);
+                const int j0 = s2 - 1 - s2 / kDeltaPeriod;
+                __builtin_amdgcn_global_load_lds((glb_void*)(a.w + min(max(j0, 0), tlast)), (lds_void*)(dst + p * kWave), 16, 0, 0);
+            }
+            if (pf) load(A, 0);
+            pf = false;
+            if (sw == full % nsw && full * kWave + lane < T2) {   // the partial piece (table_round's rule)
+                const int s2 = 2 * (full * kWave + lane);
+                const int j0 = s2 - 1 - s2 / kDeltaPeriod;
+                const double2 v = *reinterpret_cast<const double2*>(a.w + min(max(j0, 0), tlast));
+                double2 t;
+                t.x = ((s2 % kDeltaPeriod) == 0 || j0 > tlast) ? 0.0 : v.x;
+                t.y = (((s2 + 1) % kDeltaPeriod) == 0 || j0 + 1 > tlast) ? 0.0 : (j0 < 0 ? v.x : v.y);
+                dst[full * kWave + lane] = t;
+            }
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            for (int p = sw; p < full; p += nsw) {
+                const int s2 = 2 * (p * kWave + lane);
+                const int j0 = s2 - 1 - s2 / kDeltaPeriod;
+                double* d = reinterpret_cast<double*>(dst + p * kWave + lane);
+                if ((s2 % kDeltaPeriod) == 0 || j0 > tlast) d[0] = 0.0;
+                if (((s2 + 1) % kDeltaPeriod) == 0 || j0 + 1 > tlast) d[1] = 0.0;
+                else if (j0 < 0) d[1] = a.w[0];
+            }
+        }
+        for (int q0 = int(threadIdx.x) - stage_w0 * kWave; !a.dma_stage && q0 < T2; q0 += kB * nthr) {
             double2 t[kB];
             table_round(q0, nthr, t);
             if (pf) {

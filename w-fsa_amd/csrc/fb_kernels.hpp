@@ -674,7 +674,8 @@ struct CompiledArgs {
     QnFinish fin;            // fin.active: block 0 finishes the previous QN step first
     QnWave qw;               // qw.on: this step's QN update runs in this launch
     unsigned long long* trace;   // timing experiments only (WFSA_FBS_TRACE): [waves][8] s_memrealtime stamps
-    int32_t early_bub;       // delta kernel: the small-bubble waves start at entry, the others stage the table
+    int32_t early_bub;
+    int32_t dma_stage;           // the early stagers move the table by LDS-DMA (WFSA_DMA_STAGE=1)       // delta kernel: the small-bubble waves start at entry, the others stage the table
     int32_t stream_nt;       // stream rows loaded non-temporal
     int32_t defer_prefetch;  // delta kernel: the first row set issued after the wave's table / bubble loads
 };

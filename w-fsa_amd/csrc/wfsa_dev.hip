@@ -365,6 +365,7 @@ struct wfsa_dev {
     // constraints built at QN set-up, per-parity arrival counters and the
     // weights double-buffered by step parity (w_full2 / ewp2 above)
     bool use_qw = true;
+    bool dma_stage = false;          // WFSA_DMA_STAGE=1: the early stagers move the table by LDS-DMA
     bool early_bub = false;          // WFSA_EARLY_BUB=1: the small-bubble waves start at entry, the others stage (slower: the few stagers take longer)
     bool stream_nt = false;          // WFSA_STREAM_NT=1: the stream kernel's rows loaded non-temporal
     bool defer_prefetch = false;     // WFSA_DEFER_PREFETCH=1: the first row set after the table / bubble loads
@@ -2093,6 +2094,7 @@ int enqueue_compiled(wfsa_dev* ctx, bool with_grad, bool want_logq, const unsign
             c.bub.prio = ctx->bub_prio ? (ctx->qn_prio ? 3 : ctx->bub_prio_big ? 2 : 1) : 0;
             c.bub.early_big = ctx->early_big ? 1 : 0;
             c.early_bub = ctx->early_bub ? 1 : 0;
+            c.dma_stage = ctx->dma_stage ? 1 : 0;
             c.bub.small_wpb = small_waves_per_block(wfsa::small_chunks(ctx->n_small4, ctx->n_small) * kWave, ctx->i_grid);
             if (ctx->n_big > 0) {
                 c.bub.big_lds_edges = ctx->big_lds_edges;
@@ -2966,6 +2968,7 @@ int wfsa_dev_create(int device, wfsa_dev** out) {
     if (const char* e = std::getenv("WFSA_WIDE2_TIERS")) ctx->w2_all = std::strcmp(e, "2") != 0;
     if (const char* e = std::getenv("WFSA_QN_INKERNEL")) ctx->use_qw = e[0] != '0';
     if (const char* e = std::getenv("WFSA_EARLY_BUB")) ctx->early_bub = e[0] == '1';
+    if (const char* e = std::getenv("WFSA_DMA_STAGE")) ctx->dma_stage = e[0] == '1';
     if (const char* e = std::getenv("WFSA_STREAM_NT")) ctx->stream_nt = e[0] == '1';
     if (const char* e = std::getenv("WFSA_DEFER_PREFETCH")) ctx->defer_prefetch = e[0] == '1';
     if (const char* e = std::getenv("WFSA_BUB_PRIO")) {
