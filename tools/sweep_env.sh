@@ -2,7 +2,7 @@
 # bench.py's headline alone (no sub-benches, no CPU sample) under several
 # environment settings, round-robin over REPS rounds (so a drifting box
 # shifts every setting alike); one line per run, then each setting's best.
-# Usage: bash tools/sweep_env.sh [--steps K] [--reps N] name:ENV=V,ENV=V name2: ...
+# Usage: bash tools/sweep_env.sh [--steps K] [--reps N] [--workload W] name:ENV=V,ENV=V name2: ...
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}
 cd "$R" || exit 1
@@ -14,6 +14,7 @@ while [ "${1:0:2}" = "--" ]; do
     case $1 in
     --steps) ARGS=(--steps "$2" --warmup 5); shift 2 ;;
     --reps) REPS=$2; shift 2 ;;
+    --workload) ARGS+=(--workload "$2"); shift 2 ;;
     *) echo "unknown option $1"; exit 2 ;;
     esac
 done
@@ -32,7 +33,7 @@ import json, sys
 d = json.loads(open(sys.argv[1]).read().strip().splitlines()[-1])
 r = d.get("roofline", {})
 print(f"{sys.argv[2]:<16} rep {sys.argv[3]} {d['ms_per_step'] * 1e3:7.2f} us/step  stream kernel "
-      f"{1e3 * (r.get('kernel_ms_per_launch') or 0):6.2f} us", flush=True)
+      f"{1e3 * (r.get('kernel_ms_per_launch') or 0):6.2f} us  frac {r.get('frac') or 0:.3f}", flush=True)
 PY
     done
 done
