@@ -166,3 +166,27 @@ def test_fill_reducing_orders_on_a_grid():
         np.testing.assert_allclose(x, x0, rtol=1e-11, atol=1e-12)
     assert s0["positive"] == s1["positive"] == s2["positive"] == n
     assert abs(s2["log_abs_det"] - s0["log_abs_det"]) < 1e-9 * abs(s0["log_abs_det"])
+
+
+@pytest.mark.parametrize("order", [0, 1, 2])
+def test_edge_cases(order):
+    """empty and 1x1 systems, a zero diagonal entry with no coupling
+    (singular), and a forest (two independent blocks, one needing a 2x2 pivot)"""
+    x, st = W.sym_sparse_solve(np.zeros(0, np.int32), np.zeros(0, np.int32), np.zeros(0), 0, np.zeros(0), order=order)
+    assert x.size == 0 and st["positive"] == st["negative"] == 0 and st["supernodes"] == 0
+    x, st = W.sym_sparse_solve(np.array([0], np.int32), np.array([0], np.int32), np.array([2.0]), 1, np.array([4.0]),
+                               order=order)
+    assert x[0] == 2.0 and st["positive"] == 1 and abs(st["log_abs_det"] - np.log(2.0)) < 1e-15
+    with pytest.raises(W.WfsaError, match="singular"):
+        W.sym_sparse_solve(np.array([0, 1], np.int32), np.array([0, 1], np.int32), np.array([1.0, 0.0]), 2, np.ones(2),
+                           order=order)
+    i = np.array([0, 0, 1, 2, 2, 3], np.int32)
+    j = np.array([0, 1, 1, 2, 3, 3], np.int32)
+    v = np.array([2.0, 1.0, 3.0, 0.0, 1.0, 0.0])
+    A = np.zeros((4, 4))
+    A[i, j] += v
+    A[j, i] += np.where(i != j, v, 0.0)
+    b = np.arange(4.0)
+    x, st = W.sym_sparse_solve(i, j, v, 4, b, order=order)
+    np.testing.assert_allclose(x, np.linalg.solve(A, b), rtol=1e-14)
+    assert st["two_by_two"] == 1 and (st["positive"], st["negative"]) == (3, 1)

@@ -180,7 +180,7 @@ template <int MODE, int BK> constexpr int stage() { return op_size<MODE != 2, BK
 // NW waves per 128 x 128 block: 2 x (NW / 2), each a 64 x (256 / NW) tile
 // of 16 x 16 MFMA tiles (NJ of them per row of tiles)
 template <int MODE, int BK, int NW>
-__global__ __launch_bounds__(NW * 64, ((MODE == GRAD || MODE == RAW) && (NW == 4 || (NW == 8 && MODE == RAW)) && BK == 16 ? 2 : 1)) void dense_gemm_kernel(GemmArgs a) {
+__global__ __launch_bounds__(NW * 64, ((MODE == GRAD || MODE == RAW) && (NW == 4 || NW == 8) && BK == 16 ? 2 : 1)) void dense_gemm_kernel(GemmArgs a) {
     if (a.halted && *a.halted) return;
     constexpr int NT = NW * 64, NWN = NW / 2, NJ = 16 / NW, WCOLS = 16 * NJ;
     constexpr int kLdk = ldk<BK>(), kStage = stage<MODE, BK>();
@@ -1572,7 +1572,7 @@ hipError_t DensePath::enqueue_lib(const double* w, const double* p, bool structu
             m.out = nxt;
             if (dma) dense_mm_kernel<true, false><<<mm_blocks, 256, 0, s>>>(m);
             else if (step_cfg_ == 3) dense_gemm_kernel<RAW, kBkStep, 4><<<raw_blocks, 4 * 64, 0, s>>>(m);
-            else if (step_cfg_ == 5) dense_gemm_kernel<RAW, kBkGrad, 8><<<raw_blocks, 8 * 64, 0, s>>>(m);   // (8 waves, 64 x 32 each)
+            else if (step_cfg_ >= 5) dense_gemm_kernel<RAW, kBkGrad, 8><<<raw_blocks, 8 * 64, 0, s>>>(m);   // (8 waves, 64 x 32 each)
             else dense_gemm_kernel<RAW, kBkGrad, kNwGrad><<<raw_blocks, kNwGrad * 64, 0, s>>>(m);
             DTRY(hipGetLastError());
         } else if (t >= 0) {   // alpha[t+1]^T = A^T alpha[t]^T
@@ -1609,7 +1609,7 @@ hipError_t DensePath::enqueue_lib(const double* w, const double* p, bool structu
             m.out = cur;
             if (dma) dense_mm_kernel<true, false><<<mm_blocks, 256, 0, s>>>(m);
             else if (step_cfg_ == 3) dense_gemm_kernel<RAW, kBkStep, 4><<<raw_blocks, 4 * 64, 0, s>>>(m);
-            else if (step_cfg_ == 5) dense_gemm_kernel<RAW, kBkGrad, 8><<<raw_blocks, 8 * 64, 0, s>>>(m);   // (8 waves, 64 x 32 each)
+            else if (step_cfg_ >= 5) dense_gemm_kernel<RAW, kBkGrad, 8><<<raw_blocks, 8 * 64, 0, s>>>(m);   // (8 waves, 64 x 32 each)
             else dense_gemm_kernel<RAW, kBkGrad, kNwGrad><<<raw_blocks, kNwGrad * 64, 0, s>>>(m);
             DTRY(hipGetLastError());
         } else if (t < T_ - 1) {   // beta[t]^T = A Y[t+1]^T
@@ -1644,6 +1644,7 @@ hipError_t DensePath::enqueue_lib(const double* w, const double* p, bool structu
         q.amat = amat_;
         q.grad = out + 1;
         if (dma && step_cfg_ == 4) dense_mm_kernel<false, true><<<int((np / kT) * (np / kT)), 256, 0, s>>>(q);
+        else if (step_cfg_ == 6) dense_gemm_kernel<GRAD, kBkGrad, 8><<<int((np / kT) * (np / kT)), 8 * 64, 0, s>>>(q);
         else dense_gemm_kernel<GRAD, kBkGrad, kNwGrad><<<int((np / kT) * (np / kT)), kNwGrad * 64, 0, s>>>(q);
         DTRY(hipGetLastError());
     } else if (T_ >= 2) {   // G^T = z[1..]^T alpha[0..] over K = (T-1) R rows: g[S np + T] = G(S, T)
