@@ -325,8 +325,8 @@ def roofline_of(m, traffic):
         return {"bound": "mfma", "achieved": tf, "peak": F64_MFMA_PEAK_TFS, "unit": "TFLOP/s",
                 "frac": tf / F64_MFMA_PEAK_TFS if tf else None, "traffic": None,
                 "kernel": {1: "rocblas_dgemm (library fp64 MFMA GEMMs) + our epilogue kernels, one evaluation",
-                           2: "dense_gemm_kernel<RAW> (hand-written v_mfma_f64_16x16x4f64, K in two halves) + "
-                              "dense_gemm_kernel<GRAD> + our epilogue kernels, one evaluation",
+                           2: "dense_gemm_kernel<RAW> (hand-written v_mfma_f64_16x16x4f64, 8-wave 128x128 blocks, K in "
+                              "two halves) + dense_gemm_kernel<GRAD> + our epilogue kernels, one evaluation",
                            3: "dense GEMMs with LDS-DMA pipelined tiles (hand-written v_mfma_f64_16x16x4f64, "
                               "WFSA_DENSE_ENGINE=dma) + our epilogue kernels, one evaluation"}.get(
                                st1.get("dense_blas", 0),

@@ -104,7 +104,11 @@ public:
 private:
     int n_cu_ = 256;
     int grad_cfg_ = 0;   // gradient GEMM: 4-wave blocks, K slices of 16, two blocks per CU (WFSA_DENSE_GRAD_CFG=1: 8-wave, 32; 65.7 vs 69.8 ms, profiles/r04/gemm_cfg_ab.txt)
-    int step_cfg_ = 0;   // WFSA_DENSE_STEP_CFG (timing experiments): 1 per-step GEMMs with 4-wave blocks, 2 K slices of 16, 3 engine 2 with K slices of 32, 4 engine 3 with its own gradient GEMM (else the register-staged one: 64 vs 82 ms)
+    // WFSA_DENSE_STEP_CFG: 5 (default) engine 2's step GEMMs as 8-wave 128 x 128 blocks, 64 x 32 per wave,
+    // two blocks per CU (c5 0.797 -> 0.814 of the fp64 peak, profiles/r05/c5_step_gemm_8wave.txt); timing
+    // experiments: 0 the 4-wave blocks, 6 the gradient GEMM in 8-wave blocks too (0.80), 1 per-step GEMMs with
+    // 4-wave blocks, 2 K slices of 16, 3 engine 2 with K slices of 32, 4 engine 3 with its own gradient GEMM
+    int step_cfg_ = 5;
     int32_t n_params_ = 0, np_ = 0, vocab_ = 0, nct_ = 0;
     int32_t code_se_ = kCodeNone;
     int16_t sym_of_byte_[256] = {};
