@@ -368,10 +368,13 @@ def roofline_of(m, traffic):
         kernel = ("wave_pull_kernel (traversal strings: a wavefront per string, each step's nodes pulled lane by "
                   "lane over the byte-pair edge lists)" if pull else
                   "wide2_kernel (traversal strings: a wavefront per string over byte-pair edge lists, LDS rows)")
-        note = ("HBM is not this pass's bound (SURVEY 8d): a dependent per-position chain of L2 loads, LDS "
-                "gathers and LDS fixed-point gradient adds per string, 16 strings in flight per CU; its honest "
-                "efficiency figure is fp64_flops_frac.  The implementation also writes every alpha row to HBM "
-                "and reads it back (alpha_history_bytes).  PMC: profiles/r03/famb_pull_pmc.txt")
+        note = ("frac is against the algorithmic bytes (SURVEY 8d: string bytes + offset + p), which this pass "
+                "is far from: a dependent per-position chain of L2 loads, LDS gathers and LDS fixed-point "
+                "gradient adds per string, 16 strings in flight per CU.  PMC (profiles/r05/famb/pmc.txt): waves "
+                "wait 55% of their cycles, LDS bank conflicts 61% of LDS-active cycles, L2 hit rate 69%, and "
+                "2.7-4.7 TB/s of HBM traffic (raw / calibrated FETCH_SIZE + WRITE_SIZE): the alpha history "
+                "(every row written and read back, alpha_history_bytes) and L2 misses on the byte-pair entry "
+                "tables, so the pass is HBM-loaded as well as latency-bound")
         extra = {"alpha_history_bytes": 16 * rows, "nodes_per_lane": pull}
     else:
         kernel = "traversal tiers (trav_kernel<MODE_WEIGHTED> tiers 0/1 + wide_kernel tier 2), per step"

@@ -26,4 +26,6 @@ k = 5
 for _ in range(k):
     ll, g, _ = dev.objective_grad(w, want_logq=False)
 dt = (time.perf_counter() - t) / k
-print(f"dbg {os.environ.get('WFSA_W2_DBG', '0')}: {dt * 1e3:.3f} ms per evaluation, ll {ll:.6g}")
+lib = os.path.basename(os.path.dirname(os.environ.get("WFSA_LIB", "release/x")))
+print(f"{lib} dbg {os.environ.get('WFSA_W2_DBG', '0')}: {dt * 1e3:.3f} ms per evaluation, "
+      f"{n / dt / 1e6:.2f} M strings/s, ll {ll!r}, grad sum {float(np.sum(g))!r} |g| {float(np.abs(g).sum())!r}")

@@ -1114,9 +1114,17 @@ __global__ __launch_bounds__(kWide2Block) void wide2_kernel(WideArgs a) {
 #define WFSA_PULL_UB 2   // backward entries per lane in flight
 #endif
 // timing variants only (make var, never the release build): 1 no alpha
-// gather in the backward, 2 no gradient credits
+// gather in the backward, 2 no gradient credits, 3 no alpha history at all
+// (neither the forward's row stores nor the backward's gather)
 #ifndef WFSA_PULL_EXP
 #define WFSA_PULL_EXP 0
+#endif
+// 1: the alpha history in slot layout (fb_kernels.hpp wide2_rows): the forward
+// copies each finished row from LDS into the slots the backward's lanes read,
+// 64-lane coalesced both ways, and the backward needs no source lists.  As
+// fast as the compact rows, bitwise equal (profiles/r05/famb/alpha_history.txt)
+#ifndef WFSA_PULL_SLOT
+#define WFSA_PULL_SLOT 0
 #endif
 template <int NI, bool TRACK>
 __global__ __launch_bounds__(kPullBlock) void wave_pull_kernel(WideArgs a) {
@@ -1139,8 +1147,9 @@ __global__ __launch_bounds__(kPullBlock) void wave_pull_kernel(WideArgs a) {
         for (int j = int(threadIdx.x); j < m.n_params + kWave; j += int(blockDim.x)) gl[j] = 0;   // + spare slots
     __syncthreads();
     double* H = a.scratch2 + (int64_t(blockIdx.x) * nwv + wv) * a.stride2;
-    double* Mg = H + 1 + int64_t(a.max_len) * MN;   // [2][max_n] min-forward rows (rmin column)
+    double* Mg = H + a.hrows2;   // [2][max_n] min-forward rows (rmin column)
     int* ex = reinterpret_cast<int*>(Mg + 2 * int64_t(MN));   // [max_len + 2]
+    constexpr int kS = NI * kWave;   // a row of the slot layout
     auto add_fix = [&](int j, long long iv) {
         if (lgrad) block_add_fix(&gl[j], iv); else fix128_add(gfix + 2 * int64_t(j), iv);
     };
@@ -1152,6 +1161,16 @@ __global__ __launch_bounds__(kPullBlock) void wave_pull_kernel(WideArgs a) {
             if (p1 >= 0) add_fix(p1, iv);
         } else if (p0 == -2) {
             for (int q = m.pptr[g]; q < m.pptr[g + 1]; ++q) add_fix(m.pidx[q], iv);
+        }
+    };
+    // slot layout: the lane's backward sources (16-bit row indices, 0xffff
+    // none) of row 0 of a pair's backward entries, copied from the LDS row
+    auto put_slots = [&](int64_t row, int4 sl) {
+        const unsigned sw[4] = {unsigned(sl.x), unsigned(sl.y), unsigned(sl.z), unsigned(sl.w)};
+#pragma unroll
+        for (int k = 0; k < NI; ++k) {
+            const unsigned u = (sw[k >> 1] >> (16 * (k & 1))) & 0xffffu;
+            H[row * kS + k * kWave + lane] = u != 0xffffu ? R[u] : 0.0;
         }
     };
     for (;;) {
@@ -1166,10 +1185,15 @@ __global__ __launch_bounds__(kPullBlock) void wave_pull_kernel(WideArgs a) {
         // step info, 64 steps at a time in lane registers (lane j: step c*64+j):
         // the pair's forward base / T and backward base / T, |D(byte p)| (-1:
         // no edge consumes the byte), |D of position p|; read with readlane
-        int vfb = 0, vft = 0, vbb = 0, vbt = 0, vnb = 0, vna = 0, vq = 0;
+        // (slot layout: vbn, the backward base of step p + 1)
+        int vfb = 0, vft = 0, vbb = 0, vbt = 0, vnb = 0, vna = 0, vq = 0, vbn = 0;
         auto load_chunk = [&](int c) {
             const int p = c * kWave + lane;
-            vfb = vft = vbb = vbt = vnb = vna = vq = 0;
+            vfb = vft = vbb = vbt = vnb = vna = vq = vbn = 0;
+            if (WFSA_PULL_SLOT && p + 1 < L) {
+                const int b1 = P.bidx[str[p + 1]], a1 = P.bidx[str[p]];
+                if (b1 >= 0 && a1 >= 0) vbn = Q.info[a1 * K + b1].z;
+            }
             if (p < L) {
                 const int bp = P.bidx[str[p]];
                 const int apv = p == 0 ? K : P.bidx[str[p - 1]];
@@ -1224,7 +1248,11 @@ __global__ __launch_bounds__(kPullBlock) void wave_pull_kernel(WideArgs a) {
             load_chunk(0);
             prefetch(0);
         }
+#elif WFSA_PULL_SLOT
+#error "the slot layout loads the first chunk before the forward"
 #endif
+        if (WFSA_PULL_SLOT && L > 0 && __builtin_amdgcn_readlane(vnb, 0) >= 0)   // the start row's slots
+            put_slots(0, Q.bent[int64_t(__builtin_amdgcn_readlane(vbb, 0)) + lane]);
         for (int i = 0; i < L; ++i) {
 #ifdef WFSA_PULL_NOSTEPPF
             if ((i & (kWave - 1)) == 0) load_chunk(i / kWave);
@@ -1239,6 +1267,9 @@ __global__ __launch_bounds__(kPullBlock) void wave_pull_kernel(WideArgs a) {
             const int fb = __builtin_amdgcn_readlane(vfb, ii);
             const int T = __builtin_amdgcn_readlane(vft, ii);
             const int4 dh = pdh;   // the lane's destinations
+            // slot layout: the sources of step i + 1's backward, in flight over this step
+            const int4 slf = WFSA_PULL_SLOT && i + 1 < L
+                ? Q.bent[int64_t(__builtin_amdgcn_readlane(vbn, ii)) + lane] : make_int4(-1, -1, -1, -1);
             const double sc = ldexp(1.0, -exi);
             const int64_t rn = roff + last_n;
             const double* Mi = Mg + int64_t(i & 1) * MN;
@@ -1318,13 +1349,14 @@ __global__ __launch_bounds__(kPullBlock) void wave_pull_kernel(WideArgs a) {
                     if (d == 0xffffu) continue;
                     const double v = acc[k] * sc;
                     R[d] = v;
-                    H[rn + d] = v;
+                    if (WFSA_PULL_EXP != 3 && !WFSA_PULL_SLOT) H[rn + d] = v;
                     if (v > 0.0) emx = max(emx, __builtin_amdgcn_frexp_exp(v));
                     if (TRACK) Mn[d] = amin[k];
                 }
             }
             emx = wave_max_exp(emx);
             wave_sync();
+            if (WFSA_PULL_SLOT && WFSA_PULL_EXP != 3 && i + 1 < L) put_slots(i + 1, slf);
             if (TRACK) wave_fence();   // the next step reads the min row from HBM
             roff = rn;
             last_n = nb;
@@ -1417,7 +1449,10 @@ __global__ __launch_bounds__(kPullBlock) void wave_pull_kernel(WideArgs a) {
             const double sc = ldexp(1.0, -ex_next), sci = ldexp(1.0, -ex_i);
             double acc[NI], av[NI];
             int dd[NI];
-            {   // alpha of the lane's sources, in its item order (row 0 of the pair's entries)
+            if (WFSA_PULL_SLOT && WFSA_PULL_EXP != 1 && WFSA_PULL_EXP != 3) {   // the row's slots, coalesced
+#pragma unroll
+                for (int k = 0; k < NI; ++k) av[k] = H[int64_t(i) * kS + k * kWave + lane] * sci;
+            } else {   // alpha of the lane's sources, in its item order (row 0 of the pair's entries)
                 const int4 sl = have_next ? sl_next : Q.bent[int64_t(bb) + lane];
 #ifdef WFSA_PULL_NOPF   // (layout-variant builds: no prefetch)
                 have_next = false;
@@ -1429,7 +1464,7 @@ __global__ __launch_bounds__(kPullBlock) void wave_pull_kernel(WideArgs a) {
 #pragma unroll
                 for (int k = 0; k < NI; ++k) {
                     const unsigned u = (sw[k >> 1] >> (16 * (k & 1))) & 0xffffu;
-                    av[k] = WFSA_PULL_EXP == 1 ? (u != 0xffffu ? 1e-3 * sci : 0.0)
+                    av[k] = WFSA_PULL_EXP == 1 || WFSA_PULL_EXP == 3 ? (u != 0xffffu ? 1e-3 * sci : 0.0)
                                                : (u != 0xffffu ? H[roff + int(u)] * sci : 0.0);
                 }
             }

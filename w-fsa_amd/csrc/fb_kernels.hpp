@@ -295,6 +295,7 @@ struct WideArgs {
     double* scratch2;       // per wave: alpha rows (compact, 1 + max_len * max_n), min-forward rows
                              // [2 max_n], exponents [max_len + 2]
     int64_t stride2;         // doubles per wave
+    int64_t hrows2;          // wave_pull_kernel: doubles of a wave's alpha rows (the min-forward rows follow)
     unsigned* ctr;           // [2] work and block-exit counters (zero between launches)
     // wide2_kernel's order-independent sums (fixed point, fix128_* in
     // fb_kernels.hip): [2 n_params] gradient accumulators (lo, hi words, fix_frac
@@ -319,8 +320,15 @@ constexpr int kWide2Block = 1024;
 #define WFSA_PULL_BLOCK 1024
 #endif
 constexpr int kPullBlock = WFSA_PULL_BLOCK;
-inline int64_t wide2_stride(int32_t max_len, int32_t max_n) {
-    return 1 + int64_t(max_len) * max_n + 2 * int64_t(max_n) + (int64_t(max_len) + 3) / 2 + 2;
+// alpha rows of a wave: compact (wide2_kernel, 1 + max_len * max_n), or in
+// wave_pull_kernel's slot layout (a row per step of items * 64 slots, slot
+// k * 64 + lane the lane's k-th backward source); the larger of the two
+inline int64_t wide2_rows(int32_t max_len, int32_t max_n, int32_t items) {
+    const int64_t compact = 1 + int64_t(max_len) * max_n, slots = int64_t(max_len) * items * 64;
+    return compact > slots ? compact : slots;
+}
+inline int64_t wide2_stride(int32_t max_len, int32_t max_n, int32_t items = 0) {
+    return wide2_rows(max_len, max_n, items) + 2 * int64_t(max_n) + (int64_t(max_len) + 3) / 2 + 2;
 }
 // LDS of a block: the gradient table (grad_lds, + 64 spare slots) + per wave 2 rows of max_n doubles
 inline size_t wide2_lds(int32_t n_params, bool grad_lds, int waves, int32_t max_n) {

@@ -546,6 +546,7 @@ wfsa::WideArgs wide_args(wfsa_dev* ctx) {
     }
     a.scratch2 = ctx->w2_scratch.ptr;
     a.stride2 = ctx->w2_stride;
+    a.hrows2 = wfsa::wide2_rows(ctx->max_len, ctx->pt_max_n, ctx->pl_items);
     a.ctr = ctx->w2_ctr.ptr;
     a.fix = ctx->w2_fix.ptr;
     a.fix_frac = ctx->w2_fix_frac;
@@ -1972,7 +1973,7 @@ int prepare(wfsa_dev* ctx, int level) {
             ctx->w2_n = int32_t(w2l.size());
         }
         const int wpb = ctx->w2_waves;
-        ctx->w2_stride = wfsa::wide2_stride(ctx->max_len, ctx->pt_max_n);
+        ctx->w2_stride = wfsa::wide2_stride(ctx->max_len, ctx->pt_max_n, ctx->pl_items);
         const int64_t budget = (int64_t(16) << 30) / 8;   // 16 GiB of alpha rows at most
         int64_t g = std::min<int64_t>(ctx->n_cu, (int64_t(w2l.size()) + wpb - 1) / wpb);
         g = std::min<int64_t>(g, budget / (int64_t(wpb) * ctx->w2_stride));
