@@ -2486,7 +2486,15 @@ int build_qw_batches(wfsa_dev* ctx) {
     ctx->qw_nbatch = 0;
     const int32_t n = ctx->qn_n, k = ctx->qn_k;
     const std::vector<int32_t>& cptr = ctx->h_cptr;
-    const int32_t cap = kWave * wfsa::kQnWaveChunkRounds;
+    // a batch's chunks are spread 8 lanes each, 8 per round: the target cap
+    // bounds a QN wave's rounds (48: six; c3 -0.3 us/step against 256,
+    // profiles/r05/option_sweeps.txt), raised to the largest constraint's
+    // chunks when one alone needs more (then the hard limit, 256, decides)
+    static const int32_t target = [] {
+        const char* e = std::getenv("WFSA_QW_CHUNKS");   // (timing sweeps)
+        return e ? std::atoi(e) : 48;
+    }();
+    const int32_t limit = kWave * wfsa::kQnWaveChunkRounds;
     if (!ctx->qn_fused || k <= 0 || n <= 0 || int64_t(cptr.size()) != int64_t(k) + 1 ||
         int64_t(ctx->h_mchunk.size()) < n || ctx->slot_order.size() != size_t(ctx->n_params))
         return WFSA_OK;
@@ -2495,10 +2503,14 @@ int build_qw_batches(wfsa_dev* ctx) {
         for (int32_t i = cptr[size_t(c0)]; i < cptr[size_t(c1)]; ++i) t += ctx->h_mnch[size_t(i)];
         return t;
     };
+    int64_t widest = 0;
     for (int32_t c = 0; c < k; ++c) {
         const int32_t nm = cptr[size_t(c) + 1] - cptr[size_t(c)];
-        if (nm < 1 || nm > wfsa::kQnWaveMembers || chunks(c, c + 1) > cap) return WFSA_OK;
+        const int64_t nc = chunks(c, c + 1);
+        if (nm < 1 || nm > wfsa::kQnWaveMembers || nc > limit) return WFSA_OK;
+        widest = std::max(widest, nc);
     }
+    const int64_t cap = std::min<int64_t>(limit, std::max<int64_t>(widest, target > 0 ? target : limit));
     std::vector<int4> batch;
     std::vector<int32_t> con_of(size_t(n), 0), mfirst(size_t(n), 0);
     for (int32_t c0 = 0; c0 < k;) {
