@@ -2495,6 +2495,11 @@ int build_qw_batches(wfsa_dev* ctx) {
         return e ? std::atoi(e) : 48;
     }();
     const int32_t limit = kWave * wfsa::kQnWaveChunkRounds;
+    static const int32_t mcap = [] {   // members per batch (timing sweeps; at most kQnWaveMembers)
+        const char* e = std::getenv("WFSA_QW_MEMBERS");
+        const int v = e ? std::atoi(e) : 0;
+        return v > 0 && v < wfsa::kQnWaveMembers ? v : wfsa::kQnWaveMembers;
+    }();
     if (!ctx->qn_fused || k <= 0 || n <= 0 || int64_t(cptr.size()) != int64_t(k) + 1 ||
         int64_t(ctx->h_mchunk.size()) < n || ctx->slot_order.size() != size_t(ctx->n_params))
         return WFSA_OK;
@@ -2516,7 +2521,7 @@ int build_qw_batches(wfsa_dev* ctx) {
     for (int32_t c0 = 0; c0 < k;) {
         int32_t c1 = c0 + 1;
         int64_t nch = chunks(c0, c1);
-        while (c1 < k && cptr[size_t(c1) + 1] - cptr[size_t(c0)] <= wfsa::kQnWaveMembers) {
+        while (c1 < k && cptr[size_t(c1) + 1] - cptr[size_t(c0)] <= mcap) {
             const int64_t more = chunks(c1, c1 + 1);
             if (nch + more > cap) break;
             nch += more;
