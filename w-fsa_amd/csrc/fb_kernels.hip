@@ -2739,7 +2739,7 @@ __global__ __launch_bounds__(1024, (DBG == 10 ? 8 : 1)) WFSA_FBS_ATTR void fbs_k
     if (pre && !big_early) table_round(int(threadIdx.x), n_stage, t0);
     if (QN && bid == 0 && threadIdx.x == 0) {   // for the next launch
         a.qw.arrive[a.qw.parity ^ 1] = 0u;
-        if (a.qw.self_finish) a.qw.done[a.qw.parity ^ 1] = 0u;
+        if (a.qw.done) a.qw.done[a.qw.parity ^ 1] = 0u;   // (also when only a Run's last launch finishes itself)
     }
     // halted is written only by an earlier launch (the QN step's finish)
     if (a.halted && *a.halted) {

@@ -387,6 +387,7 @@ struct wfsa_dev {
     DevBuf<unsigned> qw_arrive;      // [2], zero between launches (each launch zeroes the next one's)
     DevBuf<unsigned> qw_done;        // [2] the self-finish's arrivals, likewise
     bool qw_self_finish = false;     // WFSA_QN_SELF_FINISH=1: each launch finishes its own step (fb_kernels.hip)
+    bool qw_last_self = true;        // a Run's last launch finishes its own step (WFSA_QN_LAST_SELF=0: off)
     uint64_t qw_seq = 0;             // in-kernel QN launches enqueued (their parity)
     wfsa::QnWave qw_next{};          // picked up by the next stream kernel launch (qw_next.on)
     DevBuf<unsigned long long> fbs_trace;   // timing experiments (WFSA_FBS_TRACE): per-wave stamps of the last launch
@@ -2565,11 +2566,12 @@ bool qw_usable(wfsa_dev* ctx) {
            !ctx->side_stream && ctx->i_block / kWave >= 3;
 }
 
-int enqueue_qn_step(wfsa_dev* ctx, double eta, double tol, int64_t e, bool timed, bool inkern) {
+int enqueue_qn_step(wfsa_dev* ctx, double eta, double tol, int64_t e, bool timed, bool inkern, bool last) {
     hipStream_t s = ctx->stream;
     const int32_t np = ctx->n_params;
     const int par = int(e & 1);
     const int slot = int(e % kQnDepth);
+    bool self_fin = false;
     ctx->ll_cur = ctx->ll_part.ptr + size_t(par) * ctx->ll_stride;
     const bool trellis = !ctx->dense && !ctx->mpath;
     const bool fused = trellis && ctx->qn_fused && !ctx->comm;
@@ -2669,10 +2671,15 @@ int enqueue_qn_step(wfsa_dev* ctx, double eta, double tol, int64_t e, bool timed
         w.exp_lambda = ctx->qn_exp_lambda;
         w.arrive = ctx->qw_arrive.ptr;
         w.halted = ctx->qn_halted.ptr;
+        w.done = ctx->qw_done.ptr;   // (every launch zeroes the other parity's counter)
         w.fin = f;
-        if (ctx->qw_self_finish) {   // this launch finishes its own step (its stream kernel's blocks' ll partials)
+        // this launch finishes its own step (its stream kernel's blocks' ll
+        // partials): every launch (WFSA_QN_SELF_FINISH=1), or the Run's last,
+        // whose row then needs no finish kernel of its own after it
+        // (WFSA_QN_LAST_SELF=0: that kernel)
+        self_fin = ctx->qw_self_finish || (last && ctx->qw_last_self);
+        if (self_fin) {
             w.self_finish = 1;
-            w.done = ctx->qw_done.ptr;
             w.fin.ll_part = ctx->ll_cur;
             // the stream kernel's blocks, then (bubbles not fused: the bubble
             // kernel ran first) the bubble kernel's waves -- enqueue_evaluation's order
@@ -2686,7 +2693,7 @@ int enqueue_qn_step(wfsa_dev* ctx, double eta, double tol, int64_t e, bool timed
     if (erc) return erc;
     if (ctx->qw_next.on) return fail(WFSA_ERR_HIP, "the in-kernel QN update was not launched");
     if (fused) f.n_ll = n_ll;
-    if (inkern && ctx->qw_self_finish) {   // the step published its own row: no finish pending
+    if (inkern && self_fin) {   // the step published its own row: no finish pending
         const int32_t want = ctx->i_grid + ((ctx->n_bubbles > 0 && !bubbles_fused(ctx, false)) ? ctx->b_waves : 0);
         if (n_ll != want) return fail(WFSA_ERR_HIP, "self-finish: %d log-likelihood partials, not %d", n_ll, want);
         ctx->fin_pending = false;
@@ -2997,6 +3004,7 @@ int wfsa_dev_create(int device, wfsa_dev** out) {
     if (const char* e = std::getenv("WFSA_EARLY_BIG")) ctx->early_big = e[0] == '1';
     if (const char* e = std::getenv("WFSA_QN_COST")) ctx->qw_cost = std::atof(e);
     if (const char* e = std::getenv("WFSA_QN_SELF_FINISH")) ctx->qw_self_finish = e[0] == '1';
+    if (const char* e = std::getenv("WFSA_QN_LAST_SELF")) ctx->qw_last_self = e[0] != '0';
 
     HIP_TRY(hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking));
     if (const char* e = std::getenv("WFSA_PIPE")) ctx->use_pipe = e[0] == '1';
@@ -3668,7 +3676,8 @@ static int qn_run_impl(wfsa_dev* ctx, double eta, double tol, int32_t max_steps,
         // after a halt fewer no-op steps remain queued (their library GEMMs do not skip)
         while (!stop && enq < max_steps && enq - done < (ctx->dense ? 2 : kQnDepth)) {
             const bool tm = timed_step(enq);
-            if (int rc = piped ? enqueue_qn_step_piped(ctx, eta, tol, enq, tm) : enqueue_qn_step(ctx, eta, tol, enq, tm, inkern))
+            if (int rc = piped ? enqueue_qn_step_piped(ctx, eta, tol, enq, tm)
+                               : enqueue_qn_step(ctx, eta, tol, enq, tm, inkern, enq + 1 == max_steps))
                 return rc;
             ++enq;
             ++ctx->seq;
