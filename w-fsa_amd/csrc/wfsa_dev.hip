@@ -1680,8 +1680,13 @@ int prepare(wfsa_dev* ctx, int level) {
         // stream share ends early
         // (reserved whatever WFSA_QN_INKERNEL says: the layout, and so every
         // fixed-order sum, is then the same with the update in or out)
+        static const int64_t per_qw = [] {   // parameters per QN wave (WFSA_QW_PER: timing sweeps)
+            const char* e = std::getenv("WFSA_QW_PER");
+            const int v = e ? std::atoi(e) : 0;
+            return int64_t(v >= 16 ? v : 48);
+        }();
         ctx->qw_waves = (i_wpb >= 3 && delta_want && ctx->i_tables)
-                            ? int(std::min<int64_t>(nblk, (int64_t(ctx->n_params) + 47) / 48)) : 0;
+                            ? int(std::min<int64_t>(nblk, (int64_t(ctx->n_params) + per_qw - 1) / per_qw)) : 0;
         for (int w = 0; w < i_nw; ++w) {
             const int bid = w / i_wpb, wib = w % i_wpb;
             if (bid == 0 && wib == i_wpb - 1) {   // the QN finish's wave (fbs_kernel): no groups
