@@ -15,9 +15,18 @@ import pytest
 pytestmark = pytest.mark.gpu
 
 
-def _learner(W, fsa, sym, off, wt, monkeypatch, inkernel, self_finish=False):
+# where step e's finish (its log-likelihood sum, halt test and info row) runs:
+# "last" (default): in launch e + 1's finish wave, the Run's last launch
+# finishing its own step; "next": always in the next launch, the Run's last
+# step by a finish kernel of its own (WFSA_QN_LAST_SELF=0); "self": every
+# launch finishes its own step (WFSA_QN_SELF_FINISH=1)
+FINISH = ["last", "next", "self"]
+
+
+def _learner(W, fsa, sym, off, wt, monkeypatch, inkernel, finish="last"):
     monkeypatch.setenv("WFSA_QN_INKERNEL", "1" if inkernel else "0")
-    monkeypatch.setenv("WFSA_QN_SELF_FINISH", "1" if self_finish else "0")
+    monkeypatch.setenv("WFSA_QN_SELF_FINISH", "1" if finish == "self" else "0")
+    monkeypatch.setenv("WFSA_QN_LAST_SELF", "0" if finish == "next" else "1")
     lrn = W.QuasiNewtonLearner(0)
     lrn.set_info_rmin(False)
     lrn.BuildFromPacked(fsa, sym, off, wt)
@@ -53,14 +62,14 @@ FAMILIES = {
 }
 
 
-@pytest.mark.parametrize("self_finish", [False, True], ids=["finish-next-launch", "self-finish"])
+@pytest.mark.parametrize("finish", FINISH)
 @pytest.mark.parametrize("family", sorted(FAMILIES))
-def test_inkernel_update_equals_qn_step_kernel(family, self_finish, monkeypatch):
-    """self_finish: each launch's last arrival runs the step's finish and
-    publishes its row (else the next launch's finish wave does)"""
+def test_inkernel_update_equals_qn_step_kernel(family, finish, monkeypatch):
+    """finish: where each step's finish runs (FINISH above); the runs of odd
+    and even length below exercise the Run's last launch finishing itself"""
     import wfsa_amd as W
     fsa, sym, off, wt = _corpus(W, **FAMILIES[family])
-    a = _learner(W, fsa, sym, off, wt, monkeypatch, True, self_finish)
+    a = _learner(W, fsa, sym, off, wt, monkeypatch, True, finish)
     b = _learner(W, fsa, sym, off, wt, monkeypatch, False)
     # runs of odd and even length, back to back: the weight parity and the
     # arrival counters carry across runs
@@ -104,14 +113,14 @@ def test_inkernel_update_matches_host_steps(monkeypatch):
     np.testing.assert_allclose(a.x(), b.x(), rtol=1e-11, atol=1e-13)
 
 
-@pytest.mark.parametrize("self_finish", [False, True], ids=["finish-next-launch", "self-finish"])
-def test_inkernel_halting_run(self_finish, monkeypatch):
+@pytest.mark.parametrize("finish", FINISH)
+def test_inkernel_halting_run(finish, monkeypatch):
     """a halting run stops at the same epoch with the same rows and state as
     the separate kernel; the steps enqueued after the halt are skipped and
     the next run starts cleanly"""
     import wfsa_amd as W
     fsa, sym, off, wt = _corpus(W, **FAMILIES["ambiguous"])
-    a = _learner(W, fsa, sym, off, wt, monkeypatch, True, self_finish)
+    a = _learner(W, fsa, sym, off, wt, monkeypatch, True, finish)
     b = _learner(W, fsa, sym, off, wt, monkeypatch, False)
     ra = a.Run(200, 1.0, 1e-3)
     rb = b.Run(200, 1.0, 1e-3)
