@@ -1856,9 +1856,11 @@ int prepare(wfsa_dev* ctx, int level) {
     // build's deal fit: end = c0 + c1 rows + a charge per kind of extra work)
     // and then swept round-robin on one box (profiles/r05/dealer_fit.txt):
     // class A 9, class B 17, big 13, the QN wave 6 -- c3 29.6 -> 28.1 us per
-    // step against the earlier 18 / 36 / 8 / 8
+    // step against the earlier 18 / 36 / 8 / 8; big 15 after the QN batches
+    // were capped at 48 chunks (the refit's 15.0 rows; -0.3 us per step,
+    // profiles/r05/option_sweeps.txt)
     {
-        double small_cost = 9.0, small_cost_b = 17.0, big_cost = 13.0;
+        double small_cost = 9.0, small_cost_b = 17.0, big_cost = 15.0;
         if (const char* e = std::getenv("WFSA_SMALL_COST")) small_cost = std::atof(e);
         if (const char* e = std::getenv("WFSA_SMALL_COST_B")) small_cost_b = std::atof(e);
         if (const char* e = std::getenv("WFSA_BIG_COST")) big_cost = std::atof(e);
