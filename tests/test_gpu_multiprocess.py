@@ -64,6 +64,9 @@ def _worker(rank, world, port, peer, q, late_s=0.0, abort=False):
         syn = W.Synthetic(**SPEC)
         sym, off, wt = syn.corpus()
         fsa = W.Fsa.read_text(syn.wfsa_text)
+        if abort == "d2h":
+            q.put((rank, _d2h_learn(W, fsa, sym, off, wt, world, rank)))
+            return
         if abort:
             if abort == "stall":
                 os.environ["WFSA_COMM_TIMEOUT_S"] = "3"
@@ -139,6 +142,29 @@ def _abort_learn(W, fsa, sym, off, wt, world, rank, stall=False):
     try:
         rows = lrn.Run(50, 1.0, -1.0)
         return {"raised": None, "rows": len(rows)}
+    except W.WfsaError as e:
+        return {"raised": str(e), "s": time.time() - t0}
+
+
+def _d2h_learn(W, fsa, sym, off, wt, world, rank):
+    """host transport, peer path off; rank 1's 12th payload finds its
+    device-to-host copy failed (WFSA_FAULT_HOST_D2H): it must still join that
+    payload exchange (poisoned) and fail, so rank 0 is never left in a
+    mismatched exchange -- it sees the poison (a non-finite halt) or fails at
+    its next header (WFSA_COMM_TIMEOUT_S), within seconds either way"""
+    import time
+    os.environ["WFSA_COMM_TIMEOUT_S"] = "3"
+    if rank == 1:
+        os.environ["WFSA_FAULT_HOST_D2H"] = "12"
+    t0 = time.time()
+    try:
+        lrn = W.QuasiNewtonLearner(0)
+        lrn.SetHostCommunicator(world, rank, W.torch_allreduce)
+        lrn.BuildFromPacked(fsa, sym, off, wt)
+        lrn.Finalize()
+        lrn.Init(7)
+        rows = lrn.Run(30, 1.0, -1.0)
+        return {"raised": None, "rows": len(rows), "last": list(rows[-1]) if rows else [], "s": time.time() - t0}
     except W.WfsaError as e:
         return {"raised": str(e), "s": time.time() - t0}
 
@@ -228,6 +254,22 @@ def test_two_processes_stalled_rank_times_out_over_gloo():
     assert 2.5 < got[0]["s"] < 15, got[0]
     assert got[1]["raised"], got[1]
     assert got[1]["s"] < 15, got[1]
+
+
+def test_two_processes_failed_copy_keeps_the_exchange_in_step():
+    """a member whose device-to-host copy fails after the header
+    exchange joins the payload exchange poisoned and leaves the transport
+    broken -- it never sends an 8-byte abort header into the peers' payload
+    exchange.  Rank 1 raises with the copy failure; rank 0 ends within
+    seconds, with an error or a non-finite halt (the poison), never a
+    success on a partial sum"""
+    got = _spawn(2, False, abort="d2h")
+    assert got[1]["raised"] and "device to host copy failed" in got[1]["raised"], got[1]
+    assert got[1]["s"] < 60, got[1]
+    r0 = got[0]
+    assert r0["s"] < 60, r0
+    if not r0["raised"]:   # the poison reached it: the run halted non-finite before 30 steps
+        assert r0["rows"] < 30 and not all(np.isfinite(r0["last"][:5])), r0
 
 
 # ---- the peer kernel on one device, the other members simulated ----------

@@ -135,3 +135,19 @@ def test_inkernel_halting_run(finish, monkeypatch):
     b.Init(7)
     assert np.array_equal(np.array(a.Run(5, 1.0, -1.0)), np.array(b.Run(5, 1.0, -1.0)))
     assert np.array_equal(a.x(), b.x())
+
+
+def test_poll_timeout_fails_the_run(monkeypatch):
+    """a QN wave whose arrival wait gives up must not let
+    the step pass as updated.  WFSA_FAULT_QN_POLL=1 makes the first QN wave
+    wait for one arrival too many and give up after a few polls: its
+    constraints keep x / lambda while the other waves update theirs, so the
+    run must fail with the timeout (the finish used to drop the wave's NaN
+    partials in fmin / fmax and report the step as run)"""
+    import wfsa_amd as W
+    fsa, sym, off, wt = _corpus(W, **FAMILIES["familyA"])
+    monkeypatch.setenv("WFSA_FAULT_QN_POLL", "1")
+    a = _learner(W, fsa, sym, off, wt, monkeypatch, True)
+    with pytest.raises(W.WfsaError, match="timed out"):
+        a.Run(4, 1.0, -1.0)
+    assert a.stats()["qn_inkernel_waves"] > 0   # the in-kernel update was the one that ran

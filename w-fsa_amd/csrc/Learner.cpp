@@ -409,40 +409,40 @@ void Learner::ComputeRmin(double* out) const {
     out[1] = double(s);
 }
 
-// Learner::Trim (src/Learner.cpp:350-425) without the P matrix: a used
-// parameter alone in its constraint is fixed to log 1 (-1); the used ones
-// are renumbered, x and C follow.
+// Learner::Trim (src/Learner.cpp:350-425) without the P matrix.  Ccol is
+// sorted, so a constraint is a run of equal entries.  Entry states before:
+// 0 used, -2 unused.  (1) a constraint whose used members number exactly one
+// has that member fixed (-1: weight log 1); (2) the members still free get
+// consecutive indices in their order, x is compacted the same way, and the
+// constraints that keep a free member are renumbered consecutively.
 void Learner::Trim() {
-    const int32_t n = int32_t(Ccol.size());
-    int32_t c = -1, nnz_in_c = -1;
-    for (int32_t i = 0; i < n; ++i) {
-        const int32_t this_c = Ccol[size_t(i)];
-        if (this_c != c) {
-            c = this_c;
-            if (nnz_in_c >= 0) trimmed_weights[size_t(nnz_in_c)] = -1;
-            nnz_in_c = -1;
-        }
-        if (trimmed_weights[size_t(i)] >= 0) nnz_in_c = (nnz_in_c == -1) ? i : -2;
+    const size_t n = Ccol.size();
+    for (size_t run = 0; run < n;) {
+        size_t end = run, n_used = 0, only = 0;
+        for (; end < n && Ccol[end] == Ccol[run]; ++end)
+            if (trimmed_weights[end] >= 0) {
+                ++n_used;
+                only = end;
+            }
+        if (n_used == 1) trimmed_weights[only] = -1;
+        run = end;
     }
-    if (nnz_in_c >= 0) trimmed_weights[size_t(nnz_in_c)] = -1;
-
-    std::vector<int32_t> ccol_new;
-    ccol_new.reserve(size_t(n));
-    int32_t good = 0, good_c = -1;
-    c = -1;
-    for (int32_t i = 0; i < n; ++i) {
-        if (trimmed_weights[size_t(i)] != 0) continue;
-        trimmed_weights[size_t(i)] = good++;
-        _x[size_t(trimmed_weights[size_t(i)])] = _x[size_t(i)];
-        if (c < Ccol[size_t(i)]) {
-            ++good_c;
-            c = Ccol[size_t(i)];
+    std::vector<int32_t> con_of_free;   // the renumbered constraint of each free member
+    con_of_free.reserve(n);
+    int32_t n_free = 0, n_con = 0, cur_con = 0;
+    for (size_t j = 0; j < n; ++j) {
+        if (trimmed_weights[j] != 0) continue;
+        if (n_free == 0 || Ccol[j] != cur_con) {   // the first free member of its constraint
+            cur_con = Ccol[j];
+            ++n_con;
         }
-        ccol_new.push_back(good_c);
+        _x[size_t(n_free)] = _x[j];   // (n_free <= j: compaction in place)
+        trimmed_weights[j] = n_free++;
+        con_of_free.push_back(n_con - 1);
     }
-    Ccol.swap(ccol_new);
-    Crow.resize(size_t(good) + 1);
-    _x.resize(size_t(good));
+    Ccol = std::move(con_of_free);
+    Crow.resize(size_t(n_free) + 1);
+    _x.resize(size_t(n_free));
 }
 
 double Learner::GetWeight(int32_t i) const {   // src/Learner.cpp:427-436

@@ -274,6 +274,8 @@ std::unique_ptr<Collective> make_rccl_collective(int nranks, int rank, const uin
     static_assert(sizeof(ncclUniqueId) == kCommIdBytes, "ncclUniqueId size");
     ncclUniqueId uid;
     std::memcpy(&uid, id, sizeof uid);
+    void* agree = Collective::reserve_agreement(err);   // before joining: a failure here leaves no member short
+    if (!agree) return nullptr;
     ncclComm_t c = nullptr;
     // non-blocking: a member that never joins ends the set-up after
     // WFSA_COMM_TIMEOUT_S instead of blocking this thread for good
@@ -285,10 +287,11 @@ std::unique_ptr<Collective> make_rccl_collective(int nranks, int rank, const uin
         err = r == ncclInProgress ? std::string("ncclCommInitRankConfig: the members did not all join within WFSA_COMM_TIMEOUT_S")
                                   : std::string("ncclCommInitRankConfig failed: ") + ncclGetErrorString(r);
         if (c) (void)ncclCommAbort(c);
+        (void)hipFree(agree);
         return nullptr;
     }
     auto col = std::make_unique<RcclCollective>(c, nranks, rank);
-    if (!col->reserve_agreement(err)) return nullptr;
+    col->adopt_agreement(agree);
     return col;
 }
 
@@ -302,6 +305,8 @@ std::unique_ptr<Collective> make_local_collective(int nranks, int rank, const ui
         err = "in-process group: size does not match its id (at most 16 members)";
         return nullptr;
     }
+    void* agree = Collective::reserve_agreement(err);   // before joining the group (see collective.hpp)
+    if (!agree) return nullptr;
     std::shared_ptr<LocalGroup> g;
     {
         std::lock_guard<std::mutex> lk(g_reg_m);
@@ -317,7 +322,7 @@ std::unique_ptr<Collective> make_local_collective(int nranks, int rank, const ui
         if (++g->joined == n) g_reg.erase(serial);   // every member holds the group now
     }
     auto col = std::make_unique<LocalCollective>(g, rank, device);
-    if (!col->reserve_agreement(err)) return nullptr;
+    col->adopt_agreement(agree);
     return col;
 }
 
@@ -351,6 +356,9 @@ public:
     HostCollective(int n, int r, HostAllreduceFn fn, void* user) : fn_(fn), user_(user) {
         n_ = n;
         r_ = r;
+        // fault injection (tests/test_gpu_multiprocess.py): payload number k
+        // (from 1) of this member finds its device-to-host copy failed
+        if (const char* e = std::getenv("WFSA_FAULT_HOST_D2H")) fault_at_ = std::atoi(e);
     }
     const char* kind() const override { return "host"; }
     void abort_transport(const std::string&) override {
@@ -377,15 +385,30 @@ public:
         }
         const size_t bytes = n * (op == RedOp::MaxU8 ? 1 : 8);
         if (host_.size() < bytes) host_.resize(bytes);
-        if (hipMemcpyAsync(host_.data(), buf, bytes, hipMemcpyDeviceToHost, s) != hipSuccess ||
-            hipStreamSynchronize(s) != hipSuccess) {
-            err_ = "host transport: device to host copy failed";
-            return 1;
+        // After the header the members are committed to this payload
+        // exchange: a local copy failure still joins it (so no member is left
+        // in an exchange of n elements while this one sends an 8-byte abort
+        // header), with a poisoned buffer -- all bits set: NaN doubles, which
+        // make the members' sums and minima non-finite, 0xff bytes -- and
+        // then leaves the transport broken: this member makes no further
+        // calls, so the others fail at their next header exchange (the
+        // callback's own wait limit) at the latest
+        bool local_bad = (++payloads_ == fault_at_ ||
+                          hipMemcpyAsync(host_.data(), buf, bytes, hipMemcpyDeviceToHost, s) != hipSuccess ||
+                          hipStreamSynchronize(s) != hipSuccess);
+        if (local_bad) {
+            (void)hipGetLastError();
+            std::memset(host_.data(), 0xff, bytes);
         }
         const int32_t code = op == RedOp::SumF64 ? 0 : op == RedOp::MinF64 ? 1 : 2;
         phase_ = 2;
         const int pr = fn_(user_, host_.data(), int64_t(n), code);
         phase_ = 0;
+        if (local_bad) {
+            broken_ = true;
+            err_ = "host transport: device to host copy failed";
+            return 1;
+        }
         if (pr != 0) {
             broken_ = true;
             err_ = "host transport: the all-reduce callback failed";
@@ -404,6 +427,7 @@ private:
     void* user_;
     std::vector<uint8_t> host_;
     int phase_ = 0;         // 1 / 2: inside the header / payload callback
+    int payloads_ = 0, fault_at_ = 0;   // (fault injection)
     bool broken_ = false;   // aborted, poisoned or a failed callback: the exchange is out of step
 };
 
@@ -415,8 +439,10 @@ std::unique_ptr<Collective> make_host_collective(int nranks, int rank, HostAllre
         err = "host transport: bad arguments";
         return nullptr;
     }
+    void* agree = Collective::reserve_agreement(err);
+    if (!agree) return nullptr;
     auto col = std::make_unique<HostCollective>(nranks, rank, fn, user);
-    if (!col->reserve_agreement(err)) return nullptr;
+    col->adopt_agreement(agree);
     return col;
 }
 
@@ -698,14 +724,14 @@ double comm_timeout_s() {
 
 constexpr size_t kAgreeBytes = std::max(size_t(3000) * sizeof(double), size_t(kLocalMaxRanks) * 88);
 
-bool Collective::reserve_agreement(std::string& err) {
-    if (hipMalloc(&agree_buf_, kAgreeBytes) != hipSuccess) {
+void* Collective::reserve_agreement(std::string& err) {
+    void* b = nullptr;
+    if (hipMalloc(&b, kAgreeBytes) != hipSuccess) {
         (void)hipGetLastError();
-        agree_buf_ = nullptr;
         err = "communicator set-up: no device memory for the peer path's agreement";
-        return false;
+        return nullptr;
     }
-    return true;
+    return b;
 }
 
 Collective::~Collective() {

@@ -93,7 +93,11 @@ protected:
     // agreement (every member then takes part in every exchange)
     void* agree_buf_ = nullptr;
 public:
-    bool reserve_agreement(std::string& err);   // (the make_*_collective functions call it)
+    // (the make_*_collective functions reserve it BEFORE joining the group or
+    // creating the communicator -- a member that cannot reserve it then fails
+    // alone, never leaving the others a member short -- and hand it over)
+    static void* reserve_agreement(std::string& err);
+    void adopt_agreement(void* buf) { agree_buf_ = buf; }
 protected:
 
 private:

@@ -2641,16 +2641,27 @@ __device__ __forceinline__ void qn_wave_run(const QnWave& q, int r, unsigned lon
     int ok = 1;
     if (lane == 0) {
         unsigned it = 0;
+        const unsigned limit = q.poll_limit ? q.poll_limit : kQnPollLimit;
+        const unsigned want = unsigned(q.n_arrive) + ((q.poll_fault && r == 0) ? 1u : 0u);   // (fault injection)
         // (every QN wave polls the one counter: a go token per wave's own
         // line, written by the last arrival, measured no faster, r05)
-        while (load_wt(q.arrive + q.parity) < unsigned(q.n_arrive)) {
+        while (load_wt(q.arrive + q.parity) < want) {
             __builtin_amdgcn_s_sleep(1);
-            if (++it > kQnPollLimit) {
+            if (++it > limit) {
                 ok = 0;
                 break;
             }
         }
+        // a wave that gave up leaves its constraints un-updated: the timeout
+        // word makes this step's finish report kQnTimedOut (its NaN partials
+        // alone would be dropped by the finish's fmin / fmax), and the host
+        // then fails the run instead of stepping on inconsistent weights
+        if (!ok) store_wt(q.halted + 2, 1u);
     }
+    // (a compiler barrier: no load below moves above the poll; on the
+    // hardware a workgroup-scope acquire is only a vmcnt wait -- see the
+    // ordering note at the arrival in fbs_kernel)
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
     ok = __shfl(ok, 0, kWave);
     if (tr && lane == 0) tr[5] = __builtin_amdgcn_s_memrealtime();   // (timing experiments)
     // the halt decision of this launch's finish wave: issued now, waited for
@@ -2958,6 +2969,21 @@ __global__ __launch_bounds__(1024, (DBG == 10 ? 8 : 1)) WFSA_FBS_ATTR void fbs_k
         big_bubbles();   // (an early big-bubble wave skipped the staging: it is here at entry)
     }
     WFSA_STAMP(2)
+    // Ordering of the in-launch hand-off (slot stores -> arrival -> the QN
+    // waves' reads).  The arrival is a RELAXED agent-scope atomic and the
+    // poll a relaxed sc1 load, so the HIP memory model alone gives no
+    // happens-before; an agent-scope release / acquire would, but on gfx950
+    // it is an L2 write-back / invalidate per wave (round 2's grid barrier:
+    // 38 -> 88 us).  The hardware argument instead: (1) every slot store is
+    // write-through (store_wt: sc1, to memory past the XCD's L2); (2) the
+    // storing wave waits vmcnt(0) -- its stores acknowledged by memory --
+    // before its LDS arrival, and the block's last wave adds to the global
+    // counter only after every wave of the block arrived (LDS atomics order
+    // within the block); (3) the consumer's loads are sc1 (they bypass the
+    // stale L2) and are issued after its poll matched (a compiler barrier
+    // there; vector loads are not speculated).  So a consumer that saw the
+    // count reads the stored values.  The same argument covers the done
+    // counter and the self-finish's partials.
     if (QN) {   // this wave's slot stores (and the finish wave's halt decision) retired: arrive
         if (stored) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         unsigned prev = 0u;
@@ -3664,6 +3690,14 @@ static hipError_t launch_compiled_impl(const CompiledArgs& a, int grid, int bloc
         default: hipLaunchKernelGGL((fbc_kernel<0, false, true>), g, b, 0, stream, a); break;
     }
     return hipGetLastError();
+}
+
+int fbs_qn_blocks_per_cu(int block, size_t lds) {
+    int nb = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, fbs_kernel<false, true, false, 0, false, true, true>, block,
+                                                     lds) != hipSuccess)
+        return 0;
+    return nb;
 }
 
 int bubble_waves(int32_t n_small4, int32_t n_small, int32_t n_big) { return n_big + int(small_chunks(n_small4, n_small)); }

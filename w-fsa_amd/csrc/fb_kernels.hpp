@@ -466,7 +466,9 @@ hipError_t launch_hf(const HfArgs& a, hipStream_t stream, const HfTravArgs* trav
 // halted, which every evaluation kernel of the later steps checks at entry.
 // A launch never reads a flag that the same launch writes.
 constexpr int kQnRow = 8;
-constexpr unsigned kQnRan = 0, kQnHalted = 1, kQnNonFinite = 2, kQnSkipped = 3;
+// kQnTimedOut: an in-kernel QN wave's arrival wait gave up (its constraints
+// were not updated; the finish reports it and the host fails the run)
+constexpr unsigned kQnRan = 0, kQnHalted = 1, kQnNonFinite = 2, kQnSkipped = 3, kQnTimedOut = 4;
 constexpr int kQnBlock = 256;
 constexpr int kQnMaxSeg = 1024;   // members of a constraint the fused kernel keeps in LDS
 struct QnFinish {
@@ -482,7 +484,8 @@ struct QnFinish {
     int32_t k;
     double plogp, tol;
     int32_t ring_slot;           // ring slot of the step
-    const unsigned* halted;      // [0] halted, [1] halt_pending (the finish writes [1])
+    const unsigned* halted;      // [0] halted, [1] halt_pending (the finish writes [1]),
+                                 // [2] an in-kernel QN wave's wait timed out (sc1)
     unsigned* halt_pending;
     unsigned* seq;               // device sequence counter
     unsigned* host_flag;         // host-mapped completion flag
@@ -632,11 +635,14 @@ struct QnWave {
     double eta;
     int32_t exp_lambda;
     unsigned* arrive;            // [2] per-parity arrival counters
-    unsigned* halted;            // [0] halted (earlier launches), [1] halt_pending (this launch's finish, sc1)
+    unsigned* halted;            // [0] halted (earlier launches), [1] halt_pending (this launch's finish, sc1),
+                                 // [2] set by a QN wave whose arrival wait timed out
     QnFinish fin;                // this step's publication (a skipped row after a halt; with self_finish, its row)
     int32_t self_finish;         // the launch's last finisher (after every block's log-likelihood partial and
                                  // every QN wave's partials, write-through) runs this step's finish itself
     unsigned* done;              // [2] per-parity counters of those arrivals (each launch zeroes the other's)
+    uint32_t poll_limit;         // polls before a QN wave gives up (0: kQnPollLimit)
+    int32_t poll_fault;          // fault injection (tests): QN wave 0 waits for one arrival too many
 };
 
 struct CompiledArgs {
@@ -773,6 +779,9 @@ __host__ __device__ inline int64_t small_entry(int64_t c, int l, int64_t n4, int
     return b < n4 + ns ? b : -1;
 }
 int bubble_waves(int32_t n_small4, int32_t n_small, int32_t n_big);
+// blocks of the stream kernel with the in-kernel QN update that one CU holds
+// at once (block threads, dynamic LDS bytes); 0 on error
+int fbs_qn_blocks_per_cu(int block, size_t lds);
 hipError_t launch_bubbles(const BubbleArgs& a, hipStream_t stream);
 hipError_t launch_reduce(const ReduceArgs& a, hipStream_t stream);
 // out[1 + j] = sum over k of gpart[k][j] in k order (the preparation-time gradient slabs)

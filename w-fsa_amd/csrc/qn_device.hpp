@@ -224,6 +224,9 @@ template <bool WAVE = false, bool WT = false>   // WT: the partials read write-t
 __device__ inline void qn_finish_compute(const QnFinish& f, double* red, double* info, unsigned& status) {
     const int t = WAVE ? int(threadIdx.x) % 64 : int(threadIdx.x), nt = WAVE ? 64 : int(blockDim.x), nw = nt / 64;
     double gmin = INFINITY, gmax = -INFINITY, lmin = INFINITY, ge = 0.0;
+    // a NaN partial (fmin / fmax would drop it) makes the row non-finite:
+    // counted beside the minima
+    double nanp = 0.0;
     for (int j0 = t; j0 < f.n_blocks; j0 += 4 * nt) {   // four blocks' partials in flight per thread
         double4 v[4];
 #pragma unroll
@@ -241,6 +244,7 @@ __device__ inline void qn_finish_compute(const QnFinish& f, double* red, double*
             gmax = fmax(gmax, v[b].y);
             lmin = fmin(lmin, v[b].z);
             ge = fmax(ge, v[b].w);
+            if (isnan(v[b].x) || isnan(v[b].y) || isnan(v[b].z) || isnan(v[b].w)) nanp = 1.0;
         }
     }
     // the log-likelihood partials in one order whichever form runs (the
@@ -276,11 +280,13 @@ __device__ inline void qn_finish_compute(const QnFinish& f, double* red, double*
         gmax = wave_reduce(gmax, 1);
         lmin = wave_reduce(lmin, 0);
         ge = wave_reduce(ge, 1);
+        nanp = wave_reduce(nanp, 1);
     } else {
         gmin = block_reduce(gmin, 0, red);
         gmax = block_reduce(gmax, 1, red);
         lmin = block_reduce(lmin, 0, red);
         ge = block_reduce(ge, 1, red);
+        nanp = block_reduce(nanp, 1, red);
     }
     for (int o = 32; o > 0; o >>= 1) {
         const double v = __shfl_xor(rv, o, 64), i = __shfl_xor(ri, o, 64);
@@ -318,10 +324,11 @@ __device__ inline void qn_finish_compute(const QnFinish& f, double* red, double*
             info[5] = f.rmin[0];
             info[6] = f.rmin[1];
         }
-        bool finite = true;
+        bool finite = nanp == 0.0;
         for (int i = 0; i < 7; ++i) finite = finite && isfinite(info[i]);
         const bool halt = ge <= f.tol && fabs(gmin) <= f.tol && fabs(gmax) <= f.tol;
         status = !finite ? kQnNonFinite : (halt ? kQnHalted : kQnRan);
+        if (f.halted && load_wt(f.halted + 2) != 0u) status = kQnTimedOut;   // (a QN wave's wait gave up)
     }
 }
 

@@ -387,6 +387,10 @@ struct wfsa_dev {
     DevBuf<unsigned> qw_arrive;      // [2], zero between launches (each launch zeroes the next one's)
     DevBuf<unsigned> qw_done;        // [2] the self-finish's arrivals, likewise
     bool qw_self_finish = false;     // WFSA_QN_SELF_FINISH=1: each launch finishes its own step (fb_kernels.hip)
+    size_t qw_res_lds = ~size_t(0);  // qw_resident's cache: the launch's LDS and block, blocks per CU
+    int qw_res_block = 0, qw_res_per_cu = 0;
+    uint32_t qw_poll_limit = 0;      // polls before an in-kernel QN wave gives up (0: the kernel default)
+    bool qw_poll_fault = false;      // WFSA_FAULT_QN_POLL=1 (tests): the first QN wave never sees its arrivals
     bool qw_last_self = true;        // a Run's last launch finishes its own step (WFSA_QN_LAST_SELF=0: off)
     uint64_t qw_seq = 0;             // in-kernel QN launches enqueued (their parity)
     wfsa::QnWave qw_next{};          // picked up by the next stream kernel launch (qw_next.on)
@@ -2566,11 +2570,30 @@ int build_qw_batches(wfsa_dev* ctx) {
 // step is exactly: one rank, every string compiled into the delta stream, no
 // rmin column, every constraint of 1..64 members (bubbles not fused into the
 // stream kernel run in their own kernel before it)
+//
+// The QN waves wait for every block's arrival, so every block of the grid
+// must be resident at once: the grid is checked against the CUs times the
+// blocks one CU holds at the launch's actual LDS (the big-bubble staging
+// included) -- else the update stays a kernel of its own.
+size_t qn_launch_lds(wfsa_dev* ctx) {   // enqueue_compiled's LDS for the per-iteration launch (no log q)
+    if (bubbles_fused(ctx, false) && ctx->n_big > 0)
+        return big_stage_off(ctx) + size_t(ctx->i_block / kWave) * size_t(wfsa::big_stage_bytes(ctx->big_lds_edges));
+    return ctx->i_lds;
+}
+bool qw_resident(wfsa_dev* ctx) {
+    const size_t lds = qn_launch_lds(ctx);
+    if (ctx->qw_res_lds != lds || ctx->qw_res_block != ctx->i_block) {
+        ctx->qw_res_lds = lds;
+        ctx->qw_res_block = ctx->i_block;
+        ctx->qw_res_per_cu = wfsa::fbs_qn_blocks_per_cu(ctx->i_block, lds);
+    }
+    return int64_t(ctx->i_grid) <= int64_t(ctx->n_cu) * ctx->qw_res_per_cu;
+}
 bool qw_usable(wfsa_dev* ctx) {
     return ctx->use_qw && ctx->qw_ok && ctx->qw_waves > 0 && ctx->qn_fused && !ctx->comm && !ctx->dense &&
            !ctx->mpath && !ctx->qn_rmin && ctx->n_groups > 0 && ctx->delta_on && ctx->i_tables >= 1 &&
            ctx->n_fall[0] + ctx->n_fall[1] + ctx->n_fall[2] == 0 && ctx->fixed_t_on && ctx->qn_k > 0 &&
-           !ctx->side_stream && ctx->i_block / kWave >= 3;
+           !ctx->side_stream && ctx->i_block / kWave >= 3 && qw_resident(ctx);
 }
 
 int enqueue_qn_step(wfsa_dev* ctx, double eta, double tol, int64_t e, bool timed, bool inkern, bool last) {
@@ -2679,6 +2702,8 @@ int enqueue_qn_step(wfsa_dev* ctx, double eta, double tol, int64_t e, bool timed
         w.arrive = ctx->qw_arrive.ptr;
         w.halted = ctx->qn_halted.ptr;
         w.done = ctx->qw_done.ptr;   // (every launch zeroes the other parity's counter)
+        w.poll_limit = ctx->qw_poll_limit;
+        w.poll_fault = ctx->qw_poll_fault ? 1 : 0;
         w.fin = f;
         // this launch finishes its own step (its stream kernel's blocks' ll
         // partials): every launch (WFSA_QN_SELF_FINISH=1), or the Run's last,
@@ -2999,6 +3024,12 @@ int wfsa_dev_create(int device, wfsa_dev** out) {
     if (const char* e = std::getenv("WFSA_PULL")) ctx->use_pull = e[0] != '0';
     if (const char* e = std::getenv("WFSA_WIDE2_TIERS")) ctx->w2_all = std::strcmp(e, "2") != 0;
     if (const char* e = std::getenv("WFSA_QN_INKERNEL")) ctx->use_qw = e[0] != '0';
+    // fault injection (tests/test_gpu_qn_inkernel.py): the first QN wave waits
+    // for an arrival that never comes and gives up after a few polls
+    if (const char* e = std::getenv("WFSA_FAULT_QN_POLL"); e && e[0] == '1') {
+        ctx->qw_poll_fault = true;
+        ctx->qw_poll_limit = 256;
+    }
     if (const char* e = std::getenv("WFSA_EARLY_BUB")) ctx->early_bub = e[0] == '1';
     if (const char* e = std::getenv("WFSA_DMA_STAGE")) ctx->dma_stage = e[0] == '1';
     if (const char* e = std::getenv("WFSA_STREAM_NT")) ctx->stream_nt = e[0] == '1';
@@ -3497,7 +3528,7 @@ static int qn_setup_impl(wfsa_dev* ctx, const wfsa_qn_desc* d) {
     for (DevBuf<double>* b : {&ctx->qn_x, &ctx->qn_expx, &ctx->qn_grad}) HIP_TRY(b->alloc(size_t(std::max(n, 1))));
     HIP_TRY(ctx->qn_lambda.alloc(size_t(std::max(k, 1))));
     HIP_TRY(ctx->qn_partial.alloc(size_t(std::max(k, 1)) * 8));   // two halves: the pipelined loop
-    HIP_TRY(ctx->qn_halted.alloc(2));   // halted, halt_pending
+    HIP_TRY(ctx->qn_halted.alloc(3));   // halted, halt_pending, an in-kernel QN wave timed out
     if (!ctx->qn_ring) {
         HIP_TRY(hipHostMalloc(reinterpret_cast<void**>(&ctx->qn_ring), sizeof(double) * kQnDepth * wfsa::kQnRow,
                               hipHostMallocMapped | hipHostMallocCoherent));
@@ -3618,7 +3649,7 @@ static int qn_run_impl(wfsa_dev* ctx, double eta, double tol, int32_t max_steps,
                          (long long)sz[sz.size() / 2]);
     }
     hipStream_t s = ctx->stream;
-    if (!ctx->qn_flags_clear) HIP_TRY(hipMemsetAsync(ctx->qn_halted.ptr, 0, 2 * sizeof(unsigned), s));
+    if (!ctx->qn_flags_clear) HIP_TRY(hipMemsetAsync(ctx->qn_halted.ptr, 0, 3 * sizeof(unsigned), s));
     ctx->qn_flags_clear = false;
     ctx->fin_pending = false;
     ctx->fin_for_fbs.active = 0;
@@ -3716,6 +3747,9 @@ static int qn_run_impl(wfsa_dev* ctx, double eta, double tol, int32_t max_steps,
             }
         }
         if (rs == wfsa::kQnSkipped) return fail(WFSA_ERR_HIP, "QN step %d skipped before a halt", done);
+        if (rs == wfsa::kQnTimedOut)
+            return fail(WFSA_ERR_HIP, "QN step %d: an in-kernel update wave's arrival wait timed out "
+                        "(not every block of the stream kernel was resident)", done);
         if (rs > wfsa::kQnSkipped) return fail(WFSA_ERR_HIP, "QN step %d: malformed info row (status %u)", done, rs);
         if (info_rows)
             for (int i = 0; i < 7; ++i) info_rows[size_t(done) * 7 + size_t(i)] = row[i];
