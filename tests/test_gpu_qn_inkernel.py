@@ -18,14 +18,12 @@ pytestmark = pytest.mark.gpu
 # where step e's finish (its log-likelihood sum, halt test and info row) runs:
 # "last" (default): in launch e + 1's finish wave, the Run's last launch
 # finishing its own step; "next": always in the next launch, the Run's last
-# step by a finish kernel of its own (WFSA_QN_LAST_SELF=0); "self": every
-# launch finishes its own step (WFSA_QN_SELF_FINISH=1)
-FINISH = ["last", "next", "self"]
+# step by a finish kernel of its own (WFSA_QN_LAST_SELF=0)
+FINISH = ["last", "next"]
 
 
 def _learner(W, fsa, sym, off, wt, monkeypatch, inkernel, finish="last"):
     monkeypatch.setenv("WFSA_QN_INKERNEL", "1" if inkernel else "0")
-    monkeypatch.setenv("WFSA_QN_SELF_FINISH", "1" if finish == "self" else "0")
     monkeypatch.setenv("WFSA_QN_LAST_SELF", "0" if finish == "next" else "1")
     lrn = W.QuasiNewtonLearner(0)
     lrn.set_info_rmin(False)

@@ -291,7 +291,7 @@ Factored factor_and_solve(wfsa_dev* dev, const SymEntries& A, int order, const d
             const int ord = attempt == 0 ? order : other;
             SparseLdlt s;
             const bool ordered = s.Analyze(A, ord);
-            if (std::getenv("WFSA_KKT_TRACE"))
+            if (std::getenv("WFSA_VERBOSE"))
                 std::fprintf(stderr, "[kkt] N %lld entries %zu order %d%s nnz(L) %lld flops %.3g supernodes %lld front %lld\n",
                              (long long)N, A.v.size(), ord, ordered ? "" : " (work bound: identity)", (long long)s.nnz_l,
                              s.flops, (long long)s.supernodes, (long long)s.max_front);
@@ -357,7 +357,7 @@ Factored factor_and_solve(wfsa_dev* dev, const SymEntries& A, int order, const d
     r.negative = inertia[1];
     r.det_sign = sign;
     r.kind = method == 1 ? 'b' : 'd';
-    if (std::getenv("WFSA_KKT_TRACE"))
+    if (std::getenv("WFSA_VERBOSE"))
         std::fprintf(stderr, "[kkt] N %lld device %s\n", (long long)N, method == 1 ? "blocked" : "full Bunch-Kaufman");
     return r;
 }

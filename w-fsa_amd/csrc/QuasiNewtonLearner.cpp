@@ -250,7 +250,7 @@ void QuasiNewtonLearner::RunDevice(double eta, double tol, int32_t max_epochs, d
         dev_qn_rmin = desc.info_rmin;
         dev_state_valid = false;
     }
-    static const bool trace = std::getenv("WFSA_RUN_TRACE") != nullptr;
+    static const bool trace = std::getenv("WFSA_VERBOSE") != nullptr;
     const auto t0 = clk::now();
     if (!dev_state_valid) {
         check(wfsa_dev_qn_set_state(d, _x.data(), lambda.data()), "wfsa_dev_qn_set_state");

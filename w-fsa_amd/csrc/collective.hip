@@ -37,11 +37,6 @@ ncclResult_t rccl_settle(ncclComm_t c, double limit_s) {
     }
 }
 
-// WFSA_RCCL_BLOCKING=1: a blocking communicator (RCCL's default mode)
-bool rccl_blocking() {
-    const char* e = std::getenv("WFSA_RCCL_BLOCKING");
-    return e && e[0] == '1';
-}
 
 class RcclCollective final : public Collective {
 public:
@@ -280,7 +275,7 @@ std::unique_ptr<Collective> make_rccl_collective(int nranks, int rank, const uin
     // non-blocking: a member that never joins ends the set-up after
     // WFSA_COMM_TIMEOUT_S instead of blocking this thread for good
     ncclConfig_t cfg = NCCL_CONFIG_INITIALIZER;
-    cfg.blocking = rccl_blocking() ? 1 : 0;
+    cfg.blocking = 0;
     ncclResult_t r = ncclCommInitRankConfig(&c, nranks, uid, rank, &cfg);
     if (c && (r == ncclInProgress || (r == ncclSuccess && !cfg.blocking))) r = rccl_settle(c, comm_timeout_s());
     if (r != ncclSuccess) {

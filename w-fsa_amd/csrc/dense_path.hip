@@ -1223,8 +1223,10 @@ void DensePath::free_corpus() {
 }
 
 hipError_t DensePath::load_model(const DenseModel& m, hipStream_t s) {
-    if (const char* e = std::getenv("WFSA_DENSE_GRAD_CFG")) grad_cfg_ = std::atoi(e);   // timing experiments
+#ifdef WFSA_EXPERIMENTS   // GEMM block configurations for timing experiments (experiments build only)
+    if (const char* e = std::getenv("WFSA_DENSE_GRAD_CFG")) grad_cfg_ = std::atoi(e);
     if (const char* e = std::getenv("WFSA_DENSE_STEP_CFG")) step_cfg_ = std::atoi(e);
+#endif
     free_corpus();
     free_model();
     n_params_ = m.n_params;
@@ -1250,7 +1252,6 @@ hipError_t DensePath::load_model(const DenseModel& m, hipStream_t s) {
     std::vector<double> ones(size_t(n_params_) + 2, 1.0);
     DTRY(dalloc(ones_, ones.size()));
     DTRY(hipMemcpyAsync(ones_, ones.data(), ones.size() * 8, hipMemcpyHostToDevice, s));
-    if (const char* e = std::getenv("WFSA_DENSE_BLAS")) engine_ = e[0] != '0' ? 1 : 0;
     if (const char* e = std::getenv("WFSA_DENSE_ENGINE")) {
         const std::string v(e);
         if (v == "fused") engine_ = 0;

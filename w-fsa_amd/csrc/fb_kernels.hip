@@ -2700,30 +2700,11 @@ __global__ __launch_bounds__(1024, (DBG == 10 ? 8 : 1)) WFSA_FBS_ATTR void fbs_k
 #define WFSA_STAMP(k)
 #endif
     WFSA_STAMP(0)
-    const bool early = DELTA && a.early_bub && a.bub_on && a.bub.small_wpb > 0 && a.bub.small_wpb < wpb &&
-                       DBG != 4 && DBG != 8 && DBG != 10 && DBG != 11 && DBG != 13 && !a.no_streams;
     // The delta table's first round of loads before anything else is waited
     // for (the halted flag, the wave's stream setup, the first row set): at
     // entry these scalar load chains took ~2 us ahead of the table's loads
     constexpr int kTB = 12;   // 16-byte pieces per thread and round (one round for 12k-entry tables at 512 threads)
-    const bool pre = DELTA && !a.no_streams && DBG != 4 && DBG != 11 && !early;
-    // Early big bubbles (a.bub.early_big): the block's trailing waves that own
-    // a big bubble -- one wave per bubble, read from global memory, no LDS
-    // table -- run it at entry, so the last bubble arrival (which the QN
-    // waves wait for) does not sit behind the table staging; the other waves
-    // stage the table and announce it by the LDS counter.  The ranks are the
-    // later big-bubble section's (rank r of wave w, the finish wave skipped)
-    auto big_rank = [&](int wv) {
-        int r = (nblk - 1 - bid) + nblk * (wpb - 1 - wv);
-        return r - (r > nblk - 1 ? 1 : 0);
-    };
-    int nbw = 0;   // this block's trailing early big-bubble waves
-    if (pre && QN && a.bub.early_big && a.bub_on && DBG == 0)
-        while (nbw < wpb - 1 && wpb - 1 - nbw >= a.bub.small_wpb && !(bid == 0 && nbw == 0) &&
-               big_rank(wpb - 1 - nbw) < a.bub.n_big)
-            ++nbw;
-    const bool big_early = w >= wpb - nbw;
-    const int n_stage = (wpb - nbw) * kWave;   // the staging threads: waves [0, wpb - nbw)
+    const bool pre = DELTA && !a.no_streams && DBG != 4 && DBG != 11;
     const int tlast = a.n_params - 1;
     // A piece is slots (s2, s2 + 1): weights j0 = s2 - 1 - s2 / kDeltaPeriod
     // and j0 + 1 whenever neither slot is a zero slot, and on a period
@@ -2747,7 +2728,7 @@ __global__ __launch_bounds__(1024, (DBG == 10 ? 8 : 1)) WFSA_FBS_ATTR void fbs_k
         }
     };
     double2 t0[kTB];
-    if (pre && !big_early) table_round(int(threadIdx.x), n_stage, t0);
+    if (pre) table_round(int(threadIdx.x), int(blockDim.x), t0);
     if (QN && bid == 0 && threadIdx.x == 0) {   // for the next launch
         a.qw.arrive[a.qw.parity ^ 1] = 0u;
         if (a.qw.done) a.qw.done[a.qw.parity ^ 1] = 0u;   // (also when only a Run's last launch finishes itself)
@@ -2758,20 +2739,7 @@ __global__ __launch_bounds__(1024, (DBG == 10 ? 8 : 1)) WFSA_FBS_ATTR void fbs_k
         return;
     }
     __shared__ unsigned q_arrived;   // QN: this block's waves whose bubble slots have retired
-    // Early bubbles (delta kernel): the small-bubble waves evaluate their
-    // bubbles at entry -- they need no LDS table -- while the other waves
-    // stage the table and announce it by an LDS counter; every wave waits for
-    // that counter before its stream pass (no block barrier on the way)
-    __shared__ unsigned staged_waves;
-    if (early || nbw > 0) {
-        if (threadIdx.x == 0) {
-            q_arrived = 0u;
-            staged_waves = 0u;
-        }
-        __syncthreads();
-    } else if (QN && threadIdx.x == 0) {
-        q_arrived = 0u;   // (ordered by the staging barrier)
-    }
+    if (QN && threadIdx.x == 0) q_arrived = 0u;   // (ordered by the staging barrier)
     const uint32_t zslot = uint32_t(a.n_params);
     // this wave's run of chunk rows
     const int g0 = a.wave_first[gw], g1 = a.wave_first[gw + 1];
@@ -2781,28 +2749,16 @@ __global__ __launch_bounds__(1024, (DBG == 10 ? 8 : 1)) WFSA_FBS_ATTR void fbs_k
     const uint4* st = a.stream + cb + lane;
     constexpr int D = DELTA ? kDeltaPrefetch : (DBG == 6 ? 2 : (DBG == 7 ? 6 : kStreamPrefetch));
     uint4 A[D], B[D];
-    typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-    const bool nt = a.stream_nt != 0;   // once-read stream rows: non-temporal, keep the L2 for the table
     auto load = [&](uint4 (&r)[D], int c0) {
-        if (nt) {
 #pragma unroll
-            for (int d = 0; d < D; ++d) {
-                const u32x4 v = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(st + int64_t(kWave) * min(c0 + d, last)));
-                r[d] = make_uint4(v.x, v.y, v.z, v.w);
-            }
-        } else {
-#pragma unroll
-            for (int d = 0; d < D; ++d) r[d] = st[int64_t(kWave) * min(c0 + d, last)];
-        }
+        for (int d = 0; d < D; ++d) r[d] = st[int64_t(kWave) * min(c0 + d, last)];
     };
     const bool kStreams = DBG != 3 && DBG != 4 && !a.no_streams;   // (timing experiments; bubbles-only launches)
     // the first row set in flight from the start (its latency hides behind
-    // the staging and the bubbles; but the table loads then return behind it),
-    // or issued once the wave's table / bubble loads are out (defer_prefetch)
-    const bool defer = DELTA && DBG != 4 && DBG != 11 && a.defer_prefetch != 0 && !pre;
-    if (kStreams && !defer) load(A, 0);
-    if (pre && !big_early) {   // the table: the first round's pieces (loaded at entry), then any further rounds
-        const int T2 = (a.d_tab + 1) / 2, nthr = n_stage;
+    // the staging and the bubbles)
+    if (kStreams) load(A, 0);
+    if (pre) {   // the table: the first round's pieces (loaded at entry), then any further rounds
+        const int T2 = (a.d_tab + 1) / 2, nthr = int(blockDim.x);
         double2* dst = reinterpret_cast<double2*>(lds);
 #pragma unroll
         for (int b = 0; b < kTB; ++b) {
@@ -2818,12 +2774,7 @@ __global__ __launch_bounds__(1024, (DBG == 10 ? 8 : 1)) WFSA_FBS_ATTR void fbs_k
                 if (q < T2) dst[q] = t[b];
             }
         }
-        if (nbw > 0) {   // this wave's part is in LDS: announce it (the big-bubble waves are not waiting here)
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-            if (lane == 0) atomicAdd(&staged_waves, 1u);
-        } else {
-            __syncthreads();
-        }
+        __syncthreads();
     }
     // the previous QN step's finish runs in a wave of its own -- the last
     // wave of block 0, which the host gives no groups and no bubbles -- after
@@ -2856,94 +2807,27 @@ __global__ __launch_bounds__(1024, (DBG == 10 ? 8 : 1)) WFSA_FBS_ATTR void fbs_k
 #endif
         // (the bubbles are on the QN update's critical path; the stream waves
         // beside them mostly wait for memory: the bubble waves issue first)
-        if (a.bub.prio) __builtin_amdgcn_s_setprio(2);
+        __builtin_amdgcn_s_setprio(2);
         if (b >= 0 && b < a.bub.n_small4) ll_acc += small_bubble<4, 4, RMIN>(a.bub, a.bub.sm4_tbl, a.bub.n_small4, b, b, btr);
         else if (b >= a.bub.n_small4)
             ll_acc += small_bubble<8, 8, RMIN>(a.bub, a.bub.sm_tbl, a.bub.n_small, b - a.bub.n_small4, b, btr);
-        if (a.bub.prio) __builtin_amdgcn_s_setprio(0);
+        __builtin_amdgcn_s_setprio(0);
     };
     // big bubbles, one wavefront each, from the last blocks' last waves down
     // (the finish wave's rank, nblk - 1, skipped), staged in LDS after the table
     auto big_bubbles = [&]() {
-        const int r = big_rank(w);
+        int r = (nblk - 1 - bid) + nblk * (wpb - 1 - w);
+        r -= r > nblk - 1 ? 1 : 0;
         if (r < a.bub.n_big) {
             stored = true;
             const int E = a.bub.big_lds_edges;
             char* stg = reinterpret_cast<char*>(lds) + a.bub.big_lds_off + w * big_stage_bytes(E);
             double* lw = reinterpret_cast<double*>(stg);
             int* lsd = reinterpret_cast<int*>(lw + E + 2 * kMaxBubbleNodes);
-            if (a.bub.prio > 1) __builtin_amdgcn_s_setprio(2);   // (prio 2: the big bubbles raised too)
             for (int i = r; i < a.bub.n_big; i += nw - 1) ll_acc += big_bubble(a.bub, i, lsd, lw, lw, lw + E);
-            if (a.bub.prio > 1) __builtin_amdgcn_s_setprio(0);
         }
     };
-    if (early && small_wave) small_bubbles();
-    if (kStreams && defer && early && small_wave) load(A, 0);
-    const int stage_w0 = early ? a.bub.small_wpb : 0;   // the staging waves: [stage_w0, wpb)
-    if (DELTA && !a.no_streams && DBG != 4 && DBG != 11 && !pre && w >= stage_w0) {
-        // the delta format's remapped table in 16-byte pieces: slot s holds
-        // weight s - 1 - s / kDeltaPeriod, or zero on a multiple of
-        // kDeltaPeriod and past the last weight; loads first
-        constexpr int kB = kTB;
-        const int T2 = (a.d_tab + 1) / 2;
-        double2* dst = reinterpret_cast<double2*>(lds);
-        const int nthr = int(blockDim.x) - stage_w0 * kWave;
-        bool pf = kStreams && defer;   // the deferred first row set: after this wave's first table loads
-        if (a.dma_stage) {
-            // LDS-DMA (global_load_lds_dwordx4): each 1 KiB piece straight from
-            // the weight vector at the pieces' 8-byte aligned addresses -- no
-            // registers, no LDS stores, so a few stager waves issue the whole
-            // table at once -- then, once this wave's DMA retired, its pieces'
-            // zero slots (and slot 1, weight 0) written over; the partial last
-            // piece by plain loads (a DMA writes all 64 lanes' 16 bytes)
-            const int sw = w - stage_w0, nsw = wpb - stage_w0, full = T2 / kWave;
-            for (int p = sw; p < full; p += nsw) {
-                const int s2 = 2 * (p * kWave + lane);
-                const int j0 = s2 - 1 - s2 / kDeltaPeriod;
-                __builtin_amdgcn_global_load_lds((glb_void*)(a.w + min(max(j0, 0), tlast)), (lds_void*)(dst + p * kWave), 16, 0, 0);
-            }
-            if (pf) load(A, 0);
-            pf = false;
-            if (sw == full % nsw && full * kWave + lane < T2) {   // the partial piece (table_round's rule)
-                const int s2 = 2 * (full * kWave + lane);
-                const int j0 = s2 - 1 - s2 / kDeltaPeriod;
-                const double2 v = *reinterpret_cast<const double2*>(a.w + min(max(j0, 0), tlast));
-                double2 t;
-                t.x = ((s2 % kDeltaPeriod) == 0 || j0 > tlast) ? 0.0 : v.x;
-                t.y = (((s2 + 1) % kDeltaPeriod) == 0 || j0 + 1 > tlast) ? 0.0 : (j0 < 0 ? v.x : v.y);
-                dst[full * kWave + lane] = t;
-            }
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            for (int p = sw; p < full; p += nsw) {
-                const int s2 = 2 * (p * kWave + lane);
-                const int j0 = s2 - 1 - s2 / kDeltaPeriod;
-                double* d = reinterpret_cast<double*>(dst + p * kWave + lane);
-                if ((s2 % kDeltaPeriod) == 0 || j0 > tlast) d[0] = 0.0;
-                if (((s2 + 1) % kDeltaPeriod) == 0 || j0 + 1 > tlast) d[1] = 0.0;
-                else if (j0 < 0) d[1] = a.w[0];
-            }
-        }
-        for (int q0 = int(threadIdx.x) - stage_w0 * kWave; !a.dma_stage && q0 < T2; q0 += kB * nthr) {
-            double2 t[kB];
-            table_round(q0, nthr, t);
-            if (pf) {
-                load(A, 0);
-                pf = false;
-            }
-#pragma unroll
-            for (int b = 0; b < kB; ++b) {
-                const int q = q0 + b * nthr;
-                if (q < T2) dst[q] = t[b];
-            }
-        }
-        if (pf) load(A, 0);   // (a wave with no table piece)
-        if (early) {   // this wave's part is in LDS: announce it
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-            if (lane == 0) atomicAdd(&staged_waves, 1u);
-        } else {
-            __syncthreads();
-        }
-    } else if (!DELTA && W_LDS && DBG != 4 && !a.no_streams) {
+    if (!DELTA && W_LDS && DBG != 4 && !a.no_streams) {
         // stage w[0, n_params] in 16-byte pieces, all of a thread's loads
         // issued before its first store (loads and stores unconditional --
         // an index past the end is clamped to the last piece, which is then
@@ -2965,8 +2849,8 @@ __global__ __launch_bounds__(1024, (DBG == 10 ? 8 : 1)) WFSA_FBS_ATTR void fbs_k
     finish();
     const double* wsrc = W_LDS ? lds : a.w;
     if (a.bub_on && DBG != 8 && DBG != 10 && DBG != 13 && !fin_wave) {   // this wave's bubbles, before its streams
-        if (small_wave && !early) small_bubbles();   // (small_wpb <= waves per block: bubbles_fused)
-        big_bubbles();   // (an early big-bubble wave skipped the staging: it is here at entry)
+        if (small_wave) small_bubbles();   // (small_wpb <= waves per block: bubbles_fused)
+        big_bubbles();
     }
     WFSA_STAMP(2)
     // Ordering of the in-launch hand-off (slot stores -> arrival -> the QN
@@ -2992,13 +2876,6 @@ __global__ __launch_bounds__(1024, (DBG == 10 ? 8 : 1)) WFSA_FBS_ATTR void fbs_k
         if (lane == 0 && prev == unsigned(wpb - 1))   // the block's last wave: one arrival for all its stores
             __hip_atomic_fetch_add(a.qw.arrive + a.qw.parity, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         WFSA_STAMP(3)
-    }
-    if (early || nbw > 0) {   // the table must be complete before the stream pass reads it
-        const unsigned nst = unsigned(early ? wpb - stage_w0 : wpb - nbw);
-        if (lane == 0)
-            while (__hip_atomic_load(&staged_waves, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < nst)
-                __builtin_amdgcn_s_sleep(1);
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
     }
     if (kStreams) load(B, D);
     double p = 0.0, acc0 = 0.0, acc1 = 0.0;
@@ -3142,7 +3019,6 @@ __global__ __launch_bounds__(1024, (DBG == 10 ? 8 : 1)) WFSA_FBS_ATTR void fbs_k
     // the block barrier; a second call site before it, as an option, made
     // the kernel spill 96 VGPRs)
     if (QN && w == wpb - 2 && bid < a.qw.n_waves) {
-        if (a.bub.prio > 2) __builtin_amdgcn_s_setprio(3);   // (prio 3: the QN waves raised above the stream)
 #ifdef WFSA_EXPERIMENTS
         qn_wave_run(a.qw, bid, tr);
 #else

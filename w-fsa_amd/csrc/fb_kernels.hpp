@@ -574,8 +574,6 @@ struct BubbleArgs {
     const unsigned* halted;
     int32_t dbg;             // timing experiments only (WFSA_BUB_DBG): 1 no slot stores, 2 no weight gathers
     int32_t wt;              // contribution slots stored write-through (sc1): read in the same launch (QnWave)
-    int32_t prio;            // fused small bubbles at raised wave priority (s_setprio 2); 2: the big ones too
-    int32_t early_big;       // the stream kernel's big-bubble waves run their bubble at entry, beside the staging
 };
 
 // Compiled streams of the per-iteration kernels.
@@ -688,10 +686,6 @@ struct CompiledArgs {
     QnFinish fin;            // fin.active: block 0 finishes the previous QN step first
     QnWave qw;               // qw.on: this step's QN update runs in this launch
     unsigned long long* trace;   // timing experiments only (WFSA_FBS_TRACE): [waves][8] s_memrealtime stamps
-    int32_t early_bub;
-    int32_t dma_stage;           // the early stagers move the table by LDS-DMA (WFSA_DMA_STAGE=1)       // delta kernel: the small-bubble waves start at entry, the others stage the table
-    int32_t stream_nt;       // stream rows loaded non-temporal
-    int32_t defer_prefetch;  // delta kernel: the first row set issued after the wave's table / bubble loads
 };
 
 

@@ -268,13 +268,7 @@ hipError_t launch_qn_step(const QnArgs& a_in, bool fused, hipStream_t stream) {
         grid = dim3(unsigned(std::max((a.k + 3) / 4, 1)));
         a.dbg = 3;
     }
-    static const int nt = [] {   // (experiments: WFSA_QN_BLOCK = 128 / 256)
-        const char* e = std::getenv("WFSA_QN_BLOCK");
-        return e && std::atoi(e) == 128 ? 128 : (e && std::atoi(e) == 512 ? 512 : kQnBlock);
-    }();
-    if (fused && nt == 128) hipLaunchKernelGGL((qn_step_kernel<true, 128>), grid, dim3(128), lds, stream, a);
-    else if (fused && nt == 512) hipLaunchKernelGGL((qn_step_kernel<true, 512>), grid, dim3(512), lds, stream, a);
-    else if (fused) hipLaunchKernelGGL((qn_step_kernel<true>), grid, dim3(kQnBlock), lds, stream, a);
+    if (fused) hipLaunchKernelGGL((qn_step_kernel<true>), grid, dim3(kQnBlock), lds, stream, a);
     else hipLaunchKernelGGL((qn_step_kernel<false>), grid, dim3(kQnBlock), lds, stream, a);
     return hipGetLastError();
 }

@@ -477,11 +477,7 @@ const char* SymSolver::factor_coo(int64_t n, int64_t nnz, const int32_t* ei, con
             }
         }
     }
-    static const bool only_bk = [] {   // WFSA_KKT_BLOCKED=0: the full Bunch-Kaufman only
-        const char* e = std::getenv("WFSA_KKT_BLOCKED");
-        return e && e[0] == '0';
-    }();
-    if (!only_bk) {
+    {   // the blocked factorisation first; the full Bunch-Kaufman below where it is not exact
         if (const char* e = ensure_blocked(n, s)) return e;
         if (const char* e = assemble(s)) return e;
         bool exact = false;
@@ -517,7 +513,7 @@ const char* SymSolver::factor_coo(int64_t n, int64_t nnz, const int32_t* ei, con
                 return nullptr;
             }
         }
-        if (std::getenv("WFSA_KKT_TRACE"))
+        if (std::getenv("WFSA_VERBOSE"))
             std::fprintf(stderr, "[kkt] n %lld: blocked factor %s; the full Bunch-Kaufman instead\n", (long long)n,
                          exact ? "missed the refined residual bound" : "hit a pivot it cannot take");
     }

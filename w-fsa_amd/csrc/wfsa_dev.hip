@@ -95,12 +95,6 @@ struct DevBuf {
         const size_t c = std::max<size_t>(count, 1);
         hipError_t e = hipMalloc(reinterpret_cast<void**>(&ptr), c * sizeof(T));
         if (e == hipSuccess) n = c;
-        // test hook: every fresh buffer filled with 0xff bytes (NaN doubles,
-        // -1 integers), so a read before the first write shows in the results
-        if (e == hipSuccess && std::getenv("WFSA_POISON_ALLOC")) {
-            e = hipMemset(ptr, 0xff, c * sizeof(T));
-            if (e == hipSuccess) e = hipDeviceSynchronize();
-        }
         return e;
     }
     hipError_t upload(const T* src, size_t count, hipStream_t s) {
@@ -130,8 +124,6 @@ struct wfsa_dev {
     int device = 0;
     int n_cu = kNumCu;
     hipStream_t stream = nullptr;
-    hipStream_t side_stream = nullptr;        // the bubble kernel beside the stream kernel
-    hipEvent_t fork = nullptr, join = nullptr;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     // per in-flight step: before the stream kernel, after it, after the tail
     hipEvent_t k0[kQnDepth] = {}, kc[kQnDepth] = {}, k2[kQnDepth] = {};
@@ -272,7 +264,7 @@ struct wfsa_dev {
     DevBuf<unsigned> w2_ctr;
     DevBuf<unsigned long long> w2_fix;   // the wave kernel's fixed-point sums (WideArgs::fix)
     int32_t w2_fix_frac = 52;
-    bool w2_all = true;          // every traversal string on the wave kernel (WFSA_WIDE2_TIERS=2: tier 2 only)
+    bool w2_all = true;          // every traversal string on the wave kernel
     DevBuf<int32_t> w2_list;     // its strings, longest first
     int32_t w2_n = 0;
 
@@ -291,7 +283,6 @@ struct wfsa_dev {
     unsigned seq = 0;            // last sequence number the host expects
     bool timing_pending = false; // events of the last call not yet read
     bool kernel_timing = true;
-    bool fuse_bubbles = true;    // WFSA_FUSE_BUBBLES=0: separate bubble kernel
     bool use_delta = true;       // WFSA_DELTA=0: the per-iteration pass reads the 16-bit streams
 
     DevBuf<double> gpart;        // per-block partial gradients of the compiled kernel
@@ -339,17 +330,6 @@ struct wfsa_dev {
     DevBuf<unsigned> qn_halted;
     std::vector<int32_t> qn_full_of_h, qn_cptr_h;
     bool qn_fused = false;           // qn_step_kernel sums the members' bubble slots itself
-    // pipelined QN loop (qn_run, opt-in: WFSA_PIPE=1): the stream pass and
-    // the finish of step e on pipe_stream, beside the bubbles and QN update
-    // of the next steps on stream; weights double-buffered by step parity.
-    // Measured slower at c3 (56 -> 79 us per step under rocprof, 45 -> 66
-    // us without): the concurrent kernels slow each other (QN step 10 ->
-    // 26 us beside the stream pass) and every cross-stream wait adds ~10 us
-    // of idle (profiles/r02/v9_pipe_timeline.txt)
-    bool use_pipe = false;
-    bool pipe_fbs_bubbles = true;    // the update chain's bubbles as the stream kernel's bubble waves
-    hipStream_t pipe_stream = nullptr;
-    hipEvent_t pq[kQnDepth] = {}, pf[kQnDepth] = {}, p_start = nullptr;
     int64_t pipe_init_key = -1;               // the second weight buffer's constants copied for this key
     const double* pipe_init_w = nullptr;
     const double* pipe_init_e = nullptr;
@@ -365,16 +345,8 @@ struct wfsa_dev {
     // constraints built at QN set-up, per-parity arrival counters and the
     // weights double-buffered by step parity (w_full2 / ewp2 above)
     bool use_qw = true;
-    bool dma_stage = false;          // WFSA_DMA_STAGE=1: the early stagers move the table by LDS-DMA
-    bool early_bub = false;          // WFSA_EARLY_BUB=1: the small-bubble waves start at entry, the others stage (slower: the few stagers take longer)
-    bool stream_nt = false;          // WFSA_STREAM_NT=1: the stream kernel's rows loaded non-temporal
-    bool defer_prefetch = false;     // WFSA_DEFER_PREFETCH=1: the first row set after the table / bubble loads
-    bool bub_prio = true;            // WFSA_BUB_PRIO=0: the fused small bubbles at normal wave priority
-    bool bub_prio_big = false;       // WFSA_BUB_PRIO=2: the big ones at raised priority too
-    bool qn_prio = false;            // WFSA_BUB_PRIO=3: and the QN waves above the stream
-    bool early_big = false;          // WFSA_EARLY_BIG=1: the big-bubble waves start at entry (fb_kernels.hip)
     int32_t qw_waves = 0;            // reserved at preparation
-    double qw_cost = 6.0;            // the dealer's charge per QN wave, in stream rows (WFSA_QN_COST)
+    double qw_cost = 6.0;            // the dealer's charge per QN wave, in stream rows
     bool qw_ok = false;              // batches built for the current preparation and QN set-up
     int32_t qw_nbatch = 0;
     DevBuf<int4> qw_batch;
@@ -386,7 +358,6 @@ struct wfsa_dev {
     std::vector<int4> h_qw_batch;    // host copy of the batches (diagnostics)
     DevBuf<unsigned> qw_arrive;      // [2], zero between launches (each launch zeroes the next one's)
     DevBuf<unsigned> qw_done;        // [2] the self-finish's arrivals, likewise
-    bool qw_self_finish = false;     // WFSA_QN_SELF_FINISH=1: each launch finishes its own step (fb_kernels.hip)
     size_t qw_res_lds = ~size_t(0);  // qw_resident's cache: the launch's LDS and block, blocks per CU
     int qw_res_block = 0, qw_res_per_cu = 0;
     uint32_t qw_poll_limit = 0;      // polls before an in-kernel QN wave gives up (0: the kernel default)
@@ -1614,12 +1585,8 @@ int prepare(wfsa_dev* ctx, int level) {
         // waves per CU; c3: fbs 31.3 -> 30.1 us, profiles/r01/v19_block_sweep.txt),
         // else one 1024-thread block
         ctx->i_block = (ctx->i_tables && 2 * stage_bytes <= size_t(kLdsPerCu - 1024)) ? 512 : 1024;
-        if (const char* e = std::getenv("WFSA_IBLOCK")) ctx->i_block = std::max(64, std::min(1024, std::atoi(e))) & ~63;
         const int i_wpb = ctx->i_block / kWave;
         int i_per_cu = std::max(1, kIterWavesPerCu / i_wpb);
-        if (ctx->i_tables)
-            i_per_cu = std::min<int>(i_per_cu, int(size_t(kLdsPerCu) / std::max<size_t>(stage_bytes, 1)));
-        if (const char* e = std::getenv("WFSA_IPERCU")) i_per_cu = std::atoi(e);   // experiments (LDS-capped below)
         if (ctx->i_tables)
             i_per_cu = std::min<int>(i_per_cu, int(size_t(kLdsPerCu) / std::max<size_t>(stage_bytes, 1)));
         i_per_cu = std::max(1, i_per_cu);
@@ -1667,8 +1634,6 @@ int prepare(wfsa_dev* ctx, int level) {
         // the slot stores became coalesced (profiles/r02/v12_small_cost_sweep.txt:
         // fbs 24.6 -> 23.4 us at c3; it was 32 before, profiles/r01/v18_cost_sweep.txt)
         double small_cost = 18.0, big_cost = 8.0;
-        if (const char* e = std::getenv("WFSA_SMALL_COST")) small_cost = std::atof(e);
-        if (const char* e = std::getenv("WFSA_BIG_COST")) big_cost = std::atof(e);
         int64_t n_b = 0, n_big_est = 0;
         for (int32_t i : comp) {
             n_b += h_nb[size_t(i)];
@@ -1684,11 +1649,7 @@ int prepare(wfsa_dev* ctx, int level) {
         // stream share ends early
         // (reserved whatever WFSA_QN_INKERNEL says: the layout, and so every
         // fixed-order sum, is then the same with the update in or out)
-        static const int64_t per_qw = [] {   // parameters per QN wave (WFSA_QW_PER: timing sweeps)
-            const char* e = std::getenv("WFSA_QW_PER");
-            const int v = e ? std::atoi(e) : 0;
-            return int64_t(v >= 16 ? v : 48);
-        }();
+        constexpr int64_t per_qw = 48;   // parameters per QN wave (40 / 36 / 32: no gain, profiles/r05)
         ctx->qw_waves = (i_wpb >= 3 && delta_want && ctx->i_tables)
                             ? int(std::min<int64_t>(nblk, (int64_t(ctx->n_params) + per_qw - 1) / per_qw)) : 0;
         for (int w = 0; w < i_nw; ++w) {
@@ -1806,25 +1767,8 @@ int prepare(wfsa_dev* ctx, int level) {
                     return h_bubbuf[size_t(x) + 4 + size_t(k)] < h_bubbuf[size_t(y) + 4 + size_t(k)];
             return false;
         };
-        if (!(std::getenv("WFSA_BUB_SORT") && std::getenv("WFSA_BUB_SORT")[0] == '0')) {
-            std::stable_sort(small4.begin(), small4.end(), shape_less);
-            std::stable_sort(small.begin(), small.end(), shape_less);
-        }
-        if (std::getenv("WFSA_DEBUG_BUBBLES")) {   // size histogram (diagnostics)
-            std::vector<int64_t> he(size_t(wfsa::kMaxBubbleEdges) + 1, 0), hn(size_t(wfsa::kMaxBubbleNodes) + 1, 0);
-            for (int32_t o : h_off) {
-                he[size_t(h_bubbuf[size_t(o)] >> 16)]++;
-                hn[size_t(h_bubbuf[size_t(o)] & 0xffff)]++;
-            }
-            std::fprintf(stderr, "bubbles %lld (small %zu + %zu, big %zu); by edges:", (long long)nbub, small4.size(),
-                         small.size(), big.size());
-            for (size_t e = 0; e < he.size(); ++e)
-                if (he[e]) std::fprintf(stderr, " %zu:%lld", e, (long long)he[e]);
-            std::fprintf(stderr, "\nby nodes:");
-            for (size_t v = 0; v < hn.size(); ++v)
-                if (hn[v]) std::fprintf(stderr, " %zu:%lld", v, (long long)hn[v]);
-            std::fprintf(stderr, "\n");
-        }
+        std::stable_sort(small4.begin(), small4.end(), shape_less);
+        std::stable_sort(small.begin(), small.end(), shape_less);
         {   // list position of every bubble (the fused rmin values are stored there)
             std::unordered_map<int32_t, int32_t> idx_of;
             idx_of.reserve(h_off.size());
@@ -1865,9 +1809,6 @@ int prepare(wfsa_dev* ctx, int level) {
     // profiles/r05/option_sweeps.txt)
     {
         double small_cost = 9.0, small_cost_b = 17.0, big_cost = 15.0;
-        if (const char* e = std::getenv("WFSA_SMALL_COST")) small_cost = std::atof(e);
-        if (const char* e = std::getenv("WFSA_SMALL_COST_B")) small_cost_b = std::atof(e);
-        if (const char* e = std::getenv("WFSA_BIG_COST")) big_cost = std::atof(e);
         const int nblk = ctx->i_grid;
         const int64_t nch = wfsa::small_chunks(ctx->n_small4, ctx->n_small), na = (int64_t(ctx->n_small4) + kWave - 1) / kWave;
         const int small_wpb = small_waves_per_block(nch * kWave, nblk);
@@ -2087,8 +2028,6 @@ int enqueue_compiled(wfsa_dev* ctx, bool with_grad, bool want_logq, const unsign
         c.erec_out = ctx->erec.ptr;
         c.out = ctx->out.ptr;
         c.no_slice = (!with_grad && ctx->eval_no_slice) ? 1 : 0;
-        c.stream_nt = ctx->stream_nt ? 1 : 0;
-        c.defer_prefetch = ctx->defer_prefetch ? 1 : 0;
         c.ll_part = ctx->ll_cur;
         c.logq = want_logq ? ctx->logq.ptr : nullptr;
         c.halted = halted;
@@ -2104,10 +2043,6 @@ int enqueue_compiled(wfsa_dev* ctx, bool with_grad, bool want_logq, const unsign
                 ctx->rm_sv_used = true;
             }
             c.bub_on = 1;
-            c.bub.prio = ctx->bub_prio ? (ctx->qn_prio ? 3 : ctx->bub_prio_big ? 2 : 1) : 0;
-            c.bub.early_big = ctx->early_big ? 1 : 0;
-            c.early_bub = ctx->early_bub ? 1 : 0;
-            c.dma_stage = ctx->dma_stage ? 1 : 0;
             c.bub.small_wpb = small_waves_per_block(wfsa::small_chunks(ctx->n_small4, ctx->n_small) * kWave, ctx->i_grid);
             if (ctx->n_big > 0) {
                 c.bub.big_lds_edges = ctx->big_lds_edges;
@@ -2185,8 +2120,7 @@ int enqueue_bubbles(wfsa_dev* ctx, bool want_logq, const unsigned* halted, int32
 // The bubbles ride in the stream kernel's waves when the kernel stages the
 // weights (and log q is not wanted: both would write the strings' entries).
 bool bubbles_fused(wfsa_dev* ctx, bool want_logq) {
-    if (!(ctx->n_bubbles > 0 && !want_logq && ctx->n_groups > 0 && ctx->i_tables >= 1 && !ctx->side_stream &&
-          ctx->fuse_bubbles))
+    if (!(ctx->n_bubbles > 0 && !want_logq && ctx->n_groups > 0 && ctx->i_tables >= 1))
         return false;
     // at most one chunk of 64 small bubbles per wave; the big bubbles' staging must fit beside w
     // (the last wave of block 0 is the QN finish's: no bubbles)
@@ -2239,38 +2173,26 @@ int enqueue_evaluation(wfsa_dev* ctx, bool want_logq, const unsigned* halted, in
         if (n_ll) *n_ll = 0;
         return WFSA_OK;
     }
-    // The bubble kernel reads only the weights (ewp, staged before this
-    // point) and writes its own slots and ll partials, so it runs on a second
-    // stream beside the stream kernel (not with log q, where both write the
-    // strings' entries, nor with bubble atomics into out, which the stream
-    // kernel zeroes).
+    // (a bubble kernel on a second stream beside the stream kernel: the
+    // cross-stream fork / join cost more idle time, 5-20 us, than the
+    // overlap saved -- measured and removed)
     ctx->rm_sv_used = false;   // (set by the stream kernel's launch when it stores the bubbles' rmin values)
-    const bool side = ctx->n_bubbles > 0 && ctx->side_stream && !want_logq;
-    if (side) {
-        HIP_TRY(hipEventRecord(ctx->fork, s));
-        HIP_TRY(hipStreamWaitEvent(ctx->side_stream, ctx->fork, 0));
-    }
     const bool fusedb = bubbles_fused(ctx, want_logq);
     // the ll partials: the stream kernel's blocks, then the other kernels' waves
     int32_t wave_off = ctx->n_groups > 0 ? ctx->i_grid : 0;   // one per stream-kernel block
-    if (ctx->n_bubbles > 0 && side) {
-        if (int rc = enqueue_bubbles(ctx, want_logq, halted, wave_off, ctx->side_stream)) return rc;
-        HIP_TRY(hipEventRecord(ctx->join, ctx->side_stream));
-    }
     // the per-edge weights and the zeroed result are for the traversal
     // kernels and the reduction: the fused QN step over compiled strings
     // alone reads neither, so the stream kernel skips writing them
     ctx->eval_no_slice = !with_tail && ctx->n_fall[0] + ctx->n_fall[1] + ctx->n_fall[2] == 0;
     // the QN update in the stream kernel reads the bubble slots: a separate
     // bubble kernel then runs before it (its slots visible at the boundary)
-    const bool bub_first = ctx->qw_next.on && ctx->n_bubbles > 0 && !side && !fusedb;
+    const bool bub_first = ctx->qw_next.on && ctx->n_bubbles > 0 && !fusedb;
     if (bub_first)
         if (int rc = enqueue_bubbles(ctx, want_logq, halted, wave_off, s)) return rc;
     const int crc = enqueue_compiled(ctx, false, want_logq, halted, slot);
     ctx->eval_no_slice = false;
     if (crc) return crc;
-    if (side) HIP_TRY(hipStreamWaitEvent(s, ctx->join, 0));
-    if (ctx->n_bubbles > 0 && !side && !fusedb && !bub_first) {
+    if (ctx->n_bubbles > 0 && !fusedb && !bub_first) {
         if (int rc = enqueue_bubbles(ctx, want_logq, halted, wave_off, s)) return rc;
     }
     if (ctx->n_bubbles > 0 && !fusedb) wave_off += ctx->b_waves;
@@ -2321,7 +2243,7 @@ int enqueue_evaluation(wfsa_dev* ctx, bool want_logq, const unsigned* halted, in
     }
     if (n_ll) *n_ll = wave_off;
     if (!with_tail) {
-        const bool after_kc = side || (ctx->n_bubbles > 0 && !fusedb && !bub_first) || ctx->n_fall[0] || ctx->n_fall[1] ||
+        const bool after_kc = (ctx->n_bubbles > 0 && !fusedb && !bub_first) || ctx->n_fall[0] || ctx->n_fall[1] ||
                               ctx->n_fall[2] || w2_covers_01;
         if (!after_kc && slot >= 0) ctx->k2_kc[slot] = true;
         else HIP_TRY(record(ctx, ctx->k2, slot, s));
@@ -2440,9 +2362,6 @@ int enqueue_rmin(wfsa_dev* ctx, const unsigned* halted, double* res, int par = 0
         r.sv = ctx->rm_sv.ptr;
         r.bpos = ctx->rm_bpos.ptr;
     }
-    if (std::getenv("WFSA_RMIN_TRACE"))
-        std::fprintf(stderr, "[rmin] trav_done %d sv %d par %d finish %d\n", int(trav_done), int(r.sv != nullptr), par,
-                     int(q != nullptr));
     r.w = ctx->w_full.ptr;
     r.ewp = ctx->ewp.ptr;
     r.rmin_log = ctx->rm_rs.ptr;
@@ -2502,16 +2421,9 @@ int build_qw_batches(wfsa_dev* ctx) {
     // bounds a QN wave's rounds (48: six; c3 -0.3 us/step against 256,
     // profiles/r05/option_sweeps.txt), raised to the largest constraint's
     // chunks when one alone needs more (then the hard limit, 256, decides)
-    static const int32_t target = [] {
-        const char* e = std::getenv("WFSA_QW_CHUNKS");   // (timing sweeps)
-        return e ? std::atoi(e) : 48;
-    }();
+    constexpr int32_t target = 48;   // (40 / 32 chunks: +0.2 us)
     const int32_t limit = kWave * wfsa::kQnWaveChunkRounds;
-    static const int32_t mcap = [] {   // members per batch (timing sweeps; at most kQnWaveMembers)
-        const char* e = std::getenv("WFSA_QW_MEMBERS");
-        const int v = e ? std::atoi(e) : 0;
-        return v > 0 && v < wfsa::kQnWaveMembers ? v : wfsa::kQnWaveMembers;
-    }();
+    constexpr int32_t mcap = wfsa::kQnWaveMembers;   // members per batch (45 / 36: 31.9-32.7 us)
     if (!ctx->qn_fused || k <= 0 || n <= 0 || int64_t(cptr.size()) != int64_t(k) + 1 ||
         int64_t(ctx->h_mchunk.size()) < n || ctx->slot_order.size() != size_t(ctx->n_params))
         return WFSA_OK;
@@ -2593,7 +2505,7 @@ bool qw_usable(wfsa_dev* ctx) {
     return ctx->use_qw && ctx->qw_ok && ctx->qw_waves > 0 && ctx->qn_fused && !ctx->comm && !ctx->dense &&
            !ctx->mpath && !ctx->qn_rmin && ctx->n_groups > 0 && ctx->delta_on && ctx->i_tables >= 1 &&
            ctx->n_fall[0] + ctx->n_fall[1] + ctx->n_fall[2] == 0 && ctx->fixed_t_on && ctx->qn_k > 0 &&
-           !ctx->side_stream && ctx->i_block / kWave >= 3 && qw_resident(ctx);
+           ctx->i_block / kWave >= 3 && qw_resident(ctx);
 }
 
 int enqueue_qn_step(wfsa_dev* ctx, double eta, double tol, int64_t e, bool timed, bool inkern, bool last) {
@@ -2610,11 +2522,7 @@ int enqueue_qn_step(wfsa_dev* ctx, double eta, double tol, int64_t e, bool timed
     if (fuse_rmin)
         if (int rc = rmin_prepare(ctx)) return rc;
     if (ctx->fin_pending) {   // the previous step's finish: in this step's stream kernel, or its own launch
-        static const bool host_fin = [] {
-            const char* e = std::getenv("WFSA_FIN_HOST");
-            return !(e && e[0] == '0');
-        }();
-        if (ctx->fin_hostable && trellis && ctx->n_groups > 0 && host_fin) {
+        if (ctx->fin_hostable && trellis && ctx->n_groups > 0) {
             ctx->fin_for_fbs = ctx->fin_next;
             ctx->fin_pending = false;
         } else if (int rc = flush_qn_finish(ctx)) {
@@ -2705,11 +2613,12 @@ int enqueue_qn_step(wfsa_dev* ctx, double eta, double tol, int64_t e, bool timed
         w.poll_limit = ctx->qw_poll_limit;
         w.poll_fault = ctx->qw_poll_fault ? 1 : 0;
         w.fin = f;
-        // this launch finishes its own step (its stream kernel's blocks' ll
-        // partials): every launch (WFSA_QN_SELF_FINISH=1), or the Run's last,
-        // whose row then needs no finish kernel of its own after it
-        // (WFSA_QN_LAST_SELF=0: that kernel)
-        self_fin = ctx->qw_self_finish || (last && ctx->qw_last_self);
+        // the Run's last launch finishes its own step (its stream kernel's
+        // blocks' ll partials), so its row needs no finish kernel of its own
+        // after it (WFSA_QN_LAST_SELF=0: that kernel; every launch finishing
+        // its own step put the finish's write-through reads on the critical
+        // path, 36.2 vs 28.6 us, profiles/r05)
+        self_fin = last && ctx->qw_last_self;
         if (self_fin) {
             w.self_finish = 1;
             w.fin.ll_part = ctx->ll_cur;
@@ -2734,10 +2643,7 @@ int enqueue_qn_step(wfsa_dev* ctx, double eta, double tol, int64_t e, bool timed
     }
     if (ctx->comm) COMM_TRY(ctx, ctx->out.ptr, size_t(np) + 1, wfsa::RedOp::SumF64, s);
     if (ctx->qn_rmin) {
-        static const bool fold_rmin = [] {   // WFSA_RMIN_FOLD=0: the strings pass as its own launch
-            const char* e = std::getenv("WFSA_RMIN_FOLD");
-            return !(e && e[0] == '0');
-        }();
+        constexpr bool fold_rmin = true;   // the strings pass in the QN step kernel's blocks (one launch fewer)
         double* res = ctx->rm_res.ptr + 2 * par;
         if (ctx->mpath || (ctx->dense && !ctx->comm)) {
             if (int rc = enqueue_rmin(ctx, ctx->qn_halted.ptr, res)) return rc;
@@ -2758,149 +2664,6 @@ int enqueue_qn_step(wfsa_dev* ctx, double eta, double tol, int64_t e, bool timed
     ctx->fin_next.active = 1;
     ctx->fin_pending = true;
     ctx->fin_hostable = (fused || (trellis && ctx->comm)) && ctx->n_groups > 0 && f.ll_part != nullptr;
-    return WFSA_OK;
-}
-
-// The pipelined QN step e (qn_run when pipe_ok): the trivial words'
-// gradient is a constant, so the QN update needs only the bubbles; the
-// stream pass (the step's log-likelihood, for its info row) leaves the
-// update's critical path.
-//   stream:      bubbles(e) -> [finish(e-1) done] -> QN step(e) => pq[e]
-//   pipe_stream: [pq[e-1]] -> stream pass(e) -> [pq[e]] -> finish(e) => pf[e]
-// Step e reads the weights of parity e; QN step(e) writes parity e+1, which
-// stream pass(e-1) read -- done before finish(e-1), which QN step(e) waits
-// for (it also needs finish(e-1)'s halt decision).  ll partials and the QN
-// block partials alternate by parity; finish(e) reads both halves of step e
-// before QN step(e+2) / bubbles(e+2) rewrite them (they wait for finish(e+1)).
-bool pipe_ok(wfsa_dev* ctx) {
-    return ctx->use_pipe && ctx->pipe_stream && ctx->qn_fused && !ctx->comm && !ctx->dense && !ctx->mpath &&
-           !ctx->qn_rmin && ctx->n_groups > 0 && ctx->n_fall[0] + ctx->n_fall[1] + ctx->n_fall[2] == 0 &&
-           ctx->i_tables >= 1;
-}
-
-int enqueue_qn_step_piped(wfsa_dev* ctx, double eta, double tol, int64_t e, bool timed) {
-    hipStream_t M = ctx->stream, S = ctx->pipe_stream;
-    const int par = int(e & 1);
-    const int slot = int(e % kQnDepth), prev = int((e + kQnDepth - 1) % kQnDepth);
-    const int32_t np = ctx->n_params, k = std::max(ctx->qn_k, 1);
-    double* w_cur = par ? ctx->w_full2.ptr : ctx->w_full.ptr;
-    double* ewp_cur = par ? ctx->ewp2.ptr : ctx->ewp.ptr;
-    double* w_nxt = par ? ctx->w_full.ptr : ctx->w_full2.ptr;
-    double* ewp_nxt = par ? ctx->ewp.ptr : ctx->ewp2.ptr;
-    double* partial = ctx->qn_partial.ptr + size_t(par) * 4 * size_t(k);
-    ctx->ll_cur = ctx->ll_part.ptr + size_t(par) * ctx->ll_stride;
-    ctx->w_cur = w_cur;
-    ctx->ewp_cur = ewp_cur;
-    const unsigned* halted = ctx->qn_halted.ptr;
-    // stream: the bubbles of step e -- the stream kernel's fused bubble waves
-    // without its stream pass (ll partials in the second run of i_grid
-    // slots), or the lane-per-bubble kernel (after the block partials)
-    const bool bub_fused = bubbles_fused(ctx, false) && ctx->pipe_fbs_bubbles;
-    const int32_t wave_off = ctx->i_grid;
-    if (ctx->n_bubbles > 0 && bub_fused) {
-        wfsa::CompiledArgs c{};
-        c.m = model_view(ctx);
-        c.p = ctx->p.ptr;
-        stream_args(ctx, c, true);
-        c.n_params = ctx->n_params;
-        c.tables = ctx->i_tables;
-        c.multi = ctx->n_multi > 0 ? 1 : 0;
-        c.w = w_cur;
-        c.out = ctx->out.ptr;
-        c.ll_part = ctx->ll_cur + ctx->i_grid;
-        c.halted = halted;
-        c.no_streams = 1;
-        c.bub = bubble_args(ctx, false, halted, nullptr);
-        c.bub_on = 1;
-        c.bub.small_wpb = small_waves_per_block(wfsa::small_chunks(ctx->n_small4, ctx->n_small) * kWave, ctx->i_grid);
-        size_t lds = ctx->i_lds;
-        if (ctx->n_big > 0) {
-            c.bub.big_lds_edges = ctx->big_lds_edges;
-            c.bub.big_lds_off = int32_t(big_stage_off(ctx));
-            lds = big_stage_off(ctx) + size_t(ctx->i_block / kWave) * size_t(wfsa::big_stage_bytes(ctx->big_lds_edges));
-        }
-        HIP_TRY(wfsa::launch_compiled(c, ctx->i_grid, ctx->i_block, lds, M));
-    } else if (ctx->n_bubbles > 0) {
-        if (int rc = enqueue_bubbles(ctx, false, halted, wave_off, M)) return rc;
-    }
-    if (e > 0) HIP_TRY(hipStreamWaitEvent(M, ctx->pf[prev], 0));
-    wfsa::QnArgs q{};
-    wfsa::QnFinish& f = q.fin;
-    q.out = ctx->out.ptr;
-    q.use_out = false;
-    q.fixed = ctx->fixed_grad.ptr;
-    q.contrib = ctx->n_bubbles > 0 ? ctx->contrib.ptr : nullptr;
-    q.grp_base = ctx->grp_base.ptr;
-    q.grp_nch = ctx->grp_nch.ptr;
-    q.seg_ptr = ctx->seg_ptr.ptr;
-    q.chunk_ptr = ctx->chunk_ptr.ptr;
-    q.n_full = np;
-    q.n = ctx->qn_n;
-    q.k = ctx->qn_k;
-    q.full_of = ctx->qn_full_of.ptr;
-    q.trim = ctx->qn_trim.ptr;
-    q.cptr = ctx->qn_cptr.ptr;
-    q.x = ctx->qn_x.ptr;
-    q.lambda = ctx->qn_lambda.ptr;
-    q.expx = ctx->qn_expx.ptr;
-    q.grad = ctx->qn_grad.ptr;
-    q.w_full = w_nxt;
-    q.ewp = ewp_nxt;
-    q.partial = partial;
-    q.eta = eta;
-    q.exp_lambda = ctx->qn_exp_lambda;
-    q.halted = ctx->qn_halted.ptr;
-    q.seg_cap = ctx->qn_max_nm;
-    q.chunk_cap = ctx->n_bubbles > 0 ? std::min(ctx->lead_grp_nch, wfsa::kMaxChunks) : 1;
-    f.out0 = ctx->out.ptr;
-    f.ll_part = ctx->ll_cur;
-    f.n_ll = ctx->i_grid + (ctx->n_bubbles == 0 ? 0 : bub_fused ? ctx->i_grid : ctx->b_waves);
-    f.partial = partial;
-    f.n_blocks = k;
-    f.k = ctx->qn_k;
-    f.plogp = ctx->qn_plogp;
-    f.tol = tol;
-    f.ring_slot = slot;
-    f.halted = ctx->qn_halted.ptr;
-    f.halt_pending = ctx->qn_halted.ptr + 1;
-    f.seq = ctx->counters.ptr;
-    f.host_flag = ctx->flag_dev;
-    f.host_ring = ctx->qn_ring_dev;
-    HIP_TRY(wfsa::launch_qn_step(q, true, M));
-    HIP_TRY(hipEventRecord(ctx->pq[slot], M));
-    // pipe_stream: the stream pass of step e (weights of parity e, written by
-    // QN step e-1 or the set-up), then the finish once QN step e is done
-    HIP_TRY(hipStreamWaitEvent(S, e > 0 ? ctx->pq[prev] : ctx->p_start, 0));
-    if (timed) HIP_TRY(record(ctx, ctx->k0, slot, S));
-    {
-        wfsa::CompiledArgs c{};
-        c.m = model_view(ctx);
-        c.p = ctx->p.ptr;
-        stream_args(ctx, c, true);
-        c.n_params = np;
-        c.tables = ctx->i_tables;
-        c.with_grad = 0;
-        c.multi = ctx->n_multi > 0 ? 1 : 0;
-        c.w = w_cur;
-        c.grad = ctx->out.ptr + 1;
-        c.gpart = ctx->gpart.ptr;
-        c.n_comb = ctx->n_edges + ctx->n_end;
-        c.lw_out = ctx->lw.ptr;
-        c.ew_out = ctx->ew.ptr;
-        c.erec_out = ctx->erec.ptr;
-        c.out = ctx->out.ptr;
-        c.ll_part = ctx->ll_cur;
-        c.logq = nullptr;
-        c.halted = halted;
-        c.fin.active = 0;
-        c.bub_on = 0;
-        HIP_TRY(wfsa::launch_compiled(c, ctx->i_grid, ctx->i_block, ctx->i_lds, S));
-    }
-    if (timed) HIP_TRY(record(ctx, ctx->kc, slot, S));
-    HIP_TRY(hipStreamWaitEvent(S, ctx->pq[slot], 0));
-    HIP_TRY(wfsa::launch_qn_finish(f, S));
-    if (timed) HIP_TRY(record(ctx, ctx->k2, slot, S));
-    HIP_TRY(hipEventRecord(ctx->pf[slot], S));
     return WFSA_OK;
 }
 
@@ -3015,14 +2778,11 @@ int wfsa_dev_create(int device, wfsa_dev** out) {
     ctx->n_cu = prop.multiProcessorCount > 0 ? prop.multiProcessorCount : kNumCu;
     if (const char* e = std::getenv("WFSA_GRAPH")) ctx->use_graph = e[0] == '1';
     if (const char* e = std::getenv("WFSA_TIMING")) ctx->kernel_timing = e[0] != '0';
-    if (const char* e = std::getenv("WFSA_TIMING_STRIDE")) ctx->timing_stride = std::max(1, std::atoi(e));
-    if (const char* e = std::getenv("WFSA_FUSE_BUBBLES")) ctx->fuse_bubbles = e[0] != '0';
     if (const char* e = std::getenv("WFSA_DELTA")) ctx->use_delta = e[0] != '0';
     if (const char* e = std::getenv("WFSA_DENSE"); e && e[0]) ctx->dense_mode = e[0] == '0' ? 0 : 1;
     if (const char* e = std::getenv("WFSA_TIER2")) ctx->force_tier2 = e[0] == '1';
     if (const char* e = std::getenv("WFSA_WIDE2")) ctx->use_wide2 = e[0] != '0';
     if (const char* e = std::getenv("WFSA_PULL")) ctx->use_pull = e[0] != '0';
-    if (const char* e = std::getenv("WFSA_WIDE2_TIERS")) ctx->w2_all = std::strcmp(e, "2") != 0;
     if (const char* e = std::getenv("WFSA_QN_INKERNEL")) ctx->use_qw = e[0] != '0';
     // fault injection (tests/test_gpu_qn_inkernel.py): the first QN wave waits
     // for an arrival that never comes and gives up after a few polls
@@ -3030,36 +2790,9 @@ int wfsa_dev_create(int device, wfsa_dev** out) {
         ctx->qw_poll_fault = true;
         ctx->qw_poll_limit = 256;
     }
-    if (const char* e = std::getenv("WFSA_EARLY_BUB")) ctx->early_bub = e[0] == '1';
-    if (const char* e = std::getenv("WFSA_DMA_STAGE")) ctx->dma_stage = e[0] == '1';
-    if (const char* e = std::getenv("WFSA_STREAM_NT")) ctx->stream_nt = e[0] == '1';
-    if (const char* e = std::getenv("WFSA_DEFER_PREFETCH")) ctx->defer_prefetch = e[0] == '1';
-    if (const char* e = std::getenv("WFSA_BUB_PRIO")) {
-        ctx->bub_prio = e[0] != '0';
-        ctx->bub_prio_big = e[0] == '2' || e[0] == '3';
-        ctx->qn_prio = e[0] == '3';
-    }
-    if (const char* e = std::getenv("WFSA_EARLY_BIG")) ctx->early_big = e[0] == '1';
-    if (const char* e = std::getenv("WFSA_QN_COST")) ctx->qw_cost = std::atof(e);
-    if (const char* e = std::getenv("WFSA_QN_SELF_FINISH")) ctx->qw_self_finish = e[0] == '1';
     if (const char* e = std::getenv("WFSA_QN_LAST_SELF")) ctx->qw_last_self = e[0] != '0';
 
     HIP_TRY(hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking));
-    if (const char* e = std::getenv("WFSA_PIPE")) ctx->use_pipe = e[0] == '1';
-    if (const char* e = std::getenv("WFSA_PIPE_BUB")) ctx->pipe_fbs_bubbles = e[0] != '0';
-    HIP_TRY(hipStreamCreateWithFlags(&ctx->pipe_stream, hipStreamNonBlocking));
-    HIP_TRY(hipEventCreateWithFlags(&ctx->p_start, hipEventDisableTiming));
-    for (int i = 0; i < kQnDepth; ++i) {
-        HIP_TRY(hipEventCreateWithFlags(&ctx->pq[i], hipEventDisableTiming));
-        HIP_TRY(hipEventCreateWithFlags(&ctx->pf[i], hipEventDisableTiming));
-    }
-    // measured: the cross-stream fork/join costs more idle time (5-20 us)
-    // than the overlap saves, so the side stream is opt-in
-    if (const char* e = std::getenv("WFSA_SIDE_STREAM"); e && e[0] == '1') {
-        HIP_TRY(hipStreamCreateWithFlags(&ctx->side_stream, hipStreamNonBlocking));
-        HIP_TRY(hipEventCreateWithFlags(&ctx->fork, hipEventDisableTiming));
-        HIP_TRY(hipEventCreateWithFlags(&ctx->join, hipEventDisableTiming));
-    }
     HIP_TRY(hipEventCreate(&ctx->ev0));
     HIP_TRY(hipEventCreate(&ctx->ev1));
     for (int i = 0; i < kQnDepth; ++i)
@@ -3094,18 +2827,6 @@ void wfsa_dev_destroy(wfsa_dev* ctx) {
             if (ev) (void)hipEventDestroy(ev);
     if (ctx->qn_ring) (void)hipHostFree(ctx->qn_ring);
     if (ctx->qst) (void)hipHostFree(ctx->qst);
-    if (ctx->side_stream) (void)hipStreamSynchronize(ctx->side_stream);
-    for (hipEvent_t ev : {ctx->fork, ctx->join})
-        if (ev) (void)hipEventDestroy(ev);
-    if (ctx->side_stream) (void)hipStreamDestroy(ctx->side_stream);
-    if (ctx->pipe_stream) {
-        (void)hipStreamSynchronize(ctx->pipe_stream);
-        (void)hipStreamDestroy(ctx->pipe_stream);
-    }
-    for (int i = 0; i < kQnDepth; ++i)
-        for (hipEvent_t ev : {ctx->pq[i], ctx->pf[i]})
-            if (ev) (void)hipEventDestroy(ev);
-    if (ctx->p_start) (void)hipEventDestroy(ctx->p_start);
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
     delete ctx;
 }
@@ -3630,7 +3351,7 @@ static int qn_run_impl(wfsa_dev* ctx, double eta, double tol, int32_t max_steps,
     if (ctx->in_flight) return fail(WFSA_ERR_ARG, "an evaluation is in flight");
     if (max_steps <= 0) return WFSA_OK;
     using clk = std::chrono::steady_clock;
-    static const bool trace = std::getenv("WFSA_RUN_TRACE") != nullptr;
+    static const bool trace = std::getenv("WFSA_VERBOSE") != nullptr;
     const auto tr0 = clk::now();
     auto tr_ms = [&](clk::time_point t) { return std::chrono::duration<double, std::micro>(t - tr0).count(); };
     clk::time_point tr_pro{}, tr_first{}, tr_last{}, tr_end{}, tr_enq1{};
@@ -3667,11 +3388,10 @@ static int qn_run_impl(wfsa_dev* ctx, double eta, double tol, int32_t max_steps,
     } else {
         ctx->fixed_t_on = false;
     }
-    const bool piped = pipe_ok(ctx);
-    if (!piped && ctx->use_qw && ctx->qw_waves > 0)
+    if (ctx->use_qw && ctx->qw_waves > 0)
         if (int rc = build_qw_batches(ctx)) return rc;
-    const bool inkern = !piped && qw_usable(ctx);
-    if (!inkern && !piped && ctx->use_qw && std::getenv("WFSA_VERBOSE"))
+    const bool inkern = qw_usable(ctx);
+    if (!inkern && ctx->use_qw && std::getenv("WFSA_VERBOSE"))
         std::fprintf(stderr, "[wfsa] QN update as its own kernel: batches %d waves %d fused %d comm %d rmin %d delta %d "
                      "fallback %d bubbles fused %d fixed_t %d k %d\n", int(ctx->qw_ok), ctx->qw_waves, int(ctx->qn_fused),
                      int(ctx->comm != nullptr), int(ctx->qn_rmin), int(ctx->delta_on),
@@ -3679,7 +3399,7 @@ static int qn_run_impl(wfsa_dev* ctx, double eta, double tol, int32_t max_steps,
                      int(ctx->n_bubbles == 0 || bubbles_fused(ctx, false)), int(ctx->fixed_t_on), ctx->qn_k);
     ctx->stats.qn_inkernel_waves = inkern ? ctx->qw_waves : 0;
     ctx->stats.qn_batches = inkern ? ctx->qw_nbatch : 0;
-    if (piped || inkern) {   // the second weight buffer; the pipe stream starts after everything enqueued so far
+    if (inkern) {   // the second weight buffer
         HIP_TRY(ctx->w_full2.alloc(size_t(ctx->n_params) + 2));
         HIP_TRY(ctx->ewp2.alloc(size_t(ctx->n_params) + 2));
         // its entries the QN steps never write (the trimmed-away parameters'
@@ -3695,7 +3415,6 @@ static int qn_run_impl(wfsa_dev* ctx, double eta, double tol, int32_t max_steps,
             ctx->pipe_init_w = ctx->w_full2.ptr;
             ctx->pipe_init_e = ctx->ewp2.ptr;
         }
-        if (piped) HIP_TRY(hipEventRecord(ctx->p_start, s));
     }
     // steps whose kernels are timed: every stride-th (not the first), or the
     // last of a run shorter than the stride
@@ -3714,8 +3433,7 @@ static int qn_run_impl(wfsa_dev* ctx, double eta, double tol, int32_t max_steps,
         // after a halt fewer no-op steps remain queued (their library GEMMs do not skip)
         while (!stop && enq < max_steps && enq - done < (ctx->dense ? 2 : kQnDepth)) {
             const bool tm = timed_step(enq);
-            if (int rc = piped ? enqueue_qn_step_piped(ctx, eta, tol, enq, tm)
-                               : enqueue_qn_step(ctx, eta, tol, enq, tm, inkern, enq + 1 == max_steps))
+            if (int rc = enqueue_qn_step(ctx, eta, tol, enq, tm, inkern, enq + 1 == max_steps))
                 return rc;
             ++enq;
             ++ctx->seq;
@@ -3764,11 +3482,7 @@ static int qn_run_impl(wfsa_dev* ctx, double eta, double tol, int32_t max_steps,
     if (int rc = flush_qn_finish(ctx)) return rc;
     if (enq > done)
         if (int rc = wait_published(ctx, base + unsigned(enq))) return rc;
-    if (piped || inkern) {   // the weights of the final x back in the parity-0 buffers, after both streams' work:
-        // the main stream waits on the device for the pipe stream's last
-        // finish (two blocking synchronizes here cost a host wake-up each),
-        // and the poll below then covers both
-        if (piped) HIP_TRY(hipStreamWaitEvent(s, ctx->pf[(enq + kQnDepth - 1) % kQnDepth], 0));
+    if (inkern) {   // the weights of the final x back in the parity-0 buffers
         ctx->w_cur = ctx->ewp_cur = nullptr;
         // step e writes the weights of parity e + 1: after an even number of
         // steps, none skipped by a halt, they are in the parity-0 buffers already
