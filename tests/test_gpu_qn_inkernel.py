@@ -22,11 +22,11 @@ pytestmark = pytest.mark.gpu
 FINISH = ["last", "next"]
 
 
-def _learner(W, fsa, sym, off, wt, monkeypatch, inkernel, finish="last"):
+def _learner(W, fsa, sym, off, wt, monkeypatch, inkernel, finish="last", rmin=False):
     monkeypatch.setenv("WFSA_QN_INKERNEL", "1" if inkernel else "0")
     monkeypatch.setenv("WFSA_QN_LAST_SELF", "0" if finish == "next" else "1")
     lrn = W.QuasiNewtonLearner(0)
-    lrn.set_info_rmin(False)
+    lrn.set_info_rmin(rmin)
     lrn.BuildFromPacked(fsa, sym, off, wt)
     lrn.Finalize()
     lrn.Init(7)
@@ -60,15 +60,20 @@ FAMILIES = {
 }
 
 
+@pytest.mark.parametrize("rmin", [False, True], ids=["", "rmin"])
 @pytest.mark.parametrize("finish", FINISH)
 @pytest.mark.parametrize("family", sorted(FAMILIES))
-def test_inkernel_update_equals_qn_step_kernel(family, finish, monkeypatch):
+def test_inkernel_update_equals_qn_step_kernel(family, finish, rmin, monkeypatch):
     """finish: where each step's finish runs (FINISH above); the runs of odd
-    and even length below exercise the Run's last launch finishing itself"""
+    and even length below exercise the Run's last launch finishing itself.
+    rmin: the info rows' rmin column (the product default), folded into the
+    stream kernel (RminFold: one-bubble strings' candidates at once, a
+    multi-bubble string's sum by its last bubble's arrival) against the
+    separate strings pass -- the same (value, string) in every row"""
     import wfsa_amd as W
     fsa, sym, off, wt = _corpus(W, **FAMILIES[family])
-    a = _learner(W, fsa, sym, off, wt, monkeypatch, True, finish)
-    b = _learner(W, fsa, sym, off, wt, monkeypatch, False)
+    a = _learner(W, fsa, sym, off, wt, monkeypatch, True, finish, rmin)
+    b = _learner(W, fsa, sym, off, wt, monkeypatch, False, rmin=rmin)
     # runs of odd and even length, back to back: the weight parity and the
     # arrival counters carry across runs
     # one step first: the gradient the update used and the updated x
@@ -81,9 +86,14 @@ def test_inkernel_update_equals_qn_step_kernel(family, finish, monkeypatch):
     ra = a.Run(3, 1.0, -1.0) + a.Run(4, 1.0, -1.0) + a.Run(1, 1.0, -1.0) + a.Run(12, 1.0, -1.0)
     sa = a.stats()
     rb = b.Run(20, 1.0, -1.0)
-    assert sa["qn_inkernel_waves"] > 0 and sa["qn_batches"] > 0, "the in-kernel update did not run"
+    # (the rmin column rides in the stream kernel only with the bubbles fused
+    # into it: the heavily ambiguous family's bubbles outnumber its waves)
+    if not (rmin and family == "ambiguous"):
+        assert sa["qn_inkernel_waves"] > 0 and sa["qn_batches"] > 0, "the in-kernel update did not run"
     assert b.stats()["qn_inkernel_waves"] == 0
     ra, rb = np.array(ra), np.array(rb)
+    if rmin:   # an ambiguous corpus: the column is a real minimum, not the no-string default
+        assert (ra[:, 6] >= 0).all() and (ra[:, 5] > 0).all(), ra[:, 5:7]
     bad = sorted(set(int(r) for r, _ in np.argwhere(ra != rb)))
     assert not bad, f"rows {bad} differ: {ra[bad].tolist()} vs {rb[bad].tolist()}"
     np.testing.assert_array_equal(a.x(), b.x())
@@ -111,15 +121,16 @@ def test_inkernel_update_matches_host_steps(monkeypatch):
     np.testing.assert_allclose(a.x(), b.x(), rtol=1e-11, atol=1e-13)
 
 
+@pytest.mark.parametrize("rmin", [False, True], ids=["", "rmin"])
 @pytest.mark.parametrize("finish", FINISH)
-def test_inkernel_halting_run(finish, monkeypatch):
+def test_inkernel_halting_run(finish, rmin, monkeypatch):
     """a halting run stops at the same epoch with the same rows and state as
     the separate kernel; the steps enqueued after the halt are skipped and
     the next run starts cleanly"""
     import wfsa_amd as W
     fsa, sym, off, wt = _corpus(W, **FAMILIES["ambiguous"])
-    a = _learner(W, fsa, sym, off, wt, monkeypatch, True, finish)
-    b = _learner(W, fsa, sym, off, wt, monkeypatch, False)
+    a = _learner(W, fsa, sym, off, wt, monkeypatch, True, finish, rmin)
+    b = _learner(W, fsa, sym, off, wt, monkeypatch, False, rmin=rmin)
     ra = a.Run(200, 1.0, 1e-3)
     rb = b.Run(200, 1.0, 1e-3)
     assert 0 < len(ra) < 200
@@ -133,6 +144,47 @@ def test_inkernel_halting_run(finish, monkeypatch):
     b.Init(7)
     assert np.array_equal(np.array(a.Run(5, 1.0, -1.0)), np.array(b.Run(5, 1.0, -1.0)))
     assert np.array_equal(a.x(), b.x())
+
+
+MIXED = {
+    # strings that do not compile (traversal kernels) beside compiled ones
+    "mixed": dict(n_states=256, degree=8, vocab=16, emissions=1, n_strings=8_000, max_len=64, seed=4),
+    # (single-emission states: the delta stream format, which the in-kernel update needs)
+    "mixedA": dict(n_states=1024, degree=8, vocab=16, emissions=1, n_strings=50_000, max_len=128, seed=2),
+}
+
+
+@pytest.mark.parametrize("rmin", [False, True], ids=["", "rmin"])
+@pytest.mark.parametrize("family", sorted(MIXED))
+def test_inkernel_update_with_traversal_strings(family, rmin, monkeypatch):
+    """a corpus with traversal strings keeps the one-launch
+    step.  The traversal kernels run before the stream kernel (the per-edge
+    weights from the edge-weights kernel), their gradient in `out` joins each
+    member's sum in the QN waves in qn_step_kernel's order (traversal part,
+    trivial words, slots) and their ll partials keep their slots -- so every
+    row, x and the last gradient equal the separate kernel's bit for bit"""
+    import wfsa_amd as W
+    fsa, sym, off, wt = _corpus(W, **MIXED[family])
+    dev = W.Device(0)
+    dev.load_model(fsa)
+    dev.load_corpus(sym, off, wt / wt.sum())
+    dev.recognize()
+    dev.objective_grad(np.full(len(fsa.param_names()), -1.0), want_logq=False)
+    tiers = dev.string_tiers()
+    assert (tiers >= 0).any() and (tiers < 0).any(), "the corpus must mix compiled and traversal strings"
+    del dev
+    a = _learner(W, fsa, sym, off, wt, monkeypatch, True, rmin=rmin)
+    b = _learner(W, fsa, sym, off, wt, monkeypatch, False, rmin=rmin)
+    ra = a.Run(3, 1.0, -1.0) + a.Run(6, 1.0, -1.0)
+    rb = b.Run(9, 1.0, -1.0)
+    if not rmin:
+        assert a.stats()["qn_inkernel_waves"] > 0, "the in-kernel update did not run"
+    assert b.stats()["qn_inkernel_waves"] == 0
+    ra, rb = np.array(ra), np.array(rb)
+    bad = sorted(set(int(r) for r, _ in np.argwhere(ra != rb)))
+    assert not bad, f"rows {bad} differ: {ra[bad].tolist()} vs {rb[bad].tolist()}"
+    np.testing.assert_array_equal(a.x(), b.x())
+    np.testing.assert_array_equal(a.last_grad(), b.last_grad())
 
 
 def test_poll_timeout_fails_the_run(monkeypatch):

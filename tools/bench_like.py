@@ -19,7 +19,7 @@ def main():
     lrn.BuildFromPacked(fsa, sym, off, wt)
     lrn.Finalize()
     lrn.Init(7)
-    lrn.set_info_rmin(False)
+    lrn.set_info_rmin(os.environ.get("BL_RMIN") == "1")
     k = int(os.environ.get("BL_STEPS", "20"))
     for rep in range(int(os.environ.get("BL_REPS", "6"))):
         if os.environ.get("BL_PRESLEEP"):   # an idle device before the warm-up (as after the preparation)
@@ -34,7 +34,7 @@ def main():
         lrn.Run(k, 1.0, -1.0)
         torch.cuda.synchronize()
         dt = time.perf_counter() - t0
-        print(f"rep {rep}: {dt * 1e6 / k:.1f} us/step", flush=True)
+        print(f"rep {rep}: {dt * 1e6 / k:.1f} us/step (in-kernel QN waves {lrn.stats()['qn_inkernel_waves']})", flush=True)
 
 
 if __name__ == "__main__":

@@ -2153,9 +2153,12 @@ __device__ __forceinline__ double group_sum(double v, int k, int kmax) {
         asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");     \
         if (lane_id() == 0) tr[k] = __builtin_amdgcn_s_memrealtime();    \
     }
+// zo, so (optional): the bubble's Z and its string (the folded rmin column
+// runs its (min, x) pass later, small_bubble_min)
 template <int N, int RE, bool RMIN = false>
 __device__ __forceinline__ double small_bubble(const BubbleArgs& a, const int4* __restrict__ tbl, int n, int b,
-                                               int pos, unsigned long long* tr = nullptr) {
+                                               int pos, unsigned long long* tr = nullptr, double* zo = nullptr,
+                                               int* so = nullptr) {
 #pragma clang fp contract(off)   // (both forms below: the same bits)
     constexpr int NQ = 1 + RE / 2 + RE / 4;
     int4 q[NQ];
@@ -2196,7 +2199,7 @@ __device__ __forceinline__ double small_bubble(const BubbleArgs& a, const int4* 
     bool same = q[0].x == __builtin_amdgcn_readfirstlane(q[0].x);
 #pragma unroll
     for (int e = 0; e < RE; ++e) same = same && sd[e] == __builtin_amdgcn_readfirstlane(sd[e]);
-    const bool uni = WFSA_UNI_BUBBLES && !RMIN && __all(same);
+    const bool uni = WFSA_UNI_BUBBLES && __all(same);
     if (uni) {
         const int eu = __builtin_amdgcn_readfirstlane(edges);
 #pragma unroll
@@ -2213,22 +2216,44 @@ __device__ __forceinline__ double small_bubble(const BubbleArgs& a, const int4* 
     }
     const double Z = uni ? A[__builtin_amdgcn_readfirstlane(nodes) - 1] : reg_get(A, nodes - 1);
     const double scale = -p / Z;
+    if (zo) {
+        *zo = Z;
+        *so = q[0].y;
+    }
     WFSA_BSTAMP(10)
     if (RMIN && a.rmin_acc) {   // (min, x) forward for the rmin column in B's registers (re-zeroed
                                 // for the backward); the min path never exceeds Z
 #pragma unroll
         for (int k = 0; k < N; ++k) B[k] = k == 0 ? 1.0 : INFINITY;
+        double rv;
+        if (uni) {   // (the wave's shared structure: register-direct node indices, as the sum forward)
+            const int eu = __builtin_amdgcn_readfirstlane(edges);
 #pragma unroll
-        for (int e = 0; e < RE; ++e)
-            if (e < edges && ew[e] > 0.0) {
-                const int dst = sd[e] >> 16;
-                const double v = reg_get(B, sd[e] & 0xffff) * ew[e];
+            for (int e = 0; e < RE; ++e)
+                if (e < eu) {
+                    const int s = __builtin_amdgcn_readfirstlane(sd[e]);
+                    const double v = B[s & 0xffff] * ew[e];
+                    B[s >> 16] = ew[e] > 0.0 ? fmin(B[s >> 16], v) : B[s >> 16];
+                }
+            rv = log(B[__builtin_amdgcn_readfirstlane(nodes) - 1] / Z);
+        } else {
 #pragma unroll
-                for (int k = 0; k < N; ++k) B[k] = dst == k ? fmin(B[k], v) : B[k];
-            }
-        const double rv = log(reg_get(B, nodes - 1) / Z);
-        if (a.rmin_sv) a.rmin_sv[pos] = rv;
-        else global_add(&a.rmin_acc[q[0].y], rv);
+            for (int e = 0; e < RE; ++e)
+                if (e < edges && ew[e] > 0.0) {
+                    const int dst = sd[e] >> 16;
+                    const double v = reg_get(B, sd[e] & 0xffff) * ew[e];
+#pragma unroll
+                    for (int k = 0; k < N; ++k) B[k] = dst == k ? fmin(B[k], v) : B[k];
+                }
+            rv = log(reg_get(B, nodes - 1) / Z);
+        }
+        if (a.rmin_sv) {
+            if (a.wt) store_wt(&a.rmin_sv[pos], rv);   // (read in this launch: the folded rmin column)
+            else a.rmin_sv[pos] = rv;
+        } else {
+            global_add(&a.rmin_acc[q[0].y], rv);
+        }
+
 #pragma unroll
         for (int k = 0; k < N; ++k) B[k] = 0.0;
     }
@@ -2284,7 +2309,102 @@ __device__ __forceinline__ double small_bubble(const BubbleArgs& a, const int4* 
 // weight) in LDS in parallel, lane 0 runs the two sweeps over the staged
 // edges, and the lanes write the contributions (an edge may have several
 // parameters, hence several slots).
-__device__ double big_bubble(const BubbleArgs& a, int i, int* lsd, double* lw, double* lv, double* AB) {
+// The folded rmin column's (min, x) pass over small bubble b (the class's
+// table and size, as small_bubble), after the wave's arrival -- off the QN
+// update's path: the quads and weights again (L2 hits), the min forward, and
+// log(min path / Z) with the sum forward's Z (kept from small_bubble); the
+// same arithmetic as small_bubble's RMIN pass, so the same bits
+template <int N, int RE>
+__device__ __forceinline__ double small_bubble_min(const BubbleArgs& a, const int4* __restrict__ tbl, int n, int b,
+                                                   double Z) {
+#pragma clang fp contract(off)
+    constexpr int NQ = 1 + RE / 2;   // (the header and the edges; not the slots)
+    int4 q[NQ];
+#pragma unroll
+    for (int k = 0; k < NQ; ++k) q[k] = tbl[size_t(k) * size_t(n) + size_t(b)];
+    int code[RE], sd[RE];
+#pragma unroll
+    for (int k = 0; k < RE / 2; ++k) {
+        code[2 * k] = q[1 + k].x;
+        sd[2 * k] = q[1 + k].y;
+        code[2 * k + 1] = q[1 + k].z;
+        sd[2 * k + 1] = q[1 + k].w;
+    }
+    double ew[RE];
+#pragma unroll
+    for (int e = 0; e < RE; ++e) ew[e] = a.ewp[code[e]];
+    // a waterfall over the wave's bubble shapes (sorted by shape: mostly
+    // one): the first pending lane's structure, read into scalars, runs with
+    // register-direct node indices for every lane; the lanes of that shape
+    // keep their result.  (Per-lane node indices put the node vector in
+    // scratch memory.)
+    double rv = 0.0;
+    bool pending = true;
+    while (true) {
+        const unsigned long long m = __ballot(pending);
+        if (m == 0ull) break;
+        const int lead = __ffsll(m) - 1;
+        const int hu = __builtin_amdgcn_readlane(q[0].x, lead);
+        bool mine = pending && q[0].x == hu;
+        int su[RE];
+#pragma unroll
+        for (int e = 0; e < RE; ++e) {
+            su[e] = __builtin_amdgcn_readlane(sd[e], lead);
+            mine = mine && sd[e] == su[e];
+        }
+        const int eu = hu >> 16, nu = hu & 0xffff;
+        double B[N];
+#pragma unroll
+        for (int k = 0; k < N; ++k) B[k] = k == 0 ? 1.0 : INFINITY;
+#pragma unroll
+        for (int e = 0; e < RE; ++e)
+            if (e < eu) {
+                const double v = B[su[e] & 0xffff] * ew[e];
+                B[su[e] >> 16] = ew[e] > 0.0 ? fmin(B[su[e] >> 16], v) : B[su[e] >> 16];
+            }
+        if (mine) {
+            rv = log(B[nu - 1] / Z);
+            pending = false;
+        }
+    }
+    return rv;
+}
+
+// The folded rmin column (RminFold): the candidate of the bubble at position
+// pos (value rv, string str) -- a one-bubble string's at once; a k-bubble
+// string's value stored write-through, then (the store retired) the
+// string's arrival: the k-th sums the k stored values in bubble order.
+__device__ __forceinline__ void rmin_settle(const RminFold& rf, double* sv, int pos, double rv, int str,
+                                            double& cv, double& ci) {
+    const int2 bk = rf.bk[pos];
+    double v = INFINITY, idx = -1.0;
+    if (bk.x == 1) {
+        v = rv;
+        idx = double(str);
+    } else if (bk.x > 1) {
+        store_wt(sv + pos, rv);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        const unsigned old = __hip_atomic_fetch_add(rf.cnt + bk.y, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (old == unsigned(bk.x - 1)) {   // the last of the string's bubbles: every value is stored
+            rf.cnt[bk.y] = 0u;             // (for the next launch)
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");   // (a compiler barrier)
+            double r = 0.0;
+            for (int j = 0; j < bk.x; ++j) r += load_wt(sv + rf.mpos[bk.y + j]);
+            v = r;
+            idx = double(str);
+        }
+    }
+    if (v < cv || (v == cv && idx < ci)) {
+        cv = v;
+        ci = idx;
+    }
+}
+
+// rf (the folded rmin column, or null): lane 0 settles the bubble's string
+// at once -- rare bubbles: its store retired, its string's arrival, the sum
+// by the k-th arrival -- and min-folds the candidate into (cv, ci)
+__device__ __forceinline__ double big_bubble(const BubbleArgs& a, int i, int* lsd, double* lw, double* lv, double* AB,
+                             const RminFold* rf = nullptr, double* cv = nullptr, double* ci = nullptr) {
     const int lane = lane_id();
     const int off = a.big_off[i];
     const int32_t* rec = a.bub + off;
@@ -2322,8 +2442,14 @@ __device__ double big_bubble(const BubbleArgs& a, int i, int* lsd, double* lw, d
             for (int e = 0; e < edges; ++e)
                 if (lw[e] > 0.0) B[lsd[e] >> 16] = fmin(B[lsd[e] >> 16], B[lsd[e] & 0xffff] * lw[e]);
             const double rv = log(B[nodes - 1] / Z);
-            if (a.rmin_sv) a.rmin_sv[a.n_small4 + a.n_small + i] = rv;
-            else global_add(&a.rmin_acc[rec[1]], rv);
+            const int pos = a.n_small4 + a.n_small + i;
+            if (a.rmin_sv) {
+                if (a.wt) store_wt(&a.rmin_sv[pos], rv);
+                else a.rmin_sv[pos] = rv;
+            } else {
+                global_add(&a.rmin_acc[rec[1]], rv);
+            }
+            if (rf) rmin_settle(*rf, a.rmin_sv, pos, rv, rec[1], *cv, *ci);
             for (int v = 0; v < nodes; ++v) B[v] = 0.0;
         }
         B[nodes - 1] = 1.0;
@@ -2442,7 +2568,7 @@ struct QnBatchIn {
     int c0, nc, m0, m1, nchunk;
     int64_t cbase;
     int con, fo, nch, fc, cpl;
-    double x, ft, laml;
+    double x, ft, laml, gout;
 };
 __device__ __forceinline__ QnBatchIn qn_wave_load(const QnWave& q, int b) {
     const int lane = lane_id();
@@ -2457,10 +2583,11 @@ __device__ __forceinline__ QnBatchIn qn_wave_load(const QnWave& q, int b) {
     const int m = in.m0 + lane;
     in.con = in.c0;
     in.fo = in.nch = in.fc = in.cpl = 0;
-    in.x = in.ft = in.laml = 0.0;
+    in.x = in.ft = in.laml = in.gout = 0.0;
     if (m < in.m1) {
         in.con = q.con_of[m];
         in.fo = q.full_of[m];
+        if (q.out) in.gout = q.out[1 + in.fo];   // (the traversal strings' part)
         in.x = q.x[m];
         in.ft = q.fixed_t[m];
         in.fc = q.mfirst[m];
@@ -2555,7 +2682,7 @@ __device__ __forceinline__ void qn_wave_batch(const QnWave& q, const QnBatchIn& 
         for (int u = 0; u < 4; ++u)
             if (t0 + u < nch) sm += v[u];
     }
-    double gi = 0.0;
+    double gi = in.gout;   // qn_step_kernel's order: the traversal part, + the trivial words', + the slots'
     gi += ft;
     const double sg = gi + sm;
     const double e = exp(x);
@@ -2677,6 +2804,28 @@ __device__ __forceinline__ void qn_wave_run(const QnWave& q, int r, unsigned lon
     if (tr && lane == 0) tr[6] = __builtin_amdgcn_s_memrealtime();
 }
 
+// A field of the stream kernel's argument block read where it is used,
+// through a pointer into the kernel-argument segment the compiler cannot see
+// through: kernel arguments are otherwise loaded at the entry and kept in
+// scalar registers to the end, and the QN waves' and the finishes' ~60
+// dwords of them spilled the kernel's scalar registers into vector lanes
+// (616 lane reads in the in-kernel QN variant; 131 with these three late)
+template <typename T>
+__device__ __forceinline__ T late_arg(size_t off) {
+    static_assert(sizeof(T) % 4 == 0, "argument blocks are dword multiples");
+    typedef __attribute__((address_space(4))) const char kchar;
+    typedef __attribute__((address_space(4))) const uint32_t kword;
+    kchar* kp = (kchar*)(__builtin_amdgcn_kernarg_segment_ptr());
+    asm volatile("" : "+s"(kp));
+    kword* src = reinterpret_cast<kword*>(kp + off);
+    T v;
+    uint32_t* dst = reinterpret_cast<uint32_t*>(&v);
+#pragma unroll
+    for (size_t i = 0; i < sizeof(T) / 4; ++i) dst[i] = src[i];
+    return v;
+}
+#define WFSA_LATE_ARG(field) late_arg<decltype(CompiledArgs::field)>(offsetof(CompiledArgs, field))
+
 template <bool WIDE, bool W_LDS, bool MULTI, int DBG = 0, bool RMIN = false, bool DELTA = false, bool QN = false>
 #ifdef WFSA_FBS_VGPR64   // (variant builds: a 64-VGPR budget, two 1024-thread blocks per CU)
 #define WFSA_FBS_ATTR __attribute__((amdgpu_num_vgpr(64)))
@@ -2784,8 +2933,9 @@ __global__ __launch_bounds__(1024, (DBG == 10 ? 8 : 1)) WFSA_FBS_ATTR void fbs_k
         if (fin_wave && a.fin.active && DBG != 12 && DBG != 13) {
             double finfo[7];
             unsigned fstat = kQnRan;
-            qn_finish_compute<true>(a.fin, nullptr, finfo, fstat);
-            if (lane == 0) qn_finish_publish(a.fin, finfo, fstat);
+            const QnFinish fin = WFSA_LATE_ARG(fin);
+            qn_finish_compute<true>(fin, nullptr, finfo, fstat);
+            if (lane == 0) qn_finish_publish(fin, finfo, fstat);
         }
     };
     if (DBG == 5) {   // the launch and the finish only
@@ -2794,6 +2944,11 @@ __global__ __launch_bounds__(1024, (DBG == 10 ? 8 : 1)) WFSA_FBS_ATTR void fbs_k
     }
     double ll_acc = 0.0;
     bool stored = fin_wave;   // (QN: this wave's stores must retire before it arrives)
+    // the folded rmin column (RMIN && QN, RminFold): the lane's small bubble
+    // (position, value, string) until its wave arrived, and the lane's candidate
+    constexpr bool RF = RMIN && QN;
+    int rm_pos = -1, rm_str = -1;
+    double rm_z = 1.0, rm_cv = INFINITY, rm_ci = -1.0;
     const bool small_wave = a.bub_on && DBG != 8 && DBG != 10 && DBG != 13 && !fin_wave && w < a.bub.small_wpb;
     auto small_bubbles = [&]() {   // one per lane, from the first small_wpb waves of every block (spread over all CUs)
         stored = true;
@@ -2808,9 +2963,16 @@ __global__ __launch_bounds__(1024, (DBG == 10 ? 8 : 1)) WFSA_FBS_ATTR void fbs_k
         // (the bubbles are on the QN update's critical path; the stream waves
         // beside them mostly wait for memory: the bubble waves issue first)
         __builtin_amdgcn_s_setprio(2);
-        if (b >= 0 && b < a.bub.n_small4) ll_acc += small_bubble<4, 4, RMIN>(a.bub, a.bub.sm4_tbl, a.bub.n_small4, b, b, btr);
-        else if (b >= a.bub.n_small4)
-            ll_acc += small_bubble<8, 8, RMIN>(a.bub, a.bub.sm_tbl, a.bub.n_small, b - a.bub.n_small4, b, btr);
+        // (RF: the bubbles' (min, x) pass after the arrival, small_bubble_min)
+        constexpr bool BR = RMIN && !RF;
+        double* zo = RF ? &rm_z : nullptr;
+        int* so = RF ? &rm_str : nullptr;
+        const BubbleArgs bub = WFSA_LATE_ARG(bub);
+        if (b >= 0 && b < bub.n_small4)
+            ll_acc += small_bubble<4, 4, BR>(bub, bub.sm4_tbl, bub.n_small4, b, b, btr, zo, so);
+        else if (b >= bub.n_small4)
+            ll_acc += small_bubble<8, 8, BR>(bub, bub.sm_tbl, bub.n_small, b - bub.n_small4, b, btr, zo, so);
+        if (RF && b >= 0) rm_pos = int(b);
         __builtin_amdgcn_s_setprio(0);
     };
     // big bubbles, one wavefront each, from the last blocks' last waves down
@@ -2824,7 +2986,10 @@ __global__ __launch_bounds__(1024, (DBG == 10 ? 8 : 1)) WFSA_FBS_ATTR void fbs_k
             char* stg = reinterpret_cast<char*>(lds) + a.bub.big_lds_off + w * big_stage_bytes(E);
             double* lw = reinterpret_cast<double*>(stg);
             int* lsd = reinterpret_cast<int*>(lw + E + 2 * kMaxBubbleNodes);
-            for (int i = r; i < a.bub.n_big; i += nw - 1) ll_acc += big_bubble(a.bub, i, lsd, lw, lw, lw + E);
+            const BubbleArgs bub = WFSA_LATE_ARG(bub);
+            const RminFold rf = WFSA_LATE_ARG(rf);
+            for (int i = r; i < bub.n_big; i += nw - 1)
+                ll_acc += big_bubble(bub, i, lsd, lw, lw, lw + E, RF ? &rf : nullptr, &rm_cv, &rm_ci);
         }
     };
     if (!DELTA && W_LDS && DBG != 4 && !a.no_streams) {
@@ -2876,6 +3041,16 @@ __global__ __launch_bounds__(1024, (DBG == 10 ? 8 : 1)) WFSA_FBS_ATTR void fbs_k
         if (lane == 0 && prev == unsigned(wpb - 1))   // the block's last wave: one arrival for all its stores
             __hip_atomic_fetch_add(a.qw.arrive + a.qw.parity, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         WFSA_STAMP(3)
+        // the lane's small bubble's rmin candidate, off the QN update's path
+        // (after the block's arrival, before this wave's stream pass)
+        if (RF && rm_pos >= 0) {
+            const BubbleArgs bub = WFSA_LATE_ARG(bub);
+            const RminFold rf = WFSA_LATE_ARG(rf);
+            const double rv = rm_pos < bub.n_small4
+                                  ? small_bubble_min<4, 4>(bub, bub.sm4_tbl, bub.n_small4, rm_pos, rm_z)
+                                  : small_bubble_min<8, 8>(bub, bub.sm_tbl, bub.n_small, rm_pos - bub.n_small4, rm_z);
+            rmin_settle(rf, bub.rmin_sv, rm_pos, rv, rm_str, rm_cv, rm_ci);
+        }
     }
     if (kStreams) load(B, D);
     double p = 0.0, acc0 = 0.0, acc1 = 0.0;
@@ -3002,8 +3177,21 @@ __global__ __launch_bounds__(1024, (DBG == 10 ? 8 : 1)) WFSA_FBS_ATTR void fbs_k
     WFSA_STAMP(4)
     // one log-likelihood partial per block (the QN finish sums them)
     __shared__ double wsum[1024 / kWave];
+    __shared__ double wrv[1024 / kWave], wri[1024 / kWave];   // (RF: the waves' rmin candidates)
     ll_acc = wave_sum(ll_acc);
     if (lane == 0) wsum[w] = ll_acc;
+    if (RF) {
+        // the ambiguous traversal strings (values from the kernels before this launch), strided over the grid
+        for (int i = bid * int(blockDim.x) + int(threadIdx.x); i < a.rf.n_trav; i += nblk * int(blockDim.x)) {
+            const int st = a.rf.trav[i];
+            min_pair(rm_cv, rm_ci, a.rf.rmin_log[st], double(st));
+        }
+        for (int o = 32; o > 0; o >>= 1) min_pair(rm_cv, rm_ci, __shfl_xor(rm_cv, o, kWave), __shfl_xor(rm_ci, o, kWave));
+        if (lane == 0) {
+            wrv[w] = rm_cv;
+            wri[w] = rm_ci;
+        }
+    }
     __syncthreads();
     const bool self_fin = QN && a.qw.self_finish;
     if (threadIdx.x == 0) {
@@ -3011,6 +3199,17 @@ __global__ __launch_bounds__(1024, (DBG == 10 ? 8 : 1)) WFSA_FBS_ATTR void fbs_k
         for (int i = 0; i < wpb; ++i) t += wsum[i];
         if (self_fin) store_wt(a.ll_part + bid, t);   // (read by this launch's finisher)
         else a.ll_part[bid] = t;
+        if (RF) {
+            double v = wrv[0], idx = wri[0];
+            for (int i = 1; i < wpb; ++i) min_pair(v, idx, wrv[i], wri[i]);
+            if (self_fin) {
+                store_wt(a.rf.part + 2 * bid, v);
+                store_wt(a.rf.part + 2 * bid + 1, idx);
+            } else {
+                a.rf.part[2 * bid] = v;
+                a.rf.part[2 * bid + 1] = idx;
+            }
+        }
     }
     // this block's slice of the per-edge weights and the zeroed result, for
     // the kernels after this one (nothing in this launch reads them)
@@ -3019,10 +3218,11 @@ __global__ __launch_bounds__(1024, (DBG == 10 ? 8 : 1)) WFSA_FBS_ATTR void fbs_k
     // the block barrier; a second call site before it, as an option, made
     // the kernel spill 96 VGPRs)
     if (QN && w == wpb - 2 && bid < a.qw.n_waves) {
+        const QnWave qw = WFSA_LATE_ARG(qw);
 #ifdef WFSA_EXPERIMENTS
-        qn_wave_run(a.qw, bid, tr);
+        qn_wave_run(qw, bid, tr);
 #else
-        qn_wave_run(a.qw, bid, nullptr);
+        qn_wave_run(qw, bid, nullptr);
 #endif
     }
     // Self-finish: every block's wave 0 (its log-likelihood partial) and
@@ -3040,8 +3240,9 @@ __global__ __launch_bounds__(1024, (DBG == 10 ? 8 : 1)) WFSA_FBS_ATTR void fbs_k
         if (before + 1u == unsigned(nblk + a.qw.n_waves) && load_wt(a.qw.halted + 1) == 0u) {
             double info[7];
             unsigned st = kQnRan;
-            qn_finish_compute<true, true>(a.qw.fin, nullptr, info, st);
-            if (lane == 0) qn_finish_publish(a.qw.fin, info, st);
+            const QnFinish fin = WFSA_LATE_ARG(qw.fin);
+            qn_finish_compute<true, true>(fin, nullptr, info, st);
+            if (lane == 0) qn_finish_publish(fin, info, st);
         }
     }
     WFSA_STAMP(7)
@@ -3469,7 +3670,9 @@ hipError_t launch_compiled(const CompiledArgs& a, int grid, int block, size_t ld
         default: break;
         }
 #endif
-        if (a.qw.on)   // with this step's QN update (the host checks: no rmin, bubbles fused or none)
+        if (a.qw.on && a.rf.part)   // with this step's QN update and the rmin column folded in
+            return go(fbs_kernel<false, true, false, 0, true, true, true>, grid, block, lds, stream, ev0, ev1, a);
+        if (a.qw.on)   // with this step's QN update (the host checks: bubbles fused or none)
             return go(fbs_kernel<false, true, false, 0, false, true, true>, grid, block, lds, stream, ev0, ev1, a);
         if (a.bub_on && a.bub.rmin_acc)
             return go(fbs_kernel<false, true, false, 0, true, true>, grid, block, lds, stream, ev0, ev1, a);

@@ -623,6 +623,7 @@ struct QnWave {
     const int32_t* cptr;         // [k + 1]
     const int32_t* full_of;      // [n]
     const double* fixed_t;       // [n] constant trivial-word gradient, trimmed order
+    const double* out;           // [1 + n_full] the traversal strings' gradient (kernels before this launch), or null
     const double* contrib;
     double* x;
     double* lambda;
@@ -641,6 +642,31 @@ struct QnWave {
     unsigned* done;              // [2] per-parity counters of those arrivals (each launch zeroes the other's)
     uint32_t poll_limit;         // polls before a QN wave gives up (0: kQnPollLimit)
     int32_t poll_fault;          // fault injection (tests): QN wave 0 waits for one arrival too many
+};
+
+// The rmin column inside the in-kernel QN step (fbs_kernel<..., RMIN, DELTA,
+// QN>; GetOptimizationInfo's smallest relative path probability,
+// src/QuasiNewtonLearner.cpp:80-84): no strings pass of its own.  A bubble
+// whose string has one bubble is that string's candidate at once (its lane's
+// log(min path / Z)); a string of k > 1 bubbles stores each bubble's value
+// write-through, and after the wave's arrival (its stores retired) adds one
+// to the string's counter -- the k-th adder sums the k values in bubble order
+// (the strings pass's order: the same bits) and holds the candidate.
+// Ambiguous traversal strings' values (rmin_log, written by the traversal
+// kernels before this launch) are read at the block's end.  Each block's
+// (min, string) pair -- ties to the lower string, an order-free minimum --
+// goes to part[block] beside its log-likelihood partial; the step's finish
+// reduces them.
+struct RminFold {
+    const int2* bk;          // [bubble positions] (k, run): k = bubbles of the bubble's string if it is
+                             // ambiguous, else 0; run = the string's first entry in mpos (k > 1)
+    const int32_t* mpos;     // the bubble positions of each multi-bubble string, in bubble order
+    unsigned* cnt;           // [mpos entries] the arrivals per multi-bubble string (at its run's first
+                             // entry; the k-th arrival re-zeroes it for the next launch)
+    const int32_t* trav;     // [n_trav] ambiguous traversal strings
+    int32_t n_trav;
+    const double* rmin_log;  // [S] their values
+    double* part;            // [blocks][2] this launch's block minima (log rmin, string index)
 };
 
 struct CompiledArgs {
@@ -685,6 +711,7 @@ struct CompiledArgs {
     const unsigned* halted;  // device-resident QN run: nonzero = skip (or null)
     QnFinish fin;            // fin.active: block 0 finishes the previous QN step first
     QnWave qw;               // qw.on: this step's QN update runs in this launch
+    RminFold rf;             // rf.part: the rmin column folded into this launch (with qw.on)
     unsigned long long* trace;   // timing experiments only (WFSA_FBS_TRACE): [waves][8] s_memrealtime stamps
 };
 

@@ -269,7 +269,8 @@ __device__ inline void qn_finish_compute(const QnFinish& f, double* red, double*
     double rv = INFINITY, ri = -1.0;   // rmin column from block minima, ties to the lower string
     if (f.rmin_part)
         for (int j = t; j < f.rmin_n_part; j += nt) {
-            const double v = f.rmin_part[2 * j], i = f.rmin_part[2 * j + 1];
+            const double v = WT ? load_wt(f.rmin_part + 2 * j) : f.rmin_part[2 * j];
+            const double i = WT ? load_wt(f.rmin_part + 2 * j + 1) : f.rmin_part[2 * j + 1];
             if (v < rv || (v == rv && i < ri)) {
                 rv = v;
                 ri = i;

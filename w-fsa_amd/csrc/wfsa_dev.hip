@@ -298,6 +298,15 @@ struct wfsa_dev {
     std::vector<int32_t> h_bfirst, h_nbub;   // per string: first bubble ordinal, bubbles (compiled strings)
     int max_bub_nodes = 1;                   // largest compiled bubble (nodes)
     int64_t rm_n_amb = 0;
+    // the rmin column folded into the in-kernel QN step (fb_kernels.hpp RminFold)
+    std::vector<int32_t> h_bpos;    // list position of each bubble (layout)
+    DevBuf<int2> rm_bk;             // [positions] (bubbles of its ambiguous string, its run in rm_mpos)
+    DevBuf<int32_t> rm_mpos;        // the positions of each multi-bubble string's bubbles, in bubble order
+    DevBuf<unsigned> rm_cnt;        // [rm_mpos entries] arrivals per multi-bubble string, zero between launches
+    DevBuf<int32_t> rm_trav;        // the ambiguous traversal strings
+    int32_t rm_n_trav = 0;
+    DevBuf<double> rm_bpart;        // [2][stream-kernel blocks][2] block minima, by step parity
+    double* rm_bpart_cur = nullptr; // this step's half (set by enqueue_qn_step for enqueue_compiled)
     int rm_gen = -1;             // prep_gen the list was built for
     bool qn_rmin = false;        // the device QN loop fills the rmin columns
     bool rm_eval = false;        // the evaluation being enqueued also runs the traversal min forward
@@ -1779,6 +1788,8 @@ int prepare(wfsa_dev* ctx, int level) {
                 for (int32_t o : *list) bpos[size_t(idx_of.at(o))] = pos++;
             HIP_TRY(ctx->rm_bpos.upload(bpos.data(), bpos.size(), s));
             HIP_TRY(ctx->rm_sv.alloc(bpos.size()));
+            HIP_TRY(hipStreamSynchronize(s));
+            ctx->h_bpos = std::move(bpos);
         }
         ctx->h_bubbuf = std::move(h_bubbuf);
         ctx->h_sm4_list = std::move(small4);
@@ -2062,6 +2073,16 @@ int enqueue_compiled(wfsa_dev* ctx, bool with_grad, bool want_logq, const unsign
             c.qw = ctx->qw_next;
             ctx->qw_next.on = 0;
             c.bub.wt = 1;   // the QN waves read the slots in this launch
+            if (ctx->rm_bpart_cur) {   // ... and the rmin column (RminFold)
+                c.rf.bk = ctx->rm_bk.ptr;
+                c.rf.mpos = ctx->rm_mpos.ptr;
+                c.rf.cnt = ctx->rm_cnt.ptr;
+                c.rf.trav = ctx->rm_trav.ptr;
+                c.rf.n_trav = ctx->rm_n_trav;
+                c.rf.rmin_log = ctx->rm_rs.ptr;
+                c.rf.part = ctx->rm_bpart_cur;
+                ctx->rm_bpart_cur = nullptr;
+            }
         }
         if (with_grad && tables == 0)   // the blocks accumulate into their slabs
             HIP_TRY(hipMemsetAsync(ctx->gpart.ptr, 0, size_t(ctx->c_grid) * size_t(np) * sizeof(double), s));
@@ -2154,48 +2175,23 @@ wfsa::ReduceArgs reduce_args(wfsa_dev* ctx, const unsigned* halted, int32_t n_ll
     return r;
 }
 
-int enqueue_evaluation(wfsa_dev* ctx, bool want_logq, const unsigned* halted, int slot, bool with_tail = true,
-                       int32_t* n_ll = nullptr) {
+// The traversal strings (strings that do not compile): the tier kernels in
+// weighted mode, gradient into out[1..] (zeroed and the per-edge weights
+// written before them), ll partials from slot wave_off on (advanced past
+// theirs).
+bool has_traversal(const wfsa_dev* ctx) {
+    return ctx->n_fall[0] + ctx->n_fall[1] + ctx->n_fall[2] > 0 || (ctx->w2_grid > 0 && ctx->w2_all);
+}
+int32_t trav_ll_waves(const wfsa_dev* ctx) {   // the ll partial slots enqueue_traversal fills
+    const bool w2_covers_01 = ctx->w2_grid > 0 && ctx->w2_all;
+    int32_t n = 0;
+    for (int t = 0; t < 2 && !w2_covers_01; ++t)
+        if (ctx->n_fall[t]) n += ctx->fall_grid[t] * ctx->cfg[t].waves_per_block;
+    if (ctx->n_fall[2] || w2_covers_01) n += ctx->w2_grid > 0 ? ctx->w2_grid : ctx->fall_grid[2];
+    return n;
+}
+int enqueue_traversal(wfsa_dev* ctx, bool want_logq, const unsigned* halted, int32_t& wave_off) {
     hipStream_t s = ctx->stream;
-    if (ctx->mpath) {   // matrix-file mode: out is complete when it returns
-        HIP_TRY(record(ctx, ctx->k0, slot, s));
-        HIP_TRY(ctx->mpath->enqueue(ctx->w_full.ptr, ctx->out.ptr, want_logq ? ctx->logq.ptr : nullptr, halted, s));
-        HIP_TRY(record(ctx, ctx->kc, slot, s));
-        HIP_TRY(record(ctx, ctx->k2, slot, s));
-        if (n_ll) *n_ll = 0;
-        return WFSA_OK;
-    }
-    if (ctx->dense) {   // fp64 MFMA path: out is complete when it returns
-        HIP_TRY(record(ctx, ctx->k0, slot, s));
-        HIP_TRY(ctx->dense->enqueue(ctx->ewp.ptr, false, ctx->out.ptr, want_logq ? ctx->logq.ptr : nullptr, halted, s));
-        HIP_TRY(record(ctx, ctx->kc, slot, s));
-        HIP_TRY(record(ctx, ctx->k2, slot, s));
-        if (n_ll) *n_ll = 0;
-        return WFSA_OK;
-    }
-    // (a bubble kernel on a second stream beside the stream kernel: the
-    // cross-stream fork / join cost more idle time, 5-20 us, than the
-    // overlap saved -- measured and removed)
-    ctx->rm_sv_used = false;   // (set by the stream kernel's launch when it stores the bubbles' rmin values)
-    const bool fusedb = bubbles_fused(ctx, want_logq);
-    // the ll partials: the stream kernel's blocks, then the other kernels' waves
-    int32_t wave_off = ctx->n_groups > 0 ? ctx->i_grid : 0;   // one per stream-kernel block
-    // the per-edge weights and the zeroed result are for the traversal
-    // kernels and the reduction: the fused QN step over compiled strings
-    // alone reads neither, so the stream kernel skips writing them
-    ctx->eval_no_slice = !with_tail && ctx->n_fall[0] + ctx->n_fall[1] + ctx->n_fall[2] == 0;
-    // the QN update in the stream kernel reads the bubble slots: a separate
-    // bubble kernel then runs before it (its slots visible at the boundary)
-    const bool bub_first = ctx->qw_next.on && ctx->n_bubbles > 0 && !fusedb;
-    if (bub_first)
-        if (int rc = enqueue_bubbles(ctx, want_logq, halted, wave_off, s)) return rc;
-    const int crc = enqueue_compiled(ctx, false, want_logq, halted, slot);
-    ctx->eval_no_slice = false;
-    if (crc) return crc;
-    if (ctx->n_bubbles > 0 && !fusedb && !bub_first) {
-        if (int rc = enqueue_bubbles(ctx, want_logq, halted, wave_off, s)) return rc;
-    }
-    if (ctx->n_bubbles > 0 && !fusedb) wave_off += ctx->b_waves;
     const bool w2_covers_01 = ctx->w2_grid > 0 && ctx->w2_all;
     for (int t = 0; t < 2 && !w2_covers_01; ++t) {
         if (!ctx->n_fall[t]) continue;
@@ -2241,10 +2237,75 @@ int enqueue_evaluation(wfsa_dev* ctx, bool want_logq, const unsigned* halted, in
             wave_off += ctx->fall_grid[2];
         }
     }
+    return WFSA_OK;
+}
+
+int enqueue_evaluation(wfsa_dev* ctx, bool want_logq, const unsigned* halted, int slot, bool with_tail = true,
+                       int32_t* n_ll = nullptr) {
+    hipStream_t s = ctx->stream;
+    if (ctx->mpath) {   // matrix-file mode: out is complete when it returns
+        HIP_TRY(record(ctx, ctx->k0, slot, s));
+        HIP_TRY(ctx->mpath->enqueue(ctx->w_full.ptr, ctx->out.ptr, want_logq ? ctx->logq.ptr : nullptr, halted, s));
+        HIP_TRY(record(ctx, ctx->kc, slot, s));
+        HIP_TRY(record(ctx, ctx->k2, slot, s));
+        if (n_ll) *n_ll = 0;
+        return WFSA_OK;
+    }
+    if (ctx->dense) {   // fp64 MFMA path: out is complete when it returns
+        HIP_TRY(record(ctx, ctx->k0, slot, s));
+        HIP_TRY(ctx->dense->enqueue(ctx->ewp.ptr, false, ctx->out.ptr, want_logq ? ctx->logq.ptr : nullptr, halted, s));
+        HIP_TRY(record(ctx, ctx->kc, slot, s));
+        HIP_TRY(record(ctx, ctx->k2, slot, s));
+        if (n_ll) *n_ll = 0;
+        return WFSA_OK;
+    }
+    // (a bubble kernel on a second stream beside the stream kernel: the
+    // cross-stream fork / join cost more idle time, 5-20 us, than the
+    // overlap saved -- measured and removed)
+    ctx->rm_sv_used = false;   // (set by the stream kernel's launch when it stores the bubbles' rmin values)
+    const bool fusedb = bubbles_fused(ctx, want_logq);
+    const bool trav = has_traversal(ctx);
+    // the ll partials: the stream kernel's blocks, then the bubble kernel's
+    // waves, then the traversal kernels' -- the same slots whatever order the
+    // kernels run in (the finish sums them in slot order)
+    int32_t wave_off = ctx->n_groups > 0 ? ctx->i_grid : 0;   // one per stream-kernel block
+    const int32_t trav_off = wave_off + ((ctx->n_bubbles > 0 && !fusedb) ? ctx->b_waves : 0);
+    // With this step's QN update in the stream kernel, the traversal strings
+    // run first: their gradient (in out, which the QN waves then read) and
+    // log-likelihood partials are complete at the stream kernel's start.
+    // The per-edge weights and the zeroed result they need come from the
+    // edge-weights kernel (the stream kernel's own slice of them would be
+    // too late).
+    const bool trav_first = trav && ctx->qw_next.on;
+    if (trav_first) {
+        HIP_TRY(wfsa::launch_edge_weights(ctx->w_cur ? ctx->w_cur : ctx->w_full.ptr, ctx->pptr.ptr, ctx->pidx.ptr,
+                                          ctx->lw.ptr, ctx->ew.ptr, ctx->erec.ptr, ctx->n_edges + ctx->n_end,
+                                          ctx->out.ptr, int64_t(ctx->n_params) + 1, s));
+        int32_t off = trav_off;
+        if (int rc = enqueue_traversal(ctx, want_logq, halted, off)) return rc;
+    }
+    // the per-edge weights and the zeroed result are for the traversal
+    // kernels and the reduction: the fused QN step over compiled strings
+    // alone reads neither, so the stream kernel skips writing them (and with
+    // the traversal strings first it must: out holds their gradient)
+    ctx->eval_no_slice = !with_tail && (!trav || trav_first);
+    // the QN update in the stream kernel reads the bubble slots: a separate
+    // bubble kernel then runs before it (its slots visible at the boundary)
+    const bool bub_first = ctx->qw_next.on && ctx->n_bubbles > 0 && !fusedb;
+    if (bub_first)
+        if (int rc = enqueue_bubbles(ctx, want_logq, halted, wave_off, s)) return rc;
+    const int crc = enqueue_compiled(ctx, false, want_logq, halted, slot);
+    ctx->eval_no_slice = false;
+    if (crc) return crc;
+    if (ctx->n_bubbles > 0 && !fusedb && !bub_first) {
+        if (int rc = enqueue_bubbles(ctx, want_logq, halted, wave_off, s)) return rc;
+    }
+    wave_off = trav_off;
+    if (trav_first) wave_off += trav_ll_waves(ctx);
+    else if (int rc = enqueue_traversal(ctx, want_logq, halted, wave_off)) return rc;
     if (n_ll) *n_ll = wave_off;
     if (!with_tail) {
-        const bool after_kc = (ctx->n_bubbles > 0 && !fusedb && !bub_first) || ctx->n_fall[0] || ctx->n_fall[1] ||
-                              ctx->n_fall[2] || w2_covers_01;
+        const bool after_kc = (ctx->n_bubbles > 0 && !fusedb && !bub_first) || (trav && !trav_first);
         if (!after_kc && slot >= 0) ctx->k2_kc[slot] = true;
         else HIP_TRY(record(ctx, ctx->k2, slot, s));
         return WFSA_OK;
@@ -2292,6 +2353,34 @@ int rmin_prepare(wfsa_dev* ctx) {
         }
         ctx->rm_n_amb = int64_t(amb.size());
         if (!amb.empty()) HIP_TRY(ctx->rm_amb.upload(amb.data(), amb.size(), s));
+        {   // the folded form's tables (RminFold): per bubble position its string's bubble count and
+            // run; each multi-bubble string's positions in bubble order; the traversal strings
+            const size_t nb = size_t(std::max(ctx->n_bubbles, 1));
+            std::vector<int2> bk(nb, make_int2(0, 0));
+            std::vector<int32_t> mpos, trav;
+            for (const int4& e : amb) {
+                if (e.z < 0) {
+                    trav.push_back(e.x);
+                    continue;
+                }
+                const int32_t run = e.z > 1 ? int32_t(mpos.size()) : 0;
+                for (int32_t j = 0; j < e.z; ++j) {
+                    const int32_t pos = ctx->h_bpos.at(size_t(e.y + j));
+                    bk[size_t(pos)] = make_int2(e.z, run);
+                    if (e.z > 1) mpos.push_back(pos);
+                }
+            }
+            const int32_t n_trav = int32_t(trav.size());
+            if (mpos.empty()) mpos.push_back(0);
+            if (trav.empty()) trav.push_back(0);
+            HIP_TRY(ctx->rm_bk.upload(bk.data(), bk.size(), s));
+            HIP_TRY(ctx->rm_mpos.upload(mpos.data(), mpos.size(), s));
+            HIP_TRY(ctx->rm_cnt.alloc(mpos.size()));
+            HIP_TRY(hipMemsetAsync(ctx->rm_cnt.ptr, 0, mpos.size() * sizeof(unsigned), s));
+            HIP_TRY(ctx->rm_trav.upload(trav.data(), trav.size(), s));
+            ctx->rm_n_trav = n_trav;
+            HIP_TRY(ctx->rm_bpart.alloc(4 * size_t(std::max(ctx->i_grid, 1))));
+        }
         HIP_TRY(ctx->rm_part.alloc(4 * size_t(wfsa::rmin_blocks(ctx->rm_n_amb))));   // two halves (QN parity)
         HIP_TRY(ctx->rm_rs.alloc(S));
         HIP_TRY(hipMemsetAsync(ctx->rm_rs.ptr, 0, S * sizeof(double), s));   // fused accumulation starts at 0
@@ -2502,9 +2591,11 @@ bool qw_resident(wfsa_dev* ctx) {
     return int64_t(ctx->i_grid) <= int64_t(ctx->n_cu) * ctx->qw_res_per_cu;
 }
 bool qw_usable(wfsa_dev* ctx) {
+    // (the rmin column rides along when the bubbles run in the stream kernel: RminFold)
+    const bool rmin_ok = !ctx->qn_rmin || ctx->n_bubbles == 0 || bubbles_fused(ctx, false);
     return ctx->use_qw && ctx->qw_ok && ctx->qw_waves > 0 && ctx->qn_fused && !ctx->comm && !ctx->dense &&
-           !ctx->mpath && !ctx->qn_rmin && ctx->n_groups > 0 && ctx->delta_on && ctx->i_tables >= 1 &&
-           ctx->n_fall[0] + ctx->n_fall[1] + ctx->n_fall[2] == 0 && ctx->fixed_t_on && ctx->qn_k > 0 &&
+           !ctx->mpath && rmin_ok && ctx->n_groups > 0 && ctx->delta_on && ctx->i_tables >= 1 &&
+           ctx->fixed_t_on && ctx->qn_k > 0 &&
            ctx->i_block / kWave >= 3 && qw_resident(ctx);
 }
 
@@ -2598,6 +2689,7 @@ int enqueue_qn_step(wfsa_dev* ctx, double eta, double tol, int64_t e, bool timed
         w.cptr = ctx->qn_cptr.ptr;
         w.full_of = ctx->qn_full_of.ptr;
         w.fixed_t = ctx->fixed_t.ptr;
+        w.out = has_traversal(ctx) ? ctx->out.ptr : nullptr;   // (their gradient, before this launch)
         w.contrib = ctx->n_bubbles > 0 ? ctx->contrib.ptr : nullptr;
         w.x = ctx->qn_x.ptr;
         w.lambda = ctx->qn_lambda.ptr;
@@ -2612,6 +2704,11 @@ int enqueue_qn_step(wfsa_dev* ctx, double eta, double tol, int64_t e, bool timed
         w.done = ctx->qw_done.ptr;   // (every launch zeroes the other parity's counter)
         w.poll_limit = ctx->qw_poll_limit;
         w.poll_fault = ctx->qw_poll_fault ? 1 : 0;
+        if (ctx->qn_rmin) {   // the rmin column folded into the launch: its block minima for the finish
+            ctx->rm_bpart_cur = ctx->rm_bpart.ptr + size_t(par) * 2 * size_t(ctx->i_grid);
+            f.rmin_part = ctx->rm_bpart_cur;
+            f.rmin_n_part = ctx->i_grid;
+        }
         w.fin = f;
         // the Run's last launch finishes its own step (its stream kernel's
         // blocks' ll partials), so its row needs no finish kernel of its own
@@ -2624,25 +2721,28 @@ int enqueue_qn_step(wfsa_dev* ctx, double eta, double tol, int64_t e, bool timed
             w.fin.ll_part = ctx->ll_cur;
             // the stream kernel's blocks, then (bubbles not fused: the bubble
             // kernel ran first) the bubble kernel's waves -- enqueue_evaluation's order
-            w.fin.n_ll = ctx->i_grid + ((ctx->n_bubbles > 0 && !bubbles_fused(ctx, false)) ? ctx->b_waves : 0);
+            w.fin.n_ll = ctx->i_grid + ((ctx->n_bubbles > 0 && !bubbles_fused(ctx, false)) ? ctx->b_waves : 0) +
+                         trav_ll_waves(ctx);
         }
         ++ctx->qw_seq;
     }
     ctx->rm_eval = fuse_rmin;
     const int erc = enqueue_evaluation(ctx, false, ctx->qn_halted.ptr, timed ? slot : -1, !fused && trellis, &n_ll);
     ctx->rm_eval = false;
+    ctx->rm_bpart_cur = nullptr;
     if (erc) return erc;
     if (ctx->qw_next.on) return fail(WFSA_ERR_HIP, "the in-kernel QN update was not launched");
     if (fused) f.n_ll = n_ll;
     if (inkern && self_fin) {   // the step published its own row: no finish pending
-        const int32_t want = ctx->i_grid + ((ctx->n_bubbles > 0 && !bubbles_fused(ctx, false)) ? ctx->b_waves : 0);
+        const int32_t want = ctx->i_grid + ((ctx->n_bubbles > 0 && !bubbles_fused(ctx, false)) ? ctx->b_waves : 0) +
+                             trav_ll_waves(ctx);
         if (n_ll != want) return fail(WFSA_ERR_HIP, "self-finish: %d log-likelihood partials, not %d", n_ll, want);
         ctx->fin_pending = false;
         ctx->fin_next.active = 0;
         return WFSA_OK;
     }
     if (ctx->comm) COMM_TRY(ctx, ctx->out.ptr, size_t(np) + 1, wfsa::RedOp::SumF64, s);
-    if (ctx->qn_rmin) {
+    if (ctx->qn_rmin && !inkern) {
         constexpr bool fold_rmin = true;   // the strings pass in the QN step kernel's blocks (one launch fewer)
         double* res = ctx->rm_res.ptr + 2 * par;
         if (ctx->mpath || (ctx->dense && !ctx->comm)) {
