@@ -39,6 +39,7 @@
 #include <cmath>
 #include <cstdlib>
 
+
 namespace wfsa {
 
 namespace {
@@ -2153,17 +2154,93 @@ __device__ __forceinline__ double group_sum(double v, int k, int kmax) {
         asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");     \
         if (lane_id() == 0) tr[k] = __builtin_amdgcn_s_memrealtime();    \
     }
-// zo, so (optional): the bubble's Z and its string (the folded rmin column
-// runs its (min, x) pass later, small_bubble_min)
-template <int N, int RE, bool RMIN = false>
+// The rmin column's (min, x) forward over a small bubble's edges (weights
+// ew, nodes sd, header h), log(min path / Z).  The node vector is indexed
+// register-direct: by the wave's shared structure (uni), else by a
+// waterfall over the wave's bubble shapes (sorted by shape: few) -- the
+// first pending lane's structure, read into scalars, runs for every lane and
+// the lanes of that shape keep the result (per-lane node indices put the
+// vector in scratch memory).  min(a, b) x w = min(a x w, b x w) exactly, so
+// any topological order gives the same bits.
+template <int N, int RE>
+__device__ __forceinline__ double min_path_log(const double (&ew)[RE], const int (&sd)[RE], int h, bool uni, double Z) {
+    double rv = 0.0;
+    bool pending = true;
+    while (true) {
+        const unsigned long long m = __ballot(pending);
+        if (m == 0ull) break;
+        const int lead = uni ? 0 : __ffsll(m) - 1;
+        const int hu = __builtin_amdgcn_readlane(h, lead);
+        bool mine = pending && (uni || h == hu);
+        int su[RE];
+#pragma unroll
+        for (int e = 0; e < RE; ++e) {
+            su[e] = __builtin_amdgcn_readlane(sd[e], lead);
+            mine = mine && (uni || sd[e] == su[e]);
+        }
+        const int eu = hu >> 16, nu = hu & 0xffff;
+        double B[N];
+#pragma unroll
+        for (int k = 0; k < N; ++k) B[k] = k == 0 ? 1.0 : INFINITY;
+#pragma unroll
+        for (int e = 0; e < RE; ++e)
+            if (e < eu) {
+                const double v = B[su[e] & 0xffff] * ew[e];
+                B[su[e] >> 16] = ew[e] > 0.0 ? fmin(B[su[e] >> 16], v) : B[su[e] >> 16];
+            }
+        if (mine) {
+            rv = log(B[nu - 1] / Z);
+            pending = false;
+        }
+    }
+    return rv;
+}
+
+// The folded rmin column's (min, x) pass over small bubble b (the class's
+// table and size, as small_bubble) at the wave's end -- off the bubbles'
+// and the QN update's paths, in the idle time of the kernel's tail: the
+// header and edge quads and the weights again (L2 hits), then min_path_log
+// with the sum forward's Z (kept from small_bubble): the separate pass's
+// arithmetic, the same bits
+template <int N, int RE>
+__device__ __forceinline__ double small_bubble_min(const BubbleArgs& a, const int4* __restrict__ tbl, int n, int b,
+                                                   double Z) {
+    constexpr int NQ = 1 + RE / 2;   // (the header and the edges; not the slots)
+    int4 q[NQ];
+#pragma unroll
+    for (int k = 0; k < NQ; ++k) q[k] = tbl[size_t(k) * size_t(n) + size_t(b)];
+    int code[RE], sd[RE];
+#pragma unroll
+    for (int k = 0; k < RE / 2; ++k) {
+        code[2 * k] = q[1 + k].x;
+        sd[2 * k] = q[1 + k].y;
+        code[2 * k + 1] = q[1 + k].z;
+        sd[2 * k + 1] = q[1 + k].w;
+    }
+    double ew[RE];
+#pragma unroll
+    for (int e = 0; e < RE; ++e) ew[e] = a.ewp[code[e]];
+    bool same = q[0].x == __builtin_amdgcn_readfirstlane(q[0].x);
+#pragma unroll
+    for (int e = 0; e < RE; ++e) same = same && sd[e] == __builtin_amdgcn_readfirstlane(sd[e]);
+    return min_path_log<N, RE>(ew, sd, q[0].x, WFSA_UNI_BUBBLES && __all(same), Z);
+}
+
+// rl (RMIN, optional): the folded rmin column's record of the bubble
+// (RminLane: the bubble's value, its string and the string's bubble count
+// and run; FOLD: the (min, x) pass after the backward -- VALU work beside the
+// slot stores' latency -- and a multi-bubble string's value stored for its
+// last arrival, settled at the wave's end)
+template <int N, int RE, bool RMIN = false, bool FOLD = false>
 __device__ __forceinline__ double small_bubble(const BubbleArgs& a, const int4* __restrict__ tbl, int n, int b,
-                                               int pos, unsigned long long* tr = nullptr, double* zo = nullptr,
-                                               int* so = nullptr) {
+                                               int pos, unsigned long long* tr = nullptr, const RminFold* rf = nullptr,
+                                               RminLane* rl = nullptr) {
 #pragma clang fp contract(off)   // (both forms below: the same bits)
     constexpr int NQ = 1 + RE / 2 + RE / 4;
     int4 q[NQ];
 #pragma unroll
     for (int k = 0; k < NQ; ++k) q[k] = tbl[size_t(k) * size_t(n) + size_t(b)];
+    const int2 bk = rf ? rf->bk[pos] : make_int2(0, 0);   // (in flight with the quads)
     WFSA_BSTAMP(8)
     const int nodes = q[0].x & 0xffff, edges = q[0].x >> 16;
     const double p = __longlong_as_double((long long)(uint32_t(q[0].z)) | ((long long)(uint32_t(q[0].w)) << 32));
@@ -2216,47 +2293,18 @@ __device__ __forceinline__ double small_bubble(const BubbleArgs& a, const int4* 
     }
     const double Z = uni ? A[__builtin_amdgcn_readfirstlane(nodes) - 1] : reg_get(A, nodes - 1);
     const double scale = -p / Z;
-    if (zo) {
-        *zo = Z;
-        *so = q[0].y;
-    }
+
     WFSA_BSTAMP(10)
-    if (RMIN && a.rmin_acc) {   // (min, x) forward for the rmin column in B's registers (re-zeroed
-                                // for the backward); the min path never exceeds Z
-#pragma unroll
-        for (int k = 0; k < N; ++k) B[k] = k == 0 ? 1.0 : INFINITY;
-        double rv;
-        if (uni) {   // (the wave's shared structure: register-direct node indices, as the sum forward)
-            const int eu = __builtin_amdgcn_readfirstlane(edges);
-#pragma unroll
-            for (int e = 0; e < RE; ++e)
-                if (e < eu) {
-                    const int s = __builtin_amdgcn_readfirstlane(sd[e]);
-                    const double v = B[s & 0xffff] * ew[e];
-                    B[s >> 16] = ew[e] > 0.0 ? fmin(B[s >> 16], v) : B[s >> 16];
-                }
-            rv = log(B[__builtin_amdgcn_readfirstlane(nodes) - 1] / Z);
-        } else {
-#pragma unroll
-            for (int e = 0; e < RE; ++e)
-                if (e < edges && ew[e] > 0.0) {
-                    const int dst = sd[e] >> 16;
-                    const double v = reg_get(B, sd[e] & 0xffff) * ew[e];
-#pragma unroll
-                    for (int k = 0; k < N; ++k) B[k] = dst == k ? fmin(B[k], v) : B[k];
-                }
-            rv = log(reg_get(B, nodes - 1) / Z);
-        }
+    auto rmin_pass = [&]() {   // (the min path never exceeds Z)
+        const double rv = min_path_log<N, RE>(ew, sd, q[0].x, uni, Z);
         if (a.rmin_sv) {
-            if (a.wt) store_wt(&a.rmin_sv[pos], rv);   // (read in this launch: the folded rmin column)
+            if (a.wt) store_wt(&a.rmin_sv[pos], rv);
             else a.rmin_sv[pos] = rv;
         } else {
             global_add(&a.rmin_acc[q[0].y], rv);
         }
-
-#pragma unroll
-        for (int k = 0; k < N; ++k) B[k] = 0.0;
-    }
+    };
+    if (RMIN && !FOLD && a.rmin_acc) rmin_pass();
     if (uni) B[__builtin_amdgcn_readfirstlane(nodes) - 1] = 0.0 + 1.0;
     else reg_add(B, nodes - 1, 1.0);
     // lanes of an aligned 2^k group sharing edge e's parameter (slot field
@@ -2301,6 +2349,14 @@ __device__ __forceinline__ double small_bubble(const BubbleArgs& a, const int4* 
     WFSA_BSTAMP(11)
     const double lz = log(Z);
     if (a.logq) global_add(&a.logq[q[0].y], lz);
+    if (FOLD) {
+        const double rv = min_path_log<N, RE>(ew, sd, q[0].x, uni, Z);
+        rl->rv = rv;
+        rl->str = q[0].y;
+        rl->k = bk.x;
+        rl->run = bk.y;
+        if (bk.x > 1) store_wt(&a.rmin_sv[pos], rv);   // (retired by the wave's arrival)
+    }
     return p * lz;
 }
 #undef WFSA_BSTAMP
@@ -2309,67 +2365,6 @@ __device__ __forceinline__ double small_bubble(const BubbleArgs& a, const int4* 
 // weight) in LDS in parallel, lane 0 runs the two sweeps over the staged
 // edges, and the lanes write the contributions (an edge may have several
 // parameters, hence several slots).
-// The folded rmin column's (min, x) pass over small bubble b (the class's
-// table and size, as small_bubble), after the wave's arrival -- off the QN
-// update's path: the quads and weights again (L2 hits), the min forward, and
-// log(min path / Z) with the sum forward's Z (kept from small_bubble); the
-// same arithmetic as small_bubble's RMIN pass, so the same bits
-template <int N, int RE>
-__device__ __forceinline__ double small_bubble_min(const BubbleArgs& a, const int4* __restrict__ tbl, int n, int b,
-                                                   double Z) {
-#pragma clang fp contract(off)
-    constexpr int NQ = 1 + RE / 2;   // (the header and the edges; not the slots)
-    int4 q[NQ];
-#pragma unroll
-    for (int k = 0; k < NQ; ++k) q[k] = tbl[size_t(k) * size_t(n) + size_t(b)];
-    int code[RE], sd[RE];
-#pragma unroll
-    for (int k = 0; k < RE / 2; ++k) {
-        code[2 * k] = q[1 + k].x;
-        sd[2 * k] = q[1 + k].y;
-        code[2 * k + 1] = q[1 + k].z;
-        sd[2 * k + 1] = q[1 + k].w;
-    }
-    double ew[RE];
-#pragma unroll
-    for (int e = 0; e < RE; ++e) ew[e] = a.ewp[code[e]];
-    // a waterfall over the wave's bubble shapes (sorted by shape: mostly
-    // one): the first pending lane's structure, read into scalars, runs with
-    // register-direct node indices for every lane; the lanes of that shape
-    // keep their result.  (Per-lane node indices put the node vector in
-    // scratch memory.)
-    double rv = 0.0;
-    bool pending = true;
-    while (true) {
-        const unsigned long long m = __ballot(pending);
-        if (m == 0ull) break;
-        const int lead = __ffsll(m) - 1;
-        const int hu = __builtin_amdgcn_readlane(q[0].x, lead);
-        bool mine = pending && q[0].x == hu;
-        int su[RE];
-#pragma unroll
-        for (int e = 0; e < RE; ++e) {
-            su[e] = __builtin_amdgcn_readlane(sd[e], lead);
-            mine = mine && sd[e] == su[e];
-        }
-        const int eu = hu >> 16, nu = hu & 0xffff;
-        double B[N];
-#pragma unroll
-        for (int k = 0; k < N; ++k) B[k] = k == 0 ? 1.0 : INFINITY;
-#pragma unroll
-        for (int e = 0; e < RE; ++e)
-            if (e < eu) {
-                const double v = B[su[e] & 0xffff] * ew[e];
-                B[su[e] >> 16] = ew[e] > 0.0 ? fmin(B[su[e] >> 16], v) : B[su[e] >> 16];
-            }
-        if (mine) {
-            rv = log(B[nu - 1] / Z);
-            pending = false;
-        }
-    }
-    return rv;
-}
-
 // The folded rmin column (RminFold): the candidate of the bubble at position
 // pos (value rv, string str) -- a one-bubble string's at once; a k-bubble
 // string's value stored write-through, then (the store retired) the
@@ -2400,11 +2395,29 @@ __device__ __forceinline__ void rmin_settle(const RminFold& rf, double* sv, int 
     }
 }
 
+// A multi-bubble string's arrival (its value stored write-through and
+// retired): the k-th arrival sums the k values in bubble order
+__device__ __forceinline__ void rmin_arrive(const RminFold& rf, const double* sv, const RminLane& l, double& cv,
+                                            double& ci) {
+    const unsigned old = __hip_atomic_fetch_add(rf.cnt + l.run, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (old == unsigned(l.k - 1)) {   // the string's last bubble: every value is stored
+        rf.cnt[l.run] = 0u;            // (for the next launch)
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");   // (a compiler barrier)
+        double r = 0.0;
+        for (int j = 0; j < l.k; ++j) r += load_wt(sv + rf.mpos[l.run + j]);
+        if (r < cv || (r == cv && double(l.str) < ci)) {
+            cv = r;
+            ci = double(l.str);
+        }
+    }
+}
+
 // rf (the folded rmin column, or null): lane 0 settles the bubble's string
 // at once -- rare bubbles: its store retired, its string's arrival, the sum
 // by the k-th arrival -- and min-folds the candidate into (cv, ci)
 __device__ __forceinline__ double big_bubble(const BubbleArgs& a, int i, int* lsd, double* lw, double* lv, double* AB,
-                             const RminFold* rf = nullptr, double* cv = nullptr, double* ci = nullptr) {
+                             const RminFold* rf = nullptr, double* cv = nullptr, double* ci = nullptr,
+                             RminLane* pend = nullptr) {
     const int lane = lane_id();
     const int off = a.big_off[i];
     const int32_t* rec = a.bub + off;
@@ -2449,7 +2462,16 @@ __device__ __forceinline__ double big_bubble(const BubbleArgs& a, int i, int* ls
             } else {
                 global_add(&a.rmin_acc[rec[1]], rv);
             }
-            if (rf) rmin_settle(*rf, a.rmin_sv, pos, rv, rec[1], *cv, *ci);
+            if (rf) {   // a one-bubble string's candidate now; a multi-bubble string's arrival at the
+                        // wave's end (pend), or now when pend holds one already (a second big bubble)
+                const int2 bk = rf->bk[pos];
+                if (bk.x > 1 && pend->k == 0) {
+                    store_wt(a.rmin_sv + pos, rv);
+                    *pend = RminLane{rv, rec[1], bk.x, bk.y};
+                } else {
+                    rmin_settle(*rf, a.rmin_sv, pos, rv, rec[1], *cv, *ci);
+                }
+            }
             for (int v = 0; v < nodes; ++v) B[v] = 0.0;
         }
         B[nodes - 1] = 1.0;
@@ -2947,8 +2969,10 @@ __global__ __launch_bounds__(1024, (DBG == 10 ? 8 : 1)) WFSA_FBS_ATTR void fbs_k
     // the folded rmin column (RMIN && QN, RminFold): the lane's small bubble
     // (position, value, string) until its wave arrived, and the lane's candidate
     constexpr bool RF = RMIN && QN;
-    int rm_pos = -1, rm_str = -1;
-    double rm_z = 1.0, rm_cv = INFINITY, rm_ci = -1.0;
+    RminLane rm_lane{0.0, -1, 0, 0};   // the lane's small bubble
+    RminLane rm_big{0.0, -1, 0, 0};    // lane 0: a big bubble of a multi-bubble string, pending
+    int rm_pos = -1;
+    double rm_cv = INFINITY, rm_ci = -1.0;
     const bool small_wave = a.bub_on && DBG != 8 && DBG != 10 && DBG != 13 && !fin_wave && w < a.bub.small_wpb;
     auto small_bubbles = [&]() {   // one per lane, from the first small_wpb waves of every block (spread over all CUs)
         stored = true;
@@ -2963,16 +2987,18 @@ __global__ __launch_bounds__(1024, (DBG == 10 ? 8 : 1)) WFSA_FBS_ATTR void fbs_k
         // (the bubbles are on the QN update's critical path; the stream waves
         // beside them mostly wait for memory: the bubble waves issue first)
         __builtin_amdgcn_s_setprio(2);
-        // (RF: the bubbles' (min, x) pass after the arrival, small_bubble_min)
-        constexpr bool BR = RMIN && !RF;
-        double* zo = RF ? &rm_z : nullptr;
-        int* so = RF ? &rm_str : nullptr;
         const BubbleArgs bub = WFSA_LATE_ARG(bub);
+        const RminFold rf = WFSA_LATE_ARG(rf);
+        const RminFold* rfp = RF ? &rf : nullptr;
+        RminLane* rlp = RF ? &rm_lane : nullptr;
         if (b >= 0 && b < bub.n_small4)
-            ll_acc += small_bubble<4, 4, BR>(bub, bub.sm4_tbl, bub.n_small4, b, b, btr, zo, so);
+            ll_acc += small_bubble<4, 4, RMIN, RF>(bub, bub.sm4_tbl, bub.n_small4, b, b, btr, rfp, rlp);
         else if (b >= bub.n_small4)
-            ll_acc += small_bubble<8, 8, BR>(bub, bub.sm_tbl, bub.n_small, b - bub.n_small4, b, btr, zo, so);
-        if (RF && b >= 0) rm_pos = int(b);
+            ll_acc += small_bubble<8, 8, RMIN, RF>(bub, bub.sm_tbl, bub.n_small, b - bub.n_small4, b, btr, rfp, rlp);
+        if (RF && b >= 0) {
+            rm_pos = int(b);
+            if (rm_lane.k == 1) min_pair(rm_cv, rm_ci, rm_lane.rv, double(rm_lane.str));
+        }
         __builtin_amdgcn_s_setprio(0);
     };
     // big bubbles, one wavefront each, from the last blocks' last waves down
@@ -2989,7 +3015,7 @@ __global__ __launch_bounds__(1024, (DBG == 10 ? 8 : 1)) WFSA_FBS_ATTR void fbs_k
             const BubbleArgs bub = WFSA_LATE_ARG(bub);
             const RminFold rf = WFSA_LATE_ARG(rf);
             for (int i = r; i < bub.n_big; i += nw - 1)
-                ll_acc += big_bubble(bub, i, lsd, lw, lw, lw + E, RF ? &rf : nullptr, &rm_cv, &rm_ci);
+                ll_acc += big_bubble(bub, i, lsd, lw, lw, lw + E, RF ? &rf : nullptr, &rm_cv, &rm_ci, &rm_big);
         }
     };
     if (!DELTA && W_LDS && DBG != 4 && !a.no_streams) {
@@ -3041,16 +3067,6 @@ __global__ __launch_bounds__(1024, (DBG == 10 ? 8 : 1)) WFSA_FBS_ATTR void fbs_k
         if (lane == 0 && prev == unsigned(wpb - 1))   // the block's last wave: one arrival for all its stores
             __hip_atomic_fetch_add(a.qw.arrive + a.qw.parity, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         WFSA_STAMP(3)
-        // the lane's small bubble's rmin candidate, off the QN update's path
-        // (after the block's arrival, before this wave's stream pass)
-        if (RF && rm_pos >= 0) {
-            const BubbleArgs bub = WFSA_LATE_ARG(bub);
-            const RminFold rf = WFSA_LATE_ARG(rf);
-            const double rv = rm_pos < bub.n_small4
-                                  ? small_bubble_min<4, 4>(bub, bub.sm4_tbl, bub.n_small4, rm_pos, rm_z)
-                                  : small_bubble_min<8, 8>(bub, bub.sm_tbl, bub.n_small, rm_pos - bub.n_small4, rm_z);
-            rmin_settle(rf, bub.rmin_sv, rm_pos, rv, rm_str, rm_cv, rm_ci);
-        }
     }
     if (kStreams) load(B, D);
     double p = 0.0, acc0 = 0.0, acc1 = 0.0;
@@ -3175,6 +3191,15 @@ __global__ __launch_bounds__(1024, (DBG == 10 ? 8 : 1)) WFSA_FBS_ATTR void fbs_k
     }
     flush();
     WFSA_STAMP(4)
+    // the folded rmin column: a multi-bubble string's arrival, the k-th one
+    // summing the string's stored values (retired at this wave's arrival) --
+    // at the wave's end, off the stream pass and the QN update
+    if (RF && ((rm_pos >= 0 && rm_lane.k > 1) || rm_big.k > 1)) {   // (their values stored: retired by now)
+        const RminFold rf = WFSA_LATE_ARG(rf);
+        const double* sv = WFSA_LATE_ARG(bub.rmin_sv);
+        if (rm_pos >= 0 && rm_lane.k > 1) rmin_arrive(rf, sv, rm_lane, rm_cv, rm_ci);
+        if (rm_big.k > 1) rmin_arrive(rf, sv, rm_big, rm_cv, rm_ci);
+    }
     // one log-likelihood partial per block (the QN finish sums them)
     __shared__ double wsum[1024 / kWave];
     __shared__ double wrv[1024 / kWave], wri[1024 / kWave];   // (RF: the waves' rmin candidates)

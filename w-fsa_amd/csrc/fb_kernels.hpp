@@ -484,6 +484,9 @@ struct QnFinish {
     int32_t k;
     double plogp, tol;
     int32_t ring_slot;           // ring slot of the step
+    uint32_t tag;                // the row's sequence number as the host expects it: written into the row
+                                 // with the status (row[7] = status + 16 tag), so a reader that sees the
+                                 // flag before the row's data waits for the row itself
     const unsigned* halted;      // [0] halted, [1] halt_pending (the finish writes [1]),
                                  // [2] an in-kernel QN wave's wait timed out (sc1)
     unsigned* halt_pending;
@@ -667,6 +670,13 @@ struct RminFold {
     int32_t n_trav;
     const double* rmin_log;  // [S] their values
     double* part;            // [blocks][2] this launch's block minima (log rmin, string index)
+};
+
+// a lane's small bubble in the folded column: its value and string, and its
+// string's bubble count and run (RminFold::bk) for the wave's end
+struct RminLane {
+    double rv;
+    int32_t str, k, run;
 };
 
 struct CompiledArgs {

@@ -144,7 +144,11 @@ __device__ __forceinline__ void store_wt(unsigned* p, unsigned v) {
 __device__ inline void qn_publish_row(const QnFinish& f, const double* info, unsigned status) {
     double* row = f.host_ring + size_t(f.ring_slot) * kQnRow;
     for (int i = 0; i < 7; ++i) row[i] = info ? info[i] : 0.0;
-    row[7] = double(status);
+    // the status and tag word last, released after the data: a reader that
+    // sees the tag sees the row
+    const double tw = double(status) + 16.0 * double(f.tag);
+    __hip_atomic_store(reinterpret_cast<unsigned long long*>(row + 7), (unsigned long long)(__double_as_longlong(tw)),
+                       __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
     const unsigned v = __hip_atomic_fetch_add(f.seq, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u;
     __hip_atomic_store(f.host_flag, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
@@ -267,14 +271,21 @@ __device__ inline void qn_finish_compute(const QnFinish& f, double* red, double*
     }
     ll = wave_reduce(ll, 2);
     double rv = INFINITY, ri = -1.0;   // rmin column from block minima, ties to the lower string
-    if (f.rmin_part)
-        for (int j = t; j < f.rmin_n_part; j += nt) {
-            const double v = WT ? load_wt(f.rmin_part + 2 * j) : f.rmin_part[2 * j];
-            const double i = WT ? load_wt(f.rmin_part + 2 * j + 1) : f.rmin_part[2 * j + 1];
-            if (v < rv || (v == rv && i < ri)) {
-                rv = v;
-                ri = i;
+    if (f.rmin_part)   // (eight pairs' loads in flight per thread: the folded column has a pair per block)
+        for (int j0 = t; j0 < f.rmin_n_part; j0 += 8 * nt) {
+            double v[8], i[8];
+#pragma unroll
+            for (int b = 0; b < 8; ++b) {
+                const int j = min(j0 + b * nt, f.rmin_n_part - 1);
+                v[b] = WT ? load_wt(f.rmin_part + 2 * j) : f.rmin_part[2 * j];
+                i[b] = WT ? load_wt(f.rmin_part + 2 * j + 1) : f.rmin_part[2 * j + 1];
             }
+#pragma unroll
+            for (int b = 0; b < 8; ++b)
+                if (v[b] < rv || (v[b] == rv && i[b] < ri)) {
+                    rv = v[b];
+                    ri = i[b];
+                }
         }
     if (WAVE) {
         gmin = wave_reduce(gmin, 0);

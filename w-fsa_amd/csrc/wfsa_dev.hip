@@ -1026,6 +1026,27 @@ int wait_published(wfsa_dev* ctx, unsigned want) {
     }
 }
 
+// Until ring row `row` holds the row with sequence number `want` (row[7] =
+// status + 16 tag, qn_publish_row): the flag said it was published.
+int wait_row(wfsa_dev* ctx, const double* row, unsigned want) {
+    auto tag = [&] {
+        const uint64_t bits = __atomic_load_n(reinterpret_cast<const uint64_t*>(row + 7), __ATOMIC_ACQUIRE);
+        double v;
+        std::memcpy(&v, &bits, sizeof v);
+        return unsigned(uint64_t(v) >> 4);
+    };
+    for (uint64_t spin = 1; tag() != want; ++spin) {
+        if ((spin & 0x3fff) == 0) {
+            const hipError_t e = hipStreamQuery(ctx->stream);
+            if (e == hipSuccess && tag() != want)
+                return fail(WFSA_ERR_HIP, "device finished without writing info row %u (found %u)", want, tag());
+            if (e != hipSuccess && e != hipErrorNotReady) return fail(WFSA_ERR_HIP, "device failure: %s", hipGetErrorString(e));
+        }
+        __builtin_ia32_pause();
+    }
+    return WFSA_OK;
+}
+
 // Contribution slots of the compiled bubbles in slot order pos_of (full
 // parameter j at position pos_of[j]): every (bubble edge, parameter) pair
 // gets a slot, parameter-major by position -- within a parameter small
@@ -2667,6 +2688,7 @@ int enqueue_qn_step(wfsa_dev* ctx, double eta, double tol, int64_t e, bool timed
     f.plogp = ctx->qn_plogp;
     f.tol = tol;
     f.ring_slot = slot;
+    f.tag = ctx->seq + 1u;   // (qn_run increments ctx->seq once per enqueued step)
     f.halted = ctx->qn_halted.ptr;
     f.halt_pending = ctx->qn_halted.ptr + 1;
     f.seq = ctx->counters.ptr;
@@ -3546,7 +3568,11 @@ static int qn_run_impl(wfsa_dev* ctx, double eta, double tol, int32_t max_steps,
         if (trace) (done == 0 ? tr_first : tr_last) = clk::now();
         const int slot = done % kQnDepth;
         const double* row = ctx->qn_ring + size_t(slot) * wfsa::kQnRow;
-        const unsigned rs = unsigned(row[7]);
+        // the row itself carries its sequence number: the flag may become
+        // visible before the row's data does (and two rows published by one
+        // launch may take their sequence numbers in either order)
+        if (int rc = wait_row(ctx, row, base + unsigned(done) + 1u)) return rc;
+        const unsigned rs = unsigned(uint64_t(row[7]) & 15u);
         if (ctx->kernel_timing && timed_step(done)) {
             float c = 0.f, f = 0.f;
             const hipEvent_t end = ctx->k2_kc[slot] ? ctx->kc[slot] : ctx->k2[slot];
