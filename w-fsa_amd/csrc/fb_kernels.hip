@@ -2196,36 +2196,6 @@ __device__ __forceinline__ double min_path_log(const double (&ew)[RE], const int
     return rv;
 }
 
-// The folded rmin column's (min, x) pass over small bubble b (the class's
-// table and size, as small_bubble) at the wave's end -- off the bubbles'
-// and the QN update's paths, in the idle time of the kernel's tail: the
-// header and edge quads and the weights again (L2 hits), then min_path_log
-// with the sum forward's Z (kept from small_bubble): the separate pass's
-// arithmetic, the same bits
-template <int N, int RE>
-__device__ __forceinline__ double small_bubble_min(const BubbleArgs& a, const int4* __restrict__ tbl, int n, int b,
-                                                   double Z) {
-    constexpr int NQ = 1 + RE / 2;   // (the header and the edges; not the slots)
-    int4 q[NQ];
-#pragma unroll
-    for (int k = 0; k < NQ; ++k) q[k] = tbl[size_t(k) * size_t(n) + size_t(b)];
-    int code[RE], sd[RE];
-#pragma unroll
-    for (int k = 0; k < RE / 2; ++k) {
-        code[2 * k] = q[1 + k].x;
-        sd[2 * k] = q[1 + k].y;
-        code[2 * k + 1] = q[1 + k].z;
-        sd[2 * k + 1] = q[1 + k].w;
-    }
-    double ew[RE];
-#pragma unroll
-    for (int e = 0; e < RE; ++e) ew[e] = a.ewp[code[e]];
-    bool same = q[0].x == __builtin_amdgcn_readfirstlane(q[0].x);
-#pragma unroll
-    for (int e = 0; e < RE; ++e) same = same && sd[e] == __builtin_amdgcn_readfirstlane(sd[e]);
-    return min_path_log<N, RE>(ew, sd, q[0].x, WFSA_UNI_BUBBLES && __all(same), Z);
-}
-
 // rl (RMIN, optional): the folded rmin column's record of the bubble
 // (RminLane: the bubble's value, its string and the string's bubble count
 // and run; FOLD: the (min, x) pass after the backward -- VALU work beside the
@@ -2395,6 +2365,42 @@ __device__ __forceinline__ void rmin_settle(const RminFold& rf, double* sv, int 
     }
 }
 
+// The folded column's (min, x) pass over big bubble i at the wave's end (a
+// wave-wide call; Z from the sum forward): the edges staged again -- the
+// backward overwrote the weights with contributions -- and lane 0's serial
+// sweep, as big_bubble's (the same bits); lane 0 settles the candidate
+__device__ __forceinline__ void big_bubble_min(const BubbleArgs& a, const RminFold& rf, int i, double Z, int* lsd,
+                                               double* lw, double* AB, double& cv, double& ci) {
+    const int lane = lane_id();
+    const int32_t* rec = a.bub + a.big_off[i];
+    const int hdr = rec[0];
+    const int nodes = hdr & 0xffff, edges = hdr >> 16;
+    for (int e = lane; e < edges; e += kWave) {
+        const int code = rec[4 + 2 * e];
+        lsd[e] = rec[5 + 2 * e];
+        double wgt;
+        if (code >= 0) {
+            wgt = a.ewp[code];
+        } else {
+            const int g = -code - 2;
+            double s = 0.0;
+            for (int q = a.m.pptr[g]; q < a.m.pptr[g + 1]; ++q) s += a.w[a.m.pidx[q]];
+            wgt = exp(s);
+        }
+        lw[e] = wgt;
+    }
+    wave_sync();
+    if (lane == 0) {
+        double* B = AB + kMaxBubbleNodes;
+        for (int v = 0; v < nodes; ++v) B[v] = v == 0 ? 1.0 : INFINITY;
+        for (int e = 0; e < edges; ++e)
+            if (lw[e] > 0.0) B[lsd[e] >> 16] = fmin(B[lsd[e] >> 16], B[lsd[e] & 0xffff] * lw[e]);
+        const double rv = log(B[nodes - 1] / Z);
+        rmin_settle(rf, a.rmin_sv, a.n_small4 + a.n_small + i, rv, rec[1], cv, ci);
+    }
+    wave_sync();
+}
+
 // A multi-bubble string's arrival (its value stored write-through and
 // retired): the k-th arrival sums the k values in bubble order
 __device__ __forceinline__ void rmin_arrive(const RminFold& rf, const double* sv, const RminLane& l, double& cv,
@@ -2450,7 +2456,12 @@ __device__ __forceinline__ double big_bubble(const BubbleArgs& a, int i, int* ls
         for (int e = 0; e < edges; ++e) A[lsd[e] >> 16] += A[lsd[e] & 0xffff] * lw[e];
         const double Z = A[nodes - 1];
         const double scale = -p / Z;
-        if (a.rmin_acc) {   // (min, x) forward in B's storage, then B is re-zeroed
+        // the folded column: this bubble's (min, x) pass at the wave's end,
+        // off the path to the QN update (big_bubble_min) -- unless the wave
+        // holds another already (a second big bubble: here, as before)
+        const bool defer = rf && pend->big < 0;
+        if (defer) *pend = RminLane{Z, rec[1], 0, 0, i};
+        if (a.rmin_acc && !defer) {   // (min, x) forward in B's storage, then B is re-zeroed
             for (int v = 0; v < nodes; ++v) B[v] = v == 0 ? 1.0 : INFINITY;
             for (int e = 0; e < edges; ++e)
                 if (lw[e] > 0.0) B[lsd[e] >> 16] = fmin(B[lsd[e] >> 16], B[lsd[e] & 0xffff] * lw[e]);
@@ -2462,16 +2473,7 @@ __device__ __forceinline__ double big_bubble(const BubbleArgs& a, int i, int* ls
             } else {
                 global_add(&a.rmin_acc[rec[1]], rv);
             }
-            if (rf) {   // a one-bubble string's candidate now; a multi-bubble string's arrival at the
-                        // wave's end (pend), or now when pend holds one already (a second big bubble)
-                const int2 bk = rf->bk[pos];
-                if (bk.x > 1 && pend->k == 0) {
-                    store_wt(a.rmin_sv + pos, rv);
-                    *pend = RminLane{rv, rec[1], bk.x, bk.y};
-                } else {
-                    rmin_settle(*rf, a.rmin_sv, pos, rv, rec[1], *cv, *ci);
-                }
-            }
+            if (rf) rmin_settle(*rf, a.rmin_sv, pos, rv, rec[1], *cv, *ci);
             for (int v = 0; v < nodes; ++v) B[v] = 0.0;
         }
         B[nodes - 1] = 1.0;
@@ -2969,8 +2971,8 @@ __global__ __launch_bounds__(1024, (DBG == 10 ? 8 : 1)) WFSA_FBS_ATTR void fbs_k
     // the folded rmin column (RMIN && QN, RminFold): the lane's small bubble
     // (position, value, string) until its wave arrived, and the lane's candidate
     constexpr bool RF = RMIN && QN;
-    RminLane rm_lane{0.0, -1, 0, 0};   // the lane's small bubble
-    RminLane rm_big{0.0, -1, 0, 0};    // lane 0: a big bubble of a multi-bubble string, pending
+    RminLane rm_lane{0.0, -1, 0, 0, -1};   // the lane's small bubble
+    RminLane rm_big{0.0, -1, 0, 0, -1};    // lane 0: a big bubble whose (min, x) pass is due at the wave's end
     int rm_pos = -1;
     double rm_cv = INFINITY, rm_ci = -1.0;
     const bool small_wave = a.bub_on && DBG != 8 && DBG != 10 && DBG != 13 && !fin_wave && w < a.bub.small_wpb;
@@ -3194,11 +3196,22 @@ __global__ __launch_bounds__(1024, (DBG == 10 ? 8 : 1)) WFSA_FBS_ATTR void fbs_k
     // the folded rmin column: a multi-bubble string's arrival, the k-th one
     // summing the string's stored values (retired at this wave's arrival) --
     // at the wave's end, off the stream pass and the QN update
-    if (RF && ((rm_pos >= 0 && rm_lane.k > 1) || rm_big.k > 1)) {   // (their values stored: retired by now)
+    if (RF && rm_pos >= 0 && rm_lane.k > 1) {   // (its value stored: retired by now)
         const RminFold rf = WFSA_LATE_ARG(rf);
-        const double* sv = WFSA_LATE_ARG(bub.rmin_sv);
-        if (rm_pos >= 0 && rm_lane.k > 1) rmin_arrive(rf, sv, rm_lane, rm_cv, rm_ci);
-        if (rm_big.k > 1) rmin_arrive(rf, sv, rm_big, rm_cv, rm_ci);
+        rmin_arrive(rf, WFSA_LATE_ARG(bub.rmin_sv), rm_lane, rm_cv, rm_ci);
+    }
+    if (RF) {   // a big bubble's (min, x) pass (lane 0 held its index and Z; the staging is this wave's)
+        const int big = __builtin_amdgcn_readfirstlane(rm_big.big);
+        if (big >= 0) {
+            const BubbleArgs bub = WFSA_LATE_ARG(bub);
+            const RminFold rf = WFSA_LATE_ARG(rf);
+            const double z = __shfl(rm_big.rv, 0, kWave);
+            const int E = bub.big_lds_edges;
+            char* stg = reinterpret_cast<char*>(lds) + bub.big_lds_off + w * big_stage_bytes(E);
+            double* lw = reinterpret_cast<double*>(stg);
+            int* lsd = reinterpret_cast<int*>(lw + E + 2 * kMaxBubbleNodes);
+            big_bubble_min(bub, rf, big, z, lsd, lw, lw + E, rm_cv, rm_ci);
+        }
     }
     // one log-likelihood partial per block (the QN finish sums them)
     __shared__ double wsum[1024 / kWave];

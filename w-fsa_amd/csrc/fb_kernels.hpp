@@ -677,6 +677,7 @@ struct RminFold {
 struct RminLane {
     double rv;
     int32_t str, k, run;
+    int32_t big;             // a big bubble's index whose (min, x) pass is still due (rv: its Z), or -1
 };
 
 struct CompiledArgs {
