@@ -23,6 +23,9 @@ from conftest import ROOT
 pytestmark = pytest.mark.gpu
 
 SPEC = dict(n_states=64, degree=8, vocab=16, emissions=1, n_strings=3000, max_len=64, seed=9)
+# a family-A-like corpus large enough per rank that its bubbles ride in the
+# stream kernel -- the in-kernel update's rmin column needs that
+SPEC_A = dict(n_states=256, degree=8, vocab=64, emissions=1, n_strings=60000, max_len=64, seed=9)
 
 
 def _close(a, b, rel, atol=1e-13):
@@ -49,7 +52,7 @@ def _learn(W, fsa, sym, off, wt, setup=None):
     return dict(kl=kl, grad=g, rows=[list(r) for r in rows], x=lrn.x(), info=lrn.info(), stats=lrn.stats())
 
 
-def _worker(rank, world, port, peer, q, late_s=0.0, abort=False):
+def _worker(rank, world, port, peer, q, late_s=0.0, abort=False, spec=None, rmin=True):
     import sys
     sys.path.insert(0, ROOT)
     sys.path.insert(0, os.path.join(ROOT, "w-fsa_amd"))
@@ -61,7 +64,7 @@ def _worker(rank, world, port, peer, q, late_s=0.0, abort=False):
     try:
         os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
         dist.init_process_group("gloo", rank=rank, world_size=world)
-        syn = W.Synthetic(**SPEC)
+        syn = W.Synthetic(**(spec or SPEC))
         sym, off, wt = syn.corpus()
         fsa = W.Fsa.read_text(syn.wfsa_text)
         if abort == "d2h":
@@ -76,7 +79,10 @@ def _worker(rank, world, port, peer, q, late_s=0.0, abort=False):
             res = _late_learn(W, fsa, sym, off, wt, world, rank, late_s)
             q.put((rank, res))
             return
-        res = _learn(W, fsa, sym, off, wt, lambda l: l.SetHostCommunicator(world, rank, W.torch_allreduce))
+        def setup(lrn):
+            lrn.set_info_rmin(rmin)
+            lrn.SetHostCommunicator(world, rank, W.torch_allreduce)
+        res = _learn(W, fsa, sym, off, wt, setup)
         dist.barrier()
         dist.destroy_process_group()
         q.put((rank, res))
@@ -169,11 +175,11 @@ def _d2h_learn(W, fsa, sym, off, wt, world, rank):
         return {"raised": str(e), "s": time.time() - t0}
 
 
-def _one_context():
+def _one_context(spec=None, rmin=True):
     import wfsa_amd as W
-    syn = W.Synthetic(**SPEC)
+    syn = W.Synthetic(**(spec or SPEC))
     sym, off, wt = syn.corpus()
-    return _learn(W, W.Fsa.read_text(syn.wfsa_text), sym, off, wt)
+    return _learn(W, W.Fsa.read_text(syn.wfsa_text), sym, off, wt, lambda l: l.set_info_rmin(rmin))
 
 
 def _compare(res, one):
@@ -186,11 +192,11 @@ def _compare(res, one):
     np.testing.assert_allclose(res["x"], one["x"], rtol=1e-10, atol=1e-12)
 
 
-def _spawn(world, peer, late_s=0.0, abort=False):
+def _spawn(world, peer, late_s=0.0, abort=False, spec=None, rmin=True):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, peer, q, late_s, abort)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, peer, q, late_s, abort, spec, rmin)) for r in range(world)]
     for p in procs:
         p.start()
     got = {}
@@ -209,13 +215,35 @@ def _spawn(world, peer, late_s=0.0, abort=False):
 
 
 @pytest.mark.parametrize("peer", [True, False])
-def test_two_processes_over_gloo_equal_one_context(peer):
+@pytest.mark.parametrize("corpus", ["small", "familyA"])
+def test_two_processes_over_gloo_equal_one_context(peer, corpus):
+    """familyA: VERDICT r5 item 4 -- with the peer path the device QN loop
+    keeps the update in the stream kernel across ranks: each batch's member
+    partials, the log-likelihood and the rmin pair are exchanged through the
+    peer areas inside the launch; the rows (rmin included: value and global
+    string) still equal one context's.  small: the heavily ambiguous corpus
+    whose bubbles do not fit the stream kernel -- the separate kernels"""
     world = 2
-    got = _spawn(world, peer)
-    one = _one_context()
+    spec = SPEC_A if corpus == "familyA" else SPEC
+    got = _spawn(world, peer, spec=spec)
+    one = _one_context(spec)
     for r in range(world):
         assert got[r]["stats"]["comm_ranks"] == world
         assert got[r]["stats"]["comm_peer"] == (1 if peer else 0)
+        assert (got[r]["stats"]["qn_inkernel_waves"] > 0) == (peer and corpus == "familyA"), got[r]["stats"]
+        _compare(got[r], one)
+        for a, b in zip(got[r]["rows"], one["rows"]):   # the rmin column: value and (global) string
+            assert _close(a[5], b[5], rel=1e-10) and a[6] == b[6], (a, b)
+
+
+def test_two_processes_inkernel_without_rmin_equal_one_context():
+    """the in-kernel update across ranks with the rmin column off (the
+    ambiguous corpus: its separate bubble kernel runs before the stream
+    kernel, the exchange as above)"""
+    got = _spawn(2, True, rmin=False)
+    one = _one_context(rmin=False)
+    for r in range(2):
+        assert got[r]["stats"]["qn_inkernel_waves"] > 0, got[r]["stats"]
         _compare(got[r], one)
 
 

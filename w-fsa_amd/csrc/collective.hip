@@ -456,18 +456,6 @@ struct PeerArgs {
     unsigned* status;   // host-mapped: set to 1 when the call failed
 };
 
-// area layout: [2][nranks][kPeerCap] doubles, [2][nranks][kPeerMaxChunks]
-// flags, then the poison word (padded to 16 bytes)
-__host__ __device__ inline size_t peer_area_bytes(int nranks) {
-    return 2 * size_t(nranks) * kPeerCap * sizeof(double) + 2 * size_t(nranks) * kPeerMaxChunks * sizeof(uint64_t) + 16;
-}
-__device__ __forceinline__ uint64_t* peer_flags(double* area, int nranks) {
-    return reinterpret_cast<uint64_t*>(area + 2 * size_t(nranks) * kPeerCap);
-}
-__device__ __forceinline__ uint64_t* peer_poison(double* area, int nranks) {
-    return peer_flags(area, nranks) + 2 * size_t(nranks) * kPeerMaxChunks;
-}
-
 __device__ __forceinline__ bool poisoned(double* area, int nranks) {
     return __hip_atomic_load(peer_poison(area, nranks), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0;
 }
@@ -488,13 +476,13 @@ __global__ __launch_bounds__(256) void peer_sum_kernel(PeerArgs a) {
         }
         __threadfence_system();   // the slots before the flags, on every member
         __syncthreads();
-        const size_t fl = (size_t(par) * a.nranks + a.me) * kPeerMaxChunks + c;
+        const size_t fl = (size_t(par) * a.nranks + a.me) * kPeerFlags + c;
         if (int(threadIdx.x) < a.nranks)
             __hip_atomic_store(peer_flags(a.area[threadIdx.x], a.nranks) + fl, a.seq, __ATOMIC_RELEASE,
                                __HIP_MEMORY_SCOPE_SYSTEM);
         // every member's chunk c in this rank's area; a poisoned area ends the wait
         if (int(threadIdx.x) < a.nranks) {
-            const uint64_t* f = peer_flags(a.area[a.me], a.nranks) + (size_t(par) * a.nranks + threadIdx.x) * kPeerMaxChunks + c;
+            const uint64_t* f = peer_flags(a.area[a.me], a.nranks) + (size_t(par) * a.nranks + threadIdx.x) * kPeerFlags + c;
             const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
             while (__hip_atomic_load(f, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) < a.seq) {
                 if (__builtin_amdgcn_s_memrealtime() - t0 > a.timeout || poisoned(a.area[a.me], a.nranks)) {
@@ -588,6 +576,7 @@ public:
         }
         if (status_h_) (void)hipHostFree(status_h_);
         if (aux_) (void)hipStreamDestroy(aux_);
+        if (area_tbl_) (void)hipFree(area_tbl_);
     }
 
     // this rank's area and status word (false: err says why).  Always safe to
@@ -692,6 +681,27 @@ public:
         (void)hipGetLastError();
     }
 
+    // an in-kernel exchange's view, with the next sequence number
+    bool exchange_view(PeerX& x) {
+        if (!area_tbl_) {   // the areas' pointers as a device table (once)
+            if (hipMalloc(reinterpret_cast<void**>(&area_tbl_), sizeof(args_.area)) != hipSuccess ||
+                hipMemcpy(area_tbl_, args_.area, sizeof(args_.area), hipMemcpyHostToDevice) != hipSuccess) {
+                (void)hipGetLastError();
+                if (area_tbl_) (void)hipFree(area_tbl_);
+                area_tbl_ = nullptr;
+                return false;
+            }
+        }
+        x.area = area_tbl_;
+        x.on = 1;
+        x.nranks = n_;
+        x.me = me_;
+        x.seq = ++seq_;
+        x.timeout = args_.timeout;
+        x.status = status_d_;
+        return true;
+    }
+
     // selftest access
     PeerArgs& args() { return args_; }
     double* own() const { return own_; }
@@ -709,6 +719,7 @@ private:
     bool mapped_ = false;
     uint64_t seq_ = 0;
     PeerArgs args_{};
+    double** area_tbl_ = nullptr;   // args_.area on the device (exchange_view)
 };
 
 double comm_timeout_s() {
@@ -834,6 +845,12 @@ int Collective::try_peer(hipStream_t s) {
     return done(0);
 }
 
+bool Collective::peer_exchange(PeerX& x) {
+    x = PeerX{};
+    if (peer_st_ != 1 || !peer_ || aborted_) return false;
+    return peer_->exchange_view(x);
+}
+
 int Collective::check() {
     if (aborted_) {
         err_ = "communicator aborted: " + abort_why_;
@@ -887,7 +904,7 @@ __global__ void selftest_fill_kernel(PeerArgs a, int rank, uint64_t seq, int wit
     if (with_flags && blockIdx.x == 0) {
         const int chunks = int((a.n + kPeerChunk - 1) / kPeerChunk);
         for (int c = int(threadIdx.x); c < chunks; c += int(blockDim.x))
-            __hip_atomic_store(peer_flags(area, a.nranks) + (size_t(par) * a.nranks + rank) * kPeerMaxChunks + c, seq,
+            __hip_atomic_store(peer_flags(area, a.nranks) + (size_t(par) * a.nranks + rank) * kPeerFlags + c, seq,
                                __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
     }
 }

@@ -20,6 +20,8 @@
 
 #include <hip/hip_runtime.h>
 
+#include "peer_layout.hpp"
+
 #include <cstddef>
 #include <cstdint>
 #include <memory>
@@ -73,6 +75,10 @@ public:
     //    leaves the others to the callback transport's own timeout.
     void abort(const char* why);
     bool aborted() const { return aborted_; }
+    // the in-kernel exchange's view of the peer areas with the next sequence
+    // number (one per launch that exchanges); false when the peer path is not
+    // on (x.on = 0)
+    bool peer_exchange(PeerX& x);
 
 protected:
     // the transport's own all-reduce
@@ -129,12 +135,8 @@ private:
 // of one process on one device have no such guarantee -- HIP may put their
 // streams on one hardware queue, where a spinning kernel holds back the
 // other -- so an in-process group on one device keeps the transport.
-constexpr size_t kPeerCap = size_t(1) << 16;      // doubles per rank slot (512 KiB)
-constexpr int kPeerChunk = 1024;                  // doubles per block
-constexpr int kPeerMaxChunks = int(kPeerCap / kPeerChunk);
 
 constexpr int kCommIdBytes = 128;   // WFSA_COMM_ID_BYTES
-constexpr int kLocalMaxRanks = 16;
 
 // Checks the peer kernel on one device without a second process: the other
 // members' areas are local and their contributions / flags are written

@@ -2626,8 +2626,9 @@ __device__ __forceinline__ QnBatchIn qn_wave_load(const QnWave& q, int b) {
 
 typedef __attribute__((address_space(3))) void lds_void;   // (LDS-DMA operands)
 typedef __attribute__((address_space(1))) void glb_void;
-__device__ __forceinline__ void qn_wave_batch(const QnWave& q, const QnBatchIn& in, bool ok, const unsigned& halt,
-                                              unsigned long long* tr = nullptr) {   // (tr: timing experiments, stamps 8-11)
+template <bool PX>
+__device__ __forceinline__ void qn_wave_batch(const QnWave& q, const QnBatchIn& in, bool ok_in, const unsigned& halt,
+                                              int bi, unsigned long long* tr = nullptr) {   // (tr: timing experiments, stamps 8-11)
 #pragma clang fp contract(off)
     const int lane = lane_id();
     const int c0 = in.c0, nc = in.nc, m0 = in.m0, m1 = in.m1, nchunk = in.nchunk;
@@ -2706,9 +2707,26 @@ __device__ __forceinline__ void qn_wave_batch(const QnWave& q, const QnBatchIn& 
         for (int u = 0; u < 4; ++u)
             if (t0 + u < nch) sm += v[u];
     }
-    double gi = in.gout;   // qn_step_kernel's order: the traversal part, + the trivial words', + the slots'
-    gi += ft;
-    const double sg = gi + sm;
+    bool ok = ok_in;
+    double sg;
+    if (PX && q.px.on) {
+        // across ranks: the members' partials (their traversal part and slot
+        // sums) summed over the ranks through the peer areas, in rank order,
+        // then the trivial words' constant (all-reduced at preparation); a
+        // halted step skips the exchange on every rank alike
+        double g = 0.0;
+        if (ok && halt == 0u) {
+            ok = peer_post_wait(q.px, size_t(m0), m1 - m0, valid ? in.gout + sm : 0.0, kPeerQnFlag0 + bi);
+            if (ok && valid)
+                for (int r = 0; r < q.px.nranks; ++r) g += peer_slot(q.px, r, size_t(m));
+            if (!ok && lane == 0) store_wt(q.halted + 2, 1u);   // (the finish reports it; the host the member's failure)
+        }
+        sg = g + ft;
+    } else {
+        double gi = in.gout;   // qn_step_kernel's order: the traversal part, + the trivial words', + the slots'
+        gi += ft;
+        sg = gi + sm;
+    }
     const double e = exp(x);
     // the per-constraint sums, in member order on the leader lane: eight
     // members' values fetched per round (the shuffles independent, in flight
@@ -2785,6 +2803,7 @@ __device__ __forceinline__ void qn_wave_batch(const QnWave& q, const QnBatchIn& 
 // QN wave r of the launch: wait for every block's arrival (its bubble slots
 // and the finish wave's halt decision), then its batches r, r + n_waves, ...
 constexpr unsigned kQnPollLimit = 1u << 22;   // polls of ~0.5 us under load (s_sleep 1 + an sc1 load): ~1 s, then give up
+template <bool PX>
 __device__ __forceinline__ void qn_wave_run(const QnWave& q, int r, unsigned long long* tr) {
     const int lane = lane_id();
     QnBatchIn first{};
@@ -2818,9 +2837,9 @@ __device__ __forceinline__ void qn_wave_run(const QnWave& q, int r, unsigned lon
     // the halt decision of this launch's finish wave: issued now, waited for
     // only before the first store (beside the batch's chunk loads)
     const unsigned halt = ok ? load_wt(q.halted + 1) : 0u;
-    if (r < q.n_batches) qn_wave_batch(q, first, ok != 0, halt, tr);
+    if (r < q.n_batches) qn_wave_batch<PX>(q, first, ok != 0, halt, r, tr);
     for (int b = r + q.n_waves; b < q.n_batches && halt == 0u; b += q.n_waves)
-        qn_wave_batch(q, qn_wave_load(q, b), ok != 0, halt);
+        qn_wave_batch<PX>(q, qn_wave_load(q, b), ok != 0, halt, b);
     if (halt != 0u && r == 0 && lane == 0) {   // the previous step halted: this one is skipped
         q.halted[0] = 1u;   // for the later launches
         qn_publish_row(q.fin, nullptr, kQnSkipped);
@@ -2850,7 +2869,9 @@ __device__ __forceinline__ T late_arg(size_t off) {
 }
 #define WFSA_LATE_ARG(field) late_arg<decltype(CompiledArgs::field)>(offsetof(CompiledArgs, field))
 
-template <bool WIDE, bool W_LDS, bool MULTI, int DBG = 0, bool RMIN = false, bool DELTA = false, bool QN = false>
+// PX: the QN update across ranks (QnWave::px, the finishes' exchanges): its own variants
+template <bool WIDE, bool W_LDS, bool MULTI, int DBG = 0, bool RMIN = false, bool DELTA = false, bool QN = false,
+          bool PX = false>
 #ifdef WFSA_FBS_VGPR64   // (variant builds: a 64-VGPR budget, two 1024-thread blocks per CU)
 #define WFSA_FBS_ATTR __attribute__((amdgpu_num_vgpr(64)))
 #else
@@ -2958,7 +2979,7 @@ __global__ __launch_bounds__(1024, (DBG == 10 ? 8 : 1)) WFSA_FBS_ATTR void fbs_k
             double finfo[7];
             unsigned fstat = kQnRan;
             const QnFinish fin = WFSA_LATE_ARG(fin);
-            qn_finish_compute<true>(fin, nullptr, finfo, fstat);
+            qn_finish_compute<true, false, PX>(fin, nullptr, finfo, fstat);
             if (lane == 0) qn_finish_publish(fin, finfo, fstat);
         }
     };
@@ -3258,9 +3279,9 @@ __global__ __launch_bounds__(1024, (DBG == 10 ? 8 : 1)) WFSA_FBS_ATTR void fbs_k
     if (QN && w == wpb - 2 && bid < a.qw.n_waves) {
         const QnWave qw = WFSA_LATE_ARG(qw);
 #ifdef WFSA_EXPERIMENTS
-        qn_wave_run(qw, bid, tr);
+        qn_wave_run<PX>(qw, bid, tr);
 #else
-        qn_wave_run(qw, bid, nullptr);
+        qn_wave_run<PX>(qw, bid, nullptr);
 #endif
     }
     // Self-finish: every block's wave 0 (its log-likelihood partial) and
@@ -3279,7 +3300,7 @@ __global__ __launch_bounds__(1024, (DBG == 10 ? 8 : 1)) WFSA_FBS_ATTR void fbs_k
             double info[7];
             unsigned st = kQnRan;
             const QnFinish fin = WFSA_LATE_ARG(qw.fin);
-            qn_finish_compute<true, true>(fin, nullptr, info, st);
+            qn_finish_compute<true, true, PX>(fin, nullptr, info, st);
             if (lane == 0) qn_finish_publish(fin, info, st);
         }
     }
@@ -3708,6 +3729,10 @@ hipError_t launch_compiled(const CompiledArgs& a, int grid, int block, size_t ld
         default: break;
         }
 #endif
+        if (a.qw.on && a.qw.px.on && a.rf.part)   // ... across ranks (the peer exchange)
+            return go(fbs_kernel<false, true, false, 0, true, true, true, true>, grid, block, lds, stream, ev0, ev1, a);
+        if (a.qw.on && a.qw.px.on)
+            return go(fbs_kernel<false, true, false, 0, false, true, true, true>, grid, block, lds, stream, ev0, ev1, a);
         if (a.qw.on && a.rf.part)   // with this step's QN update and the rmin column folded in
             return go(fbs_kernel<false, true, false, 0, true, true, true>, grid, block, lds, stream, ev0, ev1, a);
         if (a.qw.on)   // with this step's QN update (the host checks: bubbles fused or none)

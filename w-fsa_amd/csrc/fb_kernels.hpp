@@ -14,6 +14,8 @@
 
 #include <hip/hip_runtime.h>
 
+#include "peer_layout.hpp"
+
 #include <cstddef>
 #include <cstdint>
 #include <cstdlib>
@@ -484,6 +486,12 @@ struct QnFinish {
     int32_t k;
     double plogp, tol;
     int32_t ring_slot;           // ring slot of the step
+    // across ranks (px.on): the step's log-likelihood sum and rmin minimum
+    // exchanged through the peer areas (PeerX) in flag / slot px_slot of the
+    // finish's exchanges; rm_base: this rank's first global string
+    PeerX px;
+    int32_t px_slot;
+    double rm_base;
     uint32_t tag;                // the row's sequence number as the host expects it: written into the row
                                  // with the status (row[7] = status + 16 tag), so a reader that sees the
                                  // flag before the row's data waits for the row itself
@@ -643,6 +651,8 @@ struct QnWave {
     int32_t self_finish;         // the launch's last finisher (after every block's log-likelihood partial and
                                  // every QN wave's partials, write-through) runs this step's finish itself
     unsigned* done;              // [2] per-parity counters of those arrivals (each launch zeroes the other's)
+    PeerX px;                    // px.on: across ranks -- each batch's member partials (the slot sums and
+                                 // the traversal part) summed over the ranks through the peer areas
     uint32_t poll_limit;         // polls before a QN wave gives up (0: kQnPollLimit)
     int32_t poll_fault;          // fault injection (tests): QN wave 0 waits for one arrival too many
 };

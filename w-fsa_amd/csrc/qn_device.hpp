@@ -155,6 +155,50 @@ __device__ inline void qn_publish_row(const QnFinish& f, const double* info, uns
 
 constexpr int kMaxBlockWaves = 16;
 
+// The in-kernel exchange across ranks (PeerX, peer_layout.hpp), by one
+// wavefront: lane l's value v (l < nv) into slot [par][me][base + l] of every
+// member's area, then flag fl there; then every member's flag fl awaited in
+// this rank's area.  false: a member is late past the timeout or an area was
+// poisoned -- then every area is poisoned and the status word set, so every
+// member fails (Collective::check) instead of waiting.
+__device__ inline bool peer_post_wait(const PeerX& x, size_t base, int nv, double v, int fl) {
+    const int lane = int(threadIdx.x) & 63;
+    const int n = x.nranks, par = int(x.seq & 1);
+    const size_t mine = (size_t(par) * n + x.me) * kPeerCap + base;
+    if (lane < nv)
+        for (int r = 0; r < n; ++r) x.area[r][mine + lane] = v;   // (uncached: the stores reach the member)
+    __threadfence_system();   // the slots before the flags, on every member
+    bool ok = true;
+    if (lane < n) {
+        __hip_atomic_store(peer_flags(x.area[lane], n) + (size_t(par) * n + x.me) * kPeerFlags + fl, x.seq,
+                           __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+        const uint64_t* f = peer_flags(x.area[x.me], n) + (size_t(par) * n + lane) * kPeerFlags + fl;
+        const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+        while (__hip_atomic_load(f, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) < x.seq) {
+            if (__builtin_amdgcn_s_memrealtime() - t0 > x.timeout ||
+                __hip_atomic_load(peer_poison(x.area[x.me], n), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0) {
+                ok = false;
+                break;
+            }
+            __builtin_amdgcn_s_sleep(2);
+        }
+    }
+    ok = !__any(!ok);
+    __threadfence_system();
+    if (!ok) {
+        if (lane < n)
+            __hip_atomic_store(peer_poison(x.area[lane], n), uint64_t(1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        if (lane == 0) __hip_atomic_store(x.status, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+    return ok;
+}
+// member r's value at slot base + l of this rank's area (after peer_post_wait)
+__device__ inline double peer_slot(const PeerX& x, int r, size_t idx) {
+    const int par = int(x.seq & 1);
+    return __hip_atomic_load(x.area[x.me] + (size_t(par) * x.nranks + r) * kPeerCap + idx, __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
 // rmin column (fb_kernels.hpp RminArgs).  (value, index) minimum, ties to
 // the lower index.
 __device__ __forceinline__ void min_pair(double& v, double& i, double v2, double i2) {
@@ -224,7 +268,9 @@ __device__ inline double block_reduce(double v, int op, double* red) {
 // next QN launch) and the publication.  red: kMaxBlockWaves doubles of LDS.
 // WAVE: one wavefront computes it alone (the stream kernel's reserved finish
 // wave; no block barriers), red unused
-template <bool WAVE = false, bool WT = false>   // WT: the partials read write-through (sc1): inside the launch that wrote them
+// PX: across ranks through the peer areas (f.px; its own kernel variants:
+// the exchange's registers stay out of the one-rank kernels)
+template <bool WAVE = false, bool WT = false, bool PX = false>   // WT: the partials read write-through (sc1): inside the launch that wrote them
 __device__ inline void qn_finish_compute(const QnFinish& f, double* red, double* info, unsigned& status) {
     const int t = WAVE ? int(threadIdx.x) % 64 : int(threadIdx.x), nt = WAVE ? 64 : int(blockDim.x), nw = nt / 64;
     double gmin = INFINITY, gmax = -INFINITY, lmin = INFINITY, ge = 0.0;
@@ -314,13 +360,34 @@ __device__ inline void qn_finish_compute(const QnFinish& f, double* red, double*
             rr[t >> 6][1] = ri;
         }
         __syncthreads();
+        if (t < 64)   // (every lane of wave 0: the block's minimum)
+            for (int w = 1; w < nw; ++w)
+                if (rr[w][0] < rv || (rr[w][0] == rv && rr[w][1] < ri)) {
+                    rv = rr[w][0];
+                    ri = rr[w][1];
+                }
+    }
+    if (PX && f.px.on && t < 64) {
+        // across ranks: this rank's log-likelihood and rmin pair through the
+        // peer areas; the sum in rank order, the minimum ties to the lower
+        // (global) string
+        const double rg = ri >= 0.0 ? ri + f.rm_base : -1.0;
+        const size_t base = kPeerFinSlot + 4 * size_t(f.px_slot);
+        const double v = t == 0 ? ll : (t == 1 ? rv : rg);
+        if (peer_post_wait(f.px, base, 3, v, kPeerFinFlag + f.px_slot)) {
+            double lls = 0.0, mv = INFINITY, mi = -1.0;
+            for (int r = 0; r < f.px.nranks; ++r) {
+                lls += peer_slot(f.px, r, base);
+                min_pair(mv, mi, peer_slot(f.px, r, base + 1), peer_slot(f.px, r, base + 2));
+            }
+            ll = lls;
+            rv = mv;
+            ri = mi;
+        } else {
+            ll = NAN;   // (the host reports the member's failure: Collective::check)
+        }
     }
     if (t == 0) {
-        for (int w = 1; w < nw; ++w)
-            if (rr[w][0] < rv || (rr[w][0] == rv && rr[w][1] < ri)) {
-                rv = rr[w][0];
-                ri = rr[w][1];
-            }
         if (f.k == 0) gmin = gmax = lmin = 0.0;
         info[0] = f.plogp - (f.ll_part ? ll : *f.out0);
         info[1] = ge;
@@ -351,10 +418,11 @@ __device__ inline void qn_finish_publish(const QnFinish& f, const double* info, 
     qn_publish_row(f, info, status);
 }
 
+template <bool PX = false>
 __device__ inline void qn_finish(const QnFinish& f, double* red) {
     double info[7];
     unsigned status = kQnRan;
-    qn_finish_compute(f, red, info, status);
+    qn_finish_compute<false, false, PX>(f, red, info, status);
     if (threadIdx.x == 0) qn_finish_publish(f, info, status);
 }
 

@@ -233,10 +233,11 @@ __global__ __launch_bounds__(NT) void qn_step_kernel(QnArgs a) {
     }
 }
 
+template <bool PX>
 __global__ __launch_bounds__(kQnBlock) void qn_finish_kernel(QnFinish f) {
     if (f.halted[0] || f.halted[1]) return;   // the step was skipped (and published so)
     __shared__ double red[kMaxBlockWaves];
-    qn_finish(f, red);
+    qn_finish<PX>(f, red);
 }
 
 // initial w_full from x (qn_set_state)
@@ -290,7 +291,8 @@ hipError_t launch_gather(const double* src, const int32_t* idx, int32_t n, doubl
 }
 
 hipError_t launch_qn_finish(const QnFinish& f, hipStream_t stream) {
-    hipLaunchKernelGGL(qn_finish_kernel, dim3(1), dim3(kQnBlock), 0, stream, f);
+    if (f.px.on) hipLaunchKernelGGL(qn_finish_kernel<true>, dim3(1), dim3(kQnBlock), 0, stream, f);
+    else hipLaunchKernelGGL(qn_finish_kernel<false>, dim3(1), dim3(kQnBlock), 0, stream, f);
     return hipGetLastError();
 }
 

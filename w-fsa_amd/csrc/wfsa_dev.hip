@@ -336,6 +336,8 @@ struct wfsa_dev {
     DevBuf<double> ll_stash;   // [2] the all-reduced log-likelihood of a multi-rank step, by parity
     std::vector<int32_t> h_cptr;
     bool fin_pending = false, fin_hostable = false;
+    bool fin_next_px = false, fin_for_fbs_px = false;   // (their finishes exchange across ranks, PeerX)
+    wfsa::PeerX cur_px{};                                // this launch's exchange (enqueue_qn_step)
     DevBuf<unsigned> qn_halted;
     std::vector<int32_t> qn_full_of_h, qn_cptr_h;
     bool qn_fused = false;           // qn_step_kernel sums the members' bubble slots itself
@@ -360,6 +362,9 @@ struct wfsa_dev {
     int32_t qw_nbatch = 0;
     DevBuf<int4> qw_batch;
     DevBuf<int32_t> qw_con_of, qw_mnch, qw_mfirst;
+    DevBuf<double> qw_gch;           // (build_qw_batches across ranks: the constraints' chunk counts)
+    int64_t qw_agree_key = -1;       // across ranks: the in-kernel decision agreed for this key ...
+    bool qw_agreed = false;          // ... and its outcome
     std::vector<int64_t> h_mchunk;   // [n_params] first contribution slot of each position's chunks (layout_slots)
     std::vector<int32_t> h_mnch;     // [n_params] its chunk count
     int64_t layout_gen = 0;          // layout_slots runs
@@ -2066,6 +2071,10 @@ int enqueue_compiled(wfsa_dev* ctx, bool with_grad, bool want_logq, const unsign
         if (!with_grad) {   // a pending QN finish rides in block 0 (consumed)
             c.fin = ctx->fin_for_fbs;
             ctx->fin_for_fbs.active = 0;
+            if (c.fin.active && ctx->fin_for_fbs_px) {   // across ranks: this launch's exchange
+                c.fin.px = ctx->cur_px;
+                c.fin.px_slot = 0;
+            }
         }
         size_t lds = with_grad ? ctx->c_lds : ctx->i_lds;
         if (!with_grad && bubbles_fused(ctx, want_logq)) {
@@ -2537,15 +2546,49 @@ int build_qw_batches(wfsa_dev* ctx) {
     if (!ctx->qn_fused || k <= 0 || n <= 0 || int64_t(cptr.size()) != int64_t(k) + 1 ||
         int64_t(ctx->h_mchunk.size()) < n || ctx->slot_order.size() != size_t(ctx->n_params))
         return WFSA_OK;
-    auto chunks = [&](int32_t c0, int32_t c1) {   // slot chunks of constraints [c0, c1)
+    auto chunks = [&](int32_t c0, int32_t c1) {   // this rank's slot chunks of constraints [c0, c1)
         int64_t t = 0;
         for (int32_t i = cptr[size_t(c0)]; i < cptr[size_t(c1)]; ++i) t += ctx->h_mnch[size_t(i)];
+        return t;
+    };
+    // Across ranks the batches are the same on every rank (the in-kernel
+    // exchange pairs batch b with batch b): their bounds come from each
+    // constraint's largest chunk count over the ranks, each rank's batch then
+    // holds its own chunks.  The counts travel as a sum of every rank's row
+    // (rank r fills row r) -- the peer path's sum, with its wait limit -- when
+    // the rows fit a peer slot, else as a Min of the negated counts
+    std::vector<double> gch(static_cast<size_t>(k));
+    for (int32_t c = 0; c < k; ++c) gch[size_t(c)] = double(chunks(c, c + 1));
+    if (ctx->comm) {
+        const int nr = ctx->comm->nranks(), me = ctx->comm->rank();
+        if (size_t(k) * size_t(nr) <= wfsa::kPeerCap) {
+            std::vector<double> rows(size_t(k) * size_t(nr), 0.0);
+            std::copy(gch.begin(), gch.end(), rows.begin() + std::ptrdiff_t(size_t(me) * size_t(k)));
+            HIP_TRY(ctx->qw_gch.upload(rows.data(), rows.size(), ctx->stream));
+            COMM_TRY(ctx, ctx->qw_gch.ptr, rows.size(), wfsa::RedOp::SumF64, ctx->stream);
+            HIP_TRY(ctx->qw_gch.download(rows.data(), rows.size(), ctx->stream));
+            HIP_TRY(hipStreamSynchronize(ctx->stream));
+            COMM_CHECK(ctx);
+            for (int32_t c = 0; c < k; ++c)
+                for (int r = 0; r < nr; ++r) gch[size_t(c)] = std::max(gch[size_t(c)], rows[size_t(r) * size_t(k) + size_t(c)]);
+        } else {
+            for (double& v : gch) v = -v;
+            HIP_TRY(ctx->qw_gch.upload(gch.data(), gch.size(), ctx->stream));
+            COMM_TRY(ctx, ctx->qw_gch.ptr, gch.size(), wfsa::RedOp::MinF64, ctx->stream);
+            HIP_TRY(ctx->qw_gch.download(gch.data(), gch.size(), ctx->stream));
+            HIP_TRY(hipStreamSynchronize(ctx->stream));
+            for (double& v : gch) v = -v;
+        }
+    }
+    auto gchunks = [&](int32_t c0, int32_t c1) {   // the batching's chunk count: the ranks' largest
+        int64_t t = 0;
+        for (int32_t c = c0; c < c1; ++c) t += int64_t(gch[size_t(c)]);
         return t;
     };
     int64_t widest = 0;
     for (int32_t c = 0; c < k; ++c) {
         const int32_t nm = cptr[size_t(c) + 1] - cptr[size_t(c)];
-        const int64_t nc = chunks(c, c + 1);
+        const int64_t nc = gchunks(c, c + 1);
         if (nm < 1 || nm > wfsa::kQnWaveMembers || nc > limit) return WFSA_OK;
         widest = std::max(widest, nc);
     }
@@ -2554,13 +2597,14 @@ int build_qw_batches(wfsa_dev* ctx) {
     std::vector<int32_t> con_of(size_t(n), 0), mfirst(size_t(n), 0);
     for (int32_t c0 = 0; c0 < k;) {
         int32_t c1 = c0 + 1;
-        int64_t nch = chunks(c0, c1);
+        int64_t gn = gchunks(c0, c1);
         while (c1 < k && cptr[size_t(c1) + 1] - cptr[size_t(c0)] <= mcap) {
-            const int64_t more = chunks(c1, c1 + 1);
-            if (nch + more > cap) break;
-            nch += more;
+            const int64_t more = gchunks(c1, c1 + 1);
+            if (gn + more > cap) break;
+            gn += more;
             ++c1;
         }
+        const int64_t nch = chunks(c0, c1);   // (this rank's: at most gn)
         const int32_t m0 = cptr[size_t(c0)], m1 = cptr[size_t(c1)];
         const int64_t base = ctx->h_mchunk[size_t(m0)];
         int64_t q = 0;
@@ -2614,7 +2658,11 @@ bool qw_resident(wfsa_dev* ctx) {
 bool qw_usable(wfsa_dev* ctx) {
     // (the rmin column rides along when the bubbles run in the stream kernel: RminFold)
     const bool rmin_ok = !ctx->qn_rmin || ctx->n_bubbles == 0 || bubbles_fused(ctx, false);
-    return ctx->use_qw && ctx->qw_ok && ctx->qw_waves > 0 && ctx->qn_fused && !ctx->comm && !ctx->dense &&
+    // (across ranks: through the peer areas, PeerX -- the peer path on, the
+    // batches within the areas' flags)
+    const bool comm_ok = !ctx->comm || (std::strcmp(ctx->comm->peer_state(), "on") == 0 &&
+                                        ctx->qw_nbatch <= wfsa::kPeerMaxQnBatches);
+    return ctx->use_qw && ctx->qw_ok && ctx->qw_waves > 0 && ctx->qn_fused && comm_ok && !ctx->dense &&
            !ctx->mpath && rmin_ok && ctx->n_groups > 0 && ctx->delta_on && ctx->i_tables >= 1 &&
            ctx->fixed_t_on && ctx->qn_k > 0 &&
            ctx->i_block / kWave >= 3 && qw_resident(ctx);
@@ -2634,8 +2682,9 @@ int enqueue_qn_step(wfsa_dev* ctx, double eta, double tol, int64_t e, bool timed
     if (fuse_rmin)
         if (int rc = rmin_prepare(ctx)) return rc;
     if (ctx->fin_pending) {   // the previous step's finish: in this step's stream kernel, or its own launch
-        if (ctx->fin_hostable && trellis && ctx->n_groups > 0) {
+        if (ctx->fin_hostable && trellis && ctx->n_groups > 0 && (!ctx->fin_next_px || inkern)) {
             ctx->fin_for_fbs = ctx->fin_next;
+            ctx->fin_for_fbs_px = ctx->fin_next_px;
             ctx->fin_pending = false;
         } else if (int rc = flush_qn_finish(ctx)) {
             return rc;
@@ -2658,7 +2707,11 @@ int enqueue_qn_step(wfsa_dev* ctx, double eta, double tol, int64_t e, bool timed
     } else if (trellis && ctx->comm && ctx->n_groups > 0) {
         q.fixed = ctx->fixed_grad.ptr;   // all-reduced once at preparation
     }
-    if (trellis && ctx->comm) {   // the step's log-likelihood for its finish, which then rides in the next stream kernel
+    if (trellis && ctx->comm && inkern) {   // in-kernel across ranks: the local partials, summed over the
+                                            // ranks by the finish's exchange
+        f.ll_part = ctx->ll_cur;
+        f.rm_base = double(ctx->rm_base);
+    } else if (trellis && ctx->comm) {   // the step's log-likelihood for its finish, which then rides in the next stream kernel
         if (ctx->ll_stash.n < 2) HIP_TRY(ctx->ll_stash.alloc(2));
         q.ll_stash = ctx->ll_stash.ptr + par;
         f.ll_part = ctx->ll_stash.ptr + par;
@@ -2725,6 +2778,10 @@ int enqueue_qn_step(wfsa_dev* ctx, double eta, double tol, int64_t e, bool timed
         w.halted = ctx->qn_halted.ptr;
         w.done = ctx->qw_done.ptr;   // (every launch zeroes the other parity's counter)
         w.poll_limit = ctx->qw_poll_limit;
+        if (ctx->comm) {   // across ranks: this launch's exchanges (one sequence number)
+            if (!ctx->comm->peer_exchange(w.px)) return fail(WFSA_ERR_RCCL, "the peer exchange is not available");
+            ctx->cur_px = w.px;
+        }
         w.poll_fault = ctx->qw_poll_fault ? 1 : 0;
         if (ctx->qn_rmin) {   // the rmin column folded into the launch: its block minima for the finish
             ctx->rm_bpart_cur = ctx->rm_bpart.ptr + size_t(par) * 2 * size_t(ctx->i_grid);
@@ -2740,6 +2797,8 @@ int enqueue_qn_step(wfsa_dev* ctx, double eta, double tol, int64_t e, bool timed
         self_fin = last && ctx->qw_last_self;
         if (self_fin) {
             w.self_finish = 1;
+            w.fin.px = w.px;   // (across ranks: the exchange of a launch finishing its own step)
+            w.fin.px_slot = 1;
             w.fin.ll_part = ctx->ll_cur;
             // the stream kernel's blocks, then (bubbles not fused: the bubble
             // kernel ran first) the bubble kernel's waves -- enqueue_evaluation's order
@@ -2749,12 +2808,13 @@ int enqueue_qn_step(wfsa_dev* ctx, double eta, double tol, int64_t e, bool timed
         ++ctx->qw_seq;
     }
     ctx->rm_eval = fuse_rmin;
-    const int erc = enqueue_evaluation(ctx, false, ctx->qn_halted.ptr, timed ? slot : -1, !fused && trellis, &n_ll);
+    const int erc = enqueue_evaluation(ctx, false, ctx->qn_halted.ptr, timed ? slot : -1, !fused && !inkern && trellis,
+                                       &n_ll);
     ctx->rm_eval = false;
     ctx->rm_bpart_cur = nullptr;
     if (erc) return erc;
     if (ctx->qw_next.on) return fail(WFSA_ERR_HIP, "the in-kernel QN update was not launched");
-    if (fused) f.n_ll = n_ll;
+    if (fused || inkern) f.n_ll = n_ll;
     if (inkern && self_fin) {   // the step published its own row: no finish pending
         const int32_t want = ctx->i_grid + ((ctx->n_bubbles > 0 && !bubbles_fused(ctx, false)) ? ctx->b_waves : 0) +
                              trav_ll_waves(ctx);
@@ -2763,7 +2823,7 @@ int enqueue_qn_step(wfsa_dev* ctx, double eta, double tol, int64_t e, bool timed
         ctx->fin_next.active = 0;
         return WFSA_OK;
     }
-    if (ctx->comm) COMM_TRY(ctx, ctx->out.ptr, size_t(np) + 1, wfsa::RedOp::SumF64, s);
+    if (ctx->comm && !inkern) COMM_TRY(ctx, ctx->out.ptr, size_t(np) + 1, wfsa::RedOp::SumF64, s);
     if (ctx->qn_rmin && !inkern) {
         constexpr bool fold_rmin = true;   // the strings pass in the QN step kernel's blocks (one launch fewer)
         double* res = ctx->rm_res.ptr + 2 * par;
@@ -2784,6 +2844,7 @@ int enqueue_qn_step(wfsa_dev* ctx, double eta, double tol, int64_t e, bool timed
     // kernel zeroes); else it is launched when the next step is enqueued
     ctx->fin_next = f;
     ctx->fin_next.active = 1;
+    ctx->fin_next_px = inkern && ctx->comm;   // (its exchange takes the sequence number of the launch it runs in)
     ctx->fin_pending = true;
     ctx->fin_hostable = (fused || (trellis && ctx->comm)) && ctx->n_groups > 0 && f.ll_part != nullptr;
     return WFSA_OK;
@@ -2793,6 +2854,11 @@ int enqueue_qn_step(wfsa_dev* ctx, double eta, double tol, int64_t e, bool timed
 int flush_qn_finish(wfsa_dev* ctx) {
     if (!ctx->fin_pending) return WFSA_OK;
     ctx->fin_pending = false;
+    if (ctx->fin_next_px) {   // across ranks: a sequence number of its own
+        if (!ctx->comm || !ctx->comm->peer_exchange(ctx->fin_next.px))
+            return fail(WFSA_ERR_RCCL, "the peer exchange is not available");
+        ctx->fin_next.px_slot = 0;
+    }
     HIP_TRY(wfsa::launch_qn_finish(ctx->fin_next, ctx->stream));
     return WFSA_OK;
 }
@@ -3390,7 +3456,9 @@ static int qn_setup_impl(wfsa_dev* ctx, const wfsa_qn_desc* d) {
     // rest after), so the fused QN step sums each constraint's run in place
     int32_t max_nm = 0;
     for (int32_t c = 0; c < k; ++c) max_nm = std::max(max_nm, cptr[size_t(c) + 1] - cptr[size_t(c)]);
-    ctx->qn_fused = max_nm <= wfsa::kQnMaxSeg && !ctx->comm;
+    // (with a communicator too: the in-kernel update across ranks reads the
+    // slots in this order; the separate kernel path there reduces first)
+    ctx->qn_fused = max_nm <= wfsa::kQnMaxSeg;
     ctx->qn_max_nm = std::max(1, std::min(max_nm, wfsa::kQnMaxSeg));
     if (ctx->qn_fused) {
         std::vector<int32_t> pos_of(size_t(nf), -1);
@@ -3512,7 +3580,24 @@ static int qn_run_impl(wfsa_dev* ctx, double eta, double tol, int32_t max_steps,
     }
     if (ctx->use_qw && ctx->qw_waves > 0)
         if (int rc = build_qw_batches(ctx)) return rc;
-    const bool inkern = qw_usable(ctx);
+    bool inkern = qw_usable(ctx);
+    if (ctx->comm) {   // every rank takes the same path (the in-kernel exchange pairs the ranks' launches):
+                       // agreed once per preparation, QN set-up, layout and rmin setting
+        const int64_t key = ((ctx->prep_gen * 1000003 + ctx->qn_setup_gen) * 1000003 + ctx->layout_gen) * 2 +
+                            (ctx->qn_rmin ? 1 : 0);
+        if (ctx->qw_agree_key != key) {   // (a sum of "cannot" votes: the peer path's sum, with its wait limit)
+            double bad = inkern ? 0.0 : 1.0;
+            HIP_TRY(ctx->qw_gch.alloc(std::max<size_t>(ctx->qw_gch.n, 1)));
+            HIP_TRY(hipMemcpyAsync(ctx->qw_gch.ptr, &bad, sizeof bad, hipMemcpyHostToDevice, s));
+            COMM_TRY(ctx, ctx->qw_gch.ptr, 1, wfsa::RedOp::SumF64, s);
+            HIP_TRY(hipMemcpyAsync(&bad, ctx->qw_gch.ptr, sizeof bad, hipMemcpyDeviceToHost, s));
+            HIP_TRY(hipStreamSynchronize(s));
+            COMM_CHECK(ctx);
+            ctx->qw_agree_key = key;
+            ctx->qw_agreed = bad == 0.0;
+        }
+        inkern = ctx->qw_agreed;
+    }
     if (!inkern && ctx->use_qw && std::getenv("WFSA_VERBOSE"))
         std::fprintf(stderr, "[wfsa] QN update as its own kernel: batches %d waves %d fused %d comm %d rmin %d delta %d "
                      "fallback %d bubbles fused %d fixed_t %d k %d\n", int(ctx->qw_ok), ctx->qw_waves, int(ctx->qn_fused),
