@@ -12,7 +12,7 @@ sys.path.insert(0, os.path.join(ROOT, "w-fsa_amd"))
 def main():
     import torch
     import wfsa_amd as W
-    syn = W.Synthetic(n_states=1024, degree=8, vocab=64, emissions=1, n_strings=1_000_000, max_len=128, seed=1)
+    syn = W.Synthetic(n_states=1024, degree=8, vocab=64, emissions=1, n_strings=int(os.environ.get("BL_STRINGS", "1000000")), max_len=128, seed=1)
     sym, off, wt = syn.corpus()
     fsa = W.Fsa.read_text(syn.wfsa_text)
     lrn = W.QuasiNewtonLearner(0)

@@ -2812,22 +2812,39 @@ __device__ __forceinline__ void qn_wave_run(const QnWave& q, int r, unsigned lon
     if (lane == 0) {
         unsigned it = 0;
         const unsigned limit = q.poll_limit ? q.poll_limit : kQnPollLimit;
-        const unsigned want = unsigned(q.n_arrive) + ((q.poll_fault && r == 0) ? 1u : 0u);   // (fault injection)
-        // (every QN wave polls the one counter: a go token per wave's own
-        // line, written by the last arrival, measured no faster, r05)
-        while (load_wt(q.arrive + q.parity) < want) {
+#ifdef WFSA_EXPERIMENTS
+        if (tr) tr[11] = __builtin_amdgcn_s_memrealtime();
+#endif
+        // Wave 0 alone polls the arrival counter and then releases the other
+        // waves' go lines (this launch's tag; no reset needed).  Every QN
+        // wave polling the counter's line -- which the blocks' atomics
+        // update -- slowed the whole launch once the waves polled from their
+        // stream's end (c3 46 vs 27.5 us, 500k strings 37 vs 23.7;
+        // profiles/r06/poll_modes.txt)
+        const bool lead = r == 0;
+        const unsigned* line = lead ? q.arrive + q.parity : q.go + size_t(r) * kQnGoStride;
+        const unsigned want = lead ? unsigned(q.n_arrive) + (q.poll_fault ? 1u : 0u) : q.fin.tag;   // (fault injection)
+        while (lead ? load_wt(line) < want : load_wt(line) != want) {
+#ifdef WFSA_EXPERIMENTS
+            if (tr && it == 0) tr[13] = __builtin_amdgcn_s_memrealtime();
+#endif
             __builtin_amdgcn_s_sleep(1);
             if (++it > limit) {
                 ok = 0;
                 break;
             }
         }
+#ifdef WFSA_EXPERIMENTS
+        if (tr) tr[12] = it;
+#endif
         // a wave that gave up leaves its constraints un-updated: the timeout
         // word makes this step's finish report kQnTimedOut (its NaN partials
         // alone would be dropped by the finish's fmin / fmax), and the host
         // then fails the run instead of stepping on inconsistent weights
         if (!ok) store_wt(q.halted + 2, 1u);
     }
+    if (r == 0)   // (after a timeout too: the step then fails by the timeout word, not by every wave's wait)
+        for (int v = 1 + lane; v < q.n_waves; v += kWave) store_wt(q.go + size_t(v) * kQnGoStride, q.fin.tag);
     // (a compiler barrier: no load below moves above the poll; on the
     // hardware a workgroup-scope acquire is only a vmcnt wait -- see the
     // ordering note at the arrival in fbs_kernel)
@@ -2933,7 +2950,11 @@ __global__ __launch_bounds__(1024, (DBG == 10 ? 8 : 1)) WFSA_FBS_ATTR void fbs_k
         return;
     }
     __shared__ unsigned q_arrived;   // QN: this block's waves whose bubble slots have retired
-    if (QN && threadIdx.x == 0) q_arrived = 0u;   // (ordered by the staging barrier)
+    __shared__ unsigned blk_in;      // this block's waves whose partials are in LDS (wsum, wrv, wri)
+    if (threadIdx.x == 0) {   // (ordered by the staging barrier)
+        blk_in = 0u;
+        if (QN) q_arrived = 0u;
+    }
     const uint32_t zslot = uint32_t(a.n_params);
     // this wave's run of chunk rows
     const int g0 = a.wave_first[gw], g1 = a.wave_first[gw + 1];
@@ -3087,8 +3108,18 @@ __global__ __launch_bounds__(1024, (DBG == 10 ? 8 : 1)) WFSA_FBS_ATTR void fbs_k
         unsigned prev = 0u;
         if (lane == 0) prev = atomicAdd(&q_arrived, 1u);
         prev = __shfl(prev, 0, kWave);
-        if (lane == 0 && prev == unsigned(wpb - 1))   // the block's last wave: one arrival for all its stores
-            __hip_atomic_fetch_add(a.qw.arrive + a.qw.parity, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (lane == 0 && prev == unsigned(wpb - 1)) {   // the block's last wave: one arrival for all its stores
+            const unsigned o =
+                __hip_atomic_fetch_add(a.qw.arrive + a.qw.parity, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#ifdef WFSA_EXPERIMENTS
+            if (a.trace) {   // (the atomic's return: when it landed, in which order)
+                a.trace[size_t(blockIdx.x) * wpb * 16 + 14] = __builtin_amdgcn_s_memrealtime();
+                a.trace[size_t(blockIdx.x) * wpb * 16 + 15] = o;
+            }
+#else
+            (void)o;
+#endif
+        }
         WFSA_STAMP(3)
     }
     if (kStreams) load(B, D);
@@ -3251,9 +3282,19 @@ __global__ __launch_bounds__(1024, (DBG == 10 ? 8 : 1)) WFSA_FBS_ATTR void fbs_k
             wri[w] = rm_ci;
         }
     }
-    __syncthreads();
+    // The block's partials: the last of its waves to get here sums them (an
+    // LDS counter, no block barrier), so a QN wave goes on to its update as
+    // soon as its own stream share is done -- behind a block barrier it
+    // started only once the slowest stream wave of its block was done (c3:
+    // polls matched at 20-24 us for arrivals landed by 20,
+    // profiles/r06/fbs_trace_polls.log).  (The workgroup-scope release /
+    // acquire orders each wave's LDS partials before its count.)
+    unsigned prev_in = 0u;
+    if (lane == 0) prev_in = __hip_atomic_fetch_add(&blk_in, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_WORKGROUP);
+    prev_in = __builtin_amdgcn_readfirstlane(prev_in);   // (every lane active: lane 0's)
+    const bool writer = prev_in == unsigned(wpb - 1);
     const bool self_fin = QN && a.qw.self_finish;
-    if (threadIdx.x == 0) {
+    if (writer && lane == 0) {
         double t = 0.0;
         for (int i = 0; i < wpb; ++i) t += wsum[i];
         if (self_fin) store_wt(a.ll_part + bid, t);   // (read by this launch's finisher)
@@ -3271,12 +3312,11 @@ __global__ __launch_bounds__(1024, (DBG == 10 ? 8 : 1)) WFSA_FBS_ATTR void fbs_k
         }
     }
     // this block's slice of the per-edge weights and the zeroed result, for
-    // the kernels after this one (nothing in this launch reads them)
+    // the kernels after this one (nothing in this launch reads them; skipped
+    // when the QN update rides in the launch)
     if (W_LDS && !a.no_streams && !a.no_slice) edge_weight_slice(a, bid, nblk);
-    // the QN waves, their stream share done: this step's QN update (after
-    // the block barrier; a second call site before it, as an option, made
-    // the kernel spill 96 VGPRs)
-    if (QN && w == wpb - 2 && bid < a.qw.n_waves) {
+    const bool qn_wave = QN && w == wpb - 2 && bid < a.qw.n_waves;
+    if (qn_wave) {   // this step's QN update
         const QnWave qw = WFSA_LATE_ARG(qw);
 #ifdef WFSA_EXPERIMENTS
         qn_wave_run<PX>(qw, bid, tr);
@@ -3284,19 +3324,21 @@ __global__ __launch_bounds__(1024, (DBG == 10 ? 8 : 1)) WFSA_FBS_ATTR void fbs_k
         qn_wave_run<PX>(qw, bid, nullptr);
 #endif
     }
-    // Self-finish: every block's wave 0 (its log-likelihood partial) and
-    // every QN wave (its constraints' partials) arrive once their stores
-    // retired; the last arrival runs this step's finish (the wave form,
-    // write-through loads, the same sums as the next launch's finish wave)
-    // and publishes the row -- no finish left for the next launch, and the
-    // Run's last row needs no finish kernel of its own.  A step the previous
-    // finish halted publishes its skipped row from its QN waves instead.
-    if (self_fin && (w == 0 || (w == wpb - 2 && bid < a.qw.n_waves))) {
+    // Self-finish: every block's partials writer (its log-likelihood
+    // partial) and every QN wave (its constraints' partials) arrive once
+    // their stores retired -- a wave in both roles counts twice; the last
+    // arrival runs this step's finish (the wave form, write-through loads,
+    // the same sums as the next launch's finish wave) and publishes the row
+    // -- no finish left for the next launch, and the Run's last row needs no
+    // finish kernel of its own.  A step the previous finish halted publishes
+    // its skipped row from its QN waves instead.
+    if (self_fin && (writer || qn_wave)) {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        const unsigned add = unsigned(writer) + unsigned(qn_wave);
         unsigned before = 0u;
-        if (lane == 0) before = __hip_atomic_fetch_add(a.qw.done + a.qw.parity, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (lane == 0) before = __hip_atomic_fetch_add(a.qw.done + a.qw.parity, add, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         before = __shfl(before, 0, kWave);
-        if (before + 1u == unsigned(nblk + a.qw.n_waves) && load_wt(a.qw.halted + 1) == 0u) {
+        if (before + add == unsigned(nblk + a.qw.n_waves) && load_wt(a.qw.halted + 1) == 0u) {
             double info[7];
             unsigned st = kQnRan;
             const QnFinish fin = WFSA_LATE_ARG(qw.fin);

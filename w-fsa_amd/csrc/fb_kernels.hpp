@@ -655,7 +655,13 @@ struct QnWave {
                                  // the traversal part) summed over the ranks through the peer areas
     uint32_t poll_limit;         // polls before a QN wave gives up (0: kQnPollLimit)
     int32_t poll_fault;          // fault injection (tests): QN wave 0 waits for one arrival too many
+    unsigned* go;                // [n_waves][kQnGoStride]: wave r's go line (r > 0), set to fin.tag by wave 0
 };
+
+// QN waves' go lines: 256 bytes apart (their polls spread over the memory
+// channels), at most kQnMaxWaves of them
+constexpr int kQnGoStride = 64;
+constexpr int kQnMaxWaves = 1024;
 
 // The rmin column inside the in-kernel QN step (fbs_kernel<..., RMIN, DELTA,
 // QN>; GetOptimizationInfo's smallest relative path probability,

@@ -372,6 +372,7 @@ struct wfsa_dev {
     std::vector<int4> h_qw_batch;    // host copy of the batches (diagnostics)
     DevBuf<unsigned> qw_arrive;      // [2], zero between launches (each launch zeroes the next one's)
     DevBuf<unsigned> qw_done;        // [2] the self-finish's arrivals, likewise
+    DevBuf<unsigned> qw_go;          // [kQnMaxWaves][kQnGoStride] the QN waves' go lines (fb_kernels.hpp QnWave::go)
     size_t qw_res_lds = ~size_t(0);  // qw_resident's cache: the launch's LDS and block, blocks per CU
     int qw_res_block = 0, qw_res_per_cu = 0;
     uint32_t qw_poll_limit = 0;      // polls before an in-kernel QN wave gives up (0: the kernel default)
@@ -1686,7 +1687,8 @@ int prepare(wfsa_dev* ctx, int level) {
         // fixed-order sum, is then the same with the update in or out)
         constexpr int64_t per_qw = 48;   // parameters per QN wave (40 / 36 / 32: no gain, profiles/r05)
         ctx->qw_waves = (i_wpb >= 3 && delta_want && ctx->i_tables)
-                            ? int(std::min<int64_t>(nblk, (int64_t(ctx->n_params) + per_qw - 1) / per_qw)) : 0;
+                            ? int(std::min<int64_t>({nblk, int64_t(wfsa::kQnMaxWaves),
+                                                     (int64_t(ctx->n_params) + per_qw - 1) / per_qw})) : 0;
         for (int w = 0; w < i_nw; ++w) {
             const int bid = w / i_wpb, wib = w % i_wpb;
             if (bid == 0 && wib == i_wpb - 1) {   // the QN finish's wave (fbs_kernel): no groups
@@ -2777,6 +2779,7 @@ int enqueue_qn_step(wfsa_dev* ctx, double eta, double tol, int64_t e, bool timed
         w.arrive = ctx->qw_arrive.ptr;
         w.halted = ctx->qn_halted.ptr;
         w.done = ctx->qw_done.ptr;   // (every launch zeroes the other parity's counter)
+        w.go = ctx->qw_go.ptr;
         w.poll_limit = ctx->qw_poll_limit;
         if (ctx->comm) {   // across ranks: this launch's exchanges (one sequence number)
             if (!ctx->comm->peer_exchange(w.px)) return fail(WFSA_ERR_RCCL, "the peer exchange is not available");
@@ -2993,6 +2996,9 @@ int wfsa_dev_create(int device, wfsa_dev** out) {
     HIP_TRY(hipMemsetAsync(ctx->counters.ptr, 0, sizeof(unsigned), ctx->stream));
     HIP_TRY(ctx->qw_arrive.alloc(2));
     HIP_TRY(hipMemsetAsync(ctx->qw_arrive.ptr, 0, 2 * sizeof(unsigned), ctx->stream));
+    constexpr size_t n_go = size_t(wfsa::kQnMaxWaves) * wfsa::kQnGoStride;
+    HIP_TRY(ctx->qw_go.alloc(n_go));
+    HIP_TRY(hipMemsetAsync(ctx->qw_go.ptr, 0, n_go * sizeof(unsigned), ctx->stream));
     HIP_TRY(ctx->qw_done.alloc(2));
     HIP_TRY(hipMemsetAsync(ctx->qw_done.ptr, 0, 2 * sizeof(unsigned), ctx->stream));
     HIP_TRY(hipStreamSynchronize(ctx->stream));
@@ -3784,6 +3790,32 @@ static int qn_run_impl(wfsa_dev* ctx, double eta, double tol, int32_t max_steps,
                 std::fprintf(stderr, " %s %.2f / %.2f / %.2f;", pn[k], ph[k][ph[k].size() / 2], ph[k][ph[k].size() * 9 / 10],
                              ph[k].back());
             }
+            std::fprintf(stderr, "\n");
+        }
+        {   // the QN waves' polls (11: start, 13: first poll returned, 12: iterations) and the
+            // blocks' arrival atomics (wave 0's words 14: the atomic returned, 15: its order)
+            std::vector<double> it, per, first;
+            for (int w = 0; w < nw; ++w) {
+                if (!(w % wpb == wpb - 2 && w / wpb < ctx->qw_waves)) continue;
+                const unsigned long long* r = &t[size_t(w) * 16];
+                if (!r[11] || !r[5]) continue;
+                it.push_back(double(r[12]));
+                if (r[12] > 0) per.push_back(double(r[5] - r[11]) / 100.0 / double(r[12]));
+                if (r[13]) first.push_back(double(r[13] - r[11]) / 100.0);
+            }
+            std::vector<std::pair<double, int>> land;
+            for (int b = 0; b < ctx->i_grid; ++b) {
+                const unsigned long long* r = &t[size_t(b) * wpb * 16];
+                if (r[14]) land.push_back({double(r[14] - t0) / 100.0, int(r[15])});
+            }
+            std::sort(land.begin(), land.end());
+            auto med = [](std::vector<double> v) { std::sort(v.begin(), v.end()); return v.empty() ? -1.0 : v[v.size() / 2]; };
+            auto mx = [](const std::vector<double>& v) { return v.empty() ? -1.0 : *std::max_element(v.begin(), v.end()); };
+            std::fprintf(stderr, "[fbs-trace] QN polls: iterations p50 %.0f max %.0f; us per poll p50 %.2f max %.2f; first poll "
+                         "p50 %.2f max %.2f us; block arrivals landed: n %zu",
+                         med(it), mx(it), med(per), mx(per), med(first), mx(first), land.size());
+            for (size_t i = land.size() > 4 ? land.size() - 4 : 0; i < land.size(); ++i)
+                std::fprintf(stderr, " (%.2f us, order %d)", land[i].first, land[i].second);
             std::fprintf(stderr, "\n");
         }
         // the deal's calibration: each wave's stream-phase end (stamp 4, from
