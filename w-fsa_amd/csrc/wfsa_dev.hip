@@ -2635,9 +2635,10 @@ int build_qw_batches(wfsa_dev* ctx) {
 }
 
 // The QN update rides in the stream kernel (fb_kernels.hpp QnWave) when the
-// step is exactly: one rank, every string compiled into the delta stream, no
-// rmin column, every constraint of 1..64 members (bubbles not fused into the
-// stream kernel run in their own kernel before it)
+// compiled strings use the delta stream and the QN batches were built; the
+// rmin column needs the bubbles fused into the stream kernel (RminFold);
+// traversal strings run before the launch; across ranks the peer path must be
+// on (PeerX) -- and every rank must agree (qn_run_impl)
 //
 // The QN waves wait for every block's arrival, so every block of the grid
 // must be resident at once: the grid is checked against the CUs times the
