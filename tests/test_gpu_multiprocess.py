@@ -57,6 +57,7 @@ def _worker(rank, world, port, peer, q, late_s=0.0, abort=False, spec=None, rmin
     sys.path.insert(0, ROOT)
     sys.path.insert(0, os.path.join(ROOT, "w-fsa_amd"))
     os.environ["WFSA_PEER"] = "1" if peer else "0"
+    os.environ["WFSA_QN_INKERNEL"] = "1"   # (small shards: the cover rule alone would take the two-kernel step)
     if late_s:
         os.environ["WFSA_PEER_TIMEOUT_S"] = "3"
     import torch.distributed as dist

@@ -23,7 +23,10 @@ FINISH = ["last", "next"]
 
 
 def _learner(W, fsa, sym, off, wt, monkeypatch, inkernel, finish="last", rmin=False):
-    monkeypatch.setenv("WFSA_QN_INKERNEL", "1" if inkernel else "0")
+    if inkernel is None:   # the cover rule decides (the product default)
+        monkeypatch.delenv("WFSA_QN_INKERNEL", raising=False)
+    else:
+        monkeypatch.setenv("WFSA_QN_INKERNEL", "1" if inkernel else "0")
     monkeypatch.setenv("WFSA_QN_LAST_SELF", "0" if finish == "next" else "1")
     lrn = W.QuasiNewtonLearner(0)
     lrn.set_info_rmin(rmin)
@@ -201,3 +204,20 @@ def test_poll_timeout_fails_the_run(monkeypatch):
     with pytest.raises(W.WfsaError, match="timed out"):
         a.Run(4, 1.0, -1.0)
     assert a.stats()["qn_inkernel_waves"] > 0   # the in-kernel update was the one that ran
+
+
+def test_cover_rule_takes_two_kernels_for_short_streams(monkeypatch):
+    """with WFSA_QN_INKERNEL unset the one-launch step is taken only when the
+    deal's mean stream rows per wave cover the bubble tail (wfsa_dev.hip
+    qw_cover): a 200k-string family-A corpus (~3 rows per wave) steps with
+    the two kernels, bit for bit what the forced one-launch step gives"""
+    import wfsa_amd as W
+    fsa, sym, off, wt = _corpus(W, **FAMILIES["familyA"])
+    a = _learner(W, fsa, sym, off, wt, monkeypatch, None)
+    ra = a.Run(4, 1.0, -1.0)
+    assert a.stats()["qn_inkernel_waves"] == 0
+    b = _learner(W, fsa, sym, off, wt, monkeypatch, True)
+    rb = b.Run(4, 1.0, -1.0)
+    assert b.stats()["qn_inkernel_waves"] > 0
+    assert np.array_equal(np.array(ra), np.array(rb))
+    np.testing.assert_array_equal(a.x(), b.x())

@@ -3048,8 +3048,7 @@ __global__ __launch_bounds__(1024, (DBG == 10 ? 8 : 1)) WFSA_FBS_ATTR void fbs_k
     // big bubbles, one wavefront each, from the last blocks' last waves down
     // (the finish wave's rank, nblk - 1, skipped), staged in LDS after the table
     auto big_bubbles = [&]() {
-        int r = (nblk - 1 - bid) + nblk * (wpb - 1 - w);
-        r -= r > nblk - 1 ? 1 : 0;
+        const int r = big_rank(bid, w, nblk, wpb, a.bub.qw_waves);
         if (r < a.bub.n_big) {
             stored = true;
             const int E = a.bub.big_lds_edges;

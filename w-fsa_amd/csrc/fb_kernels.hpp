@@ -556,6 +556,20 @@ constexpr int kBigEdgeLds = 256;   // > kMaxBubbleEdges: per-wave staging of a b
 // kernel (E even): weights / contributions and alpha, beta (doubles), then
 // the edges' nodes (ints); 16-byte multiple
 __host__ __device__ inline int big_stage_bytes(int E) { return ((E + 2 * kMaxBubbleNodes) * 8 + E * 4 + 15) & ~15; }
+// The big bubbles' wave order in the stream kernel: wave rank r takes big
+// bubbles r, r + (waves - 1), ...  Ranks run from the blocks' last waves
+// backwards (those waves take no small bubbles); block 0's last wave, the QN
+// finish's, takes none; the QN waves (wave wpb - 2 of blocks [0, qw_waves))
+// come last, so they take one only when every other wave has: a QN wave with
+// a big bubble started its update late (with the rmin column its deferred
+// (min, x) pass came first too)
+__host__ __device__ inline int big_rank(int bid, int wib, int nblk, int wpb, int qw_waves) {
+    int r = (nblk - 1 - bid) + nblk * (wpb - 1 - wib);
+    r -= r > nblk - 1 ? 1 : 0;
+    if (qw_waves <= 0) return r;
+    if (wib == wpb - 2 && bid < qw_waves) return nblk * wpb - 1 - qw_waves + bid;
+    return r >= 2 * nblk - 1 - qw_waves ? r - qw_waves : r;
+}
 constexpr int kSmallBubbleQuads4 = 4;   // class A: <= 4 nodes, <= 4 edges (1 + 2 + 1 quads)
 struct BubbleArgs {
     ModelView m;
@@ -567,6 +581,7 @@ struct BubbleArgs {
     const int32_t* big_off;
     int32_t n_big;
     int32_t small_wpb;       // fused: waves [0, small_wpb) of every block take 64 small bubbles each
+    int32_t qw_waves;        // fused: the layout's QN waves (big_rank; whether or not this launch runs them)
     int32_t big_lds_edges;   // fused: max edges of a big bubble (even) ...
     int32_t big_lds_off;     // ... and the byte offset of the waves' staging in the stream kernel's LDS
     const int32_t* big_edge_base;

@@ -183,6 +183,9 @@ struct wfsa_dev {
     // format (fb_kernels.hpp): its own groups, dealing and layout; the 16-bit
     // streams above stay for the preparation-time gradient pass
     bool delta_on = false;
+    double qw_mean_rows = 0.0;       // the delta deal's mean stream rows per wave (the in-kernel QN's cover rule)
+    bool qw_cover = true;            // the stream covers the bubble tail: the one-launch step is the faster one
+    bool qw_force = false;           // WFSA_QN_INKERNEL=1: the one-launch step whenever it is possible
     int32_t d_tab = 0;
     DevBuf<uint4> dstream;
     DevBuf<int64_t> d_g_base;
@@ -1396,6 +1399,7 @@ int build_delta(wfsa_dev* ctx, const std::vector<int32_t>& comp, const std::vect
     }
     std::vector<int32_t> dorder, dwf;
     deal(grows, dorder, dwf, rows16 > 0.0 ? rowsd / rows16 : 1.0);
+    ctx->qw_mean_rows = rowsd / double(std::max(1, ctx->i_grid * (ctx->i_block / kWave) - 1));
     std::vector<int64_t> dg_base(size_t(G) + 1, 0);
     std::vector<int32_t> dg_len(size_t(std::max(G, 1)), 0), dl_str(size_t(std::max(G, 1)) * kWave, -1);
     int64_t dch = 0;
@@ -1697,8 +1701,7 @@ int prepare(wfsa_dev* ctx, int level) {
             }
             if (wib == i_wpb - 2 && bid < ctx->qw_waves) load0[size_t(w)] += ctx->qw_cost;
             if (wib < small_wpb && int64_t(wib) * nblk + bid < small_waves) load0[size_t(w)] += small_cost;   // (fbs_kernel's chunk order)
-            int64_t r = (nblk - 1 - bid) + int64_t(nblk) * (i_wpb - 1 - wib);
-            r -= r > nblk - 1 ? 1 : 0;
+            const int64_t r = wfsa::big_rank(bid, wib, nblk, i_wpb, ctx->qw_waves);
             if (r < n_big_est) load0[size_t(w)] += big_cost;
         }
         deal(rows0, order, wave_first, 1.0);
@@ -1846,8 +1849,9 @@ int prepare(wfsa_dev* ctx, int level) {
     // step against the earlier 18 / 36 / 8 / 8; big 15 after the QN batches
     // were capped at 48 chunks (the refit's 15.0 rows; -0.3 us per step,
     // profiles/r05/option_sweeps.txt)
+    constexpr double kChargeA = 9.0, kChargeB = 17.0, kChargeBig = 15.0;
     {
-        double small_cost = 9.0, small_cost_b = 17.0, big_cost = 15.0;
+        const double small_cost = kChargeA, small_cost_b = kChargeB, big_cost = kChargeBig;
         const int nblk = ctx->i_grid;
         const int64_t nch = wfsa::small_chunks(ctx->n_small4, ctx->n_small), na = (int64_t(ctx->n_small4) + kWave - 1) / kWave;
         const int small_wpb = small_waves_per_block(nch * kWave, nblk);
@@ -1858,8 +1862,7 @@ int prepare(wfsa_dev* ctx, int level) {
             if (wib == i_wpb - 2 && bid < ctx->qw_waves) c += ctx->qw_cost;
             const int64_t ch = int64_t(wib) * nblk + bid;   // fbs_kernel's chunk of this wave (wfsa::small_entry)
             if (wib < small_wpb && ch < nch) c += ch >= na ? small_cost_b : small_cost;
-            int64_t r = (nblk - 1 - bid) + int64_t(nblk) * (i_wpb - 1 - wib);
-            r -= r > nblk - 1 ? 1 : 0;
+            const int64_t r = wfsa::big_rank(bid, wib, nblk, i_wpb, ctx->qw_waves);
             if (r < ctx->n_big) c += big_cost;
             load0[size_t(w)] = c;
         }
@@ -1879,6 +1882,15 @@ int prepare(wfsa_dev* ctx, int level) {
         ctx->d_tab = 0;
         if (delta_want && ctx->i_tables)
             if (int rc = build_delta(ctx, comp, h_main, s_base, h_p, chunks, G, rows0, deal)) return rc;
+        // The one-launch step's critical path is the last bubble arrival, a
+        // go line and a QN batch; the two-kernel step's is the stream's end, a
+        // launch and the QN kernel.  So the one launch pays when the stream
+        // covers the bubble tail: the deal's mean stream rows per wave against
+        // the heaviest bubble wave's charge, at the ratio where c3's family
+        // crosses over (750k strings: 12.9 rows, two kernels 1.6 us faster;
+        // 1M: 17.2 rows, one launch 2.6 us faster; profiles/r06/xrank.txt)
+        const double heaviest = ctx->n_small > 0 ? kChargeB : ctx->n_big > 0 ? kChargeBig : ctx->n_small4 > 0 ? kChargeA : 0.0;
+        ctx->qw_cover = !ctx->delta_on || ctx->qw_mean_rows >= 15.0 / kChargeB * heaviest;
     }
     ctx->n_groups = G;
     ctx->n_compiled = nc;
@@ -2087,6 +2099,7 @@ int enqueue_compiled(wfsa_dev* ctx, bool with_grad, bool want_logq, const unsign
             }
             c.bub_on = 1;
             c.bub.small_wpb = small_waves_per_block(wfsa::small_chunks(ctx->n_small4, ctx->n_small) * kWave, ctx->i_grid);
+            c.bub.qw_waves = ctx->qw_waves;
             if (ctx->n_big > 0) {
                 c.bub.big_lds_edges = ctx->big_lds_edges;
                 c.bub.big_lds_off = int32_t(big_stage_off(ctx));
@@ -2665,7 +2678,8 @@ bool qw_usable(wfsa_dev* ctx) {
     // batches within the areas' flags)
     const bool comm_ok = !ctx->comm || (std::strcmp(ctx->comm->peer_state(), "on") == 0 &&
                                         ctx->qw_nbatch <= wfsa::kPeerMaxQnBatches);
-    return ctx->use_qw && ctx->qw_ok && ctx->qw_waves > 0 && ctx->qn_fused && comm_ok && !ctx->dense &&
+    return ctx->use_qw && (ctx->qw_cover || ctx->qw_force) && ctx->qw_ok && ctx->qw_waves > 0 && ctx->qn_fused &&
+           comm_ok && !ctx->dense &&
            !ctx->mpath && rmin_ok && ctx->n_groups > 0 && ctx->delta_on && ctx->i_tables >= 1 &&
            ctx->fixed_t_on && ctx->qn_k > 0 &&
            ctx->i_block / kWave >= 3 && qw_resident(ctx);
@@ -2975,7 +2989,10 @@ int wfsa_dev_create(int device, wfsa_dev** out) {
     if (const char* e = std::getenv("WFSA_TIER2")) ctx->force_tier2 = e[0] == '1';
     if (const char* e = std::getenv("WFSA_WIDE2")) ctx->use_wide2 = e[0] != '0';
     if (const char* e = std::getenv("WFSA_PULL")) ctx->use_pull = e[0] != '0';
-    if (const char* e = std::getenv("WFSA_QN_INKERNEL")) ctx->use_qw = e[0] != '0';
+    if (const char* e = std::getenv("WFSA_QN_INKERNEL")) {   // (unset: by the cover rule; 1: whenever possible; 0: never)
+        ctx->use_qw = e[0] != '0';
+        ctx->qw_force = e[0] == '1';
+    }
     // fault injection (tests/test_gpu_qn_inkernel.py): the first QN wave waits
     // for an arrival that never comes and gives up after a few polls
     if (const char* e = std::getenv("WFSA_FAULT_QN_POLL"); e && e[0] == '1') {
@@ -3552,9 +3569,15 @@ static int qn_run_impl(wfsa_dev* ctx, double eta, double tol, int32_t max_steps,
     const auto tr0 = clk::now();
     auto tr_ms = [&](clk::time_point t) { return std::chrono::duration<double, std::micro>(t - tr0).count(); };
     clk::time_point tr_pro{}, tr_first{}, tr_last{}, tr_end{}, tr_enq1{};
+    clk::time_point tp[8]{};   // (the prologue's phases, WFSA_VERBOSE)
+    auto mark = [&](int i) {
+        if (trace) tp[i] = clk::now();
+    };
     if (ctx->prep_level < 2)
         if (int rc = prepare(ctx, 2)) return rc;
+    mark(0);
     if (int rc = collect_timing(ctx)) return rc;
+    mark(5);
     if (std::getenv("WFSA_VERBOSE") && !ctx->h_seg_ptr.empty() && ctx->qn_fused) {   // slots per constraint
         const int32_t k = ctx->qn_k;
         const std::vector<int32_t>& cptr = ctx->h_cptr;
@@ -3567,6 +3590,7 @@ static int qn_run_impl(wfsa_dev* ctx, double eta, double tol, int32_t max_steps,
                          (long long)sz[sz.size() / 2]);
     }
     hipStream_t s = ctx->stream;
+    mark(6);
     if (!ctx->qn_flags_clear) HIP_TRY(hipMemsetAsync(ctx->qn_halted.ptr, 0, 3 * sizeof(unsigned), s));
     ctx->qn_flags_clear = false;
     ctx->fin_pending = false;
@@ -3585,9 +3609,12 @@ static int qn_run_impl(wfsa_dev* ctx, double eta, double tol, int32_t max_steps,
     } else {
         ctx->fixed_t_on = false;
     }
+    mark(1);
     if (ctx->use_qw && ctx->qw_waves > 0)
         if (int rc = build_qw_batches(ctx)) return rc;
+    mark(2);
     bool inkern = qw_usable(ctx);
+    mark(3);
     if (ctx->comm) {   // every rank takes the same path (the in-kernel exchange pairs the ranks' launches):
                        // agreed once per preparation, QN set-up, layout and rmin setting
         const int64_t key = ((ctx->prep_gen * 1000003 + ctx->qn_setup_gen) * 1000003 + ctx->layout_gen) * 2 +
@@ -3606,8 +3633,9 @@ static int qn_run_impl(wfsa_dev* ctx, double eta, double tol, int32_t max_steps,
         inkern = ctx->qw_agreed;
     }
     if (!inkern && ctx->use_qw && std::getenv("WFSA_VERBOSE"))
-        std::fprintf(stderr, "[wfsa] QN update as its own kernel: batches %d waves %d fused %d comm %d rmin %d delta %d "
-                     "fallback %d bubbles fused %d fixed_t %d k %d\n", int(ctx->qw_ok), ctx->qw_waves, int(ctx->qn_fused),
+        std::fprintf(stderr, "[wfsa] QN update as its own kernel: cover %d (%.1f rows per wave) batches %d waves %d "
+                     "fused %d comm %d rmin %d delta %d fallback %d bubbles fused %d fixed_t %d k %d\n", int(ctx->qw_cover),
+                     ctx->qw_mean_rows, int(ctx->qw_ok), ctx->qw_waves, int(ctx->qn_fused),
                      int(ctx->comm != nullptr), int(ctx->qn_rmin), int(ctx->delta_on),
                      ctx->n_fall[0] + ctx->n_fall[1] + ctx->n_fall[2],
                      int(ctx->n_bubbles == 0 || bubbles_fused(ctx, false)), int(ctx->fixed_t_on), ctx->qn_k);
@@ -3630,6 +3658,7 @@ static int qn_run_impl(wfsa_dev* ctx, double eta, double tol, int32_t max_steps,
             ctx->pipe_init_e = ctx->ewp2.ptr;
         }
     }
+    mark(4);
     // steps whose kernels are timed: every stride-th (not the first), or the
     // last of a run shorter than the stride
     auto timed_step = [&](int32_t e) {
@@ -3846,8 +3875,7 @@ static int qn_run_impl(wfsa_dev* ctx, double eta, double tol, int32_t max_steps,
                     kind = ch >= na ? 2 : 1;
                     x[kind + 1] = 1.0;
                 }
-                int64_t rb = (ctx->i_grid - 1 - bid) + int64_t(ctx->i_grid) * (wpb - 1 - wib);
-                rb -= rb > ctx->i_grid - 1 ? 1 : 0;
+                const int64_t rb = wfsa::big_rank(bid, wib, ctx->i_grid, wpb, ctx->qw_waves);
                 if (rb < ctx->n_big) {
                     x[4] = 1.0;
                     kind = kind ? kind : 3;
@@ -3919,6 +3947,9 @@ static int qn_run_impl(wfsa_dev* ctx, double eta, double tol, int32_t max_steps,
 #endif
     if (trace) {
         tr_end = clk::now();
+        std::fprintf(stderr, "[wfsa] qn_run prologue: prepared %.1f, timing %.1f, (verbose stats) %.1f, flags + fixed %.1f, "
+                     "batches %.1f, path %.1f, buffers %.1f us\n", tr_ms(tp[0]), tr_ms(tp[5]), tr_ms(tp[6]), tr_ms(tp[1]),
+                     tr_ms(tp[2]), tr_ms(tp[3]), tr_ms(tp[4]));
         std::fprintf(stderr, "[wfsa] qn_run %d steps: prologue %.1f us, first step enqueued %.1f, first row %.1f, "
                      "last row %.1f, end %.1f (start at %lld ns)\n",
                      done, tr_ms(tr_pro), tr_ms(tr_enq1), tr_ms(tr_first), done > 1 ? tr_ms(tr_last) : tr_ms(tr_first),
