@@ -12,9 +12,10 @@ run DEVICE-RESIDENT: main.cpp's epoch loop is wfsa_learner_run ->
 wfsa_dev_qn_run, which enqueues per step the forward-backward kernels (stream
 + bubble + traversal tiers), [the RCCL all-reduce of the gradient], and the QN
 update (x, lambda and the next weights stay in HBM; each step's info row lands
-in host-mapped memory).  On one GPU at c3 that is ONE launch per step: the
-stream kernel with the bubbles and the QN update inside; across
-ranks the QN update is its own kernel after the all-reduce.  Inputs are resident in HBM.  The same steps
+in host-mapped memory).  At c3 that is ONE launch per step: the stream kernel
+with the bubbles and the QN update inside; across ranks too, the
+QN batches' partials then summed over the ranks through the peer areas inside
+that launch.  Inputs are resident in HBM.  The same steps
 through the host binding of INTEGRATION.md section 2 (wfsa_dev_objective_grad
 per step: H2D weights, D2H [LL, grad], host QN update) are timed beside it
 (`boundary`).
@@ -23,7 +24,8 @@ Multi-GPU: launched by torch.distributed.run, one process per GPU (`--gpus N`
 without a launcher starts the N ranks itself, or refuses when the node has
 fewer GPUs); every rank builds the same global corpus and keeps a contiguous
 shard (Learner::BuildFrom); the gradient + log-likelihood are summed once per
-step by the one-shot peer all-reduce over xGMI (RCCL communicator; RCCL's own
+step over xGMI through the peer areas, inside the stream kernel's QN waves
+(the two-kernel step: the one-shot peer all-reduce kernel; RCCL's own
 all-reduce if the peer path's set-up check fails -- `comm` in the line says
 which).
 
@@ -530,8 +532,10 @@ def main():
         "info_rmin": rmin_pass,
         "boundary": boundary,
         "comm": ({"transport": "rccl", "ranks": st1.get("comm_ranks", world),
-                  "per_step_sum": {1: "one-shot peer all-reduce (xGMI)", 0: "ncclAllReduce",
-                                   -1: "ncclAllReduce (peer set-up check failed)"}.get(st1.get("comm_peer", 0))}
+                  "per_step_sum": ("the QN batches' partials through the peer areas (xGMI), inside the stream kernel"
+                                   if st1.get("qn_inkernel_waves") else
+                                   {1: "one-shot peer all-reduce (xGMI)", 0: "ncclAllReduce",
+                                    -1: "ncclAllReduce (peer set-up check failed)"}.get(st1.get("comm_peer", 0)))}
                  if distributed else None),
         "experiment_knobs": "none (WFSA_*_DBG refused; compiled out of the release library)",
         "live_edges_per_step": st1["last_live_edges"],
