@@ -2145,6 +2145,13 @@ __device__ __forceinline__ double group_sum(double v, int k, int kmax) {
     return v;
 }
 
+// The big bubbles' wave priority: above the small-bubble waves' 2 -- a big
+// bubble is one wave's serial sweep, and the small-bubble waves on its SIMD
+// otherwise issue first (c3 26.6 vs 26.9 us per step, with the rmin column
+// 29.6 vs 31.5; priority 2: no gain; profiles/r06/big_prio_ab.txt)
+#ifndef WFSA_BIG_PRIO
+#define WFSA_BIG_PRIO 3
+#endif
 #ifndef WFSA_UNI_BUBBLES   // (variant builds: the uniform-structure path of small bubbles)
 #define WFSA_UNI_BUBBLES 0
 #endif
@@ -3057,8 +3064,10 @@ __global__ __launch_bounds__(1024, (DBG == 10 ? 8 : 1)) WFSA_FBS_ATTR void fbs_k
             int* lsd = reinterpret_cast<int*>(lw + E + 2 * kMaxBubbleNodes);
             const BubbleArgs bub = WFSA_LATE_ARG(bub);
             const RminFold rf = WFSA_LATE_ARG(rf);
+            if (WFSA_BIG_PRIO) __builtin_amdgcn_s_setprio(WFSA_BIG_PRIO);
             for (int i = r; i < bub.n_big; i += nw - 1)
                 ll_acc += big_bubble(bub, i, lsd, lw, lw, lw + E, RF ? &rf : nullptr, &rm_cv, &rm_ci, &rm_big);
+            if (WFSA_BIG_PRIO) __builtin_amdgcn_s_setprio(0);
         }
     };
     if (!DELTA && W_LDS && DBG != 4 && !a.no_streams) {
